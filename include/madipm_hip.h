@@ -1,0 +1,100 @@
+/*
+ * madipm_hip.h — C-ABI of libmadipm_hip.so, the MI355X (gfx950) hot path of MadIPM's
+ * Mehrotra predictor-corrector (reference: klamike/MadIPM.jl v0.1.2).
+ *
+ * Conventions: 0-based indices, Float64 values, int32 row indices, int64 column pointers /
+ * nonzero counts.  Every function returns 0 on success, a negative code on error (text in
+ * madipm_last_error(), thread-local); madipm_ldl_factorize additionally returns k+1 > 0 when
+ * pivot k (internal order) is zero / non-finite, which maps to MadIPM.is_factorized == false.
+ * Device pointers are plain hipMalloc'd (or torch / AMDGPU.jl ROCArray) addresses; `stream` is a
+ * hipStream_t (NULL = default stream).  No exceptions cross this boundary.
+ *
+ * Which reference interface each entry point replaces is cited per function (file:line relative
+ * to the reference root).  INTEGRATION.md shows the Julia `ccall` binding a maintainer would add.
+ */
+#ifndef MADIPM_HIP_H
+#define MADIPM_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* madipm_stream_t; /* hipStream_t */
+
+/* ------------------------------------------------------------------ library */
+int madipm_version(void);                 /* MAJOR*10000 + MINOR*100 + PATCH */
+const char* madipm_last_error(void);
+int madipm_device_count(void);            /* hipGetDeviceCount; 0 when no GPU is present */
+
+/* ------------------------------------------------------------------ symbolic analysis (host)
+ * Replaces the symbolic phase run by the linear-solver constructor `linear_solver(aug_com; opt)`
+ * (src/KKT/normalkkt.jl:113-115; SparseKKTSystem constructor in MadNLP [EXT]) — SURVEY §8 a12. */
+typedef struct madipm_ldl_opts {
+  int32_t ordering;        /* 0 natural, 1 AMD (default), 2 user permutation */
+  double dense_alpha;      /* AMD dense-node threshold factor (default 10) */
+  int32_t relax;           /* relaxed supernode amalgamation (default 1) */
+  int32_t small_front_max; /* fronts with <= this many rows are factorised in LDS (default 128) */
+  double pivot_tol;        /* |d| <= pivot_tol  =>  pivot failure (default 0: only 0 / NaN / Inf) */
+} madipm_ldl_opts;
+
+typedef struct madipm_ldl_info {
+  int64_t n;
+  int64_t nnzK;            /* entries of the lower CSC input */
+  int64_t nnzL;            /* exact nnz(L) incl. diagonal */
+  int64_t nnzL_stored;     /* lower-trapezoid entries stored by the supernodes (incl. relaxed zeros) */
+  double flops;            /* factorisation flops, sum_j (c_j-1)(c_j+2) */
+  int32_t nsuper;          /* fronts */
+  int32_t nlevels;         /* levels of the front tree (launch schedule depth) */
+  int32_t max_front;       /* largest front order */
+  int32_t nbig;            /* fronts handled by the global-memory blocked path */
+  int64_t arena_bytes;     /* device bytes for factor + update blocks */
+} madipm_ldl_info;
+
+void madipm_ldl_default_opts(madipm_ldl_opts* opts);
+
+typedef struct madipm_symbolic* madipm_symbolic_t;
+/* colptr[n+1] (int64), rowval[nnz] (int32): lower triangle (row >= col), unique entries. */
+int madipm_symbolic_analyze(int32_t n, const int64_t* colptr, const int32_t* rowval,
+                            const madipm_ldl_opts* opts, const int32_t* user_perm,
+                            madipm_symbolic_t* out);
+int madipm_symbolic_info(madipm_symbolic_t sym, madipm_ldl_info* info);
+int madipm_symbolic_perm(madipm_symbolic_t sym, int32_t* perm /* n */);
+/* first[nsuper+1], parent[nsuper], nrows[nsuper] (any may be NULL) */
+int madipm_symbolic_supernodes(madipm_symbolic_t sym, int32_t* first, int32_t* parent, int32_t* nrows);
+void madipm_symbolic_destroy(madipm_symbolic_t sym);
+
+/* ------------------------------------------------------------------ LDL^T linear solver (device)
+ * The MadNLP.AbstractLinearSolver the reference plugs in through `linear_solver=`
+ * (src/utils.jl:72, src/structure.jl:117-123): LDLSolver (LDLFactorizations), CUDSSSolver with
+ * cudss_algorithm=MadNLP.LDL (scripts/benchmarks_gpu.jl:41-42), Ma57Solver
+ * (scripts/benchmarks_cpu.jl:36).  SURVEY §8 a11/a12/a14, boundary §8(b). */
+typedef struct madipm_ldl* madipm_ldl_t;
+/* Constructor `LS(aug_com; opt)`: symbolic analysis + device upload (src/KKT/normalkkt.jl:113-115). */
+int madipm_ldl_analyze(int32_t n, const int64_t* colptr, const int32_t* rowval,
+                       const madipm_ldl_opts* opts, const int32_t* user_perm, madipm_ldl_t* out);
+int madipm_ldl_get_info(madipm_ldl_t ls, madipm_ldl_info* info);
+/* MadNLP.factorize!(ls) (called via factorize_wrapper!, src/linear_solver.jl:10, src/solver.jl:21).
+ * d_nzval: device values in the CSC order given to madipm_ldl_analyze.  Synchronises `stream`;
+ * returns 0, or k+1 for the first failing pivot k (=> madipm_ldl_is_factorized() == 0). */
+int madipm_ldl_factorize(madipm_ldl_t ls, const double* d_nzval, madipm_stream_t stream);
+/* Asynchronous variant; the outcome is read by madipm_ldl_is_factorized / madipm_ldl_inertia. */
+int madipm_ldl_factorize_async(madipm_ldl_t ls, const double* d_nzval, madipm_stream_t stream);
+/* MadIPM.is_factorized(ls) (src/utils.jl:54-62): 1 when the last factorisation succeeded. */
+int madipm_ldl_is_factorized(madipm_ldl_t ls);
+/* MadNLP.solve!(ls, x) (src/linear_solver.jl:26 via MadNLP.solve!(kkt, d)): in place, nrhs
+ * columns of length n stored contiguously. */
+int madipm_ldl_solve(madipm_ldl_t ls, double* d_x, int32_t nrhs, madipm_stream_t stream);
+/* MadNLP.inertia(ls) -> (pos, zero, neg); MadNLP.is_inertia(ls) is true. */
+int madipm_ldl_inertia(madipm_ldl_t ls, int32_t* pos, int32_t* zero, int32_t* neg);
+/* Diagonal D of the last factorisation, internal (permuted) order, copied to host memory. */
+int madipm_ldl_get_d(madipm_ldl_t ls, double* h_d);
+int madipm_ldl_perm(madipm_ldl_t ls, int32_t* perm /* n */);
+void madipm_ldl_destroy(madipm_ldl_t ls);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MADIPM_HIP_H */

@@ -1,0 +1,237 @@
+// extern "C" entry points of libmadipm_hip.so (declared in include/madipm_hip.h).
+// Every entry point catches C++ exceptions and converts them to a negative return code plus
+// madipm_last_error() text.
+#include <cstring>
+#include <memory>
+#include <string>
+
+#include "../../include/madipm_hip.h"
+#include "common.hpp"
+#include "ldl.hpp"
+#include "symbolic.hpp"
+
+namespace madipm {
+namespace {
+thread_local std::string g_last_error;
+}
+void set_last_error(const std::string& msg) { g_last_error = msg; }
+const char* last_error() { return g_last_error.c_str(); }
+}  // namespace madipm
+
+using namespace madipm;
+
+#define MADIPM_API_BEGIN try {
+#define MADIPM_API_END                                   \
+  }                                                      \
+  catch (const madipm::Error& e) {                       \
+    set_last_error(e.what());                            \
+    return e.code < 0 ? e.code : -1;                     \
+  }                                                      \
+  catch (const std::exception& e) {                      \
+    set_last_error(std::string("exception: ") + e.what()); \
+    return -1;                                           \
+  }                                                      \
+  catch (...) {                                          \
+    set_last_error("unknown exception");                 \
+    return -1;                                           \
+  }
+
+struct madipm_symbolic {
+  SymbolicPlan plan;
+};
+
+struct madipm_ldl {
+  std::unique_ptr<LDLSolver> s;
+  hipStream_t last_stream = nullptr;
+  bool pending = false;
+};
+
+static SymbolicOptions to_sym_opts(const madipm_ldl_opts* o) {
+  SymbolicOptions s;
+  if (o) {
+    s.ordering = o->ordering;
+    s.dense_alpha = o->dense_alpha;
+    s.relax = o->relax;
+    s.small_front_max = o->small_front_max;
+  }
+  MADIPM_REQUIRE(s.small_front_max >= 1 && s.small_front_max <= 128, "small_front_max must be in [1,128]");
+  return s;
+}
+
+extern "C" {
+
+int madipm_version(void) { return 100; }
+
+const char* madipm_last_error(void) { return last_error(); }
+
+int madipm_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+void madipm_ldl_default_opts(madipm_ldl_opts* o) {
+  if (!o) return;
+  o->ordering = 1;
+  o->dense_alpha = 10.0;
+  o->relax = 1;
+  o->small_front_max = 128;
+  o->pivot_tol = 0.0;
+}
+
+int madipm_symbolic_analyze(int32_t n, const int64_t* colptr, const int32_t* rowval,
+                            const madipm_ldl_opts* opts, const int32_t* user_perm,
+                            madipm_symbolic_t* out) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(out != nullptr && colptr != nullptr, "null argument");
+  auto s = std::make_unique<madipm_symbolic>();
+  symbolic_analyze(n, colptr, rowval, to_sym_opts(opts), user_perm, s->plan);
+  *out = s.release();
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_symbolic_info(madipm_symbolic_t sym, madipm_ldl_info* info) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(sym && info, "null argument");
+  const SymbolicPlan& p = sym->plan;
+  info->n = p.N;
+  info->nnzK = p.nnzK;
+  info->nnzL = p.nnzL;
+  info->nnzL_stored = p.nnzL_super;
+  info->flops = p.flops;
+  info->nsuper = p.nsuper;
+  info->nlevels = p.nlevels;
+  info->max_front = p.max_front;
+  info->nbig = p.nbig;
+  info->arena_bytes = p.arena_size * 8;
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_symbolic_perm(madipm_symbolic_t sym, int32_t* perm) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(sym && perm, "null argument");
+  std::memcpy(perm, sym->plan.perm.data(), sizeof(int32_t) * sym->plan.perm.size());
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_symbolic_supernodes(madipm_symbolic_t sym, int32_t* first, int32_t* parent, int32_t* nrows) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(sym, "null argument");
+  const SymbolicPlan& p = sym->plan;
+  if (first) std::memcpy(first, p.first.data(), sizeof(int32_t) * p.first.size());
+  if (parent) std::memcpy(parent, p.parent.data(), sizeof(int32_t) * p.parent.size());
+  if (nrows) std::memcpy(nrows, p.nrows.data(), sizeof(int32_t) * p.nrows.size());
+  return 0;
+  MADIPM_API_END
+}
+
+void madipm_symbolic_destroy(madipm_symbolic_t sym) { delete sym; }
+
+// ------------------------------------------------------------------ LDL^T plugin
+int madipm_ldl_analyze(int32_t n, const int64_t* colptr, const int32_t* rowval, const madipm_ldl_opts* opts,
+                       const int32_t* user_perm, madipm_ldl_t* out) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(out != nullptr && colptr != nullptr, "null argument");
+  madipm_ldl_opts o;
+  madipm_ldl_default_opts(&o);
+  if (opts) o = *opts;
+  auto ls = std::make_unique<madipm_ldl>();
+  ls->s = std::make_unique<LDLSolver>(n, colptr, rowval, to_sym_opts(&o), o.pivot_tol, user_perm);
+  *out = ls.release();
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_ldl_get_info(madipm_ldl_t ls, madipm_ldl_info* info) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(ls && info, "null argument");
+  const SymbolicPlan& p = ls->s->plan();
+  info->n = p.N;
+  info->nnzK = p.nnzK;
+  info->nnzL = p.nnzL;
+  info->nnzL_stored = p.nnzL_super;
+  info->flops = p.flops;
+  info->nsuper = p.nsuper;
+  info->nlevels = p.nlevels;
+  info->max_front = p.max_front;
+  info->nbig = p.nbig;
+  info->arena_bytes = p.arena_size * 8;
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_ldl_factorize_async(madipm_ldl_t ls, const double* d_nzval, madipm_stream_t stream) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(ls, "null handle");
+  ls->s->factorize_async(d_nzval, (hipStream_t)stream);
+  ls->last_stream = (hipStream_t)stream;
+  ls->pending = true;
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_ldl_factorize(madipm_ldl_t ls, const double* d_nzval, madipm_stream_t stream) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(ls, "null handle");
+  ls->s->factorize_async(d_nzval, (hipStream_t)stream);
+  ls->pending = false;
+  return ls->s->status((hipStream_t)stream);
+  MADIPM_API_END
+}
+
+int madipm_ldl_is_factorized(madipm_ldl_t ls) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(ls, "null handle");
+  if (ls->pending) {
+    ls->s->status(ls->last_stream);
+    ls->pending = false;
+  }
+  return ls->s->factorized ? 1 : 0;
+  MADIPM_API_END
+}
+
+int madipm_ldl_solve(madipm_ldl_t ls, double* d_x, int32_t nrhs, madipm_stream_t stream) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(ls && (d_x || ls->s->n() == 0), "null argument");
+  for (int k = 0; k < nrhs; ++k) ls->s->solve_async(d_x + (int64_t)k * ls->s->n(), (hipStream_t)stream);
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_ldl_inertia(madipm_ldl_t ls, int32_t* pos, int32_t* zero, int32_t* neg) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(ls, "null handle");
+  if (ls->pending) {
+    ls->s->status(ls->last_stream);
+    ls->pending = false;
+  }
+  if (pos) *pos = ls->s->npos;
+  if (zero) *zero = ls->s->nzero;
+  if (neg) *neg = ls->s->nneg;
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_ldl_get_d(madipm_ldl_t ls, double* h_d) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(ls && h_d, "null argument");
+  MADIPM_HIP(hipDeviceSynchronize());
+  MADIPM_HIP(hipMemcpy(h_d, ls->s->d_diag(), sizeof(double) * ls->s->n(), hipMemcpyDeviceToHost));
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_ldl_perm(madipm_ldl_t ls, int32_t* perm) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(ls && perm, "null argument");
+  std::memcpy(perm, ls->s->plan().perm.data(), sizeof(int32_t) * ls->s->n());
+  return 0;
+  MADIPM_API_END
+}
+
+void madipm_ldl_destroy(madipm_ldl_t ls) { delete ls; }
+
+}  // extern "C"

@@ -1,0 +1,443 @@
+// Symbolic analysis for the multifrontal supernodal LDL^T — see symbolic.hpp.
+//
+// Elimination tree: Liu's algorithm with path compression.  Column counts: Gilbert, Ng & Peyton
+// (skeleton matrix / row-subtree leaves with least-common-ancestor compression).  Supernodes:
+// fundamental supernodes in postorder, then relaxed amalgamation with the (nrelax, zrelax)
+// thresholds popularised by CHOLMOD.  All written for this project.
+#include "symbolic.hpp"
+
+#include <algorithm>
+#include <numeric>
+
+#include "common.hpp"
+
+namespace madipm {
+
+namespace {
+
+struct Pattern {
+  // strictly-lower pattern of P K P^T: column lists (rows > col) and row lists (cols < row)
+  std::vector<int64_t> cp, rp;
+  std::vector<int32_t> ci, ri;
+};
+
+void build_pattern(int N, const int64_t* colptr, const int32_t* rowval, const std::vector<int32_t>& pinv,
+                   Pattern& P) {
+  P.cp.assign(N + 1, 0);
+  P.rp.assign(N + 1, 0);
+  for (int j = 0; j < N; ++j)
+    for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p) {
+      int i = rowval[p];
+      if (i == j) continue;
+      int a = pinv[i], b = pinv[j];
+      int hi = std::max(a, b), lo = std::min(a, b);
+      P.cp[lo + 1]++;
+      P.rp[hi + 1]++;
+    }
+  for (int j = 0; j < N; ++j) {
+    P.cp[j + 1] += P.cp[j];
+    P.rp[j + 1] += P.rp[j];
+  }
+  P.ci.resize(P.cp[N]);
+  P.ri.resize(P.rp[N]);
+  std::vector<int64_t> cc(P.cp.begin(), P.cp.end() - 1), rc(P.rp.begin(), P.rp.end() - 1);
+  for (int j = 0; j < N; ++j)
+    for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p) {
+      int i = rowval[p];
+      if (i == j) continue;
+      int a = pinv[i], b = pinv[j];
+      int hi = std::max(a, b), lo = std::min(a, b);
+      P.ci[cc[lo]++] = hi;
+      P.ri[rc[hi]++] = lo;
+    }
+}
+
+void etree(int N, const Pattern& P, std::vector<int32_t>& parent) {
+  parent.assign(N, -1);
+  std::vector<int32_t> anc(N, -1);
+  for (int k = 0; k < N; ++k)
+    for (int64_t p = P.rp[k]; p < P.rp[k + 1]; ++p) {
+      int i = P.ri[p];
+      while (i != -1 && i < k) {
+        int inext = anc[i];
+        anc[i] = k;
+        if (inext == -1) parent[i] = k;
+        i = inext;
+      }
+    }
+}
+
+void postorder(int N, const std::vector<int32_t>& parent, std::vector<int32_t>& post) {
+  std::vector<int32_t> head(N, -1), next(N, -1), stack(N);
+  for (int j = N - 1; j >= 0; --j)
+    if (parent[j] != -1) {
+      next[j] = head[parent[j]];
+      head[parent[j]] = j;
+    }
+  post.assign(N, 0);
+  int k = 0;
+  for (int j = 0; j < N; ++j) {
+    if (parent[j] != -1) continue;
+    int top = 0;
+    stack[0] = j;
+    while (top >= 0) {
+      int p = stack[top];
+      int i = head[p];
+      if (i == -1) {
+        --top;
+        post[k++] = p;
+      } else {
+        head[p] = next[i];
+        stack[++top] = i;
+      }
+    }
+  }
+}
+
+// Column counts of L (diagonal included) for a matrix whose labelling is a postorder of its etree.
+void column_counts(int N, const Pattern& P, const std::vector<int32_t>& parent, std::vector<int64_t>& cnt) {
+  cnt.assign(N, 0);
+  std::vector<int32_t> first(N, -1), maxfirst(N, -1), prevleaf(N, -1), anc(N);
+  for (int k = 0; k < N; ++k) {
+    int j = k;
+    cnt[j] = (first[j] == -1) ? 1 : 0;
+    for (; j != -1 && first[j] == -1; j = parent[j]) first[j] = k;
+  }
+  std::iota(anc.begin(), anc.end(), 0);
+  for (int j = 0; j < N; ++j) {
+    if (parent[j] != -1) cnt[parent[j]]--;
+    for (int64_t p = P.cp[j]; p < P.cp[j + 1]; ++p) {
+      int i = P.ci[p];  // i > j
+      if (first[j] <= maxfirst[i]) continue;  // j is not a leaf of the i-th row subtree
+      maxfirst[i] = first[j];
+      int jprev = prevleaf[i];
+      prevleaf[i] = j;
+      if (jprev == -1) {
+        cnt[j]++;  // first leaf: A(i,j) in the skeleton
+      } else {
+        int q = jprev;
+        while (q != anc[q]) q = anc[q];
+        for (int s = jprev, sp; s != q; s = sp) {
+          sp = anc[s];
+          anc[s] = q;
+        }
+        cnt[j]++;
+        cnt[q]--;  // overlap at the least common ancestor
+      }
+    }
+    if (parent[j] != -1) anc[j] = parent[j];
+  }
+  for (int j = 0; j < N; ++j)
+    if (parent[j] != -1) cnt[parent[j]] += cnt[j];
+}
+
+inline int64_t trap(int64_t w, int64_t r) { return w * r - w * (w - 1) / 2; }
+
+}  // namespace
+
+void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const SymbolicOptions& opt,
+                      const int32_t* user_perm, SymbolicPlan& S) {
+  S = SymbolicPlan();
+  MADIPM_REQUIRE(N >= 0, "negative dimension");
+  S.N = N;
+  const int64_t nnz = colptr[N];
+  S.nnzK = nnz;
+  MADIPM_REQUIRE(colptr[0] == 0, "colptr[0] must be 0");
+  std::vector<int64_t> diagcount(N, 0);
+  for (int j = 0; j < N; ++j) {
+    MADIPM_REQUIRE(colptr[j + 1] >= colptr[j], "colptr not monotone");
+    for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p) {
+      int i = rowval[p];
+      MADIPM_REQUIRE(i >= j && i < N, "entries must be in the lower triangle (row >= col) and in range");
+      if (i == j) diagcount[j]++;
+    }
+  }
+  if (N == 0) return;
+
+  // ---------------- 1. fill-reducing ordering
+  std::vector<int32_t> perm(N);
+  if (opt.ordering == 1) {
+    std::vector<int64_t> Ap(N + 1, 0);
+    for (int j = 0; j < N; ++j)
+      for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p) {
+        int i = rowval[p];
+        if (i == j) continue;
+        Ap[i + 1]++;
+        Ap[j + 1]++;
+      }
+    for (int j = 0; j < N; ++j) Ap[j + 1] += Ap[j];
+    std::vector<int32_t> Ai(Ap[N]);
+    std::vector<int64_t> fill(Ap.begin(), Ap.end() - 1);
+    for (int j = 0; j < N; ++j)
+      for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p) {
+        int i = rowval[p];
+        if (i == j) continue;
+        Ai[fill[i]++] = j;
+        Ai[fill[j]++] = i;
+      }
+    amd_order(N, Ap, Ai, perm, opt.dense_alpha);
+  } else if (opt.ordering == 2) {
+    MADIPM_REQUIRE(user_perm != nullptr, "user permutation missing");
+    std::copy(user_perm, user_perm + N, perm.begin());
+  } else {
+    std::iota(perm.begin(), perm.end(), 0);
+  }
+  std::vector<int32_t> pinv(N, -1);
+  for (int k = 0; k < N; ++k) {
+    MADIPM_REQUIRE(perm[k] >= 0 && perm[k] < N && pinv[perm[k]] == -1, "ordering is not a permutation");
+    pinv[perm[k]] = k;
+  }
+
+  // ---------------- 2. etree + postorder, relabel so that the labelling is a postorder
+  Pattern P;
+  build_pattern(N, colptr, rowval, pinv, P);
+  std::vector<int32_t> parent, post;
+  etree(N, P, parent);
+  postorder(N, parent, post);
+  std::vector<int32_t> perm2(N);
+  for (int k = 0; k < N; ++k) perm2[k] = perm[post[k]];
+  perm.swap(perm2);
+  for (int k = 0; k < N; ++k) pinv[perm[k]] = k;
+  build_pattern(N, colptr, rowval, pinv, P);
+  etree(N, P, parent);
+  std::vector<int64_t> cnt;
+  column_counts(N, P, parent, cnt);
+  S.perm = perm;
+  S.pinv = pinv;
+  S.nnzL = std::accumulate(cnt.begin(), cnt.end(), (int64_t)0);
+
+  // ---------------- 3. fundamental supernodes
+  std::vector<int32_t> nchild(N, 0);
+  for (int j = 0; j < N; ++j)
+    if (parent[j] != -1) nchild[parent[j]]++;
+  struct SN {
+    int first, w;
+    int64_t r, zeros;
+  };
+  std::vector<SN> fund;
+  fund.push_back({0, 1, cnt[0], 0});
+  for (int j = 1; j < N; ++j) {
+    if (parent[j - 1] == j && cnt[j - 1] == cnt[j] + 1 && nchild[j] == 1) {
+      fund.back().w++;
+    } else {
+      fund.push_back({j, 1, cnt[j], 0});
+    }
+  }
+
+  // ---------------- 4. relaxed amalgamation (merge a front with its column-adjacent child)
+  std::vector<SN> sn;
+  sn.reserve(fund.size());
+  for (const SN& f : fund) {
+    SN p = f;
+    while (opt.relax && !sn.empty()) {
+      const SN& c = sn.back();
+      int clast = c.first + c.w - 1;
+      if (clast + 1 != p.first) break;
+      int par = parent[clast];
+      if (par < p.first || par >= p.first + p.w) break;
+      int64_t ncols = c.w + p.w;
+      int64_t rnew = c.w + p.r;
+      int64_t Enew = trap(ncols, rnew);
+      int64_t zeros = Enew - (trap(c.w, c.r) - c.zeros) - (trap(p.w, p.r) - p.zeros);
+      double frac = (double)zeros / (double)Enew;
+      bool merge = ncols <= opt.nrelax[0] || (ncols <= opt.nrelax[1] && frac < opt.zrelax[0]) ||
+                   (ncols <= opt.nrelax[2] && frac < opt.zrelax[1]) || frac < opt.zrelax[2];
+      if (!merge) break;
+      p.first = c.first;
+      p.w = (int)ncols;
+      p.r = rnew;
+      p.zeros = zeros;
+      sn.pop_back();
+    }
+    sn.push_back(p);
+  }
+  const int ns = (int)sn.size();
+  S.nsuper = ns;
+  S.first.resize(ns + 1);
+  std::vector<int32_t> col2sn(N);
+  for (int s = 0; s < ns; ++s) {
+    S.first[s] = sn[s].first;
+    for (int j = sn[s].first; j < sn[s].first + sn[s].w; ++j) col2sn[j] = s;
+  }
+  S.first[ns] = N;
+  S.parent.assign(ns, -1);
+  for (int s = 0; s < ns; ++s) {
+    int last = S.first[s + 1] - 1;
+    if (parent[last] != -1) S.parent[s] = col2sn[parent[last]];
+    MADIPM_REQUIRE(S.parent[s] == -1 || S.parent[s] > s, "supernodal tree is not postordered");
+  }
+  S.child_ptr.assign(ns + 1, 0);
+  for (int s = 0; s < ns; ++s)
+    if (S.parent[s] != -1) S.child_ptr[S.parent[s] + 1]++;
+  for (int s = 0; s < ns; ++s) S.child_ptr[s + 1] += S.child_ptr[s];
+  S.child_list.resize(S.child_ptr[ns]);
+  {
+    std::vector<int32_t> fillc(S.child_ptr.begin(), S.child_ptr.end() - 1);
+    for (int s = 0; s < ns; ++s)
+      if (S.parent[s] != -1) S.child_list[fillc[S.parent[s]]++] = s;
+  }
+
+  // ---------------- 5. frontal row structures
+  S.row_ptr.assign(ns + 1, 0);
+  S.nrows.resize(ns);
+  std::vector<int32_t> marker(N, -1);
+  std::vector<std::vector<int32_t>> R(ns);
+  for (int s = 0; s < ns; ++s) {
+    int f = S.first[s], l = S.first[s + 1];
+    std::vector<int32_t>& rs = R[s];
+    for (int j = f; j < l; ++j) {
+      rs.push_back(j);
+      marker[j] = s;
+    }
+    size_t nown = rs.size();
+    for (int j = f; j < l; ++j)
+      for (int64_t p = P.cp[j]; p < P.cp[j + 1]; ++p) {
+        int i = P.ci[p];
+        if (i >= l && marker[i] != s) {
+          marker[i] = s;
+          rs.push_back(i);
+        }
+      }
+    for (int64_t q = S.child_ptr[s]; q < S.child_ptr[s + 1]; ++q) {
+      int c = S.child_list[q];
+      const std::vector<int32_t>& rc = R[c];
+      int wc = S.first[c + 1] - S.first[c];
+      for (size_t t = wc; t < rc.size(); ++t) {
+        int i = rc[t];
+        MADIPM_REQUIRE(i >= f, "child row structure escapes its parent");
+        if (i >= l && marker[i] != s) {
+          marker[i] = s;
+          rs.push_back(i);
+        }
+      }
+    }
+    std::sort(rs.begin() + nown, rs.end());
+    S.nrows[s] = (int32_t)rs.size();
+    S.row_ptr[s + 1] = S.row_ptr[s] + (int64_t)rs.size();
+  }
+  S.rows.resize(S.row_ptr[ns]);
+  for (int s = 0; s < ns; ++s) std::copy(R[s].begin(), R[s].end(), S.rows.begin() + S.row_ptr[s]);
+
+  // ---------------- 6. relative indices child -> parent
+  S.rel_ptr.assign(ns + 1, 0);
+  for (int s = 0; s < ns; ++s) {
+    int w = S.first[s + 1] - S.first[s];
+    S.rel_ptr[s + 1] = S.rel_ptr[s] + (S.nrows[s] - w);
+  }
+  S.rel.resize(S.rel_ptr[ns]);
+  std::vector<int32_t> pos(N, -1);
+  for (int s = 0; s < ns; ++s) {
+    for (int64_t t = S.row_ptr[s]; t < S.row_ptr[s + 1]; ++t) pos[S.rows[t]] = (int32_t)(t - S.row_ptr[s]);
+    for (int64_t q = S.child_ptr[s]; q < S.child_ptr[s + 1]; ++q) {
+      int c = S.child_list[q];
+      int wc = S.first[c + 1] - S.first[c];
+      for (int t = wc; t < S.nrows[c]; ++t) {
+        int row = S.rows[S.row_ptr[c] + t];
+        int ps = pos[row];
+        MADIPM_REQUIRE(ps >= 0 && S.rows[S.row_ptr[s] + ps] == row, "relative index lookup failed");
+        S.rel[S.rel_ptr[c] + (t - wc)] = ps;
+      }
+    }
+  }
+
+  // ---------------- 7. assembly map: caller's CSC entry -> (front, local offset)
+  S.asm_ptr.assign(ns + 1, 0);
+  std::vector<int32_t> ea(nnz), eb(nnz);
+  for (int j = 0; j < N; ++j)
+    for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p) {
+      int a = pinv[rowval[p]], b = pinv[j];
+      if (a < b) std::swap(a, b);
+      ea[p] = a;
+      eb[p] = b;
+      S.asm_ptr[col2sn[b] + 1]++;
+    }
+  for (int s = 0; s < ns; ++s) S.asm_ptr[s + 1] += S.asm_ptr[s];
+  S.asm_src.resize(nnz);
+  S.asm_dst.resize(nnz);
+  {
+    std::vector<int64_t> byfront(nnz);
+    std::vector<int64_t> fillp(S.asm_ptr.begin(), S.asm_ptr.end() - 1);
+    for (int64_t p = 0; p < nnz; ++p) byfront[fillp[col2sn[eb[p]]]++] = p;
+    for (int s = 0; s < ns; ++s) {
+      int r = S.nrows[s];
+      for (int64_t t = S.row_ptr[s]; t < S.row_ptr[s + 1]; ++t) pos[S.rows[t]] = (int32_t)(t - S.row_ptr[s]);
+      for (int64_t q = S.asm_ptr[s]; q < S.asm_ptr[s + 1]; ++q) {
+        int64_t p = byfront[q];
+        int lc = eb[p] - S.first[s];
+        int lr = pos[ea[p]];
+        MADIPM_REQUIRE(lr >= 0, "assembly row not in front");
+        S.asm_src[q] = p;
+        S.asm_dst[q] = (int64_t)lc * r + lr;
+      }
+      // sort by destination (the big-front assembly binary-searches column ranges) and reject
+      // duplicates, which would race in the parallel assembly
+      std::vector<std::pair<int64_t, int64_t>> d;
+      d.reserve(S.asm_ptr[s + 1] - S.asm_ptr[s]);
+      for (int64_t q = S.asm_ptr[s]; q < S.asm_ptr[s + 1]; ++q) d.emplace_back(S.asm_dst[q], S.asm_src[q]);
+      std::sort(d.begin(), d.end());
+      for (size_t t = 0; t < d.size(); ++t) {
+        MADIPM_REQUIRE(t == 0 || d[t].first != d[t - 1].first, "duplicate entries in the lower CSC input");
+        S.asm_dst[S.asm_ptr[s] + t] = d[t].first;
+        S.asm_src[S.asm_ptr[s] + t] = d[t].second;
+      }
+    }
+  }
+
+  // ---------------- 8. level schedule (height in the supernodal tree)
+  S.level.assign(ns, 0);
+  int maxlev = 0;
+  for (int s = 0; s < ns; ++s) {
+    int lv = 0;
+    for (int64_t q = S.child_ptr[s]; q < S.child_ptr[s + 1]; ++q) lv = std::max(lv, S.level[S.child_list[q]] + 1);
+    S.level[s] = lv;
+    maxlev = std::max(maxlev, lv);
+  }
+  S.nlevels = maxlev + 1;
+  S.level_ptr.assign(S.nlevels + 1, 0);
+  for (int s = 0; s < ns; ++s) S.level_ptr[S.level[s] + 1]++;
+  for (int l = 0; l < S.nlevels; ++l) S.level_ptr[l + 1] += S.level_ptr[l];
+  S.level_list.resize(ns);
+  {
+    std::vector<int32_t> fl(S.level_ptr.begin(), S.level_ptr.end() - 1);
+    for (int s = 0; s < ns; ++s) S.level_list[fl[S.level[s]]++] = s;
+  }
+
+  // ---------------- 9. storage layout + statistics
+  S.l_off.resize(ns);
+  S.u_off.resize(ns);
+  S.u_ld.resize(ns);
+  S.uvec_off.resize(ns);
+  S.is_big.resize(ns);
+  int64_t cur = 0, ucur = 0;
+  for (int s = 0; s < ns; ++s) {
+    int64_t r = S.nrows[s], w = S.first[s + 1] - S.first[s];
+    S.max_front = std::max<int>(S.max_front, (int)r);
+    S.nnzL_super += trap(w, r);
+    for (int64_t t = 0; t < w; ++t) {
+      double cc = (double)(r - t);
+      S.flops += (cc - 1.0) * (cc + 2.0);
+    }
+    S.uvec_off[s] = ucur;
+    ucur += r - w;
+    if (r <= opt.small_front_max) {
+      S.is_big[s] = 0;
+      S.l_off[s] = cur;
+      cur += r * w;
+      S.u_off[s] = cur;
+      S.u_ld[s] = (int32_t)(r - w);
+      cur += (r - w) * (r - w);
+    } else {
+      S.is_big[s] = 1;
+      S.nbig++;
+      S.l_off[s] = cur;
+      S.u_off[s] = cur + w * r + w;
+      S.u_ld[s] = (int32_t)r;
+      cur += r * r;
+    }
+    cur = (cur + 1) & ~(int64_t)1;  // 16-byte alignment of every front
+  }
+  S.arena_size = cur;
+  S.uvec_size = ucur;
+}
+
+}  // namespace madipm

@@ -1,0 +1,64 @@
+// Symbolic analysis for the multifrontal supernodal LDL^T (host side, runs once per pattern).
+//
+// Replaces the symbolic phase the reference's linear-solver constructor performs
+// (`linear_solver(aug_com; opt)`, src/KKT/normalkkt.jl:113-115; MadNLP's SparseKKTSystem ctor for
+// K2) — SURVEY §8 a12: fill-reducing ordering, elimination tree, column counts, fundamental +
+// relaxed supernodes, frontal row structures, the assembly map from the caller's CSC values to
+// frontal positions, child→parent relative indices and the level schedule used on the GPU.
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+namespace madipm {
+
+void amd_order(int n, const std::vector<int64_t>& Ap, const std::vector<int32_t>& Ai,
+               std::vector<int32_t>& perm, double dense_alpha = 10.0);
+
+struct SymbolicOptions {
+  int ordering = 1;          // 0: natural, 1: AMD, 2: user permutation
+  double dense_alpha = 10.0; // AMD dense threshold = max(16, alpha*sqrt(n))
+  int relax = 1;             // relaxed supernode amalgamation on/off
+  int nrelax[3] = {4, 16, 48};
+  double zrelax[3] = {0.8, 0.1, 0.05};
+  int small_front_max = 128; // fronts with r <= this are factorised in LDS by one workgroup
+};
+
+struct SymbolicPlan {
+  int N = 0;
+  int64_t nnzK = 0;                    // entries of the caller's lower CSC
+  std::vector<int32_t> perm, pinv;     // perm[k] = original index of pivot k
+  // supernodes (fronts), in postorder; columns of s are [first[s], first[s+1])
+  int nsuper = 0;
+  std::vector<int32_t> first, parent, nrows;
+  std::vector<int64_t> row_ptr;        // rows[row_ptr[s] .. row_ptr[s+1]) = R_s (permuted ids)
+  std::vector<int32_t> rows;           // first w_s entries = own columns, then sorted below rows
+  std::vector<int32_t> child_ptr, child_list;
+  std::vector<int64_t> rel_ptr;        // rel[rel_ptr[c] ..) = positions of R_c[w_c:] in R_parent
+  std::vector<int32_t> rel;
+  std::vector<int64_t> asm_ptr;        // per front: original entries (src nz index, local offset)
+  std::vector<int64_t> asm_src;
+  std::vector<int64_t> asm_dst;        // col_local * r + row_local
+  std::vector<int32_t> level;          // height of the front in the supernodal tree
+  std::vector<int32_t> level_ptr, level_list;
+  int nlevels = 0;
+  // storage layout (doubles)
+  std::vector<int64_t> l_off;          // L panel (r x w, col-major, ld r); big fronts: whole F
+  std::vector<int64_t> u_off;          // update block (ld u_ld)
+  std::vector<int32_t> u_ld;
+  std::vector<int64_t> uvec_off;       // solve update vector (r - w)
+  std::vector<uint8_t> is_big;
+  int64_t arena_size = 0, uvec_size = 0;
+  // statistics
+  int64_t nnzL = 0;          // exact nnz(L) incl. diagonal (column counts)
+  int64_t nnzL_super = 0;    // stored lower-trapezoid entries incl. relaxed zeros
+  double flops = 0;          // sum_j (c_j - 1)(c_j + 2) over stored supernodal columns
+  int max_front = 0, nbig = 0;
+};
+
+// Analyse the symmetric matrix given by its lower-triangular CSC pattern (0-based, entries with
+// row >= col, unique).  Throws madipm::Error on invalid input.
+void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const SymbolicOptions& opt,
+                      const int32_t* user_perm, SymbolicPlan& plan);
+
+}  // namespace madipm

@@ -1,0 +1,96 @@
+"""`HIPLDLSolver`: the MadNLP.AbstractLinearSolver the reference plugs in via `linear_solver=`.
+
+Mirrors the methods MadNLP calls on a linear solver: construction from the lower
+CSC `aug_com` (`LS(aug_com; opt)`, src/KKT/normalkkt.jl:113-115), `factorize!`, `solve!`,
+`is_inertia` / `inertia`, `improve!`, `introduce`, and MadIPM's `is_factorized`
+(src/utils.jl:54-62).  Device vectors are torch tensors on `cuda:*` (HIP); values never leave HBM.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+
+
+class HIPLDLSolver:
+    """Multifrontal supernodal LDL^T on the GPU (libmadipm_hip)."""
+
+    def __init__(self, n, colptr, rowval, *, ordering=1, relax=1, pivot_tol=0.0, perm=None,
+                 small_front_max=128):
+        self.n = int(n)
+        self._colptr = np.ascontiguousarray(colptr, np.int64)
+        self._rowval = np.ascontiguousarray(rowval, np.int32)
+        opts = L.default_ldl_opts(ordering=2 if perm is not None else ordering, relax=relax,
+                                  pivot_tol=pivot_tol, small_front_max=small_front_max)
+        up = None if perm is None else np.ascontiguousarray(perm, np.int32)
+        h = L.vp()
+        L.check(L.lib.madipm_ldl_analyze(self.n, L.ptr(self._colptr, C.c_int64), L.ptr(self._rowval, C.c_int32),
+                                         C.byref(opts), L.ptr(up, C.c_int32) if up is not None else None,
+                                         C.byref(h)), "madipm_ldl_analyze")
+        self.h = h
+
+    # ---- MadNLP interface names
+    def introduce(self) -> str:
+        return "madipm-hip supernodal LDL^T (gfx950)"
+
+    @staticmethod
+    def is_supported(dtype=np.float64) -> bool:
+        return dtype == np.float64
+
+    def info(self) -> dict:
+        inf = L.LDLInfo()
+        L.check(L.lib.madipm_ldl_get_info(self.h, C.byref(inf)), "madipm_ldl_get_info")
+        return inf.as_dict()
+
+    def factorize(self, nzval, stream=None) -> int:
+        """factorize!: nzval is a device tensor (float64, CSC order of construction)."""
+        assert nzval.dtype.itemsize == 8 and nzval.numel() == self._colptr[-1]
+        rc = L.lib.madipm_ldl_factorize(self.h, C.c_void_p(nzval.data_ptr()), C.c_void_p(_stream(stream)))
+        return L.check(rc, "madipm_ldl_factorize")
+
+    def is_factorized(self) -> bool:
+        return bool(L.check(L.lib.madipm_ldl_is_factorized(self.h), "madipm_ldl_is_factorized"))
+
+    def solve(self, x, stream=None):
+        """solve!(ls, x): in place on a device tensor of length n (or n x nrhs column blocks)."""
+        assert x.dtype.itemsize == 8 and x.is_contiguous()
+        nrhs = x.numel() // max(self.n, 1)
+        L.check(L.lib.madipm_ldl_solve(self.h, C.c_void_p(x.data_ptr()), nrhs, C.c_void_p(_stream(stream))),
+                "madipm_ldl_solve")
+        return x
+
+    def is_inertia(self) -> bool:
+        return True
+
+    def inertia(self):
+        p, z, n = C.c_int32(), C.c_int32(), C.c_int32()
+        L.check(L.lib.madipm_ldl_inertia(self.h, C.byref(p), C.byref(z), C.byref(n)), "madipm_ldl_inertia")
+        return p.value, z.value, n.value
+
+    def improve(self) -> bool:
+        return False
+
+    def diag(self) -> np.ndarray:
+        d = np.empty(self.n)
+        L.check(L.lib.madipm_ldl_get_d(self.h, L.ptr(d, C.c_double)), "madipm_ldl_get_d")
+        return d
+
+    def perm(self) -> np.ndarray:
+        p = np.empty(self.n, np.int32)
+        L.check(L.lib.madipm_ldl_perm(self.h, L.ptr(p, C.c_int32)), "madipm_ldl_perm")
+        return p
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            L.lib.madipm_ldl_destroy(h)
+            self.h = None
+
+
+def _stream(stream) -> int:
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    return int(stream)

@@ -1,0 +1,49 @@
+"""Shared test helpers: seeded KKT matrices and problem generators (test data only)."""
+from __future__ import annotations
+
+import numpy as np
+import scipy.sparse as sp
+
+
+def random_k2(m, n, density, seed, delta=1e-8, qp=False, well=False):
+    """K2 = [H + Sigma, A^T; A, -delta I] with Sigma in [1e-2, 1e2]: quasi-definite.
+    well=True: delta = 1e-2, Sigma in [0.1, 10] (O(1) element growth)."""
+    rng = np.random.default_rng(seed)
+    A = sp.random(m, n, density=density, random_state=rng, format="csr")
+    A.data[:] = rng.standard_normal(A.nnz)
+    sig = 10.0 ** rng.uniform(-1, 1, n) if well else 10.0 ** rng.uniform(-2, 2, n)
+    if well:
+        delta = 1e-2
+    H = sp.diags(sig)
+    if qp:
+        B = sp.random(n, n, density=min(1.0, 3.0 / n), random_state=rng)
+        H = H + B @ B.T
+    K = sp.bmat([[H, A.T], [A, -delta * sp.eye(m)]]).tocsc()
+    K.sum_duplicates()
+    Lw = sp.tril(K).tocsc()
+    Lw.sort_indices()
+    return K, Lw
+
+
+def block_angular_k2(m, n, nblocks, seed, coupling=0.02, delta=1e-8, well=False):
+    """Structured stand-in: block-angular A with a few coupling rows."""
+    rng = np.random.default_rng(seed)
+    rows, cols = [], []
+    bn = n // nblocks
+    for i in range(m):
+        b = (i * nblocks) // m
+        c = rng.integers(b * bn, (b + 1) * bn, size=6)
+        if rng.random() < coupling:
+            c = np.concatenate([c, rng.integers(0, n, size=20)])
+        rows += [i] * len(c)
+        cols += list(c)
+    A = sp.csr_matrix((rng.standard_normal(len(rows)), (rows, cols)), shape=(m, n))
+    A.sum_duplicates()
+    sig = 10.0 ** rng.uniform(-1, 1, n) if well else 10.0 ** rng.uniform(-2, 2, n)
+    if well:
+        delta = 1e-2
+    K = sp.bmat([[sp.diags(sig), A.T], [A, -delta * sp.eye(m)]]).tocsc()
+    K.sum_duplicates()
+    Lw = sp.tril(K).tocsc()
+    Lw.sort_indices()
+    return K, Lw
