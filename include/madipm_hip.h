@@ -93,6 +93,83 @@ int madipm_ldl_get_d(madipm_ldl_t ls, double* h_d);
 int madipm_ldl_perm(madipm_ldl_t ls, int32_t* perm /* n */);
 void madipm_ldl_destroy(madipm_ldl_t ls);
 
+/* ------------------------------------------------------------------ native MPC solver
+ * `MPCSolver(qp; kwargs...)` + `solve!(solver)` (src/structure.jl:79-178, src/solver.jl:362-418)
+ * for a QuadraticModel with SparseKKTSystem (K2), run entirely on the GPU with the LDL^T above.
+ * All problem arrays are HOST pointers (0-based COO; H = lower triangle). */
+typedef struct madipm_qp {
+  int32_t nvar, ncon;
+  int64_t nnzh, nnzj;
+  const double* c;
+  double c0;
+  const int32_t *Hrows, *Hcols;
+  const double* Hvals;
+  const int32_t *Arows, *Acols;
+  const double* Avals;
+  const double *lcon, *ucon, *lvar, *uvar;
+  const double *x0, *y0; /* may be NULL (zeros) */
+  int32_t minimize;
+} madipm_qp;
+
+/* IPMOptions (src/utils.jl:69-105) */
+typedef struct madipm_options {
+  double tol;                 /* 1e-8 */
+  int32_t max_iter;           /* 3000 */
+  double max_wall_time;       /* 1e6 */
+  double divergence_tol;      /* 1e4 */
+  int32_t scaling;            /* 1 */
+  double bound_push, bound_fac, bound_relax_factor; /* 1e-2, 1e-2, 1e-12 */
+  int32_t regularization;     /* 0 NoRegularization, 1 FixedRegularization, 2 AdaptiveRegularization */
+  double delta_p, delta_d, delta_min; /* (1e-10, 1e-10, -) */
+  int32_t step_rule;          /* 0 ConservativeStep(tau), 1 AdaptiveStep(tau_min), 2 MehrotraAdaptiveStep(gamma_f) */
+  double step_tau;            /* 0.99 */
+  int32_t max_ncorr;          /* 0 (Gondzio correctors) */
+  double mu_init, mu_min;     /* 1e-1, 1e-12 */
+  double tol_linear_solve;    /* 1e-8 */
+  int32_t check_residual;     /* 0 */
+  int32_t kkt_system;         /* 0 SparseKKTSystem (K2) */
+  int32_t print_level;        /* 0 silent, 1 iteration log to stdout */
+  madipm_ldl_opts ldl;
+} madipm_options;
+
+/* MadNLP.Status values used by MadIPM */
+enum {
+  MADIPM_REGULAR = 0,
+  MADIPM_SOLVE_SUCCEEDED = 1,
+  MADIPM_INFEASIBLE_PROBLEM_DETECTED = 2,
+  MADIPM_MAXIMUM_ITERATIONS_EXCEEDED = -1,
+  MADIPM_MAXIMUM_WALLTIME_EXCEEDED = -2,
+  MADIPM_DIVERGING_ITERATES = -3,
+  MADIPM_ERROR_IN_STEP_COMPUTATION = -4,
+  MADIPM_INTERNAL_ERROR = -5
+};
+
+typedef struct madipm_stats {
+  int32_t status, iter;
+  double objective;           /* un-scaled, sign-corrected (update_solution!, src/utils.jl:150-156) */
+  double dual_objective;
+  double inf_pr, inf_du, inf_compl, mu;
+  double total_time;          /* MPC loop only, as cnt.total_time (src/solver.jl:181,407) */
+  double linear_solver_time;  /* factorizations (GPU events) */
+  double init_time;           /* symbolic analysis + initialize! */
+} madipm_stats;
+
+typedef struct madipm_iter_trace {
+  int32_t k;
+  double obj, inf_pr, inf_du, inf_compl, mu, alpha_p, alpha_d, del_w, dx_inf, residual;
+} madipm_iter_trace;
+
+typedef struct madipm_solver* madipm_solver_t;
+void madipm_default_options(madipm_options* opt);
+int madipm_solver_create(const madipm_qp* qp, const madipm_options* opt, madipm_solver_t* out);
+int madipm_solver_solve(madipm_solver_t s, madipm_stats* stats);
+/* any pointer may be NULL: x/zl/zu length nvar, y/cons length ncon (un-scaled, as MadNLP stats) */
+int madipm_solver_get_solution(madipm_solver_t s, double* x, double* y, double* zl, double* zu, double* cons);
+/* copies up to cap records, returns the number of recorded iterations */
+int madipm_solver_trace(madipm_solver_t s, madipm_iter_trace* out, int32_t cap);
+int madipm_solver_ldl_info(madipm_solver_t s, madipm_ldl_info* info);
+void madipm_solver_destroy(madipm_solver_t s);
+
 #ifdef __cplusplus
 }
 #endif

@@ -8,6 +8,7 @@
 #include "../../include/madipm_hip.h"
 #include "common.hpp"
 #include "ldl.hpp"
+#include "mpc.hpp"
 #include "symbolic.hpp"
 
 namespace madipm {
@@ -38,6 +39,10 @@ using namespace madipm;
 
 struct madipm_symbolic {
   SymbolicPlan plan;
+};
+
+struct madipm_solver {
+  std::unique_ptr<MPCSolver> s;
 };
 
 struct madipm_ldl {
@@ -233,5 +238,93 @@ int madipm_ldl_perm(madipm_ldl_t ls, int32_t* perm) {
 }
 
 void madipm_ldl_destroy(madipm_ldl_t ls) { delete ls; }
+
+// ------------------------------------------------------------------ native MPC solver
+void madipm_default_options(madipm_options* o) {
+  if (!o) return;
+  std::memset(o, 0, sizeof(*o));
+  o->tol = 1e-8;
+  o->max_iter = 3000;
+  o->max_wall_time = 1e6;
+  o->divergence_tol = 1e4;
+  o->scaling = 1;
+  o->bound_push = 1e-2;
+  o->bound_fac = 1e-2;
+  o->bound_relax_factor = 1e-12;
+  o->regularization = 1;
+  o->delta_p = 1e-10;
+  o->delta_d = 1e-10;
+  o->delta_min = 1e-10;
+  o->step_rule = 1;
+  o->step_tau = 0.99;
+  o->max_ncorr = 0;
+  o->mu_init = 1e-1;
+  o->mu_min = 1e-12;
+  o->tol_linear_solve = 1e-8;
+  o->check_residual = 0;
+  o->kkt_system = 0;
+  o->print_level = 0;
+  madipm_ldl_default_opts(&o->ldl);
+}
+
+int madipm_solver_create(const madipm_qp* qp, const madipm_options* opt, madipm_solver_t* out) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(qp && out, "null argument");
+  madipm_options o;
+  madipm_default_options(&o);
+  if (opt) o = *opt;
+  MADIPM_REQUIRE(o.kkt_system == 0, "only kkt_system = 0 (SparseKKTSystem, K2) is implemented");
+  auto s = std::make_unique<madipm_solver>();
+  s->s = std::make_unique<MPCSolver>(*qp, o);
+  *out = s.release();
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_solver_solve(madipm_solver_t s, madipm_stats* stats) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(s, "null handle");
+  s->s->solve(stats);
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_solver_get_solution(madipm_solver_t s, double* x, double* y, double* zl, double* zu, double* cons) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(s, "null handle");
+  s->s->get_solution(x, y, zl, zu, cons);
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_solver_trace(madipm_solver_t s, madipm_iter_trace* out, int32_t cap) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(s, "null handle");
+  const auto& t = s->s->trace();
+  const int n = (int)std::min<size_t>(t.size(), cap > 0 ? (size_t)cap : 0);
+  if (out) std::copy(t.begin(), t.begin() + n, out);
+  return (int)t.size();
+  MADIPM_API_END
+}
+
+int madipm_solver_ldl_info(madipm_solver_t s, madipm_ldl_info* info) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(s && info, "null argument");
+  const SymbolicPlan& p = s->s->ldl().plan();
+  info->n = p.N;
+  info->nnzK = p.nnzK;
+  info->nnzL = p.nnzL;
+  info->nnzL_stored = p.nnzL_super;
+  info->flops = p.flops;
+  info->nsuper = p.nsuper;
+  info->nlevels = p.nlevels;
+  info->max_front = p.max_front;
+  info->nbig = p.nbig;
+  info->arena_bytes = p.arena_size * 8;
+  return 0;
+  MADIPM_API_END
+}
+
+void madipm_solver_destroy(madipm_solver_t s) { delete s; }
 
 }  // extern "C"

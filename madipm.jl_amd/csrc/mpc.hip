@@ -1,0 +1,1515 @@
+// Native MPC driver + fused IPM vector kernels (gfx950).
+//
+// Restates MadIPM's per-iteration path on the GPU (file:line relative to the reference root):
+//   update_termination_criteria!  src/solver.jl:194-222  -> k_term + k_final(TERM)
+//   set_aug_diagonal_reg! (K2)    src/kernels.jl:124-136 -> k_diag (also writes the K2 diagonal)
+//   factorize_regularized_system! src/linear_solver.jl:6-17 -> LDLSolver::factorize_async (+retry)
+//   set_predictive_rhs! / set_correction_rhs! / reduce_rhs!  src/kernels.jl:21-58 -> k_rhs
+//   solve_system! + finish_aug_solve! + residual (mul!, _kktmul!)  src/linear_solver.jl:19-44 -> k_residual
+//   get_fraction_to_boundary_step (max-ratio test)  src/kernels.jl:226-289 -> k_alpha (argmin)
+//   get_(affine_)complementarity_measure, update_barrier!  src/kernels.jl:155-220 -> k_mu
+//   update_step! (Adaptive/Conservative/MehrotraAdaptive)  src/kernels.jl:291-358 -> k_alpha/k_mu FINAL
+//   apply_step! + adjust_boundary!  src/solver.jl:308-317 -> k_apply
+//   evaluate_model!  src/solver.jl:319-326 -> k_eval (SpMV H x, J x, J^T y, objective)
+//   init_starting_point!  src/solver.jl:6-125 -> k_init_kkt, k_rhs(INIT_*), k_zinit, k_zshift1/2
+// Reductions are two-pass (per-block partials, then one finalising block in fixed order), so every
+// scalar is bitwise reproducible run to run; all scalars stay on the device and the host reads one
+// 200-byte state block per iteration (one hipStreamSynchronize, overlapped with the factorisation).
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <map>
+
+#include "mpc.hpp"
+
+namespace madipm {
+
+struct QPHost {
+  int nx = 0, m = 0, n = 0, ns = 0;
+  std::vector<double> c, lvar, uvar, lcon, ucon, x0, y0, Hv, Av;
+  std::vector<int32_t> Hr, Hc, Ar, Ac;
+  double c0 = 0, sgn = 1;
+  bool minimize = true;
+  std::vector<int32_t> ind_ineq, ind_fixed, ind_lb, ind_ub;
+  std::vector<uint8_t> fixed;
+  bool has_ineq = false;
+  std::vector<double> con_scale;
+  double obj_scale = 1;
+  std::vector<double> x, xl, xu, rhs, y;
+};
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int NPART = 16;
+constexpr int MAXB = 1024;
+constexpr double INF = std::numeric_limits<double>::infinity();
+
+struct DCsr {
+  const int64_t* rp;
+  const int32_t* ci;
+  const double* v;
+};
+
+struct DV {
+  int n, m, nx, nlb, nub;
+  double *x, *xl, *xu, *zl, *zu, *f, *jacl, *c, *y, *rhs;
+  double *pr_diag, *l_diag, *u_diag, *l_lower, *u_lower;
+  double *d, *p, *corr_lb, *corr_ub;
+  double* Kx;
+  const int64_t* diag_pos;
+  const double *Hdiag, *cs, *gfix, *cfix;
+  const int32_t *ind_lb, *ind_ub, *lbpos, *ubpos;
+  const uint8_t* fixed;
+  DCsr H, J, JT;
+  double* part;
+  DevState* st;
+};
+
+enum { OP_SUM = 0, OP_MAX = 1, OP_MIN = 2 };
+
+__device__ __forceinline__ double nmax(double a, double b) { return (b > a || b != b) ? b : a; }
+__device__ __forceinline__ double comb(double a, double b, int op) {
+  return op == OP_SUM ? a + b : (op == OP_MAX ? nmax(a, b) : fmin(a, b));
+}
+__device__ __forceinline__ double csr_dot(const DCsr& A, int row, const double* __restrict__ x) {
+  double s = 0.0;
+  for (int64_t q = A.rp[row]; q < A.rp[row + 1]; ++q) s += A.v[q] * x[A.ci[q]];
+  return s;
+}
+
+template <int NV>
+__device__ void block_partials(double (&v)[NV], const int (&ops)[NV], double* part) {
+  __shared__ double sh[NV][NT / 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    double a = v[k];
+    for (int o = 32; o > 0; o >>= 1) a = comb(a, __shfl_down(a, o, 64), ops[k]);
+    if (lane == 0) sh[k][wv] = a;
+  }
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    const int k = threadIdx.x;
+    double a = sh[k][0];
+    for (int w = 1; w < NT / 64; ++w) a = comb(a, sh[k][w], ops[k]);
+    part[blockIdx.x * NPART + k] = a;
+  }
+}
+
+// (value, index) argmin with smallest-index tie break
+__device__ __forceinline__ void amin_upd(double& v, int& ix, double nv, int ni) {
+  if (nv < v || (nv == v && ni < ix && ni >= 0)) {
+    v = nv;
+    ix = ni;
+  }
+}
+
+#define GRID_LOOP(i, N) for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < (N); i += (int64_t)gridDim.x * blockDim.x)
+
+// ------------------------------------------------------------------ KKT diagonal (kernels.jl:124-136)
+__global__ __launch_bounds__(NT) void k_diag(DV D, double dw, double dc) {
+  GRID_LOOP(i, D.n + D.m) {
+    if (i < D.n) {
+      double pr = dw;
+      const int kl = D.lbpos[i], ku = D.ubpos[i];
+      const double x = D.x[i];
+      if (kl >= 0) {
+        const double ld = D.xl[i] - x, zl = D.zl[i];
+        D.l_diag[kl] = ld;
+        D.l_lower[kl] = zl;
+        pr -= zl / ld;
+      }
+      if (ku >= 0) {
+        const double ud = x - D.xu[i], zu = D.zu[i];
+        D.u_diag[ku] = ud;
+        D.u_lower[ku] = zu;
+        pr -= zu / ud;
+      }
+      D.pr_diag[i] = pr;
+      D.Kx[D.diag_pos[i]] = pr + D.Hdiag[i];
+    } else {
+      D.Kx[D.diag_pos[i]] = dc;
+    }
+  }
+}
+
+// MadNLP.initialize!(kkt) + init_starting_point! lines 16-18
+__global__ __launch_bounds__(NT) void k_init_kkt(DV D, double dw, double dc) {
+  GRID_LOOP(i, D.n + D.m) {
+    if (i < D.n) {
+      const int kl = D.lbpos[i], ku = D.ubpos[i];
+      if (kl >= 0) {
+        D.l_diag[kl] = 1.0;
+        D.l_lower[kl] = 0.0;
+      }
+      if (ku >= 0) {
+        D.u_diag[ku] = 1.0;
+        D.u_lower[ku] = 0.0;
+      }
+      D.pr_diag[i] = dw;
+      D.Kx[D.diag_pos[i]] = dw + D.Hdiag[i];
+    } else {
+      D.Kx[D.diag_pos[i]] = dc;
+    }
+  }
+}
+
+enum { RHS_INIT_PRIMAL = 0, RHS_INIT_DUAL = 1, RHS_PRED = 2, RHS_CORR = 3, RHS_GONDZIO = 4 };
+
+// set_*_rhs! (kernels.jl:1-58) fused with reduce_rhs! [EXT]: writes the unreduced p and the
+// reduced right-hand side d[0:n+m] handed to the LDL^T solve.
+__global__ __launch_bounds__(NT) void k_rhs(DV D, int mode, double mu_g) {
+  const int n = D.n, m = D.m, nlb = D.nlb;
+  const double mu = (mode == RHS_CORR) ? D.st->mu : mu_g;
+  GRID_LOOP(i, n + m) {
+    if (i < n) {
+      double px;
+      if (mode == RHS_INIT_PRIMAL)
+        px = 0.0;
+      else if (mode == RHS_INIT_DUAL)
+        px = -D.f[i];
+      else
+        px = -D.f[i] + D.zl[i] - D.zu[i] - D.jacl[i];
+      double dr = px;
+      const int kl = D.lbpos[i], ku = D.ubpos[i];
+      const bool full = mode >= RHS_PRED;
+      if (kl >= 0) {
+        double pz = 0.0;
+        if (full) {
+          pz = (D.xl[i] - D.x[i]) * D.zl[i];
+          if (mode == RHS_CORR) {
+            const double corr = D.d[i] * D.d[n + m + kl];
+            D.corr_lb[kl] = corr;
+            pz = pz + mu - corr;
+          } else if (mode == RHS_GONDZIO) {
+            pz = pz + mu - D.corr_lb[kl];
+          }
+        }
+        D.p[n + m + kl] = pz;
+        dr -= pz / D.l_diag[kl];
+      }
+      if (ku >= 0) {
+        double pz = 0.0;
+        if (full) {
+          pz = (D.xu[i] - D.x[i]) * D.zu[i];
+          if (mode == RHS_CORR) {
+            const double corr = D.d[i] * D.d[n + m + nlb + ku];
+            D.corr_ub[ku] = corr;
+            pz = pz - mu - corr;
+          } else if (mode == RHS_GONDZIO) {
+            pz = pz - mu - D.corr_ub[ku];
+          }
+        }
+        D.p[n + m + nlb + ku] = pz;
+        dr -= pz / D.u_diag[ku];
+      }
+      D.p[i] = px;
+      D.d[i] = dr;
+    } else {
+      const double py = (mode == RHS_INIT_DUAL) ? 0.0 : -D.c[i - n];
+      D.p[i] = py;
+      D.d[i] = py;
+    }
+  }
+}
+
+// finish_aug_solve! [EXT] + residual w = p - K d (mul!/_kktmul! [EXT], linear_solver.jl:29-35)
+__global__ __launch_bounds__(NT) void k_residual(DV D, double dw, double dc) {
+  const int n = D.n, m = D.m, nlb = D.nlb;
+  double wmax = 0.0, pmax = 0.0, dxmax = 0.0;
+  GRID_LOOP(i, n + m) {
+    if (i < n) {
+      const double dx = D.d[i];
+      double kv = csr_dot(D.H, (int)i, D.d) + csr_dot(D.JT, (int)i, D.d + n) + dw * dx;
+      const int kl = D.lbpos[i], ku = D.ubpos[i];
+      if (kl >= 0) {
+        const double pl = D.p[n + m + kl];
+        const double dzl = (-pl + D.l_lower[kl] * dx) / D.l_diag[kl];
+        D.d[n + m + kl] = dzl;
+        kv -= dzl;
+        const double wl = pl - (dx * D.l_lower[kl] - dzl * D.l_diag[kl]);
+        wmax = nmax(wmax, fabs(wl));
+        pmax = nmax(pmax, fabs(pl));
+      }
+      if (ku >= 0) {
+        const double pu = D.p[n + m + nlb + ku];
+        const double dzu = (pu - D.u_lower[ku] * dx) / D.u_diag[ku];
+        D.d[n + m + nlb + ku] = dzu;
+        kv += dzu;
+        const double wu = pu - (dx * D.u_lower[ku] + dzu * D.u_diag[ku]);
+        wmax = nmax(wmax, fabs(wu));
+        pmax = nmax(pmax, fabs(pu));
+      }
+      const double pi = D.p[i];
+      wmax = nmax(wmax, fabs(pi - kv));
+      pmax = nmax(pmax, fabs(pi));
+      dxmax = nmax(dxmax, fabs(dx));
+    } else {
+      const double dy = D.d[i];
+      const double kv = csr_dot(D.J, (int)(i - n), D.d) + dc * dy;
+      const double pi = D.p[i];
+      wmax = nmax(wmax, fabs(pi - kv));
+      pmax = nmax(pmax, fabs(pi));
+    }
+  }
+  double v[3] = {wmax, pmax, dxmax};
+  const int ops[3] = {OP_MAX, OP_MAX, OP_MAX};
+  block_partials<3>(v, ops, D.part);
+}
+
+enum { ALPHA_PRED = 0, ALPHA_CONSERVATIVE = 1, ALPHA_ADAPTIVE = 2, ALPHA_MEHROTRA = 3, ALPHA_GONDZIO = 4 };
+
+// get_alpha_max_primal / get_alpha_max_dual (kernels.jl:226-272): min-ratio with argmin
+__global__ __launch_bounds__(NT) void k_alpha(DV D, int mode, double tau_param) {
+  const int n = D.n, m = D.m, nlb = D.nlb, nub = D.nub;
+  double tau = 1.0;
+  if (mode == ALPHA_CONSERVATIVE || mode == ALPHA_GONDZIO) tau = tau_param;
+  if (mode == ALPHA_ADAPTIVE) tau = fmax(1.0 - D.st->mu, tau_param);
+  double v[4] = {INF, INF, INF, INF};
+  int ix[4] = {-1, -1, -1, -1};
+  GRID_LOOP(t, (nlb > nub ? nlb : nub)) {
+    if (t < nlb) {
+      const int i = D.ind_lb[t];
+      const double dx = D.d[i];
+      if (dx < 0) amin_upd(v[0], ix[0], (-D.x[i] + D.xl[i]) * tau / dx, (int)t);
+      const double dz = D.d[n + m + t];
+      if (dz < 0) amin_upd(v[2], ix[2], (-D.zl[i]) * tau / dz, (int)t);
+    }
+    if (t < nub) {
+      const int i = D.ind_ub[t];
+      const double dx = D.d[i];
+      if (dx > 0) amin_upd(v[1], ix[1], (-D.x[i] + D.xu[i]) * tau / dx, (int)t);
+      const double dz = D.d[n + m + nlb + t];
+      const double zu = D.zu[i];
+      if (dz < 0 && zu + dz < 0) amin_upd(v[3], ix[3], (-zu) * tau / dz, (int)t);
+    }
+  }
+  __shared__ double sv[4][NT / 64];
+  __shared__ int si[4][NT / 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    double a = v[k];
+    int b = ix[k];
+    for (int o = 32; o > 0; o >>= 1) {
+      const double a2 = __shfl_down(a, o, 64);
+      const int b2 = __shfl_down(b, o, 64);
+      amin_upd(a, b, a2, b2);
+    }
+    if (lane == 0) {
+      sv[k][wv] = a;
+      si[k][wv] = b;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const int k = threadIdx.x;
+    double a = sv[k][0];
+    int b = si[k][0];
+    for (int w = 1; w < NT / 64; ++w) amin_upd(a, b, sv[k][w], si[k][w]);
+    D.part[blockIdx.x * NPART + k] = a;
+    D.part[blockIdx.x * NPART + 4 + k] = (double)b;
+  }
+}
+
+enum { MU_PRED = 0, MU_FULL = 1, MU_GONDZIO = 2 };
+
+// complementarity sums (kernels.jl:155-208); step lengths from the device state (use_state) or args
+__global__ __launch_bounds__(NT) void k_mu(DV D, int use_state, double ap_arg, double ad_arg) {
+  const int n = D.n, m = D.m, nlb = D.nlb, nub = D.nub;
+  const double ap = use_state ? D.st->alpha_aff_p : ap_arg;
+  const double ad = use_state ? D.st->alpha_aff_d : ad_arg;
+  double cl = 0, cu = 0, al = 0, au = 0;
+  GRID_LOOP(t, (nlb > nub ? nlb : nub)) {
+    if (t < nlb) {
+      const int i = D.ind_lb[t];
+      const double x = D.x[i], xl = D.xl[i], zl = D.zl[i];
+      cl += (x - xl) * zl;
+      al += ((x + ap * D.d[i]) - xl) * (zl + ad * D.d[n + m + t]);
+    }
+    if (t < nub) {
+      const int i = D.ind_ub[t];
+      const double x = D.x[i], xu = D.xu[i], zu = D.zu[i];
+      cu += (xu - x) * zu;
+      au += (xu - (x + ap * D.d[i])) * (zu + ad * D.d[n + m + nlb + t]);
+    }
+  }
+  double v[4] = {cl, cu, al, au};
+  const int ops[4] = {OP_SUM, OP_SUM, OP_SUM, OP_SUM};
+  block_partials<4>(v, ops, D.part);
+}
+
+// apply_step! + adjust_boundary! [EXT] (solver.jl:308-317)
+__global__ __launch_bounds__(NT) void k_apply(DV D) {
+  const int n = D.n, m = D.m, nlb = D.nlb;
+  const double ap = D.st->alpha_p, ad = D.st->alpha_d, mu = D.st->mu;
+  const double eps = 2.220446049250313e-16;
+  const double c1 = eps * mu, c2 = 1.8189894035458617e-12;  // eps^(3/4)
+  GRID_LOOP(i, n + m) {
+    if (i < n) {
+      const double x = D.x[i] + ap * D.d[i];
+      D.x[i] = x;
+      const int kl = D.lbpos[i], ku = D.ubpos[i];
+      if (kl >= 0) {
+        D.zl[i] += ad * D.d[n + m + kl];
+        const double xl = D.xl[i];
+        if (x - xl < c1) D.xl[i] = xl - c2 * fmax(1.0, fabs(x));
+      }
+      if (ku >= 0) {
+        D.zu[i] += ad * D.d[n + m + nlb + ku];
+        const double xu = D.xu[i];
+        if (xu - x < c1) D.xu[i] = xu + c2 * fmax(1.0, fabs(x));
+      }
+    } else {
+      D.y[i - n] += ad * D.d[i];
+    }
+  }
+}
+
+// evaluate_model! (solver.jl:319-326): obj, grad f = Hx + c, cons c = Jx - rhs, jacl = J^T y
+__global__ __launch_bounds__(NT) void k_eval(DV D) {
+  const int n = D.n;
+  double op = 0.0;
+  GRID_LOOP(i, n + D.m) {
+    if (i < n) {
+      const double x = D.x[i];
+      const double hx = csr_dot(D.H, (int)i, D.x);
+      const double g = D.cs[i] + D.gfix[i];
+      D.f[i] = D.fixed[i] ? 0.0 : hx + g;
+      D.jacl[i] = csr_dot(D.JT, (int)i, D.y);
+      op += x * g + 0.5 * x * hx;
+    } else {
+      const int j = (int)(i - n);
+      D.c[j] = csr_dot(D.J, j, D.x) - D.rhs[j] + D.cfix[j];
+    }
+  }
+  double v[1] = {op};
+  const int ops[1] = {OP_SUM};
+  block_partials<1>(v, ops, D.part);
+}
+
+// jtprod!(jacl, kkt, y)
+__global__ __launch_bounds__(NT) void k_jtprod(DV D) {
+  GRID_LOOP(i, D.n) D.jacl[i] = csr_dot(D.JT, (int)i, D.y);
+}
+
+// update_termination_criteria! pieces (solver.jl:194-204; dual_objective kernels.jl:408-417;
+// get_optimality_gap kernels.jl:419-430; get_inf_pr/get_inf_du [EXT])
+__global__ __launch_bounds__(NT) void k_term(DV D) {
+  const int n = D.n;
+  double du = 0, gap = 0, pr = 0, sy = 0, sl = 0, su = 0;
+  GRID_LOOP(i, n + D.m) {
+    if (i < n) {
+      du = nmax(du, fabs(D.f[i] - D.zl[i] + D.zu[i] + D.jacl[i]));
+      const int kl = D.lbpos[i], ku = D.ubpos[i];
+      if (kl >= 0) {
+        gap = nmax(gap, fabs((D.x[i] - D.xl[i]) * D.zl[i]));
+        sl += D.zl[i] * D.xl[i];
+      }
+      if (ku >= 0) {
+        gap = nmax(gap, fabs((D.xu[i] - D.x[i]) * D.zu[i]));
+        su += D.zu[i] * D.xu[i];
+      }
+    } else {
+      const int j = (int)(i - n);
+      pr = nmax(pr, fabs(D.c[j]));
+      sy += D.y[j] * D.rhs[j];
+    }
+  }
+  double v[6] = {du, gap, pr, sy, sl, su};
+  const int ops[6] = {OP_MAX, OP_MAX, OP_MAX, OP_SUM, OP_SUM, OP_SUM};
+  block_partials<6>(v, ops, D.part);
+}
+
+// init_starting_point! Step 3 (solver.jl:37-78): z from r = A^T y + f, then min-reductions
+__global__ __launch_bounds__(NT) void k_zinit(DV D) {
+  const int n = D.n;
+  double mxl = 0, mxu = 0, mzl = 0, mzu = 0;  // minimum(...; init=0.0)
+  GRID_LOOP(i, n) {
+    const double res = csr_dot(D.JT, (int)i, D.y) + D.f[i];
+    const double l = D.xl[i], u = D.xu[i];
+    const bool fl = isfinite(l), fu = isfinite(u);
+    const double zl = (fl && fu) ? 0.5 * res : (fl ? res : D.zl[i]);
+    const double zu = (fl && fu) ? -0.5 * res : (fu ? -res : D.zu[i]);
+    D.zl[i] = zl;
+    D.zu[i] = zu;
+    const double x = D.x[i];
+    if (D.lbpos[i] >= 0) {
+      mxl = fmin(mxl, x - l);
+      mzl = fmin(mzl, zl);
+    }
+    if (D.ubpos[i] >= 0) {
+      mxu = fmin(mxu, u - x);
+      mzu = fmin(mzu, zu);
+    }
+  }
+  double v[4] = {mxl, mxu, mzl, mzu};
+  const int ops[4] = {OP_MIN, OP_MIN, OP_MIN, OP_MIN};
+  block_partials<4>(v, ops, D.part);
+}
+
+// solver.jl:80-99: first shift, then the sums defining mu, delta_x2, delta_s2
+__global__ __launch_bounds__(NT) void k_zshift1(DV D) {
+  const int n = D.n;
+  const double dx = D.st->delta_x, ds = D.st->delta_s;
+  double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  GRID_LOOP(i, n) {
+    const bool lb = D.lbpos[i] >= 0, ub = D.ubpos[i] >= 0;
+    double x = D.x[i];
+    if (lb) x = x + dx;
+    if (ub) x = x - dx;
+    D.x[i] = x;
+    if (lb) {
+      const double zl = D.zl[i] + 1.0 + ds;
+      D.zl[i] = zl;
+      const double l = D.xl[i];
+      s[0] += x * zl;
+      s[1] += l * zl;
+      s[4] += zl;
+      s[6] += x - l;
+    }
+    if (ub) {
+      const double zu = D.zu[i] + 1.0 + ds;
+      D.zu[i] = zu;
+      const double u = D.xu[i];
+      s[2] += u * zu;
+      s[3] += x * zu;
+      s[5] += zu;
+      s[7] += u - x;
+    }
+  }
+  const int ops[8] = {OP_SUM, OP_SUM, OP_SUM, OP_SUM, OP_SUM, OP_SUM, OP_SUM, OP_SUM};
+  block_partials<8>(s, ops, D.part);
+}
+
+// solver.jl:96-123: second shift, Ipopt projection, interior assertions (violation count)
+__global__ __launch_bounds__(NT) void k_zshift2(DV D, double kappa) {
+  const int n = D.n;
+  const double dx2 = D.st->delta_x2, ds2 = D.st->delta_s2;
+  double viol = 0;
+  GRID_LOOP(i, n) {
+    const bool lb = D.lbpos[i] >= 0, ub = D.ubpos[i] >= 0;
+    double x = D.x[i];
+    if (lb) x = x + dx2;
+    if (ub) x = x - dx2;
+    if (lb) D.zl[i] = D.zl[i] + ds2;
+    if (ub) D.zu[i] = D.zu[i] + ds2;
+    const double l = D.xl[i], u = D.xu[i];
+    if (x < l) {
+      x = l + fmin(kappa * fmax(1.0, l), kappa * (u - l));
+    } else if (u < x) {
+      x = u - fmin(kappa * fmax(1.0, u), kappa * (u - l));
+    }
+    D.x[i] = x;
+    if (lb && !(D.zl[i] > 0.0 && x > l)) viol += 1;
+    if (ub && !(D.zu[i] > 0.0 && x < u)) viol += 1;
+  }
+  double v[1] = {viol};
+  const int ops[1] = {OP_SUM};
+  block_partials<1>(v, ops, D.part);
+}
+
+__global__ void k_set_mu(DevState* st, double mu) {
+  st->mu = mu;
+  st->alpha_p = st->alpha_d = 0.0;
+  st->nan_flag = 0;
+  st->max_res_ratio = 0.0;
+  st->dx_inf = 0.0;
+}
+__global__ void k_reset_iter(DevState* st) { st->max_res_ratio = 0.0; }
+
+enum {
+  FIN_RESID = 0,
+  FIN_ALPHA = 1,
+  FIN_MU_PRED = 2,
+  FIN_MU_FULL = 3,
+  FIN_EVAL = 4,
+  FIN_TERM = 5,
+  FIN_ZINIT = 6,
+  FIN_ZSHIFT1 = 7,
+  FIN_ZSHIFT2 = 8,
+  FIN_MU_GONDZIO = 9
+};
+
+struct FinParams {
+  int nb;          // number of partial blocks
+  int alpha_mode;  // for FIN_ALPHA
+  double a, b, c;  // kind-specific parameters
+};
+
+// Finalise two-pass reductions in fixed block order + scalar logic (one block).
+__global__ __launch_bounds__(NT) void k_final(DV D, int kind, FinParams P) {
+  __shared__ double res[NPART];
+  __shared__ double sh[NPART][NT / 64];
+  __shared__ int shi[4][NT / 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  DevState* st = D.st;
+  if (kind == FIN_ALPHA) {
+    double v[4];
+    int ix[4];
+    for (int k = 0; k < 4; ++k) {
+      v[k] = INF;
+      ix[k] = -1;
+    }
+    for (int b = threadIdx.x; b < P.nb; b += NT)
+      for (int k = 0; k < 4; ++k) amin_upd(v[k], ix[k], D.part[b * NPART + k], (int)D.part[b * NPART + 4 + k]);
+    for (int k = 0; k < 4; ++k) {
+      double a = v[k];
+      int bi = ix[k];
+      for (int o = 32; o > 0; o >>= 1) {
+        const double a2 = __shfl_down(a, o, 64);
+        const int b2 = __shfl_down(bi, o, 64);
+        amin_upd(a, bi, a2, b2);
+      }
+      if (lane == 0) {
+        sh[k][wv] = a;
+        shi[k][wv] = bi;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double a[4];
+      int ii[4];
+      for (int k = 0; k < 4; ++k) {
+        a[k] = sh[k][0];
+        ii[k] = shi[k][0];
+        for (int w = 1; w < NT / 64; ++w) amin_upd(a[k], ii[k], sh[k][w], shi[k][w]);
+        // mapreduce init (1.0, 0): alpha = min(1, min ratio)
+        if (!(a[k] < 1.0)) {
+          a[k] = 1.0;
+          ii[k] = -1;
+        }
+      }
+      st->a_xl = a[0];
+      st->a_xu = a[1];
+      st->a_zl = a[2];
+      st->a_zu = a[3];
+      st->i_xl = ii[0];
+      st->i_xu = ii[1];
+      st->i_zl = ii[2];
+      st->i_zu = ii[3];
+      const double ap = fmin(a[0], a[1]), ad = fmin(a[2], a[3]);
+      if (P.alpha_mode == ALPHA_PRED) {
+        st->alpha_aff_p = ap;
+        st->alpha_aff_d = ad;
+      } else if (P.alpha_mode == ALPHA_CONSERVATIVE || P.alpha_mode == ALPHA_ADAPTIVE) {
+        st->alpha_p = ap;
+        st->alpha_d = ad;
+      } else {  // MEHROTRA / GONDZIO: keep in the aff slots for the follow-up pass
+        st->alpha_aff_p = ap;
+        st->alpha_aff_d = ad;
+      }
+    }
+    return;
+  }
+  int nv = 0;
+  int ops[NPART];
+  switch (kind) {
+    case FIN_RESID: nv = 3; ops[0] = ops[1] = ops[2] = OP_MAX; break;
+    case FIN_MU_PRED:
+    case FIN_MU_FULL:
+    case FIN_MU_GONDZIO: nv = 4; for (int k = 0; k < 4; ++k) ops[k] = OP_SUM; break;
+    case FIN_EVAL: nv = 1; ops[0] = OP_SUM; break;
+    case FIN_TERM: nv = 6; ops[0] = ops[1] = ops[2] = OP_MAX; ops[3] = ops[4] = ops[5] = OP_SUM; break;
+    case FIN_ZINIT: nv = 4; for (int k = 0; k < 4; ++k) ops[k] = OP_MIN; break;
+    case FIN_ZSHIFT1: nv = 8; for (int k = 0; k < 8; ++k) ops[k] = OP_SUM; break;
+    case FIN_ZSHIFT2: nv = 1; ops[0] = OP_SUM; break;
+  }
+  for (int k = 0; k < nv; ++k) {
+    double a = (ops[k] == OP_SUM || ops[k] == OP_MAX) ? 0.0 : INF;
+    if (ops[k] == OP_MIN) a = 0.0;  // every min-reduction here has init = 0.0
+    // fixed-order accumulation: thread t takes blocks t, t+NT, ... then a fixed tree
+    for (int b = threadIdx.x; b < P.nb; b += NT) a = comb(a, D.part[b * NPART + k], ops[k]);
+    for (int o = 32; o > 0; o >>= 1) a = comb(a, __shfl_down(a, o, 64), ops[k]);
+    if (lane == 0) sh[k][wv] = a;
+  }
+  __syncthreads();
+  if (threadIdx.x < nv) {
+    const int k = threadIdx.x;
+    double a = sh[k][0];
+    for (int w = 1; w < NT / 64; ++w) a = comb(a, sh[k][w], ops[k]);
+    res[k] = a;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  switch (kind) {
+    case FIN_RESID: {
+      const double ratio = res[0] / fmax(1.0, res[1]);  // linear_solver.jl:35
+      st->res_ratio = ratio;
+      st->max_res_ratio = nmax(st->max_res_ratio, ratio);
+      st->dx_inf = res[2];
+      if (ratio != ratio || (P.a > 0 && ratio > P.a)) st->nan_flag = 1;  // SolveException
+      break;
+    }
+    case FIN_MU_PRED: {  // prediction_step! + update_barrier! (kernels.jl:176-220)
+      const double cnt = P.a;  // nlb + nub
+      const double mu_aff = cnt == 0 ? 0.0 : (res[2] + res[3]) / cnt;
+      const double mu_curr = cnt == 0 ? 0.0 : (res[0] + res[1]) / cnt;
+      double sigma = 1.0;
+      if (P.b != 0.0) {  // has_inequalities
+        const double q = mu_aff / mu_curr;
+        sigma = fmin(fmax(q * q * q, 1e-6), 10.0);
+      }
+      st->mu_aff = mu_aff;
+      st->mu_curr = mu_curr;
+      st->mu = fmax(P.c, sigma * mu_curr);
+      break;
+    }
+    case FIN_MU_FULL: {  // MehrotraAdaptiveStep (kernels.jl:309-358)
+      const double cnt = P.a, gamma_f = P.b;
+      const double gamma_a = 1.0 / (1.0 - gamma_f);
+      double mu_full = cnt == 0 ? 0.0 : (res[2] + res[3]) / cnt;
+      mu_full /= gamma_a;
+      const double max_p = st->alpha_aff_p, max_d = st->alpha_aff_d;
+      const int n = D.n, m = D.m, nlb = D.nlb;
+      double ap = 1.0, ad = 1.0;
+      if (max_p < 1.0) {
+        if (st->a_xl <= st->a_xu) {
+          const int k = st->i_xl, i = D.ind_lb[k];
+          const double tmp = mu_full / (D.zl[i] + max_d * D.d[n + m + k]);
+          ap = (D.x[i] - D.xl[i] - tmp) / (-D.d[i]);
+        } else {
+          const int k = st->i_xu, i = D.ind_ub[k];
+          const double tmp = mu_full / (D.zu[i] + max_d * D.d[n + m + nlb + k]);
+          ap = (D.xu[i] - D.x[i] - tmp) / (D.d[i]);
+        }
+      }
+      if (max_d < 1.0) {
+        if (st->a_zl <= st->a_zu) {
+          const int k = st->i_zl, i = D.ind_lb[k];
+          const double tmp = mu_full / (D.x[i] + max_p * D.d[i] - D.xl[i]);
+          ad = -(D.zl[i] - tmp) / D.d[n + m + k];
+        } else {
+          const int k = st->i_zu, i = D.ind_ub[k];
+          const double tmp = mu_full / (D.xu[i] - D.x[i] - max_p * D.d[i]);
+          ad = -(D.zu[i] - tmp) / D.d[n + m + nlb + k];
+        }
+      }
+      st->alpha_p = fmax(ap, gamma_f * max_p);
+      st->alpha_d = fmax(ad, gamma_f * max_d);
+      break;
+    }
+    case FIN_MU_GONDZIO: {
+      const double cnt = P.a;
+      st->mu_aff = cnt == 0 ? 0.0 : (res[2] + res[3]) / cnt;
+      break;
+    }
+    case FIN_EVAL: st->obj_val = P.a + res[0]; break;
+    case FIN_TERM:
+      st->inf_du_raw = res[0];
+      st->inf_compl_raw = res[1];
+      st->inf_pr_raw = res[2];
+      st->dobj = -res[3] + res[4] - res[5];
+      break;
+    case FIN_ZINIT:
+      st->delta_x = fmax(fmax(0.0, -1.5 * res[0]), -1.5 * res[1]);
+      st->delta_s = fmax(fmax(0.0, -1.5 * res[2]), -1.5 * res[3]);
+      break;
+    case FIN_ZSHIFT1: {
+      double mu = 0.0;
+      if (D.nlb > 0) mu += res[0] - res[1];
+      if (D.nub > 0) mu += res[2] - res[3];
+      st->delta_x2 = mu / (2 * (res[4] + res[5]));
+      st->delta_s2 = mu / (2 * (res[6] + res[7]));
+      break;
+    }
+    case FIN_ZSHIFT2: st->init_viol = res[0]; break;
+  }
+}
+
+__global__ void k_copy(double* __restrict__ dst, const double* __restrict__ src, int64_t n) {
+  GRID_LOOP(i, n) dst[i] = src[i];
+}
+__global__ void k_axpy_x(DV D) {
+  GRID_LOOP(i, D.n) D.x[i] += D.d[i];
+}
+__global__ void k_copy_y(DV D) {
+  GRID_LOOP(j, D.m) D.y[j] = D.d[D.n + j];
+}
+// Gondzio: set_extra_correction! (kernels.jl:74-122)
+__global__ void k_extra_corr(DV D, double ap, double ad, double tmin, double tmax) {
+  const int n = D.n, m = D.m, nlb = D.nlb, nub = D.nub;
+  GRID_LOOP(t, (nlb > nub ? nlb : nub)) {
+    if (t < nlb) {
+      const int i = D.ind_lb[t];
+      const double xx = D.x[i] + ap * D.d[i] - D.xl[i];
+      const double zz = D.zl[i] + ad * D.d[n + m + t];
+      const double v = xx * zz;
+      const double del = v < tmin ? tmin - v : (v > tmax ? tmax - v : 0.0);
+      D.corr_lb[t] = D.corr_lb[t] - del;
+    }
+    if (t < nub) {
+      const int i = D.ind_ub[t];
+      const double xx = D.xu[i] - ap * D.d[i] - D.x[i];
+      const double zz = D.zu[i] + ad * D.d[n + m + nlb + t];
+      const double v = xx * zz;
+      const double del = v < tmin ? tmin - v : (v > tmax ? tmax - v : 0.0);
+      D.corr_ub[t] = D.corr_ub[t] + del;
+    }
+  }
+}
+
+double now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+// ======================================================================= host side
+
+MPCSolver::~MPCSolver() {
+  for (auto e : fact_events_) (void)hipEventDestroy(e);
+  if (hst_) (void)hipHostFree(hst_);
+  if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+int MPCSolver::blocks(int64_t n) const {
+  int64_t b = (n + NT - 1) / NT;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(MAXB, b));
+}
+
+static void csr_from_coo(int nrow, const std::vector<int32_t>& r, const std::vector<int32_t>& c,
+                         const std::vector<double>& v, std::vector<int64_t>& rp, std::vector<int32_t>& ci,
+                         std::vector<double>& cv) {
+  // sorted by (row, col), duplicates summed
+  std::vector<int64_t> idx(r.size());
+  for (size_t k = 0; k < idx.size(); ++k) idx[k] = (int64_t)k;
+  std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) {
+    return r[a] != r[b] ? r[a] < r[b] : c[a] < c[b];
+  });
+  rp.assign(nrow + 1, 0);
+  ci.clear();
+  cv.clear();
+  for (size_t q = 0; q < idx.size(); ++q) {
+    const int64_t k = idx[q];
+    if (!ci.empty() && q > 0 && r[idx[q - 1]] == r[k] && ci.back() == c[k]) {
+      cv.back() += v[k];
+      continue;
+    }
+    ci.push_back(c[k]);
+    cv.push_back(v[k]);
+    rp[r[k] + 1]++;
+  }
+  for (int i = 0; i < nrow; ++i) rp[i + 1] += rp[i];
+}
+
+MPCSolver::MPCSolver(const madipm_qp& qp, const madipm_options& opt) : opt_(opt) {
+  const double t0 = now();
+  MADIPM_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  MADIPM_HIP(hipHostMalloc((void**)&hst_, sizeof(DevState), hipHostMallocDefault));
+  std::memset(hst_, 0, sizeof(DevState));
+  setup_host(qp);
+  t_init_ = now() - t0;
+}
+
+// Host-side construction: MPCSolver(...) (structure.jl:79-178), MadNLP.initialize!/set_scaling!
+// [EXT] and the K2 pattern of SparseKKTSystem [EXT].
+void MPCSolver::setup_host(const madipm_qp& q) {
+  H_ = std::make_unique<QPHost>();
+  QPHost& P = *H_;
+  MADIPM_REQUIRE(q.nvar >= 0 && q.ncon >= 0, "negative dimensions");
+  P.nx = q.nvar;
+  P.m = q.ncon;
+  const int nx = P.nx, m = P.m;
+  auto cp = [](const double* a, int64_t n, double dflt = 0.0) {
+    std::vector<double> v(n, dflt);
+    if (a) std::copy(a, a + n, v.begin());
+    return v;
+  };
+  P.c = cp(q.c, nx);
+  P.lvar = cp(q.lvar, nx, -INF);
+  P.uvar = cp(q.uvar, nx, INF);
+  P.lcon = cp(q.lcon, m, -INF);
+  P.ucon = cp(q.ucon, m, INF);
+  P.x0 = cp(q.x0, nx);
+  P.y0 = cp(q.y0, m);
+  P.c0 = q.c0;
+  P.minimize = q.minimize != 0;
+  P.sgn = P.minimize ? 1.0 : -1.0;
+  P.Hr.assign(q.Hrows, q.Hrows + q.nnzh);
+  P.Hc.assign(q.Hcols, q.Hcols + q.nnzh);
+  P.Hv.assign(q.Hvals, q.Hvals + q.nnzh);
+  P.Ar.assign(q.Arows, q.Arows + q.nnzj);
+  P.Ac.assign(q.Acols, q.Acols + q.nnzj);
+  P.Av.assign(q.Avals, q.Avals + q.nnzj);
+  for (int64_t k = 0; k < q.nnzh; ++k)
+    MADIPM_REQUIRE(P.Hr[k] >= P.Hc[k] && P.Hr[k] < nx && P.Hc[k] >= 0, "H must be lower-triangular COO in range");
+  for (int64_t k = 0; k < q.nnzj; ++k)
+    MADIPM_REQUIRE(P.Ar[k] >= 0 && P.Ar[k] < m && P.Ac[k] >= 0 && P.Ac[k] < nx, "A index out of range");
+  // ---- index sets: MadNLP.get_index_constraints (EnforceEquality, MakeParameter) [EXT]
+  for (int i = 0; i < m; ++i)
+    if (P.lcon[i] != P.ucon[i]) P.ind_ineq.push_back(i);
+  P.ns = (int)P.ind_ineq.size();
+  const int n = nx + P.ns;
+  P.n = n;
+  P.xl.resize(n);
+  P.xu.resize(n);
+  for (int i = 0; i < nx; ++i) {
+    P.xl[i] = P.lvar[i];
+    P.xu[i] = P.uvar[i];
+  }
+  for (int k = 0; k < P.ns; ++k) {
+    P.xl[nx + k] = P.lcon[P.ind_ineq[k]];
+    P.xu[nx + k] = P.ucon[P.ind_ineq[k]];
+  }
+  P.fixed.assign(n, 0);
+  for (int i = 0; i < n; ++i) {
+    if (P.xl[i] == P.xu[i]) {
+      P.ind_fixed.push_back(i);
+      P.fixed[i] = 1;
+    } else {
+      if (P.xl[i] != -INF) P.ind_lb.push_back(i);
+      if (P.xu[i] != INF) P.ind_ub.push_back(i);
+    }
+  }
+  // structure.jl:172-173 field swap => update_barrier! tests nlb + nub > 0
+  P.has_ineq = (P.ind_lb.size() + P.ind_ub.size()) > 0;
+  // ---- MadNLP.initialize!(cb, ...) [EXT]
+  P.x.assign(n, 0.0);
+  for (int i = 0; i < nx; ++i) P.x[i] = P.x0[i];
+  for (int i : P.ind_fixed) P.x[i] = P.xl[i];
+  P.y = P.y0;
+  P.rhs.assign(m, 0.0);
+  for (int i = 0; i < m; ++i) P.rhs[i] = (P.lcon[i] == P.ucon[i]) ? P.lcon[i] : 0.0;
+  const double tol = opt_.bound_relax_factor;
+  for (int i = 0; i < n; ++i) {
+    if (P.fixed[i]) continue;
+    if (std::isfinite(P.xl[i])) P.xl[i] = P.xl[i] - tol * std::max(1.0, std::fabs(P.xl[i]));
+    if (std::isfinite(P.xu[i])) P.xu[i] = P.xu[i] + tol * std::max(1.0, std::fabs(P.xu[i]));
+  }
+  if (P.ns) {
+    std::vector<double> ax(m, 0.0);
+    for (size_t k = 0; k < P.Av.size(); ++k) ax[P.Ar[k]] += P.Av[k] * P.x[P.Ac[k]];
+    for (int k = 0; k < P.ns; ++k) P.x[nx + k] = ax[P.ind_ineq[k]];
+  }
+  // initialize_variables! (Ipopt bound push) [EXT]
+  const double bp = opt_.bound_push, bf = opt_.bound_fac;
+  for (int i = 0; i < n; ++i) {
+    if (P.fixed[i]) continue;
+    const double l = P.xl[i], u = P.xu[i];
+    double lo = -INF, hi = INF;
+    if (std::isfinite(l)) {
+      double pl = bp * std::max(1.0, std::fabs(l));
+      if (std::isfinite(u)) pl = std::min(pl, bf * (u - l));
+      lo = l + pl;
+    }
+    if (std::isfinite(u)) {
+      double pu = bp * std::max(1.0, std::fabs(u));
+      if (std::isfinite(l)) pu = std::min(pu, bf * (u - l));
+      hi = u - pu;
+    }
+    P.x[i] = std::min(std::max(P.x[i], lo), hi);
+  }
+  // ---- set_scaling!(..., 100) [EXT] (solver.jl:148-159)
+  P.obj_scale = 1.0;
+  P.con_scale.assign(m, 1.0);
+  if (opt_.scaling) {
+    std::vector<double> g(nx);
+    for (int i = 0; i < nx; ++i) g[i] = P.sgn * P.c[i];
+    for (size_t k = 0; k < P.Hv.size(); ++k) {
+      const int r = P.Hr[k], c = P.Hc[k];
+      const double v = P.sgn * P.Hv[k];
+      g[r] += v * P.x[c];
+      if (r != c) g[c] += v * P.x[r];
+    }
+    double gmax = 0;
+    for (double v : g) gmax = std::max(gmax, std::fabs(v));
+    P.obj_scale = gmax > 0 ? std::min(1.0, 100.0 / gmax) : 1.0;
+    std::vector<double> rowmax(m, 0.0);
+    for (size_t k = 0; k < P.Av.size(); ++k) rowmax[P.Ar[k]] = std::max(rowmax[P.Ar[k]], std::fabs(P.Av[k]));
+    for (int i = 0; i < m; ++i) P.con_scale[i] = std::min(1.0, 100.0 / rowmax[i]);
+    for (int k = 0; k < P.ns; ++k) {
+      const double cs = P.con_scale[P.ind_ineq[k]];
+      P.xl[nx + k] *= cs;
+      P.xu[nx + k] *= cs;
+      P.x[nx + k] *= cs;
+    }
+    for (int i = 0; i < m; ++i) P.rhs[i] *= P.con_scale[i];
+  }
+  obj_scale_ = P.obj_scale;
+
+  // ---- device problem data
+  nx_ = nx;
+  ns_ = P.ns;
+  n_ = n;
+  m_ = m;
+  nlb_ = (int)P.ind_lb.size();
+  nub_ = (int)P.ind_ub.size();
+  L_ = (int64_t)n + m + nlb_ + nub_;
+  // scaled Hessian (full symmetric CSR over n; MakeParameter zeroes fixed rows/cols), diagonal apart
+  std::vector<int32_t> hr, hc;
+  std::vector<double> hv, Hdiag(n, 0.0);
+  std::vector<double> gfix(n, 0.0), cfix(m, 0.0);
+  double const_fixed = 0.0;
+  for (size_t k = 0; k < P.Hv.size(); ++k) {
+    const int r = P.Hr[k], c = P.Hc[k];
+    const double v = P.obj_scale * P.sgn * P.Hv[k];
+    const bool fr = P.fixed[r], fc = P.fixed[c];
+    if (fr && fc) {
+      const_fixed += (r == c ? 0.5 : 1.0) * v * P.x[r] * P.x[c];
+      continue;
+    }
+    if (fr || fc) {  // cross term with a fixed variable -> constant gradient shift
+      if (!fr) gfix[r] += v * P.x[c];
+      if (!fc) gfix[c] += v * P.x[r];
+      continue;
+    }
+    if (r == c) {
+      Hdiag[r] += v;
+      hr.push_back(r);
+      hc.push_back(c);
+      hv.push_back(v);
+    } else {
+      hr.push_back(r);
+      hc.push_back(c);
+      hv.push_back(v);
+      hr.push_back(c);
+      hc.push_back(r);
+      hv.push_back(v);
+    }
+  }
+  std::vector<int64_t> Hrp;
+  std::vector<int32_t> Hci;
+  std::vector<double> Hcv;
+  csr_from_coo(n, hr, hc, hv, Hrp, Hci, Hcv);
+  // scaled Jacobian with slack columns (m x n); fixed columns zeroed (their term -> cfix)
+  std::vector<int32_t> jr, jc;
+  std::vector<double> jv;
+  for (size_t k = 0; k < P.Av.size(); ++k) {
+    const int r = P.Ar[k], c = P.Ac[k];
+    const double v = P.con_scale[r] * P.Av[k];
+    if (P.fixed[c]) {
+      cfix[r] += v * P.x[c];
+      continue;
+    }
+    jr.push_back(r);
+    jc.push_back(c);
+    jv.push_back(v);
+  }
+  for (int k = 0; k < P.ns; ++k) {
+    jr.push_back(P.ind_ineq[k]);
+    jc.push_back(nx + k);
+    jv.push_back(-1.0);
+  }
+  std::vector<int64_t> Jrp, JTrp;
+  std::vector<int32_t> Jci, JTci;
+  std::vector<double> Jcv, JTcv;
+  csr_from_coo(m, jr, jc, jv, Jrp, Jci, Jcv);
+  csr_from_coo(n, jc, jr, jv, JTrp, JTci, JTcv);
+  std::vector<double> cs(n, 0.0);
+  for (int i = 0; i < nx; ++i) cs[i] = P.obj_scale * P.sgn * P.c[i];
+  c0s_ = P.obj_scale * (P.sgn * P.c0) + const_fixed;
+  // K2 lower CSC: diag(n+m) + H strictly-lower + J at rows n+r  (SparseKKTSystem [EXT])
+  std::vector<int32_t> kr, kc;
+  std::vector<double> kv;
+  for (int i = 0; i < n + m; ++i) {
+    kr.push_back(i);
+    kc.push_back(i);
+    kv.push_back(0.0);
+  }
+  for (int i = 0; i < n; ++i)
+    for (int64_t q = Hrp[i]; q < Hrp[i + 1]; ++q)
+      if (Hci[q] < i) {
+        kr.push_back(i);
+        kc.push_back(Hci[q]);
+        kv.push_back(Hcv[q]);
+      }
+  for (int r = 0; r < m; ++r)
+    for (int64_t q = Jrp[r]; q < Jrp[r + 1]; ++q) {
+      kr.push_back(n + r);
+      kc.push_back(Jci[q]);
+      kv.push_back(Jcv[q]);
+    }
+  // CSC = CSR of the transpose pattern (col-major)
+  std::vector<int64_t> Kcp;
+  std::vector<int32_t> Kri;
+  std::vector<double> Kv;
+  csr_from_coo(n + m, kc, kr, kv, Kcp, Kri, Kv);
+  nnzK_ = (int64_t)Kri.size();
+  std::vector<int64_t> diag_pos(n + m, -1);
+  for (int j = 0; j < n + m; ++j)
+    for (int64_t q = Kcp[j]; q < Kcp[j + 1]; ++q)
+      if (Kri[q] == j) diag_pos[j] = q;
+  for (int j = 0; j < n + m; ++j) MADIPM_REQUIRE(diag_pos[j] >= 0, "missing KKT diagonal");
+
+  // ---- LDL^T symbolic analysis + device plan (linear-solver constructor)
+  SymbolicOptions so;
+  so.ordering = opt_.ldl.ordering;
+  so.dense_alpha = opt_.ldl.dense_alpha;
+  so.relax = opt_.ldl.relax;
+  so.small_front_max = opt_.ldl.small_front_max;
+  ldl_ = std::make_unique<LDLSolver>(n + m, Kcp.data(), Kri.data(), so, opt_.ldl.pivot_tol);
+
+  // ---- uploads
+  std::vector<int32_t> lbpos(n, -1), ubpos(n, -1);
+  for (int k = 0; k < nlb_; ++k) lbpos[P.ind_lb[k]] = k;
+  for (int k = 0; k < nub_; ++k) ubpos[P.ind_ub[k]] = k;
+  hipStream_t s = stream_;
+  auto up = [&](auto& buf, const auto& vec, size_t minlen = 1) {
+    using T = typename std::decay_t<decltype(vec)>::value_type;
+    buf.alloc(std::max(vec.size(), minlen));
+    if (!vec.empty()) MADIPM_HIP(hipMemcpyAsync(buf.p, vec.data(), vec.size() * sizeof(T), hipMemcpyHostToDevice, s));
+  };
+  up(x_, P.x);
+  up(xl_, P.xl);
+  up(xu_, P.xu);
+  up(y_, P.y);
+  up(rhs_, P.rhs);
+  up(Hdiag_, Hdiag);
+  up(cs_, cs);
+  up(gfix_, gfix);
+  up(cfix_, cfix);
+  up(diag_pos_, diag_pos);
+  up(Kx_, Kv);
+  up(ind_lb_, P.ind_lb);
+  up(ind_ub_, P.ind_ub);
+  up(lbpos_, lbpos);
+  up(ubpos_, ubpos);
+  up(fixed_, P.fixed);
+  up(Hrp_, Hrp);
+  up(Hci_, Hci);
+  up(Hv_, Hcv);
+  up(Jrp_, Jrp);
+  up(Jci_, Jci);
+  up(Jv_, Jcv);
+  up(JTrp_, JTrp);
+  up(JTci_, JTci);
+  up(JTv_, JTcv);
+  auto zeros = [&](DBuf<double>& b, int64_t len) {
+    b.alloc(std::max<int64_t>(len, 1));
+    b.zero(s);
+  };
+  zeros(zl_, n);
+  zeros(zu_, n);
+  zeros(f_, n);
+  zeros(jacl_, n);
+  zeros(c_, m);
+  zeros(pr_diag_, n);
+  zeros(l_diag_, nlb_);
+  zeros(u_diag_, nub_);
+  zeros(l_lower_, nlb_);
+  zeros(u_lower_, nub_);
+  zeros(d_, L_);
+  zeros(p_, L_);
+  zeros(dsave_, L_);
+  zeros(corr_lb_, nlb_);
+  zeros(corr_ub_, nub_);
+  part_.alloc(MAXB * NPART);
+  st_.alloc(1);
+  st_.zero(s);
+  MADIPM_HIP(hipStreamSynchronize(s));
+  // norm_b (solver.jl:173) on host
+  norm_b_ = 0;
+  for (double v : P.rhs) norm_b_ = std::max(norm_b_, std::fabs(v));
+}
+
+// Launch helpers (the DV view is rebuilt from member buffers; cheap, host-only)
+#define DV_ARGS                                                                                         \
+  DV D;                                                                                                 \
+  D.n = n_;                                                                                             \
+  D.m = m_;                                                                                             \
+  D.nx = nx_;                                                                                           \
+  D.nlb = nlb_;                                                                                         \
+  D.nub = nub_;                                                                                         \
+  D.x = x_;                                                                                             \
+  D.xl = xl_;                                                                                           \
+  D.xu = xu_;                                                                                           \
+  D.zl = zl_;                                                                                           \
+  D.zu = zu_;                                                                                           \
+  D.f = f_;                                                                                             \
+  D.jacl = jacl_;                                                                                       \
+  D.c = c_;                                                                                             \
+  D.y = y_;                                                                                             \
+  D.rhs = rhs_;                                                                                         \
+  D.pr_diag = pr_diag_;                                                                                 \
+  D.l_diag = l_diag_;                                                                                   \
+  D.u_diag = u_diag_;                                                                                   \
+  D.l_lower = l_lower_;                                                                                 \
+  D.u_lower = u_lower_;                                                                                 \
+  D.d = d_;                                                                                             \
+  D.p = p_;                                                                                             \
+  D.corr_lb = corr_lb_;                                                                                 \
+  D.corr_ub = corr_ub_;                                                                                 \
+  D.Kx = Kx_;                                                                                           \
+  D.diag_pos = diag_pos_;                                                                               \
+  D.Hdiag = Hdiag_;                                                                                     \
+  D.cs = cs_;                                                                                           \
+  D.gfix = gfix_;                                                                                       \
+  D.cfix = cfix_;                                                                                       \
+  D.ind_lb = ind_lb_;                                                                                   \
+  D.ind_ub = ind_ub_;                                                                                   \
+  D.lbpos = lbpos_;                                                                                     \
+  D.ubpos = ubpos_;                                                                                     \
+  D.fixed = fixed_;                                                                                     \
+  D.H = DCsr{Hrp_, Hci_, Hv_};                                                                          \
+  D.J = DCsr{Jrp_, Jci_, Jv_};                                                                          \
+  D.JT = DCsr{JTrp_, JTci_, JTv_};                                                                      \
+  D.part = part_;                                                                                       \
+  D.st = st_;
+
+void MPCSolver::kkt_diag(double dw, double dc) {
+  DV_ARGS;
+  k_diag<<<blocks(n_ + m_), NT, 0, stream_>>>(D, dw, dc);
+}
+
+void MPCSolver::launch_reduce_final(int kind, int nb) {
+  DV_ARGS;
+  FinParams P{nb, 0, 0, 0, 0};
+  if (kind == FIN_MU_PRED) {
+    P.a = (double)(nlb_ + nub_);
+    P.b = H_->has_ineq ? 1.0 : 0.0;
+    P.c = opt_.mu_min;
+  } else if (kind == FIN_MU_FULL) {
+    P.a = (double)(nlb_ + nub_);
+    P.b = opt_.step_tau;
+  } else if (kind == FIN_MU_GONDZIO) {
+    P.a = (double)(nlb_ + nub_);
+  } else if (kind == FIN_EVAL) {
+    P.a = c0s_;
+  } else if (kind == FIN_RESID) {
+    P.a = opt_.check_residual ? opt_.tol_linear_solve : 0.0;
+  }
+  k_final<<<1, NT, 0, stream_>>>(D, kind, P);
+}
+
+// solve_system! (linear_solver.jl:19-44): rhs (mode) -> LDL^T solve -> finish + residual
+void MPCSolver::solve_system(int mode, double mu) {
+  DV_ARGS;
+  const int nb = blocks(n_ + m_);
+  k_rhs<<<nb, NT, 0, stream_>>>(D, mode, mu);
+  ldl_->solve_async(d_.p, stream_);
+  k_residual<<<nb, NT, 0, stream_>>>(D, del_w_, del_c_);
+  launch_reduce_final(FIN_RESID, nb);
+}
+
+// gondzio_correction_direction! (solver.jl:245-298): host-controlled loop, one read-back per solve
+void MPCSolver::gondzio() {
+  DV_ARGS;
+  hipStream_t s = stream_;
+  const double delta = 0.1, bmin = 0.1, bmax = 10.0, tau = 0.995;
+  const int nbz = blocks(std::max(nlb_, nub_));
+  auto ftb = [&](double& ap, double& ad) {  // get_fraction_to_boundary_step(solver, tau)
+    k_alpha<<<nbz, NT, 0, s>>>(D, ALPHA_GONDZIO, tau);
+    FinParams P{nbz, ALPHA_GONDZIO, 0, 0, 0};
+    k_final<<<1, NT, 0, s>>>(D, FIN_ALPHA, P);
+    read_state();
+    MADIPM_HIP(hipStreamSynchronize(s));
+    ap = hst_->alpha_aff_p;
+    ad = hst_->alpha_aff_d;
+  };
+  double ap, ad;
+  ftb(ap, ad);
+  for (int nc = 0; nc < opt_.max_ncorr; ++nc) {
+    const double tap = std::min(ap + delta, 1.0), tad = std::min(ad + delta, 1.0);
+    k_mu<<<nbz, NT, 0, s>>>(D, 0, tap, tad);
+    launch_reduce_final(FIN_MU_GONDZIO, nbz);
+    read_state();
+    MADIPM_HIP(hipStreamSynchronize(s));
+    const double ga = hst_->mu_aff, g = hst_->mu_curr;
+    const double mu = (ga / g) * (ga / g) * ga;  // Eq. (12)
+    k_extra_corr<<<nbz, NT, 0, s>>>(D, tap, tad, bmin * mu, bmax * mu);
+    k_copy<<<blocks(L_), NT, 0, s>>>(dsave_, d_, L_);  // copyto!(dp, d.values) happens before the solve
+    solve_system(RHS_GONDZIO, mu);
+    double hap, had;
+    ftb(hap, had);
+    if (hap < 1.005 * ap || had < 1.005 * ad) {
+      k_copy<<<blocks(L_), NT, 0, s>>>(d_, dsave_, L_);
+      break;
+    }
+    ap = hap;
+    ad = had;
+  }
+}
+
+void MPCSolver::read_state() {
+  MADIPM_HIP(hipMemcpyAsync(hst_, st_.p, sizeof(DevState), hipMemcpyDeviceToHost, stream_));
+}
+
+// factorize_system! (solver.jl:299-303) is split: the regularization update is done by the caller.
+void MPCSolver::factorize_regularized() {
+  for (int trial = 0; trial < 3; ++trial) {  // linear_solver.jl:6-17
+    kkt_diag(del_w_, del_c_);
+    hipEvent_t e0, e1;
+    MADIPM_HIP(hipEventCreate(&e0));
+    MADIPM_HIP(hipEventCreate(&e1));
+    MADIPM_HIP(hipEventRecord(e0, stream_));
+    ldl_->factorize_async(Kx_.p, stream_);
+    MADIPM_HIP(hipEventRecord(e1, stream_));
+    fact_events_.push_back(e0);
+    fact_events_.push_back(e1);
+    read_state();
+    if (ldl_->status(stream_) == 0) return;
+    del_w_ *= 100.0;
+    del_c_ *= 100.0;
+  }
+}
+
+void MPCSolver::init_starting_point() {
+  DV_ARGS;
+  const int nb = blocks(n_ + m_), nbn = blocks(n_);
+  hipStream_t s = stream_;
+  k_init_kkt<<<nb, NT, 0, s>>>(D, del_w_, del_c_);
+  hipEvent_t e0, e1;
+  MADIPM_HIP(hipEventCreate(&e0));
+  MADIPM_HIP(hipEventCreate(&e1));
+  MADIPM_HIP(hipEventRecord(e0, s));
+  ldl_->factorize_async(Kx_.p, s);
+  MADIPM_HIP(hipEventRecord(e1, s));
+  fact_events_.push_back(e0);
+  fact_events_.push_back(e1);
+  ldl_->status(s);  // init factorization: the reference does not retry here
+  // Step 1: least-squares primal correction
+  k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_PRIMAL, 0.0);
+  ldl_->solve_async(d_.p, s);
+  k_residual<<<nb, NT, 0, s>>>(D, del_w_, del_c_);
+  launch_reduce_final(FIN_RESID, nb);
+  k_axpy_x<<<nbn, NT, 0, s>>>(D);
+  // Step 2: dual least squares
+  k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_DUAL, 0.0);
+  ldl_->solve_async(d_.p, s);
+  k_residual<<<nb, NT, 0, s>>>(D, del_w_, del_c_);
+  launch_reduce_final(FIN_RESID, nb);
+  k_copy_y<<<blocks(m_), NT, 0, s>>>(D);
+  // Step 3: bound multipliers and shifts
+  k_zinit<<<nbn, NT, 0, s>>>(D);
+  launch_reduce_final(FIN_ZINIT, nbn);
+  k_zshift1<<<nbn, NT, 0, s>>>(D);
+  launch_reduce_final(FIN_ZSHIFT1, nbn);
+  k_zshift2<<<nbn, NT, 0, s>>>(D, opt_.bound_fac);
+  launch_reduce_final(FIN_ZSHIFT2, nbn);
+  read_state();
+  MADIPM_HIP(hipStreamSynchronize(s));
+  if (hst_->nan_flag) throw Error("SolveException in init_starting_point!", -4);
+  MADIPM_REQUIRE(hst_->init_viol == 0.0, "init_starting_point!: interior assertion failed");
+}
+
+void MPCSolver::initialize() {
+  DV_ARGS;
+  hipStream_t s = stream_;
+  // init_regularization! (kernels.jl:364-392)
+  switch (opt_.regularization) {
+    case 0: del_w_ = 1.0; del_c_ = 0.0; break;
+    case 1: del_w_ = 1.0; del_c_ = opt_.delta_d; break;
+    default:
+      adapt_dp_ = opt_.delta_p;
+      adapt_dd_ = opt_.delta_d;
+      adapt_dmin_ = opt_.delta_min;
+      del_w_ = 1.0;
+      del_c_ = opt_.delta_d;
+  }
+  k_set_mu<<<1, 1, 0, s>>>(st_, 0.0);
+  // callbacks at the initial point (solver.jl:166-170)
+  const int nb = blocks(n_ + m_);
+  k_eval<<<nb, NT, 0, s>>>(D);
+  launch_reduce_final(FIN_EVAL, nb);
+  // norm_c = ||primal(f)||_inf (solver.jl:174)
+  std::vector<double> fh(n_);
+  if (n_) MADIPM_HIP(hipMemcpyAsync(fh.data(), f_.p, sizeof(double) * n_, hipMemcpyDeviceToHost, s));
+  MADIPM_HIP(hipStreamSynchronize(s));
+  norm_c_ = 0;
+  for (double v : fh) norm_c_ = std::max(norm_c_, std::fabs(v));
+  init_starting_point();
+  k_set_mu<<<1, 1, 0, s>>>(st_, opt_.mu_init);  // solver.jl:179
+  k_jtprod<<<blocks(n_), NT, 0, s>>>(D);        // solver.jl:187
+  best_compl_ = INF;
+  status_ = MADIPM_REGULAR;
+  k_ = 0;
+}
+
+int MPCSolver::solve(madipm_stats* stats) {
+  DV_ARGS;
+  hipStream_t s = stream_;
+  const double t0 = now();
+  trace_.clear();
+  int status = MADIPM_REGULAR;
+  double tstart = now();
+  try {
+    initialize();
+    MADIPM_HIP(hipStreamSynchronize(s));
+    t_init_ += now() - t0;
+    tstart = now();  // solver.jl:181
+    const int nb = blocks(n_ + m_), nbz = blocks(std::max(nlb_, nub_));
+    while (true) {
+      // ---- update_termination_criteria! (+ speculative factorization of this iteration)
+      k_term<<<nb, NT, 0, s>>>(D);
+      launch_reduce_final(FIN_TERM, nb);
+      const double del_w_print = del_w_;
+      // factorize_system! = update_regularization! + factorize_regularized_system!
+      double save_w = del_w_, save_c = del_c_;
+      switch (opt_.regularization) {
+        case 0: del_w_ = 0.0; del_c_ = 0.0; break;
+        case 1: del_w_ = opt_.delta_p; del_c_ = opt_.delta_d; break;
+        default:
+          adapt_dp_ = std::max(adapt_dp_ / 10.0, adapt_dmin_);
+          adapt_dd_ = std::min(adapt_dd_ / 10.0, -adapt_dmin_);
+          del_w_ = adapt_dp_;
+          del_c_ = adapt_dd_;
+      }
+      // first trial enqueued together with the state read-back: ONE sync per iteration
+      kkt_diag(del_w_, del_c_);
+      hipEvent_t e0, e1;
+      MADIPM_HIP(hipEventCreate(&e0));
+      MADIPM_HIP(hipEventCreate(&e1));
+      MADIPM_HIP(hipEventRecord(e0, s));
+      ldl_->factorize_async(Kx_.p, s);
+      MADIPM_HIP(hipEventRecord(e1, s));
+      fact_events_.push_back(e0);
+      fact_events_.push_back(e1);
+      read_state();
+      const int frc = ldl_->status(s);  // synchronizes the stream
+      const DevState& h = *hst_;
+      if (h.nan_flag) {
+        status = MADIPM_ERROR_IN_STEP_COMPUTATION;
+        break;
+      }
+      const double dobj = h.dobj;
+      inf_pr_ = h.inf_pr_raw / std::max(1.0, norm_b_);
+      inf_du_ = h.inf_du_raw / std::max(1.0, norm_c_);
+      inf_compl_ = h.inf_compl_raw / std::max(1.0, norm_c_);
+      best_compl_ = std::min(best_compl_, inf_compl_);
+      const double obj_val = h.obj_val;
+      madipm_iter_trace tr{k_, obj_val / obj_scale_, inf_pr_, inf_du_, inf_compl_, h.mu, h.alpha_p, h.alpha_d,
+                           del_w_print, k_ == 0 ? 0.0 : h.dx_inf, h.max_res_ratio};
+      trace_.push_back(tr);
+      if (opt_.print_level > 0) {
+        if (k_ % 10 == 0) std::printf("iter    objective    inf_pr   inf_du lg(mu)  ||d||  lg(rg) alpha_du alpha_pr\n");
+        char rg[16];
+        if (del_w_print == 0)
+          std::snprintf(rg, sizeof rg, "   - ");
+        else
+          std::snprintf(rg, sizeof rg, "%5.1f", std::log10(del_w_print));
+        std::printf("%4d % 10.7e %6.2e %6.2e %5.1f %6.2e %s %6.2e %6.2e\n", k_, obj_val / obj_scale_, inf_pr_,
+                    inf_du_, std::log10(h.mu), tr.dx_inf, rg, h.alpha_d, h.alpha_p);
+      }
+      if (std::max(inf_pr_, std::max(inf_du_, inf_compl_)) <= opt_.tol) {
+        status = MADIPM_SOLVE_SUCCEEDED;
+      } else if (inf_compl_ > opt_.divergence_tol * best_compl_ && dobj > std::max(10.0 * std::fabs(obj_val), 1.0)) {
+        status = MADIPM_INFEASIBLE_PROBLEM_DETECTED;
+      } else if (obj_val < -opt_.divergence_tol * std::max(std::max(10.0, std::fabs(dobj)), 1.0)) {
+        status = MADIPM_DIVERGING_ITERATES;
+      } else if (k_ >= opt_.max_iter) {
+        status = MADIPM_MAXIMUM_ITERATIONS_EXCEEDED;
+      } else if (now() - tstart >= opt_.max_wall_time) {
+        status = MADIPM_MAXIMUM_WALLTIME_EXCEEDED;
+      }
+      if (status != MADIPM_REGULAR) {
+        del_w_ = save_w;
+        del_c_ = save_c;
+        break;
+      }
+      if (frc != 0) {  // remaining trials of factorize_regularized_system!
+        bool ok = false;
+        for (int trial = 1; trial < 3 && !ok; ++trial) {
+          del_w_ *= 100.0;
+          del_c_ *= 100.0;
+          kkt_diag(del_w_, del_c_);
+          ldl_->factorize_async(Kx_.p, s);
+          ok = ldl_->status(s) == 0;
+        }
+        if (!ok) {
+          del_w_ *= 100.0;
+          del_c_ *= 100.0;
+        }
+      }
+      k_reset_iter<<<1, 1, 0, s>>>(st_);
+      // ---- prediction_step! (solver.jl:230-237)
+      solve_system(RHS_PRED, 0.0);
+      k_alpha<<<nbz, NT, 0, s>>>(D, ALPHA_PRED, 1.0);
+      {
+        FinParams P{nbz, ALPHA_PRED, 0, 0, 0};
+        k_final<<<1, NT, 0, s>>>(D, FIN_ALPHA, P);
+      }
+      // mu_affine at (alpha_aff_p, alpha_aff_d) and mu_curr; the alphas never leave the device
+      k_mu<<<nbz, NT, 0, s>>>(D, 1, 0.0, 0.0);
+      launch_reduce_final(FIN_MU_PRED, nbz);
+      // ---- mehrotra_correction_direction! (solver.jl:239-243)
+      solve_system(RHS_CORR, 0.0);
+      // ---- gondzio_correction_direction! (solver.jl:245-298)
+      if (opt_.max_ncorr > 0) gondzio();
+      // ---- update_step_size! (solver.jl:304-307)
+      if (opt_.step_rule == 2) {
+        k_alpha<<<nbz, NT, 0, s>>>(D, ALPHA_MEHROTRA, 1.0);
+        FinParams P{nbz, ALPHA_MEHROTRA, 0, 0, 0};
+        k_final<<<1, NT, 0, s>>>(D, FIN_ALPHA, P);
+        k_mu<<<nbz, NT, 0, s>>>(D, 1, 0.0, 0.0);
+        launch_reduce_final(FIN_MU_FULL, nbz);
+      } else {
+        const int mode = opt_.step_rule == 0 ? ALPHA_CONSERVATIVE : ALPHA_ADAPTIVE;
+        k_alpha<<<nbz, NT, 0, s>>>(D, mode, opt_.step_tau);
+        FinParams P{nbz, mode, 0, 0, 0};
+        k_final<<<1, NT, 0, s>>>(D, FIN_ALPHA, P);
+      }
+      // ---- apply_step! + evaluate_model!
+      k_apply<<<nb, NT, 0, s>>>(D);
+      ++k_;
+      k_eval<<<nb, NT, 0, s>>>(D);
+      launch_reduce_final(FIN_EVAL, nb);
+      MADIPM_HIP(hipGetLastError());
+    }
+  } catch (const Error& e) {
+    if (e.code == -4)
+      status = MADIPM_ERROR_IN_STEP_COMPUTATION;
+    else
+      throw;
+  }
+  MADIPM_HIP(hipStreamSynchronize(s));
+  t_total_ = now() - tstart;
+  status_ = status;
+  t_linsol_ = 0;
+  for (size_t q = 0; q + 1 < fact_events_.size(); q += 2) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, fact_events_[q], fact_events_[q + 1]) == hipSuccess) t_linsol_ += ms * 1e-3;
+  }
+  if (stats) {
+    read_state();
+    MADIPM_HIP(hipStreamSynchronize(s));
+    stats->status = status;
+    stats->iter = k_;
+    double obj = hst_->obj_val / obj_scale_;
+    if (!H_->minimize) obj = -obj;
+    stats->objective = obj;
+    stats->dual_objective = hst_->dobj / obj_scale_;
+    stats->inf_pr = inf_pr_;
+    stats->inf_du = inf_du_;
+    stats->inf_compl = inf_compl_;
+    stats->mu = hst_->mu;
+    stats->total_time = t_total_;
+    stats->linear_solver_time = t_linsol_;
+    stats->init_time = t_init_;
+  }
+  return status;
+}
+
+}  // namespace madipm
+
+namespace madipm {
+
+// update_solution! (src/utils.jl:150-156) + MadNLP.update! [EXT]: un-scaled primal/dual solution
+void MPCSolver::get_solution(double* x, double* y, double* zl, double* zu, double* cons) {
+  MADIPM_HIP(hipStreamSynchronize(stream_));
+  const QPHost& P = *H_;
+  std::vector<double> xh(n_), yh(m_), zlh(n_), zuh(n_);
+  if (n_) {
+    MADIPM_HIP(hipMemcpy(xh.data(), x_.p, sizeof(double) * n_, hipMemcpyDeviceToHost));
+    MADIPM_HIP(hipMemcpy(zlh.data(), zl_.p, sizeof(double) * n_, hipMemcpyDeviceToHost));
+    MADIPM_HIP(hipMemcpy(zuh.data(), zu_.p, sizeof(double) * n_, hipMemcpyDeviceToHost));
+  }
+  if (m_) MADIPM_HIP(hipMemcpy(yh.data(), y_.p, sizeof(double) * m_, hipMemcpyDeviceToHost));
+  if (x) std::copy(xh.begin(), xh.begin() + nx_, x);
+  if (zl)
+    for (int i = 0; i < nx_; ++i) zl[i] = zlh[i] / obj_scale_;
+  if (zu)
+    for (int i = 0; i < nx_; ++i) zu[i] = zuh[i] / obj_scale_;
+  if (y)
+    for (int j = 0; j < m_; ++j) y[j] = yh[j] * P.con_scale[j] / obj_scale_;
+  if (cons) {
+    std::fill(cons, cons + m_, 0.0);
+    for (size_t k = 0; k < P.Av.size(); ++k) cons[P.Ar[k]] += P.Av[k] * xh[P.Ac[k]];
+  }
+}
+
+}  // namespace madipm

@@ -1,0 +1,96 @@
+// Native Mehrotra predictor-corrector driver (restates MadIPM's `mpc!`, src/solver.jl:332-360)
+// on top of the HIP LDL^T and the fused IPM vector kernels.  All vectors stay in HBM; scalar
+// reductions land in a device-resident state block; the host reads ONE small block per iteration.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/madipm_hip.h"
+#include "common.hpp"
+#include "ldl.hpp"
+
+namespace madipm {
+
+struct Csr {
+  int64_t* rp = nullptr;
+  int32_t* ci = nullptr;
+  double* v = nullptr;
+};
+
+// Device-resident scalars (one struct, copied to host once per iteration).
+struct DevState {
+  double mu, mu_curr, mu_aff;
+  double alpha_p, alpha_d;            // final step
+  double alpha_aff_p, alpha_aff_d;    // predictor (tau = 1)
+  double a_xl, a_xu, a_zl, a_zu;      // last ratio test pieces
+  double obj_val;
+  double inf_pr_raw, inf_du_raw, inf_compl_raw, dobj;
+  double res_ratio;                   // last solve_system! residual ratio
+  double max_res_ratio;               // max over the iteration's solves
+  double dx_inf;                      // ||primal(d)||_inf (print_iter)
+  double delta_x, delta_s, delta_x2, delta_s2;  // init_starting_point! shifts
+  double init_viol;                   // init assertion violations
+  int32_t i_xl, i_xu, i_zl, i_zu;     // argmin indices (-1 = init element)
+  int32_t nan_flag;
+  int32_t pad;
+};
+
+struct QPHost;  // host copy of the problem (mpc.hip)
+
+class MPCSolver {
+ public:
+  MPCSolver(const madipm_qp& qp, const madipm_options& opt);
+  ~MPCSolver();
+  int solve(madipm_stats* stats);
+  void get_solution(double* x, double* y, double* zl, double* zu, double* cons);
+  const std::vector<madipm_iter_trace>& trace() const { return trace_; }
+  LDLSolver& ldl() { return *ldl_; }
+  hipStream_t stream() const { return stream_; }
+
+ private:
+  void setup_host(const madipm_qp& qp);
+  void initialize();
+  void init_starting_point();
+  void factorize_regularized();
+  void solve_system(int mode, double mu);
+  void gondzio();
+  void launch_reduce_final(int kind, int nvals);
+  void read_state();
+  void kkt_diag(double dw, double dc);
+  int blocks(int64_t n) const;
+
+  madipm_options opt_{};
+  hipStream_t stream_ = nullptr;
+  std::unique_ptr<QPHost> H_;
+  std::unique_ptr<LDLSolver> ldl_;
+  // sizes
+  int nx_ = 0, ns_ = 0, n_ = 0, m_ = 0, nlb_ = 0, nub_ = 0;
+  int64_t nnzK_ = 0, L_ = 0;  // L_ = unreduced vector length
+  // device vectors
+  DBuf<double> x_, xl_, xu_, zl_, zu_, f_, jacl_, c_, y_, rhs_, pr_diag_, l_diag_, u_diag_, l_lower_, u_lower_;
+  DBuf<double> d_, p_, corr_lb_, corr_ub_, dsave_;
+  DBuf<double> Kx_, Hdiag_, cs_, gfix_, cfix_, lo_full_, hi_full_;
+  DBuf<int64_t> diag_pos_;
+  DBuf<int32_t> ind_lb_, ind_ub_, lbpos_, ubpos_;
+  DBuf<uint8_t> fixed_;
+  DBuf<int64_t> Hrp_, Jrp_, JTrp_;
+  DBuf<int32_t> Hci_, Jci_, JTci_;
+  DBuf<double> Hv_, Jv_, JTv_;
+  DBuf<double> part_;
+  DBuf<DevState> st_;
+  DevState* hst_ = nullptr;
+  // host scalars (MPCSolver fields of src/structure.jl:62-76)
+  double del_w_ = 0, del_c_ = 0, norm_b_ = 0, norm_c_ = 0, best_compl_ = 0, obj_scale_ = 1, c0s_ = 0;
+  double adapt_dp_ = 0, adapt_dd_ = 0, adapt_dmin_ = 0;
+  int status_ = 0, k_ = 0;
+  double inf_pr_ = 0, inf_du_ = 0, inf_compl_ = 0;
+  double t_init_ = 0, t_total_ = 0, t_linsol_ = 0;
+  std::vector<madipm_iter_trace> trace_;
+  std::vector<hipEvent_t> fact_events_;
+};
+
+}  // namespace madipm
