@@ -162,12 +162,18 @@ typedef struct madipm_iter_trace {
 typedef struct madipm_solver* madipm_solver_t;
 void madipm_default_options(madipm_options* opt);
 int madipm_solver_create(const madipm_qp* qp, const madipm_options* opt, madipm_solver_t* out);
+/* initialize! alone (src/solver.jl:127-189); the next solve() then runs only the MPC loop.
+ * Without it, solve() initializes first (as solve! does). */
+int madipm_solver_initialize(madipm_solver_t s);
+int madipm_solver_set_max_iter(madipm_solver_t s, int32_t max_iter);
 int madipm_solver_solve(madipm_solver_t s, madipm_stats* stats);
 /* any pointer may be NULL: x/zl/zu length nvar, y/cons length ncon (un-scaled, as MadNLP stats) */
 int madipm_solver_get_solution(madipm_solver_t s, double* x, double* y, double* zl, double* zu, double* cons);
 /* copies up to cap records, returns the number of recorded iterations */
 int madipm_solver_trace(madipm_solver_t s, madipm_iter_trace* out, int32_t cap);
 int madipm_solver_ldl_info(madipm_solver_t s, madipm_ldl_info* info);
+/* fill-reducing pivot order of the K2 factorization (length nvar_std + ncon, K2 unknowns [x; y]) */
+int madipm_solver_ldl_perm(madipm_solver_t s, int32_t* perm);
 void madipm_solver_destroy(madipm_solver_t s);
 
 #ifdef __cplusplus

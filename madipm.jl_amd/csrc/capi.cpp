@@ -281,6 +281,22 @@ int madipm_solver_create(const madipm_qp* qp, const madipm_options* opt, madipm_
   MADIPM_API_END
 }
 
+int madipm_solver_initialize(madipm_solver_t s) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(s, "null handle");
+  s->s->initialize_public();
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_solver_set_max_iter(madipm_solver_t s, int32_t max_iter) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(s && max_iter >= 0, "bad argument");
+  s->s->set_max_iter(max_iter);
+  return 0;
+  MADIPM_API_END
+}
+
 int madipm_solver_solve(madipm_solver_t s, madipm_stats* stats) {
   MADIPM_API_BEGIN
   MADIPM_REQUIRE(s, "null handle");
@@ -321,6 +337,15 @@ int madipm_solver_ldl_info(madipm_solver_t s, madipm_ldl_info* info) {
   info->max_front = p.max_front;
   info->nbig = p.nbig;
   info->arena_bytes = p.arena_size * 8;
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_solver_ldl_perm(madipm_solver_t s, int32_t* perm) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(s && perm, "null argument");
+  const auto& p = s->s->ldl().plan().perm;
+  std::memcpy(perm, p.data(), sizeof(int32_t) * p.size());
   return 0;
   MADIPM_API_END
 }

@@ -1290,6 +1290,19 @@ void MPCSolver::init_starting_point() {
 void MPCSolver::initialize() {
   DV_ARGS;
   hipStream_t s = stream_;
+  {  // restart from the problem's initial point (solve! always restarts)
+    const QPHost& P = *H_;
+    MADIPM_HIP(hipMemcpyAsync(x_.p, P.x.data(), sizeof(double) * n_, hipMemcpyHostToDevice, s));
+    MADIPM_HIP(hipMemcpyAsync(xl_.p, P.xl.data(), sizeof(double) * n_, hipMemcpyHostToDevice, s));
+    MADIPM_HIP(hipMemcpyAsync(xu_.p, P.xu.data(), sizeof(double) * n_, hipMemcpyHostToDevice, s));
+    if (m_) MADIPM_HIP(hipMemcpyAsync(y_.p, P.y.data(), sizeof(double) * m_, hipMemcpyHostToDevice, s));
+    zl_.zero(s);
+    zu_.zero(s);
+    d_.zero(s);
+    p_.zero(s);
+  }
+  for (auto e : fact_events_) (void)hipEventDestroy(e);
+  fact_events_.clear();
   // init_regularization! (kernels.jl:364-392)
   switch (opt_.regularization) {
     case 0: del_w_ = 1.0; del_c_ = 0.0; break;
@@ -1320,17 +1333,23 @@ void MPCSolver::initialize() {
   k_ = 0;
 }
 
+void MPCSolver::initialize_public() {
+  const double t0 = now();
+  initialize();
+  MADIPM_HIP(hipStreamSynchronize(stream_));
+  t_init_ += now() - t0;
+  initialized_ = true;
+}
+
 int MPCSolver::solve(madipm_stats* stats) {
   DV_ARGS;
   hipStream_t s = stream_;
-  const double t0 = now();
   trace_.clear();
   int status = MADIPM_REGULAR;
   double tstart = now();
   try {
-    initialize();
-    MADIPM_HIP(hipStreamSynchronize(s));
-    t_init_ += now() - t0;
+    if (!initialized_) initialize_public();
+    initialized_ = false;
     tstart = now();  // solver.jl:181
     const int nb = blocks(n_ + m_), nbz = blocks(std::max(nlb_, nub_));
     while (true) {

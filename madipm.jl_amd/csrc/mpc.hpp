@@ -46,6 +46,8 @@ class MPCSolver {
   MPCSolver(const madipm_qp& qp, const madipm_options& opt);
   ~MPCSolver();
   int solve(madipm_stats* stats);
+  void initialize_public();  // initialize! alone (so that callers can time the MPC loop only)
+  void set_max_iter(int k) { opt_.max_iter = k; }
   void get_solution(double* x, double* y, double* zl, double* zu, double* cons);
   const std::vector<madipm_iter_trace>& trace() const { return trace_; }
   LDLSolver& ldl() { return *ldl_; }
@@ -87,6 +89,7 @@ class MPCSolver {
   double del_w_ = 0, del_c_ = 0, norm_b_ = 0, norm_c_ = 0, best_compl_ = 0, obj_scale_ = 1, c0s_ = 0;
   double adapt_dp_ = 0, adapt_dd_ = 0, adapt_dmin_ = 0;
   int status_ = 0, k_ = 0;
+  bool initialized_ = false;
   double inf_pr_ = 0, inf_du_ = 0, inf_compl_ = 0;
   double t_init_ = 0, t_total_ = 0, t_linsol_ = 0;
   std::vector<madipm_iter_trace> trace_;

@@ -114,9 +114,12 @@ class IterTrace(C.Structure):
 L._sig("madipm_default_options", None, [C.POINTER(Options)])
 L._sig("madipm_solver_create", C.c_int, [C.POINTER(QPStruct), C.POINTER(Options), C.POINTER(L.vp)])
 L._sig("madipm_solver_solve", C.c_int, [L.vp, C.POINTER(Stats)])
+L._sig("madipm_solver_initialize", C.c_int, [L.vp])
+L._sig("madipm_solver_set_max_iter", C.c_int, [L.vp, C.c_int32])
 L._sig("madipm_solver_get_solution", C.c_int, [L.vp, L.f64p, L.f64p, L.f64p, L.f64p, L.f64p])
 L._sig("madipm_solver_trace", C.c_int, [L.vp, C.POINTER(IterTrace), C.c_int32])
 L._sig("madipm_solver_ldl_info", C.c_int, [L.vp, C.POINTER(L.LDLInfo)])
+L._sig("madipm_solver_ldl_perm", C.c_int, [L.vp, L.i32p])
 L._sig("madipm_solver_destroy", None, [L.vp])
 
 
@@ -246,6 +249,20 @@ class MPCSolver:
         inf = L.LDLInfo()
         L.check(L.lib.madipm_solver_ldl_info(self.h, C.byref(inf)), "ldl_info")
         return inf.as_dict()
+
+    def kkt_perm(self) -> np.ndarray:
+        """Pivot order of the K2 LDL^T (analysis output), over the K2 unknowns [x; s; y]."""
+        n = self.ldl_info()["n"]
+        p = np.empty(n, np.int32)
+        L.check(L.lib.madipm_solver_ldl_perm(self.h, L.ptr(p, C.c_int32)), "kkt_perm")
+        return p
+
+    def initialize(self):
+        """initialize! alone (src/solver.jl:127-189); the next solve() runs only the MPC loop."""
+        L.check(L.lib.madipm_solver_initialize(self.h), "initialize!")
+
+    def set_max_iter(self, k: int):
+        L.check(L.lib.madipm_solver_set_max_iter(self.h, int(k)), "set_max_iter")
 
     def solve(self) -> ExecutionStats:
         """solve!(solver) (src/solver.jl:362-418)."""

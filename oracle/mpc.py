@@ -290,11 +290,21 @@ class OracleMPC:
         t0 = time.perf_counter()
         L = self.kkt_matrix()
         K = (L + L.T - sp.diags(L.diagonal())).tocsc()
-        try:
-            self._lu = spla.splu(K)
-            self._factorized = True
-        except RuntimeError:
-            self._factorized = False
+        if getattr(self, "linear_solver", "superlu") == "ldl":
+            # oracle/ldl_ref.c: LDLFactorizations' up-looking LDL^T (static pivots) in the order
+            # `ldl_perm` (default: SuperLU's minimum degree on A+A^T)
+            from .ldl import OracleLDL
+            if getattr(self, "ldl_perm", None) is None:
+                self.ldl_perm = np.argsort(spla.splu(K, permc_spec="MMD_AT_PLUS_A").perm_c)
+            F = OracleLDL(K, self.ldl_perm)
+            self._factorized = F.factorize() == K.shape[0]
+            self._lu = F
+        else:
+            try:
+                self._lu = spla.splu(K)
+                self._factorized = True
+            except RuntimeError:
+                self._factorized = False
         self.linear_solver_time += time.perf_counter() - t0
 
     def kkt_solve(self, w):
@@ -408,7 +418,8 @@ class OracleMPC:
         with np.errstate(invalid="ignore"):
             pl = np.minimum(kappa * np.maximum(1.0, l), kappa * (u - l))
             pu = np.minimum(kappa * np.maximum(1.0, u), kappa * (u - l))
-        x[:] = np.where(x < l, l + pl, np.where(u < x, u - pu, x))
+        with np.errstate(invalid="ignore"):
+            x[:] = np.where(x < l, l + pl, np.where(u < x, u - pu, x))
         # lines 120-123
         if not (np.all(self.zl[ind_lb] > 0) and np.all(self.zu[ind_ub] > 0)
                 and np.all(x[ind_lb] > self.xl[ind_lb]) and np.all(x[ind_ub] < self.xu[ind_ub])):

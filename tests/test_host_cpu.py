@@ -1,0 +1,151 @@
+"""CPU tests of host logic and of the C-ABI library (no GPU compute calls).
+
+* every function declared in include/madipm_hip.h is exported by libmadipm_hip.so;
+* host-side symbolic analysis (AMD, etree, column counts, supernodes) against the oracle's
+  up-looking LDL^T (same order => identical nnz(L)) and a brute-force elimination;
+* MPS reader, standard_form_qp (src/utils.jl:373-505), scale_qp, option parsing.
+"""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from helpers import block_angular_k2, random_k2
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_declared_symbol():
+    from madipm_amd import _lib
+    header = open(os.path.join(ROOT, "include", "madipm_hip.h")).read()
+    header = re.sub(r"/\*.*?\*/", "", header, flags=re.S)
+    names = set(re.findall(r"\b(madipm_[a-z0-9_]+)\s*\(", header))
+    assert len(names) >= 25
+    lib = ctypes.CDLL(str(_lib.LIB_PATH))
+    missing = [n for n in sorted(names) if not hasattr(lib, n)]
+    assert not missing, missing
+    assert _lib.madipm_version() == 100
+
+
+def test_library_reports_errors_without_gpu():
+    from madipm_amd import _lib
+    o = _lib.default_ldl_opts()
+    h = ctypes.c_void_p()
+    colptr = np.array([0, 2, 3], np.int64)
+    rowval = np.array([1, 0, 1], np.int32)     # (1,0) then (0,0): row 0 in col 0 ok, but unsorted fine
+    rc = _lib.madipm_symbolic_analyze(2, _lib.ptr(colptr, ctypes.c_int64), _lib.ptr(rowval, ctypes.c_int32),
+                                      ctypes.byref(o), None, ctypes.byref(h))
+    assert rc == 0
+    _lib.madipm_symbolic_destroy(h)
+    bad = np.array([0, 1, 2], np.int32)
+    rowval2 = np.array([0, 0], np.int32)        # (0,1) is upper triangle -> rejected
+    rc = _lib.madipm_symbolic_analyze(2, _lib.ptr(np.array([0, 1, 2], np.int64), ctypes.c_int64),
+                                      _lib.ptr(rowval2, ctypes.c_int32), ctypes.byref(o), None, ctypes.byref(h))
+    assert rc < 0 and b"lower triangle" in _lib.madipm_last_error()
+
+
+def _brute_nnzL(K, perm):
+    Kp = (K[perm][:, perm].toarray() != 0)
+    N = Kp.shape[0]
+    cnt = 0
+    for j in range(N):
+        rows = np.flatnonzero(Kp[j + 1:, j]) + j + 1
+        cnt += 1 + len(rows)
+        if len(rows):
+            Kp[np.ix_(rows, rows)] = True
+    return cnt
+
+
+@pytest.mark.parametrize("m,n,dens,seed", [(5, 8, 0.3, 0), (30, 50, 0.05, 1), (80, 120, 0.03, 2)])
+@pytest.mark.parametrize("ordering", [0, 1])
+def test_symbolic_nnzL_brute_force(m, n, dens, seed, ordering):
+    from madipm_amd._lib import Symbolic, default_ldl_opts
+    K, Lw = random_k2(m, n, dens, seed)
+    S = Symbolic(K.shape[0], Lw.indptr, Lw.indices, default_ldl_opts(ordering=ordering))
+    perm = S.perm()
+    assert sorted(perm.tolist()) == list(range(K.shape[0]))
+    assert S.info()["nnzL"] == _brute_nnzL(K, perm)
+
+
+@pytest.mark.parametrize("relax", [0, 1])
+def test_symbolic_matches_oracle_ldl(relax):
+    from madipm_amd._lib import Symbolic, default_ldl_opts
+    from oracle.ldl import OracleLDL
+    K, Lw = block_angular_k2(2000, 3000, 15, 3)
+    S = Symbolic(K.shape[0], Lw.indptr, Lw.indices, default_ldl_opts(relax=relax))
+    info = S.info()
+    F = OracleLDL(K, S.perm())
+    assert F.factorize() == K.shape[0]
+    assert F.nnzL() == info["nnzL"]
+    assert info["nnzL_stored"] >= info["nnzL"]
+    first, parent, nrows = S.supernodes()
+    ns = info["nsuper"]
+    assert first[0] == 0 and first[-1] == K.shape[0] and np.all(np.diff(first) > 0)
+    assert np.all((parent == -1) | (parent > np.arange(ns)))      # postordered front tree
+    assert np.all(nrows >= np.diff(first))
+
+
+def test_amd_beats_natural_order():
+    from madipm_amd._lib import Symbolic, default_ldl_opts
+    K, Lw = block_angular_k2(3000, 4000, 20, 7)
+    nat = Symbolic(K.shape[0], Lw.indptr, Lw.indices, default_ldl_opts(ordering=0)).info()["nnzL"]
+    amd = Symbolic(K.shape[0], Lw.indptr, Lw.indices, default_ldl_opts(ordering=1)).info()["nnzL"]
+    assert amd < nat / 3
+
+
+def test_symbolic_rejects_duplicates():
+    from madipm_amd._lib import Symbolic, MadIPMError
+    with pytest.raises(MadIPMError, match="duplicate"):
+        Symbolic(2, np.array([0, 3, 4]), np.array([0, 1, 1, 1]))
+
+
+def test_read_afiro():
+    from madipm_amd import read_mps
+    qp = read_mps(os.path.join(ROOT, "tests", "golden", "afiro.mps"))
+    assert (qp.ncon, qp.nvar) == (27, 32)
+    # netlib lists AFIRO with 88 nonzeros including the 4 objective coefficients
+    assert qp.nnzj == 84 and np.count_nonzero(qp.c) == 4
+    assert np.all(qp.lvar == 0) and np.all(np.isinf(qp.uvar))
+
+
+def test_standard_form_shapes():
+    """standard_form_qp (src/utils.jl:373-505): slacks for inequality rows, w for range bounds."""
+    from madipm_amd import QuadraticModel, standard_form_qp
+    inf = np.inf
+    qp = QuadraticModel(c=[1.0, 2.0, 3.0], Hrows=[], Hcols=[], Hvals=[], Arows=[0, 0, 1, 2], Acols=[0, 1, 1, 2],
+                        Avals=[1.0, 1.0, 1.0, 1.0], lcon=[1.0, -inf, 0.0], ucon=[1.0, 4.0, 2.0],
+                        lvar=[0.0, 0.0, -1.0], uvar=[inf, 5.0, 1.0])
+    s = standard_form_qp(qp)
+    # ineq rows: 1 (only ub), 2 (range) -> ns = 2; range bounds: x1 (0..5), x2 (-1..1), s_row2 (0..2) -> nw = 3
+    assert s.nvar == 3 + 2 + 3 and s.ncon == 3 + 3
+    assert np.all(s.lcon == s.ucon)                         # all equalities
+    assert np.all(s.lvar[5:] == 0) and np.all(np.isinf(s.uvar[5:]))
+    assert s.nnzj == qp.nnzj + 2 + 2 * 3
+
+
+def test_scale_qp_equilibrates():
+    from madipm_amd import scale_qp
+    from madipm_amd.instances import random_lp
+    qp = random_lp(50, 80, 0.1, 0)
+    qp.Avals[:] *= np.exp(np.random.default_rng(0).uniform(-5, 5, qp.nnzj))
+    s = scale_qp(qp)
+    A = sp.coo_matrix((np.abs(s.Avals), (s.Arows, s.Acols)), shape=(s.ncon, s.nvar)).tocsr()
+    assert np.allclose(A.max(axis=1).toarray().ravel(), 1.0, atol=1e-3)
+    assert np.allclose(A.max(axis=0).toarray().ravel(), 1.0, atol=1e-3)
+
+
+def test_options_parsing():
+    from madipm_amd.solver import load_options, FixedRegularization, MehrotraAdaptiveStep, NormalKKTSystem
+    o = load_options(max_iter=300, regularization=FixedRegularization(1e-8, -1e-8),
+                     step_rule=MehrotraAdaptiveStep(0.9), tol=1e-7)
+    assert (o.max_iter, o.regularization, o.delta_p, o.delta_d, o.step_rule, o.step_tau, o.tol) == \
+        (300, 1, 1e-8, -1e-8, 2, 0.9, 1e-7)
+    d = load_options()
+    assert (d.tol, d.max_iter, d.mu_init, d.mu_min, d.bound_push, d.delta_p) == (1e-8, 3000, 0.1, 1e-12, 1e-2, 1e-10)
+    with pytest.raises(TypeError):
+        load_options(not_an_option=1)
+    with pytest.raises(NotImplementedError):
+        load_options(kkt_system=NormalKKTSystem)

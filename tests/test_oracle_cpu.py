@@ -1,0 +1,118 @@
+"""CPU tests of the oracle (test infrastructure): pinned against the reference's own answers and HiGHS.
+
+* simple_lp (test/runtests.jl:29-60): objective exactly 1 with NoRegularization;
+  standard_form_qp gives the same objective (test/runtests.jl:159-164).
+* AFIRO (BASELINE.json configs[0]): netlib optimum -464.75314286 (HiGHS: -464.7531428571).
+* seeded LPs: objective within 1e-6 relative of HiGHS (fp64; IPM tol 1e-8).
+* golden traces (tests/golden/oracle_traces.json, made by tools/make_golden.py): the oracle
+  reproduces its committed per-iteration trace to 1e-10 relative (regression pin).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle.mpc import OracleMPC, OracleOptions, SOLVE_SUCCEEDED
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _load_case(name):
+    from madipm_amd import read_mps, simple_lp, standard_form_qp
+    from madipm_amd.instances import random_lp
+    afiro = lambda: read_mps(os.path.join(GOLD, "afiro.mps"))  # noqa: E731
+    return {
+        "simple_lp_noreg": simple_lp, "simple_lp_std": lambda: standard_form_qp(simple_lp()),
+        "afiro_fixed": afiro, "afiro_std_fixed": lambda: standard_form_qp(afiro()),
+        "random_lp_60x120_s0": lambda: random_lp(60, 120, 0.05, 0, ineq_frac=0.3, free_frac=0.05),
+        "random_lp_100x200_s1": lambda: random_lp(100, 200, 0.03, 1, ineq_frac=0.2),
+    }[name]()
+
+
+def _opts(d):
+    return OracleOptions(**{k: tuple(v) if isinstance(v, list) else v for k, v in d.items()})
+
+
+def test_simple_lp_objective_is_one():
+    from madipm_amd import simple_lp
+    st = OracleMPC(simple_lp(), OracleOptions(regularization=("none",))).solve()
+    assert st.status == SOLVE_SUCCEEDED
+    assert st.objective == pytest.approx(1.0, abs=1e-10)
+
+
+def test_simple_lp_standard_form_same_objective():
+    from madipm_amd import simple_lp, standard_form_qp
+    a = OracleMPC(simple_lp(), OracleOptions(regularization=("none",))).solve()
+    b = OracleMPC(standard_form_qp(simple_lp()), OracleOptions()).solve()
+    assert abs(a.objective - b.objective) <= 1e-10
+
+
+@pytest.mark.parametrize("std", [False, True])
+def test_afiro_netlib_optimum(std):
+    from madipm_amd import read_mps, standard_form_qp
+    qp = read_mps(os.path.join(GOLD, "afiro.mps"))
+    if std:
+        qp = standard_form_qp(qp)
+    st = OracleMPC(qp, OracleOptions(regularization=("fixed", 1e-8, -1e-8), max_iter=300)).solve()
+    assert st.status == SOLVE_SUCCEEDED
+    assert st.objective == pytest.approx(-464.75314286, rel=1e-9)
+
+
+with open(os.path.join(GOLD, "oracle_traces.json")) as _f:
+    GOLDEN = json.load(_f)
+
+
+@pytest.mark.parametrize("name", sorted(GOLDEN))
+def test_golden_traces(name):
+    g = GOLDEN[name]
+    qp = _load_case(name)
+    st = OracleMPC(qp, _opts(g["options"])).solve()
+    assert st.status == g["status"] and st.iter == g["iter"]
+    assert st.objective == pytest.approx(g["objective"], rel=1e-10, abs=1e-12)
+    assert st.objective == pytest.approx(g["highs_objective"], rel=1e-6, abs=1e-8)
+    for a, b in zip(st.trace, g["trace"]):
+        for k in ("obj", "inf_pr", "inf_du", "inf_compl", "mu", "alpha_p", "alpha_d"):
+            assert a[k] == pytest.approx(b[k], rel=1e-10, abs=1e-14), (name, a["k"], k)
+
+
+@pytest.mark.parametrize("rule", [("adaptive", 0.99), ("conservative", 0.99), ("mehrotra", 0.99)])
+def test_step_rules_converge(rule):
+    from madipm_amd.instances import dense_dummy_qp
+    st = OracleMPC(dense_dummy_qp(10, 5), OracleOptions(step_rule=rule)).solve()
+    assert st.status == SOLVE_SUCCEEDED
+
+
+def test_gondzio_and_regularizations_agree():
+    """test/runtests.jl:67-78,122-140: variants reach the same solution (atol 1e-6)."""
+    from madipm_amd.instances import dense_dummy_qp
+    qp = dense_dummy_qp(20, 15, eq=[1, 2, 3, 8])
+    ref = OracleMPC(qp, OracleOptions(regularization=("none",))).solve()
+    for o in (OracleOptions(max_ncorr=5), OracleOptions(regularization=("fixed", 1e-8, -1e-9)),
+              OracleOptions(regularization=("adaptive", 1e-8, -1e-9, 1e-9))):
+        st = OracleMPC(qp, o).solve()
+        assert st.status == SOLVE_SUCCEEDED
+        assert st.objective == pytest.approx(ref.objective, abs=1e-6)
+        assert np.allclose(st.solution, ref.solution, atol=1e-5)
+
+
+def test_oracle_ldl_linear_solver_matches_superlu():
+    """The oracle's C LDL^T path (used as CPU baseline) gives the same MPC result as SuperLU."""
+    from madipm_amd import read_mps, standard_form_qp
+    qp = standard_form_qp(read_mps(os.path.join(GOLD, "afiro.mps")))
+    a = OracleMPC(qp, OracleOptions(regularization=("fixed", 1e-8, -1e-8))).solve()
+    o = OracleMPC(qp, OracleOptions(regularization=("fixed", 1e-8, -1e-8)))
+    o.linear_solver = "ldl"
+    b = o.solve()
+    assert a.status == b.status == SOLVE_SUCCEEDED
+    assert b.objective == pytest.approx(a.objective, rel=1e-9)
+
+
+def test_maximize_sign():
+    """update_solution! flips the objective of maximisation problems (src/utils.jl:150-156)."""
+    from madipm_amd.instances import ex10_standin
+    from madipm_amd import standard_form_qp
+    qp = standard_form_qp(ex10_standin(scale=0.02))
+    assert not qp.minimize
+    st = OracleMPC(qp, OracleOptions(regularization=("fixed", 1e-8, -1e-8), max_iter=100)).solve()
+    assert st.status == SOLVE_SUCCEEDED and st.objective > 0
