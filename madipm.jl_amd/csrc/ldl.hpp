@@ -32,6 +32,17 @@ struct FrontTab {
   const int64_t* rel_ptr;
   const int32_t* rel;
   const int32_t* perm;
+  const int64_t* crow_off;
+  const int64_t* crow;
+  const int32_t* ce_child;
+  const int32_t* ce_row;
+  const int32_t* bigch_ptr;
+  const int32_t* bigch_list;
+  const int32_t* bigslot;  // big front -> slot in the panel-inverse scratch (64x64 per slot)
+};
+
+struct SolveTask {
+  int32_t front, blk;
 };
 
 struct LDLStatus {  // device-resident, read back by status()
@@ -64,25 +75,36 @@ class LDLSolver {
   const double* d_diag() const { return D_.p; }
 
  private:
-  enum Kind { SMALL32 = 0, SMALL64 = 1, SMALL128 = 2, BIG_ASM = 3, BIG_PANEL = 4, BIG_UPDATE = 5 };
+  enum Kind { SMALL32 = 0, SMALL64 = 1, SMALL128 = 2, BIG_TILES = 3, BIG_PULL = 4, BIG_BIGCH = 5, BIG_DIAG = 6, BIG_TRSM = 7,
+              BIG_UPDATE = 8 };
   struct Launch {
     int kind;
-    int step;       // panel step for BIG_PANEL / BIG_UPDATE
+    int step;       // panel step for BIG_DIAG / BIG_TRSM / BIG_UPDATE
     int64_t off;    // offset of the front list in sched_ (then prefix[nf+1] for big kinds)
     int nf;         // number of fronts
     int64_t items;  // workgroups
   };
-  struct SolveLaunch {
-    int64_t off;
-    int nf;
+  struct SolveLevel {
+    int64_t small_off;
+    int nsmall;
+    int64_t big_off;
+    int nbig;
+    int64_t ftask_off;
+    int nftask;
+    int64_t btask_off;
+    int nbtask;
   };
   SymbolicPlan S_;
   FrontTab T_{};
   std::vector<Launch> fact_;
-  std::vector<SolveLaunch> solve_;  // per level, leaves first
+  std::vector<SolveLevel> slev_;  // per level, leaves first
+  DBuf<int32_t> tasks_, flags_, flag_off_, counters_, err_;
+  int epoch_ = 0;
   // device data
   DBuf<int32_t> first_, nrows_, rows_, u_ld_, child_ptr_, child_list_, rel_, perm_, sched_;
-  DBuf<int64_t> row_ptr_, l_off_, u_off_, uvec_off_, asm_ptr_, asm_src_, asm_dst64_, rel_ptr_;
+  DBuf<int32_t> ce_child_, ce_row_, bigch_ptr_, bigch_list_, bigslot_;
+  DBuf<double> minv_;
+  DBuf<int64_t> row_ptr_, l_off_, u_off_, uvec_off_, asm_ptr_, asm_src_, asm_dst64_, rel_ptr_, crow_off_, crow_;
   DBuf<double> arena_, D_, xi_, uvec_, vwork_;
   DBuf<LDLStatus> status_;
   LDLStatus* h_status_ = nullptr;

@@ -438,6 +438,44 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   }
   S.arena_size = cur;
   S.uvec_size = ucur;
+
+  // ---------------- 10. extend-add "pull" lists: for every parent row, the (child, child row)
+  // pairs that contribute to it, children in a fixed order.  One thread owns a parent row and sums
+  // its contributions in that order: parallel AND deterministic.  Children whose update block is
+  // larger than kPullMax rows are handled column-wise by the tiled big-front kernels instead.
+  S.crow_off.assign(ns + 1, 0);
+  for (int s = 0; s < ns; ++s) S.crow_off[s + 1] = S.crow_off[s] + S.nrows[s] + 1;
+  S.crow.assign(S.crow_off[ns], 0);
+  S.bigch_ptr.assign(ns + 1, 0);
+  S.bigch_list.clear();
+  S.ce_child.clear();
+  S.ce_row.clear();
+  {
+    std::vector<std::vector<std::pair<int32_t, int32_t>>> bucket;
+    for (int s = 0; s < ns; ++s) {
+      const int r = S.nrows[s];
+      bucket.assign(r, {});
+      for (int64_t q = S.child_ptr[s]; q < S.child_ptr[s + 1]; ++q) {
+        const int c = S.child_list[q];
+        const int uc = S.nrows[c] - (S.first[c + 1] - S.first[c]);
+        if (uc > SymbolicPlan::kPullMax) {
+          S.bigch_list.push_back(c);
+          continue;
+        }
+        for (int a = 0; a < uc; ++a) bucket[S.rel[S.rel_ptr[c] + a]].emplace_back(c, a);
+      }
+      S.bigch_ptr[s + 1] = (int32_t)S.bigch_list.size();
+      int64_t base = S.crow_off[s];
+      S.crow[base] = (int64_t)S.ce_child.size();
+      for (int i = 0; i < r; ++i) {
+        for (auto& e : bucket[i]) {
+          S.ce_child.push_back(e.first);
+          S.ce_row.push_back(e.second);
+        }
+        S.crow[base + i + 1] = (int64_t)S.ce_child.size();
+      }
+    }
+  }
 }
 
 }  // namespace madipm

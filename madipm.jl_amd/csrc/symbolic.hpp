@@ -48,6 +48,11 @@ struct SymbolicPlan {
   std::vector<int32_t> u_ld;
   std::vector<int64_t> uvec_off;       // solve update vector (r - w)
   std::vector<uint8_t> is_big;
+  // extend-add pull lists (see symbolic.cpp step 10)
+  static constexpr int kPullMax = 128;
+  std::vector<int64_t> crow_off, crow;  // per front: r+1 offsets into ce_* (global)
+  std::vector<int32_t> ce_child, ce_row;
+  std::vector<int32_t> bigch_ptr, bigch_list;  // children with update blocks > kPullMax rows
   int64_t arena_size = 0, uvec_size = 0;
   // statistics
   int64_t nnzL = 0;          // exact nnz(L) incl. diagonal (column counts)
