@@ -25,23 +25,17 @@ typedef double dbl4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ bool bad_pivot(double d, double tol) { return !(fabs(d) > tol) || isinf(d); }
 
+// wave-synchronous LDS hand-off: LDS ops of one wave complete in order; keep the compiler from
+// moving them across this point
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
   return v;
-}
-
-// largest k in [0, nf) with prefix[k] <= bid
-__device__ __forceinline__ int find_item(const int32_t* __restrict__ prefix, int nf, int bid) {
-  int lo = 0, hi = nf - 1;
-  while (lo < hi) {
-    int mid = (lo + hi + 1) >> 1;
-    if (prefix[mid] <= bid)
-      lo = mid;
-    else
-      hi = mid - 1;
-  }
-  return lo;
 }
 
 template <class T>
@@ -64,7 +58,8 @@ __global__ void k_status_init(LDLStatus* st) {
 // ------------------------------------------------------------------ small fronts (LDS)
 __global__ __launch_bounds__(NT) void k_small_factor(FrontTab T, const int32_t* __restrict__ fronts,
                                                      const double* __restrict__ Kx, double* __restrict__ arena,
-                                                     double* __restrict__ D, LDLStatus* st, double tol) {
+                                                     const double* __restrict__ fscratch, double* __restrict__ D,
+                                                     LDLStatus* st, double tol) {
   extern __shared__ __attribute__((aligned(16))) double F[];  // r x r, col-major, ld r
   const int s = fronts[blockIdx.x];
   const int f0 = T.first[s];
@@ -73,20 +68,13 @@ __global__ __launch_bounds__(NT) void k_small_factor(FrontTab T, const int32_t* 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   for (int q = tid; q < r * r; q += NT) F[q] = 0.0;
   __syncthreads();
-  for (int64_t q = T.asm_ptr[s] + tid; q < T.asm_ptr[s + 1]; q += NT) F[T.asm_dst[q]] = Kx[T.asm_src[q]];
-  __syncthreads();
-  // extend-add, "pull" form: thread i owns parent row i and adds its contributions child by child
-  // (fixed order => deterministic; distinct rows => no conflicts, no atomics)
-  for (int i = tid; i < r; i += NT) {
-    const int64_t e1 = T.crow[T.crow_off[s] + i + 1];
-    for (int64_t e = T.crow[T.crow_off[s] + i]; e < e1; ++e) {
-      const int c = T.ce_child[e], a = T.ce_row[e];
-      const double* __restrict__ U = arena + T.u_off[c] + a;
-      const int64_t ldc = T.u_ld[c];
-      const int32_t* __restrict__ rel = T.rel + T.rel_ptr[c];
-      double* Fi = F + i;
-      for (int b = 0; b <= a; ++b) Fi[rel[b] * r] += U[b * ldc];
-    }
+  const int64_t fso = T.fs_off[s];
+  if (fso < 0) {  // leaf: original entries only
+    for (int64_t q = T.asm_ptr[s] + tid; q < T.asm_ptr[s + 1]; q += NT) F[T.asm_dst[q]] = Kx[T.asm_src[q]];
+  } else {        // assembled by k_assemble (lower triangle)
+    const double* __restrict__ Fs = fscratch + fso;
+    for (int j = wv; j < r; j += NT / 64)
+      for (int i = j + lane; i < r; i += 64) F[i + j * r] = Fs[i + j * r];
   }
   __syncthreads();
   // right-looking LDL^T; column t stays unscaled until the write-out
@@ -117,161 +105,228 @@ __global__ __launch_bounds__(NT) void k_small_factor(FrontTab T, const int32_t* 
   }
 }
 
-// ------------------------------------------------------------------ big fronts (HBM)
-__device__ __forceinline__ void tile_of(int tile, int& ti, int& tj) {
-  ti = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
-  while ((ti + 1) * (ti + 2) / 2 <= tile) ++ti;
-  while (ti * (ti + 1) / 2 > tile) --ti;
-  tj = tile - ti * (ti + 1) / 2;
+// Fronts with r <= 32: one WAVE per front, 4 fronts per workgroup (the leaf level has ~10^5 of them).
+// Lane l works on row l & 31 and the columns of parity l >> 5; wave-synchronous right-looking LDL^T.
+constexpr int TINY = 32;
+__global__ __launch_bounds__(NT) void k_tiny_factor(FrontTab T, const int32_t* __restrict__ fronts, int nf,
+                                                    const double* __restrict__ Kx, double* __restrict__ arena,
+                                                    const double* __restrict__ fscratch, double* __restrict__ D,
+                                                    LDLStatus* st, double tol) {
+  constexpr int LD = TINY + 1;
+  __shared__ double Fs[4][TINY * LD];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int q = blockIdx.x * 4 + wv;
+  if (q >= nf) return;
+  const int s = fronts[q];
+  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+  double* F = Fs[wv];
+  const int i = lane & 31, par = lane >> 5;
+  for (int j = par; j < r; j += 2) F[i + j * LD] = 0.0;
+  wave_sync();
+  const int64_t fso = T.fs_off[s];
+  if (fso < 0) {
+    for (int64_t e = T.asm_ptr[s] + lane; e < T.asm_ptr[s + 1]; e += 64) {
+      const int64_t d = T.asm_dst[e];
+      F[(int)(d % r) + (int)(d / r) * LD] = Kx[T.asm_src[e]];
+    }
+  } else {
+    const double* __restrict__ Fg = fscratch + fso;
+    for (int j = par; j < r; j += 2)
+      if (i >= j && i < r) F[i + j * LD] = Fg[i + j * r];
+  }
+  wave_sync();
+  for (int t = 0; t < w; ++t) {
+    const double dinv = 1.0 / F[t + t * LD];
+    const double lit = F[i + t * LD] * dinv;
+    for (int j = t + 1 + par; j < r; j += 2)
+      if (i >= j && i < r) F[i + j * LD] -= lit * F[j + t * LD];
+    wave_sync();
+  }
+  double* __restrict__ L = arena + T.l_off[s];
+  for (int t = par; t < w; t += 2) {
+    const double d = F[t + t * LD];
+    if (i < r) L[i + (int64_t)t * r] = (i > t) ? F[i + t * LD] / d : (i == t ? d : 0.0);
+    if (i == 0) {
+      D[f0 + t] = d;
+      if (bad_pivot(d, tol)) atomicMin(&st->fail_pivot, f0 + t + 1);
+    }
+  }
+  const int u = r - w;
+  double* __restrict__ Uo = arena + T.u_off[s];
+  for (int b = par; b < u; b += 2)
+    if (i >= b && i < u) Uo[i + (int64_t)b * u] = F[(w + i) + (w + b) * LD];
 }
 
-// Assembly 1/3: zero a 64x64 lower tile of F and write the original K entries that fall in it.
-__global__ __launch_bounds__(NT) void k_big_tiles(FrontTab T, const int32_t* __restrict__ list, int nf,
-                                                  const double* __restrict__ Kx, double* __restrict__ arena) {
-  const int32_t* prefix = list + nf;
-  const int k = find_item(prefix, nf, blockIdx.x);
-  const int s = list[k];
-  int ti, tj;
-  tile_of(blockIdx.x - prefix[k], ti, tj);
+// ------------------------------------------------------------------ assembly (all big fronts, small fronts with children)
+// Phase 1 (flat, thread per chunk): part[c] = sum of the <= kChunk sources of chunk c, in order.
+__global__ __launch_bounds__(NT) void k_asm_chunks(const int64_t* __restrict__ gchunk, const int64_t* __restrict__ gsrc,
+                                                   int64_t c0, int64_t n, const double* __restrict__ Kx,
+                                                   const double* __restrict__ arena, double* __restrict__ part) {
+  const int64_t c = c0 + (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (c >= c0 + n) return;
+  const int64_t p0 = gchunk[c], p1 = gchunk[c + 1];
+  int64_t q[SymbolicPlan::kChunk];
+#pragma unroll
+  for (int u = 0; u < SymbolicPlan::kChunk; ++u) q[u] = (p0 + u < p1) ? gsrc[p0 + u] : INT64_MAX;
+  double v = 0.0;
+#pragma unroll
+  for (int u = 0; u < SymbolicPlan::kChunk; ++u)
+    if (q[u] != INT64_MAX) v += (q[u] >= 0) ? arena[q[u]] : Kx[~q[u]];
+  part[c] = v;
+}
+
+// Phase 2: one workgroup (1024 threads) per 64x64 lower tile of F (SymbolicPlan step 10): entry =
+// sum of its chunk sums in order, staged in LDS; then the big children's update blocks are added
+// child by child (coalesced along the child's rows); the tile is written to the front (big: arena,
+// ld r; small: scratch, ld r).  No atomics, deterministic.
+constexpr int ANT = 1024;
+__global__ __launch_bounds__(ANT) void k_assemble(FrontTab T, const SymbolicPlan::AsmTile* __restrict__ tiles,
+                                                  const int32_t* __restrict__ gptr, const double* __restrict__ part,
+                                                  const int32_t* __restrict__ bt, double* __restrict__ arena,
+                                                  double* __restrict__ fscratch) {
+  __shared__ double Ft[64 * 64];
+  const SymbolicPlan::AsmTile tl = tiles[blockIdx.x];
+  const int s = tl.front, ti = tl.tij & 0xffff, tj = tl.tij >> 16;
   const int r = T.nrows[s];
-  const int I0 = ti * 64, I1 = min(r, I0 + 64), J0 = tj * 64, J1 = min(r, J0 + 64);
-  double* __restrict__ F = arena + T.l_off[s];
+  const int I0 = ti * 64, J0 = tj * 64;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int j = J0 + wv; j < J1; j += NT / 64) {
-    const int i = I0 + lane;
-    if (i < I1 && i >= j) F[i + (int64_t)j * r] = 0.0;
+  if (tl.gptr >= 0) {
+    const int32_t* __restrict__ gp = gptr + tl.gptr;
+    const double* __restrict__ pc = part + tl.gchk;
+    int q0[4], q1[4];
+    double v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      q0[k] = gp[tid + k * ANT];
+      q1[k] = gp[tid + k * ANT + 1];
+      v[k] = 0.0;
+    }
+    int len = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) len = max(len, q1[k] - q0[k]);
+    for (int it = 0; it < len; it += 4) {
+      double x[4][4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[k][u] = (q0[k] + it + u < q1[k]) ? pc[q0[k] + it + u] : 0.0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[k] += x[k][u];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) Ft[tid + k * ANT] = v[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) Ft[tid + k * ANT] = 0.0;
+  }
+  if (tl.bt1 > tl.bt0) {
+    __syncthreads();
+    for (int k = tl.bt0; k < tl.bt1; ++k) {
+      const int c = bt[5 * k], b0 = bt[5 * k + 1], b1 = bt[5 * k + 2], a0 = bt[5 * k + 3], a1 = bt[5 * k + 4];
+      const double* __restrict__ U = arena + T.u_off[c];
+      const int64_t ldc = T.u_ld[c];
+      const int32_t* __restrict__ rel = T.rel + T.rel_ptr[c];
+      for (int b = b0 + wv; b < b1; b += ANT / 64) {
+        const int cb = (rel[b] - J0) * 64 - I0;
+        for (int a = max(b, a0) + lane; a < a1; a += 64) Ft[rel[a] + cb] += U[a + b * ldc];
+      }
+      __syncthreads();
+    }
   }
   __syncthreads();
-  // original entries: per column j, the destinations j*r + [max(I0,j), I1) form a contiguous key range
-  const int64_t a0 = T.asm_ptr[s], a1 = T.asm_ptr[s + 1];
-  if (a1 > a0) {
-    for (int j = J0 + wv; j < J1; j += NT / 64) {
-      const int64_t base = (int64_t)j * r;
-      const int64_t lo = lower_bound_dev<int64_t>(T.asm_dst, a0, a1, base + max(I0, j));
-      const int64_t hi = lower_bound_dev<int64_t>(T.asm_dst, lo, a1, base + I1);
-      for (int64_t q = lo + lane; q < hi; q += 64) F[T.asm_dst[q]] = Kx[T.asm_src[q]];
-    }
+  const int64_t fso = T.fs_off[s];
+  double* __restrict__ F = (fso >= 0 ? fscratch + fso : arena + T.l_off[s]);
+  const int i = I0 + lane;
+  for (int jj = wv; jj < 64; jj += ANT / 64) {
+    const int j = J0 + jj;
+    if (i < r && j < r && i >= j) F[i + (int64_t)j * r] = Ft[lane + jj * 64];
   }
 }
 
-// Assembly 2/3: children with small update blocks, "pull" form (thread = parent row, children in order).
-__global__ __launch_bounds__(NT) void k_big_pull(FrontTab T, const int32_t* __restrict__ list, int nf,
-                                                 double* __restrict__ arena) {
-  const int32_t* prefix = list + nf;
-  const int k = find_item(prefix, nf, blockIdx.x);
-  const int s = list[k];
-  const int r = T.nrows[s];
-  const int i = (blockIdx.x - prefix[k]) * NT + threadIdx.x;
-  if (i >= r) return;
-  double* __restrict__ Fi = arena + T.l_off[s] + i;
-  const int64_t e1 = T.crow[T.crow_off[s] + i + 1];
-  for (int64_t e = T.crow[T.crow_off[s] + i]; e < e1; ++e) {
-    const int c = T.ce_child[e], a = T.ce_row[e];
-    const double* __restrict__ U = arena + T.u_off[c] + a;
-    const int64_t ldc = T.u_ld[c];
-    const int32_t* __restrict__ rel = T.rel + T.rel_ptr[c];
-    for (int b = 0; b <= a; ++b) Fi[(int64_t)rel[b] * r] += U[b * ldc];
-  }
+// ------------------------------------------------------------------ big fronts (HBM)
+// Big-front kernels read their (front, item) pair from the launch's task list.
+__device__ __forceinline__ void task_of(const int32_t* __restrict__ list, int& s, int& item) {
+  const int2 t = reinterpret_cast<const int2*>(list)[blockIdx.x];
+  s = t.x;
+  item = t.y;
 }
 
-// Assembly 3/3: children with large update blocks, column-wise per 64x64 tile, children in order.
-__global__ __launch_bounds__(NT) void k_big_bigch(FrontTab T, const int32_t* __restrict__ list, int nf,
-                                                  double* __restrict__ arena) {
-  const int32_t* prefix = list + nf;
-  const int k = find_item(prefix, nf, blockIdx.x);
-  const int s = list[k];
-  int ti, tj;
-  tile_of(blockIdx.x - prefix[k], ti, tj);
-  const int r = T.nrows[s];
-  const int I0 = ti * 64, I1 = min(r, I0 + 64), J0 = tj * 64, J1 = min(r, J0 + 64);
-  double* __restrict__ F = arena + T.l_off[s];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int ci = T.bigch_ptr[s]; ci < T.bigch_ptr[s + 1]; ++ci) {
-    const int c = T.bigch_list[ci];
-    const int uc = T.nrows[c] - (T.first[c + 1] - T.first[c]);
-    const double* __restrict__ U = arena + T.u_off[c];
-    const int64_t ldc = T.u_ld[c];
-    const int32_t* __restrict__ rel = T.rel + T.rel_ptr[c];
-    const int b0 = (int)lower_bound_dev<int32_t>(rel, 0, uc, J0);
-    const int b1 = (int)lower_bound_dev<int32_t>(rel, b0, uc, J1);
-    const int c0 = (int)lower_bound_dev<int32_t>(rel, b0, uc, I0);
-    const int c1 = (int)lower_bound_dev<int32_t>(rel, c0, uc, I1);
-    for (int b = b0 + wv; b < b1; b += NT / 64) {
-      const int64_t rb = (int64_t)rel[b] * r;
-      for (int a = max(b, c0) + lane; a < c1; a += 64) F[rel[a] + rb] += U[a + b * ldc];
-    }
-    __syncthreads();
-  }
+
+// Diagonal block of 64-column panel `step` (one workgroup per front): factor it, write L11 and D,
+// and form M = L11^{-T} D^{-1} for the MFMA solve of the rows below (k_big_trsm).
+// Register-resident: lane = row i, wave wv owns columns j = wv + 4u (u < 16).  Step t publishes
+// column t through LDS (one barrier per step); the same row operations applied to an identity give
+// X = L11^{-1} on the fly (row t of X is read with readlane), so the inverse costs no extra steps.
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
 }
 
-// Diagonal block of 64-column panel `step` (one workgroup per front): factor it in LDS, write
-// L11 and D, and form M = L11^{-T} D^{-1} for the MFMA solve of the rows below (k_big_trsm).
-__global__ __launch_bounds__(NT) void k_big_diag(FrontTab T, const int32_t* __restrict__ list, int nf, int step,
+__global__ __launch_bounds__(NT) void k_big_diag(FrontTab T, const int32_t* __restrict__ list, int step,
                                                  double* __restrict__ arena, double* __restrict__ D,
                                                  double* __restrict__ Mbuf, LDLStatus* st, double tol) {
-  constexpr int LD = 65;
-  __shared__ double A[64 * LD];
-  __shared__ double X[64 * 65];
-  __shared__ double dinv[64];
-  const int32_t* prefix = list + nf;
-  const int k = find_item(prefix, nf, blockIdx.x);
-  const int s = list[k];
-  const int rb = blockIdx.x - prefix[k];
+  __shared__ double col[64 * 65];  // col[t*65 + i] = A(i, t) after step t
+  int s, item;
+  task_of(list, s, item);
+  (void)item;
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
   const int k0 = step * 64, kw = min(64, w - k0);
-  double* __restrict__ F = arena + T.l_off[s];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int j = wv; j < kw; j += NT / 64)
-    if (lane >= j && lane < kw) A[lane + j * LD] = F[(k0 + lane) + (int64_t)(k0 + j) * r];
-  __syncthreads();
-  for (int t = 0; t < kw; ++t) {
-    const double di = 1.0 / A[t + t * LD];
-    for (int j = t + 1 + wv; j < kw; j += NT / 64) {
-      const double ljd = A[j + t * LD] * di;
-      if (lane >= j && lane < kw) A[lane + j * LD] -= A[lane + t * LD] * ljd;
-    }
+  double* __restrict__ F = arena + T.l_off[s] + k0 + (int64_t)k0 * r;
+  const int tid = threadIdx.x, i = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR) => scalar branches
+  double a[16], x[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int j = wv + 4 * u;
+    a[u] = (i < kw && j < kw) ? (i >= j ? F[i + (int64_t)j * r] : 0.0) : (i == j ? 1.0 : 0.0);
+    x[u] = (i == j) ? 1.0 : 0.0;
+  }
+#pragma unroll
+  for (int t = 0; t < 64; ++t) {
+    if (wv == (t & 3)) col[t * 65 + i] = a[t >> 2];
     __syncthreads();
-  }
-  if (tid < kw) dinv[tid] = 1.0 / A[tid + tid * LD];
-  __syncthreads();
-  for (int j = wv; j < kw; j += NT / 64)
-    if (lane > j && lane < kw) A[lane + j * LD] *= dinv[j];
-  __syncthreads();
-  (void)rb;
-  for (int j = wv; j < kw; j += NT / 64)
-    if (lane >= j && lane < kw) F[(k0 + lane) + (int64_t)(k0 + j) * r] = A[lane + j * LD];
-  if (tid < kw) {
-    const double d = A[tid + tid * LD];
-    D[f0 + k0 + tid] = d;
-    if (bad_pivot(d, tol)) atomicMin(&st->fail_pivot, f0 + k0 + tid + 1);
-  }
-  // M = L11^{-T} D^{-1} (so that the rows below solve as L21 = F21 M, an MFMA product):
-  // thread j forms column j of X = L11^{-1} by forward substitution (all lanes step through the
-  // same (i, k) so the L11 reads broadcast), then writes row j of M: M[j][t] = X[t][j] / d_t.
-  if (tid < 64) {
-    const int j = tid;
-    for (int i = 0; i < 64; ++i) X[i * 65 + j] = (i == j) ? 1.0 : 0.0;
-    for (int i = 1; i < kw; ++i) {
-      double acc = 0.0;
-      for (int q = 0; q < i; ++q) acc += A[i + q * LD] * X[q * 65 + j];
-      if (i > j) X[i * 65 + j] = -acc;
+    const double dt = col[t * 65 + t], ct = col[t * 65 + i];
+    double cj[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) cj[u] = col[t * 65 + wv + 4 * u];
+    const double li = (i > t) ? ct / dt : 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const bool right = wv + 4 * u > t;  // column j right of t: factor update; else: row op on X
+      a[u] = fma(right ? -li : 0.0, cj[u], a[u]);
+      x[u] = fma(right ? 0.0 : -li, readlane_f64(x[u], t), x[u]);
     }
-    double* __restrict__ Mrow = Mbuf + (int64_t)T.bigslot[s] * 4096 + j * 64;
-    for (int t = 0; t < 64; ++t) Mrow[t] = (t < kw && j < kw && t >= j) ? X[t * 65 + j] * dinv[t] : 0.0;
+  }
+  const double di = col[i * 65 + i];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int j = wv + 4 * u;
+    if (i < kw && j < kw && i >= j) F[i + (int64_t)j * r] = (i == j) ? di : a[u] / col[j * 65 + j];
+  }
+  if (wv == 0 && i < kw) {
+    D[f0 + k0 + i] = di;
+    if (bad_pivot(di, tol)) atomicMin(&st->fail_pivot, f0 + k0 + i + 1);
+  }
+  double* __restrict__ M = Mbuf + (int64_t)T.bigslot[s] * 4096;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int j = wv + 4 * u;
+    M[j * 64 + i] = (i < kw && j < kw && i >= j) ? x[u] / di : 0.0;
   }
 }
 
 // Rows below the diagonal block of panel `step`: L21 = F21 * M (64-row tiles, f64 MFMA 16x16x4),
 // computed as the transpose D'[t][i] = sum_k M[k][t] F21[i][k] so that lanes run along F's rows.
-__global__ __launch_bounds__(NT) void k_big_trsm(FrontTab T, const int32_t* __restrict__ list, int nf, int step,
+__global__ __launch_bounds__(NT) void k_big_trsm(FrontTab T, const int32_t* __restrict__ list, int step,
                                                  double* __restrict__ arena, const double* __restrict__ Mbuf) {
   constexpr int LDT = 80;
   __shared__ __attribute__((aligned(16))) double Ms[64 * LDT];
   __shared__ __attribute__((aligned(16))) double At[64 * LDT];
-  const int32_t* prefix = list + nf;
-  const int k = find_item(prefix, nf, blockIdx.x);
-  const int s = list[k];
-  const int rt = blockIdx.x - prefix[k];
+  int s, rt;
+  task_of(list, s, rt);
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
   const int k0 = step * 64, kw = min(64, w - k0);
   const int I0 = k0 + kw + rt * 64;
@@ -315,19 +370,14 @@ __global__ __launch_bounds__(NT) void k_big_trsm(FrontTab T, const int32_t* __re
 }
 
 // Trailing update of one 64x64 lower tile: C -= (L_I D) L_J^T, f64 MFMA 16x16x4.
-__global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __restrict__ list, int nf, int step,
+__global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __restrict__ list, int step,
                                                    double* __restrict__ arena, const double* __restrict__ D) {
   constexpr int LDT = 80;  // [k][row] layout: conflict-free ds_read_b64 for the 16x4 operand pattern
   __shared__ __attribute__((aligned(16))) double Wt[32 * LDT];
   __shared__ __attribute__((aligned(16))) double Lt[32 * LDT];
-  const int32_t* prefix = list + nf;
-  const int k = find_item(prefix, nf, blockIdx.x);
-  const int s = list[k];
-  const int tile = blockIdx.x - prefix[k];
-  int ti = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
-  while ((ti + 1) * (ti + 2) / 2 <= tile) ++ti;
-  while (ti * (ti + 1) / 2 > tile) --ti;
-  const int tj = tile - ti * (ti + 1) / 2;
+  int s, tij;
+  task_of(list, s, tij);
+  const int ti = tij & 0xffff, tj = tij >> 16;
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
   const int k0 = step * 64, kw = min(64, w - k0), c0 = k0 + kw;
   const int I0 = c0 + ti * 64, J0 = c0 + tj * 64;
@@ -414,7 +464,6 @@ __global__ void k_inertia(const double* __restrict__ D, int n, LDLStatus* st) {
 constexpr int SMALL_SOLVE = 128;
 constexpr int SW = 4;  // waves (= small fronts) per workgroup
 
-__device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
 
 __global__ __launch_bounds__(NT) void k_fwd_small(FrontTab T, const int32_t* __restrict__ fronts, int nf,
                                                   const double* __restrict__ arena, const double* __restrict__ b,
@@ -427,16 +476,14 @@ __global__ __launch_bounds__(NT) void k_fwd_small(FrontTab T, const int32_t* __r
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
   double* v = vs[wv];
   const double* __restrict__ L = arena + T.l_off[s];
-  for (int i = lane; i < r; i += 64) v[i] = (i < w) ? b[T.perm[f0 + i]] : 0.0;
-  wave_sync();
-  for (int ci = T.child_ptr[s]; ci < T.child_ptr[s + 1]; ++ci) {
-    const int c = T.child_list[ci];
-    const int uc = T.nrows[c] - (T.first[c + 1] - T.first[c]);
-    const double* __restrict__ uv = uvec + T.uvec_off[c];
-    const int32_t* __restrict__ rel = T.rel + T.rel_ptr[c];
-    for (int t = lane; t < uc; t += 64) v[rel[t]] += uv[t];
-    wave_sync();
+  for (int i = lane; i < r; i += 64) {
+    double vi = (i < w) ? b[T.perm[f0 + i]] : 0.0;
+    const int64_t e = T.row_ptr[s] + i;
+    const int64_t p1 = T.sv_ptr[e + 1];
+    for (int64_t p = T.sv_ptr[e]; p < p1; ++p) vi += uvec[T.sv_src[p]];
+    v[i] = vi;
   }
+  wave_sync();
   for (int t = 0; t < w; ++t) {
     const double xt = v[t];
     const double* __restrict__ Lc = L + t * r;
@@ -492,23 +539,21 @@ __global__ __launch_bounds__(NT) void k_bwd_small(FrontTab T, const int32_t* __r
   }
 }
 
-// initial forward vector of a big front (own b entries + children's update vectors), in HBM
-__global__ __launch_bounds__(NT) void k_fwd_gather(FrontTab T, const int32_t* __restrict__ fronts,
+// initial forward vector of a big front (own b entries + children's update vectors), in HBM;
+// task = (front, 256-row chunk), thread = row, children summed in the fixed list order
+__global__ __launch_bounds__(NT) void k_fwd_gather(FrontTab T, const int32_t* __restrict__ list,
                                                    const double* __restrict__ b, const double* __restrict__ uvec,
                                                    double* __restrict__ vwork) {
-  const int s = fronts[blockIdx.x];
+  int s, chunk;
+  task_of(list, s, chunk);
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
-  double* __restrict__ v = vwork + T.row_ptr[s];
-  for (int i = threadIdx.x; i < r; i += NT) v[i] = (i < w) ? b[T.perm[f0 + i]] : 0.0;
-  __syncthreads();
-  for (int ci = T.child_ptr[s]; ci < T.child_ptr[s + 1]; ++ci) {
-    const int c = T.child_list[ci];
-    const int uc = T.nrows[c] - (T.first[c + 1] - T.first[c]);
-    const double* __restrict__ uv = uvec + T.uvec_off[c];
-    const int32_t* __restrict__ rel = T.rel + T.rel_ptr[c];
-    for (int t = threadIdx.x; t < uc; t += NT) v[rel[t]] += uv[t];
-    __syncthreads();
-  }
+  const int i = chunk * NT + threadIdx.x;
+  if (i >= r) return;
+  double vi = (i < w) ? b[T.perm[f0 + i]] : 0.0;
+  const int64_t e = T.row_ptr[s] + i;
+  const int64_t p1 = T.sv_ptr[e + 1];
+  for (int64_t p = T.sv_ptr[e]; p < p1; ++p) vi += uvec[T.sv_src[p]];
+  vwork[e] = vi;
 }
 
 __device__ __forceinline__ bool wait_flag(int32_t* f, int epoch, int32_t* err) {
@@ -603,13 +648,52 @@ __global__ __launch_bounds__(NT) void k_fwd_big(FrontTab T, const SolveTask* __r
   }
 }
 
+// Backward, big fronts, rows below the pivot block (independent of the panel chain): task =
+// (front, panel p, 256-row chunk); writes bpart[(bp_off[front] + p * nchunk + chunk) * 64 + col] =
+// sum over the chunk's rows of L(row, col) x(row).  The chain kernel sums the chunks in order.
+constexpr int BWD_CHUNK = 256;
+__global__ __launch_bounds__(NT) void k_bwd_below(FrontTab T, const int32_t* __restrict__ list,
+                                                  const int32_t* __restrict__ bp_off, const double* __restrict__ arena,
+                                                  const double* __restrict__ xi, double* __restrict__ bpart) {
+  __shared__ double tile[64 * 65];
+  __shared__ double xr[64];
+  __shared__ double part[4][64];
+  int s, pc;
+  task_of(list, s, pc);
+  const int p = pc & 0xffff, chunk = pc >> 16;
+  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+  (void)f0;
+  const double* __restrict__ L = arena + T.l_off[s];
+  const int32_t* __restrict__ rows = T.rows + T.row_ptr[s];
+  const int c0 = p * 64, kw = min(64, w - c0);
+  const int nch = (r - w + BWD_CHUNK - 1) / BWD_CHUNK;
+  const int R0 = w + chunk * BWD_CHUNK, R1 = min(r, R0 + BWD_CHUNK);
+  const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
+  double acc = 0.0;
+  for (int rb = R0; rb < R1; rb += 64) {
+    const int nr = min(64, R1 - rb);
+    for (int j = g; j < 64; j += 4) tile[lane * 65 + j] = (lane < nr && j < kw) ? L[(rb + lane) + (int64_t)(c0 + j) * r] : 0.0;
+    if (tid < 64) xr[tid] = (tid < nr) ? xi[rows[rb + tid]] : 0.0;
+    __syncthreads();
+#pragma unroll
+    for (int rr = 0; rr < 16; ++rr) acc += tile[(g * 16 + rr) * 65 + lane] * xr[g * 16 + rr];
+    __syncthreads();
+  }
+  part[g][lane] = acc;
+  __syncthreads();
+  if (g == 0)
+    bpart[((int64_t)bp_off[s] + (int64_t)p * nch + chunk) * 64 + lane] =
+        (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+}
+
 // Backward, big fronts: task = (front, 64-column pivot panel p), processed from the last panel down.
 // acc(cols) = D^{-1} y(cols) - L(below,cols)^T x(below) - sum_{q > p} L(q-block,cols)^T x_q; x_p = L_pp^{-T} acc.
 __global__ __launch_bounds__(NT) void k_bwd_big(FrontTab T, const SolveTask* __restrict__ tasks, int ntasks,
                                                 int32_t* counter, int32_t* flags, const int32_t* __restrict__ flag_off,
                                                 int epoch, const double* __restrict__ arena,
                                                 const double* __restrict__ D, double* __restrict__ xi,
-                                                double* __restrict__ out, int32_t* err) {
+                                                double* __restrict__ out, const int32_t* __restrict__ bp_off,
+                                                const double* __restrict__ bpart, int32_t* err) {
   __shared__ int s_task;
   __shared__ double tile[64 * 65];
   __shared__ double xr[64];
@@ -625,35 +709,31 @@ __global__ __launch_bounds__(NT) void k_bwd_big(FrontTab T, const SolveTask* __r
     const int s = tasks[t].front, p = tasks[t].blk;
     const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
     const double* __restrict__ L = arena + T.l_off[s];
-    const int32_t* __restrict__ rows = T.rows + T.row_ptr[s];
     const int c0 = p * 64, kw = min(64, w - c0);
     const int npan = (w + 63) >> 6;
     // diagonal block L(c0+i, c0+j) -> Ld[i*65+j]
     for (int j = g; j < kw; j += 4) Ld[lane * 65 + j] = (lane < kw) ? L[(c0 + lane) + (int64_t)(c0 + j) * r] : 0.0;
     double acc = 0.0;  // partial for column c0+lane over this wave's rows of each tile
-    // row tiles: below rows first (independent), then pivot panels q = npan-1 .. p+1 (wait for each)
-    const int nbelow = (r - w + 63) >> 6;
-    for (int k = 0; k < nbelow + (npan - 1 - p); ++k) {
-      int rb, nr;
-      const bool below = k < nbelow;
-      if (below) {
-        rb = w + k * 64;
-        nr = min(64, r - rb);
-      } else {
-        const int q = npan - 1 - (k - nbelow);
-        rb = q * 64;
-        nr = min(64, w - rb);
-        if (tid == 0) wait_flag(&flags[flag_off[s] + q], epoch, err);
-        __syncthreads();
-      }
+    // pivot panels q = npan-1 .. p+1 (wait for each); the rows below come from k_bwd_below
+    for (int k = 0; k < npan - 1 - p; ++k) {
+      const int q = npan - 1 - k;
+      const int rb = q * 64, nr = min(64, w - rb);
+      if (tid == 0) wait_flag(&flags[flag_off[s] + q], epoch, err);
+      __syncthreads();
       // stage the 64 x 64 tile L(rb.., c0..) (coalesced over rows) and the x values of its rows
       for (int j = g; j < kw; j += 4) tile[lane * 65 + j] = (lane < nr) ? L[(rb + lane) + (int64_t)(c0 + j) * r] : 0.0;
-      if (tid < 64) xr[tid] = (tid < nr) ? (below ? xi[rows[rb + tid]] : xi[f0 + rb + tid]) : 0.0;
+      if (tid < 64) xr[tid] = (tid < nr) ? xi[f0 + rb + tid] : 0.0;
       __syncthreads();
-      // column c0+lane, rows g*16 .. g*16+15 of the tile
 #pragma unroll
       for (int rr = 0; rr < 16; ++rr) acc += tile[(g * 16 + rr) * 65 + lane] * xr[g * 16 + rr];
       __syncthreads();
+    }
+    if (g == 0 && r > w) {
+      const int nch = (r - w + BWD_CHUNK - 1) / BWD_CHUNK;
+      const double* __restrict__ bp = bpart + ((int64_t)bp_off[s] + (int64_t)p * nch) * 64 + lane;
+      double below = 0.0;
+      for (int c = 0; c < nch; ++c) below += bp[c * 64];
+      acc += below;
     }
     part[g][lane] = acc;
     __syncthreads();
@@ -719,18 +799,19 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   T_.rel_ptr = rel_ptr_;
   T_.rel = rel_;
   T_.perm = perm_;
-  crow_off_.upload(S.crow_off);
-  crow_.upload(S.crow);
-  ce_child_.upload(S.ce_child);
-  ce_row_.upload(S.ce_row);
-  bigch_ptr_.upload(S.bigch_ptr);
-  bigch_list_.upload(S.bigch_list);
-  T_.crow_off = crow_off_;
-  T_.crow = crow_;
-  T_.ce_child = ce_child_;
-  T_.ce_row = ce_row_;
-  T_.bigch_ptr = bigch_ptr_;
-  T_.bigch_list = bigch_list_;
+  fs_off_.upload(S.fs_off);
+  sv_ptr_.upload(S.sv_ptr);
+  sv_src_.upload(S.sv_src);
+  atiles_.upload(S.atiles);
+  g_ptr_.upload(S.g_ptr);
+  g_src_.upload(S.g_src);
+  g_chunk_.upload(S.g_chunk);
+  gpart_.alloc(std::max<size_t>(S.g_chunk.size(), 1));
+  bt_.upload(S.bt);
+  fscratch_.alloc(std::max<int64_t>(S.fs_size, 1));
+  T_.fs_off = fs_off_;
+  T_.sv_ptr = sv_ptr_;
+  T_.sv_src = sv_src_;
   {
     std::vector<int32_t> slot(std::max(S.nsuper, 1), -1);
     int nslot = 0;
@@ -744,7 +825,13 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   // ---- launch schedule
   std::vector<int32_t> sched;
   const int ns = S.nsuper;
+  auto align2 = [&]() {
+    if (sched.size() & 1) sched.push_back(0);
+  };
   for (int lev = 0; lev < S.nlevels; ++lev) {
+    if (S.atile_lev[lev + 1] > S.atile_lev[lev])
+      fact_.push_back({ASSEMBLE, 0, S.atile_lev[lev], 0, S.atile_lev[lev + 1] - S.atile_lev[lev], S.chunk_lev[lev],
+                       S.chunk_lev[lev + 1] - S.chunk_lev[lev]});
     std::vector<int32_t> cls[3], big;
     for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
       const int s = S.level_list[q];
@@ -760,57 +847,27 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         sched.insert(sched.end(), cls[c].begin(), cls[c].end());
       }
     if (big.empty()) continue;
-    auto add_big = [&](int kind, int step, const std::vector<int32_t>& fl, const std::vector<int64_t>& cnt) {
-      std::vector<int32_t> f2;
-      std::vector<int64_t> c2;
-      for (size_t q = 0; q < fl.size(); ++q)
-        if (cnt[q] > 0) {
-          f2.push_back(fl[q]);
-          c2.push_back(cnt[q]);
-        }
-      if (f2.empty()) return;
-      Launch L{kind, step, (int64_t)sched.size(), (int)f2.size(), 0};
-      sched.insert(sched.end(), f2.begin(), f2.end());
-      int64_t acc = 0;
-      for (size_t q = 0; q < f2.size(); ++q) {
-        sched.push_back((int32_t)acc);
-        acc += c2[q];
-      }
-      sched.push_back((int32_t)acc);
-      MADIPM_REQUIRE(acc < INT_MAX, "launch too large");
-      L.items = acc;
-      fact_.push_back(L);
-    };
-    std::vector<int64_t> ctile(big.size()), cpull(big.size()), cbig(big.size());
     int maxsteps = 0;
-    for (size_t q = 0; q < big.size(); ++q) {
-      const int s = big[q];
-      const int64_t nt = cdiv(S.nrows[s], 64);
-      ctile[q] = nt * (nt + 1) / 2;
-      const bool has_pull = S.crow[S.crow_off[s] + S.nrows[s]] > S.crow[S.crow_off[s]];
-      cpull[q] = has_pull ? cdiv(S.nrows[s], NT) : 0;
-      cbig[q] = (S.bigch_ptr[s + 1] > S.bigch_ptr[s]) ? ctile[q] : 0;
-      maxsteps = std::max<int>(maxsteps, (int)cdiv(S.first[s + 1] - S.first[s], 64));
-    }
-    add_big(BIG_TILES, 0, big, ctile);
-    add_big(BIG_PULL, 0, big, cpull);
-    add_big(BIG_BIGCH, 0, big, cbig);
+    for (int s : big) maxsteps = std::max<int>(maxsteps, (int)cdiv(S.first[s + 1] - S.first[s], 64));
     for (int p = 0; p < maxsteps; ++p) {
-      std::vector<int64_t> cd(big.size(), 0), ct(big.size(), 0), cu(big.size(), 0);
-      for (size_t q = 0; q < big.size(); ++q) {
-        const int s = big[q];
+      std::vector<int32_t> td, tt, tu;  // (front, item) pairs
+      for (int s : big) {
         const int w = S.first[s + 1] - S.first[s], r = S.nrows[s];
         if (cdiv(w, 64) <= p) continue;
         const int k0 = p * 64, kw = std::min(64, w - k0);
-        const int64_t below = r - k0 - kw;
-        cd[q] = 1;
-        const int64_t nt = cdiv(below, 64);
-        ct[q] = nt;
-        cu[q] = nt * (nt + 1) / 2;
+        const int nt = (int)cdiv(r - k0 - kw, 64);
+        td.insert(td.end(), {s, 0});
+        for (int i = 0; i < nt; ++i) tt.insert(tt.end(), {s, i});
+        for (int i = 0; i < nt; ++i)
+          for (int j = 0; j <= i; ++j) tu.insert(tu.end(), {s, i | (j << 16)});
       }
-      add_big(BIG_DIAG, p, big, cd);
-      add_big(BIG_TRSM, p, big, ct);
-      add_big(BIG_UPDATE, p, big, cu);
+      const std::pair<int, std::vector<int32_t>*> kinds[3] = {{BIG_DIAG, &td}, {BIG_TRSM, &tt}, {BIG_UPDATE, &tu}};
+      for (const auto& kv : kinds) {
+        if (kv.second->empty()) continue;
+        align2();
+        fact_.push_back({kv.first, p, (int64_t)sched.size(), 0, (int64_t)kv.second->size() / 2});
+        sched.insert(sched.end(), kv.second->begin(), kv.second->end());
+      }
     }
   }
   // ---- solve schedule: per level, small fronts (wave per front) and big fronts (task queues)
@@ -822,7 +879,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         flag_off[s] = (int32_t)nflags;
         nflags += cdiv(S.first[s + 1] - S.first[s], 64);
       }
-    std::vector<int32_t> tasks;
+    std::vector<int32_t> tasks, bp_off(ns, 0);
+    int64_t nbpart = 0;
     for (int lev = 0; lev < S.nlevels; ++lev) {
       std::vector<int32_t> small, big;
       for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
@@ -836,6 +894,22 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       L.big_off = (int64_t)sched.size();
       L.nbig = (int)big.size();
       sched.insert(sched.end(), big.begin(), big.end());
+      align2();
+      L.gat_off = (int64_t)sched.size();
+      for (int s : big)
+        for (int c = 0; c < cdiv(S.nrows[s], NT); ++c) sched.insert(sched.end(), {s, c});
+      L.ngat = (int)(((int64_t)sched.size() - L.gat_off) / 2);
+      L.below_off = (int64_t)sched.size();
+      for (int s : big) {
+        const int w = S.first[s + 1] - S.first[s], r = S.nrows[s];
+        if (r == w) continue;
+        const int np = (int)cdiv(w, 64), nch = (int)cdiv(r - w, BWD_CHUNK);
+        bp_off[s] = (int32_t)nbpart;
+        nbpart += (int64_t)np * nch;
+        for (int p = 0; p < np; ++p)
+          for (int c = 0; c < nch; ++c) sched.insert(sched.end(), {s, p | (c << 16)});
+      }
+      L.nbelow = (int)(((int64_t)sched.size() - L.below_off) / 2);
       int maxblk = 0, maxpan = 0;
       for (int s : big) {
         maxblk = std::max<int>(maxblk, (int)cdiv(S.nrows[s], 64));
@@ -863,6 +937,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     }
     tasks_.upload(tasks);
     flag_off_.upload(flag_off);
+    bp_off_.upload(bp_off);
+    bpart_.alloc(std::max<int64_t>(nbpart, 1) * 64);
     flags_.alloc(std::max<int64_t>(nflags, 1));
     flags_.zero();
     counters_.alloc(2 * std::max(S.nlevels, 1));
@@ -896,30 +972,29 @@ void LDLSolver::factorize_async(const double* Kx, hipStream_t s) {
   for (const Launch& L : fact_) {
     const int32_t* list = sched_.p + L.off;
     switch (L.kind) {
+      case ASSEMBLE:
+        if (L.nchunk)
+          k_asm_chunks<<<(unsigned)cdiv(L.nchunk, NT), NT, 0, s>>>(g_chunk_, g_src_, L.chunk0, L.nchunk, Kx, arena_, gpart_);
+        k_assemble<<<(unsigned)L.items, ANT, 0, s>>>(T_, atiles_.p + L.off, g_ptr_, gpart_, bt_, arena_, fscratch_);
+        break;
       case SMALL32:
+        k_tiny_factor<<<(unsigned)cdiv(L.items, 4), NT, 0, s>>>(T_, list, (int)L.items, Kx, arena_, fscratch_, D_, status_,
+                                                               pivot_tol);
+        break;
       case SMALL64:
       case SMALL128: {
         const int R = L.kind == SMALL32 ? 32 : (L.kind == SMALL64 ? 64 : 128);
-        k_small_factor<<<(unsigned)L.items, NT, R * R * 8, s>>>(T_, list, Kx, arena_, D_, status_, pivot_tol);
+        k_small_factor<<<(unsigned)L.items, NT, R * R * 8, s>>>(T_, list, Kx, arena_, fscratch_, D_, status_, pivot_tol);
         break;
       }
-      case BIG_TILES:
-        k_big_tiles<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.nf, Kx, arena_);
-        break;
-      case BIG_PULL:
-        k_big_pull<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.nf, arena_);
-        break;
-      case BIG_BIGCH:
-        k_big_bigch<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.nf, arena_);
-        break;
       case BIG_DIAG:
-        k_big_diag<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.nf, L.step, arena_, D_, minv_, status_, pivot_tol);
+        k_big_diag<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_, minv_, status_, pivot_tol);
         break;
       case BIG_TRSM:
-        k_big_trsm<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.nf, L.step, arena_, minv_);
+        k_big_trsm<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, minv_);
         break;
       case BIG_UPDATE:
-        k_big_update<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.nf, L.step, arena_, D_);
+        k_big_update<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_);
         break;
     }
   }
@@ -954,16 +1029,17 @@ void LDLSolver::solve_async(double* b, hipStream_t s) {
     const SolveLevel& L = slev_[lev];
     if (L.nsmall) k_fwd_small<<<(unsigned)cdiv(L.nsmall, SW), NT, 0, s>>>(T_, sched_.p + L.small_off, L.nsmall, arena_, b, xi_, uvec_);
     if (L.nbig) {
-      k_fwd_gather<<<L.nbig, NT, 0, s>>>(T_, sched_.p + L.big_off, b, uvec_, vwork_);
+      k_fwd_gather<<<L.ngat, NT, 0, s>>>(T_, sched_.p + L.gat_off, b, uvec_, vwork_);
       k_fwd_big<<<std::min(L.nftask, 512), NT, 0, s>>>(T_, tasks + L.ftask_off, L.nftask, counters_.p + 2 * lev, flags_,
                                                          flag_off_, efwd, arena_, vwork_, xi_, uvec_, err_);
     }
   }
   for (int lev = nl - 1; lev >= 0; --lev) {
     const SolveLevel& L = slev_[lev];
+    if (L.nbelow) k_bwd_below<<<L.nbelow, NT, 0, s>>>(T_, sched_.p + L.below_off, bp_off_, arena_, xi_, bpart_);
     if (L.nbig)
       k_bwd_big<<<std::min(L.nbtask, 512), NT, 0, s>>>(T_, tasks + L.btask_off, L.nbtask, counters_.p + 2 * lev + 1,
-                                                         flags_, flag_off_, ebwd, arena_, D_, xi_, b, err_);
+                                                         flags_, flag_off_, ebwd, arena_, D_, xi_, b, bp_off_, bpart_, err_);
     if (L.nsmall) k_bwd_small<<<(unsigned)cdiv(L.nsmall, SW), NT, 0, s>>>(T_, sched_.p + L.small_off, L.nsmall, arena_, D_, xi_, b);
   }
   MADIPM_HIP(hipGetLastError());

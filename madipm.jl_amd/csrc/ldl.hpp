@@ -32,12 +32,9 @@ struct FrontTab {
   const int64_t* rel_ptr;
   const int32_t* rel;
   const int32_t* perm;
-  const int64_t* crow_off;
-  const int64_t* crow;
-  const int32_t* ce_child;
-  const int32_t* ce_row;
-  const int32_t* bigch_ptr;
-  const int32_t* bigch_list;
+  const int64_t* fs_off;   // small fronts assembled by k_assemble: r x r scratch offset (else -1)
+  const int64_t* sv_ptr;   // forward-solve gather lists (indexed by row_ptr[s] + i)
+  const int64_t* sv_src;
   const int32_t* bigslot;  // big front -> slot in the panel-inverse scratch (64x64 per slot)
 };
 
@@ -75,20 +72,24 @@ class LDLSolver {
   const double* d_diag() const { return D_.p; }
 
  private:
-  enum Kind { SMALL32 = 0, SMALL64 = 1, SMALL128 = 2, BIG_TILES = 3, BIG_PULL = 4, BIG_BIGCH = 5, BIG_DIAG = 6, BIG_TRSM = 7,
-              BIG_UPDATE = 8 };
+  enum Kind { ASSEMBLE = 0, SMALL32 = 1, SMALL64 = 2, SMALL128 = 3, BIG_DIAG = 4, BIG_TRSM = 5, BIG_UPDATE = 6 };
   struct Launch {
     int kind;
     int step;       // panel step for BIG_DIAG / BIG_TRSM / BIG_UPDATE
-    int64_t off;    // offset of the front list in sched_ (then prefix[nf+1] for big kinds)
-    int nf;         // number of fronts
+    int64_t off;    // ASSEMBLE: first tile; SMALL*: front list in sched_; BIG_*: (front, item) pairs in sched_
+    int nf;         // number of fronts (SMALL*)
     int64_t items;  // workgroups
+    int64_t chunk0 = 0, nchunk = 0;  // ASSEMBLE: chunk range of the level
   };
   struct SolveLevel {
     int64_t small_off;
     int nsmall;
     int64_t big_off;
     int nbig;
+    int64_t gat_off;  // (front, 256-row chunk) pairs for k_fwd_gather
+    int ngat;
+    int64_t below_off;  // (front, panel | chunk << 16) pairs for k_bwd_below
+    int nbelow;
     int64_t ftask_off;
     int nftask;
     int64_t btask_off;
@@ -98,13 +99,16 @@ class LDLSolver {
   FrontTab T_{};
   std::vector<Launch> fact_;
   std::vector<SolveLevel> slev_;  // per level, leaves first
-  DBuf<int32_t> tasks_, flags_, flag_off_, counters_, err_;
+  DBuf<int32_t> tasks_, flags_, flag_off_, counters_, err_, bp_off_;
+  DBuf<double> bpart_;
   int epoch_ = 0;
   // device data
   DBuf<int32_t> first_, nrows_, rows_, u_ld_, child_ptr_, child_list_, rel_, perm_, sched_;
-  DBuf<int32_t> ce_child_, ce_row_, bigch_ptr_, bigch_list_, bigslot_;
-  DBuf<double> minv_;
-  DBuf<int64_t> row_ptr_, l_off_, u_off_, uvec_off_, asm_ptr_, asm_src_, asm_dst64_, rel_ptr_, crow_off_, crow_;
+  DBuf<int32_t> bigslot_, g_ptr_, bt_;
+  DBuf<int64_t> fs_off_, sv_ptr_, sv_src_, g_src_, g_chunk_;
+  DBuf<SymbolicPlan::AsmTile> atiles_;
+  DBuf<double> minv_, fscratch_, gpart_;
+  DBuf<int64_t> row_ptr_, l_off_, u_off_, uvec_off_, asm_ptr_, asm_src_, asm_dst64_, rel_ptr_;
   DBuf<double> arena_, D_, xi_, uvec_, vwork_;
   DBuf<LDLStatus> status_;
   LDLStatus* h_status_ = nullptr;

@@ -439,42 +439,135 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   S.arena_size = cur;
   S.uvec_size = ucur;
 
-  // ---------------- 10. extend-add "pull" lists: for every parent row, the (child, child row)
-  // pairs that contribute to it, children in a fixed order.  One thread owns a parent row and sums
-  // its contributions in that order: parallel AND deterministic.  Children whose update block is
-  // larger than kPullMax rows are handled column-wise by the tiled big-front kernels instead.
-  S.crow_off.assign(ns + 1, 0);
-  for (int s = 0; s < ns; ++s) S.crow_off[s + 1] = S.crow_off[s] + S.nrows[s] + 1;
-  S.crow.assign(S.crow_off[ns], 0);
-  S.bigch_ptr.assign(ns + 1, 0);
-  S.bigch_list.clear();
-  S.ce_child.clear();
-  S.ce_row.clear();
-  {
-    std::vector<std::vector<std::pair<int32_t, int32_t>>> bucket;
-    for (int s = 0; s < ns; ++s) {
-      const int r = S.nrows[s];
-      bucket.assign(r, {});
-      for (int64_t q = S.child_ptr[s]; q < S.child_ptr[s + 1]; ++q) {
-        const int c = S.child_list[q];
-        const int uc = S.nrows[c] - (S.first[c + 1] - S.first[c]);
-        if (uc > SymbolicPlan::kPullMax) {
-          S.bigch_list.push_back(c);
-          continue;
-        }
-        for (int a = 0; a < uc; ++a) bucket[S.rel[S.rel_ptr[c] + a]].emplace_back(c, a);
-      }
-      S.bigch_ptr[s + 1] = (int32_t)S.bigch_list.size();
-      int64_t base = S.crow_off[s];
-      S.crow[base] = (int64_t)S.ce_child.size();
-      for (int i = 0; i < r; ++i) {
-        for (auto& e : bucket[i]) {
-          S.ce_child.push_back(e.first);
-          S.ce_row.push_back(e.second);
-        }
-        S.crow[base + i + 1] = (int64_t)S.ce_child.size();
-      }
+  // ---------------- 10. assembly plan.  Each task is one 64x64 lower tile of a front's F: its entries
+  // are the sums of their gather lists (original K entries first, then the small children's update
+  // entries in child order), then the big children's update blocks are added child by child.  A
+  // workgroup owns a tile, so the sums are parallel, conflict-free and deterministic.
+  S.fs_off.assign(ns, -1);
+  S.fs_size = 0;
+  for (int s = 0; s < ns; ++s)
+    if (!S.is_big[s] && S.child_ptr[s + 1] > S.child_ptr[s]) {
+      S.fs_off[s] = S.fs_size;
+      S.fs_size += (int64_t)S.nrows[s] * S.nrows[s];
     }
+  S.atiles.clear();
+  S.g_ptr.clear();
+  S.g_src.clear();
+  S.bt.clear();
+  S.atile_lev.assign(S.nlevels + 1, 0);
+  S.chunk_lev.assign(S.nlevels + 1, 0);
+  S.g_chunk.clear();
+  {
+    std::vector<int32_t> key, cnt;
+    std::vector<int64_t> src, sorted;
+    for (int lev = 0; lev < S.nlevels; ++lev) {
+      for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
+        const int s = S.level_list[q];
+        if (!S.is_big[s] && S.fs_off[s] < 0) continue;
+        const int r = S.nrows[s];
+        const int nt = (r + 63) / 64;
+        const int ntile = nt * (nt + 1) / 2;
+        auto tkey = [&](int row, int col) {
+          const int ti = row >> 6, tj = col >> 6;
+          return (int32_t)((ti * (ti + 1) / 2 + tj) * 4096 + (row & 63) + (col & 63) * 64);
+        };
+        key.clear();
+        src.clear();
+        for (int64_t qa = S.asm_ptr[s]; qa < S.asm_ptr[s + 1]; ++qa) {
+          const int64_t d = S.asm_dst[qa];
+          key.push_back(tkey((int)(d % r), (int)(d / r)));
+          src.push_back(~S.asm_src[qa]);
+        }
+        std::vector<int32_t> bigch;
+        for (int64_t qc = S.child_ptr[s]; qc < S.child_ptr[s + 1]; ++qc) {
+          const int c = S.child_list[qc];
+          const int uc = S.nrows[c] - (S.first[c + 1] - S.first[c]);
+          if (uc > SymbolicPlan::kGatherMax) {
+            bigch.push_back(c);
+            continue;
+          }
+          const int32_t* relc = S.rel.data() + S.rel_ptr[c];
+          for (int bb = 0; bb < uc; ++bb)
+            for (int aa = bb; aa < uc; ++aa) {
+              key.push_back(tkey(relc[aa], relc[bb]));
+              src.push_back(S.u_off[c] + aa + (int64_t)bb * S.u_ld[c]);
+            }
+        }
+        // stable counting sort by key (keeps originals-then-children order per entry)
+        const int64_t nkeys = (int64_t)ntile * 4096;
+        cnt.assign(nkeys + 1, 0);
+        for (int32_t k : key) cnt[k + 1]++;
+        for (int64_t k = 0; k < nkeys; ++k) cnt[k + 1] += cnt[k];
+        sorted.resize(src.size());
+        {
+          std::vector<int32_t> fill(cnt.begin(), cnt.end() - 1);
+          for (size_t e = 0; e < key.size(); ++e) sorted[fill[key[e]]++] = src[e];
+        }
+        for (int ti = 0; ti < nt; ++ti)
+          for (int tj = 0; tj <= ti; ++tj) {
+            const int t = ti * (ti + 1) / 2 + tj;
+            SymbolicPlan::AsmTile at{};
+            at.front = s;
+            at.tij = ti | (tj << 16);
+            const int64_t k0 = (int64_t)t * 4096, k1 = k0 + 4096;
+            if (cnt[k1] > cnt[k0]) {
+              at.gptr = (int64_t)S.g_ptr.size();
+              at.gchk = (int64_t)S.g_chunk.size();
+              int32_t nchk = 0;
+              const int64_t sbase = (int64_t)S.g_src.size() - cnt[k0];
+              for (int64_t k = k0; k < k1; ++k) {
+                S.g_ptr.push_back(nchk);
+                for (int64_t c = cnt[k]; c < cnt[k + 1]; c += SymbolicPlan::kChunk, ++nchk) S.g_chunk.push_back(sbase + c);
+              }
+              S.g_ptr.push_back(nchk);
+              S.g_src.insert(S.g_src.end(), sorted.begin() + cnt[k0], sorted.begin() + cnt[k1]);
+            } else {
+              at.gptr = -1;
+              at.gchk = 0;
+            }
+            at.bt0 = (int32_t)(S.bt.size() / 5);
+            const int I0 = ti * 64, I1 = std::min(r, I0 + 64), J0 = tj * 64, J1 = std::min(r, J0 + 64);
+            for (int c : bigch) {
+              const int uc = S.nrows[c] - (S.first[c + 1] - S.first[c]);
+              const int32_t* relc = S.rel.data() + S.rel_ptr[c];
+              const int b0 = (int)(std::lower_bound(relc, relc + uc, J0) - relc);
+              const int b1 = (int)(std::lower_bound(relc + b0, relc + uc, J1) - relc);
+              const int a0 = (int)(std::lower_bound(relc, relc + uc, I0) - relc);
+              const int a1 = (int)(std::lower_bound(relc + a0, relc + uc, I1) - relc);
+              if (b0 < b1 && a0 < a1 && a1 - 1 >= b0) {
+                const int32_t e[5] = {c, b0, b1, a0, a1};
+                S.bt.insert(S.bt.end(), e, e + 5);
+              }
+            }
+            at.bt1 = (int32_t)(S.bt.size() / 5);
+            S.atiles.push_back(at);
+          }
+      }
+      S.atile_lev[lev + 1] = (int32_t)S.atiles.size();
+      S.chunk_lev[lev + 1] = (int64_t)S.g_chunk.size();
+    }
+    S.g_chunk.push_back((int64_t)S.g_src.size());  // sentinel
+    MADIPM_REQUIRE(S.g_src.size() < (size_t)INT32_MAX * 2 && S.atiles.size() < (size_t)INT32_MAX, "assembly plan too large");
+  }
+
+  // ---------------- 11. forward-solve gather lists (all children, child order)
+  S.sv_ptr.assign(S.row_ptr[ns] + 1, 0);
+  for (int s = 0; s < ns; ++s)
+    for (int64_t qc = S.child_ptr[s]; qc < S.child_ptr[s + 1]; ++qc) {
+      const int c = S.child_list[qc];
+      const int uc = S.nrows[c] - (S.first[c + 1] - S.first[c]);
+      for (int aa = 0; aa < uc; ++aa) S.sv_ptr[S.row_ptr[s] + S.rel[S.rel_ptr[c] + aa] + 1]++;
+    }
+  for (int64_t t = 0; t < S.row_ptr[ns]; ++t) S.sv_ptr[t + 1] += S.sv_ptr[t];
+  S.sv_src.assign(S.sv_ptr[S.row_ptr[ns]], 0);
+  {
+    std::vector<int64_t> fill(S.sv_ptr.begin(), S.sv_ptr.end() - 1);
+    for (int s = 0; s < ns; ++s)
+      for (int64_t qc = S.child_ptr[s]; qc < S.child_ptr[s + 1]; ++qc) {
+        const int c = S.child_list[qc];
+        const int uc = S.nrows[c] - (S.first[c + 1] - S.first[c]);
+        for (int aa = 0; aa < uc; ++aa) S.sv_src[fill[S.row_ptr[s] + S.rel[S.rel_ptr[c] + aa]]++] = S.uvec_off[c] + aa;
+      }
   }
 }
 

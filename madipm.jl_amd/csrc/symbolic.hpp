@@ -48,11 +48,29 @@ struct SymbolicPlan {
   std::vector<int32_t> u_ld;
   std::vector<int64_t> uvec_off;       // solve update vector (r - w)
   std::vector<uint8_t> is_big;
-  // extend-add pull lists (see symbolic.cpp step 10)
-  static constexpr int kPullMax = 128;
-  std::vector<int64_t> crow_off, crow;  // per front: r+1 offsets into ce_* (global)
-  std::vector<int32_t> ce_child, ce_row;
-  std::vector<int32_t> bigch_ptr, bigch_list;  // children with update blocks > kPullMax rows
+  // assembly plan (see symbolic.cpp step 10): every big front and every small front with children
+  // is assembled tile by tile (64x64 lower tiles).  The sources of each tile entry (original K
+  // entries, then the small children's update entries, fixed order) are cut into chunks of at most
+  // kChunk consecutive sources; chunk sums are formed by a flat kernel, then each entry sums its
+  // chunks in order (deterministic, no atomics).  Big children (update blocks > kGatherMax rows)
+  // are added per tile from their row/column ranges.
+  static constexpr int kGatherMax = 128;
+  static constexpr int kChunk = 8;
+  struct AsmTile {
+    int32_t front, tij;    // tij = ti | tj << 16
+    int32_t bt0, bt1;      // range in bt (5 ints per big-child block: child, b0, b1, a0, a1)
+    int64_t gptr, gchk;    // base of the 4097 per-entry chunk offsets in g_ptr (-1: none), first chunk
+  };
+  std::vector<AsmTile> atiles;
+  std::vector<int32_t> atile_lev;      // per level: range of atiles
+  std::vector<int64_t> chunk_lev;      // per level: range of chunks
+  std::vector<int32_t> g_ptr, bt;
+  std::vector<int64_t> g_chunk;        // chunk c = sources [g_chunk[c], g_chunk[c+1])
+  std::vector<int64_t> g_src;          // >= 0: arena index; < 0: ~(index into caller's values)
+  std::vector<int64_t> fs_off;         // small fronts with children: r x r scratch (else -1)
+  int64_t fs_size = 0;
+  // forward-solve gather: for every front row, the children's update-vector entries in child order
+  std::vector<int64_t> sv_ptr, sv_src;  // sv_ptr indexed by row_ptr[s] + i
   int64_t arena_size = 0, uvec_size = 0;
   // statistics
   int64_t nnzL = 0;          // exact nnz(L) incl. diagonal (column counts)
