@@ -254,77 +254,150 @@ __device__ __forceinline__ void task_of(const int32_t* __restrict__ list, int& s
 }
 
 
-// Diagonal block of 64-column panel `step` (one workgroup per front): factor it, write L11 and D,
-// and form M = L11^{-T} D^{-1} for the MFMA solve of the rows below (k_big_trsm).
-// Register-resident: lane = row i, wave wv owns columns j = wv + 4u (u < 16).  Step t publishes
-// column t through LDS (one barrier per step); the same row operations applied to an identity give
-// X = L11^{-1} on the fly (row t of X is read with readlane), so the inverse costs no extra steps.
-__device__ __forceinline__ double readlane_f64(double v, int l) {
-  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
-  return __hiloint2double(hi, lo);
+// ---- blocked 64x64 panel kernels (16x16 sub-blocks; wave w owns sub-block row w)
+// Layout conventions: A64 = LDS 64x64 tile, col-major, ld 65.  MFMA f64 16x16x4 fragments:
+// A operand lane l = (m = l & 15, k = l >> 4); B operand lane l = (k = l >> 4, n = l & 15);
+// result D lane l, element g = (m = (l >> 4) + 4 g, n = l & 15).
+constexpr int LDA = 65;
+constexpr int LDM = 17;
+
+// Factor the 16x16 diagonal sub-block K of A64 with ONE wave (LDS column broadcast, no barriers):
+// writes the unit-lower L_KK (strictly lower part) into A64, d into Dl, and M_K = L_KK^{-T} D_K^{-1}
+// (16x16, ld 17) into MK.  The same row operations applied to an identity give X = L_KK^{-1}.
+__device__ __forceinline__ void factor16(double* A64, double* Dl, double* MK, double* cb, double* xb, int K, int lane) {
+  const int il = lane & 15, cg = lane >> 4;
+  const int i = 16 * K + il;
+  double a[4], x[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int jl = cg + 4 * m;
+    a[m] = (jl <= il) ? A64[i + (16 * K + jl) * LDA] : 0.0;
+    x[m] = (jl == il) ? 1.0 : 0.0;
+  }
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    if (cg == (t & 3)) cb[t * LDM + il] = a[t >> 2];
+    if (il == t) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) xb[t * LDM + cg + 4 * m] = x[m];
+    }
+    wave_sync();
+    const double dt = cb[t * LDM + t];
+    const double li = (il > t) ? cb[t * LDM + il] / dt : 0.0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int jl = cg + 4 * m;
+      const double cj = cb[t * LDM + jl];
+      const double xt = xb[t * LDM + jl];
+      a[m] = fma(jl > t ? -li : 0.0, cj, a[m]);
+      x[m] = fma(jl > t ? 0.0 : -li, xt, x[m]);
+    }
+  }
+  wave_sync();
+  const double di = cb[il * LDM + il];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int jl = cg + 4 * m;
+    if (jl < il) A64[i + (16 * K + jl) * LDA] = a[m] / cb[jl * LDM + jl];
+    MK[jl * LDM + il] = (jl <= il) ? x[m] / di : 0.0;  // M[k=jl][n=il] = X(il, jl) / d_il
+  }
+  if (cg == 0) Dl[i] = di;
+  wave_sync();
 }
 
+// Blocked LDL^T of the LDS tile A64 (lower part valid) by 4 waves: after the call A64 holds the
+// strictly-lower L (diagonal untouched), Dl the pivots and Ms[K] the four M_K blocks.
+__device__ __forceinline__ void diag64(double* A64, double* Dl, double* Ms, double* cbuf, int tid) {
+  const int lane = tid & 63, w = tid >> 6;
+  double* cb = cbuf + w * 2 * 16 * LDM;
+  double* xb = cb + 16 * LDM;
+  for (int K = 0; K < 4; ++K) {
+    if (w == K) factor16(A64, Dl, Ms + K * 16 * LDM, cb, xb, K, lane);
+    __syncthreads();
+    dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+    if (w > K) {  // L_wK = A_wK M_K
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int k = 4 * ks + (lane >> 4);
+        const double av = A64[(16 * w + (lane & 15)) + (16 * K + k) * LDA];
+        const double bv = Ms[K * 16 * LDM + k * LDM + (lane & 15)];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      }
+    }
+    __syncthreads();  // every wave has read A_wK before it is overwritten
+    if (w > K) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) A64[(16 * w + (lane >> 4) + 4 * g) + (16 * K + (lane & 15)) * LDA] = acc[g];
+    }
+    __syncthreads();
+    if (w > K) {  // A_wJ -= (L_wK D_K) L_JK^T, K < J <= w
+      for (int J = K + 1; J <= w; ++J) {
+        dbl4 u = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const int k = 4 * ks + (lane >> 4);
+          const double av = A64[(16 * w + (lane & 15)) + (16 * K + k) * LDA] * Dl[16 * K + k];
+          const double bv = A64[(16 * J + (lane & 15)) + (16 * K + k) * LDA];
+          u = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, u, 0, 0, 0);
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) A64[(16 * w + (lane >> 4) + 4 * g) + (16 * J + (lane & 15)) * LDA] -= u[g];
+      }
+    }
+    // next K: wave K+1 factors the block it just updated itself; the others read M_{K+1} after
+    // the barrier at the top of the next iteration
+  }
+  __syncthreads();
+}
+
+// Diagonal block of 64-column panel `step` (one workgroup per front): load, blocked factorisation,
+// write L11 (d on the diagonal), D and the M_K blocks for k_big_trsm.
 __global__ __launch_bounds__(NT) void k_big_diag(FrontTab T, const int32_t* __restrict__ list, int step,
                                                  double* __restrict__ arena, double* __restrict__ D,
                                                  double* __restrict__ Mbuf, LDLStatus* st, double tol) {
-  __shared__ double col[64 * 65];  // col[t*65 + i] = A(i, t) after step t
+  __shared__ double A64[64 * LDA];
+  __shared__ double Ms[4 * 16 * LDM];
+  __shared__ double Dl[64];
+  __shared__ double cbuf[4 * 2 * 16 * LDM];
   int s, item;
   task_of(list, s, item);
   (void)item;
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
   const int k0 = step * 64, kw = min(64, w - k0);
   double* __restrict__ F = arena + T.l_off[s] + k0 + (int64_t)k0 * r;
-  const int tid = threadIdx.x, i = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR) => scalar branches
-  double a[16], x[16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  {
+    double v[16];
 #pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int j = wv + 4 * u;
-    a[u] = (i < kw && j < kw) ? (i >= j ? F[i + (int64_t)j * r] : 0.0) : (i == j ? 1.0 : 0.0);
-    x[u] = (i == j) ? 1.0 : 0.0;
-  }
-#pragma unroll
-  for (int t = 0; t < 64; ++t) {
-    if (wv == (t & 3)) col[t * 65 + i] = a[t >> 2];
-    __syncthreads();
-    const double dt = col[t * 65 + t], ct = col[t * 65 + i];
-    double cj[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) cj[u] = col[t * 65 + wv + 4 * u];
-    const double li = (i > t) ? ct / dt : 0.0;
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const bool right = wv + 4 * u > t;  // column j right of t: factor update; else: row op on X
-      a[u] = fma(right ? -li : 0.0, cj[u], a[u]);
-      x[u] = fma(right ? 0.0 : -li, readlane_f64(x[u], t), x[u]);
+    for (int e = 0; e < 16; ++e) {
+      const int j = wv + 4 * e;
+      v[e] = (lane < kw && j < kw) ? (lane >= j ? F[lane + (int64_t)j * r] : 0.0) : (lane == j ? 1.0 : 0.0);
     }
-  }
-  const double di = col[i * 65 + i];
 #pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int j = wv + 4 * u;
-    if (i < kw && j < kw && i >= j) F[i + (int64_t)j * r] = (i == j) ? di : a[u] / col[j * 65 + j];
+    for (int e = 0; e < 16; ++e) A64[lane + (wv + 4 * e) * LDA] = v[e];
   }
-  if (wv == 0 && i < kw) {
-    D[f0 + k0 + i] = di;
-    if (bad_pivot(di, tol)) atomicMin(&st->fail_pivot, f0 + k0 + i + 1);
+  __syncthreads();
+  diag64(A64, Dl, Ms, cbuf, tid);
+  for (int j = wv; j < kw; j += 4)
+    if (lane >= j && lane < kw) F[lane + (int64_t)j * r] = (lane == j) ? Dl[j] : A64[lane + j * LDA];
+  if (tid < kw) {
+    const double d = Dl[tid];
+    D[f0 + k0 + tid] = d;
+    if (bad_pivot(d, tol)) atomicMin(&st->fail_pivot, f0 + k0 + tid + 1);
   }
   double* __restrict__ M = Mbuf + (int64_t)T.bigslot[s] * 4096;
-#pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int j = wv + 4 * u;
-    M[j * 64 + i] = (i < kw && j < kw && i >= j) ? x[u] / di : 0.0;
-  }
+  for (int e = tid; e < 4 * 16 * LDM; e += NT) M[e] = Ms[e];
 }
 
-// Rows below the diagonal block of panel `step`: L21 = F21 * M (64-row tiles, f64 MFMA 16x16x4),
-// computed as the transpose D'[t][i] = sum_k M[k][t] F21[i][k] so that lanes run along F's rows.
+// Rows below the diagonal block of panel `step` (64-row tiles; wave w owns 16 rows): blocked
+// forward substitution X_K = A_K - sum_{J<K} (L_J D_J) L_KJ^T, L_K = X_K M_K, all on f64 MFMA.
 __global__ __launch_bounds__(NT) void k_big_trsm(FrontTab T, const int32_t* __restrict__ list, int step,
-                                                 double* __restrict__ arena, const double* __restrict__ Mbuf) {
-  constexpr int LDT = 80;
-  __shared__ __attribute__((aligned(16))) double Ms[64 * LDT];
-  __shared__ __attribute__((aligned(16))) double At[64 * LDT];
+                                                 double* __restrict__ arena, const double* __restrict__ D,
+                                                 const double* __restrict__ Mbuf) {
+  __shared__ double L11[64 * LDA];
+  __shared__ double Ms[4 * 16 * LDM];
+  __shared__ double Dl[64];
+  __shared__ double Sl[4][17 * 64];  // per-wave slab: 16 rows x 64 cols, S[m + 17 * j]
   int s, rt;
   task_of(list, s, rt);
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
@@ -333,48 +406,68 @@ __global__ __launch_bounds__(NT) void k_big_trsm(FrontTab T, const int32_t* __re
   double* __restrict__ F = arena + T.l_off[s];
   const double* __restrict__ M = Mbuf + (int64_t)T.bigslot[s] * 4096;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  (void)f0;
-  for (int kk = wv; kk < 64; kk += 4) {
-    Ms[kk * LDT + lane] = M[kk * 64 + lane];
-    At[kk * LDT + lane] = (kk < kw && I0 + lane < r) ? F[(I0 + lane) + (int64_t)(k0 + kk) * r] : 0.0;
+  double* S = Sl[wv];
+  const int row = I0 + 16 * wv + (lane & 15);  // slab row of this lane; 4 columns per pass
+  {
+    double lv[16], sv[16], mv[5], dv;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int j = wv + 4 * e;
+      lv[e] = (lane < kw && j < kw && lane > j) ? F[(k0 + lane) + (int64_t)(k0 + j) * r] : 0.0;
+      const int jj = (lane >> 4) + 4 * e;
+      sv[e] = (row < r && jj < kw) ? F[row + (int64_t)(k0 + jj) * r] : 0.0;
+    }
+#pragma unroll
+    for (int e = 0; e < 5; ++e) mv[e] = (tid + e * NT < 4 * 16 * LDM) ? M[tid + e * NT] : 0.0;
+    dv = (tid < kw) ? D[f0 + k0 + tid] : 1.0;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      L11[lane + (wv + 4 * e) * LDA] = lv[e];
+      S[(lane & 15) + ((lane >> 4) + 4 * e) * 17] = sv[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 5; ++e)
+      if (tid + e * NT < 4 * 16 * LDM) Ms[tid + e * NT] = mv[e];
+    if (tid < 64) Dl[tid] = dv;
   }
   __syncthreads();
-  const int qt = (wv >> 1) * 32, qi = (wv & 1) * 32;
-  dbl4 acc[2][2];
+  for (int K = 0; K < 4; ++K) {
+    dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int J = 0; J < K; ++J) {
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int ks = 0; ks < 16; ++ks) {
-    const int kk = ks * 4 + (lane >> 4);
-    const double a0 = Ms[kk * LDT + qt + (lane & 15)];
-    const double a1 = Ms[kk * LDT + qt + 16 + (lane & 15)];
-    const double b0 = At[kk * LDT + qi + (lane & 15)];
-    const double b1 = At[kk * LDT + qi + 16 + (lane & 15)];
-    acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-    acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-    acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-    acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
-  }
-#pragma unroll
-  for (int bt = 0; bt < 2; ++bt)
-#pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int i = I0 + qi + bi * 16 + (lane & 15);
-        const int t = qt + bt * 16 + (lane >> 4) + 4 * g;
-        if (i < r && t < kw) F[i + (int64_t)(k0 + t) * r] = acc[bt][bi][g];
+      for (int ks = 0; ks < 4; ++ks) {
+        const int k = 16 * J + 4 * ks + (lane >> 4);
+        const double av = S[(lane & 15) + k * 17] * Dl[k];
+        const double bv = L11[(16 * K + (lane & 15)) + k * LDA];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
       }
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) S[((lane >> 4) + 4 * g) + (16 * K + (lane & 15)) * 17] -= acc[g];
+    wave_sync();
+    dbl4 l = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int k = 4 * ks + (lane >> 4);
+      const double av = S[(lane & 15) + (16 * K + k) * 17];
+      const double bv = Ms[K * 16 * LDM + k * LDM + (lane & 15)];
+      l = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, l, 0, 0, 0);
+    }
+    wave_sync();
+#pragma unroll
+    for (int g = 0; g < 4; ++g) S[((lane >> 4) + 4 * g) + (16 * K + (lane & 15)) * 17] = l[g];
+    wave_sync();
+  }
+  for (int j = lane >> 4; j < kw; j += 4)
+    if (row < r) F[row + (int64_t)(k0 + j) * r] = S[(lane & 15) + j * 17];
 }
 
 // Trailing update of one 64x64 lower tile: C -= (L_I D) L_J^T, f64 MFMA 16x16x4.
 __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __restrict__ list, int step,
                                                    double* __restrict__ arena, const double* __restrict__ D) {
   constexpr int LDT = 80;  // [k][row] layout: conflict-free ds_read_b64 for the 16x4 operand pattern
-  __shared__ __attribute__((aligned(16))) double Wt[32 * LDT];
-  __shared__ __attribute__((aligned(16))) double Lt[32 * LDT];
+  __shared__ __attribute__((aligned(16))) double Wt[64 * LDT];
+  __shared__ __attribute__((aligned(16))) double Lt[64 * LDT];
   int s, tij;
   task_of(list, s, tij);
   const int ti = tij & 0xffff, tj = tij >> 16;
@@ -385,39 +478,55 @@ __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __
   const double* __restrict__ Dp = D + f0 + k0;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int qr = (wv >> 1) * 32, qc = (wv & 1) * 32;
+  // all global loads of the operands first (one latency), then the LDS stores
+  double wl[16], ll[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int kk = wv + 4 * e;
+    const int64_t col = (int64_t)(k0 + kk) * r;
+    wl[e] = (kk < kw && I0 + lane < r) ? F[(I0 + lane) + col] : 0.0;
+    ll[e] = (kk < kw && J0 + lane < r) ? F[(J0 + lane) + col] : 0.0;
+  }
+  double dk[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) dk[e] = (wv + 4 * e < kw) ? Dp[wv + 4 * e] : 0.0;
+  // C tile prefetch (its latency overlaps the MFMA loop)
+  double c[2][2][4];
+#pragma unroll
+  for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int i = I0 + qr + bi * 16 + (lane & 15);
+        const int j = J0 + qc + bj * 16 + (lane >> 4) + 4 * g;
+        c[bj][bi][g] = (i < r && j < r && i >= j) ? F[i + (int64_t)j * r] : 0.0;
+      }
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int kk = wv + 4 * e;
+    Wt[kk * LDT + lane] = wl[e] * dk[e];
+    Lt[kk * LDT + lane] = ll[e];
+  }
+  __syncthreads();
   dbl4 acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
-  for (int kc = 0; kc < kw; kc += 32) {
+  const int nks = (kw + 3) >> 2;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int kk = wv + 4 * e;
-      const int kg = kc + kk;
-      double wvv = 0.0, lv = 0.0;
-      if (kg < kw) {
-        const int64_t col = (int64_t)(k0 + kg) * r;
-        if (I0 + lane < r) wvv = F[(I0 + lane) + col] * Dp[kg];
-        if (J0 + lane < r) lv = F[(J0 + lane) + col];
-      }
-      Wt[kk * LDT + lane] = wvv;
-      Lt[kk * LDT + lane] = lv;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      const int kk = ks * 4 + (lane >> 4);
-      const double a0 = Lt[kk * LDT + qc + (lane & 15)];
-      const double a1 = Lt[kk * LDT + qc + 16 + (lane & 15)];
-      const double b0 = Wt[kk * LDT + qr + (lane & 15)];
-      const double b1 = Wt[kk * LDT + qr + 16 + (lane & 15)];
-      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
-    }
-    __syncthreads();
+  for (int ks = 0; ks < 16; ++ks) {
+    if (ks >= nks) break;
+    const int kk = ks * 4 + (lane >> 4);
+    const double a0 = Lt[kk * LDT + qc + (lane & 15)];
+    const double a1 = Lt[kk * LDT + qc + 16 + (lane & 15)];
+    const double b0 = Wt[kk * LDT + qr + (lane & 15)];
+    const double b1 = Wt[kk * LDT + qr + 16 + (lane & 15)];
+    acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+    acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+    acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
   }
   // D layout: col n = lane&15 (-> row i of F), row m = (lane>>4) + 4g (-> column j of F)
 #pragma unroll
@@ -428,7 +537,7 @@ __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __
       for (int g = 0; g < 4; ++g) {
         const int i = I0 + qr + bi * 16 + (lane & 15);
         const int j = J0 + qc + bj * 16 + (lane >> 4) + 4 * g;
-        if (i < r && j < r) F[i + (int64_t)j * r] -= acc[bj][bi][g];
+        if (i < r && j < r && i >= j) F[i + (int64_t)j * r] = c[bj][bi][g] - acc[bj][bi][g];
       }
 }
 
@@ -991,7 +1100,7 @@ void LDLSolver::factorize_async(const double* Kx, hipStream_t s) {
         k_big_diag<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_, minv_, status_, pivot_tol);
         break;
       case BIG_TRSM:
-        k_big_trsm<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, minv_);
+        k_big_trsm<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_, minv_);
         break;
       case BIG_UPDATE:
         k_big_update<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_);
