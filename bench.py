@@ -71,6 +71,30 @@ def cpu_baseline(qp, perm, budget_s: float = 20.0):
                       f"(numpy) + oracle/ldl_ref.c up-looking LDL^T (1 thread), loop time {st.total_time:.2f}s"}
 
 
+# Peaks (MI355X): HBM3E 8.0 TB/s spec (/opt/skills/guides/MI355X_MICROARCH.md); f64 MFMA
+# (v_mfma_f64_16x16x4f64) 78.6 TFLOP/s dense, AMD spec (the guide tabulates no f64 row;
+# profiles/r1_mfma_f64_peak.txt holds our own measurement of the instruction's rate).
+PEAK_HBM_GBS = 8000.0
+PEAK_F64_TFS = 78.6
+
+
+def roofline(stats: list, dominant: str):
+    """Roofline object for the dominant kernel from the live HIP-event statistics of the timed region."""
+    k = next(x for x in stats if x["name"] == dominant)
+    if k["launches"] == 0 or k["time_ms"] <= 0:
+        return None
+    avg_s = k["time_ms"] / k["launches"] * 1e-3
+    flops, nbytes = k["flops"] / k["launches"], k["bytes"] / k["launches"]
+    mfma = flops / (PEAK_F64_TFS * 1e12) > nbytes / (PEAK_HBM_GBS * 1e9)
+    if mfma:
+        ach, peak, unit = flops / avg_s / 1e12, PEAK_F64_TFS, "TFLOP/s"
+    else:
+        ach, peak, unit = nbytes / avg_s / 1e9, PEAK_HBM_GBS, "GB/s"
+    return {"bound": "mfma" if mfma else "hbm", "achieved": ach, "peak": peak, "unit": unit, "frac": ach / peak,
+            "traffic": None, "kernel": dominant, "launches": k["launches"], "avg_launch_us": avg_s * 1e6,
+            "alg_bytes_per_launch": nbytes, "alg_flops_per_launch": flops}
+
+
 def aggregate(dt, iters, dist, dev):
     """Whole-job numbers: max time over ranks, sum of iterations over ranks (replicas)."""
     if dist is None:
@@ -118,10 +142,15 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    # warmup: W iterations (untimed)
-    solver.set_max_iter(max(args.warmup, 0))
+    # warmup: W iterations (untimed); every LDL^T kernel kind timed to find the dominant one
+    solver.set_kernel_timing()
+    solver.set_max_iter(max(args.warmup, 1))
     solver.solve()
-    # timed: EXACTLY K MPC iterations after initialize!
+    warm = solver.kernel_stats()
+    dominant = max(warm, key=lambda k: k["time_ms"])["name"]
+    breakdown = {k["name"]: round(k["time_ms"], 3) for k in sorted(warm, key=lambda k: -k["time_ms"]) if k["launches"]}
+    # timed: EXACTLY K MPC iterations after initialize!; HIP events around the dominant kernel only
+    solver.set_kernel_timing(1 << [k["name"] for k in warm].index(dominant))
     solver.set_max_iter(args.steps)
     solver.initialize()
     barrier()
@@ -131,6 +160,8 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     iters = st.iter
+    roof = roofline(solver.kernel_stats(), dominant)
+    solver.set_kernel_timing(0)
     dt, total_iters = aggregate(dt, iters, dist, dev)
 
     # wall-clock to optimality (the reference's total_time; max_iter 300)
@@ -162,7 +193,8 @@ def main():
                        "kkt_n": info["n"], "nnzL": info["nnzL"], "nnzL_stored": info["nnzL_stored"],
                        "fact_flops": info["flops"], "fronts": info["nsuper"], "levels": info["nlevels"],
                        "parallelism": f"replicas{world}", **opt},
-            "roofline": None,
+            "roofline": roof,
+            "kernel_ms_warmup": breakdown,
             "cpu_baseline": None,
         }
         if not args.no_cpu and world == 1:

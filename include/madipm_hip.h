@@ -93,6 +93,23 @@ int madipm_ldl_get_d(madipm_ldl_t ls, double* h_d);
 int madipm_ldl_perm(madipm_ldl_t ls, int32_t* perm /* n */);
 void madipm_ldl_destroy(madipm_ldl_t ls);
 
+/* Live per-kernel timing (no reference counterpart; measurement for bench.py's roofline).
+ * Bit k of `mask` records HIP events around every launch of kernel kind k on the launch stream
+ * (kinds: 0 k_asm_chunks, 1 k_assemble, 2 k_tiny_factor, 3 k_small_factor, 4 k_big_diag,
+ * 5 k_big_trsm, 6 k_big_update, 7 k_inertia, 8 k_fwd_small, 9 k_fwd_gather, 10 k_fwd_big,
+ * 11 k_bwd_below, 12 k_bwd_big, 13 k_bwd_small).  Setting a mask clears the statistics. */
+#define MADIPM_NKERNELS 14
+typedef struct madipm_kstat {
+  char name[32];
+  int64_t launches;
+  double time_ms;          /* summed event time of the launches */
+  double bytes;            /* algorithmic bytes of those launches */
+  double flops;            /* algorithmic flops of those launches */
+} madipm_kstat;
+int madipm_ldl_set_timing(madipm_ldl_t ls, uint32_t mask);
+/* synchronises the recorded events; out[MADIPM_NKERNELS] */
+int madipm_ldl_kernel_stats(madipm_ldl_t ls, madipm_kstat* out);
+
 /* ------------------------------------------------------------------ native MPC solver
  * `MPCSolver(qp; kwargs...)` + `solve!(solver)` (src/structure.jl:79-178, src/solver.jl:362-418)
  * for a QuadraticModel with SparseKKTSystem (K2), run entirely on the GPU with the LDL^T above.
@@ -174,6 +191,9 @@ int madipm_solver_trace(madipm_solver_t s, madipm_iter_trace* out, int32_t cap);
 int madipm_solver_ldl_info(madipm_solver_t s, madipm_ldl_info* info);
 /* fill-reducing pivot order of the K2 factorization (length nvar_std + ncon, K2 unknowns [x; y]) */
 int madipm_solver_ldl_perm(madipm_solver_t s, int32_t* perm);
+/* the solver's LDL^T: timing as madipm_ldl_set_timing / madipm_ldl_kernel_stats */
+int madipm_solver_set_timing(madipm_solver_t s, uint32_t mask);
+int madipm_solver_kernel_stats(madipm_solver_t s, madipm_kstat* out);
 void madipm_solver_destroy(madipm_solver_t s);
 
 #ifdef __cplusplus

@@ -239,6 +239,36 @@ int madipm_ldl_perm(madipm_ldl_t ls, int32_t* perm) {
 
 void madipm_ldl_destroy(madipm_ldl_t ls) { delete ls; }
 
+static void fill_kstats(LDLSolver& l, madipm_kstat* out) {
+  static_assert(MADIPM_NKERNELS == KK_COUNT, "kernel kinds");
+  KernelStat st[KK_COUNT];
+  l.kernel_stats(st);
+  for (int k = 0; k < KK_COUNT; ++k) {
+    std::memset(out[k].name, 0, sizeof(out[k].name));
+    std::strncpy(out[k].name, kernel_kind_name(k), sizeof(out[k].name) - 1);
+    out[k].launches = st[k].launches;
+    out[k].time_ms = st[k].ms;
+    out[k].bytes = st[k].bytes;
+    out[k].flops = st[k].flops;
+  }
+}
+
+int madipm_ldl_set_timing(madipm_ldl_t ls, uint32_t mask) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(ls, "null argument");
+  ls->s->set_timing(mask);
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_ldl_kernel_stats(madipm_ldl_t ls, madipm_kstat* out) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(ls && out, "null argument");
+  fill_kstats(*ls->s, out);
+  return 0;
+  MADIPM_API_END
+}
+
 // ------------------------------------------------------------------ native MPC solver
 void madipm_default_options(madipm_options* o) {
   if (!o) return;
@@ -346,6 +376,22 @@ int madipm_solver_ldl_perm(madipm_solver_t s, int32_t* perm) {
   MADIPM_REQUIRE(s && perm, "null argument");
   const auto& p = s->s->ldl().plan().perm;
   std::memcpy(perm, p.data(), sizeof(int32_t) * p.size());
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_solver_set_timing(madipm_solver_t s, uint32_t mask) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(s, "null argument");
+  s->s->ldl().set_timing(mask);
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_solver_kernel_stats(madipm_solver_t s, madipm_kstat* out) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(s && out, "null argument");
+  fill_kstats(s->s->ldl(), out);
   return 0;
   MADIPM_API_END
 }

@@ -517,16 +517,17 @@ __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __
   const int nks = (kw + 3) >> 2;
 #pragma unroll
   for (int ks = 0; ks < 16; ++ks) {
-    if (ks >= nks) break;
-    const int kk = ks * 4 + (lane >> 4);
-    const double a0 = Lt[kk * LDT + qc + (lane & 15)];
-    const double a1 = Lt[kk * LDT + qc + 16 + (lane & 15)];
-    const double b0 = Wt[kk * LDT + qr + (lane & 15)];
-    const double b1 = Wt[kk * LDT + qr + 16 + (lane & 15)];
-    acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-    acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-    acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-    acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    if (ks < nks) {  // wave-uniform
+      const int kk = ks * 4 + (lane >> 4);
+      const double a0 = Lt[kk * LDT + qc + (lane & 15)];
+      const double a1 = Lt[kk * LDT + qc + 16 + (lane & 15)];
+      const double b0 = Wt[kk * LDT + qr + (lane & 15)];
+      const double b1 = Wt[kk * LDT + qr + 16 + (lane & 15)];
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    }
   }
   // D layout: col n = lane&15 (-> row i of F), row m = (lane>>4) + 4g (-> column j of F)
 #pragma unroll
@@ -541,7 +542,8 @@ __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __
       }
 }
 
-__global__ void k_inertia(const double* __restrict__ D, int n, LDLStatus* st) {
+__global__ __launch_bounds__(NT) void k_inertia(const double* __restrict__ D, int n, LDLStatus* st) {
+  __shared__ int red[3][NT / 64];
   int pos = 0, neg = 0, zero = 0;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const double d = D[i];
@@ -554,10 +556,17 @@ __global__ void k_inertia(const double* __restrict__ D, int n, LDLStatus* st) {
     neg += __shfl_down(neg, o, 64);
     zero += __shfl_down(zero, o, 64);
   }
-  if ((threadIdx.x & 63) == 0) {
-    atomicAdd(&st->npos, pos);
-    atomicAdd(&st->nneg, neg);
-    atomicAdd(&st->nzero, zero);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][wv] = pos;
+    red[1][wv] = neg;
+    red[2][wv] = zero;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    int v = 0;
+    for (int q = 0; q < NT / 64; ++q) v += red[threadIdx.x][q];
+    atomicAdd(threadIdx.x == 0 ? &st->npos : (threadIdx.x == 1 ? &st->nneg : &st->nzero), v);
   }
 }
 
@@ -938,9 +947,27 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     if (sched.size() & 1) sched.push_back(0);
   };
   for (int lev = 0; lev < S.nlevels; ++lev) {
-    if (S.atile_lev[lev + 1] > S.atile_lev[lev])
-      fact_.push_back({ASSEMBLE, 0, S.atile_lev[lev], 0, S.atile_lev[lev + 1] - S.atile_lev[lev], S.chunk_lev[lev],
-                       S.chunk_lev[lev + 1] - S.chunk_lev[lev]});
+    if (S.atile_lev[lev + 1] > S.atile_lev[lev]) {
+      Launch L{ASSEMBLE, 0, S.atile_lev[lev], 0, S.atile_lev[lev + 1] - S.atile_lev[lev], S.chunk_lev[lev],
+               S.chunk_lev[lev + 1] - S.chunk_lev[lev]};
+      // algorithmic traffic: chunk pass reads (index, value) per source, writes one partial per chunk;
+      // the tile pass reads the entry offsets + partials (+ big-children blocks), writes the lower tile
+      const int64_t nsrc = S.g_chunk[S.chunk_lev[lev + 1]] - S.g_chunk[S.chunk_lev[lev]];
+      L.bytes2 = 16.0 * nsrc + 16.0 * L.nchunk;
+      L.flops2 = (double)nsrc;
+      for (int32_t t = S.atile_lev[lev]; t < S.atile_lev[lev + 1]; ++t) {
+        const SymbolicPlan::AsmTile& at = S.atiles[t];
+        const int r = S.nrows[at.front], ti = at.tij & 0xffff, tj = at.tij >> 16;
+        const double nr = std::min(64, r - 64 * ti), nc = std::min(64, r - 64 * tj);
+        L.bytes += 8.0 * (ti == tj ? nr * (nr + 1) / 2 : nr * nc) + (at.gptr >= 0 ? 4.0 * 4097 : 0.0);
+        for (int k = at.bt0; k < at.bt1; ++k) {
+          const int32_t* e = &S.bt[5 * k];
+          for (int b = e[1]; b < e[2]; ++b) L.bytes += 8.0 * std::max(0, e[4] - std::max(b, e[3]));
+        }
+      }
+      L.bytes += 8.0 * L.nchunk;
+      fact_.push_back(L);
+    }
     std::vector<int32_t> cls[3], big;
     for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
       const int s = S.level_list[q];
@@ -952,7 +979,14 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     }
     for (int c = 0; c < 3; ++c)
       if (!cls[c].empty()) {
-        fact_.push_back({SMALL32 + c, 0, (int64_t)sched.size(), (int)cls[c].size(), (int64_t)cls[c].size()});
+        Launch L{SMALL32 + c, 0, (int64_t)sched.size(), (int)cls[c].size(), (int64_t)cls[c].size()};
+        for (int f : cls[c]) {  // reads: K entries or the assembled front; writes: L panel, U block, D
+          const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
+          L.bytes += 8.0 * (r * w + (r - w) * (r - w) + w) +
+                     (S.fs_off[f] >= 0 ? 8.0 * r * (r + 1) / 2 : 16.0 * (S.asm_ptr[f + 1] - S.asm_ptr[f]));
+          for (int t = 0; t < (int)w; ++t) L.flops += (r - t - 1) * (r - t);
+        }
+        fact_.push_back(L);
         sched.insert(sched.end(), cls[c].begin(), cls[c].end());
       }
     if (big.empty()) continue;
@@ -960,21 +994,33 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     for (int s : big) maxsteps = std::max<int>(maxsteps, (int)cdiv(S.first[s + 1] - S.first[s], 64));
     for (int p = 0; p < maxsteps; ++p) {
       std::vector<int32_t> td, tt, tu;  // (front, item) pairs
+      double kb[3] = {0, 0, 0}, kf[3] = {0, 0, 0};
       for (int s : big) {
         const int w = S.first[s + 1] - S.first[s], r = S.nrows[s];
         if (cdiv(w, 64) <= p) continue;
         const int k0 = p * 64, kw = std::min(64, w - k0);
         const int nt = (int)cdiv(r - k0 - kw, 64);
+        const double dk = kw, nb = r - k0 - kw;
+        kb[0] += 8.0 * (dk * (dk + 1) + 4 * 16 * 17);  // diag: read + write lower, write the M blocks
+        kf[0] += dk * dk * dk / 3.0;
+        kb[1] += 8.0 * (2.0 * nb * dk + nt * (dk * (dk + 1) / 2 + 4 * 16 * 17));  // trsm: rows in/out + L11, M per tile
+        kf[1] += nb * dk * dk;
+        kb[2] += 8.0 * (nb * (nb + 1) + 2.0 * nb * dk);  // update: C in/out + the panel once
+        kf[2] += dk * nb * (nb + 1);
         td.insert(td.end(), {s, 0});
         for (int i = 0; i < nt; ++i) tt.insert(tt.end(), {s, i});
         for (int i = 0; i < nt; ++i)
           for (int j = 0; j <= i; ++j) tu.insert(tu.end(), {s, i | (j << 16)});
       }
       const std::pair<int, std::vector<int32_t>*> kinds[3] = {{BIG_DIAG, &td}, {BIG_TRSM, &tt}, {BIG_UPDATE, &tu}};
-      for (const auto& kv : kinds) {
+      for (int q = 0; q < 3; ++q) {
+        const auto& kv = kinds[q];
         if (kv.second->empty()) continue;
         align2();
-        fact_.push_back({kv.first, p, (int64_t)sched.size(), 0, (int64_t)kv.second->size() / 2});
+        Launch L{kv.first, p, (int64_t)sched.size(), 0, (int64_t)kv.second->size() / 2};
+        L.bytes = kb[q];
+        L.flops = kf[q];
+        fact_.push_back(L);
         sched.insert(sched.end(), kv.second->begin(), kv.second->end());
       }
     }
@@ -1042,6 +1088,19 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
           }
         }
       L.nbtask = (int)((int64_t)tasks.size() / 2 - L.btask_off);
+      // algorithmic traffic of one sweep: the L panel once (+ the vectors), 2 flops per panel entry
+      for (int f : small) {
+        const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
+        L.small_bytes += 8.0 * (r * w + 3.0 * r);
+        L.small_flops += 2.0 * (r * w - w * (w + 1) / 2);
+      }
+      for (int f : big) {
+        const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
+        L.big_bytes += 8.0 * (r * w + 3.0 * r);
+        L.big_flops += 2.0 * (r * w - w * (w + 1) / 2);
+        L.below_bytes += 8.0 * (r - w) * w;
+        L.gat_bytes += 8.0 * (2.0 * r + 2.0 * (S.sv_ptr[S.row_ptr[f + 1]] - S.sv_ptr[S.row_ptr[f]]));
+      }
       slev_.push_back(L);
     }
     tasks_.upload(tasks);
@@ -1073,6 +1132,65 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
 
 LDLSolver::~LDLSolver() {
   if (h_status_) (void)hipHostFree(h_status_);
+  for (hipEvent_t e : evs_) (void)hipEventDestroy(e);
+}
+
+#define TIMED(kind, bytes, flops, launch)            \
+  do {                                               \
+    const bool tm_ = t_begin(kind, s);               \
+    launch;                                          \
+    if (tm_) t_end(kind, s, (bytes), (flops));       \
+  } while (0)
+
+const char* kernel_kind_name(int k) {
+  static const char* names[KK_COUNT] = {"k_asm_chunks", "k_assemble",  "k_tiny_factor", "k_small_factor", "k_big_diag",
+                                        "k_big_trsm",   "k_big_update", "k_inertia",    "k_fwd_small",    "k_fwd_gather",
+                                        "k_fwd_big",    "k_bwd_below",  "k_bwd_big",    "k_bwd_small"};
+  return (k >= 0 && k < KK_COUNT) ? names[k] : "?";
+}
+
+void LDLSolver::set_timing(unsigned mask) {
+  tmask_ = mask;
+  ev_used_ = 0;
+  pend_.clear();
+  for (auto& k : kst_) k = KernelStat{};
+}
+
+bool LDLSolver::t_begin(int kind, hipStream_t s) {
+  if (!(tmask_ >> kind & 1u)) return false;
+  while (evs_.size() < ev_used_ + 2) {
+    hipEvent_t e;
+    MADIPM_HIP(hipEventCreate(&e));
+    evs_.push_back(e);
+  }
+  pend_.push_back({kind, ev_used_, 0.0, 0.0});
+  MADIPM_HIP(hipEventRecord(evs_[ev_used_], s));
+  ev_used_ += 2;
+  return true;
+}
+
+void LDLSolver::t_end(int kind, hipStream_t s, double bytes, double flops) {
+  Pending& p = pend_.back();
+  (void)kind;
+  p.bytes = bytes;
+  p.flops = flops;
+  MADIPM_HIP(hipEventRecord(evs_[p.e0 + 1], s));
+}
+
+void LDLSolver::kernel_stats(KernelStat out[KK_COUNT]) {
+  for (const Pending& p : pend_) {
+    MADIPM_HIP(hipEventSynchronize(evs_[p.e0 + 1]));
+    float ms = 0.f;
+    MADIPM_HIP(hipEventElapsedTime(&ms, evs_[p.e0], evs_[p.e0 + 1]));
+    KernelStat& k = kst_[p.kind];
+    k.launches++;
+    k.ms += ms;
+    k.bytes += p.bytes;
+    k.flops += p.flops;
+  }
+  pend_.clear();
+  ev_used_ = 0;
+  for (int k = 0; k < KK_COUNT; ++k) out[k] = kst_[k];
 }
 
 void LDLSolver::factorize_async(const double* Kx, hipStream_t s) {
@@ -1083,32 +1201,39 @@ void LDLSolver::factorize_async(const double* Kx, hipStream_t s) {
     switch (L.kind) {
       case ASSEMBLE:
         if (L.nchunk)
-          k_asm_chunks<<<(unsigned)cdiv(L.nchunk, NT), NT, 0, s>>>(g_chunk_, g_src_, L.chunk0, L.nchunk, Kx, arena_, gpart_);
-        k_assemble<<<(unsigned)L.items, ANT, 0, s>>>(T_, atiles_.p + L.off, g_ptr_, gpart_, bt_, arena_, fscratch_);
+          TIMED(KK_ASM_CHUNKS, L.bytes2, L.flops2,
+                (k_asm_chunks<<<(unsigned)cdiv(L.nchunk, NT), NT, 0, s>>>(g_chunk_, g_src_, L.chunk0, L.nchunk, Kx, arena_,
+                                                                         gpart_)));
+        TIMED(KK_ASSEMBLE, L.bytes, L.flops,
+              (k_assemble<<<(unsigned)L.items, ANT, 0, s>>>(T_, atiles_.p + L.off, g_ptr_, gpart_, bt_, arena_, fscratch_)));
         break;
       case SMALL32:
-        k_tiny_factor<<<(unsigned)cdiv(L.items, 4), NT, 0, s>>>(T_, list, (int)L.items, Kx, arena_, fscratch_, D_, status_,
-                                                               pivot_tol);
+        TIMED(KK_TINY, L.bytes, L.flops,
+              (k_tiny_factor<<<(unsigned)cdiv(L.items, 4), NT, 0, s>>>(T_, list, (int)L.items, Kx, arena_, fscratch_, D_,
+                                                                      status_, pivot_tol)));
         break;
       case SMALL64:
       case SMALL128: {
         const int R = L.kind == SMALL32 ? 32 : (L.kind == SMALL64 ? 64 : 128);
-        k_small_factor<<<(unsigned)L.items, NT, R * R * 8, s>>>(T_, list, Kx, arena_, fscratch_, D_, status_, pivot_tol);
+        TIMED(KK_SMALL, L.bytes, L.flops,
+              (k_small_factor<<<(unsigned)L.items, NT, R * R * 8, s>>>(T_, list, Kx, arena_, fscratch_, D_, status_,
+                                                                      pivot_tol)));
         break;
       }
       case BIG_DIAG:
-        k_big_diag<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_, minv_, status_, pivot_tol);
+        TIMED(KK_DIAG, L.bytes, L.flops,
+              (k_big_diag<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_, minv_, status_, pivot_tol)));
         break;
       case BIG_TRSM:
-        k_big_trsm<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_, minv_);
+        TIMED(KK_TRSM, L.bytes, L.flops, (k_big_trsm<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_, minv_)));
         break;
       case BIG_UPDATE:
-        k_big_update<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_);
+        TIMED(KK_UPDATE, L.bytes, L.flops, (k_big_update<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_)));
         break;
     }
   }
-  const int nb = (int)std::min<int64_t>(1024, cdiv(S_.N, NT));
-  k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, status_);
+  const int nb = (int)std::min<int64_t>(64, cdiv(S_.N, NT));
+  TIMED(KK_INERTIA, 8.0 * S_.N, 0.0, (k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, status_)));
   MADIPM_HIP(hipGetLastError());
   MADIPM_HIP(hipMemcpyAsync(h_status_, status_.p, sizeof(LDLStatus), hipMemcpyDeviceToHost, s));
 }
@@ -1136,20 +1261,32 @@ void LDLSolver::solve_async(double* b, hipStream_t s) {
   const int nl = (int)slev_.size();
   for (int lev = 0; lev < nl; ++lev) {
     const SolveLevel& L = slev_[lev];
-    if (L.nsmall) k_fwd_small<<<(unsigned)cdiv(L.nsmall, SW), NT, 0, s>>>(T_, sched_.p + L.small_off, L.nsmall, arena_, b, xi_, uvec_);
+    if (L.nsmall)
+      TIMED(KK_FWD_SMALL, L.small_bytes, L.small_flops,
+            (k_fwd_small<<<(unsigned)cdiv(L.nsmall, SW), NT, 0, s>>>(T_, sched_.p + L.small_off, L.nsmall, arena_, b, xi_,
+                                                                    uvec_)));
     if (L.nbig) {
-      k_fwd_gather<<<L.ngat, NT, 0, s>>>(T_, sched_.p + L.gat_off, b, uvec_, vwork_);
-      k_fwd_big<<<std::min(L.nftask, 512), NT, 0, s>>>(T_, tasks + L.ftask_off, L.nftask, counters_.p + 2 * lev, flags_,
-                                                         flag_off_, efwd, arena_, vwork_, xi_, uvec_, err_);
+      TIMED(KK_FWD_GATHER, L.gat_bytes, 0.0,
+            (k_fwd_gather<<<L.ngat, NT, 0, s>>>(T_, sched_.p + L.gat_off, b, uvec_, vwork_)));
+      TIMED(KK_FWD_BIG, L.big_bytes, L.big_flops,
+            (k_fwd_big<<<std::min(L.nftask, 512), NT, 0, s>>>(T_, tasks + L.ftask_off, L.nftask, counters_.p + 2 * lev,
+                                                               flags_, flag_off_, efwd, arena_, vwork_, xi_, uvec_, err_)));
     }
   }
   for (int lev = nl - 1; lev >= 0; --lev) {
     const SolveLevel& L = slev_[lev];
-    if (L.nbelow) k_bwd_below<<<L.nbelow, NT, 0, s>>>(T_, sched_.p + L.below_off, bp_off_, arena_, xi_, bpart_);
+    if (L.nbelow)
+      TIMED(KK_BWD_BELOW, L.below_bytes, 0.25 * L.below_bytes,
+            (k_bwd_below<<<L.nbelow, NT, 0, s>>>(T_, sched_.p + L.below_off, bp_off_, arena_, xi_, bpart_)));
     if (L.nbig)
-      k_bwd_big<<<std::min(L.nbtask, 512), NT, 0, s>>>(T_, tasks + L.btask_off, L.nbtask, counters_.p + 2 * lev + 1,
-                                                         flags_, flag_off_, ebwd, arena_, D_, xi_, b, bp_off_, bpart_, err_);
-    if (L.nsmall) k_bwd_small<<<(unsigned)cdiv(L.nsmall, SW), NT, 0, s>>>(T_, sched_.p + L.small_off, L.nsmall, arena_, D_, xi_, b);
+      TIMED(KK_BWD_BIG, L.big_bytes - L.below_bytes, L.big_flops - 0.25 * L.below_bytes,
+            (k_bwd_big<<<std::min(L.nbtask, 512), NT, 0, s>>>(T_, tasks + L.btask_off, L.nbtask, counters_.p + 2 * lev + 1,
+                                                               flags_, flag_off_, ebwd, arena_, D_, xi_, b, bp_off_, bpart_,
+                                                               err_)));
+    if (L.nsmall)
+      TIMED(KK_BWD_SMALL, L.small_bytes, L.small_flops,
+            (k_bwd_small<<<(unsigned)cdiv(L.nsmall, SW), NT, 0, s>>>(T_, sched_.p + L.small_off, L.nsmall, arena_, D_, xi_,
+                                                                    b)));
   }
   MADIPM_HIP(hipGetLastError());
 }

@@ -47,6 +47,19 @@ struct LDLStatus {  // device-resident, read back by status()
   int32_t npos, nneg, nzero;
 };
 
+// Kernel kinds for the live per-kernel timing (HIP events around each launch on the launch
+// stream) and their algorithmic bytes / flops per launch (DESIGN.md "Kernels and their rooflines").
+enum KernelKind {
+  KK_ASM_CHUNKS = 0, KK_ASSEMBLE, KK_TINY, KK_SMALL, KK_DIAG, KK_TRSM, KK_UPDATE, KK_INERTIA,
+  KK_FWD_SMALL, KK_FWD_GATHER, KK_FWD_BIG, KK_BWD_BELOW, KK_BWD_BIG, KK_BWD_SMALL, KK_COUNT
+};
+const char* kernel_kind_name(int k);
+
+struct KernelStat {
+  int64_t launches = 0;
+  double ms = 0.0, bytes = 0.0, flops = 0.0;
+};
+
 class LDLSolver {
  public:
   LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const SymbolicOptions& sopt,
@@ -71,6 +84,11 @@ class LDLSolver {
   // device buffers for diagnostics
   const double* d_diag() const { return D_.p; }
 
+  // live kernel timing: bit k of `mask` => HIP events around every launch of KernelKind k.
+  // set_timing() clears the accumulated statistics; kernel_stats() synchronises the events.
+  void set_timing(unsigned mask);
+  void kernel_stats(KernelStat out[KK_COUNT]);
+
  private:
   enum Kind { ASSEMBLE = 0, SMALL32 = 1, SMALL64 = 2, SMALL128 = 3, BIG_DIAG = 4, BIG_TRSM = 5, BIG_UPDATE = 6 };
   struct Launch {
@@ -80,6 +98,8 @@ class LDLSolver {
     int nf;         // number of fronts (SMALL*)
     int64_t items;  // workgroups
     int64_t chunk0 = 0, nchunk = 0;  // ASSEMBLE: chunk range of the level
+    double bytes = 0, flops = 0;       // algorithmic traffic / work of the launch
+    double bytes2 = 0, flops2 = 0;     // ASSEMBLE: of the chunk pass
   };
   struct SolveLevel {
     int64_t small_off;
@@ -94,6 +114,7 @@ class LDLSolver {
     int nftask;
     int64_t btask_off;
     int nbtask;
+    double small_bytes = 0, small_flops = 0, big_bytes = 0, big_flops = 0, below_bytes = 0, gat_bytes = 0;
   };
   SymbolicPlan S_;
   FrontTab T_{};
@@ -112,6 +133,19 @@ class LDLSolver {
   DBuf<double> arena_, D_, xi_, uvec_, vwork_;
   DBuf<LDLStatus> status_;
   LDLStatus* h_status_ = nullptr;
+  // live timing
+  unsigned tmask_ = 0;
+  std::vector<hipEvent_t> evs_;
+  size_t ev_used_ = 0;
+  struct Pending {
+    int kind;
+    size_t e0;
+    double bytes, flops;
+  };
+  std::vector<Pending> pend_;
+  KernelStat kst_[KK_COUNT];
+  bool t_begin(int kind, hipStream_t s);
+  void t_end(int kind, hipStream_t s, double bytes, double flops);
 };
 
 }  // namespace madipm

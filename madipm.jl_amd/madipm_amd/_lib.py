@@ -40,6 +40,19 @@ class LDLInfo(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+NKERNELS = 14  # MADIPM_NKERNELS
+
+
+class KStat(C.Structure):
+    _fields_ = [("name", C.c_char * 32), ("launches", C.c_int64), ("time_ms", C.c_double),
+                ("bytes", C.c_double), ("flops", C.c_double)]
+
+
+def kstats_to_list(arr) -> list:
+    return [{"name": k.name.decode(), "launches": int(k.launches), "time_ms": float(k.time_ms),
+             "bytes": float(k.bytes), "flops": float(k.flops)} for k in arr]
+
+
 def _sig(name, res, args):
     f = getattr(lib, name)
     f.restype = res
@@ -67,6 +80,8 @@ _sig("madipm_ldl_inertia", C.c_int, [vp, i32p, i32p, i32p])
 _sig("madipm_ldl_get_d", C.c_int, [vp, f64p])
 _sig("madipm_ldl_perm", C.c_int, [vp, i32p])
 _sig("madipm_ldl_destroy", None, [vp])
+_sig("madipm_ldl_set_timing", C.c_int, [vp, C.c_uint32])
+_sig("madipm_ldl_kernel_stats", C.c_int, [vp, C.POINTER(KStat)])
 
 
 class MadIPMError(RuntimeError):

@@ -82,6 +82,15 @@ class HIPLDLSolver:
         L.check(L.lib.madipm_ldl_perm(self.h, L.ptr(p, C.c_int32)), "madipm_ldl_perm")
         return p
 
+    def set_kernel_timing(self, mask: int = (1 << L.NKERNELS) - 1):
+        """HIP events around every launch of the kernel kinds in `mask`; clears the statistics."""
+        L.check(L.lib.madipm_ldl_set_timing(self.h, int(mask)), "madipm_ldl_set_timing")
+
+    def kernel_stats(self) -> list:
+        arr = (L.KStat * L.NKERNELS)()
+        L.check(L.lib.madipm_ldl_kernel_stats(self.h, arr), "madipm_ldl_kernel_stats")
+        return L.kstats_to_list(arr)
+
     def __del__(self):
         h = getattr(self, "h", None)
         if h:

@@ -120,6 +120,8 @@ L._sig("madipm_solver_get_solution", C.c_int, [L.vp, L.f64p, L.f64p, L.f64p, L.f
 L._sig("madipm_solver_trace", C.c_int, [L.vp, C.POINTER(IterTrace), C.c_int32])
 L._sig("madipm_solver_ldl_info", C.c_int, [L.vp, C.POINTER(L.LDLInfo)])
 L._sig("madipm_solver_ldl_perm", C.c_int, [L.vp, L.i32p])
+L._sig("madipm_solver_set_timing", C.c_int, [L.vp, C.c_uint32])
+L._sig("madipm_solver_kernel_stats", C.c_int, [L.vp, C.POINTER(L.KStat)])
 L._sig("madipm_solver_destroy", None, [L.vp])
 
 
@@ -256,6 +258,17 @@ class MPCSolver:
         p = np.empty(n, np.int32)
         L.check(L.lib.madipm_solver_ldl_perm(self.h, L.ptr(p, C.c_int32)), "kkt_perm")
         return p
+
+    def set_kernel_timing(self, mask: int = (1 << L.NKERNELS) - 1):
+        """Record HIP events around every launch of the LDL^T kernel kinds in `mask` (bit k = kind k,
+        include/madipm_hip.h); clears the statistics.  mask=0 turns timing off."""
+        L.check(L.lib.madipm_solver_set_timing(self.h, int(mask)), "set_timing")
+
+    def kernel_stats(self) -> list:
+        """Per kernel kind: launches, summed event time (ms), algorithmic bytes and flops."""
+        arr = (L.KStat * L.NKERNELS)()
+        L.check(L.lib.madipm_solver_kernel_stats(self.h, arr), "kernel_stats")
+        return L.kstats_to_list(arr)
 
     def initialize(self):
         """initialize! alone (src/solver.jl:127-189); the next solve() runs only the MPC loop."""
