@@ -16,6 +16,7 @@ multi-GPU: the factorization is single-GPU in this round ("replicas only", DESIG
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -90,9 +91,15 @@ def roofline(stats: list, dominant: str):
         ach, peak, unit = flops / avg_s / 1e12, PEAK_F64_TFS, "TFLOP/s"
     else:
         ach, peak, unit = nbytes / avg_s / 1e9, PEAK_HBM_GBS, "GB/s"
+    traffic, src = None, None
+    pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    if pmc:  # PMC counters can not be read inside the timed run: the latest committed pass of this workload
+        ent = json.load(open(pmc[-1]))["kernels"].get(dominant)
+        if ent:
+            traffic, src = ent["hbm_bytes_per_launch"], os.path.relpath(pmc[-1], ROOT)
     return {"bound": "mfma" if mfma else "hbm", "achieved": ach, "peak": peak, "unit": unit, "frac": ach / peak,
-            "traffic": None, "kernel": dominant, "launches": k["launches"], "avg_launch_us": avg_s * 1e6,
-            "alg_bytes_per_launch": nbytes, "alg_flops_per_launch": flops}
+            "traffic": traffic, "traffic_source": src, "kernel": dominant, "launches": k["launches"],
+            "avg_launch_us": avg_s * 1e6, "alg_bytes_per_launch": nbytes, "alg_flops_per_launch": flops}
 
 
 def aggregate(dt, iters, dist, dev):

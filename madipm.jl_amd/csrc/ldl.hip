@@ -1159,8 +1159,8 @@ void LDLSolver::set_timing(unsigned mask) {
 bool LDLSolver::t_begin(int kind, hipStream_t s) {
   if (!(tmask_ >> kind & 1u)) return false;
   while (evs_.size() < ev_used_ + 2) {
-    hipEvent_t e;
-    MADIPM_HIP(hipEventCreate(&e));
+    hipEvent_t e;  // no system-scope fence: the timestamps bracket the kernel, not a cache flush
+    MADIPM_HIP(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
     evs_.push_back(e);
   }
   pend_.push_back({kind, ev_used_, 0.0, 0.0});
