@@ -32,7 +32,8 @@ int madipm_device_count(void);            /* hipGetDeviceCount; 0 when no GPU is
  * Replaces the symbolic phase run by the linear-solver constructor `linear_solver(aug_com; opt)`
  * (src/KKT/normalkkt.jl:113-115; SparseKKTSystem constructor in MadNLP [EXT]) — SURVEY §8 a12. */
 typedef struct madipm_ldl_opts {
-  int32_t ordering;        /* 0 natural, 1 AMD (default), 2 user permutation */
+  int32_t ordering;        /* 0 natural, 1 AMD, 2 user permutation, 3 nested dissection,
+                              4 auto = AMD and ND, fewer flops wins (default) */
   double dense_alpha;      /* AMD dense-node threshold factor (default 10) */
   int32_t relax;           /* relaxed supernode amalgamation (default 1) */
   int32_t small_front_max; /* fronts with <= this many rows are factorised in LDS (default 128) */

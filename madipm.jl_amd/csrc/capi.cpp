@@ -77,7 +77,7 @@ int madipm_device_count(void) {
 
 void madipm_ldl_default_opts(madipm_ldl_opts* o) {
   if (!o) return;
-  o->ordering = 1;
+  o->ordering = 4;
   o->dense_alpha = 10.0;
   o->relax = 1;
   o->small_front_max = 128;

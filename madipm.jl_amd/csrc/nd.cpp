@@ -1,0 +1,494 @@
+// Nested-dissection fill-reducing ordering (multilevel vertex separators), host side.
+//
+// The reference's GPU linear solver (cuDSS, scripts/benchmarks_gpu.jl:41-42) orders with a
+// METIS-style nested dissection; its CPU solvers (LDLFactorizations, MA57) use minimum-degree
+// variants.  SymbolicOptions::ordering selects AMD (csrc/amd.cpp), this ND, or "auto" = both,
+// keeping the one with fewer factorisation flops (symbolic.cpp) — SURVEY §8 a12.
+//
+// Algorithm (written for this project): recursive bisection.  Each connected subgraph larger than
+// a leaf is bisected by a multilevel scheme — heavy-edge matching coarsening, greedy graph-growing
+// initial partitions on the coarsest graph (several seeds), boundary Fiduccia–Mattheyses refinement
+// while uncoarsening — and the edge cut is turned into a minimum vertex separator (König: maximum
+// bipartite matching on the cut edges, Hopcroft–Karp).  Order = [part A][part B][separator],
+// recursively; disconnected subgraphs are ordered component by component with no separator;
+// leaves, and subgraphs without a good separator (|S| > sep_ratio |V|), are ordered by AMD.
+#include <algorithm>
+#include <cstdint>
+#include <numeric>
+#include <queue>
+#include <vector>
+
+#include "common.hpp"
+#include "symbolic.hpp"
+
+namespace madipm {
+
+namespace {
+
+struct Graph {
+  int n = 0;
+  std::vector<int64_t> p;
+  std::vector<int32_t> adj, ew, vw;
+  int64_t total_vw() const { return std::accumulate(vw.begin(), vw.end(), (int64_t)0); }
+};
+
+struct Rng {
+  uint64_t s;
+  explicit Rng(uint64_t seed) : s(seed * 0x9E3779B97F4A7C15ull + 1) {}
+  uint32_t next() {
+    s ^= s << 13;
+    s ^= s >> 7;
+    s ^= s << 17;
+    return (uint32_t)(s >> 11);
+  }
+};
+
+// Heavy-edge matching and contraction.  Returns false when the graph hardly shrinks.
+bool coarsen(const Graph& g, Graph& c, std::vector<int32_t>& cmap, Rng& rng) {
+  const int n = g.n;
+  std::vector<int32_t> match(n, -1), order(n);
+  std::iota(order.begin(), order.end(), 0);
+  for (int i = n - 1; i > 0; --i) std::swap(order[i], order[rng.next() % (i + 1)]);
+  for (int v : order) {
+    if (match[v] != -1) continue;
+    int best = -1, bw = -1;
+    for (int64_t e = g.p[v]; e < g.p[v + 1]; ++e) {
+      const int u = g.adj[e];
+      if (match[u] == -1 && g.ew[e] > bw) {
+        bw = g.ew[e];
+        best = u;
+      }
+    }
+    if (best == -1) {
+      match[v] = v;
+    } else {
+      match[v] = best;
+      match[best] = v;
+    }
+  }
+  cmap.assign(n, -1);
+  int nc = 0;
+  for (int v = 0; v < n; ++v)
+    if (cmap[v] == -1) cmap[v] = cmap[match[v]] = nc++;
+  if (nc > 0.92 * n) return false;
+  c.n = nc;
+  c.vw.assign(nc, 0);
+  c.p.assign(nc + 1, 0);
+  c.adj.clear();
+  c.ew.clear();
+  std::vector<int32_t> pos(nc, -1), members(2);
+  std::vector<int32_t> rep(nc, -1);
+  for (int v = 0; v < n; ++v)
+    if (rep[cmap[v]] == -1) rep[cmap[v]] = v;
+  for (int cv = 0; cv < nc; ++cv) {
+    const int v = rep[cv];
+    const int u = match[v];
+    const int nm = (u == v) ? 1 : 2;
+    members[0] = v;
+    members[1] = u;
+    const int64_t start = (int64_t)c.adj.size();
+    for (int k = 0; k < nm; ++k) {
+      const int x = members[k];
+      c.vw[cv] += g.vw[x];
+      for (int64_t e = g.p[x]; e < g.p[x + 1]; ++e) {
+        const int cu = cmap[g.adj[e]];
+        if (cu == cv) continue;
+        if (pos[cu] >= start && pos[cu] < (int64_t)c.adj.size() && c.adj[pos[cu]] == cu) {
+          c.ew[pos[cu]] += g.ew[e];
+        } else {
+          pos[cu] = (int32_t)c.adj.size();
+          c.adj.push_back(cu);
+          c.ew.push_back(g.ew[e]);
+        }
+      }
+    }
+    c.p[cv + 1] = (int64_t)c.adj.size();
+  }
+  return true;
+}
+
+int64_t cut_weight(const Graph& g, const std::vector<uint8_t>& part) {
+  int64_t cut = 0;
+  for (int v = 0; v < g.n; ++v)
+    for (int64_t e = g.p[v]; e < g.p[v + 1]; ++e)
+      if (part[v] != part[g.adj[e]]) cut += g.ew[e];
+  return cut / 2;
+}
+
+// Greedy graph growing from `seed`: vertices join side 0 by best gain until half the weight.
+void grow(const Graph& g, int seed, std::vector<uint8_t>& part) {
+  const int64_t W = g.total_vw();
+  part.assign(g.n, 1);
+  std::vector<int64_t> gain(g.n, 0);  // (edges to side 0) - (edges to side 1), for side-1 vertices
+  for (int v = 0; v < g.n; ++v)
+    for (int64_t e = g.p[v]; e < g.p[v + 1]; ++e) gain[v] -= g.ew[e];
+  std::priority_queue<std::pair<int64_t, int>> pq;
+  int64_t w0 = 0;
+  int next_seed = seed;
+  std::vector<uint8_t> inq(g.n, 0);
+  while (2 * w0 < W) {
+    int v = -1;
+    while (!pq.empty()) {
+      auto t = pq.top();
+      pq.pop();
+      if (part[t.second] == 1 && t.first == gain[t.second]) {
+        v = t.second;
+        break;
+      }
+    }
+    if (v == -1) {  // empty frontier (disconnected coarse graph): next unassigned vertex
+      while (next_seed < g.n && part[next_seed] == 0) ++next_seed;
+      if (next_seed >= g.n) {
+        for (v = 0; v < g.n && part[v] == 0; ++v) {
+        }
+        if (v >= g.n) break;
+      } else {
+        v = next_seed;
+      }
+    }
+    part[v] = 0;
+    w0 += g.vw[v];
+    for (int64_t e = g.p[v]; e < g.p[v + 1]; ++e) {
+      const int u = g.adj[e];
+      if (part[u] == 1) {
+        gain[u] += 2 * g.ew[e];
+        pq.push({gain[u], u});
+      }
+    }
+  }
+}
+
+// Boundary FM refinement with a balance bound; a few passes, best prefix kept.
+void refine(const Graph& g, std::vector<uint8_t>& part, double imbalance) {
+  const int64_t W = g.total_vw();
+  const int64_t maxw = (int64_t)((0.5 + imbalance) * W) + 1;
+  for (int pass = 0; pass < 4; ++pass) {
+    int64_t wside[2] = {0, 0};
+    for (int v = 0; v < g.n; ++v) wside[part[v]] += g.vw[v];
+    std::vector<int64_t> gain(g.n, 0);
+    for (int v = 0; v < g.n; ++v)
+      for (int64_t e = g.p[v]; e < g.p[v + 1]; ++e) gain[v] += (part[g.adj[e]] != part[v]) ? g.ew[e] : -g.ew[e];
+    std::priority_queue<std::pair<int64_t, int>> pq;
+    for (int v = 0; v < g.n; ++v)
+      for (int64_t e = g.p[v]; e < g.p[v + 1]; ++e)
+        if (part[g.adj[e]] != part[v]) {
+          pq.push({gain[v], v});
+          break;
+        }
+    std::vector<uint8_t> locked(g.n, 0);
+    std::vector<int> moves;
+    int64_t cur = 0, best = 0;
+    size_t best_len = 0;
+    int since_best = 0;
+    while (!pq.empty() && since_best < 64) {
+      auto t = pq.top();
+      pq.pop();
+      const int v = t.second;
+      if (locked[v] || t.first != gain[v]) continue;
+      const int from = part[v], to = 1 - from;
+      if (wside[to] + g.vw[v] > maxw) continue;
+      locked[v] = 1;
+      part[v] = (uint8_t)to;
+      wside[from] -= g.vw[v];
+      wside[to] += g.vw[v];
+      cur -= gain[v];
+      moves.push_back(v);
+      for (int64_t e = g.p[v]; e < g.p[v + 1]; ++e) {
+        const int u = g.adj[e];
+        gain[u] += (part[u] == to) ? -2 * g.ew[e] : 2 * g.ew[e];
+        if (!locked[u]) pq.push({gain[u], u});
+      }
+      gain[v] = -gain[v];
+      if (cur < best) {
+        best = cur;
+        best_len = moves.size();
+        since_best = 0;
+      } else {
+        ++since_best;
+      }
+    }
+    for (size_t k = moves.size(); k > best_len; --k) part[moves[k - 1]] ^= 1;  // roll back
+    if (best == 0 || -best * 200 < cut_weight(g, part)) break;  // converged (< 0.5 % gain)
+  }
+}
+
+// Multilevel bisection of a connected graph; returns the partition of the finest graph.
+void bisect(const Graph& g0, std::vector<uint8_t>& part, Rng& rng) {
+  std::vector<Graph> levels;
+  std::vector<std::vector<int32_t>> maps;
+  levels.push_back(g0);
+  while (levels.back().n > 120) {
+    Graph c;
+    std::vector<int32_t> cmap;
+    if (!coarsen(levels.back(), c, cmap, rng)) break;
+    levels.push_back(std::move(c));
+    maps.push_back(std::move(cmap));
+  }
+  const Graph& gc = levels.back();
+  int64_t best = -1;
+  std::vector<uint8_t> trial;
+  for (int t = 0; t < 8; ++t) {
+    grow(gc, (int)(rng.next() % gc.n), trial);
+    refine(gc, trial, 0.05);
+    const int64_t cw = cut_weight(gc, trial);
+    if (best < 0 || cw < best) {
+      best = cw;
+      part = trial;
+    }
+  }
+  for (int l = (int)levels.size() - 2; l >= 0; --l) {
+    std::vector<uint8_t> fine(levels[l].n);
+    for (int v = 0; v < levels[l].n; ++v) fine[v] = part[maps[l][v]];
+    part.swap(fine);
+    refine(levels[l], part, 0.05);
+  }
+}
+
+// Minimum vertex cover of the cut edges (König), returned as sep[v] = 1.
+void vertex_separator(const Graph& g, const std::vector<uint8_t>& part, std::vector<uint8_t>& sep) {
+  const int n = g.n;
+  sep.assign(n, 0);
+  std::vector<int32_t> L, R, lid(n, -1), rid(n, -1);
+  for (int v = 0; v < n; ++v)
+    for (int64_t e = g.p[v]; e < g.p[v + 1]; ++e)
+      if (part[g.adj[e]] != part[v]) {
+        if (part[v] == 0) {
+          lid[v] = (int32_t)L.size();
+          L.push_back(v);
+        } else {
+          rid[v] = (int32_t)R.size();
+          R.push_back(v);
+        }
+        break;
+      }
+  const int nl = (int)L.size(), nr = (int)R.size();
+  std::vector<int64_t> bp(nl + 1, 0);
+  std::vector<int32_t> badj;
+  for (int a = 0; a < nl; ++a) {
+    const int v = L[a];
+    for (int64_t e = g.p[v]; e < g.p[v + 1]; ++e)
+      if (rid[g.adj[e]] >= 0) badj.push_back(rid[g.adj[e]]);
+    bp[a + 1] = (int64_t)badj.size();
+  }
+  // Hopcroft–Karp
+  std::vector<int32_t> ml(nl, -1), mr(nr, -1), dist(nl);
+  const int INF = 1 << 30;
+  auto bfs = [&]() {
+    std::vector<int32_t> q;
+    bool found = false;
+    for (int a = 0; a < nl; ++a) {
+      if (ml[a] == -1) {
+        dist[a] = 0;
+        q.push_back(a);
+      } else {
+        dist[a] = INF;
+      }
+    }
+    for (size_t h = 0; h < q.size(); ++h) {
+      const int a = q[h];
+      for (int64_t e = bp[a]; e < bp[a + 1]; ++e) {
+        const int b = badj[e];
+        const int a2 = mr[b];
+        if (a2 == -1) {
+          found = true;
+        } else if (dist[a2] == INF) {
+          dist[a2] = dist[a] + 1;
+          q.push_back(a2);
+        }
+      }
+    }
+    return found;
+  };
+  std::vector<int64_t> it(nl);
+  std::vector<int32_t> stk;
+  auto dfs = [&](int root) {  // iterative augmenting-path search along the BFS layers
+    stk.assign(1, root);
+    std::vector<int32_t> via;
+    while (!stk.empty()) {
+      const int a = stk.back();
+      bool advanced = false;
+      for (; it[a] < bp[a + 1]; ++it[a]) {
+        const int b = badj[it[a]];
+        const int a2 = mr[b];
+        if (a2 == -1) {  // augment along the stack
+          for (int k = (int)stk.size() - 1; k >= 0; --k) {
+            const int aa = stk[k];
+            const int bb = badj[it[aa]];
+            const int prev = ml[aa];
+            ml[aa] = bb;
+            mr[bb] = aa;
+            (void)prev;
+          }
+          return true;
+        }
+        if (dist[a2] == dist[a] + 1) {
+          stk.push_back(a2);
+          advanced = true;
+          break;
+        }
+      }
+      if (!advanced) {
+        dist[a] = INF;
+        stk.pop_back();
+        if (!stk.empty()) ++it[stk.back()];
+      }
+    }
+    return false;
+  };
+  while (bfs()) {
+    for (int a = 0; a < nl; ++a) it[a] = bp[a];
+    for (int a = 0; a < nl; ++a)
+      if (ml[a] == -1) dfs(a);
+  }
+  // Z = reachable from unmatched left vertices by alternating paths; cover = (L \ Z) + (R & Z)
+  std::vector<uint8_t> zl(nl, 0), zr(nr, 0);
+  std::vector<int32_t> q;
+  for (int a = 0; a < nl; ++a)
+    if (ml[a] == -1) {
+      zl[a] = 1;
+      q.push_back(a);
+    }
+  for (size_t h = 0; h < q.size(); ++h) {
+    const int a = q[h];
+    for (int64_t e = bp[a]; e < bp[a + 1]; ++e) {
+      const int b = badj[e];
+      if (zr[b] || ml[a] == b) continue;
+      zr[b] = 1;
+      const int a2 = mr[b];
+      if (a2 >= 0 && !zl[a2]) {
+        zl[a2] = 1;
+        q.push_back(a2);
+      }
+    }
+  }
+  for (int a = 0; a < nl; ++a)
+    if (!zl[a]) sep[L[a]] = 1;
+  for (int b = 0; b < nr; ++b)
+    if (zr[b]) sep[R[b]] = 1;
+}
+
+struct Dissector {
+  const std::vector<int64_t>& Ap;
+  const std::vector<int32_t>& Ai;
+  const NDOptions& opt;
+  std::vector<int32_t> loc;  // global -> local id of the subgraph being built (-1 outside)
+  std::vector<int32_t> out;
+  Rng rng{12345};
+
+  Dissector(const std::vector<int64_t>& p, const std::vector<int32_t>& i, const NDOptions& o, int n)
+      : Ap(p), Ai(i), opt(o), loc(n, -1) {}
+
+  void induced(const std::vector<int32_t>& verts, Graph& g) {
+    for (size_t k = 0; k < verts.size(); ++k) loc[verts[k]] = (int32_t)k;
+    g.n = (int)verts.size();
+    g.p.assign(g.n + 1, 0);
+    g.adj.clear();
+    for (int k = 0; k < g.n; ++k) {
+      const int v = verts[k];
+      for (int64_t e = Ap[v]; e < Ap[v + 1]; ++e) {
+        const int u = loc[Ai[e]];
+        if (u >= 0 && u != k) g.adj.push_back(u);
+      }
+      g.p[k + 1] = (int64_t)g.adj.size();
+    }
+    g.ew.assign(g.adj.size(), 1);
+    g.vw.assign(g.n, 1);
+  }
+  void clear_loc(const std::vector<int32_t>& verts) {
+    for (int v : verts) loc[v] = -1;
+  }
+
+  void leaf(const std::vector<int32_t>& verts, const Graph& g) {
+    std::vector<int32_t> lp;
+    if (g.n > 2) {
+      amd_order(g.n, g.p, g.adj, lp, opt.dense_alpha);
+    } else {
+      lp.resize(g.n);
+      std::iota(lp.begin(), lp.end(), 0);
+    }
+    for (int k : lp) out.push_back(verts[k]);
+  }
+
+  void dissect(const std::vector<int32_t>& verts, int depth) {
+    Graph g;
+    induced(verts, g);
+    clear_loc(verts);
+    if (g.n <= opt.leaf_size || depth > 60) {
+      leaf(verts, g);
+      return;
+    }
+    // connected components
+    std::vector<int32_t> comp(g.n, -1), q;
+    int nc = 0;
+    for (int s = 0; s < g.n; ++s) {
+      if (comp[s] != -1) continue;
+      q.assign(1, s);
+      comp[s] = nc;
+      for (size_t h = 0; h < q.size(); ++h)
+        for (int64_t e = g.p[q[h]]; e < g.p[q[h] + 1]; ++e)
+          if (comp[g.adj[e]] == -1) {
+            comp[g.adj[e]] = nc;
+            q.push_back(g.adj[e]);
+          }
+      ++nc;
+    }
+    if (nc > 1) {
+      std::vector<std::vector<int32_t>> parts(nc);
+      for (int k = 0; k < g.n; ++k) parts[comp[k]].push_back(verts[k]);
+      for (auto& pv : parts) dissect(pv, depth + 1);
+      return;
+    }
+    // best of a few multilevel bisections, scored by separator size and balance
+    std::vector<uint8_t> part, sep, bpart, bsep;
+    double bscore = 1e300;
+    const int tries = g.n > 20000 ? opt.tries : 1;  // several tries only where separators matter most
+    for (int t = 0; t < tries; ++t) {
+      bisect(g, part, rng);
+      vertex_separator(g, part, sep);
+      int64_t ns = 0, na = 0, nb = 0;
+      for (int k = 0; k < g.n; ++k) {
+        if (sep[k])
+          ++ns;
+        else if (part[k] == 0)
+          ++na;
+        else
+          ++nb;
+      }
+      if (na == 0 || nb == 0) continue;
+      if (t == 0 && ns > 2.0 * opt.sep_ratio * g.n) break;  // no small separator here: AMD
+      const double score = (double)ns * (1.0 + 2.0 * std::abs((double)(na - nb)) / (double)g.n);
+      if (score < bscore) {
+        bscore = score;
+        bpart = part;
+        bsep = sep;
+      }
+    }
+    int64_t ns = 0;
+    for (uint8_t s : bsep) ns += s;
+    if (bpart.empty() || ns > opt.sep_ratio * g.n) {
+      leaf(verts, g);
+      return;
+    }
+    std::vector<int32_t> A, B, S;
+    for (int k = 0; k < g.n; ++k) (bsep[k] ? S : (bpart[k] == 0 ? A : B)).push_back(verts[k]);
+    g = Graph();
+    dissect(A, depth + 1);
+    dissect(B, depth + 1);
+    out.insert(out.end(), S.begin(), S.end());
+  }
+};
+
+}  // namespace
+
+void nd_order(int n, const std::vector<int64_t>& Ap, const std::vector<int32_t>& Ai, std::vector<int32_t>& perm,
+              const NDOptions& opt) {
+  Dissector d(Ap, Ai, opt, n);
+  std::vector<int32_t> all(n);
+  std::iota(all.begin(), all.end(), 0);
+  d.out.reserve(n);
+  d.dissect(all, 0);
+  MADIPM_REQUIRE((int)d.out.size() == n, "nested dissection lost vertices");
+  perm.swap(d.out);
+}
+
+}  // namespace madipm

@@ -133,6 +133,27 @@ void column_counts(int N, const Pattern& P, const std::vector<int32_t>& parent, 
 
 inline int64_t trap(int64_t w, int64_t r) { return w * r - w * (w - 1) / 2; }
 
+// Factorisation flops sum_j (c_j - 1)(c_j + 2) of the order `perm` (etree + column counts only).
+double ordering_flops(int N, const int64_t* colptr, const int32_t* rowval, const std::vector<int32_t>& perm) {
+  std::vector<int32_t> pinv(N);
+  for (int k = 0; k < N; ++k) pinv[perm[k]] = k;
+  Pattern P;
+  build_pattern(N, colptr, rowval, pinv, P);
+  std::vector<int32_t> parent, post;
+  etree(N, P, parent);
+  postorder(N, parent, post);
+  std::vector<int32_t> p2(N);
+  for (int k = 0; k < N; ++k) p2[k] = perm[post[k]];
+  for (int k = 0; k < N; ++k) pinv[p2[k]] = k;
+  build_pattern(N, colptr, rowval, pinv, P);
+  etree(N, P, parent);
+  std::vector<int64_t> cnt;
+  column_counts(N, P, parent, cnt);
+  double f = 0.0;
+  for (int64_t c : cnt) f += (double)(c - 1) * (double)(c + 2);
+  return f;
+}
+
 }  // namespace
 
 void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const SymbolicOptions& opt,
@@ -156,7 +177,8 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
 
   // ---------------- 1. fill-reducing ordering
   std::vector<int32_t> perm(N);
-  if (opt.ordering == 1) {
+  S.order_flops_amd = S.order_flops_nd = 0.0;
+  if (opt.ordering == 1 || opt.ordering == 3 || opt.ordering == 4) {
     std::vector<int64_t> Ap(N + 1, 0);
     for (int j = 0; j < N; ++j)
       for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p) {
@@ -175,7 +197,21 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         Ai[fill[i]++] = j;
         Ai[fill[j]++] = i;
       }
-    amd_order(N, Ap, Ai, perm, opt.dense_alpha);
+    std::vector<int32_t> pa, pn;
+    if (opt.ordering != 3) {
+      amd_order(N, Ap, Ai, pa, opt.dense_alpha);
+      S.order_flops_amd = ordering_flops(N, colptr, rowval, pa);
+    }
+    if (opt.ordering != 1) {
+      NDOptions nopt;
+      nopt.dense_alpha = opt.dense_alpha;
+      nd_order(N, Ap, Ai, pn, nopt);
+      S.order_flops_nd = ordering_flops(N, colptr, rowval, pn);
+    }
+    if (opt.ordering == 1 || (opt.ordering == 4 && S.order_flops_amd <= S.order_flops_nd))
+      perm.swap(pa);
+    else
+      perm.swap(pn);
   } else if (opt.ordering == 2) {
     MADIPM_REQUIRE(user_perm != nullptr, "user permutation missing");
     std::copy(user_perm, user_perm + N, perm.begin());

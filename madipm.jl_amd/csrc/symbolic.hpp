@@ -15,8 +15,20 @@ namespace madipm {
 void amd_order(int n, const std::vector<int64_t>& Ap, const std::vector<int32_t>& Ai,
                std::vector<int32_t>& perm, double dense_alpha = 10.0);
 
+struct NDOptions {
+  int leaf_size = 256;       // subgraphs up to this size are ordered by AMD
+  int tries = 3;             // multilevel bisections per subgraph (best separator kept)
+  double sep_ratio = 0.1;    // a separator larger than this fraction => AMD for the subgraph
+  double dense_alpha = 10.0; // for the AMD leaves
+};
+
+// Nested dissection (csrc/nd.cpp); same input convention as amd_order.
+void nd_order(int n, const std::vector<int64_t>& Ap, const std::vector<int32_t>& Ai, std::vector<int32_t>& perm,
+              const NDOptions& opt);
+
 struct SymbolicOptions {
-  int ordering = 1;          // 0: natural, 1: AMD, 2: user permutation
+  int ordering = 1;          // 0: natural, 1: AMD, 2: user permutation, 3: nested dissection,
+                             // 4: auto (AMD and ND, the one with fewer factorisation flops)
   double dense_alpha = 10.0; // AMD dense threshold = max(16, alpha*sqrt(n))
   int relax = 1;             // relaxed supernode amalgamation on/off
   int nrelax[3] = {4, 16, 48};
@@ -76,6 +88,7 @@ struct SymbolicPlan {
   int64_t nnzL = 0;          // exact nnz(L) incl. diagonal (column counts)
   int64_t nnzL_super = 0;    // stored lower-trapezoid entries incl. relaxed zeros
   double flops = 0;          // sum_j (c_j - 1)(c_j + 2) over stored supernodal columns
+  double order_flops_amd = 0, order_flops_nd = 0;  // candidates evaluated by ordering 4 (auto)
   int max_front = 0, nbig = 0;
 };
 

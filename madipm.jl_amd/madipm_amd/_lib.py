@@ -115,7 +115,7 @@ class Symbolic:
         self._rowval = np.ascontiguousarray(rowval, np.int32)
         up = None if perm is None else np.ascontiguousarray(perm, np.int32)
         if opts is None:
-            opts = default_ldl_opts(ordering=2 if perm is not None else 1)
+            opts = default_ldl_opts(ordering=2 if perm is not None else 4)
         h = vp()
         check(madipm_symbolic_analyze(self.n, ptr(self._colptr, C.c_int64), ptr(self._rowval, C.c_int32),
                                       C.byref(opts), ptr(up, C.c_int32) if up is not None else None,

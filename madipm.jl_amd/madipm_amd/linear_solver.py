@@ -17,7 +17,7 @@ from . import _lib as L
 class HIPLDLSolver:
     """Multifrontal supernodal LDL^T on the GPU (libmadipm_hip)."""
 
-    def __init__(self, n, colptr, rowval, *, ordering=1, relax=1, pivot_tol=0.0, perm=None,
+    def __init__(self, n, colptr, rowval, *, ordering=4, relax=1, pivot_tol=0.0, perm=None,
                  small_front_max=128):
         self.n = int(n)
         self._colptr = np.ascontiguousarray(colptr, np.int64)

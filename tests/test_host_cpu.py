@@ -149,3 +149,30 @@ def test_options_parsing():
         load_options(not_an_option=1)
     with pytest.raises(NotImplementedError):
         load_options(kkt_system=NormalKKTSystem)
+
+
+@pytest.mark.parametrize("ordering", [3, 4])
+def test_nested_dissection_orderings(ordering):
+    """ND (csrc/nd.cpp) is a valid permutation with exact nnz(L) (oracle LDL^T in the same order); on
+    a block-angular K2 it beats AMD by a wide margin, and `auto` keeps the cheaper of the two."""
+    from madipm_amd._lib import Symbolic, default_ldl_opts
+    from oracle.ldl import OracleLDL
+    K, Lw = block_angular_k2(2000, 3000, 15, 3)
+    S = Symbolic(K.shape[0], Lw.indptr, Lw.indices, default_ldl_opts(ordering=ordering))
+    perm = S.perm()
+    assert sorted(perm.tolist()) == list(range(K.shape[0]))
+    F = OracleLDL(K, perm)
+    assert F.factorize() == K.shape[0]
+    assert F.nnzL() == S.info()["nnzL"]
+    amd = Symbolic(K.shape[0], Lw.indptr, Lw.indices, default_ldl_opts(ordering=1)).info()["flops"]
+    nd = Symbolic(K.shape[0], Lw.indptr, Lw.indices, default_ldl_opts(ordering=3)).info()["flops"]
+    if ordering == 4:
+        assert S.info()["flops"] <= min(amd, nd) * 1.0001
+
+
+@pytest.mark.parametrize("m,n,dens,seed", [(30, 50, 0.05, 1), (80, 120, 0.03, 2)])
+def test_nd_nnzL_brute_force(m, n, dens, seed):
+    from madipm_amd._lib import Symbolic, default_ldl_opts
+    K, Lw = random_k2(m, n, dens, seed)
+    S = Symbolic(K.shape[0], Lw.indptr, Lw.indices, default_ldl_opts(ordering=3))
+    assert S.info()["nnzL"] == _brute_nnzL(K, S.perm())
