@@ -98,8 +98,9 @@ void madipm_ldl_destroy(madipm_ldl_t ls);
  * Bit k of `mask` records HIP events around every launch of kernel kind k on the launch stream
  * (kinds: 0 k_asm_chunks, 1 k_assemble, 2 k_tiny_factor, 3 k_small_factor, 4 k_big_diag,
  * 5 k_big_trsm, 6 k_big_update, 7 k_inertia, 8 k_fwd_small, 9 k_fwd_gather, 10 k_fwd_big,
- * 11 k_bwd_below, 12 k_bwd_big, 13 k_bwd_small).  Setting a mask clears the statistics. */
-#define MADIPM_NKERNELS 14
+ * 11 k_bwd_below, 12 k_bwd_big, 13 k_bwd_small, 14 k_fwd_tiny, 15 k_bwd_tiny).  Setting a mask
+ * clears the statistics. */
+#define MADIPM_NKERNELS 16
 typedef struct madipm_kstat {
   char name[32];
   int64_t launches;

@@ -32,6 +32,12 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
@@ -56,11 +62,19 @@ __global__ void k_status_init(LDLStatus* st) {
 }
 
 // ------------------------------------------------------------------ small fronts (LDS)
+// Register-tiled right-looking LDL^T: the lower triangle of F is cut into 16 x 16 tiles of TS x TS
+// entries (TS = 8 for r <= 128, 4 for r <= 64); thread q < 136 owns tile q in registers.  Step t:
+// the owners of column t publish it through LDS (double-buffered), one barrier, every thread
+// applies the rank-1 update to its tile.  The column loop is unrolled by TS so register indices
+// are static.
+template <int TS>
 __global__ __launch_bounds__(NT) void k_small_factor(FrontTab T, const int32_t* __restrict__ fronts,
                                                      const double* __restrict__ Kx, double* __restrict__ arena,
                                                      const double* __restrict__ fscratch, double* __restrict__ D,
                                                      LDLStatus* st, double tol) {
   extern __shared__ __attribute__((aligned(16))) double F[];  // r x r, col-major, ld r
+  __shared__ double cb[2][16 * TS];
+  __shared__ double dp[16 * TS];
   const int s = fronts[blockIdx.x];
   const int f0 = T.first[s];
   const int w = T.first[s + 1] - f0;
@@ -77,31 +91,84 @@ __global__ __launch_bounds__(NT) void k_small_factor(FrontTab T, const int32_t* 
       for (int i = j + lane; i < r; i += 64) F[i + j * r] = Fs[i + j * r];
   }
   __syncthreads();
-  // right-looking LDL^T; column t stays unscaled until the write-out
-  for (int t = 0; t < w; ++t) {
-    const double dinv = 1.0 / F[t + t * r];
-    for (int j = t + 1 + wv; j < r; j += NT / 64) {
-      const double ljd = F[j + t * r] * dinv;
-      for (int i = j + lane; i < r; i += 64) F[i + j * r] -= F[i + t * r] * ljd;
+  // tile of this thread: q -> (ti, tj), tj <= ti, 136 lower tiles of a 16 x 16 grid
+  int ti = 0, tj = 0;
+  {
+    int q = tid;
+    while (q > ti) {
+      q -= ti + 1;
+      ++ti;
     }
-    __syncthreads();
+    tj = q;
   }
+  const bool act = tid < 136 && ti * TS < r;
+  const int i0 = ti * TS, j0 = tj * TS;
+  double a[TS][TS];
+#pragma unroll
+  for (int k = 0; k < TS; ++k)
+#pragma unroll
+    for (int c = 0; c < TS; ++c) a[k][c] = (act && i0 + k < r && j0 + c < r) ? F[(i0 + k) + (j0 + c) * r] : 0.0;
+  for (int t8 = 0; t8 < w; t8 += TS) {
+#pragma unroll
+    for (int c = 0; c < TS; ++c) {
+      const int t = t8 + c;
+      if (t < w) {  // block-uniform
+        double* colb = cb[t & 1];
+        if (act && tj == (t8 / TS)) {
+#pragma unroll
+          for (int k = 0; k < TS; ++k) colb[i0 + k] = a[k][c];
+        }
+        __syncthreads();
+        const double dt = colb[t];
+        if (tid == 0) dp[t] = dt;
+        const double dinv = 1.0 / dt;
+        double li[TS], cj[TS];
+#pragma unroll
+        for (int k = 0; k < TS; ++k) li[k] = (i0 + k > t) ? colb[i0 + k] * dinv : 0.0;
+#pragma unroll
+        for (int cc = 0; cc < TS; ++cc) cj[cc] = (j0 + cc > t) ? colb[j0 + cc] : 0.0;
+#pragma unroll
+        for (int k = 0; k < TS; ++k)
+#pragma unroll
+          for (int cc = 0; cc < TS; ++cc) a[k][cc] = fma(-li[k], cj[cc], a[k][cc]);
+      }
+    }
+  }
+  __syncthreads();
+  // write-out: L panel (ld r; d on the diagonal, zeros above), D, lower triangle of U (ld r - w)
   double* __restrict__ L = arena + T.l_off[s];
-  for (int t = wv; t < w; t += NT / 64) {
-    const double d = F[t + t * r];
-    const double dinv = 1.0 / d;
-    for (int i = lane; i < r; i += 64)
-      L[i + (int64_t)t * r] = (i > t) ? F[i + t * r] * dinv : (i == t ? d : 0.0);
-    if (lane == 0) {
-      D[f0 + t] = d;
-      if (bad_pivot(d, tol)) atomicMin(&st->fail_pivot, f0 + t + 1);
+  double* __restrict__ Uo = arena + T.u_off[s];
+  const int u = r - w;
+  if (act) {
+#pragma unroll
+    for (int c = 0; c < TS; ++c) {
+      const int j = j0 + c;
+      if (j >= r) continue;
+      if (j < w) {
+        const double dj = dp[j];
+        const double dinv = 1.0 / dj;
+#pragma unroll
+        for (int k = 0; k < TS; ++k) {
+          const int i = i0 + k;
+          if (i < r) L[i + (int64_t)j * r] = (i > j) ? a[k][c] * dinv : (i == j ? dj : 0.0);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < TS; ++k) {
+          const int i = i0 + k;
+          if (i < r && i >= j) Uo[(i - w) + (int64_t)(j - w) * u] = a[k][c];
+        }
+      }
     }
   }
-  const int u = r - w;
-  if (u > 0) {
-    double* __restrict__ Uo = arena + T.u_off[s];
-    for (int b = wv; b < u; b += NT / 64)
-      for (int a = b + lane; a < u; a += 64) Uo[a + (int64_t)b * u] = F[(w + a) + (w + b) * r];
+  // upper part of the L panel (rows above the tile grid's lower triangle): zeros, so the solves can
+  // read the r x w panel as stored
+  for (int j = wv; j < w; j += NT / 64)
+    for (int i = lane; i < j - (j % TS); i += 64) L[i + (int64_t)j * r] = 0.0;
+  if (tid < w) {
+    const double d = dp[tid];
+    D[f0 + tid] = d;
+    if (bad_pivot(d, tol)) atomicMin(&st->fail_pivot, f0 + tid + 1);
   }
 }
 
@@ -579,81 +646,259 @@ __global__ __launch_bounds__(NT) void k_inertia(const double* __restrict__ D, in
 //    panels (backward), dequeued in dependency order from one atomic counter; block i waits for the
 //    published x of panels < i (release/acquire flags tagged with a per-solve epoch), so the whole
 //    level is ONE launch and the panel GEMVs of different blocks overlap.
-constexpr int SMALL_SOLVE = 128;
 constexpr int SW = 4;  // waves (= small fronts) per workgroup
 
+
+// Small-front solves, one WAVE per front, no LDS: lane l holds rows (forward) or pivot columns
+// (backward) l and l + 64 in registers; the value of row/column t is broadcast with readlane; the L
+// entries a lane needs are its own row/column, loaded 8 steps ahead (software pipelined).
+__device__ __forceinline__ double bcast(double v0, double v1, int t) {
+  return (t < 64) ? readlane_f64(v0, t) : readlane_f64(v1, t - 64);
+}
 
 __global__ __launch_bounds__(NT) void k_fwd_small(FrontTab T, const int32_t* __restrict__ fronts, int nf,
                                                   const double* __restrict__ arena, const double* __restrict__ b,
                                                   double* __restrict__ xi, double* __restrict__ uvec) {
-  __shared__ double vs[SW][SMALL_SOLVE];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int q = blockIdx.x * SW + wv;
+  const int q = __builtin_amdgcn_readfirstlane(blockIdx.x * SW + wv);
   if (q >= nf) return;
-  const int s = fronts[q];
-  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
-  double* v = vs[wv];
+  // wave-uniform front scalars in SGPRs: scalar branches, unconditional loads, countable vmcnt
+  const int s = __builtin_amdgcn_readfirstlane(fronts[q]);
+  const int f0 = __builtin_amdgcn_readfirstlane(T.first[s]);
+  const int w = __builtin_amdgcn_readfirstlane(T.first[s + 1]) - f0;
+  const int r = __builtin_amdgcn_readfirstlane(T.nrows[s]);
   const double* __restrict__ L = arena + T.l_off[s];
-  for (int i = lane; i < r; i += 64) {
-    double vi = (i < w) ? b[T.perm[f0 + i]] : 0.0;
-    const int64_t e = T.row_ptr[s] + i;
-    const int64_t p1 = T.sv_ptr[e + 1];
-    for (int64_t p = T.sv_ptr[e]; p < p1; ++p) vi += uvec[T.sv_src[p]];
-    v[i] = vi;
+  const int i0 = lane, i1 = lane + 64;
+  const int ci0 = min(i0, r - 1), ci1 = min(i1, r - 1);
+  double v[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int i = lane + 64 * h;
+    double vi = 0.0;
+    if (i < r) {
+      vi = (i < w) ? b[T.perm[f0 + i]] : 0.0;
+      const int64_t e = T.row_ptr[s] + i;
+      const int64_t p1 = T.sv_ptr[e + 1];
+      for (int64_t p = T.sv_ptr[e]; p < p1; ++p) vi += uvec[T.sv_src[p]];
+    }
+    v[h] = vi;
   }
-  wave_sync();
-  for (int t = 0; t < w; ++t) {
-    const double xt = v[t];
-    const double* __restrict__ Lc = L + t * r;
-    for (int i = t + 1 + lane; i < r; i += 64) v[i] -= Lc[i] * xt;
-    wave_sync();
+  // forward substitution: v[i] -= L(i, t) v[t] for i > t, t < w.  Two register sets of 8 columns
+  // in ping-pong (no copies), so the loads of the next block stay in flight during this one.
+  double A0[8], A1[8], B0[8], B1[8];
+  auto load = [&](double(&c0)[8], double(&c1)[8], int tb) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // raw, clamped loads (masks applied at use: vmcnt stays countable)
+      const int64_t col = (int64_t)min(tb + k, w - 1) * r;
+      c0[k] = L[ci0 + col];
+      c1[k] = L[ci1 + col];
+    }
+  };
+  auto step = [&](const double(&c0)[8], const double(&c1)[8], int tb) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int t = tb + k;
+      if (t < w) {  // rows >= r hold garbage that is never stored
+        const double xt = bcast(v[0], v[1], t);
+        v[0] = fma(i0 > t ? -c0[k] : 0.0, xt, v[0]);
+        v[1] = fma(i1 > t ? -c1[k] : 0.0, xt, v[1]);
+      }
+    }
+  };
+  load(A0, A1, 0);
+  for (int t8 = 0; t8 < w; t8 += 16) {
+    load(B0, B1, t8 + 8);
+    step(A0, A1, t8);
+    if (t8 + 8 >= w) break;
+    load(A0, A1, t8 + 16);
+    step(B0, B1, t8 + 8);
   }
   double* __restrict__ uo = uvec + T.uvec_off[s];
-  for (int i = lane; i < r; i += 64) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int i = lane + 64 * h;
     if (i < w)
-      xi[f0 + i] = v[i];
-    else
-      uo[i - w] = v[i];
+      xi[f0 + i] = v[h];
+    else if (i < r)
+      uo[i - w] = v[h];
   }
 }
 
 __global__ __launch_bounds__(NT) void k_bwd_small(FrontTab T, const int32_t* __restrict__ fronts, int nf,
                                                   const double* __restrict__ arena, const double* __restrict__ D,
                                                   double* __restrict__ xi, double* __restrict__ out) {
-  __shared__ double vs[SW][SMALL_SOLVE];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int q = blockIdx.x * SW + wv;
+  const int q = __builtin_amdgcn_readfirstlane(blockIdx.x * SW + wv);
   if (q >= nf) return;
-  const int s = fronts[q];
-  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
-  double* v = vs[wv];
+  const int s = __builtin_amdgcn_readfirstlane(fronts[q]);
+  const int f0 = __builtin_amdgcn_readfirstlane(T.first[s]);
+  const int w = __builtin_amdgcn_readfirstlane(T.first[s + 1]) - f0;
+  const int r = __builtin_amdgcn_readfirstlane(T.nrows[s]);
   const double* __restrict__ L = arena + T.l_off[s];
   const int32_t* __restrict__ rows = T.rows + T.row_ptr[s];
-  for (int i = lane; i < r; i += 64) v[i] = (i < w) ? xi[f0 + i] / D[f0 + i] : xi[rows[i]];
-  wave_sync();
-  // v[t] -= L21(:,t)^T x(below), four columns per pass
-  for (int t0 = 0; t0 < w; t0 += 4) {
-    double a[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int i = w + lane; i < r; i += 64) {
-      const double vi = v[i];
+  const int j0 = lane, j1 = lane + 64;  // pivot columns of this lane
+  const int cj0 = min(j0, w - 1), cj1 = min(j1, w - 1);
+  // x of the rows below the pivot block (final: ancestors); lane k holds row w + k (+ 64)
+  double xb[2];
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (t0 + k < w) a[k] += L[i + (t0 + k) * r] * vi;
+  for (int h = 0; h < 2; ++h) {
+    const int i = w + lane + 64 * h;
+    xb[h] = (i < r) ? xi[rows[i]] : 0.0;
+  }
+  // v[j] = x_j / d_j - sum_{i >= w} L(i, j) x_i
+  double acc0 = 0.0, acc1 = 0.0;
+  const int nb = r - w;
+  {
+    double A0[8], A1[8], B0[8], B1[8];
+    auto load = [&](double(&l0)[8], double(&l1)[8], int kb) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int ci = min(w + kb + k, r - 1);
+        l0[k] = L[ci + (int64_t)cj0 * r];
+        l1[k] = L[ci + (int64_t)cj1 * r];
+      }
+    };
+    auto step = [&](const double(&l0)[8], const double(&l1)[8], int kb) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (kb + k < nb) {
+          const double x = bcast(xb[0], xb[1], kb + k);
+          acc0 = fma(l0[k], x, acc0);
+          acc1 = fma(l1[k], x, acc1);
+        }
+      }
+    };
+    if (nb > 0) load(A0, A1, 0);
+    for (int k8 = 0; k8 < nb; k8 += 16) {
+      load(B0, B1, k8 + 8);
+      step(A0, A1, k8);
+      if (k8 + 8 >= nb) break;
+      load(A0, A1, k8 + 16);
+      step(B0, B1, k8 + 8);
     }
+  }
+  double v[2];
+  v[0] = (j0 < w) ? xi[f0 + j0] / D[f0 + j0] - acc0 : 0.0;
+  v[1] = (j1 < w) ? xi[f0 + j1] / D[f0 + j1] - acc1 : 0.0;
+  // transposed back substitution: for t = w-1 .. 1: v[j] -= L(t, j) v[t] for j < t (ping-pong sets)
+  double A0[8], A1[8], B0[8], B1[8];
+  auto load = [&](double(&c0)[8], double(&c1)[8], int tb) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) a[k] = wave_sum(a[k]);
-    if (lane == 0)
-      for (int k = 0; k < 4 && t0 + k < w; ++k) v[t0 + k] -= a[k];
+    for (int k = 0; k < 8; ++k) {
+      const int ct = max(tb - k, 0);
+      c0[k] = L[ct + (int64_t)cj0 * r];
+      c1[k] = L[ct + (int64_t)cj1 * r];
+    }
+  };
+  auto step = [&](const double(&c0)[8], const double(&c1)[8], int tb) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int t = tb - k;
+      if (t > 0) {
+        const double xt = bcast(v[0], v[1], t);
+        v[0] = fma(t > j0 ? -c0[k] : 0.0, xt, v[0]);
+        v[1] = fma(t > j1 ? -c1[k] : 0.0, xt, v[1]);
+      }
+    }
+  };
+  load(A0, A1, w - 1);
+  for (int t8 = w - 1; t8 > 0; t8 -= 16) {
+    load(B0, B1, t8 - 8);
+    step(A0, A1, t8);
+    if (t8 - 8 <= 0) break;
+    load(A0, A1, t8 - 16);
+    step(B0, B1, t8 - 8);
   }
-  wave_sync();
-  for (int t = w - 1; t > 0; --t) {
-    const double xt = v[t];
-    for (int i = lane; i < t; i += 64) v[i] -= L[t + i * r] * xt;
-    wave_sync();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int j = lane + 64 * h;
+    if (j < w) {
+      xi[f0 + j] = v[h];
+      out[T.perm[f0 + j]] = v[h];
+    }
   }
-  for (int i = lane; i < w; i += 64) {
-    xi[f0 + i] = v[i];
-    out[T.perm[f0 + i]] = v[i];
+}
+
+// Fronts with r <= 32 (the leaf level has ~10^5): HALF a wave per front, 8 fronts per workgroup;
+// lane l & 31 holds row / pivot column l & 31, values exchanged with 32-wide shuffles.
+__global__ __launch_bounds__(NT) void k_fwd_tiny(FrontTab T, const int32_t* __restrict__ fronts, int nf,
+                                                 const double* __restrict__ arena, const double* __restrict__ b,
+                                                 double* __restrict__ xi, double* __restrict__ uvec) {
+  const int lane = threadIdx.x & 63, lr = lane & 31;
+  const int q = (blockIdx.x * SW + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  const bool live = q < nf;
+  const int s = fronts[live ? q : nf - 1];
+  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+  const double* __restrict__ L = arena + T.l_off[s];
+  double v = 0.0;
+  if (lr < r) {
+    v = (lr < w) ? b[T.perm[f0 + lr]] : 0.0;
+    const int64_t e = T.row_ptr[s] + lr;
+    const int64_t p1 = T.sv_ptr[e + 1];
+    for (int64_t p = T.sv_ptr[e]; p < p1; ++p) v += uvec[T.sv_src[p]];
+  }
+  const int wmax = max(__builtin_amdgcn_readlane(w, 0), __builtin_amdgcn_readlane(w, 32));
+  const int cl = min(lr, r - 1);
+  for (int t4 = 0; t4 < wmax; t4 += 4) {
+    double c[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c[k] = L[cl + (int64_t)min(t4 + k, w - 1) * r];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int t = t4 + k;
+      const double xt = __shfl(v, t & 31, 32);
+      v = fma((t < w && lr > t) ? -c[k] : 0.0, xt, v);
+    }
+  }
+  if (live && lr < r) {
+    if (lr < w)
+      xi[f0 + lr] = v;
+    else
+      uvec[T.uvec_off[s] + lr - w] = v;
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_bwd_tiny(FrontTab T, const int32_t* __restrict__ fronts, int nf,
+                                                 const double* __restrict__ arena, const double* __restrict__ D,
+                                                 double* __restrict__ xi, double* __restrict__ out) {
+  const int lane = threadIdx.x & 63, lr = lane & 31;
+  const int q = (blockIdx.x * SW + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  const bool live = q < nf;
+  const int s = fronts[live ? q : nf - 1];
+  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+  const double* __restrict__ L = arena + T.l_off[s];
+  const int32_t* __restrict__ rows = T.rows + T.row_ptr[s];
+  const int nb = r - w;
+  const double xb = (lr < nb) ? xi[rows[w + lr]] : 0.0;  // x of below row w + lr (final)
+  const int cj = min(lr, w - 1);
+  const int nbmax = max(__builtin_amdgcn_readlane(nb, 0), __builtin_amdgcn_readlane(nb, 32));
+  double acc = 0.0;
+  for (int k4 = 0; k4 < nbmax; k4 += 4) {
+    double c[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c[k] = L[min(w + k4 + k, r - 1) + (int64_t)cj * r];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const double x = __shfl(xb, (k4 + k) & 31, 32);
+      acc = fma((k4 + k < nb) ? c[k] : 0.0, x, acc);
+    }
+  }
+  double v = (lr < w) ? xi[f0 + lr] / D[f0 + lr] - acc : 0.0;
+  const int wmax = max(__builtin_amdgcn_readlane(w, 0), __builtin_amdgcn_readlane(w, 32));
+  for (int t4 = wmax - 1; t4 > 0; t4 -= 4) {
+    double c[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c[k] = L[min(max(t4 - k, 0), w - 1) + (int64_t)cj * r];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int t = t4 - k;
+      const double xt = __shfl(v, max(t, 0) & 31, 32);
+      v = fma((t > 0 && t < w && lr < t) ? -c[k] : 0.0, xt, v);
+    }
+  }
+  if (live && lr < w) {
+    xi[f0 + lr] = v;
+    out[T.perm[f0 + lr]] = v;
   }
 }
 
@@ -1037,12 +1282,15 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     std::vector<int32_t> tasks, bp_off(ns, 0);
     int64_t nbpart = 0;
     for (int lev = 0; lev < S.nlevels; ++lev) {
-      std::vector<int32_t> small, big;
+      std::vector<int32_t> tiny, small, big;
       for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
         const int s = S.level_list[q];
-        (S.nrows[s] > 128 ? big : small).push_back(s);
+        (S.nrows[s] > 128 ? big : (S.nrows[s] > 32 ? small : tiny)).push_back(s);
       }
       SolveLevel L{};
+      L.tiny_off = (int64_t)sched.size();
+      L.ntiny = (int)tiny.size();
+      sched.insert(sched.end(), tiny.begin(), tiny.end());
       L.small_off = (int64_t)sched.size();
       L.nsmall = (int)small.size();
       sched.insert(sched.end(), small.begin(), small.end());
@@ -1094,6 +1342,11 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         L.small_bytes += 8.0 * (r * w + 3.0 * r);
         L.small_flops += 2.0 * (r * w - w * (w + 1) / 2);
       }
+      for (int f : tiny) {
+        const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
+        L.tiny_bytes += 8.0 * (r * w + 3.0 * r);
+        L.tiny_flops += 2.0 * (r * w - w * (w + 1) / 2);
+      }
       for (int f : big) {
         const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
         L.big_bytes += 8.0 * (r * w + 3.0 * r);
@@ -1123,7 +1376,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   MADIPM_HIP(hipHostMalloc((void**)&h_status_, sizeof(LDLStatus), hipHostMallocDefault));
   static bool attr_done = false;
   if (!attr_done) {
-    MADIPM_HIP(hipFuncSetAttribute((const void*)k_small_factor, hipFuncAttributeMaxDynamicSharedMemorySize,
+    MADIPM_HIP(hipFuncSetAttribute((const void*)k_small_factor<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    128 * 128 * 8));
     attr_done = true;
   }
@@ -1145,7 +1398,8 @@ LDLSolver::~LDLSolver() {
 const char* kernel_kind_name(int k) {
   static const char* names[KK_COUNT] = {"k_asm_chunks", "k_assemble",  "k_tiny_factor", "k_small_factor", "k_big_diag",
                                         "k_big_trsm",   "k_big_update", "k_inertia",    "k_fwd_small",    "k_fwd_gather",
-                                        "k_fwd_big",    "k_bwd_below",  "k_bwd_big",    "k_bwd_small"};
+                                        "k_fwd_big",    "k_bwd_below",  "k_bwd_big",    "k_bwd_small",
+                                        "k_fwd_tiny",   "k_bwd_tiny"};
   return (k >= 0 && k < KK_COUNT) ? names[k] : "?";
 }
 
@@ -1213,13 +1467,15 @@ void LDLSolver::factorize_async(const double* Kx, hipStream_t s) {
                                                                       status_, pivot_tol)));
         break;
       case SMALL64:
-      case SMALL128: {
-        const int R = L.kind == SMALL32 ? 32 : (L.kind == SMALL64 ? 64 : 128);
         TIMED(KK_SMALL, L.bytes, L.flops,
-              (k_small_factor<<<(unsigned)L.items, NT, R * R * 8, s>>>(T_, list, Kx, arena_, fscratch_, D_, status_,
-                                                                      pivot_tol)));
+              (k_small_factor<4><<<(unsigned)L.items, NT, 64 * 64 * 8, s>>>(T_, list, Kx, arena_, fscratch_, D_,
+                                                                           status_, pivot_tol)));
         break;
-      }
+      case SMALL128:
+        TIMED(KK_SMALL, L.bytes, L.flops,
+              (k_small_factor<8><<<(unsigned)L.items, NT, 128 * 128 * 8, s>>>(T_, list, Kx, arena_, fscratch_, D_,
+                                                                             status_, pivot_tol)));
+        break;
       case BIG_DIAG:
         TIMED(KK_DIAG, L.bytes, L.flops,
               (k_big_diag<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_, minv_, status_, pivot_tol)));
@@ -1261,6 +1517,10 @@ void LDLSolver::solve_async(double* b, hipStream_t s) {
   const int nl = (int)slev_.size();
   for (int lev = 0; lev < nl; ++lev) {
     const SolveLevel& L = slev_[lev];
+    if (L.ntiny)
+      TIMED(KK_FWD_TINY, L.tiny_bytes, L.tiny_flops,
+            (k_fwd_tiny<<<(unsigned)cdiv(L.ntiny, 2 * SW), NT, 0, s>>>(T_, sched_.p + L.tiny_off, L.ntiny, arena_, b, xi_,
+                                                                      uvec_)));
     if (L.nsmall)
       TIMED(KK_FWD_SMALL, L.small_bytes, L.small_flops,
             (k_fwd_small<<<(unsigned)cdiv(L.nsmall, SW), NT, 0, s>>>(T_, sched_.p + L.small_off, L.nsmall, arena_, b, xi_,
@@ -1287,6 +1547,10 @@ void LDLSolver::solve_async(double* b, hipStream_t s) {
       TIMED(KK_BWD_SMALL, L.small_bytes, L.small_flops,
             (k_bwd_small<<<(unsigned)cdiv(L.nsmall, SW), NT, 0, s>>>(T_, sched_.p + L.small_off, L.nsmall, arena_, D_, xi_,
                                                                     b)));
+    if (L.ntiny)
+      TIMED(KK_BWD_TINY, L.tiny_bytes, L.tiny_flops,
+            (k_bwd_tiny<<<(unsigned)cdiv(L.ntiny, 2 * SW), NT, 0, s>>>(T_, sched_.p + L.tiny_off, L.ntiny, arena_, D_, xi_,
+                                                                      b)));
   }
   MADIPM_HIP(hipGetLastError());
 }

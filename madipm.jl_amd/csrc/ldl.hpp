@@ -51,7 +51,8 @@ struct LDLStatus {  // device-resident, read back by status()
 // stream) and their algorithmic bytes / flops per launch (DESIGN.md "Kernels and their rooflines").
 enum KernelKind {
   KK_ASM_CHUNKS = 0, KK_ASSEMBLE, KK_TINY, KK_SMALL, KK_DIAG, KK_TRSM, KK_UPDATE, KK_INERTIA,
-  KK_FWD_SMALL, KK_FWD_GATHER, KK_FWD_BIG, KK_BWD_BELOW, KK_BWD_BIG, KK_BWD_SMALL, KK_COUNT
+  KK_FWD_SMALL, KK_FWD_GATHER, KK_FWD_BIG, KK_BWD_BELOW, KK_BWD_BIG, KK_BWD_SMALL, KK_FWD_TINY, KK_BWD_TINY,
+  KK_COUNT
 };
 const char* kernel_kind_name(int k);
 
@@ -102,6 +103,8 @@ class LDLSolver {
     double bytes2 = 0, flops2 = 0;     // ASSEMBLE: of the chunk pass
   };
   struct SolveLevel {
+    int64_t tiny_off;  // fronts with r <= 32 (half a wave each)
+    int ntiny;
     int64_t small_off;
     int nsmall;
     int64_t big_off;
@@ -114,6 +117,7 @@ class LDLSolver {
     int nftask;
     int64_t btask_off;
     int nbtask;
+    double tiny_bytes = 0, tiny_flops = 0;
     double small_bytes = 0, small_flops = 0, big_bytes = 0, big_flops = 0, below_bytes = 0, gat_bytes = 0;
   };
   SymbolicPlan S_;

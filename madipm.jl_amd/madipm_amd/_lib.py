@@ -40,7 +40,7 @@ class LDLInfo(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
-NKERNELS = 14  # MADIPM_NKERNELS
+NKERNELS = 16  # MADIPM_NKERNELS
 
 
 class KStat(C.Structure):
