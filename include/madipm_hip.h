@@ -146,7 +146,8 @@ typedef struct madipm_options {
   double mu_init, mu_min;     /* 1e-1, 1e-12 */
   double tol_linear_solve;    /* 1e-8 */
   int32_t check_residual;     /* 0 */
-  int32_t kkt_system;         /* 0 SparseKKTSystem (K2) */
+  int32_t kkt_system;         /* 0 SparseKKTSystem (K2), 1 ScaledSparseKKTSystem (K2.5),
+                                 2 NormalKKTSystem (src/KKT/normalkkt.jl; LPs only, Cholesky semantics) */
   int32_t print_level;        /* 0 silent, 1 iteration log to stdout */
   madipm_ldl_opts ldl;
 } madipm_options;

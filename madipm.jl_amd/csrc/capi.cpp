@@ -303,7 +303,7 @@ int madipm_solver_create(const madipm_qp* qp, const madipm_options* opt, madipm_
   madipm_options o;
   madipm_default_options(&o);
   if (opt) o = *opt;
-  MADIPM_REQUIRE(o.kkt_system == 0, "only kkt_system = 0 (SparseKKTSystem, K2) is implemented");
+  MADIPM_REQUIRE(o.kkt_system >= 0 && o.kkt_system <= 2, "kkt_system must be 0 (K2), 1 (K2.5) or 2 (normal equations)");
   auto s = std::make_unique<madipm_solver>();
   s->s = std::make_unique<MPCSolver>(*qp, o);
   *out = s.release();

@@ -609,7 +609,7 @@ __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __
       }
 }
 
-__global__ __launch_bounds__(NT) void k_inertia(const double* __restrict__ D, int n, LDLStatus* st) {
+__global__ __launch_bounds__(NT) void k_inertia(const double* __restrict__ D, int n, LDLStatus* st, int spd) {
   __shared__ int red[3][NT / 64];
   int pos = 0, neg = 0, zero = 0;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -617,6 +617,7 @@ __global__ __launch_bounds__(NT) void k_inertia(const double* __restrict__ D, in
     pos += d > 0.0;
     neg += d < 0.0;
     zero += !(d > 0.0) && !(d < 0.0);
+    if (spd && !(d > 0.0)) atomicMin(&st->fail_pivot, i + 1);
   }
   for (int o = 32; o > 0; o >>= 1) {
     pos += __shfl_down(pos, o, 64);
@@ -1489,7 +1490,7 @@ void LDLSolver::factorize_async(const double* Kx, hipStream_t s) {
     }
   }
   const int nb = (int)std::min<int64_t>(64, cdiv(S_.N, NT));
-  TIMED(KK_INERTIA, 8.0 * S_.N, 0.0, (k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, status_)));
+  TIMED(KK_INERTIA, 8.0 * S_.N, 0.0, (k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, status_, spd ? 1 : 0)));
   MADIPM_HIP(hipGetLastError());
   MADIPM_HIP(hipMemcpyAsync(h_status_, status_.p, sizeof(LDLStatus), hipMemcpyDeviceToHost, s));
 }

@@ -81,6 +81,7 @@ class LDLSolver {
   int npos = 0, nneg = 0, nzero = 0;
   bool factorized = false;
   double pivot_tol = 0.0;
+  bool spd = false;  // Cholesky semantics: any non-positive pivot fails (normal equations)
 
   // device buffers for diagnostics
   const double* d_diag() const { return D_.p; }

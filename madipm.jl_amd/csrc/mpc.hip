@@ -67,7 +67,21 @@ struct DV {
   DCsr H, J, JT;
   double* part;
   DevState* st;
+  // KKT formulation (madipm_options.kkt_system): K2 / K2.5 (scaled) / normal equations
+  int kkt;
+  double* sk;               // K2.5: primal scaling s_i = sqrt(dist_l * dist_u)
+  const int32_t *Krow, *Kcol;
+  const double* K0;         // K2.5: unscaled K2 values (off-diagonal entries are constant)
+  int64_t nnzK;
+  double* Dinv;             // normal: 1 ./ pr_diag
+  double* bufm;             // normal: right-hand side / solution of the m x m system
+  const int64_t* cpp;       // normal: C entry e = sum over products [cpp[e], cpp[e+1])
+  const int2* cprod;        //   product = (position of A_ik, position of A_jk) in J's values
+  double* Cx;               //   values of C = A Sigma^{-1} A^T (lower CSC)
+  int64_t nnzC;
 };
+
+enum { KKT_K2 = 0, KKT_K25 = 1, KKT_NORMAL = 2 };
 
 enum { OP_SUM = 0, OP_MAX = 1, OP_MIN = 2 };
 
@@ -110,34 +124,55 @@ __device__ __forceinline__ void amin_upd(double& v, int& ix, double nv, int ni) 
 
 #define GRID_LOOP(i, N) for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < (N); i += (int64_t)gridDim.x * blockDim.x)
 
-// ------------------------------------------------------------------ KKT diagonal (kernels.jl:124-136)
+// ------------------------------------------------------------------ KKT diagonal (kernels.jl:124-149)
+// K2 (set_aug_diagonal! for SparseKKTSystem, kernels.jl:124-136): pr_diag into the K2 diagonal.
+// K2.5 (kernels.jl:139-149 + MadNLP._set_aug_diagonal! [EXT]): the primal block is scaled
+// symmetrically by S = diag(s), s_i = sqrt((x - xl)(xu - x)) (a missing bound contributes 1), so the
+// diagonal is s^2 (dw + H_ii) + zl (xu - x) + zu (x - xl) — bounded as x approaches a bound.
+// Normal equations (NormalKKTSystem.build_kkt!, normalkkt.jl:180-194): Dinv = 1 ./ pr_diag.
+// l_diag / u_diag keep the K2 sign convention (xl - x, x - xu) in every mode: they feed the
+// unreduced operator of the residual, which is the same for the three formulations.
 __global__ __launch_bounds__(NT) void k_diag(DV D, double dw, double dc) {
   GRID_LOOP(i, D.n + D.m) {
     if (i < D.n) {
       double pr = dw;
       const int kl = D.lbpos[i], ku = D.ubpos[i];
       const double x = D.x[i];
+      double dl = 1.0, du = 1.0, zlv = 0.0, zuv = 0.0;
       if (kl >= 0) {
         const double ld = D.xl[i] - x, zl = D.zl[i];
         D.l_diag[kl] = ld;
         D.l_lower[kl] = zl;
         pr -= zl / ld;
+        dl = -ld;
+        zlv = zl;
       }
       if (ku >= 0) {
         const double ud = x - D.xu[i], zu = D.zu[i];
         D.u_diag[ku] = ud;
         D.u_lower[ku] = zu;
         pr -= zu / ud;
+        du = -ud;
+        zuv = zu;
       }
       D.pr_diag[i] = pr;
-      D.Kx[D.diag_pos[i]] = pr + D.Hdiag[i];
-    } else {
+      if (D.kkt == KKT_NORMAL) {
+        D.Dinv[i] = 1.0 / pr;
+      } else if (D.kkt == KKT_K25) {
+        const double s2 = dl * du;
+        D.sk[i] = sqrt(s2);
+        D.Kx[D.diag_pos[i]] = s2 * (dw + D.Hdiag[i]) + zlv * du + zuv * dl;
+      } else {
+        D.Kx[D.diag_pos[i]] = pr + D.Hdiag[i];
+      }
+    } else if (D.kkt != KKT_NORMAL) {
       D.Kx[D.diag_pos[i]] = dc;
     }
   }
 }
 
-// MadNLP.initialize!(kkt) + init_starting_point! lines 16-18
+// MadNLP.initialize!(kkt) + init_starting_point! lines 16-18 (l_diag = u_diag = 1, l/u_lower = 0,
+// pr_diag = dw; K2.5 scaling factor 1)
 __global__ __launch_bounds__(NT) void k_init_kkt(DV D, double dw, double dc) {
   GRID_LOOP(i, D.n + D.m) {
     if (i < D.n) {
@@ -151,9 +186,70 @@ __global__ __launch_bounds__(NT) void k_init_kkt(DV D, double dw, double dc) {
         D.u_lower[ku] = 0.0;
       }
       D.pr_diag[i] = dw;
-      D.Kx[D.diag_pos[i]] = dw + D.Hdiag[i];
-    } else {
+      if (D.kkt == KKT_NORMAL) {
+        D.Dinv[i] = 1.0 / dw;
+      } else {
+        if (D.kkt == KKT_K25) D.sk[i] = 1.0;
+        D.Kx[D.diag_pos[i]] = dw + D.Hdiag[i];
+      }
+    } else if (D.kkt != KKT_NORMAL) {
       D.Kx[D.diag_pos[i]] = dc;
+    }
+  }
+}
+
+// K2.5: off-diagonal entries K[e] = s_row s_col K0[e] (s = 1 on the dual block)
+__global__ __launch_bounds__(NT) void k_k25_scale(DV D) {
+  GRID_LOOP(e, D.nnzK) {
+    const int r = D.Krow[e], c = D.Kcol[e];
+    if (r == c) continue;
+    const double sr = r < D.n ? D.sk[r] : 1.0, sc = c < D.n ? D.sk[c] : 1.0;
+    D.Kx[e] = sr * sc * D.K0[e];
+  }
+}
+
+// K2.5: dx = S (S^{-1} dx) after the scaled solve
+__global__ __launch_bounds__(NT) void k_k25_unscale(DV D) {
+  GRID_LOOP(i, D.n) D.d[i] *= D.sk[i];
+}
+
+// NormalKKTSystem.build_kkt! / assemble_normal_system! (normalkkt.jl:180-194, utils.jl:276-308):
+// C_ij = sum_k A_ik Sigma_k^{-1} A_jk over the precomputed product list of entry (i, j) — one
+// thread per entry of tril(C), fixed summation order, no atomics.
+__global__ __launch_bounds__(NT) void k_normal_asm(DV D) {
+  GRID_LOOP(e, D.nnzC) {
+    double v = 0.0;
+    const int64_t p1 = D.cpp[e + 1];
+    for (int64_t p = D.cpp[e]; p < p1; ++p) {
+      const int2 ab = D.cprod[p];
+      v += D.J.v[ab.x] * D.Dinv[D.J.ci[ab.x]] * D.J.v[ab.y];
+    }
+    D.Cx[e] = v;
+  }
+}
+
+// MadNLP.solve!(kkt::NormalKKTSystem, w) (normalkkt.jl:196-219), after reduce_rhs! (done by k_rhs):
+// r2 = A Sigma^{-1} r1 - r2 (one thread per row of A)
+__global__ __launch_bounds__(NT) void k_normal_rhs(DV D) {
+  GRID_LOOP(i, D.m) {
+    double s = 0.0;
+    for (int64_t q = D.J.rp[i]; q < D.J.rp[i + 1]; ++q) {
+      const int k = D.J.ci[q];
+      s += D.J.v[q] * (D.d[k] / D.pr_diag[k]);
+    }
+    D.bufm[i] = s - D.d[D.n + i];
+  }
+}
+
+// ... dy = C^{-1} r2 (LDL^T solve on bufm), then dx = Sigma^{-1} (r1 - A^T dy), wy = dy
+__global__ __launch_bounds__(NT) void k_normal_back(DV D) {
+  GRID_LOOP(i, D.n + D.m) {
+    if (i < D.n) {
+      double s = 0.0;
+      for (int64_t q = D.JT.rp[i]; q < D.JT.rp[i + 1]; ++q) s += D.JT.v[q] * D.bufm[D.JT.ci[q]];
+      D.d[i] = (D.d[i] - s) / D.pr_diag[i];
+    } else {
+      D.d[i] = D.bufm[i - D.n];
     }
   }
 }
@@ -208,7 +304,7 @@ __global__ __launch_bounds__(NT) void k_rhs(DV D, int mode, double mu_g) {
         dr -= pz / D.u_diag[ku];
       }
       D.p[i] = px;
-      D.d[i] = dr;
+      D.d[i] = (D.kkt == KKT_K25) ? dr * D.sk[i] : dr;  // K2.5: right-hand side S r1
     } else {
       const double py = (mode == RHS_INIT_DUAL) ? 0.0 : -D.c[i - n];
       D.p[i] = py;
@@ -1036,13 +1132,72 @@ void MPCSolver::setup_host(const madipm_qp& q) {
       if (Kri[q] == j) diag_pos[j] = q;
   for (int j = 0; j < n + m; ++j) MADIPM_REQUIRE(diag_pos[j] >= 0, "missing KKT diagonal");
 
-  // ---- LDL^T symbolic analysis + device plan (linear-solver constructor)
+  // ---- KKT formulation + LDL^T symbolic analysis + device plan (linear-solver constructor)
+  kkt_ = opt_.kkt_system;
+  MADIPM_REQUIRE(kkt_ == KKT_K2 || kkt_ == KKT_K25 || kkt_ == KKT_NORMAL, "unknown kkt_system");
   SymbolicOptions so;
   so.ordering = opt_.ldl.ordering;
   so.dense_alpha = opt_.ldl.dense_alpha;
   so.relax = opt_.ldl.relax;
   so.small_front_max = opt_.ldl.small_front_max;
-  ldl_ = std::make_unique<LDLSolver>(n + m, Kcp.data(), Kri.data(), so, opt_.ldl.pivot_tol);
+  std::vector<int64_t> Ccp, cpp;
+  std::vector<int32_t> Cri, cprod;
+  if (kkt_ == KKT_NORMAL) {
+    // NormalKKTSystem constructor (normalkkt.jl:29-140): LP only; pattern of tril(A A^T) with A the
+    // scaled Jacobian with slack columns (build_normal_system, utils.jl:209-274), plus the product
+    // list of every entry for the assembly kernel (positions into J's CSR values).
+    MADIPM_REQUIRE(q.nnzh == 0,
+                   "The KKT system NormalKKTSystem supports only linear programs. "
+                   "The problem has a positive number of nonzero in its Hessian.");
+    std::vector<int64_t> colp(n + 1, 0);
+    for (int32_t k : Jci) colp[k + 1]++;
+    for (int k = 0; k < n; ++k) colp[k + 1] += colp[k];
+    std::vector<int32_t> crow(Jci.size()), cpos(Jci.size());
+    {
+      std::vector<int64_t> fill(colp.begin(), colp.end() - 1);
+      for (int i = 0; i < m; ++i)
+        for (int64_t p = Jrp[i]; p < Jrp[i + 1]; ++p) {
+          const int64_t t = fill[Jci[p]]++;
+          crow[t] = i;
+          cpos[t] = (int32_t)p;
+        }
+    }
+    Ccp.assign(m + 1, 0);
+    cpp.push_back(0);
+    struct Prod {
+      int32_t j, a, b;
+    };
+    std::vector<Prod> pr;
+    for (int i = 0; i < m; ++i) {
+      pr.clear();
+      for (int64_t p = Jrp[i]; p < Jrp[i + 1]; ++p) {
+        const int k = Jci[p];
+        for (int64_t t = colp[k]; t < colp[k + 1]; ++t)
+          if (crow[t] >= i) pr.push_back({crow[t], (int32_t)p, cpos[t]});
+      }
+      std::stable_sort(pr.begin(), pr.end(), [](const Prod& x, const Prod& y) { return x.j < y.j; });
+      for (size_t t = 0; t < pr.size(); ++t) {
+        if (t == 0 || pr[t].j != pr[t - 1].j) {
+          if (t) cpp.push_back((int64_t)cprod.size() / 2);
+          Cri.push_back(pr[t].j);
+        }
+        cprod.push_back(pr[t].a);
+        cprod.push_back(pr[t].b);
+      }
+      if (!pr.empty()) {
+        cpp.push_back((int64_t)cprod.size() / 2);
+      } else {  // empty row of A: structurally singular C; keep the (zero) diagonal entry
+        Cri.push_back(i);
+        cpp.push_back((int64_t)cprod.size() / 2);
+      }
+      Ccp[i + 1] = (int64_t)Cri.size();
+    }
+    nnzC_ = (int64_t)Cri.size();
+    ldl_ = std::make_unique<LDLSolver>(m, Ccp.data(), Cri.data(), so, opt_.ldl.pivot_tol);
+    ldl_->spd = true;  // Cholesky semantics (test/test_gpu.jl:11): a non-positive pivot fails
+  } else {
+    ldl_ = std::make_unique<LDLSolver>(n + m, Kcp.data(), Kri.data(), so, opt_.ldl.pivot_tol);
+  }
 
   // ---- uploads
   std::vector<int32_t> lbpos(n, -1), ubpos(n, -1);
@@ -1098,6 +1253,21 @@ void MPCSolver::setup_host(const madipm_qp& q) {
   zeros(dsave_, L_);
   zeros(corr_lb_, nlb_);
   zeros(corr_ub_, nub_);
+  if (kkt_ == KKT_NORMAL) {
+    up(cpp_, cpp);
+    up(cprod_, cprod, 2);
+    zeros(Cx_, nnzC_);
+    zeros(Dinv_, n);
+    zeros(bufm_, m);
+  } else if (kkt_ == KKT_K25) {
+    std::vector<int32_t> krow(Kri), kcol(Kri.size());
+    for (int j = 0; j < n + m; ++j)
+      for (int64_t q = Kcp[j]; q < Kcp[j + 1]; ++q) kcol[q] = j;
+    up(Krow_, krow);
+    up(Kcol_, kcol);
+    up(K0_, Kv);
+    zeros(sk_, n);
+  }
   part_.alloc(MAXB * NPART);
   st_.alloc(1);
   st_.zero(s);
@@ -1149,11 +1319,51 @@ void MPCSolver::setup_host(const madipm_qp& q) {
   D.J = DCsr{Jrp_, Jci_, Jv_};                                                                          \
   D.JT = DCsr{JTrp_, JTci_, JTv_};                                                                      \
   D.part = part_;                                                                                       \
-  D.st = st_;
+  D.st = st_;                                                                                           \
+  D.kkt = kkt_;                                                                                         \
+  D.sk = sk_;                                                                                           \
+  D.Krow = Krow_;                                                                                       \
+  D.Kcol = Kcol_;                                                                                       \
+  D.K0 = K0_;                                                                                           \
+  D.nnzK = nnzK_;                                                                                       \
+  D.Dinv = Dinv_;                                                                                       \
+  D.bufm = bufm_;                                                                                       \
+  D.cpp = cpp_;                                                                                         \
+  D.cprod = reinterpret_cast<const int2*>(cprod_.p);                                                    \
+  D.Cx = Cx_;                                                                                           \
+  D.nnzC = nnzC_;
 
 void MPCSolver::kkt_diag(double dw, double dc) {
   DV_ARGS;
   k_diag<<<blocks(n_ + m_), NT, 0, stream_>>>(D, dw, dc);
+}
+
+// set_aug_diagonal_reg! + build_kkt! of the chosen formulation (values consumed by the LDL^T)
+void MPCSolver::assemble_kkt(double dw, double dc) {
+  DV_ARGS;
+  kkt_diag(dw, dc);
+  if (kkt_ == KKT_K25) k_k25_scale<<<blocks(nnzK_), NT, 0, stream_>>>(D);
+  if (kkt_ == KKT_NORMAL) k_normal_asm<<<blocks(nnzC_), NT, 0, stream_>>>(D);
+}
+
+const double* MPCSolver::kvals() const { return kkt_ == KKT_NORMAL ? Cx_.p : Kx_.p; }
+
+void MPCSolver::factor_enqueue(double dw, double dc) {
+  assemble_kkt(dw, dc);
+  ldl_->factorize_async(kvals(), stream_);
+}
+
+// MadNLP.solve!(kkt, d) between reduce_rhs! (k_rhs) and finish_aug_solve! (k_residual)
+void MPCSolver::kkt_solve() {
+  DV_ARGS;
+  if (kkt_ == KKT_NORMAL) {
+    k_normal_rhs<<<blocks(m_), NT, 0, stream_>>>(D);
+    ldl_->solve_async(bufm_.p, stream_);
+    k_normal_back<<<blocks(n_ + m_), NT, 0, stream_>>>(D);
+  } else {
+    ldl_->solve_async(d_.p, stream_);
+    if (kkt_ == KKT_K25) k_k25_unscale<<<blocks(n_), NT, 0, stream_>>>(D);
+  }
 }
 
 void MPCSolver::launch_reduce_final(int kind, int nb) {
@@ -1181,7 +1391,7 @@ void MPCSolver::solve_system(int mode, double mu) {
   DV_ARGS;
   const int nb = blocks(n_ + m_);
   k_rhs<<<nb, NT, 0, stream_>>>(D, mode, mu);
-  ldl_->solve_async(d_.p, stream_);
+  kkt_solve();
   k_residual<<<nb, NT, 0, stream_>>>(D, del_w_, del_c_);
   launch_reduce_final(FIN_RESID, nb);
 }
@@ -1232,12 +1442,12 @@ void MPCSolver::read_state() {
 // factorize_system! (solver.jl:299-303) is split: the regularization update is done by the caller.
 void MPCSolver::factorize_regularized() {
   for (int trial = 0; trial < 3; ++trial) {  // linear_solver.jl:6-17
-    kkt_diag(del_w_, del_c_);
+    assemble_kkt(del_w_, del_c_);
     hipEvent_t e0, e1;
     MADIPM_HIP(hipEventCreate(&e0));
     MADIPM_HIP(hipEventCreate(&e1));
     MADIPM_HIP(hipEventRecord(e0, stream_));
-    ldl_->factorize_async(Kx_.p, stream_);
+    ldl_->factorize_async(kvals(), stream_);
     MADIPM_HIP(hipEventRecord(e1, stream_));
     fact_events_.push_back(e0);
     fact_events_.push_back(e1);
@@ -1253,24 +1463,26 @@ void MPCSolver::init_starting_point() {
   const int nb = blocks(n_ + m_), nbn = blocks(n_);
   hipStream_t s = stream_;
   k_init_kkt<<<nb, NT, 0, s>>>(D, del_w_, del_c_);
+  if (kkt_ == KKT_NORMAL) k_normal_asm<<<blocks(nnzC_), NT, 0, s>>>(D);
+  if (kkt_ == KKT_K25) k_k25_scale<<<blocks(nnzK_), NT, 0, s>>>(D);  // s = 1: K2.5 = K2
   hipEvent_t e0, e1;
   MADIPM_HIP(hipEventCreate(&e0));
   MADIPM_HIP(hipEventCreate(&e1));
   MADIPM_HIP(hipEventRecord(e0, s));
-  ldl_->factorize_async(Kx_.p, s);
+  ldl_->factorize_async(kvals(), s);
   MADIPM_HIP(hipEventRecord(e1, s));
   fact_events_.push_back(e0);
   fact_events_.push_back(e1);
   ldl_->status(s);  // init factorization: the reference does not retry here
   // Step 1: least-squares primal correction
   k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_PRIMAL, 0.0);
-  ldl_->solve_async(d_.p, s);
+  kkt_solve();
   k_residual<<<nb, NT, 0, s>>>(D, del_w_, del_c_);
   launch_reduce_final(FIN_RESID, nb);
   k_axpy_x<<<nbn, NT, 0, s>>>(D);
   // Step 2: dual least squares
   k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_DUAL, 0.0);
-  ldl_->solve_async(d_.p, s);
+  kkt_solve();
   k_residual<<<nb, NT, 0, s>>>(D, del_w_, del_c_);
   launch_reduce_final(FIN_RESID, nb);
   k_copy_y<<<blocks(m_), NT, 0, s>>>(D);
@@ -1369,12 +1581,12 @@ int MPCSolver::solve(madipm_stats* stats) {
           del_c_ = adapt_dd_;
       }
       // first trial enqueued together with the state read-back: ONE sync per iteration
-      kkt_diag(del_w_, del_c_);
+      assemble_kkt(del_w_, del_c_);
       hipEvent_t e0, e1;
       MADIPM_HIP(hipEventCreate(&e0));
       MADIPM_HIP(hipEventCreate(&e1));
       MADIPM_HIP(hipEventRecord(e0, s));
-      ldl_->factorize_async(Kx_.p, s);
+      ldl_->factorize_async(kvals(), s);
       MADIPM_HIP(hipEventRecord(e1, s));
       fact_events_.push_back(e0);
       fact_events_.push_back(e1);
@@ -1425,8 +1637,7 @@ int MPCSolver::solve(madipm_stats* stats) {
         for (int trial = 1; trial < 3 && !ok; ++trial) {
           del_w_ *= 100.0;
           del_c_ *= 100.0;
-          kkt_diag(del_w_, del_c_);
-          ldl_->factorize_async(Kx_.p, s);
+          factor_enqueue(del_w_, del_c_);
           ok = ldl_->status(s) == 0;
         }
         if (!ok) {

@@ -63,6 +63,12 @@ class MPCSolver {
   void launch_reduce_final(int kind, int nvals);
   void read_state();
   void kkt_diag(double dw, double dc);
+  // build_kkt!: diagonal (+ K2.5 scaling / normal-matrix assembly) -> values handed to the LDL^T
+  void assemble_kkt(double dw, double dc);
+  const double* kvals() const;
+  // MadNLP.solve!(kkt, d) after the right-hand side is in d_: reduced solve in the chosen formulation
+  void kkt_solve();
+  void factor_enqueue(double dw, double dc);
   int blocks(int64_t n) const;
 
   madipm_options opt_{};
@@ -83,6 +89,12 @@ class MPCSolver {
   DBuf<int32_t> Hci_, Jci_, JTci_;
   DBuf<double> Hv_, Jv_, JTv_;
   DBuf<double> part_;
+  // KKT formulation (0 K2, 1 K2.5, 2 normal equations)
+  int kkt_ = 0;
+  DBuf<double> sk_, K0_, Dinv_, bufm_, Cx_;
+  DBuf<int32_t> Krow_, Kcol_, cprod_;
+  DBuf<int64_t> cpp_;
+  int64_t nnzC_ = 0;
   DBuf<DevState> st_;
   DevState* hst_ = nullptr;
   // host scalars (MPCSolver fields of src/structure.jl:62-76)

@@ -64,10 +64,13 @@ class AdaptiveRegularization:
 class SparseKKTSystem: ...          # K2 (MadNLP.SparseKKTSystem)
 
 
-class ScaledSparseKKTSystem: ...    # K2.5 (not yet implemented on the GPU)
+class ScaledSparseKKTSystem: ...    # K2.5 (MadNLP.ScaledSparseKKTSystem; src/kernels.jl:139-149)
 
 
-class NormalKKTSystem: ...          # src/KKT/normalkkt.jl (not yet implemented on the GPU)
+class NormalKKTSystem: ...          # src/KKT/normalkkt.jl (LPs only; A Sigma^-1 A^T, Cholesky semantics)
+
+
+_KKT_CODES = {SparseKKTSystem: 0, ScaledSparseKKTSystem: 1, NormalKKTSystem: 2}
 
 
 # MadNLP.Status
@@ -199,8 +202,9 @@ def load_options(**kw) -> Options:
     else:
         raise TypeError(f"unsupported step rule {rule!r}")
     kkt = kw.get("kkt_system", SparseKKTSystem)
-    if kkt is not SparseKKTSystem:
-        raise NotImplementedError(f"kkt_system={getattr(kkt, '__name__', kkt)} is not implemented on the GPU yet")
+    if kkt not in _KKT_CODES:
+        raise TypeError(f"unsupported kkt_system {getattr(kkt, '__name__', kkt)!r}")
+    o.kkt_system = _KKT_CODES[kkt]
     ls = kw.get("linear_solver", HIPLDLSolver)
     if ls is not HIPLDLSolver:
         raise NotImplementedError("linear_solver must be HIPLDLSolver (the GPU LDL^T)")

@@ -234,6 +234,7 @@ class OracleMPC:
         self.Hlow = Hl
         self.Hfull = (Hl + Hl.T - sp.diags(Hl.diagonal())).tocsr()
         # MadNLP.initialize!(kkt) [EXT]: reg=1, pr_diag=1, du_diag=0, l/u_lower=0, l/u_diag=1
+        self._k25_init = True
         self.reg = np.ones(n)
         self.pr_diag = np.ones(n)
         self.du_diag = np.zeros(m)
@@ -285,11 +286,57 @@ class OracleMPC:
                           shape=(n + m, n + m)).tocsr()
         return L
 
+    def _aug_A(self):
+        """A with slack columns (m x n): the Jacobian block of K2 / NormalKKTSystem.A
+        (normalkkt.jl:70-80: slack -1 at (ind_ineq[k], nx + k))."""
+        m, n, nx = self.m, self.n, self.nx
+        J = self.Jx.tocoo()
+        rows = np.concatenate([J.row, self.ind_ineq])
+        cols = np.concatenate([J.col, nx + np.arange(self.ns)])
+        vals = np.concatenate([J.data, -np.ones(self.ns)])
+        return sp.coo_matrix((vals, (rows, cols)), shape=(m, n)).tocsr()
+
+    def _k25_scaling(self):
+        """K2.5 (MadNLP.ScaledSparseKKTSystem [EXT], set_aug_diagonal_reg! kernels.jl:139-149):
+        s_i = sqrt((x - xl)(xu - x)) over the bounds present (a missing bound contributes 1)."""
+        s2 = np.ones(self.n)
+        s2[self.ind_lb] *= -self.l_diag          # x - xl  (l_diag = xl - x in the K2 convention)
+        s2[self.ind_ub] *= -self.u_diag          # xu - x
+        return np.sqrt(s2)
+
     def factorize_wrapper(self):
         """MadNLP.factorize_wrapper!: build_kkt! + factorize! timed into linear_solver_time [EXT]."""
         t0 = time.perf_counter()
-        L = self.kkt_matrix()
-        K = (L + L.T - sp.diags(L.diagonal())).tocsc()
+        kind = self.opt.kkt_system
+        if kind == "normal":
+            # NormalKKTSystem.build_kkt! (normalkkt.jl:180-194): C = A Sigma^{-1} A^T, Sigma = pr_diag
+            A = self._aug_A()
+            K = (A @ sp.diags(1.0 / self.pr_diag) @ A.T).tocsc()
+        else:
+            L = self.kkt_matrix()
+            K = (L + L.T - sp.diags(L.diagonal())).tocsc()
+            if kind == "K25" and getattr(self, "_k25_init", False):
+                # init_starting_point! sets pr_diag directly (solver.jl:14-16); the scaling factor
+                # is still the one of MadNLP.initialize!(kkt) (= 1): K2.5 == K2 for this factorization
+                self._k25_s = np.ones(self.n)
+            elif kind == "K25":
+                # S K2 S on the primal block; diagonal s^2 (reg + H_ii) + zl (xu - x) + zu (x - xl)
+                s = self._k25_scaling()
+                self._k25_s = s
+                S = sp.diags(np.concatenate([s, np.ones(self.m)]))
+                K = (S @ K @ S).tolil()
+                dg = s * s * (self.reg + self.Hlow.diagonal())
+                zl = np.zeros(self.n)
+                zu = np.zeros(self.n)
+                zl[self.ind_lb] = self.l_lower
+                zu[self.ind_ub] = self.u_lower
+                dist_l = np.ones(self.n)
+                dist_u = np.ones(self.n)
+                dist_l[self.ind_lb] = -self.l_diag
+                dist_u[self.ind_ub] = -self.u_diag
+                dg = dg + zl * dist_u + zu * dist_l
+                K.setdiag(np.concatenate([dg, self.du_diag]))
+                K = K.tocsc()
         if getattr(self, "linear_solver", "superlu") == "ldl":
             # oracle/ldl_ref.c: LDLFactorizations' up-looking LDL^T (static pivots) in the order
             # `ldl_perm` (default: SuperLU's minimum degree on A+A^T)
@@ -308,14 +355,32 @@ class OracleMPC:
         self.linear_solver_time += time.perf_counter() - t0
 
     def kkt_solve(self, w):
-        """MadNLP.solve!(kkt::SparseKKTSystem, w) [EXT]: reduce_rhs! → solve → finish_aug_solve!."""
+        """MadNLP.solve!(kkt, w) [EXT]: reduce_rhs! → solve → finish_aug_solve!.
+        K2 (SparseKKTSystem), K2.5 (scaled: solve S K S z = S r, d = S z) or the normal equations
+        (normalkkt.jl:196-219)."""
         n, m, nlb = self.n, self.m, self.nlb
         xp = w[:n]
         wl = w[n + m: n + m + nlb]
         wu = w[n + m + nlb:]
         xp[self.ind_lb] -= wl / self.l_diag
         xp[self.ind_ub] -= wu / self.u_diag
-        w[: n + m] = self._lu.solve(w[: n + m])
+        kind = self.opt.kkt_system
+        if kind == "normal":
+            A = self._aug_A()
+            Sig = self.pr_diag
+            wx, wy = w[:n], w[n:n + m]
+            r1 = wx / Sig                       # Sigma^{-1} r1
+            r2 = A @ r1 - wy                    # A Sigma^{-1} r1 - r2
+            dy = self._lu.solve(r2)
+            wy[:] = dy
+            wx[:] = (wx - A.T @ dy) / Sig       # Sigma^{-1} (r1 - A^T dy)
+        elif kind == "K25":
+            s = self._k25_s
+            w[:n] *= s
+            w[: n + m] = self._lu.solve(w[: n + m])
+            w[:n] *= s
+        else:
+            w[: n + m] = self._lu.solve(w[: n + m])
         xp = w[:n]
         wl[:] = (-wl + self.l_lower * xp[self.ind_lb]) / self.l_diag
         wu[:] = (wu - self.u_lower * xp[self.ind_ub]) / self.u_diag
@@ -427,7 +492,9 @@ class OracleMPC:
 
     # ------------------------------------------------------------------ kernels.jl
     def set_aug_diagonal_reg(self):
-        """kernels.jl:124-136 (K2)."""
+        """kernels.jl:124-136 (K2); the K2.5 diagonal (kernels.jl:139-149) is formed from these in
+        factorize_wrapper."""
+        self._k25_init = False
         x = self.x
         self.reg[:] = self.del_w
         self.du_diag[:] = self.del_c

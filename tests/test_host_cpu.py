@@ -138,7 +138,8 @@ def test_scale_qp_equilibrates():
 
 
 def test_options_parsing():
-    from madipm_amd.solver import load_options, FixedRegularization, MehrotraAdaptiveStep, NormalKKTSystem
+    from madipm_amd.solver import (load_options, FixedRegularization, MehrotraAdaptiveStep, NormalKKTSystem,
+                                   ScaledSparseKKTSystem, SparseKKTSystem)
     o = load_options(max_iter=300, regularization=FixedRegularization(1e-8, -1e-8),
                      step_rule=MehrotraAdaptiveStep(0.9), tol=1e-7)
     assert (o.max_iter, o.regularization, o.delta_p, o.delta_d, o.step_rule, o.step_tau, o.tol) == \
@@ -147,8 +148,10 @@ def test_options_parsing():
     assert (d.tol, d.max_iter, d.mu_init, d.mu_min, d.bound_push, d.delta_p) == (1e-8, 3000, 0.1, 1e-12, 1e-2, 1e-10)
     with pytest.raises(TypeError):
         load_options(not_an_option=1)
-    with pytest.raises(NotImplementedError):
-        load_options(kkt_system=NormalKKTSystem)
+    assert [load_options(kkt_system=k).kkt_system for k in (SparseKKTSystem, ScaledSparseKKTSystem, NormalKKTSystem)] \
+        == [0, 1, 2]
+    with pytest.raises(TypeError):
+        load_options(kkt_system=int)
 
 
 @pytest.mark.parametrize("ordering", [3, 4])

@@ -41,6 +41,9 @@ def _oracle_opts(kw):
     for k in ("max_iter", "tol", "max_ncorr"):
         if k in kw:
             o[k] = kw[k]
+    kkt = kw.get("kkt_system")
+    if kkt is not None:
+        o["kkt_system"] = {S.SparseKKTSystem: "K2", S.ScaledSparseKKTSystem: "K25", S.NormalKKTSystem: "normal"}[kkt]
     return OracleOptions(**o)
 
 
@@ -140,3 +143,48 @@ def test_tight_trace(which):
           "random_lp": lambda: random_lp(120, 250, 0.03, 5, ineq_frac=0.3),
           "random_qp": lambda: random_qp(40, 90, 0.08, 6)}[which]()
     _compare(qp, early=3, early_tol=1e-9, regularization=FixedRegularization(1e-4, -1e-4))
+
+
+# ---------------------------------------------------------------- KKT formulations on the GPU
+# K2.5 (ScaledSparseKKTSystem) and NormalKKTSystem (LP only, Cholesky semantics): each vs the
+# oracle of the same formulation, and vs the GPU K2 solution within the reference's 1e-6
+# (test/runtests.jl:107-120, 182-196; test/test_gpu.jl:9-19 runs all three on the GPU).
+def _kkt_cases():
+    import os
+    from madipm_amd import read_mps, simple_lp, standard_form_qp
+    from madipm_amd.instances import random_lp
+    gold = os.path.join(os.path.dirname(__file__), "golden", "afiro.mps")
+    return {"simple_lp": simple_lp, "afiro": lambda: read_mps(gold),
+            "afiro_std": lambda: standard_form_qp(read_mps(gold)),
+            "random_lp": lambda: random_lp(60, 120, 0.05, 0, ineq_frac=0.3, free_frac=0.05)}
+
+
+@pytest.mark.parametrize("kkt_name", ["ScaledSparseKKTSystem", "NormalKKTSystem"])
+@pytest.mark.parametrize("case", ["simple_lp", "afiro", "afiro_std", "random_lp"])
+def test_kkt_formulation_parity(kkt_name, case):
+    from madipm_amd import MPCSolver, FixedRegularization, SparseKKTSystem
+    from madipm_amd import solver as S
+    kkt = getattr(S, kkt_name)
+    qp = _kkt_cases()[case]()
+    kw = dict(regularization=FixedRegularization(1e-8, -1e-8), max_iter=300)
+    gpu, ref = _compare(qp, kkt_system=kkt, **kw)
+    k2 = MPCSolver(qp, kkt_system=SparseKKTSystem, **kw).solve()
+    assert gpu.status == k2.status
+    assert abs(gpu.objective - k2.objective) <= 1e-6 * max(1.0, abs(k2.objective))
+    assert np.max(np.abs(gpu.solution - k2.solution)) <= 1e-6 * max(1.0, np.max(np.abs(k2.solution)))
+    ytol = 1e-6 if case == "simple_lp" else 1e-5  # degenerate dual faces (see test_oracle_cpu)
+    assert np.max(np.abs(gpu.multipliers - k2.multipliers)) <= ytol * max(1.0, np.max(np.abs(k2.multipliers)))
+
+
+def test_k25_qp_parity():
+    from madipm_amd import ScaledSparseKKTSystem, FixedRegularization
+    from madipm_amd.instances import random_qp
+    _compare(random_qp(40, 80, 0.08, 3), kkt_system=ScaledSparseKKTSystem, max_iter=300,
+             regularization=FixedRegularization(1e-8, -1e-8))
+
+
+def test_normal_kkt_rejects_qp():
+    from madipm_amd import MPCSolver, NormalKKTSystem
+    from madipm_amd.instances import random_qp
+    with pytest.raises(Exception, match="only linear programs"):
+        MPCSolver(random_qp(10, 20, 0.2, 0), kkt_system=NormalKKTSystem)

@@ -1,0 +1,15 @@
+#!/bin/bash
+# One GPU validation pass (run on the gpurun box from the repo root):
+#   GPU parity tests -> full bench line (with cpu_baseline) -> rocprofv3 kernel stats of the bench.
+# usage: bash tools/gpu_check.sh TAG [bench args...]
+set -e
+TAG=${1:-check}; shift || true
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+timeout -k 10 600 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1 && echo "gpu tests ok" || { echo "gpu tests FAILED"; tail -30 $OUT/pytest_gpu.log; exit 1; }
+timeout -k 10 300 python bench.py "$@" > $OUT/bench.log 2>&1 && echo "bench ok" || { echo "bench FAILED"; tail -30 $OUT/bench.log; exit 1; }
+tail -1 $OUT/bench.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 bench.py --steps 20 --warmup 2 --no-cpu --no-opt "$@" > $OUT/prof.log 2>&1 && echo "rocprof ok" || { echo "rocprof FAILED"; tail -30 $OUT/prof.log; exit 1; }
+python tools/prof_summary.py $OUT/prof > $OUT/prof_summary.txt 2>&1 || true
+head -25 $OUT/prof_summary.txt
