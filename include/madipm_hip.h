@@ -27,6 +27,7 @@ typedef void* madipm_stream_t; /* hipStream_t */
 int madipm_version(void);                 /* MAJOR*10000 + MINOR*100 + PATCH */
 const char* madipm_last_error(void);
 int madipm_device_count(void);            /* hipGetDeviceCount; 0 when no GPU is present */
+int madipm_set_device(int32_t dev);       /* hipSetDevice for the calling thread (one process per GPU) */
 
 /* ------------------------------------------------------------------ symbolic analysis (host)
  * Replaces the symbolic phase run by the linear-solver constructor `linear_solver(aug_com; opt)`
@@ -38,6 +39,9 @@ typedef struct madipm_ldl_opts {
   int32_t relax;           /* relaxed supernode amalgamation (default 1) */
   int32_t small_front_max; /* fronts with <= this many rows are factorised in LDS (default 128) */
   double pivot_tol;        /* |d| <= pivot_tol  =>  pivot failure (default 0: only 0 / NaN / Inf) */
+  int32_t nshards;         /* > 1: subtree-sharded factorisation with nshards shards on THIS device
+                              (single process, local all-reduce; SURVEY §8 e); default 1.  Across
+                              GPUs use madipm_solver_create_dist / madipm_ldl_analyze_shard. */
 } madipm_ldl_opts;
 
 typedef struct madipm_ldl_info {
@@ -65,6 +69,13 @@ int madipm_symbolic_perm(madipm_symbolic_t sym, int32_t* perm /* n */);
 /* first[nsuper+1], parent[nsuper], nrows[nsuper] (any may be NULL) */
 int madipm_symbolic_supernodes(madipm_symbolic_t sym, int32_t* first, int32_t* parent, int32_t* nrows);
 void madipm_symbolic_destroy(madipm_symbolic_t sym);
+/* symbolic analysis of one shard of a subtree-sharded factorisation (see "subtree sharding" below),
+ * and the partition: owner[nsuper] (-1 top, else shard) and the cost-model totals */
+int madipm_symbolic_analyze_shard(int32_t n, const int64_t* colptr, const int32_t* rowval,
+                                  const madipm_ldl_opts* opts, int32_t nshards, int32_t shard,
+                                  const int32_t* user_perm, madipm_symbolic_t* out);
+int madipm_symbolic_shard_info(madipm_symbolic_t sym, int32_t* owner, double* top_cost, double* shard_cost_max,
+                               double* shard_cost_sum);
 
 /* ------------------------------------------------------------------ LDL^T linear solver (device)
  * The MadNLP.AbstractLinearSolver the reference plugs in through `linear_solver=`
@@ -93,6 +104,41 @@ int madipm_ldl_inertia(madipm_ldl_t ls, int32_t* pos, int32_t* zero, int32_t* ne
 int madipm_ldl_get_d(madipm_ldl_t ls, double* h_d);
 int madipm_ldl_perm(madipm_ldl_t ls, int32_t* perm /* n */);
 void madipm_ldl_destroy(madipm_ldl_t ls);
+
+/* ------------------------------------------------------------------ subtree sharding (SURVEY §8 e)
+ * The north star's multi-GPU mode: the front tree is cut into independent subtrees dealt to
+ * `nshards` shards (one per GPU) plus their common ancestors ("top" fronts), which every shard
+ * factorises redundantly after ONE all-reduce (sum) of the top fronts' external contributions.
+ * A solve needs two more: the top fronts' forward right-hand sides and the final solution.
+ * No reference counterpart (the reference is single-device: cuDSS / LDLFactorizations); these entry
+ * points let a host binding drive the phases with its own collective (e.g. Julia + RCCL.jl):
+ *   factorize: phase 1 -> all-reduce(xbuf, xlen) -> phase 2
+ *   solve:     phase 1 -> all-reduce(xbuf, xlen) -> phase 2 -> all-reduce(x, n)
+ * Shards must be created with the same pattern and options; every shard computes the same cut. */
+int madipm_ldl_analyze_shard(int32_t n, const int64_t* colptr, const int32_t* rowval, const madipm_ldl_opts* opts,
+                             int32_t nshards, int32_t shard, const int32_t* user_perm, madipm_ldl_t* out);
+int madipm_ldl_factorize_phase(madipm_ldl_t ls, int32_t phase /* 1 | 2 */, const double* d_nzval,
+                               madipm_stream_t stream, double** xbuf, int64_t* xlen);
+int madipm_ldl_solve_phase(madipm_ldl_t ls, int32_t phase /* 1 | 2 */, double* d_x, madipm_stream_t stream,
+                           double** xbuf, int64_t* xlen);
+/* owner[s] of every front (-1 top, else shard), and the partition's cost model totals */
+int madipm_ldl_shard_info(madipm_ldl_t ls, int32_t* owner, double* top_cost, double* shard_cost_max,
+                          double* shard_cost_sum);
+/* sum of nbuf device buffers of length n, written back to all of them (single-process shards) */
+int madipm_local_allreduce(double* const* d_bufs, int32_t nbuf, int64_t n, madipm_stream_t stream);
+
+/* RCCL communicator (one process per GPU): rank 0 makes the 128-byte id, the host broadcasts it. */
+typedef struct madipm_comm* madipm_comm_t;
+int madipm_comm_unique_id(void* id128);
+int madipm_comm_create(int32_t nranks, int32_t rank, const void* id128, madipm_comm_t* out);
+/* Host-staged communicator: each all-reduce synchronises the stream, copies the buffer to pinned host
+ * memory, calls fn(host_buf, n, ctx) (which must sum it across ranks in place and return 0) and
+ * copies it back.  For testing the multi-process protocol where RCCL cannot run (ranks sharing a GPU). */
+typedef int (*madipm_allreduce_fn)(double* host_buf, int64_t n, void* ctx);
+int madipm_comm_create_host(int32_t nranks, int32_t rank, madipm_allreduce_fn fn, void* ctx, madipm_comm_t* out);
+/* in-place fp64 sum over the communicator's ranks, ordered on `stream` */
+int madipm_comm_allreduce(madipm_comm_t comm, double* d_buf, int64_t n, madipm_stream_t stream);
+void madipm_comm_destroy(madipm_comm_t comm);
 
 /* Live per-kernel timing (no reference counterpart; measurement for bench.py's roofline).
  * Bit k of `mask` records HIP events around every launch of kernel kind k on the launch stream
@@ -182,6 +228,10 @@ typedef struct madipm_iter_trace {
 typedef struct madipm_solver* madipm_solver_t;
 void madipm_default_options(madipm_options* opt);
 int madipm_solver_create(const madipm_qp* qp, const madipm_options* opt, madipm_solver_t* out);
+/* Sharded across the processes of `comm` (shard = comm rank): every process runs the MPC loop on
+ * replicated vectors; the LDL^T is subtree-sharded with RCCL all-reduces (SURVEY §8 e). */
+int madipm_solver_create_dist(const madipm_qp* qp, const madipm_options* opt, madipm_comm_t comm,
+                              madipm_solver_t* out);
 /* initialize! alone (src/solver.jl:127-189); the next solve() then runs only the MPC loop.
  * Without it, solve() initializes first (as solve! does). */
 int madipm_solver_initialize(madipm_solver_t s);

@@ -46,9 +46,16 @@ struct madipm_solver {
 };
 
 struct madipm_ldl {
-  std::unique_ptr<LDLSolver> s;
+  std::unique_ptr<LDLSolver> own;  // unsharded, or one shard of a cross-process sharded factorisation
+  std::unique_ptr<ShardGroup> g;   // ldl.nshards > 1: all shards on this device
+  LDLSolver* s = nullptr;          // the (first) shard: plan, inertia, status flags
+  LinSolver* lin = nullptr;        // factorize / solve entry
   hipStream_t last_stream = nullptr;
   bool pending = false;
+};
+
+struct madipm_comm {
+  std::unique_ptr<Comm> c;
 };
 
 static SymbolicOptions to_sym_opts(const madipm_ldl_opts* o) {
@@ -59,6 +66,7 @@ static SymbolicOptions to_sym_opts(const madipm_ldl_opts* o) {
     s.relax = o->relax;
     s.small_front_max = o->small_front_max;
   }
+  MADIPM_REQUIRE(!o || (o->nshards >= 1 && o->nshards <= 16), "nshards must be in [1,16]");
   MADIPM_REQUIRE(s.small_front_max >= 1 && s.small_front_max <= 128, "small_front_max must be in [1,128]");
   return s;
 }
@@ -68,6 +76,13 @@ extern "C" {
 int madipm_version(void) { return 100; }
 
 const char* madipm_last_error(void) { return last_error(); }
+
+int madipm_set_device(int32_t dev) {
+  MADIPM_API_BEGIN
+  MADIPM_HIP(hipSetDevice(dev));
+  return 0;
+  MADIPM_API_END
+}
 
 int madipm_device_count(void) {
   int n = 0;
@@ -82,6 +97,7 @@ void madipm_ldl_default_opts(madipm_ldl_opts* o) {
   o->relax = 1;
   o->small_front_max = 128;
   o->pivot_tol = 0.0;
+  o->nshards = 1;
 }
 
 int madipm_symbolic_analyze(int32_t n, const int64_t* colptr, const int32_t* rowval,
@@ -92,6 +108,35 @@ int madipm_symbolic_analyze(int32_t n, const int64_t* colptr, const int32_t* row
   auto s = std::make_unique<madipm_symbolic>();
   symbolic_analyze(n, colptr, rowval, to_sym_opts(opts), user_perm, s->plan);
   *out = s.release();
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_symbolic_analyze_shard(int32_t n, const int64_t* colptr, const int32_t* rowval,
+                                  const madipm_ldl_opts* opts, int32_t nshards, int32_t shard,
+                                  const int32_t* user_perm, madipm_symbolic_t* out) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(out != nullptr && colptr != nullptr, "null argument");
+  SymbolicOptions so = to_sym_opts(opts);
+  so.nshards = nshards;
+  so.shard = shard;
+  auto s = std::make_unique<madipm_symbolic>();
+  symbolic_analyze(n, colptr, rowval, so, user_perm, s->plan);
+  *out = s.release();
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_symbolic_shard_info(madipm_symbolic_t sym, int32_t* owner, double* top_cost, double* shard_cost_max,
+                               double* shard_cost_sum) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(sym, "null handle");
+  const SymbolicPlan& p = sym->plan;
+  if (owner)
+    for (int s = 0; s < p.nsuper; ++s) owner[s] = p.owner.empty() ? 0 : p.owner[s];
+  if (top_cost) *top_cost = p.top_cost;
+  if (shard_cost_max) *shard_cost_max = p.shard_cost_max;
+  if (shard_cost_sum) *shard_cost_sum = p.shard_cost_sum;
   return 0;
   MADIPM_API_END
 }
@@ -144,11 +189,135 @@ int madipm_ldl_analyze(int32_t n, const int64_t* colptr, const int32_t* rowval, 
   madipm_ldl_default_opts(&o);
   if (opts) o = *opts;
   auto ls = std::make_unique<madipm_ldl>();
-  ls->s = std::make_unique<LDLSolver>(n, colptr, rowval, to_sym_opts(&o), o.pivot_tol, user_perm);
+  if (o.nshards > 1) {
+    ls->g = std::make_unique<ShardGroup>(o.nshards, n, colptr, rowval, to_sym_opts(&o), o.pivot_tol, user_perm);
+    ls->s = &ls->g->shard(0);
+    ls->lin = ls->g.get();
+  } else {
+    ls->own = std::make_unique<LDLSolver>(n, colptr, rowval, to_sym_opts(&o), o.pivot_tol, user_perm);
+    ls->s = ls->own.get();
+    ls->lin = ls->s;
+  }
   *out = ls.release();
   return 0;
   MADIPM_API_END
 }
+
+int madipm_ldl_analyze_shard(int32_t n, const int64_t* colptr, const int32_t* rowval, const madipm_ldl_opts* opts,
+                             int32_t nshards, int32_t shard, const int32_t* user_perm, madipm_ldl_t* out) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(out != nullptr && colptr != nullptr, "null argument");
+  madipm_ldl_opts o;
+  madipm_ldl_default_opts(&o);
+  if (opts) o = *opts;
+  o.nshards = 1;
+  SymbolicOptions so = to_sym_opts(&o);
+  so.nshards = nshards;
+  so.shard = shard;
+  auto ls = std::make_unique<madipm_ldl>();
+  ls->own = std::make_unique<LDLSolver>(n, colptr, rowval, so, o.pivot_tol, user_perm);
+  ls->s = ls->own.get();
+  ls->lin = ls->s;
+  *out = ls.release();
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_ldl_factorize_phase(madipm_ldl_t ls, int32_t phase, const double* d_nzval, madipm_stream_t stream,
+                               double** xbuf, int64_t* xlen) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(ls && ls->own && (phase == 1 || phase == 2), "bad argument");
+  hipStream_t st = (hipStream_t)stream;
+  if (phase == 1) {
+    ls->s->fact_phase1(d_nzval, st);
+    if (xbuf) *xbuf = ls->s->fact_xbuf();
+    if (xlen) *xlen = ls->s->fact_xlen();
+  } else {
+    ls->s->fact_phase2(st);
+    ls->last_stream = st;
+    ls->pending = true;
+  }
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_ldl_solve_phase(madipm_ldl_t ls, int32_t phase, double* d_x, madipm_stream_t stream, double** xbuf,
+                           int64_t* xlen) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(ls && ls->own && (phase == 1 || phase == 2) && d_x, "bad argument");
+  hipStream_t st = (hipStream_t)stream;
+  if (phase == 1) {
+    ls->s->solve_phase1(d_x, st);
+    if (xbuf) *xbuf = ls->s->solve_xbuf();
+    if (xlen) *xlen = ls->s->solve_xlen();
+  } else {
+    ls->s->solve_phase2(d_x, st);
+    if (xbuf) *xbuf = d_x;
+    if (xlen) *xlen = ls->s->sharded() ? ls->s->n() : 0;
+  }
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_ldl_shard_info(madipm_ldl_t ls, int32_t* owner /* nsuper, may be NULL */, double* top_cost,
+                          double* shard_cost_max, double* shard_cost_sum) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(ls, "null handle");
+  const SymbolicPlan& p = ls->s->plan();
+  if (owner) {
+    for (int s = 0; s < p.nsuper; ++s) owner[s] = p.owner.empty() ? 0 : p.owner[s];
+  }
+  if (top_cost) *top_cost = p.top_cost;
+  if (shard_cost_max) *shard_cost_max = p.shard_cost_max;
+  if (shard_cost_sum) *shard_cost_sum = p.shard_cost_sum;
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_local_allreduce(double* const* d_bufs, int32_t nbuf, int64_t n, madipm_stream_t stream) {
+  MADIPM_API_BEGIN
+  local_allreduce(d_bufs, nbuf, n, (hipStream_t)stream);
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_comm_unique_id(void* id128) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(id128, "null argument");
+  rccl_unique_id(id128);
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_comm_create(int32_t nranks, int32_t rank, const void* id128, madipm_comm_t* out) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(out && id128, "null argument");
+  auto c = std::make_unique<madipm_comm>();
+  c->c.reset(make_rccl_comm(nranks, rank, id128));
+  *out = c.release();
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_comm_create_host(int32_t nranks, int32_t rank, madipm_allreduce_fn fn, void* ctx, madipm_comm_t* out) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(out && fn, "null argument");
+  auto c = std::make_unique<madipm_comm>();
+  c->c.reset(make_host_comm(nranks, rank, fn, ctx));
+  *out = c.release();
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_comm_allreduce(madipm_comm_t c, double* d_buf, int64_t n, madipm_stream_t stream) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(c && (d_buf || n == 0), "null argument");
+  c->c->allreduce_sum(d_buf, n, (hipStream_t)stream);
+  return 0;
+  MADIPM_API_END
+}
+
+void madipm_comm_destroy(madipm_comm_t c) { delete c; }
 
 int madipm_ldl_get_info(madipm_ldl_t ls, madipm_ldl_info* info) {
   MADIPM_API_BEGIN
@@ -171,7 +340,7 @@ int madipm_ldl_get_info(madipm_ldl_t ls, madipm_ldl_info* info) {
 int madipm_ldl_factorize_async(madipm_ldl_t ls, const double* d_nzval, madipm_stream_t stream) {
   MADIPM_API_BEGIN
   MADIPM_REQUIRE(ls, "null handle");
-  ls->s->factorize_async(d_nzval, (hipStream_t)stream);
+  ls->lin->factorize_async(d_nzval, (hipStream_t)stream);
   ls->last_stream = (hipStream_t)stream;
   ls->pending = true;
   return 0;
@@ -181,9 +350,9 @@ int madipm_ldl_factorize_async(madipm_ldl_t ls, const double* d_nzval, madipm_st
 int madipm_ldl_factorize(madipm_ldl_t ls, const double* d_nzval, madipm_stream_t stream) {
   MADIPM_API_BEGIN
   MADIPM_REQUIRE(ls, "null handle");
-  ls->s->factorize_async(d_nzval, (hipStream_t)stream);
+  ls->lin->factorize_async(d_nzval, (hipStream_t)stream);
   ls->pending = false;
-  return ls->s->status((hipStream_t)stream);
+  return ls->lin->status((hipStream_t)stream);
   MADIPM_API_END
 }
 
@@ -191,7 +360,7 @@ int madipm_ldl_is_factorized(madipm_ldl_t ls) {
   MADIPM_API_BEGIN
   MADIPM_REQUIRE(ls, "null handle");
   if (ls->pending) {
-    ls->s->status(ls->last_stream);
+    ls->lin->status(ls->last_stream);
     ls->pending = false;
   }
   return ls->s->factorized ? 1 : 0;
@@ -201,7 +370,7 @@ int madipm_ldl_is_factorized(madipm_ldl_t ls) {
 int madipm_ldl_solve(madipm_ldl_t ls, double* d_x, int32_t nrhs, madipm_stream_t stream) {
   MADIPM_API_BEGIN
   MADIPM_REQUIRE(ls && (d_x || ls->s->n() == 0), "null argument");
-  for (int k = 0; k < nrhs; ++k) ls->s->solve_async(d_x + (int64_t)k * ls->s->n(), (hipStream_t)stream);
+  for (int k = 0; k < nrhs; ++k) ls->lin->solve_async(d_x + (int64_t)k * ls->s->n(), (hipStream_t)stream);
   return 0;
   MADIPM_API_END
 }
@@ -210,7 +379,7 @@ int madipm_ldl_inertia(madipm_ldl_t ls, int32_t* pos, int32_t* zero, int32_t* ne
   MADIPM_API_BEGIN
   MADIPM_REQUIRE(ls, "null handle");
   if (ls->pending) {
-    ls->s->status(ls->last_stream);
+    ls->lin->status(ls->last_stream);
     ls->pending = false;
   }
   if (pos) *pos = ls->s->npos;
@@ -225,6 +394,16 @@ int madipm_ldl_get_d(madipm_ldl_t ls, double* h_d) {
   MADIPM_REQUIRE(ls && h_d, "null argument");
   MADIPM_HIP(hipDeviceSynchronize());
   MADIPM_HIP(hipMemcpy(h_d, ls->s->d_diag(), sizeof(double) * ls->s->n(), hipMemcpyDeviceToHost));
+  if (ls->g) {  // sharded on this device: each column's pivot from a shard that computed it
+    const SymbolicPlan& p = ls->s->plan();
+    std::vector<double> tmp(ls->s->n());
+    for (int r = 1; r < ls->g->nshards(); ++r) {
+      MADIPM_HIP(hipMemcpy(tmp.data(), ls->g->shard(r).d_diag(), sizeof(double) * tmp.size(), hipMemcpyDeviceToHost));
+      for (int f = 0; f < p.nsuper; ++f)
+        if (p.owner[f] == r)
+          for (int j = p.first[f]; j < p.first[f + 1]; ++j) h_d[j] = tmp[j];
+    }
+  }
   return 0;
   MADIPM_API_END
 }
@@ -239,7 +418,7 @@ int madipm_ldl_perm(madipm_ldl_t ls, int32_t* perm) {
 
 void madipm_ldl_destroy(madipm_ldl_t ls) { delete ls; }
 
-static void fill_kstats(LDLSolver& l, madipm_kstat* out) {
+static void fill_kstats(LinSolver& l, madipm_kstat* out) {
   static_assert(MADIPM_NKERNELS == KK_COUNT, "kernel kinds");
   KernelStat st[KK_COUNT];
   l.kernel_stats(st);
@@ -306,6 +485,22 @@ int madipm_solver_create(const madipm_qp* qp, const madipm_options* opt, madipm_
   MADIPM_REQUIRE(o.kkt_system >= 0 && o.kkt_system <= 2, "kkt_system must be 0 (K2), 1 (K2.5) or 2 (normal equations)");
   auto s = std::make_unique<madipm_solver>();
   s->s = std::make_unique<MPCSolver>(*qp, o);
+  *out = s.release();
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_solver_create_dist(const madipm_qp* qp, const madipm_options* opt, madipm_comm_t comm,
+                              madipm_solver_t* out) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(qp && out && comm, "null argument");
+  madipm_options o;
+  madipm_default_options(&o);
+  if (opt) o = *opt;
+  MADIPM_REQUIRE(o.kkt_system >= 0 && o.kkt_system <= 2, "kkt_system must be 0 (K2), 1 (K2.5) or 2 (normal equations)");
+  o.ldl.nshards = 1;
+  auto s = std::make_unique<madipm_solver>();
+  s->s = std::make_unique<MPCSolver>(*qp, o, comm->c.get());
   *out = s.release();
   return 0;
   MADIPM_API_END

@@ -56,6 +56,14 @@ __device__ __forceinline__ int64_t lower_bound_dev(const T* a, int64_t lo, int64
   return lo;
 }
 
+// initial forward value of row i of front s: own right-hand side entry, or (sharded top fronts) the
+// exchanged sum of b and the other shards' subtree updates
+__device__ __forceinline__ double fwd_init(const FrontTab& T, int s, int i, int w, int f0, const double* __restrict__ b) {
+  const int64_t xo = T.xoff[s];
+  if (xo >= 0) return T.xch[xo + i];
+  return (i < w) ? b[T.perm[f0 + i]] : 0.0;
+}
+
 __global__ void k_status_init(LDLStatus* st) {
   st->fail_pivot = INT_MAX;
   st->npos = st->nneg = st->nzero = 0;
@@ -253,7 +261,8 @@ __global__ __launch_bounds__(ANT) void k_assemble(FrontTab T, const SymbolicPlan
                                                   double* __restrict__ fscratch) {
   __shared__ double Ft[64 * 64];
   const SymbolicPlan::AsmTile tl = tiles[blockIdx.x];
-  const int s = tl.front, ti = tl.tij & 0xffff, tj = tl.tij >> 16;
+  const int s = tl.front, ti = tl.tij & 0xffff, tj = (tl.tij >> 16) & 0x7fff;
+  const bool acc = tl.tij < 0;  // SymbolicPlan::kAccumulate: F += tile (sharded top fronts, phase 2)
   const int r = T.nrows[s];
   const int I0 = ti * 64, J0 = tj * 64;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -308,7 +317,10 @@ __global__ __launch_bounds__(ANT) void k_assemble(FrontTab T, const SymbolicPlan
   const int i = I0 + lane;
   for (int jj = wv; jj < 64; jj += ANT / 64) {
     const int j = J0 + jj;
-    if (i < r && j < r && i >= j) F[i + (int64_t)j * r] = Ft[lane + jj * 64];
+    if (i < r && j < r && i >= j) {
+      const int64_t q = i + (int64_t)j * r;
+      F[q] = acc ? F[q] + Ft[lane + jj * 64] : Ft[lane + jj * 64];
+    }
   }
 }
 
@@ -609,10 +621,13 @@ __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __
       }
 }
 
-__global__ __launch_bounds__(NT) void k_inertia(const double* __restrict__ D, int n, LDLStatus* st, int spd) {
+// (pos, neg, zero) of D over the columns with colmask == want (colmask NULL: all)
+__global__ __launch_bounds__(NT) void k_inertia(const double* __restrict__ D, int n, LDLStatus* st, int spd,
+                                                const uint8_t* __restrict__ colmask, int want) {
   __shared__ int red[3][NT / 64];
   int pos = 0, neg = 0, zero = 0;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    if (colmask && colmask[i] != want) continue;
     const double d = D[i];
     pos += d > 0.0;
     neg += d < 0.0;
@@ -677,7 +692,7 @@ __global__ __launch_bounds__(NT) void k_fwd_small(FrontTab T, const int32_t* __r
     const int i = lane + 64 * h;
     double vi = 0.0;
     if (i < r) {
-      vi = (i < w) ? b[T.perm[f0 + i]] : 0.0;
+      vi = fwd_init(T, s, i, w, f0, b);
       const int64_t e = T.row_ptr[s] + i;
       const int64_t p1 = T.sv_ptr[e + 1];
       for (int64_t p = T.sv_ptr[e]; p < p1; ++p) vi += uvec[T.sv_src[p]];
@@ -815,7 +830,7 @@ __global__ __launch_bounds__(NT) void k_bwd_small(FrontTab T, const int32_t* __r
     const int j = lane + 64 * h;
     if (j < w) {
       xi[f0 + j] = v[h];
-      out[T.perm[f0 + j]] = v[h];
+      if (T.wout[s]) out[T.perm[f0 + j]] = v[h];
     }
   }
 }
@@ -833,7 +848,7 @@ __global__ __launch_bounds__(NT) void k_fwd_tiny(FrontTab T, const int32_t* __re
   const double* __restrict__ L = arena + T.l_off[s];
   double v = 0.0;
   if (lr < r) {
-    v = (lr < w) ? b[T.perm[f0 + lr]] : 0.0;
+    v = fwd_init(T, s, lr, w, f0, b);
     const int64_t e = T.row_ptr[s] + lr;
     const int64_t p1 = T.sv_ptr[e + 1];
     for (int64_t p = T.sv_ptr[e]; p < p1; ++p) v += uvec[T.sv_src[p]];
@@ -899,7 +914,7 @@ __global__ __launch_bounds__(NT) void k_bwd_tiny(FrontTab T, const int32_t* __re
   }
   if (live && lr < w) {
     xi[f0 + lr] = v;
-    out[T.perm[f0 + lr]] = v;
+    if (T.wout[s]) out[T.perm[f0 + lr]] = v;
   }
 }
 
@@ -913,7 +928,7 @@ __global__ __launch_bounds__(NT) void k_fwd_gather(FrontTab T, const int32_t* __
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
   const int i = chunk * NT + threadIdx.x;
   if (i >= r) return;
-  double vi = (i < w) ? b[T.perm[f0 + i]] : 0.0;
+  double vi = fwd_init(T, s, i, w, f0, b);
   const int64_t e = T.row_ptr[s] + i;
   const int64_t p1 = T.sv_ptr[e + 1];
   for (int64_t p = T.sv_ptr[e]; p < p1; ++p) vi += uvec[T.sv_src[p]];
@@ -1114,11 +1129,65 @@ __global__ __launch_bounds__(NT) void k_bwd_big(FrontTab T, const SolveTask* __r
       if (lane < kw) {
         const int c = f0 + c0 + lane;
         xi[c] = a;
-        out[T.perm[c]] = a;
+        if (T.wout[s]) out[T.perm[c]] = a;
       }
       publish_flag(&flags[flag_off[s] + p], epoch);
     }
     __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------ sharding (SURVEY §8 e)
+// External forward contribution of the top fronts: task = (top front, 256-row chunk); xch[xoff + i] =
+// (shard 0: own right-hand side entry) + this shard's subtree-root update vectors, child order.
+__global__ __launch_bounds__(NT) void k_ext_gather(FrontTab T, const int32_t* __restrict__ list, int shard0,
+                                                   const int64_t* __restrict__ sx_ptr, const int64_t* __restrict__ sx_src,
+                                                   const double* __restrict__ b, const double* __restrict__ uvec,
+                                                   double* __restrict__ xch) {
+  int s, chunk;
+  task_of(list, s, chunk);
+  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+  const int i = chunk * NT + threadIdx.x;
+  if (i >= r) return;
+  const int64_t e = T.xoff[s] + i;
+  double v = (shard0 && i < w) ? b[T.perm[f0 + i]] : 0.0;
+  for (int64_t p = sx_ptr[e]; p < sx_ptr[e + 1]; ++p) v += uvec[sx_src[p]];
+  xch[e] = v;
+}
+
+// status of this shard's subtrees -> its slot (other slots 0), all-reduced with the top fronts
+__global__ void k_pack_status(const LDLStatus* st, double* slots, int shard, int nshards) {
+  const int q = threadIdx.x;
+  if (q >= nshards) return;
+  const bool me = q == shard;
+  slots[4 * q + 0] = me ? (double)st->fail_pivot : 0.0;
+  slots[4 * q + 1] = me ? (double)st->npos : 0.0;
+  slots[4 * q + 2] = me ? (double)st->nneg : 0.0;
+  slots[4 * q + 3] = me ? (double)st->nzero : 0.0;
+}
+
+__global__ void k_unpack_status(LDLStatus* st, const double* slots, int nshards) {
+  double f = (double)INT_MAX, p = 0, ng = 0, z = 0;
+  for (int q = 0; q < nshards; ++q) {
+    f = fmin(f, slots[4 * q]);
+    p += slots[4 * q + 1];
+    ng += slots[4 * q + 2];
+    z += slots[4 * q + 3];
+  }
+  st->fail_pivot = (int)f;
+  st->npos = (int)p;
+  st->nneg = (int)ng;
+  st->nzero = (int)z;
+}
+
+struct BufList {
+  double* p[16];
+};
+__global__ __launch_bounds__(NT) void k_local_allreduce(BufList B, int nbuf, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+    double v = 0.0;
+    for (int q = 0; q < nbuf; ++q) v += B.p[q][i];
+    for (int q = 0; q < nbuf; ++q) B.p[q][i] = v;
   }
 }
 
@@ -1127,10 +1196,12 @@ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 }  // namespace
 
 LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const SymbolicOptions& sopt,
-                     double ptol, const int32_t* user_perm)
-    : pivot_tol(ptol) {
+                     double ptol, const int32_t* user_perm, Comm* comm)
+    : pivot_tol(ptol), comm_(comm) {
   symbolic_analyze(n, colptr, rowval, sopt, user_perm, S_);
   const SymbolicPlan& S = S_;
+  MADIPM_REQUIRE(S.nshards == 1 || comm == nullptr || (comm->size == S.nshards && comm->rank == S.shard),
+                 "communicator does not match the shard layout");
   first_.upload(S.first);
   nrows_.upload(S.nrows);
   row_ptr_.upload(S.row_ptr);
@@ -1176,102 +1247,135 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   T_.fs_off = fs_off_;
   T_.sv_ptr = sv_ptr_;
   T_.sv_src = sv_src_;
+  const int ns = S.nsuper, NL = S.nlevels;
   {
-    std::vector<int32_t> slot(std::max(S.nsuper, 1), -1);
+    std::vector<int32_t> slot(std::max(ns, 1), -1);
     int nslot = 0;
-    for (int s = 0; s < S.nsuper; ++s)
+    for (int s = 0; s < ns; ++s)
       if (S.is_big[s]) slot[s] = nslot++;
     bigslot_.upload(slot);
     minv_.alloc((int64_t)std::max(nslot, 1) * 4096);
     T_.bigslot = bigslot_;
   }
+  // sharding tables (unsharded: xoff = -1, every x written, every column counted)
+  {
+    std::vector<int64_t> xo(std::max(ns, 1), -1);
+    std::vector<uint8_t> wo(std::max(ns, 1), 1), cm(std::max(S.N, 1), 1);
+    if (S.nshards > 1)
+      for (int s = 0; s < ns; ++s) {
+        xo[s] = S.xoff[s];
+        wo[s] = S.top(s) ? (S.shard == 0) : 1;
+        for (int j = S.first[s]; j < S.first[s + 1]; ++j) cm[j] = S.top(s) ? 2 : (S.mine(s) ? 1 : 0);
+      }
+    xoff_.upload(xo);
+    wout_.upload(wo);
+    colmask_.upload(cm);
+    xch_.alloc(std::max<int64_t>(S.xlen, 1));
+    sx_ptr_.upload(S.sx_ptr.empty() ? std::vector<int64_t>{0} : S.sx_ptr);
+    sx_src_.upload(S.sx_src.empty() ? std::vector<int64_t>{0} : S.sx_src);
+    T_.xoff = xoff_;
+    T_.xch = xch_;
+    T_.wout = wout_;
+  }
+  auto in_phase = [&](int s, int phase) { return phase == 1 ? (!S.top(s) && S.mine(s)) : S.top(s); };
 
-  // ---- launch schedule
+  // ---- factorisation launch schedules (phase 1: this shard's subtrees; phase 2: the top fronts)
   std::vector<int32_t> sched;
-  const int ns = S.nsuper;
   auto align2 = [&]() {
     if (sched.size() & 1) sched.push_back(0);
   };
-  for (int lev = 0; lev < S.nlevels; ++lev) {
-    if (S.atile_lev[lev + 1] > S.atile_lev[lev]) {
-      Launch L{ASSEMBLE, 0, S.atile_lev[lev], 0, S.atile_lev[lev + 1] - S.atile_lev[lev], S.chunk_lev[lev],
-               S.chunk_lev[lev + 1] - S.chunk_lev[lev]};
-      // algorithmic traffic: chunk pass reads (index, value) per source, writes one partial per chunk;
-      // the tile pass reads the entry offsets + partials (+ big-children blocks), writes the lower tile
-      const int64_t nsrc = S.g_chunk[S.chunk_lev[lev + 1]] - S.g_chunk[S.chunk_lev[lev]];
-      L.bytes2 = 16.0 * nsrc + 16.0 * L.nchunk;
-      L.flops2 = (double)nsrc;
-      for (int32_t t = S.atile_lev[lev]; t < S.atile_lev[lev + 1]; ++t) {
-        const SymbolicPlan::AsmTile& at = S.atiles[t];
-        const int r = S.nrows[at.front], ti = at.tij & 0xffff, tj = at.tij >> 16;
-        const double nr = std::min(64, r - 64 * ti), nc = std::min(64, r - 64 * tj);
-        L.bytes += 8.0 * (ti == tj ? nr * (nr + 1) / 2 : nr * nc) + (at.gptr >= 0 ? 4.0 * 4097 : 0.0);
-        for (int k = at.bt0; k < at.bt1; ++k) {
-          const int32_t* e = &S.bt[5 * k];
-          for (int b = e[1]; b < e[2]; ++b) L.bytes += 8.0 * std::max(0, e[4] - std::max(b, e[3]));
+  auto asm_launch = [&](int g, std::vector<Launch>& out) {
+    if (S.atile_lev[g + 1] <= S.atile_lev[g]) return;
+    Launch L{ASSEMBLE, 0, S.atile_lev[g], 0, S.atile_lev[g + 1] - S.atile_lev[g], S.chunk_lev[g],
+             S.chunk_lev[g + 1] - S.chunk_lev[g]};
+    // algorithmic traffic: chunk pass reads (index, value) per source, writes one partial per chunk;
+    // the tile pass reads the entry offsets + partials (+ big-children blocks), writes the lower tile
+    const int64_t nsrc = S.g_chunk[S.chunk_lev[g + 1]] - S.g_chunk[S.chunk_lev[g]];
+    L.bytes2 = 16.0 * nsrc + 16.0 * L.nchunk;
+    L.flops2 = (double)nsrc;
+    for (int32_t t = S.atile_lev[g]; t < S.atile_lev[g + 1]; ++t) {
+      const SymbolicPlan::AsmTile& at = S.atiles[t];
+      const int r = S.nrows[at.front], ti = at.tij & 0xffff, tj = (at.tij >> 16) & 0x7fff;
+      const double nr = std::min(64, r - 64 * ti), nc = std::min(64, r - 64 * tj);
+      L.bytes += 8.0 * (ti == tj ? nr * (nr + 1) / 2 : nr * nc) * (at.tij < 0 ? 2.0 : 1.0) +
+                 (at.gptr >= 0 ? 4.0 * 4097 : 0.0);
+      for (int k = at.bt0; k < at.bt1; ++k) {
+        const int32_t* e = &S.bt[5 * k];
+        for (int b = e[1]; b < e[2]; ++b) L.bytes += 8.0 * std::max(0, e[4] - std::max(b, e[3]));
+      }
+    }
+    L.bytes += 8.0 * L.nchunk;
+    out.push_back(L);
+  };
+  auto build_fact = [&](int phase, std::vector<Launch>& out) {
+    for (int lev = 0; lev < NL; ++lev) {
+      asm_launch(phase == 1 ? lev : NL + 1 + lev, out);
+      std::vector<int32_t> cls[3], big;
+      for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
+        const int s = S.level_list[q];
+        if (!in_phase(s, phase)) continue;
+        const int r = S.nrows[s];
+        if (!S.is_big[s])
+          cls[r <= 32 ? 0 : (r <= 64 ? 1 : 2)].push_back(s);
+        else
+          big.push_back(s);
+      }
+      for (int c = 0; c < 3; ++c)
+        if (!cls[c].empty()) {
+          Launch L{SMALL32 + c, 0, (int64_t)sched.size(), (int)cls[c].size(), (int64_t)cls[c].size()};
+          for (int f : cls[c]) {  // reads: K entries or the assembled front; writes: L panel, U block, D
+            const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
+            L.bytes += 8.0 * (r * w + (r - w) * (r - w) + w) +
+                       (S.fs_off[f] >= 0 ? 8.0 * r * (r + 1) / 2 : 16.0 * (S.asm_ptr[f + 1] - S.asm_ptr[f]));
+            for (int t = 0; t < (int)w; ++t) L.flops += (r - t - 1) * (r - t);
+          }
+          out.push_back(L);
+          sched.insert(sched.end(), cls[c].begin(), cls[c].end());
+        }
+      if (big.empty()) continue;
+      int maxsteps = 0;
+      for (int s : big) maxsteps = std::max<int>(maxsteps, (int)cdiv(S.first[s + 1] - S.first[s], 64));
+      for (int p = 0; p < maxsteps; ++p) {
+        std::vector<int32_t> td, tt, tu;  // (front, item) pairs
+        double kb[3] = {0, 0, 0}, kf[3] = {0, 0, 0};
+        for (int s : big) {
+          const int w = S.first[s + 1] - S.first[s], r = S.nrows[s];
+          if (cdiv(w, 64) <= p) continue;
+          const int k0 = p * 64, kw = std::min(64, w - k0);
+          const int nt = (int)cdiv(r - k0 - kw, 64);
+          const double dk = kw, nb = r - k0 - kw;
+          kb[0] += 8.0 * (dk * (dk + 1) + 4 * 16 * 17);  // diag: read + write lower, write the M blocks
+          kf[0] += dk * dk * dk / 3.0;
+          kb[1] += 8.0 * (2.0 * nb * dk + nt * (dk * (dk + 1) / 2 + 4 * 16 * 17));  // trsm: rows in/out + L11, M per tile
+          kf[1] += nb * dk * dk;
+          kb[2] += 8.0 * (nb * (nb + 1) + 2.0 * nb * dk);  // update: C in/out + the panel once
+          kf[2] += dk * nb * (nb + 1);
+          td.insert(td.end(), {s, 0});
+          for (int i = 0; i < nt; ++i) tt.insert(tt.end(), {s, i});
+          for (int i = 0; i < nt; ++i)
+            for (int j = 0; j <= i; ++j) tu.insert(tu.end(), {s, i | (j << 16)});
+        }
+        const std::pair<int, std::vector<int32_t>*> kinds[3] = {{BIG_DIAG, &td}, {BIG_TRSM, &tt}, {BIG_UPDATE, &tu}};
+        for (int q = 0; q < 3; ++q) {
+          const auto& kv = kinds[q];
+          if (kv.second->empty()) continue;
+          align2();
+          Launch L{kv.first, p, (int64_t)sched.size(), 0, (int64_t)kv.second->size() / 2};
+          L.bytes = kb[q];
+          L.flops = kf[q];
+          out.push_back(L);
+          sched.insert(sched.end(), kv.second->begin(), kv.second->end());
         }
       }
-      L.bytes += 8.0 * L.nchunk;
-      fact_.push_back(L);
     }
-    std::vector<int32_t> cls[3], big;
-    for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
-      const int s = S.level_list[q];
-      const int r = S.nrows[s];
-      if (!S.is_big[s])
-        cls[r <= 32 ? 0 : (r <= 64 ? 1 : 2)].push_back(s);
-      else
-        big.push_back(s);
-    }
-    for (int c = 0; c < 3; ++c)
-      if (!cls[c].empty()) {
-        Launch L{SMALL32 + c, 0, (int64_t)sched.size(), (int)cls[c].size(), (int64_t)cls[c].size()};
-        for (int f : cls[c]) {  // reads: K entries or the assembled front; writes: L panel, U block, D
-          const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
-          L.bytes += 8.0 * (r * w + (r - w) * (r - w) + w) +
-                     (S.fs_off[f] >= 0 ? 8.0 * r * (r + 1) / 2 : 16.0 * (S.asm_ptr[f + 1] - S.asm_ptr[f]));
-          for (int t = 0; t < (int)w; ++t) L.flops += (r - t - 1) * (r - t);
-        }
-        fact_.push_back(L);
-        sched.insert(sched.end(), cls[c].begin(), cls[c].end());
-      }
-    if (big.empty()) continue;
-    int maxsteps = 0;
-    for (int s : big) maxsteps = std::max<int>(maxsteps, (int)cdiv(S.first[s + 1] - S.first[s], 64));
-    for (int p = 0; p < maxsteps; ++p) {
-      std::vector<int32_t> td, tt, tu;  // (front, item) pairs
-      double kb[3] = {0, 0, 0}, kf[3] = {0, 0, 0};
-      for (int s : big) {
-        const int w = S.first[s + 1] - S.first[s], r = S.nrows[s];
-        if (cdiv(w, 64) <= p) continue;
-        const int k0 = p * 64, kw = std::min(64, w - k0);
-        const int nt = (int)cdiv(r - k0 - kw, 64);
-        const double dk = kw, nb = r - k0 - kw;
-        kb[0] += 8.0 * (dk * (dk + 1) + 4 * 16 * 17);  // diag: read + write lower, write the M blocks
-        kf[0] += dk * dk * dk / 3.0;
-        kb[1] += 8.0 * (2.0 * nb * dk + nt * (dk * (dk + 1) / 2 + 4 * 16 * 17));  // trsm: rows in/out + L11, M per tile
-        kf[1] += nb * dk * dk;
-        kb[2] += 8.0 * (nb * (nb + 1) + 2.0 * nb * dk);  // update: C in/out + the panel once
-        kf[2] += dk * nb * (nb + 1);
-        td.insert(td.end(), {s, 0});
-        for (int i = 0; i < nt; ++i) tt.insert(tt.end(), {s, i});
-        for (int i = 0; i < nt; ++i)
-          for (int j = 0; j <= i; ++j) tu.insert(tu.end(), {s, i | (j << 16)});
-      }
-      const std::pair<int, std::vector<int32_t>*> kinds[3] = {{BIG_DIAG, &td}, {BIG_TRSM, &tt}, {BIG_UPDATE, &tu}};
-      for (int q = 0; q < 3; ++q) {
-        const auto& kv = kinds[q];
-        if (kv.second->empty()) continue;
-        align2();
-        Launch L{kv.first, p, (int64_t)sched.size(), 0, (int64_t)kv.second->size() / 2};
-        L.bytes = kb[q];
-        L.flops = kf[q];
-        fact_.push_back(L);
-        sched.insert(sched.end(), kv.second->begin(), kv.second->end());
-      }
-    }
+  };
+  build_fact(1, fact1_);
+  if (S.nshards > 1) {
+    asm_launch(NL, fact1_);  // top fronts, external part (all-reduced next)
+    build_fact(2, fact2_);
   }
-  // ---- solve schedule: per level, small fronts (wave per front) and big fronts (task queues)
+
+  // ---- solve schedules: per level, small fronts (wave per front) and big fronts (task queues)
   {
     std::vector<int32_t> flag_off(ns, 0);
     int64_t nflags = 0;
@@ -1282,93 +1386,108 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       }
     std::vector<int32_t> tasks, bp_off(ns, 0);
     int64_t nbpart = 0;
-    for (int lev = 0; lev < S.nlevels; ++lev) {
-      std::vector<int32_t> tiny, small, big;
-      for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
-        const int s = S.level_list[q];
-        (S.nrows[s] > 128 ? big : (S.nrows[s] > 32 ? small : tiny)).push_back(s);
-      }
-      SolveLevel L{};
-      L.tiny_off = (int64_t)sched.size();
-      L.ntiny = (int)tiny.size();
-      sched.insert(sched.end(), tiny.begin(), tiny.end());
-      L.small_off = (int64_t)sched.size();
-      L.nsmall = (int)small.size();
-      sched.insert(sched.end(), small.begin(), small.end());
-      L.big_off = (int64_t)sched.size();
-      L.nbig = (int)big.size();
-      sched.insert(sched.end(), big.begin(), big.end());
-      align2();
-      L.gat_off = (int64_t)sched.size();
-      for (int s : big)
-        for (int c = 0; c < cdiv(S.nrows[s], NT); ++c) sched.insert(sched.end(), {s, c});
-      L.ngat = (int)(((int64_t)sched.size() - L.gat_off) / 2);
-      L.below_off = (int64_t)sched.size();
-      for (int s : big) {
-        const int w = S.first[s + 1] - S.first[s], r = S.nrows[s];
-        if (r == w) continue;
-        const int np = (int)cdiv(w, 64), nch = (int)cdiv(r - w, BWD_CHUNK);
-        bp_off[s] = (int32_t)nbpart;
-        nbpart += (int64_t)np * nch;
-        for (int p = 0; p < np; ++p)
-          for (int c = 0; c < nch; ++c) sched.insert(sched.end(), {s, p | (c << 16)});
-      }
-      L.nbelow = (int)(((int64_t)sched.size() - L.below_off) / 2);
-      int maxblk = 0, maxpan = 0;
-      for (int s : big) {
-        maxblk = std::max<int>(maxblk, (int)cdiv(S.nrows[s], 64));
-        maxpan = std::max<int>(maxpan, (int)cdiv(S.first[s + 1] - S.first[s], 64));
-      }
-      L.ftask_off = (int64_t)tasks.size() / 2;
-      for (int i = 0; i < maxblk; ++i)
-        for (int s : big)
-          if (i < cdiv(S.nrows[s], 64)) {
-            tasks.push_back(s);
-            tasks.push_back(i);
-          }
-      L.nftask = (int)((int64_t)tasks.size() / 2 - L.ftask_off);
-      L.btask_off = (int64_t)tasks.size() / 2;
-      for (int k = 0; k < maxpan; ++k)
-        for (int s : big) {
-          const int np = (int)cdiv(S.first[s + 1] - S.first[s], 64);
-          if (k < np) {
-            tasks.push_back(s);
-            tasks.push_back(np - 1 - k);
-          }
+    auto build_solve = [&](int phase, std::vector<SolveLevel>& out) {
+      for (int lev = 0; lev < NL; ++lev) {
+        std::vector<int32_t> tiny, small, big;
+        for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
+          const int s = S.level_list[q];
+          if (!in_phase(s, phase)) continue;
+          (S.nrows[s] > 128 ? big : (S.nrows[s] > 32 ? small : tiny)).push_back(s);
         }
-      L.nbtask = (int)((int64_t)tasks.size() / 2 - L.btask_off);
-      // algorithmic traffic of one sweep: the L panel once (+ the vectors), 2 flops per panel entry
-      for (int f : small) {
-        const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
-        L.small_bytes += 8.0 * (r * w + 3.0 * r);
-        L.small_flops += 2.0 * (r * w - w * (w + 1) / 2);
+        SolveLevel L{};
+        L.tiny_off = (int64_t)sched.size();
+        L.ntiny = (int)tiny.size();
+        sched.insert(sched.end(), tiny.begin(), tiny.end());
+        L.small_off = (int64_t)sched.size();
+        L.nsmall = (int)small.size();
+        sched.insert(sched.end(), small.begin(), small.end());
+        L.big_off = (int64_t)sched.size();
+        L.nbig = (int)big.size();
+        sched.insert(sched.end(), big.begin(), big.end());
+        align2();
+        L.gat_off = (int64_t)sched.size();
+        for (int s : big)
+          for (int c = 0; c < cdiv(S.nrows[s], NT); ++c) sched.insert(sched.end(), {s, c});
+        L.ngat = (int)(((int64_t)sched.size() - L.gat_off) / 2);
+        L.below_off = (int64_t)sched.size();
+        for (int s : big) {
+          const int w = S.first[s + 1] - S.first[s], r = S.nrows[s];
+          if (r == w) continue;
+          const int np = (int)cdiv(w, 64), nch = (int)cdiv(r - w, BWD_CHUNK);
+          bp_off[s] = (int32_t)nbpart;
+          nbpart += (int64_t)np * nch;
+          for (int p = 0; p < np; ++p)
+            for (int c = 0; c < nch; ++c) sched.insert(sched.end(), {s, p | (c << 16)});
+        }
+        L.nbelow = (int)(((int64_t)sched.size() - L.below_off) / 2);
+        int maxblk = 0, maxpan = 0;
+        for (int s : big) {
+          maxblk = std::max<int>(maxblk, (int)cdiv(S.nrows[s], 64));
+          maxpan = std::max<int>(maxpan, (int)cdiv(S.first[s + 1] - S.first[s], 64));
+        }
+        L.ftask_off = (int64_t)tasks.size() / 2;
+        for (int i = 0; i < maxblk; ++i)
+          for (int s : big)
+            if (i < cdiv(S.nrows[s], 64)) {
+              tasks.push_back(s);
+              tasks.push_back(i);
+            }
+        L.nftask = (int)((int64_t)tasks.size() / 2 - L.ftask_off);
+        L.btask_off = (int64_t)tasks.size() / 2;
+        for (int k = 0; k < maxpan; ++k)
+          for (int s : big) {
+            const int np = (int)cdiv(S.first[s + 1] - S.first[s], 64);
+            if (k < np) {
+              tasks.push_back(s);
+              tasks.push_back(np - 1 - k);
+            }
+          }
+        L.nbtask = (int)((int64_t)tasks.size() / 2 - L.btask_off);
+        // algorithmic traffic of one sweep: the L panel once (+ the vectors), 2 flops per panel entry
+        for (int f : small) {
+          const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
+          L.small_bytes += 8.0 * (r * w + 3.0 * r);
+          L.small_flops += 2.0 * (r * w - w * (w + 1) / 2);
+        }
+        for (int f : tiny) {
+          const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
+          L.tiny_bytes += 8.0 * (r * w + 3.0 * r);
+          L.tiny_flops += 2.0 * (r * w - w * (w + 1) / 2);
+        }
+        for (int f : big) {
+          const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
+          L.big_bytes += 8.0 * (r * w + 3.0 * r);
+          L.big_flops += 2.0 * (r * w - w * (w + 1) / 2);
+          L.below_bytes += 8.0 * (r - w) * w;
+          L.gat_bytes += 8.0 * (2.0 * r + 2.0 * (S.sv_ptr[S.row_ptr[f + 1]] - S.sv_ptr[S.row_ptr[f]]));
+        }
+        out.push_back(L);
       }
-      for (int f : tiny) {
-        const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
-        L.tiny_bytes += 8.0 * (r * w + 3.0 * r);
-        L.tiny_flops += 2.0 * (r * w - w * (w + 1) / 2);
-      }
-      for (int f : big) {
-        const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
-        L.big_bytes += 8.0 * (r * w + 3.0 * r);
-        L.big_flops += 2.0 * (r * w - w * (w + 1) / 2);
-        L.below_bytes += 8.0 * (r - w) * w;
-        L.gat_bytes += 8.0 * (2.0 * r + 2.0 * (S.sv_ptr[S.row_ptr[f + 1]] - S.sv_ptr[S.row_ptr[f]]));
-      }
-      slev_.push_back(L);
+    };
+    build_solve(1, slev1_);
+    if (S.nshards > 1) {
+      build_solve(2, slev2_);
+      align2();
+      xg_off_ = (int64_t)sched.size();
+      for (int s = 0; s < ns; ++s)
+        if (S.top(s))
+          for (int c = 0; c < cdiv(S.nrows[s], NT); ++c) sched.insert(sched.end(), {s, c});
+      nxg_ = (int)(((int64_t)sched.size() - xg_off_) / 2);
     }
-    tasks_.upload(tasks);
+    tasks_.upload(tasks.empty() ? std::vector<int32_t>{0, 0} : tasks);
     flag_off_.upload(flag_off);
     bp_off_.upload(bp_off);
     bpart_.alloc(std::max<int64_t>(nbpart, 1) * 64);
     flags_.alloc(std::max<int64_t>(nflags, 1));
     flags_.zero();
-    counters_.alloc(2 * std::max(S.nlevels, 1));
+    counters_.alloc(4 * std::max(NL, 1));
     err_.alloc(1);
     err_.zero();
   }
-  sched_.upload(sched);
+  sched_.upload(sched.empty() ? std::vector<int32_t>{0} : sched);
   arena_.alloc(std::max<int64_t>(S.arena_size, 2));
+  if (S.nshards > 1)  // top fronts: the strict upper triangles are never written, keep them 0 (all-reduced)
+    MADIPM_HIP(hipMemset(arena_.p + S.top_lo, 0, sizeof(double) * (S.arena_size - S.top_lo)));
   D_.alloc(std::max(S.N, 1));
   xi_.alloc(std::max(S.N, 1));
   uvec_.alloc(std::max<int64_t>(S.uvec_size, 1));
@@ -1448,10 +1567,8 @@ void LDLSolver::kernel_stats(KernelStat out[KK_COUNT]) {
   for (int k = 0; k < KK_COUNT; ++k) out[k] = kst_[k];
 }
 
-void LDLSolver::factorize_async(const double* Kx, hipStream_t s) {
-  if (S_.N == 0) return;
-  k_status_init<<<1, 1, 0, s>>>(status_);
-  for (const Launch& L : fact_) {
+void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStream_t s) {
+  for (const Launch& L : LL) {
     const int32_t* list = sched_.p + L.off;
     switch (L.kind) {
       case ASSEMBLE:
@@ -1489,10 +1606,44 @@ void LDLSolver::factorize_async(const double* Kx, hipStream_t s) {
         break;
     }
   }
+}
+
+// Phase 1: this shard's subtrees (unsharded: the whole factorisation) + the top fronts' external
+// assembly and the shard's status slot.
+void LDLSolver::fact_phase1(const double* Kx, hipStream_t s) {
+  if (S_.N == 0) return;
+  k_status_init<<<1, 1, 0, s>>>(status_);
+  run_fact(fact1_, Kx, s);
   const int nb = (int)std::min<int64_t>(64, cdiv(S_.N, NT));
-  TIMED(KK_INERTIA, 8.0 * S_.N, 0.0, (k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, status_, spd ? 1 : 0)));
+  const int spdf = spd ? 1 : 0;
+  if (!sharded()) {
+    TIMED(KK_INERTIA, 8.0 * S_.N, 0.0, (k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, status_, spdf, nullptr, 0)));
+    MADIPM_HIP(hipGetLastError());
+    MADIPM_HIP(hipMemcpyAsync(h_status_, status_.p, sizeof(LDLStatus), hipMemcpyDeviceToHost, s));
+    return;
+  }
+  TIMED(KK_INERTIA, 8.0 * S_.N, 0.0, (k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, status_, spdf, colmask_, 1)));
+  k_pack_status<<<1, 64, 0, s>>>(status_, arena_.p + S_.top_hi, S_.shard, S_.nshards);
+  MADIPM_HIP(hipGetLastError());
+}
+
+// Phase 2 (sharded): after the all-reduce of fact_xbuf(), every shard factorises the top fronts.
+void LDLSolver::fact_phase2(hipStream_t s) {
+  if (S_.N == 0 || !sharded()) return;
+  k_unpack_status<<<1, 1, 0, s>>>(status_, arena_.p + S_.top_hi, S_.nshards);
+  run_fact(fact2_, nullptr, s);
+  const int nb = (int)std::min<int64_t>(64, cdiv(S_.N, NT));
+  TIMED(KK_INERTIA, 8.0 * S_.N, 0.0, (k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, status_, spd ? 1 : 0, colmask_, 2)));
   MADIPM_HIP(hipGetLastError());
   MADIPM_HIP(hipMemcpyAsync(h_status_, status_.p, sizeof(LDLStatus), hipMemcpyDeviceToHost, s));
+}
+
+void LDLSolver::factorize_async(const double* Kx, hipStream_t s) {
+  fact_phase1(Kx, s);
+  if (!sharded() || S_.N == 0) return;
+  MADIPM_REQUIRE(comm_ != nullptr, "sharded LDL^T without a communicator");
+  comm_->allreduce_sum(fact_xbuf(), fact_xlen(), s);
+  fact_phase2(s);
 }
 
 int LDLSolver::status(hipStream_t s) {
@@ -1509,15 +1660,12 @@ int LDLSolver::status(hipStream_t s) {
   return factorized ? 0 : fp;
 }
 
-void LDLSolver::solve_async(double* b, hipStream_t s) {
-  if (S_.N == 0) return;
-  ++epoch_;
-  const int efwd = 2 * epoch_ - 1, ebwd = 2 * epoch_;
-  MADIPM_HIP(hipMemsetAsync(counters_.p, 0, counters_.n * sizeof(int32_t), s));
+void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* b, hipStream_t s) {
   const SolveTask* tasks = reinterpret_cast<const SolveTask*>(tasks_.p);
-  const int nl = (int)slev_.size();
-  for (int lev = 0; lev < nl; ++lev) {
-    const SolveLevel& L = slev_[lev];
+  const int efwd = 2 * epoch_ - 1;
+  int32_t* cnt = counters_.p + phase * 2 * S_.nlevels;
+  for (int lev = 0; lev < (int)V.size(); ++lev) {
+    const SolveLevel& L = V[lev];
     if (L.ntiny)
       TIMED(KK_FWD_TINY, L.tiny_bytes, L.tiny_flops,
             (k_fwd_tiny<<<(unsigned)cdiv(L.ntiny, 2 * SW), NT, 0, s>>>(T_, sched_.p + L.tiny_off, L.ntiny, arena_, b, xi_,
@@ -1530,18 +1678,24 @@ void LDLSolver::solve_async(double* b, hipStream_t s) {
       TIMED(KK_FWD_GATHER, L.gat_bytes, 0.0,
             (k_fwd_gather<<<L.ngat, NT, 0, s>>>(T_, sched_.p + L.gat_off, b, uvec_, vwork_)));
       TIMED(KK_FWD_BIG, L.big_bytes, L.big_flops,
-            (k_fwd_big<<<std::min(L.nftask, 512), NT, 0, s>>>(T_, tasks + L.ftask_off, L.nftask, counters_.p + 2 * lev,
+            (k_fwd_big<<<std::min(L.nftask, 512), NT, 0, s>>>(T_, tasks + L.ftask_off, L.nftask, cnt + 2 * lev,
                                                                flags_, flag_off_, efwd, arena_, vwork_, xi_, uvec_, err_)));
     }
   }
-  for (int lev = nl - 1; lev >= 0; --lev) {
-    const SolveLevel& L = slev_[lev];
+}
+
+void LDLSolver::bwd_levels(const std::vector<SolveLevel>& V, int phase, double* b, hipStream_t s) {
+  const SolveTask* tasks = reinterpret_cast<const SolveTask*>(tasks_.p);
+  const int ebwd = 2 * epoch_;
+  int32_t* cnt = counters_.p + phase * 2 * S_.nlevels;
+  for (int lev = (int)V.size() - 1; lev >= 0; --lev) {
+    const SolveLevel& L = V[lev];
     if (L.nbelow)
       TIMED(KK_BWD_BELOW, L.below_bytes, 0.25 * L.below_bytes,
             (k_bwd_below<<<L.nbelow, NT, 0, s>>>(T_, sched_.p + L.below_off, bp_off_, arena_, xi_, bpart_)));
     if (L.nbig)
       TIMED(KK_BWD_BIG, L.big_bytes - L.below_bytes, L.big_flops - 0.25 * L.below_bytes,
-            (k_bwd_big<<<std::min(L.nbtask, 512), NT, 0, s>>>(T_, tasks + L.btask_off, L.nbtask, counters_.p + 2 * lev + 1,
+            (k_bwd_big<<<std::min(L.nbtask, 512), NT, 0, s>>>(T_, tasks + L.btask_off, L.nbtask, cnt + 2 * lev + 1,
                                                                flags_, flag_off_, ebwd, arena_, D_, xi_, b, bp_off_, bpart_,
                                                                err_)));
     if (L.nsmall)
@@ -1553,7 +1707,102 @@ void LDLSolver::solve_async(double* b, hipStream_t s) {
             (k_bwd_tiny<<<(unsigned)cdiv(L.ntiny, 2 * SW), NT, 0, s>>>(T_, sched_.p + L.tiny_off, L.ntiny, arena_, D_, xi_,
                                                                       b)));
   }
+}
+
+// Phase 1: forward over this shard's subtrees; unsharded it is the whole solve, sharded it ends with
+// the top fronts' external forward contribution in solve_xbuf().
+void LDLSolver::solve_phase1(double* b, hipStream_t s) {
+  if (S_.N == 0) return;
+  ++epoch_;
+  MADIPM_HIP(hipMemsetAsync(counters_.p, 0, counters_.n * sizeof(int32_t), s));
+  fwd_levels(slev1_, 0, b, s);
+  if (!sharded()) {
+    bwd_levels(slev1_, 0, b, s);
+  } else if (nxg_) {
+    k_ext_gather<<<nxg_, NT, 0, s>>>(T_, sched_.p + xg_off_, S_.shard == 0 ? 1 : 0, sx_ptr_, sx_src_, b, uvec_, xch_);
+  }
   MADIPM_HIP(hipGetLastError());
+}
+
+// Phase 2 (sharded): after the all-reduce of solve_xbuf(): top forward + backward (redundant on every
+// shard), then this shard's subtrees backward.  b is zeroed first; each x lands in b exactly once over
+// the shards (top x on shard 0 only), so an all-reduce of b completes the solution.
+void LDLSolver::solve_phase2(double* b, hipStream_t s) {
+  if (S_.N == 0 || !sharded()) return;
+  MADIPM_HIP(hipMemsetAsync(b, 0, sizeof(double) * S_.N, s));
+  fwd_levels(slev2_, 1, b, s);
+  bwd_levels(slev2_, 1, b, s);
+  bwd_levels(slev1_, 0, b, s);
+  MADIPM_HIP(hipGetLastError());
+}
+
+void LDLSolver::solve_async(double* b, hipStream_t s) {
+  solve_phase1(b, s);
+  if (!sharded() || S_.N == 0) return;
+  MADIPM_REQUIRE(comm_ != nullptr, "sharded LDL^T without a communicator");
+  comm_->allreduce_sum(solve_xbuf(), solve_xlen(), s);
+  solve_phase2(b, s);
+  comm_->allreduce_sum(b, S_.N, s);
+}
+
+// ------------------------------------------------------------------ ShardGroup (P shards, one device)
+void local_allreduce(double* const* bufs, int nbuf, int64_t n, hipStream_t s) {
+  MADIPM_REQUIRE(nbuf >= 1 && nbuf <= 16, "local_allreduce: 1..16 buffers");
+  if (n <= 0) return;
+  BufList B{};
+  for (int q = 0; q < nbuf; ++q) B.p[q] = bufs[q];
+  k_local_allreduce<<<(unsigned)std::min<int64_t>(2048, cdiv(n, NT)), NT, 0, s>>>(B, nbuf, n);
+  MADIPM_HIP(hipGetLastError());
+}
+
+ShardGroup::ShardGroup(int nshards, int n, const int64_t* colptr, const int32_t* rowval, const SymbolicOptions& sopt,
+                       double pivot_tol, const int32_t* user_perm) {
+  MADIPM_REQUIRE(nshards >= 1 && nshards <= 16, "ShardGroup: 1..16 shards");
+  for (int r = 0; r < nshards; ++r) {
+    SymbolicOptions o = sopt;
+    o.nshards = nshards;
+    o.shard = r;
+    sh_.push_back(std::make_unique<LDLSolver>(n, colptr, rowval, o, pivot_tol, user_perm));
+  }
+  rhs_.resize(nshards);
+  for (int r = 1; r < nshards; ++r) rhs_[r].alloc(std::max(n, 1));
+}
+
+void ShardGroup::factorize_async(const double* Kx, hipStream_t s) {
+  const int P = (int)sh_.size();
+  for (auto& h : sh_) h->spd = spd;
+  for (int r = 0; r < P; ++r) sh_[r]->fact_phase1(Kx, s);
+  if (P > 1) {
+    std::vector<double*> bufs;
+    for (auto& h : sh_) bufs.push_back(h->fact_xbuf());
+    local_allreduce(bufs.data(), P, sh_[0]->fact_xlen(), s);
+  }
+  for (int r = 0; r < P; ++r) sh_[r]->fact_phase2(s);
+}
+
+int ShardGroup::status(hipStream_t s) {
+  int st = sh_[0]->status(s);
+  for (size_t r = 1; r < sh_.size(); ++r)
+    MADIPM_REQUIRE(sh_[r]->status(s) == st, "ShardGroup: shards disagree on the factorisation status");
+  return st;
+}
+
+void ShardGroup::solve_async(double* b, hipStream_t s) {
+  const int P = (int)sh_.size();
+  const int n = sh_[0]->n();
+  std::vector<double*> rhs(P);
+  rhs[0] = b;
+  for (int r = 1; r < P; ++r) {
+    rhs[r] = rhs_[r].p;
+    MADIPM_HIP(hipMemcpyAsync(rhs[r], b, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+  }
+  for (int r = 0; r < P; ++r) sh_[r]->solve_phase1(rhs[r], s);
+  if (P == 1) return;
+  std::vector<double*> xb;
+  for (auto& h : sh_) xb.push_back(h->solve_xbuf());
+  local_allreduce(xb.data(), P, sh_[0]->solve_xlen(), s);
+  for (int r = 0; r < P; ++r) sh_[r]->solve_phase2(rhs[r], s);
+  local_allreduce(rhs.data(), P, n, s);
 }
 
 }  // namespace madipm

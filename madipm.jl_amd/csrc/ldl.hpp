@@ -7,6 +7,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <memory>
 #include <vector>
 
 #include "common.hpp"
@@ -36,6 +37,12 @@ struct FrontTab {
   const int64_t* sv_ptr;   // forward-solve gather lists (indexed by row_ptr[s] + i)
   const int64_t* sv_src;
   const int32_t* bigslot;  // big front -> slot in the panel-inverse scratch (64x64 per slot)
+  // sharding: top fronts start their forward solve from the exchanged vector xch[xoff[s] + i]
+  // (xoff = -1 elsewhere); wout[s] = 0 suppresses the write of x to the caller's vector (top fronts
+  // on shards != 0, so that the final all-reduce adds each x once)
+  const int64_t* xoff;
+  const double* xch;
+  const uint8_t* wout;
 };
 
 struct SolveTask {
@@ -61,35 +68,74 @@ struct KernelStat {
   double ms = 0.0, bytes = 0.0, flops = 0.0;
 };
 
-class LDLSolver {
+// All-reduce (sum) of a device buffer across the shards of a sharded factorisation, ordered on
+// `s`.  RcclComm (csrc/comm.cpp) is the multi-GPU implementation (RCCL over xGMI).
+struct Comm {
+  int rank = 0, size = 1;
+  virtual ~Comm() = default;
+  virtual void allreduce_sum(double* buf, int64_t n, hipStream_t s) = 0;
+};
+Comm* make_rccl_comm(int nranks, int rank, const void* unique_id /* 128 bytes */);
+void rccl_unique_id(void* out /* 128 bytes */);
+Comm* make_host_comm(int nranks, int rank, int (*fn)(double*, int64_t, void*), void* ctx);
+
+// Linear-solver interface the MPC driver uses (MadNLP.AbstractLinearSolver methods).
+class LinSolver {
+ public:
+  virtual ~LinSolver() = default;
+  virtual void factorize_async(const double* Kx, hipStream_t s) = 0;
+  virtual int status(hipStream_t s) = 0;
+  virtual void solve_async(double* b, hipStream_t s) = 0;
+  virtual const SymbolicPlan& plan() const = 0;
+  virtual void set_timing(unsigned mask) = 0;
+  virtual void kernel_stats(KernelStat out[]) = 0;
+  virtual int n() const = 0;
+  bool spd = false;  // Cholesky semantics: any non-positive pivot fails (normal equations)
+};
+
+class LDLSolver : public LinSolver {
  public:
   LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const SymbolicOptions& sopt,
-            double pivot_tol, const int32_t* user_perm = nullptr);
+            double pivot_tol, const int32_t* user_perm = nullptr, Comm* comm = nullptr);
   ~LDLSolver();
   LDLSolver(const LDLSolver&) = delete;
   LDLSolver& operator=(const LDLSolver&) = delete;
 
   // Enqueue the numeric factorisation of the values `Kx` (device, caller's CSC order) on `s`.
-  void factorize_async(const double* Kx, hipStream_t s);
+  // Sharded: phase 1, all-reduce of the top fronts (comm), phase 2.
+  void factorize_async(const double* Kx, hipStream_t s) override;
   // Synchronise `s` and return 0 or failing pivot + 1; fills the inertia.
-  int status(hipStream_t s);
+  int status(hipStream_t s) override;
   // In-place solve K x = b for a device vector of length n (caller's ordering).
-  void solve_async(double* b, hipStream_t s);
+  void solve_async(double* b, hipStream_t s) override;
 
-  const SymbolicPlan& plan() const { return S_; }
-  int n() const { return S_.N; }
+  // Phases of a sharded factorisation / solve, for callers that run their own collective
+  // (ShardGroup below, or a host binding with its own RCCL communicator):
+  //   factorize: fact_phase1; all-reduce fact_xbuf(); fact_phase2
+  //   solve:     solve_phase1; all-reduce solve_xbuf(); solve_phase2; all-reduce b (n entries)
+  void fact_phase1(const double* Kx, hipStream_t s);
+  void fact_phase2(hipStream_t s);
+  void solve_phase1(double* b, hipStream_t s);
+  void solve_phase2(double* b, hipStream_t s);
+  double* fact_xbuf() const { return arena_.p + S_.top_lo; }
+  int64_t fact_xlen() const { return S_.nshards > 1 ? S_.top_hi - S_.top_lo + 4 * S_.nshards : 0; }
+  double* solve_xbuf() const { return xch_.p; }
+  int64_t solve_xlen() const { return S_.nshards > 1 ? S_.xlen : 0; }
+  bool sharded() const { return S_.nshards > 1; }
+
+  const SymbolicPlan& plan() const override { return S_; }
+  int n() const override { return S_.N; }
   int npos = 0, nneg = 0, nzero = 0;
   bool factorized = false;
   double pivot_tol = 0.0;
-  bool spd = false;  // Cholesky semantics: any non-positive pivot fails (normal equations)
 
   // device buffers for diagnostics
   const double* d_diag() const { return D_.p; }
 
   // live kernel timing: bit k of `mask` => HIP events around every launch of KernelKind k.
   // set_timing() clears the accumulated statistics; kernel_stats() synchronises the events.
-  void set_timing(unsigned mask);
-  void kernel_stats(KernelStat out[KK_COUNT]);
+  void set_timing(unsigned mask) override;
+  void kernel_stats(KernelStat out[KK_COUNT]) override;
 
  private:
   enum Kind { ASSEMBLE = 0, SMALL32 = 1, SMALL64 = 2, SMALL128 = 3, BIG_DIAG = 4, BIG_TRSM = 5, BIG_UPDATE = 6 };
@@ -123,8 +169,17 @@ class LDLSolver {
   };
   SymbolicPlan S_;
   FrontTab T_{};
-  std::vector<Launch> fact_;
-  std::vector<SolveLevel> slev_;  // per level, leaves first
+  Comm* comm_ = nullptr;
+  std::vector<Launch> fact1_, fact2_;      // phase 1 (this shard's subtrees; everything unsharded), phase 2 (top)
+  std::vector<SolveLevel> slev1_, slev2_;  // per level, leaves first
+  int64_t xg_off_ = 0;                     // (top front, 256-row chunk) pairs of the external forward gather
+  int nxg_ = 0;
+  void run_fact(const std::vector<Launch>& L, const double* Kx, hipStream_t s);
+  void fwd_levels(const std::vector<SolveLevel>& V, int phase, double* b, hipStream_t s);
+  void bwd_levels(const std::vector<SolveLevel>& V, int phase, double* b, hipStream_t s);
+  DBuf<int64_t> xoff_, sx_ptr_, sx_src_;
+  DBuf<double> xch_;
+  DBuf<uint8_t> wout_, colmask_;
   DBuf<int32_t> tasks_, flags_, flag_off_, counters_, err_, bp_off_;
   DBuf<double> bpart_;
   int epoch_ = 0;
@@ -152,5 +207,31 @@ class LDLSolver {
   bool t_begin(int kind, hipStream_t s);
   void t_end(int kind, hipStream_t s, double bytes, double flops);
 };
+
+// The shards of one sharded factorisation on ONE device (single process): the phases run shard by
+// shard and the all-reduces are a device kernel over the shards' buffers (local_allreduce).  It runs
+// the whole sharded data path of SURVEY §8 e on one GPU; across GPUs each process owns one
+// LDLSolver shard with an RcclComm instead.
+class ShardGroup : public LinSolver {
+ public:
+  ShardGroup(int nshards, int n, const int64_t* colptr, const int32_t* rowval, const SymbolicOptions& sopt,
+             double pivot_tol, const int32_t* user_perm = nullptr);
+  void factorize_async(const double* Kx, hipStream_t s) override;
+  int status(hipStream_t s) override;
+  void solve_async(double* b, hipStream_t s) override;
+  const SymbolicPlan& plan() const override { return sh_[0]->plan(); }
+  void set_timing(unsigned mask) override { sh_[0]->set_timing(mask); }
+  void kernel_stats(KernelStat out[]) override { sh_[0]->kernel_stats(out); }
+  int n() const override { return sh_[0]->n(); }
+  LDLSolver& shard(int r) { return *sh_[r]; }
+  int nshards() const { return (int)sh_.size(); }
+
+ private:
+  std::vector<std::unique_ptr<LDLSolver>> sh_;
+  std::vector<DBuf<double>> rhs_;
+};
+
+// bufs[q][i] <- sum_{q' in order} bufs[q'][i] for every q (q = 0..nbuf-1, nbuf <= 16)
+void local_allreduce(double* const* bufs, int nbuf, int64_t n, hipStream_t s);
 
 }  // namespace madipm

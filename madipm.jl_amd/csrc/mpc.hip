@@ -893,13 +893,28 @@ static void csr_from_coo(int nrow, const std::vector<int32_t>& r, const std::vec
   for (int i = 0; i < nrow; ++i) rp[i + 1] += rp[i];
 }
 
-MPCSolver::MPCSolver(const madipm_qp& qp, const madipm_options& opt) : opt_(opt) {
+MPCSolver::MPCSolver(const madipm_qp& qp, const madipm_options& opt, Comm* comm) : opt_(opt), comm_(comm) {
   const double t0 = now();
   MADIPM_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   MADIPM_HIP(hipHostMalloc((void**)&hst_, sizeof(DevState), hipHostMallocDefault));
   std::memset(hst_, 0, sizeof(DevState));
   setup_host(qp);
   t_init_ = now() - t0;
+}
+
+// The linear solver: one LDL^T, or a sharded one — across processes (comm, RCCL) or as a group of
+// shards on this device (ldl.nshards > 1, ShardGroup)
+std::unique_ptr<LinSolver> MPCSolver::make_linsolver(int n, const int64_t* cp, const int32_t* ri,
+                                                     const SymbolicOptions& so) {
+  if (comm_ && comm_->size > 1) {
+    SymbolicOptions o = so;
+    o.nshards = comm_->size;
+    o.shard = comm_->rank;
+    return std::make_unique<LDLSolver>(n, cp, ri, o, opt_.ldl.pivot_tol, nullptr, comm_);
+  }
+  if (opt_.ldl.nshards > 1)
+    return std::make_unique<ShardGroup>(opt_.ldl.nshards, n, cp, ri, so, opt_.ldl.pivot_tol);
+  return std::make_unique<LDLSolver>(n, cp, ri, so, opt_.ldl.pivot_tol);
 }
 
 // Host-side construction: MPCSolver(...) (structure.jl:79-178), MadNLP.initialize!/set_scaling!
@@ -1193,10 +1208,10 @@ void MPCSolver::setup_host(const madipm_qp& q) {
       Ccp[i + 1] = (int64_t)Cri.size();
     }
     nnzC_ = (int64_t)Cri.size();
-    ldl_ = std::make_unique<LDLSolver>(m, Ccp.data(), Cri.data(), so, opt_.ldl.pivot_tol);
+    ldl_ = make_linsolver(m, Ccp.data(), Cri.data(), so);
     ldl_->spd = true;  // Cholesky semantics (test/test_gpu.jl:11): a non-positive pivot fails
   } else {
-    ldl_ = std::make_unique<LDLSolver>(n + m, Kcp.data(), Kri.data(), so, opt_.ldl.pivot_tol);
+    ldl_ = make_linsolver(n + m, Kcp.data(), Kri.data(), so);
   }
 
   // ---- uploads

@@ -43,18 +43,20 @@ struct QPHost;  // host copy of the problem (mpc.hip)
 
 class MPCSolver {
  public:
-  MPCSolver(const madipm_qp& qp, const madipm_options& opt);
+  // comm != nullptr (size > 1): this process holds shard comm->rank of the sharded factorisation
+  MPCSolver(const madipm_qp& qp, const madipm_options& opt, Comm* comm = nullptr);
   ~MPCSolver();
   int solve(madipm_stats* stats);
   void initialize_public();  // initialize! alone (so that callers can time the MPC loop only)
   void set_max_iter(int k) { opt_.max_iter = k; }
   void get_solution(double* x, double* y, double* zl, double* zu, double* cons);
   const std::vector<madipm_iter_trace>& trace() const { return trace_; }
-  LDLSolver& ldl() { return *ldl_; }
+  LinSolver& ldl() { return *ldl_; }
   hipStream_t stream() const { return stream_; }
 
  private:
   void setup_host(const madipm_qp& qp);
+  std::unique_ptr<LinSolver> make_linsolver(int n, const int64_t* cp, const int32_t* ri, const SymbolicOptions& so);
   void initialize();
   void init_starting_point();
   void factorize_regularized();
@@ -74,7 +76,8 @@ class MPCSolver {
   madipm_options opt_{};
   hipStream_t stream_ = nullptr;
   std::unique_ptr<QPHost> H_;
-  std::unique_ptr<LDLSolver> ldl_;
+  std::unique_ptr<LinSolver> ldl_;
+  Comm* comm_ = nullptr;
   // sizes
   int nx_ = 0, ns_ = 0, n_ = 0, m_ = 0, nlb_ = 0, nub_ = 0;
   int64_t nnzK_ = 0, L_ = 0;  // L_ = unreduced vector length

@@ -438,14 +438,106 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     for (int s = 0; s < ns; ++s) S.level_list[fl[S.level[s]]++] = s;
   }
 
-  // ---------------- 9. storage layout + statistics
+  // ---------------- 8b. subtree sharding (SURVEY §8 e).  cost(s) ~ factorisation flops + a per-front
+  // latency term; sub(s) = cost of the subtree rooted at s.  Starting from the roots, the heaviest
+  // splittable candidate subtree is moved to the "top" (its children become candidates) while the
+  // candidates are dealt to the shards by LPT; the cut with the least (top cost + largest shard)
+  // wins.  Every shard computes the same partition (deterministic, shard-independent).
+  S.nshards = std::max(1, opt.nshards);
+  S.shard = opt.shard;
+  MADIPM_REQUIRE(S.shard >= 0 && S.shard < S.nshards, "shard id out of range");
+  if (S.nshards > 1) {
+    std::vector<double> cost(ns), sub(ns);
+    for (int s = 0; s < ns; ++s) {
+      const double r = S.nrows[s], w = S.first[s + 1] - S.first[s];
+      double f = 0.0;
+      for (int t = 0; t < (int)w; ++t) f += (r - t) * (r - t);
+      cost[s] = f + 4096.0 + 64.0 * r;
+      sub[s] = cost[s];
+      for (int64_t q = S.child_ptr[s]; q < S.child_ptr[s + 1]; ++q) sub[s] += sub[S.child_list[q]];
+    }
+    std::vector<int32_t> cands, popped;
+    for (int s = 0; s < ns; ++s)
+      if (S.parent[s] == -1) cands.push_back(s);
+    auto lpt = [&](const std::vector<int32_t>& cs, std::vector<int32_t>* bin_of) {
+      std::vector<int32_t> o(cs);
+      std::sort(o.begin(), o.end(), [&](int a, int b) { return sub[a] > sub[b] || (sub[a] == sub[b] && a < b); });
+      std::vector<double> load(S.nshards, 0.0);
+      for (int c : o) {
+        const int b = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+        load[b] += sub[c];
+        if (bin_of) (*bin_of)[c] = b;
+      }
+      return *std::max_element(load.begin(), load.end());
+    };
+    double topc = 0.0, best = lpt(cands, nullptr);
+    size_t best_pops = 0;
+    // every pop adds to the top cost, so the search ends once the top alone costs more than the best
+    // cut found (or after a bounded number of pops)
+    const size_t max_pops = std::min<size_t>((size_t)ns, 4096);
+    while (popped.size() < max_pops && topc < best) {
+      int bi = -1;
+      for (size_t k = 0; k < cands.size(); ++k) {
+        const int c = cands[k];
+        if (S.child_ptr[c + 1] > S.child_ptr[c] && (bi < 0 || sub[c] > sub[cands[bi]])) bi = (int)k;
+      }
+      if (bi < 0) break;
+      const int c = cands[bi];
+      cands.erase(cands.begin() + bi);
+      for (int64_t q = S.child_ptr[c]; q < S.child_ptr[c + 1]; ++q) cands.push_back(S.child_list[q]);
+      popped.push_back(c);
+      topc += cost[c];
+      const double obj = topc + lpt(cands, nullptr);
+      if (obj < best) {
+        best = obj;
+        best_pops = popped.size();
+      }
+    }
+    // replay the best cut
+    S.owner.assign(ns, -2);
+    cands.clear();
+    for (int s = 0; s < ns; ++s)
+      if (S.parent[s] == -1) cands.push_back(s);
+    S.top_cost = 0.0;
+    for (size_t k = 0; k < best_pops; ++k) {
+      const int c = popped[k];
+      S.owner[c] = -1;
+      S.top_cost += cost[c];
+      cands.erase(std::find(cands.begin(), cands.end(), c));
+      for (int64_t q = S.child_ptr[c]; q < S.child_ptr[c + 1]; ++q) cands.push_back(S.child_list[q]);
+    }
+    std::vector<int32_t> bin(ns, -1);
+    S.shard_cost_max = lpt(cands, &bin);
+    S.shard_cost_sum = 0.0;
+    for (int c : cands) {
+      S.owner[c] = bin[c];
+      S.shard_cost_sum += sub[c];
+    }
+    for (int s = ns - 1; s >= 0; --s)
+      if (S.owner[s] == -2) {
+        MADIPM_REQUIRE(S.parent[s] >= 0, "sharding: unassigned root");
+        S.owner[s] = S.owner[S.parent[s]];
+      }
+  } else {
+    S.owner.clear();  // unsharded: every front belongs to the (only) shard
+  }
+
+  // ---------------- 9. storage layout + statistics (top fronts last, contiguous, full F)
   S.l_off.resize(ns);
   S.u_off.resize(ns);
   S.u_ld.resize(ns);
   S.uvec_off.resize(ns);
   S.is_big.resize(ns);
   int64_t cur = 0, ucur = 0;
-  for (int s = 0; s < ns; ++s) {
+  std::vector<int32_t> storage_order;
+  for (int s = 0; s < ns; ++s)
+    if (!S.top(s)) storage_order.push_back(s);
+  const size_t ntop_begin = storage_order.size();
+  for (int s = 0; s < ns; ++s)
+    if (S.top(s)) storage_order.push_back(s);
+  for (size_t so = 0; so < storage_order.size(); ++so) {
+    const int s = storage_order[so];
+    if (so == ntop_begin) S.top_lo = cur;
     int64_t r = S.nrows[s], w = S.first[s + 1] - S.first[s];
     S.max_front = std::max<int>(S.max_front, (int)r);
     S.nnzL_super += trap(w, r);
@@ -455,7 +547,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     }
     S.uvec_off[s] = ucur;
     ucur += r - w;
-    if (r <= opt.small_front_max) {
+    if (r <= opt.small_front_max && !S.top(s)) {
       S.is_big[s] = 0;
       S.l_off[s] = cur;
       cur += r * w;
@@ -472,6 +564,9 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     }
     cur = (cur + 1) & ~(int64_t)1;  // 16-byte alignment of every front
   }
+  if (ntop_begin == storage_order.size()) S.top_lo = cur;
+  S.top_hi = cur;
+  if (S.nshards > 1) cur += 4 * S.nshards;  // status slots, all-reduced with the top fronts
   S.arena_size = cur;
   S.uvec_size = ucur;
 
@@ -479,10 +574,13 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   // are the sums of their gather lists (original K entries first, then the small children's update
   // entries in child order), then the big children's update blocks are added child by child.  A
   // workgroup owns a tile, so the sums are parallel, conflict-free and deterministic.
+  // Sharded: a top front is assembled in two parts — "external" (original entries on shard 0 + this
+  // shard's subtree-root children; written, zeros included, then all-reduced) and "internal" (its top
+  // children, accumulated after the all-reduce at the front's level).
   S.fs_off.assign(ns, -1);
   S.fs_size = 0;
   for (int s = 0; s < ns; ++s)
-    if (!S.is_big[s] && S.child_ptr[s + 1] > S.child_ptr[s]) {
+    if (!S.is_big[s] && S.child_ptr[s + 1] > S.child_ptr[s] && S.mine(s)) {
       S.fs_off[s] = S.fs_size;
       S.fs_size += (int64_t)S.nrows[s] * S.nrows[s];
     }
@@ -490,107 +588,142 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   S.g_ptr.clear();
   S.g_src.clear();
   S.bt.clear();
-  S.atile_lev.assign(S.nlevels + 1, 0);
-  S.chunk_lev.assign(S.nlevels + 1, 0);
+  S.atile_lev.assign(2 * S.nlevels + 2, 0);
+  S.chunk_lev.assign(2 * S.nlevels + 2, 0);
   S.g_chunk.clear();
   {
     std::vector<int32_t> key, cnt;
     std::vector<int64_t> src, sorted;
-    for (int lev = 0; lev < S.nlevels; ++lev) {
-      for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
-        const int s = S.level_list[q];
-        if (!S.is_big[s] && S.fs_off[s] < 0) continue;
-        const int r = S.nrows[s];
-        const int nt = (r + 63) / 64;
-        const int ntile = nt * (nt + 1) / 2;
-        auto tkey = [&](int row, int col) {
-          const int ti = row >> 6, tj = col >> 6;
-          return (int32_t)((ti * (ti + 1) / 2 + tj) * 4096 + (row & 63) + (col & 63) * 64);
-        };
-        key.clear();
-        src.clear();
+    // children of s whose update blocks this assembly reads: 0 all, 1 top children only, 2 this
+    // shard's subtree children only
+    auto child_ok = [&](int c, int which) {
+      if (which == 0) return true;
+      if (which == 1) return S.top(c);
+      return !S.top(c) && S.owner[c] == S.shard;
+    };
+    auto emit = [&](int s, bool orig, int which, bool acc, bool emit_empty) {
+      const int r = S.nrows[s];
+      const int nt = (r + 63) / 64;
+      const int ntile = nt * (nt + 1) / 2;
+      auto tkey = [&](int row, int col) {
+        const int ti = row >> 6, tj = col >> 6;
+        return (int32_t)((ti * (ti + 1) / 2 + tj) * 4096 + (row & 63) + (col & 63) * 64);
+      };
+      key.clear();
+      src.clear();
+      if (orig)
         for (int64_t qa = S.asm_ptr[s]; qa < S.asm_ptr[s + 1]; ++qa) {
           const int64_t d = S.asm_dst[qa];
           key.push_back(tkey((int)(d % r), (int)(d / r)));
           src.push_back(~S.asm_src[qa]);
         }
-        std::vector<int32_t> bigch;
-        for (int64_t qc = S.child_ptr[s]; qc < S.child_ptr[s + 1]; ++qc) {
-          const int c = S.child_list[qc];
-          const int uc = S.nrows[c] - (S.first[c + 1] - S.first[c]);
-          if (uc > SymbolicPlan::kGatherMax) {
-            bigch.push_back(c);
-            continue;
-          }
-          const int32_t* relc = S.rel.data() + S.rel_ptr[c];
-          for (int bb = 0; bb < uc; ++bb)
-            for (int aa = bb; aa < uc; ++aa) {
-              key.push_back(tkey(relc[aa], relc[bb]));
-              src.push_back(S.u_off[c] + aa + (int64_t)bb * S.u_ld[c]);
-            }
+      std::vector<int32_t> bigch;
+      for (int64_t qc = S.child_ptr[s]; qc < S.child_ptr[s + 1]; ++qc) {
+        const int c = S.child_list[qc];
+        if (!child_ok(c, which)) continue;
+        const int uc = S.nrows[c] - (S.first[c + 1] - S.first[c]);
+        if (uc > SymbolicPlan::kGatherMax) {
+          bigch.push_back(c);
+          continue;
         }
-        // stable counting sort by key (keeps originals-then-children order per entry)
-        const int64_t nkeys = (int64_t)ntile * 4096;
-        cnt.assign(nkeys + 1, 0);
-        for (int32_t k : key) cnt[k + 1]++;
-        for (int64_t k = 0; k < nkeys; ++k) cnt[k + 1] += cnt[k];
-        sorted.resize(src.size());
-        {
-          std::vector<int32_t> fill(cnt.begin(), cnt.end() - 1);
-          for (size_t e = 0; e < key.size(); ++e) sorted[fill[key[e]]++] = src[e];
-        }
-        for (int ti = 0; ti < nt; ++ti)
-          for (int tj = 0; tj <= ti; ++tj) {
-            const int t = ti * (ti + 1) / 2 + tj;
-            SymbolicPlan::AsmTile at{};
-            at.front = s;
-            at.tij = ti | (tj << 16);
-            const int64_t k0 = (int64_t)t * 4096, k1 = k0 + 4096;
-            if (cnt[k1] > cnt[k0]) {
-              at.gptr = (int64_t)S.g_ptr.size();
-              at.gchk = (int64_t)S.g_chunk.size();
-              int32_t nchk = 0;
-              const int64_t sbase = (int64_t)S.g_src.size() - cnt[k0];
-              for (int64_t k = k0; k < k1; ++k) {
-                S.g_ptr.push_back(nchk);
-                for (int64_t c = cnt[k]; c < cnt[k + 1]; c += SymbolicPlan::kChunk, ++nchk) S.g_chunk.push_back(sbase + c);
-              }
-              S.g_ptr.push_back(nchk);
-              S.g_src.insert(S.g_src.end(), sorted.begin() + cnt[k0], sorted.begin() + cnt[k1]);
-            } else {
-              at.gptr = -1;
-              at.gchk = 0;
-            }
-            at.bt0 = (int32_t)(S.bt.size() / 5);
-            const int I0 = ti * 64, I1 = std::min(r, I0 + 64), J0 = tj * 64, J1 = std::min(r, J0 + 64);
-            for (int c : bigch) {
-              const int uc = S.nrows[c] - (S.first[c + 1] - S.first[c]);
-              const int32_t* relc = S.rel.data() + S.rel_ptr[c];
-              const int b0 = (int)(std::lower_bound(relc, relc + uc, J0) - relc);
-              const int b1 = (int)(std::lower_bound(relc + b0, relc + uc, J1) - relc);
-              const int a0 = (int)(std::lower_bound(relc, relc + uc, I0) - relc);
-              const int a1 = (int)(std::lower_bound(relc + a0, relc + uc, I1) - relc);
-              if (b0 < b1 && a0 < a1 && a1 - 1 >= b0) {
-                const int32_t e[5] = {c, b0, b1, a0, a1};
-                S.bt.insert(S.bt.end(), e, e + 5);
-              }
-            }
-            at.bt1 = (int32_t)(S.bt.size() / 5);
-            S.atiles.push_back(at);
+        const int32_t* relc = S.rel.data() + S.rel_ptr[c];
+        for (int bb = 0; bb < uc; ++bb)
+          for (int aa = bb; aa < uc; ++aa) {
+            key.push_back(tkey(relc[aa], relc[bb]));
+            src.push_back(S.u_off[c] + aa + (int64_t)bb * S.u_ld[c]);
           }
       }
-      S.atile_lev[lev + 1] = (int32_t)S.atiles.size();
-      S.chunk_lev[lev + 1] = (int64_t)S.g_chunk.size();
+      // stable counting sort by key (keeps originals-then-children order per entry)
+      const int64_t nkeys = (int64_t)ntile * 4096;
+      cnt.assign(nkeys + 1, 0);
+      for (int32_t k : key) cnt[k + 1]++;
+      for (int64_t k = 0; k < nkeys; ++k) cnt[k + 1] += cnt[k];
+      sorted.resize(src.size());
+      {
+        std::vector<int32_t> fill(cnt.begin(), cnt.end() - 1);
+        for (size_t e = 0; e < key.size(); ++e) sorted[fill[key[e]]++] = src[e];
+      }
+      for (int ti = 0; ti < nt; ++ti)
+        for (int tj = 0; tj <= ti; ++tj) {
+          const int t = ti * (ti + 1) / 2 + tj;
+          SymbolicPlan::AsmTile at{};
+          at.front = s;
+          at.tij = ti | (tj << 16) | (acc ? SymbolicPlan::kAccumulate : 0);
+          const int64_t k0 = (int64_t)t * 4096, k1 = k0 + 4096;
+          const bool has_g = cnt[k1] > cnt[k0];
+          if (has_g) {
+            at.gptr = (int64_t)S.g_ptr.size();
+            at.gchk = (int64_t)S.g_chunk.size();
+            int32_t nchk = 0;
+            const int64_t sbase = (int64_t)S.g_src.size() - cnt[k0];
+            for (int64_t k = k0; k < k1; ++k) {
+              S.g_ptr.push_back(nchk);
+              for (int64_t c = cnt[k]; c < cnt[k + 1]; c += SymbolicPlan::kChunk, ++nchk) S.g_chunk.push_back(sbase + c);
+            }
+            S.g_ptr.push_back(nchk);
+            S.g_src.insert(S.g_src.end(), sorted.begin() + cnt[k0], sorted.begin() + cnt[k1]);
+          } else {
+            at.gptr = -1;
+            at.gchk = 0;
+          }
+          at.bt0 = (int32_t)(S.bt.size() / 5);
+          const int I0 = ti * 64, I1 = std::min(r, I0 + 64), J0 = tj * 64, J1 = std::min(r, J0 + 64);
+          for (int c : bigch) {
+            const int uc = S.nrows[c] - (S.first[c + 1] - S.first[c]);
+            const int32_t* relc = S.rel.data() + S.rel_ptr[c];
+            const int b0 = (int)(std::lower_bound(relc, relc + uc, J0) - relc);
+            const int b1 = (int)(std::lower_bound(relc + b0, relc + uc, J1) - relc);
+            const int a0 = (int)(std::lower_bound(relc, relc + uc, I0) - relc);
+            const int a1 = (int)(std::lower_bound(relc + a0, relc + uc, I1) - relc);
+            if (b0 < b1 && a0 < a1 && a1 - 1 >= b0) {
+              const int32_t e[5] = {c, b0, b1, a0, a1};
+              S.bt.insert(S.bt.end(), e, e + 5);
+            }
+          }
+          at.bt1 = (int32_t)(S.bt.size() / 5);
+          if (has_g || at.bt1 > at.bt0 || emit_empty) S.atiles.push_back(at);
+        }
+    };
+    const int NL = S.nlevels;
+    auto close_group = [&](int g) {
+      S.atile_lev[g + 1] = (int32_t)S.atiles.size();
+      S.chunk_lev[g + 1] = (int64_t)S.g_chunk.size();
+    };
+    // phase 1: this shard's fronts (all fronts when unsharded), level by level
+    for (int lev = 0; lev < NL; ++lev) {
+      for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
+        const int s = S.level_list[q];
+        if (S.top(s) || !S.mine(s)) continue;
+        if (!S.is_big[s] && S.fs_off[s] < 0) continue;
+        emit(s, true, 0, false, true);
+      }
+      close_group(lev);
+    }
+    // top fronts, external part (before the all-reduce; zeros included)
+    for (int s = 0; s < ns; ++s)
+      if (S.top(s)) emit(s, S.shard == 0, 2, false, true);
+    close_group(NL);
+    // phase 2: top fronts, internal part (their top children), level by level
+    for (int lev = 0; lev < NL; ++lev) {
+      for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
+        const int s = S.level_list[q];
+        if (S.top(s)) emit(s, false, 1, true, false);
+      }
+      close_group(NL + 1 + lev);
     }
     S.g_chunk.push_back((int64_t)S.g_src.size());  // sentinel
     MADIPM_REQUIRE(S.g_src.size() < (size_t)INT32_MAX * 2 && S.atiles.size() < (size_t)INT32_MAX, "assembly plan too large");
   }
 
-  // ---------------- 11. forward-solve gather lists (all children, child order)
+  // ---------------- 11. forward-solve gather lists (child order).  Sharded: a top front's rows list
+  // only its top children (sv); its subtree-root children of this shard are listed in sx (the
+  // external forward contribution, exchanged before the top forward solve).
+  auto sv_child_ok = [&](int s, int c) { return !S.top(s) || S.top(c); };
   S.sv_ptr.assign(S.row_ptr[ns] + 1, 0);
   for (int s = 0; s < ns; ++s)
     for (int64_t qc = S.child_ptr[s]; qc < S.child_ptr[s + 1]; ++qc) {
       const int c = S.child_list[qc];
+      if (!sv_child_ok(s, c)) continue;
       const int uc = S.nrows[c] - (S.first[c + 1] - S.first[c]);
       for (int aa = 0; aa < uc; ++aa) S.sv_ptr[S.row_ptr[s] + S.rel[S.rel_ptr[c] + aa] + 1]++;
     }
@@ -601,9 +734,42 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     for (int s = 0; s < ns; ++s)
       for (int64_t qc = S.child_ptr[s]; qc < S.child_ptr[s + 1]; ++qc) {
         const int c = S.child_list[qc];
+        if (!sv_child_ok(s, c)) continue;
         const int uc = S.nrows[c] - (S.first[c + 1] - S.first[c]);
         for (int aa = 0; aa < uc; ++aa) S.sv_src[fill[S.row_ptr[s] + S.rel[S.rel_ptr[c] + aa]]++] = S.uvec_off[c] + aa;
       }
+  }
+  S.xoff.assign(ns, -1);
+  S.xlen = 0;
+  for (int s = 0; s < ns; ++s)
+    if (S.top(s)) {
+      S.xoff[s] = S.xlen;
+      S.xlen += S.nrows[s];
+    }
+  S.sx_ptr.assign(S.xlen + 1, 0);
+  S.sx_src.clear();
+  if (S.xlen) {
+    for (int s = 0; s < ns; ++s) {
+      if (!S.top(s)) continue;
+      for (int64_t qc = S.child_ptr[s]; qc < S.child_ptr[s + 1]; ++qc) {
+        const int c = S.child_list[qc];
+        if (S.top(c) || S.owner[c] != S.shard) continue;
+        const int uc = S.nrows[c] - (S.first[c + 1] - S.first[c]);
+        for (int aa = 0; aa < uc; ++aa) S.sx_ptr[S.xoff[s] + S.rel[S.rel_ptr[c] + aa] + 1]++;
+      }
+    }
+    for (int64_t t = 0; t < S.xlen; ++t) S.sx_ptr[t + 1] += S.sx_ptr[t];
+    S.sx_src.assign(S.sx_ptr[S.xlen], 0);
+    std::vector<int64_t> fill(S.sx_ptr.begin(), S.sx_ptr.end() - 1);
+    for (int s = 0; s < ns; ++s) {
+      if (!S.top(s)) continue;
+      for (int64_t qc = S.child_ptr[s]; qc < S.child_ptr[s + 1]; ++qc) {
+        const int c = S.child_list[qc];
+        if (S.top(c) || S.owner[c] != S.shard) continue;
+        const int uc = S.nrows[c] - (S.first[c + 1] - S.first[c]);
+        for (int aa = 0; aa < uc; ++aa) S.sx_src[fill[S.xoff[s] + S.rel[S.rel_ptr[c] + aa]]++] = S.uvec_off[c] + aa;
+      }
+    }
   }
 }
 

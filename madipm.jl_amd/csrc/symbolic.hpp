@@ -34,6 +34,11 @@ struct SymbolicOptions {
   int nrelax[3] = {4, 16, 48};
   double zrelax[3] = {0.8, 0.1, 0.05};
   int small_front_max = 128; // fronts with r <= this are factorised in LDS by one workgroup
+  // elimination-tree subtree sharding (SURVEY §8 e): the front tree is cut into independent
+  // subtrees dealt to `nshards` shards plus a "top" (their common ancestors) factorised redundantly
+  // by every shard after one all-reduce of the top fronts' external contributions.
+  int nshards = 1;
+  int shard = 0;
 };
 
 struct SymbolicPlan {
@@ -68,14 +73,19 @@ struct SymbolicPlan {
   // are added per tile from their row/column ranges.
   static constexpr int kGatherMax = 128;
   static constexpr int kChunk = 8;
+  static constexpr int32_t kAccumulate = INT32_MIN;  // tij flag: F += tile (else F = tile)
   struct AsmTile {
-    int32_t front, tij;    // tij = ti | tj << 16
+    int32_t front, tij;    // tij = ti | tj << 16 (| kAccumulate)
     int32_t bt0, bt1;      // range in bt (5 ints per big-child block: child, b0, b1, a0, a1)
     int64_t gptr, gchk;    // base of the 4097 per-entry chunk offsets in g_ptr (-1: none), first chunk
   };
   std::vector<AsmTile> atiles;
-  std::vector<int32_t> atile_lev;      // per level: range of atiles
-  std::vector<int64_t> chunk_lev;      // per level: range of chunks
+  // assembly groups (ranges of atiles / chunks): g in [0, nlevels) = phase-1 levels (this shard's
+  // subtree fronts; every front when unsharded), g = nlevels = the top fronts' external assembly
+  // (before the all-reduce), g in (nlevels, 2 nlevels] = phase-2 levels (top fronts, F += the
+  // contributions of their top children)
+  std::vector<int32_t> atile_lev;      // size 2 nlevels + 2
+  std::vector<int64_t> chunk_lev;
   std::vector<int32_t> g_ptr, bt;
   std::vector<int64_t> g_chunk;        // chunk c = sources [g_chunk[c], g_chunk[c+1])
   std::vector<int64_t> g_src;          // >= 0: arena index; < 0: ~(index into caller's values)
@@ -84,6 +94,17 @@ struct SymbolicPlan {
   // forward-solve gather: for every front row, the children's update-vector entries in child order
   std::vector<int64_t> sv_ptr, sv_src;  // sv_ptr indexed by row_ptr[s] + i
   int64_t arena_size = 0, uvec_size = 0;
+  // sharding (nshards > 1): owner[s] = -1 for top fronts (all shards), else the owning shard
+  int nshards = 1, shard = 0;
+  std::vector<int32_t> owner;
+  int64_t top_lo = 0, top_hi = 0;      // arena range of the top fronts (F, full r x r); followed by
+                                       // 4 * nshards status slots (fail pivot, +, -, 0 counts)
+  std::vector<int64_t> xoff;           // top front -> offset of its rows in the solve exchange vector
+  int64_t xlen = 0;                    // sum of the top fronts' orders
+  std::vector<int64_t> sx_ptr, sx_src; // top rows (xoff[s] + i): this shard's subtree-root updates
+  double top_cost = 0, shard_cost_max = 0, shard_cost_sum = 0;  // partition statistics
+  bool mine(int s) const { return owner.empty() || owner[s] == shard; }
+  bool top(int s) const { return !owner.empty() && owner[s] < 0; }
   // statistics
   int64_t nnzL = 0;          // exact nnz(L) incl. diagonal (column counts)
   int64_t nnzL_super = 0;    // stored lower-trapezoid entries incl. relaxed zeros

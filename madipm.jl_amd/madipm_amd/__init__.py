@@ -15,7 +15,7 @@ def __getattr__(name):
     if name in ("MPCSolver", "madipm", "solve", "AdaptiveStep", "ConservativeStep", "MehrotraAdaptiveStep",
                 "NoRegularization", "FixedRegularization", "AdaptiveRegularization", "Mehrotra",
                 "SparseKKTSystem", "ScaledSparseKKTSystem", "NormalKKTSystem", "ExecutionStats",
-                "SOLVE_SUCCEEDED", "STATUS_NAMES"):
+                "SOLVE_SUCCEEDED", "STATUS_NAMES", "RCCLComm", "HostComm"):
         from . import solver
         return getattr(solver, name)
     if name == "HIPLDLSolver":

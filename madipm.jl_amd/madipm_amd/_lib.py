@@ -28,7 +28,7 @@ vp = C.c_void_p
 
 class LDLOpts(C.Structure):
     _fields_ = [("ordering", C.c_int32), ("dense_alpha", C.c_double), ("relax", C.c_int32),
-                ("small_front_max", C.c_int32), ("pivot_tol", C.c_double)]
+                ("small_front_max", C.c_int32), ("pivot_tol", C.c_double), ("nshards", C.c_int32)]
 
 
 class LDLInfo(C.Structure):
@@ -63,6 +63,7 @@ def _sig(name, res, args):
 madipm_version = _sig("madipm_version", C.c_int, [])
 madipm_last_error = _sig("madipm_last_error", C.c_char_p, [])
 madipm_device_count = _sig("madipm_device_count", C.c_int, [])
+madipm_set_device = _sig("madipm_set_device", C.c_int, [C.c_int32])
 madipm_ldl_default_opts = _sig("madipm_ldl_default_opts", None, [C.POINTER(LDLOpts)])
 madipm_symbolic_analyze = _sig("madipm_symbolic_analyze", C.c_int,
                                [C.c_int32, i64p, i32p, C.POINTER(LDLOpts), i32p, C.POINTER(vp)])
@@ -70,6 +71,9 @@ madipm_symbolic_info = _sig("madipm_symbolic_info", C.c_int, [vp, C.POINTER(LDLI
 madipm_symbolic_perm = _sig("madipm_symbolic_perm", C.c_int, [vp, i32p])
 madipm_symbolic_supernodes = _sig("madipm_symbolic_supernodes", C.c_int, [vp, i32p, i32p, i32p])
 madipm_symbolic_destroy = _sig("madipm_symbolic_destroy", None, [vp])
+_sig("madipm_symbolic_analyze_shard", C.c_int, [C.c_int32, i64p, i32p, C.POINTER(LDLOpts), C.c_int32, C.c_int32, i32p,
+                                                C.POINTER(vp)])
+_sig("madipm_symbolic_shard_info", C.c_int, [vp, i32p, f64p, f64p, f64p])
 _sig("madipm_ldl_analyze", C.c_int, [C.c_int32, i64p, i32p, C.POINTER(LDLOpts), i32p, C.POINTER(vp)])
 _sig("madipm_ldl_get_info", C.c_int, [vp, C.POINTER(LDLInfo)])
 _sig("madipm_ldl_factorize", C.c_int, [vp, vp, vp])
@@ -82,6 +86,18 @@ _sig("madipm_ldl_perm", C.c_int, [vp, i32p])
 _sig("madipm_ldl_destroy", None, [vp])
 _sig("madipm_ldl_set_timing", C.c_int, [vp, C.c_uint32])
 _sig("madipm_ldl_kernel_stats", C.c_int, [vp, C.POINTER(KStat)])
+_sig("madipm_ldl_analyze_shard", C.c_int, [C.c_int32, i64p, i32p, C.POINTER(LDLOpts), C.c_int32, C.c_int32, i32p,
+                                           C.POINTER(vp)])
+_sig("madipm_ldl_factorize_phase", C.c_int, [vp, C.c_int32, vp, vp, C.POINTER(vp), i64p])
+_sig("madipm_ldl_solve_phase", C.c_int, [vp, C.c_int32, vp, vp, C.POINTER(vp), i64p])
+_sig("madipm_ldl_shard_info", C.c_int, [vp, i32p, f64p, f64p, f64p])
+_sig("madipm_local_allreduce", C.c_int, [C.POINTER(vp), C.c_int32, C.c_int64, vp])
+_sig("madipm_comm_unique_id", C.c_int, [C.c_char_p])
+_sig("madipm_comm_create", C.c_int, [C.c_int32, C.c_int32, C.c_char_p, C.POINTER(vp)])
+_sig("madipm_comm_destroy", None, [vp])
+_sig("madipm_comm_allreduce", C.c_int, [vp, vp, C.c_int64, vp])
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, f64p, C.c_int64, vp)
+_sig("madipm_comm_create_host", C.c_int, [C.c_int32, C.c_int32, ALLREDUCE_FN, vp, C.POINTER(vp)])
 
 
 class MadIPMError(RuntimeError):
@@ -109,7 +125,7 @@ def default_ldl_opts(**kw) -> LDLOpts:
 class Symbolic:
     """Host-side symbolic analysis (ordering, etree, supernodes) of a lower CSC pattern."""
 
-    def __init__(self, n, colptr, rowval, opts: LDLOpts | None = None, perm=None):
+    def __init__(self, n, colptr, rowval, opts: LDLOpts | None = None, perm=None, nshards=1, shard=0):
         self.n = int(n)
         self._colptr = np.ascontiguousarray(colptr, np.int64)
         self._rowval = np.ascontiguousarray(rowval, np.int32)
@@ -117,10 +133,23 @@ class Symbolic:
         if opts is None:
             opts = default_ldl_opts(ordering=2 if perm is not None else 4)
         h = vp()
-        check(madipm_symbolic_analyze(self.n, ptr(self._colptr, C.c_int64), ptr(self._rowval, C.c_int32),
-                                      C.byref(opts), ptr(up, C.c_int32) if up is not None else None,
-                                      C.byref(h)), "madipm_symbolic_analyze")
+        upp = ptr(up, C.c_int32) if up is not None else None
+        if nshards > 1:
+            check(lib.madipm_symbolic_analyze_shard(self.n, ptr(self._colptr, C.c_int64), ptr(self._rowval, C.c_int32),
+                                                    C.byref(opts), int(nshards), int(shard), upp, C.byref(h)),
+                  "madipm_symbolic_analyze_shard")
+        else:
+            check(madipm_symbolic_analyze(self.n, ptr(self._colptr, C.c_int64), ptr(self._rowval, C.c_int32),
+                                          C.byref(opts), upp, C.byref(h)), "madipm_symbolic_analyze")
         self.h = h
+
+    def shard_info(self) -> dict:
+        ns = self.info()["nsuper"]
+        owner = np.empty(ns, np.int32)
+        tc, mx, sm = C.c_double(), C.c_double(), C.c_double()
+        check(lib.madipm_symbolic_shard_info(self.h, ptr(owner, C.c_int32), C.byref(tc), C.byref(mx), C.byref(sm)),
+              "madipm_symbolic_shard_info")
+        return {"owner": owner, "top_cost": tc.value, "shard_cost_max": mx.value, "shard_cost_sum": sm.value}
 
     def info(self) -> dict:
         inf = LDLInfo()

@@ -18,18 +18,27 @@ class HIPLDLSolver:
     """Multifrontal supernodal LDL^T on the GPU (libmadipm_hip)."""
 
     def __init__(self, n, colptr, rowval, *, ordering=4, relax=1, pivot_tol=0.0, perm=None,
-                 small_front_max=128):
+                 small_front_max=128, nshards=1, shard=None):
+        """nshards > 1 and shard None: all shards of a subtree-sharded factorisation on this device
+        (SURVEY §8 e, local all-reduce).  shard = r: only shard r (one process per GPU); drive it with
+        factorize_phase / solve_phase and your own collective (or use MPCSolver(comm=...))."""
         self.n = int(n)
         self._colptr = np.ascontiguousarray(colptr, np.int64)
         self._rowval = np.ascontiguousarray(rowval, np.int32)
         opts = L.default_ldl_opts(ordering=2 if perm is not None else ordering, relax=relax,
-                                  pivot_tol=pivot_tol, small_front_max=small_front_max)
+                                  pivot_tol=pivot_tol, small_front_max=small_front_max,
+                                  nshards=nshards if shard is None else 1)
         up = None if perm is None else np.ascontiguousarray(perm, np.int32)
+        upp = L.ptr(up, C.c_int32) if up is not None else None
         h = L.vp()
-        L.check(L.lib.madipm_ldl_analyze(self.n, L.ptr(self._colptr, C.c_int64), L.ptr(self._rowval, C.c_int32),
-                                         C.byref(opts), L.ptr(up, C.c_int32) if up is not None else None,
-                                         C.byref(h)), "madipm_ldl_analyze")
+        cp, rv = L.ptr(self._colptr, C.c_int64), L.ptr(self._rowval, C.c_int32)
+        if shard is None:
+            L.check(L.lib.madipm_ldl_analyze(self.n, cp, rv, C.byref(opts), upp, C.byref(h)), "madipm_ldl_analyze")
+        else:
+            L.check(L.lib.madipm_ldl_analyze_shard(self.n, cp, rv, C.byref(opts), int(nshards), int(shard), upp,
+                                                   C.byref(h)), "madipm_ldl_analyze_shard")
         self.h = h
+        self.nshards, self.shard = int(nshards), shard
 
     # ---- MadNLP interface names
     def introduce(self) -> str:
@@ -82,6 +91,30 @@ class HIPLDLSolver:
         L.check(L.lib.madipm_ldl_perm(self.h, L.ptr(p, C.c_int32)), "madipm_ldl_perm")
         return p
 
+    # ---- subtree sharding (one shard per process; the caller runs the all-reduces)
+    def factorize_phase(self, phase, nzval=None, stream=None):
+        """phase 1 returns (ptr, len) of the device buffer to all-reduce before phase 2."""
+        xb, xl = L.vp(), C.c_int64()
+        L.check(L.lib.madipm_ldl_factorize_phase(self.h, int(phase), C.c_void_p(nzval.data_ptr() if nzval is not None else 0),
+                                                 C.c_void_p(_stream(stream)), C.byref(xb), C.byref(xl)),
+                "madipm_ldl_factorize_phase")
+        return xb.value, xl.value
+
+    def solve_phase(self, phase, x, stream=None):
+        """phase 1 -> (ptr, len) to all-reduce; phase 2 -> (x ptr, n): all-reduce x to finish."""
+        xb, xl = L.vp(), C.c_int64()
+        L.check(L.lib.madipm_ldl_solve_phase(self.h, int(phase), C.c_void_p(x.data_ptr()), C.c_void_p(_stream(stream)),
+                                             C.byref(xb), C.byref(xl)), "madipm_ldl_solve_phase")
+        return xb.value, xl.value
+
+    def shard_info(self) -> dict:
+        ns = self.info()["nsuper"]
+        owner = np.empty(ns, np.int32)
+        tc, mx, sm = C.c_double(), C.c_double(), C.c_double()
+        L.check(L.lib.madipm_ldl_shard_info(self.h, L.ptr(owner, C.c_int32), C.byref(tc), C.byref(mx), C.byref(sm)),
+                "madipm_ldl_shard_info")
+        return {"owner": owner, "top_cost": tc.value, "shard_cost_max": mx.value, "shard_cost_sum": sm.value}
+
     def set_kernel_timing(self, mask: int = (1 << L.NKERNELS) - 1):
         """HIP events around every launch of the kernel kinds in `mask`; clears the statistics."""
         L.check(L.lib.madipm_ldl_set_timing(self.h, int(mask)), "madipm_ldl_set_timing")
@@ -96,6 +129,12 @@ class HIPLDLSolver:
         if h:
             L.lib.madipm_ldl_destroy(h)
             self.h = None
+
+
+def local_allreduce(ptrs, n, stream=None):
+    """Sum of device buffers (raw pointers) written back to all of them (single-process shards)."""
+    arr = (L.vp * len(ptrs))(*[L.vp(p) for p in ptrs])
+    L.check(L.lib.madipm_local_allreduce(arr, len(ptrs), int(n), C.c_void_p(_stream(stream))), "local_allreduce")
 
 
 def _stream(stream) -> int:

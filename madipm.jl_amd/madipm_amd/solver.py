@@ -116,6 +116,7 @@ class IterTrace(C.Structure):
 
 L._sig("madipm_default_options", None, [C.POINTER(Options)])
 L._sig("madipm_solver_create", C.c_int, [C.POINTER(QPStruct), C.POINTER(Options), C.POINTER(L.vp)])
+L._sig("madipm_solver_create_dist", C.c_int, [C.POINTER(QPStruct), C.POINTER(Options), L.vp, C.POINTER(L.vp)])
 L._sig("madipm_solver_solve", C.c_int, [L.vp, C.POINTER(Stats)])
 L._sig("madipm_solver_initialize", C.c_int, [L.vp])
 L._sig("madipm_solver_set_max_iter", C.c_int, [L.vp, C.c_int32])
@@ -126,6 +127,68 @@ L._sig("madipm_solver_ldl_perm", C.c_int, [L.vp, L.i32p])
 L._sig("madipm_solver_set_timing", C.c_int, [L.vp, C.c_uint32])
 L._sig("madipm_solver_kernel_stats", C.c_int, [L.vp, C.POINTER(L.KStat)])
 L._sig("madipm_solver_destroy", None, [L.vp])
+
+
+class RCCLComm:
+    """RCCL communicator of the sharded factorisation (one process per GPU; madipm_comm_*).
+
+    `RCCLComm.from_torch(dist)` makes rank 0's 128-byte unique id, broadcasts it with the
+    torch.distributed process group (any backend), and joins the communicator."""
+
+    def __init__(self, rank: int, size: int, uid: bytes):
+        assert len(uid) == 128
+        self.rank, self.size = int(rank), int(size)
+        h = L.vp()
+        L.check(L.lib.madipm_comm_create(self.size, self.rank, uid, C.byref(h)), "madipm_comm_create")
+        self.h = h
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(128)
+        L.check(L.lib.madipm_comm_unique_id(buf), "madipm_comm_unique_id")
+        return buf.raw
+
+    @classmethod
+    def from_torch(cls, dist) -> "RCCLComm":
+        rank, size = dist.get_rank(), dist.get_world_size()
+        box = [cls.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        return cls(rank, size, box[0])
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            L.lib.madipm_comm_destroy(h)
+            self.h = None
+
+
+class HostComm:
+    """Host-staged communicator over a torch.distributed process group (e.g. gloo): every all-reduce
+    goes device -> pinned host -> dist.all_reduce -> device.  For exercising the multi-process
+    sharded path where RCCL cannot run (several ranks on one GPU); RCCLComm is the data path."""
+
+    def __init__(self, dist):
+        import torch
+        self.rank, self.size = dist.get_rank(), dist.get_world_size()
+
+        def _fn(p, n, _ctx):
+            try:
+                a = np.ctypeslib.as_array(p, shape=(int(n),))
+                t = torch.from_numpy(a)
+                dist.all_reduce(t)
+                return 0
+            except Exception:  # pragma: no cover - reported as a C error
+                return -1
+        self._cb = L.ALLREDUCE_FN(_fn)
+        h = L.vp()
+        L.check(L.lib.madipm_comm_create_host(self.size, self.rank, self._cb, None, C.byref(h)), "madipm_comm_create_host")
+        self.h = h
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            L.lib.madipm_comm_destroy(h)
+            self.h = None
 
 
 @dataclass
@@ -165,7 +228,7 @@ _KNOWN = {"tol", "max_iter", "max_wall_time", "divergence_tol", "scaling", "boun
           "mu_min", "tol_linear_solve", "check_residual", "kkt_system", "linear_solver", "print_level",
           "rethrow_error", "ordering", "relax", "pivot_tol", "small_front_max", "dense_alpha",
           "output_file", "file_print_level", "kappa_d", "s_max", "mu_superlinear_decrease_power", "tau_min",
-          "fixed_variable_treatment", "equality_treatment"}
+          "fixed_variable_treatment", "equality_treatment", "nshards", "comm"}
 
 
 def load_options(**kw) -> Options:
@@ -209,7 +272,7 @@ def load_options(**kw) -> Options:
     if ls is not HIPLDLSolver:
         raise NotImplementedError("linear_solver must be HIPLDLSolver (the GPU LDL^T)")
     o.print_level = int(kw.get("print_level", 0))
-    for k in ("ordering", "relax", "small_front_max"):
+    for k in ("ordering", "relax", "small_front_max", "nshards"):
         if k in kw:
             setattr(o.ldl, k, int(kw[k]))
     for k in ("pivot_tol", "dense_alpha"):
@@ -248,7 +311,14 @@ class MPCSolver:
         q.minimize = int(bool(qp.minimize))
         self._q = q
         h = L.vp()
-        L.check(L.lib.madipm_solver_create(C.byref(q), C.byref(self.options), C.byref(h)), "MPCSolver")
+        comm = kwargs.get("comm")
+        if comm is not None and comm.size > 1:
+            # subtree-sharded factorisation across the processes of `comm` (SURVEY §8 e)
+            self._comm = comm
+            L.check(L.lib.madipm_solver_create_dist(C.byref(q), C.byref(self.options), comm.h, C.byref(h)),
+                    "MPCSolver")
+        else:
+            L.check(L.lib.madipm_solver_create(C.byref(q), C.byref(self.options), C.byref(h)), "MPCSolver")
         self.h = h
 
     def ldl_info(self) -> dict:

@@ -1,5 +1,6 @@
-"""world_size-2 gloo test of the bench's multi-rank aggregation (replicas: barrier, max time,
-sum of iterations) — the N>1 path of bench.py, exercised on CPU."""
+"""world_size-2 gloo tests of the N>1 host logic of bench.py on CPU: the multi-rank aggregation
+(max time; iterations of the one sharded solve, or summed over replicas) and the broadcast of the
+RCCL unique id through the process group (RCCLComm.from_torch's protocol, without the GPU)."""
 import os
 import socket
 
@@ -23,8 +24,11 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import bench
     dt, iters = 0.5 + rank, 10 + rank          # rank-local timing and iteration count
-    tot_dt, tot_it = bench.aggregate(dt, iters, dist, torch.device("cpu"))
-    q.put((rank, tot_dt, tot_it))
+    tot_dt, tot_it = bench.aggregate(dt, iters, dist, False)
+    sh_dt, sh_it = bench.aggregate(dt, 22, dist, True)
+    box = [bytes(range(128)) if rank == 0 else None]
+    dist.broadcast_object_list(box, src=0)
+    q.put((rank, tot_dt, tot_it, sh_dt, sh_it, box[0] == bytes(range(128))))
     dist.destroy_process_group()
 
 
@@ -39,6 +43,8 @@ def test_two_rank_aggregation():
     for p in procs:
         p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs)
-    for rank, tot_dt, tot_it in res:
+    for rank, tot_dt, tot_it, sh_dt, sh_it, id_ok in res:
         assert tot_dt == pytest.approx(1.5)     # max over ranks
-        assert tot_it == 21                     # sum over ranks
+        assert tot_it == 21                     # replicas: sum over ranks
+        assert sh_dt == pytest.approx(1.5) and sh_it == 22  # sharded: one solve's iterations
+        assert id_ok
