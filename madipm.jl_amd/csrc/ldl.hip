@@ -64,6 +64,28 @@ __device__ __forceinline__ double fwd_init(const FrontTab& T, int s, int i, int 
   return (i < w) ? b[T.perm[f0 + i]] : 0.0;
 }
 
+// HBM panel (r x w, ld r) -> LDS (ld rl), all threads, 16 independent loads per thread per batch
+// (one HBM round trip per 4096 doubles: a 128 x 128 front is 4 round trips)
+__device__ __forceinline__ void stage_panel(const double* __restrict__ L, double* Ls, int r, int w, int rl) {
+  const int nel = r * w;
+  for (int base = 0; base < nel; base += NT * 16) {
+    double v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int q = base + k * NT + threadIdx.x;
+      v[k] = (q < nel) ? L[q] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int q = base + k * NT + threadIdx.x;
+      if (q < nel) {
+        const int j = q / r, i = q - j * r;
+        Ls[i + j * rl] = v[k];
+      }
+    }
+  }
+}
+
 __global__ void k_status_init(LDLStatus* st) {
   st->fail_pivot = INT_MAX;
   st->npos = st->nneg = st->nzero = 0;
@@ -80,7 +102,7 @@ __global__ __launch_bounds__(NT) void k_small_factor(FrontTab T, const int32_t* 
                                                      const double* __restrict__ Kx, double* __restrict__ arena,
                                                      const double* __restrict__ fscratch, double* __restrict__ D,
                                                      LDLStatus* st, double tol) {
-  extern __shared__ __attribute__((aligned(16))) double F[];  // r x r, col-major, ld r
+  extern __shared__ __attribute__((aligned(16))) double F[];  // r x r, col-major, ld r (leaf fronts only)
   __shared__ double cb[2][16 * TS];
   __shared__ double dp[16 * TS];
   const int s = fronts[blockIdx.x];
@@ -88,17 +110,6 @@ __global__ __launch_bounds__(NT) void k_small_factor(FrontTab T, const int32_t* 
   const int w = T.first[s + 1] - f0;
   const int r = T.nrows[s];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int q = tid; q < r * r; q += NT) F[q] = 0.0;
-  __syncthreads();
-  const int64_t fso = T.fs_off[s];
-  if (fso < 0) {  // leaf: original entries only
-    for (int64_t q = T.asm_ptr[s] + tid; q < T.asm_ptr[s + 1]; q += NT) F[T.asm_dst[q]] = Kx[T.asm_src[q]];
-  } else {        // assembled by k_assemble (lower triangle)
-    const double* __restrict__ Fs = fscratch + fso;
-    for (int j = wv; j < r; j += NT / 64)
-      for (int i = j + lane; i < r; i += 64) F[i + j * r] = Fs[i + j * r];
-  }
-  __syncthreads();
   // tile of this thread: q -> (ti, tj), tj <= ti, 136 lower tiles of a 16 x 16 grid
   int ti = 0, tj = 0;
   {
@@ -112,10 +123,29 @@ __global__ __launch_bounds__(NT) void k_small_factor(FrontTab T, const int32_t* 
   const bool act = tid < 136 && ti * TS < r;
   const int i0 = ti * TS, j0 = tj * TS;
   double a[TS][TS];
+  const int64_t fso = T.fs_off[s];
+  if (fso >= 0) {
+    // assembled by k_assemble (lower triangle, ld r): every thread loads its tile straight from HBM,
+    // TS*TS independent loads in flight (no serialised staging copy); entries above the diagonal
+    // are never read
+    const double* __restrict__ Fs = fscratch + fso;
 #pragma unroll
-  for (int k = 0; k < TS; ++k)
+    for (int k = 0; k < TS; ++k)
 #pragma unroll
-    for (int c = 0; c < TS; ++c) a[k][c] = (act && i0 + k < r && j0 + c < r) ? F[(i0 + k) + (j0 + c) * r] : 0.0;
+      for (int c = 0; c < TS; ++c) {
+        const int i = i0 + k, j = j0 + c;
+        a[k][c] = (act && i < r && j <= i) ? Fs[i + (int64_t)j * r] : 0.0;
+      }
+  } else {  // leaf: original entries only, scattered into LDS
+    for (int q = tid; q < r * r; q += NT) F[q] = 0.0;
+    __syncthreads();
+    for (int64_t q = T.asm_ptr[s] + tid; q < T.asm_ptr[s + 1]; q += NT) F[T.asm_dst[q]] = Kx[T.asm_src[q]];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < TS; ++k)
+#pragma unroll
+      for (int c = 0; c < TS; ++c) a[k][c] = (act && i0 + k < r && j0 + c < r) ? F[(i0 + k) + (j0 + c) * r] : 0.0;
+  }
   for (int t8 = 0; t8 < w; t8 += TS) {
 #pragma unroll
     for (int c = 0; c < TS; ++c) {
@@ -429,6 +459,152 @@ __device__ __forceinline__ void diag64(double* A64, double* Dl, double* Ms, doub
   __syncthreads();
 }
 
+// ------------------------------------------------------------------ small fronts, blocked (r <= 128)
+// The front lives in LDS (ld = r | 1).  Pivots are taken 16 at a time: one wave factors the 16 x 16
+// diagonal block (wave-synchronous, no barriers; identity-padded when fewer than 16 pivots remain),
+// the rows below get L = A M_K on f64 MFMA, and the trailing lower triangle is updated tile by tile
+// (16 x 16 tiles, C -= (L_I D) L_J^T, f64 MFMA 16x16x4) — 3 barriers per 16 pivots instead of one per
+// pivot.  Row/column blocks of a step start right after its last pivot (not 16-aligned), exactly
+// like the big-front path.
+// Factor the kw (<= 16) pivots at (k0, k0) of A (ld) with ONE wave: strictly-lower L_KK into A,
+// pivots into Dl[k0 + t], M_K = L_KK^{-T} D^{-1} (16 x 16, ld LDM, identity-padded) into MK.
+__device__ __forceinline__ void factor16g(double* A, int ld, int k0, int kw, double* Dl, double* MK, double* cb,
+                                          double* xb, int lane) {
+  const int il = lane & 15, cg = lane >> 4;
+  double a[4], x[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int jl = cg + 4 * m;
+    a[m] = (il < kw && jl < kw) ? (jl <= il ? A[(k0 + il) + (k0 + jl) * ld] : 0.0) : (il == jl ? 1.0 : 0.0);
+    x[m] = (jl == il) ? 1.0 : 0.0;
+  }
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    if (cg == (t & 3)) cb[t * LDM + il] = a[t >> 2];
+    if (il == t) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) xb[t * LDM + cg + 4 * m] = x[m];
+    }
+    wave_sync();
+    const double dt = cb[t * LDM + t];
+    const double li = (il > t) ? cb[t * LDM + il] / dt : 0.0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int jl = cg + 4 * m;
+      const double cj = cb[t * LDM + jl];
+      const double xt = xb[t * LDM + jl];
+      a[m] = fma(jl > t ? -li : 0.0, cj, a[m]);
+      x[m] = fma(jl > t ? 0.0 : -li, xt, x[m]);
+    }
+  }
+  wave_sync();
+  const double di = cb[il * LDM + il];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int jl = cg + 4 * m;
+    if (jl < il && il < kw) A[(k0 + il) + (k0 + jl) * ld] = a[m] / cb[jl * LDM + jl];
+    MK[jl * LDM + il] = (jl <= il) ? x[m] / di : 0.0;
+  }
+  if (cg == 0 && il < kw) Dl[k0 + il] = di;
+  wave_sync();
+}
+
+__global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t* __restrict__ fronts,
+                                                      const double* __restrict__ Kx, double* __restrict__ arena,
+                                                      const double* __restrict__ fscratch, double* __restrict__ D,
+                                                      LDLStatus* st, double tol) {
+  extern __shared__ __attribute__((aligned(16))) double A[];  // r x r, ld = r | 1
+  __shared__ double Dl[128];
+  __shared__ double MK[16 * LDM];
+  __shared__ double cbuf[2 * 16 * LDM];
+  const int s = fronts[blockIdx.x];
+  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+  const int ld = r | 1;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t fso = T.fs_off[s];
+  if (fso >= 0) {
+    stage_panel(fscratch + fso, A, r, r, ld);  // assembled by k_assemble (lower part valid)
+  } else {                                     // leaf: original entries only
+    for (int q = tid; q < r * ld; q += NT) A[q] = 0.0;
+    __syncthreads();
+    for (int64_t q = T.asm_ptr[s] + tid; q < T.asm_ptr[s + 1]; q += NT) {
+      const int64_t d = T.asm_dst[q];
+      A[(int)(d % r) + (int)(d / r) * ld] = Kx[T.asm_src[q]];
+    }
+  }
+  __syncthreads();
+  for (int k0 = 0; k0 < w; k0 += 16) {
+    const int kw = min(16, w - k0);
+    const int R0 = k0 + kw;                       // first row / column after the pivots
+    const int nbr = (r - R0 + 15) >> 4;           // 16-row blocks below
+    if (wv == ((k0 >> 4) & 3)) factor16g(A, ld, k0, kw, Dl, MK, cbuf, cbuf + 16 * LDM, lane);
+    __syncthreads();
+    // panel: L_R = A[R, k0:k0+kw] M_K, row block per wave
+    for (int b = wv; b < nbr; b += 4) {
+      const int rb = R0 + 16 * b;
+      dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int k = 4 * ks + (lane >> 4), row = rb + (lane & 15);
+        const double av = (k < kw && row < r) ? A[row + (k0 + k) * ld] : 0.0;
+        const double bv = MK[k * LDM + (lane & 15)];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      }
+      // acc[g]: row rb + (lane>>4) + 4g ... D[m][n] with m = (lane>>4)+4g, n = lane&15: here the A
+      // operand carried the rows (m) and M_K the columns (n)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int row = rb + (lane >> 4) + 4 * g, col = lane & 15;
+        if (row < r && col < kw) A[row + (k0 + col) * ld] = acc[g];
+      }
+    }
+    __syncthreads();
+    // trailing update of the lower triangle of A[R0:, R0:]: tile (I, J), J <= I
+    const int ntile = nbr * (nbr + 1) / 2;
+    for (int q = wv; q < ntile; q += 4) {
+      int I = 0, rem = q;
+      while (rem > I) {
+        rem -= I + 1;
+        ++I;
+      }
+      const int J = rem;
+      const int i0 = R0 + 16 * I, j0 = R0 + 16 * J;
+      dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int k = 4 * ks + (lane >> 4);
+        const int rj = j0 + (lane & 15), ri = i0 + (lane & 15);
+        const double av = (k < kw && rj < r) ? A[rj + (k0 + k) * ld] : 0.0;                 // L_J (rows m)
+        const double bv = (k < kw && ri < r) ? A[ri + (k0 + k) * ld] * Dl[k0 + k] : 0.0;    // (L_I D) (cols n)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int j = j0 + (lane >> 4) + 4 * g, i = i0 + (lane & 15);
+        if (i < r && j < r && i >= j) A[i + j * ld] -= acc[g];
+      }
+    }
+    __syncthreads();
+  }
+  // write-out: L panel (ld r; d on the diagonal, zeros above), D, lower triangle of U (ld r - w)
+  double* __restrict__ L = arena + T.l_off[s];
+  for (int q = tid; q < r * w; q += NT) {
+    const int j = q / r, i = q - j * r;
+    L[q] = (i > j) ? A[i + j * ld] : (i == j ? Dl[j] : 0.0);
+  }
+  const int u = r - w;
+  double* __restrict__ Uo = arena + T.u_off[s];
+  for (int q = tid; q < u * u; q += NT) {
+    const int b = q / u, a = q - b * u;
+    if (a >= b) Uo[q] = A[(w + a) + (w + b) * ld];
+  }
+  if (tid < w) {
+    const double d = Dl[tid];
+    D[f0 + tid] = d;
+    if (bad_pivot(d, tol)) atomicMin(&st->fail_pivot, f0 + tid + 1);
+  }
+}
+
 // Diagonal block of 64-column panel `step` (one workgroup per front): load, blocked factorisation,
 // write L11 (d on the diagonal), D and the M_K blocks for k_big_trsm.
 __global__ __launch_bounds__(NT) void k_big_diag(FrontTab T, const int32_t* __restrict__ list, int step,
@@ -665,9 +841,12 @@ __global__ __launch_bounds__(NT) void k_inertia(const double* __restrict__ D, in
 constexpr int SW = 4;  // waves (= small fronts) per workgroup
 
 
-// Small-front solves, one WAVE per front, no LDS: lane l holds rows (forward) or pivot columns
-// (backward) l and l + 64 in registers; the value of row/column t is broadcast with readlane; the L
-// entries a lane needs are its own row/column, loaded 8 steps ahead (software pipelined).
+// Small-front solves (32 < r <= 128): one WORKGROUP per front.  The whole workgroup first copies the
+// r x w L panel into LDS with every load in flight at once (the panel is contiguous in HBM, ld r; in
+// LDS ld = r | 1 so that column-strided lane accesses of the backward solve are conflict-free), then
+// wave 0 runs the substitution from LDS: lane l holds rows (forward) or pivot columns (backward) l and
+// l + 64 in registers, the value of row/column t is broadcast with readlane.  Turning the panel read
+// from a latency chain into one bandwidth burst is what bounds these levels.
 __device__ __forceinline__ double bcast(double v0, double v1, int t) {
   return (t < 64) ? readlane_f64(v0, t) : readlane_f64(v1, t - 64);
 }
@@ -675,59 +854,50 @@ __device__ __forceinline__ double bcast(double v0, double v1, int t) {
 __global__ __launch_bounds__(NT) void k_fwd_small(FrontTab T, const int32_t* __restrict__ fronts, int nf,
                                                   const double* __restrict__ arena, const double* __restrict__ b,
                                                   double* __restrict__ xi, double* __restrict__ uvec) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int q = __builtin_amdgcn_readfirstlane(blockIdx.x * SW + wv);
-  if (q >= nf) return;
-  // wave-uniform front scalars in SGPRs: scalar branches, unconditional loads, countable vmcnt
-  const int s = __builtin_amdgcn_readfirstlane(fronts[q]);
-  const int f0 = __builtin_amdgcn_readfirstlane(T.first[s]);
-  const int w = __builtin_amdgcn_readfirstlane(T.first[s + 1]) - f0;
-  const int r = __builtin_amdgcn_readfirstlane(T.nrows[s]);
-  const double* __restrict__ L = arena + T.l_off[s];
-  const int i0 = lane, i1 = lane + 64;
-  const int ci0 = min(i0, r - 1), ci1 = min(i1, r - 1);
-  double v[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int i = lane + 64 * h;
+  extern __shared__ __attribute__((aligned(16))) double Ls[];
+  const int s = fronts[blockIdx.x];
+  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+  const int rl = r | 1;
+  stage_panel(arena + T.l_off[s], Ls, r, w, rl);
+  const int lane = threadIdx.x & 63;
+  // initial vector (own b + children's update vectors): all 256 threads, two per row, each walking
+  // half of the row's gather list with 4 loads in flight; partial sums meet in LDS
+  __shared__ double v0s[128];
+  {
+    const int i = threadIdx.x >> 1, h = threadIdx.x & 1;
     double vi = 0.0;
     if (i < r) {
-      vi = fwd_init(T, s, i, w, f0, b);
       const int64_t e = T.row_ptr[s] + i;
       const int64_t p1 = T.sv_ptr[e + 1];
-      for (int64_t p = T.sv_ptr[e]; p < p1; ++p) vi += uvec[T.sv_src[p]];
+      int64_t p = T.sv_ptr[e] + h;
+      for (; p + 6 < p1; p += 8) {
+        const int64_t q0 = T.sv_src[p], q1 = T.sv_src[p + 2], q2 = T.sv_src[p + 4], q3 = T.sv_src[p + 6];
+        vi += (uvec[q0] + uvec[q1]) + (uvec[q2] + uvec[q3]);
+      }
+      for (; p < p1; p += 2) vi += uvec[T.sv_src[p]];
     }
-    v[h] = vi;
+    vi += __shfl_xor(vi, 1, 64);
+    if (h == 0 && i < r) v0s[i] = vi + fwd_init(T, s, i, w, f0, b);
   }
-  // forward substitution: v[i] -= L(i, t) v[t] for i > t, t < w.  Two register sets of 8 columns
-  // in ping-pong (no copies), so the loads of the next block stay in flight during this one.
-  double A0[8], A1[8], B0[8], B1[8];
-  auto load = [&](double(&c0)[8], double(&c1)[8], int tb) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {  // raw, clamped loads (masks applied at use: vmcnt stays countable)
-      const int64_t col = (int64_t)min(tb + k, w - 1) * r;
-      c0[k] = L[ci0 + col];
-      c1[k] = L[ci1 + col];
-    }
-  };
-  auto step = [&](const double(&c0)[8], const double(&c1)[8], int tb) {
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+  double v[2];
+  v[0] = (lane < r) ? v0s[lane] : 0.0;
+  v[1] = (lane + 64 < r) ? v0s[lane + 64] : 0.0;
+  // forward substitution: v[i] -= L(i, t) v[t] for i > t, t < w
+  const int i0 = lane, i1 = lane + 64;
+  const int ci0 = min(i0, r - 1), ci1 = min(i1, r - 1);
+  for (int t8 = 0; t8 < w; t8 += 8) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int t = tb + k;
-      if (t < w) {  // rows >= r hold garbage that is never stored
+      const int t = t8 + k;
+      if (t < w) {  // wave-uniform
+        const double l0 = Ls[ci0 + t * rl], l1 = Ls[ci1 + t * rl];
         const double xt = bcast(v[0], v[1], t);
-        v[0] = fma(i0 > t ? -c0[k] : 0.0, xt, v[0]);
-        v[1] = fma(i1 > t ? -c1[k] : 0.0, xt, v[1]);
+        v[0] = fma(i0 > t ? -l0 : 0.0, xt, v[0]);
+        v[1] = fma(i1 > t ? -l1 : 0.0, xt, v[1]);
       }
     }
-  };
-  load(A0, A1, 0);
-  for (int t8 = 0; t8 < w; t8 += 16) {
-    load(B0, B1, t8 + 8);
-    step(A0, A1, t8);
-    if (t8 + 8 >= w) break;
-    load(A0, A1, t8 + 16);
-    step(B0, B1, t8 + 8);
   }
   double* __restrict__ uo = uvec + T.uvec_off[s];
 #pragma unroll
@@ -743,87 +913,56 @@ __global__ __launch_bounds__(NT) void k_fwd_small(FrontTab T, const int32_t* __r
 __global__ __launch_bounds__(NT) void k_bwd_small(FrontTab T, const int32_t* __restrict__ fronts, int nf,
                                                   const double* __restrict__ arena, const double* __restrict__ D,
                                                   double* __restrict__ xi, double* __restrict__ out) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int q = __builtin_amdgcn_readfirstlane(blockIdx.x * SW + wv);
-  if (q >= nf) return;
-  const int s = __builtin_amdgcn_readfirstlane(fronts[q]);
-  const int f0 = __builtin_amdgcn_readfirstlane(T.first[s]);
-  const int w = __builtin_amdgcn_readfirstlane(T.first[s + 1]) - f0;
-  const int r = __builtin_amdgcn_readfirstlane(T.nrows[s]);
-  const double* __restrict__ L = arena + T.l_off[s];
+  extern __shared__ __attribute__((aligned(16))) double Ls[];
+  const int s = fronts[blockIdx.x];
+  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+  const int rl = r | 1;
+  stage_panel(arena + T.l_off[s], Ls, r, w, rl);
+  const int lane = threadIdx.x & 63;
   const int32_t* __restrict__ rows = T.rows + T.row_ptr[s];
+  double xb[2] = {0.0, 0.0}, own[2] = {0.0, 0.0};
+  if (threadIdx.x < 64) {  // x of the rows below the pivot block (ancestors: final) and x_j / d_j
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int i = w + lane + 64 * h;
+      if (i < r) xb[h] = xi[rows[i]];
+      const int j = lane + 64 * h;
+      if (j < w) own[h] = xi[f0 + j] / D[f0 + j];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
   const int j0 = lane, j1 = lane + 64;  // pivot columns of this lane
   const int cj0 = min(j0, w - 1), cj1 = min(j1, w - 1);
-  // x of the rows below the pivot block (final: ancestors); lane k holds row w + k (+ 64)
-  double xb[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int i = w + lane + 64 * h;
-    xb[h] = (i < r) ? xi[rows[i]] : 0.0;
-  }
+  const int nb = r - w;
   // v[j] = x_j / d_j - sum_{i >= w} L(i, j) x_i
   double acc0 = 0.0, acc1 = 0.0;
-  const int nb = r - w;
-  {
-    double A0[8], A1[8], B0[8], B1[8];
-    auto load = [&](double(&l0)[8], double(&l1)[8], int kb) {
+  for (int k8 = 0; k8 < nb; k8 += 8) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int ci = min(w + kb + k, r - 1);
-        l0[k] = L[ci + (int64_t)cj0 * r];
-        l1[k] = L[ci + (int64_t)cj1 * r];
+    for (int kk = 0; kk < 8; ++kk) {
+      const int k = k8 + kk;
+      if (k < nb) {
+        const double x = bcast(xb[0], xb[1], k);
+        acc0 = fma(Ls[(w + k) + cj0 * rl], x, acc0);
+        acc1 = fma(Ls[(w + k) + cj1 * rl], x, acc1);
       }
-    };
-    auto step = [&](const double(&l0)[8], const double(&l1)[8], int kb) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        if (kb + k < nb) {
-          const double x = bcast(xb[0], xb[1], kb + k);
-          acc0 = fma(l0[k], x, acc0);
-          acc1 = fma(l1[k], x, acc1);
-        }
-      }
-    };
-    if (nb > 0) load(A0, A1, 0);
-    for (int k8 = 0; k8 < nb; k8 += 16) {
-      load(B0, B1, k8 + 8);
-      step(A0, A1, k8);
-      if (k8 + 8 >= nb) break;
-      load(A0, A1, k8 + 16);
-      step(B0, B1, k8 + 8);
     }
   }
   double v[2];
-  v[0] = (j0 < w) ? xi[f0 + j0] / D[f0 + j0] - acc0 : 0.0;
-  v[1] = (j1 < w) ? xi[f0 + j1] / D[f0 + j1] - acc1 : 0.0;
-  // transposed back substitution: for t = w-1 .. 1: v[j] -= L(t, j) v[t] for j < t (ping-pong sets)
-  double A0[8], A1[8], B0[8], B1[8];
-  auto load = [&](double(&c0)[8], double(&c1)[8], int tb) {
+  v[0] = (j0 < w) ? own[0] - acc0 : 0.0;
+  v[1] = (j1 < w) ? own[1] - acc1 : 0.0;
+  // transposed back substitution: for t = w-1 .. 1: v[j] -= L(t, j) v[t] for j < t
+  for (int t8 = w - 1; t8 > 0; t8 -= 8) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int ct = max(tb - k, 0);
-      c0[k] = L[ct + (int64_t)cj0 * r];
-      c1[k] = L[ct + (int64_t)cj1 * r];
-    }
-  };
-  auto step = [&](const double(&c0)[8], const double(&c1)[8], int tb) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int t = tb - k;
-      if (t > 0) {
+      const int t = t8 - k;
+      if (t > 0) {  // wave-uniform
+        const double l0 = Ls[t + cj0 * rl], l1 = Ls[t + cj1 * rl];
         const double xt = bcast(v[0], v[1], t);
-        v[0] = fma(t > j0 ? -c0[k] : 0.0, xt, v[0]);
-        v[1] = fma(t > j1 ? -c1[k] : 0.0, xt, v[1]);
+        v[0] = fma(t > j0 ? -l0 : 0.0, xt, v[0]);
+        v[1] = fma(t > j1 ? -l1 : 0.0, xt, v[1]);
       }
     }
-  };
-  load(A0, A1, w - 1);
-  for (int t8 = w - 1; t8 > 0; t8 -= 16) {
-    load(B0, B1, t8 - 8);
-    step(A0, A1, t8);
-    if (t8 - 8 <= 0) break;
-    load(A0, A1, t8 - 16);
-    step(B0, B1, t8 - 8);
   }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -919,20 +1058,24 @@ __global__ __launch_bounds__(NT) void k_bwd_tiny(FrontTab T, const int32_t* __re
 }
 
 // initial forward vector of a big front (own b entries + children's update vectors), in HBM;
-// task = (front, 256-row chunk), thread = row, children summed in the fixed list order
+// task = (front, chunk of GAT_ROWS rows), GAT_G lanes per row stride the row's gather list (children
+// in list order per lane, lanes combined by a fixed butterfly: deterministic)
+constexpr int GAT_G = 8, GAT_ROWS = NT / GAT_G;
 __global__ __launch_bounds__(NT) void k_fwd_gather(FrontTab T, const int32_t* __restrict__ list,
                                                    const double* __restrict__ b, const double* __restrict__ uvec,
                                                    double* __restrict__ vwork) {
   int s, chunk;
   task_of(list, s, chunk);
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
-  const int i = chunk * NT + threadIdx.x;
-  if (i >= r) return;
-  double vi = fwd_init(T, s, i, w, f0, b);
+  const int i = chunk * GAT_ROWS + threadIdx.x / GAT_G, gl = threadIdx.x & (GAT_G - 1);
+  if (i >= r) return;  // whole groups leave together
   const int64_t e = T.row_ptr[s] + i;
   const int64_t p1 = T.sv_ptr[e + 1];
-  for (int64_t p = T.sv_ptr[e]; p < p1; ++p) vi += uvec[T.sv_src[p]];
-  vwork[e] = vi;
+  double vi = 0.0;
+  for (int64_t p = T.sv_ptr[e] + gl; p < p1; p += GAT_G) vi += uvec[T.sv_src[p]];
+#pragma unroll
+  for (int o = GAT_G / 2; o > 0; o >>= 1) vi += __shfl_xor(vi, o, GAT_G);
+  if (gl == 0) vwork[e] = vi + fwd_init(T, s, i, w, f0, b);
 }
 
 __device__ __forceinline__ bool wait_flag(int32_t* f, int epoch, int32_t* err) {
@@ -1323,6 +1466,11 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       for (int c = 0; c < 3; ++c)
         if (!cls[c].empty()) {
           Launch L{SMALL32 + c, 0, (int64_t)sched.size(), (int)cls[c].size(), (int64_t)cls[c].size()};
+          L.lds = false;
+          for (int f : cls[c]) {
+            L.lds = L.lds || S.fs_off[f] < 0;
+            L.lds_bytes = std::max<int>(L.lds_bytes, 8 * S.nrows[f] * (S.nrows[f] | 1));
+          }
           for (int f : cls[c]) {  // reads: K entries or the assembled front; writes: L panel, U block, D
             const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
             L.bytes += 8.0 * (r * w + (r - w) * (r - w) + w) +
@@ -1407,7 +1555,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         align2();
         L.gat_off = (int64_t)sched.size();
         for (int s : big)
-          for (int c = 0; c < cdiv(S.nrows[s], NT); ++c) sched.insert(sched.end(), {s, c});
+          for (int c = 0; c < cdiv(S.nrows[s], GAT_ROWS); ++c) sched.insert(sched.end(), {s, c});
         L.ngat = (int)(((int64_t)sched.size() - L.gat_off) / 2);
         L.below_off = (int64_t)sched.size();
         for (int s : big) {
@@ -1448,6 +1596,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
           const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
           L.small_bytes += 8.0 * (r * w + 3.0 * r);
           L.small_flops += 2.0 * (r * w - w * (w + 1) / 2);
+          L.small_lds = std::max<int>(L.small_lds, 8 * (S.nrows[f] | 1) * (S.first[f + 1] - S.first[f]));
         }
         for (int f : tiny) {
           const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
@@ -1498,6 +1647,9 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   if (!attr_done) {
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_small_factor<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    128 * 128 * 8));
+    MADIPM_HIP(hipFuncSetAttribute((const void*)k_fwd_small, hipFuncAttributeMaxDynamicSharedMemorySize, 129 * 128 * 8));
+    MADIPM_HIP(hipFuncSetAttribute((const void*)k_small_blocked, hipFuncAttributeMaxDynamicSharedMemorySize, 129 * 128 * 8));
+    MADIPM_HIP(hipFuncSetAttribute((const void*)k_bwd_small, hipFuncAttributeMaxDynamicSharedMemorySize, 129 * 128 * 8));
     attr_done = true;
   }
   MADIPM_HIP(hipDeviceSynchronize());
@@ -1585,14 +1737,10 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
                                                                       status_, pivot_tol)));
         break;
       case SMALL64:
-        TIMED(KK_SMALL, L.bytes, L.flops,
-              (k_small_factor<4><<<(unsigned)L.items, NT, 64 * 64 * 8, s>>>(T_, list, Kx, arena_, fscratch_, D_,
-                                                                           status_, pivot_tol)));
-        break;
       case SMALL128:
         TIMED(KK_SMALL, L.bytes, L.flops,
-              (k_small_factor<8><<<(unsigned)L.items, NT, 128 * 128 * 8, s>>>(T_, list, Kx, arena_, fscratch_, D_,
-                                                                             status_, pivot_tol)));
+              (k_small_blocked<<<(unsigned)L.items, NT, L.lds_bytes, s>>>(T_, list, Kx, arena_, fscratch_, D_, status_,
+                                                                         pivot_tol)));
         break;
       case BIG_DIAG:
         TIMED(KK_DIAG, L.bytes, L.flops,
@@ -1672,7 +1820,7 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
                                                                       uvec_)));
     if (L.nsmall)
       TIMED(KK_FWD_SMALL, L.small_bytes, L.small_flops,
-            (k_fwd_small<<<(unsigned)cdiv(L.nsmall, SW), NT, 0, s>>>(T_, sched_.p + L.small_off, L.nsmall, arena_, b, xi_,
+            (k_fwd_small<<<(unsigned)L.nsmall, NT, L.small_lds, s>>>(T_, sched_.p + L.small_off, L.nsmall, arena_, b, xi_,
                                                                     uvec_)));
     if (L.nbig) {
       TIMED(KK_FWD_GATHER, L.gat_bytes, 0.0,
@@ -1700,7 +1848,7 @@ void LDLSolver::bwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
                                                                err_)));
     if (L.nsmall)
       TIMED(KK_BWD_SMALL, L.small_bytes, L.small_flops,
-            (k_bwd_small<<<(unsigned)cdiv(L.nsmall, SW), NT, 0, s>>>(T_, sched_.p + L.small_off, L.nsmall, arena_, D_, xi_,
+            (k_bwd_small<<<(unsigned)L.nsmall, NT, L.small_lds, s>>>(T_, sched_.p + L.small_off, L.nsmall, arena_, D_, xi_,
                                                                     b)));
     if (L.ntiny)
       TIMED(KK_BWD_TINY, L.tiny_bytes, L.tiny_flops,

@@ -148,6 +148,8 @@ class LDLSolver : public LinSolver {
     int64_t chunk0 = 0, nchunk = 0;  // ASSEMBLE: chunk range of the level
     double bytes = 0, flops = 0;       // algorithmic traffic / work of the launch
     double bytes2 = 0, flops2 = 0;     // ASSEMBLE: of the chunk pass
+    bool lds = true;                   // SMALL*: some front is a leaf (assembled in LDS)
+    int lds_bytes = 0;                 // SMALL*: dynamic LDS of the blocked kernel (largest front)
   };
   struct SolveLevel {
     int64_t tiny_off;  // fronts with r <= 32 (half a wave each)
@@ -164,6 +166,7 @@ class LDLSolver : public LinSolver {
     int nftask;
     int64_t btask_off;
     int nbtask;
+    int small_lds = 0;  // dynamic LDS of the small-front solve kernels (largest panel, ld r | 1)
     double tiny_bytes = 0, tiny_flops = 0;
     double small_bytes = 0, small_flops = 0, big_bytes = 0, big_flops = 0, below_bytes = 0, gat_bytes = 0;
   };

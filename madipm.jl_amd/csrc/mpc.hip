@@ -124,6 +124,23 @@ __device__ __forceinline__ void amin_upd(double& v, int& ix, double nv, int ni) 
 
 #define GRID_LOOP(i, N) for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < (N); i += (int64_t)gridDim.x * blockDim.x)
 
+// SpMV rows in groups of G lanes (G | 64): the group's lanes stride the row's entries (coalesced),
+// then a G-wide butterfly sums them (every lane of the group holds the row sum).  G is chosen per
+// problem from the mean row length (MPCSolver::spmv_group).
+#define GROUP_LOOP(i, N, G) \
+  for (int64_t i = (blockIdx.x * (int64_t)NT + threadIdx.x) / (G); i < (N); i += (int64_t)gridDim.x * (NT / (G)))
+
+template <int G>
+__device__ __forceinline__ double gdot(const DCsr& A, int64_t row, const double* __restrict__ x) {
+  const int gl = threadIdx.x & (G - 1);
+  double s = 0.0;
+  const int64_t q1 = A.rp[row + 1];
+  for (int64_t q = A.rp[row] + gl; q < q1; q += G) s += A.v[q] * x[A.ci[q]];
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, G);
+  return s;
+}
+
 // ------------------------------------------------------------------ KKT diagonal (kernels.jl:124-149)
 // K2 (set_aug_diagonal! for SparseKKTSystem, kernels.jl:124-136): pr_diag into the K2 diagonal.
 // K2.5 (kernels.jl:139-149 + MadNLP._set_aug_diagonal! [EXT]): the primal block is scaled
@@ -230,25 +247,29 @@ __global__ __launch_bounds__(NT) void k_normal_asm(DV D) {
 
 // MadNLP.solve!(kkt::NormalKKTSystem, w) (normalkkt.jl:196-219), after reduce_rhs! (done by k_rhs):
 // r2 = A Sigma^{-1} r1 - r2 (one thread per row of A)
+template <int G>
 __global__ __launch_bounds__(NT) void k_normal_rhs(DV D) {
-  GRID_LOOP(i, D.m) {
+  GROUP_LOOP(i, D.m, G) {
+    const int gl = threadIdx.x & (G - 1);
     double s = 0.0;
-    for (int64_t q = D.J.rp[i]; q < D.J.rp[i + 1]; ++q) {
+    for (int64_t q = D.J.rp[i] + gl; q < D.J.rp[i + 1]; q += G) {
       const int k = D.J.ci[q];
       s += D.J.v[q] * (D.d[k] / D.pr_diag[k]);
     }
-    D.bufm[i] = s - D.d[D.n + i];
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, G);
+    if (gl == 0) D.bufm[i] = s - D.d[D.n + i];
   }
 }
 
 // ... dy = C^{-1} r2 (LDL^T solve on bufm), then dx = Sigma^{-1} (r1 - A^T dy), wy = dy
+template <int G>
 __global__ __launch_bounds__(NT) void k_normal_back(DV D) {
-  GRID_LOOP(i, D.n + D.m) {
+  GROUP_LOOP(i, D.n + D.m, G) {
     if (i < D.n) {
-      double s = 0.0;
-      for (int64_t q = D.JT.rp[i]; q < D.JT.rp[i + 1]; ++q) s += D.JT.v[q] * D.bufm[D.JT.ci[q]];
-      D.d[i] = (D.d[i] - s) / D.pr_diag[i];
-    } else {
+      const double s = gdot<G>(D.JT, i, D.bufm);
+      if ((threadIdx.x & (G - 1)) == 0) D.d[i] = (D.d[i] - s) / D.pr_diag[i];
+    } else if ((threadIdx.x & (G - 1)) == 0) {
       D.d[i] = D.bufm[i - D.n];
     }
   }
@@ -314,13 +335,17 @@ __global__ __launch_bounds__(NT) void k_rhs(DV D, int mode, double mu_g) {
 }
 
 // finish_aug_solve! [EXT] + residual w = p - K d (mul!/_kktmul! [EXT], linear_solver.jl:29-35)
+template <int G>
 __global__ __launch_bounds__(NT) void k_residual(DV D, double dw, double dc) {
   const int n = D.n, m = D.m, nlb = D.nlb;
+  const bool lead = (threadIdx.x & (G - 1)) == 0;
   double wmax = 0.0, pmax = 0.0, dxmax = 0.0;
-  GRID_LOOP(i, n + m) {
+  GROUP_LOOP(i, n + m, G) {
     if (i < n) {
+      const double hj = gdot<G>(D.H, i, D.d) + gdot<G>(D.JT, i, D.d + n);
+      if (!lead) continue;
       const double dx = D.d[i];
-      double kv = csr_dot(D.H, (int)i, D.d) + csr_dot(D.JT, (int)i, D.d + n) + dw * dx;
+      double kv = hj + dw * dx;
       const int kl = D.lbpos[i], ku = D.ubpos[i];
       if (kl >= 0) {
         const double pl = D.p[n + m + kl];
@@ -345,8 +370,10 @@ __global__ __launch_bounds__(NT) void k_residual(DV D, double dw, double dc) {
       pmax = nmax(pmax, fabs(pi));
       dxmax = nmax(dxmax, fabs(dx));
     } else {
+      const double jd = gdot<G>(D.J, i - n, D.d);
+      if (!lead) continue;
       const double dy = D.d[i];
-      const double kv = csr_dot(D.J, (int)(i - n), D.d) + dc * dy;
+      const double kv = jd + dc * dy;
       const double pi = D.p[i];
       wmax = nmax(wmax, fabs(pi - kv));
       pmax = nmax(pmax, fabs(pi));
@@ -467,20 +494,25 @@ __global__ __launch_bounds__(NT) void k_apply(DV D) {
 }
 
 // evaluate_model! (solver.jl:319-326): obj, grad f = Hx + c, cons c = Jx - rhs, jacl = J^T y
+template <int G>
 __global__ __launch_bounds__(NT) void k_eval(DV D) {
   const int n = D.n;
+  const bool lead = (threadIdx.x & (G - 1)) == 0;
   double op = 0.0;
-  GRID_LOOP(i, n + D.m) {
+  GROUP_LOOP(i, n + D.m, G) {
     if (i < n) {
+      const double hx = gdot<G>(D.H, i, D.x);
+      const double jy = gdot<G>(D.JT, i, D.y);
+      if (!lead) continue;
       const double x = D.x[i];
-      const double hx = csr_dot(D.H, (int)i, D.x);
       const double g = D.cs[i] + D.gfix[i];
       D.f[i] = D.fixed[i] ? 0.0 : hx + g;
-      D.jacl[i] = csr_dot(D.JT, (int)i, D.y);
+      D.jacl[i] = jy;
       op += x * g + 0.5 * x * hx;
     } else {
-      const int j = (int)(i - n);
-      D.c[j] = csr_dot(D.J, j, D.x) - D.rhs[j] + D.cfix[j];
+      const int64_t j = i - n;
+      const double jx = gdot<G>(D.J, j, D.x);
+      if (lead) D.c[j] = jx - D.rhs[j] + D.cfix[j];
     }
   }
   double v[1] = {op};
@@ -1141,6 +1173,11 @@ void MPCSolver::setup_host(const madipm_qp& q) {
   std::vector<double> Kv;
   csr_from_coo(n + m, kc, kr, kv, Kcp, Kri, Kv);
   nnzK_ = (int64_t)Kri.size();
+  {  // SpMV lane-group width: ~2 entries per lane on an average row of [H A^T; A]
+    const double avg = (double)(Hci.size() + 2 * Jci.size()) / std::max(1, n + m);
+    spmv_g_ = 4;
+    while (spmv_g_ < 64 && spmv_g_ * 2 < avg) spmv_g_ *= 2;
+  }
   std::vector<int64_t> diag_pos(n + m, -1);
   for (int j = 0; j < n + m; ++j)
     for (int64_t q = Kcp[j]; q < Kcp[j + 1]; ++q)
@@ -1348,6 +1385,18 @@ void MPCSolver::setup_host(const madipm_qp& q) {
   D.Cx = Cx_;                                                                                           \
   D.nnzC = nnzC_;
 
+// launch a GROUP_LOOP SpMV kernel with the problem's lane-group width
+#define SPMV_LAUNCH(kern, grid, strm, ...)                                        \
+  do {                                                                            \
+    switch (spmv_g_) {                                                            \
+      case 4: kern<4><<<(grid), NT, 0, (strm)>>>(__VA_ARGS__); break;             \
+      case 8: kern<8><<<(grid), NT, 0, (strm)>>>(__VA_ARGS__); break;             \
+      case 16: kern<16><<<(grid), NT, 0, (strm)>>>(__VA_ARGS__); break;           \
+      case 32: kern<32><<<(grid), NT, 0, (strm)>>>(__VA_ARGS__); break;           \
+      default: kern<64><<<(grid), NT, 0, (strm)>>>(__VA_ARGS__); break;           \
+    }                                                                             \
+  } while (0)
+
 void MPCSolver::kkt_diag(double dw, double dc) {
   DV_ARGS;
   k_diag<<<blocks(n_ + m_), NT, 0, stream_>>>(D, dw, dc);
@@ -1372,9 +1421,9 @@ void MPCSolver::factor_enqueue(double dw, double dc) {
 void MPCSolver::kkt_solve() {
   DV_ARGS;
   if (kkt_ == KKT_NORMAL) {
-    k_normal_rhs<<<blocks(m_), NT, 0, stream_>>>(D);
+    SPMV_LAUNCH(k_normal_rhs, blocks(m_), stream_, D);
     ldl_->solve_async(bufm_.p, stream_);
-    k_normal_back<<<blocks(n_ + m_), NT, 0, stream_>>>(D);
+    SPMV_LAUNCH(k_normal_back, blocks(n_ + m_), stream_, D);
   } else {
     ldl_->solve_async(d_.p, stream_);
     if (kkt_ == KKT_K25) k_k25_unscale<<<blocks(n_), NT, 0, stream_>>>(D);
@@ -1407,7 +1456,7 @@ void MPCSolver::solve_system(int mode, double mu) {
   const int nb = blocks(n_ + m_);
   k_rhs<<<nb, NT, 0, stream_>>>(D, mode, mu);
   kkt_solve();
-  k_residual<<<nb, NT, 0, stream_>>>(D, del_w_, del_c_);
+  SPMV_LAUNCH(k_residual, nb, stream_, D, del_w_, del_c_);
   launch_reduce_final(FIN_RESID, nb);
 }
 
@@ -1492,13 +1541,13 @@ void MPCSolver::init_starting_point() {
   // Step 1: least-squares primal correction
   k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_PRIMAL, 0.0);
   kkt_solve();
-  k_residual<<<nb, NT, 0, s>>>(D, del_w_, del_c_);
+  SPMV_LAUNCH(k_residual, nb, s, D, del_w_, del_c_);
   launch_reduce_final(FIN_RESID, nb);
   k_axpy_x<<<nbn, NT, 0, s>>>(D);
   // Step 2: dual least squares
   k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_DUAL, 0.0);
   kkt_solve();
-  k_residual<<<nb, NT, 0, s>>>(D, del_w_, del_c_);
+  SPMV_LAUNCH(k_residual, nb, s, D, del_w_, del_c_);
   launch_reduce_final(FIN_RESID, nb);
   k_copy_y<<<blocks(m_), NT, 0, s>>>(D);
   // Step 3: bound multipliers and shifts
@@ -1544,7 +1593,7 @@ void MPCSolver::initialize() {
   k_set_mu<<<1, 1, 0, s>>>(st_, 0.0);
   // callbacks at the initial point (solver.jl:166-170)
   const int nb = blocks(n_ + m_);
-  k_eval<<<nb, NT, 0, s>>>(D);
+  SPMV_LAUNCH(k_eval, nb, s, D);
   launch_reduce_final(FIN_EVAL, nb);
   // norm_c = ||primal(f)||_inf (solver.jl:174)
   std::vector<double> fh(n_);
@@ -1691,7 +1740,7 @@ int MPCSolver::solve(madipm_stats* stats) {
       // ---- apply_step! + evaluate_model!
       k_apply<<<nb, NT, 0, s>>>(D);
       ++k_;
-      k_eval<<<nb, NT, 0, s>>>(D);
+      SPMV_LAUNCH(k_eval, nb, s, D);
       launch_reduce_final(FIN_EVAL, nb);
       MADIPM_HIP(hipGetLastError());
     }
