@@ -33,13 +33,23 @@ sys.path.insert(0, ROOT)
 
 
 def build_problem(config: str, seed: int = 0):
+    """BASELINE.json configs as concrete inputs (SURVEY §8 d).  `name@s` scales the stand-in by s."""
     from madipm_amd import standard_form_qp
-    from madipm_amd.instances import ex10_standin
-    if config == "ex10":
-        return standard_form_qp(ex10_standin(seed=seed)), "MIPLIB ex10 LP relaxation (structured stand-in)"
-    if config.startswith("ex10@"):
-        s = float(config.split("@")[1])
-        return standard_form_qp(ex10_standin(seed=seed, scale=s)), f"ex10 stand-in scaled x{s}"
+    from madipm_amd import instances as I
+    name, _, sc = config.partition("@")
+    s = float(sc) if sc else 1.0
+    tag = f" scaled x{s}" if sc else ""
+    if name == "ex10":       # configs[1] (the bench workload)
+        return standard_form_qp(I.ex10_standin(seed=seed, scale=s)), "MIPLIB ex10 LP relaxation (structured stand-in)" + tag
+    if name == "supportcase10":  # configs[3]
+        return (standard_form_qp(I.supportcase10_standin(seed=seed, scale=s)),
+                "MIPLIB supportcase10 LP relaxation (structured stand-in)" + tag)
+    if name == "dense_qp":   # configs[2]: already in standard form (equalities + bounds), natural order
+        n, m = int(round(50_000 * s)), int(round(10_000 * s))
+        return I.dense_qp(n=n, m=m, seed=seed), f"random dense convex QP n={n} m={m}"
+    if name == "neos":       # configs[4]
+        return (standard_form_qp(I.neos5052403_standin(seed=seed, scale=s)),
+                "MIPLIB neos-5052403-cygnet LP relaxation (structured stand-in)" + tag)
     raise ValueError(config)
 
 
@@ -129,6 +139,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-opt", action="store_true", help="skip the wall-clock-to-optimality solve")
+    ap.add_argument("--ordering", type=int, default=None, help="LDL ordering override (0 natural, 1 AMD, 3 ND, 4 auto)")
     ap.add_argument("--mode", choices=["shard", "replicas"], default="shard",
                     help="N > 1: one subtree-sharded solve (RCCL) or N independent replicas")
     args = ap.parse_args()
@@ -152,7 +163,14 @@ def main():
     qp, cfgname = build_problem(args.config)
     comm = RCCLComm.from_torch(dist) if sharded else None
     t_an = time.perf_counter()
-    solver = MPCSolver(qp, comm=comm, **solver_opts())
+    extra = {}
+    if args.config.startswith("dense_qp"):
+        # x first (natural order): the x columns are batched leaves eliminated by one MFMA SYRK; AMD/ND
+        # on the complete bipartite graph of a dense A would only rediscover this order, slowly
+        extra["ordering"] = 0
+    if args.ordering is not None:
+        extra["ordering"] = args.ordering
+    solver = MPCSolver(qp, comm=comm, **solver_opts(), **extra)
     t_analysis = time.perf_counter() - t_an
     info = solver.ldl_info()
 
@@ -211,12 +229,13 @@ def main():
             "config": {"workload": cfgname, "nvar": qp.nvar, "ncon": qp.ncon, "nnzj": qp.nnzj,
                        "kkt_n": info["n"], "nnzL": info["nnzL"], "nnzL_stored": info["nnzL_stored"],
                        "fact_flops": info["flops"], "fronts": info["nsuper"], "levels": info["nlevels"],
+                       "leaf_batch_members": info["lb_members"],
                        "parallelism": (f"subtree-shard{world}" if sharded else f"replicas{world}"), **opt},
             "roofline": roof,
             "kernel_ms_warmup": breakdown,
             "cpu_baseline": None,
         }
-        if not args.no_cpu and world == 1:
+        if not args.no_cpu and world == 1 and not args.config.startswith(("dense_qp", "neos")):
             try:
                 out["cpu_baseline"] = cpu_baseline(qp, solver.kkt_perm(), args.cpu_budget)
             except Exception as e:  # pragma: no cover - reported, not hidden

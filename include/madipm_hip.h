@@ -55,6 +55,8 @@ typedef struct madipm_ldl_info {
   int32_t max_front;       /* largest front order */
   int32_t nbig;            /* fronts handled by the global-memory blocked path */
   int64_t arena_bytes;     /* device bytes for factor + update blocks */
+  int32_t lb_groups;       /* batched leaf-column groups (each absorbed by one SYRK into its parent) */
+  int32_t lb_members;      /* single-column leaf fronts in those groups */
 } madipm_ldl_info;
 
 void madipm_ldl_default_opts(madipm_ldl_opts* opts);
@@ -144,9 +146,10 @@ void madipm_comm_destroy(madipm_comm_t comm);
  * Bit k of `mask` records HIP events around every launch of kernel kind k on the launch stream
  * (kinds: 0 k_asm_chunks, 1 k_assemble, 2 k_tiny_factor, 3 k_small_factor, 4 k_big_diag,
  * 5 k_big_trsm, 6 k_big_update, 7 k_inertia, 8 k_fwd_small, 9 k_fwd_gather, 10 k_fwd_big,
- * 11 k_bwd_below, 12 k_bwd_big, 13 k_bwd_small, 14 k_fwd_tiny, 15 k_bwd_tiny).  Setting a mask
+ * 11 k_bwd_below, 12 k_bwd_big, 13 k_bwd_small, 14 k_fwd_tiny, 15 k_bwd_tiny, 16 k_lb_build,
+ * 17 k_lb_syrk, 18 k_lb_gemv).  Setting a mask
  * clears the statistics. */
-#define MADIPM_NKERNELS 16
+#define MADIPM_NKERNELS 19
 typedef struct madipm_kstat {
   char name[32];
   int64_t launches;

@@ -154,7 +154,9 @@ int madipm_symbolic_info(madipm_symbolic_t sym, madipm_ldl_info* info) {
   info->nlevels = p.nlevels;
   info->max_front = p.max_front;
   info->nbig = p.nbig;
-  info->arena_bytes = p.arena_size * 8;
+  info->arena_bytes = p.arena_size * 8 + p.lb_wsize * 8;
+  info->lb_groups = (int32_t)p.lb.size();
+  info->lb_members = (int32_t)p.lb_mem.size();
   return 0;
   MADIPM_API_END
 }
@@ -332,7 +334,9 @@ int madipm_ldl_get_info(madipm_ldl_t ls, madipm_ldl_info* info) {
   info->nlevels = p.nlevels;
   info->max_front = p.max_front;
   info->nbig = p.nbig;
-  info->arena_bytes = p.arena_size * 8;
+  info->arena_bytes = p.arena_size * 8 + p.lb_wsize * 8;
+  info->lb_groups = (int32_t)p.lb.size();
+  info->lb_members = (int32_t)p.lb_mem.size();
   return 0;
   MADIPM_API_END
 }
@@ -561,7 +565,9 @@ int madipm_solver_ldl_info(madipm_solver_t s, madipm_ldl_info* info) {
   info->nlevels = p.nlevels;
   info->max_front = p.max_front;
   info->nbig = p.nbig;
-  info->arena_bytes = p.arena_size * 8;
+  info->arena_bytes = p.arena_size * 8 + p.lb_wsize * 8;
+  info->lb_groups = (int32_t)p.lb.size();
+  info->lb_members = (int32_t)p.lb_mem.size();
   return 0;
   MADIPM_API_END
 }

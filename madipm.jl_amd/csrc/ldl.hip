@@ -829,6 +829,182 @@ __global__ __launch_bounds__(NT) void k_inertia(const double* __restrict__ D, in
   }
 }
 
+// ------------------------------------------------------------------ batched leaf columns (SymbolicPlan::lb)
+// A group: n single-column leaf fronts c_j under one parent P, W (m x n, ld m) = their K columns on the
+// parent rows gpos, d_j = K(c_j, c_j).  Factor: L(:, c_j) = W(:, j) / d_j, and P absorbs
+// F_P[gpos, gpos] -= W D^{-1} W^T (one SYRK instead of n rank-1 fronts).
+
+// W / d from the caller's values: one workgroup per member column (contiguous CSC run)
+__global__ __launch_bounds__(NT) void k_lb_build(const SymbolicPlan::LBGroup* __restrict__ G,
+                                                 const int32_t* __restrict__ gid, const int32_t* __restrict__ mem,
+                                                 const int64_t* __restrict__ cs, const int64_t* __restrict__ ce,
+                                                 const int64_t* __restrict__ wbase, const int32_t* __restrict__ wrow,
+                                                 const double* __restrict__ Kx, double* __restrict__ W,
+                                                 double* __restrict__ dlb, double* __restrict__ dinv,
+                                                 double* __restrict__ D, LDLStatus* st, double tol) {
+  const int j = blockIdx.x;
+  const SymbolicPlan::LBGroup g = G[gid[j]];
+  double* __restrict__ Wc = W + g.w_off + (int64_t)(j - g.mem_off) * g.m;
+  const int64_t c0 = cs[j], c1 = ce[j];
+  const int32_t* __restrict__ wr = wrow + wbase[j] - c0;
+  for (int64_t e = c0 + threadIdx.x; e < c1; e += NT) {
+    const int k = wr[e];
+    const double v = Kx[e];
+    if (k >= 0) {
+      Wc[k] = v;
+    } else {
+      dlb[j] = v;
+      dinv[j] = 1.0 / v;
+      D[mem[j]] = v;
+      if (bad_pivot(v, tol)) atomicMin(&st->fail_pivot, mem[j] + 1);
+    }
+  }
+}
+
+// F[gpos[a], gpos[b]] -= sum_{j in [k0, k1)} W[a, j] W[b, j] / d_j for a >= b: 128 x 128 output
+// tiles (lower), 4 waves of 64 x 64 (4 x 4 f64 MFMA 16x16x4 blocks each), K staged through LDS
+// 16 columns at a time (double-buffered, operands [k][row] with a padded stride).  One launch per
+// K-chunk keeps the chunk of W (m x 2048) resident in the Infinity Cache across all tiles.
+constexpr int SYT = 128, SYK = 16, SYLD = SYT + 16;
+__global__ __launch_bounds__(NT) void k_lb_syrk(const double* __restrict__ W, const double* __restrict__ dinv, int m,
+                                                int k0, int k1, const int32_t* __restrict__ gpos,
+                                                double* __restrict__ F, int ld) {
+  __shared__ __attribute__((aligned(16))) double As[2][SYK * SYLD];  // (W D^{-1})[I rows]
+  __shared__ __attribute__((aligned(16))) double Bs[2][SYK * SYLD];  // W[J rows]
+  int I = 0, rem = blockIdx.x;
+  while (rem > I) {
+    rem -= I + 1;
+    ++I;
+  }
+  const int J = rem;
+  const int I0 = I * SYT, J0 = J * SYT;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wm = (wv >> 1) * 64, wn = (wv & 1) * 64;  // wave's 64 x 64 quadrant: I rows wm.., J rows wn..
+  const int lr = tid & (SYT - 1), lk = tid >> 7;      // loader: row lr, columns lk + 2q
+  dbl4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+  double ra[8], rb[8];
+  auto gload = [&](int kb) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = kb + lk + 2 * q;
+      const bool ok = k < k1;
+      const int64_t col = (int64_t)(ok ? k : k0) * m;
+      ra[q] = (ok && I0 + lr < m) ? W[(I0 + lr) + col] * dinv[ok ? k : k0] : 0.0;
+      rb[q] = (ok && J0 + lr < m) ? W[(J0 + lr) + col] : 0.0;
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      As[buf][(lk + 2 * q) * SYLD + lr] = ra[q];
+      Bs[buf][(lk + 2 * q) * SYLD + lr] = rb[q];
+    }
+  };
+  gload(k0);
+  sstore(0);
+  __syncthreads();
+  int buf = 0;
+  for (int kb = k0; kb < k1; kb += SYK) {
+    const bool more = kb + SYK < k1;
+    if (more) gload(kb + SYK);
+#pragma unroll
+    for (int k4 = 0; k4 < SYK / 4; ++k4) {
+      const int kk = 4 * k4 + (lane >> 4);
+      double fa[4], fb[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        fa[t] = Bs[buf][kk * SYLD + wn + 16 * t + (lane & 15)];  // A operand: W_J rows (m)
+        fb[t] = As[buf][kk * SYLD + wm + 16 * t + (lane & 15)];  // B operand: (W D^-1)_I rows (n)
+      }
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[a], fb[b], acc[a][b], 0, 0, 0);
+    }
+    if (more) {
+      sstore(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+  // acc[a][b][g]: row i = I0 + wm + 16 b + (lane & 15), column j = J0 + wn + 16 a + (lane >> 4) + 4 g
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int i = I0 + wm + 16 * b + (lane & 15), j = J0 + wn + 16 * a + (lane >> 4) + 4 * g;
+        if (i < m && j <= i) F[gpos[i] + (int64_t)gpos[j] * ld] -= acc[a][b][g];
+      }
+}
+
+// forward: s_j = b(c_j) / d_j, t = W s (two passes: column chunks of LBF_COLS -> partials, then the
+// chunks summed in order), the group's update vector = -t; the members' forward values are b(c_j)
+constexpr int LBF_COLS = 256;
+constexpr int LB_KCHUNK = 2048;  // members per SYRK launch (m x 2048 doubles of W stay cache-resident)
+__global__ __launch_bounds__(NT) void k_lb_fwd1(const double* __restrict__ W, const double* __restrict__ dlb,
+                                                const int32_t* __restrict__ mem, const int32_t* __restrict__ perm,
+                                                int m, int n, int64_t mem0, const double* __restrict__ b,
+                                                double* __restrict__ xi, double* __restrict__ part) {
+  __shared__ double sj[LBF_COLS];
+  const int c0 = blockIdx.y * LBF_COLS;
+  const int nc = min(LBF_COLS, n - c0);
+  if (threadIdx.x < nc) {
+    const int j = c0 + threadIdx.x;
+    const int col = mem[mem0 + j];
+    const double bj = b[perm[col]];
+    sj[threadIdx.x] = bj / dlb[mem0 + j];
+    if (blockIdx.x == 0) xi[col] = bj;
+  }
+  __syncthreads();
+  const int i = blockIdx.x * NT + threadIdx.x;
+  if (i >= m) return;
+  const double* __restrict__ Wc = W + (int64_t)c0 * m + i;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  int j = 0;
+  for (; j + 3 < nc; j += 4) {
+    a0 = fma(Wc[(int64_t)j * m], sj[j], a0);
+    a1 = fma(Wc[(int64_t)(j + 1) * m], sj[j + 1], a1);
+    a2 = fma(Wc[(int64_t)(j + 2) * m], sj[j + 2], a2);
+    a3 = fma(Wc[(int64_t)(j + 3) * m], sj[j + 3], a3);
+  }
+  for (; j < nc; ++j) a0 = fma(Wc[(int64_t)j * m], sj[j], a0);
+  part[(int64_t)blockIdx.y * m + i] = (a0 + a1) + (a2 + a3);
+}
+
+__global__ __launch_bounds__(NT) void k_lb_fwd2(const double* __restrict__ part, int m, int nchunk,
+                                                double* __restrict__ uv) {
+  const int i = blockIdx.x * NT + threadIdx.x;
+  if (i >= m) return;
+  double v = 0.0;
+  for (int c = 0; c < nchunk; ++c) v += part[(int64_t)c * m + i];
+  uv[i] = -v;
+}
+
+// backward: x_j = (y_j - W(:, j)^T x_P(gpos)) / d_j, one wave per member column
+__global__ __launch_bounds__(NT) void k_lb_bwd(const double* __restrict__ W, const double* __restrict__ dlb,
+                                               const int32_t* __restrict__ mem, const int32_t* __restrict__ perm,
+                                               const int32_t* __restrict__ xrow, int m, int n, int64_t mem0,
+                                               double* __restrict__ xi, double* __restrict__ out) {
+  const int j = blockIdx.x * (NT / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (j >= n) return;
+  const double* __restrict__ Wc = W + (int64_t)j * m;
+  double a = 0.0;
+  for (int k = lane; k < m; k += 64) a = fma(Wc[k], xi[xrow[k]], a);
+  a = wave_sum(a);
+  if (lane == 0) {
+    const int col = mem[mem0 + j];
+    const double x = (xi[col] - a) / dlb[mem0 + j];
+    xi[col] = x;
+    out[perm[col]] = x;
+  }
+}
+
 // ------------------------------------------------------------------ solves
 // Multifrontal forward solve per front:  v = [b(own cols); 0] + extend-add of the children's update
 // vectors;  v[0:w] <- L11^{-1} v[0:w];  v[w:] -= L21 v[0:w];  own part -> xi, rest -> update vector.
@@ -1420,7 +1596,40 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     T_.xch = xch_;
     T_.wout = wout_;
   }
-  auto in_phase = [&](int s, int phase) { return phase == 1 ? (!S.top(s) && S.mine(s)) : S.top(s); };
+  auto lb_member = [&](int s) { return !S.lb_of.empty() && S.lb_of[s] >= 0; };
+  auto in_phase = [&](int s, int phase) {
+    if (lb_member(s)) return false;  // batched leaves: W build + the parent's SYRK + GEMV solves
+    return phase == 1 ? (!S.top(s) && S.mine(s)) : S.top(s);
+  };
+  // ---- batched leaf columns
+  lb_at_level_.assign(std::max(NL, 1), {});
+  if (!S.lb.empty()) {
+    lbg_.upload(S.lb);
+    lbmem_.upload(S.lb_mem);
+    std::vector<int32_t> gid(S.lb_mem.size()), xrow;
+    std::vector<int64_t> poff;
+    int64_t np = 0;
+    for (size_t g = 0; g < S.lb.size(); ++g) {
+      const auto& G = S.lb[g];
+      for (int j = 0; j < G.n; ++j) gid[G.mem_off + j] = (int32_t)g;
+      for (int k = 0; k < G.m; ++k) xrow.push_back(S.rows[S.row_ptr[G.parent] + S.lb_gpos[G.gpos_off + k]]);
+      poff.push_back(np);
+      np += (int64_t)cdiv(G.n, LBF_COLS) * G.m;
+      lb_at_level_[S.level[G.parent]].push_back((int)g);
+    }
+    lbgid_.upload(gid);
+    lbxrow_.upload(xrow);
+    lbpoff_.upload(poff);
+    lbcs_.upload(S.lb_cs);
+    lbce_.upload(S.lb_ce);
+    lbwbase_.upload(S.lb_wbase);
+    lbwrow_.upload(S.lb_wrow);
+    lbgpos_.upload(S.lb_gpos);
+    lbW_.alloc(std::max<int64_t>(S.lb_wsize, 1));
+    lbW_.zero();  // the pattern is fixed: entries outside it stay 0
+    lbd_.alloc(2 * S.lb_mem.size());
+    lbpart_.alloc(std::max<int64_t>(np, 1));
+  }
 
   // ---- factorisation launch schedules (phase 1: this shard's subtrees; phase 2: the top fronts)
   std::vector<int32_t> sched;
@@ -1451,8 +1660,22 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     out.push_back(L);
   };
   auto build_fact = [&](int phase, std::vector<Launch>& out) {
+    if (phase == 1 && !S.lb.empty()) {
+      Launch L{LB_BUILD, 0, 0, 0, (int64_t)S.lb_mem.size()};
+      for (const auto& G : S.lb) L.bytes += 8.0 * (double)G.m * G.n * 2.0 + 12.0 * G.n * G.m;
+      out.push_back(L);
+    }
     for (int lev = 0; lev < NL; ++lev) {
       asm_launch(phase == 1 ? lev : NL + 1 + lev, out);
+      if (phase == 1)
+        for (int g : lb_at_level_[lev]) {
+          const auto& G = S.lb[g];
+          Launch L{LB_SYRK, 0, g, 0, 0};
+          L.flops = (double)G.m * (G.m + 1) * (double)G.n;
+          // W once + the parent's lower triangle read-modify-written once per K-chunk
+          L.bytes = 8.0 * (double)G.m * G.n + 16.0 * (double)G.m * (G.m + 1) / 2.0 * cdiv(G.n, LB_KCHUNK);
+          out.push_back(L);
+        }
       std::vector<int32_t> cls[3], big;
       for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
         const int s = S.level_list[q];
@@ -1671,7 +1894,7 @@ const char* kernel_kind_name(int k) {
   static const char* names[KK_COUNT] = {"k_asm_chunks", "k_assemble",  "k_tiny_factor", "k_small_factor", "k_big_diag",
                                         "k_big_trsm",   "k_big_update", "k_inertia",    "k_fwd_small",    "k_fwd_gather",
                                         "k_fwd_big",    "k_bwd_below",  "k_bwd_big",    "k_bwd_small",
-                                        "k_fwd_tiny",   "k_bwd_tiny"};
+                                        "k_fwd_tiny",   "k_bwd_tiny",   "k_lb_build",   "k_lb_syrk",      "k_lb_gemv"};
   return (k >= 0 && k < KK_COUNT) ? names[k] : "?";
 }
 
@@ -1719,6 +1942,41 @@ void LDLSolver::kernel_stats(KernelStat out[KK_COUNT]) {
   for (int k = 0; k < KK_COUNT; ++k) out[k] = kst_[k];
 }
 
+// F_P[gpos, gpos] -= W D^{-1} W^T, one launch per K-chunk of LB_KCHUNK members
+void LDLSolver::lb_syrk(int g, hipStream_t s) {
+  const auto& G = S_.lb[g];
+  const int P = G.parent;
+  double* F = S_.is_big[P] ? arena_.p + S_.l_off[P] : fscratch_.p + S_.fs_off[P];
+  const int nt = (int)cdiv(G.m, SYT);
+  const unsigned ntile = (unsigned)(nt * (nt + 1) / 2);
+  const double* dinv = lbd_.p + S_.lb_mem.size() + G.mem_off;
+  for (int k0 = 0; k0 < G.n; k0 += LB_KCHUNK)
+    k_lb_syrk<<<ntile, NT, 0, s>>>(lbW_.p + G.w_off, dinv, G.m, k0, std::min(G.n, k0 + LB_KCHUNK),
+                                   lbgpos_.p + G.gpos_off, F, S_.nrows[P]);
+}
+
+void LDLSolver::lb_fwd(const double* b, hipStream_t s) {
+  for (size_t g = 0; g < S_.lb.size(); ++g) {
+    const auto& G = S_.lb[g];
+    const int nch = (int)cdiv(G.n, LBF_COLS);
+    int64_t poff = 0;
+    for (size_t h = 0; h < g; ++h) poff += cdiv(S_.lb[h].n, LBF_COLS) * S_.lb[h].m;
+    TIMED(KK_LB_GEMV, 8.0 * G.m * (double)G.n, 2.0 * G.m * (double)G.n,
+          (k_lb_fwd1<<<dim3((unsigned)cdiv(G.m, NT), (unsigned)nch), NT, 0, s>>>(
+              lbW_.p + G.w_off, lbd_, lbmem_, perm_, G.m, G.n, G.mem_off, b, xi_, lbpart_.p + poff)));
+    k_lb_fwd2<<<(unsigned)cdiv(G.m, NT), NT, 0, s>>>(lbpart_.p + poff, G.m, nch, uvec_.p + G.uvec_off);
+  }
+}
+
+void LDLSolver::lb_bwd(int g, double* b, hipStream_t s) {
+  const auto& G = S_.lb[g];
+  int64_t xoff = 0;
+  for (int h = 0; h < g; ++h) xoff += S_.lb[h].m;
+  TIMED(KK_LB_GEMV, 8.0 * G.m * (double)G.n, 2.0 * G.m * (double)G.n,
+        (k_lb_bwd<<<(unsigned)cdiv(G.n, NT / 64), NT, 0, s>>>(lbW_.p + G.w_off, lbd_, lbmem_, perm_, lbxrow_.p + xoff,
+                                                             G.m, G.n, G.mem_off, xi_, b)));
+}
+
 void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStream_t s) {
   for (const Launch& L : LL) {
     const int32_t* list = sched_.p + L.off;
@@ -1751,6 +2009,14 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
         break;
       case BIG_UPDATE:
         TIMED(KK_UPDATE, L.bytes, L.flops, (k_big_update<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_)));
+        break;
+      case LB_BUILD:
+        TIMED(KK_LB_BUILD, L.bytes, 0.0,
+              (k_lb_build<<<(unsigned)L.items, NT, 0, s>>>(lbg_, lbgid_, lbmem_, lbcs_, lbce_, lbwbase_, lbwrow_, Kx, lbW_,
+                                                          lbd_.p, lbd_.p + S_.lb_mem.size(), D_, status_, pivot_tol)));
+        break;
+      case LB_SYRK:
+        TIMED(KK_LB_SYRK, L.bytes, L.flops, lb_syrk((int)L.off, s));
         break;
     }
   }
@@ -1812,6 +2078,7 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
   const SolveTask* tasks = reinterpret_cast<const SolveTask*>(tasks_.p);
   const int efwd = 2 * epoch_ - 1;
   int32_t* cnt = counters_.p + phase * 2 * S_.nlevels;
+  if (phase == 0 && !S_.lb.empty()) lb_fwd(b, s);
   for (int lev = 0; lev < (int)V.size(); ++lev) {
     const SolveLevel& L = V[lev];
     if (L.ntiny)
@@ -1854,6 +2121,8 @@ void LDLSolver::bwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
       TIMED(KK_BWD_TINY, L.tiny_bytes, L.tiny_flops,
             (k_bwd_tiny<<<(unsigned)cdiv(L.ntiny, 2 * SW), NT, 0, s>>>(T_, sched_.p + L.tiny_off, L.ntiny, arena_, D_, xi_,
                                                                       b)));
+    if (phase == 0)
+      for (int g : lb_at_level_[lev]) lb_bwd(g, b, s);
   }
 }
 

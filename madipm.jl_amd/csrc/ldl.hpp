@@ -59,6 +59,7 @@ struct LDLStatus {  // device-resident, read back by status()
 enum KernelKind {
   KK_ASM_CHUNKS = 0, KK_ASSEMBLE, KK_TINY, KK_SMALL, KK_DIAG, KK_TRSM, KK_UPDATE, KK_INERTIA,
   KK_FWD_SMALL, KK_FWD_GATHER, KK_FWD_BIG, KK_BWD_BELOW, KK_BWD_BIG, KK_BWD_SMALL, KK_FWD_TINY, KK_BWD_TINY,
+  KK_LB_BUILD, KK_LB_SYRK, KK_LB_GEMV,
   KK_COUNT
 };
 const char* kernel_kind_name(int k);
@@ -138,7 +139,8 @@ class LDLSolver : public LinSolver {
   void kernel_stats(KernelStat out[KK_COUNT]) override;
 
  private:
-  enum Kind { ASSEMBLE = 0, SMALL32 = 1, SMALL64 = 2, SMALL128 = 3, BIG_DIAG = 4, BIG_TRSM = 5, BIG_UPDATE = 6 };
+  enum Kind { ASSEMBLE = 0, SMALL32 = 1, SMALL64 = 2, SMALL128 = 3, BIG_DIAG = 4, BIG_TRSM = 5, BIG_UPDATE = 6,
+              LB_BUILD = 7, LB_SYRK = 8 };
   struct Launch {
     int kind;
     int step;       // panel step for BIG_DIAG / BIG_TRSM / BIG_UPDATE
@@ -181,6 +183,15 @@ class LDLSolver : public LinSolver {
   void fwd_levels(const std::vector<SolveLevel>& V, int phase, double* b, hipStream_t s);
   void bwd_levels(const std::vector<SolveLevel>& V, int phase, double* b, hipStream_t s);
   DBuf<int64_t> xoff_, sx_ptr_, sx_src_;
+  // batched leaf columns (SymbolicPlan::lb): W, pivots, member tables, per-level launch lists
+  DBuf<double> lbW_, lbd_, lbpart_;
+  DBuf<int32_t> lbmem_, lbgid_, lbwrow_, lbgpos_, lbxrow_;
+  DBuf<int64_t> lbcs_, lbce_, lbwbase_, lbpoff_;
+  DBuf<SymbolicPlan::LBGroup> lbg_;
+  std::vector<std::vector<int>> lb_at_level_;
+  void lb_syrk(int g, hipStream_t s);
+  void lb_fwd(const double* b, hipStream_t s);
+  void lb_bwd(int g, double* b, hipStream_t s);
   DBuf<double> xch_;
   DBuf<uint8_t> wout_, colmask_;
   DBuf<int32_t> tasks_, flags_, flag_off_, counters_, err_, bp_off_;

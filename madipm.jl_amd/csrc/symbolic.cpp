@@ -260,6 +260,22 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     }
   }
 
+  // ---------------- 3b. batched-leaf candidates: single-column etree leaves with a large update,
+  // many under the same parent column (a QP with a diagonal Hessian and dense A: every x_j).  They
+  // are kept out of relaxed amalgamation; step 6b decides the groups.
+  std::vector<uint8_t> lbcand(N, 0);
+  const bool use_lb = opt.leaf_batch && opt.nshards <= 1;
+  if (use_lb) {
+    std::vector<int32_t> npar(N, 0);
+    for (const SN& f : fund)
+      if (f.w == 1 && nchild[f.first] == 0 && f.r - 1 >= opt.lb_min_rows && parent[f.first] != -1)
+        npar[parent[f.first]]++;
+    for (const SN& f : fund)
+      if (f.w == 1 && nchild[f.first] == 0 && f.r - 1 >= opt.lb_min_rows && parent[f.first] != -1 &&
+          npar[parent[f.first]] >= opt.lb_min_count)
+        lbcand[f.first] = 1;
+  }
+
   // ---------------- 4. relaxed amalgamation (merge a front with its column-adjacent child)
   std::vector<SN> sn;
   sn.reserve(fund.size());
@@ -269,6 +285,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       const SN& c = sn.back();
       int clast = c.first + c.w - 1;
       if (clast + 1 != p.first) break;
+      if (lbcand[c.first] || lbcand[p.first]) break;  // batched-leaf candidates stay single columns
       int par = parent[clast];
       if (par < p.first || par >= p.first + p.w) break;
       int64_t ncols = c.w + p.w;
@@ -376,7 +393,80 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     }
   }
 
+  // ---------------- 6b. batched-leaf groups: per parent, its candidate children whose K column is one
+  // CSC column of the caller (diagonal + rows below, none to its left) and whose rows cover at least
+  // lb_min_density of the union of their rows
+  S.lb.clear();
+  S.lb_of.assign(ns, -1);
+  if (use_lb) {
+    std::vector<uint8_t> has_left(N, 0);
+    for (int j = 0; j < N; ++j)
+      for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p)
+        if (rowval[p] != j) has_left[rowval[p]] = 1;
+    std::vector<int32_t> mark(std::max(1, ns), -1), pos_in_u;
+    for (int s = 0; s < ns; ++s) {
+      std::vector<int32_t> mem;
+      for (int64_t q = S.child_ptr[s]; q < S.child_ptr[s + 1]; ++q) {
+        const int c = S.child_list[q];
+        const int oc = perm[S.first[c]];
+        if (S.first[c + 1] - S.first[c] == 1 && lbcand[S.first[c]] && !has_left[oc] &&
+            S.child_ptr[c + 1] == S.child_ptr[c])
+          mem.push_back(c);
+      }
+      if ((int)mem.size() < opt.lb_min_count) continue;
+      // union of their parent-local rows
+      std::vector<int32_t> U;
+      int64_t tot = 0;
+      for (int c : mem) {
+        const int uc = S.nrows[c] - 1;
+        tot += uc;
+        for (int a = 0; a < uc; ++a) {
+          const int pr = S.rel[S.rel_ptr[c] + a];
+          U.push_back(pr);
+        }
+      }
+      std::sort(U.begin(), U.end());
+      U.erase(std::unique(U.begin(), U.end()), U.end());
+      const double dens = (double)tot / ((double)U.size() * (double)mem.size());
+      if (dens < opt.lb_min_density) continue;
+      SymbolicPlan::LBGroup g{};
+      g.parent = s;
+      g.m = (int32_t)U.size();
+      g.n = (int32_t)mem.size();
+      g.w_off = S.lb_wsize;
+      g.mem_off = (int64_t)S.lb_mem.size();
+      g.gpos_off = (int64_t)S.lb_gpos.size();
+      S.lb_wsize += (int64_t)g.m * g.n;
+      S.lb_gpos.insert(S.lb_gpos.end(), U.begin(), U.end());
+      pos_in_u.assign(S.nrows[s], -1);
+      for (int k = 0; k < g.m; ++k) pos_in_u[U[k]] = k;
+      // parent-local position of every permuted row of the parent
+      for (int64_t t = S.row_ptr[s]; t < S.row_ptr[s + 1]; ++t) pos[S.rows[t]] = (int32_t)(t - S.row_ptr[s]);
+      for (int c : mem) {
+        const int oc = perm[S.first[c]];
+        S.lb_of[c] = (int32_t)S.lb.size();
+        S.lb_mem.push_back(S.first[c]);
+        S.lb_cs.push_back(colptr[oc]);
+        S.lb_ce.push_back(colptr[oc + 1]);
+        S.lb_wbase.push_back((int64_t)S.lb_wrow.size());
+        for (int64_t e = colptr[oc]; e < colptr[oc + 1]; ++e) {
+          const int i = rowval[e];
+          if (i == oc) {
+            S.lb_wrow.push_back(-1);
+          } else {
+            const int lr = pos[pinv[i]];
+            MADIPM_REQUIRE(lr >= 0 && pos_in_u[lr] >= 0, "batched leaf: row outside its parent");
+            S.lb_wrow.push_back(pos_in_u[lr]);
+          }
+        }
+      }
+      S.lb.push_back(g);
+    }
+  }
+  auto lb_member = [&](int s) { return !S.lb_of.empty() && S.lb_of[s] >= 0; };
+
   // ---------------- 7. assembly map: caller's CSC entry -> (front, local offset)
+  // (entries of batched-leaf members are read by the W build instead)
   S.asm_ptr.assign(ns + 1, 0);
   std::vector<int32_t> ea(nnz), eb(nnz);
   for (int j = 0; j < N; ++j)
@@ -385,15 +475,21 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       if (a < b) std::swap(a, b);
       ea[p] = a;
       eb[p] = b;
+      if (lb_member(col2sn[b])) {
+        eb[p] = -1;
+        continue;
+      }
       S.asm_ptr[col2sn[b] + 1]++;
     }
   for (int s = 0; s < ns; ++s) S.asm_ptr[s + 1] += S.asm_ptr[s];
-  S.asm_src.resize(nnz);
-  S.asm_dst.resize(nnz);
+  const int64_t nasm = S.asm_ptr[ns];
+  S.asm_src.resize(nasm);
+  S.asm_dst.resize(nasm);
   {
-    std::vector<int64_t> byfront(nnz);
+    std::vector<int64_t> byfront(nasm);
     std::vector<int64_t> fillp(S.asm_ptr.begin(), S.asm_ptr.end() - 1);
-    for (int64_t p = 0; p < nnz; ++p) byfront[fillp[col2sn[eb[p]]]++] = p;
+    for (int64_t p = 0; p < nnz; ++p)
+      if (eb[p] >= 0) byfront[fillp[col2sn[eb[p]]]++] = p;
     for (int s = 0; s < ns; ++s) {
       int r = S.nrows[s];
       for (int64_t t = S.row_ptr[s]; t < S.row_ptr[s + 1]; ++t) pos[S.rows[t]] = (int32_t)(t - S.row_ptr[s]);
@@ -546,6 +642,12 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       S.flops += (cc - 1.0) * (cc + 2.0);
     }
     S.uvec_off[s] = ucur;
+    if (lb_member(s)) {  // batched leaf: factor lives in its group's W (no front storage, no update vector)
+      S.is_big[s] = 0;
+      S.l_off[s] = S.u_off[s] = cur;
+      S.u_ld[s] = 1;
+      continue;
+    }
     ucur += r - w;
     if (r <= opt.small_front_max && !S.top(s)) {
       S.is_big[s] = 0;
@@ -566,6 +668,10 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   }
   if (ntop_begin == storage_order.size()) S.top_lo = cur;
   S.top_hi = cur;
+  for (auto& g : S.lb) {  // the groups' forward update vectors (gathered by the parent like a child's)
+    g.uvec_off = ucur;
+    ucur += g.m;
+  }
   if (S.nshards > 1) cur += 4 * S.nshards;  // status slots, all-reduced with the top fronts
   S.arena_size = cur;
   S.uvec_size = ucur;
@@ -597,6 +703,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     // children of s whose update blocks this assembly reads: 0 all, 1 top children only, 2 this
     // shard's subtree children only
     auto child_ok = [&](int c, int which) {
+      if (lb_member(c)) return false;  // batched leaves: absorbed by the group SYRK
       if (which == 0) return true;
       if (which == 1) return S.top(c);
       return !S.top(c) && S.owner[c] == S.shard;
@@ -693,7 +800,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     for (int lev = 0; lev < NL; ++lev) {
       for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
         const int s = S.level_list[q];
-        if (S.top(s) || !S.mine(s)) continue;
+        if (S.top(s) || !S.mine(s) || lb_member(s)) continue;
         if (!S.is_big[s] && S.fs_off[s] < 0) continue;
         emit(s, true, 0, false, true);
       }
@@ -718,7 +825,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   // ---------------- 11. forward-solve gather lists (child order).  Sharded: a top front's rows list
   // only its top children (sv); its subtree-root children of this shard are listed in sx (the
   // external forward contribution, exchanged before the top forward solve).
-  auto sv_child_ok = [&](int s, int c) { return !S.top(s) || S.top(c); };
+  auto sv_child_ok = [&](int s, int c) { return !lb_member(c) && (!S.top(s) || S.top(c)); };
   S.sv_ptr.assign(S.row_ptr[ns] + 1, 0);
   for (int s = 0; s < ns; ++s)
     for (int64_t qc = S.child_ptr[s]; qc < S.child_ptr[s + 1]; ++qc) {
@@ -727,6 +834,8 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       const int uc = S.nrows[c] - (S.first[c + 1] - S.first[c]);
       for (int aa = 0; aa < uc; ++aa) S.sv_ptr[S.row_ptr[s] + S.rel[S.rel_ptr[c] + aa] + 1]++;
     }
+  for (const auto& g : S.lb)
+    for (int k = 0; k < g.m; ++k) S.sv_ptr[S.row_ptr[g.parent] + S.lb_gpos[g.gpos_off + k] + 1]++;
   for (int64_t t = 0; t < S.row_ptr[ns]; ++t) S.sv_ptr[t + 1] += S.sv_ptr[t];
   S.sv_src.assign(S.sv_ptr[S.row_ptr[ns]], 0);
   {
@@ -738,6 +847,8 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         const int uc = S.nrows[c] - (S.first[c + 1] - S.first[c]);
         for (int aa = 0; aa < uc; ++aa) S.sv_src[fill[S.row_ptr[s] + S.rel[S.rel_ptr[c] + aa]]++] = S.uvec_off[c] + aa;
       }
+    for (const auto& g : S.lb)  // after the regular children (fixed order)
+      for (int k = 0; k < g.m; ++k) S.sv_src[fill[S.row_ptr[g.parent] + S.lb_gpos[g.gpos_off + k]]++] = g.uvec_off + k;
   }
   S.xoff.assign(ns, -1);
   S.xlen = 0;

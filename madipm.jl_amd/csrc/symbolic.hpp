@@ -39,6 +39,13 @@ struct SymbolicOptions {
   // by every shard after one all-reduce of the top fronts' external contributions.
   int nshards = 1;
   int shard = 0;
+  // batched leaf columns (dense-column QPs): single-column leaf fronts with >= lb_min_rows update
+  // rows, >= lb_min_count of them under one parent and dense enough, are not factorised one by one:
+  // their parent absorbs F -= W D^{-1} W^T in one MFMA SYRK (W = their K columns).  Unsharded only.
+  int leaf_batch = 1;
+  int lb_min_rows = 128;
+  int lb_min_count = 64;
+  double lb_min_density = 0.5;
 };
 
 struct SymbolicPlan {
@@ -103,6 +110,22 @@ struct SymbolicPlan {
   int64_t xlen = 0;                    // sum of the top fronts' orders
   std::vector<int64_t> sx_ptr, sx_src; // top rows (xoff[s] + i): this shard's subtree-root updates
   double top_cost = 0, shard_cost_max = 0, shard_cost_sum = 0;  // partition statistics
+  // batched leaf columns: group g = members lb_mem[mem_off .. mem_off + n) (pivot columns, permuted
+  // ids) under front `parent`; W (m x n, col-major, ld m) holds their K columns on the rows
+  // gpos[gpos_off .. + m) of the parent (sorted local rows); the group's forward update vector lives
+  // at uvec[uvec_off ..) and is gathered by the parent like a child's.
+  struct LBGroup {
+    int32_t parent, m, n, pad;
+    int64_t w_off, mem_off, gpos_off, uvec_off;
+  };
+  std::vector<LBGroup> lb;
+  std::vector<int32_t> lb_of;          // per front: group id, -1 if not a member
+  std::vector<int32_t> lb_mem;         // member pivot columns
+  std::vector<int64_t> lb_cs, lb_ce;   // member j: its entries are the caller's CSC entries [cs, ce)
+  std::vector<int64_t> lb_wbase;       // member j: lb_wrow[wbase + (e - cs)] = W row of entry e (-1: diagonal)
+  std::vector<int32_t> lb_wrow;
+  std::vector<int32_t> lb_gpos;
+  int64_t lb_wsize = 0;
   bool mine(int s) const { return owner.empty() || owner[s] == shard; }
   bool top(int s) const { return !owner.empty() && owner[s] < 0; }
   // statistics

@@ -164,14 +164,46 @@ def ex10_standin(seed=0, scale=1.0) -> QuadraticModel:
 
 
 def dense_qp(n=50_000, m=10_000, seed=0) -> QuadraticModel:
-    """BASELINE.json configs[2]: random dense convex QP, A dense N(0,1), H = diag(U[1e-2,1]), 0<=x<=10."""
+    """BASELINE.json configs[2]: random dense convex QP, A dense N(0,1) (m x n), H = diag(U[1e-2,1]),
+    0 <= x <= 10, b = A x0 with x0 ~ U[0,10] (feasible), c ~ N(0,1).  Generated in float64 with int32
+    COO indices, column-major (A's columns contiguous), so the full size (5e8 entries) stays ~8 GB."""
     rng = np.random.default_rng(seed)
-    A = rng.standard_normal((m, n))
     x0 = rng.uniform(0.0, 10.0, n)
-    b = A @ x0
     h = rng.uniform(1e-2, 1.0, n)
     c = rng.standard_normal(n)
-    ar, ac = np.nonzero(np.ones((m, n), bool))
-    return QuadraticModel(c=c, Hrows=np.arange(n), Hcols=np.arange(n), Hvals=h, Arows=ar, Acols=ac,
-                          Avals=A.ravel(), lcon=b, ucon=b.copy(), lvar=np.zeros(n), uvar=np.full(n, 10.0),
-                          name=f"dense_qp_{n}x{m}")
+    vals = np.empty(m * n)
+    b = np.zeros(m)
+    cb = max(1, (1 << 24) // m)                       # columns per generation block
+    for j0 in range(0, n, cb):
+        j1 = min(n, j0 + cb)
+        blk = rng.standard_normal((j1 - j0, m))       # rows = columns of A
+        vals[j0 * m:j1 * m] = blk.ravel()
+        b += blk.T @ x0[j0:j1]
+    ar = np.tile(np.arange(m, dtype=np.int32), n)
+    ac = np.repeat(np.arange(n, dtype=np.int32), m)
+    return QuadraticModel(c=c, Hrows=np.arange(n, dtype=np.int32), Hcols=np.arange(n, dtype=np.int32), Hvals=h,
+                          Arows=ar, Acols=ac, Avals=vals, lcon=b, ucon=b.copy(), lvar=np.zeros(n),
+                          uvar=np.full(n, 10.0), name=f"dense_qp_{n}x{m}")
+
+
+def supportcase10_standin(seed=0, scale=1.0, block_scale=1.0) -> QuadraticModel:
+    """MIPLIB supportcase10 LP-relaxation stand-in (BASELINE.json configs[3]): ~165.7k rows x 14.8k
+    [0,1] columns, ~555k nnz (catalogue shape, recalled) — many short rows.  64 blocks of
+    2589 rows x 231 columns at 3 nnz/row + 48 coupling rows.  After standard_form_qp: ~180k variables,
+    ~166k constraints (K2 of order ~346k): the large, HBM-bound KKT of the north star."""
+    nblocks = max(2, int(round(64 * scale)))
+    return packing_lp(nblocks=nblocks, rows_per_block=max(8, int(2589 * block_scale)),
+                      cols_per_block=max(4, int(231 * block_scale)), ncoupling=max(2, int(48 * block_scale)),
+                      nnz_per_row=3, seed=seed, coupling_density=0.002, name=f"supportcase10_standin_s{seed}")
+
+
+def neos5052403_standin(seed=0, scale=1.0, block_scale=1.0) -> QuadraticModel:
+    """MIPLIB neos-5052403-cygnet LP-relaxation stand-in (BASELINE.json configs[4]): ~38.3k rows x
+    32.9k columns, ~4.9M nnz (catalogue shape, recalled) — dense rows, wide separators: the config the
+    north star shards across GPUs.  16 blocks of 2370 rows x 2054 columns at 120 nnz/row + 348
+    coupling rows (1% dense)."""
+    nblocks = max(2, int(round(16 * scale)))
+    return packing_lp(nblocks=nblocks, rows_per_block=max(8, int(2370 * block_scale)),
+                      cols_per_block=max(8, int(2054 * block_scale)), ncoupling=max(2, int(348 * block_scale)),
+                      nnz_per_row=max(4, int(120 * block_scale)), seed=seed, coupling_density=0.01,
+                      name=f"neos5052403_standin_s{seed}")

@@ -188,3 +188,36 @@ def test_normal_kkt_rejects_qp():
     from madipm_amd.instances import random_qp
     with pytest.raises(Exception, match="only linear programs"):
         MPCSolver(random_qp(10, 20, 0.2, 0), kkt_system=NormalKKTSystem)
+
+
+# ---------------------------------------------------------------- BASELINE.json configs 4 / 5
+# The supportcase10 (many short rows) and neos-5052403 (dense rows, wide separators) stand-ins at a
+# scale the oracle solves in seconds; bench.py --config supportcase10 / neos runs the full sizes.
+@pytest.mark.parametrize("name,kw", [("supportcase10_standin", dict(scale=0.1, block_scale=0.3)),
+                                     ("neos5052403_standin", dict(scale=0.25, block_scale=0.15))])
+def test_config_standins_parity(name, kw):
+    from madipm_amd import FixedRegularization, standard_form_qp, MPCSolver
+    from madipm_amd import instances as I
+    qp = standard_form_qp(getattr(I, name)(**kw))
+    opts = dict(regularization=FixedRegularization(1e-8, -1e-8), max_iter=300)
+    gpu, ref = _compare(qp, **opts)
+    # the subtree-sharded factorisation (4 shards on this device) follows the same trajectory
+    sh = MPCSolver(qp, nshards=4, **opts).solve()
+    assert sh.status == gpu.status and abs(sh.iter - gpu.iter) <= 1
+    assert abs(sh.objective - gpu.objective) <= 1e-8 * max(1.0, abs(gpu.objective))
+
+
+def test_dense_qp_batched_leaves():
+    """BASELINE.json configs[2] (dense convex QP) at a size the oracle solves in seconds: the x
+    columns are eliminated as batched leaves (MFMA SYRK)."""
+    from madipm_amd import FixedRegularization, MPCSolver
+    from madipm_amd.instances import dense_qp
+    qp = dense_qp(n=1200, m=200, seed=0)
+    opts = dict(regularization=FixedRegularization(1e-8, -1e-8), max_iter=300, ordering=0)
+    s = MPCSolver(qp, **opts)
+    assert s.ldl_info()["lb_members"] >= 600
+    gpu = s.solve()
+    ref = OracleMPC(qp, _oracle_opts(opts)).solve()
+    assert gpu.status == ref.status == 1
+    assert abs(gpu.iter - ref.iter) <= 1
+    assert abs(gpu.objective - ref.objective) <= 1e-6 * max(1.0, abs(ref.objective))
