@@ -210,6 +210,165 @@ __global__ __launch_bounds__(NT) void k_small_factor(FrontTab T, const int32_t* 
   }
 }
 
+// ------------------------------------------------------------------ micro fronts (w <= 2, r <= 32)
+// The leaf level of the K2 trees (~1e5 fronts: one or two x columns and their rows).  16 lanes per
+// front, 16 fronts per workgroup, lane l owns rows l and l + 16; no frontal matrix: a leaf's original
+// entries live in its pivot columns only, so L = F(:, 0:w) D^-1 (2 x 2 block at most) and the update
+// block is U = -L D L^T (rows >= w), written column by column, coalesced over the group's lanes.
+constexpr int MG = 16;
+__global__ __launch_bounds__(NT) void k_micro_factor(FrontTab T, const int32_t* __restrict__ fronts, int nf,
+                                                     const double* __restrict__ Kx, double* __restrict__ arena,
+                                                     double* __restrict__ D, LDLStatus* st, double tol) {
+  __shared__ double Fs[NT / MG][64];  // columns 0 / 1 of F (rows 0..31); later l_i0 d0 / l_i1 d1
+  const int g = threadIdx.x / MG, l = threadIdx.x & (MG - 1);
+  const int q = blockIdx.x * (NT / MG) + g;
+  const bool live = q < nf;
+  const int s = fronts[live ? q : nf - 1];
+  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+  double* F = Fs[g];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) F[l + 16 * k] = 0.0;
+  wave_sync();
+  for (int64_t e = T.asm_ptr[s] + l; e < T.asm_ptr[s + 1]; e += MG) {
+    const int64_t d = T.asm_dst[e];
+    const int lc = (int)(d / r), lr = (int)(d - (int64_t)lc * r);
+    F[lr + 32 * lc] = Kx[T.asm_src[e]];
+  }
+  wave_sync();
+  const double d0 = F[0];
+  const double f10 = F[1];
+  const double l10 = (w == 2) ? f10 / d0 : 0.0;
+  const double d1 = (w == 2) ? F[33] - l10 * f10 : 0.0;
+  double li0[2], li1[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int i = l + 16 * h;
+    li0[h] = 0.0;
+    li1[h] = 0.0;
+    if (i >= w && i < r) {
+      li0[h] = F[i] / d0;
+      if (w == 2) li1[h] = (F[32 + i] - li0[h] * f10) / d1;
+    }
+  }
+  wave_sync();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {  // scaled columns for the update: U_ab = -(l_a0 (d0 l_b0) + l_a1 (d1 l_b1))
+    const int i = l + 16 * h;
+    F[i] = li0[h] * d0;
+    F[32 + i] = li1[h] * d1;
+  }
+  wave_sync();
+  if (!live) return;
+  double* __restrict__ L = arena + T.l_off[s];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int i = l + 16 * h;
+    if (i < r) {
+      L[i] = (i == 0) ? d0 : (i >= w ? li0[h] : l10);
+      if (w == 2) L[i + r] = (i == 0) ? 0.0 : (i == 1 ? d1 : li1[h]);
+    }
+  }
+  if (l == 0) {
+    D[f0] = d0;
+    if (bad_pivot(d0, tol)) atomicMin(&st->fail_pivot, f0 + 1);
+    if (w == 2) {
+      D[f0 + 1] = d1;
+      if (bad_pivot(d1, tol)) atomicMin(&st->fail_pivot, f0 + 2);
+    }
+  }
+  const int u = r - w;
+  double* __restrict__ Uo = arena + T.u_off[s];
+  for (int b = 0; b < u; ++b) {
+    const double sb0 = F[w + b], sb1 = F[32 + w + b];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int a = l + 16 * h - w;  // U row of this lane's row
+      if (a >= b && a < u) Uo[a + (int64_t)b * u] = -(li0[h] * sb0 + li1[h] * sb1);
+    }
+  }
+}
+
+// forward / backward solves of micro fronts (same lane layout); x_0, x_1 broadcast within the group
+__global__ __launch_bounds__(NT) void k_fwd_micro(FrontTab T, const int32_t* __restrict__ fronts, int nf,
+                                                  const double* __restrict__ arena, const double* __restrict__ b,
+                                                  double* __restrict__ xi, double* __restrict__ uvec) {
+  const int g = threadIdx.x / MG, l = threadIdx.x & (MG - 1);
+  const int q = blockIdx.x * (NT / MG) + g;
+  const bool live = q < nf;
+  const int s = fronts[live ? q : nf - 1];
+  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+  const double* __restrict__ L = arena + T.l_off[s];
+  double v[2], c0[2], c1[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int i = l + 16 * h;
+    double vi = 0.0, a0 = 0.0, a1 = 0.0;
+    if (i < r) {
+      vi = fwd_init(T, s, i, w, f0, b);
+      const int64_t e = T.row_ptr[s] + i;
+      const int64_t p1 = T.sv_ptr[e + 1];
+      for (int64_t p = T.sv_ptr[e]; p < p1; ++p) vi += uvec[T.sv_src[p]];
+      a0 = L[i];
+      if (w == 2) a1 = L[i + r];
+    }
+    v[h] = vi;
+    c0[h] = a0;
+    c1[h] = a1;
+  }
+  const double x0 = __shfl(v[0], 0, MG);
+  const double l10 = __shfl(c0[0], 1, MG);
+  const double x1 = (w == 2) ? __shfl(v[0], 1, MG) - l10 * x0 : 0.0;
+  if (!live) return;
+  double* __restrict__ uo = uvec + T.uvec_off[s];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int i = l + 16 * h;
+    if (i < w) {
+      xi[f0 + i] = (i == 0) ? x0 : x1;
+    } else if (i < r) {
+      uo[i - w] = (v[h] - c0[h] * x0) - c1[h] * x1;
+    }
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_bwd_micro(FrontTab T, const int32_t* __restrict__ fronts, int nf,
+                                                  const double* __restrict__ arena, const double* __restrict__ D,
+                                                  double* __restrict__ xi, double* __restrict__ out) {
+  const int g = threadIdx.x / MG, l = threadIdx.x & (MG - 1);
+  const int q = blockIdx.x * (NT / MG) + g;
+  const bool live = q < nf;
+  const int s = fronts[live ? q : nf - 1];
+  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+  const double* __restrict__ L = arena + T.l_off[s];
+  const int32_t* __restrict__ rows = T.rows + T.row_ptr[s];
+  double a0 = 0.0, a1 = 0.0, l10 = 0.0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int i = l + 16 * h;
+    if (i >= w && i < r) {
+      const double x = xi[rows[i]];  // final: ancestors
+      a0 = fma(L[i], x, a0);
+      if (w == 2) a1 = fma(L[i + r], x, a1);
+    }
+    if (i == 1 && w == 2) l10 = L[1];
+  }
+#pragma unroll
+  for (int o = MG / 2; o > 0; o >>= 1) {
+    a0 += __shfl_xor(a0, o, MG);
+    a1 += __shfl_xor(a1, o, MG);
+  }
+  l10 = __shfl(l10, 1, MG);
+  if (!live || l != 0) return;
+  const double v1 = (w == 2) ? xi[f0 + 1] / D[f0 + 1] - a1 : 0.0;
+  const double v0 = xi[f0] / D[f0] - a0 - l10 * v1;
+  xi[f0] = v0;
+  if (T.wout[s]) out[T.perm[f0]] = v0;
+  if (w == 2) {
+    xi[f0 + 1] = v1;
+    if (T.wout[s]) out[T.perm[f0 + 1]] = v1;
+  }
+}
+
 // Fronts with r <= 32: one WAVE per front, 4 fronts per workgroup (the leaf level has ~10^5 of them).
 // Lane l works on row l & 31 and the columns of parity l >> 5; wave-synchronous right-looking LDL^T.
 constexpr int TINY = 32;
@@ -1676,15 +1835,27 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
           L.bytes = 8.0 * (double)G.m * G.n + 16.0 * (double)G.m * (G.m + 1) / 2.0 * cdiv(G.n, LB_KCHUNK);
           out.push_back(L);
         }
-      std::vector<int32_t> cls[3], big;
+      std::vector<int32_t> cls[3], big, micro;
       for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
         const int s = S.level_list[q];
         if (!in_phase(s, phase)) continue;
-        const int r = S.nrows[s];
-        if (!S.is_big[s])
+        const int r = S.nrows[s], w = S.first[s + 1] - S.first[s];
+        if (r <= 32 && w <= 2 && S.fs_off[s] < 0 && !S.is_big[s])
+          micro.push_back(s);
+        else if (!S.is_big[s])
           cls[r <= 32 ? 0 : (r <= 64 ? 1 : 2)].push_back(s);
         else
           big.push_back(s);
+      }
+      if (!micro.empty()) {
+        Launch L{MICRO, 0, (int64_t)sched.size(), (int)micro.size(), (int64_t)micro.size()};
+        for (int f : micro) {
+          const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
+          L.bytes += 8.0 * (r * w + (r - w) * (r - w + 1) / 2 + w) + 16.0 * (S.asm_ptr[f + 1] - S.asm_ptr[f]);
+          for (int t = 0; t < (int)w; ++t) L.flops += (r - t - 1) * (r - t);
+        }
+        out.push_back(L);
+        sched.insert(sched.end(), micro.begin(), micro.end());
       }
       for (int c = 0; c < 3; ++c)
         if (!cls[c].empty()) {
@@ -1759,13 +1930,24 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     int64_t nbpart = 0;
     auto build_solve = [&](int phase, std::vector<SolveLevel>& out) {
       for (int lev = 0; lev < NL; ++lev) {
-        std::vector<int32_t> tiny, small, big;
+        std::vector<int32_t> tiny, small, big, micro;
         for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
           const int s = S.level_list[q];
           if (!in_phase(s, phase)) continue;
-          (S.nrows[s] > 128 ? big : (S.nrows[s] > 32 ? small : tiny)).push_back(s);
+          if (S.nrows[s] <= 32 && S.first[s + 1] - S.first[s] <= 2)
+            micro.push_back(s);
+          else
+            (S.nrows[s] > 128 ? big : (S.nrows[s] > 32 ? small : tiny)).push_back(s);
         }
         SolveLevel L{};
+        L.micro_off = (int64_t)sched.size();
+        L.nmicro = (int)micro.size();
+        sched.insert(sched.end(), micro.begin(), micro.end());
+        for (int f : micro) {
+          const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
+          L.micro_bytes += 8.0 * (r * w + 3.0 * r);
+          L.micro_flops += 2.0 * (r * w - w * (w + 1) / 2);
+        }
         L.tiny_off = (int64_t)sched.size();
         L.ntiny = (int)tiny.size();
         sched.insert(sched.end(), tiny.begin(), tiny.end());
@@ -1989,6 +2171,11 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
         TIMED(KK_ASSEMBLE, L.bytes, L.flops,
               (k_assemble<<<(unsigned)L.items, ANT, 0, s>>>(T_, atiles_.p + L.off, g_ptr_, gpart_, bt_, arena_, fscratch_)));
         break;
+      case MICRO:
+        TIMED(KK_TINY, L.bytes, L.flops,
+              (k_micro_factor<<<(unsigned)cdiv(L.items, NT / MG), NT, 0, s>>>(T_, list, (int)L.items, Kx, arena_, D_,
+                                                                             status_, pivot_tol)));
+        break;
       case SMALL32:
         TIMED(KK_TINY, L.bytes, L.flops,
               (k_tiny_factor<<<(unsigned)cdiv(L.items, 4), NT, 0, s>>>(T_, list, (int)L.items, Kx, arena_, fscratch_, D_,
@@ -2081,6 +2268,10 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
   if (phase == 0 && !S_.lb.empty()) lb_fwd(b, s);
   for (int lev = 0; lev < (int)V.size(); ++lev) {
     const SolveLevel& L = V[lev];
+    if (L.nmicro)
+      TIMED(KK_FWD_TINY, L.micro_bytes, L.micro_flops,
+            (k_fwd_micro<<<(unsigned)cdiv(L.nmicro, NT / MG), NT, 0, s>>>(T_, sched_.p + L.micro_off, L.nmicro, arena_, b,
+                                                                         xi_, uvec_)));
     if (L.ntiny)
       TIMED(KK_FWD_TINY, L.tiny_bytes, L.tiny_flops,
             (k_fwd_tiny<<<(unsigned)cdiv(L.ntiny, 2 * SW), NT, 0, s>>>(T_, sched_.p + L.tiny_off, L.ntiny, arena_, b, xi_,
@@ -2121,6 +2312,10 @@ void LDLSolver::bwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
       TIMED(KK_BWD_TINY, L.tiny_bytes, L.tiny_flops,
             (k_bwd_tiny<<<(unsigned)cdiv(L.ntiny, 2 * SW), NT, 0, s>>>(T_, sched_.p + L.tiny_off, L.ntiny, arena_, D_, xi_,
                                                                       b)));
+    if (L.nmicro)
+      TIMED(KK_BWD_TINY, L.micro_bytes, L.micro_flops,
+            (k_bwd_micro<<<(unsigned)cdiv(L.nmicro, NT / MG), NT, 0, s>>>(T_, sched_.p + L.micro_off, L.nmicro, arena_, D_,
+                                                                         xi_, b)));
     if (phase == 0)
       for (int g : lb_at_level_[lev]) lb_bwd(g, b, s);
   }

@@ -140,7 +140,7 @@ class LDLSolver : public LinSolver {
 
  private:
   enum Kind { ASSEMBLE = 0, SMALL32 = 1, SMALL64 = 2, SMALL128 = 3, BIG_DIAG = 4, BIG_TRSM = 5, BIG_UPDATE = 6,
-              LB_BUILD = 7, LB_SYRK = 8 };
+              LB_BUILD = 7, LB_SYRK = 8, MICRO = 9 };
   struct Launch {
     int kind;
     int step;       // panel step for BIG_DIAG / BIG_TRSM / BIG_UPDATE
@@ -156,6 +156,9 @@ class LDLSolver : public LinSolver {
   struct SolveLevel {
     int64_t tiny_off;  // fronts with r <= 32 (half a wave each)
     int ntiny;
+    int64_t micro_off;  // fronts with r <= 32, w <= 2 (16 lanes each)
+    int nmicro;
+    double micro_bytes = 0, micro_flops = 0;
     int64_t small_off;
     int nsmall;
     int64_t big_off;
