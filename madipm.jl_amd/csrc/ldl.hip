@@ -1182,61 +1182,65 @@ constexpr int SW = 4;  // waves (= small fronts) per workgroup
 // wave 0 runs the substitution from LDS: lane l holds rows (forward) or pivot columns (backward) l and
 // l + 64 in registers, the value of row/column t is broadcast with readlane.  Turning the panel read
 // from a latency chain into one bandwidth burst is what bounds these levels.
-__device__ __forceinline__ double bcast(double v0, double v1, int t) {
-  return (t < 64) ? readlane_f64(v0, t) : readlane_f64(v1, t - 64);
+__device__ __forceinline__ double bcast3(const double (&v)[3], int t) {
+  return (t < 64) ? readlane_f64(v[0], t) : ((t < 128) ? readlane_f64(v[1], t - 64) : readlane_f64(v[2], t - 128));
 }
+
+// r <= SMALL_SOLVE_MAX rows (3 per lane of wave 0), panel r x w staged in LDS (ld r | 1)
+constexpr int SMALL_SOLVE_MAX = 192;
 
 __global__ __launch_bounds__(NT) void k_fwd_small(FrontTab T, const int32_t* __restrict__ fronts, int nf,
                                                   const double* __restrict__ arena, const double* __restrict__ b,
                                                   double* __restrict__ xi, double* __restrict__ uvec) {
   extern __shared__ __attribute__((aligned(16))) double Ls[];
+  __shared__ double v0s[SMALL_SOLVE_MAX];
   const int s = fronts[blockIdx.x];
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
   const int rl = r | 1;
   stage_panel(arena + T.l_off[s], Ls, r, w, rl);
   const int lane = threadIdx.x & 63;
-  // initial vector (own b + children's update vectors): all 256 threads, two per row, each walking
-  // half of the row's gather list with 4 loads in flight; partial sums meet in LDS
-  __shared__ double v0s[128];
-  {
-    const int i = threadIdx.x >> 1, h = threadIdx.x & 1;
+  // initial vector (own b + children's update vectors): all 256 threads, rows strided, each row's
+  // gather list walked with 4 loads in flight
+  for (int i = threadIdx.x; i < r; i += NT) {
+    const int64_t e = T.row_ptr[s] + i;
+    const int64_t p1 = T.sv_ptr[e + 1];
+    int64_t p = T.sv_ptr[e];
     double vi = 0.0;
-    if (i < r) {
-      const int64_t e = T.row_ptr[s] + i;
-      const int64_t p1 = T.sv_ptr[e + 1];
-      int64_t p = T.sv_ptr[e] + h;
-      for (; p + 6 < p1; p += 8) {
-        const int64_t q0 = T.sv_src[p], q1 = T.sv_src[p + 2], q2 = T.sv_src[p + 4], q3 = T.sv_src[p + 6];
-        vi += (uvec[q0] + uvec[q1]) + (uvec[q2] + uvec[q3]);
-      }
-      for (; p < p1; p += 2) vi += uvec[T.sv_src[p]];
+    for (; p + 3 < p1; p += 4) {
+      const int64_t q0 = T.sv_src[p], q1 = T.sv_src[p + 1], q2 = T.sv_src[p + 2], q3 = T.sv_src[p + 3];
+      vi += (uvec[q0] + uvec[q1]) + (uvec[q2] + uvec[q3]);
     }
-    vi += __shfl_xor(vi, 1, 64);
-    if (h == 0 && i < r) v0s[i] = vi + fwd_init(T, s, i, w, f0, b);
+    for (; p < p1; ++p) vi += uvec[T.sv_src[p]];
+    v0s[i] = vi + fwd_init(T, s, i, w, f0, b);
   }
   __syncthreads();
   if (threadIdx.x >= 64) return;
-  double v[2];
-  v[0] = (lane < r) ? v0s[lane] : 0.0;
-  v[1] = (lane + 64 < r) ? v0s[lane + 64] : 0.0;
+  double v[3];
+  int ci[3];
+#pragma unroll
+  for (int h = 0; h < 3; ++h) {
+    const int i = lane + 64 * h;
+    v[h] = (i < r) ? v0s[i] : 0.0;
+    ci[h] = min(i, r - 1);
+  }
   // forward substitution: v[i] -= L(i, t) v[t] for i > t, t < w
-  const int i0 = lane, i1 = lane + 64;
-  const int ci0 = min(i0, r - 1), ci1 = min(i1, r - 1);
   for (int t8 = 0; t8 < w; t8 += 8) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int t = t8 + k;
       if (t < w) {  // wave-uniform
-        const double l0 = Ls[ci0 + t * rl], l1 = Ls[ci1 + t * rl];
-        const double xt = bcast(v[0], v[1], t);
-        v[0] = fma(i0 > t ? -l0 : 0.0, xt, v[0]);
-        v[1] = fma(i1 > t ? -l1 : 0.0, xt, v[1]);
+        const double xt = bcast3(v, t);
+#pragma unroll
+        for (int h = 0; h < 3; ++h) {
+          const double lv = Ls[ci[h] + t * rl];
+          v[h] = fma(lane + 64 * h > t ? -lv : 0.0, xt, v[h]);
+        }
       }
     }
   }
   double* __restrict__ uo = uvec + T.uvec_off[s];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < 3; ++h) {
     const int i = lane + 64 * h;
     if (i < w)
       xi[f0 + i] = v[h];
@@ -1249,58 +1253,60 @@ __global__ __launch_bounds__(NT) void k_bwd_small(FrontTab T, const int32_t* __r
                                                   const double* __restrict__ arena, const double* __restrict__ D,
                                                   double* __restrict__ xi, double* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) double Ls[];
+  __shared__ double xbs[SMALL_SOLVE_MAX];
   const int s = fronts[blockIdx.x];
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
   const int rl = r | 1;
   stage_panel(arena + T.l_off[s], Ls, r, w, rl);
   const int lane = threadIdx.x & 63;
   const int32_t* __restrict__ rows = T.rows + T.row_ptr[s];
-  double xb[2] = {0.0, 0.0}, own[2] = {0.0, 0.0};
-  if (threadIdx.x < 64) {  // x of the rows below the pivot block (ancestors: final) and x_j / d_j
+  const int nb = r - w;
+  // x of the rows below the pivot block (ancestors: final), all threads
+  for (int k = threadIdx.x; k < nb; k += NT) xbs[k] = xi[rows[w + k]];
+  double own[3];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int i = w + lane + 64 * h;
-      if (i < r) xb[h] = xi[rows[i]];
-      const int j = lane + 64 * h;
-      if (j < w) own[h] = xi[f0 + j] / D[f0 + j];
-    }
+  for (int h = 0; h < 3; ++h) {
+    const int j = lane + 64 * h;
+    own[h] = (threadIdx.x < 64 && j < w) ? xi[f0 + j] / D[f0 + j] : 0.0;
   }
   __syncthreads();
   if (threadIdx.x >= 64) return;
-  const int j0 = lane, j1 = lane + 64;  // pivot columns of this lane
-  const int cj0 = min(j0, w - 1), cj1 = min(j1, w - 1);
-  const int nb = r - w;
+  int cj[3];
+#pragma unroll
+  for (int h = 0; h < 3; ++h) cj[h] = min(lane + 64 * h, w - 1);
   // v[j] = x_j / d_j - sum_{i >= w} L(i, j) x_i
-  double acc0 = 0.0, acc1 = 0.0;
+  double acc[3] = {0.0, 0.0, 0.0};
   for (int k8 = 0; k8 < nb; k8 += 8) {
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
       const int k = k8 + kk;
       if (k < nb) {
-        const double x = bcast(xb[0], xb[1], k);
-        acc0 = fma(Ls[(w + k) + cj0 * rl], x, acc0);
-        acc1 = fma(Ls[(w + k) + cj1 * rl], x, acc1);
+        const double x = xbs[k];
+#pragma unroll
+        for (int h = 0; h < 3; ++h) acc[h] = fma(Ls[(w + k) + cj[h] * rl], x, acc[h]);
       }
     }
   }
-  double v[2];
-  v[0] = (j0 < w) ? own[0] - acc0 : 0.0;
-  v[1] = (j1 < w) ? own[1] - acc1 : 0.0;
+  double v[3];
+#pragma unroll
+  for (int h = 0; h < 3; ++h) v[h] = (lane + 64 * h < w) ? own[h] - acc[h] : 0.0;
   // transposed back substitution: for t = w-1 .. 1: v[j] -= L(t, j) v[t] for j < t
   for (int t8 = w - 1; t8 > 0; t8 -= 8) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int t = t8 - k;
       if (t > 0) {  // wave-uniform
-        const double l0 = Ls[t + cj0 * rl], l1 = Ls[t + cj1 * rl];
-        const double xt = bcast(v[0], v[1], t);
-        v[0] = fma(t > j0 ? -l0 : 0.0, xt, v[0]);
-        v[1] = fma(t > j1 ? -l1 : 0.0, xt, v[1]);
+        const double xt = bcast3(v, t);
+#pragma unroll
+        for (int h = 0; h < 3; ++h) {
+          const double lv = Ls[t + cj[h] * rl];
+          v[h] = fma(t > lane + 64 * h ? -lv : 0.0, xt, v[h]);
+        }
       }
     }
   }
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < 3; ++h) {
     const int j = lane + 64 * h;
     if (j < w) {
       xi[f0 + j] = v[h];
@@ -1756,6 +1762,12 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     T_.wout = wout_;
   }
   auto lb_member = [&](int s) { return !S.lb_of.empty() && S.lb_of[s] >= 0; };
+  // solve classes: fronts up to SMALL_SOLVE_MAX rows whose L panel fits in LDS take the one-launch
+  // workgroup-per-front kernels; larger ones the dependency-driven big-front kernels
+  auto solve_small = [&](int s) {
+    const int r = S.nrows[s], w = S.first[s + 1] - S.first[s];
+    return r <= SMALL_SOLVE_MAX && 8 * (r | 1) * w <= 150 * 1024;
+  };
   auto in_phase = [&](int s, int phase) {
     if (lb_member(s)) return false;  // batched leaves: W build + the parent's SYRK + GEMV solves
     return phase == 1 ? (!S.top(s) && S.mine(s)) : S.top(s);
@@ -1922,7 +1934,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     std::vector<int32_t> flag_off(ns, 0);
     int64_t nflags = 0;
     for (int s = 0; s < ns; ++s)
-      if (S.nrows[s] > 128) {
+      if (!solve_small(s)) {
         flag_off[s] = (int32_t)nflags;
         nflags += cdiv(S.first[s + 1] - S.first[s], 64);
       }
@@ -1934,10 +1946,13 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
           const int s = S.level_list[q];
           if (!in_phase(s, phase)) continue;
-          if (S.nrows[s] <= 32 && S.first[s + 1] - S.first[s] <= 2)
+          const int r = S.nrows[s], w = S.first[s + 1] - S.first[s];
+          if (r <= 32 && w <= 2)
             micro.push_back(s);
+          else if (solve_small(s))
+            (r > 32 ? small : tiny).push_back(s);
           else
-            (S.nrows[s] > 128 ? big : (S.nrows[s] > 32 ? small : tiny)).push_back(s);
+            big.push_back(s);
         }
         SolveLevel L{};
         L.micro_off = (int64_t)sched.size();

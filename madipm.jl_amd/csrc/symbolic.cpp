@@ -7,6 +7,7 @@
 #include "symbolic.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <numeric>
 
 #include "common.hpp"
@@ -683,6 +684,9 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   // Sharded: a top front is assembled in two parts — "external" (original entries on shard 0 + this
   // shard's subtree-root children; written, zeros included, then all-reduced) and "internal" (its top
   // children, accumulated after the all-reduce at the front's level).
+  // tuning knob (experiments): MADIPM_GATHER_MAX overrides opt.gather_max
+  int gather_max = opt.gather_max;
+  if (const char* e = std::getenv("MADIPM_GATHER_MAX")) gather_max = std::atoi(e);
   S.fs_off.assign(ns, -1);
   S.fs_size = 0;
   for (int s = 0; s < ns; ++s)
@@ -729,7 +733,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         const int c = S.child_list[qc];
         if (!child_ok(c, which)) continue;
         const int uc = S.nrows[c] - (S.first[c + 1] - S.first[c]);
-        if (uc > SymbolicPlan::kGatherMax) {
+        if (uc > gather_max) {
           bigch.push_back(c);
           continue;
         }

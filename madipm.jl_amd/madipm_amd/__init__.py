@@ -6,6 +6,7 @@ libmadipm_hip.so (include/madipm_hip.h).  Importing the solver requires the buil
 """
 from .qp import QuadraticModel, simple_lp, standard_form_qp, scale_qp  # noqa: F401
 from .mps import read_mps, parse_mps  # noqa: F401
+from .presolve import presolve_qp, postsolve  # noqa: F401
 
 __version__ = "0.1.0"
 

@@ -179,3 +179,70 @@ def test_nd_nnzL_brute_force(m, n, dens, seed):
     K, Lw = random_k2(m, n, dens, seed)
     S = Symbolic(K.shape[0], Lw.indptr, Lw.indices, default_ldl_opts(ordering=3))
     assert S.info()["nnzL"] == _brute_nnzL(K, S.perm())
+
+
+# ---------------------------------------------------------------- presolve_qp (src/utils.jl:319-343)
+def test_presolve_simple_lp_flag():
+    """test/runtests.jl:154-157: presolve_qp(simple_lp) returns flag == true."""
+    from madipm_amd import presolve_qp, simple_lp
+    new, flag = presolve_qp(simple_lp())
+    assert flag and new.nvar == 2 and new.ncon == 1
+
+
+def _presolve_case():
+    """LP with a fixed variable, an empty row, a singleton row and an empty column."""
+    import numpy as np
+    from madipm_amd.qp import QuadraticModel
+    inf = float("inf")
+    # x0 + x1 + x2 = 4 ; x3 fixed = 1 appears in row 0 (x0 + x1 + x2 + x3 = 5) ; row 1 empty ;
+    # row 2: 2 x1 <= 6 (singleton) ; x4 empty column with c4 = -1, 0 <= x4 <= 2
+    return QuadraticModel(
+        c=np.array([1.0, 2.0, 3.0, 5.0, -1.0]), Hrows=[], Hcols=[], Hvals=[],
+        Arows=[0, 0, 0, 0, 2], Acols=[0, 1, 2, 3, 1], Avals=[1.0, 1.0, 1.0, 1.0, 2.0],
+        lcon=np.array([5.0, -1.0, -inf]), ucon=np.array([5.0, 1.0, 6.0]),
+        lvar=np.array([0.0, 0.0, 0.0, 1.0, 0.0]), uvar=np.array([inf, inf, inf, 1.0, 2.0]))
+
+
+def test_presolve_reductions_and_postsolve():
+    import numpy as np
+    from madipm_amd import presolve_qp, postsolve
+    from oracle.mpc import OracleMPC, OracleOptions
+    qp = _presolve_case()
+    new, flag = presolve_qp(qp)
+    assert flag
+    info = new.meta["presolve"]
+    assert list(info.keep_var) == [0, 1, 2] and list(info.keep_con) == [0]
+    assert new.uvar[1] == 3.0                       # singleton row 2 x1 <= 6 became x1 <= 3
+    assert new.lcon[0] == new.ucon[0] == 4.0        # fixed x3 = 1 moved into the row
+    ref = OracleMPC(qp, OracleOptions(max_iter=300)).solve()
+    sol = OracleMPC(new, OracleOptions(max_iter=300)).solve()
+    assert ref.status == sol.status == 1
+    assert abs((sol.objective) - ref.objective) <= 1e-7 * max(1.0, abs(ref.objective))
+    xo, _ = postsolve(info, sol.solution, sol.multipliers)
+    assert np.allclose(xo, ref.solution, atol=1e-6)
+    assert xo[3] == 1.0 and xo[4] == 2.0
+
+
+def test_presolve_detects_infeasible_and_unbounded():
+    import numpy as np
+    from madipm_amd import presolve_qp
+    from madipm_amd.qp import QuadraticModel
+    inf = float("inf")
+    infeas = QuadraticModel(c=np.ones(1), Hrows=[], Hcols=[], Hvals=[], Arows=[0], Acols=[0], Avals=[1.0],
+                            lcon=np.array([5.0]), ucon=np.array([5.0]), lvar=np.zeros(1), uvar=np.array([1.0]))
+    assert presolve_qp(infeas)[1] is False
+    unb = QuadraticModel(c=np.array([-1.0, 1.0]), Hrows=[], Hcols=[], Hvals=[], Arows=[0], Acols=[1], Avals=[1.0],
+                         lcon=np.array([1.0]), ucon=np.array([1.0]), lvar=np.zeros(2), uvar=np.array([inf, inf]))
+    assert presolve_qp(unb)[1] is False
+
+
+def test_presolve_afiro_same_optimum():
+    """AFIRO through presolve -> standard form (scripts/benchmarks_cpu.jl:26-41 order): same optimum."""
+    import os
+    from madipm_amd import presolve_qp, read_mps, standard_form_qp
+    from oracle.mpc import OracleMPC, OracleOptions
+    qp = read_mps(os.path.join(os.path.dirname(__file__), "golden", "afiro.mps"))
+    new, flag = presolve_qp(qp)
+    assert flag
+    st = OracleMPC(standard_form_qp(new), OracleOptions(regularization=("fixed", 1e-8, -1e-8), max_iter=300)).solve()
+    assert st.status == 1 and abs(st.objective + 464.75314286) <= 1e-6 * 464.75
