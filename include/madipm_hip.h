@@ -37,7 +37,7 @@ typedef struct madipm_ldl_opts {
                               4 auto = AMD and ND, fewer flops wins (default) */
   double dense_alpha;      /* AMD dense-node threshold factor (default 10) */
   int32_t relax;           /* relaxed supernode amalgamation (default 1) */
-  int32_t small_front_max; /* fronts with <= this many rows are factorised in LDS (default 128) */
+  int32_t small_front_max; /* fronts with <= this many rows are factorised in LDS (default 128; up to 192 with packed LDS storage) */
   double pivot_tol;        /* |d| <= pivot_tol  =>  pivot failure (default 0: only 0 / NaN / Inf) */
   int32_t nshards;         /* > 1: subtree-sharded factorisation with nshards shards on THIS device
                               (single process, local all-reduce; SURVEY §8 e); default 1.  Across

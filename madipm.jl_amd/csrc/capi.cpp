@@ -67,7 +67,7 @@ static SymbolicOptions to_sym_opts(const madipm_ldl_opts* o) {
     s.small_front_max = o->small_front_max;
   }
   MADIPM_REQUIRE(!o || (o->nshards >= 1 && o->nshards <= 16), "nshards must be in [1,16]");
-  MADIPM_REQUIRE(s.small_front_max >= 1 && s.small_front_max <= 128, "small_front_max must be in [1,128]");
+  MADIPM_REQUIRE(s.small_front_max >= 1 && s.small_front_max <= 192, "small_front_max must be in [1,192]");
   return s;
 }
 

@@ -627,14 +627,20 @@ __device__ __forceinline__ void diag64(double* A64, double* Dl, double* Ms, doub
 // like the big-front path.
 // Factor the kw (<= 16) pivots at (k0, k0) of A (ld) with ONE wave: strictly-lower L_KK into A,
 // pivots into Dl[k0 + t], M_K = L_KK^{-T} D^{-1} (16 x 16, ld LDM, identity-padded) into MK.
-__device__ __forceinline__ void factor16g(double* A, int ld, int k0, int kw, double* Dl, double* MK, double* cb,
+template <bool PK>
+__device__ __forceinline__ int fidx(int i, int j, int r, int ld) {
+  return PK ? ((j * (2 * r - j - 1)) >> 1) + i : i + j * ld;
+}
+
+template <bool PK>
+__device__ __forceinline__ void factor16g(double* A, int r, int ld, int k0, int kw, double* Dl, double* MK, double* cb,
                                           double* xb, int lane) {
   const int il = lane & 15, cg = lane >> 4;
   double a[4], x[4];
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
     const int jl = cg + 4 * m;
-    a[m] = (il < kw && jl < kw) ? (jl <= il ? A[(k0 + il) + (k0 + jl) * ld] : 0.0) : (il == jl ? 1.0 : 0.0);
+    a[m] = (il < kw && jl < kw) ? (jl <= il ? A[fidx<PK>(k0 + il, k0 + jl, r, ld)] : 0.0) : (il == jl ? 1.0 : 0.0);
     x[m] = (jl == il) ? 1.0 : 0.0;
   }
 #pragma unroll
@@ -661,19 +667,23 @@ __device__ __forceinline__ void factor16g(double* A, int ld, int k0, int kw, dou
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
     const int jl = cg + 4 * m;
-    if (jl < il && il < kw) A[(k0 + il) + (k0 + jl) * ld] = a[m] / cb[jl * LDM + jl];
+    if (jl < il && il < kw) A[fidx<PK>(k0 + il, k0 + jl, r, ld)] = a[m] / cb[jl * LDM + jl];
     MK[jl * LDM + il] = (jl <= il) ? x[m] / di : 0.0;
   }
   if (cg == 0 && il < kw) Dl[k0 + il] = di;
   wave_sync();
 }
 
+// PK = false: square storage, ld = r | 1 (r <= 128); PK = true: packed lower-triangular columns
+// (r <= 192 fits LDS), element (i, j >= ...) at j (2r - j - 1) / 2 + i
+
+template <bool PK>
 __global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t* __restrict__ fronts,
                                                       const double* __restrict__ Kx, double* __restrict__ arena,
                                                       const double* __restrict__ fscratch, double* __restrict__ D,
                                                       LDLStatus* st, double tol) {
-  extern __shared__ __attribute__((aligned(16))) double A[];  // r x r, ld = r | 1
-  __shared__ double Dl[128];
+  extern __shared__ __attribute__((aligned(16))) double A[];  // lower part of F (square ld r|1, or packed)
+  __shared__ double Dl[192];
   __shared__ double MK[16 * LDM];
   __shared__ double cbuf[2 * 16 * LDM];
   const int s = fronts[blockIdx.x];
@@ -681,14 +691,35 @@ __global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t*
   const int ld = r | 1;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t fso = T.fs_off[s];
-  if (fso >= 0) {
-    stage_panel(fscratch + fso, A, r, r, ld);  // assembled by k_assemble (lower part valid)
-  } else {                                     // leaf: original entries only
-    for (int q = tid; q < r * ld; q += NT) A[q] = 0.0;
+  if (fso >= 0) {  // assembled by k_assemble (lower part valid)
+    if (!PK) {
+      stage_panel(fscratch + fso, A, r, r, ld);
+    } else {  // lower entries only, 16 loads in flight per thread
+      const double* __restrict__ Fs = fscratch + fso;
+      const int nel = r * r;
+      for (int base = 0; base < nel; base += NT * 16) {
+        double v[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int q = base + k * NT + tid;
+          const int j = q / r, i = q - j * r;
+          v[k] = (q < nel && i >= j) ? Fs[q] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int q = base + k * NT + tid;
+          const int j = q / r, i = q - j * r;
+          if (q < nel && i >= j) A[fidx<true>(i, j, r, ld)] = v[k];
+        }
+      }
+    }
+  } else {  // leaf: original entries only
+    const int ntot = PK ? r * (r + 1) / 2 : r * ld;
+    for (int q = tid; q < ntot; q += NT) A[q] = 0.0;
     __syncthreads();
     for (int64_t q = T.asm_ptr[s] + tid; q < T.asm_ptr[s + 1]; q += NT) {
       const int64_t d = T.asm_dst[q];
-      A[(int)(d % r) + (int)(d / r) * ld] = Kx[T.asm_src[q]];
+      A[fidx<PK>((int)(d % r), (int)(d / r), r, ld)] = Kx[T.asm_src[q]];
     }
   }
   __syncthreads();
@@ -696,7 +727,7 @@ __global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t*
     const int kw = min(16, w - k0);
     const int R0 = k0 + kw;                       // first row / column after the pivots
     const int nbr = (r - R0 + 15) >> 4;           // 16-row blocks below
-    if (wv == ((k0 >> 4) & 3)) factor16g(A, ld, k0, kw, Dl, MK, cbuf, cbuf + 16 * LDM, lane);
+    if (wv == ((k0 >> 4) & 3)) factor16g<PK>(A, r, ld, k0, kw, Dl, MK, cbuf, cbuf + 16 * LDM, lane);
     __syncthreads();
     // panel: L_R = A[R, k0:k0+kw] M_K, row block per wave
     for (int b = wv; b < nbr; b += 4) {
@@ -705,7 +736,7 @@ __global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t*
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const int k = 4 * ks + (lane >> 4), row = rb + (lane & 15);
-        const double av = (k < kw && row < r) ? A[row + (k0 + k) * ld] : 0.0;
+        const double av = (k < kw && row < r) ? A[fidx<PK>(row, k0 + k, r, ld)] : 0.0;
         const double bv = MK[k * LDM + (lane & 15)];
         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
       }
@@ -714,7 +745,7 @@ __global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t*
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int row = rb + (lane >> 4) + 4 * g, col = lane & 15;
-        if (row < r && col < kw) A[row + (k0 + col) * ld] = acc[g];
+        if (row < r && col < kw) A[fidx<PK>(row, k0 + col, r, ld)] = acc[g];
       }
     }
     __syncthreads();
@@ -733,14 +764,14 @@ __global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t*
       for (int ks = 0; ks < 4; ++ks) {
         const int k = 4 * ks + (lane >> 4);
         const int rj = j0 + (lane & 15), ri = i0 + (lane & 15);
-        const double av = (k < kw && rj < r) ? A[rj + (k0 + k) * ld] : 0.0;                 // L_J (rows m)
-        const double bv = (k < kw && ri < r) ? A[ri + (k0 + k) * ld] * Dl[k0 + k] : 0.0;    // (L_I D) (cols n)
+        const double av = (k < kw && rj < r) ? A[fidx<PK>(rj, k0 + k, r, ld)] : 0.0;       // L_J (rows m)
+        const double bv = (k < kw && ri < r) ? A[fidx<PK>(ri, k0 + k, r, ld)] * Dl[k0 + k] : 0.0;  // (L_I D) (cols n)
         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
       }
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int j = j0 + (lane >> 4) + 4 * g, i = i0 + (lane & 15);
-        if (i < r && j < r && i >= j) A[i + j * ld] -= acc[g];
+        if (i < r && j < r && i >= j) A[fidx<PK>(i, j, r, ld)] -= acc[g];
       }
     }
     __syncthreads();
@@ -749,13 +780,13 @@ __global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t*
   double* __restrict__ L = arena + T.l_off[s];
   for (int q = tid; q < r * w; q += NT) {
     const int j = q / r, i = q - j * r;
-    L[q] = (i > j) ? A[i + j * ld] : (i == j ? Dl[j] : 0.0);
+    L[q] = (i > j) ? A[fidx<PK>(i, j, r, ld)] : (i == j ? Dl[j] : 0.0);
   }
   const int u = r - w;
   double* __restrict__ Uo = arena + T.u_off[s];
   for (int q = tid; q < u * u; q += NT) {
     const int b = q / u, a = q - b * u;
-    if (a >= b) Uo[q] = A[(w + a) + (w + b) * ld];
+    if (a >= b) Uo[q] = A[fidx<PK>(w + a, w + b, r, ld)];
   }
   if (tid < w) {
     const double d = Dl[tid];
@@ -1847,7 +1878,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
           L.bytes = 8.0 * (double)G.m * G.n + 16.0 * (double)G.m * (G.m + 1) / 2.0 * cdiv(G.n, LB_KCHUNK);
           out.push_back(L);
         }
-      std::vector<int32_t> cls[3], big, micro;
+      std::vector<int32_t> cls[4], big, micro;
       for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
         const int s = S.level_list[q];
         if (!in_phase(s, phase)) continue;
@@ -1855,7 +1886,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         if (r <= 32 && w <= 2 && S.fs_off[s] < 0 && !S.is_big[s])
           micro.push_back(s);
         else if (!S.is_big[s])
-          cls[r <= 32 ? 0 : (r <= 64 ? 1 : 2)].push_back(s);
+          cls[r <= 32 ? 0 : (r <= 64 ? 1 : (r <= 128 ? 2 : 3))].push_back(s);
         else
           big.push_back(s);
       }
@@ -1869,13 +1900,14 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         out.push_back(L);
         sched.insert(sched.end(), micro.begin(), micro.end());
       }
-      for (int c = 0; c < 3; ++c)
+      for (int c = 0; c < 4; ++c)
         if (!cls[c].empty()) {
-          Launch L{SMALL32 + c, 0, (int64_t)sched.size(), (int)cls[c].size(), (int64_t)cls[c].size()};
+          Launch L{c == 3 ? SMALL192 : SMALL32 + c, 0, (int64_t)sched.size(), (int)cls[c].size(), (int64_t)cls[c].size()};
           L.lds = false;
           for (int f : cls[c]) {
             L.lds = L.lds || S.fs_off[f] < 0;
-            L.lds_bytes = std::max<int>(L.lds_bytes, 8 * S.nrows[f] * (S.nrows[f] | 1));
+            const int r = S.nrows[f];
+            L.lds_bytes = std::max<int>(L.lds_bytes, c == 3 ? 8 * r * (r + 1) / 2 : 8 * r * (r | 1));
           }
           for (int f : cls[c]) {  // reads: K entries or the assembled front; writes: L panel, U block, D
             const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
@@ -2068,7 +2100,10 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_small_factor<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    128 * 128 * 8));
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_fwd_small, hipFuncAttributeMaxDynamicSharedMemorySize, 129 * 128 * 8));
-    MADIPM_HIP(hipFuncSetAttribute((const void*)k_small_blocked, hipFuncAttributeMaxDynamicSharedMemorySize, 129 * 128 * 8));
+    MADIPM_HIP(hipFuncSetAttribute((const void*)k_small_blocked<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   129 * 128 * 8));
+    MADIPM_HIP(hipFuncSetAttribute((const void*)k_small_blocked<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   192 * 193 / 2 * 8));
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_bwd_small, hipFuncAttributeMaxDynamicSharedMemorySize, 129 * 128 * 8));
     attr_done = true;
   }
@@ -2199,8 +2234,13 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
       case SMALL64:
       case SMALL128:
         TIMED(KK_SMALL, L.bytes, L.flops,
-              (k_small_blocked<<<(unsigned)L.items, NT, L.lds_bytes, s>>>(T_, list, Kx, arena_, fscratch_, D_, status_,
-                                                                         pivot_tol)));
+              (k_small_blocked<false><<<(unsigned)L.items, NT, L.lds_bytes, s>>>(T_, list, Kx, arena_, fscratch_, D_,
+                                                                                status_, pivot_tol)));
+        break;
+      case SMALL192:
+        TIMED(KK_SMALL, L.bytes, L.flops,
+              (k_small_blocked<true><<<(unsigned)L.items, NT, L.lds_bytes, s>>>(T_, list, Kx, arena_, fscratch_, D_,
+                                                                               status_, pivot_tol)));
         break;
       case BIG_DIAG:
         TIMED(KK_DIAG, L.bytes, L.flops,

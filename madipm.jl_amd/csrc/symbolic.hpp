@@ -33,7 +33,7 @@ struct SymbolicOptions {
   int relax = 1;             // relaxed supernode amalgamation on/off
   int nrelax[3] = {4, 16, 48};
   double zrelax[3] = {0.8, 0.1, 0.05};
-  int small_front_max = 128; // fronts with r <= this are factorised in LDS by one workgroup
+  int small_front_max = 128; // fronts with r <= this are factorised in LDS by one workgroup (max 192)
   int gather_max = 128;      // children with update blocks of more rows are added block-wise (bt), not gathered
   // elimination-tree subtree sharding (SURVEY §8 e): the front tree is cut into independent
   // subtrees dealt to `nshards` shards plus a "top" (their common ancestors) factorised redundantly

@@ -161,3 +161,18 @@ def test_batched_leaf_columns_parity(m, n, ordering):
     Lw2.data *= 1.5
     assert ls.factorize(torch.from_numpy(Lw2.data.copy()).to(dev)) == 0
     assert np.allclose(ls.diag(), 1.5 * ref.diag(), rtol=1e-12)
+
+
+@pytest.mark.parametrize("sfm", [128, 192])
+def test_small_front_storage_variants(sfm):
+    """Fronts up to 192 rows can be factorised in LDS with packed lower storage (small_front_max=192)
+    instead of the big-front panel path; both give the oracle's pivots (well conditioned, 1e-12)."""
+    from madipm_amd.linear_solver import HIPLDLSolver
+    K, Lw = block_angular_k2(900, 1800, 6, 11, well=True)
+    N = K.shape[0]
+    ls = HIPLDLSolver(N, Lw.indptr, Lw.indices, small_front_max=sfm, ordering=1)
+    dev = torch.device("cuda:0")
+    assert ls.factorize(torch.from_numpy(Lw.data.copy()).to(dev)) == 0
+    ref = OracleLDL(K, ls.perm())
+    assert ref.factorize() == N
+    _check_pivots(ls.diag(), ref.diag(), K)
