@@ -5,7 +5,8 @@ metric  : IPM iterations/sec (+ wall-clock-to-optimality), MIPLIB LP
 workload: BASELINE.json configs[1] — MIPLIB ex10 LP relaxation, fp64, 1 GPU.  No MPS files exist
           offline, so a seeded structured stand-in with ex10's catalogue shape is used
           (madipm_amd.instances.ex10_standin; 69.6k rows x 17.7k [0,1] columns, ~1.1M nnz), run
-          through standard_form_qp exactly as scripts/benchmarks_*.jl do, with the benchmark's solver
+          through presolve_qp -> scale_qp -> standard_form_qp exactly as scripts/benchmarks_*.jl do
+          (reformulate = true), with the benchmark's solver
           settings: max_iter=300, FixedRegularization(1e-8, -1e-8), AdaptiveStep(0.99), tol 1e-8.
 step    : one MPC iteration (factorize + predictor/corrector solves + step), inputs resident in HBM.
           W warmup iterations (untimed solve), then EXACTLY K iterations of a fresh solve after
@@ -32,10 +33,21 @@ sys.path.insert(0, os.path.join(ROOT, "madipm.jl_amd"))
 sys.path.insert(0, ROOT)
 
 
+def reference_pipeline(qp):
+    """scripts/benchmarks_gpu.jl:29-32 (reformulate = true, l.88): presolve_qp -> scale_qp ->
+    standard_form_qp."""
+    from madipm_amd import presolve_qp, scale_qp, standard_form_qp
+    pq, flag = presolve_qp(qp)
+    if not flag:
+        raise RuntimeError("presolve: problem solved, infeasible or unbounded")
+    return standard_form_qp(scale_qp(pq))
+
+
 def build_problem(config: str, seed: int = 0):
-    """BASELINE.json configs as concrete inputs (SURVEY §8 d).  `name@s` scales the stand-in by s."""
-    from madipm_amd import standard_form_qp
+    """BASELINE.json configs as concrete inputs (SURVEY §8 d).  `name@s` scales the stand-in by s.
+    MIPLIB configs go through the reference benchmark's preprocessing (reference_pipeline)."""
     from madipm_amd import instances as I
+    standard_form_qp = reference_pipeline
     name, _, sc = config.partition("@")
     s = float(sc) if sc else 1.0
     tag = f" scaled x{s}" if sc else ""
