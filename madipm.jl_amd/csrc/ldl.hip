@@ -14,6 +14,8 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <cstdlib>
+#include <cstdio>
 
 #include "ldl.hpp"
 
@@ -62,6 +64,13 @@ __device__ __forceinline__ double fwd_init(const FrontTab& T, int s, int i, int 
   const int64_t xo = T.xoff[s];
   if (xo >= 0) return T.xch[xo + i];
   return (i < w) ? b[T.perm[f0 + i]] : 0.0;
+}
+
+// Destination of update entry a of front s: its slot in the tree parent's contiguous gather range
+// (T.upos >= 0) or the front's own update vector (read by the level kernels through sv_src).
+__device__ __forceinline__ double* uvec_dst(const FrontTab& T, int s, int a, double* uvec) {
+  const int64_t p = T.upos[T.rel_ptr[s] + a];
+  return p >= 0 ? T.gbuf + p : uvec + T.uvec_off[s] + a;
 }
 
 // HBM panel (r x w, ld r) -> LDS (ld rl), all threads, 16 independent loads per thread per batch
@@ -319,14 +328,13 @@ __global__ __launch_bounds__(NT) void k_fwd_micro(FrontTab T, const int32_t* __r
   const double l10 = __shfl(c0[0], 1, MG);
   const double x1 = (w == 2) ? __shfl(v[0], 1, MG) - l10 * x0 : 0.0;
   if (!live) return;
-  double* __restrict__ uo = uvec + T.uvec_off[s];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int i = l + 16 * h;
     if (i < w) {
       xi[f0 + i] = (i == 0) ? x0 : x1;
     } else if (i < r) {
-      uo[i - w] = (v[h] - c0[h] * x0) - c1[h] * x1;
+      *uvec_dst(T, s, i - w, uvec) = (v[h] - c0[h] * x0) - c1[h] * x1;
     }
   }
 }
@@ -1217,6 +1225,88 @@ __device__ __forceinline__ double bcast3(const double (&v)[3], int t) {
   return (t < 64) ? readlane_f64(v[0], t) : ((t < 128) ? readlane_f64(v[1], t - 64) : readlane_f64(v[2], t - 128));
 }
 
+// Blocked substitutions of ONE wave on a panel staged in LDS (col-major, ld rl), rows / columns
+// i = lane + 64 h (h < 3) held in v[h].  Pivots are taken 16 at a time: the block's L entries of
+// every row are loaded into registers up front (one LDS latency per block), then the 16-step
+// dependency chain touches only v[HB] (readlane broadcast + one fma per step), and the rows of the
+// other thirds get the block's contribution as 16 independent fmas.  HB (the third holding the
+// block) is a template parameter so every register index is static.
+template <int HB>
+__device__ __forceinline__ void fwd_block16(double (&v)[3], const double* Ls, int rl, int r, int t0, int kb, int lane) {
+  double lb[3][16];
+#pragma unroll
+  for (int h = HB; h < 3; ++h) {
+    const int i = lane + 64 * h;
+    const int ic = min(i, r - 1);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) lb[h][k] = (k < kb && i > t0 + k && i < r) ? Ls[ic + (t0 + k) * rl] : 0.0;
+  }
+  double xs[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    xs[k] = 0.0;
+    if (k < kb) {  // wave-uniform
+      xs[k] = readlane_f64(v[HB], (t0 & 63) + k);
+      v[HB] = fma(-lb[HB][k], xs[k], v[HB]);
+    }
+  }
+#pragma unroll
+  for (int h = HB + 1; h < 3; ++h)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[h] = fma(-lb[h][k], xs[k], v[h]);
+}
+
+// forward: v[i] -= L(i, t) v[t] for i > t, t < w
+__device__ __forceinline__ void fwd_subst16(double (&v)[3], const double* Ls, int rl, int r, int w, int lane) {
+  for (int t0 = 0; t0 < w; t0 += 16) {
+    const int kb = min(16, w - t0);
+    if (t0 < 64)
+      fwd_block16<0>(v, Ls, rl, r, t0, kb, lane);
+    else if (t0 < 128)
+      fwd_block16<1>(v, Ls, rl, r, t0, kb, lane);
+    else
+      fwd_block16<2>(v, Ls, rl, r, t0, kb, lane);
+  }
+}
+
+template <int HB>
+__device__ __forceinline__ void bwd_block16(double (&v)[3], const double* Ls, int rl, int w, int t0, int kb, int lane) {
+  double lb[HB + 1][16];
+#pragma unroll
+  for (int h = 0; h <= HB; ++h) {
+    const int j = lane + 64 * h;
+    const int jc = min(j, w - 1);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) lb[h][k] = (k < kb && j < t0 + k) ? Ls[(t0 + k) + jc * rl] : 0.0;
+  }
+  double xs[16];
+#pragma unroll
+  for (int k = 15; k >= 0; --k) {
+    xs[k] = 0.0;
+    if (k < kb) {  // wave-uniform
+      xs[k] = readlane_f64(v[HB], (t0 & 63) + k);
+      v[HB] = fma(-lb[HB][k], xs[k], v[HB]);
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < HB; ++h)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[h] = fma(-lb[h][k], xs[k], v[h]);
+}
+
+// backward (transposed): v[j] -= L(t, j) v[t] for j < t, t = w-1 .. 1
+__device__ __forceinline__ void bwd_subst16(double (&v)[3], const double* Ls, int rl, int w, int lane) {
+  for (int t0 = ((w - 1) >> 4) << 4; t0 >= 0; t0 -= 16) {
+    const int kb = min(16, w - t0);
+    if (t0 < 64)
+      bwd_block16<0>(v, Ls, rl, w, t0, kb, lane);
+    else if (t0 < 128)
+      bwd_block16<1>(v, Ls, rl, w, t0, kb, lane);
+    else
+      bwd_block16<2>(v, Ls, rl, w, t0, kb, lane);
+  }
+}
+
 // r <= SMALL_SOLVE_MAX rows (3 per lane of wave 0), panel r x w staged in LDS (ld r | 1)
 constexpr int SMALL_SOLVE_MAX = 192;
 
@@ -1254,21 +1344,8 @@ __global__ __launch_bounds__(NT) void k_fwd_small(FrontTab T, const int32_t* __r
     v[h] = (i < r) ? v0s[i] : 0.0;
     ci[h] = min(i, r - 1);
   }
-  // forward substitution: v[i] -= L(i, t) v[t] for i > t, t < w
-  for (int t8 = 0; t8 < w; t8 += 8) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int t = t8 + k;
-      if (t < w) {  // wave-uniform
-        const double xt = bcast3(v, t);
-#pragma unroll
-        for (int h = 0; h < 3; ++h) {
-          const double lv = Ls[ci[h] + t * rl];
-          v[h] = fma(lane + 64 * h > t ? -lv : 0.0, xt, v[h]);
-        }
-      }
-    }
-  }
+  fwd_subst16(v, Ls, rl, r, w, lane);  // v[i] -= L(i, t) v[t] for i > t, t < w
+  (void)ci;
   double* __restrict__ uo = uvec + T.uvec_off[s];
 #pragma unroll
   for (int h = 0; h < 3; ++h) {
@@ -1321,21 +1398,7 @@ __global__ __launch_bounds__(NT) void k_bwd_small(FrontTab T, const int32_t* __r
   double v[3];
 #pragma unroll
   for (int h = 0; h < 3; ++h) v[h] = (lane + 64 * h < w) ? own[h] - acc[h] : 0.0;
-  // transposed back substitution: for t = w-1 .. 1: v[j] -= L(t, j) v[t] for j < t
-  for (int t8 = w - 1; t8 > 0; t8 -= 8) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int t = t8 - k;
-      if (t > 0) {  // wave-uniform
-        const double xt = bcast3(v, t);
-#pragma unroll
-        for (int h = 0; h < 3; ++h) {
-          const double lv = Ls[t + cj[h] * rl];
-          v[h] = fma(t > lane + 64 * h ? -lv : 0.0, xt, v[h]);
-        }
-      }
-    }
-  }
+  bwd_subst16(v, Ls, rl, w, lane);  // for t = w-1 .. 1: v[j] -= L(t, j) v[t] for j < t
 #pragma unroll
   for (int h = 0; h < 3; ++h) {
     const int j = lane + 64 * h;
@@ -1381,7 +1444,7 @@ __global__ __launch_bounds__(NT) void k_fwd_tiny(FrontTab T, const int32_t* __re
     if (lr < w)
       xi[f0 + lr] = v;
     else
-      uvec[T.uvec_off[s] + lr - w] = v;
+      *uvec_dst(T, s, lr - w, uvec) = v;
   }
 }
 
@@ -1652,6 +1715,330 @@ __global__ __launch_bounds__(NT) void k_bwd_big(FrontTab T, const SolveTask* __r
   }
 }
 
+// ------------------------------------------------------------------ tree solves (dependency-driven)
+// ONE launch per direction covers every "tree" front (LDLSolver ctor: phase-1 fronts whose L panel
+// fits LDS and whose children are leaves of <= 32 rows — done by the level-0 launches — or tree
+// fronts).  A workgroup takes the next front in topological order from an atomic ticket (every
+// front it waits on holds an earlier ticket, taken by a running workgroup: no deadlock at any grid
+// size or residency), stages its L panel into LDS BEFORE waiting, then polls its dependencies'
+// flags (forward: tree children; backward: the tree parent), substitutes and publishes.  Hand-off
+// (MI355X_MICROARCH.md "inter-workgroup visibility", form R1): the payload (xi, uvec) is stored
+// write-through (sc1) by the ONE publishing wave, which drains it (vmcnt 0) before its lane 0 stores
+// the flag; every consumer load of handed-off bytes is an sc1 load behind the poll and a workgroup
+// barrier — no agent-scope fences on the dependency chain.
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool poll_flag(int32_t* f, int epoch, int32_t* err) {
+  int spins = 0;
+  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > (1 << 25)) {
+      atomicExch(err, 1);
+      return false;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only (sc1 loads follow)
+  return true;
+}
+// wave 0: poll the flags of dep[q0 .. q1) together (one lane per dependency, 64 per pass)
+__device__ __forceinline__ void poll_deps(const int32_t* __restrict__ dep, int q0, int q1, int32_t* flags, int epoch,
+                                          int32_t* err) {
+  const int lane = threadIdx.x & 63;
+  for (int q = q0; q < q1; q += 64) {
+    const int32_t* f = (q + lane < q1) ? flags + dep[q + lane] : nullptr;
+    int spins = 0;
+    for (;;) {
+      const bool ok = !f || __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+      if (__all(ok)) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1 << 25)) {
+        if (lane == 0) atomicExch(err, 1);
+        break;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ void publish_sc1(int32_t* f, int epoch) {  // the storing wave, after its sc1 stores
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_store(f, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Tree-solve substitutions, one wave, 16 pivots per block, mask-free: the panels are staged with the
+// upper triangle + diagonal zeroed and the pivot columns zero-padded to a multiple of 16, so every
+// block loads its L entries unconditionally (16-byte LDS reads, immediate offsets) and the
+// dependency chain is one readlane + one fma per pivot.
+constexpr int TREE_LDS_MAX = 156 * 1024;  // dynamic LDS of the tree solves (+ ~2 KB static)
+__device__ __forceinline__ int tree_ldt(int w) { return ((w + 15) & ~15) + 2; }  // forward: row-major ld
+__device__ __forceinline__ int tree_ldc(int r) { return ((r + 31) & ~31) + 2; }  // backward: col-major ld
+
+// forward staging: LT[i * ldt + t] = L(i, t) for t < min(i, w), else 0 (t < w16)
+__device__ __forceinline__ void stage_rowmajor(const double* __restrict__ L, double* LT, int r, int w, int ldt) {
+  const int w16 = (w + 15) & ~15;
+  const int nel = r * w16;
+  for (int base = 0; base < nel; base += NT * 16) {
+    double v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int q = base + k * NT + threadIdx.x;
+      const int j = q / r, i = q - j * r;
+      v[k] = (q < nel && j < w && i > j) ? L[q] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int q = base + k * NT + threadIdx.x;
+      const int j = q / r, i = q - j * r;
+      if (q < nel) LT[i * ldt + j] = v[k];
+    }
+  }
+}
+
+// backward staging: LC[j * ldc + t] = L(t, j) for t > j, else 0 (j < w, t < r)
+__device__ __forceinline__ void stage_colmajor(const double* __restrict__ L, double* LC, int r, int w, int ldc) {
+  const int nel = r * w;
+  for (int base = 0; base < nel; base += NT * 16) {
+    double v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int q = base + k * NT + threadIdx.x;
+      const int j = q / r, i = q - j * r;
+      v[k] = (q < nel && i > j) ? L[q] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int q = base + k * NT + threadIdx.x;
+      const int j = q / r, i = q - j * r;
+      if (q < nel) LC[j * ldc + i] = v[k];
+    }
+  }
+  const int pad = ((w + 15) & ~15) - r;  // the last pivot block may reach past row r - 1: zero rows
+  for (int q = threadIdx.x; q < w * pad; q += NT) LC[(q / pad) * ldc + r + q % pad] = 0.0;
+}
+
+template <int HB>
+__device__ __forceinline__ void fwd_block_t(double (&v)[3], const double* LT, int ldt, int r, int t0, int lane) {
+  double lb[3][16];
+#pragma unroll
+  for (int h = HB; h < 3; ++h) {
+    const double2* rp = reinterpret_cast<const double2*>(LT + min(lane + 64 * h, r - 1) * ldt + t0);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const double2 q = rp[m];
+      lb[h][2 * m] = q.x;
+      lb[h][2 * m + 1] = q.y;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const double xt = readlane_f64(v[HB], (t0 & 63) + k);
+#pragma unroll
+    for (int h = HB; h < 3; ++h) v[h] = fma(-lb[h][k], xt, v[h]);
+  }
+}
+
+// forward: v[i] -= L(i, t) v[t] for i > t, t < w (columns >= w are zero)
+__device__ __forceinline__ void fwd_subst_t(double (&v)[3], const double* LT, int ldt, int r, int w, int lane) {
+  for (int t0 = 0; t0 < w; t0 += 16) {
+    if (t0 < 64)
+      fwd_block_t<0>(v, LT, ldt, r, t0, lane);
+    else if (t0 < 128)
+      fwd_block_t<1>(v, LT, ldt, r, t0, lane);
+    else
+      fwd_block_t<2>(v, LT, ldt, r, t0, lane);
+  }
+}
+
+template <int HB>
+__device__ __forceinline__ void bwd_block_c(double (&v)[3], const double* LC, int ldc, int w, int t0, int lane) {
+  double lb[HB + 1][16];
+#pragma unroll
+  for (int h = 0; h <= HB; ++h) {
+    const double2* cp = reinterpret_cast<const double2*>(LC + min(lane + 64 * h, w - 1) * ldc + t0);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const double2 q = cp[m];
+      lb[h][2 * m] = q.x;
+      lb[h][2 * m + 1] = q.y;
+    }
+  }
+#pragma unroll
+  for (int k = 15; k >= 0; --k) {  // lanes >= w hold 0 and stay 0 until k < kb
+    const double xt = readlane_f64(v[HB], (t0 & 63) + k);
+#pragma unroll
+    for (int h = 0; h <= HB; ++h) v[h] = fma(-lb[h][k], xt, v[h]);
+  }
+}
+
+// backward (transposed): v[j] -= L(t, j) v[t] for j < t, t = w-1 .. 1
+__device__ __forceinline__ void bwd_subst_c(double (&v)[3], const double* LC, int ldc, int w, int lane) {
+  for (int t0 = ((w - 1) >> 4) << 4; t0 >= 0; t0 -= 16) {
+    if (t0 < 64)
+      bwd_block_c<0>(v, LC, ldc, w, t0, lane);
+    else if (t0 < 128)
+      bwd_block_c<1>(v, LC, ldc, w, t0, lane);
+    else
+      bwd_block_c<2>(v, LC, ldc, w, t0, lane);
+  }
+}
+
+// Dynamic LDS of the tree solve kernels: L panel (ld r|1) | block inverses | gather staging.
+__global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __restrict__ order, int nt,
+                                                 const int32_t* __restrict__ dep_ptr, const int32_t* __restrict__ dep,
+                                                 int32_t* counter, int32_t* tflags, int epoch, int lds_doubles,
+                                                 const double* __restrict__ arena, const double* __restrict__ b,
+                                                 double* xi, double* uvec, int32_t* err, int64_t* dbg) {
+  extern __shared__ __attribute__((aligned(16))) double Ls[];
+  __shared__ double v0s[SMALL_SOLVE_MAX];
+  __shared__ int s_task;
+  const int tid = threadIdx.x;
+  if (tid == 0) s_task = atomicAdd(counter, 1);
+  __syncthreads();
+  const int t = s_task;
+  if (t >= nt) return;
+  int64_t* dg = dbg ? dbg + 8 * t : nullptr;
+  if (dg && tid == 0) dg[0] = wall_clock64();
+  const int s = order[t];
+  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+  const int ldt = tree_ldt(w);
+  double* stg = Ls + r * ldt;
+  const int cap = ((lds_doubles - r * ldt) / NT) * NT;
+  stage_rowmajor(arena + T.l_off[s], Ls, r, w, ldt);
+  if (dg) {
+    __syncthreads();
+    if (tid == 0) dg[1] = wall_clock64();
+  }
+  if (tid < 64) poll_deps(dep, dep_ptr[t], dep_ptr[t + 1], tflags, epoch, err);
+  __syncthreads();
+  if (dg && tid == 0) dg[2] = wall_clock64();
+  // initial vector: the children scattered their update entries into this front's contiguous range
+  // gbuf[P0, P1) in row order; staged through LDS (16 coalesced loads in flight per thread), then
+  // thread i sums row i's segment in order (4 partial sums)
+  const int64_t e0 = T.row_ptr[s];
+  const int64_t P0 = T.sv_ptr[e0], P1 = T.sv_ptr[e0 + r];
+  const int64_t pr0 = (tid < r) ? T.sv_ptr[e0 + tid] : 0, pr1 = (tid < r) ? T.sv_ptr[e0 + tid + 1] : 0;
+  double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0;
+  for (int64_t base = P0; base < P1; base += cap) {
+    const int n = (int)min((int64_t)cap, P1 - base);
+    for (int q0 = 0; q0 < n; q0 += NT * 16) {
+      double tmp[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int q = q0 + k * NT + tid;
+        tmp[k] = (q < n) ? ld_sc1(T.gbuf + base + q) : 0.0;
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int q = q0 + k * NT + tid;
+        if (q < n) stg[q] = tmp[k];
+      }
+    }
+    __syncthreads();
+    const int lo = (int)(max(pr0, base) - base), hi = (int)(min(pr1, base + n) - base);
+    int p = lo;
+    for (; p + 3 < hi; p += 4) {
+      c0 += stg[p];
+      c1 += stg[p + 1];
+      c2 += stg[p + 2];
+      c3 += stg[p + 3];
+    }
+    for (; p < hi; ++p) c0 += stg[p];
+    __syncthreads();
+  }
+  if (tid < r) v0s[tid] = ((c0 + c1) + (c2 + c3)) + fwd_init(T, s, tid, w, f0, b);
+  __syncthreads();
+  if (dg && tid == 0) dg[3] = wall_clock64();
+  if (tid >= 64) return;
+  const int lane = tid;
+  double v[3];
+#pragma unroll
+  for (int h = 0; h < 3; ++h) {
+    const int i = lane + 64 * h;
+    v[h] = (i < r) ? v0s[i] : 0.0;
+  }
+  fwd_subst_t(v, Ls, ldt, r, w, lane);
+  if (dg && tid == 0) dg[4] = wall_clock64();
+#pragma unroll
+  for (int h = 0; h < 3; ++h) {
+    const int i = lane + 64 * h;
+    if (i < w)
+      st_sc1(xi + f0 + i, v[h]);
+    else if (i < r)
+      st_sc1(uvec_dst(T, s, i - w, uvec), v[h]);
+  }
+  publish_sc1(&tflags[s], epoch);
+  if (dg && tid == 0) {
+    dg[5] = wall_clock64();
+    dg[6] = s;
+    dg[7] = r;
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_bwd_tree(FrontTab T, const int32_t* __restrict__ order, int nt,
+                                                 const int32_t* __restrict__ pdep, int32_t* counter, int32_t* tflags,
+                                                 int epoch, const double* __restrict__ arena,
+                                                 const double* __restrict__ D, double* xi, double* __restrict__ out,
+                                                 int32_t* err) {
+  extern __shared__ __attribute__((aligned(16))) double Ls[];
+  __shared__ double xbs[SMALL_SOLVE_MAX];
+  __shared__ int s_task;
+  const int tid = threadIdx.x;
+  if (tid == 0) s_task = atomicAdd(counter, 1);
+  __syncthreads();
+  const int t = s_task;
+  if (t >= nt) return;
+  const int s = order[t];
+  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+  const int ldc = tree_ldc(r);
+  stage_colmajor(arena + T.l_off[s], Ls, r, w, ldc);
+  const int lane = tid & 63;
+  const int32_t* __restrict__ rows = T.rows + T.row_ptr[s];
+  const int nb = r - w;
+  double own[3];  // this front's forward values (previous launch): plain loads
+#pragma unroll
+  for (int h = 0; h < 3; ++h) {
+    const int j = lane + 64 * h;
+    own[h] = (tid < 64 && j < w) ? xi[f0 + j] / D[f0 + j] : 0.0;
+  }
+  if (tid < 64 && pdep[t] >= 0) poll_deps(pdep, t, t + 1, tflags, epoch, err);
+  __syncthreads();
+  for (int k = tid; k < nb; k += NT) xbs[k] = ld_sc1(xi + rows[w + k]);
+  __syncthreads();
+  if (tid >= 64) return;
+  int cj[3];
+#pragma unroll
+  for (int h = 0; h < 3; ++h) cj[h] = min(lane + 64 * h, w - 1);
+  double acc[3][2] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
+  for (int k8 = 0; k8 < nb; k8 += 8) {
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const int k = k8 + kk;
+      if (k < nb) {
+        const double x = xbs[k];
+#pragma unroll
+        for (int h = 0; h < 3; ++h) acc[h][kk & 1] = fma(Ls[(w + k) + cj[h] * ldc], x, acc[h][kk & 1]);
+      }
+    }
+  }
+  double v[3];
+#pragma unroll
+  for (int h = 0; h < 3; ++h) v[h] = (lane + 64 * h < w) ? own[h] - (acc[h][0] + acc[h][1]) : 0.0;
+  bwd_subst_c(v, Ls, ldc, w, lane);
+#pragma unroll
+  for (int h = 0; h < 3; ++h) {
+    const int j = lane + 64 * h;
+    if (j < w) {
+      st_sc1(xi + f0 + j, v[h]);
+      if (T.wout[s]) out[T.perm[f0 + j]] = v[h];
+    }
+  }
+  publish_sc1(&tflags[s], epoch);
+}
+
 // ------------------------------------------------------------------ sharding (SURVEY §8 e)
 // External forward contribution of the top fronts: task = (top front, 256-row chunk); xch[xoff + i] =
 // (shard 0: own right-hand side entry) + this shard's subtree-root update vectors, child order.
@@ -1803,6 +2190,31 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     if (lb_member(s)) return false;  // batched leaves: W build + the parent's SYRK + GEMV solves
     return phase == 1 ? (!S.top(s) && S.mine(s)) : S.top(s);
   };
+  auto tree_panel_doubles = [&](int s) {  // max(forward row-major, backward col-major) staged panel
+    const int r = S.nrows[s], w = S.first[s + 1] - S.first[s];
+    const int ldt = ((w + 15) & ~15) + 2, ldc = ((r + 31) & ~31) + 2;
+    return std::max<int64_t>((int64_t)r * ldt, (int64_t)w * ldc);
+  };
+  // tree solve set (k_fwd_tree / k_bwd_tree); MADIPM_TREE_SOLVE=0 disables it (A/B measurements)
+  std::vector<char> in_tree(std::max(ns, 1), 0);
+  {
+    const char* ev = std::getenv("MADIPM_TREE_SOLVE");
+    const bool on = !(ev && ev[0] == '0');
+    std::vector<char> lbpar(std::max(ns, 1), 0);
+    for (const auto& G : S.lb) lbpar[G.parent] = 1;
+    auto preleaf = [&](int c) { return S.child_ptr[c] == S.child_ptr[c + 1] && S.nrows[c] <= 32; };
+    for (int s = 0; on && s < ns; ++s) {  // postorder: children first
+      if (!in_phase(s, 1) || preleaf(s) || !solve_small(s) || lbpar[s] ||
+          8 * tree_panel_doubles(s) + 8 * 2048 > TREE_LDS_MAX)
+        continue;
+      bool ok = true;
+      for (int q = S.child_ptr[s]; q < S.child_ptr[s + 1] && ok; ++q) {
+        const int c = S.child_list[q];
+        ok = in_tree[c] || (preleaf(c) && in_phase(c, 1));
+      }
+      in_tree[s] = ok;
+    }
+  }
   // ---- batched leaf columns
   lb_at_level_.assign(std::max(NL, 1), {});
   if (!S.lb.empty()) {
@@ -1977,7 +2389,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         std::vector<int32_t> tiny, small, big, micro;
         for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
           const int s = S.level_list[q];
-          if (!in_phase(s, phase)) continue;
+          if (!in_phase(s, phase) || (phase == 1 && in_tree[s])) continue;
           const int r = S.nrows[s], w = S.first[s + 1] - S.first[s];
           if (r <= 32 && w <= 2)
             micro.push_back(s);
@@ -2066,6 +2478,51 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       }
     };
     build_solve(1, slev1_);
+    {  // tree solve tables
+      std::vector<int32_t> ord, dptr{0}, dl, par;
+      for (int lev = 0; lev < NL; ++lev)
+        for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q)
+          if (in_tree[S.level_list[q]]) ord.push_back(S.level_list[q]);
+      ntree_ = (int)ord.size();
+      tree_lds_ = 0;
+      for (int s : ord) {
+        for (int q = S.child_ptr[s]; q < S.child_ptr[s + 1]; ++q)
+          if (in_tree[S.child_list[q]]) dl.push_back(S.child_list[q]);
+        dptr.push_back((int32_t)dl.size());
+        const double r = S.nrows[s], w = S.first[s + 1] - S.first[s];
+        tree_bytes_ += 8.0 * (r * w + 3.0 * r);
+        tree_flops_ += 2.0 * (r * w - w * (w + 1) / 2);
+        tree_lds_ = std::max<int>(tree_lds_, 8 * tree_panel_doubles(s) + 8 * 2048);
+      }
+      tree_lds_ = std::min(TREE_LDS_MAX, tree_lds_ + 8 * 2048);  // up to 4096 staged gather sources
+      std::vector<int32_t> rord(ord.rbegin(), ord.rend());
+      for (int s : rord) par.push_back(S.parent[s] >= 0 && in_tree[S.parent[s]] ? S.parent[s] : -1);
+      auto up = [](DBuf<int32_t>& d, const std::vector<int32_t>& v) { d.upload(v.empty() ? std::vector<int32_t>{0} : v); };
+      up(tf_order_, ord);
+      up(tb_order_, rord);
+      up(tdep_ptr_, dptr);
+      up(tdep_, dl);
+      up(tpar_, par);
+      tflags_.alloc(std::max(ns, 1));
+      tflags_.zero();
+      // children of tree fronts scatter their forward update entries straight into the parent's
+      // gather range (sv order, gbuf); everyone else keeps its own update vector (uvec)
+      std::vector<int64_t> inv((size_t)std::max<int64_t>(S.uvec_size, 1), -1), upm((size_t)std::max<int64_t>(S.rel_ptr[ns], 1), -1);
+      for (int s : ord)
+        for (int64_t p = S.sv_ptr[S.row_ptr[s]]; p < S.sv_ptr[S.row_ptr[s] + S.nrows[s]]; ++p) inv[S.sv_src[p]] = p;
+      for (int c = 0; c < ns; ++c)
+        if (S.parent[c] >= 0 && in_tree[S.parent[c]])
+          for (int64_t a = 0; a < S.rel_ptr[c + 1] - S.rel_ptr[c]; ++a) {
+            upm[S.rel_ptr[c] + a] = inv[S.uvec_off[c] + a];
+            MADIPM_REQUIRE(upm[S.rel_ptr[c] + a] >= 0, "tree gather map");
+          }
+      upos_.upload(upm);
+      gbuf_.alloc(std::max<int64_t>(S.sv_ptr[S.row_ptr[ns]], 1));
+      T_.upos = upos_;
+      T_.gbuf = gbuf_;
+      const char* dv = std::getenv("MADIPM_TREE_DEBUG");
+      if (dv && dv[0] == '1' && ntree_) tdbg_.alloc((int64_t)8 * ntree_);
+    }
     if (S.nshards > 1) {
       build_solve(2, slev2_);
       align2();
@@ -2081,7 +2538,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     bpart_.alloc(std::max<int64_t>(nbpart, 1) * 64);
     flags_.alloc(std::max<int64_t>(nflags, 1));
     flags_.zero();
-    counters_.alloc(4 * std::max(NL, 1));
+    counters_.alloc(4 * std::max(NL, 1) + 4);  // + the tree-solve tickets (4 NL, 4 NL + 1)
     err_.alloc(1);
     err_.zero();
   }
@@ -2105,6 +2562,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_small_blocked<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    192 * 193 / 2 * 8));
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_bwd_small, hipFuncAttributeMaxDynamicSharedMemorySize, 129 * 128 * 8));
+    MADIPM_HIP(hipFuncSetAttribute((const void*)k_fwd_tree, hipFuncAttributeMaxDynamicSharedMemorySize, TREE_LDS_MAX));
+    MADIPM_HIP(hipFuncSetAttribute((const void*)k_bwd_tree, hipFuncAttributeMaxDynamicSharedMemorySize, TREE_LDS_MAX));
     attr_done = true;
   }
   MADIPM_HIP(hipDeviceSynchronize());
@@ -2123,10 +2582,11 @@ LDLSolver::~LDLSolver() {
   } while (0)
 
 const char* kernel_kind_name(int k) {
-  static const char* names[KK_COUNT] = {"k_asm_chunks", "k_assemble",  "k_tiny_factor", "k_small_factor", "k_big_diag",
+  static const char* names[KK_COUNT] = {"k_asm_chunks", "k_assemble",  "k_micro_factor", "k_small_blocked", "k_big_diag",
                                         "k_big_trsm",   "k_big_update", "k_inertia",    "k_fwd_small",    "k_fwd_gather",
                                         "k_fwd_big",    "k_bwd_below",  "k_bwd_big",    "k_bwd_small",
-                                        "k_fwd_tiny",   "k_bwd_tiny",   "k_lb_build",   "k_lb_syrk",      "k_lb_gemv"};
+                                        "k_fwd_tiny",   "k_bwd_tiny",   "k_lb_build",   "k_lb_syrk",      "k_lb_gemv",
+                                        "k_fwd_tree",   "k_bwd_tree"};
   return (k >= 0 && k < KK_COUNT) ? names[k] : "?";
 }
 
@@ -2316,6 +2776,34 @@ int LDLSolver::status(hipStream_t s) {
   return factorized ? 0 : fp;
 }
 
+// MADIPM_TREE_DEBUG=1: per-task wall-clock phases of k_fwd_tree (100 MHz counter), summarised per
+// level on stderr for the first few solves (diagnostics only)
+void LDLSolver::tree_debug_dump(hipStream_t s) {
+  static int ndump = 0;
+  if (ndump++ >= 4) return;
+  std::vector<int64_t> h((size_t)8 * ntree_);
+  MADIPM_HIP(hipMemcpyAsync(h.data(), tdbg_.p, h.size() * 8, hipMemcpyDeviceToHost, s));
+  MADIPM_HIP(hipStreamSynchronize(s));
+  int64_t t0 = INT64_MAX, t1 = 0;
+  for (int t = 0; t < ntree_; ++t) t0 = std::min(t0, h[8 * t]), t1 = std::max(t1, h[8 * t + 5]);
+  std::vector<double> acc((size_t)S_.nlevels * 8, 0.0);
+  std::vector<int> cnt(S_.nlevels, 0);
+  for (int t = 0; t < ntree_; ++t) {
+    const int64_t* d = &h[8 * t];
+    const int lv = S_.level[(int)d[6]];
+    cnt[lv]++;
+    acc[lv * 8 + 0] += (d[0] - t0) * 0.01;
+    for (int k = 1; k <= 5; ++k) acc[lv * 8 + k] += (d[k] - d[k - 1]) * 0.01;
+    acc[lv * 8 + 6] = std::max(acc[lv * 8 + 6], (d[5] - t0) * 0.01);
+  }
+  fprintf(stderr, "tree fwd: %d tasks, span %.1f us\n", ntree_, (t1 - t0) * 0.01);
+  for (int lv = 0; lv < S_.nlevels; ++lv)
+    if (cnt[lv])
+      fprintf(stderr, "  level %d: %5d fronts  start %.1f  stage %.2f  wait %.2f  gather %.2f  subst %.2f  store %.2f  last end %.1f us\n",
+              lv, cnt[lv], acc[lv * 8] / cnt[lv], acc[lv * 8 + 1] / cnt[lv], acc[lv * 8 + 2] / cnt[lv],
+              acc[lv * 8 + 3] / cnt[lv], acc[lv * 8 + 4] / cnt[lv], acc[lv * 8 + 5] / cnt[lv], acc[lv * 8 + 6]);
+}
+
 void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* b, hipStream_t s) {
   const SolveTask* tasks = reinterpret_cast<const SolveTask*>(tasks_.p);
   const int efwd = 2 * epoch_ - 1;
@@ -2342,6 +2830,13 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
             (k_fwd_big<<<std::min(L.nftask, 512), NT, 0, s>>>(T_, tasks + L.ftask_off, L.nftask, cnt + 2 * lev,
                                                                flags_, flag_off_, efwd, arena_, vwork_, xi_, uvec_, err_)));
     }
+    if (lev == 0 && phase == 0 && ntree_)
+      TIMED(KK_FWD_TREE, tree_bytes_, tree_flops_,
+            (k_fwd_tree<<<(unsigned)ntree_, NT, tree_lds_, s>>>(T_, tf_order_, ntree_, tdep_ptr_, tdep_,
+                                                                 counters_.p + 4 * S_.nlevels, tflags_, efwd, tree_lds_ / 8,
+                                                                 arena_, b,
+                                                                 xi_, uvec_, err_, tdbg_.p)));
+    if (lev == 0 && phase == 0 && ntree_ && tdbg_.p) tree_debug_dump(s);
   }
 }
 
@@ -2351,6 +2846,10 @@ void LDLSolver::bwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
   int32_t* cnt = counters_.p + phase * 2 * S_.nlevels;
   for (int lev = (int)V.size() - 1; lev >= 0; --lev) {
     const SolveLevel& L = V[lev];
+    if (lev == 0 && phase == 0 && ntree_)
+      TIMED(KK_BWD_TREE, tree_bytes_, tree_flops_,
+            (k_bwd_tree<<<(unsigned)ntree_, NT, tree_lds_, s>>>(T_, tb_order_, ntree_, tpar_, counters_.p + 4 * S_.nlevels + 1,
+                                                                 tflags_, ebwd, arena_, D_, xi_, b, err_)));
     if (L.nbelow)
       TIMED(KK_BWD_BELOW, L.below_bytes, 0.25 * L.below_bytes,
             (k_bwd_below<<<L.nbelow, NT, 0, s>>>(T_, sched_.p + L.below_off, bp_off_, arena_, xi_, bpart_)));

@@ -43,6 +43,10 @@ struct FrontTab {
   const int64_t* xoff;
   const double* xch;
   const uint8_t* wout;
+  // tree solves: update entry a of front c goes to gbuf[upos[rel_ptr[c] + a]] when c's parent is a
+  // tree front (its contiguous gather range), else to uvec[uvec_off[c] + a] (upos = -1)
+  const int64_t* upos;
+  double* gbuf;
 };
 
 struct SolveTask {
@@ -59,7 +63,7 @@ struct LDLStatus {  // device-resident, read back by status()
 enum KernelKind {
   KK_ASM_CHUNKS = 0, KK_ASSEMBLE, KK_TINY, KK_SMALL, KK_DIAG, KK_TRSM, KK_UPDATE, KK_INERTIA,
   KK_FWD_SMALL, KK_FWD_GATHER, KK_FWD_BIG, KK_BWD_BELOW, KK_BWD_BIG, KK_BWD_SMALL, KK_FWD_TINY, KK_BWD_TINY,
-  KK_LB_BUILD, KK_LB_SYRK, KK_LB_GEMV,
+  KK_LB_BUILD, KK_LB_SYRK, KK_LB_GEMV, KK_FWD_TREE, KK_BWD_TREE,
   KK_COUNT
 };
 const char* kernel_kind_name(int k);
@@ -195,6 +199,15 @@ class LDLSolver : public LinSolver {
   void lb_syrk(int g, hipStream_t s);
   void lb_fwd(const double* b, hipStream_t s);
   void lb_bwd(int g, double* b, hipStream_t s);
+  // tree solves (k_fwd_tree / k_bwd_tree): the phase-1 fronts solved by ONE dependency-driven launch
+  // per direction (topological ticket order, forward dependencies = tree children, backward = tree
+  // parent), between the level-0 launches and the remaining levels
+  int ntree_ = 0, tree_lds_ = 0;
+  double tree_bytes_ = 0, tree_flops_ = 0;
+  DBuf<int32_t> tf_order_, tb_order_, tdep_ptr_, tdep_, tpar_, tflags_;
+  DBuf<int64_t> tdbg_, upos_;
+  DBuf<double> gbuf_;
+  void tree_debug_dump(hipStream_t s);
   DBuf<double> xch_;
   DBuf<uint8_t> wout_, colmask_;
   DBuf<int32_t> tasks_, flags_, flag_off_, counters_, err_, bp_off_;
