@@ -685,52 +685,56 @@ __device__ __forceinline__ void factor16g(double* A, int r, int ld, int k0, int 
 // PK = false: square storage, ld = r | 1 (r <= 128); PK = true: packed lower-triangular columns
 // (r <= 192 fits LDS), element (i, j >= ...) at j (2r - j - 1) / 2 + i
 
-template <bool PK>
-__global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t* __restrict__ fronts,
-                                                      const double* __restrict__ Kx, double* __restrict__ arena,
-                                                      const double* __restrict__ fscratch, double* __restrict__ D,
-                                                      LDLStatus* st, double tol) {
-  extern __shared__ __attribute__((aligned(16))) double A[];  // lower part of F (square ld r|1, or packed)
-  __shared__ double Dl[192];
-  __shared__ double MK[16 * LDM];
-  __shared__ double cbuf[2 * 16 * LDM];
-  const int s = fronts[blockIdx.x];
-  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
-  const int ld = r | 1;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int64_t fso = T.fs_off[s];
-  if (fso >= 0) {  // assembled by k_assemble (lower part valid)
-    if (!PK) {
-      stage_panel(fscratch + fso, A, r, r, ld);
-    } else {  // lower entries only, 16 loads in flight per thread
-      const double* __restrict__ Fs = fscratch + fso;
-      const int nel = r * r;
-      for (int base = 0; base < nel; base += NT * 16) {
-        double v[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          const int q = base + k * NT + tid;
-          const int j = q / r, i = q - j * r;
-          v[k] = (q < nel && i >= j) ? Fs[q] : 0.0;
-        }
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          const int q = base + k * NT + tid;
-          const int j = q / r, i = q - j * r;
-          if (q < nel && i >= j) A[fidx<true>(i, j, r, ld)] = v[k];
-        }
-      }
-    }
-  } else {  // leaf: original entries only
-    const int ntot = PK ? r * (r + 1) / 2 : r * ld;
-    for (int q = tid; q < ntot; q += NT) A[q] = 0.0;
-    __syncthreads();
-    for (int64_t q = T.asm_ptr[s] + tid; q < T.asm_ptr[s + 1]; q += NT) {
-      const int64_t d = T.asm_dst[q];
-      A[fidx<PK>((int)(d % r), (int)(d / r), r, ld)] = Kx[T.asm_src[q]];
+// In-launch hand-offs between workgroups (MI355X_MICROARCH.md "inter-workgroup visibility", form R1):
+// payload stored sc1 and drained before ONE lane stores the flag; consumers poll relaxed and load sc1.
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool poll_flag(int32_t* f, int epoch, int32_t* err) {
+  int spins = 0;
+  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > (1 << 25)) {
+      atomicExch(err, 1);
+      return false;
     }
   }
-  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only (sc1 loads follow)
+  return true;
+}
+// wave 0: poll the flags of dep[q0 .. q1) together (one lane per dependency, 64 per pass)
+__device__ __forceinline__ void poll_deps(const int32_t* __restrict__ dep, int q0, int q1, int32_t* flags, int epoch,
+                                          int32_t* err) {
+  const int lane = threadIdx.x & 63;
+  for (int q = q0; q < q1; q += 64) {
+    const int32_t* f = (q + lane < q1) ? flags + dep[q + lane] : nullptr;
+    int spins = 0;
+    for (;;) {
+      const bool ok = !f || __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+      if (__all(ok)) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1 << 25)) {
+        if (lane == 0) atomicExch(err, 1);
+        break;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ void publish_sc1(int32_t* f, int epoch) {  // the storing wave, after its sc1 stores
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_store(f, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Blocked right-looking LDL^T of the w pivots of a front held in LDS (lower part; square ld r|1 or
+// packed), all 256 threads; pivots in Dl.
+template <bool PK>
+__device__ __forceinline__ void blocked_factor_lds(double* A, int r, int w, int ld, double* Dl, double* MK, double* cbuf) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   for (int k0 = 0; k0 < w; k0 += 16) {
     const int kw = min(16, w - k0);
     const int R0 = k0 + kw;                       // first row / column after the pivots
@@ -784,22 +788,187 @@ __global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t*
     }
     __syncthreads();
   }
-  // write-out: L panel (ld r; d on the diagonal, zeros above), D, lower triangle of U (ld r - w)
-  double* __restrict__ L = arena + T.l_off[s];
+}
+
+// write-out: L panel (ld r; d on the diagonal, zeros above), lower triangle of U (ld uld), D and the
+// pivot check.  SC1: U stored write-through (handed to a parent inside the same launch).
+template <bool PK, bool SC1>
+__device__ __forceinline__ void blocked_writeout(const double* A, int r, int w, int ld, const double* Dl, double* L,
+                                                 double* Uo, int uld, double* D, int f0, LDLStatus* st, double tol) {
+  const int tid = threadIdx.x;
   for (int q = tid; q < r * w; q += NT) {
     const int j = q / r, i = q - j * r;
     L[q] = (i > j) ? A[fidx<PK>(i, j, r, ld)] : (i == j ? Dl[j] : 0.0);
   }
   const int u = r - w;
-  double* __restrict__ Uo = arena + T.u_off[s];
   for (int q = tid; q < u * u; q += NT) {
     const int b = q / u, a = q - b * u;
-    if (a >= b) Uo[q] = A[fidx<PK>(w + a, w + b, r, ld)];
+    if (a >= b) {
+      const double x = A[fidx<PK>(w + a, w + b, r, ld)];
+      if (SC1)
+        __hip_atomic_store(Uo + a + (int64_t)b * uld, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        Uo[a + (int64_t)b * uld] = x;
+    }
   }
   if (tid < w) {
     const double d = Dl[tid];
     D[f0 + tid] = d;
     if (bad_pivot(d, tol)) atomicMin(&st->fail_pivot, f0 + tid + 1);
+  }
+}
+
+// lower part of an r x r front assembled in HBM scratch (ld r) -> LDS, 16 loads in flight per thread
+template <bool PK>
+__device__ __forceinline__ void stage_front(const double* __restrict__ Fs, double* A, int r, int ld) {
+  const int tid = threadIdx.x;
+  const int nel = r * r;
+  for (int base = 0; base < nel; base += NT * 16) {
+    double v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int q = base + k * NT + tid;
+      const int j = q / r, i = q - j * r;
+      v[k] = (q < nel && i >= j) ? Fs[q] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int q = base + k * NT + tid;
+      const int j = q / r, i = q - j * r;
+      if (q < nel && i >= j) A[fidx<PK>(i, j, r, ld)] = v[k];
+    }
+  }
+}
+
+template <bool PK>
+__global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t* __restrict__ fronts,
+                                                      const double* __restrict__ Kx, double* __restrict__ arena,
+                                                      const double* __restrict__ fscratch, double* __restrict__ D,
+                                                      LDLStatus* st, double tol) {
+  extern __shared__ __attribute__((aligned(16))) double A[];  // lower part of F (square ld r|1, or packed)
+  __shared__ double Dl[192];
+  __shared__ double MK[16 * LDM];
+  __shared__ double cbuf[2 * 16 * LDM];
+  const int s = fronts[blockIdx.x];
+  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+  const int ld = r | 1;
+  const int tid = threadIdx.x;
+  const int64_t fso = T.fs_off[s];
+  if (fso >= 0) {  // assembled by k_assemble (lower part valid)
+    if (!PK)
+      stage_panel(fscratch + fso, A, r, r, ld);
+    else
+      stage_front<true>(fscratch + fso, A, r, ld);
+  } else {  // leaf: original entries only
+    const int ntot = PK ? r * (r + 1) / 2 : r * ld;
+    for (int q = tid; q < ntot; q += NT) A[q] = 0.0;
+    __syncthreads();
+    for (int64_t q = T.asm_ptr[s] + tid; q < T.asm_ptr[s + 1]; q += NT) {
+      const int64_t d = T.asm_dst[q];
+      A[fidx<PK>((int)(d % r), (int)(d / r), r, ld)] = Kx[T.asm_src[q]];
+    }
+  }
+  __syncthreads();
+  blocked_factor_lds<PK>(A, r, w, ld, Dl, MK, cbuf);
+  blocked_writeout<PK, false>(A, r, w, ld, Dl, arena + T.l_off[s], arena + T.u_off[s], T.u_ld[s], D, f0, st, tol);
+}
+
+// ------------------------------------------------------------------ factorisation tree
+// ONE launch factorises every tree front (SymbolicPlan::ftree: phase-1 fronts of <= 192 rows whose
+// children are pre-leaves or tree fronts).  Workgroups take fronts in topological order from an
+// atomic ticket (no deadlock at any grid size); a front stages its pre-assembled scratch (original
+// entries + pre-leaf children, one gather pass before this launch) into LDS, then waits for its tree
+// children's flags and adds their update blocks child by child (sc1 loads; the children stored them
+// write-through), factorises in LDS and publishes (every wave drains, barrier, one flag store).  The
+// last workgroup to finish resets the ticket counters for the next launch.
+template <bool PK>
+__device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const int32_t* __restrict__ dep, int q0, int q1,
+                                                int32_t* flags, int epoch, double* arena, const double* fscratch,
+                                                double* D, LDLStatus* st, double tol, int32_t* err, double* A,
+                                                double* Dl, double* MK, double* cbuf, int32_t* rels, int64_t* dg) {
+  const int tid = threadIdx.x;
+  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+  const int ld = PK ? 0 : (r | 1);
+  if (!PK)
+    stage_panel(fscratch + T.fs_off[s], A, r, r, ld);
+  else
+    stage_front<true>(fscratch + T.fs_off[s], A, r, ld);
+  if (dg) {
+    __syncthreads();
+    if (tid == 0) dg[1] = wall_clock64();
+  }
+  if (tid < 64) poll_deps(dep, q0, q1, flags, epoch, err);
+  __syncthreads();
+  if (dg && tid == 0) dg[2] = wall_clock64();
+  for (int q = q0; q < q1; ++q) {  // tree children, child order
+    const int c = dep[q];
+    const int uc = T.nrows[c] - (T.first[c + 1] - T.first[c]);
+    const int64_t uld = T.u_ld[c];
+    const double* U = arena + T.u_off[c];
+    for (int a = tid; a < uc; a += NT) rels[a] = T.rel[T.rel_ptr[c] + a];
+    __syncthreads();
+    // column b by a wave, rows a >= b by its lanes: 4 columns' loads in flight per wave
+    for (int b0 = (tid >> 6) * 4; b0 < uc; b0 += 16) {
+      double x[4][3];
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int h = 0; h < 3; ++h) {
+          const int b = b0 + cb, a = b + (tid & 63) + 64 * h;
+          x[cb][h] = (b < uc && a < uc) ? __hip_atomic_load(U + a + b * uld, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                        : 0.0;
+        }
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int h = 0; h < 3; ++h) {
+          const int b = b0 + cb, a = b + (tid & 63) + 64 * h;
+          if (b < uc && a < uc) A[fidx<PK>(rels[a], rels[b], r, ld)] += x[cb][h];
+        }
+    }
+    __syncthreads();
+  }
+  if (dg && tid == 0) dg[3] = wall_clock64();
+  blocked_factor_lds<PK>(A, r, w, ld, Dl, MK, cbuf);
+  if (dg && tid == 0) dg[4] = wall_clock64();
+  blocked_writeout<PK, true>(A, r, w, ld, Dl, arena + T.l_off[s], arena + T.u_off[s], T.u_ld[s], D, f0, st, tol);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store(&flags[s], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (dg && tid == 0) {
+    dg[5] = wall_clock64();
+    dg[6] = s;
+    dg[7] = r;
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_fact_tree(FrontTab T, const int32_t* __restrict__ order, int nt,
+                                                  const int32_t* __restrict__ dep_ptr, const int32_t* __restrict__ dep,
+                                                  int32_t* counter, int32_t* flags, int epoch, double* arena,
+                                                  const double* __restrict__ fscratch, double* D, LDLStatus* st,
+                                                  double tol, int32_t* err, int64_t* dbg) {
+  extern __shared__ __attribute__((aligned(16))) double A[];
+  __shared__ double Dl[192];
+  __shared__ double MK[16 * LDM];
+  __shared__ double cbuf[2 * 16 * LDM];
+  __shared__ int32_t rels[192];
+  __shared__ int s_task;
+  if (threadIdx.x == 0) s_task = atomicAdd(counter, 1);
+  __syncthreads();
+  const int t = s_task;
+  if (t >= nt) return;
+  const int s = order[t];
+  int64_t* dg = dbg ? dbg + 8 * t : nullptr;
+  if (dg && threadIdx.x == 0) dg[0] = wall_clock64();
+  if (T.nrows[s] <= 128)
+    fact_tree_front<false>(T, s, dep, dep_ptr[t], dep_ptr[t + 1], flags, epoch, arena, fscratch, D, st, tol, err, A, Dl,
+                           MK, cbuf, rels, dg);
+  else
+    fact_tree_front<true>(T, s, dep, dep_ptr[t], dep_ptr[t + 1], flags, epoch, arena, fscratch, D, st, tol, err, A, Dl,
+                          MK, cbuf, rels, dg);
+  if (threadIdx.x == 0 && atomicAdd(counter + 1, 1) == nt - 1) {  // last one out: reset the tickets
+    counter[0] = 0;
+    counter[1] = 0;
   }
 }
 
@@ -1726,48 +1895,6 @@ __global__ __launch_bounds__(NT) void k_bwd_big(FrontTab T, const SolveTask* __r
 // write-through (sc1) by the ONE publishing wave, which drains it (vmcnt 0) before its lane 0 stores
 // the flag; every consumer load of handed-off bytes is an sc1 load behind the poll and a workgroup
 // barrier — no agent-scope fences on the dependency chain.
-__device__ __forceinline__ double ld_sc1(const double* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1(double* p, double v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ bool poll_flag(int32_t* f, int epoch, int32_t* err) {
-  int spins = 0;
-  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-    __builtin_amdgcn_s_sleep(1);
-    if (++spins > (1 << 25)) {
-      atomicExch(err, 1);
-      return false;
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only (sc1 loads follow)
-  return true;
-}
-// wave 0: poll the flags of dep[q0 .. q1) together (one lane per dependency, 64 per pass)
-__device__ __forceinline__ void poll_deps(const int32_t* __restrict__ dep, int q0, int q1, int32_t* flags, int epoch,
-                                          int32_t* err) {
-  const int lane = threadIdx.x & 63;
-  for (int q = q0; q < q1; q += 64) {
-    const int32_t* f = (q + lane < q1) ? flags + dep[q + lane] : nullptr;
-    int spins = 0;
-    for (;;) {
-      const bool ok = !f || __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
-      if (__all(ok)) break;
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1 << 25)) {
-        if (lane == 0) atomicExch(err, 1);
-        break;
-      }
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__device__ __forceinline__ void publish_sc1(int32_t* f, int epoch) {  // the storing wave, after its sc1 stores
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if ((threadIdx.x & 63) == 0) __hip_atomic_store(f, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // Tree-solve substitutions, one wave, 16 pivots per block, mask-free: the panels are staged with the
 // upper triangle + diagonal zeroed and the pivot columns zero-padded to a multiple of 16, so every
@@ -2245,6 +2372,40 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     lbpart_.alloc(std::max<int64_t>(np, 1));
   }
 
+  // ---- factorisation tree tables (k_fact_tree)
+  {
+    std::vector<int32_t> ord, dptr{0}, dl;
+    for (int lev = 0; lev < NL; ++lev)
+      for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q)
+        if (S.ftree[S.level_list[q]]) ord.push_back(S.level_list[q]);
+    nftree_ = (int)ord.size();
+    for (int s : ord) {
+      for (int q = S.child_ptr[s]; q < S.child_ptr[s + 1]; ++q)
+        if (S.ftree[S.child_list[q]]) dl.push_back(S.child_list[q]);
+      dptr.push_back((int32_t)dl.size());
+      const int r = S.nrows[s], w = S.first[s + 1] - S.first[s], u = r - w;
+      ftree_lds_ = std::max<int>(ftree_lds_, r <= 128 ? 8 * r * (r | 1) : 8 * r * (r + 1) / 2);
+      // reads: the pre-assembled lower triangle + the tree children's blocks; writes: L panel, U, D
+      ftree_bytes_ += 8.0 * (r * (r + 1) / 2.0 + r * (double)w + u * (u + 1) / 2.0 + w);
+      for (int q = S.child_ptr[s]; q < S.child_ptr[s + 1]; ++q)
+        if (S.ftree[S.child_list[q]]) {
+          const double uc = S.nrows[S.child_list[q]] - (S.first[S.child_list[q] + 1] - S.first[S.child_list[q]]);
+          ftree_bytes_ += 8.0 * uc * (uc + 1) / 2.0;
+        }
+      for (int t = 0; t < w; ++t) ftree_flops_ += (double)(r - t - 1) * (r - t);
+    }
+    auto up = [](DBuf<int32_t>& d, const std::vector<int32_t>& v) { d.upload(v.empty() ? std::vector<int32_t>{0} : v); };
+    up(ft_order_, ord);
+    up(ft_dptr_, dptr);
+    up(ft_dep_, dl);
+    fflags_.alloc(std::max(ns, 1));
+    fflags_.zero();
+    fcnt_.alloc(4);
+    fcnt_.zero();
+    const char* dv = std::getenv("MADIPM_TREE_DEBUG");
+    if (dv && dv[0] == '1' && nftree_) fdbg_.alloc((int64_t)8 * nftree_);
+  }
+
   // ---- factorisation launch schedules (phase 1: this shard's subtrees; phase 2: the top fronts)
   std::vector<int32_t> sched;
   auto align2 = [&]() {
@@ -2279,7 +2440,16 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       for (const auto& G : S.lb) L.bytes += 8.0 * (double)G.m * G.n * 2.0 + 12.0 * G.n * G.m;
       out.push_back(L);
     }
+    auto ftree_launch = [&]() {  // factorisation tree: after every level-0 launch (the pre-leaves)
+      asm_launch(2 * NL + 1, out);
+      Launch L{FTREE, 0, 0, nftree_, (int64_t)nftree_};
+      L.bytes = ftree_bytes_;
+      L.flops = ftree_flops_;
+      L.lds_bytes = ftree_lds_;
+      out.push_back(L);
+    };
     for (int lev = 0; lev < NL; ++lev) {
+      if (phase == 1 && lev == 1 && nftree_) ftree_launch();
       asm_launch(phase == 1 ? lev : NL + 1 + lev, out);
       if (phase == 1)
         for (int g : lb_at_level_[lev]) {
@@ -2293,7 +2463,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       std::vector<int32_t> cls[4], big, micro;
       for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
         const int s = S.level_list[q];
-        if (!in_phase(s, phase)) continue;
+        if (!in_phase(s, phase) || S.ftree[s]) continue;
         const int r = S.nrows[s], w = S.first[s + 1] - S.first[s];
         if (r <= 32 && w <= 2 && S.fs_off[s] < 0 && !S.is_big[s])
           micro.push_back(s);
@@ -2366,6 +2536,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         }
       }
     }
+    if (phase == 1 && NL == 1 && nftree_) ftree_launch();
   };
   build_fact(1, fact1_);
   if (S.nshards > 1) {
@@ -2563,6 +2734,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
                                    192 * 193 / 2 * 8));
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_bwd_small, hipFuncAttributeMaxDynamicSharedMemorySize, 129 * 128 * 8));
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_fwd_tree, hipFuncAttributeMaxDynamicSharedMemorySize, TREE_LDS_MAX));
+    MADIPM_HIP(hipFuncSetAttribute((const void*)k_fact_tree, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   192 * 193 / 2 * 8));
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_bwd_tree, hipFuncAttributeMaxDynamicSharedMemorySize, TREE_LDS_MAX));
     attr_done = true;
   }
@@ -2586,7 +2759,7 @@ const char* kernel_kind_name(int k) {
                                         "k_big_trsm",   "k_big_update", "k_inertia",    "k_fwd_small",    "k_fwd_gather",
                                         "k_fwd_big",    "k_bwd_below",  "k_bwd_big",    "k_bwd_small",
                                         "k_fwd_tiny",   "k_bwd_tiny",   "k_lb_build",   "k_lb_syrk",      "k_lb_gemv",
-                                        "k_fwd_tree",   "k_bwd_tree"};
+                                        "k_fwd_tree",   "k_bwd_tree",   "k_fact_tree"};
   return (k >= 0 && k < KK_COUNT) ? names[k] : "?";
 }
 
@@ -2720,6 +2893,14 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
       case LB_SYRK:
         TIMED(KK_LB_SYRK, L.bytes, L.flops, lb_syrk((int)L.off, s));
         break;
+      case FTREE:
+        ++fepoch_;
+        TIMED(KK_FACT_TREE, L.bytes, L.flops,
+              (k_fact_tree<<<(unsigned)nftree_, NT, L.lds_bytes, s>>>(T_, ft_order_, nftree_, ft_dptr_, ft_dep_, fcnt_,
+                                                                      fflags_, fepoch_, arena_, fscratch_, D_, status_,
+                                                                      pivot_tol, err_, fdbg_.p)));
+        if (fdbg_.p) tree_debug_dump(s, "fact", fdbg_.p, nftree_, "stage", "wait", "push", "factor", "store");
+        break;
     }
   }
 }
@@ -2776,19 +2957,20 @@ int LDLSolver::status(hipStream_t s) {
   return factorized ? 0 : fp;
 }
 
-// MADIPM_TREE_DEBUG=1: per-task wall-clock phases of k_fwd_tree (100 MHz counter), summarised per
-// level on stderr for the first few solves (diagnostics only)
-void LDLSolver::tree_debug_dump(hipStream_t s) {
+// MADIPM_TREE_DEBUG=1: per-task wall-clock phases of the tree kernels (100 MHz counter), summarised
+// per level on stderr for the first few launches (diagnostics only)
+void LDLSolver::tree_debug_dump(hipStream_t s, const char* what, const int64_t* dbuf, int nt, const char* p1,
+                                const char* p2, const char* p3, const char* p4, const char* p5) {
   static int ndump = 0;
-  if (ndump++ >= 4) return;
-  std::vector<int64_t> h((size_t)8 * ntree_);
-  MADIPM_HIP(hipMemcpyAsync(h.data(), tdbg_.p, h.size() * 8, hipMemcpyDeviceToHost, s));
+  if (ndump++ >= 8) return;
+  std::vector<int64_t> h((size_t)8 * nt);
+  MADIPM_HIP(hipMemcpyAsync(h.data(), dbuf, h.size() * 8, hipMemcpyDeviceToHost, s));
   MADIPM_HIP(hipStreamSynchronize(s));
   int64_t t0 = INT64_MAX, t1 = 0;
-  for (int t = 0; t < ntree_; ++t) t0 = std::min(t0, h[8 * t]), t1 = std::max(t1, h[8 * t + 5]);
+  for (int t = 0; t < nt; ++t) t0 = std::min(t0, h[8 * t]), t1 = std::max(t1, h[8 * t + 5]);
   std::vector<double> acc((size_t)S_.nlevels * 8, 0.0);
   std::vector<int> cnt(S_.nlevels, 0);
-  for (int t = 0; t < ntree_; ++t) {
+  for (int t = 0; t < nt; ++t) {
     const int64_t* d = &h[8 * t];
     const int lv = S_.level[(int)d[6]];
     cnt[lv]++;
@@ -2796,12 +2978,12 @@ void LDLSolver::tree_debug_dump(hipStream_t s) {
     for (int k = 1; k <= 5; ++k) acc[lv * 8 + k] += (d[k] - d[k - 1]) * 0.01;
     acc[lv * 8 + 6] = std::max(acc[lv * 8 + 6], (d[5] - t0) * 0.01);
   }
-  fprintf(stderr, "tree fwd: %d tasks, span %.1f us\n", ntree_, (t1 - t0) * 0.01);
+  fprintf(stderr, "tree %s: %d tasks, span %.1f us\n", what, nt, (t1 - t0) * 0.01);
   for (int lv = 0; lv < S_.nlevels; ++lv)
     if (cnt[lv])
-      fprintf(stderr, "  level %d: %5d fronts  start %.1f  stage %.2f  wait %.2f  gather %.2f  subst %.2f  store %.2f  last end %.1f us\n",
-              lv, cnt[lv], acc[lv * 8] / cnt[lv], acc[lv * 8 + 1] / cnt[lv], acc[lv * 8 + 2] / cnt[lv],
-              acc[lv * 8 + 3] / cnt[lv], acc[lv * 8 + 4] / cnt[lv], acc[lv * 8 + 5] / cnt[lv], acc[lv * 8 + 6]);
+      fprintf(stderr, "  level %d: %5d fronts  start %.1f  %s %.2f  %s %.2f  %s %.2f  %s %.2f  %s %.2f  last end %.1f us\n", lv,
+              cnt[lv], acc[lv * 8] / cnt[lv], p1, acc[lv * 8 + 1] / cnt[lv], p2, acc[lv * 8 + 2] / cnt[lv], p3,
+              acc[lv * 8 + 3] / cnt[lv], p4, acc[lv * 8 + 4] / cnt[lv], p5, acc[lv * 8 + 5] / cnt[lv], acc[lv * 8 + 6]);
 }
 
 void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* b, hipStream_t s) {
@@ -2836,7 +3018,8 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
                                                                  counters_.p + 4 * S_.nlevels, tflags_, efwd, tree_lds_ / 8,
                                                                  arena_, b,
                                                                  xi_, uvec_, err_, tdbg_.p)));
-    if (lev == 0 && phase == 0 && ntree_ && tdbg_.p) tree_debug_dump(s);
+    if (lev == 0 && phase == 0 && ntree_ && tdbg_.p)
+      tree_debug_dump(s, "fwd", tdbg_.p, ntree_, "stage", "wait", "gather", "subst", "store");
   }
 }
 

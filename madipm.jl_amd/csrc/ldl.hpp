@@ -63,7 +63,7 @@ struct LDLStatus {  // device-resident, read back by status()
 enum KernelKind {
   KK_ASM_CHUNKS = 0, KK_ASSEMBLE, KK_TINY, KK_SMALL, KK_DIAG, KK_TRSM, KK_UPDATE, KK_INERTIA,
   KK_FWD_SMALL, KK_FWD_GATHER, KK_FWD_BIG, KK_BWD_BELOW, KK_BWD_BIG, KK_BWD_SMALL, KK_FWD_TINY, KK_BWD_TINY,
-  KK_LB_BUILD, KK_LB_SYRK, KK_LB_GEMV, KK_FWD_TREE, KK_BWD_TREE,
+  KK_LB_BUILD, KK_LB_SYRK, KK_LB_GEMV, KK_FWD_TREE, KK_BWD_TREE, KK_FACT_TREE,
   KK_COUNT
 };
 const char* kernel_kind_name(int k);
@@ -144,7 +144,7 @@ class LDLSolver : public LinSolver {
 
  private:
   enum Kind { ASSEMBLE = 0, SMALL32 = 1, SMALL64 = 2, SMALL128 = 3, BIG_DIAG = 4, BIG_TRSM = 5, BIG_UPDATE = 6,
-              LB_BUILD = 7, LB_SYRK = 8, MICRO = 9, SMALL192 = 10 };
+              LB_BUILD = 7, LB_SYRK = 8, MICRO = 9, SMALL192 = 10, FTREE = 11 };
   struct Launch {
     int kind;
     int step;       // panel step for BIG_DIAG / BIG_TRSM / BIG_UPDATE
@@ -207,7 +207,14 @@ class LDLSolver : public LinSolver {
   DBuf<int32_t> tf_order_, tb_order_, tdep_ptr_, tdep_, tpar_, tflags_;
   DBuf<int64_t> tdbg_, upos_;
   DBuf<double> gbuf_;
-  void tree_debug_dump(hipStream_t s);
+  void tree_debug_dump(hipStream_t s, const char* what, const int64_t* dbuf, int nt, const char* p1, const char* p2,
+                       const char* p3, const char* p4, const char* p5);
+  // factorisation tree (k_fact_tree): fronts in topological order, their tree children, flags
+  // (per-factorisation epoch), ticket counters (reset by the launch's last workgroup)
+  int nftree_ = 0, ftree_lds_ = 0, fepoch_ = 0;
+  double ftree_bytes_ = 0, ftree_flops_ = 0;
+  DBuf<int32_t> ft_order_, ft_dptr_, ft_dep_, fflags_, fcnt_;
+  DBuf<int64_t> fdbg_;
   DBuf<double> xch_;
   DBuf<uint8_t> wout_, colmask_;
   DBuf<int32_t> tasks_, flags_, flag_off_, counters_, err_, bp_off_;

@@ -687,10 +687,33 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   // tuning knob (experiments): MADIPM_GATHER_MAX overrides opt.gather_max
   int gather_max = opt.gather_max;
   if (const char* e = std::getenv("MADIPM_GATHER_MAX")) gather_max = std::atoi(e);
+  // factorisation tree (k_fact_tree): phase-1 fronts of <= kFactTreeMax rows whose children are all
+  // pre-leaves (leaves of <= 32 rows, factorised by the level-0 launches) or tree fronts.  Their
+  // original entries and pre-leaf children are pre-assembled into scratch by ONE gather pass after
+  // the level-0 launches (group 2 NL + 1); tree children are added inside the tree kernel.
+  S.ftree.assign(ns, 0);
+  {
+    const char* ev = std::getenv("MADIPM_TREE_FACT");
+    const bool on = opt.fact_tree && !(ev && ev[0] == '0');
+    std::vector<char> lbpar(ns, 0);
+    for (const auto& g : S.lb) lbpar[g.parent] = 1;
+    for (int s = 0; on && s < ns; ++s) {  // postorder: children first
+      if (S.top(s) || !S.mine(s) || lb_member(s) || lbpar[s] || S.nrows[s] > SymbolicPlan::kFactTreeMax) continue;
+      if (S.child_ptr[s] == S.child_ptr[s + 1] && S.nrows[s] <= 32) continue;  // pre-leaf
+      bool ok = true;
+      int fanin = 0;  // tree children are added one after another by one workgroup: bound the fan-in
+      for (int64_t qc = S.child_ptr[s]; qc < S.child_ptr[s + 1] && ok; ++qc) {
+        const int c = S.child_list[qc];
+        fanin += S.ftree[c];
+        ok = S.ftree[c] || (S.child_ptr[c] == S.child_ptr[c + 1] && S.nrows[c] <= 32 && !lb_member(c));
+      }
+      S.ftree[s] = ok && fanin <= SymbolicPlan::kFactTreeFanIn;
+    }
+  }
   S.fs_off.assign(ns, -1);
   S.fs_size = 0;
   for (int s = 0; s < ns; ++s)
-    if (!S.is_big[s] && S.child_ptr[s + 1] > S.child_ptr[s] && S.mine(s)) {
+    if (S.ftree[s] || (!S.is_big[s] && S.child_ptr[s + 1] > S.child_ptr[s] && S.mine(s))) {
       S.fs_off[s] = S.fs_size;
       S.fs_size += (int64_t)S.nrows[s] * S.nrows[s];
     }
@@ -698,8 +721,8 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   S.g_ptr.clear();
   S.g_src.clear();
   S.bt.clear();
-  S.atile_lev.assign(2 * S.nlevels + 2, 0);
-  S.chunk_lev.assign(2 * S.nlevels + 2, 0);
+  S.atile_lev.assign(2 * S.nlevels + 3, 0);
+  S.chunk_lev.assign(2 * S.nlevels + 3, 0);
   S.g_chunk.clear();
   {
     std::vector<int32_t> key, cnt;
@@ -710,6 +733,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       if (lb_member(c)) return false;  // batched leaves: absorbed by the group SYRK
       if (which == 0) return true;
       if (which == 1) return S.top(c);
+      if (which == 3) return !S.ftree[c];  // tree front: pre-leaf children only
       return !S.top(c) && S.owner[c] == S.shard;
     };
     auto emit = [&](int s, bool orig, int which, bool acc, bool emit_empty) {
@@ -733,7 +757,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         const int c = S.child_list[qc];
         if (!child_ok(c, which)) continue;
         const int uc = S.nrows[c] - (S.first[c + 1] - S.first[c]);
-        if (uc > gather_max) {
+        if (uc > gather_max && which != 3) {
           bigch.push_back(c);
           continue;
         }
@@ -804,7 +828,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     for (int lev = 0; lev < NL; ++lev) {
       for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
         const int s = S.level_list[q];
-        if (S.top(s) || !S.mine(s) || lb_member(s)) continue;
+        if (S.top(s) || !S.mine(s) || lb_member(s) || S.ftree[s]) continue;
         if (!S.is_big[s] && S.fs_off[s] < 0) continue;
         emit(s, true, 0, false, true);
       }
@@ -822,6 +846,11 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       }
       close_group(NL + 1 + lev);
     }
+    // factorisation-tree pre-assembly (after the level-0 launches), tree fronts in level order
+    for (int lev = 0; lev < NL; ++lev)
+      for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q)
+        if (S.ftree[S.level_list[q]]) emit(S.level_list[q], true, 3, false, true);
+    close_group(2 * NL + 1);
     S.g_chunk.push_back((int64_t)S.g_src.size());  // sentinel
     MADIPM_REQUIRE(S.g_src.size() < (size_t)INT32_MAX * 2 && S.atiles.size() < (size_t)INT32_MAX, "assembly plan too large");
   }

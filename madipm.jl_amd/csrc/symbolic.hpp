@@ -35,6 +35,7 @@ struct SymbolicOptions {
   double zrelax[3] = {0.8, 0.1, 0.05};
   int small_front_max = 128; // fronts with r <= this are factorised in LDS by one workgroup (max 192)
   int gather_max = 128;      // children with update blocks of more rows are added block-wise (bt), not gathered
+  int fact_tree = 1;         // dependency-driven factorisation of the LDS-sized subtrees (k_fact_tree)
   // elimination-tree subtree sharding (SURVEY §8 e): the front tree is cut into independent
   // subtrees dealt to `nshards` shards plus a "top" (their common ancestors) factorised redundantly
   // by every shard after one all-reduce of the top fronts' external contributions.
@@ -91,13 +92,16 @@ struct SymbolicPlan {
   // assembly groups (ranges of atiles / chunks): g in [0, nlevels) = phase-1 levels (this shard's
   // subtree fronts; every front when unsharded), g = nlevels = the top fronts' external assembly
   // (before the all-reduce), g in (nlevels, 2 nlevels] = phase-2 levels (top fronts, F += the
-  // contributions of their top children)
-  std::vector<int32_t> atile_lev;      // size 2 nlevels + 2
+  // contributions of their top children), g = 2 nlevels + 1 = the factorisation-tree pre-assembly
+  std::vector<int32_t> atile_lev;      // size 2 nlevels + 3
   std::vector<int64_t> chunk_lev;
   std::vector<int32_t> g_ptr, bt;
   std::vector<int64_t> g_chunk;        // chunk c = sources [g_chunk[c], g_chunk[c+1])
   std::vector<int64_t> g_src;          // >= 0: arena index; < 0: ~(index into caller's values)
-  std::vector<int64_t> fs_off;         // small fronts with children: r x r scratch (else -1)
+  std::vector<int64_t> fs_off;         // small fronts with children, tree fronts: r x r scratch (else -1)
+  static constexpr int kFactTreeMax = 192;
+  static constexpr int kFactTreeFanIn = 8;
+  std::vector<uint8_t> ftree;          // factorisation-tree fronts (k_fact_tree)
   int64_t fs_size = 0;
   // forward-solve gather: for every front row, the children's update-vector entries in child order
   std::vector<int64_t> sv_ptr, sv_src;  // sv_ptr indexed by row_ptr[s] + i
