@@ -685,6 +685,52 @@ __device__ __forceinline__ void factor16g(double* A, int r, int ld, int k0, int 
 // PK = false: square storage, ld = r | 1 (r <= 128); PK = true: packed lower-triangular columns
 // (r <= 192 fits LDS), element (i, j >= ...) at j (2r - j - 1) / 2 + i
 
+// Same contract as factor16g, register-resident: lane i (& 15) keeps row i of the 16 x 16 diagonal
+// block (and row i of X = L_KK^{-1}) in registers; pivot t and the column below it are broadcast
+// with readlane (no LDS round trip in the pivot chain, the column reads overlap the reciprocal).
+// Identity-padded past kw.  Writes the strictly-lower L_KK into A, d into Dl[k0 + i] and
+// M_K = L_KK^{-T} D^{-1} (ld LDM, zero above the diagonal) into MK.
+template <bool PK>
+__device__ __forceinline__ void factor16r(double* A, int r, int ld, int k0, int kw, double* Dl, double* MK, int lane) {
+  const int i = lane & 15;
+  const int ic = min(i, kw - 1);
+  double a[16], x[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int jc = min(j, kw - 1);
+    double v = A[fidx<PK>(k0 + max(ic, jc), k0 + min(ic, jc), r, ld)];  // upper part mirrored (never read)
+    asm volatile("" : "+v"(v));  // keep the load unconditional (no per-load branch + wait)
+    a[j] = (i < kw && j < kw) ? v : (i == j ? 1.0 : 0.0);
+    x[j] = (i == j) ? 1.0 : 0.0;
+  }
+  double dmine = 1.0;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    const double dt = readlane_f64(a[t], t);
+    double col[16], xr[16];
+#pragma unroll
+    for (int j = t + 1; j < 16; ++j) col[j] = readlane_f64(a[t], j);  // L-part (j, t), unscaled
+#pragma unroll
+    for (int j = 0; j <= t; ++j) xr[j] = readlane_f64(x[j], t);       // row t of X
+    const double li = (i > t) ? a[t] / dt : 0.0;  // IEEE quotient: keeps the level path's rounding
+#pragma unroll
+    for (int j = t + 1; j < 16; ++j) a[j] = fma(-li, col[j], a[j]);
+#pragma unroll
+    for (int j = 0; j <= t; ++j) x[j] = fma(-li, xr[j], x[j]);
+    if (i == t) dmine = dt;
+    if (i > t) a[t] = li;
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (j < i && i < kw) A[fidx<PK>(k0 + i, k0 + j, r, ld)] = a[j];
+      MK[j * LDM + i] = (j <= i) ? x[j] / dmine : 0.0;
+    }
+    if (i < kw) Dl[k0 + i] = dmine;
+  }
+  wave_sync();
+}
+
 // In-launch hand-offs between workgroups (MI355X_MICROARCH.md "inter-workgroup visibility", form R1):
 // payload stored sc1 and drained before ONE lane stores the flag; consumers poll relaxed and load sc1.
 __device__ __forceinline__ double ld_sc1(const double* p) {
@@ -732,8 +778,166 @@ __device__ __forceinline__ void publish_sc1(int32_t* f, int epoch) {  // the sto
 
 // Blocked right-looking LDL^T of the w pivots of a front held in LDS (lower part; square ld r|1 or
 // packed), all 256 threads; pivots in Dl.
+//
+// Codegen notes (measured on gfx950 with tools/factor_bench.hip, tools/tile_bench.hip): one f64
+// MFMA 16x16x4 issues every 64 cycles per SIMD, an LDS round trip is ~80 cycles, and a wave has
+// nothing to hide them behind (one 256-thread workgroup per CU).  So every LDS operand of a step is
+// loaded unconditionally (clamped indices, pinned so the compiler cannot sink a load into a branch
+// with its own wait), a wave updates a STRIP of up to four 16 x 16 tiles sharing the (L_I D)
+// operand (four independent accumulator chains back to back), and the next pivot block is
+// factorised by one wave while the other three finish the trailing update (lookahead).
+#define LDL_PIN(x) asm volatile("" : "+v"(x))
+
+// L_R = A[R, k0:k0+kw] M_K for the 16-row blocks b = b0, b0 + bstep, ... below the pivots
+template <bool PK>
+__device__ __forceinline__ void panel_blocks(double* A, int r, int ld, int k0, int kw, int R0, int nbr, const double* MK,
+                                             int b0, int bstep, int lane) {
+  const int kl = lane >> 4, il = lane & 15;
+  double bv[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) bv[ks] = MK[(4 * ks + kl) * LDM + il];
+  for (int b = b0; b < nbr; b += 2 * bstep) {
+    const bool two = b + bstep < nbr;  // wave-uniform
+    double av[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int row = min(R0 + 16 * (b + u * bstep) + il, r - 1);
+        av[u][ks] = A[fidx<PK>(row, k0 + min(4 * ks + kl, kw - 1), r, ld)];
+        LDL_PIN(av[u][ks]);
+      }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) av[u][ks] = (4 * ks + kl < kw) ? av[u][ks] : 0.0;
+    dbl4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[0][ks], bv[ks], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[1][ks], bv[ks], acc1, 0, 0, 0);  // unpredicated
+    }
+    // acc[g] = D[m][n]: m = kl + 4 g (row in the block: the A operand carried the rows), n = il (pivot)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int row0 = R0 + 16 * b + kl + 4 * g, row1 = row0 + 16 * bstep;
+      if (row0 < r && il < kw) A[fidx<PK>(row0, k0 + il, r, ld)] = acc0[g];
+      if (two && row1 < r && il < kw) A[fidx<PK>(row1, k0 + il, r, ld)] = acc1[g];
+    }
+  }
+}
+
+// One strip: tiles (I, J0 .. J0+NS-1).  NS is static so the MFMA sequence has no branches (a
+// predicated MFMA makes the compiler drain the accumulators after every step).
+template <bool PK, int NS>
+__device__ __forceinline__ void trail_strip(double* A, int r, int ld, int k0, int kw, int R0, int I, int J0,
+                                            const double (&dk)[4], int lane) {
+  const int kl = lane >> 4, il = lane & 15;
+  const int i0 = R0 + 16 * I;
+  const int ri = min(i0 + il, r - 1);
+  double bv[4], av[NS][4], cv[NS][4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int kc = k0 + min(4 * ks + kl, kw - 1);
+    bv[ks] = A[fidx<PK>(ri, kc, r, ld)];
+    LDL_PIN(bv[ks]);
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+      const int rj = min(R0 + 16 * (J0 + t) + il, r - 1);
+      av[t][ks] = A[fidx<PK>(rj, kc, r, ld)];
+      LDL_PIN(av[t][ks]);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < NS; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int j = min(R0 + 16 * (J0 + t) + kl + 4 * g, r - 1);
+      cv[t][g] = A[fidx<PK>(max(ri, j), min(ri, j), r, ld)];
+      LDL_PIN(cv[t][g]);
+    }
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) bv[ks] *= dk[ks];  // dk = 0 past kw
+  dbl4 acc[NS];
+#pragma unroll
+  for (int t = 0; t < NS; ++t) acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int t = 0; t < NS; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[t][ks], bv[ks], acc[t], 0, 0, 0);
+#pragma unroll
+  for (int t = 0; t < NS; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int j = R0 + 16 * (J0 + t) + kl + 4 * g, i = i0 + il;
+      if (i < r && j < r && i >= j) A[fidx<PK>(i, j, r, ld)] = cv[t][g] - acc[t][g];
+    }
+}
+
+// C_IJ -= L_J (L_I D)^T over the 16 x 16 tiles (I, J) of the trailing lower triangle with
+// jlo <= J <= min(I, jhi), I < nbr; strips (I, J0 .. J0+3) dealt to waves w0, w0 + wstep, ...
+template <bool PK>
+__device__ __forceinline__ void trail_strips(double* A, int r, int ld, int k0, int kw, int R0, int nbr, int jlo, int jhi,
+                                             const double (&dk)[4], int w0, int wstep, int lane) {
+  int I = jlo, J0 = jlo;
+  auto adv = [&]() {
+    J0 += 4;
+    if (J0 > min(I, jhi)) {
+      ++I;
+      J0 = jlo;
+    }
+  };
+  for (int s = 0; s < w0; ++s) adv();
+  while (I < nbr) {
+    switch (min(4, min(I, jhi) - J0 + 1)) {  // tiles in this strip (wave-uniform)
+      case 1: trail_strip<PK, 1>(A, r, ld, k0, kw, R0, I, J0, dk, lane); break;
+      case 2: trail_strip<PK, 2>(A, r, ld, k0, kw, R0, I, J0, dk, lane); break;
+      case 3: trail_strip<PK, 3>(A, r, ld, k0, kw, R0, I, J0, dk, lane); break;
+      default: trail_strip<PK, 4>(A, r, ld, k0, kw, R0, I, J0, dk, lane); break;
+    }
+    for (int s = 0; s < wstep; ++s) adv();
+  }
+}
+
 template <bool PK>
 __device__ __forceinline__ void blocked_factor_lds(double* A, int r, int w, int ld, double* Dl, double* MK, double* cbuf) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nblk = (w + 15) >> 4;
+  if (wv == 0) factor16r<PK>(A, r, ld, 0, min(16, w), Dl, MK, lane);
+  __syncthreads();
+  for (int kb = 0; kb < nblk; ++kb) {
+    const int k0 = 16 * kb, kw = min(16, w - k0);
+    const int R0 = k0 + kw;                       // first row / column after the pivots
+    const int nbr = (r - R0 + 15) >> 4;           // 16-row blocks below
+    panel_blocks<PK>(A, r, ld, k0, kw, R0, nbr, MK, wv, 4, lane);
+    __syncthreads();
+    double dk[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int k = 4 * ks + (lane >> 4);
+      dk[ks] = (k < kw) ? Dl[k0 + min(k, kw - 1)] : 0.0;
+    }
+    if (kb + 1 < nblk) {
+      // the next pivot block's columns (J = 0: its diagonal block and panel rows) first ...
+      trail_strips<PK>(A, r, ld, k0, kw, R0, nbr, 0, 0, dk, wv, 4, lane);
+      __syncthreads();
+      // ... then one wave factorises it while the other three update the rest (J >= 1)
+      const int fw = (kb + 1) & 3;
+      if (wv == fw)
+        factor16r<PK>(A, r, ld, R0, min(16, w - R0), Dl, MK, lane);
+      else
+        trail_strips<PK>(A, r, ld, k0, kw, R0, nbr, 1, nbr, dk, (wv - fw + 3) & 3, 3, lane);
+    } else {
+      trail_strips<PK>(A, r, ld, k0, kw, R0, nbr, 0, nbr, dk, wv, 4, lane);
+    }
+    __syncthreads();
+  }
+}
+
+template <bool PK>
+__device__ __forceinline__ void blocked_factor_lds_old(double* A, int r, int w, int ld, double* Dl, double* MK,
+                                                       double* cbuf) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   for (int k0 = 0; k0 < w; k0 += 16) {
     const int kw = min(16, w - k0);

@@ -82,6 +82,19 @@ def test_ldl_block_angular(sfm, relax, well):
     assert ls.inertia() == (4000, 0, 3000)
 
 
+@pytest.mark.parametrize("tree_fact,tree_solve", [("0", "0"), ("1", "0"), ("0", "1"), ("1", "1")])
+@pytest.mark.parametrize("well", [True, False])
+def test_ldl_tree_and_level_paths(tree_fact, tree_solve, well, monkeypatch):
+    """The dependency-driven tree kernels (k_fact_tree, k_fwd_tree / k_bwd_tree) and the level-by-level
+    kernels they replace give the oracle's pivots and solution on the same block-angular K2 (the bench's
+    structure); MADIPM_TREE_FACT / MADIPM_TREE_SOLVE = 0 select the level path at analysis time."""
+    monkeypatch.setenv("MADIPM_TREE_FACT", tree_fact)
+    monkeypatch.setenv("MADIPM_TREE_SOLVE", tree_solve)
+    K, Lw = block_angular_k2(3000, 4000, 20, 7, well=well)
+    ls = _check_case(K, Lw, well=well)
+    assert ls.inertia() == (4000, 0, 3000)
+
+
 @pytest.mark.parametrize("well", [True, False])
 def test_ldl_qp_dense_front(well):
     K, Lw = random_k2(150, 400, 0.05, 11, qp=True, well=well)
