@@ -1077,6 +1077,196 @@ __global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t*
   blocked_writeout<PK, false>(A, r, w, ld, Dl, arena + T.l_off[s], arena + T.u_off[s], T.u_ld[s], D, f0, st, tol);
 }
 
+// ------------------------------------------------------------------ leaf absorption
+// A tree front absorbs its micro-leaf children (leaves with w <= 2, r <= 32; SymbolicPlan::absorb).
+// Per batch of leaves (<= kAbsorbRows rows): (1) thread per leaf row gathers the row's entries of the
+// leaf's two columns from the caller's K values (flat index tables: one coalesced round trip + one
+// gather); (2) thread per leaf: pivots d0, l10, d1 (+ D, pivot check); (3) thread per leaf row: its L
+// entries (to the leaf's L panel in HBM, for the solves; kept in LDS); (4) the thread owning front
+// row i adds, for every absorbed update row a listed for row i (child order), U(a, b) =
+// -(l_a0 d0 l_b0 + l_a1 d1 l_b1) into F(i, rel(b)) for the leaf's update rows b <= a — each entry of
+// F has one writer and a fixed order, no atomics.  This replaces the leaves' U blocks in HBM, the
+// micro-factor launch for them, and the gather pass that summed the U blocks.
+// one absorbed update row a (batch-local) of leaf kk[a], owned by front row `row`:
+//  * light row: F(row, col(b)) -= U(a, b) for the leaf's update rows b <= a, and, for each heavy row
+//    a' > a of the leaf, F(row(a'), row) -= U(a', a) (the heavy row's light entries);
+//  * heavy row: only F(row, col(b)) for heavy rows b <= a (incl. the diagonal).
+template <bool PK>
+__device__ __forceinline__ void absorb_entry(double* A, int r, int ld, const double* l0, const double* l1,
+                                             const double* pd0, const double* pd1, const int32_t* rel,
+                                             const int32_t* kk, const int32_t* prow, const int32_t* hv,
+                                             const int32_t* pu0, const int32_t* pend, int a, int row, bool heavy) {
+  const int k = kk[a];
+  const double p0 = l0[a] * pd0[k], p1 = l1[a] * pd1[k];
+  // 8 columns at a time: operands and targets loaded before any store (the targets of one leaf are
+  // distinct, so the eight read-modify-writes of a chunk never alias)
+#pragma unroll 1
+  for (int b = pu0[k]; b <= a; b += 8) {
+    double x0[8], x1[8], av[8];
+    int cb[8];
+    bool on[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int bb = min(b + u, a);
+      x0[u] = l0[bb];
+      x1[u] = l1[bb];
+      cb[u] = rel[bb] + row;
+      on[u] = (b + u <= a) && (!heavy || hv[bb]);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      av[u] = A[cb[u]];
+      LDL_PIN(av[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (on[u]) A[cb[u]] = av[u] - fma(p0, x0[u], p1 * x1[u]);
+  }
+  if (heavy) return;
+  const int cbase = fidx<PK>(0, row, r, ld);
+#pragma unroll 1
+  for (int a2 = a + 1; a2 < pend[k]; ++a2) {
+    if (!hv[a2]) continue;
+    const int t = cbase + prow[a2];  // F(row(a2), row), row(a2) > row
+    A[t] -= fma(l0[a2] * pd0[k], l0[a], l1[a2] * pd1[k] * l1[a]);
+  }
+}
+
+template <bool PK>
+__device__ __forceinline__ void absorb_leaves(const FrontTab& T, int s, int r, int ld, double* A, const double* Kx,
+                                              double* arena, double* D, LDLStatus* st, double tol, double* ext,
+                                              int64_t* dg) {
+  int64_t tph[4] = {0, 0, 0, 0};
+  int64_t tc = dg ? wall_clock64() : 0;
+  auto lap = [&](int k) {
+    if (dg) {
+      const int64_t t2 = wall_clock64();
+      tph[k] += t2 - tc;
+      tc = t2;
+    }
+  };
+  constexpr int NR = SymbolicPlan::kAbsorbRows, NL = SymbolicPlan::kAbsorbLeaves;
+  double* l0 = ext;
+  double* l1 = l0 + NR;
+  double* pd0 = l1 + NR;
+  double* pd1 = pd0 + NL;
+  double* pf10 = pd1 + NL;
+  int64_t* ploff = reinterpret_cast<int64_t*>(pf10 + NL);
+  int32_t* rel = reinterpret_cast<int32_t*>(ploff + NL);  // column base of the parent row
+  int32_t* kk = rel + NR;
+  int32_t* prow = kk + NR;  // parent row
+  int32_t* hv = prow + NR;  // parent row is heavy
+  int32_t* pu0 = hv + NR;   // batch-local first update row of the leaf
+  int32_t* pw = pu0 + NL;
+  int32_t* prc = pw + NL;
+  int32_t* pend = prc + NL;  // batch-local end of the leaf's rows
+  int32_t* ents = pend + NL;  // the front's row lists (rl_ent), kAbsorbEntries at most
+  const int tid = threadIdx.x;
+  const int64_t F0 = T.fr_ptr[s];
+  const int64_t e0 = T.row_ptr[s];
+  const int64_t E0 = T.rl_ptr[e0], E1 = T.rl_ptr[e0 + r];
+  for (int q = tid; q < (int)(E1 - E0); q += NT) ents[q] = T.rl_ent[E0 + q];
+  int lp = (tid < r) ? (int)(T.rl_ptr[e0 + tid] - E0) : 0;
+  const int lend = (tid < r) ? (int)(T.rl_ptr[e0 + tid + 1] - E0) : 0;
+  const bool rowheavy = (tid < r) && T.rheavy[e0 + tid];
+  const int b0 = T.ab_bptr[s], b1 = T.ab_bptr[s + 1];
+  for (int bq = b0; bq < b1; ++bq) {
+    const int k0 = T.ab_bat[bq], k1 = (bq + 1 < b1) ? T.ab_bat[bq + 1] : T.mc_ptr[s + 1];
+    const int64_t j0 = T.ab_first[k0], j1 = T.ab_first[k1];
+    const int nrow = (int)(j1 - j0), nleaf = k1 - k0;
+    // (1) gather the leaf columns' K entries, 4 rows per thread in flight
+    for (int q0 = 0; q0 < nrow; q0 += 4 * NT) {
+      int32_t sa[4], sb[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int q = q0 + u * NT + tid;
+        sa[u] = (q < nrow) ? T.ab_src0[j0 + q] : -1;
+        sb[u] = (q < nrow) ? T.ab_src1[j0 + q] : -1;
+        if (q < nrow) {
+          const int pr = T.ab_rel[j0 + q];  // parent row -> its column base in the LDS front
+          rel[q] = (pr < 0) ? 0 : fidx<PK>(0, pr, r, ld);
+          kk[q] = T.ab_k[j0 + q] - k0;
+          prow[q] = pr;
+          hv[q] = (pr < 0) ? 0 : T.rheavy[e0 + pr];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int q = q0 + u * NT + tid;
+        const double va = (sa[u] >= 0) ? Kx[sa[u]] : 0.0, vb = (sb[u] >= 0) ? Kx[sb[u]] : 0.0;
+        if (q < nrow) {
+          l0[q] = va;
+          l1[q] = vb;
+        }
+      }
+    }
+    __syncthreads();
+    lap(0);
+    // (2) per leaf: pivots
+    for (int k = tid; k < nleaf; k += NT) {
+      const int f0 = T.ab_f0[k0 + k], wrc = T.ab_wrc[k0 + k], w = wrc & 255, rc = wrc >> 8;
+      const int jf = (int)(T.ab_first[k0 + k] - j0);
+      const double d0 = l0[jf];
+      const double f10 = (rc > 1) ? l0[jf + 1] : 0.0;
+      const double l10 = (w == 2) ? f10 / d0 : 0.0;
+      const double d1 = (w == 2) ? l1[jf + 1] - l10 * f10 : 0.0;
+      pd0[k] = d0;
+      pd1[k] = d1;
+      pf10[k] = f10;
+      ploff[k] = T.ab_loff[k0 + k];
+      pu0[k] = jf + w;
+      pw[k] = w;
+      prc[k] = rc;
+      pend[k] = jf + rc;
+      D[f0] = d0;
+      if (bad_pivot(d0, tol)) atomicMin(&st->fail_pivot, f0 + 1);
+      if (w == 2) {
+        D[f0 + 1] = d1;
+        if (bad_pivot(d1, tol)) atomicMin(&st->fail_pivot, f0 + 2);
+      }
+    }
+    __syncthreads();
+    lap(1);
+    // (3) per leaf row: L entries (HBM panel: d on the diagonal, zero above; LDS: l0, l1 of update rows)
+    for (int q = tid; q < nrow; q += NT) {
+      const int k = kk[q];
+      const int w = pw[k], rc = prc[k], i = q - (pu0[k] - w);
+      const double d0 = pd0[k], d1 = pd1[k], f10 = pf10[k];
+      double* __restrict__ L = arena + ploff[k];
+      if (i >= w) {
+        const double li0 = l0[q] / d0;
+        const double li1 = (w == 2) ? (l1[q] - li0 * f10) / d1 : 0.0;
+        l0[q] = li0;
+        l1[q] = li1;
+        L[i] = li0;
+        if (w == 2) L[i + rc] = li1;
+      } else if (i == 0) {
+        L[0] = d0;
+        if (w == 2) L[rc] = 0.0;
+      } else {  // i == 1, w == 2
+        L[1] = f10 / d0;
+        L[1 + rc] = d1;
+      }
+    }
+    __syncthreads();
+    lap(2);
+    // (4) row owners: this batch's absorbed update rows of front row tid, child order
+    const int jr0 = (int)(j0 - F0), jr1 = (int)(j1 - F0);
+    // the row's list was staged in LDS (ents) at the start; a rolled loop keeps the kernel's code
+    // small (one workgroup per CU runs it once: the instruction cache is cold for every front)
+#pragma unroll 1
+    for (; lp < lend; ++lp) {
+      const int ja = ents[lp];
+      if (ja >= jr1) break;  // a later batch's entry
+      absorb_entry<PK>(A, r, ld, l0, l1, pd0, pd1, rel, kk, prow, hv, pu0, pend, ja - jr0, tid, rowheavy);
+    }
+    __syncthreads();
+    lap(3);
+  }
+  if (dg && threadIdx.x == 0)
+    for (int k = 0; k < 4; ++k) dg[8 + k] = tph[k];
+}
+
 // ------------------------------------------------------------------ factorisation tree
 // ONE launch factorises every tree front (SymbolicPlan::ftree: phase-1 fronts of <= 192 rows whose
 // children are pre-leaves or tree fronts).  Workgroups take fronts in topological order from an
@@ -1087,16 +1277,28 @@ __global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t*
 // last workgroup to finish resets the ticket counters for the next launch.
 template <bool PK>
 __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const int32_t* __restrict__ dep, int q0, int q1,
-                                                int32_t* flags, int epoch, double* arena, const double* fscratch,
+                                                int32_t* flags, int epoch, const double* Kx, double* arena,
+                                                const double* fscratch,
                                                 double* D, LDLStatus* st, double tol, int32_t* err, double* A,
                                                 double* Dl, double* MK, double* cbuf, int32_t* rels, int64_t* dg) {
   const int tid = threadIdx.x;
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
   const int ld = PK ? 0 : (r | 1);
-  if (!PK)
+  if (T.absorb[s]) {  // original entries, then the micro-leaf children absorbed in LDS
+    const int ntot = PK ? r * (r + 1) / 2 : r * ld;
+    for (int q = tid; q < ntot; q += NT) A[q] = 0.0;
+    __syncthreads();
+    for (int64_t q = T.asm_ptr[s] + tid; q < T.asm_ptr[s + 1]; q += NT) {
+      const int64_t d = T.asm_dst[q];
+      A[fidx<PK>((int)(d % r), (int)(d / r), r, ld)] = Kx[T.asm_src[q]];
+    }
+    __syncthreads();
+    absorb_leaves<PK>(T, s, r, ld, A, Kx, arena, D, st, tol, A + ((ntot + 1) & ~1), dg);  // 16-byte aligned
+  } else if (!PK) {
     stage_panel(fscratch + T.fs_off[s], A, r, r, ld);
-  else
+  } else {
     stage_front<true>(fscratch + T.fs_off[s], A, r, ld);
+  }
   if (dg) {
     __syncthreads();
     if (tid == 0) dg[1] = wall_clock64();
@@ -1148,7 +1350,8 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
 
 __global__ __launch_bounds__(NT) void k_fact_tree(FrontTab T, const int32_t* __restrict__ order, int nt,
                                                   const int32_t* __restrict__ dep_ptr, const int32_t* __restrict__ dep,
-                                                  int32_t* counter, int32_t* flags, int epoch, double* arena,
+                                                  int32_t* counter, int32_t* flags, int epoch,
+                                                  const double* __restrict__ Kx, double* arena,
                                                   const double* __restrict__ fscratch, double* D, LDLStatus* st,
                                                   double tol, int32_t* err, int64_t* dbg) {
   extern __shared__ __attribute__((aligned(16))) double A[];
@@ -1162,13 +1365,13 @@ __global__ __launch_bounds__(NT) void k_fact_tree(FrontTab T, const int32_t* __r
   const int t = s_task;
   if (t >= nt) return;
   const int s = order[t];
-  int64_t* dg = dbg ? dbg + 8 * t : nullptr;
+  int64_t* dg = dbg ? dbg + 16 * t : nullptr;
   if (dg && threadIdx.x == 0) dg[0] = wall_clock64();
   if (T.nrows[s] <= 128)
-    fact_tree_front<false>(T, s, dep, dep_ptr[t], dep_ptr[t + 1], flags, epoch, arena, fscratch, D, st, tol, err, A, Dl,
+    fact_tree_front<false>(T, s, dep, dep_ptr[t], dep_ptr[t + 1], flags, epoch, Kx, arena, fscratch, D, st, tol, err, A, Dl,
                            MK, cbuf, rels, dg);
   else
-    fact_tree_front<true>(T, s, dep, dep_ptr[t], dep_ptr[t + 1], flags, epoch, arena, fscratch, D, st, tol, err, A, Dl,
+    fact_tree_front<true>(T, s, dep, dep_ptr[t], dep_ptr[t + 1], flags, epoch, Kx, arena, fscratch, D, st, tol, err, A, Dl,
                           MK, cbuf, rels, dg);
   if (threadIdx.x == 0 && atomicAdd(counter + 1, 1) == nt - 1) {  // last one out: reset the tickets
     counter[0] = 0;
@@ -2588,7 +2791,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         if (S.ftree[S.child_list[q]]) dl.push_back(S.child_list[q]);
       dptr.push_back((int32_t)dl.size());
       const int r = S.nrows[s], w = S.first[s + 1] - S.first[s], u = r - w;
-      ftree_lds_ = std::max<int>(ftree_lds_, r <= 128 ? 8 * r * (r | 1) : 8 * r * (r + 1) / 2);
+      ftree_lds_ = std::max<int>(ftree_lds_, (r <= 128 ? 8 * ((r * (r | 1) + 1) & ~1) : 8 * ((r * (r + 1) / 2 + 1) & ~1)) +
+                                                 (S.absorb[s] ? (int)SymbolicPlan::kAbsorbLdsBytes : 0));
       // reads: the pre-assembled lower triangle + the tree children's blocks; writes: L panel, U, D
       ftree_bytes_ += 8.0 * (r * (r + 1) / 2.0 + r * (double)w + u * (u + 1) / 2.0 + w);
       for (int q = S.child_ptr[s]; q < S.child_ptr[s + 1]; ++q)
@@ -2604,10 +2808,60 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     up(ft_dep_, dl);
     fflags_.alloc(std::max(ns, 1));
     fflags_.zero();
+    {
+      std::vector<uint8_t> ab(S.absorb.begin(), S.absorb.end());
+      if (ab.empty()) ab.push_back(0);
+      absorb_.upload(ab);
+      mc_ptr_.upload(S.mc_ptr);
+      mc_list_.upload(S.mc_list.empty() ? std::vector<int32_t>{0} : S.mc_list);
+      rl_ptr_.upload(S.rl_ptr);
+      rl_ent_.upload(S.rl_ent.empty() ? std::vector<int32_t>{0} : S.rl_ent);
+      auto up32 = [](DBuf<int32_t>& d, const std::vector<int32_t>& v) { d.upload(v.empty() ? std::vector<int32_t>{0} : v); };
+      up32(ab_src0_, S.ab_src0);
+      up32(ab_src1_, S.ab_src1);
+      up32(ab_rel_, S.ab_rel);
+      up32(ab_k_, S.ab_k);
+      up32(ab_bptr_, S.ab_bptr);
+      up32(ab_bat_, S.ab_bat);
+      fr_ptr_.upload(S.fr_ptr);
+      ab_first_.upload(S.ab_first);
+      up32(ab_f0_, S.ab_f0);
+      {
+        std::vector<uint8_t> hvv(S.rheavy.begin(), S.rheavy.end());
+        if (hvv.empty()) hvv.push_back(0);
+        rheavy_.upload(hvv);
+        T_.rheavy = rheavy_;
+      }
+      up32(ab_wrc_, S.ab_wrc);
+      {
+        std::vector<int64_t> lo(S.mc_list.size() + 1, 0);
+        for (size_t k = 0; k < S.mc_list.size(); ++k) lo[k] = S.l_off[S.mc_list[k]];
+        ab_loff_.upload(lo);
+      }
+      T_.ab_f0 = ab_f0_;
+      T_.ab_wrc = ab_wrc_;
+      T_.ab_loff = ab_loff_;
+      T_.ab_src0 = ab_src0_;
+      T_.ab_src1 = ab_src1_;
+      T_.ab_rel = ab_rel_;
+      T_.ab_k = ab_k_;
+      T_.ab_bptr = ab_bptr_;
+      T_.ab_bat = ab_bat_;
+      T_.fr_ptr = fr_ptr_;
+      T_.ab_first = ab_first_;
+      T_.absorb = absorb_;
+      T_.mc_ptr = mc_ptr_;
+      T_.mc_list = mc_list_;
+      T_.rl_ptr = rl_ptr_;
+      T_.rl_ent = rl_ent_;
+    }
     fcnt_.alloc(4);
     fcnt_.zero();
     const char* dv = std::getenv("MADIPM_TREE_DEBUG");
-    if (dv && dv[0] == '1' && nftree_) fdbg_.alloc((int64_t)8 * nftree_);
+    if (dv && dv[0] == '1' && nftree_) {
+      fdbg_.alloc((int64_t)16 * nftree_);
+      fdbg_.zero();
+    }
   }
 
   // ---- factorisation launch schedules (phase 1: this shard's subtrees; phase 2: the top fronts)
@@ -2668,6 +2922,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
         const int s = S.level_list[q];
         if (!in_phase(s, phase) || S.ftree[s]) continue;
+        if (S.parent[s] >= 0 && S.absorb[S.parent[s]]) continue;  // factorised by its absorbing parent
         const int r = S.nrows[s], w = S.first[s + 1] - S.first[s];
         if (r <= 32 && w <= 2 && S.fs_off[s] < 0 && !S.is_big[s])
           micro.push_back(s);
@@ -2939,7 +3194,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_bwd_small, hipFuncAttributeMaxDynamicSharedMemorySize, 129 * 128 * 8));
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_fwd_tree, hipFuncAttributeMaxDynamicSharedMemorySize, TREE_LDS_MAX));
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_fact_tree, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   192 * 193 / 2 * 8));
+                                   (int)SymbolicPlan::kFactTreeLdsMax));
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_bwd_tree, hipFuncAttributeMaxDynamicSharedMemorySize, TREE_LDS_MAX));
     attr_done = true;
   }
@@ -3101,9 +3356,9 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
         ++fepoch_;
         TIMED(KK_FACT_TREE, L.bytes, L.flops,
               (k_fact_tree<<<(unsigned)nftree_, NT, L.lds_bytes, s>>>(T_, ft_order_, nftree_, ft_dptr_, ft_dep_, fcnt_,
-                                                                      fflags_, fepoch_, arena_, fscratch_, D_, status_,
+                                                                      fflags_, fepoch_, Kx, arena_, fscratch_, D_, status_,
                                                                       pivot_tol, err_, fdbg_.p)));
-        if (fdbg_.p) tree_debug_dump(s, "fact", fdbg_.p, nftree_, "stage", "wait", "push", "factor", "store");
+        if (fdbg_.p) tree_debug_dump(s, "fact", fdbg_.p, nftree_, "stage", "wait", "push", "factor", "store", 16);
         break;
     }
   }
@@ -3147,12 +3402,12 @@ void LDLSolver::factorize_async(const double* Kx, hipStream_t s) {
   fact_phase2(s);
 }
 
-int LDLSolver::status(hipStream_t s) {
+int LDLSolver::status(hipStream_t s, bool sync) {
   if (S_.N == 0) {
     factorized = true;
     return 0;
   }
-  MADIPM_HIP(hipStreamSynchronize(s));
+  if (sync) MADIPM_HIP(hipStreamSynchronize(s));
   npos = h_status_->npos;
   nneg = h_status_->nneg;
   nzero = h_status_->nzero;
@@ -3164,12 +3419,28 @@ int LDLSolver::status(hipStream_t s) {
 // MADIPM_TREE_DEBUG=1: per-task wall-clock phases of the tree kernels (100 MHz counter), summarised
 // per level on stderr for the first few launches (diagnostics only)
 void LDLSolver::tree_debug_dump(hipStream_t s, const char* what, const int64_t* dbuf, int nt, const char* p1,
-                                const char* p2, const char* p3, const char* p4, const char* p5) {
+                                const char* p2, const char* p3, const char* p4, const char* p5, int stride) {
   static int ndump = 0;
   if (ndump++ >= 8) return;
-  std::vector<int64_t> h((size_t)8 * nt);
-  MADIPM_HIP(hipMemcpyAsync(h.data(), dbuf, h.size() * 8, hipMemcpyDeviceToHost, s));
+  std::vector<int64_t> hs((size_t)stride * nt), h((size_t)8 * nt);
+  MADIPM_HIP(hipMemcpyAsync(hs.data(), dbuf, hs.size() * 8, hipMemcpyDeviceToHost, s));
   MADIPM_HIP(hipStreamSynchronize(s));
+  for (int t = 0; t < nt; ++t)
+    for (int k = 0; k < 8; ++k) h[8 * t + k] = hs[(size_t)stride * t + k];
+  if (stride == 16) {  // absorption phases (gather / pivots / L / row owners), per level
+    std::vector<double> ab((size_t)S_.nlevels * 4, 0.0);
+    std::vector<int> na(S_.nlevels, 0);
+    for (int t = 0; t < nt; ++t) {
+      const int lv = S_.level[(int)h[8 * t + 6]];
+      if (hs[(size_t)16 * t + 8] == 0 && hs[(size_t)16 * t + 11] == 0) continue;
+      na[lv]++;
+      for (int k = 0; k < 4; ++k) ab[lv * 4 + k] += hs[(size_t)16 * t + 8 + k] * 0.01;
+    }
+    for (int lv = 0; lv < S_.nlevels; ++lv)
+      if (na[lv])
+        fprintf(stderr, "  absorb level %d: %d fronts  gather %.2f  pivots %.2f  L %.2f  rows %.2f us\n", lv, na[lv],
+                ab[lv * 4] / na[lv], ab[lv * 4 + 1] / na[lv], ab[lv * 4 + 2] / na[lv], ab[lv * 4 + 3] / na[lv]);
+  }
   int64_t t0 = INT64_MAX, t1 = 0;
   for (int t = 0; t < nt; ++t) t0 = std::min(t0, h[8 * t]), t1 = std::max(t1, h[8 * t + 5]);
   std::vector<double> acc((size_t)S_.nlevels * 8, 0.0);
@@ -3223,7 +3494,7 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
                                                                  arena_, b,
                                                                  xi_, uvec_, err_, tdbg_.p)));
     if (lev == 0 && phase == 0 && ntree_ && tdbg_.p)
-      tree_debug_dump(s, "fwd", tdbg_.p, ntree_, "stage", "wait", "gather", "subst", "store");
+      tree_debug_dump(s, "fwd", tdbg_.p, ntree_, "stage", "wait", "gather", "subst", "store", 8);
   }
 }
 
@@ -3333,10 +3604,10 @@ void ShardGroup::factorize_async(const double* Kx, hipStream_t s) {
   for (int r = 0; r < P; ++r) sh_[r]->fact_phase2(s);
 }
 
-int ShardGroup::status(hipStream_t s) {
-  int st = sh_[0]->status(s);
+int ShardGroup::status(hipStream_t s, bool sync) {
+  int st = sh_[0]->status(s, sync);
   for (size_t r = 1; r < sh_.size(); ++r)
-    MADIPM_REQUIRE(sh_[r]->status(s) == st, "ShardGroup: shards disagree on the factorisation status");
+    MADIPM_REQUIRE(sh_[r]->status(s, false) == st, "ShardGroup: shards disagree on the factorisation status");
   return st;
 }
 

@@ -47,6 +47,24 @@ struct FrontTab {
   // tree front (its contiguous gather range), else to uvec[uvec_off[c] + a] (upos = -1)
   const int64_t* upos;
   double* gbuf;
+  // leaf absorption (SymbolicPlan::absorb / mc_* / rl_*)
+  const uint8_t* absorb;
+  const int32_t* mc_ptr;
+  const int32_t* mc_list;
+  const int64_t* rl_ptr;
+  const int32_t* rl_ent;
+  const int64_t* fr_ptr;
+  const int64_t* ab_first;
+  const int32_t* ab_src0;
+  const int32_t* ab_src1;
+  const int32_t* ab_rel;
+  const int32_t* ab_k;
+  const int32_t* ab_bptr;
+  const int32_t* ab_bat;
+  const int32_t* ab_f0;
+  const int32_t* ab_wrc;
+  const int64_t* ab_loff;
+  const uint8_t* rheavy;
 };
 
 struct SolveTask {
@@ -89,7 +107,8 @@ class LinSolver {
  public:
   virtual ~LinSolver() = default;
   virtual void factorize_async(const double* Kx, hipStream_t s) = 0;
-  virtual int status(hipStream_t s) = 0;
+  // sync = false: the caller already waited for an event recorded after factorize_async
+  virtual int status(hipStream_t s, bool sync = true) = 0;
   virtual void solve_async(double* b, hipStream_t s) = 0;
   virtual const SymbolicPlan& plan() const = 0;
   virtual void set_timing(unsigned mask) = 0;
@@ -110,7 +129,7 @@ class LDLSolver : public LinSolver {
   // Sharded: phase 1, all-reduce of the top fronts (comm), phase 2.
   void factorize_async(const double* Kx, hipStream_t s) override;
   // Synchronise `s` and return 0 or failing pivot + 1; fills the inertia.
-  int status(hipStream_t s) override;
+  int status(hipStream_t s, bool sync = true) override;
   // In-place solve K x = b for a device vector of length n (caller's ordering).
   void solve_async(double* b, hipStream_t s) override;
 
@@ -208,13 +227,17 @@ class LDLSolver : public LinSolver {
   DBuf<int64_t> tdbg_, upos_;
   DBuf<double> gbuf_;
   void tree_debug_dump(hipStream_t s, const char* what, const int64_t* dbuf, int nt, const char* p1, const char* p2,
-                       const char* p3, const char* p4, const char* p5);
+                       const char* p3, const char* p4, const char* p5, int stride);
   // factorisation tree (k_fact_tree): fronts in topological order, their tree children, flags
   // (per-factorisation epoch), ticket counters (reset by the launch's last workgroup)
   int nftree_ = 0, ftree_lds_ = 0, fepoch_ = 0;
   double ftree_bytes_ = 0, ftree_flops_ = 0;
   DBuf<int32_t> ft_order_, ft_dptr_, ft_dep_, fflags_, fcnt_;
-  DBuf<int64_t> fdbg_;
+  DBuf<int64_t> fdbg_, rl_ptr_, fr_ptr_, ab_first_;
+  DBuf<int32_t> ab_src0_, ab_src1_, ab_rel_, ab_k_, ab_bptr_, ab_bat_, ab_f0_, ab_wrc_;
+  DBuf<int64_t> ab_loff_;
+  DBuf<uint8_t> absorb_, rheavy_;
+  DBuf<int32_t> mc_ptr_, mc_list_, rl_ent_;
   DBuf<double> xch_;
   DBuf<uint8_t> wout_, colmask_;
   DBuf<int32_t> tasks_, flags_, flag_off_, counters_, err_, bp_off_;
@@ -254,7 +277,7 @@ class ShardGroup : public LinSolver {
   ShardGroup(int nshards, int n, const int64_t* colptr, const int32_t* rowval, const SymbolicOptions& sopt,
              double pivot_tol, const int32_t* user_perm = nullptr);
   void factorize_async(const double* Kx, hipStream_t s) override;
-  int status(hipStream_t s) override;
+  int status(hipStream_t s, bool sync = true) override;
   void solve_async(double* b, hipStream_t s) override;
   const SymbolicPlan& plan() const override { return sh_[0]->plan(); }
   void set_timing(unsigned mask) override { sh_[0]->set_timing(mask); }

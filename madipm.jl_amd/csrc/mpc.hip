@@ -45,7 +45,7 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int NPART = 16;
-constexpr int MAXB = 1024;
+constexpr int MAXB = 4096;  // partial-reduction blocks (part_ holds MAXB x NPART)
 constexpr double INF = std::numeric_limits<double>::infinity();
 
 struct DCsr {
@@ -648,7 +648,10 @@ __global__ void k_set_mu(DevState* st, double mu) {
   st->max_res_ratio = 0.0;
   st->dx_inf = 0.0;
 }
-__global__ void k_reset_iter(DevState* st) { st->max_res_ratio = 0.0; }
+__global__ void k_reset_iter(DevState* st, int clear_nan) {
+  st->max_res_ratio = 0.0;
+  if (clear_nan) st->nan_flag = 0;
+}
 
 enum {
   FIN_RESID = 0,
@@ -891,6 +894,7 @@ double now() {
 
 MPCSolver::~MPCSolver() {
   for (auto e : fact_events_) (void)hipEventDestroy(e);
+  if (ev_state_) (void)hipEventDestroy(ev_state_);
   if (hst_) (void)hipHostFree(hst_);
   if (stream_) (void)hipStreamDestroy(stream_);
 }
@@ -899,6 +903,10 @@ int MPCSolver::blocks(int64_t n) const {
   int64_t b = (n + NT - 1) / NT;
   return (int)std::max<int64_t>(1, std::min<int64_t>(MAXB, b));
 }
+
+// GROUP_LOOP SpMV kernels: one row per lane group (spmv_g_ lanes), so a group walks one row instead
+// of a dependent chain of rows (the row loads are latency-bound)
+int MPCSolver::spmv_blocks(int64_t rows) const { return blocks(rows * spmv_g_); }
 
 static void csr_from_coo(int nrow, const std::vector<int32_t>& r, const std::vector<int32_t>& c,
                          const std::vector<double>& v, std::vector<int64_t>& rp, std::vector<int32_t>& ci,
@@ -928,6 +936,7 @@ static void csr_from_coo(int nrow, const std::vector<int32_t>& r, const std::vec
 MPCSolver::MPCSolver(const madipm_qp& qp, const madipm_options& opt, Comm* comm) : opt_(opt), comm_(comm) {
   const double t0 = now();
   MADIPM_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  MADIPM_HIP(hipEventCreateWithFlags(&ev_state_, hipEventDisableTiming));
   MADIPM_HIP(hipHostMalloc((void**)&hst_, sizeof(DevState), hipHostMallocDefault));
   std::memset(hst_, 0, sizeof(DevState));
   setup_host(qp);
@@ -1421,9 +1430,9 @@ void MPCSolver::factor_enqueue(double dw, double dc) {
 void MPCSolver::kkt_solve() {
   DV_ARGS;
   if (kkt_ == KKT_NORMAL) {
-    SPMV_LAUNCH(k_normal_rhs, blocks(m_), stream_, D);
+    SPMV_LAUNCH(k_normal_rhs, spmv_blocks(m_), stream_, D);
     ldl_->solve_async(bufm_.p, stream_);
-    SPMV_LAUNCH(k_normal_back, blocks(n_ + m_), stream_, D);
+    SPMV_LAUNCH(k_normal_back, spmv_blocks(n_ + m_), stream_, D);
   } else {
     ldl_->solve_async(d_.p, stream_);
     if (kkt_ == KKT_K25) k_k25_unscale<<<blocks(n_), NT, 0, stream_>>>(D);
@@ -1453,11 +1462,11 @@ void MPCSolver::launch_reduce_final(int kind, int nb) {
 // solve_system! (linear_solver.jl:19-44): rhs (mode) -> LDL^T solve -> finish + residual
 void MPCSolver::solve_system(int mode, double mu) {
   DV_ARGS;
-  const int nb = blocks(n_ + m_);
+  const int nb = blocks(n_ + m_), nbs = spmv_blocks(n_ + m_);
   k_rhs<<<nb, NT, 0, stream_>>>(D, mode, mu);
   kkt_solve();
-  SPMV_LAUNCH(k_residual, nb, stream_, D, del_w_, del_c_);
-  launch_reduce_final(FIN_RESID, nb);
+  SPMV_LAUNCH(k_residual, nbs, stream_, D, del_w_, del_c_);
+  launch_reduce_final(FIN_RESID, nbs);
 }
 
 // gondzio_correction_direction! (solver.jl:245-298): host-controlled loop, one read-back per solve
@@ -1617,6 +1626,43 @@ void MPCSolver::initialize_public() {
   initialized_ = true;
 }
 
+// prediction_step! (solver.jl:230-237) + mehrotra_correction_direction! (solver.jl:239-243)
+void MPCSolver::directions(bool redo) {
+  DV_ARGS;
+  hipStream_t s = stream_;
+  const int nbz = blocks(std::max(nlb_, nub_));
+  k_reset_iter<<<1, 1, 0, s>>>(st_, redo ? 1 : 0);
+  solve_system(RHS_PRED, 0.0);
+  k_alpha<<<nbz, NT, 0, s>>>(D, ALPHA_PRED, 1.0);
+  {
+    FinParams P{nbz, ALPHA_PRED, 0, 0, 0};
+    k_final<<<1, NT, 0, s>>>(D, FIN_ALPHA, P);
+  }
+  // mu_affine at (alpha_aff_p, alpha_aff_d) and mu_curr; the alphas never leave the device
+  k_mu<<<nbz, NT, 0, s>>>(D, 1, 0.0, 0.0);
+  launch_reduce_final(FIN_MU_PRED, nbz);
+  solve_system(RHS_CORR, 0.0);
+}
+
+// update_step_size! (solver.jl:304-307)
+void MPCSolver::step_size() {
+  DV_ARGS;
+  hipStream_t s = stream_;
+  const int nbz = blocks(std::max(nlb_, nub_));
+  if (opt_.step_rule == 2) {
+    k_alpha<<<nbz, NT, 0, s>>>(D, ALPHA_MEHROTRA, 1.0);
+    FinParams P{nbz, ALPHA_MEHROTRA, 0, 0, 0};
+    k_final<<<1, NT, 0, s>>>(D, FIN_ALPHA, P);
+    k_mu<<<nbz, NT, 0, s>>>(D, 1, 0.0, 0.0);
+    launch_reduce_final(FIN_MU_FULL, nbz);
+  } else {
+    const int mode = opt_.step_rule == 0 ? ALPHA_CONSERVATIVE : ALPHA_ADAPTIVE;
+    k_alpha<<<nbz, NT, 0, s>>>(D, mode, opt_.step_tau);
+    FinParams P{nbz, mode, 0, 0, 0};
+    k_final<<<1, NT, 0, s>>>(D, FIN_ALPHA, P);
+  }
+}
+
 int MPCSolver::solve(madipm_stats* stats) {
   DV_ARGS;
   hipStream_t s = stream_;
@@ -1655,8 +1701,22 @@ int MPCSolver::solve(madipm_stats* stats) {
       fact_events_.push_back(e0);
       fact_events_.push_back(e1);
       read_state();
-      const int frc = ldl_->status(s);  // synchronizes the stream
+      MADIPM_HIP(hipEventRecord(ev_state_, s));
+      // speculation: this iteration's directions (prediction_step!, mehrotra_correction_direction!,
+      // update_step_size!) are enqueued BEFORE the host reads the termination test and the
+      // factorisation status, so the GPU is busy while the host decides; they write scratch vectors
+      // and step scalars only (the iterate is updated by k_apply, enqueued after the decision), are
+      // discarded on termination and recomputed after a failed factorisation's retries.  Gondzio's
+      // loop synchronises internally: not speculated.
+      const bool spec = opt_.max_ncorr == 0;
+      if (spec) {
+        directions(false);
+        step_size();
+      }
+      MADIPM_HIP(hipEventSynchronize(ev_state_));
+      const int frc = ldl_->status(s, false);
       const DevState& h = *hst_;
+      last_ = h;
       if (h.nan_flag) {
         status = MADIPM_ERROR_IN_STEP_COMPUTATION;
         break;
@@ -1708,40 +1768,21 @@ int MPCSolver::solve(madipm_stats* stats) {
           del_w_ *= 100.0;
           del_c_ *= 100.0;
         }
+        if (spec) {  // the speculated directions used the failed factor: recompute
+          directions(true);
+          step_size();
+        }
       }
-      k_reset_iter<<<1, 1, 0, s>>>(st_);
-      // ---- prediction_step! (solver.jl:230-237)
-      solve_system(RHS_PRED, 0.0);
-      k_alpha<<<nbz, NT, 0, s>>>(D, ALPHA_PRED, 1.0);
-      {
-        FinParams P{nbz, ALPHA_PRED, 0, 0, 0};
-        k_final<<<1, NT, 0, s>>>(D, FIN_ALPHA, P);
-      }
-      // mu_affine at (alpha_aff_p, alpha_aff_d) and mu_curr; the alphas never leave the device
-      k_mu<<<nbz, NT, 0, s>>>(D, 1, 0.0, 0.0);
-      launch_reduce_final(FIN_MU_PRED, nbz);
-      // ---- mehrotra_correction_direction! (solver.jl:239-243)
-      solve_system(RHS_CORR, 0.0);
-      // ---- gondzio_correction_direction! (solver.jl:245-298)
-      if (opt_.max_ncorr > 0) gondzio();
-      // ---- update_step_size! (solver.jl:304-307)
-      if (opt_.step_rule == 2) {
-        k_alpha<<<nbz, NT, 0, s>>>(D, ALPHA_MEHROTRA, 1.0);
-        FinParams P{nbz, ALPHA_MEHROTRA, 0, 0, 0};
-        k_final<<<1, NT, 0, s>>>(D, FIN_ALPHA, P);
-        k_mu<<<nbz, NT, 0, s>>>(D, 1, 0.0, 0.0);
-        launch_reduce_final(FIN_MU_FULL, nbz);
-      } else {
-        const int mode = opt_.step_rule == 0 ? ALPHA_CONSERVATIVE : ALPHA_ADAPTIVE;
-        k_alpha<<<nbz, NT, 0, s>>>(D, mode, opt_.step_tau);
-        FinParams P{nbz, mode, 0, 0, 0};
-        k_final<<<1, NT, 0, s>>>(D, FIN_ALPHA, P);
+      if (!spec) {
+        directions(false);
+        gondzio();  // gondzio_correction_direction! (solver.jl:245-298)
+        step_size();
       }
       // ---- apply_step! + evaluate_model!
       k_apply<<<nb, NT, 0, s>>>(D);
       ++k_;
-      SPMV_LAUNCH(k_eval, nb, s, D);
-      launch_reduce_final(FIN_EVAL, nb);
+      SPMV_LAUNCH(k_eval, spmv_blocks(n_ + m_), s, D);
+      launch_reduce_final(FIN_EVAL, spmv_blocks(n_ + m_));
       MADIPM_HIP(hipGetLastError());
     }
   } catch (const Error& e) {
@@ -1759,18 +1800,23 @@ int MPCSolver::solve(madipm_stats* stats) {
     if (hipEventElapsedTime(&ms, fact_events_[q], fact_events_[q + 1]) == hipSuccess) t_linsol_ += ms * 1e-3;
   }
   if (stats) {
-    read_state();
-    MADIPM_HIP(hipStreamSynchronize(s));
+    // the state read at the last termination test (the speculated directions after it changed only
+    // step scalars, never the iterate)
+    if (trace_.empty()) {
+      read_state();
+      MADIPM_HIP(hipStreamSynchronize(s));
+      last_ = *hst_;
+    }
     stats->status = status;
     stats->iter = k_;
-    double obj = hst_->obj_val / obj_scale_;
+    double obj = last_.obj_val / obj_scale_;
     if (!H_->minimize) obj = -obj;
     stats->objective = obj;
-    stats->dual_objective = hst_->dobj / obj_scale_;
+    stats->dual_objective = last_.dobj / obj_scale_;
     stats->inf_pr = inf_pr_;
     stats->inf_du = inf_du_;
     stats->inf_compl = inf_compl_;
-    stats->mu = hst_->mu;
+    stats->mu = last_.mu;
     stats->total_time = t_total_;
     stats->linear_solver_time = t_linsol_;
     stats->init_time = t_init_;

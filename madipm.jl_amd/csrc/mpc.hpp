@@ -62,6 +62,8 @@ class MPCSolver {
   void factorize_regularized();
   void solve_system(int mode, double mu);
   void gondzio();
+  void directions(bool redo);  // predictor + corrector directions (speculated before the status read)
+  void step_size();
   void launch_reduce_final(int kind, int nvals);
   void read_state();
   void kkt_diag(double dw, double dc);
@@ -72,6 +74,7 @@ class MPCSolver {
   void kkt_solve();
   void factor_enqueue(double dw, double dc);
   int blocks(int64_t n) const;
+  int spmv_blocks(int64_t rows) const;
 
   madipm_options opt_{};
   hipStream_t stream_ = nullptr;
@@ -110,6 +113,8 @@ class MPCSolver {
   double t_init_ = 0, t_total_ = 0, t_linsol_ = 0;
   std::vector<madipm_iter_trace> trace_;
   std::vector<hipEvent_t> fact_events_;
+  hipEvent_t ev_state_ = nullptr;  // recorded after the per-iteration state read-back
+  DevState last_{};                // the state of the last termination test
 };
 
 }  // namespace madipm

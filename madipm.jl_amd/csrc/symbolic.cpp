@@ -7,6 +7,7 @@
 #include "symbolic.hpp"
 
 #include <algorithm>
+#include <climits>
 #include <cstdlib>
 #include <numeric>
 
@@ -710,10 +711,133 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       S.ftree[s] = ok && fanin <= SymbolicPlan::kFactTreeFanIn;
     }
   }
+  // leaf absorption: a tree front whose pre-leaf children are all micro leaves (w <= 2, r <= 32)
+  // factorises them itself inside k_fact_tree and adds their rank-1/2 updates straight into its LDS
+  // front (row-owner lists rl_*: for front row i, the (child k, update row a) pairs in child order),
+  // replacing the micro launch + the gather pre-assembly for that front.
+  S.absorb.assign(ns, 0);
+  S.mc_ptr.assign(ns + 1, 0);
+  S.mc_list.clear();
+  S.rl_ptr.assign(S.row_ptr[ns] + 1, 0);
+  S.rl_ent.clear();
+  {
+    // experimental (off by default): the row-owner pass is latency-bound on dense rows and loses to
+    // the gather pre-assembly on the ex10 stand-in; MADIPM_ABSORB=1 enables it
+    const char* ev = std::getenv("MADIPM_ABSORB");
+    const bool on = ev && ev[0] == '1';
+    auto micro_leaf = [&](int c) {
+      return S.child_ptr[c] == S.child_ptr[c + 1] && S.nrows[c] <= 32 && S.first[c + 1] - S.first[c] <= 2;
+    };
+    for (int s = 0; s < ns; ++s) {
+      S.mc_ptr[s + 1] = S.mc_ptr[s];
+      if (!on || !S.ftree[s]) continue;
+      const int64_t r = S.nrows[s];
+      const int64_t front_bytes = 8 * (r <= 128 ? r * (r | 1) : r * (r + 1) / 2);
+      if (front_bytes + SymbolicPlan::kAbsorbLdsBytes > SymbolicPlan::kFactTreeLdsMax) continue;
+      int nmc = 0;
+      bool ok = true;
+      for (int64_t qc = S.child_ptr[s]; qc < S.child_ptr[s + 1] && ok; ++qc) {
+        const int c = S.child_list[qc];
+        if (S.ftree[c]) continue;
+        ok = micro_leaf(c);
+        ++nmc;
+      }
+      if (!ok || nmc == 0) continue;
+      int64_t nent = 0;  // the row lists are staged in LDS: bounded
+      for (int64_t qc = S.child_ptr[s]; qc < S.child_ptr[s + 1]; ++qc)
+        if (!S.ftree[S.child_list[qc]]) nent += S.nrows[S.child_list[qc]];
+      if (nent > SymbolicPlan::kAbsorbEntries) continue;
+      S.absorb[s] = 1;
+      for (int64_t qc = S.child_ptr[s]; qc < S.child_ptr[s + 1]; ++qc)
+        if (!S.ftree[S.child_list[qc]]) S.mc_list.push_back(S.child_list[qc]);
+      S.mc_ptr[s + 1] = (int32_t)S.mc_list.size();
+    }
+    // flat leaf-row tables: the rows of a front's absorbed leaves in child order; per row the caller's
+    // CSC index of its entry in the leaf's column 0 / 1 (-1: structural zero), its parent row (-1 for a
+    // pivot row) and its leaf; per leaf its first flat row; batches of <= kAbsorbRows rows /
+    // kAbsorbLeaves leaves per front
+    const int nmc_all = (int)S.mc_list.size();
+    S.ab_first.assign(nmc_all + 1, 0);
+    S.ab_f0.assign(nmc_all + 1, 0);
+    S.ab_wrc.assign(nmc_all + 1, 0);
+    S.fr_ptr.assign(ns + 1, 0);
+    S.ab_bptr.assign(ns + 1, 0);
+    S.ab_src0.clear();
+    S.ab_src1.clear();
+    S.ab_rel.clear();
+    S.ab_k.clear();
+    S.ab_bat.clear();
+    std::vector<int64_t> col0(32), col1(32);
+    for (int s = 0; s < ns; ++s) {
+      S.fr_ptr[s] = (int64_t)S.ab_src0.size();
+      int rows_in = 0, leaves_in = 0;
+      for (int k = S.mc_ptr[s]; k < S.mc_ptr[s + 1]; ++k) {
+        const int c = S.mc_list[k];
+        const int rc = S.nrows[c], wc = S.first[c + 1] - S.first[c];
+        if (k == S.mc_ptr[s] || rows_in + rc > SymbolicPlan::kAbsorbRows || leaves_in + 1 > SymbolicPlan::kAbsorbLeaves) {
+          S.ab_bat.push_back(k);
+          rows_in = 0;
+          leaves_in = 0;
+        }
+        rows_in += rc;
+        leaves_in += 1;
+        S.ab_first[k] = (int64_t)S.ab_src0.size();
+        S.ab_f0[k] = S.first[c];
+        S.ab_wrc[k] = wc | (rc << 8);
+        std::fill(col0.begin(), col0.end(), -1);
+        std::fill(col1.begin(), col1.end(), -1);
+        for (int64_t q = S.asm_ptr[c]; q < S.asm_ptr[c + 1]; ++q) {
+          const int64_t d = S.asm_dst[q];
+          const int lc = (int)(d / rc), lr = (int)(d % rc);
+          (lc == 0 ? col0 : col1)[lr] = S.asm_src[q];
+        }
+        for (int i = 0; i < rc; ++i) {
+          MADIPM_REQUIRE(col0[i] < INT32_MAX && col1[i] < INT32_MAX, "absorbed leaf: CSC index beyond int32");
+          S.ab_src0.push_back((int32_t)col0[i]);
+          S.ab_src1.push_back((int32_t)col1[i]);
+          S.ab_rel.push_back(i >= wc ? S.rel[S.rel_ptr[c] + (i - wc)] : -1);
+          S.ab_k.push_back(k);
+        }
+      }
+      S.ab_bptr[s + 1] = (int32_t)S.ab_bat.size();
+    }
+    S.fr_ptr[ns] = (int64_t)S.ab_src0.size();
+    S.ab_first[nmc_all] = (int64_t)S.ab_src0.size();
+    // row-owner lists: for front row i, the front-relative flat indices of the absorbed update rows
+    // landing in row i, in child order (= increasing)
+    for (int s = 0; s < ns; ++s)
+      for (int k = S.mc_ptr[s]; k < S.mc_ptr[s + 1]; ++k) {
+        const int c = S.mc_list[k];
+        for (int64_t a = 0; a < S.rel_ptr[c + 1] - S.rel_ptr[c]; ++a) S.rl_ptr[S.row_ptr[s] + S.rel[S.rel_ptr[c] + a] + 1]++;
+      }
+    for (int64_t t = 0; t < S.row_ptr[ns]; ++t) S.rl_ptr[t + 1] += S.rl_ptr[t];
+    S.rl_ent.assign(S.rl_ptr[S.row_ptr[ns]], 0);
+    std::vector<int64_t> fill(S.rl_ptr.begin(), S.rl_ptr.end() - 1);
+    for (int s = 0; s < ns; ++s)
+      for (int k = S.mc_ptr[s]; k < S.mc_ptr[s + 1]; ++k) {
+        const int c = S.mc_list[k];
+        const int wc = S.first[c + 1] - S.first[c];
+        for (int64_t a = 0; a < S.rel_ptr[c + 1] - S.rel_ptr[c]; ++a)
+          S.rl_ent[fill[S.row_ptr[s] + S.rel[S.rel_ptr[c] + a]]++] = (int32_t)(S.ab_first[k] + wc + a - S.fr_ptr[s]);
+      }
+    // heavy rows (in most absorbed leaves): their (heavy row, light column) entries are added by the
+    // light column's owner instead, so no thread carries a dense row alone
+    S.rheavy.assign(S.row_ptr[ns], 0);
+    const char* hev = std::getenv("MADIPM_ABSORB_HEAVY");
+    const bool heavy_on = hev && hev[0] == '1';
+    for (int s = 0; s < ns; ++s) {
+      if (!S.absorb[s]) continue;
+      const int64_t e0 = S.row_ptr[s];
+      const int r = S.nrows[s];
+      const double mean = (double)(S.rl_ptr[e0 + r] - S.rl_ptr[e0]) / std::max(1, r);
+      for (int i = 0; i < r; ++i)
+        S.rheavy[e0 + i] = heavy_on && (S.rl_ptr[e0 + i + 1] - S.rl_ptr[e0 + i]) > std::max(24.0, 3.0 * mean);
+    }
+  }
   S.fs_off.assign(ns, -1);
   S.fs_size = 0;
   for (int s = 0; s < ns; ++s)
-    if (S.ftree[s] || (!S.is_big[s] && S.child_ptr[s + 1] > S.child_ptr[s] && S.mine(s))) {
+    if ((S.ftree[s] && !S.absorb[s]) || (!S.ftree[s] && !S.is_big[s] && S.child_ptr[s + 1] > S.child_ptr[s] && S.mine(s))) {
       S.fs_off[s] = S.fs_size;
       S.fs_size += (int64_t)S.nrows[s] * S.nrows[s];
     }
@@ -849,7 +973,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     // factorisation-tree pre-assembly (after the level-0 launches), tree fronts in level order
     for (int lev = 0; lev < NL; ++lev)
       for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q)
-        if (S.ftree[S.level_list[q]]) emit(S.level_list[q], true, 3, false, true);
+        if (S.ftree[S.level_list[q]] && !S.absorb[S.level_list[q]]) emit(S.level_list[q], true, 3, false, true);
     close_group(2 * NL + 1);
     S.g_chunk.push_back((int64_t)S.g_src.size());  // sentinel
     MADIPM_REQUIRE(S.g_src.size() < (size_t)INT32_MAX * 2 && S.atiles.size() < (size_t)INT32_MAX, "assembly plan too large");

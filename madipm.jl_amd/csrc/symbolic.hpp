@@ -102,6 +102,24 @@ struct SymbolicPlan {
   static constexpr int kFactTreeMax = 192;
   static constexpr int kFactTreeFanIn = 8;
   std::vector<uint8_t> ftree;          // factorisation-tree fronts (k_fact_tree)
+  // leaf absorption (tree fronts whose pre-leaf children are all micro leaves): their micro children
+  // mc_list[mc_ptr[s] ..), and per front row (row_ptr[s] + i) the (child k << 5 | update row a)
+  // pairs landing in that row, child order
+  static constexpr int64_t kFactTreeLdsMax = 150 * 1024;  // dynamic LDS of k_fact_tree
+  static constexpr int kAbsorbRows = 512, kAbsorbLeaves = 128;  // per absorption batch
+  static constexpr int kAbsorbEntries = 4096;                   // row-list entries per front (LDS)
+  // batch staging in LDS: l0, l1 (8 B each) + column base, leaf, parent row, heavy flag (4 B each) per
+  // row; d0, d1, f10, l_off (8 B each) + first update row, w, rc, end row (4 B each) per leaf
+  static constexpr int64_t kAbsorbLdsBytes = 32 * kAbsorbRows + 48 * kAbsorbLeaves + 4 * kAbsorbEntries;
+  std::vector<uint8_t> absorb;
+  std::vector<int32_t> mc_ptr, mc_list;
+  std::vector<int64_t> rl_ptr;
+  std::vector<int32_t> rl_ent;        // front-relative flat row of the absorbed update row
+  std::vector<int64_t> fr_ptr, ab_first;  // per front: its flat rows; per absorbed leaf: first flat row
+  std::vector<int32_t> ab_src0, ab_src1, ab_rel, ab_k;  // per flat row
+  std::vector<int32_t> ab_f0, ab_wrc;  // per absorbed leaf: first pivot, w | rc << 8 (l_off: LDLSolver)
+  std::vector<uint8_t> rheavy;        // per front row (row_ptr[s] + i): dense in the absorbed leaves
+  std::vector<int32_t> ab_bptr, ab_bat;  // per front: batch starts (leaf index k) ab_bat[ab_bptr[s] ..)
   int64_t fs_size = 0;
   // forward-solve gather: for every front row, the children's update-vector entries in child order
   std::vector<int64_t> sv_ptr, sv_src;  // sv_ptr indexed by row_ptr[s] + i

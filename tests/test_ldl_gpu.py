@@ -96,6 +96,17 @@ def test_ldl_tree_and_level_paths(tree_fact, tree_solve, well, monkeypatch):
 
 
 @pytest.mark.parametrize("well", [True, False])
+def test_ldl_leaf_absorption(well, monkeypatch):
+    """Experimental leaf absorption (MADIPM_ABSORB=1): tree fronts factorise their micro-leaf children
+    themselves and add the leaves' updates in LDS (row-owner lists) — same pivots / solution as the
+    oracle."""
+    monkeypatch.setenv("MADIPM_ABSORB", "1")
+    K, Lw = block_angular_k2(3000, 4000, 20, 7, well=well)
+    ls = _check_case(K, Lw, well=well)
+    assert ls.inertia() == (4000, 0, 3000)
+
+
+@pytest.mark.parametrize("well", [True, False])
 def test_ldl_qp_dense_front(well):
     K, Lw = random_k2(150, 400, 0.05, 11, qp=True, well=well)
     ls = _check_case(K, Lw, small_front_max=128, well=well)
