@@ -831,7 +831,7 @@ __device__ __forceinline__ void panel_blocks(double* A, int r, int ld, int k0, i
 // predicated MFMA makes the compiler drain the accumulators after every step).
 template <bool PK, int NS>
 __device__ __forceinline__ void trail_strip(double* A, int r, int ld, int k0, int kw, int R0, int I, int J0,
-                                            const double (&dk)[4], int lane) {
+                                            const double (&dk)[4], int lane, int jend) {
   const int kl = lane >> 4, il = lane & 15;
   const int i0 = R0 + 16 * I;
   const int ri = min(i0 + il, r - 1);
@@ -870,7 +870,7 @@ __device__ __forceinline__ void trail_strip(double* A, int r, int ld, int k0, in
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int j = R0 + 16 * (J0 + t) + kl + 4 * g, i = i0 + il;
-      if (i < r && j < r && i >= j) A[fidx<PK>(i, j, r, ld)] = cv[t][g] - acc[t][g];
+      if (i < r && j < jend && i >= j) A[fidx<PK>(i, j, r, ld)] = cv[t][g] - acc[t][g];
     }
 }
 
@@ -878,7 +878,8 @@ __device__ __forceinline__ void trail_strip(double* A, int r, int ld, int k0, in
 // jlo <= J <= min(I, jhi), I < nbr; strips (I, J0 .. J0+3) dealt to waves w0, w0 + wstep, ...
 template <bool PK>
 __device__ __forceinline__ void trail_strips(double* A, int r, int ld, int k0, int kw, int R0, int nbr, int jlo, int jhi,
-                                             const double (&dk)[4], int w0, int wstep, int lane) {
+                                             const double (&dk)[4], int w0, int wstep, int lane, int jend) {
+  if (jlo > jhi) return;
   int I = jlo, J0 = jlo;
   auto adv = [&]() {
     J0 += 4;
@@ -890,26 +891,119 @@ __device__ __forceinline__ void trail_strips(double* A, int r, int ld, int k0, i
   for (int s = 0; s < w0; ++s) adv();
   while (I < nbr) {
     switch (min(4, min(I, jhi) - J0 + 1)) {  // tiles in this strip (wave-uniform)
-      case 1: trail_strip<PK, 1>(A, r, ld, k0, kw, R0, I, J0, dk, lane); break;
-      case 2: trail_strip<PK, 2>(A, r, ld, k0, kw, R0, I, J0, dk, lane); break;
-      case 3: trail_strip<PK, 3>(A, r, ld, k0, kw, R0, I, J0, dk, lane); break;
-      default: trail_strip<PK, 4>(A, r, ld, k0, kw, R0, I, J0, dk, lane); break;
+      case 1: trail_strip<PK, 1>(A, r, ld, k0, kw, R0, I, J0, dk, lane, jend); break;
+      case 2: trail_strip<PK, 2>(A, r, ld, k0, kw, R0, I, J0, dk, lane, jend); break;
+      case 3: trail_strip<PK, 3>(A, r, ld, k0, kw, R0, I, J0, dk, lane, jend); break;
+      default: trail_strip<PK, 4>(A, r, ld, k0, kw, R0, I, J0, dk, lane, jend); break;
     }
     for (int s = 0; s < wstep; ++s) adv();
   }
 }
 
+// Deferred Schur complement: U -= L_U D L_U^T over all w pivots in one pass (tiles of the lower
+// triangle of A[w:, w:]).  K runs over the pivots in 16-column chunks with the accumulators held in
+// registers, so each C tile is loaded and stored once (the per-block right-looking update touches it
+// w/16 times); the next chunk's operands are loaded before the current chunk's MFMAs.
+template <bool PK, int NS>
+__device__ __forceinline__ void schur_strip(double* A, int r, int ld, int w, const double* Dl, int I, int J0, int lane) {
+  const int kl = lane >> 4, il = lane & 15;
+  const int i0 = w + 16 * I;
+  const int ri = min(i0 + il, r - 1);
+  int rj[NS];
+#pragma unroll
+  for (int t = 0; t < NS; ++t) rj[t] = min(w + 16 * (J0 + t) + il, r - 1);
+  dbl4 acc[NS];
+#pragma unroll
+  for (int t = 0; t < NS; ++t) acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
+  double bv[4], av[NS][4];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int kc = min(k0 + 4 * ks + kl, w - 1);
+      const double d = Dl[kc];
+      double b = A[fidx<PK>(ri, kc, r, ld)];
+      LDL_PIN(b);
+      bv[ks] = (k0 + 4 * ks + kl < w) ? b * d : 0.0;
+#pragma unroll
+      for (int t = 0; t < NS; ++t) {
+        av[t][ks] = A[fidx<PK>(rj[t], kc, r, ld)];
+        LDL_PIN(av[t][ks]);
+      }
+    }
+  };
+  load(0);
+  for (int k0 = 0; k0 < w; k0 += 16) {
+    double b2[4], a2[NS][4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      b2[ks] = bv[ks];
+#pragma unroll
+      for (int t = 0; t < NS; ++t) a2[t][ks] = av[t][ks];
+    }
+    if (k0 + 16 < w) load(k0 + 16);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int t = 0; t < NS; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a2[t][ks], b2[ks], acc[t], 0, 0, 0);
+  }
+  double cv[NS][4];
+#pragma unroll
+  for (int t = 0; t < NS; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int j = min(w + 16 * (J0 + t) + kl + 4 * g, r - 1);
+      cv[t][g] = A[fidx<PK>(max(ri, j), min(ri, j), r, ld)];
+      LDL_PIN(cv[t][g]);
+    }
+#pragma unroll
+  for (int t = 0; t < NS; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int j = w + 16 * (J0 + t) + kl + 4 * g, i = i0 + il;
+      if (i < r && j < r && i >= j) A[fidx<PK>(i, j, r, ld)] = cv[t][g] - acc[t][g];
+    }
+}
+
 template <bool PK>
-__device__ __forceinline__ void blocked_factor_lds(double* A, int r, int w, int ld, double* Dl, double* MK, double* cbuf) {
+__device__ __forceinline__ void schur_strips(double* A, int r, int ld, int w, const double* Dl, int wv, int lane) {
+  const int nbu = (r - w + 15) >> 4;
+  int I = 0, J0 = 0;
+  auto adv = [&]() {
+    J0 += 4;
+    if (J0 > I) {
+      ++I;
+      J0 = 0;
+    }
+  };
+  for (int q = 0; q < wv; ++q) adv();
+  while (I < nbu) {
+    switch (min(4, I - J0 + 1)) {
+      case 1: schur_strip<PK, 1>(A, r, ld, w, Dl, I, J0, lane); break;
+      case 2: schur_strip<PK, 2>(A, r, ld, w, Dl, I, J0, lane); break;
+      case 3: schur_strip<PK, 3>(A, r, ld, w, Dl, I, J0, lane); break;
+      default: schur_strip<PK, 4>(A, r, ld, w, Dl, I, J0, lane); break;
+    }
+    for (int q = 0; q < 4; ++q) adv();
+  }
+}
+
+// defer: the right-looking block steps update only the pivot columns (columns < w); the update
+// block U gets its whole Schur complement afterwards in one pass (schur_strips)
+template <bool PK>
+__device__ __forceinline__ void blocked_factor_lds(double* A, int r, int w, int ld, double* Dl, double* MK, double* cbuf,
+                                                   int defer = 0) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nblk = (w + 15) >> 4;
+  defer = defer && w < r;
+  const int jend = defer ? w : r;
   if (wv == 0) factor16r<PK>(A, r, ld, 0, min(16, w), Dl, MK, lane);
   __syncthreads();
   for (int kb = 0; kb < nblk; ++kb) {
     const int k0 = 16 * kb, kw = min(16, w - k0);
     const int R0 = k0 + kw;                       // first row / column after the pivots
     const int nbr = (r - R0 + 15) >> 4;           // 16-row blocks below
+    const int jhi = defer ? ((w - R0 + 15) >> 4) - 1 : nbr;  // last column block updated
     panel_blocks<PK>(A, r, ld, k0, kw, R0, nbr, MK, wv, 4, lane);
     __syncthreads();
     double dk[4];
@@ -920,17 +1014,21 @@ __device__ __forceinline__ void blocked_factor_lds(double* A, int r, int w, int 
     }
     if (kb + 1 < nblk) {
       // the next pivot block's columns (J = 0: its diagonal block and panel rows) first ...
-      trail_strips<PK>(A, r, ld, k0, kw, R0, nbr, 0, 0, dk, wv, 4, lane);
+      trail_strips<PK>(A, r, ld, k0, kw, R0, nbr, 0, 0, dk, wv, 4, lane, jend);
       __syncthreads();
       // ... then one wave factorises it while the other three update the rest (J >= 1)
       const int fw = (kb + 1) & 3;
       if (wv == fw)
         factor16r<PK>(A, r, ld, R0, min(16, w - R0), Dl, MK, lane);
       else
-        trail_strips<PK>(A, r, ld, k0, kw, R0, nbr, 1, nbr, dk, (wv - fw + 3) & 3, 3, lane);
-    } else {
-      trail_strips<PK>(A, r, ld, k0, kw, R0, nbr, 0, nbr, dk, wv, 4, lane);
+        trail_strips<PK>(A, r, ld, k0, kw, R0, nbr, 1, jhi, dk, (wv - fw + 3) & 3, 3, lane, jend);
+    } else if (!defer) {
+      trail_strips<PK>(A, r, ld, k0, kw, R0, nbr, 0, nbr, dk, wv, 4, lane, jend);
     }
+    __syncthreads();
+  }
+  if (defer) {
+    schur_strips<PK>(A, r, ld, w, Dl, wv, lane);
     __syncthreads();
   }
 }
@@ -1073,7 +1171,7 @@ __global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t*
     }
   }
   __syncthreads();
-  blocked_factor_lds<PK>(A, r, w, ld, Dl, MK, cbuf);
+  blocked_factor_lds<PK>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer);
   blocked_writeout<PK, false>(A, r, w, ld, Dl, arena + T.l_off[s], arena + T.u_off[s], T.u_ld[s], D, f0, st, tol);
 }
 
@@ -1335,7 +1433,7 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
     __syncthreads();
   }
   if (dg && tid == 0) dg[3] = wall_clock64();
-  blocked_factor_lds<PK>(A, r, w, ld, Dl, MK, cbuf);
+  blocked_factor_lds<PK>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer);
   if (dg && tid == 0) dg[4] = wall_clock64();
   blocked_writeout<PK, true>(A, r, w, ld, Dl, arena + T.l_off[s], arena + T.u_off[s], T.u_ld[s], D, f0, st, tol);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2430,7 +2528,10 @@ __global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __re
   __shared__ double v0s[SMALL_SOLVE_MAX];
   __shared__ int s_task;
   const int tid = threadIdx.x;
-  if (tid == 0) s_task = atomicAdd(counter, 1);
+  if (tid == 0) {
+    s_task = atomicAdd(counter, 1);
+    if (s_task == nt - 1) atomicExch(counter, 0);  // every ticket taken: ready for the next launch
+  }
   __syncthreads();
   const int t = s_task;
   if (t >= nt) return;
@@ -2521,7 +2622,10 @@ __global__ __launch_bounds__(NT) void k_bwd_tree(FrontTab T, const int32_t* __re
   __shared__ double xbs[SMALL_SOLVE_MAX];
   __shared__ int s_task;
   const int tid = threadIdx.x;
-  if (tid == 0) s_task = atomicAdd(counter, 1);
+  if (tid == 0) {
+    s_task = atomicAdd(counter, 1);
+    if (s_task == nt - 1) atomicExch(counter, 0);  // every ticket taken: ready for the next launch
+  }
   __syncthreads();
   const int t = s_task;
   if (t >= nt) return;
@@ -2655,6 +2759,10 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   rel_.upload(S.rel);
   perm_.upload(S.perm);
   T_.first = first_;
+  {
+    const char* ev = std::getenv("MADIPM_SCHUR_DEFER");
+    T_.schur_defer = (ev && ev[0] == '0') ? 0 : 1;
+  }
   T_.nrows = nrows_;
   T_.row_ptr = row_ptr_;
   T_.rows = rows_;
@@ -3169,6 +3277,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     flags_.alloc(std::max<int64_t>(nflags, 1));
     flags_.zero();
     counters_.alloc(4 * std::max(NL, 1) + 4);  // + the tree-solve tickets (4 NL, 4 NL + 1)
+    counters_.zero();
     err_.alloc(1);
     err_.zero();
   }
@@ -3538,7 +3647,11 @@ void LDLSolver::bwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
 void LDLSolver::solve_phase1(double* b, hipStream_t s) {
   if (S_.N == 0) return;
   ++epoch_;
-  MADIPM_HIP(hipMemsetAsync(counters_.p, 0, counters_.n * sizeof(int32_t), s));
+  // the big-front task queues need zeroed counters; the tree kernels reset their own tickets
+  bool queues = false;
+  for (const SolveLevel& L : slev1_) queues |= L.nbig > 0;
+  for (const SolveLevel& L : slev2_) queues |= L.nbig > 0;
+  if (queues) MADIPM_HIP(hipMemsetAsync(counters_.p, 0, counters_.n * sizeof(int32_t), s));
   fwd_levels(slev1_, 0, b, s);
   if (!sharded()) {
     bwd_levels(slev1_, 0, b, s);

@@ -65,6 +65,7 @@ struct FrontTab {
   const int32_t* ab_wrc;
   const int64_t* ab_loff;
   const uint8_t* rheavy;
+  int schur_defer;  // in-LDS factorisation: update block U in one pass after the pivots (MADIPM_SCHUR_DEFER)
 };
 
 struct SolveTask {

@@ -45,7 +45,9 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int NPART = 16;
-constexpr int MAXB = 4096;  // partial-reduction blocks (part_ holds MAXB x NPART)
+constexpr int MAXB = 4096;  // partial-reduction blocks (part_ holds NPART x MAXB, value-major)
+// partial k of block b: value-major so k_final's loads of one value are coalesced
+__device__ __forceinline__ int pidx(int b, int k) { return k * MAXB + b; }
 constexpr double INF = std::numeric_limits<double>::infinity();
 
 struct DCsr {
@@ -110,7 +112,7 @@ __device__ void block_partials(double (&v)[NV], const int (&ops)[NV], double* pa
     const int k = threadIdx.x;
     double a = sh[k][0];
     for (int w = 1; w < NT / 64; ++w) a = comb(a, sh[k][w], ops[k]);
-    part[blockIdx.x * NPART + k] = a;
+    part[pidx(blockIdx.x, k)] = a;
   }
 }
 
@@ -279,9 +281,14 @@ enum { RHS_INIT_PRIMAL = 0, RHS_INIT_DUAL = 1, RHS_PRED = 2, RHS_CORR = 3, RHS_G
 
 // set_*_rhs! (kernels.jl:1-58) fused with reduce_rhs! [EXT]: writes the unreduced p and the
 // reduced right-hand side d[0:n+m] handed to the LDL^T solve.
-__global__ __launch_bounds__(NT) void k_rhs(DV D, int mode, double mu_g) {
+// reset: 1 = start of an iteration's directions (max_res_ratio), 2 = also clear the NaN flag (redo)
+__global__ __launch_bounds__(NT) void k_rhs(DV D, int mode, double mu_g, int reset) {
   const int n = D.n, m = D.m, nlb = D.nlb;
   const double mu = (mode == RHS_CORR) ? D.st->mu : mu_g;
+  if (reset && blockIdx.x == 0 && threadIdx.x == 0) {
+    D.st->max_res_ratio = 0.0;
+    if (reset == 2) D.st->nan_flag = 0;
+  }
   GRID_LOOP(i, n + m) {
     if (i < n) {
       double px;
@@ -434,8 +441,8 @@ __global__ __launch_bounds__(NT) void k_alpha(DV D, int mode, double tau_param) 
     double a = sv[k][0];
     int b = si[k][0];
     for (int w = 1; w < NT / 64; ++w) amin_upd(a, b, sv[k][w], si[k][w]);
-    D.part[blockIdx.x * NPART + k] = a;
-    D.part[blockIdx.x * NPART + 4 + k] = (double)b;
+    D.part[pidx(blockIdx.x, k)] = a;
+    D.part[pidx(blockIdx.x, 4 + k)] = (double)b;
   }
 }
 
@@ -648,10 +655,6 @@ __global__ void k_set_mu(DevState* st, double mu) {
   st->max_res_ratio = 0.0;
   st->dx_inf = 0.0;
 }
-__global__ void k_reset_iter(DevState* st, int clear_nan) {
-  st->max_res_ratio = 0.0;
-  if (clear_nan) st->nan_flag = 0;
-}
 
 enum {
   FIN_RESID = 0,
@@ -686,8 +689,20 @@ __global__ __launch_bounds__(NT) void k_final(DV D, int kind, FinParams P) {
       v[k] = INF;
       ix[k] = -1;
     }
-    for (int b = threadIdx.x; b < P.nb; b += NT)
-      for (int k = 0; k < 4; ++k) amin_upd(v[k], ix[k], D.part[b * NPART + k], (int)D.part[b * NPART + 4 + k]);
+    // all of a thread's partials are loaded before they are combined (independent loads in flight);
+    // combined in fixed block order
+    for (int k = 0; k < 4; ++k) {
+      double pv[MAXB / NT], pi[MAXB / NT];
+#pragma unroll
+      for (int j = 0; j < MAXB / NT; ++j) {
+        const int b = min((int)threadIdx.x + j * NT, P.nb - 1);
+        pv[j] = D.part[pidx(b, k)];
+        pi[j] = D.part[pidx(b, 4 + k)];
+      }
+#pragma unroll
+      for (int j = 0; j < MAXB / NT; ++j)
+        if ((int)threadIdx.x + j * NT < P.nb) amin_upd(v[k], ix[k], pv[j], (int)pi[j]);
+    }
     for (int k = 0; k < 4; ++k) {
       double a = v[k];
       int bi = ix[k];
@@ -754,7 +769,12 @@ __global__ __launch_bounds__(NT) void k_final(DV D, int kind, FinParams P) {
     double a = (ops[k] == OP_SUM || ops[k] == OP_MAX) ? 0.0 : INF;
     if (ops[k] == OP_MIN) a = 0.0;  // every min-reduction here has init = 0.0
     // fixed-order accumulation: thread t takes blocks t, t+NT, ... then a fixed tree
-    for (int b = threadIdx.x; b < P.nb; b += NT) a = comb(a, D.part[b * NPART + k], ops[k]);
+    double pv[MAXB / NT];
+#pragma unroll
+    for (int j = 0; j < MAXB / NT; ++j) pv[j] = D.part[pidx(min((int)threadIdx.x + j * NT, P.nb - 1), k)];
+#pragma unroll
+    for (int j = 0; j < MAXB / NT; ++j)
+      if ((int)threadIdx.x + j * NT < P.nb) a = comb(a, pv[j], ops[k]);
     for (int o = 32; o > 0; o >>= 1) a = comb(a, __shfl_down(a, o, 64), ops[k]);
     if (lane == 0) sh[k][wv] = a;
   }
@@ -1460,10 +1480,10 @@ void MPCSolver::launch_reduce_final(int kind, int nb) {
 }
 
 // solve_system! (linear_solver.jl:19-44): rhs (mode) -> LDL^T solve -> finish + residual
-void MPCSolver::solve_system(int mode, double mu) {
+void MPCSolver::solve_system(int mode, double mu, int reset) {
   DV_ARGS;
   const int nb = blocks(n_ + m_), nbs = spmv_blocks(n_ + m_);
-  k_rhs<<<nb, NT, 0, stream_>>>(D, mode, mu);
+  k_rhs<<<nb, NT, 0, stream_>>>(D, mode, mu, reset);
   kkt_solve();
   SPMV_LAUNCH(k_residual, nbs, stream_, D, del_w_, del_c_);
   launch_reduce_final(FIN_RESID, nbs);
@@ -1548,13 +1568,13 @@ void MPCSolver::init_starting_point() {
   fact_events_.push_back(e1);
   ldl_->status(s);  // init factorization: the reference does not retry here
   // Step 1: least-squares primal correction
-  k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_PRIMAL, 0.0);
+  k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_PRIMAL, 0.0, 0);
   kkt_solve();
   SPMV_LAUNCH(k_residual, nb, s, D, del_w_, del_c_);
   launch_reduce_final(FIN_RESID, nb);
   k_axpy_x<<<nbn, NT, 0, s>>>(D);
   // Step 2: dual least squares
-  k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_DUAL, 0.0);
+  k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_DUAL, 0.0, 0);
   kkt_solve();
   SPMV_LAUNCH(k_residual, nb, s, D, del_w_, del_c_);
   launch_reduce_final(FIN_RESID, nb);
@@ -1631,8 +1651,7 @@ void MPCSolver::directions(bool redo) {
   DV_ARGS;
   hipStream_t s = stream_;
   const int nbz = blocks(std::max(nlb_, nub_));
-  k_reset_iter<<<1, 1, 0, s>>>(st_, redo ? 1 : 0);
-  solve_system(RHS_PRED, 0.0);
+  solve_system(RHS_PRED, 0.0, redo ? 2 : 1);
   k_alpha<<<nbz, NT, 0, s>>>(D, ALPHA_PRED, 1.0);
   {
     FinParams P{nbz, ALPHA_PRED, 0, 0, 0};

@@ -60,7 +60,7 @@ class MPCSolver {
   void initialize();
   void init_starting_point();
   void factorize_regularized();
-  void solve_system(int mode, double mu);
+  void solve_system(int mode, double mu, int reset = 0);
   void gondzio();
   void directions(bool redo);  // predictor + corrector directions (speculated before the status read)
   void step_size();
