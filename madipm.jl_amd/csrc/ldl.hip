@@ -731,6 +731,66 @@ __device__ __forceinline__ void factor16r(double* A, int r, int ld, int k0, int 
   wave_sync();
 }
 
+// Same contract as factor16r with the elements spread over the whole wave: lane (i = lane & 15,
+// g = lane >> 4) holds A(i, 4g .. 4g+3) and X(i, 4g .. 4g+3).  Step t: the 16 lanes holding column t
+// write it to LDS (lane i == t: row t of X), then every lane reads back the pivot, its row's entry and
+// its four columns' entries (one wave: a wave-scope fence orders them, no barrier).  Same
+// operations in the same order as factor16r (bitwise identical results); a lane does 4 + 4 FMAs per
+// step instead of 16 + 16, and no SGPR broadcasts (factor16r spends ~34 v_readlane per step).
+// cb: 512 doubles of LDS scratch.
+template <bool PK>
+__device__ __forceinline__ void factor16s(double* A, int r, int ld, int k0, int kw, double* Dl, double* MK, double* cb,
+                                          int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  const int ic = min(i, kw - 1);
+  double a[4], x[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int j = 4 * g + m, jc = min(j, kw - 1);
+    double v = A[fidx<PK>(k0 + max(ic, jc), k0 + min(ic, jc), r, ld)];  // upper part mirrored (never read)
+    asm volatile("" : "+v"(v));  // keep the load unconditional
+    a[m] = (i < kw && j < kw) ? v : (i == j ? 1.0 : 0.0);
+    x[m] = (i == j) ? 1.0 : 0.0;
+  }
+  double* col = cb;        // col[16 t + i] = A(i, t) at step t
+  double* xrw = cb + 256;  // xrw[16 t + j] = X(t, j) at step t
+  double dmine = 1.0;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    const int gt = t >> 2, mt = t & 3;
+    if (g == gt) col[16 * t + i] = a[mt];
+    if (i == t) {
+      reinterpret_cast<double2*>(xrw + 16 * t + 4 * g)[0] = double2{x[0], x[1]};
+      reinterpret_cast<double2*>(xrw + 16 * t + 4 * g)[1] = double2{x[2], x[3]};
+    }
+    wave_sync();  // cross-lane hand-off through LDS: keep the reads after the writes
+    const double dt = col[16 * t + t];
+    const double ci = col[16 * t + i];
+    const double2 c01 = reinterpret_cast<const double2*>(col + 16 * t + 4 * g)[0];
+    const double2 c23 = reinterpret_cast<const double2*>(col + 16 * t + 4 * g)[1];
+    const double2 x01 = reinterpret_cast<const double2*>(xrw + 16 * t + 4 * g)[0];
+    const double2 x23 = reinterpret_cast<const double2*>(xrw + 16 * t + 4 * g)[1];
+    const double cj[4] = {c01.x, c01.y, c23.x, c23.y}, xr[4] = {x01.x, x01.y, x23.x, x23.y};
+    const double li = (i > t) ? ci / dt : 0.0;  // IEEE quotient, as factor16r
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int j = 4 * g + m;
+      a[m] = (j > t) ? fma(-li, cj[m], a[m]) : a[m];
+      x[m] = (j <= t) ? fma(-li, xr[m], x[m]) : x[m];
+    }
+    if (i == t) dmine = dt;
+    if (g == gt && i > t) a[mt] = li;
+  }
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int j = 4 * g + m;
+    if (j < i && i < kw) A[fidx<PK>(k0 + i, k0 + j, r, ld)] = a[m];
+    MK[j * LDM + i] = (j <= i) ? x[m] / dmine : 0.0;
+  }
+  if (g == 0 && i < kw) Dl[k0 + i] = dmine;
+  wave_sync();
+}
+
 // In-launch hand-offs between workgroups (MI355X_MICROARCH.md "inter-workgroup visibility", form R1):
 // payload stored sc1 and drained before ONE lane stores the flag; consumers poll relaxed and load sc1.
 __device__ __forceinline__ double ld_sc1(const double* p) {
@@ -989,16 +1049,29 @@ __device__ __forceinline__ void schur_strips(double* A, int r, int ld, int w, co
 
 // defer: the right-looking block steps update only the pivot columns (columns < w); the update
 // block U gets its whole Schur complement afterwards in one pass (schur_strips)
+// pt (diagnostics, MADIPM_TREE_DEBUG): thread 0 accumulates the phase times (first pivot block,
+// panels, J = 0 strips, lookahead sections, Schur pass) into pt[0..4]
 template <bool PK>
 __device__ __forceinline__ void blocked_factor_lds(double* A, int r, int w, int ld, double* Dl, double* MK, double* cbuf,
-                                                   int defer = 0) {
+                                                   int defer = 0, int64_t* pt = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nblk = (w + 15) >> 4;
   defer = defer && w < r;
   const int jend = defer ? w : r;
-  if (wv == 0) factor16r<PK>(A, r, ld, 0, min(16, w), Dl, MK, lane);
+  int64_t tp[5] = {0, 0, 0, 0, 0}, tl = (pt && tid == 0) ? wall_clock64() : 0;
+  auto stamp = [&](int k) {
+    if (pt && tid == 0) {
+      const int64_t now = wall_clock64();
+      tp[k] += now - tl;
+      tl = now;
+    }
+  };
+  const int64_t cyc0 = (pt && tid == 0) ? (int64_t)clock64() : 0;
+  if (wv == 0) factor16s<PK>(A, r, ld, 0, min(16, w), Dl, MK, cbuf, lane);
   __syncthreads();
+  stamp(0);
+  const int64_t cyc1 = (pt && tid == 0) ? (int64_t)clock64() : 0;
   for (int kb = 0; kb < nblk; ++kb) {
     const int k0 = 16 * kb, kw = min(16, w - k0);
     const int R0 = k0 + kw;                       // first row / column after the pivots
@@ -1006,6 +1079,7 @@ __device__ __forceinline__ void blocked_factor_lds(double* A, int r, int w, int 
     const int jhi = defer ? ((w - R0 + 15) >> 4) - 1 : nbr;  // last column block updated
     panel_blocks<PK>(A, r, ld, k0, kw, R0, nbr, MK, wv, 4, lane);
     __syncthreads();
+    stamp(1);
     double dk[4];
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
@@ -1016,20 +1090,27 @@ __device__ __forceinline__ void blocked_factor_lds(double* A, int r, int w, int 
       // the next pivot block's columns (J = 0: its diagonal block and panel rows) first ...
       trail_strips<PK>(A, r, ld, k0, kw, R0, nbr, 0, 0, dk, wv, 4, lane, jend);
       __syncthreads();
+      stamp(2);
       // ... then one wave factorises it while the other three update the rest (J >= 1)
       const int fw = (kb + 1) & 3;
       if (wv == fw)
-        factor16r<PK>(A, r, ld, R0, min(16, w - R0), Dl, MK, lane);
+        factor16s<PK>(A, r, ld, R0, min(16, w - R0), Dl, MK, cbuf, lane);
       else
         trail_strips<PK>(A, r, ld, k0, kw, R0, nbr, 1, jhi, dk, (wv - fw + 3) & 3, 3, lane, jend);
     } else if (!defer) {
       trail_strips<PK>(A, r, ld, k0, kw, R0, nbr, 0, nbr, dk, wv, 4, lane, jend);
     }
     __syncthreads();
+    stamp(3);
   }
   if (defer) {
     schur_strips<PK>(A, r, ld, w, Dl, wv, lane);
     __syncthreads();
+    stamp(4);
+  }
+  if (pt && tid == 0) {
+    for (int k = 0; k < 5; ++k) pt[k] = tp[k];
+    pt[5] = cyc1 - cyc0;  // shader clocks of the first pivot block (vs pt[0] in 100 MHz ticks)
   }
 }
 
@@ -1150,7 +1231,7 @@ __global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t*
   extern __shared__ __attribute__((aligned(16))) double A[];  // lower part of F (square ld r|1, or packed)
   __shared__ double Dl[192];
   __shared__ double MK[16 * LDM];
-  __shared__ double cbuf[2 * 16 * LDM];
+  __shared__ __attribute__((aligned(16))) double cbuf[2 * 16 * LDM];
   const int s = fronts[blockIdx.x];
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
   const int ld = r | 1;
@@ -1433,7 +1514,7 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
     __syncthreads();
   }
   if (dg && tid == 0) dg[3] = wall_clock64();
-  blocked_factor_lds<PK>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer);
+  blocked_factor_lds<PK>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer, dg ? dg + 8 : nullptr);
   if (dg && tid == 0) dg[4] = wall_clock64();
   blocked_writeout<PK, true>(A, r, w, ld, Dl, arena + T.l_off[s], arena + T.u_off[s], T.u_ld[s], D, f0, st, tol);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1455,7 +1536,7 @@ __global__ __launch_bounds__(NT) void k_fact_tree(FrontTab T, const int32_t* __r
   extern __shared__ __attribute__((aligned(16))) double A[];
   __shared__ double Dl[192];
   __shared__ double MK[16 * LDM];
-  __shared__ double cbuf[2 * 16 * LDM];
+  __shared__ __attribute__((aligned(16))) double cbuf[2 * 16 * LDM];
   __shared__ int32_t rels[192];
   __shared__ int s_task;
   if (threadIdx.x == 0) s_task = atomicAdd(counter, 1);
@@ -3536,19 +3617,20 @@ void LDLSolver::tree_debug_dump(hipStream_t s, const char* what, const int64_t* 
   MADIPM_HIP(hipStreamSynchronize(s));
   for (int t = 0; t < nt; ++t)
     for (int k = 0; k < 8; ++k) h[8 * t + k] = hs[(size_t)stride * t + k];
-  if (stride == 16) {  // absorption phases (gather / pivots / L / row owners), per level
-    std::vector<double> ab((size_t)S_.nlevels * 4, 0.0);
+  if (stride == 16) {  // factor sub-phases (or absorption phases), per level
+    std::vector<double> ab((size_t)S_.nlevels * 6, 0.0);
     std::vector<int> na(S_.nlevels, 0);
     for (int t = 0; t < nt; ++t) {
       const int lv = S_.level[(int)h[8 * t + 6]];
-      if (hs[(size_t)16 * t + 8] == 0 && hs[(size_t)16 * t + 11] == 0) continue;
       na[lv]++;
-      for (int k = 0; k < 4; ++k) ab[lv * 4 + k] += hs[(size_t)16 * t + 8 + k] * 0.01;
+      for (int k = 0; k < 6; ++k) ab[lv * 6 + k] += hs[(size_t)16 * t + 8 + k] * 0.01;
     }
     for (int lv = 0; lv < S_.nlevels; ++lv)
       if (na[lv])
-        fprintf(stderr, "  absorb level %d: %d fronts  gather %.2f  pivots %.2f  L %.2f  rows %.2f us\n", lv, na[lv],
-                ab[lv * 4] / na[lv], ab[lv * 4 + 1] / na[lv], ab[lv * 4 + 2] / na[lv], ab[lv * 4 + 3] / na[lv]);
+        fprintf(stderr,
+                "  factor level %d: %d fronts  first16 [kcyc/100] %.2f  first16 %.2f  panels %.2f  J0 %.2f  look %.2f  schur %.2f us\n",
+                lv, na[lv], ab[lv * 6 + 5] / na[lv], ab[lv * 6] / na[lv], ab[lv * 6 + 1] / na[lv], ab[lv * 6 + 2] / na[lv],
+                ab[lv * 6 + 3] / na[lv], ab[lv * 6 + 4] / na[lv]);
   }
   int64_t t0 = INT64_MAX, t1 = 0;
   for (int t = 0; t < nt; ++t) t0 = std::min(t0, h[8 * t]), t1 = std::max(t1, h[8 * t + 5]);
