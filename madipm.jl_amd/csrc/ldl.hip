@@ -75,8 +75,30 @@ __device__ __forceinline__ double* uvec_dst(const FrontTab& T, int s, int a, dou
 
 // HBM panel (r x w, ld r) -> LDS (ld rl), all threads, 16 independent loads per thread per batch
 // (one HBM round trip per 4096 doubles: a 128 x 128 front is 4 round trips)
+// (i, j) of the column-major indices q = q0, q0 + NT, q0 + 2 NT, ... of an r-row matrix: one integer
+// division per thread instead of one per element (a division is ~15 VALU instructions, and the
+// staging / write-out loops of a front are otherwise dominated by them)
+struct ColWalk {
+  int i, j, di, dj, r;
+  __device__ __forceinline__ ColWalk(int q0, int r_) : r(r_) {
+    j = q0 / r_;
+    i = q0 - j * r_;
+    dj = NT / r_;
+    di = NT - dj * r_;
+  }
+  __device__ __forceinline__ void next() {
+    i += di;
+    j += dj;
+    if (i >= r) {
+      i -= r;
+      ++j;
+    }
+  }
+};
+
 __device__ __forceinline__ void stage_panel(const double* __restrict__ L, double* Ls, int r, int w, int rl) {
   const int nel = r * w;
+  ColWalk wk(threadIdx.x, r);
   for (int base = 0; base < nel; base += NT * 16) {
     double v[16];
 #pragma unroll
@@ -87,10 +109,8 @@ __device__ __forceinline__ void stage_panel(const double* __restrict__ L, double
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int q = base + k * NT + threadIdx.x;
-      if (q < nel) {
-        const int j = q / r, i = q - j * r;
-        Ls[i + j * rl] = v[k];
-      }
+      if (q < nel) Ls[wk.i + wk.j * rl] = v[k];
+      wk.next();
     }
   }
 }
@@ -1176,22 +1196,28 @@ __device__ __forceinline__ void blocked_factor_lds_old(double* A, int r, int w, 
 // write-out: L panel (ld r; d on the diagonal, zeros above), lower triangle of U (ld uld), D and the
 // pivot check.  SC1: U stored write-through (handed to a parent inside the same launch).
 template <bool PK, bool SC1>
-__device__ __forceinline__ void blocked_writeout(const double* A, int r, int w, int ld, const double* Dl, double* L,
-                                                 double* Uo, int uld, double* D, int f0, LDLStatus* st, double tol) {
+__device__ __forceinline__ void writeout_u(const double* A, int r, int w, int ld, double* Uo, int uld);
+template <bool PK>
+__device__ __forceinline__ void writeout_ld(const double* A, int r, int w, int ld, const double* Dl, double* L, double* D,
+                                           int f0, LDLStatus* st, double tol) {
   const int tid = threadIdx.x;
-  for (int q = tid; q < r * w; q += NT) {
-    const int j = q / r, i = q - j * r;
-    L[q] = (i > j) ? A[fidx<PK>(i, j, r, ld)] : (i == j ? Dl[j] : 0.0);
-  }
-  const int u = r - w;
-  for (int q = tid; q < u * u; q += NT) {
-    const int b = q / u, a = q - b * u;
-    if (a >= b) {
-      const double x = A[fidx<PK>(w + a, w + b, r, ld)];
-      if (SC1)
-        __hip_atomic_store(Uo + a + (int64_t)b * uld, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else
-        Uo[a + (int64_t)b * uld] = x;
+  const int nel = r * w;
+  ColWalk wk(tid, r);
+  for (int base = 0; base < nel; base += NT * 8) {
+    double v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // unconditional LDS loads (clamped), selects
+      const int i = min(wk.i, r - 1), j = min(wk.j, w - 1);
+      double a = A[fidx<PK>(max(i, j), min(i, j), r, ld)];
+      asm volatile("" : "+v"(a));
+      const double d = Dl[j];
+      v[k] = (i > j) ? a : (i == j ? d : 0.0);
+      wk.next();
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int q = base + k * NT + tid;
+      if (q < nel) L[q] = v[k];
     }
   }
   if (tid < w) {
@@ -1200,26 +1226,65 @@ __device__ __forceinline__ void blocked_writeout(const double* A, int r, int w, 
     if (bad_pivot(d, tol)) atomicMin(&st->fail_pivot, f0 + tid + 1);
   }
 }
+template <bool PK, bool SC1>
+__device__ __forceinline__ void blocked_writeout(const double* A, int r, int w, int ld, const double* Dl, double* L,
+                                                 double* Uo, int uld, double* D, int f0, LDLStatus* st, double tol) {
+  writeout_ld<PK>(A, r, w, ld, Dl, L, D, f0, st, tol);
+  writeout_u<PK, SC1>(A, r, w, ld, Uo, uld);
+}
+// lower triangle of the update block U (ld uld); SC1: stored write-through (handed to a parent
+// inside the same launch)
+template <bool PK, bool SC1>
+__device__ __forceinline__ void writeout_u(const double* A, int r, int w, int ld, double* Uo, int uld) {
+  const int tid = threadIdx.x;
+  const int u = r - w;
+  if (u <= 0) return;
+  const int nel = u * u;
+  ColWalk wk(tid, u);
+  for (int base = 0; base < nel; base += NT * 8) {
+    double v[8];
+    int64_t dst[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // unconditional LDS loads (clamped)
+      const int q = base + k * NT + tid;
+      const int a = min(wk.i, u - 1), b = min(wk.j, u - 1);
+      double x = A[fidx<PK>(w + max(a, b), w + min(a, b), r, ld)];
+      asm volatile("" : "+v"(x));
+      v[k] = x;
+      dst[k] = (q < nel && a >= b) ? a + (int64_t)b * uld : -1;
+      wk.next();
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (dst[k] >= 0) {
+        if (SC1)
+          __hip_atomic_store(Uo + dst[k], v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+          Uo[dst[k]] = v[k];
+      }
+  }
+}
 
 // lower part of an r x r front assembled in HBM scratch (ld r) -> LDS, 16 loads in flight per thread
 template <bool PK>
 __device__ __forceinline__ void stage_front(const double* __restrict__ Fs, double* A, int r, int ld) {
   const int tid = threadIdx.x;
   const int nel = r * r;
+  ColWalk wk(tid, r);
   for (int base = 0; base < nel; base += NT * 16) {
     double v[16];
+    int dst[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int q = base + k * NT + tid;
-      const int j = q / r, i = q - j * r;
-      v[k] = (q < nel && i >= j) ? Fs[q] : 0.0;
+      const bool ok = q < nel && wk.i >= wk.j;
+      v[k] = ok ? Fs[q] : 0.0;
+      dst[k] = ok ? fidx<PK>(wk.i, wk.j, r, ld) : -1;
+      wk.next();
     }
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int q = base + k * NT + tid;
-      const int j = q / r, i = q - j * r;
-      if (q < nel && i >= j) A[fidx<PK>(i, j, r, ld)] = v[k];
-    }
+    for (int k = 0; k < 16; ++k)
+      if (dst[k] >= 0) A[dst[k]] = v[k];
   }
 }
 
@@ -1492,34 +1557,43 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
     const double* U = arena + T.u_off[c];
     for (int a = tid; a < uc; a += NT) rels[a] = T.rel[T.rel_ptr[c] + a];
     __syncthreads();
-    // column b by a wave, rows a >= b by its lanes: 4 columns' loads in flight per wave
-    for (int b0 = (tid >> 6) * 4; b0 < uc; b0 += 16) {
-      double x[4][3];
+    // entries (a >= b) of the child's U, flattened over its square index space: 16 loads in
+    // flight per thread (a child's update block takes one or two memory round trips)
+    const int n2 = uc * uc;
+    const float inv = 1.0f / (float)max(uc, 1);
+    for (int base = 0; base < n2; base += NT * 16) {
+      double x[16];
+      int dst[16];
 #pragma unroll
-      for (int cb = 0; cb < 4; ++cb)
+      for (int k = 0; k < 16; ++k) {
+        const int e = base + k * NT + tid;
+        int b = (int)((float)e * inv);
+        b -= (b * uc > e) ? 1 : 0;
+        b += ((b + 1) * uc <= e) ? 1 : 0;
+        const int a = e - b * uc;
+        const bool ok = e < n2 && a >= b;
+        x[k] = ok ? __hip_atomic_load(U + a + b * uld, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+        dst[k] = ok ? fidx<PK>(rels[min(a, uc - 1)], rels[min(b, uc - 1)], r, ld) : -1;
+      }
+      // distinct destinations within a child: all reads, then all writes (no read-after-write chain)
+      double o[16];
 #pragma unroll
-        for (int h = 0; h < 3; ++h) {
-          const int b = b0 + cb, a = b + (tid & 63) + 64 * h;
-          x[cb][h] = (b < uc && a < uc) ? __hip_atomic_load(U + a + b * uld, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                        : 0.0;
-        }
+      for (int k = 0; k < 16; ++k) o[k] = A[max(dst[k], 0)];
 #pragma unroll
-      for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-        for (int h = 0; h < 3; ++h) {
-          const int b = b0 + cb, a = b + (tid & 63) + 64 * h;
-          if (b < uc && a < uc) A[fidx<PK>(rels[a], rels[b], r, ld)] += x[cb][h];
-        }
+      for (int k = 0; k < 16; ++k)
+        if (dst[k] >= 0) A[dst[k]] = o[k] + x[k];
     }
     __syncthreads();
   }
   if (dg && tid == 0) dg[3] = wall_clock64();
   blocked_factor_lds<PK>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer, dg ? dg + 8 : nullptr);
   if (dg && tid == 0) dg[4] = wall_clock64();
-  blocked_writeout<PK, true>(A, r, w, ld, Dl, arena + T.l_off[s], arena + T.u_off[s], T.u_ld[s], D, f0, st, tol);
+  // the parent reads only U: publish it first, then write L and D (read by later launches)
+  writeout_u<PK, true>(A, r, w, ld, arena + T.u_off[s], T.u_ld[s]);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) __hip_atomic_store(&flags[s], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  writeout_ld<PK>(A, r, w, ld, Dl, arena + T.l_off[s], D, f0, st, tol);
   if (dg && tid == 0) {
     dg[5] = wall_clock64();
     dg[6] = s;
@@ -2494,40 +2568,40 @@ __device__ __forceinline__ int tree_ldc(int r) { return ((r + 31) & ~31) + 2; } 
 __device__ __forceinline__ void stage_rowmajor(const double* __restrict__ L, double* LT, int r, int w, int ldt) {
   const int w16 = (w + 15) & ~15;
   const int nel = r * w16;
+  ColWalk wk(threadIdx.x, r);
   for (int base = 0; base < nel; base += NT * 16) {
     double v[16];
+    int dst[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int q = base + k * NT + threadIdx.x;
-      const int j = q / r, i = q - j * r;
-      v[k] = (q < nel && j < w && i > j) ? L[q] : 0.0;
+      v[k] = (q < nel && wk.j < w && wk.i > wk.j) ? L[q] : 0.0;
+      dst[k] = (q < nel) ? wk.i * ldt + wk.j : -1;
+      wk.next();
     }
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int q = base + k * NT + threadIdx.x;
-      const int j = q / r, i = q - j * r;
-      if (q < nel) LT[i * ldt + j] = v[k];
-    }
+    for (int k = 0; k < 16; ++k)
+      if (dst[k] >= 0) LT[dst[k]] = v[k];
   }
 }
 
 // backward staging: LC[j * ldc + t] = L(t, j) for t > j, else 0 (j < w, t < r)
 __device__ __forceinline__ void stage_colmajor(const double* __restrict__ L, double* LC, int r, int w, int ldc) {
   const int nel = r * w;
+  ColWalk wk(threadIdx.x, r);
   for (int base = 0; base < nel; base += NT * 16) {
     double v[16];
+    int dst[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int q = base + k * NT + threadIdx.x;
-      const int j = q / r, i = q - j * r;
-      v[k] = (q < nel && i > j) ? L[q] : 0.0;
+      v[k] = (q < nel && wk.i > wk.j) ? L[q] : 0.0;
+      dst[k] = (q < nel) ? wk.j * ldc + wk.i : -1;
+      wk.next();
     }
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int q = base + k * NT + threadIdx.x;
-      const int j = q / r, i = q - j * r;
-      if (q < nel) LC[j * ldc + i] = v[k];
-    }
+    for (int k = 0; k < 16; ++k)
+      if (dst[k] >= 0) LC[dst[k]] = v[k];
   }
   const int pad = ((w + 15) & ~15) - r;  // the last pivot block may reach past row r - 1: zero rows
   for (int q = threadIdx.x; q < w * pad; q += NT) LC[(q / pad) * ldc + r + q % pad] = 0.0;
