@@ -675,6 +675,38 @@ struct FinParams {
   double a, b, c;  // kind-specific parameters
 };
 
+// Per-wave partial reduction of up to 8 values over nb block partials: every load of the thread
+// (J rows x 8 values) is issued before the first is combined (one memory round trip), the 8 value
+// chains are reduced side by side; fixed order (thread t takes blocks t, t + NT, ..., then a fixed
+// shuffle tree), so the result is bitwise reproducible.
+template <int J>
+__device__ __forceinline__ void final_partials(const DV& D, int nb, int nv, const int (&ops)[NPART],
+                                               double (&sh)[NPART][NT / 64]) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  double pv[8][J];
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+#pragma unroll
+    for (int j = 0; j < J; ++j) pv[k][j] = D.part[pidx(min((int)threadIdx.x + j * NT, nb - 1), k)];
+  double a[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int op = ops[k < nv ? k : 0];
+    a[k] = 0.0;  // every reduction here starts at 0.0 (sum, max, and min with init 0)
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+      if ((int)threadIdx.x + j * NT < nb) a[k] = comb(a[k], pv[k][j], op);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] = comb(a[k], __shfl_down(a[k], o, 64), ops[k < nv ? k : 0]);
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (k < nv) sh[k][wv] = a[k];
+}
+
 // Finalise two-pass reductions in fixed block order + scalar logic (one block).
 __global__ __launch_bounds__(NT) void k_final(DV D, int kind, FinParams P) {
   __shared__ double res[NPART];
@@ -691,26 +723,36 @@ __global__ __launch_bounds__(NT) void k_final(DV D, int kind, FinParams P) {
     }
     // all of a thread's partials are loaded before they are combined (independent loads in flight);
     // combined in fixed block order
-    for (int k = 0; k < 4; ++k) {
-      double pv[MAXB / NT], pi[MAXB / NT];
+    {
+      // up to 4 partial rows per thread (alpha reductions have nb <= MAXB / 4 = 1024 blocks
+      // of bound entries in practice; more rows fall back to a loop)
+      for (int j0 = 0; j0 * NT < P.nb; j0 += 4) {
+        double pv[4][4], pi[4][4];
 #pragma unroll
-      for (int j = 0; j < MAXB / NT; ++j) {
-        const int b = min((int)threadIdx.x + j * NT, P.nb - 1);
-        pv[j] = D.part[pidx(b, k)];
-        pi[j] = D.part[pidx(b, 4 + k)];
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int b = min((int)threadIdx.x + (j0 + j) * NT, P.nb - 1);
+            pv[k][j] = D.part[pidx(b, k)];
+            pi[k][j] = D.part[pidx(b, 4 + k)];
+          }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if ((int)threadIdx.x + (j0 + j) * NT < P.nb) amin_upd(v[k], ix[k], pv[k][j], (int)pi[k][j]);
       }
-#pragma unroll
-      for (int j = 0; j < MAXB / NT; ++j)
-        if ((int)threadIdx.x + j * NT < P.nb) amin_upd(v[k], ix[k], pv[j], (int)pi[j]);
     }
-    for (int k = 0; k < 4; ++k) {
-      double a = v[k];
-      int bi = ix[k];
-      for (int o = 32; o > 0; o >>= 1) {
-        const double a2 = __shfl_down(a, o, 64);
-        const int b2 = __shfl_down(bi, o, 64);
-        amin_upd(a, bi, a2, b2);
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const double a2 = __shfl_down(v[k], o, 64);
+        const int b2 = __shfl_down(ix[k], o, 64);
+        amin_upd(v[k], ix[k], a2, b2);
       }
+    for (int k = 0; k < 4; ++k) {
+      const double a = v[k];
+      const int bi = ix[k];
       if (lane == 0) {
         sh[k][wv] = a;
         shi[k][wv] = bi;
@@ -765,18 +807,27 @@ __global__ __launch_bounds__(NT) void k_final(DV D, int kind, FinParams P) {
     case FIN_ZSHIFT1: nv = 8; for (int k = 0; k < 8; ++k) ops[k] = OP_SUM; break;
     case FIN_ZSHIFT2: nv = 1; ops[0] = OP_SUM; break;
   }
-  for (int k = 0; k < nv; ++k) {
-    double a = (ops[k] == OP_SUM || ops[k] == OP_MAX) ? 0.0 : INF;
-    if (ops[k] == OP_MIN) a = 0.0;  // every min-reduction here has init = 0.0
-    // fixed-order accumulation: thread t takes blocks t, t+NT, ... then a fixed tree
-    double pv[MAXB / NT];
+  {
+    const int J = (P.nb + NT - 1) / NT;  // partial rows per thread
+    if (J <= 1) {
+      final_partials<1>(D, P.nb, nv, ops, sh);
+    } else if (J <= 2) {
+      final_partials<2>(D, P.nb, nv, ops, sh);
+    } else if (J <= 4) {
+      final_partials<4>(D, P.nb, nv, ops, sh);
+    } else {  // many partial rows: one value at a time (16 loads in flight, no register blow-up)
+      for (int k = 0; k < nv; ++k) {
+        double a = 0.0;
+        double pv[MAXB / NT];
 #pragma unroll
-    for (int j = 0; j < MAXB / NT; ++j) pv[j] = D.part[pidx(min((int)threadIdx.x + j * NT, P.nb - 1), k)];
+        for (int j = 0; j < MAXB / NT; ++j) pv[j] = D.part[pidx(min((int)threadIdx.x + j * NT, P.nb - 1), k)];
 #pragma unroll
-    for (int j = 0; j < MAXB / NT; ++j)
-      if ((int)threadIdx.x + j * NT < P.nb) a = comb(a, pv[j], ops[k]);
-    for (int o = 32; o > 0; o >>= 1) a = comb(a, __shfl_down(a, o, 64), ops[k]);
-    if (lane == 0) sh[k][wv] = a;
+        for (int j = 0; j < MAXB / NT; ++j)
+          if ((int)threadIdx.x + j * NT < P.nb) a = comb(a, pv[j], ops[k]);
+        for (int o = 32; o > 0; o >>= 1) a = comb(a, __shfl_down(a, o, 64), ops[k]);
+        if (lane == 0) sh[k][wv] = a;
+      }
+    }
   }
   __syncthreads();
   if (threadIdx.x < nv) {
