@@ -451,7 +451,10 @@ __global__ __launch_bounds__(NT) void k_tiny_factor(FrontTab T, const int32_t* _
 
 // ------------------------------------------------------------------ assembly (all big fronts, small fronts with children)
 // Phase 1 (flat, thread per chunk): part[c] = sum of the <= kChunk sources of chunk c, in order.
-__global__ __launch_bounds__(NT) void k_asm_chunks(const int64_t* __restrict__ gchunk, const int64_t* __restrict__ gsrc,
+// Chunk sums: thread per chunk of <= kChunk sources, summed in source order.  Sources are int32
+// when the arena and K fit (IDX = int32_t), else int64.
+template <typename IDX>
+__global__ __launch_bounds__(NT) void k_asm_chunks(const int64_t* __restrict__ gchunk, const IDX* __restrict__ gsrc,
                                                    int64_t c0, int64_t n, const double* __restrict__ Kx,
                                                    const double* __restrict__ arena, double* __restrict__ part) {
   const int64_t c = c0 + (int64_t)blockIdx.x * NT + threadIdx.x;
@@ -459,7 +462,7 @@ __global__ __launch_bounds__(NT) void k_asm_chunks(const int64_t* __restrict__ g
   const int64_t p0 = gchunk[c], p1 = gchunk[c + 1];
   int64_t q[SymbolicPlan::kChunk];
 #pragma unroll
-  for (int u = 0; u < SymbolicPlan::kChunk; ++u) q[u] = (p0 + u < p1) ? gsrc[p0 + u] : INT64_MAX;
+  for (int u = 0; u < SymbolicPlan::kChunk; ++u) q[u] = (p0 + u < p1) ? (int64_t)gsrc[p0 + u] : INT64_MAX;
   double v = 0.0;
 #pragma unroll
   for (int u = 0; u < SymbolicPlan::kChunk; ++u)
@@ -2938,7 +2941,16 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   sv_src_.upload(S.sv_src);
   atiles_.upload(S.atiles);
   g_ptr_.upload(S.g_ptr);
-  g_src_.upload(S.g_src);
+  {  // int32 sources when every arena / K index fits
+    bool fits = true;
+    for (int64_t q : S.g_src) fits = fits && q >= INT32_MIN && q <= INT32_MAX;
+    if (fits && !S.g_src.empty()) {
+      std::vector<int32_t> g32(S.g_src.begin(), S.g_src.end());
+      g_src32_.upload(g32);
+    } else {
+      g_src_.upload(S.g_src);
+    }
+  }
   g_chunk_.upload(S.g_chunk);
   gpart_.alloc(std::max<size_t>(S.g_chunk.size(), 1));
   bt_.upload(S.bt);
@@ -3572,8 +3584,10 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
       case ASSEMBLE:
         if (L.nchunk)
           TIMED(KK_ASM_CHUNKS, L.bytes2, L.flops2,
-                (k_asm_chunks<<<(unsigned)cdiv(L.nchunk, NT), NT, 0, s>>>(g_chunk_, g_src_, L.chunk0, L.nchunk, Kx, arena_,
-                                                                         gpart_)));
+                (g_src32_.p ? k_asm_chunks<int32_t><<<(unsigned)cdiv(L.nchunk, NT), NT, 0, s>>>(
+                                  g_chunk_, g_src32_, L.chunk0, L.nchunk, Kx, arena_, gpart_)
+                            : k_asm_chunks<int64_t><<<(unsigned)cdiv(L.nchunk, NT), NT, 0, s>>>(
+                                  g_chunk_, g_src_, L.chunk0, L.nchunk, Kx, arena_, gpart_)));
         TIMED(KK_ASSEMBLE, L.bytes, L.flops,
               (k_assemble<<<(unsigned)L.items, ANT, 0, s>>>(T_, atiles_.p + L.off, g_ptr_, gpart_, bt_, arena_, fscratch_)));
         break;
