@@ -259,8 +259,9 @@ __global__ __launch_bounds__(NT) void k_micro_factor(FrontTab T, const int32_t* 
   for (int k = 0; k < 4; ++k) F[l + 16 * k] = 0.0;
   wave_sync();
   for (int64_t e = T.asm_ptr[s] + l; e < T.asm_ptr[s + 1]; e += MG) {
-    const int64_t d = T.asm_dst[e];
-    const int lc = (int)(d / r), lr = (int)(d - (int64_t)lc * r);
+    // original entries lie in the front's own (w <= 2) columns: d < 2 r, no division
+    const int d = (int)T.asm_dst[e];
+    const int lc = d >= r ? 1 : 0, lr = d - lc * r;
     F[lr + 32 * lc] = Kx[T.asm_src[e]];
   }
   wave_sync();
@@ -418,8 +419,8 @@ __global__ __launch_bounds__(NT) void k_tiny_factor(FrontTab T, const int32_t* _
   const int64_t fso = T.fs_off[s];
   if (fso < 0) {
     for (int64_t e = T.asm_ptr[s] + lane; e < T.asm_ptr[s + 1]; e += 64) {
-      const int64_t d = T.asm_dst[e];
-      F[(int)(d % r) + (int)(d / r) * LD] = Kx[T.asm_src[e]];
+      const int d = (int)T.asm_dst[e], dj = d / r;  // d < r^2: 32-bit division
+      F[(d - dj * r) + dj * LD] = Kx[T.asm_src[e]];
     }
   } else {
     const double* __restrict__ Fg = fscratch + fso;
@@ -1315,8 +1316,8 @@ __global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t*
     for (int q = tid; q < ntot; q += NT) A[q] = 0.0;
     __syncthreads();
     for (int64_t q = T.asm_ptr[s] + tid; q < T.asm_ptr[s + 1]; q += NT) {
-      const int64_t d = T.asm_dst[q];
-      A[fidx<PK>((int)(d % r), (int)(d / r), r, ld)] = Kx[T.asm_src[q]];
+      const int d = (int)T.asm_dst[q], dj = d / r;  // d < r^2: 32-bit division
+      A[fidx<PK>(d - dj * r, dj, r, ld)] = Kx[T.asm_src[q]];
     }
   }
   __syncthreads();
@@ -1536,8 +1537,8 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
     for (int q = tid; q < ntot; q += NT) A[q] = 0.0;
     __syncthreads();
     for (int64_t q = T.asm_ptr[s] + tid; q < T.asm_ptr[s + 1]; q += NT) {
-      const int64_t d = T.asm_dst[q];
-      A[fidx<PK>((int)(d % r), (int)(d / r), r, ld)] = Kx[T.asm_src[q]];
+      const int d = (int)T.asm_dst[q], dj = d / r;  // d < r^2: 32-bit division
+      A[fidx<PK>(d - dj * r, dj, r, ld)] = Kx[T.asm_src[q]];
     }
     __syncthreads();
     absorb_leaves<PK>(T, s, r, ld, A, Kx, arena, D, st, tol, A + ((ntot + 1) & ~1), dg);  // 16-byte aligned
