@@ -247,7 +247,7 @@ __global__ __launch_bounds__(NT) void k_small_factor(FrontTab T, const int32_t* 
 constexpr int MG = 16;
 __global__ __launch_bounds__(NT) void k_micro_factor(FrontTab T, const int32_t* __restrict__ fronts, int nf,
                                                      const double* __restrict__ Kx, double* __restrict__ arena,
-                                                     double* __restrict__ D, LDLStatus* st, double tol) {
+                                                     double* __restrict__ D, LDLStatus* st, double tol, int write_u) {
   __shared__ double Fs[NT / MG][64];  // columns 0 / 1 of F (rows 0..31); later l_i0 d0 / l_i1 d1
   const int g = threadIdx.x / MG, l = threadIdx.x & (MG - 1);
   const int q = blockIdx.x * (NT / MG) + g;
@@ -306,6 +306,7 @@ __global__ __launch_bounds__(NT) void k_micro_factor(FrontTab T, const int32_t* 
       if (bad_pivot(d1, tol)) atomicMin(&st->fail_pivot, f0 + 2);
     }
   }
+  if (!write_u) return;  // the gather forms the update entries from L (micro_u_)
   const int u = r - w;
   double* __restrict__ Uo = arena + T.u_off[s];
   for (int b = 0; b < u; ++b) {
@@ -457,17 +458,55 @@ __global__ __launch_bounds__(NT) void k_tiny_factor(FrontTab T, const int32_t* _
 template <typename IDX>
 __global__ __launch_bounds__(NT) void k_asm_chunks(const int64_t* __restrict__ gchunk, const IDX* __restrict__ gsrc,
                                                    int64_t c0, int64_t n, const double* __restrict__ Kx,
-                                                   const double* __restrict__ arena, double* __restrict__ part) {
+                                                   const double* __restrict__ arena, double* __restrict__ part,
+                                                   const int64_t* __restrict__ mdesc) {
   const int64_t c = c0 + (int64_t)blockIdx.x * NT + threadIdx.x;
   if (c >= c0 + n) return;
   const int64_t p0 = gchunk[c], p1 = gchunk[c + 1];
   int64_t q[SymbolicPlan::kChunk];
 #pragma unroll
   for (int u = 0; u < SymbolicPlan::kChunk; ++u) q[u] = (p0 + u < p1) ? (int64_t)gsrc[p0 + u] : INT64_MAX;
+  // three batches of independent loads: leaf descriptors, then every value operand, then the sums
+  constexpr int KC = SymbolicPlan::kChunk;
+  bool mic[KC];
+  int64_t dsc[KC];
+#pragma unroll
+  for (int u = 0; u < KC; ++u) {
+    mic[u] = sizeof(IDX) == 4 && q[u] != INT64_MAX && q[u] >= 0 && (q[u] & 0x40000000);
+    dsc[u] = mic[u] ? mdesc[((int)q[u] >> 10) & 0xfffff] : 0;
+  }
+  double x0[KC], x1[KC], x2[KC], x3[KC], x4[KC], x5[KC];
+#pragma unroll
+  for (int u = 0; u < KC; ++u) {
+    if (mic[u]) {  // d0, l_a0, l_b0 and (w = 2) l_a1, l_b1, d1; w = 1 re-reads column 0 (unused)
+      const int qi = (int)q[u];
+      const int a = (qi >> 5) & 31, b = qi & 31, r = (int)((dsc[u] >> 2) & 63), w = (int)(dsc[u] & 3);
+      const double* L = arena + (dsc[u] >> 8);
+      const int c1 = (w == 2) ? r : 0;
+      x0[u] = L[0];
+      x1[u] = L[w + a];
+      x2[u] = L[w + b];
+      x3[u] = L[c1 + w + a];
+      x4[u] = L[c1 + w + b];
+      x5[u] = L[c1 + (w == 2 ? 1 : 0)];
+    } else {
+      x0[u] = (q[u] == INT64_MAX) ? 0.0 : ((q[u] < 0) ? Kx[~q[u]] : arena[q[u]]);
+      x1[u] = x2[u] = x3[u] = x4[u] = x5[u] = 0.0;
+    }
+  }
   double v = 0.0;
 #pragma unroll
-  for (int u = 0; u < SymbolicPlan::kChunk; ++u)
-    if (q[u] != INT64_MAX) v += (q[u] >= 0) ? arena[q[u]] : Kx[~q[u]];
+  for (int u = 0; u < KC; ++u) {
+    if (q[u] == INT64_MAX) continue;
+    if (mic[u]) {  // U(a, b) = -(l_a0 (l_b0 d0) + l_a1 (l_b1 d1)), as k_micro_factor forms it
+      const bool two = (dsc[u] & 3) == 2;
+      const double sb0 = x2[u] * x0[u];
+      const double la1 = two ? x3[u] : 0.0, sb1 = two ? x4[u] * x5[u] : 0.0;
+      v += -(x1[u] * sb0 + la1 * sb1);
+    } else {
+      v += x0[u];
+    }
+  }
   part[c] = v;
 }
 
@@ -2942,11 +2981,50 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   sv_src_.upload(S.sv_src);
   atiles_.upload(S.atiles);
   g_ptr_.upload(S.g_ptr);
-  {  // int32 sources when every arena / K index fits
-    bool fits = true;
-    for (int64_t q : S.g_src) fits = fits && q >= INT32_MIN && q <= INT32_MAX;
-    if (fits && !S.g_src.empty()) {
+  {
+    // int32 sources when every arena / K index fits.  Optionally leaf (micro) fronts' update entries
+    // are not materialised: a source (front c, a, b) is encoded as 0x40000000 | mid << 10 | a << 5 | b
+    // and the gather forms U(a, b) = -(l_a0 d0 l_b0 + l_a1 d1 l_b1) from c's L panel (r x w <= 32 x 2,
+    // pivots on its diagonal) — k_micro_factor then writes no U block (~90 MB per ex10 factorisation).
+    bool fits = !S.g_src.empty();
+    for (int64_t q : S.g_src) fits = fits && q >= INT32_MIN && q < (1LL << 30);
+    micro_u_ = false;
+    if (fits) {
       std::vector<int32_t> g32(S.g_src.begin(), S.g_src.end());
+      std::vector<std::pair<int64_t, int>> mu;  // (u_off, front) of the micro fronts
+      for (int f = 0; f < (int)S.nrows.size(); ++f) {
+        const int r = S.nrows[f], w = S.first[f + 1] - S.first[f];
+        const bool absorbed = S.parent[f] >= 0 && S.absorb[S.parent[f]];
+        if (r <= 32 && w <= 2 && S.fs_off[f] < 0 && !S.is_big[f] && !S.ftree[f] && !absorbed && r > w)
+          mu.push_back({S.u_off[f], f});
+      }
+      // experimental (MADIPM_LEAF_FROM_L=1): measured on ex10 the leaf factorisation halves
+      // (0.23 -> 0.11 ms per warm-up) but the gather, now 6 scattered loads per leaf source instead
+      // of 1, grows 0.35 -> 0.57 ms (address-bound) — so the U blocks stay materialised by default
+      const char* ev = std::getenv("MADIPM_LEAF_FROM_L");
+      const bool want = ev && ev[0] == '1';
+      if (want && !mu.empty() && mu.size() < (1u << 20) && S.arena_size < (1LL << 55)) {
+        std::sort(mu.begin(), mu.end());
+        std::vector<int64_t> desc(mu.size());
+        for (size_t k = 0; k < mu.size(); ++k) {
+          const int f = mu[k].second, r = S.nrows[f], w = S.first[f + 1] - S.first[f];
+          desc[k] = (S.l_off[f] << 8) | ((int64_t)r << 2) | w;
+        }
+        for (int32_t& q : g32) {
+          if (q < 0) continue;
+          auto it = std::upper_bound(mu.begin(), mu.end(), std::make_pair((int64_t)q, INT32_MAX));
+          if (it == mu.begin()) continue;
+          --it;
+          const int f = it->second;
+          const int u = S.nrows[f] - (S.first[f + 1] - S.first[f]);
+          const int64_t off = q - it->first, ld = S.u_ld[f];
+          if (off >= ld * u) continue;  // not inside this leaf's update block
+          const int a = (int)(off % ld), b = (int)(off / ld);
+          q = (int32_t)(0x40000000 | ((int)(it - mu.begin()) << 10) | (a << 5) | b);
+        }
+        mdesc_.upload(desc);
+        micro_u_ = true;
+      }
       g_src32_.upload(g32);
     } else {
       g_src_.upload(S.g_src);
@@ -3586,16 +3664,16 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
         if (L.nchunk)
           TIMED(KK_ASM_CHUNKS, L.bytes2, L.flops2,
                 (g_src32_.p ? k_asm_chunks<int32_t><<<(unsigned)cdiv(L.nchunk, NT), NT, 0, s>>>(
-                                  g_chunk_, g_src32_, L.chunk0, L.nchunk, Kx, arena_, gpart_)
+                                  g_chunk_, g_src32_, L.chunk0, L.nchunk, Kx, arena_, gpart_, mdesc_.p)
                             : k_asm_chunks<int64_t><<<(unsigned)cdiv(L.nchunk, NT), NT, 0, s>>>(
-                                  g_chunk_, g_src_, L.chunk0, L.nchunk, Kx, arena_, gpart_)));
+                                  g_chunk_, g_src_, L.chunk0, L.nchunk, Kx, arena_, gpart_, nullptr)));
         TIMED(KK_ASSEMBLE, L.bytes, L.flops,
               (k_assemble<<<(unsigned)L.items, ANT, 0, s>>>(T_, atiles_.p + L.off, g_ptr_, gpart_, bt_, arena_, fscratch_)));
         break;
       case MICRO:
         TIMED(KK_TINY, L.bytes, L.flops,
               (k_micro_factor<<<(unsigned)cdiv(L.items, NT / MG), NT, 0, s>>>(T_, list, (int)L.items, Kx, arena_, D_,
-                                                                             status_, pivot_tol)));
+                                                                             status_, pivot_tol, micro_u_ ? 0 : 1)));
         break;
       case SMALL32:
         TIMED(KK_TINY, L.bytes, L.flops,

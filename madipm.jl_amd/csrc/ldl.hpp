@@ -249,6 +249,8 @@ class LDLSolver : public LinSolver {
   DBuf<int32_t> bigslot_, g_ptr_, bt_;
   DBuf<int64_t> fs_off_, sv_ptr_, sv_src_, g_src_, g_chunk_;
   DBuf<int32_t> g_src32_;
+  DBuf<int64_t> mdesc_;  // leaf fronts: (L offset << 8) | (r << 2) | w
+  bool micro_u_ = false;  // leaf update entries formed by the gather from L
   DBuf<SymbolicPlan::AsmTile> atiles_;
   DBuf<double> minv_, fscratch_, gpart_;
   DBuf<int64_t> row_ptr_, l_off_, u_off_, uvec_off_, asm_ptr_, asm_src_, asm_dst64_, rel_ptr_;

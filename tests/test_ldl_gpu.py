@@ -107,6 +107,16 @@ def test_ldl_leaf_absorption(well, monkeypatch):
 
 
 @pytest.mark.parametrize("well", [True, False])
+def test_ldl_leaf_entries_from_l(well, monkeypatch):
+    """Experimental MADIPM_LEAF_FROM_L=1: leaf fronts write no update block; the assembly gather
+    forms each leaf update entry from the leaf's L panel and pivots — same pivots / solution."""
+    monkeypatch.setenv("MADIPM_LEAF_FROM_L", "1")
+    K, Lw = block_angular_k2(3000, 4000, 20, 7, well=well)
+    ls = _check_case(K, Lw, well=well)
+    assert ls.inertia() == (4000, 0, 3000)
+
+
+@pytest.mark.parametrize("well", [True, False])
 def test_ldl_qp_dense_front(well):
     K, Lw = random_k2(150, 400, 0.05, 11, qp=True, well=well)
     ls = _check_case(K, Lw, small_front_max=128, well=well)
