@@ -703,103 +703,19 @@ __device__ __forceinline__ int fidx(int i, int j, int r, int ld) {
   return PK ? ((j * (2 * r - j - 1)) >> 1) + i : i + j * ld;
 }
 
-template <bool PK>
-__device__ __forceinline__ void factor16g(double* A, int r, int ld, int k0, int kw, double* Dl, double* MK, double* cb,
-                                          double* xb, int lane) {
-  const int il = lane & 15, cg = lane >> 4;
-  double a[4], x[4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    const int jl = cg + 4 * m;
-    a[m] = (il < kw && jl < kw) ? (jl <= il ? A[fidx<PK>(k0 + il, k0 + jl, r, ld)] : 0.0) : (il == jl ? 1.0 : 0.0);
-    x[m] = (jl == il) ? 1.0 : 0.0;
-  }
-#pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    if (cg == (t & 3)) cb[t * LDM + il] = a[t >> 2];
-    if (il == t) {
-#pragma unroll
-      for (int m = 0; m < 4; ++m) xb[t * LDM + cg + 4 * m] = x[m];
-    }
-    wave_sync();
-    const double dt = cb[t * LDM + t];
-    const double li = (il > t) ? cb[t * LDM + il] / dt : 0.0;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int jl = cg + 4 * m;
-      const double cj = cb[t * LDM + jl];
-      const double xt = xb[t * LDM + jl];
-      a[m] = fma(jl > t ? -li : 0.0, cj, a[m]);
-      x[m] = fma(jl > t ? 0.0 : -li, xt, x[m]);
-    }
-  }
-  wave_sync();
-  const double di = cb[il * LDM + il];
-#pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    const int jl = cg + 4 * m;
-    if (jl < il && il < kw) A[fidx<PK>(k0 + il, k0 + jl, r, ld)] = a[m] / cb[jl * LDM + jl];
-    MK[jl * LDM + il] = (jl <= il) ? x[m] / di : 0.0;
-  }
-  if (cg == 0 && il < kw) Dl[k0 + il] = di;
-  wave_sync();
-}
 
 // PK = false: square storage, ld = r | 1 (r <= 128); PK = true: packed lower-triangular columns
 // (r <= 192 fits LDS), element (i, j >= ...) at j (2r - j - 1) / 2 + i
 
-// Same contract as factor16g, register-resident: lane i (& 15) keeps row i of the 16 x 16 diagonal
-// block (and row i of X = L_KK^{-1}) in registers; pivot t and the column below it are broadcast
-// with readlane (no LDS round trip in the pivot chain, the column reads overlap the reciprocal).
-// Identity-padded past kw.  Writes the strictly-lower L_KK into A, d into Dl[k0 + i] and
-// M_K = L_KK^{-T} D^{-1} (ld LDM, zero above the diagonal) into MK.
-template <bool PK>
-__device__ __forceinline__ void factor16r(double* A, int r, int ld, int k0, int kw, double* Dl, double* MK, int lane) {
-  const int i = lane & 15;
-  const int ic = min(i, kw - 1);
-  double a[16], x[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int jc = min(j, kw - 1);
-    double v = A[fidx<PK>(k0 + max(ic, jc), k0 + min(ic, jc), r, ld)];  // upper part mirrored (never read)
-    asm volatile("" : "+v"(v));  // keep the load unconditional (no per-load branch + wait)
-    a[j] = (i < kw && j < kw) ? v : (i == j ? 1.0 : 0.0);
-    x[j] = (i == j) ? 1.0 : 0.0;
-  }
-  double dmine = 1.0;
-#pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    const double dt = readlane_f64(a[t], t);
-    double col[16], xr[16];
-#pragma unroll
-    for (int j = t + 1; j < 16; ++j) col[j] = readlane_f64(a[t], j);  // L-part (j, t), unscaled
-#pragma unroll
-    for (int j = 0; j <= t; ++j) xr[j] = readlane_f64(x[j], t);       // row t of X
-    const double li = (i > t) ? a[t] / dt : 0.0;  // IEEE quotient: keeps the level path's rounding
-#pragma unroll
-    for (int j = t + 1; j < 16; ++j) a[j] = fma(-li, col[j], a[j]);
-#pragma unroll
-    for (int j = 0; j <= t; ++j) x[j] = fma(-li, xr[j], x[j]);
-    if (i == t) dmine = dt;
-    if (i > t) a[t] = li;
-  }
-  if (lane < 16) {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      if (j < i && i < kw) A[fidx<PK>(k0 + i, k0 + j, r, ld)] = a[j];
-      MK[j * LDM + i] = (j <= i) ? x[j] / dmine : 0.0;
-    }
-    if (i < kw) Dl[k0 + i] = dmine;
-  }
-  wave_sync();
-}
-
-// Same contract as factor16r with the elements spread over the whole wave: lane (i = lane & 15,
+// Factor the 16 x 16 diagonal block K at (k0, k0) of the front in LDS with ONE wave (identity-padded
+// past kw): writes the strictly-lower unit L_KK into A, d into Dl[k0 + i] and M_K = L_KK^{-T} D^{-1}
+// (ld LDM, zero above the diagonal) into MK.  The elements are spread over the whole wave: lane (i = lane & 15,
 // g = lane >> 4) holds A(i, 4g .. 4g+3) and X(i, 4g .. 4g+3).  Step t: the 16 lanes holding column t
 // write it to LDS (lane i == t: row t of X), then every lane reads back the pivot, its row's entry and
-// its four columns' entries (one wave: a wave-scope fence orders them, no barrier).  Same
-// operations in the same order as factor16r (bitwise identical results); a lane does 4 + 4 FMAs per
-// step instead of 16 + 16, and no SGPR broadcasts (factor16r spends ~34 v_readlane per step).
+// its four columns' entries (one wave: a wave-scope fence orders them, no barrier).  l = a / d is
+// the IEEE quotient (the level path's rounding); a lane does 4 + 4 FMAs per step and no SGPR
+// broadcasts (a lane-per-row version with v_readlane broadcasts needs ~34 of them per step and ran
+// 4.5 us per block against 3.7 us for this one).
 // cb: 512 doubles of LDS scratch.
 template <bool PK>
 __device__ __forceinline__ void factor16s(double* A, int r, int ld, int k0, int kw, double* Dl, double* MK, double* cb,
@@ -834,7 +750,7 @@ __device__ __forceinline__ void factor16s(double* A, int r, int ld, int k0, int 
     const double2 x01 = reinterpret_cast<const double2*>(xrw + 16 * t + 4 * g)[0];
     const double2 x23 = reinterpret_cast<const double2*>(xrw + 16 * t + 4 * g)[1];
     const double cj[4] = {c01.x, c01.y, c23.x, c23.y}, xr[4] = {x01.x, x01.y, x23.x, x23.y};
-    const double li = (i > t) ? ci / dt : 0.0;  // IEEE quotient, as factor16r
+    const double li = (i > t) ? ci / dt : 0.0;  // IEEE quotient
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       const int j = 4 * g + m;
@@ -1177,64 +1093,6 @@ __device__ __forceinline__ void blocked_factor_lds(double* A, int r, int w, int 
   }
 }
 
-template <bool PK>
-__device__ __forceinline__ void blocked_factor_lds_old(double* A, int r, int w, int ld, double* Dl, double* MK,
-                                                       double* cbuf) {
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int k0 = 0; k0 < w; k0 += 16) {
-    const int kw = min(16, w - k0);
-    const int R0 = k0 + kw;                       // first row / column after the pivots
-    const int nbr = (r - R0 + 15) >> 4;           // 16-row blocks below
-    if (wv == ((k0 >> 4) & 3)) factor16g<PK>(A, r, ld, k0, kw, Dl, MK, cbuf, cbuf + 16 * LDM, lane);
-    __syncthreads();
-    // panel: L_R = A[R, k0:k0+kw] M_K, row block per wave
-    for (int b = wv; b < nbr; b += 4) {
-      const int rb = R0 + 16 * b;
-      dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int k = 4 * ks + (lane >> 4), row = rb + (lane & 15);
-        const double av = (k < kw && row < r) ? A[fidx<PK>(row, k0 + k, r, ld)] : 0.0;
-        const double bv = MK[k * LDM + (lane & 15)];
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-      }
-      // acc[g]: row rb + (lane>>4) + 4g ... D[m][n] with m = (lane>>4)+4g, n = lane&15: here the A
-      // operand carried the rows (m) and M_K the columns (n)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int row = rb + (lane >> 4) + 4 * g, col = lane & 15;
-        if (row < r && col < kw) A[fidx<PK>(row, k0 + col, r, ld)] = acc[g];
-      }
-    }
-    __syncthreads();
-    // trailing update of the lower triangle of A[R0:, R0:]: tile (I, J), J <= I
-    const int ntile = nbr * (nbr + 1) / 2;
-    for (int q = wv; q < ntile; q += 4) {
-      int I = 0, rem = q;
-      while (rem > I) {
-        rem -= I + 1;
-        ++I;
-      }
-      const int J = rem;
-      const int i0 = R0 + 16 * I, j0 = R0 + 16 * J;
-      dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int k = 4 * ks + (lane >> 4);
-        const int rj = j0 + (lane & 15), ri = i0 + (lane & 15);
-        const double av = (k < kw && rj < r) ? A[fidx<PK>(rj, k0 + k, r, ld)] : 0.0;       // L_J (rows m)
-        const double bv = (k < kw && ri < r) ? A[fidx<PK>(ri, k0 + k, r, ld)] * Dl[k0 + k] : 0.0;  // (L_I D) (cols n)
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int j = j0 + (lane >> 4) + 4 * g, i = i0 + (lane & 15);
-        if (i < r && j < r && i >= j) A[fidx<PK>(i, j, r, ld)] -= acc[g];
-      }
-    }
-    __syncthreads();
-  }
-}
 
 // write-out: L panel (ld r; d on the diagonal, zeros above), lower triangle of U (ld uld), D and the
 // pivot check.  SC1: U stored write-through (handed to a parent inside the same launch).
