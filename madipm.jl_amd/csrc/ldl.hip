@@ -3395,6 +3395,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   vwork_.alloc(std::max<int64_t>(S.row_ptr[ns], 1));
   status_.alloc(1);
   MADIPM_HIP(hipHostMalloc((void**)&h_status_, sizeof(LDLStatus), hipHostMallocDefault));
+  st_ = status_.p;
+  h_st_ = h_status_;
   static bool attr_done = false;
   if (!attr_done) {
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_small_factor<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -3531,27 +3533,27 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
       case MICRO:
         TIMED(KK_TINY, L.bytes, L.flops,
               (k_micro_factor<<<(unsigned)cdiv(L.items, NT / MG), NT, 0, s>>>(T_, list, (int)L.items, Kx, arena_, D_,
-                                                                             status_, pivot_tol, micro_u_ ? 0 : 1)));
+                                                                             st_, pivot_tol, micro_u_ ? 0 : 1)));
         break;
       case SMALL32:
         TIMED(KK_TINY, L.bytes, L.flops,
               (k_tiny_factor<<<(unsigned)cdiv(L.items, 4), NT, 0, s>>>(T_, list, (int)L.items, Kx, arena_, fscratch_, D_,
-                                                                      status_, pivot_tol)));
+                                                                      st_, pivot_tol)));
         break;
       case SMALL64:
       case SMALL128:
         TIMED(KK_SMALL, L.bytes, L.flops,
               (k_small_blocked<false><<<(unsigned)L.items, NT, L.lds_bytes, s>>>(T_, list, Kx, arena_, fscratch_, D_,
-                                                                                status_, pivot_tol)));
+                                                                                st_, pivot_tol)));
         break;
       case SMALL192:
         TIMED(KK_SMALL, L.bytes, L.flops,
               (k_small_blocked<true><<<(unsigned)L.items, NT, L.lds_bytes, s>>>(T_, list, Kx, arena_, fscratch_, D_,
-                                                                               status_, pivot_tol)));
+                                                                               st_, pivot_tol)));
         break;
       case BIG_DIAG:
         TIMED(KK_DIAG, L.bytes, L.flops,
-              (k_big_diag<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_, minv_, status_, pivot_tol)));
+              (k_big_diag<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_, minv_, st_, pivot_tol)));
         break;
       case BIG_TRSM:
         TIMED(KK_TRSM, L.bytes, L.flops, (k_big_trsm<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_, minv_)));
@@ -3562,7 +3564,7 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
       case LB_BUILD:
         TIMED(KK_LB_BUILD, L.bytes, 0.0,
               (k_lb_build<<<(unsigned)L.items, NT, 0, s>>>(lbg_, lbgid_, lbmem_, lbcs_, lbce_, lbwbase_, lbwrow_, Kx, lbW_,
-                                                          lbd_.p, lbd_.p + S_.lb_mem.size(), D_, status_, pivot_tol)));
+                                                          lbd_.p, lbd_.p + S_.lb_mem.size(), D_, st_, pivot_tol)));
         break;
       case LB_SYRK:
         TIMED(KK_LB_SYRK, L.bytes, L.flops, lb_syrk((int)L.off, s));
@@ -3571,7 +3573,7 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
         ++fepoch_;
         TIMED(KK_FACT_TREE, L.bytes, L.flops,
               (k_fact_tree<<<(unsigned)nftree_, NT, L.lds_bytes, s>>>(T_, ft_order_, nftree_, ft_dptr_, ft_dep_, fcnt_,
-                                                                      fflags_, fepoch_, Kx, arena_, fscratch_, D_, status_,
+                                                                      fflags_, fepoch_, Kx, arena_, fscratch_, D_, st_,
                                                                       pivot_tol, err_, fdbg_.p)));
         if (fdbg_.p) tree_debug_dump(s, "fact", fdbg_.p, nftree_, "stage", "wait", "push", "factor", "store", 16);
         break;
@@ -3583,30 +3585,30 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
 // assembly and the shard's status slot.
 void LDLSolver::fact_phase1(const double* Kx, hipStream_t s) {
   if (S_.N == 0) return;
-  k_status_init<<<1, 1, 0, s>>>(status_);
+  k_status_init<<<1, 1, 0, s>>>(st_);
   run_fact(fact1_, Kx, s);
   const int nb = (int)std::min<int64_t>(64, cdiv(S_.N, NT));
   const int spdf = spd ? 1 : 0;
   if (!sharded()) {
-    TIMED(KK_INERTIA, 8.0 * S_.N, 0.0, (k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, status_, spdf, nullptr, 0)));
+    TIMED(KK_INERTIA, 8.0 * S_.N, 0.0, (k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, st_, spdf, nullptr, 0)));
     MADIPM_HIP(hipGetLastError());
-    MADIPM_HIP(hipMemcpyAsync(h_status_, status_.p, sizeof(LDLStatus), hipMemcpyDeviceToHost, s));
+    if (!ext_status_) MADIPM_HIP(hipMemcpyAsync(h_st_, st_, sizeof(LDLStatus), hipMemcpyDeviceToHost, s));
     return;
   }
-  TIMED(KK_INERTIA, 8.0 * S_.N, 0.0, (k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, status_, spdf, colmask_, 1)));
-  k_pack_status<<<1, 64, 0, s>>>(status_, arena_.p + S_.top_hi, S_.shard, S_.nshards);
+  TIMED(KK_INERTIA, 8.0 * S_.N, 0.0, (k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, st_, spdf, colmask_, 1)));
+  k_pack_status<<<1, 64, 0, s>>>(st_, arena_.p + S_.top_hi, S_.shard, S_.nshards);
   MADIPM_HIP(hipGetLastError());
 }
 
 // Phase 2 (sharded): after the all-reduce of fact_xbuf(), every shard factorises the top fronts.
 void LDLSolver::fact_phase2(hipStream_t s) {
   if (S_.N == 0 || !sharded()) return;
-  k_unpack_status<<<1, 1, 0, s>>>(status_, arena_.p + S_.top_hi, S_.nshards);
+  k_unpack_status<<<1, 1, 0, s>>>(st_, arena_.p + S_.top_hi, S_.nshards);
   run_fact(fact2_, nullptr, s);
   const int nb = (int)std::min<int64_t>(64, cdiv(S_.N, NT));
-  TIMED(KK_INERTIA, 8.0 * S_.N, 0.0, (k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, status_, spd ? 1 : 0, colmask_, 2)));
+  TIMED(KK_INERTIA, 8.0 * S_.N, 0.0, (k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, st_, spd ? 1 : 0, colmask_, 2)));
   MADIPM_HIP(hipGetLastError());
-  MADIPM_HIP(hipMemcpyAsync(h_status_, status_.p, sizeof(LDLStatus), hipMemcpyDeviceToHost, s));
+  MADIPM_HIP(hipMemcpyAsync(h_st_, st_, sizeof(LDLStatus), hipMemcpyDeviceToHost, s));
 }
 
 void LDLSolver::factorize_async(const double* Kx, hipStream_t s) {
@@ -3617,16 +3619,27 @@ void LDLSolver::factorize_async(const double* Kx, hipStream_t s) {
   fact_phase2(s);
 }
 
+bool LDLSolver::external_status(LDLStatus* dev, LDLStatus* host) {
+  if (sharded() || !dev || !host) return false;
+  st_ = dev;
+  h_st_ = host;
+  ext_status_ = true;
+  k_status_init<<<1, 1, 0, nullptr>>>(st_);
+  MADIPM_HIP(hipDeviceSynchronize());
+  return true;
+}
+
 int LDLSolver::status(hipStream_t s, bool sync) {
   if (S_.N == 0) {
     factorized = true;
     return 0;
   }
+  if (sync && ext_status_) MADIPM_HIP(hipMemcpyAsync(h_st_, st_, sizeof(LDLStatus), hipMemcpyDeviceToHost, s));
   if (sync) MADIPM_HIP(hipStreamSynchronize(s));
-  npos = h_status_->npos;
-  nneg = h_status_->nneg;
-  nzero = h_status_->nzero;
-  const int fp = h_status_->fail_pivot;
+  npos = h_st_->npos;
+  nneg = h_st_->nneg;
+  nzero = h_st_->nzero;
+  const int fp = h_st_->fail_pivot;
   factorized = (fp == INT_MAX);
   return factorized ? 0 : fp;
 }

@@ -110,6 +110,14 @@ class LinSolver {
   virtual void factorize_async(const double* Kx, hipStream_t s) = 0;
   // sync = false: the caller already waited for an event recorded after factorize_async
   virtual int status(hipStream_t s, bool sync = true) = 0;
+  // Keep the factorisation status at caller-provided device / pinned-host addresses, so the caller's
+  // own per-iteration read-back carries it (no separate copy); status(s, false) then reads the
+  // caller's copy.  Returns false when unsupported (sharded solvers).
+  virtual bool external_status(LDLStatus* dev, LDLStatus* host) {
+    (void)dev;
+    (void)host;
+    return false;
+  }
   virtual void solve_async(double* b, hipStream_t s) = 0;
   virtual const SymbolicPlan& plan() const = 0;
   virtual void set_timing(unsigned mask) = 0;
@@ -131,6 +139,7 @@ class LDLSolver : public LinSolver {
   void factorize_async(const double* Kx, hipStream_t s) override;
   // Synchronise `s` and return 0 or failing pivot + 1; fills the inertia.
   int status(hipStream_t s, bool sync = true) override;
+  bool external_status(LDLStatus* dev, LDLStatus* host) override;
   // In-place solve K x = b for a device vector of length n (caller's ordering).
   void solve_async(double* b, hipStream_t s) override;
 
@@ -257,6 +266,9 @@ class LDLSolver : public LinSolver {
   DBuf<double> arena_, D_, xi_, uvec_, vwork_;
   DBuf<LDLStatus> status_;
   LDLStatus* h_status_ = nullptr;
+  LDLStatus* st_ = nullptr;    // status in use: status_ or the caller's (external_status)
+  LDLStatus* h_st_ = nullptr;  // its host copy
+  bool ext_status_ = false;
   // live timing
   unsigned tmask_ = 0;
   std::vector<hipEvent_t> evs_;

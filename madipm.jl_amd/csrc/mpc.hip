@@ -1402,6 +1402,7 @@ void MPCSolver::setup_host(const madipm_qp& q) {
   }
   part_.alloc(MAXB * NPART);
   st_.alloc(1);
+  ldl_->external_status(&st_.p->ldl_status, &hst_->ldl_status);  // carried by read_state()
   st_.zero(s);
   MADIPM_HIP(hipStreamSynchronize(s));
   // norm_b (solver.jl:173) on host

@@ -37,6 +37,7 @@ struct DevState {
   int32_t i_xl, i_xu, i_zl, i_zu;     // argmin indices (-1 = init element)
   int32_t nan_flag;
   int32_t pad;
+  LDLStatus ldl_status;  // the linear solver's status (external_status): one read-back per iteration
 };
 
 struct QPHost;  // host copy of the problem (mpc.hip)
