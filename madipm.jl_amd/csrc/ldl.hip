@@ -1491,9 +1491,14 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
   if (dg && tid == 0) dg[4] = wall_clock64();
   // the parent reads only U: publish it first, then write L and D (read by later launches)
   writeout_u<PK, true>(A, r, w, ld, arena + T.u_off[s], T.u_ld[s]);
+  if (dg) {
+    __syncthreads();
+    if (tid == 0) dg[14] = wall_clock64();
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) __hip_atomic_store(&flags[s], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (dg && tid == 0) dg[15] = wall_clock64();
   writeout_ld<PK>(A, r, w, ld, Dl, arena + T.l_off[s], D, f0, st, tol);
   if (dg && tid == 0) {
     dg[5] = wall_clock64();
@@ -3663,6 +3668,18 @@ void LDLSolver::tree_debug_dump(hipStream_t s, const char* what, const int64_t* 
       na[lv]++;
       for (int k = 0; k < 6; ++k) ab[lv * 6 + k] += hs[(size_t)16 * t + 8 + k] * 0.01;
     }
+    std::vector<double> sq((size_t)S_.nlevels * 3, 0.0);
+    for (int t = 0; t < nt; ++t) {
+      const int lv = S_.level[(int)h[8 * t + 6]];
+      const int64_t* d = &hs[(size_t)16 * t];
+      sq[lv * 3] += (d[14] - d[4]) * 0.01;
+      sq[lv * 3 + 1] += (d[15] - d[14]) * 0.01;
+      sq[lv * 3 + 2] += (d[5] - d[15]) * 0.01;
+    }
+    for (int lv = 0; lv < S_.nlevels; ++lv)
+      if (na[lv])
+        fprintf(stderr, "  store level %d: U issue %.2f  drain+flag %.2f  L/D %.2f us\n", lv, sq[lv * 3] / na[lv],
+                sq[lv * 3 + 1] / na[lv], sq[lv * 3 + 2] / na[lv]);
     for (int lv = 0; lv < S_.nlevels; ++lv)
       if (na[lv])
         fprintf(stderr,
