@@ -1101,24 +1101,32 @@ __device__ __forceinline__ void writeout_u(const double* A, int r, int w, int ld
 template <bool PK>
 __device__ __forceinline__ void writeout_ld(const double* A, int r, int w, int ld, const double* Dl, double* L, double* D,
                                            int f0, LDLStatus* st, double tol) {
-  const int tid = threadIdx.x;
-  const int nel = r * w;
-  ColWalk wk(tid, r);
-  for (int base = 0; base < nel; base += NT * 8) {
-    double v[8];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // L panel (ld r; d on the diagonal, zeros above): columns dealt to waves as in writeout_u
+  for (int j0 = 4 * wv; j0 < w; j0 += 16) {
+    double x[4][3];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {  // unconditional LDS loads (clamped), selects
-      const int i = min(wk.i, r - 1), j = min(wk.j, w - 1);
-      double a = A[fidx<PK>(max(i, j), min(i, j), r, ld)];
-      asm volatile("" : "+v"(a));
+    for (int cb = 0; cb < 4; ++cb) {
+      const int j = min(j0 + cb, w - 1);
+      const int base = PK ? ((j * (2 * r - j - 1)) >> 1) : j * ld;
       const double d = Dl[j];
-      v[k] = (i > j) ? a : (i == j ? d : 0.0);
-      wk.next();
+#pragma unroll
+      for (int h = 0; h < 3; ++h) {
+        const int i = lane + 64 * h, ic = min(max(i, j), r - 1);
+        double a = A[base + ic];
+        asm volatile("" : "+v"(a));
+        x[cb][h] = (i > j) ? a : (i == j ? d : 0.0);
+      }
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int q = base + k * NT + tid;
-      if (q < nel) L[q] = v[k];
+    for (int cb = 0; cb < 4; ++cb) {
+      const int j = j0 + cb;
+#pragma unroll
+      for (int h = 0; h < 3; ++h) {
+        const int i = lane + 64 * h;
+        if (j < w && i < r) L[i + (int64_t)j * r] = x[cb][h];
+      }
     }
   }
   if (tid < w) {
@@ -1135,35 +1143,53 @@ __device__ __forceinline__ void blocked_writeout(const double* A, int r, int w, 
 }
 // lower triangle of the update block U (ld uld); SC1: stored write-through (handed to a parent
 // inside the same launch)
-template <bool PK, bool SC1>
-__device__ __forceinline__ void writeout_u(const double* A, int r, int w, int ld, double* Uo, int uld) {
-  const int tid = threadIdx.x;
+// columns dealt to waves, NC per wave and round, NH 64-row chunks per column; a column's rows run
+// over the lanes, so the LDS and global addresses are a wave-uniform column base + the row (no
+// per-element index arithmetic: with one wave per SIMD that arithmetic bounded this loop)
+template <bool PK, bool SC1, int NH, int NC>
+__device__ __forceinline__ void writeout_u_cols(const double* A, int r, int w, int ld, double* Uo, int uld) {
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int u = r - w;
-  if (u <= 0) return;
-  const int nel = u * u;
-  ColWalk wk(tid, u);
-  for (int base = 0; base < nel; base += NT * 8) {
-    double v[8];
-    int64_t dst[8];
+  for (int b0 = NC * wv; b0 < u; b0 += 4 * NC) {
+    double x[NC][NH];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {  // unconditional LDS loads (clamped)
-      const int q = base + k * NT + tid;
-      const int a = min(wk.i, u - 1), b = min(wk.j, u - 1);
-      double x = A[fidx<PK>(w + max(a, b), w + min(a, b), r, ld)];
-      asm volatile("" : "+v"(x));
-      v[k] = x;
-      dst[k] = (q < nel && a >= b) ? a + (int64_t)b * uld : -1;
-      wk.next();
+    for (int cb = 0; cb < NC; ++cb) {
+      const int b = min(b0 + cb, u - 1), j = w + b;
+      const int base = PK ? ((j * (2 * r - j - 1)) >> 1) : j * ld;  // fidx(i, j) = base + i
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        const int a = min(b + lane + 64 * h, u - 1);
+        x[cb][h] = A[base + w + a];
+        asm volatile("" : "+v"(x[cb][h]));
+      }
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (dst[k] >= 0) {
-        if (SC1)
-          __hip_atomic_store(Uo + dst[k], v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
-          Uo[dst[k]] = v[k];
+    for (int cb = 0; cb < NC; ++cb) {
+      const int b = b0 + cb;
+      double* col = Uo + (int64_t)b * uld;
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        const int a = b + lane + 64 * h;
+        if (b < u && a < u) {
+          if (SC1)
+            __hip_atomic_store(col + a, x[cb][h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          else
+            col[a] = x[cb][h];
+        }
       }
+    }
   }
+}
+template <bool PK, bool SC1>
+__device__ __forceinline__ void writeout_u(const double* A, int r, int w, int ld, double* Uo, int uld) {
+  const int u = r - w;
+  if (u <= 64)
+    writeout_u_cols<PK, SC1, 1, 8>(A, r, w, ld, Uo, uld);
+  else if (u <= 128)
+    writeout_u_cols<PK, SC1, 2, 6>(A, r, w, ld, Uo, uld);
+  else
+    writeout_u_cols<PK, SC1, 3, 4>(A, r, w, ld, Uo, uld);
 }
 
 // lower part of an r x r front assembled in HBM scratch (ld r) -> LDS, 16 loads in flight per thread
