@@ -575,10 +575,11 @@ __global__ __launch_bounds__(ANT) void k_assemble(FrontTab T, const SymbolicPlan
   const int64_t fso = T.fs_off[s];
   double* __restrict__ F = (fso >= 0 ? fscratch + fso : arena + T.l_off[s]);
   const int i = I0 + lane;
+  const int img = (fso >= 0) ? T.fs_img[s] : 0;  // tree front: write its LDS image
   for (int jj = wv; jj < 64; jj += ANT / 64) {
     const int j = J0 + jj;
     if (i < r && j < r && i >= j) {
-      const int64_t q = i + (int64_t)j * r;
+      const int64_t q = !img ? i + (int64_t)j * r : (r > 128 ? (int64_t)((j * (2 * r - j - 1)) >> 1) + i : i + (int64_t)j * (r | 1));
       F[q] = acc ? F[q] + Ft[lane + jj * 64] : Ft[lane + jj * 64];
     }
   }
@@ -1465,10 +1466,22 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
     }
     __syncthreads();
     absorb_leaves<PK>(T, s, r, ld, A, Kx, arena, D, st, tol, A + ((ntot + 1) & ~1), dg);  // 16-byte aligned
-  } else if (!PK) {
-    stage_panel(fscratch + T.fs_off[s], A, r, r, ld);
-  } else {
-    stage_front<true>(fscratch + T.fs_off[s], A, r, ld);
+  } else {  // pre-assembled as the LDS image: a straight copy, 16 loads in flight per thread
+    const double* __restrict__ src = fscratch + T.fs_off[s];
+    const int n = PK ? r * (r + 1) / 2 : r * ld;
+    for (int base = 0; base < n; base += NT * 16) {
+      double v[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int q = base + k * NT + tid;
+        v[k] = (q < n) ? src[q] : 0.0;
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int q = base + k * NT + tid;
+        if (q < n) A[q] = v[k];
+      }
+    }
   }
   if (dg) {
     __syncthreads();
@@ -2924,6 +2937,12 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   bt_.upload(S.bt);
   fscratch_.alloc(std::max<int64_t>(S.fs_size, 1));
   T_.fs_off = fs_off_;
+  {
+    std::vector<uint8_t> img(std::max<size_t>(S.nrows.size(), 1), 0);
+    for (size_t f = 0; f < S.nrows.size(); ++f) img[f] = (S.ftree[f] && !S.absorb[f] && S.fs_off[f] >= 0) ? 1 : 0;
+    fs_img_.upload(img);
+    T_.fs_img = fs_img_;
+  }
   T_.sv_ptr = sv_ptr_;
   T_.sv_src = sv_src_;
   const int ns = S.nsuper, NL = S.nlevels;

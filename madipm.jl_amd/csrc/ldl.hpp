@@ -65,6 +65,7 @@ struct FrontTab {
   const int32_t* ab_wrc;
   const int64_t* ab_loff;
   const uint8_t* rheavy;
+  const uint8_t* fs_img;  // 1: fscratch holds the front's LDS image (tree fronts), else ld r
   int schur_defer;  // in-LDS factorisation: update block U in one pass after the pivots (MADIPM_SCHUR_DEFER)
 };
 
@@ -246,7 +247,7 @@ class LDLSolver : public LinSolver {
   DBuf<int64_t> fdbg_, rl_ptr_, fr_ptr_, ab_first_;
   DBuf<int32_t> ab_src0_, ab_src1_, ab_rel_, ab_k_, ab_bptr_, ab_bat_, ab_f0_, ab_wrc_;
   DBuf<int64_t> ab_loff_;
-  DBuf<uint8_t> absorb_, rheavy_;
+  DBuf<uint8_t> absorb_, rheavy_, fs_img_;
   DBuf<int32_t> mc_ptr_, mc_list_, rl_ent_;
   DBuf<double> xch_;
   DBuf<uint8_t> wout_, colmask_;
