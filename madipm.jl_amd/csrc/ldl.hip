@@ -1230,11 +1230,22 @@ __global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t*
   const int ld = r | 1;
   const int tid = threadIdx.x;
   const int64_t fso = T.fs_off[s];
-  if (fso >= 0) {  // assembled by k_assemble (lower part valid)
-    if (!PK)
-      stage_panel(fscratch + fso, A, r, r, ld);
-    else
-      stage_front<true>(fscratch + fso, A, r, ld);
+  if (fso >= 0) {  // assembled by k_assemble as the LDS image (lower part valid): a straight copy
+    const double* __restrict__ src = fscratch + fso;
+    const int n = PK ? r * (r + 1) / 2 : r * ld;
+    for (int base = 0; base < n; base += NT * 16) {
+      double v[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int q = base + k * NT + tid;
+        v[k] = (q < n) ? src[q] : 0.0;
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int q = base + k * NT + tid;
+        if (q < n) A[q] = v[k];
+      }
+    }
   } else {  // leaf: original entries only
     const int ntot = PK ? r * (r + 1) / 2 : r * ld;
     for (int q = tid; q < ntot; q += NT) A[q] = 0.0;
@@ -2938,8 +2949,14 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   fscratch_.alloc(std::max<int64_t>(S.fs_size, 1));
   T_.fs_off = fs_off_;
   {
+    // fronts staged into LDS by k_fact_tree (all sizes) and k_small_blocked (r > 32, not big, not a
+    // batched-leaf parent, whose SYRK writes ld r) are pre-assembled as their LDS image
     std::vector<uint8_t> img(std::max<size_t>(S.nrows.size(), 1), 0);
-    for (size_t f = 0; f < S.nrows.size(); ++f) img[f] = (S.ftree[f] && !S.absorb[f] && S.fs_off[f] >= 0) ? 1 : 0;
+    std::vector<uint8_t> lbpar(S.nrows.size(), 0);
+    for (const auto& G : S.lb) lbpar[G.parent] = 1;
+    for (size_t f = 0; f < S.nrows.size(); ++f)
+      img[f] = (S.fs_off[f] >= 0 &&
+                (S.ftree[f] ? !S.absorb[f] : (!S.is_big[f] && !lbpar[f] && S.nrows[f] > 32))) ? 1 : 0;
     fs_img_.upload(img);
     T_.fs_img = fs_img_;
   }

@@ -839,9 +839,9 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   for (int s = 0; s < ns; ++s)
     if ((S.ftree[s] && !S.absorb[s]) || (!S.ftree[s] && !S.is_big[s] && S.child_ptr[s + 1] > S.child_ptr[s] && S.mine(s))) {
       S.fs_off[s] = S.fs_size;
-      // tree fronts are pre-assembled as their LDS image (square ld r | 1, or packed lower for
-      // r > 128): room for r (r | 1) doubles
-      S.fs_size += (int64_t)S.nrows[s] * (S.ftree[s] ? (S.nrows[s] | 1) : S.nrows[s]);
+      // fronts staged into LDS are pre-assembled as their LDS image (square ld r | 1, or packed
+      // lower for r > 128): room for r (r | 1) doubles
+      S.fs_size += (int64_t)S.nrows[s] * (S.nrows[s] | 1);
     }
   S.atiles.clear();
   S.g_ptr.clear();
