@@ -1458,6 +1458,44 @@ __device__ __forceinline__ void absorb_leaves(const FrontTab& T, int s, int r, i
 // children's flags and adds their update blocks child by child (sc1 loads; the children stored them
 // write-through), factorises in LDS and publishes (every wave drains, barrier, one flag store).  The
 // last workgroup to finish resets the ticket counters for the next launch.
+// Child update block -> parent front in LDS: child columns dealt to waves (NC per wave and round,
+// NH 64-row chunks), all of a round's loads (sc1: handed over inside the launch) issued before the
+// read-modify-writes; the parent column base is wave-uniform, so a row costs one rels lookup.
+// Destinations are distinct within a child, so all LDS reads of a round precede its writes.
+template <bool PK, int NH, int NC>
+__device__ __forceinline__ void push_cols(double* A, int r, int ld, const double* U, int64_t uld, int uc,
+                                          const int32_t* rels) {
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (int b0 = NC * wv; b0 < uc; b0 += 4 * NC) {
+    double x[NC][NH];
+    int dst[NC][NH];
+#pragma unroll
+    for (int cb = 0; cb < NC; ++cb) {
+      const int b = b0 + cb, bc = min(b, uc - 1);
+      const int j = rels[bc];
+      const int base = PK ? ((j * (2 * r - j - 1)) >> 1) : j * ld;  // fidx(i, j) = base + i
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        const int a = b + lane + 64 * h;
+        const bool ok = b < uc && a < uc;
+        x[cb][h] = ok ? __hip_atomic_load(U + a + (int64_t)bc * uld, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+        dst[cb][h] = ok ? base + rels[min(a, uc - 1)] : -1;
+      }
+    }
+    double o[NC][NH];
+#pragma unroll
+    for (int cb = 0; cb < NC; ++cb)
+#pragma unroll
+      for (int h = 0; h < NH; ++h) o[cb][h] = A[max(dst[cb][h], 0)];
+#pragma unroll
+    for (int cb = 0; cb < NC; ++cb)
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+        if (dst[cb][h] >= 0) A[dst[cb][h]] = o[cb][h] + x[cb][h];
+  }
+}
+
 template <bool PK>
 __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const int32_t* __restrict__ dep, int q0, int q1,
                                                 int32_t* flags, int epoch, const double* Kx, double* arena,
@@ -1508,32 +1546,12 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
     const double* U = arena + T.u_off[c];
     for (int a = tid; a < uc; a += NT) rels[a] = T.rel[T.rel_ptr[c] + a];
     __syncthreads();
-    // entries (a >= b) of the child's U, flattened over its square index space: 16 loads in
-    // flight per thread (a child's update block takes one or two memory round trips)
-    const int n2 = uc * uc;
-    const float inv = 1.0f / (float)max(uc, 1);
-    for (int base = 0; base < n2; base += NT * 16) {
-      double x[16];
-      int dst[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int e = base + k * NT + tid;
-        int b = (int)((float)e * inv);
-        b -= (b * uc > e) ? 1 : 0;
-        b += ((b + 1) * uc <= e) ? 1 : 0;
-        const int a = e - b * uc;
-        const bool ok = e < n2 && a >= b;
-        x[k] = ok ? __hip_atomic_load(U + a + b * uld, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
-        dst[k] = ok ? fidx<PK>(rels[min(a, uc - 1)], rels[min(b, uc - 1)], r, ld) : -1;
-      }
-      // distinct destinations within a child: all reads, then all writes (no read-after-write chain)
-      double o[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) o[k] = A[max(dst[k], 0)];
-#pragma unroll
-      for (int k = 0; k < 16; ++k)
-        if (dst[k] >= 0) A[dst[k]] = o[k] + x[k];
-    }
+    if (uc <= 64)
+      push_cols<PK, 1, 8>(A, r, ld, U, uld, uc, rels);
+    else if (uc <= 128)
+      push_cols<PK, 2, 6>(A, r, ld, U, uld, uc, rels);
+    else
+      push_cols<PK, 3, 4>(A, r, ld, U, uld, uc, rels);
     __syncthreads();
   }
   if (dg && tid == 0) dg[3] = wall_clock64();
