@@ -95,6 +95,18 @@ def test_ldl_tree_and_level_paths(tree_fact, tree_solve, well, monkeypatch):
     assert ls.inertia() == (4000, 0, 3000)
 
 
+@pytest.mark.parametrize("defer", ["0", "1"])
+@pytest.mark.parametrize("sfm", [128, 192])
+def test_ldl_schur_update_variants(defer, sfm, monkeypatch):
+    """In-LDS factorisation with the update block's Schur complement formed once after all pivots
+    (MADIPM_SCHUR_DEFER=1, default) or at every 16-pivot step (0): the oracle's pivots to 1e-12
+    (well conditioned), square (<= 128 rows) and packed (<= 192 rows) LDS storage."""
+    monkeypatch.setenv("MADIPM_SCHUR_DEFER", defer)
+    K, Lw = block_angular_k2(3000, 4000, 20, 7, well=True)
+    ls = _check_case(K, Lw, small_front_max=sfm, well=True)
+    assert ls.inertia() == (4000, 0, 3000)
+
+
 @pytest.mark.parametrize("well", [True, False])
 def test_ldl_leaf_absorption(well, monkeypatch):
     """Experimental leaf absorption (MADIPM_ABSORB=1): tree fronts factorise their micro-leaf children
