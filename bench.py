@@ -74,35 +74,101 @@ def solver_opts():
                 tol=1e-8)
 
 
+def host_cpu_info() -> dict:
+    """nproc / lscpu of the host the baseline ran on (core count stated)."""
+    info = {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in ("Model name", "Socket(s)", "Core(s) per socket", "Thread(s) per core", "CPU max MHz"):
+                info[k.strip()] = v.strip()
+    except Exception:
+        pass
+    return info
+
+
+def baseline_threads() -> int:
+    """The host cores this process may use: its affinity set, capped by OMP_NUM_THREADS (16 per GPU
+    on the gpurun boxes, whose nproc counts the whole machine)."""
+    n = len(os.sched_getaffinity(0))
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return max(1, n)
+
+
 def cpu_baseline(qp, perm, budget_s: float = 20.0):
-    """Oracle (CPU restatement, oracle/) timed on this host: bounded sample of MPC iterations.
+    """CPU baseline on this host (SURVEY §8 d; scripts/benchmarks_cpu.jl:26-50 drives MadIPM with a
+    multithreaded supernodal LDL^T, HSL MA57, which is unavailable here): the oracle's MPC loop
+    (oracle/mpc.py, a restatement of src/solver.jl) with Intel MKL PARDISO (oracle/pardiso.py,
+    supernodal symmetric-indefinite, the same fill-reducing order as the GPU) as its linear solver.
 
-    The oracle factors K2 with oracle/ldl_ref.c (LDLFactorizations' algorithm) in the SAME
-    fill-reducing order as the GPU (`perm`, computed by the analysis phase, untimed on both
-    sides), so both sides factor identical nnz(L)."""
+    * `threads` run: to optimality at the host's core share -> the parity record (status, objective,
+      iterations vs the GPU) and the timings;
+    * 1-thread run: a bounded sample (about `budget_s` of CPU work).
+    `value` = MPC iterations / (PARDISO factorisation + solve time): the rate a native host driver
+    would reach with PARDISO (the numpy loop around it is not counted); the full loop rate is
+    reported beside it."""
     from oracle.mpc import OracleMPC, OracleOptions
+    from oracle import pardiso
 
-    def run(k):
+    def run(k, threads):
+        got = pardiso.set_threads(threads)
         o = OracleMPC(qp, OracleOptions(regularization=("fixed", 1e-8, -1e-8), step_rule=("adaptive", 0.99),
-                                        max_iter=k), record_trace=False)
-        o.linear_solver = "ldl"
+                                        max_iter=k, tol=1e-8), record_trace=False)
+        o.linear_solver = "pardiso"
         o.ldl_perm = perm
-        return o.solve()
+        t0 = time.perf_counter()
+        st = o.solve()
+        F = o._pardiso
+        return st, {"threads": got, "iters": st.iter, "loop_s": st.total_time, "wall_s": time.perf_counter() - t0,
+                    "pardiso_factor_s": F.t_factor, "pardiso_solve_s": F.t_solve, "factorizations": F.nfactor,
+                    "solves": F.nsolve, "pardiso_analysis_s": F.t_analysis, "nnzL_pardiso": F.nnzL,
+                    "perturbed_pivots": F.nperturbed}
+    T = baseline_threads()
+    st, full = run(300, T)
+    it_t = full["iters"] / (full["pardiso_factor_s"] + full["pardiso_solve_s"])
+    # 1 thread: bounded sample, scaled from the multithreaded per-iteration PARDISO time
+    per_it = (full["pardiso_factor_s"] + full["pardiso_solve_s"]) / max(1, full["factorizations"]) * 3.0
+    k1 = int(max(2, min(full["iters"], budget_s / max(per_it, 1e-3))))
+    _, one = run(k1, 1)
+    it_1 = one["iters"] / (one["pardiso_factor_s"] + one["pardiso_solve_s"]) if one["iters"] else None
+    return st, {
+        "value": it_t, "unit": "iters/s", "cores": T, "kind": "port",
+        "sample": (f"oracle/mpc.py MPC loop + MKL PARDISO (mtype -2, GPU's fill-reducing order) on the same "
+                   f"standard-form problem, {T} threads to optimality ({full['iters']} iterations); value = "
+                   f"iterations / PARDISO factor+solve time; 1-thread sample of {one['iters']} iterations"),
+        "loop_iters_per_s": full["iters"] / full["loop_s"] if full["loop_s"] > 0 else None,
+        "value_1thread": it_1, "runs": {"threads": full, "one_thread": one}, "host": host_cpu_info()}
+
+
+def highs_baseline(qp, time_limit: float = 120.0):
+    """Third-party CPU datapoint: HiGHS 1.x interior point (scipy.optimize.linprog 'highs-ipm', presolve
+    off, crossover as scipy runs it) on the same standard-form LP; wall time and objective."""
+    import numpy as np
+    import scipy.sparse as sp
+    from scipy.optimize import linprog
+    if qp.nnzh or not np.all(qp.lcon == qp.ucon):
+        return None
+    A = sp.csr_matrix((qp.Avals, (qp.Arows, qp.Acols)), shape=(qp.ncon, qp.nvar))
+    bnds = [(a if np.isfinite(a) else None, b if np.isfinite(b) else None) for a, b in zip(qp.lvar, qp.uvar)]
+    sg = 1.0 if qp.minimize else -1.0
     t0 = time.perf_counter()
-    run(1)       # calibration: initialize! + 1 iteration
-    per_it = max(1e-3, (time.perf_counter() - t0) / 2.0)
-    k = int(max(1, min(50, budget_s / per_it)))
-    st = run(k)
-    return {"value": st.iter / st.total_time if st.total_time > 0 else None, "unit": "iters/s", "cores": 1,
-            "kind": "port",
-            "sample": f"{st.iter} MPC iterations of the same standard-form ex10 stand-in, oracle/mpc.py "
-                      f"(numpy) + oracle/ldl_ref.c up-looking LDL^T (1 thread), loop time {st.total_time:.2f}s"}
+    r = linprog(sg * qp.c, A_eq=A, b_eq=qp.lcon, bounds=bnds, method="highs-ipm",
+                options=dict(presolve=False, disp=False, time_limit=time_limit))
+    dt = time.perf_counter() - t0
+    return {"status": int(r.status), "message": r.message, "objective": sg * float(r.fun) + qp.c0 if r.fun is not None else None,
+            "ipm_iterations": int(getattr(r, "nit", 0) or 0), "wall_s": dt}
 
 
 # Peaks (MI355X): HBM3E 8.0 TB/s spec (/opt/skills/guides/MI355X_MICROARCH.md); f64 MFMA
 # (v_mfma_f64_16x16x4f64) 78.6 TFLOP/s dense, AMD spec (the guide tabulates no f64 row;
 # profiles/r1_mfma_f64_peak.txt holds our own measurement of the instruction's rate).
 PEAK_HBM_GBS = 8000.0
+STATUS = {1: "SOLVE_SUCCEEDED", 2: "INFEASIBLE_PROBLEM_DETECTED", -1: "MAXIMUM_ITERATIONS_EXCEEDED",
+          -2: "MAXIMUM_WALLTIME_EXCEEDED", -3: "DIVERGING_ITERATES", -4: "ERROR_IN_STEP_COMPUTATION"}
 PEAK_F64_TFS = 78.6
 
 
@@ -149,7 +215,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="ex10")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--highs", action=argparse.BooleanOptionalAction, default=True,
+                    help="time HiGHS-IPM (scipy) on the same LP as a third-party CPU datapoint")
     ap.add_argument("--no-opt", action="store_true", help="skip the wall-clock-to-optimality solve")
     ap.add_argument("--ordering", type=int, default=None, help="LDL ordering override (0 natural, 1 AMD, 3 ND, 4 auto)")
     ap.add_argument("--mode", choices=["shard", "replicas"], default="shard",
@@ -246,12 +314,29 @@ def main():
             "roofline": roof,
             "kernel_ms_warmup": breakdown,
             "cpu_baseline": None,
+            "parity": None,
         }
         if not args.no_cpu and world == 1 and not args.config.startswith(("dense_qp", "neos")):
             try:
-                out["cpu_baseline"] = cpu_baseline(qp, solver.kkt_perm(), args.cpu_budget)
+                ref, out["cpu_baseline"] = cpu_baseline(qp, solver.kkt_perm(), args.cpu_budget)
+                if opt:
+                    # parity at the benchmarked size: the GPU solve to optimality vs the oracle's (same
+                    # problem, same settings; BASELINE.md parity rule |dobj| <= 1e-6 max(1, |obj|))
+                    rel = abs(opt["objective"] - ref.objective) / max(1.0, abs(ref.objective))
+                    out["parity"] = {"reference": "oracle/mpc.py + MKL PARDISO (CPU)",
+                                     "status_gpu": opt["status"], "status_ref": STATUS.get(ref.status, ref.status),
+                                     "status_equal": STATUS.get(ref.status) == opt["status"],
+                                     "objective_gpu": opt["objective"], "objective_ref": ref.objective,
+                                     "rel_obj_diff": rel, "iters_gpu": opt["iters_to_opt"], "iters_ref": ref.iter,
+                                     "ok": bool(STATUS.get(ref.status) == opt["status"] and rel <= 1e-6
+                                                and abs(opt["iters_to_opt"] - ref.iter) <= 1)}
             except Exception as e:  # pragma: no cover - reported, not hidden
                 out["cpu_baseline"] = {"error": repr(e)}
+            if args.highs:
+                try:
+                    out["cpu_baseline"]["highs_ipm"] = highs_baseline(qp)
+                except Exception as e:  # pragma: no cover
+                    out["cpu_baseline"]["highs_ipm"] = {"error": repr(e)}
         print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()

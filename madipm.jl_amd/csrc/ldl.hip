@@ -115,9 +115,10 @@ __device__ __forceinline__ void stage_panel(const double* __restrict__ L, double
   }
 }
 
-__global__ void k_status_init(LDLStatus* st) {
+__global__ void k_status_init(LDLStatus* st, int all = 0) {
   st->fail_pivot = INT_MAX;
   st->npos = st->nneg = st->nzero = 0;
+  if (all) st->err = 0;
 }
 
 // ------------------------------------------------------------------ small fronts (LDS)
@@ -1230,7 +1231,9 @@ __global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t*
   const int ld = r | 1;
   const int tid = threadIdx.x;
   const int64_t fso = T.fs_off[s];
-  if (fso >= 0) {  // assembled by k_assemble as the LDS image (lower part valid): a straight copy
+  if (fso >= 0 && !T.fs_img[s]) {  // batched-leaf parent: the SYRK and k_assemble wrote ld r
+    stage_front<PK>(fscratch + fso, A, r, ld);
+  } else if (fso >= 0) {  // assembled by k_assemble as the LDS image (lower part valid): a straight copy
     const double* __restrict__ src = fscratch + fso;
     const int n = PK ? r * (r + 1) / 2 : r * ld;
     for (int base = 0; base < n; base += NT * 16) {
@@ -3467,8 +3470,6 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     flags_.zero();
     counters_.alloc(4 * std::max(NL, 1) + 4);  // + the tree-solve tickets (4 NL, 4 NL + 1)
     counters_.zero();
-    err_.alloc(1);
-    err_.zero();
   }
   sched_.upload(sched.empty() ? std::vector<int32_t>{0} : sched);
   arena_.alloc(std::max<int64_t>(S.arena_size, 2));
@@ -3482,6 +3483,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   MADIPM_HIP(hipHostMalloc((void**)&h_status_, sizeof(LDLStatus), hipHostMallocDefault));
   st_ = status_.p;
   h_st_ = h_status_;
+  status_.zero();
+  h_st_->err = 0;
   static bool attr_done = false;
   if (!attr_done) {
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_small_factor<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -3659,7 +3662,7 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
         TIMED(KK_FACT_TREE, L.bytes, L.flops,
               (k_fact_tree<<<(unsigned)nftree_, NT, L.lds_bytes, s>>>(T_, ft_order_, nftree_, ft_dptr_, ft_dep_, fcnt_,
                                                                       fflags_, fepoch_, Kx, arena_, fscratch_, D_, st_,
-                                                                      pivot_tol, err_, fdbg_.p)));
+                                                                      pivot_tol, &st_->err, fdbg_.p)));
         if (fdbg_.p) tree_debug_dump(s, "fact", fdbg_.p, nftree_, "stage", "wait", "push", "factor", "store", 16);
         break;
     }
@@ -3709,7 +3712,7 @@ bool LDLSolver::external_status(LDLStatus* dev, LDLStatus* host) {
   st_ = dev;
   h_st_ = host;
   ext_status_ = true;
-  k_status_init<<<1, 1, 0, nullptr>>>(st_);
+  k_status_init<<<1, 1, 0, nullptr>>>(st_, 1);
   MADIPM_HIP(hipDeviceSynchronize());
   return true;
 }
@@ -3721,6 +3724,12 @@ int LDLSolver::status(hipStream_t s, bool sync) {
   }
   if (sync && ext_status_) MADIPM_HIP(hipMemcpyAsync(h_st_, st_, sizeof(LDLStatus), hipMemcpyDeviceToHost, s));
   if (sync) MADIPM_HIP(hipStreamSynchronize(s));
+  if (h_st_->err) {  // a lost hand-off gives a wrong factor or solve: never report it as success
+    h_st_->err = 0;
+    k_status_init<<<1, 1, 0, s>>>(st_, 1);
+    MADIPM_HIP(hipStreamSynchronize(s));
+    throw Error("LDL^T: a dependency hand-off between fronts timed out (factor or solve is invalid)", -5);
+  }
   npos = h_st_->npos;
   nneg = h_st_->nneg;
   nzero = h_st_->nzero;
@@ -3811,14 +3820,14 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
             (k_fwd_gather<<<L.ngat, NT, 0, s>>>(T_, sched_.p + L.gat_off, b, uvec_, vwork_)));
       TIMED(KK_FWD_BIG, L.big_bytes, L.big_flops,
             (k_fwd_big<<<std::min(L.nftask, 512), NT, 0, s>>>(T_, tasks + L.ftask_off, L.nftask, cnt + 2 * lev,
-                                                               flags_, flag_off_, efwd, arena_, vwork_, xi_, uvec_, err_)));
+                                                               flags_, flag_off_, efwd, arena_, vwork_, xi_, uvec_, &st_->err)));
     }
     if (lev == 0 && phase == 0 && ntree_)
       TIMED(KK_FWD_TREE, tree_bytes_, tree_flops_,
             (k_fwd_tree<<<(unsigned)ntree_, NT, tree_lds_, s>>>(T_, tf_order_, ntree_, tdep_ptr_, tdep_,
                                                                  counters_.p + 4 * S_.nlevels, tflags_, efwd, tree_lds_ / 8,
                                                                  arena_, b,
-                                                                 xi_, uvec_, err_, tdbg_.p)));
+                                                                 xi_, uvec_, &st_->err, tdbg_.p)));
     if (lev == 0 && phase == 0 && ntree_ && tdbg_.p)
       tree_debug_dump(s, "fwd", tdbg_.p, ntree_, "stage", "wait", "gather", "subst", "store", 8);
   }
@@ -3833,7 +3842,7 @@ void LDLSolver::bwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
     if (lev == 0 && phase == 0 && ntree_)
       TIMED(KK_BWD_TREE, tree_bytes_, tree_flops_,
             (k_bwd_tree<<<(unsigned)ntree_, NT, tree_lds_, s>>>(T_, tb_order_, ntree_, tpar_, counters_.p + 4 * S_.nlevels + 1,
-                                                                 tflags_, ebwd, arena_, D_, xi_, b, err_)));
+                                                                 tflags_, ebwd, arena_, D_, xi_, b, &st_->err)));
     if (L.nbelow)
       TIMED(KK_BWD_BELOW, L.below_bytes, 0.25 * L.below_bytes,
             (k_bwd_below<<<L.nbelow, NT, 0, s>>>(T_, sched_.p + L.below_off, bp_off_, arena_, xi_, bpart_)));
@@ -3841,7 +3850,7 @@ void LDLSolver::bwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
       TIMED(KK_BWD_BIG, L.big_bytes - L.below_bytes, L.big_flops - 0.25 * L.below_bytes,
             (k_bwd_big<<<std::min(L.nbtask, 512), NT, 0, s>>>(T_, tasks + L.btask_off, L.nbtask, cnt + 2 * lev + 1,
                                                                flags_, flag_off_, ebwd, arena_, D_, xi_, b, bp_off_, bpart_,
-                                                               err_)));
+                                                               &st_->err)));
     if (L.nsmall)
       TIMED(KK_BWD_SMALL, L.small_bytes, L.small_flops,
             (k_bwd_small<<<(unsigned)L.nsmall, NT, L.small_lds, s>>>(T_, sched_.p + L.small_off, L.nsmall, arena_, D_, xi_,

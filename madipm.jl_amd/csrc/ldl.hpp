@@ -76,6 +76,7 @@ struct SolveTask {
 struct LDLStatus {  // device-resident, read back by status()
   int32_t fail_pivot;  // min failing internal pivot + 1 (INT32_MAX when none)
   int32_t npos, nneg, nzero;
+  int32_t err;  // sticky: a dependency hand-off (flag poll) timed out in a factorisation or solve
 };
 
 // Kernel kinds for the live per-kernel timing (HIP events around each launch on the launch
@@ -251,7 +252,7 @@ class LDLSolver : public LinSolver {
   DBuf<int32_t> mc_ptr_, mc_list_, rl_ent_;
   DBuf<double> xch_;
   DBuf<uint8_t> wout_, colmask_;
-  DBuf<int32_t> tasks_, flags_, flag_off_, counters_, err_, bp_off_;
+  DBuf<int32_t> tasks_, flags_, flag_off_, counters_, bp_off_;
   DBuf<double> bpart_;
   int epoch_ = 0;
   // device data

@@ -475,6 +475,7 @@ __global__ __launch_bounds__(NT) void k_mu(DV D, int use_state, double ap_arg, d
 
 // apply_step! + adjust_boundary! [EXT] (solver.jl:308-317)
 __global__ __launch_bounds__(NT) void k_apply(DV D) {
+  if (D.st->nan_flag) return;  // SolveException raised in this iteration's directions: no step
   const int n = D.n, m = D.m, nlb = D.nlb;
   const double ap = D.st->alpha_p, ad = D.st->alpha_d, mu = D.st->mu;
   const double eps = 2.220446049250313e-16;
@@ -1493,9 +1494,25 @@ void MPCSolver::assemble_kkt(double dw, double dc) {
 
 const double* MPCSolver::kvals() const { return kkt_ == KKT_NORMAL ? Cx_.p : Kx_.p; }
 
+// factorize! between two pooled timing events (cnt.linear_solver_time, MadNLP.factorize_wrapper!);
+// the pool grows only when a solve needs more pairs than any earlier one did
+void MPCSolver::timed_factorize() {
+  if (nfev_ + 2 > fact_events_.size()) {
+    for (int q = 0; q < 64; ++q) {
+      hipEvent_t e;
+      MADIPM_HIP(hipEventCreate(&e));
+      fact_events_.push_back(e);
+    }
+  }
+  MADIPM_HIP(hipEventRecord(fact_events_[nfev_], stream_));
+  ldl_->factorize_async(kvals(), stream_);
+  MADIPM_HIP(hipEventRecord(fact_events_[nfev_ + 1], stream_));
+  nfev_ += 2;
+}
+
 void MPCSolver::factor_enqueue(double dw, double dc) {
   assemble_kkt(dw, dc);
-  ldl_->factorize_async(kvals(), stream_);
+  timed_factorize();
 }
 
 // MadNLP.solve!(kkt, d) between reduce_rhs! (k_rhs) and finish_aug_solve! (k_residual)
@@ -1584,25 +1601,6 @@ void MPCSolver::read_state() {
   MADIPM_HIP(hipMemcpyAsync(hst_, st_.p, sizeof(DevState), hipMemcpyDeviceToHost, stream_));
 }
 
-// factorize_system! (solver.jl:299-303) is split: the regularization update is done by the caller.
-void MPCSolver::factorize_regularized() {
-  for (int trial = 0; trial < 3; ++trial) {  // linear_solver.jl:6-17
-    assemble_kkt(del_w_, del_c_);
-    hipEvent_t e0, e1;
-    MADIPM_HIP(hipEventCreate(&e0));
-    MADIPM_HIP(hipEventCreate(&e1));
-    MADIPM_HIP(hipEventRecord(e0, stream_));
-    ldl_->factorize_async(kvals(), stream_);
-    MADIPM_HIP(hipEventRecord(e1, stream_));
-    fact_events_.push_back(e0);
-    fact_events_.push_back(e1);
-    read_state();
-    if (ldl_->status(stream_) == 0) return;
-    del_w_ *= 100.0;
-    del_c_ *= 100.0;
-  }
-}
-
 void MPCSolver::init_starting_point() {
   DV_ARGS;
   const int nb = blocks(n_ + m_), nbn = blocks(n_);
@@ -1610,15 +1608,10 @@ void MPCSolver::init_starting_point() {
   k_init_kkt<<<nb, NT, 0, s>>>(D, del_w_, del_c_);
   if (kkt_ == KKT_NORMAL) k_normal_asm<<<blocks(nnzC_), NT, 0, s>>>(D);
   if (kkt_ == KKT_K25) k_k25_scale<<<blocks(nnzK_), NT, 0, s>>>(D);  // s = 1: K2.5 = K2
-  hipEvent_t e0, e1;
-  MADIPM_HIP(hipEventCreate(&e0));
-  MADIPM_HIP(hipEventCreate(&e1));
-  MADIPM_HIP(hipEventRecord(e0, s));
-  ldl_->factorize_async(kvals(), s);
-  MADIPM_HIP(hipEventRecord(e1, s));
-  fact_events_.push_back(e0);
-  fact_events_.push_back(e1);
-  ldl_->status(s);  // init factorization: the reference does not retry here
+  timed_factorize();
+  // init factorization: the reference does not retry here; a solve with an unfactorized LDL^T is a
+  // step-computation failure (oracle/mpc.py solve_system)
+  if (ldl_->status(s) != 0) throw Error("init_starting_point!: KKT factorization failed", -4);
   // Step 1: least-squares primal correction
   k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_PRIMAL, 0.0, 0);
   kkt_solve();
@@ -1658,8 +1651,7 @@ void MPCSolver::initialize() {
     d_.zero(s);
     p_.zero(s);
   }
-  for (auto e : fact_events_) (void)hipEventDestroy(e);
-  fact_events_.clear();
+  nfev_ = 0;
   // init_regularization! (kernels.jl:364-392)
   switch (opt_.regularization) {
     case 0: del_w_ = 1.0; del_c_ = 0.0; break;
@@ -1744,7 +1736,7 @@ int MPCSolver::solve(madipm_stats* stats) {
     if (!initialized_) initialize_public();
     initialized_ = false;
     tstart = now();  // solver.jl:181
-    const int nb = blocks(n_ + m_), nbz = blocks(std::max(nlb_, nub_));
+    const int nb = blocks(n_ + m_);
     while (true) {
       // ---- update_termination_criteria! (+ speculative factorization of this iteration)
       k_term<<<nb, NT, 0, s>>>(D);
@@ -1762,15 +1754,7 @@ int MPCSolver::solve(madipm_stats* stats) {
           del_c_ = adapt_dd_;
       }
       // first trial enqueued together with the state read-back: ONE sync per iteration
-      assemble_kkt(del_w_, del_c_);
-      hipEvent_t e0, e1;
-      MADIPM_HIP(hipEventCreate(&e0));
-      MADIPM_HIP(hipEventCreate(&e1));
-      MADIPM_HIP(hipEventRecord(e0, s));
-      ldl_->factorize_async(kvals(), s);
-      MADIPM_HIP(hipEventRecord(e1, s));
-      fact_events_.push_back(e0);
-      fact_events_.push_back(e1);
+      factor_enqueue(del_w_, del_c_);
       read_state();
       MADIPM_HIP(hipEventRecord(ev_state_, s));
       // speculation: this iteration's directions (prediction_step!, mehrotra_correction_direction!,
@@ -1789,7 +1773,11 @@ int MPCSolver::solve(madipm_stats* stats) {
       const DevState& h = *hst_;
       last_ = h;
       if (h.nan_flag) {
+        // SolveException in the previous iteration's solve_system! (linear_solver.jl:40-41): the
+        // reference throws before apply_step!, so k_apply skipped the step on the device and the
+        // iteration is not counted (cnt.k += 1 is inside apply_step!, solver.jl:316)
         status = MADIPM_ERROR_IN_STEP_COMPUTATION;
+        if (k_ > 0) --k_;
         break;
       }
       const double dobj = h.dobj;
@@ -1835,9 +1823,11 @@ int MPCSolver::solve(madipm_stats* stats) {
           factor_enqueue(del_w_, del_c_);
           ok = ldl_->status(s) == 0;
         }
-        if (!ok) {
+        if (!ok) {  // every trial failed: the solve would use an unfactorized LDL^T
           del_w_ *= 100.0;
           del_c_ *= 100.0;
+          status = MADIPM_ERROR_IN_STEP_COMPUTATION;
+          break;
         }
         if (spec) {  // the speculated directions used the failed factor: recompute
           directions(true);
@@ -1866,7 +1856,7 @@ int MPCSolver::solve(madipm_stats* stats) {
   t_total_ = now() - tstart;
   status_ = status;
   t_linsol_ = 0;
-  for (size_t q = 0; q + 1 < fact_events_.size(); q += 2) {
+  for (size_t q = 0; q + 1 < nfev_; q += 2) {
     float ms = 0;
     if (hipEventElapsedTime(&ms, fact_events_[q], fact_events_[q + 1]) == hipSuccess) t_linsol_ += ms * 1e-3;
   }

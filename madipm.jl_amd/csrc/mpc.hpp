@@ -60,7 +60,6 @@ class MPCSolver {
   std::unique_ptr<LinSolver> make_linsolver(int n, const int64_t* cp, const int32_t* ri, const SymbolicOptions& so);
   void initialize();
   void init_starting_point();
-  void factorize_regularized();
   void solve_system(int mode, double mu, int reset = 0);
   void gondzio();
   void directions(bool redo);  // predictor + corrector directions (speculated before the status read)
@@ -74,6 +73,7 @@ class MPCSolver {
   // MadNLP.solve!(kkt, d) after the right-hand side is in d_: reduced solve in the chosen formulation
   void kkt_solve();
   void factor_enqueue(double dw, double dc);
+  void timed_factorize();
   int blocks(int64_t n) const;
   int spmv_blocks(int64_t rows) const;
 
@@ -113,7 +113,8 @@ class MPCSolver {
   double inf_pr_ = 0, inf_du_ = 0, inf_compl_ = 0;
   double t_init_ = 0, t_total_ = 0, t_linsol_ = 0;
   std::vector<madipm_iter_trace> trace_;
-  std::vector<hipEvent_t> fact_events_;
+  std::vector<hipEvent_t> fact_events_;  // pool of (begin, end) pairs around each factorize!
+  size_t nfev_ = 0;                      // events of the current solve
   hipEvent_t ev_state_ = nullptr;  // recorded after the per-iteration state read-back
   DevState last_{};                // the state of the last termination test
 };

@@ -10,6 +10,8 @@
 #include <climits>
 #include <cstdlib>
 #include <numeric>
+#include <chrono>
+#include <cstdio>
 
 #include "common.hpp"
 
@@ -162,6 +164,15 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
                       const int32_t* user_perm, SymbolicPlan& S) {
   S = SymbolicPlan();
   MADIPM_REQUIRE(N >= 0, "negative dimension");
+  // MADIPM_SYMBOLIC_TIMING=1: wall time of each step on stderr (diagnostics)
+  const bool timing = std::getenv("MADIPM_SYMBOLIC_TIMING") != nullptr;
+  auto t_last = std::chrono::steady_clock::now();
+  auto stamp = [&](const char* what) {
+    if (!timing) return;
+    const auto t = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "symbolic %-28s %9.3f s\n", what, std::chrono::duration<double>(t - t_last).count());
+    t_last = t;
+  };
   S.N = N;
   const int64_t nnz = colptr[N];
   S.nnzK = nnz;
@@ -177,6 +188,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   }
   if (N == 0) return;
 
+  stamp("before 1");
   // ---------------- 1. fill-reducing ordering
   std::vector<int32_t> perm(N);
   S.order_flops_amd = S.order_flops_nd = 0.0;
@@ -226,6 +238,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     pinv[perm[k]] = k;
   }
 
+  stamp("before 2");
   // ---------------- 2. etree + postorder, relabel so that the labelling is a postorder
   Pattern P;
   build_pattern(N, colptr, rowval, pinv, P);
@@ -234,16 +247,21 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   postorder(N, parent, post);
   std::vector<int32_t> perm2(N);
   for (int k = 0; k < N; ++k) perm2[k] = perm[post[k]];
-  perm.swap(perm2);
-  for (int k = 0; k < N; ++k) pinv[perm[k]] = k;
-  build_pattern(N, colptr, rowval, pinv, P);
-  etree(N, P, parent);
+  bool ident = true;  // the ordering is already a postorder (e.g. natural order of a QP's K2): no relabel
+  for (int k = 0; k < N && ident; ++k) ident = post[k] == k;
+  if (!ident) {
+    perm.swap(perm2);
+    for (int k = 0; k < N; ++k) pinv[perm[k]] = k;
+    build_pattern(N, colptr, rowval, pinv, P);
+    etree(N, P, parent);
+  }
   std::vector<int64_t> cnt;
   column_counts(N, P, parent, cnt);
   S.perm = perm;
   S.pinv = pinv;
   S.nnzL = std::accumulate(cnt.begin(), cnt.end(), (int64_t)0);
 
+  stamp("before 3");
   // ---------------- 3. fundamental supernodes
   std::vector<int32_t> nchild(N, 0);
   for (int j = 0; j < N; ++j)
@@ -262,6 +280,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     }
   }
 
+  stamp("before 3b");
   // ---------------- 3b. batched-leaf candidates: single-column etree leaves with a large update,
   // many under the same parent column (a QP with a diagonal Hessian and dense A: every x_j).  They
   // are kept out of relaxed amalgamation; step 6b decides the groups.
@@ -278,6 +297,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         lbcand[f.first] = 1;
   }
 
+  stamp("before 4");
   // ---------------- 4. relaxed amalgamation (merge a front with its column-adjacent child)
   std::vector<SN> sn;
   sn.reserve(fund.size());
@@ -332,6 +352,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       if (S.parent[s] != -1) S.child_list[fillc[S.parent[s]]++] = s;
   }
 
+  stamp("before 5");
   // ---------------- 5. frontal row structures
   S.row_ptr.assign(ns + 1, 0);
   S.nrows.resize(ns);
@@ -373,6 +394,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   S.rows.resize(S.row_ptr[ns]);
   for (int s = 0; s < ns; ++s) std::copy(R[s].begin(), R[s].end(), S.rows.begin() + S.row_ptr[s]);
 
+  stamp("before 6");
   // ---------------- 6. relative indices child -> parent
   S.rel_ptr.assign(ns + 1, 0);
   for (int s = 0; s < ns; ++s) {
@@ -395,6 +417,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     }
   }
 
+  stamp("before 6b");
   // ---------------- 6b. batched-leaf groups: per parent, its candidate children whose K column is one
   // CSC column of the caller (diagonal + rows below, none to its left) and whose rows cover at least
   // lb_min_density of the union of their rows
@@ -418,17 +441,16 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       if ((int)mem.size() < opt.lb_min_count) continue;
       // union of their parent-local rows
       std::vector<int32_t> U;
+      std::vector<uint8_t> inU(S.nrows[s], 0);  // parent-local rows hit by a member (marks: O(tot + r))
       int64_t tot = 0;
       for (int c : mem) {
         const int uc = S.nrows[c] - 1;
         tot += uc;
-        for (int a = 0; a < uc; ++a) {
-          const int pr = S.rel[S.rel_ptr[c] + a];
-          U.push_back(pr);
-        }
+        const int32_t* rl = S.rel.data() + S.rel_ptr[c];
+        for (int a = 0; a < uc; ++a) inU[rl[a]] = 1;
       }
-      std::sort(U.begin(), U.end());
-      U.erase(std::unique(U.begin(), U.end()), U.end());
+      for (int i = 0; i < S.nrows[s]; ++i)
+        if (inU[i]) U.push_back(i);
       const double dens = (double)tot / ((double)U.size() * (double)mem.size());
       if (dens < opt.lb_min_density) continue;
       SymbolicPlan::LBGroup g{};
@@ -467,6 +489,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   }
   auto lb_member = [&](int s) { return !S.lb_of.empty() && S.lb_of[s] >= 0; };
 
+  stamp("before 7");
   // ---------------- 7. assembly map: caller's CSC entry -> (front, local offset)
   // (entries of batched-leaf members are read by the W build instead)
   S.asm_ptr.assign(ns + 1, 0);
@@ -517,6 +540,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     }
   }
 
+  stamp("before 8");
   // ---------------- 8. level schedule (height in the supernodal tree)
   S.level.assign(ns, 0);
   int maxlev = 0;
@@ -536,6 +560,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     for (int s = 0; s < ns; ++s) S.level_list[fl[S.level[s]]++] = s;
   }
 
+  stamp("before 8b");
   // ---------------- 8b. subtree sharding (SURVEY §8 e).  cost(s) ~ factorisation flops + a per-front
   // latency term; sub(s) = cost of the subtree rooted at s.  Starting from the roots, the heaviest
   // splittable candidate subtree is moved to the "top" (its children become candidates) while the
@@ -620,6 +645,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     S.owner.clear();  // unsharded: every front belongs to the (only) shard
   }
 
+  stamp("before 9");
   // ---------------- 9. storage layout + statistics (top fronts last, contiguous, full F)
   S.l_off.resize(ns);
   S.u_off.resize(ns);
@@ -678,6 +704,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   S.arena_size = cur;
   S.uvec_size = ucur;
 
+  stamp("before 10");
   // ---------------- 10. assembly plan.  Each task is one 64x64 lower tile of a front's F: its entries
   // are the sums of their gather lists (original K entries first, then the small children's update
   // entries in child order), then the big children's update blocks are added child by child.  A
@@ -981,6 +1008,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     MADIPM_REQUIRE(S.g_src.size() < (size_t)INT32_MAX * 2 && S.atiles.size() < (size_t)INT32_MAX, "assembly plan too large");
   }
 
+  stamp("before 11");
   // ---------------- 11. forward-solve gather lists (child order).  Sharded: a top front's rows list
   // only its top children (sv); its subtree-root children of this shard are listed in sx (the
   // external forward contribution, exchanged before the top forward solve).
@@ -1041,6 +1069,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       }
     }
   }
+  stamp("11 (end)");
 }
 
 }  // namespace madipm

@@ -16,7 +16,9 @@ def __getattr__(name):
     if name in ("MPCSolver", "madipm", "solve", "AdaptiveStep", "ConservativeStep", "MehrotraAdaptiveStep",
                 "NoRegularization", "FixedRegularization", "AdaptiveRegularization", "Mehrotra",
                 "SparseKKTSystem", "ScaledSparseKKTSystem", "NormalKKTSystem", "ExecutionStats",
-                "SOLVE_SUCCEEDED", "STATUS_NAMES", "RCCLComm", "HostComm"):
+                "SOLVE_SUCCEEDED", "INFEASIBLE_PROBLEM_DETECTED", "MAXIMUM_ITERATIONS_EXCEEDED",
+                "MAXIMUM_WALLTIME_EXCEEDED", "DIVERGING_ITERATES", "ERROR_IN_STEP_COMPUTATION", "INTERNAL_ERROR",
+                "STATUS_NAMES", "RCCLComm", "HostComm"):
         from . import solver
         return getattr(solver, name)
     if name == "HIPLDLSolver":

@@ -80,6 +80,12 @@ STATUS_NAMES = {
     -4: "ERROR_IN_STEP_COMPUTATION", -5: "INTERNAL_ERROR",
 }
 SOLVE_SUCCEEDED = 1
+INFEASIBLE_PROBLEM_DETECTED = 2
+MAXIMUM_ITERATIONS_EXCEEDED = -1
+MAXIMUM_WALLTIME_EXCEEDED = -2
+DIVERGING_ITERATES = -3
+ERROR_IN_STEP_COMPUTATION = -4
+INTERNAL_ERROR = -5
 
 
 class Options(C.Structure):
@@ -235,7 +241,10 @@ def load_options(**kw) -> Options:
     """load_options (src/utils.jl:121-148): IPM options + linear-solver options."""
     unknown = set(kw) - _KNOWN
     if unknown:
-        raise TypeError(f"unknown options: {sorted(unknown)}")
+        # MadNLP.print_ignored_options (src/utils.jl:140-142): unsupported options are reported, not fatal
+        import sys
+        print("The following options are ignored: " + ", ".join(f"{k} = {kw[k]!r}" for k in sorted(unknown)),
+              file=sys.stderr)
     o = Options()
     L.lib.madipm_default_options(C.byref(o))
     for k in ("tol", "max_iter", "max_wall_time", "divergence_tol", "bound_push", "bound_fac",
@@ -354,13 +363,23 @@ class MPCSolver:
     def solve(self) -> ExecutionStats:
         """solve!(solver) (src/solver.jl:362-418)."""
         st = Stats()
-        L.check(L.lib.madipm_solver_solve(self.h, C.byref(st)), "solve!")
+        rc = L.lib.madipm_solver_solve(self.h, C.byref(st))
+        if rc < 0:
+            # solve!'s catch-all (src/solver.jl:398-403): INTERNAL_ERROR, rethrown only with rethrow_error
+            if self.rethrow_error:
+                L.check(rc, "solve!")
+            st.status = INTERNAL_ERROR
+            st.iter = len(self.trace()) - 1 if self.trace() else 0
         nx, m = self.qp.nvar, self.qp.ncon
         x, zl, zu = np.empty(nx), np.empty(nx), np.empty(nx)
         y, cons = np.empty(m), np.empty(m)
-        L.check(L.lib.madipm_solver_get_solution(self.h, L.ptr(x, C.c_double), L.ptr(y, C.c_double),
-                                                 L.ptr(zl, C.c_double), L.ptr(zu, C.c_double),
-                                                 L.ptr(cons, C.c_double)), "get_solution")
+        rs = L.lib.madipm_solver_get_solution(self.h, L.ptr(x, C.c_double), L.ptr(y, C.c_double),
+                                              L.ptr(zl, C.c_double), L.ptr(zu, C.c_double), L.ptr(cons, C.c_double))
+        if rs < 0:
+            if rc >= 0:
+                L.check(rs, "get_solution")
+            for a in (x, y, zl, zu, cons):
+                a.fill(np.nan)
         return ExecutionStats(status=st.status, iter=st.iter, objective=st.objective,
                               dual_objective=st.dual_objective, solution=x, constraints=cons,
                               multipliers=y, multipliers_L=zl, multipliers_U=zu, primal_feas=st.inf_pr,

@@ -72,6 +72,8 @@ class OracleLDL:
         return r
 
     def solve(self, b):
+        if not getattr(self, "ok", False):
+            raise FloatingPointError("OracleLDL.solve: the factorization stopped at a zero pivot")
         x = np.ascontiguousarray(b, np.float64).copy()
         lib().ldl_ref_solve(self.h, x.ctypes.data)
         return x

@@ -92,6 +92,7 @@ class OracleMPC:
         self.opt = opt or OracleOptions()
         self.qp = qp
         self.record_trace = record_trace
+        self.residuals = []          # residual ratio of every solve_system! call (diagnostics)
         nx = int(len(qp.c))
         m = int(len(qp.lcon))
         lvar = np.asarray(qp.lvar, float)
@@ -337,7 +338,15 @@ class OracleMPC:
                 dg = dg + zl * dist_u + zu * dist_l
                 K.setdiag(np.concatenate([dg, self.du_diag]))
                 K = K.tocsc()
-        if getattr(self, "linear_solver", "superlu") == "ldl":
+        if getattr(self, "linear_solver", "superlu") == "pardiso":
+            # CPU baseline (oracle/pardiso.py): MKL PARDISO, pattern analysed once per solver
+            from .pardiso import PardisoLDL
+            F = getattr(self, "_pardiso", None)
+            if F is None or not F.same_pattern(K):
+                F = self._pardiso = PardisoLDL(K, getattr(self, "ldl_perm", None))
+            self._factorized = F.factorize(K)
+            self._lu = F
+        elif getattr(self, "linear_solver", "superlu") == "ldl":
             # oracle/ldl_ref.c: LDLFactorizations' up-looking LDL^T (static pivots) in the order
             # `ldl_perm` (default: SuperLU's minimum degree on A+A^T)
             from .ldl import OracleLDL
@@ -345,6 +354,12 @@ class OracleMPC:
                 self.ldl_perm = np.argsort(spla.splu(K, permc_spec="MMD_AT_PLUS_A").perm_c)
             F = OracleLDL(K, self.ldl_perm)
             self._factorized = F.factorize() == K.shape[0]
+            # the HIP library's `pivot_tol` option (madipm_ldl_opts): a pivot with |d| <= tol (or a
+            # non-finite one) also reports is_factorized == false; LDLFactorizations' own test is d == 0
+            tol = getattr(self, "pivot_tol", 0.0)
+            if self._factorized and tol > 0.0:
+                dg = F.diag()
+                self._factorized = bool(np.all(np.abs(dg) > tol) and np.all(np.isfinite(dg)))
             self._lu = F
         else:
             try:
@@ -408,12 +423,17 @@ class OracleMPC:
 
     def solve_system(self, p):
         """solve_system! src/linear_solver.jl:19-44 (copy, solve, residual check)."""
+        if not getattr(self, "_factorized", True):
+            # every trial of factorize_regularized_system! failed: LDLFactorizations' ldiv! refuses an
+            # unfactorized object [EXT]; the HIP library reports it as a step-computation failure
+            raise FloatingPointError("solve with an unfactorized KKT system")
         d = self.kkt_solve(p.copy())
         w = self.kkt_mul(d, -1.0, 1.0, p.copy())
         norm_w = np.max(np.abs(w)) if len(w) else 0.0
         norm_p = np.max(np.abs(p)) if len(p) else 0.0
         ratio = norm_w / max(1.0, norm_p)
         self.last_residual = ratio
+        self.residuals.append(ratio)
         if math.isnan(ratio) or (self.opt.check_residual and ratio > self.opt.tol_linear_solve):
             raise FloatingPointError("SolveException")
         return d

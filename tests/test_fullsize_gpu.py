@@ -1,0 +1,112 @@
+"""Parity at the BENCHMARKED sizes (BASELINE.json configs[1], [2], [3]).
+
+* ex10 and supportcase10 stand-ins at full size, exactly as bench.py builds and solves them
+  (presolve_qp -> scale_qp -> standard_form_qp; FixedRegularization(1e-8, -1e-8), AdaptiveStep(0.99),
+  tol 1e-8): the GPU solve vs the oracle (oracle/mpc.py) driven by MKL PARDISO in the GPU's pivot
+  order.  Status equal, iterations within 1, objective within 1e-6 max(1, |obj|) (BASELINE.md rule).
+* the dense convex QP n = 50,000, m = 10,000 (nnz(L) = 5.5e8: beyond any oracle): size-independent
+  properties of the returned point, computed on the host from the unscaled solution —
+  primal feasibility, dual feasibility (stationarity), complementarity, bounds, and the duality gap
+  between the primal objective and the Lagrangian dual bound built from (y, zl, zu).
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu_solve(qp, **extra):
+    import bench
+    from madipm_amd import MPCSolver
+    s = MPCSolver(qp, **bench.solver_opts(), **extra)
+    return s, s.solve()
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("config", ["ex10", "supportcase10"])
+def test_fullsize_vs_oracle(config):
+    import bench
+    from oracle.mpc import OracleMPC, OracleOptions
+    from oracle import pardiso
+    qp, _ = bench.build_problem(config)
+    s, gpu = _gpu_solve(qp)
+    assert gpu.status_name == "SOLVE_SUCCEEDED", gpu.status_name
+    pardiso.set_threads(bench.baseline_threads())
+    o = OracleMPC(qp, OracleOptions(regularization=("fixed", 1e-8, -1e-8), step_rule=("adaptive", 0.99),
+                                    max_iter=300, tol=1e-8), record_trace=False)
+    o.linear_solver = "pardiso"
+    o.ldl_perm = s.kkt_perm()
+    ref = o.solve()
+    print(f"{config}: gpu {gpu.status_name} {gpu.iter} it obj {gpu.objective!r}; "
+          f"oracle {ref.status} {ref.iter} it obj {ref.objective!r}")
+    assert ref.status == gpu.status
+    assert abs(gpu.iter - ref.iter) <= 1, (gpu.iter, ref.iter)
+    assert abs(gpu.objective - ref.objective) <= 1e-6 * max(1.0, abs(ref.objective)), (gpu.objective, ref.objective)
+    # the returned primal points agree to the IPM's tolerance (both are 1e-8-optimal vertices/faces)
+    dx = np.max(np.abs(gpu.solution - ref.solution)) / max(1.0, np.max(np.abs(ref.solution)))
+    assert dx <= 1e-4, dx
+
+
+def _kkt_properties(qp, st):
+    """Optimality measures of (x, y, zl, zu) for min c'x + x'Hx/2, Ax = b, l <= x <= u (unscaled),
+    with MadNLP's sign convention: stationarity c + Hx + A'y - zl + zu = 0 (src/kernels.jl:408-430
+    dual objective uses -y'b + zl'l - zu'u - x'Hx/2)."""
+    import scipy.sparse as sp
+    n, m = qp.nvar, qp.ncon
+    A = sp.csr_matrix((qp.Avals, (qp.Arows, qp.Acols)), shape=(m, n))
+    x, y, zl, zu = st.solution, st.multipliers, st.multipliers_L, st.multipliers_U
+    hx = np.zeros(n)
+    np.add.at(hx, qp.Hrows, qp.Hvals * x[qp.Hcols])
+    off = qp.Hrows != qp.Hcols
+    np.add.at(hx, qp.Hcols[off], qp.Hvals[off] * x[qp.Hrows[off]])
+    b = qp.lcon
+    pr = np.max(np.abs(A @ x - b)) / (1.0 + np.max(np.abs(b)))
+    g = qp.c + hx
+    du = np.max(np.abs(g + A.T @ y - zl + zu)) / (1.0 + np.max(np.abs(qp.c)))
+    lo, hi = np.isfinite(qp.lvar), np.isfinite(qp.uvar)
+    compl = max(np.max(np.abs((x - qp.lvar)[lo] * zl[lo]), initial=0.0),
+                np.max(np.abs((qp.uvar - x)[hi] * zu[hi]), initial=0.0))
+    pobj = qp.c0 + qp.c @ x + 0.5 * x @ hx
+    dobj = qp.c0 - y @ b + zl[lo] @ qp.lvar[lo] - zu[hi] @ qp.uvar[hi] - 0.5 * x @ hx
+    return dict(pr=pr, du=du, compl=compl, pobj=pobj, dobj=dobj,
+                bounds=max(np.max((qp.lvar - x)[lo], initial=-1.0), np.max((x - qp.uvar)[hi], initial=-1.0)),
+                zmin=min(np.min(zl[lo], initial=0.0), np.min(zu[hi], initial=0.0)))
+
+
+def test_kkt_properties_small_dense_qp_vs_oracle():
+    """The property check itself, pinned on a small dense QP where the oracle also runs."""
+    from madipm_amd import instances as I
+    from oracle.mpc import OracleMPC, OracleOptions
+    qp = I.dense_qp(n=600, m=120, seed=0)
+    s, gpu = _gpu_solve(qp, ordering=0)
+    ref = OracleMPC(qp, OracleOptions(regularization=("fixed", 1e-8, -1e-8), tol=1e-8, max_iter=300)).solve()
+    assert gpu.status_name == "SOLVE_SUCCEEDED" and ref.status == 1
+    assert abs(gpu.objective - ref.objective) <= 1e-6 * max(1.0, abs(ref.objective))
+    p = _kkt_properties(qp, gpu)
+    q = _kkt_properties(qp, ref)
+    for k in ("pr", "du"):
+        assert p[k] <= 1e-6 and q[k] <= 1e-6, (k, p[k], q[k])
+    assert abs(p["pobj"] - p["dobj"]) <= 1e-6 * max(1.0, abs(p["pobj"])), p
+    assert abs(p["pobj"] - gpu.objective) <= 1e-9 * max(1.0, abs(p["pobj"]))
+
+
+@pytest.mark.timeout(1200)
+def test_dense_qp_fullsize_properties():
+    """configs[2] at full size (n = 50,000, m = 10,000; 5e8 entries in A): no oracle can factor it, so
+    the answer is checked by the optimality conditions it must satisfy."""
+    from madipm_amd import instances as I
+    qp = I.dense_qp(n=50_000, m=10_000, seed=0)
+    s, gpu = _gpu_solve(qp, ordering=0)
+    assert gpu.status_name == "SOLVE_SUCCEEDED", gpu.status_name
+    info = s.ldl_info()
+    assert info["lb_members"] == 50_000 and info["nnzL"] >= 5e8
+    p = _kkt_properties(qp, gpu)
+    print("dense QP 50k x 10k:", {k: float(v) for k, v in p.items()}, "iters", gpu.iter)
+    assert p["pr"] <= 1e-6 and p["du"] <= 1e-6, p
+    assert p["bounds"] <= 1e-8 and p["zmin"] >= -1e-10, p
+    # weak duality + a tiny gap: the objective is optimal to the IPM tolerance
+    assert p["pobj"] - p["dobj"] >= -1e-6 * max(1.0, abs(p["pobj"]))
+    assert abs(p["pobj"] - p["dobj"]) <= 1e-6 * max(1.0, abs(p["pobj"])), p
+    assert abs(p["pobj"] - gpu.objective) <= 1e-8 * max(1.0, abs(p["pobj"]))

@@ -146,8 +146,8 @@ def test_options_parsing():
         (300, 1, 1e-8, -1e-8, 2, 0.9, 1e-7)
     d = load_options()
     assert (d.tol, d.max_iter, d.mu_init, d.mu_min, d.bound_push, d.delta_p) == (1e-8, 3000, 0.1, 1e-12, 1e-2, 1e-10)
-    with pytest.raises(TypeError):
-        load_options(not_an_option=1)
+    # unknown options are printed as ignored (MadNLP.print_ignored_options, src/utils.jl:140-142)
+    assert load_options(not_an_option=1).max_iter == 3000
     assert [load_options(kkt_system=k).kkt_system for k in (SparseKKTSystem, ScaledSparseKKTSystem, NormalKKTSystem)] \
         == [0, 1, 2]
     with pytest.raises(TypeError):

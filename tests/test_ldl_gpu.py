@@ -179,15 +179,16 @@ def _dense_k2(m, n, seed, delta=1e-2):
     return K, Lw
 
 
-@pytest.mark.parametrize("m,n,ordering", [(150, 1000, 0), (200, 3000, 0), (150, 1000, 1)])
-def test_batched_leaf_columns_parity(m, n, ordering):
+@pytest.mark.parametrize("m,n,ordering,sfm", [(150, 1000, 0, 128), (200, 3000, 0, 128), (150, 1000, 1, 128),
+                                               (128, 1000, 0, 128), (150, 1000, 0, 192), (100, 800, 0, 128)])
+def test_batched_leaf_columns_parity(m, n, ordering, sfm):
     """K2 of a QP with diagonal H and dense A: the x_j are single-column leaves with m-row updates,
     eliminated as ONE group (W build + MFMA SYRK into the y front + GEMV solves).  Well conditioned:
     pivots and solution vs the oracle LDL^T in the same order to 1e-12 (relative)."""
     from madipm_amd.linear_solver import HIPLDLSolver
     K, Lw = _dense_k2(m, n, 3)
     N = K.shape[0]
-    ls = HIPLDLSolver(N, Lw.indptr, Lw.indices, ordering=ordering)
+    ls = HIPLDLSolver(N, Lw.indptr, Lw.indices, ordering=ordering, small_front_max=sfm)
     info = ls.info()
     assert info["lb_groups"] >= 1 and info["lb_members"] >= n // 2
     dev = torch.device("cuda:0")

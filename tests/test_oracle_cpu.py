@@ -150,3 +150,45 @@ def test_oracle_k25_qp_agrees():
     ref = OracleMPC(qp, OracleOptions(max_iter=300)).solve()
     st = OracleMPC(qp, OracleOptions(max_iter=300, kkt_system="K25")).solve()
     _cmp_sol(st, ref, ytol=1e-5)
+
+
+@pytest.mark.skipif(not __import__("oracle.pardiso", fromlist=["available"]).available(), reason="MKL absent")
+def test_oracle_pardiso_linear_solver_matches_superlu():
+    """bench.py's CPU baseline (oracle MPC + MKL PARDISO) reaches the same answer as the oracle's
+    default SuperLU solve: AFIRO's netlib optimum and the same iteration count; and the failure-path
+    semantics (pivot_tol, unfactorized solve) hold for the LDL^T oracle."""
+    from madipm_amd import read_mps, standard_form_qp
+    from oracle import pardiso
+    qp = standard_form_qp(read_mps(os.path.join(os.path.dirname(__file__), "golden", "afiro.mps")))
+    pardiso.set_threads(2)
+    a = OracleMPC(qp, OracleOptions(regularization=("fixed", 1e-8, -1e-8)))
+    a.linear_solver = "pardiso"
+    sa = a.solve()
+    sb = OracleMPC(qp, OracleOptions(regularization=("fixed", 1e-8, -1e-8))).solve()
+    assert sa.status == sb.status == SOLVE_SUCCEEDED and sa.iter == sb.iter
+    assert abs(sa.objective + 464.7531428571) <= 1e-7 * 464.75
+    assert a._pardiso.nperturbed == 0 and a._pardiso.nfactor == sa.iter + 1
+
+
+def test_oracle_failed_factorization_is_step_error():
+    """Every trial of factorize_regularized_system! failing (del_w = 0 on a free LP column) makes the
+    next solve a step-computation error (oracle semantics the GPU tests compare against)."""
+    from madipm_amd.qp import QuadraticModel
+    from oracle.mpc import ERROR_IN_STEP_COMPUTATION
+    inf = np.inf
+    qp = QuadraticModel(c=np.array([1.0, 1.0, 0.0]), Hrows=[], Hcols=[], Hvals=[], Arows=[0, 0, 1, 1, 1],
+                        Acols=[0, 1, 0, 1, 2], Avals=[1.0, 1.0, 1.0, -1.0, 1.0], lcon=[1.0, 0.0], ucon=[1.0, 0.0],
+                        lvar=[0.0, 0.0, -inf], uvar=[inf, inf, inf])
+    o = OracleMPC(qp, OracleOptions(regularization=("fixed", 0.0, -1e-8)))
+    o.linear_solver = "ldl"
+    o.ldl_perm = np.array([2, 4, 3, 1, 0])
+    st = o.solve()
+    assert st.status == ERROR_IN_STEP_COMPUTATION and st.iter == 0 and len(st.trace) == 1
+    # pivot_tol: del_w = 1e-12 and 1e-10 rejected, 1e-8 accepted -> the retry path converges
+    o = OracleMPC(qp, OracleOptions(regularization=("fixed", 1e-12, -1e-8)))
+    o.linear_solver = "ldl"
+    o.ldl_perm = np.array([2, 4, 3, 1, 0])
+    o.pivot_tol = 1e-9
+    st = o.solve()
+    assert st.status == SOLVE_SUCCEEDED and abs(st.objective - 1.0) <= 1e-7
+    assert all(abs(t["del_w"] - 1e-8) <= 1e-20 for t in st.trace[1:])
