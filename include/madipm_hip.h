@@ -161,6 +161,78 @@ int madipm_ldl_set_timing(madipm_ldl_t ls, uint32_t mask);
 /* synchronises the recorded events; out[MADIPM_NKERNELS] */
 int madipm_ldl_kernel_stats(madipm_ldl_t ls, madipm_kstat* out);
 
+/* ------------------------------------------------------------------ array-type overrides
+ * The ROCArray counterparts of the methods MadIPM's CUDA extension overrides so that MPCSolver
+ * runs on device arrays (ext/MadIPMCUDAExt/cuda_wrapper.jl, MadIPMCUDAExt.jl).  Device pointers,
+ * 0-based, int32 indices as the reference's CuSparseMatrix{Float64,Int32}; every sum has a fixed
+ * order (bitwise reproducible), and transfer / assemble_normal_system follow the reference CPU
+ * loops' order and rounding exactly.  Asynchronous on `stream` unless stated. */
+
+/* MadNLP.transfer!(dest::CSC, src::COO, map) (cuda_wrapper.jl:4-24, used by build_kkt!/
+ * compress_hessian! :26-30): dest .= 0; dest[map[k]] += src[k] for k = 0..nsrc-1, sources of one
+ * entry summed in ascending k.  The plan is built once from the map (host or device pointer). */
+typedef struct madipm_transfer* madipm_transfer_t;
+int madipm_transfer_create(int64_t nsrc, const int64_t* map, int32_t map_on_device, int64_t ndest,
+                           madipm_transfer_t* out);
+int madipm_transfer(madipm_transfer_t t, double* d_dest, const double* d_src, madipm_stream_t stream);
+void madipm_transfer_destroy(madipm_transfer_t t);
+
+/* compress_jacobian!(::NormalKKTSystem) (normalkkt.jl:163-172, cuda_wrapper.jl:32-41):
+ * AV[nnz-n_slack .. nnz-1] = -1 (in place), then ATnz[i] = AV[csr_map[i]] for i < nnz. */
+int madipm_compress_jacobian(double* d_AV, int64_t nnz, int32_t n_slack, const int64_t* d_csr_map,
+                             double* d_ATnz, madipm_stream_t stream);
+
+/* MadIPMOperator(A::CuSparseMatrixCSR; transa, symmetric) (cuda_wrapper.jl:43-83) and its mul!
+ * (:85-94).  A is m x n CSR (rowptr m+1, colval/nzval nnz; device).  symmetric != 0 (and nnz > 0):
+ * the operator is mat = tril(A,-1) + A', copied at creation like the reference's `mat`;
+ * otherwise the caller's arrays are read live at every apply ('T' through a transposed index plan
+ * built at creation).  apply: y = alpha op(A) x + beta y (y is not read when beta == 0); y has
+ * m rows for 'N' / symmetric, n for 'T'.  size reports size(A) and nnz(A) (Base.size, nnz). */
+typedef struct madipm_spmv* madipm_spmv_t;
+int madipm_spmv_create(int32_t m, int32_t n, int64_t nnz, const int32_t* d_rowptr, const int32_t* d_colval,
+                       const double* d_nzval, char transa, int32_t symmetric, madipm_spmv_t* out);
+int madipm_spmv_apply(madipm_spmv_t op, const double* d_x, double* d_y, double alpha, double beta,
+                      madipm_stream_t stream);
+int madipm_spmv_size(madipm_spmv_t op, int32_t* m, int32_t* n, int64_t* nnz);
+void madipm_spmv_destroy(madipm_spmv_t op);
+
+/* MadIPM.coo_to_csr(n_rows, n_cols, Ai, Aj, Ax) (src/utils.jl:158-201; GPU cuda_wrapper.jl:96-106),
+ * device arrays, 0-based.  Entries are grouped by row in input order (utils.jl's counting sort);
+ * sort_cols != 0 orders each row by column (ties in input order), the layout cuSPARSE produces.
+ * Duplicates are kept, as in the reference.  rowptr: n_rows+1.  Synchronises `stream`. */
+int madipm_coo_to_csr(int32_t n_rows, int32_t n_cols, int64_t nnz, const int32_t* d_Ai, const int32_t* d_Aj,
+                      const double* d_Ax, int32_t* d_rowptr, int32_t* d_colval, double* d_nzval,
+                      int32_t sort_cols, madipm_stream_t stream);
+
+/* MadIPM.build_normal_system(n_rows, n_cols, Jtp, Jtj) (src/utils.jl:209-274; the GPU path runs it
+ * on host copies too, normalkkt.jl:104): HOST arrays.  Pattern of tril(J J') for J in CSR:
+ * column i of the lower CSC (Cp[n_rows+1], Cj) lists the rows j >= i sharing a column with row i,
+ * ascending.  *nnz_out always receives the count; Cj (capacity cap) is filled when it is large
+ * enough (-4 otherwise); pass Cj = NULL to size it. */
+int madipm_build_normal_system(int32_t n_rows, int32_t n_cols, const int32_t* Jtp, const int32_t* Jtj,
+                               int32_t* Cp, int32_t* Cj, int64_t cap, int64_t* nnz_out);
+
+/* MadIPM.assemble_normal_system!(n_rows, n_cols, Jtp, Jtj, Jtx, Cp, Cj, Cx, Dx) (src/utils.jl:
+ * 276-308; GPU cuda_wrapper.jl:108-156): Cx[c] = sum_k (Jx[i,k] Dx[k]) Jx[j,k] for entry c = (j,
+ * column i), merge-joined over each row's ascending column indices (the GPU reference's
+ * precondition, which coo_to_csr with sort_cols provides).  Device arrays. */
+int madipm_assemble_normal_system(int32_t n_rows, int32_t n_cols, const int32_t* d_Jtp, const int32_t* d_Jtj,
+                                  const double* d_Jtx, const int32_t* d_Cp, const int32_t* d_Cj, double* d_Cx,
+                                  const double* d_Dx, madipm_stream_t stream);
+
+/* fill_structure!(A::CSR, rows, cols) (MadIPMCUDAExt.jl:15-32; hess_structure!/jac_lin_structure!):
+ * rows[c] = i, cols[c] = colval[c] for the entries c of row i. */
+int madipm_csr_fill_structure(int32_t n_rows, const int32_t* d_Ap, const int32_t* d_Aj, int32_t* d_rows,
+                              int32_t* d_cols, madipm_stream_t stream);
+
+/* NLPModels.obj(qp, x) (MadIPMCUDAExt.jl:34-38): v = H x; obj = c0 + c'x + v'x/2 written to
+ * d_work[512] (d_work: 513 doubles of scratch) and, when h_obj != NULL, to *h_obj (synchronises).
+ * NLPModels.grad!(qp, x, g) (:40-45): g = H x + c.  H: a symmetric madipm_spmv_t of size n. */
+int madipm_qp_obj(madipm_spmv_t H, const double* d_c, double c0, const double* d_x, double* d_v, int32_t n,
+                  double* d_work, double* h_obj, madipm_stream_t stream);
+int madipm_qp_grad(madipm_spmv_t H, const double* d_c, const double* d_x, double* d_g, int32_t n,
+                   madipm_stream_t stream);
+
 /* ------------------------------------------------------------------ native MPC solver
  * `MPCSolver(qp; kwargs...)` + `solve!(solver)` (src/structure.jl:79-178, src/solver.jl:362-418)
  * for a QuadraticModel with SparseKKTSystem (K2), run entirely on the GPU with the LDL^T above.

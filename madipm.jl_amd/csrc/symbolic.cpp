@@ -178,12 +178,39 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   S.nnzK = nnz;
   MADIPM_REQUIRE(colptr[0] == 0, "colptr[0] must be 0");
   std::vector<int64_t> diagcount(N, 0);
+  // Either triangle is accepted (LDLFactorizations takes the upper one, MadNLP's aug_com the lower
+  // one), even mixed, as long as every off-diagonal pair {i, j} is stored in one triangle only:
+  // the factorisation maps each entry to its symmetric position, so a full symmetric matrix would
+  // be counted twice and is rejected.
+  bool has_upper = false;
   for (int j = 0; j < N; ++j) {
     MADIPM_REQUIRE(colptr[j + 1] >= colptr[j], "colptr not monotone");
     for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p) {
       int i = rowval[p];
-      MADIPM_REQUIRE(i >= j && i < N, "entries must be in the lower triangle (row >= col) and in range");
+      MADIPM_REQUIRE(i >= 0 && i < N, "row index out of range");
       if (i == j) diagcount[j]++;
+      if (i < j) has_upper = true;
+    }
+  }
+  if (has_upper) {
+    // pairs stored above the diagonal must not also be stored below it
+    std::vector<int64_t> up_ptr(N + 1, 0);
+    for (int j = 0; j < N; ++j)
+      for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p)
+        if (rowval[p] < j) up_ptr[rowval[p] + 1]++;  // (i, j), i < j  ->  bucket i, value j
+    for (int i = 0; i < N; ++i) up_ptr[i + 1] += up_ptr[i];
+    std::vector<int32_t> up(up_ptr[N]);
+    std::vector<int64_t> fillu(up_ptr.begin(), up_ptr.end() - 1);
+    for (int j = 0; j < N; ++j)
+      for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p)
+        if (rowval[p] < j) up[fillu[rowval[p]]++] = j;
+    std::vector<int32_t> mark(N, -1);
+    for (int j = 0; j < N; ++j) {  // column j's lower entries (i, j), i > j, vs the upper (j, i)
+      for (int64_t q = up_ptr[j]; q < up_ptr[j + 1]; ++q) mark[up[q]] = j;
+      for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p)
+        MADIPM_REQUIRE(!(rowval[p] > j && mark[rowval[p]] == j),
+                       "entry (" + std::to_string(rowval[p]) + "," + std::to_string(j) +
+                           ") is stored in both triangles: pass one triangle of the symmetric matrix");
     }
   }
   if (N == 0) return;
@@ -285,7 +312,8 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   // many under the same parent column (a QP with a diagonal Hessian and dense A: every x_j).  They
   // are kept out of relaxed amalgamation; step 6b decides the groups.
   std::vector<uint8_t> lbcand(N, 0);
-  const bool use_lb = opt.leaf_batch && opt.nshards <= 1;
+  // batched leaves read their K column as one contiguous CSC run (diagonal + rows below): lower only
+  const bool use_lb = opt.leaf_batch && opt.nshards <= 1 && !has_upper;
   if (use_lb) {
     std::vector<int32_t> npar(N, 0);
     for (const SN& f : fund)
@@ -533,7 +561,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       for (int64_t q = S.asm_ptr[s]; q < S.asm_ptr[s + 1]; ++q) d.emplace_back(S.asm_dst[q], S.asm_src[q]);
       std::sort(d.begin(), d.end());
       for (size_t t = 0; t < d.size(); ++t) {
-        MADIPM_REQUIRE(t == 0 || d[t].first != d[t - 1].first, "duplicate entries in the lower CSC input");
+        MADIPM_REQUIRE(t == 0 || d[t].first != d[t - 1].first, "duplicate entries in the CSC input (a pair {i, j} stored twice)");
         S.asm_dst[S.asm_ptr[s] + t] = d[t].first;
         S.asm_src[S.asm_ptr[s] + t] = d[t].second;
       }

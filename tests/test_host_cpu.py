@@ -40,11 +40,19 @@ def test_library_reports_errors_without_gpu():
                                       ctypes.byref(o), None, ctypes.byref(h))
     assert rc == 0
     _lib.madipm_symbolic_destroy(h)
-    bad = np.array([0, 1, 2], np.int32)
-    rowval2 = np.array([0, 0], np.int32)        # (0,1) is upper triangle -> rejected
-    rc = _lib.madipm_symbolic_analyze(2, _lib.ptr(np.array([0, 1, 2], np.int64), ctypes.c_int64),
+    rowval2 = np.array([0, 0, 1], np.int32)     # upper triangle (0,0), (0,1), (1,1): accepted
+    rc = _lib.madipm_symbolic_analyze(2, _lib.ptr(np.array([0, 1, 3], np.int64), ctypes.c_int64),
                                       _lib.ptr(rowval2, ctypes.c_int32), ctypes.byref(o), None, ctypes.byref(h))
-    assert rc < 0 and b"lower triangle" in _lib.madipm_last_error()
+    assert rc == 0
+    _lib.madipm_symbolic_destroy(h)
+    rowval3 = np.array([0, 1, 0, 1], np.int32)  # full symmetric: (1,0) and (0,1) -> rejected
+    rc = _lib.madipm_symbolic_analyze(2, _lib.ptr(np.array([0, 2, 4], np.int64), ctypes.c_int64),
+                                      _lib.ptr(rowval3, ctypes.c_int32), ctypes.byref(o), None, ctypes.byref(h))
+    assert rc < 0 and b"both triangles" in _lib.madipm_last_error()
+    rowval4 = np.array([0, 5], np.int32)        # out of range
+    rc = _lib.madipm_symbolic_analyze(2, _lib.ptr(np.array([0, 1, 2], np.int64), ctypes.c_int64),
+                                      _lib.ptr(rowval4, ctypes.c_int32), ctypes.byref(o), None, ctypes.byref(h))
+    assert rc < 0 and b"out of range" in _lib.madipm_last_error()
 
 
 def _brute_nnzL(K, perm):

@@ -190,7 +190,10 @@ def test_batched_leaf_columns_parity(m, n, ordering, sfm):
     N = K.shape[0]
     ls = HIPLDLSolver(N, Lw.indptr, Lw.indices, ordering=ordering, small_front_max=sfm)
     info = ls.info()
-    assert info["lb_groups"] >= 1 and info["lb_members"] >= n // 2
+    if m >= 128:  # lb_min_rows (symbolic.hpp): shorter update columns are factorised one by one
+        assert info["lb_groups"] >= 1 and info["lb_members"] >= n // 2
+    else:
+        assert info["lb_groups"] == 0
     dev = torch.device("cuda:0")
     assert ls.factorize(torch.from_numpy(Lw.data.copy()).to(dev)) == 0
     ref = OracleLDL(K, ls.perm())
