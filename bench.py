@@ -200,6 +200,22 @@ def roofline(stats: list, dominant: str):
             "avg_launch_us": avg_s * 1e6, "alg_bytes_per_launch": nbytes, "alg_flops_per_launch": flops}
 
 
+def iteration_roofline(info: dict, ms_per_step: float, vec_passes: int = 60) -> dict:
+    """Whole-iteration roofline from SURVEY 8(d)'s per-phase algorithmic counts: factorisation
+    B = 8 nnzL + 12 nnzK, F = the analysis' flop count; 2 solves B = 2 x 16 nnzL, F = 2 x 4 nnzL;
+    2 residual SpMVs B = 2 x (12 nnzK + 16 N); vector kernels B ~ vec_passes x 8 N (an estimate of
+    the ~60 length-N vector reads/writes of the RHS / step / barrier / evaluation kernels).  Each
+    phase is bounded by max(B / 8 TB/s, F / 78.6 TF/s); frac = sum of the bounds / measured step."""
+    nnzL, nnzK, N, F = float(info["nnzL"]), float(info["nnzK"]), float(info["n"]), float(info["flops"])
+    phases = {"factorization": (8 * nnzL + 12 * nnzK, F), "solves": (32 * nnzL, 8 * nnzL),
+              "residuals": (2 * (12 * nnzK + 16 * N), 4 * nnzK), "vector_kernels": (vec_passes * 8 * N, 0.0)}
+    bound = {k: max(b / (PEAK_HBM_GBS * 1e9), f / (PEAK_F64_TFS * 1e12)) * 1e6 for k, (b, f) in phases.items()}
+    t_roof = sum(bound.values())
+    return {"alg_bytes": sum(b for b, _ in phases.values()), "alg_flops": sum(f for _, f in phases.values()),
+            "bound_us": {k: round(v, 2) for k, v in bound.items()}, "time_at_roofline_us": t_roof,
+            "measured_us": ms_per_step * 1e3, "frac": t_roof / (ms_per_step * 1e3)}
+
+
 def aggregate(dt, iters, dist, sharded):
     """Whole-job numbers: max time over ranks; iterations = those of the one sharded solve, or the
     sum over ranks (replicas)."""
@@ -317,6 +333,7 @@ def main():
                        "leaf_batch_members": info["lb_members"],
                        "parallelism": (f"subtree-shard{world}" if sharded else f"replicas{world}"), **opt},
             "roofline": roof,
+            "iteration_roofline": iteration_roofline(info, 1e3 * dt / max(iters, 1)),
             "kernel_ms_warmup": breakdown,
             "cpu_baseline": None,
             "parity": None,

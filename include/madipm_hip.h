@@ -57,6 +57,8 @@ typedef struct madipm_ldl_info {
   int64_t arena_bytes;     /* device bytes for factor + update blocks */
   int32_t lb_groups;       /* batched leaf-column groups (each absorbed by one SYRK into its parent) */
   int32_t lb_members;      /* single-column leaf fronts in those groups */
+  int32_t fold_fronts;     /* tree fronts that fold their micro leaves (LDS product lists) */
+  int32_t fold_leaves;     /* micro leaves folded by them */
 } madipm_ldl_info;
 
 void madipm_ldl_default_opts(madipm_ldl_opts* opts);

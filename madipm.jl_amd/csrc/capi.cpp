@@ -157,6 +157,9 @@ int madipm_symbolic_info(madipm_symbolic_t sym, madipm_ldl_info* info) {
   info->arena_bytes = p.arena_size * 8 + p.lb_wsize * 8;
   info->lb_groups = (int32_t)p.lb.size();
   info->lb_members = (int32_t)p.lb_mem.size();
+  info->fold_fronts = 0;
+  for (uint8_t a : p.absorb) info->fold_fronts += a;
+  info->fold_leaves = (int32_t)p.mc_list.size();
   return 0;
   MADIPM_API_END
 }
@@ -337,6 +340,9 @@ int madipm_ldl_get_info(madipm_ldl_t ls, madipm_ldl_info* info) {
   info->arena_bytes = p.arena_size * 8 + p.lb_wsize * 8;
   info->lb_groups = (int32_t)p.lb.size();
   info->lb_members = (int32_t)p.lb_mem.size();
+  info->fold_fronts = 0;
+  for (uint8_t a : p.absorb) info->fold_fronts += a;
+  info->fold_leaves = (int32_t)p.mc_list.size();
   return 0;
   MADIPM_API_END
 }
@@ -568,6 +574,9 @@ int madipm_solver_ldl_info(madipm_solver_t s, madipm_ldl_info* info) {
   info->arena_bytes = p.arena_size * 8 + p.lb_wsize * 8;
   info->lb_groups = (int32_t)p.lb.size();
   info->lb_members = (int32_t)p.lb_mem.size();
+  info->fold_fronts = 0;
+  for (uint8_t a : p.absorb) info->fold_fronts += a;
+  info->fold_leaves = (int32_t)p.mc_list.size();
   return 0;
   MADIPM_API_END
 }

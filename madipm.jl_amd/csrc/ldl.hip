@@ -1263,147 +1263,104 @@ __global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t*
   blocked_writeout<PK, false>(A, r, w, ld, Dl, arena + T.l_off[s], arena + T.u_off[s], T.u_ld[s], D, f0, st, tol);
 }
 
-// ------------------------------------------------------------------ leaf absorption
-// A tree front absorbs its micro-leaf children (leaves with w <= 2, r <= 32; SymbolicPlan::absorb).
-// Per batch of leaves (<= kAbsorbRows rows): (1) thread per leaf row gathers the row's entries of the
-// leaf's two columns from the caller's K values (flat index tables: one coalesced round trip + one
-// gather); (2) thread per leaf: pivots d0, l10, d1 (+ D, pivot check); (3) thread per leaf row: its L
-// entries (to the leaf's L panel in HBM, for the solves; kept in LDS); (4) the thread owning front
-// row i adds, for every absorbed update row a listed for row i (child order), U(a, b) =
-// -(l_a0 d0 l_b0 + l_a1 d1 l_b1) into F(i, rel(b)) for the leaf's update rows b <= a — each entry of
-// F has one writer and a fixed order, no atomics.  This replaces the leaves' U blocks in HBM, the
-// micro-factor launch for them, and the gather pass that summed the U blocks.
-// one absorbed update row a (batch-local) of leaf kk[a], owned by front row `row`:
-//  * light row: F(row, col(b)) -= U(a, b) for the leaf's update rows b <= a, and, for each heavy row
-//    a' > a of the leaf, F(row(a'), row) -= U(a', a) (the heavy row's light entries);
-//  * heavy row: only F(row, col(b)) for heavy rows b <= a (incl. the diagonal).
+// ------------------------------------------------------------------ leaf folding
+// A tree front folds its micro-leaf children (w <= 2, r <= 32; SymbolicPlan::absorb) into its LDS
+// front instead of k_micro_factor writing their update blocks to HBM and the gather pre-assembly
+// summing them.  Per batch of leaves: (1) thread per leaf row gathers the row's entries of the leaf's
+// two columns from the caller's K values; (2) thread per leaf: pivots d0, l10, d1; (3) thread per
+// leaf row: its l (and l d) in LDS; (4) the product list: thread t walks its chunk of destination-sorted products
+// F(i, j) -= l0(q1) l0(q2) d0 + l1(q1) l1(q2) d1, one partial sum per destination run, so every
+// entry of F has one writer and a fixed order (leaf order) — no atomics, balanced by product count
+// whatever the row density.
+// Latency: every phase is one or two global round trips at most (8 leaf rows per thread in flight;
+// product entries 16 per thread in flight, the next group's loads issued before the current group's
+// arithmetic, the first group before phase 1).
 template <bool PK>
-__device__ __forceinline__ void absorb_entry(double* A, int r, int ld, const double* l0, const double* l1,
-                                             const double* pd0, const double* pd1, const int32_t* rel,
-                                             const int32_t* kk, const int32_t* prow, const int32_t* hv,
-                                             const int32_t* pu0, const int32_t* pend, int a, int row, bool heavy) {
-  const int k = kk[a];
-  const double p0 = l0[a] * pd0[k], p1 = l1[a] * pd1[k];
-  // 8 columns at a time: operands and targets loaded before any store (the targets of one leaf are
-  // distinct, so the eight read-modify-writes of a chunk never alias)
-#pragma unroll 1
-  for (int b = pu0[k]; b <= a; b += 8) {
-    double x0[8], x1[8], av[8];
-    int cb[8];
-    bool on[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int bb = min(b + u, a);
-      x0[u] = l0[bb];
-      x1[u] = l1[bb];
-      cb[u] = rel[bb] + row;
-      on[u] = (b + u <= a) && (!heavy || hv[bb]);
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      av[u] = A[cb[u]];
-      LDL_PIN(av[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (on[u]) A[cb[u]] = av[u] - fma(p0, x0[u], p1 * x1[u]);
-  }
-  if (heavy) return;
-  const int cbase = fidx<PK>(0, row, r, ld);
-#pragma unroll 1
-  for (int a2 = a + 1; a2 < pend[k]; ++a2) {
-    if (!hv[a2]) continue;
-    const int t = cbase + prow[a2];  // F(row(a2), row), row(a2) > row
-    A[t] -= fma(l0[a2] * pd0[k], l0[a], l1[a2] * pd1[k] * l1[a]);
-  }
-}
-
-template <bool PK>
-__device__ __forceinline__ void absorb_leaves(const FrontTab& T, int s, int r, int ld, double* A, const double* Kx,
-                                              double* arena, double* D, LDLStatus* st, double tol, double* ext,
-                                              int64_t* dg) {
-  int64_t tph[4] = {0, 0, 0, 0};
-  int64_t tc = dg ? wall_clock64() : 0;
+__device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A, const double* Kx, double* arena,
+                                            double* D, LDLStatus* st, double tol, double* ext, int64_t* fdg) {
+  int64_t tph[4] = {0, 0, 0, 0}, tc = fdg ? wall_clock64() : 0;
   auto lap = [&](int k) {
-    if (dg) {
+    if (fdg) {
       const int64_t t2 = wall_clock64();
       tph[k] += t2 - tc;
       tc = t2;
     }
   };
-  constexpr int NR = SymbolicPlan::kAbsorbRows, NL = SymbolicPlan::kAbsorbLeaves;
-  double* l0 = ext;
-  double* l1 = l0 + NR;
-  double* pd0 = l1 + NR;
-  double* pd1 = pd0 + NL;
-  double* pf10 = pd1 + NL;
-  int64_t* ploff = reinterpret_cast<int64_t*>(pf10 + NL);
-  int32_t* rel = reinterpret_cast<int32_t*>(ploff + NL);  // column base of the parent row
-  int32_t* kk = rel + NR;
-  int32_t* prow = kk + NR;  // parent row
-  int32_t* hv = prow + NR;  // parent row is heavy
-  int32_t* pu0 = hv + NR;   // batch-local first update row of the leaf
-  int32_t* pw = pu0 + NL;
-  int32_t* prc = pw + NL;
-  int32_t* pend = prc + NL;  // batch-local end of the leaf's rows
-  int32_t* ents = pend + NL;  // the front's row lists (rl_ent), kAbsorbEntries at most
+  constexpr int RPT = 8;   // leaf rows per thread and pass
+  constexpr int GP = 16;   // product entries per thread and group
+  const int RM = T.fold_rmax[s], LM = T.fold_lmax[s];
+  double2* LQ = reinterpret_cast<double2*>(ext);  // per batch row: K values of columns 0/1, then (l0, l1)
+  double2* PQ = LQ + RM;                          // (l0 d0, l1 d1)
+  double* pd0 = reinterpret_cast<double*>(PQ + RM);
+  double* pd1 = pd0 + LM;
+  double* pf10 = pd1 + LM;
+  int64_t* ploff = reinterpret_cast<int64_t*>(pf10 + LM);
+  int32_t* prow0 = reinterpret_cast<int32_t*>(ploff + LM);  // batch-local first row of the leaf
+  int32_t* pwrc = prow0 + LM;
+  int32_t* kk = pwrc + LM;                                   // per batch row: batch-local leaf
   const int tid = threadIdx.x;
-  const int64_t F0 = T.fr_ptr[s];
-  const int64_t e0 = T.row_ptr[s];
-  const int64_t E0 = T.rl_ptr[e0], E1 = T.rl_ptr[e0 + r];
-  for (int q = tid; q < (int)(E1 - E0); q += NT) ents[q] = T.rl_ent[E0 + q];
-  int lp = (tid < r) ? (int)(T.rl_ptr[e0 + tid] - E0) : 0;
-  const int lend = (tid < r) ? (int)(T.rl_ptr[e0 + tid + 1] - E0) : 0;
-  const bool rowheavy = (tid < r) && T.rheavy[e0 + tid];
-  const int b0 = T.ab_bptr[s], b1 = T.ab_bptr[s + 1];
-  for (int bq = b0; bq < b1; ++bq) {
-    const int k0 = T.ab_bat[bq], k1 = (bq + 1 < b1) ? T.ab_bat[bq + 1] : T.mc_ptr[s + 1];
-    const int64_t j0 = T.ab_first[k0], j1 = T.ab_first[k1];
-    const int nrow = (int)(j1 - j0), nleaf = k1 - k0;
-    // (1) gather the leaf columns' K entries, 4 rows per thread in flight
-    for (int q0 = 0; q0 < nrow; q0 += 4 * NT) {
-      int32_t sa[4], sb[4];
+  const int b0 = T.fold_bptr[s], b1 = T.fold_bptr[s + 1];
+  uint2 e[GP];
+  auto load_group = [&](uint2 (&g)[GP], const uint2* P, int k, int len) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < GP; ++u) g[u] = (k + u < len) ? P[(int64_t)(k + u) * NT] : uint2{SymbolicPlan::kFoldPadDst, 0u};
+  };
+  load_group(e, T.fold_prod + T.fold_poff[b0] + tid, 0, T.fold_plen[b0]);
+  for (int bq = b0; bq < b1; ++bq) {
+    const int k0 = T.fold_bat[bq], k1 = (bq + 1 < b1) ? T.fold_bat[bq + 1] : T.mc_ptr[s + 1];
+    const int64_t j0 = T.ab_first[k0];
+    const int nrow = (int)(T.ab_first[k1] - j0), nleaf = k1 - k0;
+    // (1) the leaf rows' K entries (leaf tables loaded beside them)
+    int32_t lf[2], lw[2];
+    int64_t lo[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = tid + h * NT;
+      lf[h] = (k < nleaf) ? (int32_t)(T.ab_first[k0 + k] - j0) : 0;
+      lw[h] = (k < nleaf) ? T.ab_wrc[k0 + k] : 0;
+      lo[h] = (k < nleaf) ? T.ab_loff[k0 + k] : 0;
+    }
+    for (int q0 = 0; q0 < nrow; q0 += RPT * NT) {
+      int32_t sa[RPT], sb[RPT];
+#pragma unroll
+      for (int u = 0; u < RPT; ++u) {
         const int q = q0 + u * NT + tid;
         sa[u] = (q < nrow) ? T.ab_src0[j0 + q] : -1;
         sb[u] = (q < nrow) ? T.ab_src1[j0 + q] : -1;
-        if (q < nrow) {
-          const int pr = T.ab_rel[j0 + q];  // parent row -> its column base in the LDS front
-          rel[q] = (pr < 0) ? 0 : fidx<PK>(0, pr, r, ld);
-          kk[q] = T.ab_k[j0 + q] - k0;
-          prow[q] = pr;
-          hv[q] = (pr < 0) ? 0 : T.rheavy[e0 + pr];
-        }
+      }
+      double va[RPT], vb[RPT];
+#pragma unroll
+      for (int u = 0; u < RPT; ++u) {
+        va[u] = (sa[u] >= 0) ? Kx[sa[u]] : 0.0;
+        vb[u] = (sb[u] >= 0) ? Kx[sb[u]] : 0.0;
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < RPT; ++u) {
         const int q = q0 + u * NT + tid;
-        const double va = (sa[u] >= 0) ? Kx[sa[u]] : 0.0, vb = (sb[u] >= 0) ? Kx[sb[u]] : 0.0;
-        if (q < nrow) {
-          l0[q] = va;
-          l1[q] = vb;
-        }
+        if (q < nrow) LQ[q] = double2{va[u], vb[u]};
       }
+    }
+    for (int k = tid, h = 0; k < nleaf; k += NT, ++h) {
+      const int q0 = (h == 0) ? lf[0] : (h == 1 ? lf[1] : (int)(T.ab_first[k0 + k] - j0));
+      const int wrc = (h == 0) ? lw[0] : (h == 1 ? lw[1] : T.ab_wrc[k0 + k]);
+      prow0[k] = q0;
+      pwrc[k] = wrc;
+      ploff[k] = (h == 0) ? lo[0] : (h == 1 ? lo[1] : T.ab_loff[k0 + k]);
+      for (int i = 0; i < (wrc >> 8); ++i) kk[q0 + i] = k;
     }
     __syncthreads();
     lap(0);
-    // (2) per leaf: pivots
+    // (2) per leaf: pivots (+ D and the pivot check)
     for (int k = tid; k < nleaf; k += NT) {
-      const int f0 = T.ab_f0[k0 + k], wrc = T.ab_wrc[k0 + k], w = wrc & 255, rc = wrc >> 8;
-      const int jf = (int)(T.ab_first[k0 + k] - j0);
-      const double d0 = l0[jf];
-      const double f10 = (rc > 1) ? l0[jf + 1] : 0.0;
+      const int f0 = T.ab_f0[k0 + k], wrc = pwrc[k], w = wrc & 255, rc = wrc >> 8;
+      const int jf = prow0[k];
+      const double d0 = LQ[jf].x;
+      const double f10 = (rc > 1) ? LQ[jf + 1].x : 0.0;
       const double l10 = (w == 2) ? f10 / d0 : 0.0;
-      const double d1 = (w == 2) ? l1[jf + 1] - l10 * f10 : 0.0;
+      const double d1 = (w == 2) ? LQ[jf + 1].y - l10 * f10 : 0.0;
       pd0[k] = d0;
       pd1[k] = d1;
       pf10[k] = f10;
-      ploff[k] = T.ab_loff[k0 + k];
-      pu0[k] = jf + w;
-      pw[k] = w;
-      prc[k] = rc;
-      pend[k] = jf + rc;
       D[f0] = d0;
       if (bad_pivot(d0, tol)) atomicMin(&st->fail_pivot, f0 + 1);
       if (w == 2) {
@@ -1413,17 +1370,19 @@ __device__ __forceinline__ void absorb_leaves(const FrontTab& T, int s, int r, i
     }
     __syncthreads();
     lap(1);
-    // (3) per leaf row: L entries (HBM panel: d on the diagonal, zero above; LDS: l0, l1 of update rows)
+    // (3) per leaf row: L entries (HBM panel for the solves: d on the diagonal, zero above; LDS: l
+    // and l d of the update rows)
     for (int q = tid; q < nrow; q += NT) {
       const int k = kk[q];
-      const int w = pw[k], rc = prc[k], i = q - (pu0[k] - w);
+      const int wrc = pwrc[k], w = wrc & 255, rc = wrc >> 8, i = q - prow0[k];
       const double d0 = pd0[k], d1 = pd1[k], f10 = pf10[k];
       double* __restrict__ L = arena + ploff[k];
       if (i >= w) {
-        const double li0 = l0[q] / d0;
-        const double li1 = (w == 2) ? (l1[q] - li0 * f10) / d1 : 0.0;
-        l0[q] = li0;
-        l1[q] = li1;
+        const double2 a = LQ[q];
+        const double li0 = a.x / d0;
+        const double li1 = (w == 2) ? (a.y - li0 * f10) / d1 : 0.0;
+        LQ[q] = double2{li0, li1};
+        PQ[q] = double2{li0 * d0, li1 * d1};
         L[i] = li0;
         if (w == 2) L[i + rc] = li1;
       } else if (i == 0) {
@@ -1436,21 +1395,54 @@ __device__ __forceinline__ void absorb_leaves(const FrontTab& T, int s, int r, i
     }
     __syncthreads();
     lap(2);
-    // (4) row owners: this batch's absorbed update rows of front row tid, child order
-    const int jr0 = (int)(j0 - F0), jr1 = (int)(j1 - F0);
-    // the row's list was staged in LDS (ents) at the start; a rolled loop keeps the kernel's code
-    // small (one workgroup per CU runs it once: the instruction cache is cold for every front)
-#pragma unroll 1
-    for (; lp < lend; ++lp) {
-      const int ja = ents[lp];
-      if (ja >= jr1) break;  // a later batch's entry
-      absorb_entry<PK>(A, r, ld, l0, l1, pd0, pd1, rel, kk, prow, hv, pu0, pend, ja - jr0, tid, rowheavy);
+    // (4) this thread's chunk of the destination-sorted products (entry k at 256 k + tid: each load
+    // instruction is coalesced)
+    const uint2* __restrict__ P = T.fold_prod + T.fold_poff[bq] + tid;
+    const int len = T.fold_plen[bq];
+    int cur = -1;
+    double acc = 0.0;
+    for (int k = 0; k < len; k += GP) {
+      uint2 nx[GP];
+      if (k + GP < len) {
+        load_group(nx, P, k + GP, len);
+      } else if (bq + 1 < b1) {  // the next batch's first group
+        load_group(nx, T.fold_prod + T.fold_poff[bq + 1] + tid, 0, T.fold_plen[bq + 1]);
+      }
+      // every LDS operand of the group is read before its first update of A
+      double v[GP];
+#pragma unroll
+      for (int u = 0; u < GP; ++u) {
+        const double2 la = LQ[e[u].x >> 16], pb = PQ[e[u].y];  // padding reads row 0: harmless
+        v[u] = la.x * pb.x + la.y * pb.y;
+      }
+      // a destination is owned by one thread and gets one run: its partial sum is subtracted with a
+      // non-returning LDS atomic (one writer per address, so the result is deterministic), which needs
+      // no wait for the old value — a plain read-modify-write would serialise every run on the LDS
+      // round trip, and divergent runs across the wave on all of them
+#pragma unroll
+      for (int u = 0; u < GP; ++u) {
+        const int dst = (int)(e[u].x & 0xffffu);
+        if (dst == (int)SymbolicPlan::kFoldPadDst) continue;  // padding: the chunk has ended
+        if (dst != cur) {
+          if (cur >= 0) __hip_atomic_fetch_add(A + cur, -acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          cur = dst;
+          acc = v[u];
+        } else {
+          acc += v[u];
+        }
+      }
+      if (k + GP < len || bq + 1 < b1) {
+#pragma unroll
+        for (int u = 0; u < GP; ++u) e[u] = nx[u];
+      }
     }
+    if (len == 0 && bq + 1 < b1) load_group(e, T.fold_prod + T.fold_poff[bq + 1] + tid, 0, T.fold_plen[bq + 1]);
+    if (cur >= 0) __hip_atomic_fetch_add(A + cur, -acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     __syncthreads();
     lap(3);
   }
-  if (dg && threadIdx.x == 0)
-    for (int k = 0; k < 4; ++k) dg[8 + k] = tph[k];
+  if (fdg && threadIdx.x == 0)
+    for (int k = 0; k < 4; ++k) fdg[k] = tph[k];
 }
 
 // ------------------------------------------------------------------ factorisation tree
@@ -1508,7 +1500,7 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
   const int tid = threadIdx.x;
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
   const int ld = PK ? 0 : (r | 1);
-  if (T.absorb[s]) {  // original entries, then the micro-leaf children absorbed in LDS
+  if (T.absorb[s]) {  // original entries, then the micro-leaf children folded in LDS
     const int ntot = PK ? r * (r + 1) / 2 : r * ld;
     for (int q = tid; q < ntot; q += NT) A[q] = 0.0;
     __syncthreads();
@@ -1517,7 +1509,7 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
       A[fidx<PK>(d - dj * r, dj, r, ld)] = Kx[T.asm_src[q]];
     }
     __syncthreads();
-    absorb_leaves<PK>(T, s, r, ld, A, Kx, arena, D, st, tol, A + ((ntot + 1) & ~1), dg);  // 16-byte aligned
+    fold_leaves<PK>(T, s, A, Kx, arena, D, st, tol, A + ((ntot + 1) & ~1), dg ? dg + 16 : nullptr);  // 16-byte aligned
   } else {  // pre-assembled as the LDS image: a straight copy, 16 loads in flight per thread
     const double* __restrict__ src = fscratch + T.fs_off[s];
     const int n = PK ? r * (r + 1) / 2 : r * ld;
@@ -1595,9 +1587,9 @@ __global__ __launch_bounds__(NT) void k_fact_tree(FrontTab T, const int32_t* __r
   const int t = s_task;
   if (t >= nt) return;
   const int s = order[t];
-  int64_t* dg = dbg ? dbg + 16 * t : nullptr;
+  int64_t* dg = dbg ? dbg + 24 * t : nullptr;
   if (dg && threadIdx.x == 0) dg[0] = wall_clock64();
-  if (T.nrows[s] <= 128)
+  if (T.nrows[s] <= 128 && !T.fold_pk[s])
     fact_tree_front<false>(T, s, dep, dep_ptr[t], dep_ptr[t + 1], flags, epoch, Kx, arena, fscratch, D, st, tol, err, A, Dl,
                            MK, cbuf, rels, dg);
   else
@@ -3091,15 +3083,25 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         if (S.ftree[S.child_list[q]]) dl.push_back(S.child_list[q]);
       dptr.push_back((int32_t)dl.size());
       const int r = S.nrows[s], w = S.first[s + 1] - S.first[s], u = r - w;
-      ftree_lds_ = std::max<int>(ftree_lds_, (r <= 128 ? 8 * ((r * (r | 1) + 1) & ~1) : 8 * ((r * (r + 1) / 2 + 1) & ~1)) +
-                                                 (S.absorb[s] ? (int)SymbolicPlan::kAbsorbLdsBytes : 0));
-      // reads: the pre-assembled lower triangle + the tree children's blocks; writes: L panel, U, D
-      ftree_bytes_ += 8.0 * (r * (r + 1) / 2.0 + r * (double)w + u * (u + 1) / 2.0 + w);
-      for (int q = S.child_ptr[s]; q < S.child_ptr[s + 1]; ++q)
-        if (S.ftree[S.child_list[q]]) {
-          const double uc = S.nrows[S.child_list[q]] - (S.first[S.child_list[q] + 1] - S.first[S.child_list[q]]);
-          ftree_bytes_ += 8.0 * uc * (uc + 1) / 2.0;
-        }
+      const bool sq = r <= 128 && !S.fold_pk[s];
+      ftree_lds_ = std::max<int>(ftree_lds_, (sq ? 8 * ((r * (r | 1) + 1) & ~1) : 8 * ((r * (r + 1) / 2 + 1) & ~1)) +
+                                                 (S.absorb[s] ? SymbolicPlan::kFoldRowBytes * S.fold_rmax[s] +
+                                                                    SymbolicPlan::kFoldLeafBytes * S.fold_lmax[s]
+                                                              : 0));
+      // folded leaves: their K entries read, their L entries written
+      for (int k = S.absorb[s] ? S.mc_ptr[s] : 0; k < (S.absorb[s] ? S.mc_ptr[s + 1] : 0); ++k) {
+        const int c = S.mc_list[k];
+        const double rc = S.nrows[c], wc = S.first[c + 1] - S.first[c];
+        ftree_bytes_ += 12.0 * (S.asm_ptr[c + 1] - S.asm_ptr[c]) + 8.0 * (rc * wc - wc * (wc - 1) / 2.0);
+        for (int t = 0; t < (int)wc; ++t) ftree_flops_ += (rc - t - 1) * (rc - t);
+      }
+      // algorithmic bytes as SURVEY 8(d) prices the factorisation (B_fact = 8 nnzL + 12 nnzK): the L
+      // entries this front writes (stored lower trapezoid of its panel, D on the diagonal) and the
+      // caller's K entries it reads (12 B: value + index).  The staging traffic the kernel moves on
+      // top (the image or K scatter, the tree children's U blocks, the U write-out) is not counted:
+      // it is the implementation's, not the algorithm's.
+      (void)u;
+      ftree_bytes_ += 8.0 * (r * (double)w - w * (w - 1) / 2.0) + 12.0 * (double)(S.asm_ptr[s + 1] - S.asm_ptr[s]);
       for (int t = 0; t < w; ++t) ftree_flops_ += (double)(r - t - 1) * (r - t);
     }
     auto up = [](DBuf<int32_t>& d, const std::vector<int32_t>& v) { d.upload(v.empty() ? std::vector<int32_t>{0} : v); };
@@ -3109,57 +3111,53 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     fflags_.alloc(std::max(ns, 1));
     fflags_.zero();
     {
-      std::vector<uint8_t> ab(S.absorb.begin(), S.absorb.end());
-      if (ab.empty()) ab.push_back(0);
-      absorb_.upload(ab);
-      mc_ptr_.upload(S.mc_ptr);
-      mc_list_.upload(S.mc_list.empty() ? std::vector<int32_t>{0} : S.mc_list);
-      rl_ptr_.upload(S.rl_ptr);
-      rl_ent_.upload(S.rl_ent.empty() ? std::vector<int32_t>{0} : S.rl_ent);
+      auto up8 = [](DBuf<uint8_t>& d, const std::vector<uint8_t>& v) { d.upload(v.empty() ? std::vector<uint8_t>{0} : v); };
       auto up32 = [](DBuf<int32_t>& d, const std::vector<int32_t>& v) { d.upload(v.empty() ? std::vector<int32_t>{0} : v); };
+      auto up64 = [](DBuf<int64_t>& d, const std::vector<int64_t>& v) { d.upload(v.empty() ? std::vector<int64_t>{0} : v); };
+      up8(absorb_, S.absorb);
+      up8(fold_pk_, S.fold_pk);
+      up32(mc_ptr_, S.mc_ptr);
+      up64(ab_first_, S.ab_first);
       up32(ab_src0_, S.ab_src0);
       up32(ab_src1_, S.ab_src1);
-      up32(ab_rel_, S.ab_rel);
       up32(ab_k_, S.ab_k);
-      up32(ab_bptr_, S.ab_bptr);
-      up32(ab_bat_, S.ab_bat);
-      fr_ptr_.upload(S.fr_ptr);
-      ab_first_.upload(S.ab_first);
       up32(ab_f0_, S.ab_f0);
-      {
-        std::vector<uint8_t> hvv(S.rheavy.begin(), S.rheavy.end());
-        if (hvv.empty()) hvv.push_back(0);
-        rheavy_.upload(hvv);
-        T_.rheavy = rheavy_;
-      }
       up32(ab_wrc_, S.ab_wrc);
       {
         std::vector<int64_t> lo(S.mc_list.size() + 1, 0);
         for (size_t k = 0; k < S.mc_list.size(); ++k) lo[k] = S.l_off[S.mc_list[k]];
         ab_loff_.upload(lo);
       }
+      up32(fold_bptr_, S.fold_bptr);
+      up32(fold_bat_, S.fold_bat);
+      up64(fold_poff_, S.fold_poff);
+      up32(fold_plen_, S.fold_plen);
+      up32(fold_rmax_, S.fold_rmax);
+      up32(fold_lmax_, S.fold_lmax);
+      fold_prod_.upload(S.fold_prod.empty() ? std::vector<uint32_t>{SymbolicPlan::kFoldPadDst, 0u} : S.fold_prod);
+      T_.absorb = absorb_;
+      T_.fold_pk = fold_pk_;
+      T_.mc_ptr = mc_ptr_;
+      T_.ab_first = ab_first_;
+      T_.ab_src0 = ab_src0_;
+      T_.ab_src1 = ab_src1_;
+      T_.ab_k = ab_k_;
       T_.ab_f0 = ab_f0_;
       T_.ab_wrc = ab_wrc_;
       T_.ab_loff = ab_loff_;
-      T_.ab_src0 = ab_src0_;
-      T_.ab_src1 = ab_src1_;
-      T_.ab_rel = ab_rel_;
-      T_.ab_k = ab_k_;
-      T_.ab_bptr = ab_bptr_;
-      T_.ab_bat = ab_bat_;
-      T_.fr_ptr = fr_ptr_;
-      T_.ab_first = ab_first_;
-      T_.absorb = absorb_;
-      T_.mc_ptr = mc_ptr_;
-      T_.mc_list = mc_list_;
-      T_.rl_ptr = rl_ptr_;
-      T_.rl_ent = rl_ent_;
+      T_.fold_bptr = fold_bptr_;
+      T_.fold_bat = fold_bat_;
+      T_.fold_poff = fold_poff_;
+      T_.fold_plen = fold_plen_;
+      T_.fold_rmax = fold_rmax_;
+      T_.fold_lmax = fold_lmax_;
+      T_.fold_prod = reinterpret_cast<const uint2*>(fold_prod_.p);
     }
     fcnt_.alloc(4);
     fcnt_.zero();
     const char* dv = std::getenv("MADIPM_TREE_DEBUG");
     if (dv && dv[0] == '1' && nftree_) {
-      fdbg_.alloc((int64_t)16 * nftree_);
+      fdbg_.alloc((int64_t)24 * nftree_);
       fdbg_.zero();
     }
   }
@@ -3658,12 +3656,20 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
         TIMED(KK_LB_SYRK, L.bytes, L.flops, lb_syrk((int)L.off, s));
         break;
       case FTREE:
+        if (!ftree_checked_) {  // static + dynamic LDS must fit the CU (160 KB on gfx950)
+          hipFuncAttributes fa{};
+          MADIPM_HIP(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(k_fact_tree)));
+          MADIPM_REQUIRE(fa.sharedSizeBytes + (size_t)L.lds_bytes <= 160 * 1024,
+                         "k_fact_tree: LDS " + std::to_string(fa.sharedSizeBytes) + " + " +
+                             std::to_string(L.lds_bytes) + " bytes exceeds 160 KB");
+          ftree_checked_ = true;
+        }
         ++fepoch_;
         TIMED(KK_FACT_TREE, L.bytes, L.flops,
               (k_fact_tree<<<(unsigned)nftree_, NT, L.lds_bytes, s>>>(T_, ft_order_, nftree_, ft_dptr_, ft_dep_, fcnt_,
                                                                       fflags_, fepoch_, Kx, arena_, fscratch_, D_, st_,
                                                                       pivot_tol, &st_->err, fdbg_.p)));
-        if (fdbg_.p) tree_debug_dump(s, "fact", fdbg_.p, nftree_, "stage", "wait", "push", "factor", "store", 16);
+        if (fdbg_.p) tree_debug_dump(s, "fact", fdbg_.p, nftree_, "stage", "wait", "push", "factor", "store", 24);
         break;
     }
   }
@@ -3749,18 +3755,23 @@ void LDLSolver::tree_debug_dump(hipStream_t s, const char* what, const int64_t* 
   MADIPM_HIP(hipStreamSynchronize(s));
   for (int t = 0; t < nt; ++t)
     for (int k = 0; k < 8; ++k) h[8 * t + k] = hs[(size_t)stride * t + k];
-  if (stride == 16) {  // factor sub-phases (or absorption phases), per level
-    std::vector<double> ab((size_t)S_.nlevels * 6, 0.0);
+  if (stride == 24) {  // factor sub-phases, leaf-folding phases, per level
+    std::vector<double> ab((size_t)S_.nlevels * 6, 0.0), fo((size_t)S_.nlevels * 4, 0.0);
     std::vector<int> na(S_.nlevels, 0);
     for (int t = 0; t < nt; ++t) {
       const int lv = S_.level[(int)h[8 * t + 6]];
       na[lv]++;
-      for (int k = 0; k < 6; ++k) ab[lv * 6 + k] += hs[(size_t)16 * t + 8 + k] * 0.01;
+      for (int k = 0; k < 6; ++k) ab[lv * 6 + k] += hs[(size_t)24 * t + 8 + k] * 0.01;
+      for (int k = 0; k < 4; ++k) fo[lv * 4 + k] += hs[(size_t)24 * t + 16 + k] * 0.01;
     }
+    for (int lv = 0; lv < S_.nlevels; ++lv)
+      if (na[lv])
+        fprintf(stderr, "  fold level %d: gather %.2f  pivots %.2f  L %.2f  products %.2f us\n", lv, fo[lv * 4] / na[lv],
+                fo[lv * 4 + 1] / na[lv], fo[lv * 4 + 2] / na[lv], fo[lv * 4 + 3] / na[lv]);
     std::vector<double> sq((size_t)S_.nlevels * 3, 0.0);
     for (int t = 0; t < nt; ++t) {
       const int lv = S_.level[(int)h[8 * t + 6]];
-      const int64_t* d = &hs[(size_t)16 * t];
+      const int64_t* d = &hs[(size_t)24 * t];
       sq[lv * 3] += (d[14] - d[4]) * 0.01;
       sq[lv * 3 + 1] += (d[15] - d[14]) * 0.01;
       sq[lv * 3 + 2] += (d[5] - d[15]) * 0.01;

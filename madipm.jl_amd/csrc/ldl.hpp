@@ -47,24 +47,24 @@ struct FrontTab {
   // tree front (its contiguous gather range), else to uvec[uvec_off[c] + a] (upos = -1)
   const int64_t* upos;
   double* gbuf;
-  // leaf absorption (SymbolicPlan::absorb / mc_* / rl_*)
+  // leaf folding (SymbolicPlan::absorb / fold_* / ab_*)
   const uint8_t* absorb;
+  const uint8_t* fold_pk;
   const int32_t* mc_ptr;
-  const int32_t* mc_list;
-  const int64_t* rl_ptr;
-  const int32_t* rl_ent;
-  const int64_t* fr_ptr;
   const int64_t* ab_first;
   const int32_t* ab_src0;
   const int32_t* ab_src1;
-  const int32_t* ab_rel;
   const int32_t* ab_k;
-  const int32_t* ab_bptr;
-  const int32_t* ab_bat;
   const int32_t* ab_f0;
   const int32_t* ab_wrc;
   const int64_t* ab_loff;
-  const uint8_t* rheavy;
+  const int32_t* fold_bptr;
+  const int32_t* fold_bat;
+  const int64_t* fold_poff;
+  const int32_t* fold_plen;
+  const int32_t* fold_rmax;
+  const int32_t* fold_lmax;
+  const uint2* fold_prod;
   const uint8_t* fs_img;  // 1: fscratch holds the front's LDS image (tree fronts), else ld r
   int schur_defer;  // in-LDS factorisation: update block U in one pass after the pivots (MADIPM_SCHUR_DEFER)
 };
@@ -243,13 +243,14 @@ class LDLSolver : public LinSolver {
   // factorisation tree (k_fact_tree): fronts in topological order, their tree children, flags
   // (per-factorisation epoch), ticket counters (reset by the launch's last workgroup)
   int nftree_ = 0, ftree_lds_ = 0, fepoch_ = 0;
+  bool ftree_checked_ = false;
   double ftree_bytes_ = 0, ftree_flops_ = 0;
   DBuf<int32_t> ft_order_, ft_dptr_, ft_dep_, fflags_, fcnt_;
-  DBuf<int64_t> fdbg_, rl_ptr_, fr_ptr_, ab_first_;
-  DBuf<int32_t> ab_src0_, ab_src1_, ab_rel_, ab_k_, ab_bptr_, ab_bat_, ab_f0_, ab_wrc_;
-  DBuf<int64_t> ab_loff_;
-  DBuf<uint8_t> absorb_, rheavy_, fs_img_;
-  DBuf<int32_t> mc_ptr_, mc_list_, rl_ent_;
+  DBuf<int64_t> fdbg_, ab_first_, ab_loff_, fold_poff_;
+  DBuf<int32_t> ab_src0_, ab_src1_, ab_k_, ab_f0_, ab_wrc_, fold_bptr_, fold_bat_, fold_plen_, fold_rmax_, fold_lmax_;
+  DBuf<uint8_t> absorb_, fold_pk_, fs_img_;
+  DBuf<int32_t> mc_ptr_;
+  DBuf<uint32_t> fold_prod_;
   DBuf<double> xch_;
   DBuf<uint8_t> wout_, colmask_;
   DBuf<int32_t> tasks_, flags_, flag_off_, counters_, bp_off_;

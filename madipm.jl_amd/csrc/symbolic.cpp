@@ -19,6 +19,8 @@ namespace madipm {
 
 namespace {
 
+constexpr int NT_FOLD = 256;  // threads of k_fact_tree (product-list chunks)
+
 struct Pattern {
   // strictly-lower pattern of P K P^T: column lists (rows > col) and row lists (cols < row)
   std::vector<int64_t> cp, rp;
@@ -766,79 +768,90 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       S.ftree[s] = ok && fanin <= SymbolicPlan::kFactTreeFanIn;
     }
   }
-  // leaf absorption: a tree front whose pre-leaf children are all micro leaves (w <= 2, r <= 32)
-  // factorises them itself inside k_fact_tree and adds their rank-1/2 updates straight into its LDS
-  // front (row-owner lists rl_*: for front row i, the (child k, update row a) pairs in child order),
-  // replacing the micro launch + the gather pre-assembly for that front.
-  S.absorb.assign(ns, 0);
-  S.mc_ptr.assign(ns + 1, 0);
+  // leaf folding (SymbolicPlan::absorb): a tree front whose pre-leaf children are all micro leaves
+  // (w <= 2, r <= 32) factorises them itself inside k_fact_tree and subtracts their rank-1/2 updates
+  // from its LDS front through destination-sorted product lists, replacing the micro launch and the
+  // gather pre-assembly for that front (MADIPM_FOLD=0 disables it).
+  const int ns_all = ns;
+  S.absorb.assign(ns_all, 0);
+  S.fold_pk.assign(ns_all, 0);
+  S.mc_ptr.assign(ns_all + 1, 0);
   S.mc_list.clear();
-  S.rl_ptr.assign(S.row_ptr[ns] + 1, 0);
-  S.rl_ent.clear();
+  S.fold_bptr.assign(ns_all + 1, 0);
+  S.fold_rmax.assign(ns_all, 0);
+  S.fold_lmax.assign(ns_all, 0);
+  S.fold_bat.clear();
+  S.fold_poff.clear();
+  S.fold_plen.clear();
+  S.fold_prod.clear();
+  S.ab_first.clear();
+  S.ab_src0.clear();
+  S.ab_src1.clear();
+  S.ab_k.clear();
+  S.ab_f0.clear();
+  S.ab_wrc.clear();
   {
-    // experimental (off by default): the row-owner pass is latency-bound on dense rows and loses to
-    // the gather pre-assembly on the ex10 stand-in; MADIPM_ABSORB=1 enables it
-    const char* ev = std::getenv("MADIPM_ABSORB");
-    const bool on = ev && ev[0] == '1';
+    const char* ev = std::getenv("MADIPM_FOLD");
+    const bool on = !(ev && ev[0] == '0');
+    constexpr int64_t LMAX = SymbolicPlan::kFoldLdsMax;
+    constexpr int64_t RB = SymbolicPlan::kFoldRowBytes, LB = SymbolicPlan::kFoldLeafBytes;
     auto micro_leaf = [&](int c) {
-      return S.child_ptr[c] == S.child_ptr[c + 1] && S.nrows[c] <= 32 && S.first[c + 1] - S.first[c] <= 2;
+      return S.child_ptr[c] == S.child_ptr[c + 1] && S.nrows[c] <= 32 && S.first[c + 1] - S.first[c] <= 2 &&
+             S.nrows[c] > S.first[c + 1] - S.first[c];
     };
-    for (int s = 0; s < ns; ++s) {
+    auto sq_bytes = [](int64_t r) { return 8 * ((r * (r | 1) + 1) & ~1LL); };
+    auto pk_bytes = [](int64_t r) { return 8 * ((r * (r + 1) / 2 + 1) & ~1LL); };
+    std::vector<int64_t> col0(32), col1(32);
+    struct Prod {
+      uint32_t dst, q1, q2;
+    };
+    std::vector<Prod> pr;
+    std::vector<int64_t> bnd;
+    for (int s = 0; s < ns_all; ++s) {
       S.mc_ptr[s + 1] = S.mc_ptr[s];
+      S.fold_bptr[s + 1] = S.fold_bptr[s];
       if (!on || !S.ftree[s]) continue;
       const int64_t r = S.nrows[s];
-      const int64_t front_bytes = 8 * (r <= 128 ? r * (r | 1) : r * (r + 1) / 2);
-      if (front_bytes + SymbolicPlan::kAbsorbLdsBytes > SymbolicPlan::kFactTreeLdsMax) continue;
-      int nmc = 0;
+      int64_t nmc = 0, nrow = 0;
       bool ok = true;
       for (int64_t qc = S.child_ptr[s]; qc < S.child_ptr[s + 1] && ok; ++qc) {
         const int c = S.child_list[qc];
         if (S.ftree[c]) continue;
         ok = micro_leaf(c);
         ++nmc;
+        nrow += S.nrows[c];
       }
       if (!ok || nmc == 0) continue;
-      int64_t nent = 0;  // the row lists are staged in LDS: bounded
-      for (int64_t qc = S.child_ptr[s]; qc < S.child_ptr[s + 1]; ++qc)
-        if (!S.ftree[S.child_list[qc]]) nent += S.nrows[S.child_list[qc]];
-      if (nent > SymbolicPlan::kAbsorbEntries) continue;
+      // storage: square (r <= 128) when the front and all its leaf rows fit, else packed lower;
+      // leaves in batches when even that does not fit
+      int pk;
+      int64_t budget;
+      if (r <= 128 && sq_bytes(r) + RB * nrow + LB * nmc <= LMAX) {
+        pk = 0;
+        budget = LMAX - sq_bytes(r);
+      } else {
+        pk = 1;
+        budget = LMAX - pk_bytes(r);
+      }
+      if (budget < RB * 32 + LB) continue;  // not even one leaf fits beside the front
       S.absorb[s] = 1;
+      S.fold_pk[s] = (uint8_t)pk;
+      const int64_t ld = r | 1;
+      auto fidx = [&](int64_t i, int64_t j) -> uint32_t {
+        return (uint32_t)(pk ? (j * (2 * r - j - 1)) / 2 + i : i + j * ld);
+      };
+      const int k0 = (int)S.mc_list.size();
       for (int64_t qc = S.child_ptr[s]; qc < S.child_ptr[s + 1]; ++qc)
         if (!S.ftree[S.child_list[qc]]) S.mc_list.push_back(S.child_list[qc]);
-      S.mc_ptr[s + 1] = (int32_t)S.mc_list.size();
-    }
-    // flat leaf-row tables: the rows of a front's absorbed leaves in child order; per row the caller's
-    // CSC index of its entry in the leaf's column 0 / 1 (-1: structural zero), its parent row (-1 for a
-    // pivot row) and its leaf; per leaf its first flat row; batches of <= kAbsorbRows rows /
-    // kAbsorbLeaves leaves per front
-    const int nmc_all = (int)S.mc_list.size();
-    S.ab_first.assign(nmc_all + 1, 0);
-    S.ab_f0.assign(nmc_all + 1, 0);
-    S.ab_wrc.assign(nmc_all + 1, 0);
-    S.fr_ptr.assign(ns + 1, 0);
-    S.ab_bptr.assign(ns + 1, 0);
-    S.ab_src0.clear();
-    S.ab_src1.clear();
-    S.ab_rel.clear();
-    S.ab_k.clear();
-    S.ab_bat.clear();
-    std::vector<int64_t> col0(32), col1(32);
-    for (int s = 0; s < ns; ++s) {
-      S.fr_ptr[s] = (int64_t)S.ab_src0.size();
-      int rows_in = 0, leaves_in = 0;
-      for (int k = S.mc_ptr[s]; k < S.mc_ptr[s + 1]; ++k) {
+      const int k1 = (int)S.mc_list.size();
+      S.mc_ptr[s + 1] = k1;
+      // flat leaf rows (child order)
+      for (int k = k0; k < k1; ++k) {
         const int c = S.mc_list[k];
         const int rc = S.nrows[c], wc = S.first[c + 1] - S.first[c];
-        if (k == S.mc_ptr[s] || rows_in + rc > SymbolicPlan::kAbsorbRows || leaves_in + 1 > SymbolicPlan::kAbsorbLeaves) {
-          S.ab_bat.push_back(k);
-          rows_in = 0;
-          leaves_in = 0;
-        }
-        rows_in += rc;
-        leaves_in += 1;
-        S.ab_first[k] = (int64_t)S.ab_src0.size();
-        S.ab_f0[k] = S.first[c];
-        S.ab_wrc[k] = wc | (rc << 8);
+        S.ab_first.push_back((int64_t)S.ab_src0.size());
+        S.ab_f0.push_back(S.first[c]);
+        S.ab_wrc.push_back(wc | (rc << 8));
         std::fill(col0.begin(), col0.end(), -1);
         std::fill(col1.begin(), col1.end(), -1);
         for (int64_t q = S.asm_ptr[c]; q < S.asm_ptr[c + 1]; ++q) {
@@ -847,47 +860,67 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
           (lc == 0 ? col0 : col1)[lr] = S.asm_src[q];
         }
         for (int i = 0; i < rc; ++i) {
-          MADIPM_REQUIRE(col0[i] < INT32_MAX && col1[i] < INT32_MAX, "absorbed leaf: CSC index beyond int32");
+          MADIPM_REQUIRE(col0[i] < INT32_MAX && col1[i] < INT32_MAX, "folded leaf: CSC index beyond int32");
           S.ab_src0.push_back((int32_t)col0[i]);
           S.ab_src1.push_back((int32_t)col1[i]);
-          S.ab_rel.push_back(i >= wc ? S.rel[S.rel_ptr[c] + (i - wc)] : -1);
           S.ab_k.push_back(k);
         }
       }
-      S.ab_bptr[s + 1] = (int32_t)S.ab_bat.size();
-    }
-    S.fr_ptr[ns] = (int64_t)S.ab_src0.size();
-    S.ab_first[nmc_all] = (int64_t)S.ab_src0.size();
-    // row-owner lists: for front row i, the front-relative flat indices of the absorbed update rows
-    // landing in row i, in child order (= increasing)
-    for (int s = 0; s < ns; ++s)
-      for (int k = S.mc_ptr[s]; k < S.mc_ptr[s + 1]; ++k) {
-        const int c = S.mc_list[k];
-        for (int64_t a = 0; a < S.rel_ptr[c + 1] - S.rel_ptr[c]; ++a) S.rl_ptr[S.row_ptr[s] + S.rel[S.rel_ptr[c] + a] + 1]++;
+      // batches and their product lists
+      int kb = k0;
+      while (kb < k1) {
+        int ke = kb;
+        int64_t rows = 0;
+        while (ke < k1 && RB * (rows + S.nrows[S.mc_list[ke]]) + LB * (ke - kb + 1) <= budget) rows += S.nrows[S.mc_list[ke++]];
+        MADIPM_REQUIRE(ke > kb, "fold: a leaf does not fit the batch budget");
+        S.fold_bat.push_back(kb);
+        S.fold_rmax[s] = std::max<int32_t>(S.fold_rmax[s], (int32_t)rows);
+        S.fold_lmax[s] = std::max<int32_t>(S.fold_lmax[s], ke - kb);
+        const int64_t row0 = S.ab_first[kb];
+        pr.clear();
+        for (int k = kb; k < ke; ++k) {
+          const int c = S.mc_list[k];
+          const int rc = S.nrows[c], wc = S.first[c + 1] - S.first[c];
+          const int32_t* rl = S.rel.data() + S.rel_ptr[c];
+          const uint32_t qb0 = (uint32_t)(S.ab_first[k] - row0);
+          for (int a = wc; a < rc; ++a)
+            for (int b = wc; b <= a; ++b)  // rel ascending: parent row of b <= that of a
+              pr.push_back({fidx(rl[a - wc], rl[b - wc]), qb0 + a, qb0 + b});
+        }
+        std::stable_sort(pr.begin(), pr.end(), [](const Prod& x, const Prod& y) { return x.dst < y.dst; });
+        // 256 chunks at destination boundaries, balanced by count
+        const int64_t P = (int64_t)pr.size();
+        bnd.assign(NT_FOLD + 1, P);
+        bnd[0] = 0;
+        for (int t = 1; t < NT_FOLD; ++t) {
+          int64_t q = std::max(bnd[t - 1], (P * t) / NT_FOLD);
+          while (q > 0 && q < P && pr[q].dst == pr[q - 1].dst) ++q;
+          bnd[t] = q;
+        }
+        int64_t len = 0;
+        for (int t = 0; t < NT_FOLD; ++t) len = std::max(len, bnd[t + 1] - bnd[t]);
+        const int64_t off = (int64_t)S.fold_prod.size() / 2;
+        S.fold_poff.push_back(off);
+        S.fold_plen.push_back((int32_t)len);
+        S.fold_prod.resize(2 * (off + len * NT_FOLD));
+        for (int t = 0; t < NT_FOLD; ++t)
+          for (int64_t k = 0; k < len; ++k) {
+            uint32_t* e = &S.fold_prod[2 * (off + k * NT_FOLD + t)];
+            const int64_t q = bnd[t] + k;
+            if (q < bnd[t + 1]) {
+              MADIPM_REQUIRE(pr[q].dst < SymbolicPlan::kFoldPadDst && pr[q].q1 < 65536, "fold: index beyond 16 bits");
+              e[0] = pr[q].dst | (pr[q].q1 << 16);
+              e[1] = pr[q].q2;
+            } else {
+              e[0] = SymbolicPlan::kFoldPadDst;
+              e[1] = 0;
+            }
+          }
+        kb = ke;
       }
-    for (int64_t t = 0; t < S.row_ptr[ns]; ++t) S.rl_ptr[t + 1] += S.rl_ptr[t];
-    S.rl_ent.assign(S.rl_ptr[S.row_ptr[ns]], 0);
-    std::vector<int64_t> fill(S.rl_ptr.begin(), S.rl_ptr.end() - 1);
-    for (int s = 0; s < ns; ++s)
-      for (int k = S.mc_ptr[s]; k < S.mc_ptr[s + 1]; ++k) {
-        const int c = S.mc_list[k];
-        const int wc = S.first[c + 1] - S.first[c];
-        for (int64_t a = 0; a < S.rel_ptr[c + 1] - S.rel_ptr[c]; ++a)
-          S.rl_ent[fill[S.row_ptr[s] + S.rel[S.rel_ptr[c] + a]]++] = (int32_t)(S.ab_first[k] + wc + a - S.fr_ptr[s]);
-      }
-    // heavy rows (in most absorbed leaves): their (heavy row, light column) entries are added by the
-    // light column's owner instead, so no thread carries a dense row alone
-    S.rheavy.assign(S.row_ptr[ns], 0);
-    const char* hev = std::getenv("MADIPM_ABSORB_HEAVY");
-    const bool heavy_on = hev && hev[0] == '1';
-    for (int s = 0; s < ns; ++s) {
-      if (!S.absorb[s]) continue;
-      const int64_t e0 = S.row_ptr[s];
-      const int r = S.nrows[s];
-      const double mean = (double)(S.rl_ptr[e0 + r] - S.rl_ptr[e0]) / std::max(1, r);
-      for (int i = 0; i < r; ++i)
-        S.rheavy[e0 + i] = heavy_on && (S.rl_ptr[e0 + i + 1] - S.rl_ptr[e0 + i]) > std::max(24.0, 3.0 * mean);
+      S.fold_bptr[s + 1] = (int32_t)S.fold_bat.size();
     }
+    S.ab_first.push_back((int64_t)S.ab_src0.size());
   }
   S.fs_off.assign(ns, -1);
   S.fs_size = 0;

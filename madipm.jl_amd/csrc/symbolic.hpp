@@ -102,24 +102,32 @@ struct SymbolicPlan {
   static constexpr int kFactTreeMax = 192;
   static constexpr int kFactTreeFanIn = 8;
   std::vector<uint8_t> ftree;          // factorisation-tree fronts (k_fact_tree)
-  // leaf absorption (tree fronts whose pre-leaf children are all micro leaves): their micro children
-  // mc_list[mc_ptr[s] ..), and per front row (row_ptr[s] + i) the (child k << 5 | update row a)
-  // pairs landing in that row, child order
+  // leaf folding (tree fronts whose pre-leaf children are all micro leaves: w <= 2, r <= 32): the
+  // front factorises its micro leaves in LDS and subtracts their rank-1/2 updates through
+  // destination-sorted product lists, instead of k_micro_factor writing update blocks to HBM and
+  // the gather pre-assembly summing them.  Leaf rows are flattened per front in child order (ab_*);
+  // the leaves are cut into batches whose rows fit LDS beside the front.  Per batch the products
+  // (F(i, j) -= l(q1) . p(q2) over the two leaf columns, p = l d) are sorted by LDS destination
+  // (leaf order within one destination), cut into 256 chunks at destination boundaries and stored
+  // interleaved (entry k of thread t at fold_poff + 256 k + t) so each load instruction is coalesced.
   static constexpr int64_t kFactTreeLdsMax = 150 * 1024;  // dynamic LDS of k_fact_tree
-  static constexpr int kAbsorbRows = 512, kAbsorbLeaves = 128;  // per absorption batch
-  static constexpr int kAbsorbEntries = 4096;                   // row-list entries per front (LDS)
-  // batch staging in LDS: l0, l1 (8 B each) + column base, leaf, parent row, heavy flag (4 B each) per
-  // row; d0, d1, f10, l_off (8 B each) + first update row, w, rc, end row (4 B each) per leaf
-  static constexpr int64_t kAbsorbLdsBytes = 32 * kAbsorbRows + 48 * kAbsorbLeaves + 4 * kAbsorbEntries;
-  std::vector<uint8_t> absorb;
-  std::vector<int32_t> mc_ptr, mc_list;
-  std::vector<int64_t> rl_ptr;
-  std::vector<int32_t> rl_ent;        // front-relative flat row of the absorbed update row
-  std::vector<int64_t> fr_ptr, ab_first;  // per front: its flat rows; per absorbed leaf: first flat row
-  std::vector<int32_t> ab_src0, ab_src1, ab_rel, ab_k;  // per flat row
-  std::vector<int32_t> ab_f0, ab_wrc;  // per absorbed leaf: first pivot, w | rc << 8 (l_off: LDLSolver)
-  std::vector<uint8_t> rheavy;        // per front row (row_ptr[s] + i): dense in the absorbed leaves
-  std::vector<int32_t> ab_bptr, ab_bat;  // per front: batch starts (leaf index k) ab_bat[ab_bptr[s] ..)
+  static constexpr int64_t kFoldLdsMax = 148 * 1024;      // fold front + leaf rows (k_fact_tree's
+                                                          // static LDS is ~10.4 KB of the CU's 160 KB)
+  static constexpr int kFoldRowBytes = 36;                // LDS per leaf row: (l0, l1), (l0 d0, l1 d1), leaf
+  static constexpr int kFoldLeafBytes = 48;               // LDS per leaf: d0, d1, f10, L offset, row0, w | rc
+  static constexpr uint32_t kFoldPadDst = 0xffffu;        // destination of a padding entry
+  std::vector<uint8_t> absorb;        // front folds its micro leaves
+  std::vector<uint8_t> fold_pk;       // fold front stored packed in LDS (to leave room for the leaf rows)
+  std::vector<int32_t> mc_ptr, mc_list;  // per front: its folded micro leaves (child order)
+  std::vector<int64_t> ab_first;      // per folded leaf: first flat row (rows of front s are contiguous)
+  std::vector<int32_t> ab_src0, ab_src1, ab_k;  // per flat row: caller's K index of columns 0 / 1, leaf
+  std::vector<int32_t> ab_f0, ab_wrc;  // per folded leaf: first pivot, w | rc << 8 (l_off: LDLSolver)
+  std::vector<int32_t> fold_bptr;     // per front: its batches [fold_bptr[s], fold_bptr[s + 1])
+  std::vector<int32_t> fold_bat;      // per batch: first leaf index (into mc_list)
+  std::vector<int64_t> fold_poff;     // per batch: first product entry
+  std::vector<int32_t> fold_plen;     // per batch: entries per thread
+  std::vector<int32_t> fold_rmax, fold_lmax;  // per front: largest batch (rows, leaves): its LDS carve
+  std::vector<uint32_t> fold_prod;    // 2 words per entry: dst | q1 << 16, q2 (batch-local rows)
   int64_t fs_size = 0;
   // forward-solve gather: for every front row, the children's update-vector entries in child order
   std::vector<int64_t> sv_ptr, sv_src;  // sv_ptr indexed by row_ptr[s] + i

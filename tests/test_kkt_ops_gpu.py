@@ -215,7 +215,7 @@ def test_ldl_either_triangle(which):
     one gives the lower-triangle factorisation's pivots and solution."""
     from helpers import random_k2
     from madipm_amd.linear_solver import HIPLDLSolver
-    K, Lw = random_k2(200, 300, 0.02, 9)
+    K, Lw = random_k2(200, 300, 0.02, 9, well=True)
     N = K.shape[0]
     if which == "upper":
         M = sp.triu(K).tocsc()

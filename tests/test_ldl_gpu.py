@@ -107,15 +107,21 @@ def test_ldl_schur_update_variants(defer, sfm, monkeypatch):
     assert ls.inertia() == (4000, 0, 3000)
 
 
+@pytest.mark.parametrize("fold", ["0", "1"])
 @pytest.mark.parametrize("well", [True, False])
-def test_ldl_leaf_absorption(well, monkeypatch):
-    """Experimental leaf absorption (MADIPM_ABSORB=1): tree fronts factorise their micro-leaf children
-    themselves and add the leaves' updates in LDS (row-owner lists) — same pivots / solution as the
-    oracle."""
-    monkeypatch.setenv("MADIPM_ABSORB", "1")
+def test_ldl_leaf_folding(fold, well, monkeypatch):
+    """Leaf folding (default; MADIPM_FOLD=0 turns it off): tree fronts factorise their micro-leaf
+    children themselves and subtract the leaves' rank-1/2 updates in LDS through destination-sorted
+    product lists — same pivots / solution as the oracle, with and without it."""
+    monkeypatch.setenv("MADIPM_FOLD", fold)
     K, Lw = block_angular_k2(3000, 4000, 20, 7, well=well)
     ls = _check_case(K, Lw, well=well)
     assert ls.inertia() == (4000, 0, 3000)
+    info = ls.info()
+    if fold == "1":
+        assert info["fold_fronts"] >= 1 and info["fold_leaves"] >= 100
+    else:
+        assert info["fold_fronts"] == 0
 
 
 @pytest.mark.parametrize("well", [True, False])
