@@ -11,7 +11,8 @@ from pathlib import Path
 import numpy as np
 
 _HERE = Path(__file__).resolve().parent
-LIB_PATH = _HERE / "lib" / "libmadipm_hip.so"
+# MADIPM_LIB (A/B measurements of build variants) points at another build of the same library
+LIB_PATH = Path(os.environ["MADIPM_LIB"]) if os.environ.get("MADIPM_LIB") else _HERE / "lib" / "libmadipm_hip.so"
 
 if not LIB_PATH.exists():
     raise ImportError(
