@@ -11,7 +11,22 @@ presolve operations of that package, applied to a fixed point:
 * singleton rows a x_j in [l, u]: turned into bounds on x_j and dropped (infeasible when the
   bounds cross);
 * empty columns of an LP-like variable (no A entries, no H entries): fixed at the bound the cost
-  points to (unbounded when that bound is infinite).
+  points to (unbounded when that bound is infinite);
+* free rows (lcon = -Inf, ucon = +Inf): dropped (multiplier 0);
+* unconstrained variables with a diagonal Hessian entry only (no A entries, H_jj > 0): fixed at the
+  minimiser clip(-c_j / H_jj, l_j, u_j);
+* free linear column singletons in an equality row (x_j free, no H entries, one A entry a_ij, row i
+  an equality with right-hand side b_i): x_j = (b_i - sum_k a_ik x_k) / a_ij is substituted into the
+  objective (c0 += c_j b_i / a_ij, c_k -= c_j a_ik / a_ij), row i and column j are dropped, and the
+  row's multiplier is recovered exactly as y_i = -c_j / a_ij (MadNLP's sign convention
+  c + H x + A' y - zl + zu = 0).
+
+Which reductions QuadraticModels.presolve 0.9.14 applies, and in which order, is [EXT, unverified]:
+the package is not vendored and cannot be run here.  The list above restates the operations its
+published presolve module is built from (remove_ifix!, empty_rows!, singleton_rows!, free_rows!,
+unconstrained_variables!, free_linear_singleton_columns!), to a fixed point; parity is pinned on
+optimal objectives (the presolved problem's optimum plus c0 equals the original's:
+tests/test_host_cpu.py presolve tests, AFIRO's netlib optimum).
 
 `postsolve(pre, x, y, zl, zu)` maps a solution of the presolved problem back to the original
 variables and constraints (removed rows get multiplier 0, removed singleton rows the multiplier
@@ -39,6 +54,7 @@ class PresolveInfo:
     keep_con: np.ndarray              # original indices of the surviving rows
     xfix: np.ndarray                  # value of every original variable removed (NaN if kept)
     singleton_rows: list = field(default_factory=list)  # (row, var, a) turned into bounds
+    free_singletons: list = field(default_factory=list)  # (row, var, a_ij, b_i, cols, vals, c_j), removal order
     status: str = "ok"                # "ok" | "infeasible" | "unbounded" | "empty"
 
 
@@ -63,6 +79,7 @@ def presolve(qp: QuadraticModel):
     con_alive = np.ones(m, bool)
     xfix = np.full(n, np.nan)
     singles = []
+    fsing = []
     status = "ok"
     tol = 1e-12
 
@@ -133,10 +150,16 @@ def presolve(qp: QuadraticModel):
                 singles.append((int(i), int(j), float(a)))
                 con_alive[i] = False
             changed = True
+        # free rows: no bound on either side
+        fr = np.flatnonzero(con_alive & np.isneginf(lcon) & np.isposinf(ucon))
+        if len(fr):
+            con_alive[fr] = False
+            changed = True
         # empty columns (no A, no H): fix at the bound the cost points to
         live_e = (Av != 0.0) & var_alive[Ac] & con_alive[Ar]
         ccount = np.bincount(Ac[live_e], minlength=n)
-        hcount = np.bincount(np.concatenate([Hr[Hv != 0.0], Hc[Hv != 0.0]]), minlength=n)
+        hlive = (Hv != 0.0) & var_alive[Hr] & var_alive[Hc]
+        hcount = np.bincount(np.concatenate([Hr[hlive], Hc[hlive]]), minlength=n)
         ec = np.flatnonzero(var_alive & (ccount == 0) & (hcount == 0) & (lvar < uvar))
         if len(ec):
             vals = np.where(c[ec] > 0, lvar[ec], np.where(c[ec] < 0, uvar[ec],
@@ -146,12 +169,55 @@ def presolve(qp: QuadraticModel):
                 break
             fix_vars(ec, vals)
             changed = True
+            continue
+        # unconstrained variables with only a diagonal Hessian entry: fixed at their minimiser
+        hdiag = np.zeros(n)
+        offd = np.zeros(n, bool)
+        dmask = hlive & (Hr == Hc)
+        np.add.at(hdiag, Hr[dmask], Hv[dmask])
+        omask = hlive & (Hr != Hc)
+        offd[Hr[omask]] = True
+        offd[Hc[omask]] = True
+        uc = np.flatnonzero(var_alive & (ccount == 0) & ~offd & (hdiag > 0) & (lvar < uvar))
+        if len(uc):
+            fix_vars(uc, np.clip(-c[uc] / hdiag[uc], lvar[uc], uvar[uc]))
+            changed = True
+            continue
+        # free linear column singletons in equality rows
+        cand = np.flatnonzero(var_alive & (ccount == 1) & (hcount == 0) & np.isneginf(lvar) & np.isposinf(uvar))
+        if len(cand):
+            ecol = {}
+            for k in np.flatnonzero(live_e & (ccount[Ac] == 1)):
+                ecol[int(Ac[k])] = k
+            le = np.flatnonzero(live_e)
+            le = le[np.argsort(Ar[le], kind="stable")]
+            rptr = np.searchsorted(Ar[le], np.arange(m + 1))
+            used_rows = set()
+            for j in cand:
+                k = ecol.get(int(j))
+                if k is None:
+                    continue
+                i, a = int(Ar[k]), float(Av[k])
+                if i in used_rows or not con_alive[i] or lcon[i] != ucon[i] or not np.isfinite(lcon[i]) or abs(a) <= tol:
+                    continue
+                row = le[rptr[i]:rptr[i + 1]]
+                row = row[(Ac[row] != j) & var_alive[Ac[row]]]
+                cols, vals = Ac[row].copy(), Av[row].copy()
+                cj, bi = float(c[j]), float(lcon[i])
+                c0 += cj * bi / a
+                np.add.at(c, cols, -cj * vals / a)
+                fsing.append((i, int(j), a, bi, cols, vals, cj))
+                con_alive[i] = False
+                var_alive[j] = False
+                xfix[j] = np.nan
+                used_rows.add(i)
+                changed = True
     if status == "ok" and not var_alive.any():
         status = "empty"
     keep_var = np.flatnonzero(var_alive)
     keep_con = np.flatnonzero(con_alive)
     info = PresolveInfo(n=n, m=m, keep_var=keep_var, keep_con=keep_con, xfix=xfix, singleton_rows=singles,
-                        status=status)
+                        free_singletons=fsing, status=status)
     if status != "ok":
         return qp, info
     vmap = np.full(n, -1, np.int64)
@@ -176,4 +242,7 @@ def postsolve(info: PresolveInfo, x, y=None):
     yo = np.zeros(info.m)
     if y is not None:
         yo[info.keep_con] = y
+    for i, j, a, b, cols, vals, cj in reversed(info.free_singletons):  # later removals are known first
+        xo[j] = (b - float(np.dot(vals, xo[cols]))) / a
+        yo[i] = -cj / a
     return xo, yo

@@ -254,3 +254,48 @@ def test_presolve_afiro_same_optimum():
     assert flag
     st = OracleMPC(standard_form_qp(new), OracleOptions(regularization=("fixed", 1e-8, -1e-8), max_iter=300)).solve()
     assert st.status == 1 and abs(st.objective + 464.75314286) <= 1e-6 * 464.75
+
+
+def _presolve_case2():
+    """min x0 + 2 x1 + x2^2/2 ... with a free row, a free column singleton in an equality row and an
+    unconstrained quadratic variable:
+       row 0:  x0 + x1 + x3 = 4        (x3 free, column singleton, cost 3)
+       row 1:  x0 - x1 <= 1
+       row 2:  -inf <= x0 + x2 <= inf  (free row)
+       x4: no A entries, H_44 = 2, c4 = -2, bounds [0, 0.5]  -> x4 = 0.5
+    """
+    import numpy as np
+    from madipm_amd.qp import QuadraticModel
+    inf = np.inf
+    return QuadraticModel(
+        c=np.array([1.0, 2.0, 0.5, 3.0, -2.0]), c0=0.25,
+        Hrows=np.array([2, 4]), Hcols=np.array([2, 4]), Hvals=np.array([1.0, 2.0]),
+        Arows=np.array([0, 0, 0, 1, 1, 2, 2]), Acols=np.array([0, 1, 3, 0, 1, 0, 2]),
+        Avals=np.array([1.0, 1.0, 1.0, 1.0, -1.0, 1.0, 1.0]),
+        lcon=np.array([4.0, -inf, -inf]), ucon=np.array([4.0, 1.0, inf]),
+        lvar=np.array([0.0, 0.0, 0.0, -inf, 0.0]), uvar=np.array([3.0, 3.0, 2.0, inf, 0.5]))
+
+
+def test_presolve_free_rows_singleton_columns_unconstrained_quadratic():
+    import numpy as np
+    from madipm_amd import presolve_qp, postsolve
+    from oracle.mpc import OracleMPC, OracleOptions
+    qp = _presolve_case2()
+    new, flag = presolve_qp(qp)
+    assert flag
+    info = new.meta["presolve"]
+    assert 2 not in info.keep_con                      # free row dropped
+    assert 0 not in info.keep_con and 3 not in info.keep_var   # free column singleton + its row
+    assert 4 not in info.keep_var and info.xfix[4] == 0.5      # unconstrained quadratic variable
+    assert len(info.free_singletons) == 1
+    ref = OracleMPC(qp, OracleOptions(max_iter=300)).solve()
+    sol = OracleMPC(new, OracleOptions(max_iter=300)).solve()
+    assert ref.status == sol.status == 1
+    assert abs(sol.objective - ref.objective) <= 1e-7 * max(1.0, abs(ref.objective))
+    xo, yo = postsolve(info, sol.solution, sol.multipliers)
+    assert np.allclose(xo, ref.solution, atol=1e-6)
+    # the recovered row multiplier: stationarity of the free x3 is c3 + a03 y0 = 0
+    assert abs(yo[0] - (-3.0)) <= 1e-12
+    A = np.zeros((3, 5))
+    A[qp.Arows, qp.Acols] = qp.Avals
+    assert abs(A[0] @ xo - 4.0) <= 1e-8
