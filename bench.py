@@ -218,15 +218,30 @@ def iteration_roofline(info: dict, ms_per_step: float, vec_passes: int = 60) -> 
 
 def aggregate(dt, iters, dist, sharded):
     """Whole-job numbers: max time over ranks; iterations = those of the one sharded solve, or the
-    sum over ranks (replicas)."""
+    sum over ranks (replicas).  Also returns every rank's own time (s)."""
     if dist is None:
-        return dt, float(iters)
+        return dt, float(iters), [dt]
     import torch
-    t = torch.tensor([dt], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ts = [torch.zeros(1, dtype=torch.float64) for _ in range(dist.get_world_size())]
+    dist.all_gather(ts, torch.tensor([dt], dtype=torch.float64))
+    per_rank = [float(t.item()) for t in ts]
     it = torch.tensor([float(iters)], dtype=torch.float64)
     dist.all_reduce(it, op=dist.ReduceOp.MAX if sharded else dist.ReduceOp.SUM)
-    return float(t.item()), float(it.item())
+    return max(per_rank), float(it.item()), per_rank
+
+
+def collective_volume(info, warm):
+    """Sharded factorisation: doubles all-reduced per factorisation / per solve (ldl_info xch_*), and
+    per MPC iteration with the solves-per-factorisation ratio seen in the warm-up launch counts."""
+    if not info.get("xch_fact"):
+        return None
+    launches = {k["name"]: k["launches"] for k in warm}
+    nfact = launches.get("k_fact_tree") or launches.get("k_small_blocked") or 1
+    nsolve = launches.get("k_bwd_tree") or launches.get("k_bwd_tiny") or 2 * nfact
+    spf = nsolve / nfact
+    return {"fact_bytes": 8 * info["xch_fact"], "solve_bytes": 8 * info["xch_solve"], "solves_per_fact": spf,
+            "allreduces_per_iter": 1 + 2 * spf,
+            "bytes_per_iter": 8 * (info["xch_fact"] + spf * info["xch_solve"])}
 
 
 def main():
@@ -300,7 +315,7 @@ def main():
     iters = st.iter
     roof = roofline(solver.kernel_stats(), dominant)
     solver.set_kernel_timing(0)
-    dt, total_iters = aggregate(dt, iters, dist, sharded)
+    dt, total_iters, per_rank = aggregate(dt, iters, dist, sharded)
 
     # wall-clock to optimality (the reference's total_time; max_iter 300)
     opt = {}
@@ -335,6 +350,8 @@ def main():
             "roofline": roof,
             "iteration_roofline": iteration_roofline(info, 1e3 * dt / max(iters, 1)),
             "kernel_ms_warmup": breakdown,
+            "per_rank_s": per_rank,
+            "collectives": collective_volume(info, warm),
             "cpu_baseline": None,
             "parity": None,
         }

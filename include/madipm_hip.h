@@ -59,6 +59,9 @@ typedef struct madipm_ldl_info {
   int32_t lb_members;      /* single-column leaf fronts in those groups */
   int32_t fold_fronts;     /* tree fronts that fold their micro leaves (LDS product lists) */
   int32_t fold_leaves;     /* micro leaves folded by them */
+  int64_t xch_fact;        /* sharded: doubles all-reduced per factorisation (top-front lower triangles
+                              + 4 status slots per shard); 0 unsharded */
+  int64_t xch_solve;       /* sharded: doubles all-reduced per solve (two collectives); 0 unsharded */
 } madipm_ldl_info;
 
 void madipm_ldl_default_opts(madipm_ldl_opts* opts);

@@ -141,10 +141,8 @@ int madipm_symbolic_shard_info(madipm_symbolic_t sym, int32_t* owner, double* to
   MADIPM_API_END
 }
 
-int madipm_symbolic_info(madipm_symbolic_t sym, madipm_ldl_info* info) {
-  MADIPM_API_BEGIN
-  MADIPM_REQUIRE(sym && info, "null argument");
-  const SymbolicPlan& p = sym->plan;
+// madipm_ldl_info from a plan (+ the device solver for the exchange sizes, when there is one)
+static void fill_info(const SymbolicPlan& p, const LinSolver* ls, madipm_ldl_info* info) {
   info->n = p.N;
   info->nnzK = p.nnzK;
   info->nnzL = p.nnzL;
@@ -160,6 +158,14 @@ int madipm_symbolic_info(madipm_symbolic_t sym, madipm_ldl_info* info) {
   info->fold_fronts = 0;
   for (uint8_t a : p.absorb) info->fold_fronts += a;
   info->fold_leaves = (int32_t)p.mc_list.size();
+  info->xch_fact = ls ? ls->xch_fact() : 0;
+  info->xch_solve = ls ? ls->xch_solve() : 0;
+}
+
+int madipm_symbolic_info(madipm_symbolic_t sym, madipm_ldl_info* info) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(sym && info, "null argument");
+  fill_info(sym->plan, nullptr, info);
   return 0;
   MADIPM_API_END
 }
@@ -327,22 +333,7 @@ void madipm_comm_destroy(madipm_comm_t c) { delete c; }
 int madipm_ldl_get_info(madipm_ldl_t ls, madipm_ldl_info* info) {
   MADIPM_API_BEGIN
   MADIPM_REQUIRE(ls && info, "null argument");
-  const SymbolicPlan& p = ls->s->plan();
-  info->n = p.N;
-  info->nnzK = p.nnzK;
-  info->nnzL = p.nnzL;
-  info->nnzL_stored = p.nnzL_super;
-  info->flops = p.flops;
-  info->nsuper = p.nsuper;
-  info->nlevels = p.nlevels;
-  info->max_front = p.max_front;
-  info->nbig = p.nbig;
-  info->arena_bytes = p.arena_size * 8 + p.lb_wsize * 8;
-  info->lb_groups = (int32_t)p.lb.size();
-  info->lb_members = (int32_t)p.lb_mem.size();
-  info->fold_fronts = 0;
-  for (uint8_t a : p.absorb) info->fold_fronts += a;
-  info->fold_leaves = (int32_t)p.mc_list.size();
+  fill_info(ls->s->plan(), ls->lin, info);
   return 0;
   MADIPM_API_END
 }
@@ -561,22 +552,7 @@ int madipm_solver_trace(madipm_solver_t s, madipm_iter_trace* out, int32_t cap) 
 int madipm_solver_ldl_info(madipm_solver_t s, madipm_ldl_info* info) {
   MADIPM_API_BEGIN
   MADIPM_REQUIRE(s && info, "null argument");
-  const SymbolicPlan& p = s->s->ldl().plan();
-  info->n = p.N;
-  info->nnzK = p.nnzK;
-  info->nnzL = p.nnzL;
-  info->nnzL_stored = p.nnzL_super;
-  info->flops = p.flops;
-  info->nsuper = p.nsuper;
-  info->nlevels = p.nlevels;
-  info->max_front = p.max_front;
-  info->nbig = p.nbig;
-  info->arena_bytes = p.arena_size * 8 + p.lb_wsize * 8;
-  info->lb_groups = (int32_t)p.lb.size();
-  info->lb_members = (int32_t)p.lb_mem.size();
-  info->fold_fronts = 0;
-  for (uint8_t a : p.absorb) info->fold_fronts += a;
-  info->fold_leaves = (int32_t)p.mc_list.size();
+  fill_info(s->s->ldl().plan(), &s->s->ldl(), info);
   return 0;
   MADIPM_API_END
 }

@@ -2830,6 +2830,21 @@ __global__ void k_pack_status(const LDLStatus* st, double* slots, int shard, int
   slots[4 * q + 3] = me ? (double)st->nzero : 0.0;
 }
 
+// Top-front exchange buffer (sharded factorisation): only the lower triangles of the top fronts
+// (plus the status slots) travel through the all-reduce — half the bytes of the full r x r blocks.
+// One workgroup per top-front column: col[3 c] = arena offset of F(c, c), col[3 c + 1] = packed
+// offset, col[3 c + 2] = length r - c.
+__global__ __launch_bounds__(NT) void k_tri_pack(const int64_t* __restrict__ col, const double* __restrict__ arena,
+                                                 double* __restrict__ xp, int dir) {
+  const int64_t a = col[3 * blockIdx.x], p = col[3 * blockIdx.x + 1], n = col[3 * blockIdx.x + 2];
+  for (int64_t i = threadIdx.x; i < n; i += NT) {
+    if (dir == 0)
+      xp[p + i] = arena[a + i];
+    else
+      const_cast<double*>(arena)[a + i] = xp[p + i];
+  }
+}
+
 __global__ void k_unpack_status(LDLStatus* st, const double* slots, int nshards) {
   double f = (double)INT_MAX, p = 0, ng = 0, z = 0;
   for (int q = 0; q < nshards; ++q) {
@@ -3471,8 +3486,25 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   }
   sched_.upload(sched.empty() ? std::vector<int32_t>{0} : sched);
   arena_.alloc(std::max<int64_t>(S.arena_size, 2));
-  if (S.nshards > 1)  // top fronts: the strict upper triangles are never written, keep them 0 (all-reduced)
+  if (S.nshards > 1) {  // top fronts: the strict upper triangles are never written, keep them 0
     MADIPM_HIP(hipMemset(arena_.p + S.top_lo, 0, sizeof(double) * (S.arena_size - S.top_lo)));
+    // exchange buffer: the top fronts' lower triangles (column by column) + 4 status slots per shard
+    std::vector<int64_t> tc;
+    int64_t po = 0;
+    for (int s = 0; s < ns; ++s)
+      if (S.top(s)) {
+        const int64_t r = S.nrows[s];
+        for (int64_t c = 0; c < r; ++c) {
+          tc.insert(tc.end(), {S.l_off[s] + c * r + c, po, r - c});
+          po += r - c;
+        }
+      }
+    ntopcol_ = (int)(tc.size() / 3);
+    xpack_tri_ = po;
+    topcol_.upload(tc.empty() ? std::vector<int64_t>{0, 0, 0} : tc);
+    xpack_.alloc(po + 4 * S.nshards);
+    xpack_.zero();
+  }
   D_.alloc(std::max(S.N, 1));
   xi_.alloc(std::max(S.N, 1));
   uvec_.alloc(std::max<int64_t>(S.uvec_size, 1));
@@ -3691,12 +3723,18 @@ void LDLSolver::fact_phase1(const double* Kx, hipStream_t s) {
   }
   TIMED(KK_INERTIA, 8.0 * S_.N, 0.0, (k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, st_, spdf, colmask_, 1)));
   k_pack_status<<<1, 64, 0, s>>>(st_, arena_.p + S_.top_hi, S_.shard, S_.nshards);
+  if (ntopcol_) k_tri_pack<<<(unsigned)ntopcol_, NT, 0, s>>>(topcol_, arena_, xpack_, 0);
+  MADIPM_HIP(hipMemcpyAsync(xpack_.p + xpack_tri_, arena_.p + S_.top_hi, sizeof(double) * 4 * S_.nshards,
+                            hipMemcpyDeviceToDevice, s));
   MADIPM_HIP(hipGetLastError());
 }
 
 // Phase 2 (sharded): after the all-reduce of fact_xbuf(), every shard factorises the top fronts.
 void LDLSolver::fact_phase2(hipStream_t s) {
   if (S_.N == 0 || !sharded()) return;
+  if (ntopcol_) k_tri_pack<<<(unsigned)ntopcol_, NT, 0, s>>>(topcol_, arena_, xpack_, 1);
+  MADIPM_HIP(hipMemcpyAsync(arena_.p + S_.top_hi, xpack_.p + xpack_tri_, sizeof(double) * 4 * S_.nshards,
+                            hipMemcpyDeviceToDevice, s));
   k_unpack_status<<<1, 1, 0, s>>>(st_, arena_.p + S_.top_hi, S_.nshards);
   run_fact(fact2_, nullptr, s);
   const int nb = (int)std::min<int64_t>(64, cdiv(S_.N, NT));

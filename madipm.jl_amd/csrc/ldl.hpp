@@ -125,6 +125,9 @@ class LinSolver {
   virtual void set_timing(unsigned mask) = 0;
   virtual void kernel_stats(KernelStat out[]) = 0;
   virtual int n() const = 0;
+  // doubles all-reduced per factorisation / per solve (0 unsharded)
+  virtual int64_t xch_fact() const { return 0; }
+  virtual int64_t xch_solve() const { return 0; }
   bool spd = false;  // Cholesky semantics: any non-positive pivot fails (normal equations)
 };
 
@@ -153,11 +156,13 @@ class LDLSolver : public LinSolver {
   void fact_phase2(hipStream_t s);
   void solve_phase1(double* b, hipStream_t s);
   void solve_phase2(double* b, hipStream_t s);
-  double* fact_xbuf() const { return arena_.p + S_.top_lo; }
-  int64_t fact_xlen() const { return S_.nshards > 1 ? S_.top_hi - S_.top_lo + 4 * S_.nshards : 0; }
+  double* fact_xbuf() const { return xpack_.p; }  // the top fronts' lower triangles + status slots
+  int64_t fact_xlen() const { return S_.nshards > 1 ? xpack_tri_ + 4 * S_.nshards : 0; }
   double* solve_xbuf() const { return xch_.p; }
   int64_t solve_xlen() const { return S_.nshards > 1 ? S_.xlen : 0; }
   bool sharded() const { return S_.nshards > 1; }
+  int64_t xch_fact() const override { return fact_xlen(); }
+  int64_t xch_solve() const override { return sharded() ? solve_xlen() + S_.N : 0; }
 
   const SymbolicPlan& plan() const override { return S_; }
   int n() const override { return S_.N; }
@@ -252,6 +257,10 @@ class LDLSolver : public LinSolver {
   DBuf<int32_t> mc_ptr_;
   DBuf<uint32_t> fold_prod_;
   DBuf<double> xch_;
+  DBuf<double> xpack_;     // sharded: packed top-front lower triangles (+ status slots), all-reduced
+  DBuf<int64_t> topcol_;   // per top-front column: arena offset, packed offset, length
+  int ntopcol_ = 0;
+  int64_t xpack_tri_ = 0;
   DBuf<uint8_t> wout_, colmask_;
   DBuf<int32_t> tasks_, flags_, flag_off_, counters_, bp_off_;
   DBuf<double> bpart_;
@@ -302,6 +311,8 @@ class ShardGroup : public LinSolver {
   void set_timing(unsigned mask) override { sh_[0]->set_timing(mask); }
   void kernel_stats(KernelStat out[]) override { sh_[0]->kernel_stats(out); }
   int n() const override { return sh_[0]->n(); }
+  int64_t xch_fact() const override { return sh_[0]->xch_fact(); }
+  int64_t xch_solve() const override { return sh_[0]->xch_solve(); }
   LDLSolver& shard(int r) { return *sh_[r]; }
   int nshards() const { return (int)sh_.size(); }
 

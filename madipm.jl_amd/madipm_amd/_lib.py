@@ -37,7 +37,8 @@ class LDLInfo(C.Structure):
                 ("flops", C.c_double), ("nsuper", C.c_int32), ("nlevels", C.c_int32),
                 ("max_front", C.c_int32), ("nbig", C.c_int32), ("arena_bytes", C.c_int64),
                 ("lb_groups", C.c_int32), ("lb_members", C.c_int32),
-                ("fold_fronts", C.c_int32), ("fold_leaves", C.c_int32)]
+                ("fold_fronts", C.c_int32), ("fold_leaves", C.c_int32),
+                ("xch_fact", C.c_int64), ("xch_solve", C.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -24,11 +24,11 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import bench
     dt, iters = 0.5 + rank, 10 + rank          # rank-local timing and iteration count
-    tot_dt, tot_it = bench.aggregate(dt, iters, dist, False)
-    sh_dt, sh_it = bench.aggregate(dt, 22, dist, True)
+    tot_dt, tot_it, per_rank = bench.aggregate(dt, iters, dist, False)
+    sh_dt, sh_it, _ = bench.aggregate(dt, 22, dist, True)
     box = [bytes(range(128)) if rank == 0 else None]
     dist.broadcast_object_list(box, src=0)
-    q.put((rank, tot_dt, tot_it, sh_dt, sh_it, box[0] == bytes(range(128))))
+    q.put((rank, tot_dt, tot_it, sh_dt, sh_it, box[0] == bytes(range(128)), per_rank))
     dist.destroy_process_group()
 
 
@@ -43,8 +43,18 @@ def test_two_rank_aggregation():
     for p in procs:
         p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs)
-    for rank, tot_dt, tot_it, sh_dt, sh_it, id_ok in res:
+    for rank, tot_dt, tot_it, sh_dt, sh_it, id_ok, per_rank in res:
+        assert per_rank == pytest.approx([0.5, 1.5])  # every rank's own time, in rank order
         assert tot_dt == pytest.approx(1.5)     # max over ranks
         assert tot_it == 21                     # replicas: sum over ranks
         assert sh_dt == pytest.approx(1.5) and sh_it == 22  # sharded: one solve's iterations
         assert id_ok
+
+
+def test_collective_volume():
+    import bench
+    assert bench.collective_volume({"xch_fact": 0, "xch_solve": 0}, []) is None
+    warm = [{"name": "k_fact_tree", "launches": 3}, {"name": "k_bwd_tree", "launches": 9}]
+    v = bench.collective_volume({"xch_fact": 1000, "xch_solve": 300}, warm)
+    assert v["solves_per_fact"] == 3 and v["allreduces_per_iter"] == 7
+    assert v["fact_bytes"] == 8000 and v["solve_bytes"] == 2400 and v["bytes_per_iter"] == 8 * (1000 + 3 * 300)

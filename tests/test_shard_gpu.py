@@ -70,6 +70,12 @@ def test_phase_protocol_with_separate_shards():
     vals = torch.from_numpy(Lw.data.copy()).to(DEV)
     bufs = [s.factorize_phase(1, vals) for s in sh]
     assert len({ln for _, ln in bufs}) == 1 and bufs[0][1] > 0
+    # the exchange carries only the top fronts' lower triangles + 4 status slots per shard
+    from madipm_amd._lib import Symbolic, default_ldl_opts
+    _, _, nrows = Symbolic(N, Lw.indptr, Lw.indices, default_ldl_opts(), nshards=P, shard=0).supernodes()
+    r = nrows[sh[0].shard_info()["owner"] == -1].astype(np.int64)
+    assert bufs[0][1] == (r * (r + 1) // 2).sum() + 4 * P == sh[0].info()["xch_fact"]
+    assert sh[0].info()["xch_solve"] > N
     local_allreduce([p for p, _ in bufs], bufs[0][1])
     for s in sh:
         s.factorize_phase(2)
