@@ -116,6 +116,13 @@ __device__ __forceinline__ void stage_panel(const double* __restrict__ L, double
 }
 
 __global__ void k_status_init(LDLStatus* st, int all = 0) {
+  const uint64_t now = wall_clock64();
+  if (all) {
+    st->ticks = 0;
+  } else if (st->t1 > st->t0) {
+    st->ticks += st->t1 - st->t0;  // the previous factorisation
+  }
+  st->t0 = st->t1 = now;
   st->fail_pivot = INT_MAX;
   st->npos = st->nneg = st->nzero = 0;
   if (all) st->err = 0;
@@ -1823,6 +1830,7 @@ __global__ __launch_bounds__(NT) void k_inertia(const double* __restrict__ D, in
     for (int q = 0; q < NT / 64; ++q) v += red[threadIdx.x][q];
     atomicAdd(threadIdx.x == 0 ? &st->npos : (threadIdx.x == 1 ? &st->nneg : &st->nzero), v);
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && want != 1) st->t1 = wall_clock64();  // end of the factorisation
 }
 
 // ------------------------------------------------------------------ batched leaf columns (SymbolicPlan::lb)
@@ -3759,6 +3767,18 @@ bool LDLSolver::external_status(LDLStatus* dev, LDLStatus* host) {
   k_status_init<<<1, 1, 0, nullptr>>>(st_, 1);
   MADIPM_HIP(hipDeviceSynchronize());
   return true;
+}
+
+double LDLSolver::fact_seconds(hipStream_t s) {
+  if (S_.N == 0) return 0.0;
+  LDLStatus h;
+  MADIPM_HIP(hipMemcpyAsync(&h, st_, sizeof(LDLStatus), hipMemcpyDeviceToHost, s));
+  MADIPM_HIP(hipStreamSynchronize(s));
+  int dev = 0, khz = 0;
+  MADIPM_HIP(hipGetDevice(&dev));
+  MADIPM_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+  const uint64_t t = h.ticks + (h.t1 > h.t0 ? h.t1 - h.t0 : 0);
+  return khz > 0 ? (double)t / (1e3 * khz) : 0.0;
 }
 
 int LDLSolver::status(hipStream_t s, bool sync) {

@@ -77,6 +77,10 @@ struct LDLStatus {  // device-resident, read back by status()
   int32_t fail_pivot;  // min failing internal pivot + 1 (INT32_MAX when none)
   int32_t npos, nneg, nzero;
   int32_t err;  // sticky: a dependency hand-off (flag poll) timed out in a factorisation or solve
+  int32_t pad_;
+  // device wall clock (wall_clock64, hipDeviceAttributeWallClockRate): t0 at the start of the latest
+  // factorisation, t1 at its end; ticks = the sum over the earlier ones (folded in by the next start)
+  uint64_t t0, t1, ticks;
 };
 
 // Kernel kinds for the live per-kernel timing (HIP events around each launch on the launch
@@ -128,6 +132,8 @@ class LinSolver {
   // doubles all-reduced per factorisation / per solve (0 unsharded)
   virtual int64_t xch_fact() const { return 0; }
   virtual int64_t xch_solve() const { return 0; }
+  // seconds of device time spent in factorisations so far (synchronises s; cnt.linear_solver_time)
+  virtual double fact_seconds(hipStream_t s) = 0;
   bool spd = false;  // Cholesky semantics: any non-positive pivot fails (normal equations)
 };
 
@@ -163,6 +169,7 @@ class LDLSolver : public LinSolver {
   bool sharded() const { return S_.nshards > 1; }
   int64_t xch_fact() const override { return fact_xlen(); }
   int64_t xch_solve() const override { return sharded() ? solve_xlen() + S_.N : 0; }
+  double fact_seconds(hipStream_t s) override;
 
   const SymbolicPlan& plan() const override { return S_; }
   int n() const override { return S_.N; }
@@ -313,6 +320,7 @@ class ShardGroup : public LinSolver {
   int n() const override { return sh_[0]->n(); }
   int64_t xch_fact() const override { return sh_[0]->xch_fact(); }
   int64_t xch_solve() const override { return sh_[0]->xch_solve(); }
+  double fact_seconds(hipStream_t s) override { return sh_[0]->fact_seconds(s); }
   LDLSolver& shard(int r) { return *sh_[r]; }
   int nshards() const { return (int)sh_.size(); }
 

@@ -14,7 +14,8 @@
 //   init_starting_point!  src/solver.jl:6-125 -> k_init_kkt, k_rhs(INIT_*), k_zinit, k_zshift1/2
 // Reductions are two-pass (per-block partials, then one finalising block in fixed order), so every
 // scalar is bitwise reproducible run to run; all scalars stay on the device and the host reads one
-// 200-byte state block per iteration (one hipStreamSynchronize, overlapped with the factorisation).
+// 200-byte state block per iteration (published by k_publish into coherent host memory; the host
+// spins on its counter, overlapped with the factorisation and the speculated directions).
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -45,7 +46,7 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int NPART = 16;
-constexpr int MAXB = 4096;  // partial-reduction blocks (part_ holds NPART x MAXB, value-major)
+constexpr int MAXB = 2048;  // partial-reduction blocks (part_ holds NPART x MAXB, value-major)
 // partial k of block b: value-major so k_final's loads of one value are coalesced
 __device__ __forceinline__ int pidx(int b, int k) { return k * MAXB + b; }
 constexpr double INF = std::numeric_limits<double>::infinity();
@@ -676,73 +677,43 @@ struct FinParams {
   double a, b, c;  // kind-specific parameters
 };
 
-// Per-wave partial reduction of up to 8 values over nb block partials: every load of the thread
-// (J rows x 8 values) is issued before the first is combined (one memory round trip), the 8 value
-// chains are reduced side by side; fixed order (thread t takes blocks t, t + NT, ..., then a fixed
-// shuffle tree), so the result is bitwise reproducible.
-template <int J>
-__device__ __forceinline__ void final_partials(const DV& D, int nb, int nv, const int (&ops)[NPART],
-                                               double (&sh)[NPART][NT / 64]) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  double pv[8][J];
-#pragma unroll
-  for (int k = 0; k < 8; ++k)
-#pragma unroll
-    for (int j = 0; j < J; ++j) pv[k][j] = D.part[pidx(min((int)threadIdx.x + j * NT, nb - 1), k)];
-  double a[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int op = ops[k < nv ? k : 0];
-    a[k] = 0.0;  // every reduction here starts at 0.0 (sum, max, and min with init 0)
-#pragma unroll
-    for (int j = 0; j < J; ++j)
-      if ((int)threadIdx.x + j * NT < nb) a[k] = comb(a[k], pv[k][j], op);
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) a[k] = comb(a[k], __shfl_down(a[k], o, 64), ops[k < nv ? k : 0]);
-  if (lane == 0)
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (k < nv) sh[k][wv] = a[k];
+// k_final runs as ONE block of NTF threads that reads every partial in a single memory round trip:
+// thread t owns blocks 2t, 2t + 1 (one 16-B load per value; nb <= MAXB = 2 NTF), so all nv x 16 B of
+// a thread are in flight together (a one-block reader is bound by its bytes in flight, not by HBM).
+// Fixed combine order (pair, then a shuffle tree, then the waves in order): bitwise reproducible.
+// (Finalising inside the producing kernel instead — block 0 polling per-block flags, or a ticket —
+// measured slower on ex10: the in-launch hand-off costs more than this launch.)
+constexpr int NTF = 1024;
+static_assert(MAXB == 2 * NTF, "k_final: two partial rows per thread");
+
+__device__ __forceinline__ double2 part2(const DV& D, int b, int k) {
+  return *reinterpret_cast<const double2*>(D.part + pidx(b, k));
 }
 
-// Finalise two-pass reductions in fixed block order + scalar logic (one block).
-__global__ __launch_bounds__(NT) void k_final(DV D, int kind, FinParams P) {
+// Combine the block partials in fixed order + scalar logic (one block of NTF threads).
+__global__ __launch_bounds__(NTF) void k_final(DV D, int kind, FinParams P) {
   __shared__ double res[NPART];
-  __shared__ double sh[NPART][NT / 64];
-  __shared__ int shi[4][NT / 64];
+  __shared__ double sh[8][NTF / 64];
+  __shared__ int shi[4][NTF / 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int b0 = 2 * threadIdx.x;
+  const bool h0 = b0 < P.nb, h1 = b0 + 1 < P.nb;
   DevState* st = D.st;
   if (kind == FIN_ALPHA) {
     double v[4];
     int ix[4];
+    double2 pv[4], pi[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      pv[k] = h0 ? part2(D, b0, k) : make_double2(INF, INF);
+      pi[k] = h0 ? part2(D, b0, 4 + k) : make_double2(-1.0, -1.0);
+    }
+#pragma unroll
     for (int k = 0; k < 4; ++k) {
       v[k] = INF;
       ix[k] = -1;
-    }
-    // all of a thread's partials are loaded before they are combined (independent loads in flight);
-    // combined in fixed block order
-    {
-      // up to 4 partial rows per thread (alpha reductions have nb <= MAXB / 4 = 1024 blocks
-      // of bound entries in practice; more rows fall back to a loop)
-      for (int j0 = 0; j0 * NT < P.nb; j0 += 4) {
-        double pv[4][4], pi[4][4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int b = min((int)threadIdx.x + (j0 + j) * NT, P.nb - 1);
-            pv[k][j] = D.part[pidx(b, k)];
-            pi[k][j] = D.part[pidx(b, 4 + k)];
-          }
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if ((int)threadIdx.x + (j0 + j) * NT < P.nb) amin_upd(v[k], ix[k], pv[k][j], (int)pi[k][j]);
-      }
+      if (h0) amin_upd(v[k], ix[k], pv[k].x, (int)pi[k].x);
+      if (h1) amin_upd(v[k], ix[k], pv[k].y, (int)pi[k].y);
     }
     for (int o = 32; o > 0; o >>= 1)
 #pragma unroll
@@ -751,14 +722,12 @@ __global__ __launch_bounds__(NT) void k_final(DV D, int kind, FinParams P) {
         const int b2 = __shfl_down(ix[k], o, 64);
         amin_upd(v[k], ix[k], a2, b2);
       }
-    for (int k = 0; k < 4; ++k) {
-      const double a = v[k];
-      const int bi = ix[k];
-      if (lane == 0) {
-        sh[k][wv] = a;
-        shi[k][wv] = bi;
+    if (lane == 0)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        sh[k][wv] = v[k];
+        shi[k][wv] = ix[k];
       }
-    }
     __syncthreads();
     if (threadIdx.x == 0) {
       double a[4];
@@ -766,7 +735,7 @@ __global__ __launch_bounds__(NT) void k_final(DV D, int kind, FinParams P) {
       for (int k = 0; k < 4; ++k) {
         a[k] = sh[k][0];
         ii[k] = shi[k][0];
-        for (int w = 1; w < NT / 64; ++w) amin_upd(a[k], ii[k], sh[k][w], shi[k][w]);
+        for (int w = 1; w < NTF / 64; ++w) amin_upd(a[k], ii[k], sh[k][w], shi[k][w]);
         // mapreduce init (1.0, 0): alpha = min(1, min ratio)
         if (!(a[k] < 1.0)) {
           a[k] = 1.0;
@@ -809,32 +778,25 @@ __global__ __launch_bounds__(NT) void k_final(DV D, int kind, FinParams P) {
     case FIN_ZSHIFT2: nv = 1; ops[0] = OP_SUM; break;
   }
   {
-    const int J = (P.nb + NT - 1) / NT;  // partial rows per thread
-    if (J <= 1) {
-      final_partials<1>(D, P.nb, nv, ops, sh);
-    } else if (J <= 2) {
-      final_partials<2>(D, P.nb, nv, ops, sh);
-    } else if (J <= 4) {
-      final_partials<4>(D, P.nb, nv, ops, sh);
-    } else {  // many partial rows: one value at a time (16 loads in flight, no register blow-up)
-      for (int k = 0; k < nv; ++k) {
-        double a = 0.0;
-        double pv[MAXB / NT];
+    double2 pv[8];
 #pragma unroll
-        for (int j = 0; j < MAXB / NT; ++j) pv[j] = D.part[pidx(min((int)threadIdx.x + j * NT, P.nb - 1), k)];
+    for (int k = 0; k < 8; ++k) pv[k] = (h0 && k < nv) ? part2(D, b0, k) : make_double2(0.0, 0.0);
 #pragma unroll
-        for (int j = 0; j < MAXB / NT; ++j)
-          if ((int)threadIdx.x + j * NT < P.nb) a = comb(a, pv[j], ops[k]);
-        for (int o = 32; o > 0; o >>= 1) a = comb(a, __shfl_down(a, o, 64), ops[k]);
-        if (lane == 0) sh[k][wv] = a;
-      }
+    for (int k = 0; k < 8; ++k) {
+      if (k >= nv) break;
+      const int op = ops[k];
+      double a = 0.0;  // every reduction here starts at 0.0 (sum, max, and min with init 0)
+      if (h0) a = comb(a, pv[k].x, op);
+      if (h1) a = comb(a, pv[k].y, op);
+      for (int o = 32; o > 0; o >>= 1) a = comb(a, __shfl_down(a, o, 64), op);
+      if (lane == 0) sh[k][wv] = a;
     }
   }
   __syncthreads();
   if (threadIdx.x < nv) {
     const int k = threadIdx.x;
     double a = sh[k][0];
-    for (int w = 1; w < NT / 64; ++w) a = comb(a, sh[k][w], ops[k]);
+    for (int w = 1; w < NTF / 64; ++w) a = comb(a, sh[k][w], ops[k]);
     res[k] = a;
   }
   __syncthreads();
@@ -924,6 +886,20 @@ __global__ __launch_bounds__(NT) void k_final(DV D, int kind, FinParams P) {
   }
 }
 
+// publish the device state to the host mirror: payload with system-scope stores, drained and
+// released, then the counter (one wave; the host spins on the counter, MPCSolver::wait_state)
+static_assert(sizeof(DevState) % 8 == 0 && sizeof(DevState) <= 64 * 8, "k_publish: one word per lane");
+__global__ void k_publish(const DevState* __restrict__ st, DevState* host, uint32_t* hseq, uint32_t seq) {
+  const int i = threadIdx.x;
+  if (i < (int)(sizeof(DevState) / 8))
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(host) + i, reinterpret_cast<const uint64_t*>(st)[i],
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (i == 0) __hip_atomic_store(hseq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ void k_copy(double* __restrict__ dst, const double* __restrict__ src, int64_t n) {
   GRID_LOOP(i, n) dst[i] = src[i];
 }
@@ -965,8 +941,6 @@ double now() {
 // ======================================================================= host side
 
 MPCSolver::~MPCSolver() {
-  for (auto e : fact_events_) (void)hipEventDestroy(e);
-  if (ev_state_) (void)hipEventDestroy(ev_state_);
   if (hst_) (void)hipHostFree(hst_);
   if (stream_) (void)hipStreamDestroy(stream_);
 }
@@ -1008,9 +982,11 @@ static void csr_from_coo(int nrow, const std::vector<int32_t>& r, const std::vec
 MPCSolver::MPCSolver(const madipm_qp& qp, const madipm_options& opt, Comm* comm) : opt_(opt), comm_(comm) {
   const double t0 = now();
   MADIPM_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-  MADIPM_HIP(hipEventCreateWithFlags(&ev_state_, hipEventDisableTiming));
-  MADIPM_HIP(hipHostMalloc((void**)&hst_, sizeof(DevState), hipHostMallocDefault));
-  std::memset(hst_, 0, sizeof(DevState));
+  // state mirror + publication counter on their own line: coherent host memory, written by k_publish
+  constexpr size_t seq_off = (sizeof(DevState) + 63) / 64 * 64;
+  MADIPM_HIP(hipHostMalloc((void**)&hst_, seq_off + 64, hipHostMallocCoherent));
+  std::memset((void*)hst_, 0, seq_off + 64);
+  hseq_ = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(hst_) + seq_off);
   setup_host(qp);
   t_init_ = now() - t0;
 }
@@ -1497,17 +1473,7 @@ const double* MPCSolver::kvals() const { return kkt_ == KKT_NORMAL ? Cx_.p : Kx_
 // factorize! between two pooled timing events (cnt.linear_solver_time, MadNLP.factorize_wrapper!);
 // the pool grows only when a solve needs more pairs than any earlier one did
 void MPCSolver::timed_factorize() {
-  if (nfev_ + 2 > fact_events_.size()) {
-    for (int q = 0; q < 64; ++q) {
-      hipEvent_t e;
-      MADIPM_HIP(hipEventCreate(&e));
-      fact_events_.push_back(e);
-    }
-  }
-  MADIPM_HIP(hipEventRecord(fact_events_[nfev_], stream_));
   ldl_->factorize_async(kvals(), stream_);
-  MADIPM_HIP(hipEventRecord(fact_events_[nfev_ + 1], stream_));
-  nfev_ += 2;
 }
 
 void MPCSolver::factor_enqueue(double dw, double dc) {
@@ -1545,7 +1511,7 @@ void MPCSolver::launch_reduce_final(int kind, int nb) {
   } else if (kind == FIN_RESID) {
     P.a = opt_.check_residual ? opt_.tol_linear_solve : 0.0;
   }
-  k_final<<<1, NT, 0, stream_>>>(D, kind, P);
+  k_final<<<1, NTF, 0, stream_>>>(D, kind, P);
 }
 
 // solve_system! (linear_solver.jl:19-44): rhs (mode) -> LDL^T solve -> finish + residual
@@ -1567,9 +1533,9 @@ void MPCSolver::gondzio() {
   auto ftb = [&](double& ap, double& ad) {  // get_fraction_to_boundary_step(solver, tau)
     k_alpha<<<nbz, NT, 0, s>>>(D, ALPHA_GONDZIO, tau);
     FinParams P{nbz, ALPHA_GONDZIO, 0, 0, 0};
-    k_final<<<1, NT, 0, s>>>(D, FIN_ALPHA, P);
+    k_final<<<1, NTF, 0, s>>>(D, FIN_ALPHA, P);
     read_state();
-    MADIPM_HIP(hipStreamSynchronize(s));
+    wait_state();
     ap = hst_->alpha_aff_p;
     ad = hst_->alpha_aff_d;
   };
@@ -1580,7 +1546,7 @@ void MPCSolver::gondzio() {
     k_mu<<<nbz, NT, 0, s>>>(D, 0, tap, tad);
     launch_reduce_final(FIN_MU_GONDZIO, nbz);
     read_state();
-    MADIPM_HIP(hipStreamSynchronize(s));
+    wait_state();
     const double ga = hst_->mu_aff, g = hst_->mu_curr;
     const double mu = (ga / g) * (ga / g) * ga;  // Eq. (12)
     k_extra_corr<<<nbz, NT, 0, s>>>(D, tap, tad, bmin * mu, bmax * mu);
@@ -1598,7 +1564,24 @@ void MPCSolver::gondzio() {
 }
 
 void MPCSolver::read_state() {
-  MADIPM_HIP(hipMemcpyAsync(hst_, st_.p, sizeof(DevState), hipMemcpyDeviceToHost, stream_));
+  k_publish<<<1, 64, 0, stream_>>>(st_, hst_, hseq_, ++pub_seq_);
+  MADIPM_HIP(hipGetLastError());
+}
+
+// Host spin on the publication counter (no event record in the stream: each one costs a ~5 us
+// bubble between kernels); bounded, and a failed stream surfaces as its HIP error.
+void MPCSolver::wait_state() {
+  const double t0 = now();
+  for (uint64_t spin = 0;; ++spin) {
+    if (__atomic_load_n(hseq_, __ATOMIC_ACQUIRE) == pub_seq_) return;
+    if ((spin & 1023) == 1023) {
+      const hipError_t e = hipStreamQuery(stream_);
+      if (e != hipSuccess && e != hipErrorNotReady) MADIPM_HIP(e);
+      if (e == hipSuccess && __atomic_load_n(hseq_, __ATOMIC_ACQUIRE) != pub_seq_)
+        throw Error("state publication lost (stream idle, counter not updated)", -5);
+      if (now() - t0 > 600.0) throw Error("state publication: timed out", -5);
+    }
+  }
 }
 
 void MPCSolver::init_starting_point() {
@@ -1632,7 +1615,7 @@ void MPCSolver::init_starting_point() {
   k_zshift2<<<nbn, NT, 0, s>>>(D, opt_.bound_fac);
   launch_reduce_final(FIN_ZSHIFT2, nbn);
   read_state();
-  MADIPM_HIP(hipStreamSynchronize(s));
+  wait_state();
   if (hst_->nan_flag) throw Error("SolveException in init_starting_point!", -4);
   MADIPM_REQUIRE(hst_->init_viol == 0.0, "init_starting_point!: interior assertion failed");
 }
@@ -1651,7 +1634,7 @@ void MPCSolver::initialize() {
     d_.zero(s);
     p_.zero(s);
   }
-  nfev_ = 0;
+  fs0_ = ldl_->fact_seconds(s);
   // init_regularization! (kernels.jl:364-392)
   switch (opt_.regularization) {
     case 0: del_w_ = 1.0; del_c_ = 0.0; break;
@@ -1699,7 +1682,7 @@ void MPCSolver::directions(bool redo) {
   k_alpha<<<nbz, NT, 0, s>>>(D, ALPHA_PRED, 1.0);
   {
     FinParams P{nbz, ALPHA_PRED, 0, 0, 0};
-    k_final<<<1, NT, 0, s>>>(D, FIN_ALPHA, P);
+    k_final<<<1, NTF, 0, s>>>(D, FIN_ALPHA, P);
   }
   // mu_affine at (alpha_aff_p, alpha_aff_d) and mu_curr; the alphas never leave the device
   k_mu<<<nbz, NT, 0, s>>>(D, 1, 0.0, 0.0);
@@ -1715,14 +1698,14 @@ void MPCSolver::step_size() {
   if (opt_.step_rule == 2) {
     k_alpha<<<nbz, NT, 0, s>>>(D, ALPHA_MEHROTRA, 1.0);
     FinParams P{nbz, ALPHA_MEHROTRA, 0, 0, 0};
-    k_final<<<1, NT, 0, s>>>(D, FIN_ALPHA, P);
+    k_final<<<1, NTF, 0, s>>>(D, FIN_ALPHA, P);
     k_mu<<<nbz, NT, 0, s>>>(D, 1, 0.0, 0.0);
     launch_reduce_final(FIN_MU_FULL, nbz);
   } else {
     const int mode = opt_.step_rule == 0 ? ALPHA_CONSERVATIVE : ALPHA_ADAPTIVE;
     k_alpha<<<nbz, NT, 0, s>>>(D, mode, opt_.step_tau);
     FinParams P{nbz, mode, 0, 0, 0};
-    k_final<<<1, NT, 0, s>>>(D, FIN_ALPHA, P);
+    k_final<<<1, NTF, 0, s>>>(D, FIN_ALPHA, P);
   }
 }
 
@@ -1753,23 +1736,24 @@ int MPCSolver::solve(madipm_stats* stats) {
           del_w_ = adapt_dp_;
           del_c_ = adapt_dd_;
       }
-      // first trial enqueued together with the state read-back: ONE sync per iteration
-      factor_enqueue(del_w_, del_c_);
+      // first trial enqueued together with the state read-back: ONE sync per iteration.  At
+      // k >= max_iter the termination test ends the solve whatever it finds: nothing to speculate.
+      const bool last = k_ >= opt_.max_iter;
+      if (!last) factor_enqueue(del_w_, del_c_);
       read_state();
-      MADIPM_HIP(hipEventRecord(ev_state_, s));
       // speculation: this iteration's directions (prediction_step!, mehrotra_correction_direction!,
       // update_step_size!) are enqueued BEFORE the host reads the termination test and the
       // factorisation status, so the GPU is busy while the host decides; they write scratch vectors
       // and step scalars only (the iterate is updated by k_apply, enqueued after the decision), are
       // discarded on termination and recomputed after a failed factorisation's retries.  Gondzio's
       // loop synchronises internally: not speculated.
-      const bool spec = opt_.max_ncorr == 0;
+      const bool spec = opt_.max_ncorr == 0 && !last;
       if (spec) {
         directions(false);
         step_size();
       }
-      MADIPM_HIP(hipEventSynchronize(ev_state_));
-      const int frc = ldl_->status(s, false);
+      wait_state();
+      const int frc = last ? 0 : ldl_->status(s, false);
       const DevState& h = *hst_;
       last_ = h;
       if (h.nan_flag) {
@@ -1855,17 +1839,13 @@ int MPCSolver::solve(madipm_stats* stats) {
   MADIPM_HIP(hipStreamSynchronize(s));
   t_total_ = now() - tstart;
   status_ = status;
-  t_linsol_ = 0;
-  for (size_t q = 0; q + 1 < nfev_; q += 2) {
-    float ms = 0;
-    if (hipEventElapsedTime(&ms, fact_events_[q], fact_events_[q + 1]) == hipSuccess) t_linsol_ += ms * 1e-3;
-  }
+  t_linsol_ = ldl_->fact_seconds(s) - fs0_;
   if (stats) {
     // the state read at the last termination test (the speculated directions after it changed only
     // step scalars, never the iterate)
     if (trace_.empty()) {
       read_state();
-      MADIPM_HIP(hipStreamSynchronize(s));
+      wait_state();
       last_ = *hst_;
     }
     stats->status = status;

@@ -65,7 +65,8 @@ class MPCSolver {
   void directions(bool redo);  // predictor + corrector directions (speculated before the status read)
   void step_size();
   void launch_reduce_final(int kind, int nvals);
-  void read_state();
+  void read_state();  // enqueue the publication of the device state to the host mirror
+  void wait_state();  // wait (host spin) until the last publication has landed
   void kkt_diag(double dw, double dc);
   // build_kkt!: diagonal (+ K2.5 scaling / normal-matrix assembly) -> values handed to the LDL^T
   void assemble_kkt(double dw, double dc);
@@ -104,7 +105,9 @@ class MPCSolver {
   DBuf<int64_t> cpp_;
   int64_t nnzC_ = 0;
   DBuf<DevState> st_;
-  DevState* hst_ = nullptr;
+  DevState* hst_ = nullptr;          // host mirror of st_ (coherent pinned memory, written by k_publish)
+  uint32_t* hseq_ = nullptr;         // publication counter beside it
+  uint32_t pub_seq_ = 0;
   // host scalars (MPCSolver fields of src/structure.jl:62-76)
   double del_w_ = 0, del_c_ = 0, norm_b_ = 0, norm_c_ = 0, best_compl_ = 0, obj_scale_ = 1, c0s_ = 0;
   double adapt_dp_ = 0, adapt_dd_ = 0, adapt_dmin_ = 0;
@@ -113,9 +116,7 @@ class MPCSolver {
   double inf_pr_ = 0, inf_du_ = 0, inf_compl_ = 0;
   double t_init_ = 0, t_total_ = 0, t_linsol_ = 0;
   std::vector<madipm_iter_trace> trace_;
-  std::vector<hipEvent_t> fact_events_;  // pool of (begin, end) pairs around each factorize!
-  size_t nfev_ = 0;                      // events of the current solve
-  hipEvent_t ev_state_ = nullptr;  // recorded after the per-iteration state read-back
+  double fs0_ = 0;  // device factorisation seconds at initialize! (cnt.linear_solver_time origin)
   DevState last_{};                // the state of the last termination test
 };
 

@@ -221,3 +221,16 @@ def test_dense_qp_batched_leaves():
     assert gpu.status == ref.status == 1
     assert abs(gpu.iter - ref.iter) <= 1
     assert abs(gpu.objective - ref.objective) <= 1e-6 * max(1.0, abs(ref.objective))
+
+
+@pytest.mark.parametrize("max_iter", [0, 1, 4])
+def test_max_iter_stop(max_iter):
+    """MAXIMUM_ITERATIONS_EXCEEDED after exactly max_iter steps (the last termination test enqueues no
+    speculative factorisation), same iterate as the oracle: objective and trace agree early."""
+    import os
+    from madipm_amd import read_mps, FixedRegularization, MAXIMUM_ITERATIONS_EXCEEDED
+    qp = read_mps(os.path.join(os.path.dirname(__file__), "golden", "afiro.mps"))
+    gpu, ref = _compare(qp, early=min(max_iter, 2), iter_slack=0,
+                        regularization=FixedRegularization(1e-8, -1e-8), max_iter=max_iter)
+    assert gpu.status == MAXIMUM_ITERATIONS_EXCEEDED and gpu.iter == max_iter
+    assert len(gpu.trace) == max_iter + 1
