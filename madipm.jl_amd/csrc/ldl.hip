@@ -12,6 +12,8 @@
 // Quasi-definite KKT matrices (FixedRegularization(1e-8,-1e-8)) admit static
 // pivoting in any symmetric order; zero / non-finite pivots are reported (is_factorized=false).
 #include <algorithm>
+#include <array>
+#include <map>
 #include <climits>
 #include <cmath>
 #include <cstdlib>
@@ -1464,37 +1466,50 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
 // NH 64-row chunks), all of a round's loads (sc1: handed over inside the launch) issued before the
 // read-modify-writes; the parent column base is wave-uniform, so a row costs one rels lookup.
 // Destinations are distinct within a child, so all LDS reads of a round precede its writes.
+#ifndef PUSH_NC2
+#define PUSH_NC2 8
+#endif
+#ifndef PUSH_NC3
+#define PUSH_NC3 6
+#endif
 template <bool PK, int NH, int NC>
 __device__ __forceinline__ void push_cols(double* A, int r, int ld, const double* U, int64_t uld, int uc,
                                           const int32_t* rels) {
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   for (int b0 = NC * wv; b0 < uc; b0 += 4 * NC) {
+    // every global load of the round first, from clamped addresses (no branches between them)
     double x[NC][NH];
+#pragma unroll
+    for (int cb = 0; cb < NC; ++cb) {
+      const int bc = min(b0 + cb, uc - 1);
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        const int ac = min(b0 + cb + lane + 64 * h, uc - 1);
+        x[cb][h] = __hip_atomic_load(U + ac + (int64_t)bc * uld, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    // then the destinations (relative indices in LDS) and the read-modify-writes
     int dst[NC][NH];
 #pragma unroll
     for (int cb = 0; cb < NC; ++cb) {
-      const int b = b0 + cb, bc = min(b, uc - 1);
-      const int j = rels[bc];
+      const int b = b0 + cb, j = rels[min(b, uc - 1)];
       const int base = PK ? ((j * (2 * r - j - 1)) >> 1) : j * ld;  // fidx(i, j) = base + i
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
         const int a = b + lane + 64 * h;
-        const bool ok = b < uc && a < uc;
-        x[cb][h] = ok ? __hip_atomic_load(U + a + (int64_t)bc * uld, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
-        dst[cb][h] = ok ? base + rels[min(a, uc - 1)] : -1;
+        dst[cb][h] = (b < uc && a < uc) ? base + rels[min(a, uc - 1)] : -1;
       }
     }
-    double o[NC][NH];
 #pragma unroll
     for (int cb = 0; cb < NC; ++cb)
 #pragma unroll
-      for (int h = 0; h < NH; ++h) o[cb][h] = A[max(dst[cb][h], 0)];
+      for (int h = 0; h < NH; ++h) x[cb][h] += A[max(dst[cb][h], 0)];
 #pragma unroll
     for (int cb = 0; cb < NC; ++cb)
 #pragma unroll
       for (int h = 0; h < NH; ++h)
-        if (dst[cb][h] >= 0) A[dst[cb][h]] = o[cb][h] + x[cb][h];
+        if (dst[cb][h] >= 0) A[dst[cb][h]] = x[cb][h];
   }
 }
 
@@ -1538,6 +1553,11 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
     __syncthreads();
     if (tid == 0) dg[1] = wall_clock64();
   }
+  if (q1 > q0) {  // the first child's relative indices are symbolic: load them before the wait
+    const int c = dep[q0];
+    const int uc = T.nrows[c] - (T.first[c + 1] - T.first[c]);
+    for (int a = tid; a < uc; a += NT) rels[a] = T.rel[T.rel_ptr[c] + a];
+  }
   if (tid < 64) poll_deps(dep, q0, q1, flags, epoch, err);
   __syncthreads();
   if (dg && tid == 0) dg[2] = wall_clock64();
@@ -1546,14 +1566,17 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
     const int uc = T.nrows[c] - (T.first[c + 1] - T.first[c]);
     const int64_t uld = T.u_ld[c];
     const double* U = arena + T.u_off[c];
-    for (int a = tid; a < uc; a += NT) rels[a] = T.rel[T.rel_ptr[c] + a];
-    __syncthreads();
+    if (q > q0) {
+      for (int a = tid; a < uc; a += NT) rels[a] = T.rel[T.rel_ptr[c] + a];
+      __syncthreads();
+    }
+    // one memory round trip per round: 4 waves x NC columns (1 wave per SIMD here, registers are free)
     if (uc <= 64)
       push_cols<PK, 1, 8>(A, r, ld, U, uld, uc, rels);
     else if (uc <= 128)
-      push_cols<PK, 2, 6>(A, r, ld, U, uld, uc, rels);
+      push_cols<PK, 2, PUSH_NC2>(A, r, ld, U, uld, uc, rels);
     else
-      push_cols<PK, 3, 4>(A, r, ld, U, uld, uc, rels);
+      push_cols<PK, 3, PUSH_NC3>(A, r, ld, U, uld, uc, rels);
     __syncthreads();
   }
   if (dg && tid == 0) dg[3] = wall_clock64();
@@ -3126,6 +3149,21 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       (void)u;
       ftree_bytes_ += 8.0 * (r * (double)w - w * (w - 1) / 2.0) + 12.0 * (double)(S.asm_ptr[s + 1] - S.asm_ptr[s]);
       for (int t = 0; t < w; ++t) ftree_flops_ += (double)(r - t - 1) * (r - t);
+    }
+    if (const char* ev = std::getenv("MADIPM_TREE_DEBUG"); ev && ev[0] == '1') {  // per-level front shapes
+      std::map<int, std::array<double, 7>> lv;  // count, sum r, max r, sum w, sum lds, max lds, sum leaves
+      for (int s : ord) {
+        const int r = S.nrows[s], w = S.first[s + 1] - S.first[s];
+        const bool sq = r <= 128 && !S.fold_pk[s];
+        const double lds = (sq ? 8.0 * r * (r | 1) : 4.0 * r * (r + 1)) +
+                           (S.absorb[s] ? SymbolicPlan::kFoldRowBytes * S.fold_rmax[s] + SymbolicPlan::kFoldLeafBytes * S.fold_lmax[s] : 0);
+        auto& a = lv[S.level[s]];
+        a[0] += 1, a[1] += r, a[2] = std::max<double>(a[2], r), a[3] += w, a[4] += lds, a[5] = std::max(a[5], lds);
+        a[6] += S.absorb[s] ? S.mc_ptr[s + 1] - S.mc_ptr[s] : 0;
+      }
+      for (auto& [l, a] : lv)
+        fprintf(stderr, "tree level %d: %4.0f fronts  r avg %.0f max %.0f  w avg %.1f  LDS avg %.0f max %.0f KB  leaves avg %.0f\n", l,
+                a[0], a[1] / a[0], a[2], a[3] / a[0], a[4] / a[0] / 1024, a[5] / 1024, a[6] / a[0]);
     }
     auto up = [](DBuf<int32_t>& d, const std::vector<int32_t>& v) { d.upload(v.empty() ? std::vector<int32_t>{0} : v); };
     up(ft_order_, ord);

@@ -807,10 +807,27 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     };
     std::vector<Prod> pr;
     std::vector<int64_t> bnd;
+    // k_fact_tree runs one workgroup per CU, tickets in level order: the tree fronts past the first
+    // `slots` start only when an earlier front retires, so folding (staging the leaves inside the
+    // front's own critical path) is left to the micro launch for the late fronts of that level
+    // (MADIPM_FOLD_SLOTS overrides the MI355X CU count; 0 = no limit)
+    int slots = 256;
+    if (const char* e = std::getenv("MADIPM_FOLD_SLOTS")) slots = std::atoi(e);
+    std::vector<char> late(ns_all, 0);
+    {
+      std::vector<int> ord;
+      for (int lev = 0; lev < S.nlevels; ++lev)
+        for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q)
+          if (S.ftree[S.level_list[q]]) ord.push_back(S.level_list[q]);
+      if (slots > 0 && (int)ord.size() > slots) {
+        const int lcut = S.level[ord[slots]];
+        for (size_t q = slots; q < ord.size() && S.level[ord[q]] == lcut; ++q) late[ord[q]] = 1;
+      }
+    }
     for (int s = 0; s < ns_all; ++s) {
       S.mc_ptr[s + 1] = S.mc_ptr[s];
       S.fold_bptr[s + 1] = S.fold_bptr[s];
-      if (!on || !S.ftree[s]) continue;
+      if (!on || !S.ftree[s] || late[s]) continue;
       const int64_t r = S.nrows[s];
       int64_t nmc = 0, nrow = 0;
       bool ok = true;
