@@ -483,10 +483,31 @@ struct Dissector {
 void nd_order(int n, const std::vector<int64_t>& Ap, const std::vector<int32_t>& Ai, std::vector<int32_t>& perm,
               const NDOptions& opt) {
   Dissector d(Ap, Ai, opt, n);
-  std::vector<int32_t> all(n);
-  std::iota(all.begin(), all.end(), 0);
+  // Dense vertices (degree above AMD's threshold, max(16, alpha sqrt(n))) are deferred and ordered
+  // last, as AMD does: they would sit in every separator anyway, and leaving them in the graph makes
+  // each level's induced subgraph / bisection cost O(their degree) -- for a dense-column QP (A dense,
+  // H diagonal) that is every edge of the matrix at every level.  Dissection then runs on the rest.
+  int64_t dense = (int64_t)std::max(16.0, opt.dense_alpha * std::sqrt((double)n));
+  dense = std::min<int64_t>(n - 2, dense);
+  if (opt.dense_alpha < 0) dense = n;
+  // When more than half the vertices pass the threshold (a dense A block makes both its row and its
+  // column vertices "dense"), the lowest degree class is put back until at most half are deferred:
+  // for [H A'; A 0] with A dense m x n, m < n, that defers exactly the m constraint vertices.
+  for (;;) {
+    int64_t cnt = 0, lo = INT64_MAX;
+    for (int v = 0; v < n; ++v) {
+      const int64_t dg = Ap[v + 1] - Ap[v];
+      if (dg > dense) ++cnt, lo = std::min(lo, dg);
+    }
+    if (2 * cnt <= n) break;
+    dense = lo;
+  }
+  std::vector<int32_t> all, deferred;
+  all.reserve(n);
+  for (int v = 0; v < n; ++v) (Ap[v + 1] - Ap[v] > dense ? deferred : all).push_back(v);
   d.out.reserve(n);
   d.dissect(all, 0);
+  d.out.insert(d.out.end(), deferred.begin(), deferred.end());
   MADIPM_REQUIRE((int)d.out.size() == n, "nested dissection lost vertices");
   perm.swap(d.out);
 }

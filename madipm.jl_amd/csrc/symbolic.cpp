@@ -139,25 +139,42 @@ void column_counts(int N, const Pattern& P, const std::vector<int32_t>& parent, 
 
 inline int64_t trap(int64_t w, int64_t r) { return w * r - w * (w - 1) / 2; }
 
-// Factorisation flops sum_j (c_j - 1)(c_j + 2) of the order `perm` (etree + column counts only).
-double ordering_flops(int N, const int64_t* colptr, const int32_t* rowval, const std::vector<int32_t>& perm) {
-  std::vector<int32_t> pinv(N);
-  for (int k = 0; k < N; ++k) pinv[perm[k]] = k;
-  Pattern P;
-  build_pattern(N, colptr, rowval, pinv, P);
-  std::vector<int32_t> parent, post;
-  etree(N, P, parent);
-  postorder(N, parent, post);
-  std::vector<int32_t> p2(N);
-  for (int k = 0; k < N; ++k) p2[k] = perm[post[k]];
-  for (int k = 0; k < N; ++k) pinv[p2[k]] = k;
-  build_pattern(N, colptr, rowval, pinv, P);
-  etree(N, P, parent);
+// Everything the analysis needs about one fill-reducing order: the order relabelled as a postorder
+// of its etree, the strictly-lower pattern in that labelling, the etree, the column counts of L and
+// the factorisation flops sum_j (c_j - 1)(c_j + 2).  Candidate orders are compared by flops and the
+// winner's analysis is kept (no second pass over the matrix for it).
+struct OrderAnalysis {
+  std::vector<int32_t> perm, pinv, parent;
   std::vector<int64_t> cnt;
-  column_counts(N, P, parent, cnt);
-  double f = 0.0;
-  for (int64_t c : cnt) f += (double)(c - 1) * (double)(c + 2);
-  return f;
+  Pattern P;
+  double flops = 0.0;
+};
+
+void analyse_order(int N, const int64_t* colptr, const int32_t* rowval, std::vector<int32_t> perm,
+                   OrderAnalysis& A) {
+  A.pinv.assign(N, -1);
+  for (int k = 0; k < N; ++k) {
+    MADIPM_REQUIRE(perm[k] >= 0 && perm[k] < N && A.pinv[perm[k]] == -1, "ordering is not a permutation");
+    A.pinv[perm[k]] = k;
+  }
+  build_pattern(N, colptr, rowval, A.pinv, A.P);
+  std::vector<int32_t> post;
+  etree(N, A.P, A.parent);
+  postorder(N, A.parent, post);
+  bool ident = true;  // the ordering is already a postorder (e.g. natural order of a QP's K2): no relabel
+  for (int k = 0; k < N && ident; ++k) ident = post[k] == k;
+  if (!ident) {
+    std::vector<int32_t> perm2(N);
+    for (int k = 0; k < N; ++k) perm2[k] = perm[post[k]];
+    perm.swap(perm2);
+    for (int k = 0; k < N; ++k) A.pinv[perm[k]] = k;
+    build_pattern(N, colptr, rowval, A.pinv, A.P);
+    etree(N, A.P, A.parent);
+  }
+  A.perm.swap(perm);
+  column_counts(N, A.P, A.parent, A.cnt);
+  A.flops = 0.0;
+  for (int64_t c : A.cnt) A.flops += (double)(c - 1) * (double)(c + 2);
 }
 
 }  // namespace
@@ -218,8 +235,9 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   if (N == 0) return;
 
   stamp("before 1");
-  // ---------------- 1. fill-reducing ordering
-  std::vector<int32_t> perm(N);
+  // ---------------- 1. fill-reducing ordering; 2. etree + postorder (relabel so that the labelling
+  // is a postorder) and column counts of the chosen order
+  OrderAnalysis OA;
   S.order_flops_amd = S.order_flops_nd = 0.0;
   if (opt.ordering == 1 || opt.ordering == 3 || opt.ordering == 4) {
     std::vector<int64_t> Ap(N + 1, 0);
@@ -240,52 +258,46 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         Ai[fill[i]++] = j;
         Ai[fill[j]++] = i;
       }
+    std::vector<int64_t>().swap(fill);
     std::vector<int32_t> pa, pn;
-    if (opt.ordering != 3) {
-      amd_order(N, Ap, Ai, pa, opt.dense_alpha);
-      S.order_flops_amd = ordering_flops(N, colptr, rowval, pa);
-    }
+    if (opt.ordering != 3) amd_order(N, Ap, Ai, pa, opt.dense_alpha);
+    stamp("1: AMD");
     if (opt.ordering != 1) {
       NDOptions nopt;
       nopt.dense_alpha = opt.dense_alpha;
       nd_order(N, Ap, Ai, pn, nopt);
-      S.order_flops_nd = ordering_flops(N, colptr, rowval, pn);
     }
-    if (opt.ordering == 1 || (opt.ordering == 4 && S.order_flops_amd <= S.order_flops_nd))
-      perm.swap(pa);
-    else
-      perm.swap(pn);
+    stamp("1: ND");
+    std::vector<int64_t>().swap(Ap);
+    std::vector<int32_t>().swap(Ai);
+    if (opt.ordering != 3) {
+      analyse_order(N, colptr, rowval, std::move(pa), OA);
+      S.order_flops_amd = OA.flops;
+    }
+    if (opt.ordering != 1) {
+      if (opt.ordering == 4 && pn == OA.perm) {  // ND found AMD's (postordered) order: nothing to compare
+        S.order_flops_nd = OA.flops;
+      } else {
+        OrderAnalysis B;
+        analyse_order(N, colptr, rowval, std::move(pn), B);
+        S.order_flops_nd = B.flops;
+        if (opt.ordering == 3 || B.flops < OA.flops) std::swap(OA, B);
+      }
+    }
   } else if (opt.ordering == 2) {
     MADIPM_REQUIRE(user_perm != nullptr, "user permutation missing");
-    std::copy(user_perm, user_perm + N, perm.begin());
+    analyse_order(N, colptr, rowval, std::vector<int32_t>(user_perm, user_perm + N), OA);
   } else {
-    std::iota(perm.begin(), perm.end(), 0);
+    std::vector<int32_t> id(N);
+    std::iota(id.begin(), id.end(), 0);
+    analyse_order(N, colptr, rowval, std::move(id), OA);
   }
-  std::vector<int32_t> pinv(N, -1);
-  for (int k = 0; k < N; ++k) {
-    MADIPM_REQUIRE(perm[k] >= 0 && perm[k] < N && pinv[perm[k]] == -1, "ordering is not a permutation");
-    pinv[perm[k]] = k;
-  }
-
-  stamp("before 2");
-  // ---------------- 2. etree + postorder, relabel so that the labelling is a postorder
-  Pattern P;
-  build_pattern(N, colptr, rowval, pinv, P);
-  std::vector<int32_t> parent, post;
-  etree(N, P, parent);
-  postorder(N, parent, post);
-  std::vector<int32_t> perm2(N);
-  for (int k = 0; k < N; ++k) perm2[k] = perm[post[k]];
-  bool ident = true;  // the ordering is already a postorder (e.g. natural order of a QP's K2): no relabel
-  for (int k = 0; k < N && ident; ++k) ident = post[k] == k;
-  if (!ident) {
-    perm.swap(perm2);
-    for (int k = 0; k < N; ++k) pinv[perm[k]] = k;
-    build_pattern(N, colptr, rowval, pinv, P);
-    etree(N, P, parent);
-  }
-  std::vector<int64_t> cnt;
-  column_counts(N, P, parent, cnt);
+  stamp("2: etree, counts");
+  std::vector<int32_t>& perm = OA.perm;
+  std::vector<int32_t>& pinv = OA.pinv;
+  std::vector<int32_t>& parent = OA.parent;
+  std::vector<int64_t>& cnt = OA.cnt;
+  Pattern& P = OA.P;
   S.perm = perm;
   S.pinv = pinv;
   S.nnzL = std::accumulate(cnt.begin(), cnt.end(), (int64_t)0);
