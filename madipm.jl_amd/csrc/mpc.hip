@@ -152,43 +152,45 @@ __device__ __forceinline__ double gdot(const DCsr& A, int64_t row, const double*
 // Normal equations (NormalKKTSystem.build_kkt!, normalkkt.jl:180-194): Dinv = 1 ./ pr_diag.
 // l_diag / u_diag keep the K2 sign convention (xl - x, x - xu) in every mode: they feed the
 // unreduced operator of the residual, which is the same for the three formulations.
-__global__ __launch_bounds__(NT) void k_diag(DV D, double dw, double dc) {
-  GRID_LOOP(i, D.n + D.m) {
-    if (i < D.n) {
-      double pr = dw;
-      const int kl = D.lbpos[i], ku = D.ubpos[i];
-      const double x = D.x[i];
-      double dl = 1.0, du = 1.0, zlv = 0.0, zuv = 0.0;
-      if (kl >= 0) {
-        const double ld = D.xl[i] - x, zl = D.zl[i];
-        D.l_diag[kl] = ld;
-        D.l_lower[kl] = zl;
-        pr -= zl / ld;
-        dl = -ld;
-        zlv = zl;
-      }
-      if (ku >= 0) {
-        const double ud = x - D.xu[i], zu = D.zu[i];
-        D.u_diag[ku] = ud;
-        D.u_lower[ku] = zu;
-        pr -= zu / ud;
-        du = -ud;
-        zuv = zu;
-      }
-      D.pr_diag[i] = pr;
-      if (D.kkt == KKT_NORMAL) {
-        D.Dinv[i] = 1.0 / pr;
-      } else if (D.kkt == KKT_K25) {
-        const double s2 = dl * du;
-        D.sk[i] = sqrt(s2);
-        D.Kx[D.diag_pos[i]] = s2 * (dw + D.Hdiag[i]) + zlv * du + zuv * dl;
-      } else {
-        D.Kx[D.diag_pos[i]] = pr + D.Hdiag[i];
-      }
-    } else if (D.kkt != KKT_NORMAL) {
-      D.Kx[D.diag_pos[i]] = dc;
+__device__ __forceinline__ void diag_entry(const DV& D, int64_t i, double dw, double dc) {
+  if (i < D.n) {
+    double pr = dw;
+    const int kl = D.lbpos[i], ku = D.ubpos[i];
+    const double x = D.x[i];
+    double dl = 1.0, du = 1.0, zlv = 0.0, zuv = 0.0;
+    if (kl >= 0) {
+      const double ld = D.xl[i] - x, zl = D.zl[i];
+      D.l_diag[kl] = ld;
+      D.l_lower[kl] = zl;
+      pr -= zl / ld;
+      dl = -ld;
+      zlv = zl;
     }
+    if (ku >= 0) {
+      const double ud = x - D.xu[i], zu = D.zu[i];
+      D.u_diag[ku] = ud;
+      D.u_lower[ku] = zu;
+      pr -= zu / ud;
+      du = -ud;
+      zuv = zu;
+    }
+    D.pr_diag[i] = pr;
+    if (D.kkt == KKT_NORMAL) {
+      D.Dinv[i] = 1.0 / pr;
+    } else if (D.kkt == KKT_K25) {
+      const double s2 = dl * du;
+      D.sk[i] = sqrt(s2);
+      D.Kx[D.diag_pos[i]] = s2 * (dw + D.Hdiag[i]) + zlv * du + zuv * dl;
+    } else {
+      D.Kx[D.diag_pos[i]] = pr + D.Hdiag[i];
+    }
+  } else if (D.kkt != KKT_NORMAL) {
+    D.Kx[D.diag_pos[i]] = dc;
   }
+}
+
+__global__ __launch_bounds__(NT) void k_diag(DV D, double dw, double dc) {
+  GRID_LOOP(i, D.n + D.m) diag_entry(D, i, dw, dc);
 }
 
 // MadNLP.initialize!(kkt) + init_starting_point! lines 16-18 (l_diag = u_diag = 1, l/u_lower = 0,
@@ -343,82 +345,22 @@ __global__ __launch_bounds__(NT) void k_rhs(DV D, int mode, double mu_g, int res
 }
 
 // finish_aug_solve! [EXT] + residual w = p - K d (mul!/_kktmul! [EXT], linear_solver.jl:29-35)
-template <int G>
-__global__ __launch_bounds__(NT) void k_residual(DV D, double dw, double dc) {
-  const int n = D.n, m = D.m, nlb = D.nlb;
-  const bool lead = (threadIdx.x & (G - 1)) == 0;
-  double wmax = 0.0, pmax = 0.0, dxmax = 0.0;
-  GROUP_LOOP(i, n + m, G) {
-    if (i < n) {
-      const double hj = gdot<G>(D.H, i, D.d) + gdot<G>(D.JT, i, D.d + n);
-      if (!lead) continue;
-      const double dx = D.d[i];
-      double kv = hj + dw * dx;
-      const int kl = D.lbpos[i], ku = D.ubpos[i];
-      if (kl >= 0) {
-        const double pl = D.p[n + m + kl];
-        const double dzl = (-pl + D.l_lower[kl] * dx) / D.l_diag[kl];
-        D.d[n + m + kl] = dzl;
-        kv -= dzl;
-        const double wl = pl - (dx * D.l_lower[kl] - dzl * D.l_diag[kl]);
-        wmax = nmax(wmax, fabs(wl));
-        pmax = nmax(pmax, fabs(pl));
-      }
-      if (ku >= 0) {
-        const double pu = D.p[n + m + nlb + ku];
-        const double dzu = (pu - D.u_lower[ku] * dx) / D.u_diag[ku];
-        D.d[n + m + nlb + ku] = dzu;
-        kv += dzu;
-        const double wu = pu - (dx * D.u_lower[ku] + dzu * D.u_diag[ku]);
-        wmax = nmax(wmax, fabs(wu));
-        pmax = nmax(pmax, fabs(pu));
-      }
-      const double pi = D.p[i];
-      wmax = nmax(wmax, fabs(pi - kv));
-      pmax = nmax(pmax, fabs(pi));
-      dxmax = nmax(dxmax, fabs(dx));
-    } else {
-      const double jd = gdot<G>(D.J, i - n, D.d);
-      if (!lead) continue;
-      const double dy = D.d[i];
-      const double kv = jd + dc * dy;
-      const double pi = D.p[i];
-      wmax = nmax(wmax, fabs(pi - kv));
-      pmax = nmax(pmax, fabs(pi));
-    }
-  }
-  double v[3] = {wmax, pmax, dxmax};
-  const int ops[3] = {OP_MAX, OP_MAX, OP_MAX};
-  block_partials<3>(v, ops, D.part);
-}
-
+// amode >= 0: the max-ratio step test of k_alpha (same mode, tau and expressions) is evaluated here,
+// by the lane that has just formed dz for the variable, into partial slots 8..15 — k_final(FIN_RESID,
+// with_alpha) then finalises both, saving k_alpha and its finaliser per direction.  The (value,
+// smallest index) argmin does not depend on the combine order, so the step is bitwise k_alpha's.
 enum { ALPHA_PRED = 0, ALPHA_CONSERVATIVE = 1, ALPHA_ADAPTIVE = 2, ALPHA_MEHROTRA = 3, ALPHA_GONDZIO = 4 };
+constexpr int PART_ALPHA = 8;  // first partial slot of the fused step test (4 values, 4 indices)
 
-// get_alpha_max_primal / get_alpha_max_dual (kernels.jl:226-272): min-ratio with argmin
-__global__ __launch_bounds__(NT) void k_alpha(DV D, int mode, double tau_param) {
-  const int n = D.n, m = D.m, nlb = D.nlb, nub = D.nub;
+__device__ __forceinline__ double alpha_tau(const DV& D, int mode, double tau_param) {
   double tau = 1.0;
   if (mode == ALPHA_CONSERVATIVE || mode == ALPHA_GONDZIO) tau = tau_param;
   if (mode == ALPHA_ADAPTIVE) tau = fmax(1.0 - D.st->mu, tau_param);
-  double v[4] = {INF, INF, INF, INF};
-  int ix[4] = {-1, -1, -1, -1};
-  GRID_LOOP(t, (nlb > nub ? nlb : nub)) {
-    if (t < nlb) {
-      const int i = D.ind_lb[t];
-      const double dx = D.d[i];
-      if (dx < 0) amin_upd(v[0], ix[0], (-D.x[i] + D.xl[i]) * tau / dx, (int)t);
-      const double dz = D.d[n + m + t];
-      if (dz < 0) amin_upd(v[2], ix[2], (-D.zl[i]) * tau / dz, (int)t);
-    }
-    if (t < nub) {
-      const int i = D.ind_ub[t];
-      const double dx = D.d[i];
-      if (dx > 0) amin_upd(v[1], ix[1], (-D.x[i] + D.xu[i]) * tau / dx, (int)t);
-      const double dz = D.d[n + m + nlb + t];
-      const double zu = D.zu[i];
-      if (dz < 0 && zu + dz < 0) amin_upd(v[3], ix[3], (-zu) * tau / dz, (int)t);
-    }
-  }
+  return tau;
+}
+
+// block argmin of (v[k], ix[k]), k < 4, into part slots base + k (values) and base + 4 + k (indices)
+__device__ void block_argmin4(const double (&v)[4], const int (&ix)[4], double* part, int base) {
   __shared__ double sv[4][NT / 64];
   __shared__ int si[4][NT / 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -442,9 +384,98 @@ __global__ __launch_bounds__(NT) void k_alpha(DV D, int mode, double tau_param) 
     double a = sv[k][0];
     int b = si[k][0];
     for (int w = 1; w < NT / 64; ++w) amin_upd(a, b, sv[k][w], si[k][w]);
-    D.part[pidx(blockIdx.x, k)] = a;
-    D.part[pidx(blockIdx.x, 4 + k)] = (double)b;
+    part[pidx(blockIdx.x, base + k)] = a;
+    part[pidx(blockIdx.x, base + 4 + k)] = (double)b;
   }
+}
+
+template <int G>
+__global__ __launch_bounds__(NT) void k_residual(DV D, double dw, double dc, int amode, double atau) {
+  const int n = D.n, m = D.m, nlb = D.nlb;
+  const bool lead = (threadIdx.x & (G - 1)) == 0;
+  double wmax = 0.0, pmax = 0.0, dxmax = 0.0;
+  const bool fa = amode >= 0;
+  const double tau = fa ? alpha_tau(D, amode, atau) : 1.0;
+  double av[4] = {INF, INF, INF, INF};
+  int ai[4] = {-1, -1, -1, -1};
+  GROUP_LOOP(i, n + m, G) {
+    if (i < n) {
+      const double hj = gdot<G>(D.H, i, D.d) + gdot<G>(D.JT, i, D.d + n);
+      if (!lead) continue;
+      const double dx = D.d[i];
+      double kv = hj + dw * dx;
+      const int kl = D.lbpos[i], ku = D.ubpos[i];
+      if (kl >= 0) {
+        const double pl = D.p[n + m + kl];
+        const double dzl = (-pl + D.l_lower[kl] * dx) / D.l_diag[kl];
+        D.d[n + m + kl] = dzl;
+        if (fa) {  // k_alpha's lower-bound terms, t = kl
+          if (dx < 0) amin_upd(av[0], ai[0], (-D.x[i] + D.xl[i]) * tau / dx, kl);
+          if (dzl < 0) amin_upd(av[2], ai[2], (-D.zl[i]) * tau / dzl, kl);
+        }
+        kv -= dzl;
+        const double wl = pl - (dx * D.l_lower[kl] - dzl * D.l_diag[kl]);
+        wmax = nmax(wmax, fabs(wl));
+        pmax = nmax(pmax, fabs(pl));
+      }
+      if (ku >= 0) {
+        const double pu = D.p[n + m + nlb + ku];
+        const double dzu = (pu - D.u_lower[ku] * dx) / D.u_diag[ku];
+        D.d[n + m + nlb + ku] = dzu;
+        if (fa) {  // upper-bound terms, t = ku
+          if (dx > 0) amin_upd(av[1], ai[1], (-D.x[i] + D.xu[i]) * tau / dx, ku);
+          const double zu = D.zu[i];
+          if (dzu < 0 && zu + dzu < 0) amin_upd(av[3], ai[3], (-zu) * tau / dzu, ku);
+        }
+        kv += dzu;
+        const double wu = pu - (dx * D.u_lower[ku] + dzu * D.u_diag[ku]);
+        wmax = nmax(wmax, fabs(wu));
+        pmax = nmax(pmax, fabs(pu));
+      }
+      const double pi = D.p[i];
+      wmax = nmax(wmax, fabs(pi - kv));
+      pmax = nmax(pmax, fabs(pi));
+      dxmax = nmax(dxmax, fabs(dx));
+    } else {
+      const double jd = gdot<G>(D.J, i - n, D.d);
+      if (!lead) continue;
+      const double dy = D.d[i];
+      const double kv = jd + dc * dy;
+      const double pi = D.p[i];
+      wmax = nmax(wmax, fabs(pi - kv));
+      pmax = nmax(pmax, fabs(pi));
+    }
+  }
+  double v[3] = {wmax, pmax, dxmax};
+  const int ops[3] = {OP_MAX, OP_MAX, OP_MAX};
+  block_partials<3>(v, ops, D.part);
+  if (fa) block_argmin4(av, ai, D.part, PART_ALPHA);
+}
+
+// get_alpha_max_primal / get_alpha_max_dual (kernels.jl:226-272): min-ratio with argmin
+__global__ __launch_bounds__(NT) void k_alpha(DV D, int mode, double tau_param) {
+  const int n = D.n, m = D.m, nlb = D.nlb, nub = D.nub;
+  const double tau = alpha_tau(D, mode, tau_param);
+  double v[4] = {INF, INF, INF, INF};
+  int ix[4] = {-1, -1, -1, -1};
+  GRID_LOOP(t, (nlb > nub ? nlb : nub)) {
+    if (t < nlb) {
+      const int i = D.ind_lb[t];
+      const double dx = D.d[i];
+      if (dx < 0) amin_upd(v[0], ix[0], (-D.x[i] + D.xl[i]) * tau / dx, (int)t);
+      const double dz = D.d[n + m + t];
+      if (dz < 0) amin_upd(v[2], ix[2], (-D.zl[i]) * tau / dz, (int)t);
+    }
+    if (t < nub) {
+      const int i = D.ind_ub[t];
+      const double dx = D.d[i];
+      if (dx > 0) amin_upd(v[1], ix[1], (-D.x[i] + D.xu[i]) * tau / dx, (int)t);
+      const double dz = D.d[n + m + nlb + t];
+      const double zu = D.zu[i];
+      if (dz < 0 && zu + dz < 0) amin_upd(v[3], ix[3], (-zu) * tau / dz, (int)t);
+    }
+  }
+  block_argmin4(v, ix, D.part, 0);
 }
 
 enum { MU_PRED = 0, MU_FULL = 1, MU_GONDZIO = 2 };
@@ -536,10 +567,13 @@ __global__ __launch_bounds__(NT) void k_jtprod(DV D) {
 
 // update_termination_criteria! pieces (solver.jl:194-204; dual_objective kernels.jl:408-417;
 // get_optimality_gap kernels.jl:419-430; get_inf_pr/get_inf_du [EXT])
-__global__ __launch_bounds__(NT) void k_term(DV D) {
+// diag != 0: also k_diag's work for the next factorisation (same grid, same iterate reads; the
+// regularisation is decided on the host before this launch), one launch less per iteration
+__global__ __launch_bounds__(NT) void k_term(DV D, int diag, double dw, double dc) {
   const int n = D.n;
   double du = 0, gap = 0, pr = 0, sy = 0, sl = 0, su = 0;
   GRID_LOOP(i, n + D.m) {
+    if (diag) diag_entry(D, i, dw, dc);
     if (i < n) {
       du = nmax(du, fabs(D.f[i] - D.zl[i] + D.zu[i] + D.jacl[i]));
       const int kl = D.lbpos[i], ku = D.ubpos[i];
@@ -673,8 +707,9 @@ enum {
 
 struct FinParams {
   int nb;          // number of partial blocks
-  int alpha_mode;  // for FIN_ALPHA
+  int alpha_mode;  // for FIN_ALPHA (and FIN_RESID with_alpha)
   double a, b, c;  // kind-specific parameters
+  int with_alpha;  // FIN_RESID: also finalise the step test k_residual fused (slots PART_ALPHA..)
 };
 
 // k_final runs as ONE block of NTF threads that reads every partial in a single memory round trip:
@@ -690,6 +725,77 @@ __device__ __forceinline__ double2 part2(const DV& D, int b, int k) {
   return *reinterpret_cast<const double2*>(D.part + pidx(b, k));
 }
 
+// the step test's argmin over the block partials in slots base.. (FIN_ALPHA: 0, fused: PART_ALPHA);
+// every thread of the block calls it (shuffles, __syncthreads), thread 0 writes the state
+__device__ void fin_alpha(const DV& D, const FinParams& P, int base, double (&sh)[8][NTF / 64], int (&shi)[4][NTF / 64]) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int b0 = 2 * threadIdx.x;
+  const bool h0 = b0 < P.nb, h1 = b0 + 1 < P.nb;
+  DevState* st = D.st;
+  double v[4];
+  int ix[4];
+  double2 pv[4], pi[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    pv[k] = h0 ? part2(D, b0, base + k) : make_double2(INF, INF);
+    pi[k] = h0 ? part2(D, b0, base + 4 + k) : make_double2(-1.0, -1.0);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[k] = INF;
+    ix[k] = -1;
+    if (h0) amin_upd(v[k], ix[k], pv[k].x, (int)pi[k].x);
+    if (h1) amin_upd(v[k], ix[k], pv[k].y, (int)pi[k].y);
+  }
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const double a2 = __shfl_down(v[k], o, 64);
+      const int b2 = __shfl_down(ix[k], o, 64);
+      amin_upd(v[k], ix[k], a2, b2);
+    }
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      sh[k][wv] = v[k];
+      shi[k][wv] = ix[k];
+    }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a[4];
+    int ii[4];
+    for (int k = 0; k < 4; ++k) {
+      a[k] = sh[k][0];
+      ii[k] = shi[k][0];
+      for (int w = 1; w < NTF / 64; ++w) amin_upd(a[k], ii[k], sh[k][w], shi[k][w]);
+      // mapreduce init (1.0, 0): alpha = min(1, min ratio)
+      if (!(a[k] < 1.0)) {
+        a[k] = 1.0;
+        ii[k] = -1;
+      }
+    }
+    st->a_xl = a[0];
+    st->a_xu = a[1];
+    st->a_zl = a[2];
+    st->a_zu = a[3];
+    st->i_xl = ii[0];
+    st->i_xu = ii[1];
+    st->i_zl = ii[2];
+    st->i_zu = ii[3];
+    const double ap = fmin(a[0], a[1]), ad = fmin(a[2], a[3]);
+    if (P.alpha_mode == ALPHA_PRED) {
+      st->alpha_aff_p = ap;
+      st->alpha_aff_d = ad;
+    } else if (P.alpha_mode == ALPHA_CONSERVATIVE || P.alpha_mode == ALPHA_ADAPTIVE) {
+      st->alpha_p = ap;
+      st->alpha_d = ad;
+    } else {  // MEHROTRA / GONDZIO: keep in the aff slots for the follow-up pass
+      st->alpha_aff_p = ap;
+      st->alpha_aff_d = ad;
+    }
+  }
+}
+
 // Combine the block partials in fixed order + scalar logic (one block of NTF threads).
 __global__ __launch_bounds__(NTF) void k_final(DV D, int kind, FinParams P) {
   __shared__ double res[NPART];
@@ -700,69 +806,12 @@ __global__ __launch_bounds__(NTF) void k_final(DV D, int kind, FinParams P) {
   const bool h0 = b0 < P.nb, h1 = b0 + 1 < P.nb;
   DevState* st = D.st;
   if (kind == FIN_ALPHA) {
-    double v[4];
-    int ix[4];
-    double2 pv[4], pi[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      pv[k] = h0 ? part2(D, b0, k) : make_double2(INF, INF);
-      pi[k] = h0 ? part2(D, b0, 4 + k) : make_double2(-1.0, -1.0);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      v[k] = INF;
-      ix[k] = -1;
-      if (h0) amin_upd(v[k], ix[k], pv[k].x, (int)pi[k].x);
-      if (h1) amin_upd(v[k], ix[k], pv[k].y, (int)pi[k].y);
-    }
-    for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const double a2 = __shfl_down(v[k], o, 64);
-        const int b2 = __shfl_down(ix[k], o, 64);
-        amin_upd(v[k], ix[k], a2, b2);
-      }
-    if (lane == 0)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        sh[k][wv] = v[k];
-        shi[k][wv] = ix[k];
-      }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double a[4];
-      int ii[4];
-      for (int k = 0; k < 4; ++k) {
-        a[k] = sh[k][0];
-        ii[k] = shi[k][0];
-        for (int w = 1; w < NTF / 64; ++w) amin_upd(a[k], ii[k], sh[k][w], shi[k][w]);
-        // mapreduce init (1.0, 0): alpha = min(1, min ratio)
-        if (!(a[k] < 1.0)) {
-          a[k] = 1.0;
-          ii[k] = -1;
-        }
-      }
-      st->a_xl = a[0];
-      st->a_xu = a[1];
-      st->a_zl = a[2];
-      st->a_zu = a[3];
-      st->i_xl = ii[0];
-      st->i_xu = ii[1];
-      st->i_zl = ii[2];
-      st->i_zu = ii[3];
-      const double ap = fmin(a[0], a[1]), ad = fmin(a[2], a[3]);
-      if (P.alpha_mode == ALPHA_PRED) {
-        st->alpha_aff_p = ap;
-        st->alpha_aff_d = ad;
-      } else if (P.alpha_mode == ALPHA_CONSERVATIVE || P.alpha_mode == ALPHA_ADAPTIVE) {
-        st->alpha_p = ap;
-        st->alpha_d = ad;
-      } else {  // MEHROTRA / GONDZIO: keep in the aff slots for the follow-up pass
-        st->alpha_aff_p = ap;
-        st->alpha_aff_d = ad;
-      }
-    }
+    fin_alpha(D, P, 0, sh, shi);
     return;
+  }
+  if (P.with_alpha) {  // FIN_RESID of a solve whose k_residual also ran the step test
+    fin_alpha(D, P, PART_ALPHA, sh, shi);
+    __syncthreads();
   }
   int nv = 0;
   int ops[NPART];
@@ -1461,9 +1510,9 @@ void MPCSolver::kkt_diag(double dw, double dc) {
 }
 
 // set_aug_diagonal_reg! + build_kkt! of the chosen formulation (values consumed by the LDL^T)
-void MPCSolver::assemble_kkt(double dw, double dc) {
+void MPCSolver::assemble_kkt(double dw, double dc, bool diag_done) {
   DV_ARGS;
-  kkt_diag(dw, dc);
+  if (!diag_done) kkt_diag(dw, dc);
   if (kkt_ == KKT_K25) k_k25_scale<<<blocks(nnzK_), NT, 0, stream_>>>(D);
   if (kkt_ == KKT_NORMAL) k_normal_asm<<<blocks(nnzC_), NT, 0, stream_>>>(D);
 }
@@ -1494,9 +1543,13 @@ void MPCSolver::kkt_solve() {
   }
 }
 
-void MPCSolver::launch_reduce_final(int kind, int nb) {
+void MPCSolver::launch_reduce_final(int kind, int nb, int amode) {
   DV_ARGS;
-  FinParams P{nb, 0, 0, 0, 0};
+  FinParams P{nb, 0, 0, 0, 0, 0};
+  if (amode >= 0) {
+    P.alpha_mode = amode;
+    P.with_alpha = 1;
+  }
   if (kind == FIN_MU_PRED) {
     P.a = (double)(nlb_ + nub_);
     P.b = H_->has_ineq ? 1.0 : 0.0;
@@ -1515,13 +1568,13 @@ void MPCSolver::launch_reduce_final(int kind, int nb) {
 }
 
 // solve_system! (linear_solver.jl:19-44): rhs (mode) -> LDL^T solve -> finish + residual
-void MPCSolver::solve_system(int mode, double mu, int reset) {
+void MPCSolver::solve_system(int mode, double mu, int reset, int amode, double atau) {
   DV_ARGS;
   const int nb = blocks(n_ + m_), nbs = spmv_blocks(n_ + m_);
   k_rhs<<<nb, NT, 0, stream_>>>(D, mode, mu, reset);
   kkt_solve();
-  SPMV_LAUNCH(k_residual, nbs, stream_, D, del_w_, del_c_);
-  launch_reduce_final(FIN_RESID, nbs);
+  SPMV_LAUNCH(k_residual, nbs, stream_, D, del_w_, del_c_, amode, atau);
+  launch_reduce_final(FIN_RESID, nbs, amode);
 }
 
 // gondzio_correction_direction! (solver.jl:245-298): host-controlled loop, one read-back per solve
@@ -1532,7 +1585,7 @@ void MPCSolver::gondzio() {
   const int nbz = blocks(std::max(nlb_, nub_));
   auto ftb = [&](double& ap, double& ad) {  // get_fraction_to_boundary_step(solver, tau)
     k_alpha<<<nbz, NT, 0, s>>>(D, ALPHA_GONDZIO, tau);
-    FinParams P{nbz, ALPHA_GONDZIO, 0, 0, 0};
+    FinParams P{nbz, ALPHA_GONDZIO, 0, 0, 0, 0};
     k_final<<<1, NTF, 0, s>>>(D, FIN_ALPHA, P);
     read_state();
     wait_state();
@@ -1598,13 +1651,13 @@ void MPCSolver::init_starting_point() {
   // Step 1: least-squares primal correction
   k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_PRIMAL, 0.0, 0);
   kkt_solve();
-  SPMV_LAUNCH(k_residual, nb, s, D, del_w_, del_c_);
+  SPMV_LAUNCH(k_residual, nb, s, D, del_w_, del_c_, -1, 1.0);
   launch_reduce_final(FIN_RESID, nb);
   k_axpy_x<<<nbn, NT, 0, s>>>(D);
   // Step 2: dual least squares
   k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_DUAL, 0.0, 0);
   kkt_solve();
-  SPMV_LAUNCH(k_residual, nb, s, D, del_w_, del_c_);
+  SPMV_LAUNCH(k_residual, nb, s, D, del_w_, del_c_, -1, 1.0);
   launch_reduce_final(FIN_RESID, nb);
   k_copy_y<<<blocks(m_), NT, 0, s>>>(D);
   // Step 3: bound multipliers and shifts
@@ -1674,38 +1727,46 @@ void MPCSolver::initialize_public() {
 }
 
 // prediction_step! (solver.jl:230-237) + mehrotra_correction_direction! (solver.jl:239-243)
-void MPCSolver::directions(bool redo) {
+void MPCSolver::directions(bool redo, bool fuse_step) {
   DV_ARGS;
   hipStream_t s = stream_;
   const int nbz = blocks(std::max(nlb_, nub_));
-  solve_system(RHS_PRED, 0.0, redo ? 2 : 1);
-  k_alpha<<<nbz, NT, 0, s>>>(D, ALPHA_PRED, 1.0);
-  {
-    FinParams P{nbz, ALPHA_PRED, 0, 0, 0};
-    k_final<<<1, NTF, 0, s>>>(D, FIN_ALPHA, P);
-  }
+  // the affine step test (get_alpha_max_primal/dual with tau = 1) runs inside the solve's k_residual
+  solve_system(RHS_PRED, 0.0, redo ? 2 : 1, ALPHA_PRED, 1.0);
   // mu_affine at (alpha_aff_p, alpha_aff_d) and mu_curr; the alphas never leave the device
   k_mu<<<nbz, NT, 0, s>>>(D, 1, 0.0, 0.0);
   launch_reduce_final(FIN_MU_PRED, nbz);
-  solve_system(RHS_CORR, 0.0);
+  double tau = 1.0;
+  const int amode = fuse_step ? step_alpha_mode(tau) : -1;
+  solve_system(RHS_CORR, 0.0, 0, amode, tau);
+}
+
+// the step test update_step_size! runs for the configured rule (its mode and tau parameter)
+int MPCSolver::step_alpha_mode(double& tau) const {
+  if (opt_.step_rule == 2) {
+    tau = 1.0;
+    return ALPHA_MEHROTRA;
+  }
+  tau = opt_.step_tau;
+  return opt_.step_rule == 0 ? ALPHA_CONSERVATIVE : ALPHA_ADAPTIVE;
 }
 
 // update_step_size! (solver.jl:304-307)
-void MPCSolver::step_size() {
+// fused: the corrector solve already ran the step test (directions(.., true))
+void MPCSolver::step_size(bool fused) {
   DV_ARGS;
   hipStream_t s = stream_;
   const int nbz = blocks(std::max(nlb_, nub_));
-  if (opt_.step_rule == 2) {
-    k_alpha<<<nbz, NT, 0, s>>>(D, ALPHA_MEHROTRA, 1.0);
-    FinParams P{nbz, ALPHA_MEHROTRA, 0, 0, 0};
+  double tau = 1.0;
+  const int mode = step_alpha_mode(tau);
+  if (!fused) {
+    k_alpha<<<nbz, NT, 0, s>>>(D, mode, tau);
+    FinParams P{nbz, mode, 0, 0, 0, 0};
     k_final<<<1, NTF, 0, s>>>(D, FIN_ALPHA, P);
+  }
+  if (opt_.step_rule == 2) {
     k_mu<<<nbz, NT, 0, s>>>(D, 1, 0.0, 0.0);
     launch_reduce_final(FIN_MU_FULL, nbz);
-  } else {
-    const int mode = opt_.step_rule == 0 ? ALPHA_CONSERVATIVE : ALPHA_ADAPTIVE;
-    k_alpha<<<nbz, NT, 0, s>>>(D, mode, opt_.step_tau);
-    FinParams P{nbz, mode, 0, 0, 0};
-    k_final<<<1, NTF, 0, s>>>(D, FIN_ALPHA, P);
   }
 }
 
@@ -1722,8 +1783,6 @@ int MPCSolver::solve(madipm_stats* stats) {
     const int nb = blocks(n_ + m_);
     while (true) {
       // ---- update_termination_criteria! (+ speculative factorization of this iteration)
-      k_term<<<nb, NT, 0, s>>>(D);
-      launch_reduce_final(FIN_TERM, nb);
       const double del_w_print = del_w_;
       // factorize_system! = update_regularization! + factorize_regularized_system!
       double save_w = del_w_, save_c = del_c_;
@@ -1739,7 +1798,12 @@ int MPCSolver::solve(madipm_stats* stats) {
       // first trial enqueued together with the state read-back: ONE sync per iteration.  At
       // k >= max_iter the termination test ends the solve whatever it finds: nothing to speculate.
       const bool last = k_ >= opt_.max_iter;
-      if (!last) factor_enqueue(del_w_, del_c_);
+      k_term<<<nb, NT, 0, s>>>(D, last ? 0 : 1, del_w_, del_c_);
+      launch_reduce_final(FIN_TERM, nb);
+      if (!last) {
+        assemble_kkt(del_w_, del_c_, true);
+        timed_factorize();
+      }
       read_state();
       // speculation: this iteration's directions (prediction_step!, mehrotra_correction_direction!,
       // update_step_size!) are enqueued BEFORE the host reads the termination test and the
@@ -1749,8 +1813,8 @@ int MPCSolver::solve(madipm_stats* stats) {
       // loop synchronises internally: not speculated.
       const bool spec = opt_.max_ncorr == 0 && !last;
       if (spec) {
-        directions(false);
-        step_size();
+        directions(false, true);
+        step_size(true);
       }
       wait_state();
       const int frc = last ? 0 : ldl_->status(s, false);
@@ -1814,14 +1878,14 @@ int MPCSolver::solve(madipm_stats* stats) {
           break;
         }
         if (spec) {  // the speculated directions used the failed factor: recompute
-          directions(true);
-          step_size();
+          directions(true, true);
+          step_size(true);
         }
       }
       if (!spec) {
-        directions(false);
+        directions(false, false);
         gondzio();  // gondzio_correction_direction! (solver.jl:245-298)
-        step_size();
+        step_size(false);
       }
       // ---- apply_step! + evaluate_model!
       k_apply<<<nb, NT, 0, s>>>(D);

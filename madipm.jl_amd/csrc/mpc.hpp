@@ -60,16 +60,20 @@ class MPCSolver {
   std::unique_ptr<LinSolver> make_linsolver(int n, const int64_t* cp, const int32_t* ri, const SymbolicOptions& so);
   void initialize();
   void init_starting_point();
-  void solve_system(int mode, double mu, int reset = 0);
+  // amode >= 0: k_residual also runs the step test of that mode (k_alpha fused, see k_residual)
+  void solve_system(int mode, double mu, int reset = 0, int amode = -1, double atau = 1.0);
   void gondzio();
-  void directions(bool redo);  // predictor + corrector directions (speculated before the status read)
-  void step_size();
-  void launch_reduce_final(int kind, int nvals);
+  // predictor + corrector directions (speculated before the status read); fuse_step: the corrector's
+  // solve also runs update_step_size!'s step test (only when nothing changes d in between: no Gondzio)
+  void directions(bool redo, bool fuse_step);
+  void step_size(bool fused);
+  void launch_reduce_final(int kind, int nvals, int amode = -1);
+  int step_alpha_mode(double& tau) const;
   void read_state();  // enqueue the publication of the device state to the host mirror
   void wait_state();  // wait (host spin) until the last publication has landed
   void kkt_diag(double dw, double dc);
   // build_kkt!: diagonal (+ K2.5 scaling / normal-matrix assembly) -> values handed to the LDL^T
-  void assemble_kkt(double dw, double dc);
+  void assemble_kkt(double dw, double dc, bool diag_done = false);
   const double* kvals() const;
   // MadNLP.solve!(kkt, d) after the right-hand side is in d_: reduced solve in the chosen formulation
   void kkt_solve();
