@@ -99,7 +99,7 @@ __device__ __forceinline__ double csr_dot(const DCsr& A, int row, const double* 
 }
 
 template <int NV>
-__device__ void block_partials(double (&v)[NV], const int (&ops)[NV], double* part) {
+__device__ void block_partials(double (&v)[NV], const int (&ops)[NV], double* part, int base = 0) {
   __shared__ double sh[NV][NT / 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
@@ -113,7 +113,7 @@ __device__ void block_partials(double (&v)[NV], const int (&ops)[NV], double* pa
     const int k = threadIdx.x;
     double a = sh[k][0];
     for (int w = 1; w < NT / 64; ++w) a = comb(a, sh[k][w], ops[k]);
-    part[pidx(blockIdx.x, k)] = a;
+    part[pidx(blockIdx.x, base + k)] = a;
   }
 }
 
@@ -345,12 +345,12 @@ __global__ __launch_bounds__(NT) void k_rhs(DV D, int mode, double mu_g, int res
 }
 
 // finish_aug_solve! [EXT] + residual w = p - K d (mul!/_kktmul! [EXT], linear_solver.jl:29-35)
-// amode >= 0: the max-ratio step test of k_alpha (same mode, tau and expressions) is evaluated here,
-// by the lane that has just formed dz for the variable, into partial slots 8..15 — k_final(FIN_RESID,
-// with_alpha) then finalises both, saving k_alpha and its finaliser per direction.  The (value,
-// smallest index) argmin does not depend on the combine order, so the step is bitwise k_alpha's.
 enum { ALPHA_PRED = 0, ALPHA_CONSERVATIVE = 1, ALPHA_ADAPTIVE = 2, ALPHA_MEHROTRA = 3, ALPHA_GONDZIO = 4 };
-constexpr int PART_ALPHA = 8;  // first partial slot of the fused step test (4 values, 4 indices)
+// k_alpha may write its partials from slot PART_ALPHA (4 values, 4 indices) so that the residual's
+// finaliser finalises both (one k_final less per direction).  Measured and reverted: the step test
+// inside k_residual itself — its division-heavy tail then runs on one lane per SpMV lane group
+// (k_residual 20.9 -> 32.2 us per launch, more than the two launches it saved).
+constexpr int PART_ALPHA = 8;
 
 __device__ __forceinline__ double alpha_tau(const DV& D, int mode, double tau_param) {
   double tau = 1.0;
@@ -390,14 +390,10 @@ __device__ void block_argmin4(const double (&v)[4], const int (&ix)[4], double* 
 }
 
 template <int G>
-__global__ __launch_bounds__(NT) void k_residual(DV D, double dw, double dc, int amode, double atau) {
+__global__ __launch_bounds__(NT) void k_residual(DV D, double dw, double dc) {
   const int n = D.n, m = D.m, nlb = D.nlb;
   const bool lead = (threadIdx.x & (G - 1)) == 0;
   double wmax = 0.0, pmax = 0.0, dxmax = 0.0;
-  const bool fa = amode >= 0;
-  const double tau = fa ? alpha_tau(D, amode, atau) : 1.0;
-  double av[4] = {INF, INF, INF, INF};
-  int ai[4] = {-1, -1, -1, -1};
   GROUP_LOOP(i, n + m, G) {
     if (i < n) {
       const double hj = gdot<G>(D.H, i, D.d) + gdot<G>(D.JT, i, D.d + n);
@@ -409,10 +405,6 @@ __global__ __launch_bounds__(NT) void k_residual(DV D, double dw, double dc, int
         const double pl = D.p[n + m + kl];
         const double dzl = (-pl + D.l_lower[kl] * dx) / D.l_diag[kl];
         D.d[n + m + kl] = dzl;
-        if (fa) {  // k_alpha's lower-bound terms, t = kl
-          if (dx < 0) amin_upd(av[0], ai[0], (-D.x[i] + D.xl[i]) * tau / dx, kl);
-          if (dzl < 0) amin_upd(av[2], ai[2], (-D.zl[i]) * tau / dzl, kl);
-        }
         kv -= dzl;
         const double wl = pl - (dx * D.l_lower[kl] - dzl * D.l_diag[kl]);
         wmax = nmax(wmax, fabs(wl));
@@ -422,11 +414,6 @@ __global__ __launch_bounds__(NT) void k_residual(DV D, double dw, double dc, int
         const double pu = D.p[n + m + nlb + ku];
         const double dzu = (pu - D.u_lower[ku] * dx) / D.u_diag[ku];
         D.d[n + m + nlb + ku] = dzu;
-        if (fa) {  // upper-bound terms, t = ku
-          if (dx > 0) amin_upd(av[1], ai[1], (-D.x[i] + D.xu[i]) * tau / dx, ku);
-          const double zu = D.zu[i];
-          if (dzu < 0 && zu + dzu < 0) amin_upd(av[3], ai[3], (-zu) * tau / dzu, ku);
-        }
         kv += dzu;
         const double wu = pu - (dx * D.u_lower[ku] + dzu * D.u_diag[ku]);
         wmax = nmax(wmax, fabs(wu));
@@ -449,11 +436,10 @@ __global__ __launch_bounds__(NT) void k_residual(DV D, double dw, double dc, int
   double v[3] = {wmax, pmax, dxmax};
   const int ops[3] = {OP_MAX, OP_MAX, OP_MAX};
   block_partials<3>(v, ops, D.part);
-  if (fa) block_argmin4(av, ai, D.part, PART_ALPHA);
 }
 
 // get_alpha_max_primal / get_alpha_max_dual (kernels.jl:226-272): min-ratio with argmin
-__global__ __launch_bounds__(NT) void k_alpha(DV D, int mode, double tau_param) {
+__global__ __launch_bounds__(NT) void k_alpha(DV D, int mode, double tau_param, int base) {
   const int n = D.n, m = D.m, nlb = D.nlb, nub = D.nub;
   const double tau = alpha_tau(D, mode, tau_param);
   double v[4] = {INF, INF, INF, INF};
@@ -475,7 +461,7 @@ __global__ __launch_bounds__(NT) void k_alpha(DV D, int mode, double tau_param) 
       if (dz < 0 && zu + dz < 0) amin_upd(v[3], ix[3], (-zu) * tau / dz, (int)t);
     }
   }
-  block_argmin4(v, ix, D.part, 0);
+  block_argmin4(v, ix, D.part, base);
 }
 
 enum { MU_PRED = 0, MU_FULL = 1, MU_GONDZIO = 2 };
@@ -535,7 +521,7 @@ __global__ __launch_bounds__(NT) void k_apply(DV D) {
 
 // evaluate_model! (solver.jl:319-326): obj, grad f = Hx + c, cons c = Jx - rhs, jacl = J^T y
 template <int G>
-__global__ __launch_bounds__(NT) void k_eval(DV D) {
+__global__ __launch_bounds__(NT) void k_eval(DV D, int slot) {
   const int n = D.n;
   const bool lead = (threadIdx.x & (G - 1)) == 0;
   double op = 0.0;
@@ -557,7 +543,7 @@ __global__ __launch_bounds__(NT) void k_eval(DV D) {
   }
   double v[1] = {op};
   const int ops[1] = {OP_SUM};
-  block_partials<1>(v, ops, D.part);
+  block_partials<1>(v, ops, D.part, slot);
 }
 
 // jtprod!(jacl, kkt, y)
@@ -707,10 +693,13 @@ enum {
 
 struct FinParams {
   int nb;          // number of partial blocks
-  int alpha_mode;  // for FIN_ALPHA (and FIN_RESID with_alpha)
+  int alpha_mode;  // for FIN_ALPHA (and FIN_RESID with nb_alpha > 0)
   double a, b, c;  // kind-specific parameters
-  int with_alpha;  // FIN_RESID: also finalise the step test k_residual fused (slots PART_ALPHA..)
+  int nb_alpha;    // FIN_RESID: > 0 -> also finalise k_alpha's nb_alpha partials (slots PART_ALPHA..)
+  int nb_eval;     // FIN_TERM: > 0 -> also finalise evaluate_model!'s objective (k_eval's nb_eval
+                   // partials in slot PART_EVAL, the previous iteration's; P.c = its constant)
 };
+constexpr int PART_EVAL = 6;
 
 // k_final runs as ONE block of NTF threads that reads every partial in a single memory round trip:
 // thread t owns blocks 2t, 2t + 1 (one 16-B load per value; nb <= MAXB = 2 NTF), so all nv x 16 B of
@@ -727,10 +716,11 @@ __device__ __forceinline__ double2 part2(const DV& D, int b, int k) {
 
 // the step test's argmin over the block partials in slots base.. (FIN_ALPHA: 0, fused: PART_ALPHA);
 // every thread of the block calls it (shuffles, __syncthreads), thread 0 writes the state
-__device__ void fin_alpha(const DV& D, const FinParams& P, int base, double (&sh)[8][NTF / 64], int (&shi)[4][NTF / 64]) {
+__device__ void fin_alpha(const DV& D, const FinParams& P, int nb, int base, double (&sh)[8][NTF / 64],
+                          int (&shi)[4][NTF / 64]) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int b0 = 2 * threadIdx.x;
-  const bool h0 = b0 < P.nb, h1 = b0 + 1 < P.nb;
+  const bool h0 = b0 < nb, h1 = b0 + 1 < nb;
   DevState* st = D.st;
   double v[4];
   int ix[4];
@@ -796,6 +786,24 @@ __device__ void fin_alpha(const DV& D, const FinParams& P, int base, double (&sh
   }
 }
 
+// one OP_SUM value over nb partials of `slot`, combined in the generic path's order; thread 0 returns it
+__device__ double fin_sum_slot(const DV& D, int nb, int slot, double (&sh)[8][NTF / 64]) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int b0 = 2 * threadIdx.x;
+  const bool h0 = b0 < nb, h1 = b0 + 1 < nb;
+  const double2 pv = h0 ? part2(D, b0, slot) : make_double2(0.0, 0.0);
+  double a = 0.0;
+  if (h0) a = comb(a, pv.x, OP_SUM);
+  if (h1) a = comb(a, pv.y, OP_SUM);
+  for (int o = 32; o > 0; o >>= 1) a = comb(a, __shfl_down(a, o, 64), OP_SUM);
+  if (lane == 0) sh[0][wv] = a;
+  __syncthreads();
+  double r = sh[0][0];
+  for (int w = 1; w < NTF / 64; ++w) r = comb(r, sh[0][w], OP_SUM);
+  __syncthreads();
+  return r;
+}
+
 // Combine the block partials in fixed order + scalar logic (one block of NTF threads).
 __global__ __launch_bounds__(NTF) void k_final(DV D, int kind, FinParams P) {
   __shared__ double res[NPART];
@@ -806,12 +814,16 @@ __global__ __launch_bounds__(NTF) void k_final(DV D, int kind, FinParams P) {
   const bool h0 = b0 < P.nb, h1 = b0 + 1 < P.nb;
   DevState* st = D.st;
   if (kind == FIN_ALPHA) {
-    fin_alpha(D, P, 0, sh, shi);
+    fin_alpha(D, P, P.nb, 0, sh, shi);
     return;
   }
-  if (P.with_alpha) {  // FIN_RESID of a solve whose k_residual also ran the step test
-    fin_alpha(D, P, PART_ALPHA, sh, shi);
+  if (P.nb_alpha > 0) {  // FIN_RESID + the FIN_ALPHA of the k_alpha launched after the residual
+    fin_alpha(D, P, P.nb_alpha, PART_ALPHA, sh, shi);
     __syncthreads();
+  }
+  if (P.nb_eval > 0) {  // FIN_TERM: the previous iteration's FIN_EVAL, deferred to this launch
+    const double r = fin_sum_slot(D, P.nb_eval, PART_EVAL, sh);
+    if (threadIdx.x == 0) st->obj_val = P.c + r;
   }
   int nv = 0;
   int ops[NPART];
@@ -1543,12 +1555,13 @@ void MPCSolver::kkt_solve() {
   }
 }
 
-void MPCSolver::launch_reduce_final(int kind, int nb, int amode) {
+void MPCSolver::launch_reduce_final(int kind, int nb, int amode, int nb_eval) {
   DV_ARGS;
-  FinParams P{nb, 0, 0, 0, 0, 0};
+  FinParams P{nb, 0, 0, 0, 0, 0, nb_eval};
+  if (nb_eval > 0) P.c = c0s_;
   if (amode >= 0) {
     P.alpha_mode = amode;
-    P.with_alpha = 1;
+    P.nb_alpha = blocks(std::max(nlb_, nub_));
   }
   if (kind == FIN_MU_PRED) {
     P.a = (double)(nlb_ + nub_);
@@ -1573,7 +1586,9 @@ void MPCSolver::solve_system(int mode, double mu, int reset, int amode, double a
   const int nb = blocks(n_ + m_), nbs = spmv_blocks(n_ + m_);
   k_rhs<<<nb, NT, 0, stream_>>>(D, mode, mu, reset);
   kkt_solve();
-  SPMV_LAUNCH(k_residual, nbs, stream_, D, del_w_, del_c_, amode, atau);
+  SPMV_LAUNCH(k_residual, nbs, stream_, D, del_w_, del_c_);
+  // amode >= 0: the step test of that mode on the new direction, finalised with the residual
+  if (amode >= 0) k_alpha<<<blocks(std::max(nlb_, nub_)), NT, 0, stream_>>>(D, amode, atau, PART_ALPHA);
   launch_reduce_final(FIN_RESID, nbs, amode);
 }
 
@@ -1584,8 +1599,8 @@ void MPCSolver::gondzio() {
   const double delta = 0.1, bmin = 0.1, bmax = 10.0, tau = 0.995;
   const int nbz = blocks(std::max(nlb_, nub_));
   auto ftb = [&](double& ap, double& ad) {  // get_fraction_to_boundary_step(solver, tau)
-    k_alpha<<<nbz, NT, 0, s>>>(D, ALPHA_GONDZIO, tau);
-    FinParams P{nbz, ALPHA_GONDZIO, 0, 0, 0, 0};
+    k_alpha<<<nbz, NT, 0, s>>>(D, ALPHA_GONDZIO, tau, 0);
+    FinParams P{nbz, ALPHA_GONDZIO, 0, 0, 0, 0, 0};
     k_final<<<1, NTF, 0, s>>>(D, FIN_ALPHA, P);
     read_state();
     wait_state();
@@ -1651,13 +1666,13 @@ void MPCSolver::init_starting_point() {
   // Step 1: least-squares primal correction
   k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_PRIMAL, 0.0, 0);
   kkt_solve();
-  SPMV_LAUNCH(k_residual, nb, s, D, del_w_, del_c_, -1, 1.0);
+  SPMV_LAUNCH(k_residual, nb, s, D, del_w_, del_c_);
   launch_reduce_final(FIN_RESID, nb);
   k_axpy_x<<<nbn, NT, 0, s>>>(D);
   // Step 2: dual least squares
   k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_DUAL, 0.0, 0);
   kkt_solve();
-  SPMV_LAUNCH(k_residual, nb, s, D, del_w_, del_c_, -1, 1.0);
+  SPMV_LAUNCH(k_residual, nb, s, D, del_w_, del_c_);
   launch_reduce_final(FIN_RESID, nb);
   k_copy_y<<<blocks(m_), NT, 0, s>>>(D);
   // Step 3: bound multipliers and shifts
@@ -1702,7 +1717,7 @@ void MPCSolver::initialize() {
   k_set_mu<<<1, 1, 0, s>>>(st_, 0.0);
   // callbacks at the initial point (solver.jl:166-170)
   const int nb = blocks(n_ + m_);
-  SPMV_LAUNCH(k_eval, nb, s, D);
+  SPMV_LAUNCH(k_eval, nb, s, D, 0);
   launch_reduce_final(FIN_EVAL, nb);
   // norm_c = ||primal(f)||_inf (solver.jl:174)
   std::vector<double> fh(n_);
@@ -1716,6 +1731,7 @@ void MPCSolver::initialize() {
   best_compl_ = INF;
   status_ = MADIPM_REGULAR;
   k_ = 0;
+  eval_pending_ = false;
 }
 
 void MPCSolver::initialize_public() {
@@ -1731,7 +1747,7 @@ void MPCSolver::directions(bool redo, bool fuse_step) {
   DV_ARGS;
   hipStream_t s = stream_;
   const int nbz = blocks(std::max(nlb_, nub_));
-  // the affine step test (get_alpha_max_primal/dual with tau = 1) runs inside the solve's k_residual
+  // the affine step test (get_alpha_max_primal/dual with tau = 1) is finalised with the residual
   solve_system(RHS_PRED, 0.0, redo ? 2 : 1, ALPHA_PRED, 1.0);
   // mu_affine at (alpha_aff_p, alpha_aff_d) and mu_curr; the alphas never leave the device
   k_mu<<<nbz, NT, 0, s>>>(D, 1, 0.0, 0.0);
@@ -1760,8 +1776,8 @@ void MPCSolver::step_size(bool fused) {
   double tau = 1.0;
   const int mode = step_alpha_mode(tau);
   if (!fused) {
-    k_alpha<<<nbz, NT, 0, s>>>(D, mode, tau);
-    FinParams P{nbz, mode, 0, 0, 0, 0};
+    k_alpha<<<nbz, NT, 0, s>>>(D, mode, tau, 0);
+    FinParams P{nbz, mode, 0, 0, 0, 0, 0};
     k_final<<<1, NTF, 0, s>>>(D, FIN_ALPHA, P);
   }
   if (opt_.step_rule == 2) {
@@ -1799,7 +1815,8 @@ int MPCSolver::solve(madipm_stats* stats) {
       // k >= max_iter the termination test ends the solve whatever it finds: nothing to speculate.
       const bool last = k_ >= opt_.max_iter;
       k_term<<<nb, NT, 0, s>>>(D, last ? 0 : 1, del_w_, del_c_);
-      launch_reduce_final(FIN_TERM, nb);
+      launch_reduce_final(FIN_TERM, nb, -1, eval_pending_ ? spmv_blocks(n_ + m_) : 0);
+      eval_pending_ = false;
       if (!last) {
         assemble_kkt(del_w_, del_c_, true);
         timed_factorize();
@@ -1890,8 +1907,10 @@ int MPCSolver::solve(madipm_stats* stats) {
       // ---- apply_step! + evaluate_model!
       k_apply<<<nb, NT, 0, s>>>(D);
       ++k_;
-      SPMV_LAUNCH(k_eval, spmv_blocks(n_ + m_), s, D);
-      launch_reduce_final(FIN_EVAL, spmv_blocks(n_ + m_));
+      // evaluate_model!: its objective is finalised by the next iteration's FIN_TERM (one launch
+      // less; nothing reads obj_val before the termination test)
+      SPMV_LAUNCH(k_eval, spmv_blocks(n_ + m_), s, D, PART_EVAL);
+      eval_pending_ = true;
       MADIPM_HIP(hipGetLastError());
     }
   } catch (const Error& e) {

@@ -60,14 +60,14 @@ class MPCSolver {
   std::unique_ptr<LinSolver> make_linsolver(int n, const int64_t* cp, const int32_t* ri, const SymbolicOptions& so);
   void initialize();
   void init_starting_point();
-  // amode >= 0: k_residual also runs the step test of that mode (k_alpha fused, see k_residual)
+  // amode >= 0: k_alpha of that mode runs after the residual and is finalised with it (one k_final less)
   void solve_system(int mode, double mu, int reset = 0, int amode = -1, double atau = 1.0);
   void gondzio();
   // predictor + corrector directions (speculated before the status read); fuse_step: the corrector's
   // solve also runs update_step_size!'s step test (only when nothing changes d in between: no Gondzio)
   void directions(bool redo, bool fuse_step);
   void step_size(bool fused);
-  void launch_reduce_final(int kind, int nvals, int amode = -1);
+  void launch_reduce_final(int kind, int nvals, int amode = -1, int nb_eval = 0);
   int step_alpha_mode(double& tau) const;
   void read_state();  // enqueue the publication of the device state to the host mirror
   void wait_state();  // wait (host spin) until the last publication has landed
@@ -114,6 +114,7 @@ class MPCSolver {
   uint32_t pub_seq_ = 0;
   // host scalars (MPCSolver fields of src/structure.jl:62-76)
   double del_w_ = 0, del_c_ = 0, norm_b_ = 0, norm_c_ = 0, best_compl_ = 0, obj_scale_ = 1, c0s_ = 0;
+  bool eval_pending_ = false;  // k_eval's objective partials await the next FIN_TERM
   double adapt_dp_ = 0, adapt_dd_ = 0, adapt_dmin_ = 0;
   int status_ = 0, k_ = 0;
   bool initialized_ = false;
