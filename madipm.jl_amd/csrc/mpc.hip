@@ -285,9 +285,28 @@ enum { RHS_INIT_PRIMAL = 0, RHS_INIT_DUAL = 1, RHS_PRED = 2, RHS_CORR = 3, RHS_G
 // set_*_rhs! (kernels.jl:1-58) fused with reduce_rhs! [EXT]: writes the unreduced p and the
 // reduced right-hand side d[0:n+m] handed to the LDL^T solve.
 // reset: 1 = start of an iteration's directions (max_res_ratio), 2 = also clear the NaN flag (redo)
-__global__ __launch_bounds__(NT) void k_rhs(DV D, int mode, double mu_g, int reset) {
+// publish the device state to the host mirror: payload with system-scope stores, drained and
+// released, then the counter (the host spins on the counter, MPCSolver::wait_state)
+static_assert(sizeof(DevState) % 8 == 0 && sizeof(DevState) <= 64 * 8, "k_publish: one word per lane");
+__device__ __forceinline__ void publish_state(const DevState* __restrict__ st, DevState* host, uint32_t* hseq,
+                                              uint32_t seq) {  // called by one whole wave
+  const int i = threadIdx.x;
+  if (i < (int)(sizeof(DevState) / 8))
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(host) + i, reinterpret_cast<const uint64_t*>(st)[i],
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (i == 0) __hip_atomic_store(hseq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// host != nullptr: wave 0 of block 0 first publishes the state (k_publish's work: the speculated
+// predictor's k_rhs is the first launch after the factorisation, one launch less per iteration)
+__global__ __launch_bounds__(NT) void k_rhs(DV D, int mode, double mu_g, int reset, DevState* host, uint32_t* hseq,
+                                            uint32_t seq) {
   const int n = D.n, m = D.m, nlb = D.nlb;
   const double mu = (mode == RHS_CORR) ? D.st->mu : mu_g;
+  if (host && blockIdx.x == 0 && threadIdx.x < 64) publish_state(D.st, host, hseq, seq);
   if (reset && blockIdx.x == 0 && threadIdx.x == 0) {
     D.st->max_res_ratio = 0.0;
     if (reset == 2) D.st->nan_flag = 0;
@@ -947,18 +966,8 @@ __global__ __launch_bounds__(NTF) void k_final(DV D, int kind, FinParams P) {
   }
 }
 
-// publish the device state to the host mirror: payload with system-scope stores, drained and
-// released, then the counter (one wave; the host spins on the counter, MPCSolver::wait_state)
-static_assert(sizeof(DevState) % 8 == 0 && sizeof(DevState) <= 64 * 8, "k_publish: one word per lane");
 __global__ void k_publish(const DevState* __restrict__ st, DevState* host, uint32_t* hseq, uint32_t seq) {
-  const int i = threadIdx.x;
-  if (i < (int)(sizeof(DevState) / 8))
-    __hip_atomic_store(reinterpret_cast<uint64_t*>(host) + i, reinterpret_cast<const uint64_t*>(st)[i],
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (i == 0) __hip_atomic_store(hseq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  publish_state(st, host, hseq, seq);
 }
 
 __global__ void k_copy(double* __restrict__ dst, const double* __restrict__ src, int64_t n) {
@@ -1584,7 +1593,14 @@ void MPCSolver::launch_reduce_final(int kind, int nb, int amode, int nb_eval) {
 void MPCSolver::solve_system(int mode, double mu, int reset, int amode, double atau) {
   DV_ARGS;
   const int nb = blocks(n_ + m_), nbs = spmv_blocks(n_ + m_);
-  k_rhs<<<nb, NT, 0, stream_>>>(D, mode, mu, reset);
+  DevState* host = nullptr;
+  uint32_t seq = 0;
+  if (publish_next_) {  // read_state() folded into this launch
+    host = hst_;
+    seq = ++pub_seq_;
+    publish_next_ = false;
+  }
+  k_rhs<<<nb, NT, 0, stream_>>>(D, mode, mu, reset, host, hseq_, seq);
   kkt_solve();
   SPMV_LAUNCH(k_residual, nbs, stream_, D, del_w_, del_c_);
   // amode >= 0: the step test of that mode on the new direction, finalised with the residual
@@ -1664,13 +1680,13 @@ void MPCSolver::init_starting_point() {
   // step-computation failure (oracle/mpc.py solve_system)
   if (ldl_->status(s) != 0) throw Error("init_starting_point!: KKT factorization failed", -4);
   // Step 1: least-squares primal correction
-  k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_PRIMAL, 0.0, 0);
+  k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_PRIMAL, 0.0, 0, nullptr, nullptr, 0);
   kkt_solve();
   SPMV_LAUNCH(k_residual, nb, s, D, del_w_, del_c_);
   launch_reduce_final(FIN_RESID, nb);
   k_axpy_x<<<nbn, NT, 0, s>>>(D);
   // Step 2: dual least squares
-  k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_DUAL, 0.0, 0);
+  k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_DUAL, 0.0, 0, nullptr, nullptr, 0);
   kkt_solve();
   SPMV_LAUNCH(k_residual, nb, s, D, del_w_, del_c_);
   launch_reduce_final(FIN_RESID, nb);
@@ -1821,7 +1837,6 @@ int MPCSolver::solve(madipm_stats* stats) {
         assemble_kkt(del_w_, del_c_, true);
         timed_factorize();
       }
-      read_state();
       // speculation: this iteration's directions (prediction_step!, mehrotra_correction_direction!,
       // update_step_size!) are enqueued BEFORE the host reads the termination test and the
       // factorisation status, so the GPU is busy while the host decides; they write scratch vectors
@@ -1829,9 +1844,12 @@ int MPCSolver::solve(madipm_stats* stats) {
       // discarded on termination and recomputed after a failed factorisation's retries.  Gondzio's
       // loop synchronises internally: not speculated.
       const bool spec = opt_.max_ncorr == 0 && !last;
-      if (spec) {
+      if (spec) {  // the state read-back rides on the predictor's first launch
+        publish_next_ = true;
         directions(false, true);
         step_size(true);
+      } else {
+        read_state();
       }
       wait_state();
       const int frc = last ? 0 : ldl_->status(s, false);

@@ -112,6 +112,7 @@ class MPCSolver {
   DevState* hst_ = nullptr;          // host mirror of st_ (coherent pinned memory, written by k_publish)
   uint32_t* hseq_ = nullptr;         // publication counter beside it
   uint32_t pub_seq_ = 0;
+  bool publish_next_ = false;        // the next solve_system's k_rhs publishes the state
   // host scalars (MPCSolver fields of src/structure.jl:62-76)
   double del_w_ = 0, del_c_ = 0, norm_b_ = 0, norm_c_ = 0, best_compl_ = 0, obj_scale_ = 1, c0s_ = 0;
   bool eval_pending_ = false;  // k_eval's objective partials await the next FIN_TERM
