@@ -300,12 +300,52 @@ __device__ __forceinline__ void publish_state(const DevState* __restrict__ st, D
   if (i == 0) __hip_atomic_store(hseq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// FIN_MU_PRED folded into the corrector's k_rhs: every block reduces k_mu's nb partials (slots 0..3)
+// in the same fixed order, so all blocks agree on mu bit for bit; block 0 records it in the state
+struct MuFold {
+  int nb;                         // 0: mu from the state (FIN_MU_PRED ran)
+  double cnt, has_ineq, mu_min;   // nlb + nub, has_inequalities, mu_min (FIN_MU_PRED's parameters)
+};
+
 // host != nullptr: wave 0 of block 0 first publishes the state (k_publish's work: the speculated
 // predictor's k_rhs is the first launch after the factorisation, one launch less per iteration)
 __global__ __launch_bounds__(NT) void k_rhs(DV D, int mode, double mu_g, int reset, DevState* host, uint32_t* hseq,
-                                            uint32_t seq) {
+                                            uint32_t seq, MuFold mf) {
   const int n = D.n, m = D.m, nlb = D.nlb;
-  const double mu = (mode == RHS_CORR) ? D.st->mu : mu_g;
+  double mu = (mode == RHS_CORR) ? D.st->mu : mu_g;
+  if (mf.nb > 0) {  // prediction_step! + update_barrier! (kernels.jl:176-220), as k_final(FIN_MU_PRED)
+    __shared__ double shm[4][NT / 64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int b = threadIdx.x; b < mf.nb; b += NT)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[k] += D.part[pidx(b, k)];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      for (int o = 32; o > 0; o >>= 1) a[k] += __shfl_down(a[k], o, 64);
+      if (lane == 0) shm[k][wv] = a[k];
+    }
+    __syncthreads();
+    double r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      r[k] = shm[k][0];
+      for (int w = 1; w < NT / 64; ++w) r[k] += shm[k][w];
+    }
+    const double mu_aff = mf.cnt == 0 ? 0.0 : (r[2] + r[3]) / mf.cnt;
+    const double mu_curr = mf.cnt == 0 ? 0.0 : (r[0] + r[1]) / mf.cnt;
+    double sigma = 1.0;
+    if (mf.has_ineq != 0.0) {
+      const double q = mu_aff / mu_curr;
+      sigma = fmin(fmax(q * q * q, 1e-6), 10.0);
+    }
+    mu = fmax(mf.mu_min, sigma * mu_curr);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      D.st->mu_aff = mu_aff;
+      D.st->mu_curr = mu_curr;
+      D.st->mu = mu;
+    }
+  }
   if (host && blockIdx.x == 0 && threadIdx.x < 64) publish_state(D.st, host, hseq, seq);
   if (reset && blockIdx.x == 0 && threadIdx.x == 0) {
     D.st->max_res_ratio = 0.0;
@@ -1590,7 +1630,7 @@ void MPCSolver::launch_reduce_final(int kind, int nb, int amode, int nb_eval) {
 }
 
 // solve_system! (linear_solver.jl:19-44): rhs (mode) -> LDL^T solve -> finish + residual
-void MPCSolver::solve_system(int mode, double mu, int reset, int amode, double atau) {
+void MPCSolver::solve_system(int mode, double mu, int reset, int amode, double atau, int mu_nb) {
   DV_ARGS;
   const int nb = blocks(n_ + m_), nbs = spmv_blocks(n_ + m_);
   DevState* host = nullptr;
@@ -1600,7 +1640,9 @@ void MPCSolver::solve_system(int mode, double mu, int reset, int amode, double a
     seq = ++pub_seq_;
     publish_next_ = false;
   }
-  k_rhs<<<nb, NT, 0, stream_>>>(D, mode, mu, reset, host, hseq_, seq);
+  MuFold mf{0, 0.0, 0.0, 0.0};
+  if (mu_nb > 0) mf = MuFold{mu_nb, (double)(nlb_ + nub_), H_->has_ineq ? 1.0 : 0.0, opt_.mu_min};
+  k_rhs<<<nb, NT, 0, stream_>>>(D, mode, mu, reset, host, hseq_, seq, mf);
   kkt_solve();
   SPMV_LAUNCH(k_residual, nbs, stream_, D, del_w_, del_c_);
   // amode >= 0: the step test of that mode on the new direction, finalised with the residual
@@ -1680,13 +1722,13 @@ void MPCSolver::init_starting_point() {
   // step-computation failure (oracle/mpc.py solve_system)
   if (ldl_->status(s) != 0) throw Error("init_starting_point!: KKT factorization failed", -4);
   // Step 1: least-squares primal correction
-  k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_PRIMAL, 0.0, 0, nullptr, nullptr, 0);
+  k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_PRIMAL, 0.0, 0, nullptr, nullptr, 0, MuFold{0, 0.0, 0.0, 0.0});
   kkt_solve();
   SPMV_LAUNCH(k_residual, nb, s, D, del_w_, del_c_);
   launch_reduce_final(FIN_RESID, nb);
   k_axpy_x<<<nbn, NT, 0, s>>>(D);
   // Step 2: dual least squares
-  k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_DUAL, 0.0, 0, nullptr, nullptr, 0);
+  k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_DUAL, 0.0, 0, nullptr, nullptr, 0, MuFold{0, 0.0, 0.0, 0.0});
   kkt_solve();
   SPMV_LAUNCH(k_residual, nb, s, D, del_w_, del_c_);
   launch_reduce_final(FIN_RESID, nb);
@@ -1765,12 +1807,12 @@ void MPCSolver::directions(bool redo, bool fuse_step) {
   const int nbz = blocks(std::max(nlb_, nub_));
   // the affine step test (get_alpha_max_primal/dual with tau = 1) is finalised with the residual
   solve_system(RHS_PRED, 0.0, redo ? 2 : 1, ALPHA_PRED, 1.0);
-  // mu_affine at (alpha_aff_p, alpha_aff_d) and mu_curr; the alphas never leave the device
+  // mu_affine at (alpha_aff_p, alpha_aff_d) and mu_curr; the alphas never leave the device.  The
+  // barrier update (FIN_MU_PRED) is finalised inside the corrector's k_rhs (no separate launch).
   k_mu<<<nbz, NT, 0, s>>>(D, 1, 0.0, 0.0);
-  launch_reduce_final(FIN_MU_PRED, nbz);
   double tau = 1.0;
   const int amode = fuse_step ? step_alpha_mode(tau) : -1;
-  solve_system(RHS_CORR, 0.0, 0, amode, tau);
+  solve_system(RHS_CORR, 0.0, 0, amode, tau, nbz);
 }
 
 // the step test update_step_size! runs for the configured rule (its mode and tau parameter)

@@ -61,7 +61,8 @@ class MPCSolver {
   void initialize();
   void init_starting_point();
   // amode >= 0: k_alpha of that mode runs after the residual and is finalised with it (one k_final less)
-  void solve_system(int mode, double mu, int reset = 0, int amode = -1, double atau = 1.0);
+  // mu_nb > 0: the corrector's k_rhs finalises the barrier update from k_mu's mu_nb partials
+  void solve_system(int mode, double mu, int reset = 0, int amode = -1, double atau = 1.0, int mu_nb = 0);
   void gondzio();
   // predictor + corrector directions (speculated before the status read); fuse_step: the corrector's
   // solve also runs update_step_size!'s step test (only when nothing changes d in between: no Gondzio)
