@@ -775,20 +775,26 @@ __device__ __forceinline__ double2 part2(const DV& D, int b, int k) {
 
 // the step test's argmin over the block partials in slots base.. (FIN_ALPHA: 0, fused: PART_ALPHA);
 // every thread of the block calls it (shuffles, __syncthreads), thread 0 writes the state
-__device__ void fin_alpha(const DV& D, const FinParams& P, int nb, int base, double (&sh)[8][NTF / 64],
-                          int (&shi)[4][NTF / 64]) {
+// loads first (fin_alpha_load), so that a finaliser combining several reductions has every load of
+// the thread in flight together; the reduce needs the same nb
+__device__ __forceinline__ void fin_alpha_load(const DV& D, int nb, int base, double2 (&pv)[4], double2 (&pi)[4]) {
+  const int b0 = 2 * threadIdx.x;
+  const bool h0 = b0 < nb;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    pv[k] = h0 ? part2(D, b0, base + k) : make_double2(INF, INF);
+    pi[k] = h0 ? part2(D, b0, base + 4 + k) : make_double2(-1.0, -1.0);
+  }
+}
+
+__device__ void fin_alpha(const DV& D, const FinParams& P, int nb, const double2 (&pv)[4], const double2 (&pi)[4],
+                          double (&sh)[8][NTF / 64], int (&shi)[4][NTF / 64]) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int b0 = 2 * threadIdx.x;
   const bool h0 = b0 < nb, h1 = b0 + 1 < nb;
   DevState* st = D.st;
   double v[4];
   int ix[4];
-  double2 pv[4], pi[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    pv[k] = h0 ? part2(D, b0, base + k) : make_double2(INF, INF);
-    pi[k] = h0 ? part2(D, b0, base + 4 + k) : make_double2(-1.0, -1.0);
-  }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     v[k] = INF;
@@ -845,12 +851,12 @@ __device__ void fin_alpha(const DV& D, const FinParams& P, int nb, int base, dou
   }
 }
 
-// one OP_SUM value over nb partials of `slot`, combined in the generic path's order; thread 0 returns it
-__device__ double fin_sum_slot(const DV& D, int nb, int slot, double (&sh)[8][NTF / 64]) {
+// one OP_SUM value over nb partials (pv = this thread's pair, loaded by the caller), combined in the
+// generic path's order; thread 0 returns it
+__device__ double fin_sum_slot(int nb, double2 pv, double (&sh)[8][NTF / 64]) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int b0 = 2 * threadIdx.x;
   const bool h0 = b0 < nb, h1 = b0 + 1 < nb;
-  const double2 pv = h0 ? part2(D, b0, slot) : make_double2(0.0, 0.0);
   double a = 0.0;
   if (h0) a = comb(a, pv.x, OP_SUM);
   if (h1) a = comb(a, pv.y, OP_SUM);
@@ -873,16 +879,10 @@ __global__ __launch_bounds__(NTF) void k_final(DV D, int kind, FinParams P) {
   const bool h0 = b0 < P.nb, h1 = b0 + 1 < P.nb;
   DevState* st = D.st;
   if (kind == FIN_ALPHA) {
-    fin_alpha(D, P, P.nb, 0, sh, shi);
+    double2 apv[4], api[4];
+    fin_alpha_load(D, P.nb, 0, apv, api);
+    fin_alpha(D, P, P.nb, apv, api, sh, shi);
     return;
-  }
-  if (P.nb_alpha > 0) {  // FIN_RESID + the FIN_ALPHA of the k_alpha launched after the residual
-    fin_alpha(D, P, P.nb_alpha, PART_ALPHA, sh, shi);
-    __syncthreads();
-  }
-  if (P.nb_eval > 0) {  // FIN_TERM: the previous iteration's FIN_EVAL, deferred to this launch
-    const double r = fin_sum_slot(D, P.nb_eval, PART_EVAL, sh);
-    if (threadIdx.x == 0) st->obj_val = P.c + r;
   }
   int nv = 0;
   int ops[NPART];
@@ -897,10 +897,22 @@ __global__ __launch_bounds__(NTF) void k_final(DV D, int kind, FinParams P) {
     case FIN_ZSHIFT1: nv = 8; for (int k = 0; k < 8; ++k) ops[k] = OP_SUM; break;
     case FIN_ZSHIFT2: nv = 1; ops[0] = OP_SUM; break;
   }
-  {
-    double2 pv[8];
+  // every load of the thread is issued before the first reduction (one memory round trip)
+  double2 pv[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) pv[k] = (h0 && k < nv) ? part2(D, b0, k) : make_double2(0.0, 0.0);
+  for (int k = 0; k < 8; ++k) pv[k] = (h0 && k < nv) ? part2(D, b0, k) : make_double2(0.0, 0.0);
+  double2 apv[4], api[4];
+  if (P.nb_alpha > 0) fin_alpha_load(D, P.nb_alpha, PART_ALPHA, apv, api);
+  const double2 epv = (P.nb_eval > 0 && b0 < P.nb_eval) ? part2(D, b0, PART_EVAL) : make_double2(0.0, 0.0);
+  if (P.nb_alpha > 0) {  // FIN_RESID + the FIN_ALPHA of the k_alpha launched after the residual
+    fin_alpha(D, P, P.nb_alpha, apv, api, sh, shi);
+    __syncthreads();
+  }
+  if (P.nb_eval > 0) {  // FIN_TERM: the previous iteration's FIN_EVAL, deferred to this launch
+    const double r = fin_sum_slot(P.nb_eval, epv, sh);
+    if (threadIdx.x == 0) st->obj_val = P.c + r;
+  }
+  {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       if (k >= nv) break;
