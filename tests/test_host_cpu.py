@@ -299,3 +299,22 @@ def test_presolve_free_rows_singleton_columns_unconstrained_quadratic():
     A = np.zeros((3, 5))
     A[qp.Arows, qp.Acols] = qp.Avals
     assert abs(A[0] @ xo - 4.0) <= 1e-8
+
+
+@pytest.mark.parametrize("ordering", [1, 3, 4])
+def test_dense_block_orderings_defer_constraint_vertices(ordering):
+    """K2 of a QP with a dense A (m x n, m < n) and a diagonal H: every ordering must eliminate the
+    x columns first (batched leaves) and the m constraint vertices last, the optimal fill
+    n (m + 1) + m (m + 1) / 2.  Nested dissection defers the dense vertices (csrc/nd.cpp) like AMD."""
+    from madipm_amd._lib import Symbolic, default_ldl_opts
+    n, m = 300, 40
+    N = n + m
+    colptr = np.concatenate([np.arange(n + 1, dtype=np.int64) * (m + 1),
+                             n * (m + 1) + np.arange(1, m + 1, dtype=np.int64)])
+    blk = np.empty((n, m + 1), np.int32)
+    blk[:, 0] = np.arange(n)
+    blk[:, 1:] = n + np.arange(m)[None, :]
+    rows = np.concatenate([blk.ravel(), n + np.arange(m, dtype=np.int32)])
+    S = Symbolic(N, colptr, rows, default_ldl_opts(ordering=ordering))
+    assert S.info()["nnzL"] == n * (m + 1) + m * (m + 1) // 2
+    assert sorted(S.perm()[-m:].tolist()) == list(range(n, N))
