@@ -574,9 +574,25 @@ __global__ __launch_bounds__(ANT) void k_assemble(FrontTab T, const SymbolicPlan
       const double* __restrict__ U = arena + T.u_off[c];
       const int64_t ldc = T.u_ld[c];
       const int32_t* __restrict__ rel = T.rel + T.rel_ptr[c];
-      for (int b = b0 + wv; b < b1; b += ANT / 64) {
-        const int cb = (rel[b] - J0) * 64 - I0;
-        for (int a = max(b, a0) + lane; a < a1; a += 64) Ft[rel[a] + cb] += U[a + b * ldc];
+      // a wave takes 4 of its columns at once: the row map rel[a] is loaded once for them and their
+      // 4 U loads are in flight together (one dependent round trip per row chunk, not per column)
+      constexpr int NW = ANT / 64;
+      for (int b = b0 + wv; b < b1; b += 4 * NW) {
+        int cb[4], bk[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          bk[k] = b + k * NW;
+          cb[k] = (bk[k] < b1) ? (rel[bk[k]] - J0) * 64 - I0 : 0;
+        }
+        for (int a = max(b, a0) + lane; a < a1; a += 64) {
+          const int ra = rel[a];
+          double u[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) u[k] = (bk[k] < b1 && a >= bk[k]) ? U[a + bk[k] * ldc] : 0.0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (bk[k] < b1 && a >= bk[k]) Ft[ra + cb[k]] += u[k];
+        }
       }
       __syncthreads();
     }
