@@ -99,7 +99,7 @@ __device__ __forceinline__ double csr_dot(const DCsr& A, int row, const double* 
 }
 
 template <int NV>
-__device__ void block_partials(double (&v)[NV], const int (&ops)[NV], double* part, int base = 0) {
+__device__ void block_partials(double (&v)[NV], const int (&ops)[NV], double* part, int base = 0, int bid = -1) {
   __shared__ double sh[NV][NT / 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
@@ -113,7 +113,7 @@ __device__ void block_partials(double (&v)[NV], const int (&ops)[NV], double* pa
     const int k = threadIdx.x;
     double a = sh[k][0];
     for (int w = 1; w < NT / 64; ++w) a = comb(a, sh[k][w], ops[k]);
-    part[pidx(blockIdx.x, base + k)] = a;
+    part[pidx(bid >= 0 ? bid : (int)blockIdx.x, base + k)] = a;
   }
 }
 
@@ -132,6 +132,11 @@ __device__ __forceinline__ void amin_upd(double& v, int& ix, double nv, int ni) 
 // problem from the mean row length (MPCSolver::spmv_group).
 #define GROUP_LOOP(i, N, G) \
   for (int64_t i = (blockIdx.x * (int64_t)NT + threadIdx.x) / (G); i < (N); i += (int64_t)gridDim.x * (NT / (G)))
+// the same loops over a sub-grid of nblk blocks (block bid of it): kernels whose blocks split into roles
+#define GROUP_LOOP_B(i, N, G, bid, nblk) \
+  for (int64_t i = ((bid) * (int64_t)NT + threadIdx.x) / (G); i < (N); i += (int64_t)(nblk) * (NT / (G)))
+#define GRID_LOOP_B(i, N, bid, nblk) \
+  for (int64_t i = (bid) * (int64_t)blockDim.x + threadIdx.x; i < (N); i += (int64_t)(nblk) * blockDim.x)
 
 template <int G>
 __device__ __forceinline__ double gdot(const DCsr& A, int64_t row, const double* __restrict__ x) {
@@ -419,7 +424,7 @@ __device__ __forceinline__ double alpha_tau(const DV& D, int mode, double tau_pa
 }
 
 // block argmin of (v[k], ix[k]), k < 4, into part slots base + k (values) and base + 4 + k (indices)
-__device__ void block_argmin4(const double (&v)[4], const int (&ix)[4], double* part, int base) {
+__device__ void block_argmin4(const double (&v)[4], const int (&ix)[4], double* part, int base, int bid) {
   __shared__ double sv[4][NT / 64];
   __shared__ int si[4][NT / 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -443,17 +448,25 @@ __device__ void block_argmin4(const double (&v)[4], const int (&ix)[4], double* 
     double a = sv[k][0];
     int b = si[k][0];
     for (int w = 1; w < NT / 64; ++w) amin_upd(a, b, sv[k][w], si[k][w]);
-    part[pidx(blockIdx.x, base + k)] = a;
-    part[pidx(blockIdx.x, base + 4 + k)] = (double)b;
+    part[pidx(bid, base + k)] = a;
+    part[pidx(bid, base + 4 + k)] = (double)b;
   }
 }
 
+__device__ void alpha_body(const DV& D, int mode, double tau_param, int base, int bid, int nblk, bool from_p);
+
+// nres < gridDim.x: blocks [nres, gridDim.x) run the step test of mode amode (alpha_body, partials
+// from slot PART_ALPHA) beside the nres residual blocks — one launch for both
 template <int G>
-__global__ __launch_bounds__(NT) void k_residual(DV D, double dw, double dc) {
+__global__ __launch_bounds__(NT) void k_residual(DV D, double dw, double dc, int nres, int amode, double atau) {
   const int n = D.n, m = D.m, nlb = D.nlb;
+  if ((int)blockIdx.x >= nres) {
+    alpha_body(D, amode, atau, PART_ALPHA, (int)blockIdx.x - nres, (int)gridDim.x - nres, true);
+    return;
+  }
   const bool lead = (threadIdx.x & (G - 1)) == 0;
   double wmax = 0.0, pmax = 0.0, dxmax = 0.0;
-  GROUP_LOOP(i, n + m, G) {
+  GROUP_LOOP_B(i, n + m, G, (int)blockIdx.x, nres) {
     if (i < n) {
       const double hj = gdot<G>(D.H, i, D.d) + gdot<G>(D.JT, i, D.d + n);
       if (!lead) continue;
@@ -494,33 +507,39 @@ __global__ __launch_bounds__(NT) void k_residual(DV D, double dw, double dc) {
   }
   double v[3] = {wmax, pmax, dxmax};
   const int ops[3] = {OP_MAX, OP_MAX, OP_MAX};
-  block_partials<3>(v, ops, D.part);
+  block_partials<3>(v, ops, D.part, 0, (int)blockIdx.x);
 }
 
 // get_alpha_max_primal / get_alpha_max_dual (kernels.jl:226-272): min-ratio with argmin
-__global__ __launch_bounds__(NT) void k_alpha(DV D, int mode, double tau_param, int base) {
+// from_p: dz formed here from the reduced rhs p and dx, exactly as k_residual's finish_aug_solve
+// forms it (the step-test blocks of a k_residual launch run beside the residual blocks that store it)
+__device__ void alpha_body(const DV& D, int mode, double tau_param, int base, int bid, int nblk, bool from_p) {
   const int n = D.n, m = D.m, nlb = D.nlb, nub = D.nub;
   const double tau = alpha_tau(D, mode, tau_param);
   double v[4] = {INF, INF, INF, INF};
   int ix[4] = {-1, -1, -1, -1};
-  GRID_LOOP(t, (nlb > nub ? nlb : nub)) {
+  GRID_LOOP_B(t, (nlb > nub ? nlb : nub), bid, nblk) {
     if (t < nlb) {
       const int i = D.ind_lb[t];
       const double dx = D.d[i];
       if (dx < 0) amin_upd(v[0], ix[0], (-D.x[i] + D.xl[i]) * tau / dx, (int)t);
-      const double dz = D.d[n + m + t];
+      const double dz = from_p ? (-D.p[n + m + t] + D.l_lower[t] * dx) / D.l_diag[t] : D.d[n + m + t];
       if (dz < 0) amin_upd(v[2], ix[2], (-D.zl[i]) * tau / dz, (int)t);
     }
     if (t < nub) {
       const int i = D.ind_ub[t];
       const double dx = D.d[i];
       if (dx > 0) amin_upd(v[1], ix[1], (-D.x[i] + D.xu[i]) * tau / dx, (int)t);
-      const double dz = D.d[n + m + nlb + t];
+      const double dz = from_p ? (D.p[n + m + nlb + t] - D.u_lower[t] * dx) / D.u_diag[t] : D.d[n + m + nlb + t];
       const double zu = D.zu[i];
       if (dz < 0 && zu + dz < 0) amin_upd(v[3], ix[3], (-zu) * tau / dz, (int)t);
     }
   }
-  block_argmin4(v, ix, D.part, base);
+  block_argmin4(v, ix, D.part, base, bid);
+}
+
+__global__ __launch_bounds__(NT) void k_alpha(DV D, int mode, double tau_param, int base) {
+  alpha_body(D, mode, tau_param, base, blockIdx.x, gridDim.x, false);
 }
 
 enum { MU_PRED = 0, MU_FULL = 1, MU_GONDZIO = 2 };
@@ -1656,9 +1675,10 @@ void MPCSolver::solve_system(int mode, double mu, int reset, int amode, double a
   if (mu_nb > 0) mf = MuFold{mu_nb, (double)(nlb_ + nub_), H_->has_ineq ? 1.0 : 0.0, opt_.mu_min};
   k_rhs<<<nb, NT, 0, stream_>>>(D, mode, mu, reset, host, hseq_, seq, mf);
   kkt_solve();
-  SPMV_LAUNCH(k_residual, nbs, stream_, D, del_w_, del_c_);
-  // amode >= 0: the step test of that mode on the new direction, finalised with the residual
-  if (amode >= 0) k_alpha<<<blocks(std::max(nlb_, nub_)), NT, 0, stream_>>>(D, amode, atau, PART_ALPHA);
+  // amode >= 0: the step test of that mode on the new direction runs in the same launch (its own
+  // blocks) and is finalised with the residual
+  const int nbz = amode >= 0 ? blocks(std::max(nlb_, nub_)) : 0;
+  SPMV_LAUNCH(k_residual, nbs + nbz, stream_, D, del_w_, del_c_, nbs, amode, atau);
   launch_reduce_final(FIN_RESID, nbs, amode);
 }
 
@@ -1736,13 +1756,13 @@ void MPCSolver::init_starting_point() {
   // Step 1: least-squares primal correction
   k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_PRIMAL, 0.0, 0, nullptr, nullptr, 0, MuFold{0, 0.0, 0.0, 0.0});
   kkt_solve();
-  SPMV_LAUNCH(k_residual, nb, s, D, del_w_, del_c_);
+  SPMV_LAUNCH(k_residual, nb, s, D, del_w_, del_c_, nb, -1, 1.0);
   launch_reduce_final(FIN_RESID, nb);
   k_axpy_x<<<nbn, NT, 0, s>>>(D);
   // Step 2: dual least squares
   k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_DUAL, 0.0, 0, nullptr, nullptr, 0, MuFold{0, 0.0, 0.0, 0.0});
   kkt_solve();
-  SPMV_LAUNCH(k_residual, nb, s, D, del_w_, del_c_);
+  SPMV_LAUNCH(k_residual, nb, s, D, del_w_, del_c_, nb, -1, 1.0);
   launch_reduce_final(FIN_RESID, nb);
   k_copy_y<<<blocks(m_), NT, 0, s>>>(D);
   // Step 3: bound multipliers and shifts
