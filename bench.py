@@ -22,6 +22,7 @@ multi-GPU: (N > 1, launched by torch.distributed.run) ONE solve of the workload 
 from __future__ import annotations
 
 import argparse
+import re
 import glob
 import json
 import os
@@ -190,7 +191,11 @@ def roofline(stats: list, dominant: str):
     else:
         ach, peak, unit = nbytes / avg_s / 1e9, PEAK_HBM_GBS, "GB/s"
     traffic, src = None, None
-    pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    def _rv(path):  # r<round>_v<n>: numeric order (r2_v10 after r2_v3)
+        m = re.search(r"r(\d+)_v(\d+)", os.path.basename(path))
+        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
+
+    pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), key=_rv)
     if pmc:  # PMC counters can not be read inside the timed run: the latest committed pass of this workload
         ent = json.load(open(pmc[-1]))["kernels"].get(dominant)
         if ent:
