@@ -100,54 +100,28 @@ def baseline_threads() -> int:
     return max(1, n)
 
 
-def cpu_baseline(qp, perm, budget_s: float = 20.0):
-    """CPU baseline on this host (SURVEY §8 d; scripts/benchmarks_cpu.jl:26-50 drives MadIPM with a
-    multithreaded supernodal LDL^T, HSL MA57, which is unavailable here): the oracle's MPC loop
-    (oracle/mpc.py, a restatement of src/solver.jl) with Intel MKL PARDISO (oracle/pardiso.py,
-    supernodal symmetric-indefinite, the same fill-reducing order as the GPU) as its linear solver.
-
-    * `threads` run: to optimality at the host's core share -> the parity record (status, objective,
-      iterations vs the GPU) and the timings;
-    * 1-thread run: a bounded sample (about `budget_s` of CPU work).
-    `value` = MPC iterations / (PARDISO factorisation + solve time): the rate a native host driver
-    would reach with PARDISO (the numpy loop around it is not counted); the full loop rate is
-    reported beside it."""
-    from oracle.mpc import OracleMPC, OracleOptions
-    from oracle import pardiso
-
-    def run(k, threads):
-        got = pardiso.set_threads(threads)
-        o = OracleMPC(qp, OracleOptions(regularization=("fixed", 1e-8, -1e-8), step_rule=("adaptive", 0.99),
-                                        max_iter=k, tol=1e-8), record_trace=False)
-        o.linear_solver = "pardiso"
-        o.ldl_perm = perm
-        t0 = time.perf_counter()
-        st = o.solve()
-        F = o._pardiso
-        return st, {"threads": got, "iters": st.iter, "loop_s": st.total_time, "wall_s": time.perf_counter() - t0,
-                    "pardiso_factor_s": F.t_factor, "pardiso_solve_s": F.t_solve, "factorizations": F.nfactor,
-                    "solves": F.nsolve, "pardiso_analysis_s": F.t_analysis, "nnzL_pardiso": F.nnzL,
-                    "perturbed_pivots": F.nperturbed}
-    T = baseline_threads()
-    st, full = run(300, T)
-    it_t = full["iters"] / (full["pardiso_factor_s"] + full["pardiso_solve_s"])
-    # 1 thread: bounded sample, scaled from the multithreaded per-iteration PARDISO time
-    per_it = (full["pardiso_factor_s"] + full["pardiso_solve_s"]) / max(1, full["factorizations"]) * 3.0
-    k1 = int(max(2, min(full["iters"], budget_s / max(per_it, 1e-3))))
-    _, one = run(k1, 1)
-    it_1 = one["iters"] / (one["pardiso_factor_s"] + one["pardiso_solve_s"]) if one["iters"] else None
-    # value: the faster of the two thread counts (on the ex10 fronts PARDISO's threading overhead can
-    # exceed its parallel gain); both are reported
-    best_1 = it_1 is not None and it_1 > it_t
-    return st, {
-        "value": it_1 if best_1 else it_t, "unit": "iters/s", "cores": 1 if best_1 else T, "kind": "port",
-        "sample": (f"oracle/mpc.py MPC loop + MKL PARDISO (mtype -2, GPU's fill-reducing order) on the same "
-                   f"standard-form problem, {T} threads to optimality ({full['iters']} iterations) and 1 thread "
-                   f"({one['iters']} iterations); value = iterations / PARDISO factor+solve time of the faster run "
-                   f"({'1 thread' if best_1 else f'{T} threads'})"),
-        "value_threads": it_t,
-        "loop_iters_per_s": full["iters"] / full["loop_s"] if full["loop_s"] > 0 else None,
-        "value_1thread": it_1, "runs": {"threads": full, "one_thread": one}, "host": host_cpu_info()}
+def cpu_baseline(config: str, perm, max_threads: int, timeout_s: float = 240.0):
+    """CPU baseline on this host (SURVEY §8 d): oracle/cpu_baseline.py in a process of its own (no torch,
+    no HIP runtime; MKL's Intel OpenMP with idle threads sleeping; pinned to `max_threads` CPUs), the
+    oracle's MPC loop with MKL PARDISO to optimality at 1, 2, 4, 8, 16 threads (capped at the host share);
+    value = iterations / PARDISO factor+solve time of the fastest thread count.  Returns (ref, record):
+    ref = (status, objective, iterations) of the CPU solve for the parity check."""
+    import subprocess
+    import tempfile
+    import numpy as np
+    with tempfile.TemporaryDirectory() as td:
+        pf = os.path.join(td, "perm.npy")
+        np.save(pf, np.asarray(perm, np.int32))
+        env = {k: v for k, v in os.environ.items() if not k.startswith(("OMP_", "MKL_", "KMP_", "GOMP_"))}
+        env["PYTHONPATH"] = ROOT
+        cmd = [sys.executable, "-m", "oracle.cpu_baseline", "--config", config, "--perm", pf,
+               "--max-threads", str(max_threads), "--threads", "1,2,4,8,16"]
+        r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout_s)
+    if r.returncode != 0:
+        raise RuntimeError(f"cpu_baseline exited {r.returncode}: {r.stderr[-2000:]}")
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    rec["host"] = host_cpu_info()
+    return (rec.pop("ref_status"), rec.pop("ref_objective"), rec.pop("ref_iter")), rec
 
 
 def highs_baseline(qp, time_limit: float = 120.0):
@@ -174,17 +148,23 @@ def highs_baseline(qp, time_limit: float = 120.0):
 # profiles/r1_mfma_f64_peak.txt holds our own measurement of the instruction's rate).
 PEAK_HBM_GBS = 8000.0
 STATUS = {1: "SOLVE_SUCCEEDED", 2: "INFEASIBLE_PROBLEM_DETECTED", -1: "MAXIMUM_ITERATIONS_EXCEEDED",
-          -2: "MAXIMUM_WALLTIME_EXCEEDED", -3: "DIVERGING_ITERATES", -4: "ERROR_IN_STEP_COMPUTATION"}
+          -2: "MAXIMUM_WALLTIME_EXCEEDED", -3: "DIVERGING_ITERATES", -4: "ERROR_IN_STEP_COMPUTATION",
+          -5: "INTERNAL_ERROR"}
 PEAK_F64_TFS = 78.6
 
 
 def roofline(stats: list, dominant: str):
-    """Roofline object for the dominant kernel from the live HIP-event statistics of the timed region."""
+    """Roofline object for the dominant kernel from the live HIP-event statistics of the timed region.
+    achieved = SURVEY 8(d)'s algorithmic bytes per launch (8 nnzL + 12 nnzK of the columns the launch
+    factorises, exact column counts of the symbolic analysis; 8 nnzL of the columns a solve launch
+    substitutes) / the event-timed average launch; the kernel's own staging-traffic model is reported
+    beside it as `staging_bytes_per_launch`, the PMC-measured HBM bytes as `traffic`."""
     k = next(x for x in stats if x["name"] == dominant)
     if k["launches"] == 0 or k["time_ms"] <= 0:
         return None
     avg_s = k["time_ms"] / k["launches"] * 1e-3
-    flops, nbytes = k["flops"] / k["launches"], k["bytes"] / k["launches"]
+    flops, nbytes = k["flops"] / k["launches"], k["alg_bytes"] / k["launches"]
+    staging = k["bytes"] / k["launches"]
     mfma = flops / (PEAK_F64_TFS * 1e12) > nbytes / (PEAK_HBM_GBS * 1e9)
     if mfma:
         ach, peak, unit = flops / avg_s / 1e12, PEAK_F64_TFS, "TFLOP/s"
@@ -202,7 +182,9 @@ def roofline(stats: list, dominant: str):
             traffic, src = ent["hbm_bytes_per_launch"], os.path.relpath(pmc[-1], ROOT)
     return {"bound": "mfma" if mfma else "hbm", "achieved": ach, "peak": peak, "unit": unit, "frac": ach / peak,
             "traffic": traffic, "traffic_source": src, "kernel": dominant, "launches": k["launches"],
-            "avg_launch_us": avg_s * 1e6, "alg_bytes_per_launch": nbytes, "alg_flops_per_launch": flops}
+            "avg_launch_us": avg_s * 1e6, "alg_bytes_per_launch": nbytes, "alg_flops_per_launch": flops,
+            "alg_bytes_definition": "SURVEY 8(d): 8 nnzL + 12 nnzK of the columns the launch factorises",
+            "staging_bytes_per_launch": staging}
 
 
 def iteration_roofline(info: dict, ms_per_step: float, vec_passes: int = 60) -> dict:
@@ -219,6 +201,14 @@ def iteration_roofline(info: dict, ms_per_step: float, vec_passes: int = 60) -> 
     return {"alg_bytes": sum(b for b, _ in phases.values()), "alg_flops": sum(f for _, f in phases.values()),
             "bound_us": {k: round(v, 2) for k, v in bound.items()}, "time_at_roofline_us": t_roof,
             "measured_us": ms_per_step * 1e3, "frac": t_roof / (ms_per_step * 1e3)}
+
+
+def rocm_version() -> str | None:
+    try:
+        with open("/opt/rocm/.info/version") as f:
+            return f.read().strip()
+    except OSError:
+        return None
 
 
 def aggregate(dt, iters, dist, sharded):
@@ -256,7 +246,6 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="ex10")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--highs", action=argparse.BooleanOptionalAction, default=True,
                     help="time HiGHS-IPM (scipy) on the same LP as a third-party CPU datapoint")
     ap.add_argument("--no-opt", action="store_true", help="skip the wall-clock-to-optimality solve")
@@ -346,6 +335,7 @@ def main():
             "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,
             "dtype": "f64",
+            "rocm": rocm_version(),
             "data": "synthetic (seeded structured stand-in; no MIPLIB MPS offline)",
             "config": {"workload": cfgname, "nvar": qp.nvar, "ncon": qp.ncon, "nnzj": qp.nnzj,
                        "kkt_n": info["n"], "nnzL": info["nnzL"], "nnzL_stored": info["nnzL_stored"],
@@ -362,18 +352,19 @@ def main():
         }
         if not args.no_cpu and world == 1 and not args.config.startswith(("dense_qp", "neos")):
             try:
-                ref, out["cpu_baseline"] = cpu_baseline(qp, solver.kkt_perm(), args.cpu_budget)
+                (r_status, r_obj, r_iter), out["cpu_baseline"] = cpu_baseline(args.config, solver.kkt_perm(),
+                                                                               baseline_threads())
                 if opt:
                     # parity at the benchmarked size: the GPU solve to optimality vs the oracle's (same
                     # problem, same settings; BASELINE.md parity rule |dobj| <= 1e-6 max(1, |obj|))
-                    rel = abs(opt["objective"] - ref.objective) / max(1.0, abs(ref.objective))
+                    rel = abs(opt["objective"] - r_obj) / max(1.0, abs(r_obj))
                     out["parity"] = {"reference": "oracle/mpc.py + MKL PARDISO (CPU)",
-                                     "status_gpu": opt["status"], "status_ref": STATUS.get(ref.status, ref.status),
-                                     "status_equal": STATUS.get(ref.status) == opt["status"],
-                                     "objective_gpu": opt["objective"], "objective_ref": ref.objective,
-                                     "rel_obj_diff": rel, "iters_gpu": opt["iters_to_opt"], "iters_ref": ref.iter,
-                                     "ok": bool(STATUS.get(ref.status) == opt["status"] and rel <= 1e-6
-                                                and abs(opt["iters_to_opt"] - ref.iter) <= 1)}
+                                     "status_gpu": opt["status"], "status_ref": STATUS.get(r_status, r_status),
+                                     "status_equal": STATUS.get(r_status) == opt["status"],
+                                     "objective_gpu": opt["objective"], "objective_ref": r_obj,
+                                     "rel_obj_diff": rel, "iters_gpu": opt["iters_to_opt"], "iters_ref": r_iter,
+                                     "ok": bool(STATUS.get(r_status) == opt["status"] and rel <= 1e-6
+                                                and abs(opt["iters_to_opt"] - r_iter) <= 1)}
             except Exception as e:  # pragma: no cover - reported, not hidden
                 out["cpu_baseline"] = {"error": repr(e)}
             if args.highs:

@@ -159,8 +159,10 @@ typedef struct madipm_kstat {
   char name[32];
   int64_t launches;
   double time_ms;          /* summed event time of the launches */
-  double bytes;            /* algorithmic bytes of those launches */
+  double bytes;            /* staging-traffic model of those launches (what the kernel moves) */
   double flops;            /* algorithmic flops of those launches */
+  double alg_bytes;        /* SURVEY 8(d)'s algorithmic bytes of those launches: 8 nnzL + 12 nnzK of the
+                              columns they factorise, 8 nnzL of the columns a solve launch substitutes */
 } madipm_kstat;
 int madipm_ldl_set_timing(madipm_ldl_t ls, uint32_t mask);
 /* synchronises the recorded events; out[MADIPM_NKERNELS] */
@@ -204,7 +206,8 @@ void madipm_spmv_destroy(madipm_spmv_t op);
 /* MadIPM.coo_to_csr(n_rows, n_cols, Ai, Aj, Ax) (src/utils.jl:158-201; GPU cuda_wrapper.jl:96-106),
  * device arrays, 0-based.  Entries are grouped by row in input order (utils.jl's counting sort);
  * sort_cols != 0 orders each row by column (ties in input order), the layout cuSPARSE produces.
- * Duplicates are kept, as in the reference.  rowptr: n_rows+1.  Synchronises `stream`. */
+ * Duplicates are kept, as in the reference.  rowptr: n_rows+1.  Synchronises `stream`.
+ * An index outside [0, n_rows) x [0, n_cols) is an error (negative return; outputs invalid). */
 int madipm_coo_to_csr(int32_t n_rows, int32_t n_cols, int64_t nnz, const int32_t* d_Ai, const int32_t* d_Aj,
                       const double* d_Ax, int32_t* d_rowptr, int32_t* d_colval, double* d_nzval,
                       int32_t sort_cols, madipm_stream_t stream);
@@ -237,6 +240,23 @@ int madipm_qp_obj(madipm_spmv_t H, const double* d_c, double c0, const double* d
                   double* d_work, double* h_obj, madipm_stream_t stream);
 int madipm_qp_grad(madipm_spmv_t H, const double* d_c, const double* d_x, double* d_g, int32_t n,
                    madipm_stream_t stream);
+
+/* update_step! (src/kernels.jl:291-358) with get_alpha_max_primal / get_alpha_max_dual
+ * (src/kernels.jl:226-272) on DEVICE vectors over the bounded coordinates (the reference's views
+ * x_lr, xl_r, zl_r, dx_lr, dual_lb(d) and x_ur, xu_r, zu_r, dx_ur, dual_ub(d)); the same kernels the
+ * native MPC loop runs.  rule: 0 ConservativeStep(tau), 1 AdaptiveStep(tau_min = tau; uses mu),
+ * 2 MehrotraAdaptiveStep(gamma_f = tau).  The argmin follows the reference's left fold with
+ * init (1.0, 0): the LAST index among equal ratios; index -1 = the init element (Julia's 0). */
+typedef struct madipm_step_result {
+  double alpha_p, alpha_d;                      /* solver.alpha_p / alpha_d after update_step! */
+  double alpha_xl, alpha_xu, alpha_zl, alpha_zu; /* the four max-ratio values (tau of the rule) */
+  int32_t i_xl, i_xu, i_zl, i_zu;               /* their argmin indices, 0-based */
+} madipm_step_result;
+int madipm_update_step(int32_t rule, double tau, double mu, int32_t nlb, int32_t nub,
+                       const double* d_x_lr, const double* d_xl_r, const double* d_zl_r, const double* d_dx_lr,
+                       const double* d_dzl, const double* d_x_ur, const double* d_xu_r, const double* d_zu_r,
+                       const double* d_dx_ur, const double* d_dzu, madipm_step_result* out,
+                       madipm_stream_t stream);
 
 /* ------------------------------------------------------------------ native MPC solver
  * `MPCSolver(qp; kwargs...)` + `solve!(solver)` (src/structure.jl:79-178, src/solver.jl:362-418)
@@ -298,7 +318,20 @@ typedef struct madipm_stats {
   double total_time;          /* MPC loop only, as cnt.total_time (src/solver.jl:181,407) */
   double linear_solver_time;  /* factorizations (GPU events) */
   double init_time;           /* symbolic analysis + initialize! */
+  int32_t exception;          /* MADIPM_EXC_*: the exception solve!'s catch-all caught (status INTERNAL_ERROR);
+                                 a binding with rethrow_error = true rethrows it (src/solver.jl:398-403) */
 } madipm_stats;
+
+/* Exceptions of the MPC loop.  Both end in solve!'s catch-all (src/solver.jl:398-403) as
+ * INTERNAL_ERROR: linear_solver.jl:41 throws the TYPE MadNLP.SolveException, which is not
+ * `isa MadNLP.LinearSolverException`, and the linear solver's own refusal to solve with an
+ * unfactorized matrix (after factorize_regularized_system!'s three failed trials,
+ * linear_solver.jl:6-17; LDLFactorizations' ldiv! [EXT]) is not one either. */
+enum {
+  MADIPM_EXC_NONE = 0,
+  MADIPM_EXC_SOLVE = 1,         /* residual NaN, or > tol_linear_solve with check_residual */
+  MADIPM_EXC_UNFACTORIZED = 2   /* solve with a failed factorization */
+};
 
 typedef struct madipm_iter_trace {
   int32_t k;

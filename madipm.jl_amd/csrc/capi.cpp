@@ -430,6 +430,7 @@ static void fill_kstats(LinSolver& l, madipm_kstat* out) {
     out[k].time_ms = st[k].ms;
     out[k].bytes = st[k].bytes;
     out[k].flops = st[k].flops;
+    out[k].alg_bytes = st[k].alg_bytes;
   }
 }
 
@@ -583,5 +584,19 @@ int madipm_solver_kernel_stats(madipm_solver_t s, madipm_kstat* out) {
 }
 
 void madipm_solver_destroy(madipm_solver_t s) { delete s; }
+
+int madipm_update_step(int32_t rule, double tau, double mu, int32_t nlb, int32_t nub, const double* d_x_lr,
+                       const double* d_xl_r, const double* d_zl_r, const double* d_dx_lr, const double* d_dzl,
+                       const double* d_x_ur, const double* d_xu_r, const double* d_zu_r, const double* d_dx_ur,
+                       const double* d_dzu, madipm_step_result* out, madipm_stream_t stream) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(out, "null argument");
+  MADIPM_REQUIRE(nlb == 0 || (d_x_lr && d_xl_r && d_zl_r && d_dx_lr && d_dzl), "null lower-bound vector");
+  MADIPM_REQUIRE(nub == 0 || (d_x_ur && d_xu_r && d_zu_r && d_dx_ur && d_dzu), "null upper-bound vector");
+  const double* v[10] = {d_x_lr, d_xl_r, d_zl_r, d_dx_lr, d_dzl, d_x_ur, d_xu_r, d_zu_r, d_dx_ur, d_dzu};
+  update_step_standalone(rule, tau, mu, nlb, nub, v, out, (hipStream_t)stream);
+  return 0;
+  MADIPM_API_END
+}
 
 }  // extern "C"

@@ -16,7 +16,9 @@
 // Unlike the reference's kernels (an un-synchronised scatter in transfer!, cuSPARSE's unspecified
 // SpMV order), every sum here has a fixed order: results are bitwise reproducible, and the
 // scatter-adds / normal-equation products follow the reference CPU loops' order and association
-// exactly (FMA contraction off where products are summed), so they equal the CPU methods bit for bit.
+// exactly (FMA contraction off where products are summed), so they equal the CPU methods bit for bit
+// on finite inputs (assemble_normal_system!'s CPU loop also adds 0 * x for the columns two rows do not
+// share, which the merge-join skips: with Inf / NaN values, or for the sign of a zero, they differ).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -114,11 +116,20 @@ __global__ __launch_bounds__(NT) void k_spmv_rows32(int32_t nrows, const int32_t
 }
 
 // ------------------------------------------------------------------ coo_to_csr (utils.jl:158-201)
+// also validates the indices: an entry outside [0, nrows) x [0, ncols) sets *bad (its key is clamped
+// into the sort range, and the caller reports the error after the launch sequence)
 __global__ __launch_bounds__(NT) void k_coo_keys(int64_t nnz, const int32_t* __restrict__ Ai,
-                                                 const int32_t* __restrict__ Aj, int32_t ncols, int sort_cols,
-                                                 uint64_t* __restrict__ key, int64_t* __restrict__ val) {
+                                                 const int32_t* __restrict__ Aj, int32_t nrows, int32_t ncols,
+                                                 int sort_cols, uint64_t* __restrict__ key, int64_t* __restrict__ val,
+                                                 int32_t* __restrict__ bad) {
   for (int64_t k = blockIdx.x * (int64_t)NT + threadIdx.x; k < nnz; k += (int64_t)gridDim.x * NT) {
-    key[k] = sort_cols ? (uint64_t)Ai[k] * (uint64_t)ncols + (uint64_t)Aj[k] : (uint64_t)Ai[k];
+    int32_t i = Ai[k], j = Aj[k];
+    if (i < 0 || i >= nrows || j < 0 || j >= ncols) {
+      *bad = 1;
+      i = 0;
+      j = 0;
+    }
+    key[k] = sort_cols ? (uint64_t)i * (uint64_t)ncols + (uint64_t)j : (uint64_t)i;
     val[k] = k;
   }
 }
@@ -520,8 +531,11 @@ int madipm_coo_to_csr(int32_t n_rows, int32_t n_cols, int64_t nnz, const int32_t
   DBuf<uint64_t> k_in(std::max<int64_t>(1, nnz)), k_out(std::max<int64_t>(1, nnz));
   DBuf<int64_t> v_in(std::max<int64_t>(1, nnz)), v_out(std::max<int64_t>(1, nnz));
   const uint64_t scale = sort_cols ? (uint64_t)std::max(1, n_cols) : 1;
+  DBuf<int32_t> bad(1);
+  bad.zero(s);
   if (nnz > 0) {
-    k_coo_keys<<<grid_for(nnz), NT, 0, s>>>(nnz, d_Ai, d_Aj, std::max(1, n_cols), sort_cols, k_in, v_in);
+    k_coo_keys<<<grid_for(nnz), NT, 0, s>>>(nnz, d_Ai, d_Aj, n_rows, std::max(1, n_cols), sort_cols, k_in, v_in,
+                                            bad.p);
     // LSD radix sort is stable: equal keys keep the input order (utils.jl's counting sort order)
     const uint64_t maxkey = ((uint64_t)std::max(1, n_rows)) * scale;
     int end_bit = 1;
@@ -537,6 +551,9 @@ int madipm_coo_to_csr(int32_t n_rows, int32_t n_cols, int64_t nnz, const int32_t
   k_coo_rowptr<<<grid_for((int64_t)n_rows + 1), NT, 0, s>>>(n_rows, nnz, k_out, scale, d_rowptr);
   MADIPM_HIP(hipGetLastError());
   MADIPM_HIP(hipStreamSynchronize(s));  // the temporaries are released on return
+  int32_t hbad = 0;
+  MADIPM_HIP(hipMemcpy(&hbad, bad.p, sizeof(int32_t), hipMemcpyDeviceToHost));
+  MADIPM_REQUIRE(hbad == 0, "madipm_coo_to_csr: a row or column index is out of range (outputs are invalid)");
   return 0;
   KKT_API_END
 }

@@ -257,7 +257,7 @@ __global__ __launch_bounds__(NT) void k_small_factor(FrontTab T, const int32_t* 
 constexpr int MG = 16;
 __global__ __launch_bounds__(NT) void k_micro_factor(FrontTab T, const int32_t* __restrict__ fronts, int nf,
                                                      const double* __restrict__ Kx, double* __restrict__ arena,
-                                                     double* __restrict__ D, LDLStatus* st, double tol, int write_u) {
+                                                     double* __restrict__ D, LDLStatus* st, double tol) {
   __shared__ double Fs[NT / MG][64];  // columns 0 / 1 of F (rows 0..31); later l_i0 d0 / l_i1 d1
   const int g = threadIdx.x / MG, l = threadIdx.x & (MG - 1);
   const int q = blockIdx.x * (NT / MG) + g;
@@ -316,7 +316,6 @@ __global__ __launch_bounds__(NT) void k_micro_factor(FrontTab T, const int32_t* 
       if (bad_pivot(d1, tol)) atomicMin(&st->fail_pivot, f0 + 2);
     }
   }
-  if (!write_u) return;  // the gather forms the update entries from L (micro_u_)
   const int u = r - w;
   double* __restrict__ Uo = arena + T.u_off[s];
   for (int b = 0; b < u; ++b) {
@@ -468,55 +467,22 @@ __global__ __launch_bounds__(NT) void k_tiny_factor(FrontTab T, const int32_t* _
 template <typename IDX>
 __global__ __launch_bounds__(NT) void k_asm_chunks(const int64_t* __restrict__ gchunk, const IDX* __restrict__ gsrc,
                                                    int64_t c0, int64_t n, const double* __restrict__ Kx,
-                                                   const double* __restrict__ arena, double* __restrict__ part,
-                                                   const int64_t* __restrict__ mdesc) {
+                                                   const double* __restrict__ arena, double* __restrict__ part) {
   const int64_t c = c0 + (int64_t)blockIdx.x * NT + threadIdx.x;
   if (c >= c0 + n) return;
   const int64_t p0 = gchunk[c], p1 = gchunk[c + 1];
-  int64_t q[SymbolicPlan::kChunk];
-#pragma unroll
-  for (int u = 0; u < SymbolicPlan::kChunk; ++u) q[u] = (p0 + u < p1) ? (int64_t)gsrc[p0 + u] : INT64_MAX;
-  // three batches of independent loads: leaf descriptors, then every value operand, then the sums
   constexpr int KC = SymbolicPlan::kChunk;
-  bool mic[KC];
-  int64_t dsc[KC];
+  int64_t q[KC];
 #pragma unroll
-  for (int u = 0; u < KC; ++u) {
-    mic[u] = sizeof(IDX) == 4 && q[u] != INT64_MAX && q[u] >= 0 && (q[u] & 0x40000000);
-    dsc[u] = mic[u] ? mdesc[((int)q[u] >> 10) & 0xfffff] : 0;
-  }
-  double x0[KC], x1[KC], x2[KC], x3[KC], x4[KC], x5[KC];
+  for (int u = 0; u < KC; ++u) q[u] = (p0 + u < p1) ? (int64_t)gsrc[p0 + u] : INT64_MAX;
+  // every value operand in flight before the sum
+  double x[KC];
 #pragma unroll
-  for (int u = 0; u < KC; ++u) {
-    if (mic[u]) {  // d0, l_a0, l_b0 and (w = 2) l_a1, l_b1, d1; w = 1 re-reads column 0 (unused)
-      const int qi = (int)q[u];
-      const int a = (qi >> 5) & 31, b = qi & 31, r = (int)((dsc[u] >> 2) & 63), w = (int)(dsc[u] & 3);
-      const double* L = arena + (dsc[u] >> 8);
-      const int c1 = (w == 2) ? r : 0;
-      x0[u] = L[0];
-      x1[u] = L[w + a];
-      x2[u] = L[w + b];
-      x3[u] = L[c1 + w + a];
-      x4[u] = L[c1 + w + b];
-      x5[u] = L[c1 + (w == 2 ? 1 : 0)];
-    } else {
-      x0[u] = (q[u] == INT64_MAX) ? 0.0 : ((q[u] < 0) ? Kx[~q[u]] : arena[q[u]]);
-      x1[u] = x2[u] = x3[u] = x4[u] = x5[u] = 0.0;
-    }
-  }
+  for (int u = 0; u < KC; ++u) x[u] = (q[u] == INT64_MAX) ? 0.0 : ((q[u] < 0) ? Kx[~q[u]] : arena[q[u]]);
   double v = 0.0;
 #pragma unroll
-  for (int u = 0; u < KC; ++u) {
-    if (q[u] == INT64_MAX) continue;
-    if (mic[u]) {  // U(a, b) = -(l_a0 (l_b0 d0) + l_a1 (l_b1 d1)), as k_micro_factor forms it
-      const bool two = (dsc[u] & 3) == 2;
-      const double sb0 = x2[u] * x0[u];
-      const double la1 = two ? x3[u] : 0.0, sb1 = two ? x4[u] * x5[u] : 0.0;
-      v += -(x1[u] * sb0 + la1 * sb1);
-    } else {
-      v += x0[u];
-    }
-  }
+  for (int u = 0; u < KC; ++u)
+    if (q[u] != INT64_MAX) v += x[u];
   part[c] = v;
 }
 
@@ -2970,49 +2936,13 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   atiles_.upload(S.atiles);
   g_ptr_.upload(S.g_ptr);
   {
-    // int32 sources when every arena / K index fits.  Optionally leaf (micro) fronts' update entries
-    // are not materialised: a source (front c, a, b) is encoded as 0x40000000 | mid << 10 | a << 5 | b
-    // and the gather forms U(a, b) = -(l_a0 d0 l_b0 + l_a1 d1 l_b1) from c's L panel (r x w <= 32 x 2,
-    // pivots on its diagonal) — k_micro_factor then writes no U block (~90 MB per ex10 factorisation).
+    // int32 sources when every arena / K index fits (leaf update blocks stay materialised: forming
+    // them from the leaves' L panels in the gather was measured slower, r1 — 6 scattered loads per
+    // source instead of 1)
     bool fits = !S.g_src.empty();
     for (int64_t q : S.g_src) fits = fits && q >= INT32_MIN && q < (1LL << 30);
-    micro_u_ = false;
     if (fits) {
       std::vector<int32_t> g32(S.g_src.begin(), S.g_src.end());
-      std::vector<std::pair<int64_t, int>> mu;  // (u_off, front) of the micro fronts
-      for (int f = 0; f < (int)S.nrows.size(); ++f) {
-        const int r = S.nrows[f], w = S.first[f + 1] - S.first[f];
-        const bool absorbed = S.parent[f] >= 0 && S.absorb[S.parent[f]];
-        if (r <= 32 && w <= 2 && S.fs_off[f] < 0 && !S.is_big[f] && !S.ftree[f] && !absorbed && r > w)
-          mu.push_back({S.u_off[f], f});
-      }
-      // experimental (MADIPM_LEAF_FROM_L=1): measured on ex10 the leaf factorisation halves
-      // (0.23 -> 0.11 ms per warm-up) but the gather, now 6 scattered loads per leaf source instead
-      // of 1, grows 0.35 -> 0.57 ms (address-bound) — so the U blocks stay materialised by default
-      const char* ev = std::getenv("MADIPM_LEAF_FROM_L");
-      const bool want = ev && ev[0] == '1';
-      if (want && !mu.empty() && mu.size() < (1u << 20) && S.arena_size < (1LL << 55)) {
-        std::sort(mu.begin(), mu.end());
-        std::vector<int64_t> desc(mu.size());
-        for (size_t k = 0; k < mu.size(); ++k) {
-          const int f = mu[k].second, r = S.nrows[f], w = S.first[f + 1] - S.first[f];
-          desc[k] = (S.l_off[f] << 8) | ((int64_t)r << 2) | w;
-        }
-        for (int32_t& q : g32) {
-          if (q < 0) continue;
-          auto it = std::upper_bound(mu.begin(), mu.end(), std::make_pair((int64_t)q, INT32_MAX));
-          if (it == mu.begin()) continue;
-          --it;
-          const int f = it->second;
-          const int u = S.nrows[f] - (S.first[f + 1] - S.first[f]);
-          const int64_t off = q - it->first, ld = S.u_ld[f];
-          if (off >= ld * u) continue;  // not inside this leaf's update block
-          const int a = (int)(off % ld), b = (int)(off / ld);
-          q = (int32_t)(0x40000000 | ((int)(it - mu.begin()) << 10) | (a << 5) | b);
-        }
-        mdesc_.upload(desc);
-        micro_u_ = true;
-      }
       g_src32_.upload(g32);
     } else {
       g_src_.upload(S.g_src);
@@ -3155,15 +3085,15 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         const int c = S.mc_list[k];
         const double rc = S.nrows[c], wc = S.first[c + 1] - S.first[c];
         ftree_bytes_ += 12.0 * (S.asm_ptr[c + 1] - S.asm_ptr[c]) + 8.0 * (rc * wc - wc * (wc - 1) / 2.0);
+        ftree_alg_ += fact_alg(c);
         for (int t = 0; t < (int)wc; ++t) ftree_flops_ += (rc - t - 1) * (rc - t);
       }
-      // algorithmic bytes as SURVEY 8(d) prices the factorisation (B_fact = 8 nnzL + 12 nnzK): the L
-      // entries this front writes (stored lower trapezoid of its panel, D on the diagonal) and the
-      // caller's K entries it reads (12 B: value + index).  The staging traffic the kernel moves on
-      // top (the image or K scatter, the tree children's U blocks, the U write-out) is not counted:
-      // it is the implementation's, not the algorithm's.
+      // staging model: the stored lower trapezoid of the panel written and the front's scatter list
+      // read (ftree_bytes_); SURVEY 8(d)'s algorithmic bytes (B_fact = 8 nnzL + 12 nnzK of the
+      // front's columns, exact column counts) in ftree_alg_
       (void)u;
       ftree_bytes_ += 8.0 * (r * (double)w - w * (w - 1) / 2.0) + 12.0 * (double)(S.asm_ptr[s + 1] - S.asm_ptr[s]);
+      ftree_alg_ += fact_alg(s);
       for (int t = 0; t < w; ++t) ftree_flops_ += (double)(r - t - 1) * (r - t);
     }
     if (const char* ev = std::getenv("MADIPM_TREE_DEBUG"); ev && ev[0] == '1') {  // per-level front shapes
@@ -3271,12 +3201,14 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     if (phase == 1 && !S.lb.empty()) {
       Launch L{LB_BUILD, 0, 0, 0, (int64_t)S.lb_mem.size()};
       for (const auto& G : S.lb) L.bytes += 8.0 * (double)G.m * G.n * 2.0 + 12.0 * G.n * G.m;
+      for (int32_t c : S.lb_mem) L.alg += fact_alg_cols(c, c + 1);
       out.push_back(L);
     }
     auto ftree_launch = [&]() {  // factorisation tree: after every level-0 launch (the pre-leaves)
       asm_launch(2 * NL + 1, out);
       Launch L{FTREE, 0, 0, nftree_, (int64_t)nftree_};
       L.bytes = ftree_bytes_;
+      L.alg = ftree_alg_;
       L.flops = ftree_flops_;
       L.lds_bytes = ftree_lds_;
       out.push_back(L);
@@ -3311,6 +3243,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         for (int f : micro) {
           const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
           L.bytes += 8.0 * (r * w + (r - w) * (r - w + 1) / 2 + w) + 16.0 * (S.asm_ptr[f + 1] - S.asm_ptr[f]);
+          L.alg += fact_alg(f);
           for (int t = 0; t < (int)w; ++t) L.flops += (r - t - 1) * (r - t);
         }
         out.push_back(L);
@@ -3329,6 +3262,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
             const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
             L.bytes += 8.0 * (r * w + (r - w) * (r - w) + w) +
                        (S.fs_off[f] >= 0 ? 8.0 * r * (r + 1) / 2 : 16.0 * (S.asm_ptr[f + 1] - S.asm_ptr[f]));
+            L.alg += fact_alg(f);
             for (int t = 0; t < (int)w; ++t) L.flops += (r - t - 1) * (r - t);
           }
           out.push_back(L);
@@ -3339,7 +3273,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       for (int s : big) maxsteps = std::max<int>(maxsteps, (int)cdiv(S.first[s + 1] - S.first[s], 64));
       for (int p = 0; p < maxsteps; ++p) {
         std::vector<int32_t> td, tt, tu;  // (front, item) pairs
-        double kb[3] = {0, 0, 0}, kf[3] = {0, 0, 0};
+        double kb[3] = {0, 0, 0}, kf[3] = {0, 0, 0}, ka = 0;
         for (int s : big) {
           const int w = S.first[s + 1] - S.first[s], r = S.nrows[s];
           if (cdiv(w, 64) <= p) continue;
@@ -3347,6 +3281,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
           const int nt = (int)cdiv(r - k0 - kw, 64);
           const double dk = kw, nb = r - k0 - kw;
           kb[0] += 8.0 * (dk * (dk + 1) + 4 * 16 * 17);  // diag: read + write lower, write the M blocks
+          ka += fact_alg_cols(S.first[s] + k0, S.first[s] + k0 + kw);  // 8(d): the panel's columns
           kf[0] += dk * dk * dk / 3.0;
           kb[1] += 8.0 * (2.0 * nb * dk + nt * (dk * (dk + 1) / 2 + 4 * 16 * 17));  // trsm: rows in/out + L11, M per tile
           kf[1] += nb * dk * dk;
@@ -3364,6 +3299,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
           align2();
           Launch L{kv.first, p, (int64_t)sched.size(), 0, (int64_t)kv.second->size() / 2};
           L.bytes = kb[q];
+          L.alg = q == 0 ? ka : 0.0;
           L.flops = kf[q];
           out.push_back(L);
           sched.insert(sched.end(), kv.second->begin(), kv.second->end());
@@ -3411,6 +3347,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
           const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
           L.micro_bytes += 8.0 * (r * w + 3.0 * r);
           L.micro_flops += 2.0 * (r * w - w * (w + 1) / 2);
+          L.micro_alg += solve_alg(f);
         }
         L.tiny_off = (int64_t)sched.size();
         L.ntiny = (int)tiny.size();
@@ -3465,18 +3402,23 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
           const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
           L.small_bytes += 8.0 * (r * w + 3.0 * r);
           L.small_flops += 2.0 * (r * w - w * (w + 1) / 2);
+          L.small_alg += solve_alg(f);
           L.small_lds = std::max<int>(L.small_lds, 8 * (S.nrows[f] | 1) * (S.first[f + 1] - S.first[f]));
         }
         for (int f : tiny) {
           const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
           L.tiny_bytes += 8.0 * (r * w + 3.0 * r);
           L.tiny_flops += 2.0 * (r * w - w * (w + 1) / 2);
+          L.tiny_alg += solve_alg(f);
         }
         for (int f : big) {
           const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
           L.big_bytes += 8.0 * (r * w + 3.0 * r);
           L.big_flops += 2.0 * (r * w - w * (w + 1) / 2);
           L.below_bytes += 8.0 * (r - w) * w;
+          const double sa = solve_alg(f), da = std::min(sa, 4.0 * w * (w + 1));  // diagonal block / below it
+          L.big_alg += da;
+          L.below_alg += sa - da;
           L.gat_bytes += 8.0 * (2.0 * r + 2.0 * (S.sv_ptr[S.row_ptr[f + 1]] - S.sv_ptr[S.row_ptr[f]]));
         }
         out.push_back(L);
@@ -3497,6 +3439,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         const double r = S.nrows[s], w = S.first[s + 1] - S.first[s];
         tree_bytes_ += 8.0 * (r * w + 3.0 * r);
         tree_flops_ += 2.0 * (r * w - w * (w + 1) / 2);
+        tree_alg_ += solve_alg(s);
         tree_lds_ = std::max<int>(tree_lds_, 8 * tree_panel_doubles(s) + 8 * 2048);
       }
       tree_lds_ = std::min(TREE_LDS_MAX, tree_lds_ + 8 * 2048);  // up to 4096 staged gather sources
@@ -3601,11 +3544,12 @@ LDLSolver::~LDLSolver() {
   for (hipEvent_t e : evs_) (void)hipEventDestroy(e);
 }
 
-#define TIMED(kind, bytes, flops, launch)            \
-  do {                                               \
-    const bool tm_ = t_begin(kind, s);               \
-    launch;                                          \
-    if (tm_) t_end(kind, s, (bytes), (flops));       \
+// bytes: the launch's staging-traffic model; alg: SURVEY 8(d)'s bytes of the same launch
+#define TIMED(kind, bytes, alg, flops, launch)          \
+  do {                                                  \
+    const bool tm_ = t_begin(kind, s);                  \
+    launch;                                             \
+    if (tm_) t_end(kind, s, (bytes), (alg), (flops));   \
   } while (0)
 
 const char* kernel_kind_name(int k) {
@@ -3631,16 +3575,17 @@ bool LDLSolver::t_begin(int kind, hipStream_t s) {
     MADIPM_HIP(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
     evs_.push_back(e);
   }
-  pend_.push_back({kind, ev_used_, 0.0, 0.0});
+  pend_.push_back({kind, ev_used_, 0.0, 0.0, 0.0});
   MADIPM_HIP(hipEventRecord(evs_[ev_used_], s));
   ev_used_ += 2;
   return true;
 }
 
-void LDLSolver::t_end(int kind, hipStream_t s, double bytes, double flops) {
+void LDLSolver::t_end(int kind, hipStream_t s, double bytes, double alg, double flops) {
   Pending& p = pend_.back();
   (void)kind;
   p.bytes = bytes;
+  p.alg = alg;
   p.flops = flops;
   MADIPM_HIP(hipEventRecord(evs_[p.e0 + 1], s));
 }
@@ -3654,6 +3599,7 @@ void LDLSolver::kernel_stats(KernelStat out[KK_COUNT]) {
     k.launches++;
     k.ms += ms;
     k.bytes += p.bytes;
+    k.alg_bytes += p.alg;
     k.flops += p.flops;
   }
   pend_.clear();
@@ -3680,7 +3626,7 @@ void LDLSolver::lb_fwd(const double* b, hipStream_t s) {
     const int nch = (int)cdiv(G.n, LBF_COLS);
     int64_t poff = 0;
     for (size_t h = 0; h < g; ++h) poff += cdiv(S_.lb[h].n, LBF_COLS) * S_.lb[h].m;
-    TIMED(KK_LB_GEMV, 8.0 * G.m * (double)G.n, 2.0 * G.m * (double)G.n,
+    TIMED(KK_LB_GEMV, 8.0 * G.m * (double)G.n, lb_alg(g), 2.0 * G.m * (double)G.n,
           (k_lb_fwd1<<<dim3((unsigned)cdiv(G.m, NT), (unsigned)nch), NT, 0, s>>>(
               lbW_.p + G.w_off, lbd_, lbmem_, perm_, G.m, G.n, G.mem_off, b, xi_, lbpart_.p + poff)));
     k_lb_fwd2<<<(unsigned)cdiv(G.m, NT), NT, 0, s>>>(lbpart_.p + poff, G.m, nch, uvec_.p + G.uvec_off);
@@ -3691,9 +3637,27 @@ void LDLSolver::lb_bwd(int g, double* b, hipStream_t s) {
   const auto& G = S_.lb[g];
   int64_t xoff = 0;
   for (int h = 0; h < g; ++h) xoff += S_.lb[h].m;
-  TIMED(KK_LB_GEMV, 8.0 * G.m * (double)G.n, 2.0 * G.m * (double)G.n,
+  TIMED(KK_LB_GEMV, 8.0 * G.m * (double)G.n, lb_alg(g), 2.0 * G.m * (double)G.n,
         (k_lb_bwd<<<(unsigned)cdiv(G.n, NT / 64), NT, 0, s>>>(lbW_.p + G.w_off, lbd_, lbmem_, perm_, lbxrow_.p + xoff,
                                                              G.m, G.n, G.mem_off, xi_, b)));
+}
+
+double LDLSolver::fact_alg_cols(int c0, int c1) const {
+  double b = 0.0;
+  for (int c = c0; c < c1; ++c) b += 8.0 * S_.colcnt[c] + 12.0 * S_.kcol[c];
+  return b;
+}
+double LDLSolver::lb_alg(size_t g) const {  // solve bytes of a batched-leaf group: 8 nnzL of its members
+  const auto& G = S_.lb[g];
+  double b = 0.0;
+  for (int64_t k = G.mem_off; k < G.mem_off + G.n; ++k) b += 8.0 * S_.colcnt[S_.lb_mem[k]];
+  return b;
+}
+double LDLSolver::fact_alg(int s) const { return fact_alg_cols(S_.first[s], S_.first[s + 1]); }
+double LDLSolver::solve_alg(int s) const {
+  double b = 0.0;
+  for (int c = S_.first[s]; c < S_.first[s + 1]; ++c) b += 8.0 * S_.colcnt[c];
+  return b;
 }
 
 void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStream_t s) {
@@ -3702,52 +3666,52 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
     switch (L.kind) {
       case ASSEMBLE:
         if (L.nchunk)
-          TIMED(KK_ASM_CHUNKS, L.bytes2, L.flops2,
+          TIMED(KK_ASM_CHUNKS, L.bytes2, 0.0, L.flops2,
                 (g_src32_.p ? k_asm_chunks<int32_t><<<(unsigned)cdiv(L.nchunk, NT), NT, 0, s>>>(
-                                  g_chunk_, g_src32_, L.chunk0, L.nchunk, Kx, arena_, gpart_, mdesc_.p)
+                                  g_chunk_, g_src32_, L.chunk0, L.nchunk, Kx, arena_, gpart_)
                             : k_asm_chunks<int64_t><<<(unsigned)cdiv(L.nchunk, NT), NT, 0, s>>>(
-                                  g_chunk_, g_src_, L.chunk0, L.nchunk, Kx, arena_, gpart_, nullptr)));
-        TIMED(KK_ASSEMBLE, L.bytes, L.flops,
+                                  g_chunk_, g_src_, L.chunk0, L.nchunk, Kx, arena_, gpart_)));
+        TIMED(KK_ASSEMBLE, L.bytes, 0.0, L.flops,
               (k_assemble<<<(unsigned)L.items, ANT, 0, s>>>(T_, atiles_.p + L.off, g_ptr_, gpart_, bt_, arena_, fscratch_)));
         break;
       case MICRO:
-        TIMED(KK_TINY, L.bytes, L.flops,
+        TIMED(KK_TINY, L.bytes, L.alg, L.flops,
               (k_micro_factor<<<(unsigned)cdiv(L.items, NT / MG), NT, 0, s>>>(T_, list, (int)L.items, Kx, arena_, D_,
-                                                                             st_, pivot_tol, micro_u_ ? 0 : 1)));
+                                                                             st_, pivot_tol)));
         break;
       case SMALL32:
-        TIMED(KK_TINY, L.bytes, L.flops,
+        TIMED(KK_TINY, L.bytes, L.alg, L.flops,
               (k_tiny_factor<<<(unsigned)cdiv(L.items, 4), NT, 0, s>>>(T_, list, (int)L.items, Kx, arena_, fscratch_, D_,
                                                                       st_, pivot_tol)));
         break;
       case SMALL64:
       case SMALL128:
-        TIMED(KK_SMALL, L.bytes, L.flops,
+        TIMED(KK_SMALL, L.bytes, L.alg, L.flops,
               (k_small_blocked<false><<<(unsigned)L.items, NT, L.lds_bytes, s>>>(T_, list, Kx, arena_, fscratch_, D_,
                                                                                 st_, pivot_tol)));
         break;
       case SMALL192:
-        TIMED(KK_SMALL, L.bytes, L.flops,
+        TIMED(KK_SMALL, L.bytes, L.alg, L.flops,
               (k_small_blocked<true><<<(unsigned)L.items, NT, L.lds_bytes, s>>>(T_, list, Kx, arena_, fscratch_, D_,
                                                                                st_, pivot_tol)));
         break;
       case BIG_DIAG:
-        TIMED(KK_DIAG, L.bytes, L.flops,
+        TIMED(KK_DIAG, L.bytes, L.alg, L.flops,
               (k_big_diag<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_, minv_, st_, pivot_tol)));
         break;
       case BIG_TRSM:
-        TIMED(KK_TRSM, L.bytes, L.flops, (k_big_trsm<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_, minv_)));
+        TIMED(KK_TRSM, L.bytes, 0.0, L.flops, (k_big_trsm<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_, minv_)));
         break;
       case BIG_UPDATE:
-        TIMED(KK_UPDATE, L.bytes, L.flops, (k_big_update<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_)));
+        TIMED(KK_UPDATE, L.bytes, 0.0, L.flops, (k_big_update<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_)));
         break;
       case LB_BUILD:
-        TIMED(KK_LB_BUILD, L.bytes, 0.0,
+        TIMED(KK_LB_BUILD, L.bytes, L.alg, 0.0,
               (k_lb_build<<<(unsigned)L.items, NT, 0, s>>>(lbg_, lbgid_, lbmem_, lbcs_, lbce_, lbwbase_, lbwrow_, Kx, lbW_,
                                                           lbd_.p, lbd_.p + S_.lb_mem.size(), D_, st_, pivot_tol)));
         break;
       case LB_SYRK:
-        TIMED(KK_LB_SYRK, L.bytes, L.flops, lb_syrk((int)L.off, s));
+        TIMED(KK_LB_SYRK, L.bytes, 0.0, L.flops, lb_syrk((int)L.off, s));
         break;
       case FTREE:
         if (!ftree_checked_) {  // static + dynamic LDS must fit the CU (160 KB on gfx950)
@@ -3759,7 +3723,7 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
           ftree_checked_ = true;
         }
         ++fepoch_;
-        TIMED(KK_FACT_TREE, L.bytes, L.flops,
+        TIMED(KK_FACT_TREE, L.bytes, L.alg, L.flops,
               (k_fact_tree<<<(unsigned)nftree_, NT, L.lds_bytes, s>>>(T_, ft_order_, nftree_, ft_dptr_, ft_dep_, fcnt_,
                                                                       fflags_, fepoch_, Kx, arena_, fscratch_, D_, st_,
                                                                       pivot_tol, &st_->err, fdbg_.p)));
@@ -3778,12 +3742,12 @@ void LDLSolver::fact_phase1(const double* Kx, hipStream_t s) {
   const int nb = (int)std::min<int64_t>(64, cdiv(S_.N, NT));
   const int spdf = spd ? 1 : 0;
   if (!sharded()) {
-    TIMED(KK_INERTIA, 8.0 * S_.N, 0.0, (k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, st_, spdf, nullptr, 0)));
+    TIMED(KK_INERTIA, 8.0 * S_.N, 0.0, 0.0, (k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, st_, spdf, nullptr, 0)));
     MADIPM_HIP(hipGetLastError());
     if (!ext_status_) MADIPM_HIP(hipMemcpyAsync(h_st_, st_, sizeof(LDLStatus), hipMemcpyDeviceToHost, s));
     return;
   }
-  TIMED(KK_INERTIA, 8.0 * S_.N, 0.0, (k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, st_, spdf, colmask_, 1)));
+  TIMED(KK_INERTIA, 8.0 * S_.N, 0.0, 0.0, (k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, st_, spdf, colmask_, 1)));
   k_pack_status<<<1, 64, 0, s>>>(st_, arena_.p + S_.top_hi, S_.shard, S_.nshards);
   if (ntopcol_) k_tri_pack<<<(unsigned)ntopcol_, NT, 0, s>>>(topcol_, arena_, xpack_, 0);
   MADIPM_HIP(hipMemcpyAsync(xpack_.p + xpack_tri_, arena_.p + S_.top_hi, sizeof(double) * 4 * S_.nshards,
@@ -3800,7 +3764,7 @@ void LDLSolver::fact_phase2(hipStream_t s) {
   k_unpack_status<<<1, 1, 0, s>>>(st_, arena_.p + S_.top_hi, S_.nshards);
   run_fact(fact2_, nullptr, s);
   const int nb = (int)std::min<int64_t>(64, cdiv(S_.N, NT));
-  TIMED(KK_INERTIA, 8.0 * S_.N, 0.0, (k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, st_, spd ? 1 : 0, colmask_, 2)));
+  TIMED(KK_INERTIA, 8.0 * S_.N, 0.0, 0.0, (k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, st_, spd ? 1 : 0, colmask_, 2)));
   MADIPM_HIP(hipGetLastError());
   MADIPM_HIP(hipMemcpyAsync(h_st_, st_, sizeof(LDLStatus), hipMemcpyDeviceToHost, s));
 }
@@ -3927,26 +3891,26 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
   for (int lev = 0; lev < (int)V.size(); ++lev) {
     const SolveLevel& L = V[lev];
     if (L.nmicro)
-      TIMED(KK_FWD_TINY, L.micro_bytes, L.micro_flops,
+      TIMED(KK_FWD_TINY, L.micro_bytes, L.micro_alg, L.micro_flops,
             (k_fwd_micro<<<(unsigned)cdiv(L.nmicro, NT / MG), NT, 0, s>>>(T_, sched_.p + L.micro_off, L.nmicro, arena_, b,
                                                                          xi_, uvec_)));
     if (L.ntiny)
-      TIMED(KK_FWD_TINY, L.tiny_bytes, L.tiny_flops,
+      TIMED(KK_FWD_TINY, L.tiny_bytes, L.tiny_alg, L.tiny_flops,
             (k_fwd_tiny<<<(unsigned)cdiv(L.ntiny, 2 * SW), NT, 0, s>>>(T_, sched_.p + L.tiny_off, L.ntiny, arena_, b, xi_,
                                                                       uvec_)));
     if (L.nsmall)
-      TIMED(KK_FWD_SMALL, L.small_bytes, L.small_flops,
+      TIMED(KK_FWD_SMALL, L.small_bytes, L.small_alg, L.small_flops,
             (k_fwd_small<<<(unsigned)L.nsmall, NT, L.small_lds, s>>>(T_, sched_.p + L.small_off, L.nsmall, arena_, b, xi_,
                                                                     uvec_)));
     if (L.nbig) {
-      TIMED(KK_FWD_GATHER, L.gat_bytes, 0.0,
+      TIMED(KK_FWD_GATHER, L.gat_bytes, 0.0, 0.0,
             (k_fwd_gather<<<L.ngat, NT, 0, s>>>(T_, sched_.p + L.gat_off, b, uvec_, vwork_)));
-      TIMED(KK_FWD_BIG, L.big_bytes, L.big_flops,
+      TIMED(KK_FWD_BIG, L.big_bytes, L.big_alg + L.below_alg, L.big_flops,
             (k_fwd_big<<<std::min(L.nftask, 512), NT, 0, s>>>(T_, tasks + L.ftask_off, L.nftask, cnt + 2 * lev,
                                                                flags_, flag_off_, efwd, arena_, vwork_, xi_, uvec_, &st_->err)));
     }
     if (lev == 0 && phase == 0 && ntree_)
-      TIMED(KK_FWD_TREE, tree_bytes_, tree_flops_,
+      TIMED(KK_FWD_TREE, tree_bytes_, tree_alg_, tree_flops_,
             (k_fwd_tree<<<(unsigned)ntree_, NT, tree_lds_, s>>>(T_, tf_order_, ntree_, tdep_ptr_, tdep_,
                                                                  counters_.p + 4 * S_.nlevels, tflags_, efwd, tree_lds_ / 8,
                                                                  arena_, b,
@@ -3963,27 +3927,27 @@ void LDLSolver::bwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
   for (int lev = (int)V.size() - 1; lev >= 0; --lev) {
     const SolveLevel& L = V[lev];
     if (lev == 0 && phase == 0 && ntree_)
-      TIMED(KK_BWD_TREE, tree_bytes_, tree_flops_,
+      TIMED(KK_BWD_TREE, tree_bytes_, tree_alg_, tree_flops_,
             (k_bwd_tree<<<(unsigned)ntree_, NT, tree_lds_, s>>>(T_, tb_order_, ntree_, tpar_, counters_.p + 4 * S_.nlevels + 1,
                                                                  tflags_, ebwd, arena_, D_, xi_, b, &st_->err)));
     if (L.nbelow)
-      TIMED(KK_BWD_BELOW, L.below_bytes, 0.25 * L.below_bytes,
+      TIMED(KK_BWD_BELOW, L.below_bytes, L.below_alg, 0.25 * L.below_bytes,
             (k_bwd_below<<<L.nbelow, NT, 0, s>>>(T_, sched_.p + L.below_off, bp_off_, arena_, xi_, bpart_)));
     if (L.nbig)
-      TIMED(KK_BWD_BIG, L.big_bytes - L.below_bytes, L.big_flops - 0.25 * L.below_bytes,
+      TIMED(KK_BWD_BIG, L.big_bytes - L.below_bytes, L.big_alg, L.big_flops - 0.25 * L.below_bytes,
             (k_bwd_big<<<std::min(L.nbtask, 512), NT, 0, s>>>(T_, tasks + L.btask_off, L.nbtask, cnt + 2 * lev + 1,
                                                                flags_, flag_off_, ebwd, arena_, D_, xi_, b, bp_off_, bpart_,
                                                                &st_->err)));
     if (L.nsmall)
-      TIMED(KK_BWD_SMALL, L.small_bytes, L.small_flops,
+      TIMED(KK_BWD_SMALL, L.small_bytes, L.small_alg, L.small_flops,
             (k_bwd_small<<<(unsigned)L.nsmall, NT, L.small_lds, s>>>(T_, sched_.p + L.small_off, L.nsmall, arena_, D_, xi_,
                                                                     b)));
     if (L.ntiny)
-      TIMED(KK_BWD_TINY, L.tiny_bytes, L.tiny_flops,
+      TIMED(KK_BWD_TINY, L.tiny_bytes, L.tiny_alg, L.tiny_flops,
             (k_bwd_tiny<<<(unsigned)cdiv(L.ntiny, 2 * SW), NT, 0, s>>>(T_, sched_.p + L.tiny_off, L.ntiny, arena_, D_, xi_,
                                                                       b)));
     if (L.nmicro)
-      TIMED(KK_BWD_TINY, L.micro_bytes, L.micro_flops,
+      TIMED(KK_BWD_TINY, L.micro_bytes, L.micro_alg, L.micro_flops,
             (k_bwd_micro<<<(unsigned)cdiv(L.nmicro, NT / MG), NT, 0, s>>>(T_, sched_.p + L.micro_off, L.nmicro, arena_, D_,
                                                                          xi_, b)));
     if (phase == 0)

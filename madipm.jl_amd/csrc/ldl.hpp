@@ -96,6 +96,8 @@ const char* kernel_kind_name(int k);
 struct KernelStat {
   int64_t launches = 0;
   double ms = 0.0, bytes = 0.0, flops = 0.0;
+  double alg_bytes = 0.0;  // SURVEY 8(d)'s bytes of the launches (8 nnzL + 12 nnzK of the columns factorised,
+                           // 8 nnzL of the columns a solve launch substitutes); `bytes` = the staging model
 };
 
 // All-reduce (sum) of a device buffer across the shards of a sharded factorisation, ordered on
@@ -195,7 +197,8 @@ class LDLSolver : public LinSolver {
     int nf;         // number of fronts (SMALL*)
     int64_t items;  // workgroups
     int64_t chunk0 = 0, nchunk = 0;  // ASSEMBLE: chunk range of the level
-    double bytes = 0, flops = 0;       // algorithmic traffic / work of the launch
+    double bytes = 0, flops = 0;       // staging traffic model / algorithmic work of the launch
+    double alg = 0;                    // SURVEY 8(d) bytes of the columns the launch factorises
     double bytes2 = 0, flops2 = 0;     // ASSEMBLE: of the chunk pass
     bool lds = true;                   // SMALL*: some front is a leaf (assembled in LDS)
     int lds_bytes = 0;                 // SMALL*: dynamic LDS of the blocked kernel (largest front)
@@ -205,7 +208,7 @@ class LDLSolver : public LinSolver {
     int ntiny;
     int64_t micro_off;  // fronts with r <= 32, w <= 2 (16 lanes each)
     int nmicro;
-    double micro_bytes = 0, micro_flops = 0;
+    double micro_bytes = 0, micro_flops = 0, micro_alg = 0;
     int64_t small_off;
     int nsmall;
     int64_t big_off;
@@ -221,6 +224,8 @@ class LDLSolver : public LinSolver {
     int small_lds = 0;  // dynamic LDS of the small-front solve kernels (largest panel, ld r | 1)
     double tiny_bytes = 0, tiny_flops = 0;
     double small_bytes = 0, small_flops = 0, big_bytes = 0, big_flops = 0, below_bytes = 0, gat_bytes = 0;
+    // SURVEY 8(d) bytes per direction: 8 nnzL of the fronts' columns (big: diagonal block / below it)
+    double tiny_alg = 0, small_alg = 0, big_alg = 0, below_alg = 0;
   };
   SymbolicPlan S_;
   FrontTab T_{};
@@ -246,7 +251,12 @@ class LDLSolver : public LinSolver {
   // per direction (topological ticket order, forward dependencies = tree children, backward = tree
   // parent), between the level-0 launches and the remaining levels
   int ntree_ = 0, tree_lds_ = 0;
-  double tree_bytes_ = 0, tree_flops_ = 0;
+  double tree_bytes_ = 0, tree_flops_ = 0, tree_alg_ = 0;
+  // SURVEY 8(d) bytes of front s: factorisation 8 nnzL + 12 nnzK of its columns; solve 8 nnzL
+  double fact_alg(int s) const;
+  double fact_alg_cols(int c0, int c1) const;
+  double solve_alg(int s) const;
+  double lb_alg(size_t g) const;
   DBuf<int32_t> tf_order_, tb_order_, tdep_ptr_, tdep_, tpar_, tflags_;
   DBuf<int64_t> tdbg_, upos_;
   DBuf<double> gbuf_;
@@ -256,7 +266,7 @@ class LDLSolver : public LinSolver {
   // (per-factorisation epoch), ticket counters (reset by the launch's last workgroup)
   int nftree_ = 0, ftree_lds_ = 0, fepoch_ = 0;
   bool ftree_checked_ = false;
-  double ftree_bytes_ = 0, ftree_flops_ = 0;
+  double ftree_bytes_ = 0, ftree_flops_ = 0, ftree_alg_ = 0;
   DBuf<int32_t> ft_order_, ft_dptr_, ft_dep_, fflags_, fcnt_;
   DBuf<int64_t> fdbg_, ab_first_, ab_loff_, fold_poff_;
   DBuf<int32_t> ab_src0_, ab_src1_, ab_k_, ab_f0_, ab_wrc_, fold_bptr_, fold_bat_, fold_plen_, fold_rmax_, fold_lmax_;
@@ -277,8 +287,6 @@ class LDLSolver : public LinSolver {
   DBuf<int32_t> bigslot_, g_ptr_, bt_;
   DBuf<int64_t> fs_off_, sv_ptr_, sv_src_, g_src_, g_chunk_;
   DBuf<int32_t> g_src32_;
-  DBuf<int64_t> mdesc_;  // leaf fronts: (L offset << 8) | (r << 2) | w
-  bool micro_u_ = false;  // leaf update entries formed by the gather from L
   DBuf<SymbolicPlan::AsmTile> atiles_;
   DBuf<double> minv_, fscratch_, gpart_;
   DBuf<int64_t> row_ptr_, l_off_, u_off_, uvec_off_, asm_ptr_, asm_src_, asm_dst64_, rel_ptr_;
@@ -295,12 +303,12 @@ class LDLSolver : public LinSolver {
   struct Pending {
     int kind;
     size_t e0;
-    double bytes, flops;
+    double bytes, flops, alg;
   };
   std::vector<Pending> pend_;
   KernelStat kst_[KK_COUNT];
   bool t_begin(int kind, hipStream_t s);
-  void t_end(int kind, hipStream_t s, double bytes, double flops);
+  void t_end(int kind, hipStream_t s, double bytes, double alg, double flops);
 };
 
 // The shards of one sharded factorisation on ONE device (single process): the phases run shard by

@@ -117,9 +117,13 @@ __device__ void block_partials(double (&v)[NV], const int (&ops)[NV], double* pa
   }
 }
 
-// (value, index) argmin with smallest-index tie break
+// (value, index) argmin in the order of the reference's left fold (kernels.jl:226-272:
+// mapreduce(...; init = (1.0, 0)) with `elem1[1] < elem2[1] ? elem1 : elem2`): a later element
+// replaces the accumulator unless the accumulator is strictly smaller, so among equal ratios the
+// LAST index wins.  As a total order, (value ascending, index descending): associative, so any
+// combine tree gives the fold's answer.  The init element is index -1 (below every real index).
 __device__ __forceinline__ void amin_upd(double& v, int& ix, double nv, int ni) {
-  if (nv < v || (nv == v && ni < ix && ni >= 0)) {
+  if (nv < v || (nv == v && ni > ix)) {
     v = nv;
     ix = ni;
   }
@@ -842,8 +846,9 @@ __device__ void fin_alpha(const DV& D, const FinParams& P, int nb, const double2
       a[k] = sh[k][0];
       ii[k] = shi[k][0];
       for (int w = 1; w < NTF / 64; ++w) amin_upd(a[k], ii[k], sh[k][w], shi[k][w]);
-      // mapreduce init (1.0, 0): alpha = min(1, min ratio)
-      if (!(a[k] < 1.0)) {
+      // mapreduce init (1.0, 0) is the fold's first element: an element whose ratio is exactly 1.0
+      // comes later and replaces it (the index is the element's); larger ratios keep (1.0, init)
+      if (!(a[k] <= 1.0)) {
         a[k] = 1.0;
         ii[k] = -1;
       }
@@ -1752,7 +1757,10 @@ void MPCSolver::init_starting_point() {
   timed_factorize();
   // init factorization: the reference does not retry here; a solve with an unfactorized LDL^T is a
   // step-computation failure (oracle/mpc.py solve_system)
-  if (ldl_->status(s) != 0) throw Error("init_starting_point!: KKT factorization failed", -4);
+  if (ldl_->status(s) != 0) {
+    exception_ = MADIPM_EXC_UNFACTORIZED;
+    throw Error("init_starting_point!: KKT factorization failed", -4);
+  }
   // Step 1: least-squares primal correction
   k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_PRIMAL, 0.0, 0, nullptr, nullptr, 0, MuFold{0, 0.0, 0.0, 0.0});
   kkt_solve();
@@ -1774,7 +1782,10 @@ void MPCSolver::init_starting_point() {
   launch_reduce_final(FIN_ZSHIFT2, nbn);
   read_state();
   wait_state();
-  if (hst_->nan_flag) throw Error("SolveException in init_starting_point!", -4);
+  if (hst_->nan_flag) {
+    exception_ = MADIPM_EXC_SOLVE;
+    throw Error("SolveException in init_starting_point!", -4);
+  }
   MADIPM_REQUIRE(hst_->init_viol == 0.0, "init_starting_point!: interior assertion failed");
 }
 
@@ -1881,6 +1892,7 @@ int MPCSolver::solve(madipm_stats* stats) {
   hipStream_t s = stream_;
   trace_.clear();
   int status = MADIPM_REGULAR;
+  exception_ = MADIPM_EXC_NONE;
   double tstart = now();
   try {
     if (!initialized_) initialize_public();
@@ -1932,8 +1944,11 @@ int MPCSolver::solve(madipm_stats* stats) {
       if (h.nan_flag) {
         // SolveException in the previous iteration's solve_system! (linear_solver.jl:40-41): the
         // reference throws before apply_step!, so k_apply skipped the step on the device and the
-        // iteration is not counted (cnt.k += 1 is inside apply_step!, solver.jl:316)
-        status = MADIPM_ERROR_IN_STEP_COMPUTATION;
+        // iteration is not counted (cnt.k += 1 is inside apply_step!, solver.jl:316).  It throws the
+        // TYPE MadNLP.SolveException, which is not `isa MadNLP.LinearSolverException`, so solve!'s
+        // catch-all maps it to INTERNAL_ERROR (solver.jl:398-403)
+        status = MADIPM_INTERNAL_ERROR;
+        exception_ = MADIPM_EXC_SOLVE;
         if (k_ > 0) --k_;
         break;
       }
@@ -1980,10 +1995,13 @@ int MPCSolver::solve(madipm_stats* stats) {
           factor_enqueue(del_w_, del_c_);
           ok = ldl_->status(s) == 0;
         }
-        if (!ok) {  // every trial failed: the solve would use an unfactorized LDL^T
+        if (!ok) {  // every trial failed: prediction_step!'s solve would use an unfactorized LDL^T,
+          // which the linear solver refuses with an exception that is no LinearSolverException
+          // (LDLFactorizations' ldiv! [EXT]) -> solve!'s catch-all: INTERNAL_ERROR (solver.jl:398-403)
           del_w_ *= 100.0;
           del_c_ *= 100.0;
-          status = MADIPM_ERROR_IN_STEP_COMPUTATION;
+          status = MADIPM_INTERNAL_ERROR;
+          exception_ = MADIPM_EXC_UNFACTORIZED;
           break;
         }
         if (spec) {  // the speculated directions used the failed factor: recompute
@@ -2006,8 +2024,10 @@ int MPCSolver::solve(madipm_stats* stats) {
       MADIPM_HIP(hipGetLastError());
     }
   } catch (const Error& e) {
+    // init_starting_point!'s failures (code -4): the same two exceptions, caught by solve!'s
+    // catch-all (solver.jl:398-403)
     if (e.code == -4)
-      status = MADIPM_ERROR_IN_STEP_COMPUTATION;
+      status = MADIPM_INTERNAL_ERROR;
     else
       throw;
   }
@@ -2036,6 +2056,7 @@ int MPCSolver::solve(madipm_stats* stats) {
     stats->total_time = t_total_;
     stats->linear_solver_time = t_linsol_;
     stats->init_time = t_init_;
+    stats->exception = exception_;
   }
   return status;
 }
@@ -2066,6 +2087,70 @@ void MPCSolver::get_solution(double* x, double* y, double* zl, double* zu, doubl
     std::fill(cons, cons + m_, 0.0);
     for (size_t k = 0; k < P.Av.size(); ++k) cons[P.Ar[k]] += P.Av[k] * xh[P.Ac[k]];
   }
+}
+
+}  // namespace madipm
+
+namespace madipm {
+
+// update_step! (kernels.jl:291-358) on caller-given bounded-coordinate vectors, through the solver's
+// own step-test kernels (k_alpha + k_final(FIN_ALPHA), and k_mu + k_final(FIN_MU_FULL) for
+// MehrotraAdaptiveStep).  The vectors are laid out as a problem with n = nlb + nub primal
+// coordinates, the lower-bounded ones first, no constraints: ind_lb = [0, nlb), ind_ub = [nlb, n).
+void update_step_standalone(int rule, double tau_param, double mu, int nlb, int nub, const double* const* v,
+                            madipm_step_result* out, hipStream_t s) {
+  const int n = nlb + nub;
+  MADIPM_REQUIRE(nlb >= 0 && nub >= 0 && n > 0, "update_step: no bounded coordinate");
+  MADIPM_REQUIRE(rule >= 0 && rule <= 2, "update_step: rule must be 0, 1 or 2");
+  DBuf<double> x(n), xl(n), xu(n), zl(n), zu(n), d(n + nlb + nub), part((size_t)NPART * MAXB);
+  DBuf<int32_t> ilb(std::max(nlb, 1)), iub(std::max(nub, 1));
+  DBuf<DevState> st(1);
+  std::vector<int32_t> io(n);
+  for (int i = 0; i < n; ++i) io[i] = i;
+  ilb.upload(io.data(), nlb, s);
+  iub.upload(io.data() + nlb, nub, s);
+  MADIPM_HIP(hipMemsetAsync(x.p, 0, sizeof(double) * n, s));
+  MADIPM_HIP(hipMemsetAsync(xl.p, 0, sizeof(double) * n, s));
+  MADIPM_HIP(hipMemsetAsync(xu.p, 0, sizeof(double) * n, s));
+  MADIPM_HIP(hipMemsetAsync(zl.p, 0, sizeof(double) * n, s));
+  MADIPM_HIP(hipMemsetAsync(zu.p, 0, sizeof(double) * n, s));
+  auto cp = [&](double* dst, const double* src, int cnt) {
+    if (cnt) MADIPM_HIP(hipMemcpyAsync(dst, src, sizeof(double) * cnt, hipMemcpyDeviceToDevice, s));
+  };
+  // v: x_lr, xl_r, zl_r, dx_lr, dzl, x_ur, xu_r, zu_r, dx_ur, dzu
+  cp(x.p, v[0], nlb), cp(xl.p, v[1], nlb), cp(zl.p, v[2], nlb), cp(d.p, v[3], nlb), cp(d.p + n, v[4], nlb);
+  cp(x.p + nlb, v[5], nub), cp(xu.p + nlb, v[6], nub), cp(zu.p + nlb, v[7], nub), cp(d.p + nlb, v[8], nub);
+  cp(d.p + n + nlb, v[9], nub);
+  DV D{};
+  D.n = n;
+  D.m = 0;
+  D.nx = n;
+  D.nlb = nlb;
+  D.nub = nub;
+  D.x = x.p, D.xl = xl.p, D.xu = xu.p, D.zl = zl.p, D.zu = zu.p, D.d = d.p;
+  D.ind_lb = ilb.p, D.ind_ub = iub.p;
+  D.part = part.p;
+  D.st = st.p;
+  k_set_mu<<<1, 1, 0, s>>>(st.p, mu);
+  const int nbz = (int)std::max<int64_t>(1, std::min<int64_t>(MAXB, (std::max(nlb, nub) + NT - 1) / NT));
+  const int mode = rule == 0 ? ALPHA_CONSERVATIVE : (rule == 1 ? ALPHA_ADAPTIVE : ALPHA_MEHROTRA);
+  const double tau = rule == 2 ? 1.0 : tau_param;
+  k_alpha<<<nbz, NT, 0, s>>>(D, mode, tau, 0);
+  FinParams P{nbz, mode, 0, 0, 0, 0, 0};
+  k_final<<<1, NTF, 0, s>>>(D, FIN_ALPHA, P);
+  if (rule == 2) {
+    k_mu<<<nbz, NT, 0, s>>>(D, 1, 0.0, 0.0);
+    FinParams Q{nbz, 0, (double)(nlb + nub), tau_param, 0, 0, 0};
+    k_final<<<1, NTF, 0, s>>>(D, FIN_MU_FULL, Q);
+  }
+  MADIPM_HIP(hipGetLastError());
+  DevState h{};
+  MADIPM_HIP(hipMemcpyAsync(&h, st.p, sizeof(DevState), hipMemcpyDeviceToHost, s));
+  MADIPM_HIP(hipStreamSynchronize(s));
+  out->alpha_p = h.alpha_p;
+  out->alpha_d = h.alpha_d;
+  out->alpha_xl = h.a_xl, out->alpha_xu = h.a_xu, out->alpha_zl = h.a_zl, out->alpha_zu = h.a_zu;
+  out->i_xl = h.i_xl, out->i_xu = h.i_xu, out->i_zl = h.i_zl, out->i_zu = h.i_zu;
 }
 
 }  // namespace madipm

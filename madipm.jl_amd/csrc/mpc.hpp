@@ -119,6 +119,7 @@ class MPCSolver {
   bool eval_pending_ = false;  // k_eval's objective partials await the next FIN_TERM
   double adapt_dp_ = 0, adapt_dd_ = 0, adapt_dmin_ = 0;
   int status_ = 0, k_ = 0;
+  int exception_ = 0;  // MADIPM_EXC_* of the last solve (what solve!'s catch-all caught)
   bool initialized_ = false;
   double inf_pr_ = 0, inf_du_ = 0, inf_compl_ = 0;
   double t_init_ = 0, t_total_ = 0, t_linsol_ = 0;
@@ -126,5 +127,9 @@ class MPCSolver {
   double fs0_ = 0;  // device factorisation seconds at initialize! (cnt.linear_solver_time origin)
   DevState last_{};                // the state of the last termination test
 };
+
+// update_step! on caller-given vectors (madipm_update_step); v = the 10 device pointers in header order
+void update_step_standalone(int rule, double tau_param, double mu, int nlb, int nub, const double* const* v,
+                            madipm_step_result* out, hipStream_t s);
 
 }  // namespace madipm

@@ -301,6 +301,12 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   S.perm = perm;
   S.pinv = pinv;
   S.nnzL = std::accumulate(cnt.begin(), cnt.end(), (int64_t)0);
+  S.colcnt.resize(N);
+  S.kcol.resize(N);
+  for (int j = 0; j < N; ++j) {
+    S.colcnt[j] = (int32_t)cnt[j];
+    S.kcol[j] = (int32_t)(P.cp[j + 1] - P.cp[j] + (diagcount[perm[j]] ? 1 : 0));
+  }
 
   stamp("before 3");
   // ---------------- 3. fundamental supernodes

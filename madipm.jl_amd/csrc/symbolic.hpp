@@ -159,6 +159,10 @@ struct SymbolicPlan {
   int64_t lb_wsize = 0;
   bool mine(int s) const { return owner.empty() || owner[s] == shard; }
   bool top(int s) const { return !owner.empty() && owner[s] < 0; }
+  // SURVEY 8(d)'s algorithmic counts per pivot column (permuted ids): nnz of L's column (diagonal
+  // included) and of the caller's K in that pivot column (lower triangle in pivot order, diagonal
+  // included) -- B_fact = sum 8 colcnt + 12 kcol, B_solve = 2 x 8 sum colcnt
+  std::vector<int32_t> colcnt, kcol;
   // statistics
   int64_t nnzL = 0;          // exact nnz(L) incl. diagonal (column counts)
   int64_t nnzL_super = 0;    // stored lower-trapezoid entries incl. relaxed zeros

@@ -182,7 +182,7 @@ MadNLP.is_supported(::Type{HIPLDLSolver}, ::Type{Float64}) = true
 MadNLP.default_options(::Type{HIPLDLSolver}) = HIPLDLOptions()
 
 # ------------------------------------------------------------ whole-solver route (native MPC driver)
-# struct madipm_qp / madipm_options / madipm_stats of include/madipm_hip.h
+# struct madipm_qp / madipm_options / madipm_stats of include/madipm_hip.h (same field order: C layout)
 struct MadipmQP
     nvar::Int32; ncon::Int32; nnzh::Int64; nnzj::Int64
     c::Ptr{Float64}; c0::Float64
@@ -192,41 +192,132 @@ struct MadipmQP
     x0::Ptr{Float64}; y0::Ptr{Float64}; minimize::Int32
 end
 
+struct MadipmOptions          # IPMOptions (src/utils.jl:69-105) + the linear solver's options
+    tol::Float64; max_iter::Int32; max_wall_time::Float64; divergence_tol::Float64; scaling::Int32
+    bound_push::Float64; bound_fac::Float64; bound_relax_factor::Float64
+    regularization::Int32; delta_p::Float64; delta_d::Float64; delta_min::Float64
+    step_rule::Int32; step_tau::Float64; max_ncorr::Int32
+    mu_init::Float64; mu_min::Float64; tol_linear_solve::Float64; check_residual::Int32
+    kkt_system::Int32; print_level::Int32
+    ldl::LdlOpts
+end
+
+struct MadipmStats
+    status::Int32; iter::Int32
+    objective::Float64; dual_objective::Float64
+    inf_pr::Float64; inf_du::Float64; inf_compl::Float64; mu::Float64
+    total_time::Float64; linear_solver_time::Float64; init_time::Float64
+    exception::Int32          # MADIPM_EXC_*: 1 SolveException, 2 solve with an unfactorized matrix
+end
+
+# rebuild an immutable struct with some fields replaced
+_with(x::T; kw...) where {T} = T((haskey(kw, f) ? convert(fieldtype(T, f), kw[f]) : getfield(x, f) for f in fieldnames(T))...)
+
+const _IPM_SCALARS = (:tol, :max_iter, :max_wall_time, :divergence_tol, :bound_push, :bound_fac,
+                      :bound_relax_factor, :max_ncorr, :mu_init, :mu_min, :tol_linear_solve)
+const _LDL_KEYS = (:ordering, :dense_alpha, :relax, :small_front_max, :pivot_tol, :nshards)
+
+# load_options (src/utils.jl:121-148) onto struct madipm_options: the IPMOptions keyword names and
+# types of the reference; leftovers are reported as ignored (MadNLP.print_ignored_options, l.140-142)
+function madipm_options(; kwargs...)
+    r = Ref{MadipmOptions}()
+    ccall((:madipm_default_options, libmadipm), Cvoid, (Ref{MadipmOptions},), r)
+    o = r[]
+    kw = Dict{Symbol,Any}(kwargs)
+    set = Dict{Symbol,Any}()
+    for k in _IPM_SCALARS
+        haskey(kw, k) && (set[k] = pop!(kw, k))
+    end
+    haskey(kw, :scaling) && (set[:scaling] = Int32(pop!(kw, :scaling)))
+    haskey(kw, :check_residual) && (set[:check_residual] = Int32(pop!(kw, :check_residual)))
+    if haskey(kw, :regularization)
+        reg = pop!(kw, :regularization)
+        if reg isa MadIPM.NoRegularization
+            set[:regularization] = 0
+        elseif reg isa MadIPM.FixedRegularization
+            set[:regularization] = 1; set[:delta_p] = reg.delta_p; set[:delta_d] = reg.delta_d
+        elseif reg isa MadIPM.AdaptiveRegularization
+            set[:regularization] = 2; set[:delta_p] = reg.delta_p; set[:delta_d] = reg.delta_d
+            set[:delta_min] = reg.delta_min
+        else
+            error("madipm_hip: unsupported regularization $(typeof(reg))")
+        end
+    end
+    if haskey(kw, :step_rule)
+        rule = pop!(kw, :step_rule)
+        if rule isa MadIPM.ConservativeStep
+            set[:step_rule] = 0; set[:step_tau] = rule.tau
+        elseif rule isa MadIPM.AdaptiveStep
+            set[:step_rule] = 1; set[:step_tau] = rule.tau_min
+        elseif rule isa MadIPM.MehrotraAdaptiveStep
+            set[:step_rule] = 2; set[:step_tau] = rule.gamma_f
+        else
+            error("madipm_hip: unsupported step rule $(typeof(rule))")
+        end
+    end
+    if haskey(kw, :kkt_system)
+        K = pop!(kw, :kkt_system)
+        set[:kkt_system] = K <: MadNLP.ScaledSparseKKTSystem ? 1 : K <: MadIPM.NormalKKTSystem ? 2 :
+                           K <: MadNLP.SparseKKTSystem ? 0 : error("madipm_hip: unsupported kkt_system $K")
+    end
+    haskey(kw, :print_level) && (set[:print_level] = Int32(pop!(kw, :print_level) <= MadNLP.INFO))
+    haskey(kw, :barrier_update) && pop!(kw, :barrier_update) isa MadIPM.Mehrotra
+    haskey(kw, :linear_solver) && pop!(kw, :linear_solver)   # the native route always uses the HIP LDL^T
+    ldl = Dict{Symbol,Any}(k => pop!(kw, k) for k in _LDL_KEYS if haskey(kw, k))
+    rethrow_error = Bool(pop!(kw, :rethrow_error, false))
+    isempty(kw) || @warn "The following options are ignored: $(join(keys(kw), ", "))"
+    o = _with(o; set...)
+    isempty(ldl) || (o = _with(o; ldl=_with(o.ldl; ldl...)))
+    return o, rethrow_error
+end
+
+struct HIPSolveException <: Exception
+    code::Int32
+end
+Base.showerror(io::IO, e::HIPSolveException) =
+    print(io, e.code == 1 ? "MadNLP.SolveException (residual check of solve_system!)" :
+              "solve with an unfactorized KKT system")
+
 """
-    madipm_hip(qp::QuadraticModel{Float64}; options...) -> (status, objective, iter, x, y, zl, zu)
+    madipm_hip(qp::QuadraticModel{Float64}; kwargs...) -> NamedTuple
 
 `MPCSolver(qp; kwargs...)` + `solve!` run entirely on the GPU (src/structure.jl:79-178,
-src/solver.jl:362-418).  `options` are the fields of `struct madipm_options`, set through
-`madipm_default_options` + the keyword names of `IPMOptions` (src/utils.jl:69-119).
+src/solver.jl:362-418), with the reference's keyword names (`IPMOptions`, src/utils.jl:69-119;
+`regularization`, `step_rule`, `kkt_system` take the reference's types) plus the linear solver's
+(`ordering`, `relax`, `small_front_max`, `pivot_tol`, `nshards`).  Returns the fields of
+MadNLP.MadNLPExecutionStats that update_solution! fills (src/utils.jl:150-156).  An exception caught by
+solve!'s catch-all (status INTERNAL_ERROR) is rethrown when `rethrow_error = true` (src/solver.jl:402).
 """
-function madipm_hip(qp::QuadraticModel{Float64}; set_options! = (o -> o))
+function madipm_hip(qp::QuadraticModel{Float64}; kwargs...)
     d, m = qp.data, qp.meta
     Hr, Hc = Int32.(d.H.rows) .- Int32(1), Int32.(d.H.cols) .- Int32(1)
     Ar, Ac = Int32.(d.A.rows) .- Int32(1), Int32.(d.A.cols) .- Int32(1)
-    opts = zeros(UInt8, 4096)                       # struct madipm_options, filled by the library
-    ccall((:madipm_default_options, libmadipm), Cvoid, (Ptr{UInt8},), opts)
-    set_options!(opts)
+    opts, rethrow_error = madipm_options(; kwargs...)
     h = Ref{Ptr{Cvoid}}(C_NULL)
-    GC.@preserve Hr Hc Ar Ac d m opts begin
+    GC.@preserve Hr Hc Ar Ac d m begin
         q = Ref(MadipmQP(m.nvar, m.ncon, length(d.H.vals), length(d.A.vals), pointer(d.c), d.c0,
                          pointer(Hr), pointer(Hc), pointer(d.H.vals), pointer(Ar), pointer(Ac), pointer(d.A.vals),
                          pointer(m.lcon), pointer(m.ucon), pointer(m.lvar), pointer(m.uvar),
                          pointer(m.x0), pointer(m.y0), Int32(m.minimize)))
-        check(ccall((:madipm_solver_create, libmadipm), Cint, (Ref{MadipmQP}, Ptr{UInt8}, Ref{Ptr{Cvoid}}),
-                    q, opts, h), "madipm_solver_create")
+        check(ccall((:madipm_solver_create, libmadipm), Cint,
+                    (Ref{MadipmQP}, Ref{MadipmOptions}, Ref{Ptr{Cvoid}}), q, Ref(opts), h), "madipm_solver_create")
     end
-    stats = zeros(UInt8, 256)                       # struct madipm_stats
+    st = Ref{MadipmStats}()
     try
-        check(ccall((:madipm_solver_solve, libmadipm), Cint, (Ptr{Cvoid}, Ptr{UInt8}), h[], stats), "madipm_solver_solve")
+        check(ccall((:madipm_solver_solve, libmadipm), Cint, (Ptr{Cvoid}, Ref{MadipmStats}), h[], st),
+              "madipm_solver_solve")
+        s = st[]
+        (rethrow_error && s.status == Int32(MadNLP.INTERNAL_ERROR) && s.exception > 0) &&
+            throw(HIPSolveException(s.exception))
         x, zl, zu = zeros(m.nvar), zeros(m.nvar), zeros(m.nvar)
-        y = zeros(m.ncon)
+        y, cons = zeros(m.ncon), zeros(m.ncon)
         check(ccall((:madipm_solver_get_solution, libmadipm), Cint,
                     (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
-                    h[], x, y, zl, zu, C_NULL), "madipm_solver_get_solution")
-        status = reinterpret(Int32, stats[1:4])[1]
-        objective = reinterpret(Float64, stats[9:16])[1]
-        iter = reinterpret(Int32, stats[5:8])[1]
-        return (status, objective, iter, x, y, zl, zu)
+                    h[], x, y, zl, zu, cons), "madipm_solver_get_solution")
+        return (status = MadNLP.Status(s.status), iter = Int(s.iter), objective = s.objective,
+                dual_objective = s.dual_objective, solution = x, constraints = cons, multipliers = y,
+                multipliers_L = zl, multipliers_U = zu, primal_feas = s.inf_pr, dual_feas = s.inf_du,
+                total_time = s.total_time, linear_solver_time = s.linear_solver_time)
     finally
         ccall((:madipm_solver_destroy, libmadipm), Cvoid, (Ptr{Cvoid},), h[])
     end

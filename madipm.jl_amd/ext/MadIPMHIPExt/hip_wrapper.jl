@@ -18,9 +18,21 @@ end
 
 hipstream() = AMDGPU.stream().stream                 # hipStream_t of the task-local stream
 
-# 0-based copies of 1-based index arrays, one per source array (kept alive with it)
-const ZB = WeakKeyDict{Any,Any}()
-zero_based(x::ROCVector{Ti}) where {Ti<:Integer} = get!(() -> x .- one(Ti), ZB, x)
+# Per-array caches keyed by object IDENTITY (objectid), never by content: hashing a device array would
+# read it element by element from the host.  The entry is dropped by a finalizer on the key array.
+function cached!(f, cache::Dict{UInt,Any}, x)
+    id = objectid(x)
+    v = get(cache, id, nothing)
+    v === nothing || return v
+    v = f()
+    cache[id] = v
+    finalizer(_ -> delete!(cache, id), x)
+    return v
+end
+
+# 0-based copies of 1-based index arrays (structure arrays: never change after construction)
+const ZB = Dict{UInt,Any}()
+zero_based(x::ROCVector{Ti}) where {Ti<:Integer} = cached!(() -> x .- one(Ti), ZB, x)
 
 # ------------------------------------------------------------ transfer!  (cuda_wrapper.jl:4-24)
 mutable struct TransferPlan
@@ -28,10 +40,10 @@ mutable struct TransferPlan
     nsrc::Int
     ndest::Int
 end
-const PLANS = WeakKeyDict{Any,TransferPlan}()
+const PLANS = Dict{UInt,Any}()
 
 function transfer_plan(map::ROCVector{Int}, ndest::Int)
-    p = get(PLANS, map, nothing)
+    p = get(PLANS, objectid(map), nothing)
     (p !== nothing && p.ndest == ndest) && return p
     hmap = Int64.(Array(map)) .- 1                    # 0-based, host; counting-sorted by the library
     h = Ref{Ptr{Cvoid}}(C_NULL)
@@ -39,7 +51,9 @@ function transfer_plan(map::ROCVector{Int}, ndest::Int)
                 length(hmap), hmap, Int32(0), ndest, h), "madipm_transfer_create")
     p = TransferPlan(h[], length(hmap), ndest)
     finalizer(q -> ccall((:madipm_transfer_destroy, libmadipm), Cvoid, (Ptr{Cvoid},), q.handle), p)
-    PLANS[map] = p
+    p0 = get(PLANS, objectid(map), nothing)
+    PLANS[objectid(map)] = p
+    p0 === nothing && finalizer(_ -> delete!(PLANS, objectid(map)), map)
     return p
 end
 

@@ -18,7 +18,7 @@ def __getattr__(name):
                 "SparseKKTSystem", "ScaledSparseKKTSystem", "NormalKKTSystem", "ExecutionStats",
                 "SOLVE_SUCCEEDED", "INFEASIBLE_PROBLEM_DETECTED", "MAXIMUM_ITERATIONS_EXCEEDED",
                 "MAXIMUM_WALLTIME_EXCEEDED", "DIVERGING_ITERATES", "ERROR_IN_STEP_COMPUTATION", "INTERNAL_ERROR",
-                "STATUS_NAMES", "RCCLComm", "HostComm"):
+                "STATUS_NAMES", "RCCLComm", "HostComm", "SolveException", "UnfactorizedSolveException"):
         from . import solver
         return getattr(solver, name)
     if name == "HIPLDLSolver":

@@ -49,12 +49,12 @@ NKERNELS = 22  # MADIPM_NKERNELS
 
 class KStat(C.Structure):
     _fields_ = [("name", C.c_char * 32), ("launches", C.c_int64), ("time_ms", C.c_double),
-                ("bytes", C.c_double), ("flops", C.c_double)]
+                ("bytes", C.c_double), ("flops", C.c_double), ("alg_bytes", C.c_double)]
 
 
 def kstats_to_list(arr) -> list:
     return [{"name": k.name.decode(), "launches": int(k.launches), "time_ms": float(k.time_ms),
-             "bytes": float(k.bytes), "flops": float(k.flops)} for k in arr]
+             "bytes": float(k.bytes), "flops": float(k.flops), "alg_bytes": float(k.alg_bytes)} for k in arr]
 
 
 def _sig(name, res, args):

@@ -186,24 +186,30 @@ class Model:
     def constraints(self, F, S) -> list:
         return list(self._cons.get((F, S), []))
 
-    def get_bounds(self, v: VariableIndex):
-        """MOI.Utilities.get_bounds: the intersection of the VariableIndex-in-set constraints on v."""
-        lo, hi = -math.inf, math.inf
+    def all_bounds(self):
+        """MOI.Utilities.get_bounds for every variable at once: the intersection of the
+        VariableIndex-in-set constraints on each, in ONE pass over those constraints."""
+        lo = [-math.inf] * self._nvar
+        hi = [math.inf] * self._nvar
         for (F, S), lst in self._cons.items():
             if F is not VariableIndex:
                 continue
             for _, f, s in lst:
-                if f != v:
-                    continue
+                i = f.value
                 if S is EqualTo:
-                    lo, hi = max(lo, s.value), min(hi, s.value)
+                    lo[i], hi[i] = max(lo[i], s.value), min(hi[i], s.value)
                 elif S is GreaterThan:
-                    lo = max(lo, s.lower)
+                    lo[i] = max(lo[i], s.lower)
                 elif S is LessThan:
-                    hi = min(hi, s.upper)
+                    hi[i] = min(hi[i], s.upper)
                 elif S is Interval:
-                    lo, hi = max(lo, s.lower), min(hi, s.upper)
+                    lo[i], hi[i] = max(lo[i], s.lower), min(hi[i], s.upper)
         return lo, hi
+
+    def get_bounds(self, v: VariableIndex):
+        """MOI.Utilities.get_bounds: the intersection of the VariableIndex-in-set constraints on v."""
+        lo, hi = self.all_bounds()
+        return lo[v.value], hi[v.value]
 
 
 def supports_constraint(F, S) -> bool:
@@ -222,8 +228,9 @@ def parse_variable(model: Model):
     nvar = len(vars_)
     lvar, uvar, x0 = np.zeros(nvar), np.zeros(nvar), np.zeros(nvar)
     index_map = {vi: VariableIndex(i) for i, vi in enumerate(vars_)}
+    lo, hi = model.all_bounds()  # one pass over the bound constraints (not one per variable)
     for i, vi in enumerate(vars_):
-        lvar[i], uvar[i] = model.get_bounds(vi)
+        lvar[i], uvar[i] = lo[vi.value], hi[vi.value]
         val = model.primal_start.get(vi)
         if val is not None:
             x0[i] = val

@@ -71,10 +71,15 @@ def presolve(qp: QuadraticModel):
     n, m = qp.nvar, qp.ncon
     lvar, uvar = qp.lvar.copy(), qp.uvar.copy()
     lcon, ucon = qp.lcon.copy(), qp.ucon.copy()
-    c = qp.c.copy()
-    c0 = float(qp.c0)
+    # every reduction below is stated for a minimisation (the minimiser of an unconstrained variable,
+    # the bound an empty column's cost points to, y_i = -c_j / a_ij): a MAX model is reduced as
+    # min -f and the objective is negated back at the end; recovered multipliers are those of min -f,
+    # MadNLP's internal convention (the solver's multipliers of a MAX model are too)
+    sg = 1.0 if qp.minimize else -1.0
+    c = sg * qp.c
+    c0 = sg * float(qp.c0)
     Ar, Ac, Av = qp.Arows.copy(), qp.Acols.copy(), qp.Avals.copy()
-    Hr, Hc, Hv = qp.Hrows.copy(), qp.Hcols.copy(), qp.Hvals.copy()
+    Hr, Hc, Hv = qp.Hrows.copy(), qp.Hcols.copy(), sg * qp.Hvals
     var_alive = np.ones(n, bool)
     con_alive = np.ones(m, bool)
     xfix = np.full(n, np.nan)
@@ -227,7 +232,7 @@ def presolve(qp: QuadraticModel):
     ea = (Av != 0.0) & var_alive[Ac] & con_alive[Ar]
     eh = (Hv != 0.0) & var_alive[Hr] & var_alive[Hc]
     new = QuadraticModel(
-        c=c[keep_var], c0=c0, Hrows=vmap[Hr[eh]], Hcols=vmap[Hc[eh]], Hvals=Hv[eh],
+        c=sg * c[keep_var], c0=sg * c0, Hrows=vmap[Hr[eh]], Hcols=vmap[Hc[eh]], Hvals=sg * Hv[eh],
         Arows=cmap[Ar[ea]], Acols=vmap[Ac[ea]], Avals=Av[ea],
         lcon=lcon[keep_con], ucon=ucon[keep_con], lvar=lvar[keep_var], uvar=uvar[keep_var],
         x0=np.clip(qp.x0[keep_var], lvar[keep_var], uvar[keep_var]), y0=qp.y0[keep_con],

@@ -12,6 +12,7 @@ Python mirror of `ext/MadIPMCUDAExt/cuda_wrapper.jl` + `MadIPMCUDAExt.jl` (what 
     build_normal_system(n_rows, n_cols, Jtp, Jtj)  cuda_wrapper.jl:214-234 -> build_normal_system (host)
     fill_structure!(A, rows, cols)                 MadIPMCUDAExt.jl:15-32 -> fill_structure
     NLPModels.obj / grad!                          MadIPMCUDAExt.jl:34-45 -> qp_obj / qp_grad
+    update_step!(rule, solver) + get_alpha_max_*   kernels.jl:226-358     -> update_step
 """
 from __future__ import annotations
 
@@ -38,6 +39,16 @@ L._sig("madipm_assemble_normal_system", C.c_int, [C.c_int32, C.c_int32, vp, vp, 
 L._sig("madipm_csr_fill_structure", C.c_int, [C.c_int32, vp, vp, vp, vp, vp])
 L._sig("madipm_qp_obj", C.c_int, [vp, vp, C.c_double, vp, vp, C.c_int32, vp, f64p, vp])
 L._sig("madipm_qp_grad", C.c_int, [vp, vp, vp, vp, C.c_int32, vp])
+
+
+class StepResult(C.Structure):
+    _fields_ = [("alpha_p", C.c_double), ("alpha_d", C.c_double), ("alpha_xl", C.c_double),
+                ("alpha_xu", C.c_double), ("alpha_zl", C.c_double), ("alpha_zu", C.c_double),
+                ("i_xl", C.c_int32), ("i_xu", C.c_int32), ("i_zl", C.c_int32), ("i_zu", C.c_int32)]
+
+
+L._sig("madipm_update_step", C.c_int, [C.c_int32, C.c_double, C.c_double, C.c_int32, C.c_int32] + [vp] * 10
+       + [C.POINTER(StepResult), vp])
 
 
 def _stream(stream) -> int:
@@ -208,3 +219,20 @@ def qp_grad(H: MadIPMOperator, c, x, g, stream=None):
     L.check(L.lib.madipm_qp_grad(H.h, _dptr(c, torch.float64), _dptr(x, torch.float64), _dptr(g, torch.float64),
                                  x.numel(), _stream(stream)), "madipm_qp_grad")
     return g
+
+
+_RULES = {"conservative": 0, "adaptive": 1, "mehrotra": 2}
+
+
+def update_step(rule: str, tau: float, mu: float, x_lr, xl_r, zl_r, dx_lr, dzl, x_ur, xu_r, zu_r, dx_ur, dzu,
+                stream=None) -> dict:
+    """update_step!(rule, solver) (kernels.jl:291-358) on device vectors over the bounded coordinates:
+    rule "conservative" (tau), "adaptive" (tau_min = tau, with mu), "mehrotra" (gamma_f = tau).
+    Returns alpha_p, alpha_d, the four max ratios and their 0-based argmin indices (-1 = init)."""
+    f64 = _torch().float64
+    nlb, nub = int(x_lr.numel()), int(x_ur.numel())
+    r = StepResult()
+    ptrs = [_dptr(t, f64) for t in (x_lr, xl_r, zl_r, dx_lr, dzl, x_ur, xu_r, zu_r, dx_ur, dzu)]
+    L.check(L.lib.madipm_update_step(_RULES[rule], float(tau), float(mu), nlb, nub, *ptrs, C.byref(r),
+                                     _stream(stream)), "update_step!")
+    return {k: getattr(r, k) for k, _ in StepResult._fields_}

@@ -110,7 +110,22 @@ class Stats(C.Structure):
     _fields_ = [("status", C.c_int32), ("iter", C.c_int32), ("objective", C.c_double),
                 ("dual_objective", C.c_double), ("inf_pr", C.c_double), ("inf_du", C.c_double),
                 ("inf_compl", C.c_double), ("mu", C.c_double), ("total_time", C.c_double),
-                ("linear_solver_time", C.c_double), ("init_time", C.c_double)]
+                ("linear_solver_time", C.c_double), ("init_time", C.c_double), ("exception", C.c_int32)]
+
+
+# The exceptions solve!'s catch-all turns into INTERNAL_ERROR (src/solver.jl:398-403) and rethrows
+# when rethrow_error = true (the reference benchmark sets it, scripts/benchmarks_cpu.jl:39).
+class SolveException(Exception):
+    """MadNLP.SolveException, thrown (as a type) by solve_system! (src/linear_solver.jl:40-41)."""
+
+
+class UnfactorizedSolveException(Exception):
+    """The linear solver refusing a solve after every trial of factorize_regularized_system!
+    (src/linear_solver.jl:6-17) failed (LDLFactorizations' ldiv! on an unfactorized object [EXT])."""
+
+
+EXC_NONE, EXC_SOLVE, EXC_UNFACTORIZED = 0, 1, 2
+_EXCEPTIONS = {EXC_SOLVE: SolveException, EXC_UNFACTORIZED: UnfactorizedSolveException}
 
 
 class IterTrace(C.Structure):
@@ -370,6 +385,10 @@ class MPCSolver:
                 L.check(rc, "solve!")
             st.status = INTERNAL_ERROR
             st.iter = len(self.trace()) - 1 if self.trace() else 0
+        elif st.status == INTERNAL_ERROR and st.exception in _EXCEPTIONS and self.rethrow_error:
+            raise _EXCEPTIONS[st.exception](
+                "MPC loop: " + ("residual check of solve_system! (src/linear_solver.jl:40-41)"
+                                if st.exception == EXC_SOLVE else "solve with an unfactorized KKT system"))
         nx, m = self.qp.nvar, self.qp.ncon
         x, zl, zu = np.empty(nx), np.empty(nx), np.empty(nx)
         y, cons = np.empty(m), np.empty(m)

@@ -30,6 +30,23 @@ MAXIMUM_WALLTIME_EXCEEDED = -2
 DIVERGING_ITERATES = -3
 INFEASIBLE_PROBLEM_DETECTED = 2
 ERROR_IN_STEP_COMPUTATION = -4
+INTERNAL_ERROR = -5
+
+
+class SolveException(Exception):
+    """MadNLP.SolveException: src/linear_solver.jl:41 throws the TYPE (`throw(MadNLP.SolveException)`),
+    and a DataType is never `isa MadNLP.LinearSolverException`, so solve! (src/solver.jl:379-405) lands
+    in its catch-all: INTERNAL_ERROR, rethrown when rethrow_error (the benchmark scripts set it,
+    scripts/benchmarks_cpu.jl:39).  [EXT assumption: SolveException is a type, as in MadNLP 0.8.]"""
+
+
+class UnfactorizedSolveException(Exception):
+    """The linear solver refusing to solve with an unfactorized matrix (after every trial of
+    factorize_regularized_system!, src/linear_solver.jl:6-17, failed): LDLFactorizations' ldiv!
+    throws an exception that is no LinearSolverException [EXT] -> INTERNAL_ERROR as above."""
+
+
+EXC_NONE, EXC_SOLVE, EXC_UNFACTORIZED = 0, 1, 2
 
 
 @dataclass
@@ -52,6 +69,7 @@ class OracleOptions:
     mu_min: float = 1e-12
     tol_linear_solve: float = 1e-8
     check_residual: bool = False
+    rethrow_error: bool = False
     kkt_system: str = "K2"     # "K2" (SparseKKTSystem) | "K25" (ScaledSparseKKTSystem) | "normal"
 
 
@@ -68,6 +86,7 @@ class OracleStats:
     total_time: float = 0.0
     linear_solver_time: float = 0.0
     trace: list = field(default_factory=list)
+    exception: int = EXC_NONE
 
 
 def get_index_constraints(lvar, uvar, lcon, ucon):
@@ -425,8 +444,8 @@ class OracleMPC:
         """solve_system! src/linear_solver.jl:19-44 (copy, solve, residual check)."""
         if not getattr(self, "_factorized", True):
             # every trial of factorize_regularized_system! failed: LDLFactorizations' ldiv! refuses an
-            # unfactorized object [EXT]; the HIP library reports it as a step-computation failure
-            raise FloatingPointError("solve with an unfactorized KKT system")
+            # unfactorized object [EXT]
+            raise UnfactorizedSolveException("solve with an unfactorized KKT system")
         d = self.kkt_solve(p.copy())
         w = self.kkt_mul(d, -1.0, 1.0, p.copy())
         norm_w = np.max(np.abs(w)) if len(w) else 0.0
@@ -435,7 +454,7 @@ class OracleMPC:
         self.last_residual = ratio
         self.residuals.append(ratio)
         if math.isnan(ratio) or (self.opt.check_residual and ratio > self.opt.tol_linear_solve):
-            raise FloatingPointError("SolveException")
+            raise SolveException("residual check of solve_system!")
         return d
 
     # ---------------------------------------------------------------- views
@@ -609,14 +628,16 @@ class OracleMPC:
 
     @staticmethod
     def _argmin_ratio(num, den, mask):
-        """mapreduce((val, i), min-by-first; init=(1.0, 0)) of kernels.jl:226-272.
-        Returns (alpha, index or -1 for the init element)."""
+        """mapreduce((val, i), (e1, e2) -> e1[1] < e2[1] ? e1 : e2; init=(1.0, 0)) of kernels.jl:226-272,
+        a LEFT fold: a later element replaces the accumulator unless the accumulator is strictly
+        smaller, so among equal ratios the last index wins, and an element whose ratio is exactly
+        1.0 replaces the init element.  Returns (alpha, index or -1 for the init element)."""
         if not np.any(mask):
             return 1.0, -1
         with np.errstate(divide="ignore", invalid="ignore"):
             vals = np.where(mask, num / den, INF)
-        i = int(np.argmin(vals))
-        if vals[i] < 1.0:
+        i = len(vals) - 1 - int(np.argmin(vals[::-1]))   # last occurrence of the minimum
+        if vals[i] <= 1.0:
             return float(vals[i]), i
         return 1.0, -1
 
@@ -644,49 +665,13 @@ class OracleMPC:
         return min(a_xl, a_xu), min(a_zl, a_zu)
 
     def update_step(self, d):
-        """update_step! kernels.jl:291-358."""
-        rule = self.opt.step_rule
-        if rule[0] == "conservative":
-            self.alpha_p, self.alpha_d = self.fraction_to_boundary(d, rule[1])
-        elif rule[0] == "adaptive":
-            tau = max(1 - self.mu, rule[1])
-            self.alpha_p, self.alpha_d = self.fraction_to_boundary(d, tau)
-        elif rule[0] == "mehrotra":
-            gamma_f = rule[1]
-            gamma_a = 1.0 / (1.0 - gamma_f)
-            dx, _, dzl, dzu = self._split(d)
-            a_xl, a_xu, i_xl, i_xu = self.alpha_max_primal(d, 1.0)
-            a_zl, a_zu, i_zl, i_zu = self.alpha_max_dual(d, 1.0)
-            max_p, max_d = min(a_xl, a_xu), min(a_zl, a_zu)
-            mu_full = self.affine_complementarity_measure(d, max_p, max_d) / gamma_a
-            x = self.x
-            xlr, xlb = x[self.ind_lb], self.xl[self.ind_lb]
-            xur, xub = x[self.ind_ub], self.xu[self.ind_ub]
-            zl, zu = self.zl[self.ind_lb], self.zu[self.ind_ub]
-            dxl, dxu = dx[self.ind_lb], dx[self.ind_ub]
-            ap, ad = 1.0, 1.0
-            if max_p < 1.0:
-                if a_xl <= a_xu:
-                    i = i_xl
-                    tmp = mu_full / (zl[i] + max_d * dzl[i])
-                    ap = (xlr[i] - xlb[i] - tmp) / (-dxl[i])
-                else:
-                    i = i_xu
-                    tmp = mu_full / (zu[i] + max_d * dzu[i])
-                    ap = (xub[i] - xur[i] - tmp) / dxu[i]
-            if max_d < 1.0:
-                if a_zl <= a_zu:
-                    i = i_zl
-                    tmp = mu_full / (xlr[i] + max_p * dxl[i] - xlb[i])
-                    ad = -(zl[i] - tmp) / dzl[i]
-                else:
-                    i = i_zu
-                    tmp = mu_full / (xub[i] - xur[i] - max_p * dxu[i])
-                    ad = -(zu[i] - tmp) / dzu[i]
-            self.alpha_p = max(ap, gamma_f * max_p)
-            self.alpha_d = max(ad, gamma_f * max_d)
-        else:
-            raise ValueError(rule)
+        """update_step! kernels.jl:291-358 (on the bounded-coordinate views, step_on_vectors)."""
+        dx, _, dzl, dzu = self._split(d)
+        x = self.x
+        r = step_on_vectors(self.opt.step_rule, self.mu, x[self.ind_lb], self.xl[self.ind_lb], self.zl[self.ind_lb],
+                            dx[self.ind_lb], dzl, x[self.ind_ub], self.xu[self.ind_ub], self.zu[self.ind_ub],
+                            dx[self.ind_ub], dzu)
+        self.alpha_p, self.alpha_d = r["alpha_p"], r["alpha_d"]
 
     def update_regularization(self):
         """kernels.jl:370-401."""
@@ -837,12 +822,17 @@ class OracleMPC:
         """solve! src/solver.jl:362-418 (exceptions → status)."""
         t0 = time.perf_counter()
         self._start = t0
+        self.exception = EXC_NONE
         try:
             self.initialize()
             self._start = time.perf_counter()      # src/solver.jl:181
             self.mpc()
-        except FloatingPointError:
-            self.status = ERROR_IN_STEP_COMPUTATION
+        except (SolveException, UnfactorizedSolveException) as e:
+            # neither is a MadNLP.LinearSolverException: the catch-all (src/solver.jl:398-403)
+            self.status = INTERNAL_ERROR
+            self.exception = EXC_SOLVE if isinstance(e, SolveException) else EXC_UNFACTORIZED
+            if self.opt.rethrow_error:
+                raise
         total = time.perf_counter() - self._start
         return self.stats(total)
 
@@ -859,7 +849,67 @@ class OracleMPC:
                            multipliers_L=self.zl[: self.nx] / self.obj_scale,
                            multipliers_U=self.zu[: self.nx] / self.obj_scale,
                            total_time=total_time, linear_solver_time=self.linear_solver_time,
-                           trace=list(self.trace))
+                           trace=list(self.trace), exception=getattr(self, "exception", EXC_NONE))
+
+
+def step_on_vectors(rule, mu, x_lr, xl_r, zl_r, dx_lr, dzl, x_ur, xu_r, zu_r, dx_ur, dzu) -> dict:
+    """update_step!(rule, solver) (kernels.jl:291-358) with get_alpha_max_primal / _dual
+    (kernels.jl:226-272) on the bounded-coordinate views.  rule: ("conservative", tau) |
+    ("adaptive", tau_min) | ("mehrotra", gamma_f).  Indices 0-based, -1 = the init element."""
+    am = OracleMPC._argmin_ratio
+
+    def primal(tau):
+        a_l, i_l = am((-x_lr + xl_r) * tau, dx_lr, dx_lr < 0)
+        a_u, i_u = am((-x_ur + xu_r) * tau, dx_ur, dx_ur > 0)
+        return a_l, a_u, i_l, i_u
+
+    def dual(tau):
+        a_l, i_l = am(-zl_r * tau, dzl, dzl < 0)
+        a_u, i_u = am(-zu_r * tau, dzu, (dzu < 0) & (zu_r + dzu < 0))   # kernels.jl:263
+        return a_l, a_u, i_l, i_u
+
+    kind, par = rule[0], rule[1]
+    if kind in ("conservative", "adaptive"):
+        tau = par if kind == "conservative" else max(1 - mu, par)
+        a_xl, a_xu, i_xl, i_xu = primal(tau)
+        a_zl, a_zu, i_zl, i_zu = dual(tau)
+        ap, ad = min(a_xl, a_xu), min(a_zl, a_zu)
+    elif kind == "mehrotra":
+        gamma_f = par
+        gamma_a = 1.0 / (1.0 - gamma_f)
+        a_xl, a_xu, i_xl, i_xu = primal(1.0)
+        a_zl, a_zu, i_zl, i_zu = dual(1.0)
+        max_p, max_d = min(a_xl, a_xu), min(a_zl, a_zu)
+        cnt = len(x_lr) + len(x_ur)
+        mu_full = 0.0
+        if cnt:   # get_affine_complementarity_measure (kernels.jl:176-208)
+            mu_full = (np.sum(((x_lr + max_p * dx_lr) - xl_r) * (zl_r + max_d * dzl))
+                       + np.sum((xu_r - (x_ur + max_p * dx_ur)) * (zu_r + max_d * dzu))) / cnt
+        mu_full /= gamma_a
+        ap, ad = 1.0, 1.0
+        if max_p < 1.0:
+            if a_xl <= a_xu:
+                i = i_xl
+                tmp = mu_full / (zl_r[i] + max_d * dzl[i])
+                ap = (x_lr[i] - xl_r[i] - tmp) / (-dx_lr[i])
+            else:
+                i = i_xu
+                tmp = mu_full / (zu_r[i] + max_d * dzu[i])
+                ap = (xu_r[i] - x_ur[i] - tmp) / dx_ur[i]
+        if max_d < 1.0:
+            if a_zl <= a_zu:
+                i = i_zl
+                tmp = mu_full / (x_lr[i] + max_p * dx_lr[i] - xl_r[i])
+                ad = -(zl_r[i] - tmp) / dzl[i]
+            else:
+                i = i_zu
+                tmp = mu_full / (xu_r[i] - x_ur[i] - max_p * dx_ur[i])
+                ad = -(zu_r[i] - tmp) / dzu[i]
+        ap, ad = max(ap, gamma_f * max_p), max(ad, gamma_f * max_d)
+    else:
+        raise ValueError(rule)
+    return dict(alpha_p=float(ap), alpha_d=float(ad), alpha_xl=a_xl, alpha_xu=a_xu, alpha_zl=a_zl, alpha_zu=a_zu,
+                i_xl=i_xl, i_xu=i_xu, i_zl=i_zl, i_zu=i_zu)
 
 
 def _initialize_variables(x, xl, xu, bound_push, bound_fac, free):

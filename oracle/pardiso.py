@@ -36,7 +36,7 @@ def mkl():
         # Intel OpenMP runtime beside it crashes multithreaded PARDISO (measured: SIGSEGV at 8 threads).
         # Selected through the environment before the library loads (MKL_Set_Threading_Layer after
         # loading leaves MKL single-threaded).
-        os.environ["MKL_THREADING_LAYER"] = "GNU"
+        os.environ.setdefault("MKL_THREADING_LAYER", "GNU")
         _MKL = C.CDLL(MKL_PATH)
         _MKL.pardiso.restype = None
         _MKL.MKL_Set_Num_Threads.argtypes = [C.c_int]

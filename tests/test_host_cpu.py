@@ -301,6 +301,36 @@ def test_presolve_free_rows_singleton_columns_unconstrained_quadratic():
     assert abs(A[0] @ xo - 4.0) <= 1e-8
 
 
+def test_presolve_maximize_model():
+    """A MAX model (max -f == min f, case2 negated) presolves to the negated min model: same optimum
+    (sign-flipped), same postsolved x, and the recovered multipliers in the solver's convention (those of
+    min -f: the oracle's multipliers of the original MAX model)."""
+    import numpy as np
+    from madipm_amd import presolve_qp, postsolve
+    from madipm_amd.qp import QuadraticModel
+    from oracle.mpc import OracleMPC, OracleOptions
+    q = _presolve_case2()
+    qmax = QuadraticModel(c=-q.c, c0=-q.c0, Hrows=q.Hrows, Hcols=q.Hcols, Hvals=-q.Hvals, Arows=q.Arows,
+                          Acols=q.Acols, Avals=q.Avals, lcon=q.lcon, ucon=q.ucon, lvar=q.lvar, uvar=q.uvar,
+                          minimize=False)
+    nmin, _ = presolve_qp(q)
+    new, flag = presolve_qp(qmax)
+    assert flag and not new.minimize
+    assert np.array_equal(new.c, -nmin.c) and new.c0 == -nmin.c0 and np.array_equal(new.Hvals, -nmin.Hvals)
+    info = new.meta["presolve"]
+    assert info.xfix[4] == 0.5                          # the maximiser of -x4^2 + 2 x4 on [0, 0.5]
+    ref = OracleMPC(qmax, OracleOptions(max_iter=300)).solve()
+    sol = OracleMPC(new, OracleOptions(max_iter=300)).solve()
+    assert ref.status == sol.status == 1
+    assert abs(sol.objective - ref.objective) <= 1e-7 * max(1.0, abs(ref.objective))
+    xo, yo = postsolve(info, sol.solution, sol.multipliers)
+    assert np.allclose(xo, ref.solution, atol=1e-6)
+    assert abs(yo[0] - (-3.0)) <= 1e-12                 # y of min -f: same as the MIN model's
+    assert np.allclose(yo[info.keep_con], ref.multipliers[info.keep_con], atol=1e-5)
+    refmin = OracleMPC(q, OracleOptions(max_iter=300)).solve()
+    assert np.allclose(ref.multipliers, refmin.multipliers, atol=1e-6)
+
+
 @pytest.mark.parametrize("ordering", [1, 3, 4])
 def test_dense_block_orderings_defer_constraint_vertices(ordering):
     """K2 of a QP with a dense A (m x n, m < n) and a diagonal H: every ordering must eliminate the

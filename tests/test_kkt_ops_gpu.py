@@ -91,6 +91,15 @@ def test_coo_to_csr_bitexact(m, n, nnz, seed):
     assert np.array_equal(_np(Bp), Rp) and np.array_equal(_np(Bj), Aj[o]) and np.array_equal(_np(Bx), Ax[o])
 
 
+def test_coo_to_csr_rejects_out_of_range():
+    """An index outside [0, n_rows) x [0, n_cols) is reported, not turned into a corrupt CSR."""
+    from madipm_amd.rocm_wrapper import coo_to_csr
+    Ax = np.ones(3)
+    for Ai, Aj in (([0, 5, 1], [0, 1, 2]), ([0, 1, 1], [0, -1, 2]), ([0, 1, 1], [0, 1, 3])):
+        with pytest.raises(Exception, match="out of range"):
+            coo_to_csr(4, 3, _t(np.array(Ai, np.int32)), _t(np.array(Aj, np.int32)), _t(Ax))
+
+
 def test_fill_structure_exact():
     from madipm_amd.rocm_wrapper import fill_structure
     from oracle import kkt_ops as O

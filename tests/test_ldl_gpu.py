@@ -125,16 +125,6 @@ def test_ldl_leaf_folding(fold, well, monkeypatch):
 
 
 @pytest.mark.parametrize("well", [True, False])
-def test_ldl_leaf_entries_from_l(well, monkeypatch):
-    """Experimental MADIPM_LEAF_FROM_L=1: leaf fronts write no update block; the assembly gather
-    forms each leaf update entry from the leaf's L panel and pivots — same pivots / solution."""
-    monkeypatch.setenv("MADIPM_LEAF_FROM_L", "1")
-    K, Lw = block_angular_k2(3000, 4000, 20, 7, well=well)
-    ls = _check_case(K, Lw, well=well)
-    assert ls.inertia() == (4000, 0, 3000)
-
-
-@pytest.mark.parametrize("well", [True, False])
 def test_ldl_qp_dense_front(well):
     K, Lw = random_k2(150, 400, 0.05, 11, qp=True, well=well)
     ls = _check_case(K, Lw, small_front_max=128, well=well)
@@ -232,3 +222,40 @@ def test_small_front_storage_variants(sfm):
     ref = OracleLDL(K, ls.perm())
     assert ref.factorize() == N
     _check_pivots(ls.diag(), ref.diag(), K)
+
+
+@pytest.mark.parametrize("case", ["block", "qp_dense_front", "batched_leaves"])
+def test_alg_bytes_sum_to_survey_counts(case):
+    """bench.py's roofline prices a launch by SURVEY 8(d)'s algorithmic bytes (madipm_kstat.alg_bytes):
+    over one factorisation the launches' alg_bytes add up to exactly 8 nnzL + 12 nnzK, and over one solve
+    to 2 x 8 nnzL (every column factorised / substituted once, by exactly one launch)."""
+    from madipm_amd.linear_solver import HIPLDLSolver
+    if case == "block":
+        K, Lw = block_angular_k2(3000, 4000, 20, 7)
+        kw = {}
+    elif case == "qp_dense_front":
+        K, Lw = random_k2(150, 400, 0.05, 11, qp=True)
+        kw = {}
+    else:
+        K, Lw = _dense_k2(150, 1000, 5)
+        kw = {"ordering": 0}
+    N = K.shape[0]
+    ls = HIPLDLSolver(N, Lw.indptr, Lw.indices, **kw)
+    info = ls.info()
+    if case == "batched_leaves":
+        assert info["lb_members"] >= 500
+    dev = torch.device("cuda:0")
+    vals = torch.from_numpy(Lw.data.copy()).to(dev)
+    solve_kinds = {"k_fwd_small", "k_fwd_gather", "k_fwd_big", "k_bwd_below", "k_bwd_big", "k_bwd_small",
+                   "k_fwd_tiny", "k_bwd_tiny", "k_lb_gemv", "k_fwd_tree", "k_bwd_tree"}
+    ls.set_kernel_timing()
+    assert ls.factorize(vals) == 0
+    st = ls.kernel_stats()
+    fact = sum(k["alg_bytes"] for k in st if k["name"] not in solve_kinds)
+    assert fact == pytest.approx(8.0 * info["nnzL"] + 12.0 * info["nnzK"], rel=1e-12), (case, fact)
+    ls.set_kernel_timing()
+    x = torch.ones(N, dtype=torch.float64, device=dev)
+    ls.solve(x)
+    st = ls.kernel_stats()
+    sol = sum(k["alg_bytes"] for k in st if k["name"] in solve_kinds)
+    assert sol == pytest.approx(16.0 * info["nnzL"], rel=1e-12), (case, sol)

@@ -5,10 +5,13 @@
   (Sigma_j = 0, H = 0): its pivot is exactly del_w when it is eliminated before its row, and the
   library's `pivot_tol` option (mirrored by the oracle) rejects del_w = 1e-12 and 1e-10, accepts 1e-8.
   With max_ncorr = 0 this also runs the recomputation of the speculatively enqueued directions.
-* every trial failing (del_w = 0): the solve would use an unfactorized LDL^T -> ERROR_IN_STEP_COMPUTATION
-  with the iterate untouched and the iteration not counted (cnt.k += 1 is in apply_step!, solver.jl:316).
-* check_residual with an impossible tol_linear_solve -> SolveException (linear_solver.jl:40-41)
-  -> ERROR_IN_STEP_COMPUTATION (solver.jl:392-394).
+* every trial failing (del_w = 0): the solve would use an unfactorized LDL^T, which the linear solver
+  refuses with an exception that is no MadNLP.LinearSolverException -> solve!'s catch-all:
+  INTERNAL_ERROR (solver.jl:398-403), the iterate untouched and the iteration not counted
+  (cnt.k += 1 is in apply_step!, solver.jl:316); rethrown with rethrow_error = true.
+* check_residual with an impossible tol_linear_solve -> `throw(MadNLP.SolveException)`
+  (linear_solver.jl:40-41) throws the TYPE, which is not `isa LinearSolverException` -> INTERNAL_ERROR
+  (solver.jl:398-403), rethrown with rethrow_error = true (scripts/benchmarks_cpu.jl:39 sets it).
 * INFEASIBLE_PROBLEM_DETECTED / DIVERGING_ITERATES (solver.jl:209-213).
 * maximization: the objective sign flip of update_solution! (src/utils.jl:150-156).
 Tolerances as tests/test_mpc_gpu.py: status and iteration count equal, objective 1e-6 relative.
@@ -69,28 +72,46 @@ def test_regularization_retry_matches_oracle(max_ncorr):
             assert abs(tg[key] - tr[key]) <= 1e-6 * abs(tr[key]) + 1e-12, (tg["k"], key, tg[key], tr[key])
 
 
-def test_all_trials_fail_is_step_error():
-    from madipm_amd import ERROR_IN_STEP_COMPUTATION
+def test_all_trials_fail_is_internal_error():
+    from madipm_amd import INTERNAL_ERROR
+    from madipm_amd.solver import EXC_UNFACTORIZED
     qp = _free_column_lp()
     gpu, ref = _run_pair(qp, (0.0, -1e-8))
-    assert gpu.status == ref.status == ERROR_IN_STEP_COMPUTATION, (gpu.status_name, ref.status)
+    assert gpu.status == ref.status == INTERNAL_ERROR, (gpu.status_name, ref.status)
+    assert ref.exception == EXC_UNFACTORIZED
     assert gpu.iter == ref.iter == 0
     assert len(gpu.trace) == len(ref.trace) == 1
     # the iterate is the one after initialize!: no step was applied
     assert np.allclose(gpu.solution, ref.solution, rtol=1e-9, atol=1e-12), (gpu.solution, ref.solution)
+    # rethrow_error = true: solve! rethrows (src/solver.jl:402)
+    from madipm_amd import MPCSolver, FixedRegularization, UnfactorizedSolveException
+    import oracle.mpc as om
+    with pytest.raises(UnfactorizedSolveException):
+        MPCSolver(qp, regularization=FixedRegularization(0.0, -1e-8), ordering=1, max_iter=100,
+                  rethrow_error=True).solve()
+    o = OracleMPC(qp, OracleOptions(regularization=("fixed", 0.0, -1e-8), max_iter=100, rethrow_error=True))
+    o.linear_solver = "ldl"
+    o.ldl_perm = MPCSolver(qp, ordering=1).kkt_perm()
+    with pytest.raises(om.UnfactorizedSolveException):
+        o.solve()
 
 
 def test_check_residual_impossible_tol():
-    from madipm_amd import ERROR_IN_STEP_COMPUTATION, MPCSolver, FixedRegularization
+    from madipm_amd import INTERNAL_ERROR, MPCSolver, FixedRegularization, SolveException
     from madipm_amd import read_mps, standard_form_qp
+    from madipm_amd.solver import EXC_SOLVE
     import os
     qp = standard_form_qp(read_mps(os.path.join(os.path.dirname(__file__), "golden", "afiro.mps")))
     gpu = MPCSolver(qp, regularization=FixedRegularization(1e-8, -1e-8), check_residual=True,
                     tol_linear_solve=1e-300).solve()
     ref = OracleMPC(qp, OracleOptions(regularization=("fixed", 1e-8, -1e-8), check_residual=True,
                                       tol_linear_solve=1e-300)).solve()
-    assert gpu.status == ref.status == ERROR_IN_STEP_COMPUTATION
+    assert gpu.status == ref.status == INTERNAL_ERROR
+    assert ref.exception == EXC_SOLVE
     assert gpu.iter == ref.iter == 0
+    with pytest.raises(SolveException):
+        MPCSolver(qp, regularization=FixedRegularization(1e-8, -1e-8), check_residual=True,
+                  tol_linear_solve=1e-300, rethrow_error=True).solve()
     # a loose tolerance never triggers: same answer as without the check
     ok = MPCSolver(qp, regularization=FixedRegularization(1e-8, -1e-8), check_residual=True,
                    tol_linear_solve=1e-6).solve()

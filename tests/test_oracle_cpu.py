@@ -170,11 +170,12 @@ def test_oracle_pardiso_linear_solver_matches_superlu():
     assert a._pardiso.nperturbed == 0 and a._pardiso.nfactor == sa.iter + 1
 
 
-def test_oracle_failed_factorization_is_step_error():
+def test_oracle_failed_factorization_is_internal_error():
     """Every trial of factorize_regularized_system! failing (del_w = 0 on a free LP column) makes the
-    next solve a step-computation error (oracle semantics the GPU tests compare against)."""
+    next solve throw an exception that is no LinearSolverException: solve!'s catch-all sets
+    INTERNAL_ERROR (src/solver.jl:398-403; oracle semantics the GPU tests compare against)."""
     from madipm_amd.qp import QuadraticModel
-    from oracle.mpc import ERROR_IN_STEP_COMPUTATION
+    from oracle.mpc import INTERNAL_ERROR, EXC_UNFACTORIZED
     inf = np.inf
     qp = QuadraticModel(c=np.array([1.0, 1.0, 0.0]), Hrows=[], Hcols=[], Hvals=[], Arows=[0, 0, 1, 1, 1],
                         Acols=[0, 1, 0, 1, 2], Avals=[1.0, 1.0, 1.0, -1.0, 1.0], lcon=[1.0, 0.0], ucon=[1.0, 0.0],
@@ -183,7 +184,8 @@ def test_oracle_failed_factorization_is_step_error():
     o.linear_solver = "ldl"
     o.ldl_perm = np.array([2, 4, 3, 1, 0])
     st = o.solve()
-    assert st.status == ERROR_IN_STEP_COMPUTATION and st.iter == 0 and len(st.trace) == 1
+    assert st.status == INTERNAL_ERROR and st.exception == EXC_UNFACTORIZED
+    assert st.iter == 0 and len(st.trace) == 1
     # pivot_tol: del_w = 1e-12 and 1e-10 rejected, 1e-8 accepted -> the retry path converges
     o = OracleMPC(qp, OracleOptions(regularization=("fixed", 1e-12, -1e-8)))
     o.linear_solver = "ldl"
