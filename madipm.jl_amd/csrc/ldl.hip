@@ -997,7 +997,7 @@ __device__ __forceinline__ void schur_strip(double* A, int r, int ld, int w, con
 }
 
 template <bool PK>
-__device__ __forceinline__ void schur_strips(double* A, int r, int ld, int w, const double* Dl, int wv, int lane) {
+__device__ __forceinline__ void schur_strips(double* A, int r, int ld, int w, const double* Dl, int wv, int nw, int lane) {
   const int nbu = (r - w + 15) >> 4;
   int I = 0, J0 = 0;
   auto adv = [&]() {
@@ -1015,7 +1015,7 @@ __device__ __forceinline__ void schur_strips(double* A, int r, int ld, int w, co
       case 3: schur_strip<PK, 3>(A, r, ld, w, Dl, I, J0, lane); break;
       default: schur_strip<PK, 4>(A, r, ld, w, Dl, I, J0, lane); break;
     }
-    for (int q = 0; q < 4; ++q) adv();
+    for (int q = 0; q < nw; ++q) adv();
   }
 }
 
@@ -1027,7 +1027,7 @@ template <bool PK>
 __device__ __forceinline__ void blocked_factor_lds(double* A, int r, int w, int ld, double* Dl, double* MK, double* cbuf,
                                                    int defer = 0, int64_t* pt = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), nw = blockDim.x >> 6;
   const int nblk = (w + 15) >> 4;
   defer = defer && w < r;
   const int jend = defer ? w : r;
@@ -1049,7 +1049,7 @@ __device__ __forceinline__ void blocked_factor_lds(double* A, int r, int w, int 
     const int R0 = k0 + kw;                       // first row / column after the pivots
     const int nbr = (r - R0 + 15) >> 4;           // 16-row blocks below
     const int jhi = defer ? ((w - R0 + 15) >> 4) - 1 : nbr;  // last column block updated
-    panel_blocks<PK>(A, r, ld, k0, kw, R0, nbr, MK, wv, 4, lane);
+    panel_blocks<PK>(A, r, ld, k0, kw, R0, nbr, MK, wv, nw, lane);
     __syncthreads();
     stamp(1);
     double dk[4];
@@ -1060,23 +1060,23 @@ __device__ __forceinline__ void blocked_factor_lds(double* A, int r, int w, int 
     }
     if (kb + 1 < nblk) {
       // the next pivot block's columns (J = 0: its diagonal block and panel rows) first ...
-      trail_strips<PK>(A, r, ld, k0, kw, R0, nbr, 0, 0, dk, wv, 4, lane, jend);
+      trail_strips<PK>(A, r, ld, k0, kw, R0, nbr, 0, 0, dk, wv, nw, lane, jend);
       __syncthreads();
       stamp(2);
-      // ... then one wave factorises it while the other three update the rest (J >= 1)
-      const int fw = (kb + 1) & 3;
+      // ... then one wave factorises it while the others update the rest (J >= 1)
+      const int fw = (kb + 1) % nw;
       if (wv == fw)
         factor16s<PK>(A, r, ld, R0, min(16, w - R0), Dl, MK, cbuf, lane);
       else
-        trail_strips<PK>(A, r, ld, k0, kw, R0, nbr, 1, jhi, dk, (wv - fw + 3) & 3, 3, lane, jend);
+        trail_strips<PK>(A, r, ld, k0, kw, R0, nbr, 1, jhi, dk, (wv - fw + nw - 1) % nw, nw - 1, lane, jend);
     } else if (!defer) {
-      trail_strips<PK>(A, r, ld, k0, kw, R0, nbr, 0, nbr, dk, wv, 4, lane, jend);
+      trail_strips<PK>(A, r, ld, k0, kw, R0, nbr, 0, nbr, dk, wv, nw, lane, jend);
     }
     __syncthreads();
     stamp(3);
   }
   if (defer) {
-    schur_strips<PK>(A, r, ld, w, Dl, wv, lane);
+    schur_strips<PK>(A, r, ld, w, Dl, wv, nw, lane);
     __syncthreads();
     stamp(4);
   }
@@ -1095,9 +1095,9 @@ template <bool PK>
 __device__ __forceinline__ void writeout_ld(const double* A, int r, int w, int ld, const double* Dl, double* L, double* D,
                                            int f0, LDLStatus* st, double tol) {
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), nw = blockDim.x >> 6;
   // L panel (ld r; d on the diagonal, zeros above): columns dealt to waves as in writeout_u
-  for (int j0 = 4 * wv; j0 < w; j0 += 16) {
+  for (int j0 = 4 * wv; j0 < w; j0 += 4 * nw) {
     double x[4][3];
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
@@ -1142,9 +1142,9 @@ __device__ __forceinline__ void blocked_writeout(const double* A, int r, int w, 
 template <bool PK, bool SC1, int NH, int NC>
 __device__ __forceinline__ void writeout_u_cols(const double* A, int r, int w, int ld, double* Uo, int uld) {
   const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
   const int u = r - w;
-  for (int b0 = NC * wv; b0 < u; b0 += 4 * NC) {
+  for (int b0 = NC * wv; b0 < u; b0 += nw * NC) {
     double x[NC][NH];
 #pragma unroll
     for (int cb = 0; cb < NC; ++cb) {
@@ -1266,6 +1266,12 @@ __global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t*
 // Latency: every phase is one or two global round trips at most (8 leaf rows per thread in flight;
 // product entries 16 per thread in flight, the next group's loads issued before the current group's
 // arithmetic, the first group before phase 1).
+// k_fact_tree's workgroup: 8 waves (2 per SIMD) — every memory phase of a tree front (the leaf fold,
+// the staging copy, the children's pushes, the write-out) is latency-bound, and a second wave per SIMD
+// doubles the loads in flight; the in-LDS factorisation deals its tiles over the 8 waves
+constexpr int FTN = SymbolicPlan::kFoldThreads;
+static_assert(FTN == 512, "k_fact_tree: 512 threads");
+
 template <bool PK>
 __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A, const double* Kx, double* arena,
                                             double* D, LDLStatus* st, double tol, double* ext, int64_t* fdg) {
@@ -1294,7 +1300,7 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
   uint2 e[GP];
   auto load_group = [&](uint2 (&g)[GP], const uint2* P, int k, int len) {
 #pragma unroll
-    for (int u = 0; u < GP; ++u) g[u] = (k + u < len) ? P[(int64_t)(k + u) * NT] : uint2{SymbolicPlan::kFoldPadDst, 0u};
+    for (int u = 0; u < GP; ++u) g[u] = (k + u < len) ? P[(int64_t)(k + u) * FTN] : uint2{SymbolicPlan::kFoldPadDst, 0u};
   };
   load_group(e, T.fold_prod + T.fold_poff[b0] + tid, 0, T.fold_plen[b0]);
   for (int bq = b0; bq < b1; ++bq) {
@@ -1306,16 +1312,16 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
     int64_t lo[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int k = tid + h * NT;
+      const int k = tid + h * FTN;
       lf[h] = (k < nleaf) ? (int32_t)(T.ab_first[k0 + k] - j0) : 0;
       lw[h] = (k < nleaf) ? T.ab_wrc[k0 + k] : 0;
       lo[h] = (k < nleaf) ? T.ab_loff[k0 + k] : 0;
     }
-    for (int q0 = 0; q0 < nrow; q0 += RPT * NT) {
+    for (int q0 = 0; q0 < nrow; q0 += RPT * FTN) {
       int32_t sa[RPT], sb[RPT];
 #pragma unroll
       for (int u = 0; u < RPT; ++u) {
-        const int q = q0 + u * NT + tid;
+        const int q = q0 + u * FTN + tid;
         sa[u] = (q < nrow) ? T.ab_src0[j0 + q] : -1;
         sb[u] = (q < nrow) ? T.ab_src1[j0 + q] : -1;
       }
@@ -1327,11 +1333,11 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
       }
 #pragma unroll
       for (int u = 0; u < RPT; ++u) {
-        const int q = q0 + u * NT + tid;
+        const int q = q0 + u * FTN + tid;
         if (q < nrow) LQ[q] = double2{va[u], vb[u]};
       }
     }
-    for (int k = tid, h = 0; k < nleaf; k += NT, ++h) {
+    for (int k = tid, h = 0; k < nleaf; k += FTN, ++h) {
       const int q0 = (h == 0) ? lf[0] : (h == 1 ? lf[1] : (int)(T.ab_first[k0 + k] - j0));
       const int wrc = (h == 0) ? lw[0] : (h == 1 ? lw[1] : T.ab_wrc[k0 + k]);
       prow0[k] = q0;
@@ -1342,7 +1348,7 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
     __syncthreads();
     lap(0);
     // (2) per leaf: pivots (+ D and the pivot check)
-    for (int k = tid; k < nleaf; k += NT) {
+    for (int k = tid; k < nleaf; k += FTN) {
       const int f0 = T.ab_f0[k0 + k], wrc = pwrc[k], w = wrc & 255, rc = wrc >> 8;
       const int jf = prow0[k];
       const double d0 = LQ[jf].x;
@@ -1363,7 +1369,7 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
     lap(1);
     // (3) per leaf row: L entries (HBM panel for the solves: d on the diagonal, zero above; LDS: l
     // and l d of the update rows)
-    for (int q = tid; q < nrow; q += NT) {
+    for (int q = tid; q < nrow; q += FTN) {
       const int k = kk[q];
       const int wrc = pwrc[k], w = wrc & 255, rc = wrc >> 8, i = q - prow0[k];
       const double d0 = pd0[k], d1 = pd1[k], f10 = pf10[k];
@@ -1458,8 +1464,8 @@ template <bool PK, int NH, int NC>
 __device__ __forceinline__ void push_cols(double* A, int r, int ld, const double* U, int64_t uld, int uc,
                                           const int32_t* rels) {
   const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  for (int b0 = NC * wv; b0 < uc; b0 += 4 * NC) {
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
+  for (int b0 = NC * wv; b0 < uc; b0 += nw * NC) {
     // every global load of the round first, from clamped addresses (no branches between them)
     double x[NC][NH];
 #pragma unroll
@@ -1506,9 +1512,9 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
   const int ld = PK ? 0 : (r | 1);
   if (T.absorb[s]) {  // original entries, then the micro-leaf children folded in LDS
     const int ntot = PK ? r * (r + 1) / 2 : r * ld;
-    for (int q = tid; q < ntot; q += NT) A[q] = 0.0;
+    for (int q = tid; q < ntot; q += FTN) A[q] = 0.0;
     __syncthreads();
-    for (int64_t q = T.asm_ptr[s] + tid; q < T.asm_ptr[s + 1]; q += NT) {
+    for (int64_t q = T.asm_ptr[s] + tid; q < T.asm_ptr[s + 1]; q += FTN) {
       const int d = (int)T.asm_dst[q], dj = d / r;  // d < r^2: 32-bit division
       A[fidx<PK>(d - dj * r, dj, r, ld)] = Kx[T.asm_src[q]];
     }
@@ -1517,16 +1523,16 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
   } else {  // pre-assembled as the LDS image: a straight copy, 16 loads in flight per thread
     const double* __restrict__ src = fscratch + T.fs_off[s];
     const int n = PK ? r * (r + 1) / 2 : r * ld;
-    for (int base = 0; base < n; base += NT * 16) {
+    for (int base = 0; base < n; base += FTN * 16) {
       double v[16];
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
-        const int q = base + k * NT + tid;
+        const int q = base + k * FTN + tid;
         v[k] = (q < n) ? src[q] : 0.0;
       }
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
-        const int q = base + k * NT + tid;
+        const int q = base + k * FTN + tid;
         if (q < n) A[q] = v[k];
       }
     }
@@ -1538,7 +1544,7 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
   if (q1 > q0) {  // the first child's relative indices are symbolic: load them before the wait
     const int c = dep[q0];
     const int uc = T.nrows[c] - (T.first[c + 1] - T.first[c]);
-    for (int a = tid; a < uc; a += NT) rels[a] = T.rel[T.rel_ptr[c] + a];
+    for (int a = tid; a < uc; a += FTN) rels[a] = T.rel[T.rel_ptr[c] + a];
   }
   if (tid < 64) poll_deps(dep, q0, q1, flags, epoch, err);
   __syncthreads();
@@ -1549,10 +1555,10 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
     const int64_t uld = T.u_ld[c];
     const double* U = arena + T.u_off[c];
     if (q > q0) {
-      for (int a = tid; a < uc; a += NT) rels[a] = T.rel[T.rel_ptr[c] + a];
+      for (int a = tid; a < uc; a += FTN) rels[a] = T.rel[T.rel_ptr[c] + a];
       __syncthreads();
     }
-    // one memory round trip per round: 4 waves x NC columns (1 wave per SIMD here, registers are free)
+    // one memory round trip per round: 8 waves x NC columns
     if (uc <= 64)
       push_cols<PK, 1, 8>(A, r, ld, U, uld, uc, rels);
     else if (uc <= 128)
@@ -1582,7 +1588,7 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
   }
 }
 
-__global__ __launch_bounds__(NT) void k_fact_tree(FrontTab T, const int32_t* __restrict__ order, int nt,
+__global__ __launch_bounds__(FTN) void k_fact_tree(FrontTab T, const int32_t* __restrict__ order, int nt,
                                                   const int32_t* __restrict__ dep_ptr, const int32_t* __restrict__ dep,
                                                   int32_t* counter, int32_t* flags, int epoch,
                                                   const double* __restrict__ Kx, double* arena,
@@ -1837,6 +1843,10 @@ __global__ __launch_bounds__(NT) void k_inertia(const double* __restrict__ D, in
   }
   if (blockIdx.x == 0 && threadIdx.x == 0 && want != 1) st->t1 = wall_clock64();  // end of the factorisation
 }
+
+// LDLSolver::count_inertia (lazily, after a factorisation without k_inertia): clear the counts; then
+// k_inertia with want = 1 and no column mask counts every pivot and leaves the t1 stamp alone
+__global__ void k_zero_counts(LDLStatus* st) { st->npos = st->nneg = st->nzero = 0; }
 
 // ------------------------------------------------------------------ batched leaf columns (SymbolicPlan::lb)
 // A group: n single-column leaf fronts c_j under one parent P, W (m x n, ld m) = their K columns on the
@@ -2655,12 +2665,179 @@ __device__ __forceinline__ void bwd_subst_c(double (&v)[3], const double* LC, in
   }
 }
 
-// Dynamic LDS of the tree solve kernels: L panel (ld r|1) | block inverses | gather staging.
-__global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __restrict__ order, int nt,
-                                                 const int32_t* __restrict__ dep_ptr, const int32_t* __restrict__ dep,
+// Folded micro leaves of a chain task (w <= 2, r <= 32, no children; their parents are fronts of the
+// chain), one thread per leaf, every load of a leaf issued before its arithmetic.
+// Forward (k_fwd_micro's arithmetic): x0 = b0, x1 = b1 - l10 x0 to xi; the update entries
+// (0 - l_a0 x0) - l_a1 x1 to the parent's gather range (gbuf), read back by the chain's fronts.
+__device__ __forceinline__ void fwd_leaves(const SolveLeaf* __restrict__ lv, int n0, int n1, const int2* __restrict__ lrow,
+                                           const double* __restrict__ arena, const double* __restrict__ b,
+                                           double* __restrict__ xi, double* __restrict__ gbuf) {
+  for (int k = n0 + (int)threadIdx.x; k < n1; k += NT) {
+    const SolveLeaf L = lv[k];
+    const int r = L.rw & 255, w = L.rw >> 8, u = r - w;
+    const double* __restrict__ P = arena + L.loff;
+    const double b0 = b[L.p0];
+    const double b1 = (w == 2) ? b[L.p1] : 0.0, l10 = (w == 2) ? P[1] : 0.0;
+    const double x0 = b0, x1 = (w == 2) ? b1 - l10 * x0 : 0.0;
+    xi[L.f0] = x0;
+    if (w == 2) xi[L.f0 + 1] = x1;
+    for (int a0 = 0; a0 < u; a0 += 8) {
+      double p[8], q[8];
+      int d[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int a = min(a0 + j, u - 1);
+        p[j] = P[w + a];
+        q[j] = (w == 2) ? P[w + a + r] : 0.0;
+        d[j] = lrow[L.roff + a].x;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (a0 + j < u) gbuf[d[j]] = (0.0 - p[j] * x0) - q[j] * x1;
+    }
+  }
+}
+
+// Backward (k_bwd_micro's arithmetic, rows summed in order): the rows' final x (ancestors: the chain's
+// fronts, stored earlier by this workgroup -> sc1 loads) -> x of the two pivots, to xi and the caller's b.
+__device__ __forceinline__ void bwd_leaves(const SolveLeaf* __restrict__ lv, int n0, int n1, const int2* __restrict__ lrow,
+                                           const double* __restrict__ arena, const double* __restrict__ D,
+                                           double* __restrict__ xi, double* __restrict__ out) {
+  for (int k = n0 + (int)threadIdx.x; k < n1; k += NT) {
+    const SolveLeaf L = lv[k];
+    const int r = L.rw & 255, w = L.rw >> 8, u = r - w;
+    const double* __restrict__ P = arena + L.loff;
+    double a0 = 0.0, a1 = 0.0;
+    for (int c0 = 0; c0 < u; c0 += 8) {
+      int src[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) src[j] = lrow[L.roff + min(c0 + j, u - 1)].y;
+      double p[8], q[8], x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int a = min(c0 + j, u - 1);
+        p[j] = P[w + a];
+        q[j] = (w == 2) ? P[w + a + r] : 0.0;
+        x[j] = ld_sc1(xi + src[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (c0 + j < u) {
+          a0 = fma(p[j], x[j], a0);
+          a1 = fma(q[j], x[j], a1);
+        }
+    }
+    const double l10 = (w == 2) ? P[1] : 0.0;
+    const double v1 = (w == 2) ? xi[L.f0 + 1] / D[L.f0 + 1] - a1 : 0.0;
+    const double v0 = xi[L.f0] / D[L.f0] - a0 - l10 * v1;
+    xi[L.f0] = v0;
+    out[L.p0] = v0;
+    if (w == 2) {
+      xi[L.f0 + 1] = v1;
+      out[L.p1] = v1;
+    }
+  }
+}
+
+// The same leaves as flat launches (MADIPM_SOLVE_FOLD=1, default): LPL lanes per leaf, each lane forms
+// x0, x1 itself (the same loads) and takes rows a = j, j + LPL, ...; the leaf record carries every
+// index, so a lane's loads are one dependent level deep (record -> b, L, row table).  Forward before
+// k_fwd_tree (it gathers the update entries from gbuf), backward after k_bwd_tree (final ancestors).
+constexpr int LPL = 4, LROWS = (32 + LPL - 1) / LPL;
+__global__ __launch_bounds__(NT) void k_fwd_leaves(const SolveLeaf* __restrict__ lv, int nleaf,
+                                                   const int2* __restrict__ lrow, const double* __restrict__ arena,
+                                                   const double* __restrict__ b, double* __restrict__ xi,
+                                                   double* __restrict__ gbuf) {
+  const int gid = blockIdx.x * NT + threadIdx.x;
+  const int k = gid / LPL, j = gid % LPL;
+  if (k >= nleaf) return;
+  const SolveLeaf L = lv[k];
+  const int r = L.rw & 255, w = L.rw >> 8, u = r - w;
+  const double* __restrict__ P = arena + L.loff;
+  double p[LROWS], q[LROWS];
+  int d[LROWS];
+#pragma unroll
+  for (int m = 0; m < LROWS; ++m) {
+    const int a = min(j + LPL * m, u - 1);
+    const bool ok = u > 0;
+    p[m] = ok ? P[w + a] : 0.0;
+    q[m] = (ok && w == 2) ? P[w + a + r] : 0.0;
+    d[m] = ok ? lrow[L.roff + a].x : 0;
+  }
+  const double b0 = b[L.p0];
+  const double b1 = (w == 2) ? b[L.p1] : 0.0, l10 = (w == 2) ? P[1] : 0.0;
+  const double x0 = b0, x1 = (w == 2) ? b1 - l10 * x0 : 0.0;
+  if (j == 0) {
+    xi[L.f0] = x0;
+    if (w == 2) xi[L.f0 + 1] = x1;
+  }
+#pragma unroll
+  for (int m = 0; m < LROWS; ++m)
+    if (j + LPL * m < u) gbuf[d[m]] = (0.0 - p[m] * x0) - q[m] * x1;
+}
+
+__global__ __launch_bounds__(NT) void k_bwd_leaves(const SolveLeaf* __restrict__ lv, int nleaf,
+                                                   const int2* __restrict__ lrow, const double* __restrict__ arena,
+                                                   const double* __restrict__ D, double* __restrict__ xi,
+                                                   double* __restrict__ out) {
+  const int gid = blockIdx.x * NT + threadIdx.x;
+  const int k = gid / LPL, j = gid % LPL;
+  if (k >= nleaf) return;  // whole leaves only: the LPL lanes of a leaf exit together
+  const SolveLeaf L = lv[k];
+  const int r = L.rw & 255, w = L.rw >> 8, u = r - w;
+  const double* __restrict__ P = arena + L.loff;
+  int src[LROWS];
+#pragma unroll
+  for (int m = 0; m < LROWS; ++m) src[m] = (u > 0) ? lrow[L.roff + min(j + LPL * m, u - 1)].y : 0;
+  double p[LROWS], q[LROWS], x[LROWS];
+#pragma unroll
+  for (int m = 0; m < LROWS; ++m) {
+    const int a = min(j + LPL * m, u - 1);
+    const bool ok = u > 0;
+    p[m] = ok ? P[w + a] : 0.0;
+    q[m] = (ok && w == 2) ? P[w + a + r] : 0.0;
+    x[m] = ok ? xi[src[m]] : 0.0;  // the tree fronts' final x (previous launch)
+  }
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+  for (int m = 0; m < LROWS; ++m)
+    if (j + LPL * m < u) {
+      a0 = fma(p[m], x[m], a0);
+      a1 = fma(q[m], x[m], a1);
+    }
+  // ((lane 0 + lane 1) + (lane 2 + lane 3)): a fixed order
+  a0 += __shfl_xor(a0, 1, LPL);
+  a1 += __shfl_xor(a1, 1, LPL);
+  a0 += __shfl_xor(a0, 2, LPL);
+  a1 += __shfl_xor(a1, 2, LPL);
+  if (j != 0) return;
+  const double l10 = (w == 2) ? P[1] : 0.0;
+  const double v1 = (w == 2) ? xi[L.f0 + 1] / D[L.f0 + 1] - a1 : 0.0;
+  const double v0 = xi[L.f0] / D[L.f0] - a0 - l10 * v1;
+  xi[L.f0] = v0;
+  out[L.p0] = v0;
+  if (w == 2) {
+    xi[L.f0 + 1] = v1;
+    out[L.p1] = v1;
+  }
+}
+
+// Tree solves over CHAIN tasks: a task is a maximal chain of tree fronts in which every front is the
+// only tree child of the next (LDLSolver ctor), solved back to back by one workgroup (forward deepest
+// first, backward top first) together with the folded micro leaves of its fronts: inside a chain no
+// flag hand-off, no second workgroup start, and the leaves need no launch of their own.  Only the
+// chain's ends talk to other workgroups (forward: the tree children of its deepest front, poll; its top
+// publishes.  Backward: the top polls its tree parent; every front publishes for the tasks below).
+// Inside the chain a front's stores (update entries, x) are drained (vmcnt 0) before the barrier that
+// precedes the next front's sc1 loads of them.
+// Dynamic LDS of the tree solve kernels: L panel | gather staging.
+__global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __restrict__ cptr, const int32_t* __restrict__ clist,
+                                                 int nt, const int32_t* __restrict__ dep_ptr, const int32_t* __restrict__ dep,
                                                  int32_t* counter, int32_t* tflags, int epoch, int lds_doubles,
                                                  const double* __restrict__ arena, const double* __restrict__ b,
-                                                 double* xi, double* uvec, int32_t* err, int64_t* dbg) {
+                                                 double* xi, double* uvec, int32_t* err, int64_t* dbg,
+                                                 const int32_t* __restrict__ lptr, const SolveLeaf* __restrict__ leaves,
+                                                 const int2* __restrict__ lrow) {
   extern __shared__ __attribute__((aligned(16))) double Ls[];
   __shared__ double v0s[SMALL_SOLVE_MAX];
   __shared__ int s_task;
@@ -2674,87 +2851,101 @@ __global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __re
   if (t >= nt) return;
   int64_t* dg = dbg ? dbg + 8 * t : nullptr;
   if (dg && tid == 0) dg[0] = wall_clock64();
-  const int s = order[t];
-  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
-  const int ldt = tree_ldt(w);
-  double* stg = Ls + r * ldt;
-  const int cap = ((lds_doubles - r * ldt) / NT) * NT;
-  stage_rowmajor(arena + T.l_off[s], Ls, r, w, ldt);
+  const int q0 = cptr[t], q1 = cptr[t + 1];
+  // the folded leaves first: they depend on b only
+  if (lptr[t + 1] > lptr[t]) {
+    fwd_leaves(leaves, lptr[t], lptr[t + 1], lrow, arena, b, xi, T.gbuf);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   if (dg) {
     __syncthreads();
     if (tid == 0) dg[1] = wall_clock64();
   }
-  if (tid < 64) poll_deps(dep, dep_ptr[t], dep_ptr[t + 1], tflags, epoch, err);
-  __syncthreads();
-  if (dg && tid == 0) dg[2] = wall_clock64();
-  // initial vector: the children scattered their update entries into this front's contiguous range
-  // gbuf[P0, P1) in row order; staged through LDS (16 coalesced loads in flight per thread), then
-  // thread i sums row i's segment in order (4 partial sums)
-  const int64_t e0 = T.row_ptr[s];
-  const int64_t P0 = T.sv_ptr[e0], P1 = T.sv_ptr[e0 + r];
-  const int64_t pr0 = (tid < r) ? T.sv_ptr[e0 + tid] : 0, pr1 = (tid < r) ? T.sv_ptr[e0 + tid + 1] : 0;
-  double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0;
-  for (int64_t base = P0; base < P1; base += cap) {
-    const int n = (int)min((int64_t)cap, P1 - base);
-    for (int q0 = 0; q0 < n; q0 += NT * 16) {
-      double tmp[16];
+  for (int q = q0; q < q1; ++q) {
+    const int s = clist[q];
+    const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+    const int ldt = tree_ldt(w);
+    double* stg = Ls + r * ldt;
+    const int cap = ((lds_doubles - r * ldt) / NT) * NT;
+    stage_rowmajor(arena + T.l_off[s], Ls, r, w, ldt);
+    if (q == q0 && tid < 64) poll_deps(dep, dep_ptr[t], dep_ptr[t + 1], tflags, epoch, err);
+    __syncthreads();  // + the previous front's / the leaves' drained stores (vmcnt 0 before it)
+    if (dg && tid == 0 && q == q0) dg[2] = wall_clock64();
+    // initial vector: the children scattered their update entries into this front's contiguous range
+    // gbuf[P0, P1) in row order; staged through LDS (16 coalesced loads in flight per thread), then
+    // thread i sums row i's segment in order (4 partial sums)
+    const int64_t e0 = T.row_ptr[s];
+    const int64_t P0 = T.sv_ptr[e0], P1 = T.sv_ptr[e0 + r];
+    const int64_t pr0 = (tid < r) ? T.sv_ptr[e0 + tid] : 0, pr1 = (tid < r) ? T.sv_ptr[e0 + tid + 1] : 0;
+    double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0;
+    for (int64_t base = P0; base < P1; base += cap) {
+      const int n = (int)min((int64_t)cap, P1 - base);
+      for (int g0 = 0; g0 < n; g0 += NT * 16) {
+        double tmp[16];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int q = q0 + k * NT + tid;
-        tmp[k] = (q < n) ? ld_sc1(T.gbuf + base + q) : 0.0;
+        for (int k = 0; k < 16; ++k) {
+          const int g = g0 + k * NT + tid;
+          tmp[k] = (g < n) ? ld_sc1(T.gbuf + base + g) : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int g = g0 + k * NT + tid;
+          if (g < n) stg[g] = tmp[k];
+        }
       }
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int q = q0 + k * NT + tid;
-        if (q < n) stg[q] = tmp[k];
+      __syncthreads();
+      const int lo = (int)(max(pr0, base) - base), hi = (int)(min(pr1, base + n) - base);
+      int p = lo;
+      for (; p + 3 < hi; p += 4) {
+        c0 += stg[p];
+        c1 += stg[p + 1];
+        c2 += stg[p + 2];
+        c3 += stg[p + 3];
       }
+      for (; p < hi; ++p) c0 += stg[p];
+      __syncthreads();
     }
+    if (tid < r) v0s[tid] = ((c0 + c1) + (c2 + c3)) + fwd_init(T, s, tid, w, f0, b);
     __syncthreads();
-    const int lo = (int)(max(pr0, base) - base), hi = (int)(min(pr1, base + n) - base);
-    int p = lo;
-    for (; p + 3 < hi; p += 4) {
-      c0 += stg[p];
-      c1 += stg[p + 1];
-      c2 += stg[p + 2];
-      c3 += stg[p + 3];
+    if (dg && tid == 0 && q == q1 - 1) dg[3] = wall_clock64();
+    if (tid < 64) {
+      const int lane = tid;
+      double v[3];
+#pragma unroll
+      for (int h = 0; h < 3; ++h) {
+        const int i = lane + 64 * h;
+        v[h] = (i < r) ? v0s[i] : 0.0;
+      }
+      fwd_subst_t(v, Ls, ldt, r, w, lane);
+      if (dg && tid == 0 && q == q1 - 1) dg[4] = wall_clock64();
+#pragma unroll
+      for (int h = 0; h < 3; ++h) {
+        const int i = lane + 64 * h;
+        if (i < w)
+          st_sc1(xi + f0 + i, v[h]);
+        else if (i < r)
+          st_sc1(uvec_dst(T, s, i - w, uvec), v[h]);
+      }
+      if (q == q1 - 1)
+        publish_sc1(&tflags[s], epoch);  // the chain's top: its tree parent is another task's
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    for (; p < hi; ++p) c0 += stg[p];
-    __syncthreads();
+    __syncthreads();  // wave 0 is done with Ls; its stores are drained
   }
-  if (tid < r) v0s[tid] = ((c0 + c1) + (c2 + c3)) + fwd_init(T, s, tid, w, f0, b);
-  __syncthreads();
-  if (dg && tid == 0) dg[3] = wall_clock64();
-  if (tid >= 64) return;
-  const int lane = tid;
-  double v[3];
-#pragma unroll
-  for (int h = 0; h < 3; ++h) {
-    const int i = lane + 64 * h;
-    v[h] = (i < r) ? v0s[i] : 0.0;
-  }
-  fwd_subst_t(v, Ls, ldt, r, w, lane);
-  if (dg && tid == 0) dg[4] = wall_clock64();
-#pragma unroll
-  for (int h = 0; h < 3; ++h) {
-    const int i = lane + 64 * h;
-    if (i < w)
-      st_sc1(xi + f0 + i, v[h]);
-    else if (i < r)
-      st_sc1(uvec_dst(T, s, i - w, uvec), v[h]);
-  }
-  publish_sc1(&tflags[s], epoch);
   if (dg && tid == 0) {
     dg[5] = wall_clock64();
-    dg[6] = s;
-    dg[7] = r;
+    dg[6] = clist[q1 - 1];
+    dg[7] = T.nrows[clist[q1 - 1]];
   }
 }
 
-__global__ __launch_bounds__(NT) void k_bwd_tree(FrontTab T, const int32_t* __restrict__ order, int nt,
-                                                 const int32_t* __restrict__ pdep, int32_t* counter, int32_t* tflags,
+__global__ __launch_bounds__(NT) void k_bwd_tree(FrontTab T, const int32_t* __restrict__ cptr, const int32_t* __restrict__ clist,
+                                                 int nt, const int32_t* __restrict__ pdep, int32_t* counter, int32_t* tflags,
                                                  int epoch, const double* __restrict__ arena,
                                                  const double* __restrict__ D, double* xi, double* __restrict__ out,
-                                                 int32_t* err) {
+                                                 int32_t* err, const int32_t* __restrict__ lptr,
+                                                 const SolveLeaf* __restrict__ leaves, const int2* __restrict__ lrow) {
   extern __shared__ __attribute__((aligned(16))) double Ls[];
   __shared__ double xbs[SMALL_SOLVE_MAX];
   __shared__ int s_task;
@@ -2764,54 +2955,61 @@ __global__ __launch_bounds__(NT) void k_bwd_tree(FrontTab T, const int32_t* __re
     if (s_task == nt - 1) atomicExch(counter, 0);  // every ticket taken: ready for the next launch
   }
   __syncthreads();
-  const int t = s_task;
+  const int t = s_task;  // backward ticket t = forward task nt - 1 - t (reverse topological order)
   if (t >= nt) return;
-  const int s = order[t];
-  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
-  const int ldc = tree_ldc(r);
-  stage_colmajor(arena + T.l_off[s], Ls, r, w, ldc);
+  const int tf = nt - 1 - t;
+  const int q0 = cptr[tf], q1 = cptr[tf + 1];
   const int lane = tid & 63;
-  const int32_t* __restrict__ rows = T.rows + T.row_ptr[s];
-  const int nb = r - w;
-  double own[3];  // this front's forward values (previous launch): plain loads
+  for (int q = q1 - 1; q >= q0; --q) {  // top first
+    const int s = clist[q];
+    const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+    const int ldc = tree_ldc(r);
+    stage_colmajor(arena + T.l_off[s], Ls, r, w, ldc);
+    const int32_t* __restrict__ rows = T.rows + T.row_ptr[s];
+    const int nb = r - w;
+    double own[3];  // this front's forward values (previous launch): plain loads
 #pragma unroll
-  for (int h = 0; h < 3; ++h) {
-    const int j = lane + 64 * h;
-    own[h] = (tid < 64 && j < w) ? xi[f0 + j] / D[f0 + j] : 0.0;
-  }
-  if (tid < 64 && pdep[t] >= 0) poll_deps(pdep, t, t + 1, tflags, epoch, err);
-  __syncthreads();
-  for (int k = tid; k < nb; k += NT) xbs[k] = ld_sc1(xi + rows[w + k]);
-  __syncthreads();
-  if (tid >= 64) return;
-  int cj[3];
+    for (int h = 0; h < 3; ++h) {
+      const int j = lane + 64 * h;
+      own[h] = (tid < 64 && j < w) ? xi[f0 + j] / D[f0 + j] : 0.0;
+    }
+    if (q == q1 - 1 && tid < 64 && pdep[t] >= 0) poll_deps(pdep, t, t + 1, tflags, epoch, err);
+    __syncthreads();  // + the previous (parent) front's drained x stores
+    for (int k = tid; k < nb; k += NT) xbs[k] = ld_sc1(xi + rows[w + k]);
+    __syncthreads();
+    if (tid < 64) {
+      int cj[3];
 #pragma unroll
-  for (int h = 0; h < 3; ++h) cj[h] = min(lane + 64 * h, w - 1);
-  double acc[3][2] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
-  for (int k8 = 0; k8 < nb; k8 += 8) {
+      for (int h = 0; h < 3; ++h) cj[h] = min(lane + 64 * h, w - 1);
+      double acc[3][2] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
+      for (int k8 = 0; k8 < nb; k8 += 8) {
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      const int k = k8 + kk;
-      if (k < nb) {
-        const double x = xbs[k];
+        for (int kk = 0; kk < 8; ++kk) {
+          const int k = k8 + kk;
+          if (k < nb) {
+            const double x = xbs[k];
 #pragma unroll
-        for (int h = 0; h < 3; ++h) acc[h][kk & 1] = fma(Ls[(w + k) + cj[h] * ldc], x, acc[h][kk & 1]);
+            for (int h = 0; h < 3; ++h) acc[h][kk & 1] = fma(Ls[(w + k) + cj[h] * ldc], x, acc[h][kk & 1]);
+          }
+        }
       }
-    }
-  }
-  double v[3];
+      double v[3];
 #pragma unroll
-  for (int h = 0; h < 3; ++h) v[h] = (lane + 64 * h < w) ? own[h] - (acc[h][0] + acc[h][1]) : 0.0;
-  bwd_subst_c(v, Ls, ldc, w, lane);
+      for (int h = 0; h < 3; ++h) v[h] = (lane + 64 * h < w) ? own[h] - (acc[h][0] + acc[h][1]) : 0.0;
+      bwd_subst_c(v, Ls, ldc, w, lane);
 #pragma unroll
-  for (int h = 0; h < 3; ++h) {
-    const int j = lane + 64 * h;
-    if (j < w) {
-      st_sc1(xi + f0 + j, v[h]);
-      if (T.wout[s]) out[T.perm[f0 + j]] = v[h];
+      for (int h = 0; h < 3; ++h) {
+        const int j = lane + 64 * h;
+        if (j < w) {
+          st_sc1(xi + f0 + j, v[h]);
+          if (T.wout[s]) out[T.perm[f0 + j]] = v[h];
+        }
+      }
+      publish_sc1(&tflags[s], epoch);  // tasks whose top hangs below s poll it
     }
+    __syncthreads();  // wave 0 is done with Ls; its stores are drained
   }
-  publish_sc1(&tflags[s], epoch);
+  if (lptr[tf + 1] > lptr[tf]) bwd_leaves(leaves, lptr[tf], lptr[tf + 1], lrow, arena, D, xi, out);
 }
 
 // ------------------------------------------------------------------ sharding (SURVEY §8 e)
@@ -3031,6 +3229,21 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         ok = in_tree[c] || (preleaf(c) && in_phase(c, 1));
       }
       in_tree[s] = ok;
+    }
+  }
+  // micro leaves (w <= 2, r <= 32, no children) under tree fronts, solved from precomputed leaf records
+  // (SolveLeaf): MADIPM_SOLVE_FOLD=1 (default) by the flat k_fwd_leaves / k_bwd_leaves launches, =2
+  // inside the tree tasks (k_fwd_tree / k_bwd_tree, beside their parent front), =0 by the generic
+  // level-0 micro launches (k_fwd_micro / k_bwd_micro)
+  std::vector<char> sleaf(std::max(ns, 1), 0);
+  {
+    const char* ev = std::getenv("MADIPM_SOLVE_FOLD");
+    sfold_ = ev ? std::atoi(ev) : 1;
+    const bool on = sfold_ > 0;
+    for (int c = 0; on && c < ns; ++c) {
+      const int p = S.parent[c];
+      sleaf[c] = p >= 0 && in_tree[p] && in_phase(c, 1) && S.child_ptr[c] == S.child_ptr[c + 1] && S.nrows[c] <= 32 &&
+                 S.first[c + 1] - S.first[c] <= 2;
     }
   }
   // ---- batched leaf columns
@@ -3330,7 +3543,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         std::vector<int32_t> tiny, small, big, micro;
         for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
           const int s = S.level_list[q];
-          if (!in_phase(s, phase) || (phase == 1 && in_tree[s])) continue;
+          if (!in_phase(s, phase) || (phase == 1 && (in_tree[s] || sleaf[s]))) continue;
           const int r = S.nrows[s], w = S.first[s + 1] - S.first[s];
           if (r <= 32 && w <= 2)
             micro.push_back(s);
@@ -3426,33 +3639,11 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     };
     build_solve(1, slev1_);
     {  // tree solve tables
-      std::vector<int32_t> ord, dptr{0}, dl, par;
+      std::vector<int32_t> ord;
       for (int lev = 0; lev < NL; ++lev)
         for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q)
           if (in_tree[S.level_list[q]]) ord.push_back(S.level_list[q]);
       ntree_ = (int)ord.size();
-      tree_lds_ = 0;
-      for (int s : ord) {
-        for (int q = S.child_ptr[s]; q < S.child_ptr[s + 1]; ++q)
-          if (in_tree[S.child_list[q]]) dl.push_back(S.child_list[q]);
-        dptr.push_back((int32_t)dl.size());
-        const double r = S.nrows[s], w = S.first[s + 1] - S.first[s];
-        tree_bytes_ += 8.0 * (r * w + 3.0 * r);
-        tree_flops_ += 2.0 * (r * w - w * (w + 1) / 2);
-        tree_alg_ += solve_alg(s);
-        tree_lds_ = std::max<int>(tree_lds_, 8 * tree_panel_doubles(s) + 8 * 2048);
-      }
-      tree_lds_ = std::min(TREE_LDS_MAX, tree_lds_ + 8 * 2048);  // up to 4096 staged gather sources
-      std::vector<int32_t> rord(ord.rbegin(), ord.rend());
-      for (int s : rord) par.push_back(S.parent[s] >= 0 && in_tree[S.parent[s]] ? S.parent[s] : -1);
-      auto up = [](DBuf<int32_t>& d, const std::vector<int32_t>& v) { d.upload(v.empty() ? std::vector<int32_t>{0} : v); };
-      up(tf_order_, ord);
-      up(tb_order_, rord);
-      up(tdep_ptr_, dptr);
-      up(tdep_, dl);
-      up(tpar_, par);
-      tflags_.alloc(std::max(ns, 1));
-      tflags_.zero();
       // children of tree fronts scatter their forward update entries straight into the parent's
       // gather range (sv order, gbuf); everyone else keeps its own update vector (uvec)
       std::vector<int64_t> inv((size_t)std::max<int64_t>(S.uvec_size, 1), -1), upm((size_t)std::max<int64_t>(S.rel_ptr[ns], 1), -1);
@@ -3464,6 +3655,102 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
             upm[S.rel_ptr[c] + a] = inv[S.uvec_off[c] + a];
             MADIPM_REQUIRE(upm[S.rel_ptr[c] + a] >= 0, "tree gather map");
           }
+      auto inv_pos = [&](int c, int a) { return upm[S.rel_ptr[c] + a]; };
+      tree_lds_ = 0;
+      for (int s : ord) {
+        const double r = S.nrows[s], w = S.first[s + 1] - S.first[s];
+        tree_bytes_ += 8.0 * (r * w + 3.0 * r);
+        tree_flops_ += 2.0 * (r * w - w * (w + 1) / 2);
+        tree_alg_ += solve_alg(s);
+        tree_lds_ = std::max<int>(tree_lds_, 8 * tree_panel_doubles(s) + 8 * 2048);
+      }
+      tree_lds_ = std::min(TREE_LDS_MAX, tree_lds_ + 8 * 2048);  // up to 4096 staged gather sources
+      // chain tasks: a tree front that is the only tree child of its tree parent is solved by the
+      // parent's workgroup right before it (MADIPM_CHAIN_SOLVE=0: one task per front).  Tasks in the
+      // order of their top front in `ord` (levels ascending): a task's forward dependencies (the tree
+      // children of its deepest front: tops of other tasks) have earlier tickets, and in reverse order
+      // the backward one (the tree parent of its top) does.
+      const char* ce = std::getenv("MADIPM_CHAIN_SOLVE");  // opt-in: measured slower on ex10 (r3)
+      const bool chains = ce && ce[0] == '1';
+      std::vector<int32_t> ntc(std::max(ns, 1), 0), only(std::max(ns, 1), -1);
+      for (int s : ord)
+        if (S.parent[s] >= 0 && in_tree[S.parent[s]]) {
+          ntc[S.parent[s]]++;
+          only[S.parent[s]] = s;
+        }
+      auto joins = [&](int c) { return chains && S.parent[c] >= 0 && in_tree[S.parent[c]] && ntc[S.parent[c]] == 1; };
+      std::vector<int32_t> cptr{0}, clist, dptr{0}, dl, tops, lptr{0};
+      std::vector<SolveLeaf> lv;
+      std::vector<int2> lrow;
+      for (int s : ord) {
+        if (joins(s)) continue;  // solved inside its parent's task
+        std::vector<int32_t> ch{s};
+        while (ntc[ch.back()] == 1 && joins(only[ch.back()])) ch.push_back(only[ch.back()]);
+        std::reverse(ch.begin(), ch.end());  // deepest first
+        for (int f : ch) {
+          clist.push_back(f);
+          for (int q = S.child_ptr[f]; q < S.child_ptr[f + 1] && sfold_ == 2; ++q) {  // folded leaves, child order
+            const int c = S.child_list[q];
+            if (!sleaf[c]) continue;
+            const int r = S.nrows[c], w = S.first[c + 1] - S.first[c], f0 = S.first[c];
+            SolveLeaf L{S.l_off[c], f0, r | (w << 8), S.perm[f0], w == 2 ? S.perm[f0 + 1] : -1, (int32_t)lrow.size(), 0};
+            lv.push_back(L);
+            for (int a = 0; a < r - w; ++a) {
+              const int64_t g = inv_pos(c, a);
+              MADIPM_REQUIRE(g >= 0 && g < INT32_MAX, "tree solve: folded leaf gather position");
+              lrow.push_back(int2{(int32_t)g, S.rows[S.row_ptr[c] + w + a]});
+            }
+          }
+        }
+        for (int q = S.child_ptr[ch[0]]; q < S.child_ptr[ch[0] + 1]; ++q)
+          if (in_tree[S.child_list[q]]) dl.push_back(S.child_list[q]);
+        cptr.push_back((int32_t)clist.size());
+        dptr.push_back((int32_t)dl.size());
+        lptr.push_back((int32_t)lv.size());
+        tops.push_back(s);
+      }
+      if (sfold_ == 1) {  // the flat leaf launches: every folded leaf, in postorder (L panels in order)
+        for (int c = 0; c < ns; ++c) {
+          if (!sleaf[c]) continue;
+          const int r = S.nrows[c], w = S.first[c + 1] - S.first[c], f0 = S.first[c];
+          lv.push_back(SolveLeaf{S.l_off[c], f0, r | (w << 8), S.perm[f0], w == 2 ? S.perm[f0 + 1] : -1,
+                                 (int32_t)lrow.size(), 0});
+          for (int a = 0; a < r - w; ++a) {
+            const int64_t g = inv_pos(c, a);
+            MADIPM_REQUIRE(g >= 0 && g < INT32_MAX, "tree solve: folded leaf gather position");
+            lrow.push_back(int2{(int32_t)g, S.rows[S.row_ptr[c] + w + a]});
+          }
+        }
+      }
+      ntask_ = (int)tops.size();
+      std::vector<int32_t> par;  // backward ticket t -> task ntask - 1 - t: the tree parent of its top
+      for (int t = ntask_ - 1; t >= 0; --t) {
+        const int p = S.parent[tops[t]];
+        par.push_back(p >= 0 && in_tree[p] ? p : -1);
+      }
+      auto up = [](DBuf<int32_t>& d, const std::vector<int32_t>& v) { d.upload(v.empty() ? std::vector<int32_t>{0} : v); };
+      up(tc_ptr_, cptr);
+      up(tc_list_, clist);
+      up(tdep_ptr_, dptr);
+      up(tdep_, dl);
+      up(tpar_, par);
+      up(tl_ptr_, lptr);
+      tleaf_.upload(lv.empty() ? std::vector<SolveLeaf>(1) : lv);
+      tlrow_.upload(lrow.empty() ? std::vector<int2>(1) : lrow);
+      nsleaf_ = (int64_t)lv.size();
+      for (const SolveLeaf& L : lv) {
+        const double r = L.rw & 255, w = L.rw >> 8;
+        const double a = 8.0 * (S.colcnt[L.f0] + (w == 2 ? S.colcnt[L.f0 + 1] : 0));
+        if (sfold_ == 2) {
+          tree_alg_ += a;
+        } else {
+          leaf_alg_ += a;
+          leaf_bytes_ += 8.0 * (r * w + 3.0 * r) + 32.0 + 8.0 * (r - w);
+          leaf_flops_ += 2.0 * (r * w - w * (w + 1) / 2);
+        }
+      }
+      tflags_.alloc(std::max(ns, 1));
+      tflags_.zero();
       upos_.upload(upm);
       gbuf_.alloc(std::max<int64_t>(S.sv_ptr[S.row_ptr[ns]], 1));
       T_.upos = upos_;
@@ -3724,7 +4011,7 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
         }
         ++fepoch_;
         TIMED(KK_FACT_TREE, L.bytes, L.alg, L.flops,
-              (k_fact_tree<<<(unsigned)nftree_, NT, L.lds_bytes, s>>>(T_, ft_order_, nftree_, ft_dptr_, ft_dep_, fcnt_,
+              (k_fact_tree<<<(unsigned)nftree_, FTN, L.lds_bytes, s>>>(T_, ft_order_, nftree_, ft_dptr_, ft_dep_, fcnt_,
                                                                       fflags_, fepoch_, Kx, arena_, fscratch_, D_, st_,
                                                                       pivot_tol, &st_->err, fdbg_.p)));
         if (fdbg_.p) tree_debug_dump(s, "fact", fdbg_.p, nftree_, "stage", "wait", "push", "factor", "store", 24);
@@ -3737,11 +4024,15 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
 // assembly and the shard's status slot.
 void LDLSolver::fact_phase1(const double* Kx, hipStream_t s) {
   if (S_.N == 0) return;
-  k_status_init<<<1, 1, 0, s>>>(st_);
+  if (!(ext_reset && ext_status_ && !sharded())) k_status_init<<<1, 1, 0, s>>>(st_);
   run_fact(fact1_, Kx, s);
   const int nb = (int)std::min<int64_t>(64, cdiv(S_.N, NT));
   const int spdf = spd ? 1 : 0;
   if (!sharded()) {
+    if (lazy_inertia && !spd && ext_status_) {  // the driver's next kernel stamps t1
+      inertia_stale_ = true;
+      return;
+    }
     TIMED(KK_INERTIA, 8.0 * S_.N, 0.0, 0.0, (k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, st_, spdf, nullptr, 0)));
     MADIPM_HIP(hipGetLastError());
     if (!ext_status_) MADIPM_HIP(hipMemcpyAsync(h_st_, st_, sizeof(LDLStatus), hipMemcpyDeviceToHost, s));
@@ -3797,6 +4088,17 @@ double LDLSolver::fact_seconds(hipStream_t s) {
   MADIPM_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
   const uint64_t t = h.ticks + (h.t1 > h.t0 ? h.t1 - h.t0 : 0);
   return khz > 0 ? (double)t / (1e3 * khz) : 0.0;
+}
+
+// lazy_inertia: count the current factor's inertia now (inertia() of a driver that skips k_inertia)
+void LDLSolver::count_inertia(hipStream_t s) {
+  if (!inertia_stale_ || S_.N == 0) return;
+  inertia_stale_ = false;
+  const int nb = (int)std::min<int64_t>(64, cdiv(S_.N, NT));
+  k_zero_counts<<<1, 1, 0, s>>>(st_);
+  k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, st_, 0, nullptr, 1);
+  MADIPM_HIP(hipGetLastError());
+  status(s, true);
 }
 
 int LDLSolver::status(hipStream_t s, bool sync) {
@@ -3876,6 +4178,27 @@ void LDLSolver::tree_debug_dump(hipStream_t s, const char* what, const int64_t* 
     acc[lv * 8 + 6] = std::max(acc[lv * 8 + 6], (d[5] - t0) * 0.01);
   }
   fprintf(stderr, "tree %s: %d tasks, span %.1f us\n", what, nt, (t1 - t0) * 0.01);
+  if (stride == 24) {  // the critical path: from the last front to end, back through the latest child
+    std::vector<int> task_of(S_.nsuper, -1);
+    for (int t = 0; t < nt; ++t) task_of[(int)h[8 * t + 6]] = t;
+    int t = 0;
+    for (int q = 1; q < nt; ++q)
+      if (h[8 * q + 5] > h[8 * t + 5]) t = q;
+    for (int depth = 0; t >= 0 && depth < 12; ++depth) {
+      const int64_t* d = &h[8 * t];
+      const int sf = (int)d[6];
+      auto us = [&](int k) { return (d[k] - t0) * 0.01; };
+      fprintf(stderr, "  crit front %6d lev %d r %3d w %3d: start %6.1f %s %6.1f %s %6.1f %s %6.1f %s %6.1f %s %6.1f\n", sf,
+              S_.level[sf], S_.nrows[sf], S_.first[sf + 1] - S_.first[sf], us(0), p1, us(1), p2, us(2), p3, us(3), p4,
+              us(4), p5, us(5));
+      int nxt = -1;
+      for (int q = S_.child_ptr[sf]; q < S_.child_ptr[sf + 1]; ++q) {
+        const int c = S_.child_list[q], tc = task_of[c];
+        if (tc >= 0 && (nxt < 0 || h[8 * tc + 5] > h[8 * nxt + 5])) nxt = tc;
+      }
+      t = nxt;
+    }
+  }
   for (int lv = 0; lv < S_.nlevels; ++lv)
     if (cnt[lv])
       fprintf(stderr, "  level %d: %5d fronts  start %.1f  %s %.2f  %s %.2f  %s %.2f  %s %.2f  %s %.2f  last end %.1f us\n", lv,
@@ -3909,14 +4232,18 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
             (k_fwd_big<<<std::min(L.nftask, 512), NT, 0, s>>>(T_, tasks + L.ftask_off, L.nftask, cnt + 2 * lev,
                                                                flags_, flag_off_, efwd, arena_, vwork_, xi_, uvec_, &st_->err)));
     }
+    if (lev == 0 && phase == 0 && ntree_ && sfold_ == 1 && nsleaf_)
+      TIMED(KK_FWD_TINY, leaf_bytes_, leaf_alg_, leaf_flops_,
+            (k_fwd_leaves<<<(unsigned)cdiv(nsleaf_ * LPL, NT), NT, 0, s>>>(tleaf_, (int)nsleaf_, tlrow_, arena_, b, xi_,
+                                                                         T_.gbuf)));
     if (lev == 0 && phase == 0 && ntree_)
       TIMED(KK_FWD_TREE, tree_bytes_, tree_alg_, tree_flops_,
-            (k_fwd_tree<<<(unsigned)ntree_, NT, tree_lds_, s>>>(T_, tf_order_, ntree_, tdep_ptr_, tdep_,
+            (k_fwd_tree<<<(unsigned)ntask_, NT, tree_lds_, s>>>(T_, tc_ptr_, tc_list_, ntask_, tdep_ptr_, tdep_,
                                                                  counters_.p + 4 * S_.nlevels, tflags_, efwd, tree_lds_ / 8,
-                                                                 arena_, b,
-                                                                 xi_, uvec_, &st_->err, tdbg_.p)));
+                                                                 arena_, b, xi_, uvec_, &st_->err, tdbg_.p, tl_ptr_, tleaf_,
+                                                                 tlrow_)));
     if (lev == 0 && phase == 0 && ntree_ && tdbg_.p)
-      tree_debug_dump(s, "fwd", tdbg_.p, ntree_, "stage", "wait", "gather", "subst", "store", 8);
+      tree_debug_dump(s, "fwd", tdbg_.p, ntask_, "leaves", "wait", "gather", "subst", "store", 8);
   }
 }
 
@@ -3928,8 +4255,13 @@ void LDLSolver::bwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
     const SolveLevel& L = V[lev];
     if (lev == 0 && phase == 0 && ntree_)
       TIMED(KK_BWD_TREE, tree_bytes_, tree_alg_, tree_flops_,
-            (k_bwd_tree<<<(unsigned)ntree_, NT, tree_lds_, s>>>(T_, tb_order_, ntree_, tpar_, counters_.p + 4 * S_.nlevels + 1,
-                                                                 tflags_, ebwd, arena_, D_, xi_, b, &st_->err)));
+            (k_bwd_tree<<<(unsigned)ntask_, NT, tree_lds_, s>>>(T_, tc_ptr_, tc_list_, ntask_, tpar_,
+                                                                 counters_.p + 4 * S_.nlevels + 1, tflags_, ebwd, arena_, D_,
+                                                                 xi_, b, &st_->err, tl_ptr_, tleaf_, tlrow_)));
+    if (lev == 0 && phase == 0 && ntree_ && sfold_ == 1 && nsleaf_)
+      TIMED(KK_BWD_TINY, leaf_bytes_, leaf_alg_, leaf_flops_,
+            (k_bwd_leaves<<<(unsigned)cdiv(nsleaf_ * LPL, NT), NT, 0, s>>>(tleaf_, (int)nsleaf_, tlrow_, arena_, D_, xi_,
+                                                                         b)));
     if (L.nbelow)
       TIMED(KK_BWD_BELOW, L.below_bytes, L.below_alg, 0.25 * L.below_bytes,
             (k_bwd_below<<<L.nbelow, NT, 0, s>>>(T_, sched_.p + L.below_off, bp_off_, arena_, xi_, bpart_)));

@@ -73,6 +73,14 @@ struct SolveTask {
   int32_t front, blk;
 };
 
+// a micro leaf (w <= 2, r <= 32, no children) folded into a tree-solve chain task: its L panel, first
+// pivot, r | w << 8, the caller's indices of its two pivots, and the offset of its below rows' entries
+// in the row table (int2: gbuf position of the forward update entry, xi index of the row)
+struct SolveLeaf {
+  int64_t loff;
+  int32_t f0, rw, p0, p1, roff, pad;
+};
+
 struct LDLStatus {  // device-resident, read back by status()
   int32_t fail_pivot;  // min failing internal pivot + 1 (INT32_MAX when none)
   int32_t npos, nneg, nzero;
@@ -82,6 +90,19 @@ struct LDLStatus {  // device-resident, read back by status()
   // factorisation, t1 at its end; ticks = the sum over the earlier ones (folded in by the next start)
   uint64_t t0, t1, ticks;
 };
+
+// Start of a factorisation (k_status_init's work; one thread): fold the previous factorisation's
+// time in, stamp t0, clear the pivot check and the inertia counts.  A caller whose own kernel runs
+// right before the factorisation does this itself (LinSolver::ext_reset) and saves that launch.
+__device__ __forceinline__ void ldl_status_start(LDLStatus* st) {
+  const uint64_t now = wall_clock64();
+  if (st->t1 > st->t0) st->ticks += st->t1 - st->t0;
+  st->t0 = st->t1 = now;
+  st->fail_pivot = INT32_MAX;
+  st->npos = st->nneg = st->nzero = 0;
+}
+// end of a factorisation whose inertia is counted lazily (LinSolver::lazy_inertia): stamp t1
+__device__ __forceinline__ void ldl_status_end(LDLStatus* st) { st->t1 = wall_clock64(); }
 
 // Kernel kinds for the live per-kernel timing (HIP events around each launch on the launch
 // stream) and their algorithmic bytes / flops per launch (DESIGN.md "Kernels and their rooflines").
@@ -137,6 +158,13 @@ class LinSolver {
   // seconds of device time spent in factorisations so far (synchronises s; cnt.linear_solver_time)
   virtual double fact_seconds(hipStream_t s) = 0;
   bool spd = false;  // Cholesky semantics: any non-positive pivot fails (normal equations)
+  // launch savings for a driver that owns the kernels around the factorisation (MPCSolver):
+  //   ext_reset: the driver's kernel right before every factorisation runs ldl_status_start on the
+  //     status block (external_status) — no k_status_init launch;
+  //   lazy_inertia: no k_inertia after the factorisation (the driver's next kernel runs
+  //     ldl_status_end); the pivot check does not need it unless spd, and inertia() counts on demand
+  bool ext_reset = false, lazy_inertia = false;
+  virtual void count_inertia(hipStream_t s) { (void)s; }
 };
 
 class LDLSolver : public LinSolver {
@@ -161,6 +189,7 @@ class LDLSolver : public LinSolver {
   //   factorize: fact_phase1; all-reduce fact_xbuf(); fact_phase2
   //   solve:     solve_phase1; all-reduce solve_xbuf(); solve_phase2; all-reduce b (n entries)
   void fact_phase1(const double* Kx, hipStream_t s);
+  void count_inertia(hipStream_t s) override;  // lazy_inertia: the counts of the current factor
   void fact_phase2(hipStream_t s);
   void solve_phase1(double* b, hipStream_t s);
   void solve_phase2(double* b, hipStream_t s);
@@ -257,7 +286,13 @@ class LDLSolver : public LinSolver {
   double fact_alg_cols(int c0, int c1) const;
   double solve_alg(int s) const;
   double lb_alg(size_t g) const;
-  DBuf<int32_t> tf_order_, tb_order_, tdep_ptr_, tdep_, tpar_, tflags_;
+  DBuf<int32_t> tc_ptr_, tc_list_, tdep_ptr_, tdep_, tpar_, tflags_, tl_ptr_;
+  int ntask_ = 0;         // chain tasks (fronts solved back to back by one workgroup)
+  int64_t nsleaf_ = 0;    // micro leaves solved from leaf records (sfold_ 1: flat launches, 2: in the tasks)
+  int sfold_ = 1;
+  double leaf_bytes_ = 0, leaf_flops_ = 0, leaf_alg_ = 0;  // the flat leaf launches (per direction)
+  DBuf<SolveLeaf> tleaf_;
+  DBuf<int2> tlrow_;
   DBuf<int64_t> tdbg_, upos_;
   DBuf<double> gbuf_;
   void tree_debug_dump(hipStream_t s, const char* what, const int64_t* dbuf, int nt, const char* p1, const char* p2,
@@ -296,6 +331,7 @@ class LDLSolver : public LinSolver {
   LDLStatus* st_ = nullptr;    // status in use: status_ or the caller's (external_status)
   LDLStatus* h_st_ = nullptr;  // its host copy
   bool ext_status_ = false;
+  bool inertia_stale_ = false;  // lazy_inertia: npos / nneg / nzero not counted for the current factor
   // live timing
   unsigned tmask_ = 0;
   std::vector<hipEvent_t> evs_;

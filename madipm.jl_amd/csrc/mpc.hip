@@ -198,13 +198,16 @@ __device__ __forceinline__ void diag_entry(const DV& D, int64_t i, double dw, do
   }
 }
 
-__global__ __launch_bounds__(NT) void k_diag(DV D, double dw, double dc) {
+// rs != nullptr: the factorisation that follows starts here (LinSolver::ext_reset)
+__global__ __launch_bounds__(NT) void k_diag(DV D, double dw, double dc, LDLStatus* rs) {
+  if (rs && blockIdx.x == 0 && threadIdx.x == 0) ldl_status_start(rs);
   GRID_LOOP(i, D.n + D.m) diag_entry(D, i, dw, dc);
 }
 
 // MadNLP.initialize!(kkt) + init_starting_point! lines 16-18 (l_diag = u_diag = 1, l/u_lower = 0,
 // pr_diag = dw; K2.5 scaling factor 1)
-__global__ __launch_bounds__(NT) void k_init_kkt(DV D, double dw, double dc) {
+__global__ __launch_bounds__(NT) void k_init_kkt(DV D, double dw, double dc, LDLStatus* rs) {
+  if (rs && blockIdx.x == 0 && threadIdx.x == 0) ldl_status_start(rs);
   GRID_LOOP(i, D.n + D.m) {
     if (i < D.n) {
       const int kl = D.lbpos[i], ku = D.ubpos[i];
@@ -318,8 +321,10 @@ struct MuFold {
 
 // host != nullptr: wave 0 of block 0 first publishes the state (k_publish's work: the speculated
 // predictor's k_rhs is the first launch after the factorisation, one launch less per iteration)
+// t1 != nullptr: the factorisation before this launch ended (LinSolver::lazy_inertia)
 __global__ __launch_bounds__(NT) void k_rhs(DV D, int mode, double mu_g, int reset, DevState* host, uint32_t* hseq,
-                                            uint32_t seq, MuFold mf) {
+                                            uint32_t seq, MuFold mf, LDLStatus* t1) {
+  if (t1 && blockIdx.x == 0 && threadIdx.x == 0) ldl_status_end(t1);
   const int n = D.n, m = D.m, nlb = D.nlb;
   double mu = (mode == RHS_CORR) ? D.st->mu : mu_g;
   if (mf.nb > 0) {  // prediction_step! + update_barrier! (kernels.jl:176-220), as k_final(FIN_MU_PRED)
@@ -780,41 +785,46 @@ struct FinParams {
   int nb_alpha;    // FIN_RESID: > 0 -> also finalise k_alpha's nb_alpha partials (slots PART_ALPHA..)
   int nb_eval;     // FIN_TERM: > 0 -> also finalise evaluate_model!'s objective (k_eval's nb_eval
                    // partials in slot PART_EVAL, the previous iteration's; P.c = its constant)
+  LDLStatus* rs;   // != nullptr: a factorisation follows this launch (LinSolver::ext_reset)
 };
 constexpr int PART_EVAL = 6;
 
-// k_final runs as ONE block of NTF threads that reads every partial in a single memory round trip:
-// thread t owns blocks 2t, 2t + 1 (one 16-B load per value; nb <= MAXB = 2 NTF), so all nv x 16 B of
-// a thread are in flight together (a one-block reader is bound by its bytes in flight, not by HBM).
-// Fixed combine order (pair, then a shuffle tree, then the waves in order): bitwise reproducible.
+// k_final runs as ONE block of NTF = 256 threads that reads every partial in a single memory round
+// trip: thread t owns blocks 8t .. 8t + 7 (four 16-B loads per value; nb <= MAXB = 8 NTF), all of a
+// thread's loads in flight together.  Fixed combine order (the thread's 8 blocks in order, a shuffle
+// tree over the wave, then the 4 waves in order): bitwise reproducible.  (Measured, tools/
+// final_bench.hip: a 1024-thread finaliser costs ~1 us more than a 256-thread one after the same
+// producer, and its 16-wave serial combine more again.)
 // (Finalising inside the producing kernel instead — block 0 polling per-block flags, or a ticket —
 // measured slower on ex10: the in-launch hand-off costs more than this launch.)
-constexpr int NTF = 1024;
-static_assert(MAXB == 2 * NTF, "k_final: two partial rows per thread");
+constexpr int NTF = 256, FPT = 8;  // threads, partial blocks per thread
+static_assert(MAXB == FPT * NTF, "k_final: eight partial rows per thread");
 
-__device__ __forceinline__ double2 part2(const DV& D, int b, int k) {
-  return *reinterpret_cast<const double2*>(D.part + pidx(b, k));
-}
-
-// the step test's argmin over the block partials in slots base.. (FIN_ALPHA: 0, fused: PART_ALPHA);
-// every thread of the block calls it (shuffles, __syncthreads), thread 0 writes the state
-// loads first (fin_alpha_load), so that a finaliser combining several reductions has every load of
-// the thread in flight together; the reduce needs the same nb
-__device__ __forceinline__ void fin_alpha_load(const DV& D, int nb, int base, double2 (&pv)[4], double2 (&pi)[4]) {
-  const int b0 = 2 * threadIdx.x;
-  const bool h0 = b0 < nb;
+__device__ __forceinline__ void part8(const DV& D, int k, int nb, double (&v)[FPT], double fill) {
+  const int b0 = FPT * threadIdx.x;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    pv[k] = h0 ? part2(D, b0, base + k) : make_double2(INF, INF);
-    pi[k] = h0 ? part2(D, b0, base + 4 + k) : make_double2(-1.0, -1.0);
+  for (int h = 0; h < FPT; h += 2) {
+    const double2 q = (b0 + h < nb) ? *reinterpret_cast<const double2*>(D.part + pidx(b0 + h, k)) : make_double2(fill, fill);
+    v[h] = q.x;
+    v[h + 1] = (b0 + h + 1 < nb) ? q.y : fill;
   }
 }
 
-__device__ void fin_alpha(const DV& D, const FinParams& P, int nb, const double2 (&pv)[4], const double2 (&pi)[4],
+// the step test's argmin over the block partials in slots base.. (FIN_ALPHA: 0, fused: PART_ALPHA);
+// every thread of the block calls it (shuffles, __syncthreads), thread 0 writes the state.  The loads
+// come first (fin_alpha_load), so that a finaliser combining several reductions has every load of the
+// thread in flight together; the reduce needs the same nb
+__device__ __forceinline__ void fin_alpha_load(const DV& D, int nb, int base, double (&pv)[4][FPT], double (&pi)[4][FPT]) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    part8(D, base + k, nb, pv[k], INF);
+    part8(D, base + 4 + k, nb, pi[k], -1.0);
+  }
+}
+
+__device__ void fin_alpha(const DV& D, const FinParams& P, const double (&pv)[4][FPT], const double (&pi)[4][FPT],
                           double (&sh)[8][NTF / 64], int (&shi)[4][NTF / 64]) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int b0 = 2 * threadIdx.x;
-  const bool h0 = b0 < nb, h1 = b0 + 1 < nb;
   DevState* st = D.st;
   double v[4];
   int ix[4];
@@ -822,8 +832,8 @@ __device__ void fin_alpha(const DV& D, const FinParams& P, int nb, const double2
   for (int k = 0; k < 4; ++k) {
     v[k] = INF;
     ix[k] = -1;
-    if (h0) amin_upd(v[k], ix[k], pv[k].x, (int)pi[k].x);
-    if (h1) amin_upd(v[k], ix[k], pv[k].y, (int)pi[k].y);
+#pragma unroll
+    for (int h = 0; h < FPT; ++h) amin_upd(v[k], ix[k], pv[k][h], (int)pi[k][h]);
   }
   for (int o = 32; o > 0; o >>= 1)
 #pragma unroll
@@ -842,9 +852,11 @@ __device__ void fin_alpha(const DV& D, const FinParams& P, int nb, const double2
   if (threadIdx.x == 0) {
     double a[4];
     int ii[4];
+#pragma unroll
     for (int k = 0; k < 4; ++k) {
       a[k] = sh[k][0];
       ii[k] = shi[k][0];
+#pragma unroll
       for (int w = 1; w < NTF / 64; ++w) amin_upd(a[k], ii[k], sh[k][w], shi[k][w]);
       // mapreduce init (1.0, 0) is the fold's first element: an element whose ratio is exactly 1.0
       // comes later and replaces it (the index is the element's); larger ratios keep (1.0, init)
@@ -875,19 +887,18 @@ __device__ void fin_alpha(const DV& D, const FinParams& P, int nb, const double2
   }
 }
 
-// one OP_SUM value over nb partials (pv = this thread's pair, loaded by the caller), combined in the
-// generic path's order; thread 0 returns it
-__device__ double fin_sum_slot(int nb, double2 pv, double (&sh)[8][NTF / 64]) {
+// one OP_SUM value over the partials this thread loaded (ev), in the generic path's order; every
+// thread returns it
+__device__ double fin_sum_slot(const double (&ev)[FPT], double (&sh)[8][NTF / 64]) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int b0 = 2 * threadIdx.x;
-  const bool h0 = b0 < nb, h1 = b0 + 1 < nb;
   double a = 0.0;
-  if (h0) a = comb(a, pv.x, OP_SUM);
-  if (h1) a = comb(a, pv.y, OP_SUM);
+#pragma unroll
+  for (int h = 0; h < FPT; ++h) a = comb(a, ev[h], OP_SUM);
   for (int o = 32; o > 0; o >>= 1) a = comb(a, __shfl_down(a, o, 64), OP_SUM);
   if (lane == 0) sh[0][wv] = a;
   __syncthreads();
   double r = sh[0][0];
+#pragma unroll
   for (int w = 1; w < NTF / 64; ++w) r = comb(r, sh[0][w], OP_SUM);
   __syncthreads();
   return r;
@@ -899,13 +910,11 @@ __global__ __launch_bounds__(NTF) void k_final(DV D, int kind, FinParams P) {
   __shared__ double sh[8][NTF / 64];
   __shared__ int shi[4][NTF / 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int b0 = 2 * threadIdx.x;
-  const bool h0 = b0 < P.nb, h1 = b0 + 1 < P.nb;
   DevState* st = D.st;
   if (kind == FIN_ALPHA) {
-    double2 apv[4], api[4];
+    double apv[4][FPT], api[4][FPT];
     fin_alpha_load(D, P.nb, 0, apv, api);
-    fin_alpha(D, P, P.nb, apv, api, sh, shi);
+    fin_alpha(D, P, apv, api, sh, shi);
     return;
   }
   int nv = 0;
@@ -921,42 +930,51 @@ __global__ __launch_bounds__(NTF) void k_final(DV D, int kind, FinParams P) {
     case FIN_ZSHIFT1: nv = 8; for (int k = 0; k < 8; ++k) ops[k] = OP_SUM; break;
     case FIN_ZSHIFT2: nv = 1; ops[0] = OP_SUM; break;
   }
-  // every load of the thread is issued before the first reduction (one memory round trip)
-  double2 pv[8];
+  // every load of the thread is issued before the first reduction (one memory round trip); every
+  // reduction here starts at 0.0 (sum, max, and min with init 0), so absent blocks load 0.0
+  double pv[8][FPT];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) pv[k] = (h0 && k < nv) ? part2(D, b0, k) : make_double2(0.0, 0.0);
-  double2 apv[4], api[4];
+  for (int k = 0; k < 8; ++k) {
+    if (k < nv)
+      part8(D, k, P.nb, pv[k], 0.0);
+    else
+#pragma unroll
+      for (int h = 0; h < FPT; ++h) pv[k][h] = 0.0;
+  }
+  double apv[4][FPT], api[4][FPT];
   if (P.nb_alpha > 0) fin_alpha_load(D, P.nb_alpha, PART_ALPHA, apv, api);
-  const double2 epv = (P.nb_eval > 0 && b0 < P.nb_eval) ? part2(D, b0, PART_EVAL) : make_double2(0.0, 0.0);
+  double ev[FPT];
+  if (P.nb_eval > 0)
+    part8(D, PART_EVAL, P.nb_eval, ev, 0.0);
   if (P.nb_alpha > 0) {  // FIN_RESID + the FIN_ALPHA of the k_alpha launched after the residual
-    fin_alpha(D, P, P.nb_alpha, apv, api, sh, shi);
+    fin_alpha(D, P, apv, api, sh, shi);
     __syncthreads();
   }
   if (P.nb_eval > 0) {  // FIN_TERM: the previous iteration's FIN_EVAL, deferred to this launch
-    const double r = fin_sum_slot(P.nb_eval, epv, sh);
+    const double r = fin_sum_slot(ev, sh);
     if (threadIdx.x == 0) st->obj_val = P.c + r;
   }
-  {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      if (k >= nv) break;
-      const int op = ops[k];
-      double a = 0.0;  // every reduction here starts at 0.0 (sum, max, and min with init 0)
-      if (h0) a = comb(a, pv[k].x, op);
-      if (h1) a = comb(a, pv[k].y, op);
-      for (int o = 32; o > 0; o >>= 1) a = comb(a, __shfl_down(a, o, 64), op);
-      if (lane == 0) sh[k][wv] = a;
-    }
+  for (int k = 0; k < 8; ++k) {
+    if (k >= nv) break;
+    const int op = ops[k];
+    double a = 0.0;
+#pragma unroll
+    for (int h = 0; h < FPT; ++h) a = comb(a, pv[k][h], op);
+    for (int o = 32; o > 0; o >>= 1) a = comb(a, __shfl_down(a, o, 64), op);
+    if (lane == 0) sh[k][wv] = a;
   }
   __syncthreads();
   if (threadIdx.x < nv) {
     const int k = threadIdx.x;
     double a = sh[k][0];
+#pragma unroll
     for (int w = 1; w < NTF / 64; ++w) a = comb(a, sh[k][w], ops[k]);
     res[k] = a;
   }
   __syncthreads();
   if (threadIdx.x != 0) return;
+  if (P.rs) ldl_status_start(P.rs);
   switch (kind) {
     case FIN_RESID: {
       const double ratio = res[0] / fmax(1.0, res[1]);  // linear_solver.jl:35
@@ -1525,7 +1543,12 @@ void MPCSolver::setup_host(const madipm_qp& q) {
   }
   part_.alloc(MAXB * NPART);
   st_.alloc(1);
-  ldl_->external_status(&st_.p->ldl_status, &hst_->ldl_status);  // carried by read_state()
+  if (ldl_->external_status(&st_.p->ldl_status, &hst_->ldl_status)) {  // carried by read_state()
+    // the MPC's own kernels start / end each factorisation: no k_status_init, no k_inertia (K2, K2.5:
+    // the pivot check needs no inertia; the normal equations' Cholesky check keeps k_inertia)
+    ldl_->ext_reset = true;
+    ldl_->lazy_inertia = !ldl_->spd;
+  }
   st_.zero(s);
   MADIPM_HIP(hipStreamSynchronize(s));
   // norm_b (solver.jl:173) on host
@@ -1603,7 +1626,7 @@ void MPCSolver::setup_host(const madipm_qp& q) {
 
 void MPCSolver::kkt_diag(double dw, double dc) {
   DV_ARGS;
-  k_diag<<<blocks(n_ + m_), NT, 0, stream_>>>(D, dw, dc);
+  k_diag<<<blocks(n_ + m_), NT, 0, stream_>>>(D, dw, dc, fact_reset());
 }
 
 // set_aug_diagonal_reg! + build_kkt! of the chosen formulation (values consumed by the LDL^T)
@@ -1620,6 +1643,16 @@ const double* MPCSolver::kvals() const { return kkt_ == KKT_NORMAL ? Cx_.p : Kx_
 // the pool grows only when a solve needs more pairs than any earlier one did
 void MPCSolver::timed_factorize() {
   ldl_->factorize_async(kvals(), stream_);
+  fact_end_pending_ = ldl_->lazy_inertia;  // the next k_rhs stamps the factorisation's end
+}
+
+// the status block the kernel right before a factorisation resets (LinSolver::ext_reset), or nullptr
+LDLStatus* MPCSolver::fact_reset() const { return ldl_->ext_reset ? &st_.p->ldl_status : nullptr; }
+// the status block the first kernel after a factorisation stamps (LinSolver::lazy_inertia), or nullptr
+LDLStatus* MPCSolver::take_fact_end() {
+  LDLStatus* p = fact_end_pending_ ? &st_.p->ldl_status : nullptr;
+  fact_end_pending_ = false;
+  return p;
 }
 
 void MPCSolver::factor_enqueue(double dw, double dc) {
@@ -1640,9 +1673,9 @@ void MPCSolver::kkt_solve() {
   }
 }
 
-void MPCSolver::launch_reduce_final(int kind, int nb, int amode, int nb_eval) {
+void MPCSolver::launch_reduce_final(int kind, int nb, int amode, int nb_eval, LDLStatus* rs) {
   DV_ARGS;
-  FinParams P{nb, 0, 0, 0, 0, 0, nb_eval};
+  FinParams P{nb, 0, 0, 0, 0, 0, nb_eval, rs};
   if (nb_eval > 0) P.c = c0s_;
   if (amode >= 0) {
     P.alpha_mode = amode;
@@ -1678,7 +1711,7 @@ void MPCSolver::solve_system(int mode, double mu, int reset, int amode, double a
   }
   MuFold mf{0, 0.0, 0.0, 0.0};
   if (mu_nb > 0) mf = MuFold{mu_nb, (double)(nlb_ + nub_), H_->has_ineq ? 1.0 : 0.0, opt_.mu_min};
-  k_rhs<<<nb, NT, 0, stream_>>>(D, mode, mu, reset, host, hseq_, seq, mf);
+  k_rhs<<<nb, NT, 0, stream_>>>(D, mode, mu, reset, host, hseq_, seq, mf, take_fact_end());
   kkt_solve();
   // amode >= 0: the step test of that mode on the new direction runs in the same launch (its own
   // blocks) and is finalised with the residual
@@ -1751,7 +1784,7 @@ void MPCSolver::init_starting_point() {
   DV_ARGS;
   const int nb = blocks(n_ + m_), nbn = blocks(n_);
   hipStream_t s = stream_;
-  k_init_kkt<<<nb, NT, 0, s>>>(D, del_w_, del_c_);
+  k_init_kkt<<<nb, NT, 0, s>>>(D, del_w_, del_c_, fact_reset());
   if (kkt_ == KKT_NORMAL) k_normal_asm<<<blocks(nnzC_), NT, 0, s>>>(D);
   if (kkt_ == KKT_K25) k_k25_scale<<<blocks(nnzK_), NT, 0, s>>>(D);  // s = 1: K2.5 = K2
   timed_factorize();
@@ -1762,13 +1795,13 @@ void MPCSolver::init_starting_point() {
     throw Error("init_starting_point!: KKT factorization failed", -4);
   }
   // Step 1: least-squares primal correction
-  k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_PRIMAL, 0.0, 0, nullptr, nullptr, 0, MuFold{0, 0.0, 0.0, 0.0});
+  k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_PRIMAL, 0.0, 0, nullptr, nullptr, 0, MuFold{0, 0.0, 0.0, 0.0}, take_fact_end());
   kkt_solve();
   SPMV_LAUNCH(k_residual, nb, s, D, del_w_, del_c_, nb, -1, 1.0);
   launch_reduce_final(FIN_RESID, nb);
   k_axpy_x<<<nbn, NT, 0, s>>>(D);
   // Step 2: dual least squares
-  k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_DUAL, 0.0, 0, nullptr, nullptr, 0, MuFold{0, 0.0, 0.0, 0.0});
+  k_rhs<<<nb, NT, 0, s>>>(D, RHS_INIT_DUAL, 0.0, 0, nullptr, nullptr, 0, MuFold{0, 0.0, 0.0, 0.0}, take_fact_end());
   kkt_solve();
   SPMV_LAUNCH(k_residual, nb, s, D, del_w_, del_c_, nb, -1, 1.0);
   launch_reduce_final(FIN_RESID, nb);
@@ -1917,7 +1950,7 @@ int MPCSolver::solve(madipm_stats* stats) {
       // k >= max_iter the termination test ends the solve whatever it finds: nothing to speculate.
       const bool last = k_ >= opt_.max_iter;
       k_term<<<nb, NT, 0, s>>>(D, last ? 0 : 1, del_w_, del_c_);
-      launch_reduce_final(FIN_TERM, nb, -1, eval_pending_ ? spmv_blocks(n_ + m_) : 0);
+      launch_reduce_final(FIN_TERM, nb, -1, eval_pending_ ? spmv_blocks(n_ + m_) : 0, last ? nullptr : fact_reset());
       eval_pending_ = false;
       if (!last) {
         assemble_kkt(del_w_, del_c_, true);

@@ -68,7 +68,7 @@ class MPCSolver {
   // solve also runs update_step_size!'s step test (only when nothing changes d in between: no Gondzio)
   void directions(bool redo, bool fuse_step);
   void step_size(bool fused);
-  void launch_reduce_final(int kind, int nvals, int amode = -1, int nb_eval = 0);
+  void launch_reduce_final(int kind, int nvals, int amode = -1, int nb_eval = 0, LDLStatus* rs = nullptr);
   int step_alpha_mode(double& tau) const;
   void read_state();  // enqueue the publication of the device state to the host mirror
   void wait_state();  // wait (host spin) until the last publication has landed
@@ -80,6 +80,8 @@ class MPCSolver {
   void kkt_solve();
   void factor_enqueue(double dw, double dc);
   void timed_factorize();
+  LDLStatus* fact_reset() const;
+  LDLStatus* take_fact_end();
   int blocks(int64_t n) const;
   int spmv_blocks(int64_t rows) const;
 
@@ -114,6 +116,7 @@ class MPCSolver {
   uint32_t* hseq_ = nullptr;         // publication counter beside it
   uint32_t pub_seq_ = 0;
   bool publish_next_ = false;        // the next solve_system's k_rhs publishes the state
+  bool fact_end_pending_ = false;    // the next solve_system's k_rhs stamps the factorisation's end
   // host scalars (MPCSolver fields of src/structure.jl:62-76)
   double del_w_ = 0, del_c_ = 0, norm_b_ = 0, norm_c_ = 0, best_compl_ = 0, obj_scale_ = 1, c0s_ = 0;
   bool eval_pending_ = false;  // k_eval's objective partials await the next FIN_TERM

@@ -19,7 +19,7 @@ namespace madipm {
 
 namespace {
 
-constexpr int NT_FOLD = 256;  // threads of k_fact_tree (product-list chunks)
+constexpr int NT_FOLD = SymbolicPlan::kFoldThreads;  // threads of k_fact_tree (product-list chunks)
 
 struct Pattern {
   // strictly-lower pattern of P K P^T: column lists (rows > col) and row lists (cols < row)
@@ -923,7 +923,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
               pr.push_back({fidx(rl[a - wc], rl[b - wc]), qb0 + a, qb0 + b});
         }
         std::stable_sort(pr.begin(), pr.end(), [](const Prod& x, const Prod& y) { return x.dst < y.dst; });
-        // 256 chunks at destination boundaries, balanced by count
+        // NT_FOLD chunks at destination boundaries, balanced by count
         const int64_t P = (int64_t)pr.size();
         bnd.assign(NT_FOLD + 1, P);
         bnd[0] = 0;

@@ -100,6 +100,7 @@ struct SymbolicPlan {
   std::vector<int64_t> g_src;          // >= 0: arena index; < 0: ~(index into caller's values)
   std::vector<int64_t> fs_off;         // small fronts with children, tree fronts: r x r scratch (else -1)
   static constexpr int kFactTreeMax = 192;
+  static constexpr int kFoldThreads = 512;  // threads of k_fact_tree: product-list chunks per batch
   static constexpr int kFactTreeFanIn = 8;
   std::vector<uint8_t> ftree;          // factorisation-tree fronts (k_fact_tree)
   // leaf folding (tree fronts whose pre-leaf children are all micro leaves: w <= 2, r <= 32): the

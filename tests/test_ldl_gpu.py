@@ -107,6 +107,28 @@ def test_ldl_schur_update_variants(defer, sfm, monkeypatch):
     assert ls.inertia() == (4000, 0, 3000)
 
 
+@pytest.mark.parametrize("chain,sfold", [("0", "1"), ("0", "0"), ("0", "2"), ("1", "2"), ("1", "1")])
+@pytest.mark.parametrize("well", [True, False])
+def test_ldl_chain_solve_and_leaf_fold(chain, sfold, well, monkeypatch):
+    """Tree solves with one task per front (default) or over chain tasks (MADIPM_CHAIN_SOLVE=1), and
+    the micro leaves under tree fronts solved from leaf records by flat launches (MADIPM_SOLVE_FOLD=1,
+    default), inside the tree tasks (=2) or by the generic micro launches (=0): same solution as the
+    oracle in every combination, and for several right-hand sides in a row (flag epochs)."""
+    monkeypatch.setenv("MADIPM_CHAIN_SOLVE", chain)
+    monkeypatch.setenv("MADIPM_SOLVE_FOLD", sfold)
+    K, Lw = block_angular_k2(3000, 4000, 20, 7, well=well)
+    ls = _check_case(K, Lw, well=well)
+    ref = OracleLDL(K, ls.perm())
+    assert ref.factorize() == K.shape[0]
+    rng = np.random.default_rng(5)
+    for _ in range(3):
+        b = rng.standard_normal(K.shape[0])
+        x = torch.from_numpy(b.copy()).cuda()
+        ls.solve(x)
+        xr = ref.solve(b)
+        assert np.max(np.abs(x.cpu().numpy() - xr)) <= (1e-12 if well else 1e-6) * np.max(np.abs(xr))
+
+
 @pytest.mark.parametrize("fold", ["0", "1"])
 @pytest.mark.parametrize("well", [True, False])
 def test_ldl_leaf_folding(fold, well, monkeypatch):

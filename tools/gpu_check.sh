@@ -7,7 +7,7 @@ TAG=${1:-check}; shift || true
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 && echo "gpu tests ok" || { echo "gpu tests FAILED"; tail -30 $OUT/pytest_gpu.log; exit 1; }
+timeout -k 10 600 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 && echo "gpu tests ok" || { echo "gpu tests FAILED"; tail -30 $OUT/pytest_gpu.log; exit 1; }
 timeout -k 10 300 python bench.py "$@" > $OUT/bench.log 2>&1 && echo "bench ok" || { echo "bench FAILED"; tail -30 $OUT/bench.log; exit 1; }
 tail -1 $OUT/bench.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 20 --warmup 2 --no-cpu --no-opt "$@" > $OUT/prof.log 2>&1 && echo "rocprof ok" || { echo "rocprof FAILED"; tail -30 $OUT/prof.log; exit 1; }
