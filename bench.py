@@ -225,18 +225,27 @@ def aggregate(dt, iters, dist, sharded):
     return max(per_rank), float(it.item()), per_rank
 
 
-def collective_volume(info, warm):
-    """Sharded factorisation: doubles all-reduced per factorisation / per solve (ldl_info xch_*), and
-    per MPC iteration with the solves-per-factorisation ratio seen in the warm-up launch counts."""
+def collective_volume(info, warm, world=None):
+    """Sharded factorisation: doubles exchanged per factorisation (all-reduce of the top fronts) and per
+    solve (all-reduce of the top rows + in-place all-gather of the subtree solution slices; ldl_info
+    xch_*), per MPC iteration with the solves-per-factorisation ratio seen in the warm-up launch
+    counts; with `world`, the ring model's bytes each rank sends per iteration (all-reduce of m
+    doubles: 2 (P-1)/P 8m; all-gather of G doubles in P slices: (P-1)/P 8G)."""
     if not info.get("xch_fact"):
         return None
     launches = {k["name"]: k["launches"] for k in warm}
     nfact = launches.get("k_fact_tree") or launches.get("k_small_blocked") or 1
     nsolve = launches.get("k_bwd_tree") or launches.get("k_bwd_tiny") or 2 * nfact
     spf = nsolve / nfact
-    return {"fact_bytes": 8 * info["xch_fact"], "solve_bytes": 8 * info["xch_solve"], "solves_per_fact": spf,
-            "allreduces_per_iter": 1 + 2 * spf,
-            "bytes_per_iter": 8 * (info["xch_fact"] + spf * info["xch_solve"])}
+    gat = info.get("xch_gather", 0)
+    out = {"fact_bytes": 8 * info["xch_fact"], "solve_bytes": 8 * (info["xch_solve"] + gat),
+           "solve_allreduce_bytes": 8 * info["xch_solve"], "solve_allgather_bytes": 8 * gat,
+           "solves_per_fact": spf, "collectives_per_iter": 1 + 2 * spf,
+           "bytes_per_iter": 8 * (info["xch_fact"] + spf * (info["xch_solve"] + gat))}
+    if world and world > 1:
+        f = (world - 1) / world
+        out["wire_bytes_per_rank_per_iter"] = 8 * f * (2 * info["xch_fact"] + spf * (2 * info["xch_solve"] + gat))
+    return out
 
 
 def main():
@@ -346,7 +355,7 @@ def main():
             "iteration_roofline": iteration_roofline(info, 1e3 * dt / max(iters, 1)),
             "kernel_ms_warmup": breakdown,
             "per_rank_s": per_rank,
-            "collectives": collective_volume(info, warm),
+            "collectives": collective_volume(info, warm, world),
             "cpu_baseline": None,
             "parity": None,
         }

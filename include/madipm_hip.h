@@ -61,7 +61,10 @@ typedef struct madipm_ldl_info {
   int32_t fold_leaves;     /* micro leaves folded by them */
   int64_t xch_fact;        /* sharded: doubles all-reduced per factorisation (top-front lower triangles
                               + 4 status slots per shard); 0 unsharded */
-  int64_t xch_solve;       /* sharded: doubles all-reduced per solve (two collectives); 0 unsharded */
+  int64_t xch_solve;       /* sharded: doubles all-reduced per solve (the top fronts' forward right-hand
+                              sides); 0 unsharded */
+  int64_t xch_gather;      /* sharded: doubles of the per-solve in-place all-gather of the shards'
+                              subtree solution slices (nshards slices); 0 unsharded */
 } madipm_ldl_info;
 
 void madipm_ldl_default_opts(madipm_ldl_opts* opts);
@@ -116,17 +119,22 @@ void madipm_ldl_destroy(madipm_ldl_t ls);
  * The north star's multi-GPU mode: the front tree is cut into independent subtrees dealt to
  * `nshards` shards (one per GPU) plus their common ancestors ("top" fronts), which every shard
  * factorises redundantly after ONE all-reduce (sum) of the top fronts' external contributions.
- * A solve needs two more: the top fronts' forward right-hand sides and the final solution.
+ * A solve needs two more: an all-reduce of the top fronts' forward right-hand sides and an all-gather
+ * of the shards' subtree solution slices (the top solution is computed redundantly on every shard).
  * No reference counterpart (the reference is single-device: cuDSS / LDLFactorizations); these entry
  * points let a host binding drive the phases with its own collective (e.g. Julia + RCCL.jl):
  *   factorize: phase 1 -> all-reduce(xbuf, xlen) -> phase 2
- *   solve:     phase 1 -> all-reduce(xbuf, xlen) -> phase 2 -> all-reduce(x, n)
+ *   solve:     phase 1 -> all-reduce(xbuf, xlen) -> phase 2 -> all-gather(xbuf, xlen) -> phase 3
+ * The solve's phase 2 returns the gather buffer: nshards slices of xlen / nshards doubles, this
+ * shard's slice (at shard * xlen / nshards) filled and the others zero, so an in-place all-gather
+ * (madipm_comm_allgather, ncclAllGather) or a sum all-reduce of the whole buffer completes it.
+ * Phase 3 scatters the other shards' slices into x (xbuf = NULL, xlen = 0).
  * Shards must be created with the same pattern and options; every shard computes the same cut. */
 int madipm_ldl_analyze_shard(int32_t n, const int64_t* colptr, const int32_t* rowval, const madipm_ldl_opts* opts,
                              int32_t nshards, int32_t shard, const int32_t* user_perm, madipm_ldl_t* out);
 int madipm_ldl_factorize_phase(madipm_ldl_t ls, int32_t phase /* 1 | 2 */, const double* d_nzval,
                                madipm_stream_t stream, double** xbuf, int64_t* xlen);
-int madipm_ldl_solve_phase(madipm_ldl_t ls, int32_t phase /* 1 | 2 */, double* d_x, madipm_stream_t stream,
+int madipm_ldl_solve_phase(madipm_ldl_t ls, int32_t phase /* 1 | 2 | 3 */, double* d_x, madipm_stream_t stream,
                            double** xbuf, int64_t* xlen);
 /* owner[s] of every front (-1 top, else shard), and the partition's cost model totals */
 int madipm_ldl_shard_info(madipm_ldl_t ls, int32_t* owner, double* top_cost, double* shard_cost_max,
@@ -145,6 +153,9 @@ typedef int (*madipm_allreduce_fn)(double* host_buf, int64_t n, void* ctx);
 int madipm_comm_create_host(int32_t nranks, int32_t rank, madipm_allreduce_fn fn, void* ctx, madipm_comm_t* out);
 /* in-place fp64 sum over the communicator's ranks, ordered on `stream` */
 int madipm_comm_allreduce(madipm_comm_t comm, double* d_buf, int64_t n, madipm_stream_t stream);
+/* in-place all-gather of nranks slices of nper doubles (rank r's slice at d_buf + r * nper, the other
+ * slices zero on entry; a host-staged communicator sums the whole buffer), ordered on `stream` */
+int madipm_comm_allgather(madipm_comm_t comm, double* d_buf, int64_t nper, madipm_stream_t stream);
 void madipm_comm_destroy(madipm_comm_t comm);
 
 /* Live per-kernel timing (no reference counterpart; measurement for bench.py's roofline).

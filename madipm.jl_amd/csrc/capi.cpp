@@ -160,6 +160,7 @@ static void fill_info(const SymbolicPlan& p, const LinSolver* ls, madipm_ldl_inf
   info->fold_leaves = (int32_t)p.mc_list.size();
   info->xch_fact = ls ? ls->xch_fact() : 0;
   info->xch_solve = ls ? ls->xch_solve() : 0;
+  info->xch_gather = ls ? ls->xch_gather() : 0;
 }
 
 int madipm_symbolic_info(madipm_symbolic_t sym, madipm_ldl_info* info) {
@@ -255,16 +256,20 @@ int madipm_ldl_factorize_phase(madipm_ldl_t ls, int32_t phase, const double* d_n
 int madipm_ldl_solve_phase(madipm_ldl_t ls, int32_t phase, double* d_x, madipm_stream_t stream, double** xbuf,
                            int64_t* xlen) {
   MADIPM_API_BEGIN
-  MADIPM_REQUIRE(ls && ls->own && (phase == 1 || phase == 2) && d_x, "bad argument");
+  MADIPM_REQUIRE(ls && ls->own && phase >= 1 && phase <= 3 && d_x, "bad argument");
   hipStream_t st = (hipStream_t)stream;
   if (phase == 1) {
     ls->s->solve_phase1(d_x, st);
     if (xbuf) *xbuf = ls->s->solve_xbuf();
     if (xlen) *xlen = ls->s->solve_xlen();
-  } else {
+  } else if (phase == 2) {
     ls->s->solve_phase2(d_x, st);
-    if (xbuf) *xbuf = d_x;
-    if (xlen) *xlen = ls->s->sharded() ? ls->s->n() : 0;
+    if (xbuf) *xbuf = ls->s->solve_gbuf();
+    if (xlen) *xlen = ls->s->xch_gather();
+  } else {
+    ls->s->solve_phase3(d_x, st);
+    if (xbuf) *xbuf = nullptr;
+    if (xlen) *xlen = 0;
   }
   return 0;
   MADIPM_API_END
@@ -324,6 +329,14 @@ int madipm_comm_allreduce(madipm_comm_t c, double* d_buf, int64_t n, madipm_stre
   MADIPM_API_BEGIN
   MADIPM_REQUIRE(c && (d_buf || n == 0), "null argument");
   c->c->allreduce_sum(d_buf, n, (hipStream_t)stream);
+  return 0;
+  MADIPM_API_END
+}
+
+int madipm_comm_allgather(madipm_comm_t c, double* d_buf, int64_t nper, madipm_stream_t stream) {
+  MADIPM_API_BEGIN
+  MADIPM_REQUIRE(c && (d_buf || nper == 0) && nper >= 0, "null argument");
+  c->c->allgather_inplace(d_buf, nper, (hipStream_t)stream);
   return 0;
   MADIPM_API_END
 }

@@ -1,7 +1,8 @@
 // RCCL communicator for the sharded factorisation (SURVEY §8 e): one process per GPU, one
 // communicator per solver, every collective an in-place fp64 sum ordered on the solver's stream
 // (no host synchronisation).  Over xGMI the ring all-reduce of the top fronts is per-link bound;
-// the payload per factorisation is sum(top r^2) doubles and per solve sum(top r) + n doubles.
+// the payload per factorisation is sum(top r (r+1)/2) doubles, per solve an all-reduce of sum(top r)
+// doubles and an in-place all-gather of the shards' subtree solution slices (n - top columns).
 #include <rccl/rccl.h>
 
 #include <cstring>
@@ -37,6 +38,11 @@ struct RcclComm final : Comm {
   void allreduce_sum(double* buf, int64_t n, hipStream_t s) override {
     if (n <= 0) return;
     MADIPM_NCCL(ncclAllReduce(buf, buf, (size_t)n, ncclDouble, ncclSum, c, s));
+  }
+  // in place: rank r's slice already sits at buf + r nper (ring: (size-1) nper doubles per link)
+  void allgather_inplace(double* buf, int64_t nper, hipStream_t s) override {
+    if (nper <= 0) return;
+    MADIPM_NCCL(ncclAllGather(buf + (int64_t)rank * nper, buf, (size_t)nper, ncclDouble, c, s));
   }
 };
 

@@ -3081,6 +3081,24 @@ __global__ __launch_bounds__(NT) void k_local_allreduce(BufList B, int nbuf, int
   }
 }
 
+// Sharded solve, solution exchange: slice `me` of g <- this shard's subtree x (caller positions
+// gidx), every other slice <- 0 (so that a sum all-reduce can stand in for the all-gather) ...
+__global__ __launch_bounds__(NT) void k_gather_pack(const int32_t* gidx, int64_t n, int64_t per, int me,
+                                                    const double* b, double* g) {
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+    const int32_t p = gidx[i];
+    g[i] = (i / per == me && p >= 0) ? b[p] : 0.0;
+  }
+}
+// ... and after the gather, the other shards' x into the caller's vector
+__global__ __launch_bounds__(NT) void k_gather_scatter(const int32_t* gidx, int64_t n, int64_t per, int me,
+                                                       const double* g, double* b) {
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+    const int32_t p = gidx[i];
+    if (i / per != me && p >= 0) b[p] = g[i];
+  }
+}
+
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 }  // namespace
@@ -3179,12 +3197,25 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   {
     std::vector<int64_t> xo(std::max(ns, 1), -1);
     std::vector<uint8_t> wo(std::max(ns, 1), 1), cm(std::max(S.N, 1), 1);
-    if (S.nshards > 1)
+    // solution exchange: every shard writes the top x it computes redundantly; the subtree x are
+    // all-gathered by shard slices (the partition is shard-independent, so every shard knows them all)
+    std::vector<int32_t> gi;
+    if (S.nshards > 1) {
+      std::vector<std::vector<int32_t>> own(S.nshards);
       for (int s = 0; s < ns; ++s) {
         xo[s] = S.xoff[s];
-        wo[s] = S.top(s) ? (S.shard == 0) : 1;
-        for (int j = S.first[s]; j < S.first[s + 1]; ++j) cm[j] = S.top(s) ? 2 : (S.mine(s) ? 1 : 0);
+        for (int j = S.first[s]; j < S.first[s + 1]; ++j) {
+          cm[j] = S.top(s) ? 2 : (S.mine(s) ? 1 : 0);
+          if (!S.top(s)) own[S.owner[s]].push_back(S.perm[j]);
+        }
       }
+      for (const auto& o : own) gper_ = std::max<int64_t>(gper_, (int64_t)o.size());
+      gper_ = std::max<int64_t>(gper_, 1);
+      gi.assign((size_t)(S.nshards * gper_), -1);
+      for (int q = 0; q < S.nshards; ++q) std::copy(own[q].begin(), own[q].end(), gi.begin() + q * gper_);
+    }
+    gidx_.upload(gi.empty() ? std::vector<int32_t>{-1} : gi);
+    gsol_.alloc(std::max<int64_t>(S.nshards * gper_, 1));
     xoff_.upload(xo);
     wout_.upload(wo);
     colmask_.upload(cm);
@@ -4307,14 +4338,25 @@ void LDLSolver::solve_phase1(double* b, hipStream_t s) {
 }
 
 // Phase 2 (sharded): after the all-reduce of solve_xbuf(): top forward + backward (redundant on every
-// shard), then this shard's subtrees backward.  b is zeroed first; each x lands in b exactly once over
-// the shards (top x on shard 0 only), so an all-reduce of b completes the solution.
+// shard, which each write the top x to b), then this shard's subtrees backward, and this shard's
+// subtree x packed into its slice of solve_gbuf() (other slices zeroed) for the all-gather.
 void LDLSolver::solve_phase2(double* b, hipStream_t s) {
   if (S_.N == 0 || !sharded()) return;
-  MADIPM_HIP(hipMemsetAsync(b, 0, sizeof(double) * S_.N, s));
   fwd_levels(slev2_, 1, b, s);
   bwd_levels(slev2_, 1, b, s);
   bwd_levels(slev1_, 0, b, s);
+  const int64_t n = S_.nshards * gper_;
+  k_gather_pack<<<(unsigned)std::min<int64_t>(1024, cdiv(n, NT)), NT, 0, s>>>(gidx_, n, gper_, S_.shard, b, gsol_);
+  MADIPM_HIP(hipGetLastError());
+}
+
+// Phase 3 (sharded): after the all-gather of solve_gbuf(): the other shards' subtree x into b (every
+// entry of b is then this solve's x: top and own entries from phase 2, the rest from the gather).
+void LDLSolver::solve_phase3(double* b, hipStream_t s) {
+  if (S_.N == 0 || !sharded()) return;
+  const int64_t n = S_.nshards * gper_;
+  k_gather_scatter<<<(unsigned)std::min<int64_t>(1024, cdiv(n, NT)), NT, 0, s>>>(gidx_, n, gper_, S_.shard, gsol_,
+                                                                                  b);
   MADIPM_HIP(hipGetLastError());
 }
 
@@ -4322,9 +4364,11 @@ void LDLSolver::solve_async(double* b, hipStream_t s) {
   solve_phase1(b, s);
   if (!sharded() || S_.N == 0) return;
   MADIPM_REQUIRE(comm_ != nullptr, "sharded LDL^T without a communicator");
+  MADIPM_REQUIRE(comm_->size == S_.nshards && comm_->rank == S_.shard, "communicator does not match the shards");
   comm_->allreduce_sum(solve_xbuf(), solve_xlen(), s);
   solve_phase2(b, s);
-  comm_->allreduce_sum(b, S_.N, s);
+  comm_->allgather_inplace(solve_gbuf(), gper_, s);
+  solve_phase3(b, s);
 }
 
 // ------------------------------------------------------------------ ShardGroup (P shards, one device)
@@ -4384,7 +4428,10 @@ void ShardGroup::solve_async(double* b, hipStream_t s) {
   for (auto& h : sh_) xb.push_back(h->solve_xbuf());
   local_allreduce(xb.data(), P, sh_[0]->solve_xlen(), s);
   for (int r = 0; r < P; ++r) sh_[r]->solve_phase2(rhs[r], s);
-  local_allreduce(rhs.data(), P, n, s);
+  std::vector<double*> gb;
+  for (auto& h : sh_) gb.push_back(h->solve_gbuf());
+  local_allreduce(gb.data(), P, P * sh_[0]->solve_gper(), s);  // the gather (slices zero elsewhere)
+  sh_[0]->solve_phase3(b, s);  // the other shards' copies are scratch
 }
 
 }  // namespace madipm

@@ -127,6 +127,10 @@ struct Comm {
   int rank = 0, size = 1;
   virtual ~Comm() = default;
   virtual void allreduce_sum(double* buf, int64_t n, hipStream_t s) = 0;
+  // In-place all-gather of `size` slices of nper doubles: rank q's slice is buf[q nper, (q+1) nper)
+  // and the other slices are zero on entry, so a sum all-reduce of the whole buffer is a valid (twice
+  // as heavy) implementation — the default, for communicators without a gather (HostComm).
+  virtual void allgather_inplace(double* buf, int64_t nper, hipStream_t s) { allreduce_sum(buf, nper * size, s); }
 };
 Comm* make_rccl_comm(int nranks, int rank, const void* unique_id /* 128 bytes */);
 void rccl_unique_id(void* out /* 128 bytes */);
@@ -152,9 +156,11 @@ class LinSolver {
   virtual void set_timing(unsigned mask) = 0;
   virtual void kernel_stats(KernelStat out[]) = 0;
   virtual int n() const = 0;
-  // doubles all-reduced per factorisation / per solve (0 unsharded)
+  // doubles all-reduced per factorisation / per solve, and all-gathered per solve (the whole
+  // buffer, nshards slices) — 0 unsharded
   virtual int64_t xch_fact() const { return 0; }
   virtual int64_t xch_solve() const { return 0; }
+  virtual int64_t xch_gather() const { return 0; }
   // seconds of device time spent in factorisations so far (synchronises s; cnt.linear_solver_time)
   virtual double fact_seconds(hipStream_t s) = 0;
   bool spd = false;  // Cholesky semantics: any non-positive pivot fails (normal equations)
@@ -187,19 +193,25 @@ class LDLSolver : public LinSolver {
   // Phases of a sharded factorisation / solve, for callers that run their own collective
   // (ShardGroup below, or a host binding with its own RCCL communicator):
   //   factorize: fact_phase1; all-reduce fact_xbuf(); fact_phase2
-  //   solve:     solve_phase1; all-reduce solve_xbuf(); solve_phase2; all-reduce b (n entries)
+  //   solve:     solve_phase1; all-reduce solve_xbuf(); solve_phase2; all-gather solve_gbuf()
+  //              (nshards slices of solve_gper(); this shard's slice filled, the others zero);
+  //              solve_phase3
   void fact_phase1(const double* Kx, hipStream_t s);
   void count_inertia(hipStream_t s) override;  // lazy_inertia: the counts of the current factor
   void fact_phase2(hipStream_t s);
   void solve_phase1(double* b, hipStream_t s);
   void solve_phase2(double* b, hipStream_t s);
+  void solve_phase3(double* b, hipStream_t s);
   double* fact_xbuf() const { return xpack_.p; }  // the top fronts' lower triangles + status slots
   int64_t fact_xlen() const { return S_.nshards > 1 ? xpack_tri_ + 4 * S_.nshards : 0; }
   double* solve_xbuf() const { return xch_.p; }
   int64_t solve_xlen() const { return S_.nshards > 1 ? S_.xlen : 0; }
+  double* solve_gbuf() const { return gsol_.p; }
+  int64_t solve_gper() const { return gper_; }  // doubles per shard slice of solve_gbuf()
   bool sharded() const { return S_.nshards > 1; }
   int64_t xch_fact() const override { return fact_xlen(); }
-  int64_t xch_solve() const override { return sharded() ? solve_xlen() + S_.N : 0; }
+  int64_t xch_solve() const override { return sharded() ? solve_xlen() : 0; }
+  int64_t xch_gather() const override { return sharded() ? S_.nshards * gper_ : 0; }
   double fact_seconds(hipStream_t s) override;
 
   const SymbolicPlan& plan() const override { return S_; }
@@ -314,6 +326,11 @@ class LDLSolver : public LinSolver {
   int ntopcol_ = 0;
   int64_t xpack_tri_ = 0;
   DBuf<uint8_t> wout_, colmask_;
+  // sharded solve: caller positions of every shard's subtree columns, nshards slices of gper_
+  // (padding -1), and the gathered solution slices
+  DBuf<int32_t> gidx_;
+  DBuf<double> gsol_;
+  int64_t gper_ = 0;
   DBuf<int32_t> tasks_, flags_, flag_off_, counters_, bp_off_;
   DBuf<double> bpart_;
   int epoch_ = 0;
@@ -364,6 +381,7 @@ class ShardGroup : public LinSolver {
   int n() const override { return sh_[0]->n(); }
   int64_t xch_fact() const override { return sh_[0]->xch_fact(); }
   int64_t xch_solve() const override { return sh_[0]->xch_solve(); }
+  int64_t xch_gather() const override { return sh_[0]->xch_gather(); }
   double fact_seconds(hipStream_t s) override { return sh_[0]->fact_seconds(s); }
   LDLSolver& shard(int r) { return *sh_[r]; }
   int nshards() const { return (int)sh_.size(); }

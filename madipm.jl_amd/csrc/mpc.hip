@@ -1111,7 +1111,7 @@ MPCSolver::~MPCSolver() {
 
 int MPCSolver::blocks(int64_t n) const {
   int64_t b = (n + NT - 1) / NT;
-  return (int)std::max<int64_t>(1, std::min<int64_t>(MAXB, b));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(maxb_, b));
 }
 
 // GROUP_LOOP SpMV kernels: one row per lane group (spmv_g_ lanes), so a group walks one row instead
@@ -1394,6 +1394,7 @@ void MPCSolver::setup_host(const madipm_qp& q) {
   std::vector<double> Kv;
   csr_from_coo(n + m, kc, kr, kv, Kcp, Kri, Kv);
   nnzK_ = (int64_t)Kri.size();
+  if (const char* e = std::getenv("MADIPM_PART_BLOCKS")) maxb_ = std::max(1, std::min(MAXB, std::atoi(e)));
   {  // SpMV lane-group width: ~2 entries per lane on an average row of [H A^T; A]
     const double avg = (double)(Hci.size() + 2 * Jci.size()) / std::max(1, n + m);
     spmv_g_ = 4;

@@ -107,6 +107,7 @@ class MPCSolver {
   // KKT formulation (0 K2, 1 K2.5, 2 normal equations)
   int kkt_ = 0;
   int spmv_g_ = 8;  // lanes per row in the SpMV kernels
+  int maxb_ = 2048;  // partial-reduction blocks per producer launch (<= MAXB; MADIPM_PART_BLOCKS)
   DBuf<double> sk_, K0_, Dinv_, bufm_, Cx_;
   DBuf<int32_t> Krow_, Kcol_, cprod_;
   DBuf<int64_t> cpp_;

@@ -38,7 +38,7 @@ class LDLInfo(C.Structure):
                 ("max_front", C.c_int32), ("nbig", C.c_int32), ("arena_bytes", C.c_int64),
                 ("lb_groups", C.c_int32), ("lb_members", C.c_int32),
                 ("fold_fronts", C.c_int32), ("fold_leaves", C.c_int32),
-                ("xch_fact", C.c_int64), ("xch_solve", C.c_int64)]
+                ("xch_fact", C.c_int64), ("xch_solve", C.c_int64), ("xch_gather", C.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -100,6 +100,7 @@ _sig("madipm_comm_unique_id", C.c_int, [C.c_char_p])
 _sig("madipm_comm_create", C.c_int, [C.c_int32, C.c_int32, C.c_char_p, C.POINTER(vp)])
 _sig("madipm_comm_destroy", None, [vp])
 _sig("madipm_comm_allreduce", C.c_int, [vp, vp, C.c_int64, vp])
+_sig("madipm_comm_allgather", C.c_int, [vp, vp, C.c_int64, vp])
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, f64p, C.c_int64, vp)
 _sig("madipm_comm_create_host", C.c_int, [C.c_int32, C.c_int32, ALLREDUCE_FN, vp, C.POINTER(vp)])
 

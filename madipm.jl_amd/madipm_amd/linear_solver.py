@@ -101,7 +101,9 @@ class HIPLDLSolver:
         return xb.value, xl.value
 
     def solve_phase(self, phase, x, stream=None):
-        """phase 1 -> (ptr, len) to all-reduce; phase 2 -> (x ptr, n): all-reduce x to finish."""
+        """phase 1 -> (ptr, len) to all-reduce; phase 2 -> (ptr, len) of the gather buffer (nshards
+        slices, this shard's filled, the others zero): all-gather it in place (or sum all-reduce it);
+        phase 3 scatters the gathered slices into x -> (0, 0)."""
         xb, xl = L.vp(), C.c_int64()
         L.check(L.lib.madipm_ldl_solve_phase(self.h, int(phase), C.c_void_p(x.data_ptr()), C.c_void_p(_stream(stream)),
                                              C.byref(xb), C.byref(xl)), "madipm_ldl_solve_phase")

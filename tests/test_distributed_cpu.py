@@ -55,6 +55,8 @@ def test_collective_volume():
     import bench
     assert bench.collective_volume({"xch_fact": 0, "xch_solve": 0}, []) is None
     warm = [{"name": "k_fact_tree", "launches": 3}, {"name": "k_bwd_tree", "launches": 9}]
-    v = bench.collective_volume({"xch_fact": 1000, "xch_solve": 300}, warm)
-    assert v["solves_per_fact"] == 3 and v["allreduces_per_iter"] == 7
-    assert v["fact_bytes"] == 8000 and v["solve_bytes"] == 2400 and v["bytes_per_iter"] == 8 * (1000 + 3 * 300)
+    v = bench.collective_volume({"xch_fact": 1000, "xch_solve": 300, "xch_gather": 500}, warm, world=2)
+    assert v["solves_per_fact"] == 3 and v["collectives_per_iter"] == 7
+    assert v["fact_bytes"] == 8000 and v["solve_bytes"] == 6400 and v["bytes_per_iter"] == 8 * (1000 + 3 * 800)
+    # ring model, P = 2: all-reduce m -> m doubles sent per rank, all-gather G -> G / 2
+    assert v["wire_bytes_per_rank_per_iter"] == pytest.approx(8 * (1000 + 3 * (300 + 250)))

@@ -75,7 +75,11 @@ def test_phase_protocol_with_separate_shards():
     _, _, nrows = Symbolic(N, Lw.indptr, Lw.indices, default_ldl_opts(), nshards=P, shard=0).supernodes()
     r = nrows[sh[0].shard_info()["owner"] == -1].astype(np.int64)
     assert bufs[0][1] == (r * (r + 1) // 2).sum() + 4 * P == sh[0].info()["xch_fact"]
-    assert sh[0].info()["xch_solve"] > N
+    # per solve: the top fronts' forward right-hand sides (all-reduce) + the subtree solution slices
+    # (all-gather, P slices of the largest shard's column count): less than n + top rows together
+    ntop = int(r.sum())
+    assert sh[0].info()["xch_solve"] == ntop
+    assert N - ntop <= sh[0].info()["xch_gather"] <= P * (N - ntop)
     local_allreduce([p for p, _ in bufs], bufs[0][1])
     for s in sh:
         s.factorize_phase(2)
@@ -84,7 +88,10 @@ def test_phase_protocol_with_separate_shards():
     bufs = [s.solve_phase(1, x) for s, x in zip(sh, xs)]
     local_allreduce([p for p, _ in bufs], bufs[0][1])
     bufs = [s.solve_phase(2, x) for s, x in zip(sh, xs)]
-    local_allreduce([p for p, _ in bufs], N)
+    assert bufs[0][1] == sh[0].info()["xch_gather"]
+    local_allreduce([p for p, _ in bufs], bufs[0][1])  # the all-gather (other slices are zero)
+    for s, x in zip(sh, xs):
+        assert s.solve_phase(3, x) == (None, 0)
     torch.cuda.synchronize()
     for x in xs:
         assert np.max(np.abs(x.cpu().numpy() - x0)) <= 1e-12 * np.max(np.abs(x0))
