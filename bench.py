@@ -170,7 +170,7 @@ def roofline(stats: list, dominant: str):
         ach, peak, unit = flops / avg_s / 1e12, PEAK_F64_TFS, "TFLOP/s"
     else:
         ach, peak, unit = nbytes / avg_s / 1e9, PEAK_HBM_GBS, "GB/s"
-    traffic, src = None, None
+    traffic, src, traffic_lo = None, None, None
     def _rv(path):  # r<round>_v<n>: numeric order (r2_v10 after r2_v3)
         m = re.search(r"r(\d+)_v(\d+)", os.path.basename(path))
         return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
@@ -180,8 +180,11 @@ def roofline(stats: list, dominant: str):
         ent = json.load(open(pmc[-1]))["kernels"].get(dominant)
         if ent:
             traffic, src = ent["hbm_bytes_per_launch"], os.path.relpath(pmc[-1], ROOT)
+            traffic_lo = ent.get("hbm_bytes_lo_per_launch")
     return {"bound": "mfma" if mfma else "hbm", "achieved": ach, "peak": peak, "unit": unit, "frac": ach / peak,
-            "traffic": traffic, "traffic_source": src, "kernel": dominant, "launches": k["launches"],
+            "traffic": traffic, "traffic_lo": traffic_lo, "traffic_source": src,
+            "traffic_definition": "PMC bytes per launch: 2 FETCH_SIZE + WRITE_SIZE (upper bound; traffic_lo = "
+                                  "FETCH_SIZE + WRITE_SIZE, exact for 8-B gathers; profiles/r3_e1_fetch_calib.txt)", "kernel": dominant, "launches": k["launches"],
             "avg_launch_us": avg_s * 1e6, "alg_bytes_per_launch": nbytes, "alg_flops_per_launch": flops,
             "alg_bytes_definition": "SURVEY 8(d): 8 nnzL + 12 nnzK of the columns the launch factorises",
             "staging_bytes_per_launch": staging}

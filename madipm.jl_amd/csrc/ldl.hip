@@ -27,6 +27,13 @@ namespace {
 constexpr int NT = 256;
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
+// Pin loaded values (an empty asm that "modifies" them) so the compiler keeps clamped loads
+// unconditional instead of sinking them into the branch of their conditional use.  The asm needs the
+// value, so it waits for the load: pin a batch only after ALL its loads are issued (pinning each load
+// right after it serialised the LDS loads of the MFMA loops on the LDS latency).
+#define LDL_PIN(x) asm volatile("" : "+v"(x))
+#define LDL_PIN4(a) asm volatile("" : "+v"((a)[0]), "+v"((a)[1]), "+v"((a)[2]), "+v"((a)[3]))
+
 __device__ __forceinline__ bool bad_pivot(double d, double tol) { return !(fabs(d) > tol) || isinf(d); }
 
 // wave-synchronous LDS hand-off: LDS ops of one wave complete in order; keep the compiler from
@@ -715,13 +722,17 @@ __device__ __forceinline__ void factor16s(double* A, int r, int ld, int k0, int 
                                           int lane) {
   const int i = lane & 15, g = lane >> 4;
   const int ic = min(i, kw - 1);
-  double a[4], x[4];
+  double a[4], x[4], v[4];
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
     const int j = 4 * g + m, jc = min(j, kw - 1);
-    double v = A[fidx<PK>(k0 + max(ic, jc), k0 + min(ic, jc), r, ld)];  // upper part mirrored (never read)
-    asm volatile("" : "+v"(v));  // keep the load unconditional
-    a[m] = (i < kw && j < kw) ? v : (i == j ? 1.0 : 0.0);
+    v[m] = A[fidx<PK>(k0 + max(ic, jc), k0 + min(ic, jc), r, ld)];  // upper part mirrored (never read)
+  }
+  LDL_PIN4(v);  // keep the loads unconditional (pinned after all four are issued)
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int j = 4 * g + m;
+    a[m] = (i < kw && j < kw) ? v[m] : (i == j ? 1.0 : 0.0);
     x[m] = (i == j) ? 1.0 : 0.0;
   }
   double* col = cb;        // col[16 t + i] = A(i, t) at step t
@@ -756,6 +767,86 @@ __device__ __forceinline__ void factor16s(double* A, int r, int ld, int k0, int 
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
     const int j = 4 * g + m;
+    if (j < i && i < kw) A[fidx<PK>(k0 + i, k0 + j, r, ld)] = a[m];
+    MK[j * LDM + i] = (j <= i) ? x[m] / dmine : 0.0;
+  }
+  if (g == 0 && i < kw) Dl[k0 + i] = dmine;
+  wave_sync();
+}
+
+// Register-resident variant of factor16s (same interface and output): no LDS hand-off per step.
+// Lane (i = lane & 15, g = lane >> 4) holds A(i, j) and X(i, j) for the four columns j = 4m + g in
+// a[m], x[m]: column t lives in register t >> 2 of row group t & 3.  Step t:
+//   d_t = A(t, t): v_readlane (wave-uniform);
+//   A(i, t) to every row group: v_permlane16_swap + v_permlane32_swap (gfx950) of row group t & 3;
+//   A(t, j), X(t, j) of the lane's columns: DPP row_newbcast:t inside the lane's 16-lane row.
+// Every row i > t is updated with the mirrored row t (A(t, j), j > t) where factor16s reads column t
+// (A(j, t)): both hold the same Schur complement entry, rounded along mirrored paths, so the two
+// variants agree to rounding (not bitwise).  l = A(i, t) / d_t is the same IEEE quotient.
+template <int T>
+__device__ __forceinline__ double dpp_row_bcast(double v) {  // lane T of every 16-lane row, to the row
+  int lo = __double2loint(v), hi = __double2hiint(v);
+  lo = __builtin_amdgcn_update_dpp(0, lo, 0x150 + T, 0xf, 0xf, false);
+  hi = __builtin_amdgcn_update_dpp(0, hi, 0x150 + T, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+template <int G>
+__device__ __forceinline__ int xrow_bcast32(int v) {  // row G (16 lanes) of the wave, to every row
+  const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);  // [r0 r0 r2 r2] | [r1 r1 r3 r3]
+  const int y = (G & 1) ? (int)p[1] : (int)p[0];
+  const auto q = __builtin_amdgcn_permlane32_swap(y, y, false, false);  // [rA rA rA rA] | [rB rB rB rB]
+  return (G & 2) ? (int)q[1] : (int)q[0];
+}
+template <int G>
+__device__ __forceinline__ double xrow_bcast(double v) {
+  return __hiloint2double(xrow_bcast32<G>(__double2hiint(v)), xrow_bcast32<G>(__double2loint(v)));
+}
+template <int T>
+__device__ __forceinline__ void f16r_step(double (&a)[4], double (&x)[4], double& dmine, int i, int g) {
+  constexpr int gt = T & 3, mt = T >> 2;
+  const double dt = readlane_f64(a[mt], T + 16 * gt);
+  const double ci = xrow_bcast<gt>(a[mt]);
+  const double li = (i > T) ? ci / dt : 0.0;  // IEEE quotient
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int j = 4 * m + g;
+    const double sa = dpp_row_bcast<T>(a[m]);  // A(t, j)
+    const double sx = dpp_row_bcast<T>(x[m]);  // X(t, j)
+    a[m] = (j > T) ? fma(-li, sa, a[m]) : a[m];
+    x[m] = (j <= T) ? fma(-li, sx, x[m]) : x[m];
+  }
+  if (i == T) dmine = dt;
+  if (g == gt && i > T) a[mt] = li;
+}
+template <int T>
+__device__ __forceinline__ void f16r_steps(double (&a)[4], double (&x)[4], double& dmine, int i, int g) {
+  if constexpr (T < 16) {
+    f16r_step<T>(a, x, dmine, i, g);
+    f16r_steps<T + 1>(a, x, dmine, i, g);
+  }
+}
+template <bool PK>
+__device__ __forceinline__ void factor16r(double* A, int r, int ld, int k0, int kw, double* Dl, double* MK, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  const int ic = min(i, kw - 1);
+  double a[4], x[4], v[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int j = 4 * m + g, jc = min(j, kw - 1);
+    v[m] = A[fidx<PK>(k0 + max(ic, jc), k0 + min(ic, jc), r, ld)];  // mirrored: the full symmetric block
+  }
+  LDL_PIN4(v);
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int j = 4 * m + g;
+    a[m] = (i < kw && j < kw) ? v[m] : (i == j ? 1.0 : 0.0);
+    x[m] = (i == j) ? 1.0 : 0.0;
+  }
+  double dmine = 1.0;
+  f16r_steps<0>(a, x, dmine, i, g);
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int j = 4 * m + g;
     if (j < i && i < kw) A[fidx<PK>(k0 + i, k0 + j, r, ld)] = a[m];
     MK[j * LDM + i] = (j <= i) ? x[m] / dmine : 0.0;
   }
@@ -818,7 +909,6 @@ __device__ __forceinline__ void publish_sc1(int32_t* f, int epoch) {  // the sto
 // with its own wait), a wave updates a STRIP of up to four 16 x 16 tiles sharing the (L_I D)
 // operand (four independent accumulator chains back to back), and the next pivot block is
 // factorised by one wave while the other three finish the trailing update (lookahead).
-#define LDL_PIN(x) asm volatile("" : "+v"(x))
 
 // L_R = A[R, k0:k0+kw] M_K for the 16-row blocks b = b0, b0 + bstep, ... below the pivots
 template <bool PK>
@@ -837,8 +927,9 @@ __device__ __forceinline__ void panel_blocks(double* A, int r, int ld, int k0, i
       for (int ks = 0; ks < 4; ++ks) {
         const int row = min(R0 + 16 * (b + u * bstep) + il, r - 1);
         av[u][ks] = A[fidx<PK>(row, k0 + min(4 * ks + kl, kw - 1), r, ld)];
-        LDL_PIN(av[u][ks]);
       }
+    LDL_PIN4(av[0]);
+    LDL_PIN4(av[1]);
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -872,12 +963,10 @@ __device__ __forceinline__ void trail_strip(double* A, int r, int ld, int k0, in
   for (int ks = 0; ks < 4; ++ks) {
     const int kc = k0 + min(4 * ks + kl, kw - 1);
     bv[ks] = A[fidx<PK>(ri, kc, r, ld)];
-    LDL_PIN(bv[ks]);
 #pragma unroll
     for (int t = 0; t < NS; ++t) {
       const int rj = min(R0 + 16 * (J0 + t) + il, r - 1);
       av[t][ks] = A[fidx<PK>(rj, kc, r, ld)];
-      LDL_PIN(av[t][ks]);
     }
   }
 #pragma unroll
@@ -886,8 +975,13 @@ __device__ __forceinline__ void trail_strip(double* A, int r, int ld, int k0, in
     for (int g = 0; g < 4; ++g) {
       const int j = min(R0 + 16 * (J0 + t) + kl + 4 * g, r - 1);
       cv[t][g] = A[fidx<PK>(max(ri, j), min(ri, j), r, ld)];
-      LDL_PIN(cv[t][g]);
     }
+  // pins in issue order, after every load (the MFMA operands first: their waits come first)
+  LDL_PIN4(bv);
+#pragma unroll
+  for (int t = 0; t < NS; ++t) LDL_PIN4(av[t]);
+#pragma unroll
+  for (int t = 0; t < NS; ++t) LDL_PIN4(cv[t]);
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) bv[ks] *= dk[ks];  // dk = 0 past kw
   dbl4 acc[NS];
@@ -947,30 +1041,31 @@ __device__ __forceinline__ void schur_strip(double* A, int r, int ld, int w, con
   dbl4 acc[NS];
 #pragma unroll
   for (int t = 0; t < NS; ++t) acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
-  double bv[4], av[NS][4];
+  // raw operands of the next 16-pivot chunk: issued one chunk ahead, pinned (waited for) only at the
+  // top of the iteration that consumes them, i.e. after the previous chunk's MFMAs
+  double bn[4], dn[4], an[NS][4];
   auto load = [&](int k0) {
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const int kc = min(k0 + 4 * ks + kl, w - 1);
-      const double d = Dl[kc];
-      double b = A[fidx<PK>(ri, kc, r, ld)];
-      LDL_PIN(b);
-      bv[ks] = (k0 + 4 * ks + kl < w) ? b * d : 0.0;
+      dn[ks] = Dl[kc];
+      bn[ks] = A[fidx<PK>(ri, kc, r, ld)];
 #pragma unroll
-      for (int t = 0; t < NS; ++t) {
-        av[t][ks] = A[fidx<PK>(rj[t], kc, r, ld)];
-        LDL_PIN(av[t][ks]);
-      }
+      for (int t = 0; t < NS; ++t) an[t][ks] = A[fidx<PK>(rj[t], kc, r, ld)];
     }
   };
   load(0);
   for (int k0 = 0; k0 < w; k0 += 16) {
+    LDL_PIN4(dn);
+    LDL_PIN4(bn);
+#pragma unroll
+    for (int t = 0; t < NS; ++t) LDL_PIN4(an[t]);
     double b2[4], a2[NS][4];
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      b2[ks] = bv[ks];
+      b2[ks] = (k0 + 4 * ks + kl < w) ? bn[ks] * dn[ks] : 0.0;
 #pragma unroll
-      for (int t = 0; t < NS; ++t) a2[t][ks] = av[t][ks];
+      for (int t = 0; t < NS; ++t) a2[t][ks] = an[t][ks];
     }
     if (k0 + 16 < w) load(k0 + 16);
 #pragma unroll
@@ -985,8 +1080,9 @@ __device__ __forceinline__ void schur_strip(double* A, int r, int ld, int w, con
     for (int g = 0; g < 4; ++g) {
       const int j = min(w + 16 * (J0 + t) + kl + 4 * g, r - 1);
       cv[t][g] = A[fidx<PK>(max(ri, j), min(ri, j), r, ld)];
-      LDL_PIN(cv[t][g]);
     }
+#pragma unroll
+  for (int t = 0; t < NS; ++t) LDL_PIN4(cv[t]);
 #pragma unroll
   for (int t = 0; t < NS; ++t)
 #pragma unroll
@@ -1024,8 +1120,17 @@ __device__ __forceinline__ void schur_strips(double* A, int r, int ld, int w, co
 // pt (diagnostics, MADIPM_TREE_DEBUG): thread 0 accumulates the phase times (first pivot block,
 // panels, J = 0 strips, lookahead sections, Schur pass) into pt[0..4]
 template <bool PK>
+__device__ __forceinline__ void factor16x(double* A, int r, int ld, int k0, int kw, double* Dl, double* MK, double* cb,
+                                          int lane, int f16r) {
+  if (f16r)
+    factor16r<PK>(A, r, ld, k0, kw, Dl, MK, lane);
+  else
+    factor16s<PK>(A, r, ld, k0, kw, Dl, MK, cb, lane);
+}
+
+template <bool PK>
 __device__ __forceinline__ void blocked_factor_lds(double* A, int r, int w, int ld, double* Dl, double* MK, double* cbuf,
-                                                   int defer = 0, int64_t* pt = nullptr) {
+                                                   int defer = 0, int64_t* pt = nullptr, int f16r = 0) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), nw = blockDim.x >> 6;
   const int nblk = (w + 15) >> 4;
@@ -1040,7 +1145,7 @@ __device__ __forceinline__ void blocked_factor_lds(double* A, int r, int w, int 
     }
   };
   const int64_t cyc0 = (pt && tid == 0) ? (int64_t)clock64() : 0;
-  if (wv == 0) factor16s<PK>(A, r, ld, 0, min(16, w), Dl, MK, cbuf, lane);
+  if (wv == 0) factor16x<PK>(A, r, ld, 0, min(16, w), Dl, MK, cbuf, lane, f16r);
   __syncthreads();
   stamp(0);
   const int64_t cyc1 = (pt && tid == 0) ? (int64_t)clock64() : 0;
@@ -1066,7 +1171,7 @@ __device__ __forceinline__ void blocked_factor_lds(double* A, int r, int w, int 
       // ... then one wave factorises it while the others update the rest (J >= 1)
       const int fw = (kb + 1) % nw;
       if (wv == fw)
-        factor16s<PK>(A, r, ld, R0, min(16, w - R0), Dl, MK, cbuf, lane);
+        factor16x<PK>(A, r, ld, R0, min(16, w - R0), Dl, MK, cbuf, lane, f16r);
       else
         trail_strips<PK>(A, r, ld, k0, kw, R0, nbr, 1, jhi, dk, (wv - fw + nw - 1) % nw, nw - 1, lane, jend);
     } else if (!defer) {
@@ -1098,18 +1203,27 @@ __device__ __forceinline__ void writeout_ld(const double* A, int r, int w, int l
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), nw = blockDim.x >> 6;
   // L panel (ld r; d on the diagonal, zeros above): columns dealt to waves as in writeout_u
   for (int j0 = 4 * wv; j0 < w; j0 += 4 * nw) {
-    double x[4][3];
+    double x[4][3], dd[4];
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
       const int j = min(j0 + cb, w - 1);
       const int base = PK ? ((j * (2 * r - j - 1)) >> 1) : j * ld;
-      const double d = Dl[j];
+      dd[cb] = Dl[j];
 #pragma unroll
       for (int h = 0; h < 3; ++h) {
         const int i = lane + 64 * h, ic = min(max(i, j), r - 1);
-        double a = A[base + ic];
-        asm volatile("" : "+v"(a));
-        x[cb][h] = (i > j) ? a : (i == j ? d : 0.0);
+        x[cb][h] = A[base + ic];
+      }
+    }
+    LDL_PIN4(dd);
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      asm volatile("" : "+v"(x[cb][0]), "+v"(x[cb][1]), "+v"(x[cb][2]));
+      const int j = min(j0 + cb, w - 1);
+#pragma unroll
+      for (int h = 0; h < 3; ++h) {
+        const int i = lane + 64 * h;
+        x[cb][h] = (i > j) ? x[cb][h] : (i == j ? dd[cb] : 0.0);
       }
     }
 #pragma unroll
@@ -1154,9 +1268,12 @@ __device__ __forceinline__ void writeout_u_cols(const double* A, int r, int w, i
       for (int h = 0; h < NH; ++h) {
         const int a = min(b + lane + 64 * h, u - 1);
         x[cb][h] = A[base + w + a];
-        asm volatile("" : "+v"(x[cb][h]));
       }
     }
+#pragma unroll
+    for (int cb = 0; cb < NC; ++cb)
+#pragma unroll
+      for (int h = 0; h < NH; ++h) LDL_PIN(x[cb][h]);
 #pragma unroll
     for (int cb = 0; cb < NC; ++cb) {
       const int b = b0 + cb;
@@ -1250,7 +1367,7 @@ __global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t*
     }
   }
   __syncthreads();
-  blocked_factor_lds<PK>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer);
+  blocked_factor_lds<PK>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer, nullptr, T.f16r);
   blocked_writeout<PK, false>(A, r, w, ld, Dl, arena + T.l_off[s], arena + T.u_off[s], T.u_ld[s], D, f0, st, tol);
 }
 
@@ -1568,7 +1685,7 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
     __syncthreads();
   }
   if (dg && tid == 0) dg[3] = wall_clock64();
-  blocked_factor_lds<PK>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer, dg ? dg + 8 : nullptr);
+  blocked_factor_lds<PK>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer, dg ? dg + 8 : nullptr, T.f16r);
   if (dg && tid == 0) dg[4] = wall_clock64();
   // the parent reads only U: publish it first, then write L and D (read by later launches)
   writeout_u<PK, true>(A, r, w, ld, arena + T.u_off[s], T.u_ld[s]);
@@ -3130,6 +3247,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   {
     const char* ev = std::getenv("MADIPM_SCHUR_DEFER");
     T_.schur_defer = (ev && ev[0] == '0') ? 0 : 1;
+    const char* e16 = std::getenv("MADIPM_F16R");  // register-resident 16-pivot block factor (factor16r)
+    T_.f16r = (e16 && e16[0] == '0') ? 0 : 1;
   }
   T_.nrows = nrows_;
   T_.row_ptr = row_ptr_;

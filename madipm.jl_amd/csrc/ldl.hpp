@@ -38,8 +38,8 @@ struct FrontTab {
   const int64_t* sv_src;
   const int32_t* bigslot;  // big front -> slot in the panel-inverse scratch (64x64 per slot)
   // sharding: top fronts start their forward solve from the exchanged vector xch[xoff[s] + i]
-  // (xoff = -1 elsewhere); wout[s] = 0 suppresses the write of x to the caller's vector (top fronts
-  // on shards != 0, so that the final all-reduce adds each x once)
+  // (xoff = -1 elsewhere); wout[s] = 0 would suppress the write of x to the caller's vector (every
+  // shard writes the top x it computes redundantly: all 1)
   const int64_t* xoff;
   const double* xch;
   const uint8_t* wout;
@@ -67,6 +67,7 @@ struct FrontTab {
   const uint2* fold_prod;
   const uint8_t* fs_img;  // 1: fscratch holds the front's LDS image (tree fronts), else ld r
   int schur_defer;  // in-LDS factorisation: update block U in one pass after the pivots (MADIPM_SCHUR_DEFER)
+  int f16r;         // 16-pivot diagonal blocks factorised in registers (factor16r; MADIPM_F16R=0: factor16s)
 };
 
 struct SolveTask {

@@ -17,6 +17,7 @@
 // 200-byte state block per iteration (published by k_publish into coherent host memory; the host
 // spins on its counter, overlapped with the factorisation and the speculated directions).
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -786,6 +787,7 @@ struct FinParams {
   int nb_eval;     // FIN_TERM: > 0 -> also finalise evaluate_model!'s objective (k_eval's nb_eval
                    // partials in slot PART_EVAL, the previous iteration's; P.c = its constant)
   LDLStatus* rs;   // != nullptr: a factorisation follows this launch (LinSolver::ext_reset)
+  int64_t* dbg = nullptr;  // diagnostics (MADIPM_FINAL_DEBUG): thread 0's wall clock at entry / reduced / end
 };
 constexpr int PART_EVAL = 6;
 
@@ -800,27 +802,32 @@ constexpr int PART_EVAL = 6;
 constexpr int NTF = 256, FPT = 8;  // threads, partial blocks per thread
 static_assert(MAXB == FPT * NTF, "k_final: eight partial rows per thread");
 
-__device__ __forceinline__ void part8(const DV& D, int k, int nb, double (&v)[FPT], double fill) {
+// A thread's partials of one slot: its FPT blocks as FPT/2 16-B loads.  The loads are unconditional
+// (every slot holds MAXB partials, stale past nb) and issued for EVERY slot of the launch before the
+// first selection (part8_sel pins its raw values, i.e. waits for them, then selects the fill past nb):
+// a predicated load compiles to a branch around the load with a wait inside, which serialised the
+// ~90 loads of the fused residual + step-test finaliser into ~90 memory latencies (14 us measured).
+typedef double2 Raw8[FPT / 2];
+__device__ __forceinline__ void part8_load(const DV& D, int k, Raw8& q) {
+  const int b0 = FPT * threadIdx.x;
+#pragma unroll
+  for (int h = 0; h < FPT; h += 2) q[h / 2] = *reinterpret_cast<const double2*>(D.part + pidx(b0 + h, k));
+}
+__device__ __forceinline__ void part8_sel(Raw8& q, int nb, double (&v)[FPT], double fill) {
+  static_assert(FPT == 8, "part8_sel pins four double2");
+  asm volatile("" : "+v"(q[0].x), "+v"(q[0].y), "+v"(q[1].x), "+v"(q[1].y), "+v"(q[2].x), "+v"(q[2].y), "+v"(q[3].x),
+               "+v"(q[3].y));
   const int b0 = FPT * threadIdx.x;
 #pragma unroll
   for (int h = 0; h < FPT; h += 2) {
-    const double2 q = (b0 + h < nb) ? *reinterpret_cast<const double2*>(D.part + pidx(b0 + h, k)) : make_double2(fill, fill);
-    v[h] = q.x;
-    v[h + 1] = (b0 + h + 1 < nb) ? q.y : fill;
+    v[h] = (b0 + h < nb) ? q[h / 2].x : fill;
+    v[h + 1] = (b0 + h + 1 < nb) ? q[h / 2].y : fill;
   }
 }
 
-// the step test's argmin over the block partials in slots base.. (FIN_ALPHA: 0, fused: PART_ALPHA);
-// every thread of the block calls it (shuffles, __syncthreads), thread 0 writes the state.  The loads
-// come first (fin_alpha_load), so that a finaliser combining several reductions has every load of the
-// thread in flight together; the reduce needs the same nb
-__device__ __forceinline__ void fin_alpha_load(const DV& D, int nb, int base, double (&pv)[4][FPT], double (&pi)[4][FPT]) {
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    part8(D, base + k, nb, pv[k], INF);
-    part8(D, base + 4 + k, nb, pi[k], -1.0);
-  }
-}
+// the step test's argmin over the block partials in slots base.. (FIN_ALPHA: 0, fused: PART_ALPHA):
+// 4 ratio slots, then 4 index slots; every thread of the block calls it (shuffles, __syncthreads),
+// thread 0 writes the state
 
 __device__ void fin_alpha(const DV& D, const FinParams& P, const double (&pv)[4][FPT], const double (&pi)[4][FPT],
                           double (&sh)[8][NTF / 64], int (&shi)[4][NTF / 64]) {
@@ -904,59 +911,65 @@ __device__ double fin_sum_slot(const double (&ev)[FPT], double (&sh)[8][NTF / 64
   return r;
 }
 
-// Combine the block partials in fixed order + scalar logic (one block of NTF threads).
+// Combine the block partials in fixed order + scalar logic (one block of NTF threads).  Instantiated
+// per (value slots NV, fused step test AL, fused objective EV) so that a thread holds exactly the
+// partials of its launch (launch_final picks the instance).
+template <int NV, bool AL, bool EV>
 __global__ __launch_bounds__(NTF) void k_final(DV D, int kind, FinParams P) {
   __shared__ double res[NPART];
   __shared__ double sh[8][NTF / 64];
   __shared__ int shi[4][NTF / 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   DevState* st = D.st;
-  if (kind == FIN_ALPHA) {
+  if (P.dbg && threadIdx.x == 0) {
+    P.dbg[0] = (int64_t)wall_clock64();
+    P.dbg[3] = kind | (AL && NV > 0 ? 16 : 0) | (EV ? 32 : 0);
+  }
+  // every load of the launch first (one memory round trip), then the selections and reductions
+  constexpr int NA = AL ? 8 : 0;
+  Raw8 q[NV > 0 ? NV : 1], aq[AL ? 8 : 1], eq[1];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) part8_load(D, k, q[k]);
+#pragma unroll
+  for (int k = 0; k < NA; ++k) part8_load(D, (NV > 0 ? PART_ALPHA : 0) + k, aq[k]);
+  if (EV) part8_load(D, PART_EVAL, eq[0]);
+  if (AL) {  // FIN_ALPHA, or FIN_RESID + the FIN_ALPHA of the k_alpha launched after the residual
+    const int nba = NV > 0 ? P.nb_alpha : P.nb;
     double apv[4][FPT], api[4][FPT];
-    fin_alpha_load(D, P.nb, 0, apv, api);
-    fin_alpha(D, P, apv, api, sh, shi);
-    return;
-  }
-  int nv = 0;
-  int ops[NPART];
-  switch (kind) {
-    case FIN_RESID: nv = 3; ops[0] = ops[1] = ops[2] = OP_MAX; break;
-    case FIN_MU_PRED:
-    case FIN_MU_FULL:
-    case FIN_MU_GONDZIO: nv = 4; for (int k = 0; k < 4; ++k) ops[k] = OP_SUM; break;
-    case FIN_EVAL: nv = 1; ops[0] = OP_SUM; break;
-    case FIN_TERM: nv = 6; ops[0] = ops[1] = ops[2] = OP_MAX; ops[3] = ops[4] = ops[5] = OP_SUM; break;
-    case FIN_ZINIT: nv = 4; for (int k = 0; k < 4; ++k) ops[k] = OP_MIN; break;
-    case FIN_ZSHIFT1: nv = 8; for (int k = 0; k < 8; ++k) ops[k] = OP_SUM; break;
-    case FIN_ZSHIFT2: nv = 1; ops[0] = OP_SUM; break;
-  }
-  // every load of the thread is issued before the first reduction (one memory round trip); every
-  // reduction here starts at 0.0 (sum, max, and min with init 0), so absent blocks load 0.0
-  double pv[8][FPT];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    if (k < nv)
-      part8(D, k, P.nb, pv[k], 0.0);
-    else
-#pragma unroll
-      for (int h = 0; h < FPT; ++h) pv[k][h] = 0.0;
-  }
-  double apv[4][FPT], api[4][FPT];
-  if (P.nb_alpha > 0) fin_alpha_load(D, P.nb_alpha, PART_ALPHA, apv, api);
-  double ev[FPT];
-  if (P.nb_eval > 0)
-    part8(D, PART_EVAL, P.nb_eval, ev, 0.0);
-  if (P.nb_alpha > 0) {  // FIN_RESID + the FIN_ALPHA of the k_alpha launched after the residual
+    for (int k = 0; k < 4; ++k) {
+      part8_sel(aq[k], nba, apv[k], INF);
+      part8_sel(aq[4 + k], nba, api[k], -1.0);
+    }
     fin_alpha(D, P, apv, api, sh, shi);
+    if (NV == 0) return;
     __syncthreads();
   }
-  if (P.nb_eval > 0) {  // FIN_TERM: the previous iteration's FIN_EVAL, deferred to this launch
+  if (EV) {  // FIN_TERM: the previous iteration's FIN_EVAL, deferred to this launch
+    double ev[FPT];
+    part8_sel(eq[0], P.nb_eval, ev, 0.0);
     const double r = fin_sum_slot(ev, sh);
     if (threadIdx.x == 0) st->obj_val = P.c + r;
   }
+  constexpr int nv = NV;
+  int ops[NPART];
+  switch (kind) {
+    case FIN_RESID: ops[0] = ops[1] = ops[2] = OP_MAX; break;
+    case FIN_MU_PRED:
+    case FIN_MU_FULL:
+    case FIN_MU_GONDZIO: for (int k = 0; k < 4; ++k) ops[k] = OP_SUM; break;
+    case FIN_EVAL: ops[0] = OP_SUM; break;
+    case FIN_TERM: ops[0] = ops[1] = ops[2] = OP_MAX; ops[3] = ops[4] = ops[5] = OP_SUM; break;
+    case FIN_ZINIT: for (int k = 0; k < 4; ++k) ops[k] = OP_MIN; break;
+    case FIN_ZSHIFT1: for (int k = 0; k < 8; ++k) ops[k] = OP_SUM; break;
+    case FIN_ZSHIFT2: ops[0] = OP_SUM; break;
+  }
+  // every reduction here starts at 0.0 (sum, max, and min with init 0), so absent blocks count 0.0
+  double pv[NV > 0 ? NV : 1][FPT];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    if (k >= nv) break;
+  for (int k = 0; k < NV; ++k) part8_sel(q[k], P.nb, pv[k], 0.0);
+#pragma unroll
+  for (int k = 0; k < nv; ++k) {
     const int op = ops[k];
     double a = 0.0;
 #pragma unroll
@@ -974,6 +987,7 @@ __global__ __launch_bounds__(NTF) void k_final(DV D, int kind, FinParams P) {
   }
   __syncthreads();
   if (threadIdx.x != 0) return;
+  if (P.dbg) P.dbg[1] = (int64_t)wall_clock64();
   if (P.rs) ldl_status_start(P.rs);
   switch (kind) {
     case FIN_RESID: {
@@ -1058,6 +1072,37 @@ __global__ __launch_bounds__(NTF) void k_final(DV D, int kind, FinParams P) {
     }
     case FIN_ZSHIFT2: st->init_viol = res[0]; break;
   }
+  if (P.dbg) {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    P.dbg[2] = (int64_t)wall_clock64();
+  }
+}
+
+// the k_final instance of a finaliser launch (slots, fused step test, fused objective)
+void launch_final(const DV& D, int kind, const FinParams& P, hipStream_t s) {
+  switch (kind) {
+    case FIN_ALPHA: k_final<0, true, false><<<1, NTF, 0, s>>>(D, kind, P); break;
+    case FIN_RESID:
+      if (P.nb_alpha > 0)
+        k_final<3, true, false><<<1, NTF, 0, s>>>(D, kind, P);
+      else
+        k_final<3, false, false><<<1, NTF, 0, s>>>(D, kind, P);
+      break;
+    case FIN_MU_PRED:
+    case FIN_MU_FULL:
+    case FIN_MU_GONDZIO:
+    case FIN_ZINIT: k_final<4, false, false><<<1, NTF, 0, s>>>(D, kind, P); break;
+    case FIN_EVAL:
+    case FIN_ZSHIFT2: k_final<1, false, false><<<1, NTF, 0, s>>>(D, kind, P); break;
+    case FIN_TERM:
+      if (P.nb_eval > 0)
+        k_final<6, false, true><<<1, NTF, 0, s>>>(D, kind, P);
+      else
+        k_final<6, false, false><<<1, NTF, 0, s>>>(D, kind, P);
+      break;
+    case FIN_ZSHIFT1: k_final<8, false, false><<<1, NTF, 0, s>>>(D, kind, P); break;
+    default: throw Error("k_final: unknown finaliser kind", -2);
+  }
 }
 
 __global__ void k_publish(const DevState* __restrict__ st, DevState* host, uint32_t* hseq, uint32_t seq) {
@@ -1105,6 +1150,23 @@ double now() {
 // ======================================================================= host side
 
 MPCSolver::~MPCSolver() {
+  if (fdbg_.p) {  // MADIPM_FINAL_DEBUG: per finaliser kind, thread 0's mean time to the reduced values / to the end
+    std::vector<int64_t> h((size_t)4 * kFinDbg);
+    (void)hipStreamSynchronize(stream_);
+    (void)hipMemcpy(h.data(), fdbg_.p, h.size() * 8, hipMemcpyDeviceToHost);
+    std::map<int64_t, std::array<double, 3>> acc;
+    for (int64_t q = 0; q < std::min<int64_t>(fdbg_n_, kFinDbg); ++q) {
+      const int64_t* e = &h[4 * q];
+      auto& a = acc[e[3]];
+      a[0] += 1;
+      a[1] += (e[1] - e[0]) * 1e-2;  // 100 MHz ticks -> us
+      a[2] += (e[2] - e[0]) * 1e-2;
+    }
+    for (auto& kv : acc)
+      std::fprintf(stderr, "k_final kind %2lld (alpha %d eval %d): %6.0f launches  reduced %6.2f us  end %6.2f us\n",
+                   (long long)(kv.first & 15), (int)((kv.first >> 4) & 1), (int)((kv.first >> 5) & 1), kv.second[0],
+                   kv.second[1] / kv.second[0], kv.second[2] / kv.second[0]);
+  }
   if (hst_) (void)hipHostFree(hst_);
   if (stream_) (void)hipStreamDestroy(stream_);
 }
@@ -1121,26 +1183,40 @@ int MPCSolver::spmv_blocks(int64_t rows) const { return blocks(rows * spmv_g_); 
 static void csr_from_coo(int nrow, const std::vector<int32_t>& r, const std::vector<int32_t>& c,
                          const std::vector<double>& v, std::vector<int64_t>& rp, std::vector<int32_t>& ci,
                          std::vector<double>& cv) {
-  // sorted by (row, col), duplicates summed
-  std::vector<int64_t> idx(r.size());
-  for (size_t k = 0; k < idx.size(); ++k) idx[k] = (int64_t)k;
-  std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) {
-    return r[a] != r[b] ? r[a] < r[b] : c[a] < c[b];
-  });
+  // sorted by (row, col), duplicates summed in input order.  Counting sort by row (stable), then each
+  // row's run sorted by column only when it is not already (O(nnz) for the usual column-major or
+  // row-major input; a comparison sort of 1e9 dense-QP entries took minutes)
+  const int64_t nnz = (int64_t)r.size();
+  std::vector<int64_t> start(nrow + 1, 0);
+  for (int64_t k = 0; k < nnz; ++k) start[r[k] + 1]++;
+  for (int i = 0; i < nrow; ++i) start[i + 1] += start[i];
+  std::vector<int64_t> idx(nnz);
+  {
+    std::vector<int64_t> fill(start.begin(), start.end() - 1);
+    for (int64_t k = 0; k < nnz; ++k) idx[fill[r[k]]++] = k;
+  }
   rp.assign(nrow + 1, 0);
   ci.clear();
   cv.clear();
-  for (size_t q = 0; q < idx.size(); ++q) {
-    const int64_t k = idx[q];
-    if (!ci.empty() && q > 0 && r[idx[q - 1]] == r[k] && ci.back() == c[k]) {
-      cv.back() += v[k];
-      continue;
+  ci.reserve(nnz);
+  cv.reserve(nnz);
+  for (int i = 0; i < nrow; ++i) {
+    const auto b = idx.begin() + start[i], e = idx.begin() + start[i + 1];
+    bool sorted = true;
+    for (auto q = b; q + 1 < e && sorted; ++q) sorted = c[*q] <= c[*(q + 1)];
+    if (!sorted) std::stable_sort(b, e, [&](int64_t x, int64_t y) { return c[x] < c[y]; });
+    const size_t row0 = ci.size();
+    for (auto q = b; q < e; ++q) {
+      const int64_t k = *q;
+      if (ci.size() > row0 && ci.back() == c[k]) {
+        cv.back() += v[k];
+        continue;
+      }
+      ci.push_back(c[k]);
+      cv.push_back(v[k]);
     }
-    ci.push_back(c[k]);
-    cv.push_back(v[k]);
-    rp[r[k] + 1]++;
+    rp[i + 1] = (int64_t)ci.size();
   }
-  for (int i = 0; i < nrow; ++i) rp[i + 1] += rp[i];
 }
 
 MPCSolver::MPCSolver(const madipm_qp& qp, const madipm_options& opt, Comm* comm) : opt_(opt), comm_(comm) {
@@ -1395,6 +1471,10 @@ void MPCSolver::setup_host(const madipm_qp& q) {
   csr_from_coo(n + m, kc, kr, kv, Kcp, Kri, Kv);
   nnzK_ = (int64_t)Kri.size();
   if (const char* e = std::getenv("MADIPM_PART_BLOCKS")) maxb_ = std::max(1, std::min(MAXB, std::atoi(e)));
+  if (const char* e = std::getenv("MADIPM_FINAL_DEBUG"); e && e[0] == '1') {
+    fdbg_.alloc(4 * kFinDbg);
+    MADIPM_HIP(hipMemset(fdbg_.p, 0, 4 * kFinDbg * sizeof(int64_t)));
+  }
   {  // SpMV lane-group width: ~2 entries per lane on an average row of [H A^T; A]
     const double avg = (double)(Hci.size() + 2 * Jci.size()) / std::max(1, n + m);
     spmv_g_ = 4;
@@ -1696,7 +1776,8 @@ void MPCSolver::launch_reduce_final(int kind, int nb, int amode, int nb_eval, LD
   } else if (kind == FIN_RESID) {
     P.a = opt_.check_residual ? opt_.tol_linear_solve : 0.0;
   }
-  k_final<<<1, NTF, 0, stream_>>>(D, kind, P);
+  if (fdbg_.p) P.dbg = fdbg_.p + 4 * (fdbg_n_++ % kFinDbg);
+  launch_final(D, kind, P, stream_);
 }
 
 // solve_system! (linear_solver.jl:19-44): rhs (mode) -> LDL^T solve -> finish + residual
@@ -1730,7 +1811,7 @@ void MPCSolver::gondzio() {
   auto ftb = [&](double& ap, double& ad) {  // get_fraction_to_boundary_step(solver, tau)
     k_alpha<<<nbz, NT, 0, s>>>(D, ALPHA_GONDZIO, tau, 0);
     FinParams P{nbz, ALPHA_GONDZIO, 0, 0, 0, 0, 0};
-    k_final<<<1, NTF, 0, s>>>(D, FIN_ALPHA, P);
+    launch_final(D, FIN_ALPHA, P, s);
     read_state();
     wait_state();
     ap = hst_->alpha_aff_p;
@@ -1913,7 +1994,7 @@ void MPCSolver::step_size(bool fused) {
   if (!fused) {
     k_alpha<<<nbz, NT, 0, s>>>(D, mode, tau, 0);
     FinParams P{nbz, mode, 0, 0, 0, 0, 0};
-    k_final<<<1, NTF, 0, s>>>(D, FIN_ALPHA, P);
+    launch_final(D, FIN_ALPHA, P, s);
   }
   if (opt_.step_rule == 2) {
     k_mu<<<nbz, NT, 0, s>>>(D, 1, 0.0, 0.0);
@@ -2171,11 +2252,11 @@ void update_step_standalone(int rule, double tau_param, double mu, int nlb, int 
   const double tau = rule == 2 ? 1.0 : tau_param;
   k_alpha<<<nbz, NT, 0, s>>>(D, mode, tau, 0);
   FinParams P{nbz, mode, 0, 0, 0, 0, 0};
-  k_final<<<1, NTF, 0, s>>>(D, FIN_ALPHA, P);
+  launch_final(D, FIN_ALPHA, P, s);
   if (rule == 2) {
     k_mu<<<nbz, NT, 0, s>>>(D, 1, 0.0, 0.0);
     FinParams Q{nbz, 0, (double)(nlb + nub), tau_param, 0, 0, 0};
-    k_final<<<1, NTF, 0, s>>>(D, FIN_MU_FULL, Q);
+    launch_final(D, FIN_MU_FULL, Q, s);
   }
   MADIPM_HIP(hipGetLastError());
   DevState h{};

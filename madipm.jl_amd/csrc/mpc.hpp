@@ -107,6 +107,9 @@ class MPCSolver {
   // KKT formulation (0 K2, 1 K2.5, 2 normal equations)
   int kkt_ = 0;
   int spmv_g_ = 8;  // lanes per row in the SpMV kernels
+  static constexpr int kFinDbg = 4096;
+  DBuf<int64_t> fdbg_;  // MADIPM_FINAL_DEBUG: k_final stamps (ring of kFinDbg launches)
+  int64_t fdbg_n_ = 0;
   int maxb_ = 2048;  // partial-reduction blocks per producer launch (<= MAXB; MADIPM_PART_BLOCKS)
   DBuf<double> sk_, K0_, Dinv_, bufm_, Cx_;
   DBuf<int32_t> Krow_, Kcol_, cprod_;

@@ -107,6 +107,24 @@ def test_ldl_schur_update_variants(defer, sfm, monkeypatch):
     assert ls.inertia() == (4000, 0, 3000)
 
 
+@pytest.mark.parametrize("f16r", ["0", "1"])
+@pytest.mark.parametrize("sfm", [128, 192])
+@pytest.mark.parametrize("well", [True, False])
+def test_ldl_diag_block_variants(f16r, sfm, well, monkeypatch):
+    """The 16-pivot diagonal blocks of the in-LDS factorisation factorised in registers (factor16r:
+    DPP row broadcasts + gfx950 permlane swaps, MADIPM_F16R=1, default) or through an LDS hand-off per
+    pivot (factor16s, 0): the oracle's pivots to 1e-12 (well conditioned) and its solution; the two
+    variants round the Schur complement along mirrored paths, so they agree to rounding, not bitwise.
+    The block-angular K2 has fronts of 16 .. 150 columns (several diagonal blocks each) and a
+    120-column root (k_small_blocked); the QP case a dense front."""
+    monkeypatch.setenv("MADIPM_F16R", f16r)
+    K, Lw = block_angular_k2(3000, 4000, 20, 7, well=well)
+    ls = _check_case(K, Lw, small_front_max=sfm, well=well)
+    assert ls.inertia() == (4000, 0, 3000)
+    K, Lw = _dense_k2(150, 1000, 5)
+    _check_case(K, Lw, small_front_max=sfm, well=True)
+
+
 @pytest.mark.parametrize("chain,sfold", [("0", "1"), ("0", "0"), ("0", "2"), ("1", "2"), ("1", "1")])
 @pytest.mark.parametrize("well", [True, False])
 def test_ldl_chain_solve_and_leaf_fold(chain, sfold, well, monkeypatch):

@@ -15,6 +15,16 @@ __global__ __launch_bounds__(256) void k_prod(double* part, int nb) {
   if (threadIdx.x < NV) part[threadIdx.x * MAXB + blockIdx.x] = sh[threadIdx.x];
 }
 
+// the same partials after streaming `nbig` doubles of writes (a producer with a large dirty footprint,
+// like the MPC's residual / right-hand-side kernels)
+__global__ __launch_bounds__(256) void k_prod_big(double* part, int nb, double* big, int64_t nbig) {
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < nbig; i += (int64_t)gridDim.x * 256) big[i] = (double)i;
+  __shared__ double sh[NV];
+  if (threadIdx.x < NV) sh[threadIdx.x] = blockIdx.x * 1e-3 + threadIdx.x;
+  __syncthreads();
+  if (threadIdx.x < NV) part[threadIdx.x * MAXB + blockIdx.x] = sh[threadIdx.x];
+}
+
 __global__ void k_empty(double* out) {
   if (threadIdx.x == 0 && out[0] == 12345.0) out[1] = 1.0;
 }
@@ -60,11 +70,21 @@ int main() {
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   const int nb = 1929, R = 400;
+  double* big;
+  const int64_t NBIG = 8ll << 20;  // 64 MiB
+  hipMalloc(&big, NBIG * 8);
+  int64_t nbig = 0;
+  auto prod = [&]() {
+    if (nbig)
+      k_prod_big<<<nb, 256>>>(part, nb, big, nbig);
+    else
+      k_prod<<<nb, 256>>>(part, nb);
+  };
   auto run = [&](int which) {
-    for (int it = 0; it < 20; ++it) k_prod<<<nb, 256>>>(part, nb);
+    for (int it = 0; it < 20; ++it) prod();
     hipEventRecord(e0);
     for (int it = 0; it < R; ++it) {
-      k_prod<<<nb, 256>>>(part, nb);
+      prod();
       if (which == 1) k_empty<<<1, 64>>>(out);
       if (which == 2) k_fin<1024><<<1, 1024>>>(part, nb, out);
       if (which == 3) k_fin<256><<<1, 256>>>(part, nb, out);
@@ -76,9 +96,12 @@ int main() {
     hipEventElapsedTime(&ms, e0, e1);
     return 1e3 * ms / R;
   };
-  const double base = run(0);
-  std::printf("producer alone          %7.2f us\n", base);
   const char* nm[] = {"", "empty kernel", "k_fin 1024 thr", "k_fin 256 thr", "k_fin 512 thr"};
-  for (int w = 1; w <= 4; ++w) std::printf("+ %-20s %7.2f us\n", nm[w], run(w) - base);
+  for (int64_t nbg : {0ll, 1ll << 20, 4ll << 20, 8ll << 20}) {
+    nbig = nbg;
+    const double base = run(0);
+    std::printf("producer (+ %3lld MiB written) alone %7.2f us\n", (long long)(nbg * 8 >> 20), base);
+    for (int w = 1; w <= 4; ++w) std::printf("  + %-20s %7.2f us\n", nm[w], run(w) - base);
+  }
   return 0;
 }
