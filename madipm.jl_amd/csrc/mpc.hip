@@ -791,204 +791,68 @@ struct FinParams {
 };
 constexpr int PART_EVAL = 6;
 
-// k_final runs as ONE block of NTF = 256 threads that reads every partial in a single memory round
-// trip: thread t owns blocks 8t .. 8t + 7 (four 16-B loads per value; nb <= MAXB = 8 NTF), all of a
-// thread's loads in flight together.  Fixed combine order (the thread's 8 blocks in order, a shuffle
-// tree over the wave, then the 4 waves in order): bitwise reproducible.  (Measured, tools/
-// final_bench.hip: a 1024-thread finaliser costs ~1 us more than a 256-thread one after the same
-// producer, and its 16-wave serial combine more again.)
+// k_final combines the producers' block partials (nb <= MAXB per slot) in two levels inside ONE launch:
+// FG workgroups of FT threads, thread t of workgroup g owning block g FT + t; each workgroup reduces its
+// FT blocks (wave shuffles, then wave 0 before wave 1) and stores one partial per value write-through
+// (sc1), and the last workgroup to take a ticket combines the FG partials in workgroup order and runs
+// the scalar logic.  Fixed combine order: bitwise reproducible.  One workgroup reading every partial was
+// bound by a single CU's memory parallelism (~1 us per 16-KB slot, 11 us for the residual + step test:
+// MADIPM_FINAL_DEBUG stamps); spread over FG CUs each reads ~1/FG of it in one round trip.
 // (Finalising inside the producing kernel instead — block 0 polling per-block flags, or a ticket —
 // measured slower on ex10: the in-launch hand-off costs more than this launch.)
-constexpr int NTF = 256, FPT = 8;  // threads, partial blocks per thread
-static_assert(MAXB == FPT * NTF, "k_final: eight partial rows per thread");
+constexpr int FG = 16, FT = 128;  // workgroups, threads per workgroup (one partial block per thread)
+static_assert(MAXB == FG * FT, "k_final: one partial block per thread");
+constexpr int NL2 = 24;  // level-2 value slots: 8 generic + 4 alpha values + 4 alpha indices + eval
 
-// A thread's partials of one slot: its FPT blocks as FPT/2 16-B loads.  The loads are unconditional
-// (every slot holds MAXB partials, stale past nb) and issued for EVERY slot of the launch before the
-// first selection (part8_sel pins its raw values, i.e. waits for them, then selects the fill past nb):
-// a predicated load compiles to a branch around the load with a wait inside, which serialised the
-// ~90 loads of the fused residual + step-test finaliser into ~90 memory latencies (14 us measured).
-typedef double2 Raw8[FPT / 2];
-__device__ __forceinline__ void part8_load(const DV& D, int k, Raw8& q) {
-  const int b0 = FPT * threadIdx.x;
-#pragma unroll
-  for (int h = 0; h < FPT; h += 2) q[h / 2] = *reinterpret_cast<const double2*>(D.part + pidx(b0 + h, k));
-}
-__device__ __forceinline__ void part8_sel(Raw8& q, int nb, double (&v)[FPT], double fill) {
-  static_assert(FPT == 8, "part8_sel pins four double2");
-  asm volatile("" : "+v"(q[0].x), "+v"(q[0].y), "+v"(q[1].x), "+v"(q[1].y), "+v"(q[2].x), "+v"(q[2].y), "+v"(q[3].x),
-               "+v"(q[3].y));
-  const int b0 = FPT * threadIdx.x;
-#pragma unroll
-  for (int h = 0; h < FPT; h += 2) {
-    v[h] = (b0 + h < nb) ? q[h / 2].x : fill;
-    v[h + 1] = (b0 + h + 1 < nb) ? q[h / 2].y : fill;
-  }
-}
+__device__ __forceinline__ double ld_sc1(const double* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void st_sc1(double* p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
-// the step test's argmin over the block partials in slots base.. (FIN_ALPHA: 0, fused: PART_ALPHA):
-// 4 ratio slots, then 4 index slots; every thread of the block calls it (shuffles, __syncthreads),
-// thread 0 writes the state
-
-__device__ void fin_alpha(const DV& D, const FinParams& P, const double (&pv)[4][FPT], const double (&pi)[4][FPT],
-                          double (&sh)[8][NTF / 64], int (&shi)[4][NTF / 64]) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+// the step test's result (fraction-to-boundary ratios and their argmins) into the state
+__device__ void fin_alpha_store(const DV& D, const FinParams& P, double (&a)[4], int (&ii)[4]) {
   DevState* st = D.st;
-  double v[4];
-  int ix[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    v[k] = INF;
-    ix[k] = -1;
-#pragma unroll
-    for (int h = 0; h < FPT; ++h) amin_upd(v[k], ix[k], pv[k][h], (int)pi[k][h]);
+    // mapreduce init (1.0, 0) is the fold's first element: an element whose ratio is exactly 1.0
+    // comes later and replaces it (the index is the element's); larger ratios keep (1.0, init)
+    if (!(a[k] <= 1.0)) {
+      a[k] = 1.0;
+      ii[k] = -1;
+    }
   }
-  for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const double a2 = __shfl_down(v[k], o, 64);
-      const int b2 = __shfl_down(ix[k], o, 64);
-      amin_upd(v[k], ix[k], a2, b2);
-    }
-  if (lane == 0)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      sh[k][wv] = v[k];
-      shi[k][wv] = ix[k];
-    }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double a[4];
-    int ii[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      a[k] = sh[k][0];
-      ii[k] = shi[k][0];
-#pragma unroll
-      for (int w = 1; w < NTF / 64; ++w) amin_upd(a[k], ii[k], sh[k][w], shi[k][w]);
-      // mapreduce init (1.0, 0) is the fold's first element: an element whose ratio is exactly 1.0
-      // comes later and replaces it (the index is the element's); larger ratios keep (1.0, init)
-      if (!(a[k] <= 1.0)) {
-        a[k] = 1.0;
-        ii[k] = -1;
-      }
-    }
-    st->a_xl = a[0];
-    st->a_xu = a[1];
-    st->a_zl = a[2];
-    st->a_zu = a[3];
-    st->i_xl = ii[0];
-    st->i_xu = ii[1];
-    st->i_zl = ii[2];
-    st->i_zu = ii[3];
-    const double ap = fmin(a[0], a[1]), ad = fmin(a[2], a[3]);
-    if (P.alpha_mode == ALPHA_PRED) {
-      st->alpha_aff_p = ap;
-      st->alpha_aff_d = ad;
-    } else if (P.alpha_mode == ALPHA_CONSERVATIVE || P.alpha_mode == ALPHA_ADAPTIVE) {
-      st->alpha_p = ap;
-      st->alpha_d = ad;
-    } else {  // MEHROTRA / GONDZIO: keep in the aff slots for the follow-up pass
-      st->alpha_aff_p = ap;
-      st->alpha_aff_d = ad;
-    }
+  st->a_xl = a[0];
+  st->a_xu = a[1];
+  st->a_zl = a[2];
+  st->a_zu = a[3];
+  st->i_xl = ii[0];
+  st->i_xu = ii[1];
+  st->i_zl = ii[2];
+  st->i_zu = ii[3];
+  const double ap = fmin(a[0], a[1]), ad = fmin(a[2], a[3]);
+  if (P.alpha_mode == ALPHA_PRED) {
+    st->alpha_aff_p = ap;
+    st->alpha_aff_d = ad;
+  } else if (P.alpha_mode == ALPHA_CONSERVATIVE || P.alpha_mode == ALPHA_ADAPTIVE) {
+    st->alpha_p = ap;
+    st->alpha_d = ad;
+  } else {  // MEHROTRA / GONDZIO: keep in the aff slots for the follow-up pass
+    st->alpha_aff_p = ap;
+    st->alpha_aff_d = ad;
   }
 }
 
-// one OP_SUM value over the partials this thread loaded (ev), in the generic path's order; every
-// thread returns it
-__device__ double fin_sum_slot(const double (&ev)[FPT], double (&sh)[8][NTF / 64]) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  double a = 0.0;
-#pragma unroll
-  for (int h = 0; h < FPT; ++h) a = comb(a, ev[h], OP_SUM);
-  for (int o = 32; o > 0; o >>= 1) a = comb(a, __shfl_down(a, o, 64), OP_SUM);
-  if (lane == 0) sh[0][wv] = a;
-  __syncthreads();
-  double r = sh[0][0];
-#pragma unroll
-  for (int w = 1; w < NTF / 64; ++w) r = comb(r, sh[0][w], OP_SUM);
-  __syncthreads();
-  return r;
-}
-
-// Combine the block partials in fixed order + scalar logic (one block of NTF threads).  Instantiated
-// per (value slots NV, fused step test AL, fused objective EV) so that a thread holds exactly the
-// partials of its launch (launch_final picks the instance).
-template <int NV, bool AL, bool EV>
-__global__ __launch_bounds__(NTF) void k_final(DV D, int kind, FinParams P) {
-  __shared__ double res[NPART];
-  __shared__ double sh[8][NTF / 64];
-  __shared__ int shi[4][NTF / 64];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  DevState* st = D.st;
-  if (P.dbg && threadIdx.x == 0) {
-    P.dbg[0] = (int64_t)wall_clock64();
-    P.dbg[3] = kind | (AL && NV > 0 ? 16 : 0) | (EV ? 32 : 0);
-  }
-  // every load of the launch first (one memory round trip), then the selections and reductions
-  constexpr int NA = AL ? 8 : 0;
-  Raw8 q[NV > 0 ? NV : 1], aq[AL ? 8 : 1], eq[1];
-#pragma unroll
-  for (int k = 0; k < NV; ++k) part8_load(D, k, q[k]);
-#pragma unroll
-  for (int k = 0; k < NA; ++k) part8_load(D, (NV > 0 ? PART_ALPHA : 0) + k, aq[k]);
-  if (EV) part8_load(D, PART_EVAL, eq[0]);
-  if (AL) {  // FIN_ALPHA, or FIN_RESID + the FIN_ALPHA of the k_alpha launched after the residual
-    const int nba = NV > 0 ? P.nb_alpha : P.nb;
-    double apv[4][FPT], api[4][FPT];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      part8_sel(aq[k], nba, apv[k], INF);
-      part8_sel(aq[4 + k], nba, api[k], -1.0);
-    }
-    fin_alpha(D, P, apv, api, sh, shi);
-    if (NV == 0) return;
-    __syncthreads();
-  }
-  if (EV) {  // FIN_TERM: the previous iteration's FIN_EVAL, deferred to this launch
-    double ev[FPT];
-    part8_sel(eq[0], P.nb_eval, ev, 0.0);
-    const double r = fin_sum_slot(ev, sh);
-    if (threadIdx.x == 0) st->obj_val = P.c + r;
-  }
-  constexpr int nv = NV;
-  int ops[NPART];
+__device__ __forceinline__ void fin_ops(int kind, int (&ops)[8]) {
+  for (int k = 0; k < 8; ++k) ops[k] = OP_SUM;
   switch (kind) {
     case FIN_RESID: ops[0] = ops[1] = ops[2] = OP_MAX; break;
-    case FIN_MU_PRED:
-    case FIN_MU_FULL:
-    case FIN_MU_GONDZIO: for (int k = 0; k < 4; ++k) ops[k] = OP_SUM; break;
-    case FIN_EVAL: ops[0] = OP_SUM; break;
-    case FIN_TERM: ops[0] = ops[1] = ops[2] = OP_MAX; ops[3] = ops[4] = ops[5] = OP_SUM; break;
+    case FIN_TERM: ops[0] = ops[1] = ops[2] = OP_MAX; break;
     case FIN_ZINIT: for (int k = 0; k < 4; ++k) ops[k] = OP_MIN; break;
-    case FIN_ZSHIFT1: for (int k = 0; k < 8; ++k) ops[k] = OP_SUM; break;
-    case FIN_ZSHIFT2: ops[0] = OP_SUM; break;
+    default: break;
   }
-  // every reduction here starts at 0.0 (sum, max, and min with init 0), so absent blocks count 0.0
-  double pv[NV > 0 ? NV : 1][FPT];
-#pragma unroll
-  for (int k = 0; k < NV; ++k) part8_sel(q[k], P.nb, pv[k], 0.0);
-#pragma unroll
-  for (int k = 0; k < nv; ++k) {
-    const int op = ops[k];
-    double a = 0.0;
-#pragma unroll
-    for (int h = 0; h < FPT; ++h) a = comb(a, pv[k][h], op);
-    for (int o = 32; o > 0; o >>= 1) a = comb(a, __shfl_down(a, o, 64), op);
-    if (lane == 0) sh[k][wv] = a;
-  }
-  __syncthreads();
-  if (threadIdx.x < nv) {
-    const int k = threadIdx.x;
-    double a = sh[k][0];
-#pragma unroll
-    for (int w = 1; w < NTF / 64; ++w) a = comb(a, sh[k][w], ops[k]);
-    res[k] = a;
-  }
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  if (P.dbg) P.dbg[1] = (int64_t)wall_clock64();
-  if (P.rs) ldl_status_start(P.rs);
+}
+
+// the scalar logic of each finaliser kind on the reduced values res[] (thread 0 of the last workgroup)
+__device__ void fin_tail(const DV& D, int kind, const FinParams& P, const double* res) {
+  DevState* st = D.st;
   switch (kind) {
     case FIN_RESID: {
       const double ratio = res[0] / fmax(1.0, res[1]);  // linear_solver.jl:35
@@ -1072,6 +936,161 @@ __global__ __launch_bounds__(NTF) void k_final(DV D, int kind, FinParams P) {
     }
     case FIN_ZSHIFT2: st->init_viol = res[0]; break;
   }
+}
+
+// Instantiated per (value slots NV, fused step test AL, fused objective EV) so that a thread holds
+// exactly the partials of its launch (launch_final picks the instance).  Level-2 partials and the
+// ticket live past the NPART x MAXB partials (part_): L2 = part + NPART MAXB, NL2 x FG doubles, then the
+// ticket counter (reset by the last workgroup).
+template <int NV, bool AL, bool EV>
+__global__ __launch_bounds__(FT) void k_final(DV D, int kind, FinParams P) {
+  __shared__ double res[NL2];
+  __shared__ int s_last;
+  DevState* st = D.st;
+  double* L2 = D.part + NPART * MAXB;
+  int32_t* ticket = reinterpret_cast<int32_t*>(L2 + NL2 * FG);
+  const int g = blockIdx.x, b = g * FT + threadIdx.x;
+  if (P.dbg && threadIdx.x == 0 && g == 0) {
+    P.dbg[0] = (int64_t)wall_clock64();
+    P.dbg[3] = kind | (AL && NV > 0 ? 16 : 0) | (EV ? 32 : 0);
+  }
+  // every load first (unconditional: each slot holds MAXB partials, stale past nb), then the pins
+  // (waits) and the selections — a predicated load compiles to a branch with a wait inside
+  constexpr int NA = AL ? 8 : 0;
+  double q[NV > 0 ? NV : 1], aq[AL ? 8 : 1], eq = 0.0;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) q[k] = D.part[pidx(b, k)];
+#pragma unroll
+  for (int k = 0; k < NA; ++k) aq[k] = D.part[pidx(b, (NV > 0 ? PART_ALPHA : 0) + k)];
+  if (EV) eq = D.part[pidx(b, PART_EVAL)];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) asm volatile("" : "+v"(q[k]));
+#pragma unroll
+  for (int k = 0; k < NA; ++k) asm volatile("" : "+v"(aq[k]));
+  if (EV) asm volatile("" : "+v"(eq));
+  if (P.dbg && threadIdx.x == 0 && g == 0) P.dbg[4] = (int64_t)wall_clock64();  // loads returned
+  int ops[8];
+  fin_ops(kind, ops);
+  // level 1: this workgroup's blocks — every value's shuffle tree in lockstep (one latency chain for all
+  // of them, not one per value), then the waves in order
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  double w1[NV > 0 ? NV : 1], av[4];
+  int ai[4];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) w1[k] = b < P.nb ? q[k] : 0.0;
+  const int nba = NV > 0 ? P.nb_alpha : P.nb;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    av[k] = (AL && b < nba) ? aq[k] : INF;
+    ai[k] = (AL && b < nba) ? (int)aq[AL ? 4 + k : 0] : -1;
+  }
+  double e1 = (EV && b < P.nb_eval) ? eq : 0.0;
+  for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) w1[k] = comb(w1[k], __shfl_down(w1[k], o, 64), ops[k]);
+    if (AL)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const double a2 = __shfl_down(av[k], o, 64);
+        const int b2 = __shfl_down(ai[k], o, 64);
+        amin_upd(av[k], ai[k], a2, b2);
+      }
+    if (EV) e1 += __shfl_down(e1, o, 64);
+  }
+  __shared__ double shv[NL2][FT / 64];
+  __shared__ int shx[4][FT / 64];
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) shv[k][wv] = w1[k];
+    if (AL)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        shv[8 + k][wv] = av[k];
+        shx[k][wv] = ai[k];
+      }
+    if (EV) shv[16][wv] = e1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      double a = shv[k][0];
+#pragma unroll
+      for (int w = 1; w < FT / 64; ++w) a = comb(a, shv[k][w], ops[k]);
+      st_sc1(L2 + k * FG + g, a);
+    }
+    if (AL)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        double a = shv[8 + k][0];
+        int ix = shx[k][0];
+#pragma unroll
+        for (int w = 1; w < FT / 64; ++w) amin_upd(a, ix, shv[8 + k][w], shx[k][w]);
+        st_sc1(L2 + (8 + k) * FG + g, a);
+        st_sc1(L2 + (12 + k) * FG + g, (double)ix);
+      }
+    if (EV) {
+      double a = shv[16][0];
+#pragma unroll
+      for (int w = 1; w < FT / 64; ++w) a += shv[16][w];
+      st_sc1(L2 + 16 * FG + g, a);
+    }
+    if (P.dbg && g == 0) P.dbg[5] = (int64_t)wall_clock64();  // level 1 reduced
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == FG - 1;
+    if (P.dbg && s_last) P.dbg[6] = (int64_t)wall_clock64();  // last ticket taken
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // level 2 (last workgroup): every level-2 partial loaded at once (one per thread, sc1), then thread k
+  // combines value slot k over the workgroups in order
+  const int t = threadIdx.x;
+  __shared__ double l2s[NL2 * FG];
+  constexpr int NUSE = AL ? (EV ? 17 : 16) : (EV ? 17 : NV);  // slots in use: 0..NV-1, 8..15 (alpha), 16 (eval)
+  static_assert(NUSE * FG <= 3 * FT, "level 2: at most three loads per thread");
+#pragma unroll
+  for (int h = 0; h < 3; ++h) {
+    const int e = t + h * FT;
+    if (e < NUSE * FG) l2s[e] = ld_sc1(L2 + e);
+  }
+  __syncthreads();
+  if (t < NV) {
+    double a = l2s[t * FG];
+#pragma unroll
+    for (int w = 1; w < FG; ++w) a = comb(a, l2s[t * FG + w], ops[t]);
+    res[t] = a;
+  } else if (AL && t >= 8 && t < 12) {
+    double a = l2s[t * FG];
+    int ix = (int)l2s[(t + 4) * FG];
+#pragma unroll
+    for (int w = 1; w < FG; ++w) amin_upd(a, ix, l2s[t * FG + w], (int)l2s[(t + 4) * FG + w]);
+    res[t] = a;
+    res[t + 4] = (double)ix;
+  } else if (EV && t == 16) {
+    double a = l2s[16 * FG];
+#pragma unroll
+    for (int w = 1; w < FG; ++w) a += l2s[16 * FG + w];
+    res[16] = a;
+  }
+  __syncthreads();
+  if (t != 0) return;
+  *ticket = 0;  // every workgroup has taken its ticket: reset for the next launch
+  if (P.dbg) P.dbg[1] = (int64_t)wall_clock64();
+  if (AL) {
+    double a[4];
+    int ii[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      a[k] = res[8 + k];
+      ii[k] = (int)res[12 + k];
+    }
+    fin_alpha_store(D, P, a, ii);
+  }
+  if (EV) st->obj_val = P.c + res[16];  // FIN_TERM: the previous iteration's FIN_EVAL, deferred here
+  if (NV > 0) {
+    if (P.rs) ldl_status_start(P.rs);
+    fin_tail(D, kind, P, res);
+  }
   if (P.dbg) {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     P.dbg[2] = (int64_t)wall_clock64();
@@ -1081,26 +1100,26 @@ __global__ __launch_bounds__(NTF) void k_final(DV D, int kind, FinParams P) {
 // the k_final instance of a finaliser launch (slots, fused step test, fused objective)
 void launch_final(const DV& D, int kind, const FinParams& P, hipStream_t s) {
   switch (kind) {
-    case FIN_ALPHA: k_final<0, true, false><<<1, NTF, 0, s>>>(D, kind, P); break;
+    case FIN_ALPHA: k_final<0, true, false><<<FG, FT, 0, s>>>(D, kind, P); break;
     case FIN_RESID:
       if (P.nb_alpha > 0)
-        k_final<3, true, false><<<1, NTF, 0, s>>>(D, kind, P);
+        k_final<3, true, false><<<FG, FT, 0, s>>>(D, kind, P);
       else
-        k_final<3, false, false><<<1, NTF, 0, s>>>(D, kind, P);
+        k_final<3, false, false><<<FG, FT, 0, s>>>(D, kind, P);
       break;
     case FIN_MU_PRED:
     case FIN_MU_FULL:
     case FIN_MU_GONDZIO:
-    case FIN_ZINIT: k_final<4, false, false><<<1, NTF, 0, s>>>(D, kind, P); break;
+    case FIN_ZINIT: k_final<4, false, false><<<FG, FT, 0, s>>>(D, kind, P); break;
     case FIN_EVAL:
-    case FIN_ZSHIFT2: k_final<1, false, false><<<1, NTF, 0, s>>>(D, kind, P); break;
+    case FIN_ZSHIFT2: k_final<1, false, false><<<FG, FT, 0, s>>>(D, kind, P); break;
     case FIN_TERM:
       if (P.nb_eval > 0)
-        k_final<6, false, true><<<1, NTF, 0, s>>>(D, kind, P);
+        k_final<6, false, true><<<FG, FT, 0, s>>>(D, kind, P);
       else
-        k_final<6, false, false><<<1, NTF, 0, s>>>(D, kind, P);
+        k_final<6, false, false><<<FG, FT, 0, s>>>(D, kind, P);
       break;
-    case FIN_ZSHIFT1: k_final<8, false, false><<<1, NTF, 0, s>>>(D, kind, P); break;
+    case FIN_ZSHIFT1: k_final<8, false, false><<<FG, FT, 0, s>>>(D, kind, P); break;
     default: throw Error("k_final: unknown finaliser kind", -2);
   }
 }
@@ -1151,21 +1170,28 @@ double now() {
 
 MPCSolver::~MPCSolver() {
   if (fdbg_.p) {  // MADIPM_FINAL_DEBUG: per finaliser kind, thread 0's mean time to the reduced values / to the end
-    std::vector<int64_t> h((size_t)4 * kFinDbg);
+    std::vector<int64_t> h((size_t)8 * kFinDbg);
     (void)hipStreamSynchronize(stream_);
     (void)hipMemcpy(h.data(), fdbg_.p, h.size() * 8, hipMemcpyDeviceToHost);
-    std::map<int64_t, std::array<double, 3>> acc;
+    std::map<int64_t, std::array<double, 6>> acc;
     for (int64_t q = 0; q < std::min<int64_t>(fdbg_n_, kFinDbg); ++q) {
-      const int64_t* e = &h[4 * q];
+      const int64_t* e = &h[8 * q];
       auto& a = acc[e[3]];
       a[0] += 1;
-      a[1] += (e[1] - e[0]) * 1e-2;  // 100 MHz ticks -> us
-      a[2] += (e[2] - e[0]) * 1e-2;
+      a[1] += (e[4] - e[0]) * 1e-2;  // 100 MHz ticks -> us
+      a[2] += (e[5] - e[0]) * 1e-2;
+      a[3] += (e[6] - e[0]) * 1e-2;
+      a[4] += (e[1] - e[0]) * 1e-2;
+      a[5] += (e[2] - e[0]) * 1e-2;
     }
-    for (auto& kv : acc)
-      std::fprintf(stderr, "k_final kind %2lld (alpha %d eval %d): %6.0f launches  reduced %6.2f us  end %6.2f us\n",
-                   (long long)(kv.first & 15), (int)((kv.first >> 4) & 1), (int)((kv.first >> 5) & 1), kv.second[0],
-                   kv.second[1] / kv.second[0], kv.second[2] / kv.second[0]);
+    for (auto& kv : acc) {
+      const double n = kv.second[0];
+      std::fprintf(stderr,
+                   "k_final kind %2lld (alpha %d eval %d): %6.0f launches  wg0 loads %6.2f  wg0 level-1 %6.2f  last ticket "
+                   "%6.2f  reduced %6.2f  end %6.2f us\n",
+                   (long long)(kv.first & 15), (int)((kv.first >> 4) & 1), (int)((kv.first >> 5) & 1), n,
+                   kv.second[1] / n, kv.second[2] / n, kv.second[3] / n, kv.second[4] / n, kv.second[5] / n);
+    }
   }
   if (hst_) (void)hipHostFree(hst_);
   if (stream_) (void)hipStreamDestroy(stream_);
@@ -1472,8 +1498,8 @@ void MPCSolver::setup_host(const madipm_qp& q) {
   nnzK_ = (int64_t)Kri.size();
   if (const char* e = std::getenv("MADIPM_PART_BLOCKS")) maxb_ = std::max(1, std::min(MAXB, std::atoi(e)));
   if (const char* e = std::getenv("MADIPM_FINAL_DEBUG"); e && e[0] == '1') {
-    fdbg_.alloc(4 * kFinDbg);
-    MADIPM_HIP(hipMemset(fdbg_.p, 0, 4 * kFinDbg * sizeof(int64_t)));
+    fdbg_.alloc(8 * kFinDbg);
+    MADIPM_HIP(hipMemset(fdbg_.p, 0, 8 * kFinDbg * sizeof(int64_t)));
   }
   {  // SpMV lane-group width: ~2 entries per lane on an average row of [H A^T; A]
     const double avg = (double)(Hci.size() + 2 * Jci.size()) / std::max(1, n + m);
@@ -1622,7 +1648,8 @@ void MPCSolver::setup_host(const madipm_qp& q) {
     up(K0_, Kv);
     zeros(sk_, n);
   }
-  part_.alloc(MAXB * NPART);
+  part_.alloc(MAXB * NPART + NL2 * FG + 8);  // + k_final's level-2 partials and ticket
+  MADIPM_HIP(hipMemset(part_.p, 0, (MAXB * NPART + NL2 * FG + 8) * sizeof(double)));
   st_.alloc(1);
   if (ldl_->external_status(&st_.p->ldl_status, &hst_->ldl_status)) {  // carried by read_state()
     // the MPC's own kernels start / end each factorisation: no k_status_init, no k_inertia (K2, K2.5:
@@ -1776,7 +1803,7 @@ void MPCSolver::launch_reduce_final(int kind, int nb, int amode, int nb_eval, LD
   } else if (kind == FIN_RESID) {
     P.a = opt_.check_residual ? opt_.tol_linear_solve : 0.0;
   }
-  if (fdbg_.p) P.dbg = fdbg_.p + 4 * (fdbg_n_++ % kFinDbg);
+  if (fdbg_.p) P.dbg = fdbg_.p + 8 * (fdbg_n_++ % kFinDbg);
   launch_final(D, kind, P, stream_);
 }
 
@@ -2217,13 +2244,14 @@ void update_step_standalone(int rule, double tau_param, double mu, int nlb, int 
   const int n = nlb + nub;
   MADIPM_REQUIRE(nlb >= 0 && nub >= 0 && n > 0, "update_step: no bounded coordinate");
   MADIPM_REQUIRE(rule >= 0 && rule <= 2, "update_step: rule must be 0, 1 or 2");
-  DBuf<double> x(n), xl(n), xu(n), zl(n), zu(n), d(n + nlb + nub), part((size_t)NPART * MAXB);
+  DBuf<double> x(n), xl(n), xu(n), zl(n), zu(n), d(n + nlb + nub), part((size_t)NPART * MAXB + NL2 * FG + 8);
   DBuf<int32_t> ilb(std::max(nlb, 1)), iub(std::max(nub, 1));
   DBuf<DevState> st(1);
   std::vector<int32_t> io(n);
   for (int i = 0; i < n; ++i) io[i] = i;
   ilb.upload(io.data(), nlb, s);
   iub.upload(io.data() + nlb, nub, s);
+  MADIPM_HIP(hipMemsetAsync(part.p, 0, sizeof(double) * part.n, s));  // k_final's ticket starts at 0
   MADIPM_HIP(hipMemsetAsync(x.p, 0, sizeof(double) * n, s));
   MADIPM_HIP(hipMemsetAsync(xl.p, 0, sizeof(double) * n, s));
   MADIPM_HIP(hipMemsetAsync(xu.p, 0, sizeof(double) * n, s));

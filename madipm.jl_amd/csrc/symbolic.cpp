@@ -7,6 +7,7 @@
 #include "symbolic.hpp"
 
 #include <algorithm>
+#include <cstring>
 #include <climits>
 #include <cstdlib>
 #include <numeric>
@@ -827,7 +828,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     std::vector<int64_t> bnd;
     // k_fact_tree runs one workgroup per CU, tickets in level order: the tree fronts past the first
     // `slots` start only when an earlier front retires, so folding (staging the leaves inside the
-    // front's own critical path) is left to the micro launch for the late fronts of that level
+    // front's own critical path) is left to the micro launch for those late fronts
     // (MADIPM_FOLD_SLOTS overrides the MI355X CU count; 0 = no limit)
     int slots = 256;
     if (const char* e = std::getenv("MADIPM_FOLD_SLOTS")) slots = std::atoi(e);
@@ -838,8 +839,14 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q)
           if (S.ftree[S.level_list[q]]) ord.push_back(S.level_list[q]);
       if (slots > 0 && (int)ord.size() > slots) {
+        // every front past the first `slots` tickets leaves its leaves to the micro launch + gather: a
+        // late front's fold lies on the critical path (it starts when an earlier front retires), while
+        // the micro launch and the gather run before the tree on the whole GPU (ex10: tree span 210 ->
+        // 178 us; MADIPM_FOLD_LATE=cut restores the r2 rule: only the level cut by the slot count)
+        const char* la = std::getenv("MADIPM_FOLD_LATE");
+        const bool all = !(la && std::strcmp(la, "cut") == 0);
         const int lcut = S.level[ord[slots]];
-        for (size_t q = slots; q < ord.size() && S.level[ord[q]] == lcut; ++q) late[ord[q]] = 1;
+        for (size_t q = slots; q < ord.size() && (all || S.level[ord[q]] == lcut); ++q) late[ord[q]] = 1;
       }
     }
     for (int s = 0; s < ns_all; ++s) {

@@ -152,8 +152,11 @@ def test_ldl_chain_solve_and_leaf_fold(chain, sfold, well, monkeypatch):
 def test_ldl_leaf_folding(fold, well, monkeypatch):
     """Leaf folding (default; MADIPM_FOLD=0 turns it off): tree fronts factorise their micro-leaf
     children themselves and subtract the leaves' rank-1/2 updates in LDS through destination-sorted
-    product lists — same pivots / solution as the oracle, with and without it."""
+    product lists — same pivots / solution as the oracle, with and without it.  MADIPM_FOLD_SLOTS=0:
+    every tree front folds (by default the fronts past the first 256 tickets leave their leaves to the
+    micro launch + gather)."""
     monkeypatch.setenv("MADIPM_FOLD", fold)
+    monkeypatch.setenv("MADIPM_FOLD_SLOTS", "0")
     K, Lw = block_angular_k2(3000, 4000, 20, 7, well=well)
     ls = _check_case(K, Lw, well=well)
     assert ls.inertia() == (4000, 0, 3000)
