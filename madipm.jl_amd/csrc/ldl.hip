@@ -262,65 +262,9 @@ __global__ __launch_bounds__(NT) void k_small_factor(FrontTab T, const int32_t* 
 // entries live in its pivot columns only, so L = F(:, 0:w) D^-1 (2 x 2 block at most) and the update
 // block is U = -L D L^T (rows >= w), written column by column, coalesced over the group's lanes.
 constexpr int MG = 16;
-// The rows of the micro leaves folded into their tree-front parents (SymbolicPlan::absorb), one thread
-// per leaf row q (ab_* numbering, leaf k = ab_k[q]): the row's K entries (ab_src0/1) and its leaf's
-// pivots d0, l10, d1 (re-derived from the leaf's first two rows by every row of the leaf: cached
-// loads), then the row's L entries (for the solves), the fold stream entries (l0, l1), (l0 d0, l1 d1)
-// at position q, and by the first row D and the pivot check — what k_fact_tree's fold copies per batch
-// instead of gathering K values and deriving the pivots on its own critical path.  Same arithmetic as
-// the in-kernel fold it replaces (IEEE quotients, same operation order).
-__device__ __forceinline__ void fold_leaf_row(const FrontTab& T, int64_t q, const double* __restrict__ Kx,
-                                              double* __restrict__ arena, double* __restrict__ D, LDLStatus* st,
-                                              double tol) {
-  const int k = T.ab_k[q];
-  const int64_t j0 = T.ab_first[k];
-  const int wrc = T.ab_wrc[k], w = wrc & 255, r = wrc >> 8, i = (int)(q - j0);
-  const int32_t s00 = T.ab_src0[j0], s10 = (r > 1) ? T.ab_src0[j0 + 1] : -1, s11 = (r > 1) ? T.ab_src1[j0 + 1] : -1;
-  const int32_t sa = T.ab_src0[q], sb = T.ab_src1[q];
-  const double a00 = (s00 >= 0) ? Kx[s00] : 0.0, a10 = (s10 >= 0) ? Kx[s10] : 0.0, a11 = (s11 >= 0) ? Kx[s11] : 0.0;
-  const double va = (sa >= 0) ? Kx[sa] : 0.0, vb = (sb >= 0) ? Kx[sb] : 0.0;
-  const double d0 = a00, f10 = a10;
-  const double l10 = (w == 2) ? f10 / d0 : 0.0;
-  const double d1 = (w == 2) ? a11 - l10 * f10 : 0.0;
-  double* __restrict__ L = arena + T.ab_loff[k];
-  if (i >= w) {
-    const double li0 = va / d0;
-    const double li1 = (w == 2) ? (vb - li0 * f10) / d1 : 0.0;
-    T.fstream[q] = double2{li0, li1};
-    T.fstream[T.nfrow + q] = double2{li0 * d0, li1 * d1};
-    L[i] = li0;
-    if (w == 2) L[i + r] = li1;
-  } else {
-    T.fstream[q] = double2{0.0, 0.0};
-    T.fstream[T.nfrow + q] = double2{0.0, 0.0};
-    if (i == 0) {
-      L[0] = d0;
-      if (w == 2) L[r] = 0.0;
-      const int f0 = T.ab_f0[k];
-      D[f0] = d0;
-      if (bad_pivot(d0, tol)) atomicMin(&st->fail_pivot, f0 + 1);
-      if (w == 2) {
-        D[f0 + 1] = d1;
-        if (bad_pivot(d1, tol)) atomicMin(&st->fail_pivot, f0 + 2);
-      }
-    } else {  // i == 1, w == 2
-      L[1] = f10 / d0;
-      L[1 + r] = d1;
-    }
-  }
-}
-
-// blocks < nbm: groups of the micro fronts of the level-0 list (nf); blocks >= nbm: one thread per
-// folded leaf row (fold_leaf_row, nfold rows)
-__global__ __launch_bounds__(NT) void k_micro_factor(FrontTab T, const int32_t* __restrict__ fronts, int nf, int64_t nfold,
+__global__ __launch_bounds__(NT) void k_micro_factor(FrontTab T, const int32_t* __restrict__ fronts, int nf,
                                                      const double* __restrict__ Kx, double* __restrict__ arena,
                                                      double* __restrict__ D, LDLStatus* st, double tol) {
-  const int nbm = (nf + NT / MG - 1) / (NT / MG);
-  if ((int)blockIdx.x >= nbm) {  // block-uniform
-    const int64_t q = ((int64_t)blockIdx.x - nbm) * NT + threadIdx.x;
-    if (q < nfold) fold_leaf_row(T, q, Kx, arena, D, st, tol);
-    return;
-  }
   __shared__ double Fs[NT / MG][64];  // columns 0 / 1 of F (rows 0..31); later l_i0 d0 / l_i1 d1
   const int g = threadIdx.x / MG, l = threadIdx.x & (MG - 1);
   const int q = blockIdx.x * (NT / MG) + g;
@@ -1464,16 +1408,18 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
       tc = t2;
     }
   };
-  (void)Kx;
-  (void)arena;
-  (void)D;
-  (void)st;
-  (void)tol;
-  constexpr int RPT = 4;   // leaf rows per thread and pass (2 x 16 B each)
+  constexpr int RPT = 8;   // leaf rows per thread and pass
   constexpr int GP = 16;   // product entries per thread and group
-  const int RM = T.fold_rmax[s];
-  double2* LQ = reinterpret_cast<double2*>(ext);  // per batch row: (l0, l1)
+  const int RM = T.fold_rmax[s], LM = T.fold_lmax[s];
+  double2* LQ = reinterpret_cast<double2*>(ext);  // per batch row: K values of columns 0/1, then (l0, l1)
   double2* PQ = LQ + RM;                          // (l0 d0, l1 d1)
+  double* pd0 = reinterpret_cast<double*>(PQ + RM);
+  double* pd1 = pd0 + LM;
+  double* pf10 = pd1 + LM;
+  int64_t* ploff = reinterpret_cast<int64_t*>(pf10 + LM);
+  int32_t* prow0 = reinterpret_cast<int32_t*>(ploff + LM);  // batch-local first row of the leaf
+  int32_t* pwrc = prow0 + LM;
+  int32_t* kk = pwrc + LM;                                   // per batch row: batch-local leaf
   const int tid = threadIdx.x;
   const int b0 = T.fold_bptr[s], b1 = T.fold_bptr[s + 1];
   uint2 e[GP];
@@ -1485,30 +1431,92 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
   for (int bq = b0; bq < b1; ++bq) {
     const int k0 = T.fold_bat[bq], k1 = (bq + 1 < b1) ? T.fold_bat[bq + 1] : T.mc_ptr[s + 1];
     const int64_t j0 = T.ab_first[k0];
-    const int nrow = (int)(T.ab_first[k1] - j0);
-    // (1) the batch's rows of the fold stream (the leaves' pre-pass in the level-0 micro launch formed
-    // their pivots, L panels and (l, l d) rows): one contiguous copy, RPT rows per thread in flight
-    const double2* __restrict__ sq = T.fstream + j0;
-    const double2* __restrict__ sp = T.fstream + T.nfrow + j0;
+    const int nrow = (int)(T.ab_first[k1] - j0), nleaf = k1 - k0;
+    // (1) the leaf rows' K entries (leaf tables loaded beside them)
+    int32_t lf[2], lw[2];
+    int64_t lo[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = tid + h * FTN;
+      lf[h] = (k < nleaf) ? (int32_t)(T.ab_first[k0 + k] - j0) : 0;
+      lw[h] = (k < nleaf) ? T.ab_wrc[k0 + k] : 0;
+      lo[h] = (k < nleaf) ? T.ab_loff[k0 + k] : 0;
+    }
     for (int q0 = 0; q0 < nrow; q0 += RPT * FTN) {
-      double2 a[RPT], b[RPT];
+      int32_t sa[RPT], sb[RPT];
 #pragma unroll
       for (int u = 0; u < RPT; ++u) {
-        const int q = min(q0 + u * FTN + tid, nrow - 1);
-        a[u] = sq[q];
-        b[u] = sp[q];
+        const int q = q0 + u * FTN + tid;
+        sa[u] = (q < nrow) ? T.ab_src0[j0 + q] : -1;
+        sb[u] = (q < nrow) ? T.ab_src1[j0 + q] : -1;
+      }
+      double va[RPT], vb[RPT];
+#pragma unroll
+      for (int u = 0; u < RPT; ++u) {
+        va[u] = (sa[u] >= 0) ? Kx[sa[u]] : 0.0;
+        vb[u] = (sb[u] >= 0) ? Kx[sb[u]] : 0.0;
       }
 #pragma unroll
       for (int u = 0; u < RPT; ++u) {
         const int q = q0 + u * FTN + tid;
-        if (q < nrow) {
-          LQ[q] = a[u];
-          PQ[q] = b[u];
-        }
+        if (q < nrow) LQ[q] = double2{va[u], vb[u]};
       }
+    }
+    for (int k = tid, h = 0; k < nleaf; k += FTN, ++h) {
+      const int q0 = (h == 0) ? lf[0] : (h == 1 ? lf[1] : (int)(T.ab_first[k0 + k] - j0));
+      const int wrc = (h == 0) ? lw[0] : (h == 1 ? lw[1] : T.ab_wrc[k0 + k]);
+      prow0[k] = q0;
+      pwrc[k] = wrc;
+      ploff[k] = (h == 0) ? lo[0] : (h == 1 ? lo[1] : T.ab_loff[k0 + k]);
+      for (int i = 0; i < (wrc >> 8); ++i) kk[q0 + i] = k;
     }
     __syncthreads();
     lap(0);
+    // (2) per leaf: pivots (+ D and the pivot check)
+    for (int k = tid; k < nleaf; k += FTN) {
+      const int f0 = T.ab_f0[k0 + k], wrc = pwrc[k], w = wrc & 255, rc = wrc >> 8;
+      const int jf = prow0[k];
+      const double d0 = LQ[jf].x;
+      const double f10 = (rc > 1) ? LQ[jf + 1].x : 0.0;
+      const double l10 = (w == 2) ? f10 / d0 : 0.0;
+      const double d1 = (w == 2) ? LQ[jf + 1].y - l10 * f10 : 0.0;
+      pd0[k] = d0;
+      pd1[k] = d1;
+      pf10[k] = f10;
+      D[f0] = d0;
+      if (bad_pivot(d0, tol)) atomicMin(&st->fail_pivot, f0 + 1);
+      if (w == 2) {
+        D[f0 + 1] = d1;
+        if (bad_pivot(d1, tol)) atomicMin(&st->fail_pivot, f0 + 2);
+      }
+    }
+    __syncthreads();
+    lap(1);
+    // (3) per leaf row: L entries (HBM panel for the solves: d on the diagonal, zero above; LDS: l
+    // and l d of the update rows)
+    for (int q = tid; q < nrow; q += FTN) {
+      const int k = kk[q];
+      const int wrc = pwrc[k], w = wrc & 255, rc = wrc >> 8, i = q - prow0[k];
+      const double d0 = pd0[k], d1 = pd1[k], f10 = pf10[k];
+      double* __restrict__ L = arena + ploff[k];
+      if (i >= w) {
+        const double2 a = LQ[q];
+        const double li0 = a.x / d0;
+        const double li1 = (w == 2) ? (a.y - li0 * f10) / d1 : 0.0;
+        LQ[q] = double2{li0, li1};
+        PQ[q] = double2{li0 * d0, li1 * d1};
+        L[i] = li0;
+        if (w == 2) L[i + rc] = li1;
+      } else if (i == 0) {
+        L[0] = d0;
+        if (w == 2) L[rc] = 0.0;
+      } else {  // i == 1, w == 2
+        L[1] = f10 / d0;
+        L[1 + rc] = d1;
+      }
+    }
+    __syncthreads();
+    lap(2);
     // (4) this thread's chunk of the destination-sorted products (entry k at 256 k + tid: each load
     // instruction is coalesced)
     const uint2* __restrict__ P = T.fold_prod + T.fold_poff[bq] + tid;
@@ -3455,15 +3463,13 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
                                                  (S.absorb[s] ? SymbolicPlan::kFoldRowBytes * S.fold_rmax[s] +
                                                                     SymbolicPlan::kFoldLeafBytes * S.fold_lmax[s]
                                                               : 0));
-      // folded leaves (their pre-pass in the level-0 micro launch): K entries read, L entries and the
-      // fold stream (32 B per row) written; the tree launch reads the stream back (32 B per row)
+      // folded leaves: their K entries read, their L entries written
       for (int k = S.absorb[s] ? S.mc_ptr[s] : 0; k < (S.absorb[s] ? S.mc_ptr[s + 1] : 0); ++k) {
         const int c = S.mc_list[k];
         const double rc = S.nrows[c], wc = S.first[c + 1] - S.first[c];
-        fold_bytes_ += 12.0 * (S.asm_ptr[c + 1] - S.asm_ptr[c]) + 8.0 * (rc * wc - wc * (wc - 1) / 2.0) + 32.0 * rc;
-        ftree_bytes_ += 32.0 * rc;
-        fold_alg_ += fact_alg(c);
-        for (int t = 0; t < (int)wc; ++t) fold_flops_ += (rc - t - 1) * (rc - t);
+        ftree_bytes_ += 12.0 * (S.asm_ptr[c + 1] - S.asm_ptr[c]) + 8.0 * (rc * wc - wc * (wc - 1) / 2.0);
+        ftree_alg_ += fact_alg(c);
+        for (int t = 0; t < (int)wc; ++t) ftree_flops_ += (rc - t - 1) * (rc - t);
       }
       // staging model: the stored lower trapezoid of the panel written and the front's scatter list
       // read (ftree_bytes_); SURVEY 8(d)'s algorithmic bytes (B_fact = 8 nnzL + 12 nnzK of the
@@ -3512,10 +3518,6 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         for (size_t k = 0; k < S.mc_list.size(); ++k) lo[k] = S.l_off[S.mc_list[k]];
         ab_loff_.upload(lo);
       }
-      const int64_t nfrow = S.ab_first.empty() ? 0 : S.ab_first.back();
-      fstream_.alloc(std::max<int64_t>(2 * nfrow, 2));
-      T_.fstream = fstream_.p;
-      T_.nfrow = nfrow;
       up32(fold_bptr_, S.fold_bptr);
       up32(fold_bat_, S.fold_bat);
       up64(fold_poff_, S.fold_poff);
@@ -3619,22 +3621,16 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         else
           big.push_back(s);
       }
-      // folded leaf rows (their pre-pass)
-      const int64_t nfold = (phase == 1 && lev == 0 && !S.ab_first.empty()) ? S.ab_first.back() : 0;
-      if (!micro.empty() || nfold > 0) {
-        Launch L{MICRO, 0, (int64_t)sched.size(), (int)micro.size(), (int64_t)micro.size() + nfold};
+      if (!micro.empty()) {
+        Launch L{MICRO, 0, (int64_t)sched.size(), (int)micro.size(), (int64_t)micro.size()};
         for (int f : micro) {
           const double r = S.nrows[f], w = S.first[f + 1] - S.first[f];
           L.bytes += 8.0 * (r * w + (r - w) * (r - w + 1) / 2 + w) + 16.0 * (S.asm_ptr[f + 1] - S.asm_ptr[f]);
           L.alg += fact_alg(f);
           for (int t = 0; t < (int)w; ++t) L.flops += (r - t - 1) * (r - t);
         }
-        L.bytes += fold_bytes_;
-        L.alg += fold_alg_;
-        L.flops += fold_flops_;
         out.push_back(L);
         sched.insert(sched.end(), micro.begin(), micro.end());
-        if (micro.empty()) sched.push_back(0);  // the list pointer stays valid
       }
       for (int c = 0; c < 4; ++c)
         if (!cls[c].empty()) {
@@ -4137,8 +4133,8 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
         break;
       case MICRO:
         TIMED(KK_TINY, L.bytes, L.alg, L.flops,
-              (k_micro_factor<<<(unsigned)(cdiv(L.nf, NT / MG) + cdiv(L.items - L.nf, NT)), NT, 0, s>>>(
-                  T_, list, L.nf, L.items - L.nf, Kx, arena_, D_, st_, pivot_tol)));
+              (k_micro_factor<<<(unsigned)cdiv(L.items, NT / MG), NT, 0, s>>>(T_, list, (int)L.items, Kx, arena_, D_,
+                                                                             st_, pivot_tol)));
         break;
       case SMALL32:
         TIMED(KK_TINY, L.bytes, L.alg, L.flops,

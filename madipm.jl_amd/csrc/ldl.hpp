@@ -66,10 +66,6 @@ struct FrontTab {
   const int32_t* fold_lmax;
   const uint2* fold_prod;
   const uint8_t* fs_img;  // 1: fscratch holds the front's LDS image (tree fronts), else ld r
-  // fold stream (written by the folded leaves' pre-pass, read by k_fact_tree's fold): per folded leaf
-  // row j (ab_first numbering) fstream[j] = (l0, l1), fstream[nfrow + j] = (l0 d0, l1 d1)
-  double2* fstream;
-  int64_t nfrow;
   int schur_defer;  // in-LDS factorisation: update block U in one pass after the pivots (MADIPM_SCHUR_DEFER)
   int f16r;         // 16-pivot diagonal blocks factorised in registers (factor16r; MADIPM_F16R=0: factor16s)
 };
@@ -319,8 +315,6 @@ class LDLSolver : public LinSolver {
   int nftree_ = 0, ftree_lds_ = 0, fepoch_ = 0;
   bool ftree_checked_ = false;
   double ftree_bytes_ = 0, ftree_flops_ = 0, ftree_alg_ = 0;
-  double fold_bytes_ = 0, fold_flops_ = 0, fold_alg_ = 0;  // the folded leaves' pre-pass (micro launch)
-  DBuf<double2> fstream_;
   DBuf<int32_t> ft_order_, ft_dptr_, ft_dep_, fflags_, fcnt_;
   DBuf<int64_t> fdbg_, ab_first_, ab_loff_, fold_poff_;
   DBuf<int32_t> ab_src0_, ab_src1_, ab_k_, ab_f0_, ab_wrc_, fold_bptr_, fold_bat_, fold_plen_, fold_rmax_, fold_lmax_;

@@ -153,14 +153,24 @@ struct OrderAnalysis {
 
 void analyse_order(int N, const int64_t* colptr, const int32_t* rowval, std::vector<int32_t> perm,
                    OrderAnalysis& A) {
+  const bool timing = std::getenv("MADIPM_SYMBOLIC_TIMING") != nullptr;
+  auto t_last = std::chrono::steady_clock::now();
+  auto stamp = [&](const char* what) {
+    if (!timing) return;
+    const auto t = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "  analyse_order %-20s %9.3f s\n", what, std::chrono::duration<double>(t - t_last).count());
+    t_last = t;
+  };
   A.pinv.assign(N, -1);
   for (int k = 0; k < N; ++k) {
     MADIPM_REQUIRE(perm[k] >= 0 && perm[k] < N && A.pinv[perm[k]] == -1, "ordering is not a permutation");
     A.pinv[perm[k]] = k;
   }
   build_pattern(N, colptr, rowval, A.pinv, A.P);
+  stamp("pattern");
   std::vector<int32_t> post;
   etree(N, A.P, A.parent);
+  stamp("etree");
   postorder(N, A.parent, post);
   bool ident = true;  // the ordering is already a postorder (e.g. natural order of a QP's K2): no relabel
   for (int k = 0; k < N && ident; ++k) ident = post[k] == k;
@@ -173,7 +183,9 @@ void analyse_order(int N, const int64_t* colptr, const int32_t* rowval, std::vec
     etree(N, A.P, A.parent);
   }
   A.perm.swap(perm);
+  stamp("postorder/relabel");
   column_counts(N, A.P, A.parent, A.cnt);
+  stamp("column counts");
   A.flops = 0.0;
   for (int64_t c : A.cnt) A.flops += (double)(c - 1) * (double)(c + 2);
 }

@@ -111,13 +111,12 @@ struct SymbolicPlan {
   // (F(i, j) -= l(q1) . p(q2) over the two leaf columns, p = l d) are sorted by LDS destination
   // (leaf order within one destination), cut into kFoldThreads chunks at destination boundaries and
   // stored interleaved (entry k of thread t at fold_poff + kFoldThreads k + t) so each load instruction
-  // is coalesced.  The leaves' pivots, L panels and (l, l d) rows come from a pre-pass in the level-0
-  // micro launch (the fold stream); the tree front copies its batch's rows from it.
+  // is coalesced.
   static constexpr int64_t kFactTreeLdsMax = 150 * 1024;  // dynamic LDS of k_fact_tree
   static constexpr int64_t kFoldLdsMax = 148 * 1024;      // fold front + leaf rows (k_fact_tree's
                                                           // static LDS is ~10.4 KB of the CU's 160 KB)
-  static constexpr int kFoldRowBytes = 32;                // LDS per leaf row: (l0, l1), (l0 d0, l1 d1)
-  static constexpr int kFoldLeafBytes = 0;                // per leaf: nothing (the pre-pass formed the pivots)
+  static constexpr int kFoldRowBytes = 36;                // LDS per leaf row: (l0, l1), (l0 d0, l1 d1), leaf
+  static constexpr int kFoldLeafBytes = 48;               // LDS per leaf: d0, d1, f10, L offset, row0, w | rc
   static constexpr uint32_t kFoldPadDst = 0xffffu;        // destination of a padding entry
   std::vector<uint8_t> absorb;        // front folds its micro leaves
   std::vector<uint8_t> fold_pk;       // fold front stored packed in LDS (to leave room for the leaf rows)
