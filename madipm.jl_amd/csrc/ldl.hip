@@ -1872,18 +1872,18 @@ __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __
   const double* __restrict__ Dp = D + f0 + k0;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int qr = (wv >> 1) * 32, qc = (wv & 1) * 32;
-  // all global loads of the operands first (one latency), then the LDS stores
-  double wl[16], ll[16];
+  // all global loads of the operands first (one latency), from clamped addresses (a predicated load
+  // compiles into a branch with a wait inside), masked at the LDS store
+  double wl[16], ll[16], dk[16];
+  const int ri = min(I0 + lane, r - 1), rj = min(J0 + lane, r - 1);
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
-    const int kk = wv + 4 * e;
+    const int kk = min(wv + 4 * e, kw - 1);
     const int64_t col = (int64_t)(k0 + kk) * r;
-    wl[e] = (kk < kw && I0 + lane < r) ? F[(I0 + lane) + col] : 0.0;
-    ll[e] = (kk < kw && J0 + lane < r) ? F[(J0 + lane) + col] : 0.0;
+    wl[e] = F[ri + col];
+    ll[e] = F[rj + col];
+    dk[e] = Dp[kk];
   }
-  double dk[16];
-#pragma unroll
-  for (int e = 0; e < 16; ++e) dk[e] = (wv + 4 * e < kw) ? Dp[wv + 4 * e] : 0.0;
   // C tile prefetch (its latency overlaps the MFMA loop)
   double c[2][2][4];
 #pragma unroll
@@ -1892,15 +1892,15 @@ __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __
     for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int i = I0 + qr + bi * 16 + (lane & 15);
-        const int j = J0 + qc + bj * 16 + (lane >> 4) + 4 * g;
-        c[bj][bi][g] = (i < r && j < r && i >= j) ? F[i + (int64_t)j * r] : 0.0;
+        const int i = min(I0 + qr + bi * 16 + (lane & 15), r - 1);
+        const int j = min(J0 + qc + bj * 16 + (lane >> 4) + 4 * g, r - 1);
+        c[bj][bi][g] = F[i + (int64_t)j * r];  // masked at the store
       }
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const int kk = wv + 4 * e;
-    Wt[kk * LDT + lane] = wl[e] * dk[e];
-    Lt[kk * LDT + lane] = ll[e];
+    Wt[kk * LDT + lane] = (kk < kw && I0 + lane < r) ? wl[e] * dk[e] : 0.0;
+    Lt[kk * LDT + lane] = (kk < kw && J0 + lane < r) ? ll[e] : 0.0;
   }
   __syncthreads();
   dbl4 acc[2][2];
@@ -2010,7 +2010,10 @@ __global__ __launch_bounds__(NT) void k_lb_build(const SymbolicPlan::LBGroup* __
 // 16 columns at a time (double-buffered, operands [k][row] with a padded stride).  One launch per
 // K-chunk keeps the chunk of W (m x 2048) resident in the Infinity Cache across all tiles.
 constexpr int SYT = 128, SYK = 16, SYLD = SYT + 16;
-__global__ __launch_bounds__(NT) void k_lb_syrk(const double* __restrict__ W, const double* __restrict__ dinv, int m,
+#ifndef SYRK_WAVES
+#define SYRK_WAVES 2  // waves per SIMD the register budget is cut for (2: accumulators in VGPRs, 2 WGs per CU)
+#endif
+__global__ __launch_bounds__(NT, SYRK_WAVES) void k_lb_syrk(const double* __restrict__ W, const double* __restrict__ dinv, int m,
                                                 int k0, int k1, const int32_t* __restrict__ gpos,
                                                 double* __restrict__ F, int ld) {
   __shared__ __attribute__((aligned(16))) double As[2][SYK * SYLD];  // (W D^{-1})[I rows]
@@ -2030,26 +2033,31 @@ __global__ __launch_bounds__(NT) void k_lb_syrk(const double* __restrict__ W, co
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
-  double ra[8], rb[8];
+  // the next chunk's operands: loads from clamped addresses, issued together and consumed (masked,
+  // scaled) only at the LDS store after the current chunk's MFMAs — a predicated load compiled into a
+  // branch with a wait inside, exposing 8 memory latencies per chunk (SQ_WAIT_ANY 55 % of wave cycles)
+  double ra[8], rb[8], rd[8];
   auto gload = [&](int kb) {
+    const int ri = min(I0 + lr, m - 1), rj = min(J0 + lr, m - 1);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      const int k = kb + lk + 2 * q;
-      const bool ok = k < k1;
-      const int64_t col = (int64_t)(ok ? k : k0) * m;
-      ra[q] = (ok && I0 + lr < m) ? W[(I0 + lr) + col] * dinv[ok ? k : k0] : 0.0;
-      rb[q] = (ok && J0 + lr < m) ? W[(J0 + lr) + col] : 0.0;
+      const int kc = min(kb + lk + 2 * q, k1 - 1);
+      const int64_t col = (int64_t)kc * m;
+      ra[q] = W[ri + col];
+      rb[q] = W[rj + col];
+      rd[q] = dinv[kc];
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int kb, int buf) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      As[buf][(lk + 2 * q) * SYLD + lr] = ra[q];
-      Bs[buf][(lk + 2 * q) * SYLD + lr] = rb[q];
+      const bool ok = kb + lk + 2 * q < k1;
+      As[buf][(lk + 2 * q) * SYLD + lr] = (ok && I0 + lr < m) ? ra[q] * rd[q] : 0.0;
+      Bs[buf][(lk + 2 * q) * SYLD + lr] = (ok && J0 + lr < m) ? rb[q] : 0.0;
     }
   };
   gload(k0);
-  sstore(0);
+  sstore(k0, 0);
   __syncthreads();
   int buf = 0;
   for (int kb = k0; kb < k1; kb += SYK) {
@@ -2070,21 +2078,37 @@ __global__ __launch_bounds__(NT) void k_lb_syrk(const double* __restrict__ W, co
         for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[a], fb[b], acc[a][b], 0, 0, 0);
     }
     if (more) {
-      sstore(buf ^ 1);
+      sstore(kb + SYK, buf ^ 1);
       __syncthreads();
       buf ^= 1;
     }
   }
-  // acc[a][b][g]: row i = I0 + wm + 16 b + (lane & 15), column j = J0 + wn + 16 a + (lane >> 4) + 4 g
+  // acc[a][b][g]: row i = I0 + wm + 16 b + (lane & 15), column j = J0 + wn + 16 a + (lane >> 4) + 4 g.
+  // F read-modify-written 16 entries at a time: the reads from clamped addresses, all in flight
+  // together, the writes masked (a masked read-modify-write per entry compiled into a branch with a
+  // wait inside: 64 serial memory latencies per lane)
+  int gi[4], gj[4][4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) gi[b] = gpos[min(I0 + wm + 16 * b + (lane & 15), m - 1)];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) gj[a][g] = gpos[min(J0 + wn + 16 * a + (lane >> 4) + 4 * g, m - 1)];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    double fv[4][4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) fv[b][g] = F[gi[b] + (int64_t)gj[a][g] * ld];
 #pragma unroll
     for (int b = 0; b < 4; ++b)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int i = I0 + wm + 16 * b + (lane & 15), j = J0 + wn + 16 * a + (lane >> 4) + 4 * g;
-        if (i < m && j <= i) F[gpos[i] + (int64_t)gpos[j] * ld] -= acc[a][b][g];
+        if (i < m && j <= i) F[gi[b] + (int64_t)gj[a][g] * ld] = fv[b][g] - acc[a][b][g];
       }
+  }
 }
 
 // forward: s_j = b(c_j) / d_j, t = W s (two passes: column chunks of LBF_COLS -> partials, then the

@@ -89,7 +89,7 @@ enum { KKT_K2 = 0, KKT_K25 = 1, KKT_NORMAL = 2 };
 
 enum { OP_SUM = 0, OP_MAX = 1, OP_MIN = 2 };
 
-__device__ __forceinline__ double nmax(double a, double b) { return (b > a || b != b) ? b : a; }
+__device__ __forceinline__ double nmax(double a, double b) { return ((b > a) | (b != b)) ? b : a; }
 __device__ __forceinline__ double comb(double a, double b, int op) {
   return op == OP_SUM ? a + b : (op == OP_MAX ? nmax(a, b) : fmin(a, b));
 }
@@ -124,10 +124,9 @@ __device__ void block_partials(double (&v)[NV], const int (&ops)[NV], double* pa
 // LAST index wins.  As a total order, (value ascending, index descending): associative, so any
 // combine tree gives the fold's answer.  The init element is index -1 (below every real index).
 __device__ __forceinline__ void amin_upd(double& v, int& ix, double nv, int ni) {
-  if (nv < v || (nv == v && ni > ix)) {
-    v = nv;
-    ix = ni;
-  }
+  const bool take = (nv < v) | ((nv == v) & (ni > ix));  // no short circuit: selects, not branches
+  v = take ? nv : v;
+  ix = take ? ni : ix;
 }
 
 #define GRID_LOOP(i, N) for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < (N); i += (int64_t)gridDim.x * blockDim.x)
@@ -840,14 +839,18 @@ __device__ void fin_alpha_store(const DV& D, const FinParams& P, double (&a)[4],
   }
 }
 
-__device__ __forceinline__ void fin_ops(int kind, int (&ops)[8]) {
-  for (int k = 0; k < 8; ++k) ops[k] = OP_SUM;
-  switch (kind) {
-    case FIN_RESID: ops[0] = ops[1] = ops[2] = OP_MAX; break;
-    case FIN_TERM: ops[0] = ops[1] = ops[2] = OP_MAX; break;
-    case FIN_ZINIT: for (int k = 0; k < 4; ++k) ops[k] = OP_MIN; break;
-    default: break;
-  }
+// value slots and combine operation of each finaliser kind (compile time: the k_final instance's
+// combines are branch-free)
+constexpr int fin_nv(int kind) {
+  return kind == FIN_RESID ? 3
+         : kind == FIN_TERM ? 6
+         : (kind == FIN_MU_PRED || kind == FIN_MU_FULL || kind == FIN_MU_GONDZIO || kind == FIN_ZINIT) ? 4
+         : kind == FIN_ZSHIFT1 ? 8
+         : (kind == FIN_EVAL || kind == FIN_ZSHIFT2) ? 1
+                                                     : 0;
+}
+__host__ __device__ constexpr int fin_op(int kind, int k) {
+  return (kind == FIN_RESID || (kind == FIN_TERM && k < 3)) ? OP_MAX : (kind == FIN_ZINIT ? OP_MIN : OP_SUM);
 }
 
 // the scalar logic of each finaliser kind on the reduced values res[] (thread 0 of the last workgroup)
@@ -938,12 +941,14 @@ __device__ void fin_tail(const DV& D, int kind, const FinParams& P, const double
   }
 }
 
-// Instantiated per (value slots NV, fused step test AL, fused objective EV) so that a thread holds
-// exactly the partials of its launch (launch_final picks the instance).  Level-2 partials and the
+// Instantiated per (finaliser kind KIND, fused step test AL, fused objective EV) so that a thread holds
+// exactly the partials of its launch and every combine is a compile-time operation (launch_final
+// picks the instance).  Level-2 partials and the
 // ticket live past the NPART x MAXB partials (part_): L2 = part + NPART MAXB, NL2 x FG doubles, then the
 // ticket counter (reset by the last workgroup).
-template <int NV, bool AL, bool EV>
+template <int KIND, bool AL, bool EV>
 __global__ __launch_bounds__(FT) void k_final(DV D, int kind, FinParams P) {
+  constexpr int NV = fin_nv(KIND);
   __shared__ double res[NL2];
   __shared__ int s_last;
   DevState* st = D.st;
@@ -969,8 +974,6 @@ __global__ __launch_bounds__(FT) void k_final(DV D, int kind, FinParams P) {
   for (int k = 0; k < NA; ++k) asm volatile("" : "+v"(aq[k]));
   if (EV) asm volatile("" : "+v"(eq));
   if (P.dbg && threadIdx.x == 0 && g == 0) P.dbg[4] = (int64_t)wall_clock64();  // loads returned
-  int ops[8];
-  fin_ops(kind, ops);
   // level 1: this workgroup's blocks — every value's shuffle tree in lockstep (one latency chain for all
   // of them, not one per value), then the waves in order
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -987,7 +990,7 @@ __global__ __launch_bounds__(FT) void k_final(DV D, int kind, FinParams P) {
   double e1 = (EV && b < P.nb_eval) ? eq : 0.0;
   for (int o = 32; o > 0; o >>= 1) {
 #pragma unroll
-    for (int k = 0; k < NV; ++k) w1[k] = comb(w1[k], __shfl_down(w1[k], o, 64), ops[k]);
+    for (int k = 0; k < NV; ++k) w1[k] = comb(w1[k], __shfl_down(w1[k], o, 64), fin_op(KIND, k));
     if (AL)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -1016,7 +1019,7 @@ __global__ __launch_bounds__(FT) void k_final(DV D, int kind, FinParams P) {
     for (int k = 0; k < NV; ++k) {
       double a = shv[k][0];
 #pragma unroll
-      for (int w = 1; w < FT / 64; ++w) a = comb(a, shv[k][w], ops[k]);
+      for (int w = 1; w < FT / 64; ++w) a = comb(a, shv[k][w], fin_op(KIND, k));
       st_sc1(L2 + k * FG + g, a);
     }
     if (AL)
@@ -1057,7 +1060,7 @@ __global__ __launch_bounds__(FT) void k_final(DV D, int kind, FinParams P) {
   if (t < NV) {
     double a = l2s[t * FG];
 #pragma unroll
-    for (int w = 1; w < FG; ++w) a = comb(a, l2s[t * FG + w], ops[t]);
+    for (int w = 1; w < FG; ++w) a = comb(a, l2s[t * FG + w], fin_op(KIND, t));
     res[t] = a;
   } else if (AL && t >= 8 && t < 12) {
     double a = l2s[t * FG];
@@ -1100,26 +1103,26 @@ __global__ __launch_bounds__(FT) void k_final(DV D, int kind, FinParams P) {
 // the k_final instance of a finaliser launch (slots, fused step test, fused objective)
 void launch_final(const DV& D, int kind, const FinParams& P, hipStream_t s) {
   switch (kind) {
-    case FIN_ALPHA: k_final<0, true, false><<<FG, FT, 0, s>>>(D, kind, P); break;
+    case FIN_ALPHA: k_final<FIN_ALPHA, true, false><<<FG, FT, 0, s>>>(D, kind, P); break;
     case FIN_RESID:
       if (P.nb_alpha > 0)
-        k_final<3, true, false><<<FG, FT, 0, s>>>(D, kind, P);
+        k_final<FIN_RESID, true, false><<<FG, FT, 0, s>>>(D, kind, P);
       else
-        k_final<3, false, false><<<FG, FT, 0, s>>>(D, kind, P);
+        k_final<FIN_RESID, false, false><<<FG, FT, 0, s>>>(D, kind, P);
       break;
-    case FIN_MU_PRED:
-    case FIN_MU_FULL:
-    case FIN_MU_GONDZIO:
-    case FIN_ZINIT: k_final<4, false, false><<<FG, FT, 0, s>>>(D, kind, P); break;
-    case FIN_EVAL:
-    case FIN_ZSHIFT2: k_final<1, false, false><<<FG, FT, 0, s>>>(D, kind, P); break;
+    case FIN_MU_PRED: k_final<FIN_MU_PRED, false, false><<<FG, FT, 0, s>>>(D, kind, P); break;
+    case FIN_MU_FULL: k_final<FIN_MU_FULL, false, false><<<FG, FT, 0, s>>>(D, kind, P); break;
+    case FIN_MU_GONDZIO: k_final<FIN_MU_GONDZIO, false, false><<<FG, FT, 0, s>>>(D, kind, P); break;
+    case FIN_ZINIT: k_final<FIN_ZINIT, false, false><<<FG, FT, 0, s>>>(D, kind, P); break;
+    case FIN_EVAL: k_final<FIN_EVAL, false, false><<<FG, FT, 0, s>>>(D, kind, P); break;
+    case FIN_ZSHIFT2: k_final<FIN_ZSHIFT2, false, false><<<FG, FT, 0, s>>>(D, kind, P); break;
     case FIN_TERM:
       if (P.nb_eval > 0)
-        k_final<6, false, true><<<FG, FT, 0, s>>>(D, kind, P);
+        k_final<FIN_TERM, false, true><<<FG, FT, 0, s>>>(D, kind, P);
       else
-        k_final<6, false, false><<<FG, FT, 0, s>>>(D, kind, P);
+        k_final<FIN_TERM, false, false><<<FG, FT, 0, s>>>(D, kind, P);
       break;
-    case FIN_ZSHIFT1: k_final<8, false, false><<<FG, FT, 0, s>>>(D, kind, P); break;
+    case FIN_ZSHIFT1: k_final<FIN_ZSHIFT1, false, false><<<FG, FT, 0, s>>>(D, kind, P); break;
     default: throw Error("k_final: unknown finaliser kind", -2);
   }
 }
