@@ -479,17 +479,19 @@ __global__ __launch_bounds__(NT) void k_asm_chunks(const int64_t* __restrict__ g
   if (c >= c0 + n) return;
   const int64_t p0 = gchunk[c], p1 = gchunk[c + 1];
   constexpr int KC = SymbolicPlan::kChunk;
+  // every index, then every value operand in flight before the sum: unconditional loads (clamped
+  // index, selected source pointer), masked at the sum — predicated loads compiled into branches
+  // with a wait each
   int64_t q[KC];
 #pragma unroll
-  for (int u = 0; u < KC; ++u) q[u] = (p0 + u < p1) ? (int64_t)gsrc[p0 + u] : INT64_MAX;
-  // every value operand in flight before the sum
+  for (int u = 0; u < KC; ++u) q[u] = (int64_t)gsrc[min(p0 + u, max(p1 - 1, p0))];
   double x[KC];
 #pragma unroll
-  for (int u = 0; u < KC; ++u) x[u] = (q[u] == INT64_MAX) ? 0.0 : ((q[u] < 0) ? Kx[~q[u]] : arena[q[u]]);
+  for (int u = 0; u < KC; ++u) x[u] = *((q[u] < 0) ? Kx + ~q[u] : arena + q[u]);
   double v = 0.0;
 #pragma unroll
   for (int u = 0; u < KC; ++u)
-    if (q[u] != INT64_MAX) v += x[u];
+    if (p0 + u < p1) v += x[u];
   part[c] = v;
 }
 
@@ -2903,18 +2905,19 @@ __global__ __launch_bounds__(NT) void k_fwd_leaves(const SolveLeaf* __restrict__
   const SolveLeaf L = lv[k];
   const int r = L.rw & 255, w = L.rw >> 8, u = r - w;
   const double* __restrict__ P = arena + L.loff;
+  // unconditional loads from clamped in-range addresses (a leaf with no update rows reads its own
+  // pivot entry; the row table is padded by one record), masked at the use
   double p[LROWS], q[LROWS];
   int d[LROWS];
 #pragma unroll
   for (int m = 0; m < LROWS; ++m) {
-    const int a = min(j + LPL * m, u - 1);
-    const bool ok = u > 0;
-    p[m] = ok ? P[w + a] : 0.0;
-    q[m] = (ok && w == 2) ? P[w + a + r] : 0.0;
-    d[m] = ok ? lrow[L.roff + a].x : 0;
+    const int a = max(min(j + LPL * m, u - 1), 0);
+    p[m] = P[min(w + a, r - 1)];
+    q[m] = P[(w == 2) ? min(w + a, r - 1) + r : 0];
+    d[m] = lrow[L.roff + a].x;
   }
-  const double b0 = b[L.p0];
-  const double b1 = (w == 2) ? b[L.p1] : 0.0, l10 = (w == 2) ? P[1] : 0.0;
+  const double b0 = b[L.p0], b1r = b[(w == 2) ? L.p1 : L.p0], l10r = P[1 < r ? 1 : 0];
+  const double b1 = (w == 2) ? b1r : 0.0, l10 = (w == 2) ? l10r : 0.0;
   const double x0 = b0, x1 = (w == 2) ? b1 - l10 * x0 : 0.0;
   if (j == 0) {
     xi[L.f0] = x0;
@@ -2922,7 +2925,7 @@ __global__ __launch_bounds__(NT) void k_fwd_leaves(const SolveLeaf* __restrict__
   }
 #pragma unroll
   for (int m = 0; m < LROWS; ++m)
-    if (j + LPL * m < u) gbuf[d[m]] = (0.0 - p[m] * x0) - q[m] * x1;
+    if (j + LPL * m < u) gbuf[d[m]] = (0.0 - p[m] * x0) - (w == 2 ? q[m] : 0.0) * x1;
 }
 
 __global__ __launch_bounds__(NT) void k_bwd_leaves(const SolveLeaf* __restrict__ lv, int nleaf,
@@ -2935,18 +2938,21 @@ __global__ __launch_bounds__(NT) void k_bwd_leaves(const SolveLeaf* __restrict__
   const SolveLeaf L = lv[k];
   const int r = L.rw & 255, w = L.rw >> 8, u = r - w;
   const double* __restrict__ P = arena + L.loff;
+  // unconditional loads from clamped in-range addresses, masked at the use (as k_fwd_leaves)
   int src[LROWS];
 #pragma unroll
-  for (int m = 0; m < LROWS; ++m) src[m] = (u > 0) ? lrow[L.roff + min(j + LPL * m, u - 1)].y : 0;
+  for (int m = 0; m < LROWS; ++m) src[m] = lrow[L.roff + max(min(j + LPL * m, u - 1), 0)].y;
   double p[LROWS], q[LROWS], x[LROWS];
 #pragma unroll
   for (int m = 0; m < LROWS; ++m) {
-    const int a = min(j + LPL * m, u - 1);
-    const bool ok = u > 0;
-    p[m] = ok ? P[w + a] : 0.0;
-    q[m] = (ok && w == 2) ? P[w + a + r] : 0.0;
-    x[m] = ok ? xi[src[m]] : 0.0;  // the tree fronts' final x (previous launch)
+    const int a = max(min(j + LPL * m, u - 1), 0);
+    p[m] = P[min(w + a, r - 1)];
+    q[m] = P[(w == 2) ? min(w + a, r - 1) + r : 0];
+    x[m] = xi[src[m]];  // the tree fronts' final x (previous launch)
   }
+  // the pivots' own entries, for lane 0's tail (loaded with the rest)
+  const int f1 = L.f0 + (w == 2 ? 1 : 0);
+  const double l10r = P[1 < r ? 1 : 0], xf0 = xi[L.f0], df0 = D[L.f0], xf1 = xi[f1], df1 = D[f1];
   double a0 = 0.0, a1 = 0.0;
 #pragma unroll
   for (int m = 0; m < LROWS; ++m)
@@ -2960,9 +2966,9 @@ __global__ __launch_bounds__(NT) void k_bwd_leaves(const SolveLeaf* __restrict__
   a0 += __shfl_xor(a0, 2, LPL);
   a1 += __shfl_xor(a1, 2, LPL);
   if (j != 0) return;
-  const double l10 = (w == 2) ? P[1] : 0.0;
-  const double v1 = (w == 2) ? xi[L.f0 + 1] / D[L.f0 + 1] - a1 : 0.0;
-  const double v0 = xi[L.f0] / D[L.f0] - a0 - l10 * v1;
+  const double l10 = (w == 2) ? l10r : 0.0;
+  const double v1 = (w == 2) ? xf1 / df1 - a1 : 0.0;
+  const double v0 = xf0 / df0 - a0 - l10 * v1;
   xi[L.f0] = v0;
   out[L.p0] = v0;
   if (w == 2) {
@@ -3930,7 +3936,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       up(tpar_, par);
       up(tl_ptr_, lptr);
       tleaf_.upload(lv.empty() ? std::vector<SolveLeaf>(1) : lv);
-      tlrow_.upload(lrow.empty() ? std::vector<int2>(1) : lrow);
+      lrow.push_back(int2{0, 0});  // padding: the leaf kernels' clamped loads of a leaf without update rows
+      tlrow_.upload(lrow);
       nsleaf_ = (int64_t)lv.size();
       for (const SolveLeaf& L : lv) {
         const double r = L.rw & 255, w = L.rw >> 8;

@@ -147,7 +147,15 @@ __device__ __forceinline__ double gdot(const DCsr& A, int64_t row, const double*
   const int gl = threadIdx.x & (G - 1);
   double s = 0.0;
   const int64_t q1 = A.rp[row + 1];
-  for (int64_t q = A.rp[row] + gl; q < q1; q += G) s += A.v[q] * x[A.ci[q]];
+  // two entries per lane and trip, both issued before either is summed (clamped index, the second
+  // masked): the gathers of consecutive trips no longer wait for each other; same summation order
+  for (int64_t q = A.rp[row] + gl; q < q1; q += 2 * G) {
+    const int64_t qb = min(q + G, q1 - 1);
+    const double va = A.v[q], vb = A.v[qb];
+    const double xa = x[A.ci[q]], xb = x[A.ci[qb]];
+    s = fma(va, xa, s);
+    s = fma((q + G < q1) ? vb : 0.0, xb, s);
+  }
 #pragma unroll
   for (int o = G / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, G);
   return s;
@@ -365,47 +373,56 @@ __global__ __launch_bounds__(NT) void k_rhs(DV D, int mode, double mu_g, int res
     D.st->max_res_ratio = 0.0;
     if (reset == 2) D.st->nan_flag = 0;
   }
+  // every operand of the row loaded first and unconditionally (clamped indices; the bound blocks'
+  // entries right after the bound positions), the mode / bound tests applied afterwards: behind
+  // `if (kl >= 0)` the loads were dependent round trips of their own
+  const int nub = D.nub;
   GRID_LOOP(i, n + m) {
     if (i < n) {
+      const int kl = D.lbpos[i], ku = D.ubpos[i];
+      const double f = D.f[i], zl = D.zl[i], zu = D.zu[i], jl = D.jacl[i];
+      const double x = D.x[i], xl = D.xl[i], xu = D.xu[i], di = D.d[i];
+      const int kl0 = kl >= 0 ? kl : 0, ku0 = ku >= 0 ? ku : 0;
+      const double ldg = D.l_diag[kl0], udg = D.u_diag[ku0], clb = D.corr_lb[kl0], cub = D.corr_ub[ku0];
+      const double dzl = D.d[nlb > 0 ? n + m + kl0 : 0], dzu = D.d[nub > 0 ? n + m + nlb + ku0 : 0];
       double px;
       if (mode == RHS_INIT_PRIMAL)
         px = 0.0;
       else if (mode == RHS_INIT_DUAL)
-        px = -D.f[i];
+        px = -f;
       else
-        px = -D.f[i] + D.zl[i] - D.zu[i] - D.jacl[i];
+        px = -f + zl - zu - jl;
       double dr = px;
-      const int kl = D.lbpos[i], ku = D.ubpos[i];
       const bool full = mode >= RHS_PRED;
       if (kl >= 0) {
         double pz = 0.0;
         if (full) {
-          pz = (D.xl[i] - D.x[i]) * D.zl[i];
+          pz = (xl - x) * zl;
           if (mode == RHS_CORR) {
-            const double corr = D.d[i] * D.d[n + m + kl];
+            const double corr = di * dzl;
             D.corr_lb[kl] = corr;
             pz = pz + mu - corr;
           } else if (mode == RHS_GONDZIO) {
-            pz = pz + mu - D.corr_lb[kl];
+            pz = pz + mu - clb;
           }
         }
         D.p[n + m + kl] = pz;
-        dr -= pz / D.l_diag[kl];
+        dr -= pz / ldg;
       }
       if (ku >= 0) {
         double pz = 0.0;
         if (full) {
-          pz = (D.xu[i] - D.x[i]) * D.zu[i];
+          pz = (xu - x) * zu;
           if (mode == RHS_CORR) {
-            const double corr = D.d[i] * D.d[n + m + nlb + ku];
+            const double corr = di * dzu;
             D.corr_ub[ku] = corr;
             pz = pz - mu - corr;
           } else if (mode == RHS_GONDZIO) {
-            pz = pz - mu - D.corr_ub[ku];
+            pz = pz - mu - cub;
           }
         }
         D.p[n + m + nlb + ku] = pz;
-        dr -= pz / D.u_diag[ku];
+        dr -= pz / udg;
       }
       D.p[i] = px;
       D.d[i] = (D.kkt == KKT_K25) ? dr * D.sk[i] : dr;  // K2.5: right-hand side S r1
@@ -476,40 +493,42 @@ __global__ __launch_bounds__(NT) void k_residual(DV D, double dw, double dc, int
   const bool lead = (threadIdx.x & (G - 1)) == 0;
   double wmax = 0.0, pmax = 0.0, dxmax = 0.0;
   GROUP_LOOP_B(i, n + m, G, (int)blockIdx.x, nres) {
+    // the row's own entries and its bound blocks do not depend on the dot products: loaded first,
+    // unconditionally (clamped indices; every lane of the group, one cache line), so their latency
+    // overlaps the gathers — behind `if (!lead)` / `if (kl >= 0)` they were two more round trips
+    const double dxi = D.d[i], pi = D.p[i];
+    const int kl = (i < n) ? D.lbpos[i] : -1, ku = (i < n) ? D.ubpos[i] : -1;
+    const int kl0 = kl >= 0 ? kl : 0, ku0 = ku >= 0 ? ku : 0;
+    const double pl = D.p[kl >= 0 ? n + m + kl : i], llo = D.l_lower[kl0], ldi = D.l_diag[kl0];
+    const double pu = D.p[ku >= 0 ? n + m + nlb + ku : i], ulo = D.u_lower[ku0], udi = D.u_diag[ku0];
     if (i < n) {
       const double hj = gdot<G>(D.H, i, D.d) + gdot<G>(D.JT, i, D.d + n);
       if (!lead) continue;
-      const double dx = D.d[i];
+      const double dx = dxi;
       double kv = hj + dw * dx;
-      const int kl = D.lbpos[i], ku = D.ubpos[i];
       if (kl >= 0) {
-        const double pl = D.p[n + m + kl];
-        const double dzl = (-pl + D.l_lower[kl] * dx) / D.l_diag[kl];
+        const double dzl = (-pl + llo * dx) / ldi;
         D.d[n + m + kl] = dzl;
         kv -= dzl;
-        const double wl = pl - (dx * D.l_lower[kl] - dzl * D.l_diag[kl]);
+        const double wl = pl - (dx * llo - dzl * ldi);
         wmax = nmax(wmax, fabs(wl));
         pmax = nmax(pmax, fabs(pl));
       }
       if (ku >= 0) {
-        const double pu = D.p[n + m + nlb + ku];
-        const double dzu = (pu - D.u_lower[ku] * dx) / D.u_diag[ku];
+        const double dzu = (pu - ulo * dx) / udi;
         D.d[n + m + nlb + ku] = dzu;
         kv += dzu;
-        const double wu = pu - (dx * D.u_lower[ku] + dzu * D.u_diag[ku]);
+        const double wu = pu - (dx * ulo + dzu * udi);
         wmax = nmax(wmax, fabs(wu));
         pmax = nmax(pmax, fabs(pu));
       }
-      const double pi = D.p[i];
       wmax = nmax(wmax, fabs(pi - kv));
       pmax = nmax(pmax, fabs(pi));
       dxmax = nmax(dxmax, fabs(dx));
     } else {
       const double jd = gdot<G>(D.J, i - n, D.d);
       if (!lead) continue;
-      const double dy = D.d[i];
-      const double kv = jd + dc * dy;
-      const double pi = D.p[i];
+      const double kv = jd + dc * dxi;
       wmax = nmax(wmax, fabs(pi - kv));
       pmax = nmax(pmax, fabs(pi));
     }
@@ -527,20 +546,27 @@ __device__ void alpha_body(const DV& D, int mode, double tau_param, int base, in
   const double tau = alpha_tau(D, mode, tau_param);
   double v[4] = {INF, INF, INF, INF};
   int ix[4] = {-1, -1, -1, -1};
+  // every operand loaded unconditionally (clamped indices) right after the bound's index, the tests
+  // applied as selects: behind `if (dx < 0)` etc. the loads were dependent round trips of their own
   GRID_LOOP_B(t, (nlb > nub ? nlb : nub), bid, nblk) {
+    const int tl = t < nlb ? (int)t : 0, tu = t < nub ? (int)t : 0;
+    const int il = nlb > 0 ? D.ind_lb[tl] : 0, iu = nub > 0 ? D.ind_ub[tu] : 0;
+    const double dxl = D.d[il], xl_x = D.x[il], xl_l = D.xl[il], zl = D.zl[il];
+    const double pl = from_p ? D.p[nlb > 0 ? n + m + tl : 0] : D.d[nlb > 0 ? n + m + tl : 0], lo = D.l_lower[tl],
+                 ldg = D.l_diag[tl];
+    const double dxu = D.d[iu], xu_x = D.x[iu], xu_u = D.xu[iu], zu = D.zu[iu];
+    const int qu = nub > 0 ? n + m + nlb + tu : 0;  // in range
+    const double pu = from_p ? D.p[qu] : D.d[qu], uo = D.u_lower[tu], udg = D.u_diag[tu];
     if (t < nlb) {
-      const int i = D.ind_lb[t];
-      const double dx = D.d[i];
-      if (dx < 0) amin_upd(v[0], ix[0], (-D.x[i] + D.xl[i]) * tau / dx, (int)t);
-      const double dz = from_p ? (-D.p[n + m + t] + D.l_lower[t] * dx) / D.l_diag[t] : D.d[n + m + t];
-      if (dz < 0) amin_upd(v[2], ix[2], (-D.zl[i]) * tau / dz, (int)t);
+      const double dx = dxl;
+      if (dx < 0) amin_upd(v[0], ix[0], (-xl_x + xl_l) * tau / dx, (int)t);
+      const double dz = from_p ? (-pl + lo * dx) / ldg : pl;
+      if (dz < 0) amin_upd(v[2], ix[2], (-zl) * tau / dz, (int)t);
     }
     if (t < nub) {
-      const int i = D.ind_ub[t];
-      const double dx = D.d[i];
-      if (dx > 0) amin_upd(v[1], ix[1], (-D.x[i] + D.xu[i]) * tau / dx, (int)t);
-      const double dz = from_p ? (D.p[n + m + nlb + t] - D.u_lower[t] * dx) / D.u_diag[t] : D.d[n + m + nlb + t];
-      const double zu = D.zu[i];
+      const double dx = dxu;
+      if (dx > 0) amin_upd(v[1], ix[1], (-xu_x + xu_u) * tau / dx, (int)t);
+      const double dz = from_p ? (pu - uo * dx) / udg : pu;
       if (dz < 0 && zu + dz < 0) amin_upd(v[3], ix[3], (-zu) * tau / dz, (int)t);
     }
   }

@@ -13,6 +13,8 @@
 #include <numeric>
 #include <chrono>
 #include <cstdio>
+#include <thread>
+#include <memory>
 
 #include "common.hpp"
 
@@ -28,35 +30,90 @@ struct Pattern {
   std::vector<int32_t> ci, ri;
 };
 
+// Host threads for the O(nnz) passes of the analysis (MADIPM_ANALYSIS_THREADS, default: the
+// hardware threads, at most 16).  Every parallel pass gives the sequential result bit for bit.
+int analysis_threads() {
+  static const int nt = [] {
+    int t = (int)std::thread::hardware_concurrency();
+    if (const char* e = std::getenv("MADIPM_ANALYSIS_THREADS")) t = std::atoi(e);
+    return std::max(1, std::min(t, 16));
+  }();
+  return nt;
+}
+
+// f(t, j0, j1) on T contiguous column ranges balanced by entries (colptr), one thread each
+template <class F>
+void par_columns(int N, const int64_t* colptr, int T, F f) {
+  if (T <= 1) {
+    f(0, 0, N);
+    return;
+  }
+  std::vector<int> cut(T + 1, N);
+  cut[0] = 0;
+  for (int t = 1; t < T; ++t) {
+    const int64_t target = colptr[N] / T * t;
+    cut[t] = (int)(std::lower_bound(colptr, colptr + N + 1, target) - colptr);
+    cut[t] = std::max(cut[t], cut[t - 1]);
+  }
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t) th.emplace_back(f, t, cut[t], cut[t + 1]);
+  for (auto& x : th) x.join();
+}
+
+// Strictly-lower pattern of P K P^T by column and by row: a counting sort of the entries into
+// column / row buckets.  Threaded over column ranges when the matrix is dense enough to pay (private
+// bucket counts per thread, offsets in thread order: the same bucket order as one pass).
 void build_pattern(int N, const int64_t* colptr, const int32_t* rowval, const std::vector<int32_t>& pinv,
                    Pattern& P) {
+  const int64_t nnz = colptr[N];
+  int T = analysis_threads();
+  if (nnz < 16 * (int64_t)N || (int64_t)T * N > (int64_t)1 << 27 || nnz < ((int64_t)1 << 22)) T = 1;
+  std::vector<std::vector<int64_t>> cc(T, std::vector<int64_t>(N + 1, 0)), rc(T, std::vector<int64_t>(N + 1, 0));
+  par_columns(N, colptr, T, [&](int t, int j0, int j1) {
+    int64_t* c = cc[t].data();
+    int64_t* r = rc[t].data();
+    for (int j = j0; j < j1; ++j) {
+      const int b = pinv[j];
+      for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p) {
+        const int i = rowval[p];
+        if (i == j) continue;
+        const int a = pinv[i];
+        c[std::min(a, b)]++;
+        r[std::max(a, b)]++;
+      }
+    }
+  });
   P.cp.assign(N + 1, 0);
   P.rp.assign(N + 1, 0);
-  for (int j = 0; j < N; ++j)
-    for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p) {
-      int i = rowval[p];
-      if (i == j) continue;
-      int a = pinv[i], b = pinv[j];
-      int hi = std::max(a, b), lo = std::min(a, b);
-      P.cp[lo + 1]++;
-      P.rp[hi + 1]++;
+  for (int k = 0; k < N; ++k) {  // bucket starts, then each thread's offset inside each bucket
+    int64_t sc = 0, sr = 0;
+    for (int t = 0; t < T; ++t) {
+      const int64_t c = cc[t][k], r = rc[t][k];
+      cc[t][k] = sc;
+      rc[t][k] = sr;
+      sc += c;
+      sr += r;
     }
-  for (int j = 0; j < N; ++j) {
-    P.cp[j + 1] += P.cp[j];
-    P.rp[j + 1] += P.rp[j];
+    P.cp[k + 1] = P.cp[k] + sc;
+    P.rp[k + 1] = P.rp[k] + sr;
   }
   P.ci.resize(P.cp[N]);
   P.ri.resize(P.rp[N]);
-  std::vector<int64_t> cc(P.cp.begin(), P.cp.end() - 1), rc(P.rp.begin(), P.rp.end() - 1);
-  for (int j = 0; j < N; ++j)
-    for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p) {
-      int i = rowval[p];
-      if (i == j) continue;
-      int a = pinv[i], b = pinv[j];
-      int hi = std::max(a, b), lo = std::min(a, b);
-      P.ci[cc[lo]++] = hi;
-      P.ri[rc[hi]++] = lo;
+  par_columns(N, colptr, T, [&](int t, int j0, int j1) {
+    int64_t* c = cc[t].data();
+    int64_t* r = rc[t].data();
+    for (int j = j0; j < j1; ++j) {
+      const int b = pinv[j];
+      for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p) {
+        const int i = rowval[p];
+        if (i == j) continue;
+        const int a = pinv[i];
+        const int hi = std::max(a, b), lo = std::min(a, b);
+        P.ci[P.cp[lo] + c[lo]++] = hi;
+        P.ri[P.rp[hi] + r[hi]++] = lo;
+      }
     }
+  });
 }
 
 void etree(int N, const Pattern& P, std::vector<int32_t>& parent) {
@@ -413,6 +470,57 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       if (S.parent[s] != -1) S.child_list[fillc[S.parent[s]]++] = s;
   }
 
+  // ---------------- 4b. batched-leaf groups, decided from the pattern before any row structure is
+  // built: per parent, its candidate children whose K column is one CSC column of the caller
+  // (diagonal + rows below, none to its left) and whose rows cover at least lb_min_density of the
+  // union of their rows.  A member's rows are its L column's (a leaf: its K column's below the
+  // diagonal, P's column list); the members keep only their pivot row as front structure (nrows 1):
+  // their factor is the group's W, and on a dense-column QP their m-row lists were the analysis' bulk
+  // (dense QP 50k x 10k: 5e8 row entries materialised, copied, relative-indexed and gathered).
+  S.lb.clear();
+  S.lb_of.assign(ns, -1);
+  std::vector<std::vector<int32_t>> lb_members_of;  // per group: member fronts
+  std::vector<std::vector<int32_t>> lb_union;       // per group: union of the members' rows (ascending)
+  std::vector<int32_t> lb_group_of_parent(ns, -1);
+  std::vector<uint8_t> has_left;
+  if (use_lb) {
+    has_left.assign(N, 0);
+    for (int j = 0; j < N; ++j)
+      for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p)
+        if (rowval[p] != j) has_left[rowval[p]] = 1;
+    std::vector<int32_t> seen(N, -1);
+    for (int s = 0; s < ns; ++s) {
+      std::vector<int32_t> mem;
+      for (int64_t q = S.child_ptr[s]; q < S.child_ptr[s + 1]; ++q) {
+        const int c = S.child_list[q];
+        const int oc = perm[S.first[c]];
+        if (S.first[c + 1] - S.first[c] == 1 && lbcand[S.first[c]] && !has_left[oc] &&
+            S.child_ptr[c + 1] == S.child_ptr[c])
+          mem.push_back(c);
+      }
+      if ((int)mem.size() < opt.lb_min_count) continue;
+      std::vector<int32_t> U;
+      int64_t tot = 0;
+      for (int c : mem) {
+        const int j = S.first[c];
+        tot += P.cp[j + 1] - P.cp[j];
+        for (int64_t p = P.cp[j]; p < P.cp[j + 1]; ++p)
+          if (seen[P.ci[p]] != s) {
+            seen[P.ci[p]] = s;
+            U.push_back(P.ci[p]);
+          }
+      }
+      const double dens = (double)tot / ((double)U.size() * (double)mem.size());
+      if (dens < opt.lb_min_density) continue;
+      std::sort(U.begin(), U.end());
+      lb_group_of_parent[s] = (int32_t)lb_members_of.size();
+      for (int c : mem) S.lb_of[c] = (int32_t)lb_members_of.size();
+      lb_members_of.push_back(std::move(mem));
+      lb_union.push_back(std::move(U));
+    }
+  }
+  auto lb_member = [&](int s) { return !S.lb_of.empty() && S.lb_of[s] >= 0; };
+
   stamp("before 5");
   // ---------------- 5. frontal row structures
   S.row_ptr.assign(ns + 1, 0);
@@ -427,6 +535,11 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       marker[j] = s;
     }
     size_t nown = rs.size();
+    if (lb_member(s)) {  // batched leaf: pivot row only (its rows are its group's business)
+      S.nrows[s] = 1;
+      S.row_ptr[s + 1] = S.row_ptr[s] + 1;
+      continue;
+    }
     for (int j = f; j < l; ++j)
       for (int64_t p = P.cp[j]; p < P.cp[j + 1]; ++p) {
         int i = P.ci[p];
@@ -435,8 +548,15 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
           rs.push_back(i);
         }
       }
+    if (lb_group_of_parent[s] >= 0)
+      for (int i : lb_union[lb_group_of_parent[s]])
+        if (i >= l && marker[i] != s) {
+          marker[i] = s;
+          rs.push_back(i);
+        }
     for (int64_t q = S.child_ptr[s]; q < S.child_ptr[s + 1]; ++q) {
       int c = S.child_list[q];
+      if (lb_member(c)) continue;
       const std::vector<int32_t>& rc = R[c];
       int wc = S.first[c + 1] - S.first[c];
       for (size_t t = wc; t < rc.size(); ++t) {
@@ -448,7 +568,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         }
       }
     }
-    std::sort(rs.begin() + nown, rs.end());
+    if (!std::is_sorted(rs.begin() + nown, rs.end())) std::sort(rs.begin() + nown, rs.end());
     S.nrows[s] = (int32_t)rs.size();
     S.row_ptr[s + 1] = S.row_ptr[s] + (int64_t)rs.size();
   }
@@ -479,41 +599,15 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   }
 
   stamp("before 6b");
-  // ---------------- 6b. batched-leaf groups: per parent, its candidate children whose K column is one
-  // CSC column of the caller (diagonal + rows below, none to its left) and whose rows cover at least
-  // lb_min_density of the union of their rows
-  S.lb.clear();
-  S.lb_of.assign(ns, -1);
-  if (use_lb) {
-    std::vector<uint8_t> has_left(N, 0);
-    for (int j = 0; j < N; ++j)
-      for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p)
-        if (rowval[p] != j) has_left[rowval[p]] = 1;
-    std::vector<int32_t> mark(std::max(1, ns), -1), pos_in_u;
-    for (int s = 0; s < ns; ++s) {
-      std::vector<int32_t> mem;
-      for (int64_t q = S.child_ptr[s]; q < S.child_ptr[s + 1]; ++q) {
-        const int c = S.child_list[q];
-        const int oc = perm[S.first[c]];
-        if (S.first[c + 1] - S.first[c] == 1 && lbcand[S.first[c]] && !has_left[oc] &&
-            S.child_ptr[c + 1] == S.child_ptr[c])
-          mem.push_back(c);
-      }
-      if ((int)mem.size() < opt.lb_min_count) continue;
-      // union of their parent-local rows
-      std::vector<int32_t> U;
-      std::vector<uint8_t> inU(S.nrows[s], 0);  // parent-local rows hit by a member (marks: O(tot + r))
-      int64_t tot = 0;
-      for (int c : mem) {
-        const int uc = S.nrows[c] - 1;
-        tot += uc;
-        const int32_t* rl = S.rel.data() + S.rel_ptr[c];
-        for (int a = 0; a < uc; ++a) inU[rl[a]] = 1;
-      }
-      for (int i = 0; i < S.nrows[s]; ++i)
-        if (inU[i]) U.push_back(i);
-      const double dens = (double)tot / ((double)U.size() * (double)mem.size());
-      if (dens < opt.lb_min_density) continue;
+  // ---------------- 6b. batched-leaf group tables (groups decided in 4b): W rows = the union U in
+  // parent-local positions (gpos), and for every entry of a member's caller CSC column its W row
+  if (!lb_members_of.empty()) {
+    std::vector<int32_t> pos_in_u;
+    for (size_t gi = 0; gi < lb_members_of.size(); ++gi) {
+      const std::vector<int32_t>& mem = lb_members_of[gi];
+      const std::vector<int32_t>& U = lb_union[gi];
+      const int s = S.parent[mem[0]];
+      for (int64_t t = S.row_ptr[s]; t < S.row_ptr[s + 1]; ++t) pos[S.rows[t]] = (int32_t)(t - S.row_ptr[s]);
       SymbolicPlan::LBGroup g{};
       g.parent = s;
       g.m = (int32_t)U.size();
@@ -522,82 +616,140 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       g.mem_off = (int64_t)S.lb_mem.size();
       g.gpos_off = (int64_t)S.lb_gpos.size();
       S.lb_wsize += (int64_t)g.m * g.n;
-      S.lb_gpos.insert(S.lb_gpos.end(), U.begin(), U.end());
       pos_in_u.assign(S.nrows[s], -1);
-      for (int k = 0; k < g.m; ++k) pos_in_u[U[k]] = k;
-      // parent-local position of every permuted row of the parent
-      for (int64_t t = S.row_ptr[s]; t < S.row_ptr[s + 1]; ++t) pos[S.rows[t]] = (int32_t)(t - S.row_ptr[s]);
+      for (int k = 0; k < g.m; ++k) {
+        const int lr = pos[U[k]];
+        MADIPM_REQUIRE(lr >= 0 && S.rows[S.row_ptr[s] + lr] == U[k], "batched leaf: row outside its parent");
+        S.lb_gpos.push_back(lr);
+        pos_in_u[lr] = k;
+      }
+      const size_t m0 = S.lb_mem.size();
+      int64_t wtot = (int64_t)S.lb_wrow.size();
       for (int c : mem) {
         const int oc = perm[S.first[c]];
-        S.lb_of[c] = (int32_t)S.lb.size();
         S.lb_mem.push_back(S.first[c]);
         S.lb_cs.push_back(colptr[oc]);
         S.lb_ce.push_back(colptr[oc + 1]);
-        S.lb_wbase.push_back((int64_t)S.lb_wrow.size());
-        for (int64_t e = colptr[oc]; e < colptr[oc + 1]; ++e) {
-          const int i = rowval[e];
-          if (i == oc) {
-            S.lb_wrow.push_back(-1);
-          } else {
-            const int lr = pos[pinv[i]];
-            MADIPM_REQUIRE(lr >= 0 && pos_in_u[lr] >= 0, "batched leaf: row outside its parent");
-            S.lb_wrow.push_back(pos_in_u[lr]);
-          }
-        }
+        S.lb_wbase.push_back(wtot);
+        wtot += colptr[oc + 1] - colptr[oc];
       }
+      S.lb_wrow.resize(wtot);  // once (the threads below fill it)
+      // every entry of the members' CSC columns -> its W row (threads over members)
+      const int T = std::min<int>(analysis_threads(), std::max<int>(1, (int)(mem.size() / 64)));
+      std::vector<std::thread> th;
+      bool bad = false;
+      std::vector<uint8_t> badt(T, 0);
+      for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t]() {
+          for (size_t q = m0 + t; q < m0 + mem.size(); q += T) {
+            const int oc = perm[S.lb_mem[q]];
+            int32_t* wr = S.lb_wrow.data() + S.lb_wbase[q];
+            for (int64_t e = colptr[oc]; e < colptr[oc + 1]; ++e) {
+              const int i = rowval[e];
+              int32_t v = -1;
+              if (i != oc) {
+                const int lr = pos[pinv[i]];
+                if (lr < 0 || pos_in_u[lr] < 0) badt[t] = 1;
+                v = lr >= 0 ? pos_in_u[lr] : -1;
+              }
+              wr[e - colptr[oc]] = v;
+            }
+          }
+        });
+      for (auto& x : th) x.join();
+      for (uint8_t b : badt) bad = bad || b;
+      MADIPM_REQUIRE(!bad, "batched leaf: row outside its parent");
       S.lb.push_back(g);
     }
   }
-  auto lb_member = [&](int s) { return !S.lb_of.empty() && S.lb_of[s] >= 0; };
 
   stamp("before 7");
   // ---------------- 7. assembly map: caller's CSC entry -> (front, local offset)
   // (entries of batched-leaf members are read by the W build instead)
+  // (threads: entries by column ranges with per-thread front counts, then fronts dealt to threads;
+  // the same map as one pass)
   S.asm_ptr.assign(ns + 1, 0);
-  std::vector<int32_t> ea(nnz), eb(nnz);
-  for (int j = 0; j < N; ++j)
-    for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p) {
-      int a = pinv[rowval[p]], b = pinv[j];
-      if (a < b) std::swap(a, b);
-      ea[p] = a;
-      eb[p] = b;
-      if (lb_member(col2sn[b])) {
-        eb[p] = -1;
-        continue;
+  // per entry (a, b) = (row, column) in the permuted lower triangle; uninitialised storage, touched
+  // only for the entries of non-member columns (a batched-leaf member's column is all W entries)
+  std::unique_ptr<int32_t[]> ea_buf(new int32_t[std::max<int64_t>(nnz, 1)]), eb_buf(new int32_t[std::max<int64_t>(nnz, 1)]);
+  int32_t* ea = ea_buf.get();
+  int32_t* eb = eb_buf.get();
+  auto member_col = [&](int j) { return lb_member(col2sn[pinv[j]]); };
+  int TA = analysis_threads();
+  if (nnz < ((int64_t)1 << 22) || (int64_t)TA * (ns + N) > (int64_t)1 << 27) TA = 1;
+  std::vector<std::vector<int64_t>> acnt(TA, std::vector<int64_t>(ns + 1, 0));
+  par_columns(N, colptr, TA, [&](int t, int j0, int j1) {
+    int64_t* cnt_t = acnt[t].data();
+    for (int j = j0; j < j1; ++j)
+      for (int64_t p = member_col(j) ? colptr[j + 1] : colptr[j]; p < colptr[j + 1]; ++p) {
+        int a = pinv[rowval[p]], b = pinv[j];
+        if (a < b) std::swap(a, b);
+        ea[p] = a;
+        eb[p] = b;
+        if (lb_member(col2sn[b])) {
+          eb[p] = -1;
+          continue;
+        }
+        cnt_t[col2sn[b]]++;
       }
-      S.asm_ptr[col2sn[b] + 1]++;
+  });
+  for (int s = 0; s < ns; ++s) {
+    int64_t acc = 0;
+    for (int t = 0; t < TA; ++t) {
+      const int64_t c = acnt[t][s];
+      acnt[t][s] = acc;
+      acc += c;
     }
-  for (int s = 0; s < ns; ++s) S.asm_ptr[s + 1] += S.asm_ptr[s];
+    S.asm_ptr[s + 1] = S.asm_ptr[s] + acc;
+  }
   const int64_t nasm = S.asm_ptr[ns];
   S.asm_src.resize(nasm);
   S.asm_dst.resize(nasm);
   {
     std::vector<int64_t> byfront(nasm);
-    std::vector<int64_t> fillp(S.asm_ptr.begin(), S.asm_ptr.end() - 1);
-    for (int64_t p = 0; p < nnz; ++p)
-      if (eb[p] >= 0) byfront[fillp[col2sn[eb[p]]]++] = p;
-    for (int s = 0; s < ns; ++s) {
-      int r = S.nrows[s];
-      for (int64_t t = S.row_ptr[s]; t < S.row_ptr[s + 1]; ++t) pos[S.rows[t]] = (int32_t)(t - S.row_ptr[s]);
-      for (int64_t q = S.asm_ptr[s]; q < S.asm_ptr[s + 1]; ++q) {
-        int64_t p = byfront[q];
-        int lc = eb[p] - S.first[s];
-        int lr = pos[ea[p]];
-        MADIPM_REQUIRE(lr >= 0, "assembly row not in front");
-        S.asm_src[q] = p;
-        S.asm_dst[q] = (int64_t)lc * r + lr;
+    par_columns(N, colptr, TA, [&](int t, int j0, int j1) {
+      int64_t* off = acnt[t].data();
+      for (int j = j0; j < j1; ++j) {
+        if (member_col(j)) continue;
+        for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p)
+          if (eb[p] >= 0) {
+            const int sf = col2sn[eb[p]];
+            byfront[S.asm_ptr[sf] + off[sf]++] = p;
+          }
       }
-      // sort by destination (the big-front assembly binary-searches column ranges) and reject
-      // duplicates, which would race in the parallel assembly
-      std::vector<std::pair<int64_t, int64_t>> d;
-      d.reserve(S.asm_ptr[s + 1] - S.asm_ptr[s]);
-      for (int64_t q = S.asm_ptr[s]; q < S.asm_ptr[s + 1]; ++q) d.emplace_back(S.asm_dst[q], S.asm_src[q]);
-      std::sort(d.begin(), d.end());
-      for (size_t t = 0; t < d.size(); ++t) {
-        MADIPM_REQUIRE(t == 0 || d[t].first != d[t - 1].first, "duplicate entries in the CSC input (a pair {i, j} stored twice)");
-        S.asm_dst[S.asm_ptr[s] + t] = d[t].first;
-        S.asm_src[S.asm_ptr[s] + t] = d[t].second;
-      }
+    });
+    std::vector<std::thread> th;
+    std::vector<uint8_t> bad_row(TA, 0), dup(TA, 0);
+    for (int t = 0; t < TA; ++t)
+      th.emplace_back([&, t]() {
+        std::vector<int32_t> lpos(N, -1);
+        std::vector<std::pair<int64_t, int64_t>> d;
+        for (int s = t; s < ns; s += TA) {
+          const int r = S.nrows[s];
+          for (int64_t q = S.row_ptr[s]; q < S.row_ptr[s + 1]; ++q) lpos[S.rows[q]] = (int32_t)(q - S.row_ptr[s]);
+          d.clear();
+          for (int64_t q = S.asm_ptr[s]; q < S.asm_ptr[s + 1]; ++q) {
+            const int64_t p = byfront[q];
+            const int lc = eb[p] - S.first[s];
+            const int lr = lpos[ea[p]];
+            if (lr < 0) bad_row[t] = 1;
+            d.emplace_back((int64_t)lc * r + lr, p);
+          }
+          // sort by destination (the big-front assembly binary-searches column ranges) and reject
+          // duplicates, which would race in the parallel assembly
+          std::sort(d.begin(), d.end());
+          for (size_t u = 0; u < d.size(); ++u) {
+            if (u > 0 && d[u].first == d[u - 1].first) dup[t] = 1;
+            S.asm_dst[S.asm_ptr[s] + u] = d[u].first;
+            S.asm_src[S.asm_ptr[s] + u] = d[u].second;
+          }
+          for (int64_t q = S.row_ptr[s]; q < S.row_ptr[s + 1]; ++q) lpos[S.rows[q]] = -1;
+        }
+      });
+    for (auto& x : th) x.join();
+    for (int t = 0; t < TA; ++t) {
+      MADIPM_REQUIRE(!bad_row[t], "assembly row not in front");
+      MADIPM_REQUIRE(!dup[t], "duplicate entries in the CSC input (a pair {i, j} stored twice)");
     }
   }
 
@@ -723,7 +875,9 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   for (size_t so = 0; so < storage_order.size(); ++so) {
     const int s = storage_order[so];
     if (so == ntop_begin) S.top_lo = cur;
-    int64_t r = S.nrows[s], w = S.first[s + 1] - S.first[s];
+    // a batched-leaf member keeps only its pivot row as front structure: its L column (the group's W
+    // column) has colcnt entries, which the statistics count
+    int64_t r = lb_member(s) ? (int64_t)S.colcnt[S.first[s]] : S.nrows[s], w = S.first[s + 1] - S.first[s];
     S.max_front = std::max<int>(S.max_front, (int)r);
     S.nnzL_super += trap(w, r);
     for (int64_t t = 0; t < w; ++t) {
