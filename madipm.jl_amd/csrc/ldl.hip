@@ -1543,17 +1543,17 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
       // non-returning LDS atomic (one writer per address, so the result is deterministic), which needs
       // no wait for the old value — a plain read-modify-write would serialise every run on the LDS
       // round trip, and divergent runs across the wave on all of them
+      // branch-free run bookkeeping (selects, one predicated atomic per entry): the nested branches
+      // of the plain form cost ~25 instructions and three exec-mask round trips per entry
 #pragma unroll
       for (int u = 0; u < GP; ++u) {
         const int dst = (int)(e[u].x & 0xffffu);
-        if (dst == (int)SymbolicPlan::kFoldPadDst) continue;  // padding: the chunk has ended
-        if (dst != cur) {
-          if (cur >= 0) __hip_atomic_fetch_add(A + cur, -acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          cur = dst;
-          acc = v[u];
-        } else {
-          acc += v[u];
-        }
+        const bool pad = dst == (int)SymbolicPlan::kFoldPadDst;  // padding: the chunk has ended
+        const bool start = !pad & (dst != cur);
+        if (start & (cur >= 0)) __hip_atomic_fetch_add(A + cur, -acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const double sum = acc + (pad ? 0.0 : v[u]);
+        acc = start ? v[u] : sum;
+        cur = start ? dst : cur;
       }
       if (k + GP < len || bq + 1 < b1) {
 #pragma unroll
@@ -3478,10 +3478,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
 
   // ---- factorisation tree tables (k_fact_tree)
   {
-    std::vector<int32_t> ord, dptr{0}, dl;
-    for (int lev = 0; lev < NL; ++lev)
-      for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q)
-        if (S.ftree[S.level_list[q]]) ord.push_back(S.level_list[q]);
+    std::vector<int32_t> ord(S.ft_order), dptr{0}, dl;  // ticket order (SymbolicPlan::ft_order)
     nftree_ = (int)ord.size();
     for (int s : ord) {
       for (int q = S.child_ptr[s]; q < S.child_ptr[s + 1]; ++q)

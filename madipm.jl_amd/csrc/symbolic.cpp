@@ -1000,10 +1000,26 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     if (const char* e = std::getenv("MADIPM_FOLD_SLOTS")) slots = std::atoi(e);
     std::vector<char> late(ns_all, 0);
     {
+      // k_fact_tree's ticket order: by level (children before parents, so a workgroup waiting on its
+      // children never blocks the tickets they need), and within a level by descending tail — the
+      // estimated work from the front up to the root — so the fronts of the longest chains take the
+      // first CUs (MADIPM_TREE_PRIO=0: plain level order)
+      std::vector<double> tail(ns_all, 0.0);
+      for (int s = ns_all - 1; s >= 0; --s) {  // parents have larger indices (postorder)
+        const double r = S.nrows[s], w = S.first[s + 1] - S.first[s];
+        tail[s] = r * r + r * w + (S.parent[s] >= 0 ? tail[S.parent[s]] : 0.0);
+      }
+      const char* pe = std::getenv("MADIPM_TREE_PRIO");
+      const bool prio = !(pe && pe[0] == '0');
       std::vector<int> ord;
-      for (int lev = 0; lev < S.nlevels; ++lev)
+      for (int lev = 0; lev < S.nlevels; ++lev) {
+        const size_t o0 = ord.size();
         for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q)
           if (S.ftree[S.level_list[q]]) ord.push_back(S.level_list[q]);
+        if (prio)
+          std::stable_sort(ord.begin() + o0, ord.end(), [&](int a, int b) { return tail[a] > tail[b]; });
+      }
+      S.ft_order.assign(ord.begin(), ord.end());
       if (slots > 0 && (int)ord.size() > slots) {
         // every front past the first `slots` tickets leaves its leaves to the micro launch + gather: a
         // late front's fold lies on the critical path (it starts when an earlier front retires), while
@@ -1129,6 +1145,24 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       S.fold_bptr[s + 1] = (int32_t)S.fold_bat.size();
     }
     S.ab_first.push_back((int64_t)S.ab_src0.size());
+    if (std::getenv("MADIPM_FOLD_STATS")) {  // diagnostics: per level, the folded leaves and products
+      std::vector<double> acc((size_t)S.nlevels * 6, 0.0);
+      for (int s = 0; s < ns_all; ++s) {
+        if (!S.absorb[s]) continue;
+        double* a = &acc[(size_t)S.level[s] * 6];
+        a[0] += 1;
+        a[1] += S.mc_ptr[s + 1] - S.mc_ptr[s];
+        a[2] += (double)(S.ab_first[S.mc_ptr[s + 1]] - S.ab_first[S.mc_ptr[s]]);
+        for (int b = S.fold_bptr[s]; b < S.fold_bptr[s + 1]; ++b) a[3] += (double)S.fold_plen[b] * NT_FOLD;
+        a[4] += S.fold_bptr[s + 1] - S.fold_bptr[s];
+        a[5] += S.nrows[s];
+      }
+      for (int lv = 0; lv < S.nlevels; ++lv)
+        if (acc[lv * 6] > 0)
+          fprintf(stderr, "fold level %d: %d fronts  r %.1f  leaves %.1f  leaf rows %.1f  product slots %.1f  batches %.2f\n", lv,
+                  (int)acc[lv * 6], acc[lv * 6 + 5] / acc[lv * 6], acc[lv * 6 + 1] / acc[lv * 6], acc[lv * 6 + 2] / acc[lv * 6],
+                  acc[lv * 6 + 3] / acc[lv * 6], acc[lv * 6 + 4] / acc[lv * 6]);
+    }
   }
   S.fs_off.assign(ns, -1);
   S.fs_size = 0;

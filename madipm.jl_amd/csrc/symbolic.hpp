@@ -103,6 +103,7 @@ struct SymbolicPlan {
   static constexpr int kFoldThreads = 512;  // threads of k_fact_tree: product-list chunks per batch
   static constexpr int kFactTreeFanIn = 8;
   std::vector<uint8_t> ftree;          // factorisation-tree fronts (k_fact_tree)
+  std::vector<int32_t> ft_order;       // their ticket order (level by level, longest tail first)
   // leaf folding (tree fronts whose pre-leaf children are all micro leaves: w <= 2, r <= 32): the
   // front factorises its micro leaves in LDS and subtracts their rank-1/2 updates through
   // destination-sorted product lists, instead of k_micro_factor writing update blocks to HBM and

@@ -13,6 +13,8 @@ tr = list(csv.DictReader(open(trace)))
 tr.sort(key=lambda r: int(r['Start_Timestamp']))
 names = [re.search(r'(k_\w+|__amd\w+)', r['Kernel_Name']).group(1) for r in tr]
 idx = [i for i, n in enumerate(names) if n == 'k_inertia']
+if not idx:  # the fused MPC loop has no separate inertia launch: nothing more to break down
+    sys.exit(0)
 last = idx[-1]
 start = max(i for i in range(last) if names[i] == 'k_status_init')
 agg = collections.OrderedDict()
