@@ -1399,6 +1399,16 @@ __global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t*
 constexpr int FTN = SymbolicPlan::kFoldThreads;
 static_assert(FTN == 512, "k_fact_tree: 512 threads");
 
+// one copy for both storage variants (a static __shared__ inside the template would be allocated twice)
+struct FoldBatchTab {
+  int64_t j[SymbolicPlan::kFoldMaxBatches + 1], po[SymbolicPlan::kFoldMaxBatches];
+  int32_t k[SymbolicPlan::kFoldMaxBatches + 1], pl[SymbolicPlan::kFoldMaxBatches];
+};
+__device__ __forceinline__ FoldBatchTab& fold_batch_tab() {
+  __shared__ FoldBatchTab t;
+  return t;
+}
+
 template <bool PK>
 __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A, const double* Kx, double* arena,
                                             double* D, LDLStatus* st, double tol, double* ext, int64_t* fdg) {
@@ -1423,17 +1433,38 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
   int32_t* pwrc = prow0 + LM;
   int32_t* kk = pwrc + LM;                                   // per batch row: batch-local leaf
   const int tid = threadIdx.x;
-  const int b0 = T.fold_bptr[s], b1 = T.fold_bptr[s + 1];
+  const int b0 = T.fold_bptr[s], nb = T.fold_bptr[s + 1] - b0;
+  // the batch table (first leaf, first row, product offset and length), loaded once into LDS: read
+  // from global per batch it cost two dependent round trips at each batch's gather and products
+  FoldBatchTab& ft = fold_batch_tab();
+  int32_t *tb_k = ft.k, *tb_pl = ft.pl;
+  int64_t *tb_j = ft.j, *tb_po = ft.po;
+  if (tid <= nb) {
+    const int bq = b0 + tid, bc = min(bq, b0 + nb - 1);  // the sentinel entry (tid == nb) is the next batch's start
+    const int32_t k = T.fold_bat[bq], pl = T.fold_plen[bc];
+    const int64_t j = T.fold_row0[bq], po = T.fold_poff[bc];
+    tb_k[tid] = k;
+    tb_j[tid] = j;
+    if (tid < nb) tb_po[tid] = po, tb_pl[tid] = pl;
+  }
+  __syncthreads();
+  // product entries: thread t walks chunks t, t + FTN, ... (kFoldChains independent accumulation
+  // chains); a group holds GH entries of each
+  constexpr int NC = SymbolicPlan::kFoldChains, NCH = NC * FTN, GH = GP / NC;
+  static_assert(GP % NC == 0, "fold: whole groups per chain");
   uint2 e[GP];
   auto load_group = [&](uint2 (&g)[GP], const uint2* P, int k, int len) {
 #pragma unroll
-    for (int u = 0; u < GP; ++u) g[u] = (k + u < len) ? P[(int64_t)(k + u) * FTN] : uint2{SymbolicPlan::kFoldPadDst, 0u};
+    for (int u = 0; u < GP; ++u) {
+      const int kk = k + u / NC;  // uniform: a scalar branch, not a per-lane wait
+      g[u] = (kk < len) ? P[(int64_t)kk * NCH + (u % NC) * FTN] : uint2{0u, 0u};
+    }
   };
-  load_group(e, T.fold_prod + T.fold_poff[b0] + tid, 0, T.fold_plen[b0]);
-  for (int bq = b0; bq < b1; ++bq) {
-    const int k0 = T.fold_bat[bq], k1 = (bq + 1 < b1) ? T.fold_bat[bq + 1] : T.mc_ptr[s + 1];
-    const int64_t j0 = T.ab_first[k0];
-    const int nrow = (int)(T.ab_first[k1] - j0), nleaf = k1 - k0;
+  load_group(e, T.fold_prod + tb_po[0] + tid, 0, tb_pl[0]);
+  for (int b = 0; b < nb; ++b) {
+    const int k0 = tb_k[b], k1 = tb_k[b + 1];
+    const int64_t j0 = tb_j[b];
+    const int nrow = (int)(tb_j[b + 1] - j0), nleaf = k1 - k0;
     // (1) the leaf rows' K entries (leaf tables loaded beside them)
     int32_t lf[2], lw[2];
     int64_t lo[2];
@@ -1519,49 +1550,45 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
     }
     __syncthreads();
     lap(2);
-    // (4) this thread's chunk of the destination-sorted products (entry k at 256 k + tid: each load
-    // instruction is coalesced)
-    const uint2* __restrict__ P = T.fold_prod + T.fold_poff[bq] + tid;
-    const int len = T.fold_plen[bq];
-    int cur = -1;
-    double acc = 0.0;
-    for (int k = 0; k < len; k += GP) {
+    // (4) this thread's chunks of the destination-sorted products (entry k of chunk c at NCH k + c:
+    // each load instruction is coalesced)
+    const uint2* __restrict__ P = T.fold_prod + tb_po[b] + tid;
+    const int len = tb_pl[b];
+    double acc[NC];  // per chain: the negated sum of its open run
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[c] = 0.0;
+    for (int k = 0; k < len; k += GH) {
       uint2 nx[GP];
-      if (k + GP < len) {
-        load_group(nx, P, k + GP, len);
-      } else if (bq + 1 < b1) {  // the next batch's first group
-        load_group(nx, T.fold_prod + T.fold_poff[bq + 1] + tid, 0, T.fold_plen[bq + 1]);
+      if (k + GH < len) {
+        load_group(nx, P, k + GH, len);
+      } else if (b + 1 < nb) {  // the next batch's first group
+        load_group(nx, T.fold_prod + tb_po[b + 1] + tid, 0, tb_pl[b + 1]);
       }
       // every LDS operand of the group is read before its first update of A
       double v[GP];
 #pragma unroll
       for (int u = 0; u < GP; ++u) {
-        const double2 la = LQ[e[u].x >> 16], pb = PQ[e[u].y];  // padding reads row 0: harmless
-        v[u] = la.x * pb.x + la.y * pb.y;
+        const double2 la = LQ[e[u].x >> 16], pb = PQ[e[u].y & ~SymbolicPlan::kFoldRunEnd];
+        v[u] = fma(la.x, pb.x, la.y * pb.y);
       }
-      // a destination is owned by one thread and gets one run: its partial sum is subtracted with a
-      // non-returning LDS atomic (one writer per address, so the result is deterministic), which needs
-      // no wait for the old value — a plain read-modify-write would serialise every run on the LDS
-      // round trip, and divergent runs across the wave on all of them
-      // branch-free run bookkeeping (selects, one predicated atomic per entry): the nested branches
-      // of the plain form cost ~25 instructions and three exec-mask round trips per entry
+      // a destination is owned by one chain and gets one run per batch; the run's sum is subtracted
+      // at its last entry (marked by the analysis) with a non-returning LDS atomic — one writer per
+      // address, so the result is deterministic, and no wait for the old value (a plain
+      // read-modify-write would serialise every run on the LDS round trip).  Branch-free: selects and
+      // one predicated atomic per entry; padding never ends a run, and acc restarts every batch.
 #pragma unroll
       for (int u = 0; u < GP; ++u) {
-        const int dst = (int)(e[u].x & 0xffffu);
-        const bool pad = dst == (int)SymbolicPlan::kFoldPadDst;  // padding: the chunk has ended
-        const bool start = !pad & (dst != cur);
-        if (start & (cur >= 0)) __hip_atomic_fetch_add(A + cur, -acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const double sum = acc + (pad ? 0.0 : v[u]);
-        acc = start ? v[u] : sum;
-        cur = start ? dst : cur;
+        const bool end = (int32_t)e[u].y < 0;
+        const double sum = acc[u % NC] - v[u];
+        if (end) __hip_atomic_fetch_add(A + (e[u].x & 0xffffu), sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        acc[u % NC] = end ? 0.0 : sum;
       }
-      if (k + GP < len || bq + 1 < b1) {
+      if (k + GH < len || b + 1 < nb) {
 #pragma unroll
         for (int u = 0; u < GP; ++u) e[u] = nx[u];
       }
     }
-    if (len == 0 && bq + 1 < b1) load_group(e, T.fold_prod + T.fold_poff[bq + 1] + tid, 0, T.fold_plen[bq + 1]);
-    if (cur >= 0) __hip_atomic_fetch_add(A + cur, -acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (len == 0 && b + 1 < nb) load_group(e, T.fold_prod + tb_po[b + 1] + tid, 0, tb_pl[b + 1]);
     __syncthreads();
     lap(3);
   }
@@ -3547,11 +3574,12 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       }
       up32(fold_bptr_, S.fold_bptr);
       up32(fold_bat_, S.fold_bat);
+      up64(fold_row0_, S.fold_row0);
       up64(fold_poff_, S.fold_poff);
       up32(fold_plen_, S.fold_plen);
       up32(fold_rmax_, S.fold_rmax);
       up32(fold_lmax_, S.fold_lmax);
-      fold_prod_.upload(S.fold_prod.empty() ? std::vector<uint32_t>{SymbolicPlan::kFoldPadDst, 0u} : S.fold_prod);
+      fold_prod_.upload(S.fold_prod.empty() ? std::vector<uint32_t>{0u, 0u} : S.fold_prod);
       T_.absorb = absorb_;
       T_.fold_pk = fold_pk_;
       T_.mc_ptr = mc_ptr_;
@@ -3564,6 +3592,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       T_.ab_loff = ab_loff_;
       T_.fold_bptr = fold_bptr_;
       T_.fold_bat = fold_bat_;
+      T_.fold_row0 = fold_row0_;
       T_.fold_poff = fold_poff_;
       T_.fold_plen = fold_plen_;
       T_.fold_rmax = fold_rmax_;

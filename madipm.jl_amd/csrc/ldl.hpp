@@ -60,6 +60,7 @@ struct FrontTab {
   const int64_t* ab_loff;
   const int32_t* fold_bptr;
   const int32_t* fold_bat;
+  const int64_t* fold_row0;
   const int64_t* fold_poff;
   const int32_t* fold_plen;
   const int32_t* fold_rmax;
@@ -316,7 +317,7 @@ class LDLSolver : public LinSolver {
   bool ftree_checked_ = false;
   double ftree_bytes_ = 0, ftree_flops_ = 0, ftree_alg_ = 0;
   DBuf<int32_t> ft_order_, ft_dptr_, ft_dep_, fflags_, fcnt_;
-  DBuf<int64_t> fdbg_, ab_first_, ab_loff_, fold_poff_;
+  DBuf<int64_t> fdbg_, ab_first_, ab_loff_, fold_poff_, fold_row0_;
   DBuf<int32_t> ab_src0_, ab_src1_, ab_k_, ab_f0_, ab_wrc_, fold_bptr_, fold_bat_, fold_plen_, fold_rmax_, fold_lmax_;
   DBuf<uint8_t> absorb_, fold_pk_, fs_img_;
   DBuf<int32_t> mc_ptr_;

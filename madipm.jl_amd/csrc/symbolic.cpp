@@ -966,6 +966,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   S.fold_rmax.assign(ns_all, 0);
   S.fold_lmax.assign(ns_all, 0);
   S.fold_bat.clear();
+  S.fold_row0.clear();
   S.fold_poff.clear();
   S.fold_plen.clear();
   S.fold_prod.clear();
@@ -1058,6 +1059,18 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         budget = LMAX - pk_bytes(r);
       }
       if (budget < RB * 32 + LB) continue;  // not even one leaf fits beside the front
+      {  // the batch table lives in LDS: fronts needing more batches leave their leaves unfolded
+        int nb = 0;
+        int64_t rows = 0, nl = 0;
+        for (int64_t qc = S.child_ptr[s]; qc < S.child_ptr[s + 1]; ++qc) {
+          const int c = S.child_list[qc];
+          if (S.ftree[c]) continue;
+          if (nl == 0 || RB * (rows + S.nrows[c]) + LB * (nl + 1) > budget) ++nb, rows = 0, nl = 0;
+          rows += S.nrows[c];
+          ++nl;
+        }
+        if (nb > SymbolicPlan::kFoldMaxBatches) continue;
+      }
       S.absorb[s] = 1;
       S.fold_pk[s] = (uint8_t)pk;
       const int64_t ld = r | 1;
@@ -1098,6 +1111,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         while (ke < k1 && RB * (rows + S.nrows[S.mc_list[ke]]) + LB * (ke - kb + 1) <= budget) rows += S.nrows[S.mc_list[ke++]];
         MADIPM_REQUIRE(ke > kb, "fold: a leaf does not fit the batch budget");
         S.fold_bat.push_back(kb);
+        S.fold_row0.push_back(S.ab_first[kb]);
         S.fold_rmax[s] = std::max<int32_t>(S.fold_rmax[s], (int32_t)rows);
         S.fold_lmax[s] = std::max<int32_t>(S.fold_lmax[s], ke - kb);
         const int64_t row0 = S.ab_first[kb];
@@ -1112,31 +1126,34 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
               pr.push_back({fidx(rl[a - wc], rl[b - wc]), qb0 + a, qb0 + b});
         }
         std::stable_sort(pr.begin(), pr.end(), [](const Prod& x, const Prod& y) { return x.dst < y.dst; });
-        // NT_FOLD chunks at destination boundaries, balanced by count
+        // NCH chunks at destination boundaries, balanced by count
+        constexpr int NCH = SymbolicPlan::kFoldChains * NT_FOLD;
         const int64_t P = (int64_t)pr.size();
-        bnd.assign(NT_FOLD + 1, P);
+        bnd.assign(NCH + 1, P);
         bnd[0] = 0;
-        for (int t = 1; t < NT_FOLD; ++t) {
-          int64_t q = std::max(bnd[t - 1], (P * t) / NT_FOLD);
+        for (int t = 1; t < NCH; ++t) {
+          int64_t q = std::max(bnd[t - 1], (P * t) / NCH);
           while (q > 0 && q < P && pr[q].dst == pr[q - 1].dst) ++q;
           bnd[t] = q;
         }
         int64_t len = 0;
-        for (int t = 0; t < NT_FOLD; ++t) len = std::max(len, bnd[t + 1] - bnd[t]);
+        for (int t = 0; t < NCH; ++t) len = std::max(len, bnd[t + 1] - bnd[t]);
         const int64_t off = (int64_t)S.fold_prod.size() / 2;
         S.fold_poff.push_back(off);
         S.fold_plen.push_back((int32_t)len);
-        S.fold_prod.resize(2 * (off + len * NT_FOLD));
-        for (int t = 0; t < NT_FOLD; ++t)
+        S.fold_prod.resize(2 * (off + len * NCH));
+        for (int t = 0; t < NCH; ++t)
           for (int64_t k = 0; k < len; ++k) {
-            uint32_t* e = &S.fold_prod[2 * (off + k * NT_FOLD + t)];
+            uint32_t* e = &S.fold_prod[2 * (off + k * NCH + t)];
             const int64_t q = bnd[t] + k;
             if (q < bnd[t + 1]) {
-              MADIPM_REQUIRE(pr[q].dst < SymbolicPlan::kFoldPadDst && pr[q].q1 < 65536, "fold: index beyond 16 bits");
+              MADIPM_REQUIRE(pr[q].dst < 65536 && pr[q].q1 < 65536 && pr[q].q2 < SymbolicPlan::kFoldRunEnd,
+                             "fold: index beyond 16 bits");
+              const bool end = q + 1 == bnd[t + 1] || pr[q + 1].dst != pr[q].dst;
               e[0] = pr[q].dst | (pr[q].q1 << 16);
-              e[1] = pr[q].q2;
-            } else {
-              e[0] = SymbolicPlan::kFoldPadDst;
+              e[1] = pr[q].q2 | (end ? SymbolicPlan::kFoldRunEnd : 0u);
+            } else {  // padding: row 0 (always staged), never the end of a run
+              e[0] = 0;
               e[1] = 0;
             }
           }
@@ -1145,6 +1162,10 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       S.fold_bptr[s + 1] = (int32_t)S.fold_bat.size();
     }
     S.ab_first.push_back((int64_t)S.ab_src0.size());
+    // sentinels: the batch after a front's last one starts at that front's end (leaves and rows are
+    // appended front by front), so batch b always ends where batch b + 1 begins
+    S.fold_bat.push_back((int32_t)S.mc_list.size());
+    S.fold_row0.push_back(S.ab_first.back());
     if (std::getenv("MADIPM_FOLD_STATS")) {  // diagnostics: per level, the folded leaves and products
       std::vector<double> acc((size_t)S.nlevels * 6, 0.0);
       for (int s = 0; s < ns_all; ++s) {
@@ -1153,7 +1174,8 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         a[0] += 1;
         a[1] += S.mc_ptr[s + 1] - S.mc_ptr[s];
         a[2] += (double)(S.ab_first[S.mc_ptr[s + 1]] - S.ab_first[S.mc_ptr[s]]);
-        for (int b = S.fold_bptr[s]; b < S.fold_bptr[s + 1]; ++b) a[3] += (double)S.fold_plen[b] * NT_FOLD;
+        for (int b = S.fold_bptr[s]; b < S.fold_bptr[s + 1]; ++b)
+          a[3] += (double)S.fold_plen[b] * SymbolicPlan::kFoldChains * NT_FOLD;
         a[4] += S.fold_bptr[s + 1] - S.fold_bptr[s];
         a[5] += S.nrows[s];
       }

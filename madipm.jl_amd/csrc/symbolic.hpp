@@ -110,15 +110,22 @@ struct SymbolicPlan {
   // the gather pre-assembly summing them.  Leaf rows are flattened per front in child order (ab_*);
   // the leaves are cut into batches whose rows fit LDS beside the front.  Per batch the products
   // (F(i, j) -= l(q1) . p(q2) over the two leaf columns, p = l d) are sorted by LDS destination
-  // (leaf order within one destination), cut into kFoldThreads chunks at destination boundaries and
-  // stored interleaved (entry k of thread t at fold_poff + kFoldThreads k + t) so each load instruction
-  // is coalesced.
+  // (leaf order within one destination), cut into kFoldChains x kFoldThreads chunks at destination
+  // boundaries (thread t walks chunks t, t + kFoldThreads, ... as independent accumulation chains)
+  // and stored interleaved (entry k of chunk c at fold_poff + kFoldChains kFoldThreads k + c) so each
+  // load instruction is coalesced.  An entry's top bit marks the last product of its destination run
+  // (the run's sum is subtracted there); padding entries carry no mark and read row 0.
   static constexpr int64_t kFactTreeLdsMax = 150 * 1024;  // dynamic LDS of k_fact_tree
   static constexpr int64_t kFoldLdsMax = 148 * 1024;      // fold front + leaf rows (k_fact_tree's
                                                           // static LDS is ~10.4 KB of the CU's 160 KB)
   static constexpr int kFoldRowBytes = 36;                // LDS per leaf row: (l0, l1), (l0 d0, l1 d1), leaf
   static constexpr int kFoldLeafBytes = 48;               // LDS per leaf: d0, d1, f10, L offset, row0, w | rc
-  static constexpr uint32_t kFoldPadDst = 0xffffu;        // destination of a padding entry
+  // product chunks per k_fact_tree thread.  2 (independent accumulation chains) measured slower on
+  // ex10: a chunk cannot split a destination run, so the longest runs set the padded length and the
+  // product slots grew 80k -> 135k per level-2 front (tree span 178 -> 190 us)
+  static constexpr int kFoldChains = 1;
+  static constexpr uint32_t kFoldRunEnd = 1u << 31;       // entry word 1: last product of its run
+  static constexpr int kFoldMaxBatches = 32;              // leaf batches per folding front (LDS table)
   std::vector<uint8_t> absorb;        // front folds its micro leaves
   std::vector<uint8_t> fold_pk;       // fold front stored packed in LDS (to leave room for the leaf rows)
   std::vector<int32_t> mc_ptr, mc_list;  // per front: its folded micro leaves (child order)
@@ -126,11 +133,12 @@ struct SymbolicPlan {
   std::vector<int32_t> ab_src0, ab_src1, ab_k;  // per flat row: caller's K index of columns 0 / 1, leaf
   std::vector<int32_t> ab_f0, ab_wrc;  // per folded leaf: first pivot, w | rc << 8 (l_off: LDLSolver)
   std::vector<int32_t> fold_bptr;     // per front: its batches [fold_bptr[s], fold_bptr[s + 1])
-  std::vector<int32_t> fold_bat;      // per batch: first leaf index (into mc_list)
+  std::vector<int32_t> fold_bat;      // per batch: first leaf index (into mc_list); + end sentinel
+  std::vector<int64_t> fold_row0;     // per batch: its first flat leaf row (ab_first of fold_bat); + sentinel
   std::vector<int64_t> fold_poff;     // per batch: first product entry
-  std::vector<int32_t> fold_plen;     // per batch: entries per thread
+  std::vector<int32_t> fold_plen;     // per batch: entries per chunk
   std::vector<int32_t> fold_rmax, fold_lmax;  // per front: largest batch (rows, leaves): its LDS carve
-  std::vector<uint32_t> fold_prod;    // 2 words per entry: dst | q1 << 16, q2 (batch-local rows)
+  std::vector<uint32_t> fold_prod;    // 2 words per entry: dst | q1 << 16, q2 | run end (batch-local rows)
   int64_t fs_size = 0;
   // forward-solve gather: for every front row, the children's update-vector entries in child order
   std::vector<int64_t> sv_ptr, sv_src;  // sv_ptr indexed by row_ptr[s] + i
