@@ -3636,6 +3636,14 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     L.bytes += 8.0 * L.nchunk;
     out.push_back(L);
   };
+  auto lb_syrk_launch = [&](int g, std::vector<Launch>& out) {
+    const auto& G = S.lb[g];
+    Launch L{LB_SYRK, 0, g, 0, 0};
+    L.flops = (double)G.m * (G.m + 1) * (double)G.n;
+    // W once + the parent's lower triangle read-modify-written once per K-chunk
+    L.bytes = 8.0 * (double)G.m * G.n + 16.0 * (double)G.m * (G.m + 1) / 2.0 * cdiv(G.n, LB_KCHUNK);
+    out.push_back(L);
+  };
   auto build_fact = [&](int phase, std::vector<Launch>& out) {
     if (phase == 1 && !S.lb.empty()) {
       Launch L{LB_BUILD, 0, 0, 0, (int64_t)S.lb_mem.size()};
@@ -3656,14 +3664,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       if (phase == 1 && lev == 1 && nftree_) ftree_launch();
       asm_launch(phase == 1 ? lev : NL + 1 + lev, out);
       if (phase == 1)
-        for (int g : lb_at_level_[lev]) {
-          const auto& G = S.lb[g];
-          Launch L{LB_SYRK, 0, g, 0, 0};
-          L.flops = (double)G.m * (G.m + 1) * (double)G.n;
-          // W once + the parent's lower triangle read-modify-written once per K-chunk
-          L.bytes = 8.0 * (double)G.m * G.n + 16.0 * (double)G.m * (G.m + 1) / 2.0 * cdiv(G.n, LB_KCHUNK);
-          out.push_back(L);
-        }
+        for (int g : lb_at_level_[lev])
+          if (!S.top(S.lb[g].parent)) lb_syrk_launch(g, out);  // top parents: after their external part
       std::vector<int32_t> cls[4], big, micro;
       for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
         const int s = S.level_list[q];
@@ -3750,6 +3752,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   build_fact(1, fact1_);
   if (S.nshards > 1) {
     asm_launch(NL, fact1_);  // top fronts, external part (all-reduced next)
+    for (size_t g = 0; g < S.lb.size(); ++g)  // this shard's batched leaves under top fronts: into it
+      if (S.top(S.lb[g].parent)) lb_syrk_launch((int)g, fact1_);
     build_fact(2, fact2_);
   }
 

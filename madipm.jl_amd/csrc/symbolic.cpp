@@ -403,7 +403,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   // are kept out of relaxed amalgamation; step 6b decides the groups.
   std::vector<uint8_t> lbcand(N, 0);
   // batched leaves read their K column as one contiguous CSC run (diagonal + rows below): lower only
-  const bool use_lb = opt.leaf_batch && opt.nshards <= 1 && !has_upper;
+  const bool use_lb = opt.leaf_batch && !has_upper;
   if (use_lb) {
     std::vector<int32_t> npar(N, 0);
     for (const SN& f : fund)
@@ -854,6 +854,47 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         MADIPM_REQUIRE(S.parent[s] >= 0, "sharding: unassigned root");
         S.owner[s] = S.owner[S.parent[s]];
       }
+    // batched-leaf groups keep this shard's members only (compacted in place, member order kept).  A
+    // group under a subtree front lies wholly on that subtree's shard; under a top front its members
+    // are dealt like any subtree roots, and each shard's SYRK adds its members' W D^-1 W^T to the top
+    // front's external part (all-reduced with it) and its GEMV forward contribution to the exchanged
+    // external forward sums.  A group with no member here vanishes on this shard.
+    if (!S.lb.empty()) {
+      size_t ng = 0, nm = 0, nw = 0;
+      int64_t wsize = 0;
+      for (size_t gi = 0; gi < S.lb.size(); ++gi) {
+        SymbolicPlan::LBGroup g = S.lb[gi];
+        const int64_t m0 = g.mem_off;
+        int n = 0;
+        const size_t nm0 = nm;
+        for (int j = 0; j < S.lb[gi].n; ++j) {
+          const size_t q = (size_t)(m0 + j);
+          if (S.owner[col2sn[S.lb_mem[q]]] != S.shard) continue;
+          const int64_t len = S.lb_ce[q] - S.lb_cs[q], wb = S.lb_wbase[q];
+          S.lb_mem[nm] = S.lb_mem[q];
+          S.lb_cs[nm] = S.lb_cs[q];
+          S.lb_ce[nm] = S.lb_ce[q];
+          std::memmove(S.lb_wrow.data() + nw, S.lb_wrow.data() + wb, sizeof(int32_t) * (size_t)len);
+          S.lb_wbase[nm] = (int64_t)nw;
+          nw += (size_t)len;
+          ++nm;
+          ++n;
+        }
+        if (n == 0) continue;
+        g.mem_off = (int64_t)nm0;
+        g.n = n;
+        g.w_off = wsize;
+        wsize += (int64_t)g.m * n;
+        S.lb[ng++] = g;
+      }
+      S.lb.resize(ng);
+      S.lb_mem.resize(nm);
+      S.lb_cs.resize(nm);
+      S.lb_ce.resize(nm);
+      S.lb_wbase.resize(nm);
+      S.lb_wrow.resize(nw);
+      S.lb_wsize = wsize;
+    }
   } else {
     S.owner.clear();  // unsharded: every front belongs to the (only) shard
   }
@@ -1011,15 +1052,19 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         tail[s] = r * r + r * w + (S.parent[s] >= 0 ? tail[S.parent[s]] : 0.0);
       }
       const char* pe = std::getenv("MADIPM_TREE_PRIO");
-      const bool prio = !(pe && pe[0] == '0');
+      const int prio = pe ? std::atoi(pe) : 1;
       std::vector<int> ord;
       for (int lev = 0; lev < S.nlevels; ++lev) {
         const size_t o0 = ord.size();
         for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q)
           if (S.ftree[S.level_list[q]]) ord.push_back(S.level_list[q]);
-        if (prio)
+        if (prio == 1)
           std::stable_sort(ord.begin() + o0, ord.end(), [&](int a, int b) { return tail[a] > tail[b]; });
       }
+      // MADIPM_TREE_PRIO=2: one global order by descending tail (a child's tail exceeds its parent's,
+      // so this is topological): the longest chains' upper fronts take CUs before other chains' leaves
+      if (prio == 2)
+        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return tail[a] > tail[b]; });
       S.ft_order.assign(ord.begin(), ord.end());
       if (slots > 0 && (int)ord.size() > slots) {
         // every front past the first `slots` tickets leaves its leaves to the micro launch + gather: a
@@ -1346,8 +1391,10 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       const int uc = S.nrows[c] - (S.first[c + 1] - S.first[c]);
       for (int aa = 0; aa < uc; ++aa) S.sv_ptr[S.row_ptr[s] + S.rel[S.rel_ptr[c] + aa] + 1]++;
     }
+  // a group under a top front (sharded) contributes to the external forward sums (sx) instead
   for (const auto& g : S.lb)
-    for (int k = 0; k < g.m; ++k) S.sv_ptr[S.row_ptr[g.parent] + S.lb_gpos[g.gpos_off + k] + 1]++;
+    if (!S.top(g.parent))
+      for (int k = 0; k < g.m; ++k) S.sv_ptr[S.row_ptr[g.parent] + S.lb_gpos[g.gpos_off + k] + 1]++;
   for (int64_t t = 0; t < S.row_ptr[ns]; ++t) S.sv_ptr[t + 1] += S.sv_ptr[t];
   S.sv_src.assign(S.sv_ptr[S.row_ptr[ns]], 0);
   {
@@ -1360,7 +1407,8 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         for (int aa = 0; aa < uc; ++aa) S.sv_src[fill[S.row_ptr[s] + S.rel[S.rel_ptr[c] + aa]]++] = S.uvec_off[c] + aa;
       }
     for (const auto& g : S.lb)  // after the regular children (fixed order)
-      for (int k = 0; k < g.m; ++k) S.sv_src[fill[S.row_ptr[g.parent] + S.lb_gpos[g.gpos_off + k]]++] = g.uvec_off + k;
+      if (!S.top(g.parent))
+        for (int k = 0; k < g.m; ++k) S.sv_src[fill[S.row_ptr[g.parent] + S.lb_gpos[g.gpos_off + k]]++] = g.uvec_off + k;
   }
   S.xoff.assign(ns, -1);
   S.xlen = 0;
@@ -1381,6 +1429,9 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         for (int aa = 0; aa < uc; ++aa) S.sx_ptr[S.xoff[s] + S.rel[S.rel_ptr[c] + aa] + 1]++;
       }
     }
+    for (const auto& g : S.lb)  // this shard's members of groups under top fronts
+      if (S.top(g.parent))
+        for (int k = 0; k < g.m; ++k) S.sx_ptr[S.xoff[g.parent] + S.lb_gpos[g.gpos_off + k] + 1]++;
     for (int64_t t = 0; t < S.xlen; ++t) S.sx_ptr[t + 1] += S.sx_ptr[t];
     S.sx_src.assign(S.sx_ptr[S.xlen], 0);
     std::vector<int64_t> fill(S.sx_ptr.begin(), S.sx_ptr.end() - 1);
@@ -1393,6 +1444,9 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         for (int aa = 0; aa < uc; ++aa) S.sx_src[fill[S.xoff[s] + S.rel[S.rel_ptr[c] + aa]]++] = S.uvec_off[c] + aa;
       }
     }
+    for (const auto& g : S.lb)  // after the regular children (fixed order)
+      if (S.top(g.parent))
+        for (int k = 0; k < g.m; ++k) S.sx_src[fill[S.xoff[g.parent] + S.lb_gpos[g.gpos_off + k]]++] = g.uvec_off + k;
   }
   stamp("11 (end)");
 }

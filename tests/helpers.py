@@ -47,3 +47,17 @@ def block_angular_k2(m, n, nblocks, seed, coupling=0.02, delta=1e-8, well=False)
     Lw = sp.tril(K).tocsc()
     Lw.sort_indices()
     return K, Lw
+
+
+def dense_k2(m, n, seed, delta=1e-2):
+    """K2 of a QP with diagonal H and dense A (m x n): the x_j are single-column leaves with m-row
+    updates (batched leaves); returns (K, lower CSC with sorted indices)."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(seed)
+    A = rng.standard_normal((m, n))
+    sig = 10.0 ** rng.uniform(-1, 1, n)
+    K = sp.bmat([[sp.diags(sig), sp.csr_matrix(A.T)], [sp.csr_matrix(A), -delta * sp.eye(m)]]).tocsc()
+    K.sum_duplicates()
+    Lw = sp.tril(K).tocsc()
+    Lw.sort_indices()
+    return K, Lw

@@ -206,16 +206,7 @@ def test_ldl_zero_pivot_reported():
 
 
 # ---------------------------------------------------------------- batched leaf columns (dense QP, config 3)
-def _dense_k2(m, n, seed, delta=1e-2):
-    import scipy.sparse as sp
-    rng = np.random.default_rng(seed)
-    A = rng.standard_normal((m, n))
-    sig = 10.0 ** rng.uniform(-1, 1, n)
-    K = sp.bmat([[sp.diags(sig), sp.csr_matrix(A.T)], [sp.csr_matrix(A), -delta * sp.eye(m)]]).tocsc()
-    K.sum_duplicates()
-    Lw = sp.tril(K).tocsc()
-    Lw.sort_indices()
-    return K, Lw
+from helpers import dense_k2 as _dense_k2  # noqa: E402
 
 
 @pytest.mark.parametrize("m,n,ordering,sfm", [(150, 1000, 0, 128), (200, 3000, 0, 128), (150, 1000, 1, 128),

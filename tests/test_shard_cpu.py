@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 from madipm_amd._lib import Symbolic, default_ldl_opts
-from tests.helpers import block_angular_k2, random_k2
+from tests.helpers import block_angular_k2, dense_k2, random_k2
 
 
 def _owners(Lw, P, shard=0):
@@ -52,3 +52,22 @@ def test_unsharded_plan_has_no_top():
     _, Lw = block_angular_k2(600, 1200, 12, 1)
     S = Symbolic(Lw.shape[0], Lw.indptr, Lw.indices, default_ldl_opts())
     assert (S.shard_info()["owner"] == 0).all()
+
+
+@pytest.mark.parametrize("P", [2, 3, 4])
+def test_batched_leaves_dealt_to_shards(P):
+    """Dense-column K2: the batched-leaf group under the (top) y front keeps, on each shard, exactly
+    that shard's members — every x_j on one shard, balanced within one — and the exchange sizes of
+    the sharded plan are shard-independent."""
+    K, Lw = dense_k2(150, 1000, 3)
+    N = K.shape[0]
+    S1 = Symbolic(N, Lw.indptr, Lw.indices, default_ldl_opts(ordering=0))
+    assert S1.info()["lb_groups"] == 1 and S1.info()["lb_members"] == 1000
+    mem = []
+    for r in range(P):
+        S = Symbolic(N, Lw.indptr, Lw.indices, default_ldl_opts(ordering=0), nshards=P, shard=r)
+        inf, own = S.info(), S.shard_info()["owner"]
+        assert inf["lb_groups"] == 1
+        mem.append(inf["lb_members"])
+        assert (own == -1).sum() >= 1  # the y front is on top
+    assert sum(mem) == 1000 and max(mem) - min(mem) <= 1

@@ -10,7 +10,7 @@ reaches the same status, iteration count (+-1) and objective (1e-8 relative) as 
 import numpy as np
 import pytest
 
-from helpers import block_angular_k2, random_k2
+from helpers import block_angular_k2, dense_k2, random_k2
 from oracle.ldl import OracleLDL
 
 pytestmark = pytest.mark.gpu
@@ -53,6 +53,40 @@ def test_sharded_group_matches_unsharded(P, kind):
     xr = o.solve(b)
     assert np.max(np.abs(x1 - xr)) <= 1e-11 * np.max(np.abs(xr))
     # a second factorisation / solve reuses the buffers (epochs, counters, zeroed top region)
+    rc2, x2 = _solve(grp, Lw, 2.0 * b)
+    assert rc2 == 0 and np.max(np.abs(x2 - 2.0 * x1)) <= 1e-12 * np.max(np.abs(x1))
+
+
+@pytest.mark.parametrize("P", [2, 3, 4])
+def test_sharded_batched_leaves(P):
+    """Dense-column K2 (diagonal H, dense A: every x_j a batched leaf under the y front) sharded P
+    ways: the y front is the top, the x_j are dealt to the shards, each shard's MFMA SYRK adds its
+    members' W D^-1 W^T to the top front's external part (all-reduced) and its GEMV forward sums to
+    the exchanged top right-hand side.  Same pivots / solution as unsharded to 1e-12, and the
+    oracle's."""
+    from madipm_amd.linear_solver import HIPLDLSolver
+    from madipm_amd._lib import Symbolic, default_ldl_opts
+    K, Lw = dense_k2(150, 1000, 3)
+    N = K.shape[0]
+    b = np.random.default_rng(P).standard_normal(N)
+    ref = HIPLDLSolver(N, Lw.indptr, Lw.indices, ordering=0)
+    assert ref.info()["lb_members"] == 1000
+    rc0, x0 = _solve(ref, Lw, b)
+    # every member on exactly one shard
+    mem = [Symbolic(N, Lw.indptr, Lw.indices, default_ldl_opts(ordering=0), nshards=P, shard=r).info()["lb_members"]
+           for r in range(P)]
+    assert sum(mem) == 1000 and min(mem) > 0
+    grp = HIPLDLSolver(N, Lw.indptr, Lw.indices, ordering=0, nshards=P)
+    rc1, x1 = _solve(grp, Lw, b)
+    assert rc0 == rc1 == 0 and grp.is_factorized()
+    d0, d1 = ref.diag(), grp.diag()
+    assert np.all(np.abs(d1 - d0) <= 1e-12 * np.abs(d0)), np.max(np.abs(d1 - d0) / np.abs(d0))
+    assert np.max(np.abs(x1 - x0)) <= 1e-12 * np.max(np.abs(x0))
+    assert grp.inertia() == ref.inertia() == (1000, 0, 150)
+    o = OracleLDL(K, ref.perm())
+    assert o.factorize() == N
+    xr = o.solve(b)
+    assert np.max(np.abs(x1 - xr)) <= 1e-11 * np.max(np.abs(xr))
     rc2, x2 = _solve(grp, Lw, 2.0 * b)
     assert rc2 == 0 and np.max(np.abs(x2 - 2.0 * x1)) <= 1e-12 * np.max(np.abs(x1))
 
@@ -137,15 +171,22 @@ def _mpc_cases():
     gold = os.path.join(os.path.dirname(__file__), "golden", "afiro.mps")
     return {"afiro_std": lambda: standard_form_qp(read_mps(gold)),
             "random_lp": lambda: random_lp(200, 400, 0.02, 3, ineq_frac=0.3),
-            "ex10_small": lambda: standard_form_qp(ex10_standin(scale=0.05))}
+            "ex10_small": lambda: standard_form_qp(ex10_standin(scale=0.05)),
+            "dense_qp": lambda: __import__("madipm_amd.instances", fromlist=["dense_qp"]).dense_qp(n=1200, m=200,
+                                                                                                   seed=0)}
 
 
 @pytest.mark.parametrize("P", [2, 4])
-@pytest.mark.parametrize("case", ["afiro_std", "random_lp", "ex10_small"])
+@pytest.mark.parametrize("case", ["afiro_std", "random_lp", "ex10_small", "dense_qp"])
 def test_mpc_on_sharded_solver(P, case):
+    """The MPC loop on a sharded solver (dense_qp: batched leaves dealt to the shards) reaches the
+    unsharded solve's status, iteration count and objective."""
     from madipm_amd import MPCSolver, FixedRegularization
     qp = _mpc_cases()[case]()
     kw = dict(regularization=FixedRegularization(1e-8, -1e-8), max_iter=300)
+    if case == "dense_qp":
+        kw["ordering"] = 0  # natural order: the x columns are the batched leaves
+        assert MPCSolver(qp, nshards=P, **kw).ldl_info()["lb_members"] > 0
     a = MPCSolver(qp, **kw).solve()
     b = MPCSolver(qp, nshards=P, **kw).solve()
     assert a.status == b.status == 1
