@@ -543,33 +543,69 @@ __global__ __launch_bounds__(ANT) void k_assemble(FrontTab T, const SymbolicPlan
     for (int k = 0; k < 4; ++k) Ft[tid + k * ANT] = 0.0;
   }
   if (tl.bt1 > tl.bt0) {
-    __syncthreads();
-    for (int k = tl.bt0; k < tl.bt1; ++k) {
-      const int c = bt[5 * k], b0 = bt[5 * k + 1], b1 = bt[5 * k + 2], a0 = bt[5 * k + 3], a1 = bt[5 * k + 4];
-      const double* __restrict__ U = arena + T.u_off[c];
-      const int64_t ldc = T.u_ld[c];
-      const int32_t* __restrict__ rel = T.rel + T.rel_ptr[c];
-      // a wave takes 4 of its columns at once: the row map rel[a] is loaded once for them and their
-      // 4 U loads are in flight together (one dependent round trip per row chunk, not per column)
-      constexpr int NW = ANT / 64;
-      for (int b = b0 + wv; b < b1; b += 4 * NW) {
-        int cb[4], bk[4];
+    // Big children's update blocks, child by child (fixed order: a barrier between children, whose
+    // entries may land on the same tile entry).  The children's symbolic table (bt entry, U offset
+    // and ld, row-map offset) is staged in LDS per 64 children, so a child's operand loads (its row
+    // map and U entries, ~9 per lane) are ONE round trip, issued while the previous child's adds run
+    // (r2 read bt -> u_off -> rel / U per child: three dependent round trips each).  A wave takes 4
+    // columns (b0 + wv + 16 j) and a lane one row (a0 + lane) of the child's <= 64 x 64 block; masked
+    // lanes load from inside the same column (no extra lines), added nothing.
+    constexpr int CH = 64;
+    __shared__ int32_t sbt[CH * 5], sld[CH];
+    __shared__ int64_t suo[CH], srp[CH];
+    constexpr int NW = ANT / 64;
+    struct Ops {  // one child's operands for this lane (raw: the row map is applied at the add)
+      double u[4];
+      int ra, rb[4], ok;
+    };
+    auto load = [&](int k, Ops& o) {
+      const int b0 = sbt[5 * k + 1], b1 = sbt[5 * k + 2], a0 = sbt[5 * k + 3], a1 = sbt[5 * k + 4];
+      const double* __restrict__ U = arena + suo[k];
+      const int64_t ldc = sld[k];
+      const int32_t* __restrict__ rel = T.rel + srp[k];
+      const int a = a0 + lane, ac = min(a, a1 - 1);
+      o.ra = rel[ac];
+      o.ok = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          bk[k] = b + k * NW;
-          cb[k] = (bk[k] < b1) ? (rel[bk[k]] - J0) * 64 - I0 : 0;
-        }
-        for (int a = max(b, a0) + lane; a < a1; a += 64) {
-          const int ra = rel[a];
-          double u[4];
+      for (int j = 0; j < 4; ++j) {
+        const int bk = b0 + wv + NW * j, bc = min(bk, b1 - 1);
+        o.rb[j] = rel[bc];
+        o.u[j] = U[max(ac, bc) + (int64_t)bc * ldc];
+        o.ok |= ((bk < b1) & (a < a1) & (a >= bk)) << j;
+      }
+    };
+    auto add = [&](const Ops& o) {
 #pragma unroll
-          for (int k = 0; k < 4; ++k) u[k] = (bk[k] < b1 && a >= bk[k]) ? U[a + bk[k] * ldc] : 0.0;
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            if (bk[k] < b1 && a >= bk[k]) Ft[ra + cb[k]] += u[k];
-        }
+      for (int j = 0; j < 4; ++j)
+        if ((o.ok >> j) & 1) Ft[(o.ra - I0) + (o.rb[j] - J0) * 64] += o.u[j];
+    };
+    for (int kc = tl.bt0; kc < tl.bt1; kc += CH) {
+      const int nk = min(CH, tl.bt1 - kc);
+      __syncthreads();  // the chunk sums are in Ft; the previous table is no longer read
+      if (tid < nk * 5) sbt[tid] = bt[5 * kc + tid];
+      __syncthreads();
+      if (tid < nk) {
+        const int c = sbt[5 * tid];
+        suo[tid] = T.u_off[c];
+        sld[tid] = (int32_t)T.u_ld[c];
+        srp[tid] = T.rel_ptr[c];
       }
       __syncthreads();
+      // two operand sets, alternately loaded and added (no register copies: a copy of a loaded value
+      // waits for it, which serialised the pipeline)
+      // the loads are issued unconditionally (clamped child: a conditional issue leaves the wait
+      // counter ambiguous and the compiler waits for everything)
+      Ops o0, o1;
+      load(0, o0);
+      for (int k = 0; k < nk; k += 2) {
+        load(min(k + 1, nk - 1), o1);
+        add(o0);
+        __syncthreads();
+        if (k + 1 >= nk) break;
+        load(min(k + 2, nk - 1), o0);
+        add(o1);
+        __syncthreads();
+      }
     }
   }
   __syncthreads();
@@ -1790,14 +1826,17 @@ __global__ __launch_bounds__(NT) void k_big_diag(FrontTab T, const int32_t* __re
   double* __restrict__ F = arena + T.l_off[s] + k0 + (int64_t)k0 * r;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   {
+    // all 16 loads in flight from clamped addresses, masked after (a predicated load compiles into a
+    // branch with a wait of its own)
     double v[16];
+    const int lc = min(lane, kw - 1);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) v[e] = F[lc + (int64_t)min(wv + 4 * e, kw - 1) * r];
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int j = wv + 4 * e;
-      v[e] = (lane < kw && j < kw) ? (lane >= j ? F[lane + (int64_t)j * r] : 0.0) : (lane == j ? 1.0 : 0.0);
+      A64[lane + j * LDA] = (lane < kw && j < kw) ? (lane >= j ? v[e] : 0.0) : (lane == j ? 1.0 : 0.0);
     }
-#pragma unroll
-    for (int e = 0; e < 16; ++e) A64[lane + (wv + 4 * e) * LDA] = v[e];
   }
   __syncthreads();
   diag64(A64, Dl, Ms, cbuf, tid);
@@ -1832,26 +1871,28 @@ __global__ __launch_bounds__(NT) void k_big_trsm(FrontTab T, const int32_t* __re
   double* S = Sl[wv];
   const int row = I0 + 16 * wv + (lane & 15);  // slab row of this lane; 4 columns per pass
   {
+    // every operand load in flight at once from clamped addresses, masked at the LDS stores (a
+    // predicated load compiles into a branch with a wait of its own)
     double lv[16], sv[16], mv[5], dv;
+    const int lc = min(lane, kw - 1), rc = min(row, r - 1);
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      const int j = wv + 4 * e;
-      lv[e] = (lane < kw && j < kw && lane > j) ? F[(k0 + lane) + (int64_t)(k0 + j) * r] : 0.0;
-      const int jj = (lane >> 4) + 4 * e;
-      sv[e] = (row < r && jj < kw) ? F[row + (int64_t)(k0 + jj) * r] : 0.0;
+      lv[e] = F[(k0 + lc) + (int64_t)(k0 + min(wv + 4 * e, kw - 1)) * r];
+      sv[e] = F[rc + (int64_t)(k0 + min((lane >> 4) + 4 * e, kw - 1)) * r];
     }
 #pragma unroll
-    for (int e = 0; e < 5; ++e) mv[e] = (tid + e * NT < 4 * 16 * LDM) ? M[tid + e * NT] : 0.0;
-    dv = (tid < kw) ? D[f0 + k0 + tid] : 1.0;
+    for (int e = 0; e < 5; ++e) mv[e] = M[min(tid + e * NT, 4 * 16 * LDM - 1)];
+    dv = D[f0 + k0 + min(tid, kw - 1)];
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      L11[lane + (wv + 4 * e) * LDA] = lv[e];
-      S[(lane & 15) + ((lane >> 4) + 4 * e) * 17] = sv[e];
+      const int j = wv + 4 * e, jj = (lane >> 4) + 4 * e;
+      L11[lane + j * LDA] = (lane < kw && j < kw && lane > j) ? lv[e] : 0.0;
+      S[(lane & 15) + jj * 17] = (row < r && jj < kw) ? sv[e] : 0.0;
     }
 #pragma unroll
     for (int e = 0; e < 5; ++e)
       if (tid + e * NT < 4 * 16 * LDM) Ms[tid + e * NT] = mv[e];
-    if (tid < 64) Dl[tid] = dv;
+    if (tid < 64) Dl[tid] = (tid < kw) ? dv : 1.0;
   }
   __syncthreads();
   for (int K = 0; K < 4; ++K) {
@@ -2562,21 +2603,32 @@ __global__ __launch_bounds__(NT) void k_fwd_big(FrontTab T, const SolveTask* __r
     const int row = row0 + lane;
     const bool pivot_blk = row0 < w;
     const int kw = pivot_blk ? min(64, w - row0) : 0;
+    // every load below is issued unconditionally from a clamped address and masked after: a
+    // predicated load compiles into a branch with a wait of its own (16 serial round trips per batch)
+    const int rowc = row0 + min(lane, nrow - 1);
     // prefetch the diagonal block (columns row0 .. row0+kw-1 of this row block) into LDS
-    for (int tt = g; tt < kw; tt += 4)
-      Ld[tt * 65 + lane] = (lane < nrow) ? L[row + (int64_t)(row0 + tt) * r] : 0.0;
+    if (kw > 0) {
+      double v[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) v[e] = L[rowc + (int64_t)(row0 + min(g + 4 * e, kw - 1)) * r];
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        if (g + 4 * e < kw) Ld[(g + 4 * e) * 65 + lane] = (lane < nrow) ? v[e] : 0.0;
+    }
     double acc = 0.0;
     for (int p = 0; p < np; ++p) {
       double lv[16];
       const int cb = p * 64 + g * 16;
 #pragma unroll
-      for (int cc = 0; cc < 16; ++cc)
-        lv[cc] = (lane < nrow && cb + cc < w) ? L[row + (int64_t)(cb + cc) * r] : 0.0;
+      for (int cc = 0; cc < 16; ++cc) lv[cc] = L[rowc + (int64_t)min(cb + cc, w - 1) * r];
+#pragma unroll
+      for (int cc = 0; cc < 16; ++cc) lv[cc] = (lane < nrow && cb + cc < w) ? lv[cc] : 0.0;
       if (tid == 0) wait_flag(&flags[flag_off[s] + p], epoch, err);
       __syncthreads();
       if (tid < 64) {
         const int c = p * 64 + tid;
-        xs[tid] = (c < w) ? xi[f0 + c] : 0.0;
+        const double xv = xi[f0 + min(c, w - 1)];
+        xs[tid] = (c < w) ? xv : 0.0;
       }
       __syncthreads();
 #pragma unroll
@@ -2628,8 +2680,16 @@ __global__ __launch_bounds__(NT) void k_bwd_below(FrontTab T, const int32_t* __r
   double acc = 0.0;
   for (int rb = R0; rb < R1; rb += 64) {
     const int nr = min(64, R1 - rb);
-    for (int j = g; j < 64; j += 4) tile[lane * 65 + j] = (lane < nr && j < kw) ? L[(rb + lane) + (int64_t)(c0 + j) * r] : 0.0;
-    if (tid < 64) xr[tid] = (tid < nr) ? xi[rows[rb + tid]] : 0.0;
+    {  // unconditional loads from clamped addresses, masked at the LDS stores
+      double v[16];
+      const int rc = rb + min(lane, nr - 1);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) v[e] = L[rc + (int64_t)(c0 + min(g + 4 * e, kw - 1)) * r];
+      const double xv = (tid < 64) ? xi[rows[rb + min(tid, nr - 1)]] : 0.0;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) tile[lane * 65 + g + 4 * e] = (lane < nr && g + 4 * e < kw) ? v[e] : 0.0;
+      if (tid < 64) xr[tid] = (tid < nr) ? xv : 0.0;
+    }
     __syncthreads();
 #pragma unroll
     for (int rr = 0; rr < 16; ++rr) acc += tile[(g * 16 + rr) * 65 + lane] * xr[g * 16 + rr];
@@ -2667,8 +2727,15 @@ __global__ __launch_bounds__(NT) void k_bwd_big(FrontTab T, const SolveTask* __r
     const double* __restrict__ L = arena + T.l_off[s];
     const int c0 = p * 64, kw = min(64, w - c0);
     const int npan = (w + 63) >> 6;
-    // diagonal block L(c0+i, c0+j) -> Ld[i*65+j]
-    for (int j = g; j < kw; j += 4) Ld[lane * 65 + j] = (lane < kw) ? L[(c0 + lane) + (int64_t)(c0 + j) * r] : 0.0;
+    // diagonal block L(c0+i, c0+j) -> Ld[i*65+j] (unconditional clamped loads, masked at the store)
+    {
+      double v[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) v[e] = L[(c0 + min(lane, kw - 1)) + (int64_t)(c0 + min(g + 4 * e, kw - 1)) * r];
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        if (g + 4 * e < kw) Ld[lane * 65 + g + 4 * e] = (lane < kw) ? v[e] : 0.0;
+    }
     double acc = 0.0;  // partial for column c0+lane over this wave's rows of each tile
     // pivot panels q = npan-1 .. p+1 (wait for each); the rows below come from k_bwd_below
     for (int k = 0; k < npan - 1 - p; ++k) {
@@ -2677,8 +2744,17 @@ __global__ __launch_bounds__(NT) void k_bwd_big(FrontTab T, const SolveTask* __r
       if (tid == 0) wait_flag(&flags[flag_off[s] + q], epoch, err);
       __syncthreads();
       // stage the 64 x 64 tile L(rb.., c0..) (coalesced over rows) and the x values of its rows
-      for (int j = g; j < kw; j += 4) tile[lane * 65 + j] = (lane < nr) ? L[(rb + lane) + (int64_t)(c0 + j) * r] : 0.0;
-      if (tid < 64) xr[tid] = (tid < nr) ? xi[f0 + rb + tid] : 0.0;
+      {
+        double v[16];
+        const int rc = rb + min(lane, nr - 1);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) v[e] = L[rc + (int64_t)(c0 + min(g + 4 * e, kw - 1)) * r];
+        const double xv = (tid < 64) ? xi[f0 + rb + min(tid, nr - 1)] : 0.0;
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+          if (g + 4 * e < kw) tile[lane * 65 + g + 4 * e] = (lane < nr) ? v[e] : 0.0;
+        if (tid < 64) xr[tid] = (tid < nr) ? xv : 0.0;
+      }
       __syncthreads();
 #pragma unroll
       for (int rr = 0; rr < 16; ++rr) acc += tile[(g * 16 + rr) * 65 + lane] * xr[g * 16 + rr];
