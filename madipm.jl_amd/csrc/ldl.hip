@@ -1926,35 +1926,53 @@ __global__ __launch_bounds__(NT) void k_big_trsm(FrontTab T, const int32_t* __re
     if (row < r) F[row + (int64_t)(k0 + j) * r] = S[(lane & 15) + j * 17];
 }
 
-// Trailing update of one 64x64 lower tile: C -= (L_I D) L_J^T, f64 MFMA 16x16x4.
-__global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __restrict__ list, int step,
+// Trailing update of one 64x64 lower tile: C -= (L_I D) L_J^T, f64 MFMA 16x16x4, over K = the
+// columns of up to kpan panels (deferred multi-panel update).  Task tij = ti | tj << 16 | mode << 31:
+//   mode 0 (local): K = panel `step` only, tiles relative to the panel's end, columns limited to the
+//     end of the panel group (kpan panels from (step / kpan) kpan): the group's later panels only;
+//   mode 1 (trailing): K = the panels of the group ending at `step`, tiles relative to the group's
+//     end: the rest of the front, ONE load/store of C per group instead of one per panel.
+// kpan = 1: every step is a group of one (the r2 right-looking update).  The K chunks of 64 are
+// staged through LDS one after another; the next chunk's operands are loaded (from
+// clamped addresses) while the current chunk's MFMAs run.
+__global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __restrict__ list, int step, int kpan,
                                                    double* __restrict__ arena, const double* __restrict__ D) {
   constexpr int LDT = 80;  // [k][row] layout: conflict-free ds_read_b64 for the 16x4 operand pattern
   __shared__ __attribute__((aligned(16))) double Wt[64 * LDT];
   __shared__ __attribute__((aligned(16))) double Lt[64 * LDT];
   int s, tij;
   task_of(list, s, tij);
-  const int ti = tij & 0xffff, tj = tij >> 16;
+  const int ti = tij & 0xffff, tj = (tij >> 16) & 0x7fff;
+  const bool trailing = tij < 0;
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
-  const int k0 = step * 64, kw = min(64, w - k0), c0 = k0 + kw;
+  const int g0 = (step / kpan) * kpan;                         // first panel of the group
+  const int gend = min(64 * (g0 + kpan), w);                   // first column after the group
+  const int kb = trailing ? 64 * g0 : 64 * step;               // K range [kb, ke)
+  const int ke = trailing ? gend : min(64 * step + 64, w);
+  const int c0 = ke;                                           // tiles relative to the K range's end
+  const int jlim = trailing ? r : gend;
   const int I0 = c0 + ti * 64, J0 = c0 + tj * 64;
+  const int nch = (ke - kb + 63) >> 6;                         // K chunks of 64 (<= kpan)
   double* __restrict__ F = arena + T.l_off[s];
-  const double* __restrict__ Dp = D + f0 + k0;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int qr = (wv >> 1) * 32, qc = (wv & 1) * 32;
-  // all global loads of the operands first (one latency), from clamped addresses (a predicated load
-  // compiles into a branch with a wait inside), masked at the LDS store
-  double wl[16], ll[16], dk[16];
   const int ri = min(I0 + lane, r - 1), rj = min(J0 + lane, r - 1);
+  // operands of chunk ch: columns kb + 64 ch + wv + 4 e (clamped into the K range); one register
+  // set, reloaded with the next chunk right after its LDS stores, so those loads run under the
+  // current chunk's MFMAs (which read LDS only)
+  double wl[16], ll[16], dk[16];
+  auto load = [&](int ch) {
 #pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const int kk = min(wv + 4 * e, kw - 1);
-    const int64_t col = (int64_t)(k0 + kk) * r;
-    wl[e] = F[ri + col];
-    ll[e] = F[rj + col];
-    dk[e] = Dp[kk];
-  }
-  // C tile prefetch (its latency overlaps the MFMA loop)
+    for (int e = 0; e < 16; ++e) {
+      const int kk = min(kb + 64 * ch + wv + 4 * e, ke - 1);
+      const int64_t col = (int64_t)kk * r;
+      wl[e] = F[ri + col];
+      ll[e] = F[rj + col];
+      dk[e] = D[f0 + kk];
+    }
+  };
+  load(0);
+  // C tile prefetch (its latency overlaps the first chunk)
   double c[2][2][4];
 #pragma unroll
   for (int bj = 0; bj < 2; ++bj)
@@ -1966,32 +1984,37 @@ __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __
         const int j = min(J0 + qc + bj * 16 + (lane >> 4) + 4 * g, r - 1);
         c[bj][bi][g] = F[i + (int64_t)j * r];  // masked at the store
       }
-#pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const int kk = wv + 4 * e;
-    Wt[kk * LDT + lane] = (kk < kw && I0 + lane < r) ? wl[e] * dk[e] : 0.0;
-    Lt[kk * LDT + lane] = (kk < kw && J0 + lane < r) ? ll[e] : 0.0;
-  }
-  __syncthreads();
   dbl4 acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
-  const int nks = (kw + 3) >> 2;
+  for (int ch = 0; ch < nch; ++ch) {
+    const int kc = kb + 64 * ch, kw = min(64, ke - kc);
 #pragma unroll
-  for (int ks = 0; ks < 16; ++ks) {
-    if (ks < nks) {  // wave-uniform
-      const int kk = ks * 4 + (lane >> 4);
-      const double a0 = Lt[kk * LDT + qc + (lane & 15)];
-      const double a1 = Lt[kk * LDT + qc + 16 + (lane & 15)];
-      const double b0 = Wt[kk * LDT + qr + (lane & 15)];
-      const double b1 = Wt[kk * LDT + qr + 16 + (lane & 15)];
-      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    for (int e = 0; e < 16; ++e) {
+      const int kk = wv + 4 * e;
+      Wt[kk * LDT + lane] = (kk < kw && I0 + lane < r) ? wl[e] * dk[e] : 0.0;
+      Lt[kk * LDT + lane] = (kk < kw && J0 + lane < r) ? ll[e] : 0.0;
     }
+    __syncthreads();
+    if (ch + 1 < nch) load(ch + 1);  // wave-uniform
+    const int nks = (kw + 3) >> 2;
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      if (ks < nks) {  // wave-uniform
+        const int kk = ks * 4 + (lane >> 4);
+        const double a0 = Lt[kk * LDT + qc + (lane & 15)];
+        const double a1 = Lt[kk * LDT + qc + 16 + (lane & 15)];
+        const double b0 = Wt[kk * LDT + qr + (lane & 15)];
+        const double b1 = Wt[kk * LDT + qr + 16 + (lane & 15)];
+        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+      }
+    }
+    if (ch + 1 < nch) __syncthreads();  // the LDS tiles are rewritten by the next chunk
   }
   // D layout: col n = lane&15 (-> row i of F), row m = (lane>>4) + 4g (-> column j of F)
 #pragma unroll
@@ -2002,7 +2025,7 @@ __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __
       for (int g = 0; g < 4; ++g) {
         const int i = I0 + qr + bi * 16 + (lane & 15);
         const int j = J0 + qc + bj * 16 + (lane >> 4) + 4 * g;
-        if (i < r && j < r && i >= j) F[i + (int64_t)j * r] = c[bj][bi][g] - acc[bj][bi][g];
+        if (i < r && j < jlim && i >= j) F[i + (int64_t)j * r] = c[bj][bi][g] - acc[bj][bi][g];
       }
 }
 
@@ -3400,6 +3423,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   {
     const char* ev = std::getenv("MADIPM_SCHUR_DEFER");
     T_.schur_defer = (ev && ev[0] == '0') ? 0 : 1;
+    const char* ek = std::getenv("MADIPM_BIG_KPAN");  // panels per deferred big-front update group
+    big_kpan_ = ek ? std::max(1, std::min(8, std::atoi(ek))) : 4;
     const char* e16 = std::getenv("MADIPM_F16R");  // register-resident 16-pivot block factor (factor16r)
     T_.f16r = (e16 && e16[0] == '0') ? 0 : 1;
   }
@@ -3793,7 +3818,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         double kb[3] = {0, 0, 0}, kf[3] = {0, 0, 0}, ka = 0;
         for (int s : big) {
           const int w = S.first[s + 1] - S.first[s], r = S.nrows[s];
-          if (cdiv(w, 64) <= p) continue;
+          const int npan = (int)cdiv(w, 64);
+          if (npan <= p) continue;
           const int k0 = p * 64, kw = std::min(64, w - k0);
           const int nt = (int)cdiv(r - k0 - kw, 64);
           const double dk = kw, nb = r - k0 - kw;
@@ -3802,12 +3828,27 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
           kf[0] += dk * dk * dk / 3.0;
           kb[1] += 8.0 * (2.0 * nb * dk + nt * (dk * (dk + 1) / 2 + 4 * 16 * 17));  // trsm: rows in/out + L11, M per tile
           kf[1] += nb * dk * dk;
-          kb[2] += 8.0 * (nb * (nb + 1) + 2.0 * nb * dk);  // update: C in/out + the panel once
-          kf[2] += dk * nb * (nb + 1);
           td.insert(td.end(), {s, 0});
           for (int i = 0; i < nt; ++i) tt.insert(tt.end(), {s, i});
-          for (int i = 0; i < nt; ++i)
-            for (int j = 0; j <= i; ++j) tu.insert(tu.end(), {s, i | (j << 16)});
+          // deferred multi-panel update (k_big_update): panel groups of big_kpan_ panels; inside a
+          // group each panel updates the group's later panels only (local tiles), the group's last
+          // panel updates the rest of the front with K = the whole group (trailing tiles)
+          const int g0 = (p / big_kpan_) * big_kpan_, gl = std::min(g0 + big_kpan_, npan) - 1;
+          const int gend = std::min(64 * (gl + 1), w);
+          if (p < gl) {
+            const double nc = gend - (k0 + kw);  // the group's later columns
+            for (int j = 0; j < (int)cdiv((int)nc, 64); ++j)
+              for (int i = j; i < nt; ++i) tu.insert(tu.end(), {s, i | (j << 16)});
+            kb[2] += 8.0 * (2.0 * nb * nc + nb * dk + nc * dk);  // C in/out + the panel rows once
+            kf[2] += 2.0 * dk * nc * (nb - 0.5 * nc);
+          } else {
+            const int c0 = gend, ntt = (int)cdiv(r - c0, 64);
+            const double K = gend - 64 * g0, nbt = r - c0;
+            for (int i = 0; i < ntt; ++i)
+              for (int j = 0; j <= i; ++j) tu.insert(tu.end(), {s, (int32_t)((uint32_t)(i | (j << 16)) | 0x80000000u)});
+            kb[2] += 8.0 * (nbt * (nbt + 1) + 2.0 * nbt * K);  // C in/out once per group + the group's panels
+            kf[2] += K * nbt * (nbt + 1);
+          }
         }
         const std::pair<int, std::vector<int32_t>*> kinds[3] = {{BIG_DIAG, &td}, {BIG_TRSM, &tt}, {BIG_UPDATE, &tu}};
         for (int q = 0; q < 3; ++q) {
@@ -4297,7 +4338,8 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
         TIMED(KK_TRSM, L.bytes, 0.0, L.flops, (k_big_trsm<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_, minv_)));
         break;
       case BIG_UPDATE:
-        TIMED(KK_UPDATE, L.bytes, 0.0, L.flops, (k_big_update<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_)));
+        TIMED(KK_UPDATE, L.bytes, 0.0, L.flops,
+              (k_big_update<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, big_kpan_, arena_, D_)));
         break;
       case LB_BUILD:
         TIMED(KK_LB_BUILD, L.bytes, L.alg, 0.0,

@@ -125,6 +125,24 @@ def test_ldl_diag_block_variants(f16r, sfm, well, monkeypatch):
     _check_case(K, Lw, small_front_max=sfm, well=True)
 
 
+@pytest.mark.parametrize("kpan", ["1", "2", "4"])
+@pytest.mark.parametrize("n,m", [(320, 100), (130, 200)])
+def test_big_front_panel_groups(kpan, n, m, monkeypatch):
+    """A dense K2 (dense SPD H, dense A: one big front of n + m columns, several 64-column panels
+    with a partial last one) on the big-front path with the deferred multi-panel trailing update in
+    groups of MADIPM_BIG_KPAN panels (1 = right-looking per panel): pivots and solution of the oracle."""
+    import scipy.sparse as sp
+    monkeypatch.setenv("MADIPM_BIG_KPAN", kpan)
+    rng = np.random.default_rng(11)
+    B = rng.standard_normal((n, n))
+    H = B @ B.T / n + np.eye(n)
+    A = rng.standard_normal((m, n))
+    K = sp.csc_matrix(np.block([[H, A.T], [A, -1e-2 * np.eye(m)]]))
+    Lw = sp.tril(K).tocsc()
+    Lw.sort_indices()
+    _check_case(K, Lw, small_front_max=16, well=True)
+
+
 @pytest.mark.parametrize("chain,sfold", [("0", "1"), ("0", "0"), ("0", "2"), ("1", "2"), ("1", "1")])
 @pytest.mark.parametrize("well", [True, False])
 def test_ldl_chain_solve_and_leaf_fold(chain, sfold, well, monkeypatch):
