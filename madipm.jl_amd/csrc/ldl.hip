@@ -1051,9 +1051,9 @@ __device__ __forceinline__ void trail_strip(double* A, int r, int ld, int k0, in
 // jlo <= J <= min(I, jhi), I < nbr; strips (I, J0 .. J0+3) dealt to waves w0, w0 + wstep, ...
 template <bool PK>
 __device__ __forceinline__ void trail_strips(double* A, int r, int ld, int k0, int kw, int R0, int nbr, int jlo, int jhi,
-                                             const double (&dk)[4], int w0, int wstep, int lane, int jend) {
+                                             const double (&dk)[4], int w0, int wstep, int lane, int jend, int i0 = 0) {
   if (jlo > jhi) return;
-  int I = jlo, J0 = jlo;
+  int I = max(jlo, i0), J0 = jlo;  // rows I >= i0 only
   auto adv = [&]() {
     J0 += 4;
     if (J0 > min(I, jhi)) {
@@ -1237,6 +1237,171 @@ __device__ __forceinline__ void blocked_factor_lds(double* A, int r, int w, int 
   }
 }
 
+// ---- Pipelined schedule of the same factorisation (MADIPM_FACT_PIPE=1, default; needs factor16r).
+// In blocked_factor_lds every pivot block costs panel + column-0 strips + max(next diagonal factor,
+// trailing update), three workgroup barriers apart, and the diagonal factor (~2.6 us of division and
+// lane-swap latency) dominates.  Here wave 0 runs the pivot chain alone: once block k is factorised it
+// forms the panel tile of row block 0 below it (the next pivot rows), updates the next diagonal tile
+// with it and factorises that tile at once — while waves 1.. form the rest of block k's panel and its
+// trailing update.  Hand-offs are LDS counters (workgroup-scope release / acquire), not barriers, so
+// the chain never waits for the trailing update of its own step:
+//   mk     = k + 1  wave 0: block k's M_K (buffer k & 1), pivots and L_kk are in LDS
+//   pt     = k + 1  wave 0: panel tile 0 of step k is in LDS
+//   j0    += 1      each other wave, after its priority tiles of step k: column block 0 (tiles (I, 0),
+//                   I >= 1) and the diagonal tile (1, 1) — everything wave 0 reads at step k + 1
+//   ob    += 1      barrier among the other waves (panel rows complete before the trailing update)
+// Tile (0, 0) of a non-final step is wave 0's alone.  Every tile and panel block is formed by the
+// same MFMA sequence from the same operands as in blocked_factor_lds: the two schedules agree
+// bitwise (test_ldl_fact_pipe_bitwise).  A wait that spins for ~2^20 polls sets `abort` (a schedule
+// bug must not hang the GPU: the factor is then garbage and the tests fail).
+struct PipeCtr {
+  int mk, pt, j0, ob, abort;
+  int64_t ow;  // diagnostics: wave 1's wait ticks
+};
+__device__ __forceinline__ PipeCtr& pipe_ctr() {
+  __shared__ PipeCtr c;
+  return c;
+}
+__device__ __forceinline__ void pipe_wait(int* f, int v, int* abort) {
+  int spins = 0;
+  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v) {
+    if (__hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return;
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > (1 << 20)) {
+      __hip_atomic_store(abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return;
+    }
+  }
+}
+// one lane per wave, after the wave's LDS writes (the release orders them before the counter)
+__device__ __forceinline__ void pipe_set(int* f, int v) {
+  if ((threadIdx.x & 63) == 0) __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void pipe_add(int* f) {
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(f, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <bool PK>
+__device__ __forceinline__ void blocked_factor_pipe(double* A, int r, int w, int ld, double* Dl, double* MK0,
+                                                    double* MK1, int defer = 0, int64_t* pt = nullptr) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), nw = blockDim.x >> 6;
+  const int no = nw - 1;  // waves 1 .. nw - 1: panel rest + trailing update
+  const int nblk = (w + 15) >> 4;
+  defer = defer && w < r;
+  const int jend = defer ? w : r;
+  PipeCtr& pc = pipe_ctr();
+  int64_t t0 = (pt && tid == 0) ? wall_clock64() : 0;
+  if (tid == 0) pc = PipeCtr{0, 0, 0, 0, 0, 0};
+  // diagnostics (pt): wave 0's wait / diagonal-factor ticks, wave 1's wait ticks
+  const bool dbg = pt && (tid == 0 || tid == 64);
+  int64_t tw = 0, tf = 0, tc = 0;
+  auto lap = [&](int64_t& acc) {
+    if (dbg) {
+      const int64_t now = wall_clock64();
+      acc += now - tc;
+      tc = now;
+    }
+  };
+  if (wv == 0) factor16r<PK>(A, r, ld, 0, min(16, w), Dl, MK0, lane);
+  __syncthreads();  // block 0 factorised; the counters are zero
+  const int64_t t1 = (pt && tid == 0) ? wall_clock64() : 0;
+  int gen = 0;  // O-barrier generation (waves 1..)
+  for (int kb = 0; kb < nblk; ++kb) {
+    const int k0 = 16 * kb, kw = min(16, w - k0);
+    const int R0 = k0 + kw;
+    const int nbr = (r - R0 + 15) >> 4;
+    const int jhi = defer ? ((w - R0 + 15) >> 4) - 1 : nbr;
+    const bool last = kb + 1 == nblk;
+    const double* MKc = (kb & 1) ? MK1 : MK0;
+    double dk[4];
+    int64_t tx = 0;
+    if (dbg) tc = wall_clock64();
+    if (wv == 0) {
+      // the pivot chain: step kb - 1's priority tiles (this step's raw panel tile 0 and diagonal tile)
+      if (kb > 0) pipe_wait(&pc.j0, no * kb, &pc.abort);
+      lap(tw);
+      if (nbr > 0) panel_blocks<PK>(A, r, ld, k0, kw, R0, 1, MKc, 0, 1, lane);
+      pipe_set(&pc.pt, kb + 1);
+      if (!last) {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const int k = 4 * ks + (lane >> 4);
+          dk[ks] = (k < kw) ? Dl[k0 + min(k, kw - 1)] : 0.0;
+        }
+        trail_strip<PK, 1>(A, r, ld, k0, kw, R0, 0, 0, dk, lane, jend);  // the next diagonal tile
+        wave_sync();
+        lap(tx);
+        factor16r<PK>(A, r, ld, R0, min(16, w - R0), Dl, (kb & 1) ? MK0 : MK1, lane);
+        pipe_set(&pc.mk, kb + 2);
+        lap(tf);
+      }
+    } else {
+      const int ow = wv - 1;
+      if (kb > 0) {
+        pipe_wait(&pc.mk, kb + 1, &pc.abort);      // block kb's M_K and pivots
+        pipe_wait(&pc.j0, no * kb, &pc.abort);     // every other wave's column-0 tiles of step kb - 1 (raw panel rows)
+      }
+      lap(tw);
+      panel_blocks<PK>(A, r, ld, k0, kw, R0, nbr, MKc, 1 + ow, no, lane);  // rows 1 .. nbr - 1
+      ++gen;
+      lap(tx);
+      pipe_add(&pc.ob);
+      pipe_wait(&pc.ob, no * gen, &pc.abort);
+      pipe_wait(&pc.pt, kb + 1, &pc.abort);
+      lap(tw);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int k = 4 * ks + (lane >> 4);
+        dk[ks] = (k < kw) ? Dl[k0 + min(k, kw - 1)] : 0.0;
+      }
+      if (!last) {
+        // priority: strip (1, 0..1) (tile (1, 1) only inside the update range), then (I, 0) for I >= 2
+        const bool d11 = nbr > 1 && jhi >= 1;
+        for (int it = ow; it < nbr - 1; it += no) {
+          if (it == 0) {
+            if (d11)
+              trail_strip<PK, 2>(A, r, ld, k0, kw, R0, 1, 0, dk, lane, jend);
+            else
+              trail_strip<PK, 1>(A, r, ld, k0, kw, R0, 1, 0, dk, lane, jend);
+          } else {
+            trail_strip<PK, 1>(A, r, ld, k0, kw, R0, it + 1, 0, dk, lane, jend);
+          }
+        }
+        pipe_add(&pc.j0);
+        // the rest: rows I >= 2, column blocks 1 .. jhi
+        trail_strips<PK>(A, r, ld, k0, kw, R0, nbr, 1, jhi, dk, ow, no, lane, jend, 2);
+      } else if (!defer) {
+        trail_strips<PK>(A, r, ld, k0, kw, R0, nbr, 0, nbr, dk, ow, no, lane, jend);
+      }
+    }
+  }
+  if (dbg && tid == 64) pc.ow = tw;
+  __syncthreads();
+  const int64_t t2 = (pt && tid == 0) ? wall_clock64() : 0;
+  if (defer) {
+    schur_strips<PK>(A, r, ld, w, Dl, wv, nw, lane);
+    __syncthreads();
+  }
+  if (pt && tid == 0) {
+    pt[0] = t1 - t0;
+    pt[1] = t2 - t1;  // the pipelined block steps
+    pt[2] = tw;       // wave 0 waiting for the other waves' priority tiles
+    pt[3] = tf;       // wave 0 in factor16r
+    pt[4] = wall_clock64() - t2;
+    pt[5] = pc.ow;    // wave 1 waiting (M_K, barrier, panel tile 0, column-0 tiles)
+  }
+}
+
+template <bool PK>
+__device__ __forceinline__ void factor_lds(const FrontTab& T, double* A, int r, int w, int ld, double* Dl, double* MK,
+                                           double* cbuf, int64_t* pt = nullptr) {
+  if (T.fpipe && T.f16r && (blockDim.x >> 6) >= 2)
+    blocked_factor_pipe<PK>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer, pt);
+  else
+    blocked_factor_lds<PK>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer, pt, T.f16r);
+}
+
 
 // write-out: L panel (ld r; d on the diagonal, zeros above), lower triangle of U (ld uld), D and the
 // pivot check.  SC1: U stored write-through (handed to a parent inside the same launch).
@@ -1413,7 +1578,7 @@ __global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t*
     }
   }
   __syncthreads();
-  blocked_factor_lds<PK>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer, nullptr, T.f16r);
+  factor_lds<PK>(T, A, r, w, ld, Dl, MK, cbuf);
   blocked_writeout<PK, false>(A, r, w, ld, Dl, arena + T.l_off[s], arena + T.u_off[s], T.u_ld[s], D, f0, st, tol);
 }
 
@@ -1758,7 +1923,7 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
     __syncthreads();
   }
   if (dg && tid == 0) dg[3] = wall_clock64();
-  blocked_factor_lds<PK>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer, dg ? dg + 8 : nullptr, T.f16r);
+  factor_lds<PK>(T, A, r, w, ld, Dl, MK, cbuf, dg ? dg + 8 : nullptr);
   if (dg && tid == 0) dg[4] = wall_clock64();
   // the parent reads only U: publish it first, then write L and D (read by later launches)
   writeout_u<PK, true>(A, r, w, ld, arena + T.u_off[s], T.u_ld[s]);
@@ -3427,6 +3592,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     big_kpan_ = ek ? std::max(1, std::min(8, std::atoi(ek))) : 4;
     const char* e16 = std::getenv("MADIPM_F16R");  // register-resident 16-pivot block factor (factor16r)
     T_.f16r = (e16 && e16[0] == '0') ? 0 : 1;
+    const char* ep = std::getenv("MADIPM_FACT_PIPE");  // pipelined in-LDS factorisation schedule
+    T_.fpipe = (ep && ep[0] == '0') ? 0 : 1;
   }
   T_.nrows = nrows_;
   T_.row_ptr = row_ptr_;
@@ -4508,7 +4675,13 @@ void LDLSolver::tree_debug_dump(hipStream_t s, const char* what, const int64_t* 
         fprintf(stderr, "  store level %d: U issue %.2f  drain+flag %.2f  L/D %.2f us\n", lv, sq[lv * 3] / na[lv],
                 sq[lv * 3 + 1] / na[lv], sq[lv * 3 + 2] / na[lv]);
     for (int lv = 0; lv < S_.nlevels; ++lv)
-      if (na[lv])
+      if (na[lv] && T_.fpipe && T_.f16r)
+        fprintf(stderr,
+                "  factor level %d: %d fronts  first16 %.2f  block steps %.2f  (wave 0: waits %.2f  diag factors %.2f; "
+                "wave 1 waits %.2f)  schur %.2f us\n",
+                lv, na[lv], ab[lv * 6] / na[lv], ab[lv * 6 + 1] / na[lv], ab[lv * 6 + 2] / na[lv], ab[lv * 6 + 3] / na[lv],
+                ab[lv * 6 + 5] / na[lv], ab[lv * 6 + 4] / na[lv]);
+      else if (na[lv])
         fprintf(stderr,
                 "  factor level %d: %d fronts  first16 [kcyc/100] %.2f  first16 %.2f  panels %.2f  J0 %.2f  look %.2f  schur %.2f us\n",
                 lv, na[lv], ab[lv * 6 + 5] / na[lv], ab[lv * 6] / na[lv], ab[lv * 6 + 1] / na[lv], ab[lv * 6 + 2] / na[lv],

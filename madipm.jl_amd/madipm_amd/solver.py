@@ -375,8 +375,10 @@ class MPCSolver:
     def set_max_iter(self, k: int):
         L.check(L.lib.madipm_solver_set_max_iter(self.h, int(k)), "set_max_iter")
 
-    def solve(self) -> ExecutionStats:
-        """solve!(solver) (src/solver.jl:362-418)."""
+    def solve(self, fetch_solution: bool = True) -> ExecutionStats:
+        """solve!(solver) (src/solver.jl:362-418).  fetch_solution=False skips update_solution!'s
+        device-to-host copies of x, y, z_L, z_U and the constraint values (the reference runs it after
+        cnt.total_time is taken, solver.jl:406-413); the returned arrays are then None."""
         st = Stats()
         rc = L.lib.madipm_solver_solve(self.h, C.byref(st))
         if rc < 0:
@@ -389,6 +391,14 @@ class MPCSolver:
             raise _EXCEPTIONS[st.exception](
                 "MPC loop: " + ("residual check of solve_system! (src/linear_solver.jl:40-41)"
                                 if st.exception == EXC_SOLVE else "solve with an unfactorized KKT system"))
+        if not fetch_solution:
+            return ExecutionStats(status=st.status, iter=st.iter, objective=st.objective,
+                                  dual_objective=st.dual_objective, solution=None, constraints=None,
+                                  multipliers=None, multipliers_L=None, multipliers_U=None, primal_feas=st.inf_pr,
+                                  dual_feas=st.inf_du, inf_compl=st.inf_compl,
+                                  counters=Counters(k=st.iter, total_time=st.total_time,
+                                                    linear_solver_time=st.linear_solver_time, init_time=st.init_time),
+                                  trace=None)
         nx, m = self.qp.nvar, self.qp.ncon
         x, zl, zu = np.empty(nx), np.empty(nx), np.empty(nx)
         y, cons = np.empty(m), np.empty(m)

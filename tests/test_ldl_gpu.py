@@ -125,6 +125,48 @@ def test_ldl_diag_block_variants(f16r, sfm, well, monkeypatch):
     _check_case(K, Lw, small_front_max=sfm, well=True)
 
 
+def _factor_solve(K, Lw, sfm, seed=0):
+    from madipm_amd.linear_solver import HIPLDLSolver
+    N = K.shape[0]
+    ls = HIPLDLSolver(N, Lw.indptr, Lw.indices, small_front_max=sfm)
+    dev = torch.device("cuda:0")
+    assert ls.factorize(torch.from_numpy(Lw.data.copy()).to(dev)) == 0
+    b = np.random.default_rng(seed).standard_normal(N)
+    x = torch.from_numpy(b.copy()).to(dev)
+    ls.solve(x)
+    torch.cuda.synchronize()
+    return ls.diag().copy(), x.cpu().numpy(), ls
+
+
+@pytest.mark.parametrize("defer", ["0", "1"])
+@pytest.mark.parametrize("sfm", [128, 192])
+@pytest.mark.parametrize("case", ["block_well", "block_ipm", "dense_front", "random"])
+def test_ldl_fact_pipe_bitwise(case, sfm, defer, monkeypatch):
+    """The pipelined in-LDS schedule (blocked_factor_pipe: wave 0 runs the pivot chain, the other
+    waves the panel and trailing update, LDS-counter hand-offs; MADIPM_FACT_PIPE=1, default) forms
+    every tile with the same MFMA sequence from the same operands as the barrier schedule
+    (blocked_factor_lds, MADIPM_FACT_PIPE=0): pivots and solution agree BITWISE, on k_fact_tree
+    (8 waves) and k_small_blocked (4 waves; the 120-column root, dense fronts of 1-12 pivot blocks,
+    square and packed storage, deferred and per-step Schur updates) — and the oracle's to 1e-12."""
+    monkeypatch.setenv("MADIPM_SCHUR_DEFER", defer)
+    if case.startswith("block"):
+        K, Lw = block_angular_k2(3000, 4000, 20, 7, well=case == "block_well")
+    elif case == "dense_front":
+        K, Lw = _dense_k2(150, 1000, 5)
+    else:
+        K, Lw = random_k2(400, 900, 0.004, 4, well=True)
+    out = {}
+    for pipe in ("0", "1"):
+        monkeypatch.setenv("MADIPM_FACT_PIPE", pipe)
+        out[pipe] = _factor_solve(K, Lw, sfm)
+    (d0, x0, _), (d1, x1, ls1) = out["0"], out["1"]
+    assert np.array_equal(d0.view(np.uint64), d1.view(np.uint64)), \
+        f"pivots differ at {np.flatnonzero(d0 != d1)[:8]}"
+    assert np.array_equal(x0.view(np.uint64), x1.view(np.uint64))
+    if case != "block_ipm":
+        _check_case(K, Lw, small_front_max=sfm, well=True)
+
+
 @pytest.mark.parametrize("kpan", ["1", "2", "4"])
 @pytest.mark.parametrize("n,m", [(320, 100), (130, 200)])
 def test_big_front_panel_groups(kpan, n, m, monkeypatch):
