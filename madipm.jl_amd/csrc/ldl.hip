@@ -89,11 +89,11 @@ __device__ __forceinline__ double* uvec_dst(const FrontTab& T, int s, int a, dou
 // staging / write-out loops of a front are otherwise dominated by them)
 struct ColWalk {
   int i, j, di, dj, r;
-  __device__ __forceinline__ ColWalk(int q0, int r_) : r(r_) {
+  __device__ __forceinline__ ColWalk(int q0, int r_, int stride = NT) : r(r_) {
     j = q0 / r_;
     i = q0 - j * r_;
-    dj = NT / r_;
-    di = NT - dj * r_;
+    dj = stride / r_;
+    di = stride - dj * r_;
   }
   __device__ __forceinline__ void next() {
     i += di;
@@ -848,12 +848,20 @@ __device__ __forceinline__ void fmac_row_bcast(double& acc, double mul) {
                : "+v"(acc)
                : "v"(mul), "n"(T));
 }
-template <int T>
+// RCP (MADIPM_F16R=2): l = A(i, t) * (1 / d_t) with the reciprocal from v_rcp_f64 + two Newton steps
+// (within an ulp of the IEEE quotient; ~6 dependent instructions on the pivot chain instead of the
+// ~10 of the IEEE division sequence)
+__device__ __forceinline__ double recip_nr(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  r = fma(fma(-d, r, 1.0), r, r);
+  return fma(fma(-d, r, 1.0), r, r);
+}
+template <int T, bool RCP>
 __device__ __forceinline__ void f16r_step(double (&a)[4], double (&x)[4], double& dmine, int i, int g) {
   constexpr int gt = T & 3, mt = T >> 2;
   const double dt = readlane_f64(a[mt], T + 16 * gt);
   const double ci = xrow_bcast<gt>(a[mt]);
-  const double li = (i > T) ? ci / dt : 0.0;  // IEEE quotient
+  const double li = (i > T) ? (RCP ? ci * recip_nr(dt) : ci / dt) : 0.0;  // IEEE quotient unless RCP
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
     const int j = 4 * m + g;
@@ -865,14 +873,14 @@ __device__ __forceinline__ void f16r_step(double (&a)[4], double (&x)[4], double
   if (i == T) dmine = dt;
   if (g == gt && i > T) a[mt] = li;
 }
-template <int T>
+template <int T, bool RCP>
 __device__ __forceinline__ void f16r_steps(double (&a)[4], double (&x)[4], double& dmine, int i, int g) {
   if constexpr (T < 16) {
-    f16r_step<T>(a, x, dmine, i, g);
-    f16r_steps<T + 1>(a, x, dmine, i, g);
+    f16r_step<T, RCP>(a, x, dmine, i, g);
+    f16r_steps<T + 1, RCP>(a, x, dmine, i, g);
   }
 }
-template <bool PK>
+template <bool PK, bool RCP = false>
 __device__ __forceinline__ void factor16r(double* A, int r, int ld, int k0, int kw, double* Dl, double* MK, int lane) {
   const int i = lane & 15, g = lane >> 4;
   const int ic = min(i, kw - 1);
@@ -890,7 +898,7 @@ __device__ __forceinline__ void factor16r(double* A, int r, int ld, int k0, int 
     x[m] = (i == j) ? 1.0 : 0.0;
   }
   double dmine = 1.0;
-  f16r_steps<0>(a, x, dmine, i, g);
+  f16r_steps<0, RCP>(a, x, dmine, i, g);
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
     const int j = 4 * m + g;
@@ -1168,7 +1176,9 @@ __device__ __forceinline__ void schur_strips(double* A, int r, int ld, int w, co
 template <bool PK>
 __device__ __forceinline__ void factor16x(double* A, int r, int ld, int k0, int kw, double* Dl, double* MK, double* cb,
                                           int lane, int f16r) {
-  if (f16r)
+  if (f16r == 2)
+    factor16r<PK, true>(A, r, ld, k0, kw, Dl, MK, lane);
+  else if (f16r)
     factor16r<PK>(A, r, ld, k0, kw, Dl, MK, lane);
   else
     factor16s<PK>(A, r, ld, k0, kw, Dl, MK, cb, lane);
@@ -1281,7 +1291,7 @@ __device__ __forceinline__ void pipe_add(int* f) {
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(f, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <bool PK>
+template <bool PK, bool RCP>
 __device__ __forceinline__ void blocked_factor_pipe(double* A, int r, int w, int ld, double* Dl, double* MK0,
                                                     double* MK1, int defer = 0, int64_t* pt = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1303,7 +1313,7 @@ __device__ __forceinline__ void blocked_factor_pipe(double* A, int r, int w, int
       tc = now;
     }
   };
-  if (wv == 0) factor16r<PK>(A, r, ld, 0, min(16, w), Dl, MK0, lane);
+  if (wv == 0) factor16r<PK, RCP>(A, r, ld, 0, min(16, w), Dl, MK0, lane);
   __syncthreads();  // block 0 factorised; the counters are zero
   const int64_t t1 = (pt && tid == 0) ? wall_clock64() : 0;
   int gen = 0;  // O-barrier generation (waves 1..)
@@ -1332,7 +1342,7 @@ __device__ __forceinline__ void blocked_factor_pipe(double* A, int r, int w, int
         trail_strip<PK, 1>(A, r, ld, k0, kw, R0, 0, 0, dk, lane, jend);  // the next diagonal tile
         wave_sync();
         lap(tx);
-        factor16r<PK>(A, r, ld, R0, min(16, w - R0), Dl, (kb & 1) ? MK0 : MK1, lane);
+        factor16r<PK, RCP>(A, r, ld, R0, min(16, w - R0), Dl, (kb & 1) ? MK0 : MK1, lane);
         pipe_set(&pc.mk, kb + 2);
         lap(tf);
       }
@@ -1396,8 +1406,10 @@ __device__ __forceinline__ void blocked_factor_pipe(double* A, int r, int w, int
 template <bool PK>
 __device__ __forceinline__ void factor_lds(const FrontTab& T, double* A, int r, int w, int ld, double* Dl, double* MK,
                                            double* cbuf, int64_t* pt = nullptr) {
-  if (T.fpipe && T.f16r && (blockDim.x >> 6) >= 2)
-    blocked_factor_pipe<PK>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer, pt);
+  if (T.fpipe && T.f16r == 2 && (blockDim.x >> 6) >= 2)
+    blocked_factor_pipe<PK, true>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer, pt);
+  else if (T.fpipe && T.f16r && (blockDim.x >> 6) >= 2)
+    blocked_factor_pipe<PK, false>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer, pt);
   else
     blocked_factor_lds<PK>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer, pt, T.f16r);
 }
@@ -1514,17 +1526,17 @@ __device__ __forceinline__ void writeout_u(const double* A, int r, int w, int ld
 }
 
 // lower part of an r x r front assembled in HBM scratch (ld r) -> LDS, 16 loads in flight per thread
-template <bool PK>
+template <bool PK, int NTH = NT>
 __device__ __forceinline__ void stage_front(const double* __restrict__ Fs, double* A, int r, int ld) {
   const int tid = threadIdx.x;
   const int nel = r * r;
-  ColWalk wk(tid, r);
-  for (int base = 0; base < nel; base += NT * 16) {
+  ColWalk wk(tid, r, NTH);
+  for (int base = 0; base < nel; base += NTH * 16) {
     double v[16];
     int dst[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-      const int q = base + k * NT + tid;
+      const int q = base + k * NTH + tid;
       const bool ok = q < nel && wk.i >= wk.j;
       v[k] = ok ? Fs[q] : 0.0;
       dst[k] = ok ? fidx<PK>(wk.i, wk.j, r, ld) : -1;
@@ -1536,8 +1548,11 @@ __device__ __forceinline__ void stage_front(const double* __restrict__ Fs, doubl
   }
 }
 
+// k_small_blocked: 8 waves (2 per SIMD): twice the loads in flight of the staging copy and write-out,
+// and 7 waves beside the pivot chain of the pipelined factorisation (the 120-column ex10 root)
+constexpr int SBT = 512;
 template <bool PK>
-__global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t* __restrict__ fronts,
+__global__ __launch_bounds__(SBT) void k_small_blocked(FrontTab T, const int32_t* __restrict__ fronts,
                                                       const double* __restrict__ Kx, double* __restrict__ arena,
                                                       const double* __restrict__ fscratch, double* __restrict__ D,
                                                       LDLStatus* st, double tol) {
@@ -1551,28 +1566,28 @@ __global__ __launch_bounds__(NT) void k_small_blocked(FrontTab T, const int32_t*
   const int tid = threadIdx.x;
   const int64_t fso = T.fs_off[s];
   if (fso >= 0 && !T.fs_img[s]) {  // batched-leaf parent: the SYRK and k_assemble wrote ld r
-    stage_front<PK>(fscratch + fso, A, r, ld);
+    stage_front<PK, SBT>(fscratch + fso, A, r, ld);
   } else if (fso >= 0) {  // assembled by k_assemble as the LDS image (lower part valid): a straight copy
     const double* __restrict__ src = fscratch + fso;
     const int n = PK ? r * (r + 1) / 2 : r * ld;
-    for (int base = 0; base < n; base += NT * 16) {
+    for (int base = 0; base < n; base += SBT * 16) {
       double v[16];
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
-        const int q = base + k * NT + tid;
+        const int q = base + k * SBT + tid;
         v[k] = (q < n) ? src[q] : 0.0;
       }
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
-        const int q = base + k * NT + tid;
+        const int q = base + k * SBT + tid;
         if (q < n) A[q] = v[k];
       }
     }
   } else {  // leaf: original entries only
     const int ntot = PK ? r * (r + 1) / 2 : r * ld;
-    for (int q = tid; q < ntot; q += NT) A[q] = 0.0;
+    for (int q = tid; q < ntot; q += SBT) A[q] = 0.0;
     __syncthreads();
-    for (int64_t q = T.asm_ptr[s] + tid; q < T.asm_ptr[s + 1]; q += NT) {
+    for (int64_t q = T.asm_ptr[s] + tid; q < T.asm_ptr[s + 1]; q += SBT) {
       const int d = (int)T.asm_dst[q], dj = d / r;  // d < r^2: 32-bit division
       A[fidx<PK>(d - dj * r, dj, r, ld)] = Kx[T.asm_src[q]];
     }
@@ -3591,7 +3606,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     const char* ek = std::getenv("MADIPM_BIG_KPAN");  // panels per deferred big-front update group
     big_kpan_ = ek ? std::max(1, std::min(8, std::atoi(ek))) : 4;
     const char* e16 = std::getenv("MADIPM_F16R");  // register-resident 16-pivot block factor (factor16r)
-    T_.f16r = (e16 && e16[0] == '0') ? 0 : 1;
+    T_.f16r = e16 ? std::max(0, std::min(2, std::atoi(e16))) : 2;  // r3: reciprocal default (k_fact_tree -3 us)
     const char* ep = std::getenv("MADIPM_FACT_PIPE");  // pipelined in-LDS factorisation schedule
     T_.fpipe = (ep && ep[0] == '0') ? 0 : 1;
   }
@@ -4489,12 +4504,12 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
       case SMALL64:
       case SMALL128:
         TIMED(KK_SMALL, L.bytes, L.alg, L.flops,
-              (k_small_blocked<false><<<(unsigned)L.items, NT, L.lds_bytes, s>>>(T_, list, Kx, arena_, fscratch_, D_,
+              (k_small_blocked<false><<<(unsigned)L.items, SBT, L.lds_bytes, s>>>(T_, list, Kx, arena_, fscratch_, D_,
                                                                                 st_, pivot_tol)));
         break;
       case SMALL192:
         TIMED(KK_SMALL, L.bytes, L.alg, L.flops,
-              (k_small_blocked<true><<<(unsigned)L.items, NT, L.lds_bytes, s>>>(T_, list, Kx, arena_, fscratch_, D_,
+              (k_small_blocked<true><<<(unsigned)L.items, SBT, L.lds_bytes, s>>>(T_, list, Kx, arena_, fscratch_, D_,
                                                                                st_, pivot_tol)));
         break;
       case BIG_DIAG:

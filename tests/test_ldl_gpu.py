@@ -107,14 +107,15 @@ def test_ldl_schur_update_variants(defer, sfm, monkeypatch):
     assert ls.inertia() == (4000, 0, 3000)
 
 
-@pytest.mark.parametrize("f16r", ["0", "1"])
+@pytest.mark.parametrize("f16r", ["0", "1", "2"])
 @pytest.mark.parametrize("sfm", [128, 192])
 @pytest.mark.parametrize("well", [True, False])
 def test_ldl_diag_block_variants(f16r, sfm, well, monkeypatch):
     """The 16-pivot diagonal blocks of the in-LDS factorisation factorised in registers (factor16r:
-    DPP row broadcasts + gfx950 permlane swaps, MADIPM_F16R=1, default) or through an LDS hand-off per
-    pivot (factor16s, 0): the oracle's pivots to 1e-12 (well conditioned) and its solution; the two
-    variants round the Schur complement along mirrored paths, so they agree to rounding, not bitwise.
+    DPP row broadcasts + gfx950 permlane swaps; l = a * (1/d) with a Newton-refined v_rcp_f64,
+    MADIPM_F16R=2, default, or the IEEE quotient a / d, 1) or through an LDS hand-off per pivot
+    (factor16s, 0): the oracle's pivots to 1e-12 (well conditioned) and its solution; the variants
+    round differently (mirrored Schur paths, reciprocal vs quotient), so they agree to rounding.
     The block-angular K2 has fronts of 16 .. 150 columns (several diagonal blocks each) and a
     120-column root (k_small_blocked); the QP case a dense front."""
     monkeypatch.setenv("MADIPM_F16R", f16r)
@@ -138,10 +139,11 @@ def _factor_solve(K, Lw, sfm, seed=0):
     return ls.diag().copy(), x.cpu().numpy(), ls
 
 
+@pytest.mark.parametrize("f16r", ["1", "2"])
 @pytest.mark.parametrize("defer", ["0", "1"])
 @pytest.mark.parametrize("sfm", [128, 192])
 @pytest.mark.parametrize("case", ["block_well", "block_ipm", "dense_front", "random"])
-def test_ldl_fact_pipe_bitwise(case, sfm, defer, monkeypatch):
+def test_ldl_fact_pipe_bitwise(case, sfm, defer, f16r, monkeypatch):
     """The pipelined in-LDS schedule (blocked_factor_pipe: wave 0 runs the pivot chain, the other
     waves the panel and trailing update, LDS-counter hand-offs; MADIPM_FACT_PIPE=1, default) forms
     every tile with the same MFMA sequence from the same operands as the barrier schedule
@@ -149,6 +151,7 @@ def test_ldl_fact_pipe_bitwise(case, sfm, defer, monkeypatch):
     (8 waves) and k_small_blocked (4 waves; the 120-column root, dense fronts of 1-12 pivot blocks,
     square and packed storage, deferred and per-step Schur updates) — and the oracle's to 1e-12."""
     monkeypatch.setenv("MADIPM_SCHUR_DEFER", defer)
+    monkeypatch.setenv("MADIPM_F16R", f16r)
     if case.startswith("block"):
         K, Lw = block_angular_k2(3000, 4000, 20, 7, well=case == "block_well")
     elif case == "dense_front":

@@ -10,12 +10,15 @@ cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 if [ -n "$SEL" ]; then
   timeout -k 10 400 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 120 --timeout-method thread -k "$SEL" > $OUT/pytest_sel.log 2>&1 && echo "selected tests ok: $(tail -1 $OUT/pytest_sel.log)" || { echo "selected tests FAILED"; tail -40 $OUT/pytest_sel.log; exit 1; }
 fi
+# KNOB empty: each VALUES item is a comma-separated list of VAR=value assignments
 for v in ${VALUES:-1}; do
-  env $KNOB=$v timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu "$@" > $OUT/bench_$v.log 2>&1 || { echo "bench $v FAILED"; tail -20 $OUT/bench_$v.log; exit 1; }
-  echo "$KNOB=$v $(grep -o '"value": [0-9.]*' $OUT/bench_$v.log) $(grep -o '"avg_launch_us": [0-9.]*' $OUT/bench_$v.log)"
+  if [ -n "$KNOB" ]; then asg="$KNOB=$v"; else asg="${v//,/ }"; fi
+  tag=$(echo "$v" | tr ',=' '__')
+  env $asg timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu "$@" > $OUT/bench_$tag.log 2>&1 || { echo "bench $v FAILED"; tail -20 $OUT/bench_$tag.log; exit 1; }
+  echo "$asg $(grep -o '"value": [0-9.]*' $OUT/bench_$tag.log) $(grep -o '"avg_launch_us": [0-9.]*' $OUT/bench_$tag.log)"
 done
 if [ -n "$DBG" ]; then
-  MADIPM_TREE_DEBUG=1 timeout -k 10 200 python bench.py --steps 2 --warmup 1 --no-cpu --no-opt "$@" > $OUT/tree_debug_bench.log 2> $OUT/tree_debug.txt && echo "tree debug ok" && head -30 $OUT/tree_debug.txt
+  env $DBG MADIPM_TREE_DEBUG=1 timeout -k 10 200 python bench.py --steps 2 --warmup 1 --no-cpu --no-opt "$@" > $OUT/tree_debug_bench.log 2> $OUT/tree_debug.txt && echo "tree debug ok" && head -30 $OUT/tree_debug.txt
 fi
 if [ -n "$PROF" ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 20 --warmup 2 --no-cpu --no-opt "$@" > $OUT/prof.log 2>&1 && echo "rocprof ok"
