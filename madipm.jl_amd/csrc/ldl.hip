@@ -3122,6 +3122,36 @@ __device__ __forceinline__ void bwd_subst_c(double (&v)[3], const double* LC, in
   }
 }
 
+// backward (transposed) on the forward's row-major panel: v[j] -= L(t, j) v[t] for j < t, t = w-1 .. 0,
+// L(t, j) = LT[t ldt + j] — the same fma sequence as bwd_subst_c (bitwise the same x).  Used by the
+// forward kernel for an elimination-tree root (r == w) whose panel it already holds in LDS.
+template <int HB>
+__device__ __forceinline__ void bwd_block_t(double (&v)[3], const double* LT, int ldt, int w, int t0, int lane) {
+  double lb[HB + 1][16];
+#pragma unroll
+  for (int h = 0; h <= HB; ++h) {
+    const int j = min(lane + 64 * h, w - 1);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) lb[h][k] = LT[min(t0 + k, w - 1) * ldt + j];
+  }
+#pragma unroll
+  for (int k = 15; k >= 0; --k) {
+    const double xt = readlane_f64(v[HB], (t0 & 63) + k);
+#pragma unroll
+    for (int h = 0; h <= HB; ++h) v[h] = fma(-lb[h][k], xt, v[h]);
+  }
+}
+__device__ __forceinline__ void bwd_subst_t(double (&v)[3], const double* LT, int ldt, int w, int lane) {
+  for (int t0 = ((w - 1) >> 4) << 4; t0 >= 0; t0 -= 16) {
+    if (t0 < 64)
+      bwd_block_t<0>(v, LT, ldt, w, t0, lane);
+    else if (t0 < 128)
+      bwd_block_t<1>(v, LT, ldt, w, t0, lane);
+    else
+      bwd_block_t<2>(v, LT, ldt, w, t0, lane);
+  }
+}
+
 // Folded micro leaves of a chain task (w <= 2, r <= 32, no children; their parents are fronts of the
 // chain), one thread per leaf, every load of a leaf issued before its arithmetic.
 // Forward (k_fwd_micro's arithmetic): x0 = b0, x1 = b1 - l10 x0 to xi; the update entries
@@ -3298,7 +3328,8 @@ __global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __re
                                                  const double* __restrict__ arena, const double* __restrict__ b,
                                                  double* xi, double* uvec, int32_t* err, int64_t* dbg,
                                                  const int32_t* __restrict__ lptr, const SolveLeaf* __restrict__ leaves,
-                                                 const int2* __restrict__ lrow) {
+                                                 const int2* __restrict__ lrow, const uint8_t* __restrict__ rootbwd,
+                                                 const double* __restrict__ Dg, int leaves_in_task) {
   extern __shared__ __attribute__((aligned(16))) double Ls[];
   __shared__ double v0s[SMALL_SOLVE_MAX];
   __shared__ int s_task;
@@ -3314,7 +3345,7 @@ __global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __re
   if (dg && tid == 0) dg[0] = wall_clock64();
   const int q0 = cptr[t], q1 = cptr[t + 1];
   // the folded leaves first: they depend on b only
-  if (lptr[t + 1] > lptr[t]) {
+  if (leaves_in_task && lptr[t + 1] > lptr[t]) {
     fwd_leaves(leaves, lptr[t], lptr[t + 1], lrow, arena, b, xi, T.gbuf);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -3340,6 +3371,17 @@ __global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __re
     for (int h = 0; h < 3; ++h) {
       const int i = (tid & 63) + 64 * h;
       udst[h] = (tid < 64 && i >= w && i < r) ? uvec_dst(T, s, i - w, uvec) : xi + f0 + min(i, max(w - 1, 0));
+    }
+    // an elimination-tree root (r == w) also runs its backward substitution here (MADIPM_ROOT_BWD=1):
+    // its pivots and the caller's positions are loaded before the wait
+    const bool rb = q == q1 - 1 && rootbwd[t];
+    double dpiv[3];
+    int pj[3];
+#pragma unroll
+    for (int h = 0; h < 3; ++h) {
+      const int j = min((tid & 63) + 64 * h, max(w - 1, 0));
+      dpiv[h] = (rb && tid < 64) ? Dg[f0 + j] : 1.0;
+      pj[h] = (rb && tid < 64) ? T.perm[f0 + j] : 0;
     }
     if (q == q0 && tid < 64) poll_deps(dep, dep_ptr[t], dep_ptr[t + 1], tflags, epoch, err);
     __syncthreads();  // + the previous front's / the leaves' drained stores (vmcnt 0 before it)
@@ -3388,15 +3430,31 @@ __global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __re
       }
       fwd_subst_t(v, Ls, ldt, r, w, lane);
       if (dg && tid == 0 && q == q1 - 1) dg[4] = wall_clock64();
+      if (rb) {  // k_bwd_tree's work for this root: x = L^-T (D^-1 y), published with the backward epoch
 #pragma unroll
-      for (int h = 0; h < 3; ++h) {
-        const int i = lane + 64 * h;
-        if (i < r) st_sc1(udst[h], v[h]);
+        for (int h = 0; h < 3; ++h) v[h] = (lane + 64 * h < w) ? v[h] / dpiv[h] : 0.0;
+        bwd_subst_t(v, Ls, ldt, w, lane);
+        double* out = const_cast<double*>(b);  // the caller's vector: x at this root's pivots (read by no other task)
+#pragma unroll
+        for (int h = 0; h < 3; ++h) {
+          const int j = lane + 64 * h;
+          if (j < w) {
+            st_sc1(xi + f0 + j, v[h]);
+            if (T.wout[s]) out[pj[h]] = v[h];
+          }
+        }
+        publish_sc1(&tflags[s], epoch + 1);
+      } else {
+#pragma unroll
+        for (int h = 0; h < 3; ++h) {
+          const int i = lane + 64 * h;
+          if (i < r) st_sc1(udst[h], v[h]);
+        }
+        if (q == q1 - 1)
+          publish_sc1(&tflags[s], epoch);  // the chain's top: its tree parent is another task's
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      if (q == q1 - 1)
-        publish_sc1(&tflags[s], epoch);  // the chain's top: its tree parent is another task's
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();  // wave 0 is done with Ls; its stores are drained
   }
@@ -3412,7 +3470,8 @@ __global__ __launch_bounds__(NT) void k_bwd_tree(FrontTab T, const int32_t* __re
                                                  int epoch, const double* __restrict__ arena,
                                                  const double* __restrict__ D, double* xi, double* __restrict__ out,
                                                  int32_t* err, const int32_t* __restrict__ lptr,
-                                                 const SolveLeaf* __restrict__ leaves, const int2* __restrict__ lrow) {
+                                                 const SolveLeaf* __restrict__ leaves, const int2* __restrict__ lrow,
+                                                 const uint8_t* __restrict__ rootbwd, int leaves_in_task) {
   extern __shared__ __attribute__((aligned(16))) double Ls[];
   __shared__ double xbs[SMALL_SOLVE_MAX];
   __shared__ int s_task;
@@ -3425,6 +3484,7 @@ __global__ __launch_bounds__(NT) void k_bwd_tree(FrontTab T, const int32_t* __re
   const int t = s_task;  // backward ticket t = forward task nt - 1 - t (reverse topological order)
   if (t >= nt) return;
   const int tf = nt - 1 - t;
+  if (rootbwd[tf]) return;  // solved and published by k_fwd_tree
   const int q0 = cptr[tf], q1 = cptr[tf + 1];
   const int lane = tid & 63;
   for (int q = q1 - 1; q >= q0; --q) {  // top first
@@ -3482,7 +3542,7 @@ __global__ __launch_bounds__(NT) void k_bwd_tree(FrontTab T, const int32_t* __re
     }
     __syncthreads();  // wave 0 is done with Ls; its stores are drained
   }
-  if (lptr[tf + 1] > lptr[tf]) bwd_leaves(leaves, lptr[tf], lptr[tf + 1], lrow, arena, D, xi, out);
+  if (leaves_in_task && lptr[tf + 1] > lptr[tf]) bwd_leaves(leaves, lptr[tf], lptr[tf + 1], lrow, arena, D, xi, out);
 }
 
 // ------------------------------------------------------------------ sharding (SURVEY §8 e)
@@ -3743,8 +3803,9 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   }
   // micro leaves (w <= 2, r <= 32, no children) under tree fronts, solved from precomputed leaf records
   // (SolveLeaf): MADIPM_SOLVE_FOLD=1 (default) by the flat k_fwd_leaves / k_bwd_leaves launches, =2
-  // inside the tree tasks (k_fwd_tree / k_bwd_tree, beside their parent front), =0 by the generic
-  // level-0 micro launches (k_fwd_micro / k_bwd_micro)
+  // inside the tree tasks (k_fwd_tree / k_bwd_tree, beside their parent front), =4 forward by the flat
+  // launch and backward inside the tree tasks (after the task's fronts have published their x), =0 by
+  // the generic level-0 micro launches (k_fwd_micro / k_bwd_micro)
   std::vector<char> sleaf(std::max(ns, 1), 0);
   {
     const char* ev = std::getenv("MADIPM_SOLVE_FOLD");
@@ -4218,7 +4279,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         std::reverse(ch.begin(), ch.end());  // deepest first
         for (int f : ch) {
           clist.push_back(f);
-          for (int q = S.child_ptr[f]; q < S.child_ptr[f + 1] && sfold_ == 2; ++q) {  // folded leaves, child order
+          for (int q = S.child_ptr[f]; q < S.child_ptr[f + 1] && (sfold_ == 2 || sfold_ == 4); ++q) {  // folded leaves
             const int c = S.child_list[q];
             if (!sleaf[c]) continue;
             const int r = S.nrows[c], w = S.first[c + 1] - S.first[c], f0 = S.first[c];
@@ -4252,6 +4313,18 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         }
       }
       ntask_ = (int)tops.size();
+      {  // elimination-tree roots solved backward by k_fwd_tree (MADIPM_ROOT_BWD=0 disables): one-front
+         // tasks without leaves whose front has no parent at all (r == w)
+        const char* rbe = std::getenv("MADIPM_ROOT_BWD");
+        const bool on = !(rbe && rbe[0] == '0');
+        std::vector<uint8_t> rbv(std::max(ntask_, 1), 0);
+        for (int t = 0; on && t < ntask_; ++t) {
+          const int f = tops[t];
+          rbv[t] = cptr[t + 1] - cptr[t] == 1 && lptr[t + 1] == lptr[t] && S.parent[f] < 0 &&
+                   S.nrows[f] == S.first[f + 1] - S.first[f];
+        }
+        trootbwd_.upload(rbv);
+      }
       std::vector<int32_t> par;  // backward ticket t -> task ntask - 1 - t: the tree parent of its top
       for (int t = ntask_ - 1; t >= 0; --t) {
         const int p = S.parent[tops[t]];
@@ -4769,7 +4842,7 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
             (k_fwd_big<<<std::min(L.nftask, 512), NT, 0, s>>>(T_, tasks + L.ftask_off, L.nftask, cnt + 2 * lev,
                                                                flags_, flag_off_, efwd, arena_, vwork_, xi_, uvec_, &st_->err)));
     }
-    if (lev == 0 && phase == 0 && ntree_ && sfold_ == 1 && nsleaf_)
+    if (lev == 0 && phase == 0 && ntree_ && (sfold_ == 1 || sfold_ == 4) && nsleaf_)
       TIMED(KK_FWD_TINY, leaf_bytes_, leaf_alg_, leaf_flops_,
             (k_fwd_leaves<<<(unsigned)cdiv(nsleaf_ * LPL, NT), NT, 0, s>>>(tleaf_, (int)nsleaf_, tlrow_, arena_, b, xi_,
                                                                          T_.gbuf)));
@@ -4778,7 +4851,7 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
             (k_fwd_tree<<<(unsigned)ntask_, NT, tree_lds_, s>>>(T_, tc_ptr_, tc_list_, ntask_, tdep_ptr_, tdep_,
                                                                  counters_.p + 4 * S_.nlevels, tflags_, efwd, tree_lds_ / 8,
                                                                  arena_, b, xi_, uvec_, &st_->err, tdbg_.p, tl_ptr_, tleaf_,
-                                                                 tlrow_)));
+                                                                 tlrow_, trootbwd_, D_, sfold_ == 2 ? 1 : 0)));
     if (lev == 0 && phase == 0 && ntree_ && tdbg_.p)
       tree_debug_dump(s, "fwd", tdbg_.p, ntask_, "leaves", "wait", "gather", "subst", "store", 8);
   }
@@ -4791,10 +4864,12 @@ void LDLSolver::bwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
   for (int lev = (int)V.size() - 1; lev >= 0; --lev) {
     const SolveLevel& L = V[lev];
     if (lev == 0 && phase == 0 && ntree_)
-      TIMED(KK_BWD_TREE, tree_bytes_, tree_alg_, tree_flops_,
+      TIMED(KK_BWD_TREE, tree_bytes_ + (sfold_ == 4 ? leaf_bytes_ : 0.0), tree_alg_ + (sfold_ == 4 ? leaf_alg_ : 0.0),
+            tree_flops_ + (sfold_ == 4 ? leaf_flops_ : 0.0),
             (k_bwd_tree<<<(unsigned)ntask_, NT, tree_lds_, s>>>(T_, tc_ptr_, tc_list_, ntask_, tpar_,
                                                                  counters_.p + 4 * S_.nlevels + 1, tflags_, ebwd, arena_, D_,
-                                                                 xi_, b, &st_->err, tl_ptr_, tleaf_, tlrow_)));
+                                                                 xi_, b, &st_->err, tl_ptr_, tleaf_, tlrow_, trootbwd_,
+                                                                 (sfold_ == 2 || sfold_ == 4) ? 1 : 0)));
     if (lev == 0 && phase == 0 && ntree_ && sfold_ == 1 && nsleaf_)
       TIMED(KK_BWD_TINY, leaf_bytes_, leaf_alg_, leaf_flops_,
             (k_bwd_leaves<<<(unsigned)cdiv(nsleaf_ * LPL, NT), NT, 0, s>>>(tleaf_, (int)nsleaf_, tlrow_, arena_, D_, xi_,

@@ -170,6 +170,24 @@ def test_ldl_fact_pipe_bitwise(case, sfm, defer, f16r, monkeypatch):
         _check_case(K, Lw, small_front_max=sfm, well=True)
 
 
+@pytest.mark.parametrize("case", ["block_well", "block_ipm", "random"])
+def test_root_backward_in_forward_bitwise(case, monkeypatch):
+    """An elimination-tree root (r == w) solved backward by the forward tree kernel right after its
+    forward substitution (panel already in LDS; MADIPM_ROOT_BWD=1, default) instead of by k_bwd_tree:
+    the same fma sequence on the row-major panel, so the solution is BITWISE that of the separate
+    backward task (=0) — and the oracle's."""
+    if case.startswith("block"):
+        K, Lw = block_angular_k2(3000, 4000, 20, 7, well=case == "block_well")
+    else:
+        K, Lw = random_k2(400, 900, 0.004, 4, well=True)
+    out = {}
+    for rb in ("0", "1"):
+        monkeypatch.setenv("MADIPM_ROOT_BWD", rb)
+        out[rb] = _factor_solve(K, Lw, 128)
+    assert np.array_equal(out["0"][1].view(np.uint64), out["1"][1].view(np.uint64))
+    _check_case(K, Lw, well=case != "block_ipm")
+
+
 @pytest.mark.parametrize("kpan", ["1", "2", "4"])
 @pytest.mark.parametrize("n,m", [(320, 100), (130, 200)])
 def test_big_front_panel_groups(kpan, n, m, monkeypatch):
@@ -188,12 +206,14 @@ def test_big_front_panel_groups(kpan, n, m, monkeypatch):
     _check_case(K, Lw, small_front_max=16, well=True)
 
 
-@pytest.mark.parametrize("chain,sfold", [("0", "1"), ("0", "0"), ("0", "2"), ("1", "2"), ("1", "1")])
+@pytest.mark.parametrize("chain,sfold", [("0", "1"), ("0", "0"), ("0", "2"), ("1", "2"), ("1", "1"), ("0", "4"),
+                                         ("1", "4")])
 @pytest.mark.parametrize("well", [True, False])
 def test_ldl_chain_solve_and_leaf_fold(chain, sfold, well, monkeypatch):
     """Tree solves with one task per front (default) or over chain tasks (MADIPM_CHAIN_SOLVE=1), and
     the micro leaves under tree fronts solved from leaf records by flat launches (MADIPM_SOLVE_FOLD=1,
-    default), inside the tree tasks (=2) or by the generic micro launches (=0): same solution as the
+    default), inside the tree tasks (=2), forward flat + backward in the tasks (=4) or by the generic
+    micro launches (=0): same solution as the
     oracle in every combination, and for several right-hand sides in a row (flag epochs)."""
     monkeypatch.setenv("MADIPM_CHAIN_SOLVE", chain)
     monkeypatch.setenv("MADIPM_SOLVE_FOLD", sfold)
