@@ -309,11 +309,14 @@ enum { RHS_INIT_PRIMAL = 0, RHS_INIT_DUAL = 1, RHS_PRED = 2, RHS_CORR = 3, RHS_G
 // released, then the counter (the host spins on the counter, MPCSolver::wait_state)
 static_assert(sizeof(DevState) % 8 == 0 && sizeof(DevState) <= 64 * 8, "k_publish: one word per lane");
 __device__ __forceinline__ void publish_state(const DevState* __restrict__ st, DevState* host, uint32_t* hseq,
-                                              uint32_t seq) {  // called by one whole wave
+                                              uint32_t seq, bool fresh = false) {  // called by one whole wave
+  // fresh: the state was just stored by lane 0 of this wave: read it back from L2 (agent-scope loads)
   const int i = threadIdx.x;
-  if (i < (int)(sizeof(DevState) / 8))
-    __hip_atomic_store(reinterpret_cast<uint64_t*>(host) + i, reinterpret_cast<const uint64_t*>(st)[i],
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (i < (int)(sizeof(DevState) / 8)) {
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(st) + i;
+    const uint64_t v = fresh ? __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *src;
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(host) + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -813,6 +816,9 @@ struct FinParams {
                    // partials in slot PART_EVAL, the previous iteration's; P.c = its constant)
   LDLStatus* rs;   // != nullptr: a factorisation follows this launch (LinSolver::ext_reset)
   int64_t* dbg = nullptr;  // diagnostics (MADIPM_FINAL_DEBUG): thread 0's wall clock at entry / reduced / end
+  DevState* host = nullptr;  // != nullptr: wave 0 of the last workgroup publishes the state (sequence seq)
+  uint32_t* hseq = nullptr;
+  uint32_t seq = 0;
 };
 constexpr int PART_EVAL = 6;
 
@@ -1102,27 +1108,35 @@ __global__ __launch_bounds__(FT) void k_final(DV D, int kind, FinParams P) {
     res[16] = a;
   }
   __syncthreads();
-  if (t != 0) return;
-  *ticket = 0;  // every workgroup has taken its ticket: reset for the next launch
-  if (P.dbg) P.dbg[1] = (int64_t)wall_clock64();
-  if (AL) {
-    double a[4];
-    int ii[4];
+  if (t >= 64) return;
+  if (t == 0) {
+    *ticket = 0;  // every workgroup has taken its ticket: reset for the next launch
+    if (P.dbg) P.dbg[1] = (int64_t)wall_clock64();
+    if (AL) {
+      double a[4];
+      int ii[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      a[k] = res[8 + k];
-      ii[k] = (int)res[12 + k];
+      for (int k = 0; k < 4; ++k) {
+        a[k] = res[8 + k];
+        ii[k] = (int)res[12 + k];
+      }
+      fin_alpha_store(D, P, a, ii);
     }
-    fin_alpha_store(D, P, a, ii);
+    if (EV) st->obj_val = P.c + res[16];  // FIN_TERM: the previous iteration's FIN_EVAL, deferred here
+    if (NV > 0) {
+      if (P.rs) ldl_status_start(P.rs);
+      fin_tail(D, kind, P, res);
+    }
+    if (P.dbg) {
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      P.dbg[2] = (int64_t)wall_clock64();
+    }
   }
-  if (EV) st->obj_val = P.c + res[16];  // FIN_TERM: the previous iteration's FIN_EVAL, deferred here
-  if (NV > 0) {
-    if (P.rs) ldl_status_start(P.rs);
-    fin_tail(D, kind, P, res);
-  }
-  if (P.dbg) {
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    P.dbg[2] = (int64_t)wall_clock64();
+  if (P.host) {  // publish the state right here (the termination test's, before the factorisation):
+    // lane 0's state stores drained to L2, the wave reads them back past L1 and publishes
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    publish_state(st, P.host, P.hseq, P.seq, true);
   }
 }
 
@@ -1810,9 +1824,14 @@ void MPCSolver::kkt_solve() {
   }
 }
 
-void MPCSolver::launch_reduce_final(int kind, int nb, int amode, int nb_eval, LDLStatus* rs) {
+void MPCSolver::launch_reduce_final(int kind, int nb, int amode, int nb_eval, LDLStatus* rs, bool publish) {
   DV_ARGS;
   FinParams P{nb, 0, 0, 0, 0, 0, nb_eval, rs};
+  if (publish) {
+    P.host = hst_;
+    P.hseq = hseq_;
+    P.seq = ++pub_seq_;
+  }
   if (nb_eval > 0) P.c = c0s_;
   if (amode >= 0) {
     P.alpha_mode = amode;
@@ -2088,29 +2107,17 @@ int MPCSolver::solve(madipm_stats* stats) {
       // k >= max_iter the termination test ends the solve whatever it finds: nothing to speculate.
       const bool last = k_ >= opt_.max_iter;
       k_term<<<nb, NT, 0, s>>>(D, last ? 0 : 1, del_w_, del_c_);
-      launch_reduce_final(FIN_TERM, nb, -1, eval_pending_ ? spmv_blocks(n_ + m_) : 0, last ? nullptr : fact_reset());
+      // the termination test's state is published by its own finaliser: the host decides while the GPU
+      // runs this iteration's (speculative) factorisation, and a converged solve enqueues no directions
+      launch_reduce_final(FIN_TERM, nb, -1, eval_pending_ ? spmv_blocks(n_ + m_) : 0, last ? nullptr : fact_reset(),
+                          true);
       eval_pending_ = false;
       if (!last) {
         assemble_kkt(del_w_, del_c_, true);
         timed_factorize();
       }
-      // speculation: this iteration's directions (prediction_step!, mehrotra_correction_direction!,
-      // update_step_size!) are enqueued BEFORE the host reads the termination test and the
-      // factorisation status, so the GPU is busy while the host decides; they write scratch vectors
-      // and step scalars only (the iterate is updated by k_apply, enqueued after the decision), are
-      // discarded on termination and recomputed after a failed factorisation's retries.  Gondzio's
-      // loop synchronises internally: not speculated.
-      const bool spec = opt_.max_ncorr == 0 && !last;
-      if (spec) {  // the state read-back rides on the predictor's first launch
-        publish_next_ = true;
-        directions(false, true);
-        step_size(true);
-      } else {
-        read_state();
-      }
       wait_state();
-      const int frc = last ? 0 : ldl_->status(s, false);
-      const DevState& h = *hst_;
+      const DevState h = *hst_;
       last_ = h;
       if (h.nan_flag) {
         // SolveException in the previous iteration's solve_system! (linear_solver.jl:40-41): the
@@ -2158,6 +2165,21 @@ int MPCSolver::solve(madipm_stats* stats) {
         del_c_ = save_c;
         break;
       }
+      // speculation: this iteration's directions (prediction_step!, mehrotra_correction_direction!,
+      // update_step_size!) are enqueued BEFORE the host reads the factorisation status, so the GPU is
+      // busy while the host decides; they write scratch vectors and step scalars only (the iterate is
+      // updated by k_apply, enqueued after the decision) and are recomputed after a failed
+      // factorisation's retries.  Gondzio's loop synchronises internally: not speculated.
+      const bool spec = opt_.max_ncorr == 0;
+      if (spec) {  // the state read-back (with the factorisation status) rides on the predictor's first launch
+        publish_next_ = true;
+        directions(false, true);
+        step_size(true);
+      } else {
+        read_state();
+      }
+      wait_state();
+      const int frc = ldl_->status(s, false);
       if (frc != 0) {  // remaining trials of factorize_regularized_system!
         bool ok = false;
         for (int trial = 1; trial < 3 && !ok; ++trial) {

@@ -68,7 +68,8 @@ class MPCSolver {
   // solve also runs update_step_size!'s step test (only when nothing changes d in between: no Gondzio)
   void directions(bool redo, bool fuse_step);
   void step_size(bool fused);
-  void launch_reduce_final(int kind, int nvals, int amode = -1, int nb_eval = 0, LDLStatus* rs = nullptr);
+  void launch_reduce_final(int kind, int nvals, int amode = -1, int nb_eval = 0, LDLStatus* rs = nullptr,
+                           bool publish = false);
   int step_alpha_mode(double& tau) const;
   void read_state();  // enqueue the publication of the device state to the host mirror
   void wait_state();  // wait (host spin) until the last publication has landed
