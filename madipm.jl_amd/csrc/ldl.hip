@@ -684,12 +684,23 @@ __device__ __forceinline__ void factor16(double* A64, double* Dl, double* MK, do
 
 // Blocked LDL^T of the LDS tile A64 (lower part valid) by 4 waves: after the call A64 holds the
 // strictly-lower L (diagonal untouched), Dl the pivots and Ms[K] the four M_K blocks.
-__device__ __forceinline__ void diag64(double* A64, double* Dl, double* Ms, double* cbuf, int tid) {
+template <bool PK, bool RCP>
+__device__ __forceinline__ void factor16r(double* A, int r, int ld, int k0, int kw, double* Dl, double* MK, int lane);
+// f16r (MADIPM_F16R): 2 / 1 = the register-resident diagonal factor (reciprocal / IEEE quotient) on the
+// tile's 16-pivot blocks (identity-padded past kw: always 16 pivots), 0 = the LDS hand-off factor16
+__device__ __forceinline__ void diag64(double* A64, double* Dl, double* Ms, double* cbuf, int tid, int f16r) {
   const int lane = tid & 63, w = tid >> 6;
   double* cb = cbuf + w * 2 * 16 * LDM;
   double* xb = cb + 16 * LDM;
   for (int K = 0; K < 4; ++K) {
-    if (w == K) factor16(A64, Dl, Ms + K * 16 * LDM, cb, xb, K, lane);
+    if (w == K) {
+      if (f16r == 2)
+        factor16r<false, true>(A64, 64, LDA, 16 * K, 16, Dl, Ms + K * 16 * LDM, lane);
+      else if (f16r == 1)
+        factor16r<false, false>(A64, 64, LDA, 16 * K, 16, Dl, Ms + K * 16 * LDM, lane);
+      else
+        factor16(A64, Dl, Ms + K * 16 * LDM, cb, xb, K, lane);
+    }
     __syncthreads();
     dbl4 acc = {0.0, 0.0, 0.0, 0.0};
     if (w > K) {  // L_wK = A_wK M_K
@@ -880,7 +891,7 @@ __device__ __forceinline__ void f16r_steps(double (&a)[4], double (&x)[4], doubl
     f16r_steps<T + 1, RCP>(a, x, dmine, i, g);
   }
 }
-template <bool PK, bool RCP = false>
+template <bool PK, bool RCP>
 __device__ __forceinline__ void factor16r(double* A, int r, int ld, int k0, int kw, double* Dl, double* MK, int lane) {
   const int i = lane & 15, g = lane >> 4;
   const int ic = min(i, kw - 1);
@@ -1179,7 +1190,7 @@ __device__ __forceinline__ void factor16x(double* A, int r, int ld, int k0, int 
   if (f16r == 2)
     factor16r<PK, true>(A, r, ld, k0, kw, Dl, MK, lane);
   else if (f16r)
-    factor16r<PK>(A, r, ld, k0, kw, Dl, MK, lane);
+    factor16r<PK, false>(A, r, ld, k0, kw, Dl, MK, lane);
   else
     factor16s<PK>(A, r, ld, k0, kw, Dl, MK, cb, lane);
 }
@@ -2019,7 +2030,7 @@ __global__ __launch_bounds__(NT) void k_big_diag(FrontTab T, const int32_t* __re
     }
   }
   __syncthreads();
-  diag64(A64, Dl, Ms, cbuf, tid);
+  diag64(A64, Dl, Ms, cbuf, tid, T.f16r);
   for (int j = wv; j < kw; j += 4)
     if (lane >= j && lane < kw) F[lane + (int64_t)j * r] = (lane == j) ? Dl[j] : A64[lane + j * LDA];
   if (tid < kw) {

@@ -1540,6 +1540,7 @@ void MPCSolver::setup_host(const madipm_qp& q) {
   csr_from_coo(n + m, kc, kr, kv, Kcp, Kri, Kv);
   nnzK_ = (int64_t)Kri.size();
   if (const char* e = std::getenv("MADIPM_PART_BLOCKS")) maxb_ = std::max(1, std::min(MAXB, std::atoi(e)));
+  if (const char* e = std::getenv("MADIPM_SPEC_NEAR")) spec_near_ = std::max(0.0, std::atof(e));
   if (const char* e = std::getenv("MADIPM_FINAL_DEBUG"); e && e[0] == '1') {
     fdbg_.alloc(8 * kFinDbg);
     MADIPM_HIP(hipMemset(fdbg_.p, 0, 8 * kFinDbg * sizeof(int64_t)));
@@ -2112,7 +2113,13 @@ int MPCSolver::solve(madipm_stats* stats) {
       launch_reduce_final(FIN_TERM, nb, -1, eval_pending_ ? spmv_blocks(n_ + m_) : 0, last ? nullptr : fact_reset(),
                           true);
       eval_pending_ = false;
-      if (!last) {
+      // the factorisation is enqueued before the host reads the termination test (speculatively),
+      // except when the previous iteration's residuals were within spec_near_ x tol: there the solve
+      // is likely to stop now, and a converged test would leave the whole factorisation as waste
+      // (~0.3 ms on ex10) where holding it back costs one host turn-around (~20 us) otherwise
+      const bool hold = !last && spec_near_ > 0 && k_ > 0 &&
+                        std::max(inf_pr_, std::max(inf_du_, inf_compl_)) <= spec_near_ * opt_.tol;
+      if (!last && !hold) {
         assemble_kkt(del_w_, del_c_, true);
         timed_factorize();
       }
@@ -2170,6 +2177,10 @@ int MPCSolver::solve(madipm_stats* stats) {
       // busy while the host decides; they write scratch vectors and step scalars only (the iterate is
       // updated by k_apply, enqueued after the decision) and are recomputed after a failed
       // factorisation's retries.  Gondzio's loop synchronises internally: not speculated.
+      if (hold) {
+        assemble_kkt(del_w_, del_c_, true);
+        timed_factorize();
+      }
       const bool spec = opt_.max_ncorr == 0;
       if (spec) {  // the state read-back (with the factorisation status) rides on the predictor's first launch
         publish_next_ = true;

@@ -130,6 +130,7 @@ class MPCSolver {
   int exception_ = 0;  // MADIPM_EXC_* of the last solve (what solve!'s catch-all caught)
   bool initialized_ = false;
   double inf_pr_ = 0, inf_du_ = 0, inf_compl_ = 0;
+  double spec_near_ = 10.0;  // MADIPM_SPEC_NEAR: hold the speculative factorisation when residuals <= this x tol (0: never)
   double t_init_ = 0, t_total_ = 0, t_linsol_ = 0;
   std::vector<madipm_iter_trace> trace_;
   double fs0_ = 0;  // device factorisation seconds at initialize! (cnt.linear_solver_time origin)
