@@ -688,7 +688,18 @@ template <bool PK, bool RCP>
 __device__ __forceinline__ void factor16r(double* A, int r, int ld, int k0, int kw, double* Dl, double* MK, int lane);
 // f16r (MADIPM_F16R): 2 / 1 = the register-resident diagonal factor (reciprocal / IEEE quotient) on the
 // tile's 16-pivot blocks (identity-padded past kw: always 16 pivots), 0 = the LDS hand-off factor16
-__device__ __forceinline__ void diag64(double* A64, double* Dl, double* Ms, double* cbuf, int tid, int f16r) {
+template <bool PK, bool RCP>
+__device__ __forceinline__ void blocked_factor_pipe(double* A, int r, int w, int ld, double* Dl, double* MK0,
+                                                    double* MK1, int defer, int64_t* pt, double* MKall);
+__device__ __forceinline__ void diag64(double* A64, double* Dl, double* Ms, double* cbuf, int tid, int f16r,
+                                       int fpipe) {
+  if (fpipe && f16r) {  // the pipelined schedule (blocked_factor_pipe) on the identity-padded 64 x 64 tile
+    if (f16r == 2)
+      blocked_factor_pipe<false, true>(A64, 64, 64, LDA, Dl, nullptr, nullptr, 0, nullptr, Ms);
+    else
+      blocked_factor_pipe<false, false>(A64, 64, 64, LDA, Dl, nullptr, nullptr, 0, nullptr, Ms);
+    return;
+  }
   const int lane = tid & 63, w = tid >> 6;
   double* cb = cbuf + w * 2 * 16 * LDM;
   double* xb = cb + 16 * LDM;
@@ -1304,7 +1315,9 @@ __device__ __forceinline__ void pipe_add(int* f) {
 
 template <bool PK, bool RCP>
 __device__ __forceinline__ void blocked_factor_pipe(double* A, int r, int w, int ld, double* Dl, double* MK0,
-                                                    double* MK1, int defer = 0, int64_t* pt = nullptr) {
+                                                    double* MK1, int defer, int64_t* pt, double* MKall) {
+  // MKall != nullptr: block k's M_K is kept at MKall + 16 k LDM (k_big_diag hands all of them to
+  // k_big_trsm) instead of the two alternating buffers MK0 / MK1
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), nw = blockDim.x >> 6;
   const int no = nw - 1;  // waves 1 .. nw - 1: panel rest + trailing update
@@ -1324,7 +1337,7 @@ __device__ __forceinline__ void blocked_factor_pipe(double* A, int r, int w, int
       tc = now;
     }
   };
-  if (wv == 0) factor16r<PK, RCP>(A, r, ld, 0, min(16, w), Dl, MK0, lane);
+  if (wv == 0) factor16r<PK, RCP>(A, r, ld, 0, min(16, w), Dl, MKall ? MKall : MK0, lane);
   __syncthreads();  // block 0 factorised; the counters are zero
   const int64_t t1 = (pt && tid == 0) ? wall_clock64() : 0;
   int gen = 0;  // O-barrier generation (waves 1..)
@@ -1334,7 +1347,7 @@ __device__ __forceinline__ void blocked_factor_pipe(double* A, int r, int w, int
     const int nbr = (r - R0 + 15) >> 4;
     const int jhi = defer ? ((w - R0 + 15) >> 4) - 1 : nbr;
     const bool last = kb + 1 == nblk;
-    const double* MKc = (kb & 1) ? MK1 : MK0;
+    const double* MKc = MKall ? MKall + kb * 16 * LDM : ((kb & 1) ? MK1 : MK0);
     double dk[4];
     int64_t tx = 0;
     if (dbg) tc = wall_clock64();
@@ -1353,7 +1366,8 @@ __device__ __forceinline__ void blocked_factor_pipe(double* A, int r, int w, int
         trail_strip<PK, 1>(A, r, ld, k0, kw, R0, 0, 0, dk, lane, jend);  // the next diagonal tile
         wave_sync();
         lap(tx);
-        factor16r<PK, RCP>(A, r, ld, R0, min(16, w - R0), Dl, (kb & 1) ? MK0 : MK1, lane);
+        factor16r<PK, RCP>(A, r, ld, R0, min(16, w - R0), Dl,
+                           MKall ? MKall + (kb + 1) * 16 * LDM : ((kb & 1) ? MK0 : MK1), lane);
         pipe_set(&pc.mk, kb + 2);
         lap(tf);
       }
@@ -1418,9 +1432,9 @@ template <bool PK>
 __device__ __forceinline__ void factor_lds(const FrontTab& T, double* A, int r, int w, int ld, double* Dl, double* MK,
                                            double* cbuf, int64_t* pt = nullptr) {
   if (T.fpipe && T.f16r == 2 && (blockDim.x >> 6) >= 2)
-    blocked_factor_pipe<PK, true>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer, pt);
+    blocked_factor_pipe<PK, true>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer, pt, nullptr);
   else if (T.fpipe && T.f16r && (blockDim.x >> 6) >= 2)
-    blocked_factor_pipe<PK, false>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer, pt);
+    blocked_factor_pipe<PK, false>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer, pt, nullptr);
   else
     blocked_factor_lds<PK>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer, pt, T.f16r);
 }
@@ -2030,7 +2044,7 @@ __global__ __launch_bounds__(NT) void k_big_diag(FrontTab T, const int32_t* __re
     }
   }
   __syncthreads();
-  diag64(A64, Dl, Ms, cbuf, tid, T.f16r);
+  diag64(A64, Dl, Ms, cbuf, tid, T.f16r, T.fpipe);
   for (int j = wv; j < kw; j += 4)
     if (lane >= j && lane < kw) F[lane + (int64_t)j * r] = (lane == j) ? Dl[j] : A64[lane + j * LDA];
   if (tid < kw) {

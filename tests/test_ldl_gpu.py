@@ -188,14 +188,16 @@ def test_root_backward_in_forward_bitwise(case, monkeypatch):
     _check_case(K, Lw, well=case != "block_ipm")
 
 
+@pytest.mark.parametrize("pipe", ["0", "1"])
 @pytest.mark.parametrize("kpan", ["1", "2", "4"])
 @pytest.mark.parametrize("n,m", [(320, 100), (130, 200)])
-def test_big_front_panel_groups(kpan, n, m, monkeypatch):
+def test_big_front_panel_groups(kpan, n, m, pipe, monkeypatch):
     """A dense K2 (dense SPD H, dense A: one big front of n + m columns, several 64-column panels
     with a partial last one) on the big-front path with the deferred multi-panel trailing update in
     groups of MADIPM_BIG_KPAN panels (1 = right-looking per panel): pivots and solution of the oracle."""
     import scipy.sparse as sp
     monkeypatch.setenv("MADIPM_BIG_KPAN", kpan)
+    monkeypatch.setenv("MADIPM_FACT_PIPE", pipe)  # k_big_diag's 64 x 64 tile: pipelined or barrier schedule
     rng = np.random.default_rng(11)
     B = rng.standard_normal((n, n))
     H = B @ B.T / n + np.eye(n)
