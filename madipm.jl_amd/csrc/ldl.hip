@@ -693,7 +693,10 @@ __device__ __forceinline__ void blocked_factor_pipe(double* A, int r, int w, int
                                                     double* MK1, int defer, int64_t* pt, double* MKall);
 __device__ __forceinline__ void diag64(double* A64, double* Dl, double* Ms, double* cbuf, int tid, int f16r,
                                        int fpipe) {
-  if (fpipe && f16r) {  // the pipelined schedule (blocked_factor_pipe) on the identity-padded 64 x 64 tile
+  // MADIPM_FACT_PIPE=2: the pipelined schedule (blocked_factor_pipe) on the identity-padded 64 x 64 tile
+  // too — measured slower there (supportcase10 k_big_diag 18.1 -> 19.8 us, profiles/r3_p8_*: four pivot
+  // blocks leave the other waves too little to overlap), so the barrier schedule stays the default
+  if (fpipe == 2 && f16r) {
     if (f16r == 2)
       blocked_factor_pipe<false, true>(A64, 64, 64, LDA, Dl, nullptr, nullptr, 0, nullptr, Ms);
     else
@@ -3693,7 +3696,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     const char* e16 = std::getenv("MADIPM_F16R");  // register-resident 16-pivot block factor (factor16r)
     T_.f16r = e16 ? std::max(0, std::min(2, std::atoi(e16))) : 2;  // r3: reciprocal default (k_fact_tree -3 us)
     const char* ep = std::getenv("MADIPM_FACT_PIPE");  // pipelined in-LDS factorisation schedule
-    T_.fpipe = (ep && ep[0] == '0') ? 0 : 1;
+    T_.fpipe = ep ? std::max(0, std::min(2, std::atoi(ep))) : 1;  // 2: also k_big_diag's tile
   }
   T_.nrows = nrows_;
   T_.row_ptr = row_ptr_;

@@ -1037,8 +1037,11 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     // k_fact_tree runs one workgroup per CU, tickets in level order: the tree fronts past the first
     // `slots` start only when an earlier front retires, so folding (staging the leaves inside the
     // front's own critical path) is left to the micro launch for those late fronts
-    // (MADIPM_FOLD_SLOTS overrides the MI355X CU count; 0 = no limit)
-    int slots = 256;
+    // (MADIPM_FOLD_SLOTS overrides the MI355X CU count; 0 = no limit).  r3: no limit by default — with
+    // the pipelined in-LDS factorisation the late fronts' folds cost k_fact_tree less (163 -> 189 us)
+    // than the micro launch + gather pre-assembly they replace (~40 us and three launches): ex10
+    // 1547 -> 1593 iters/s (profiles/r3_p8b_*)
+    int slots = 0;
     if (const char* e = std::getenv("MADIPM_FOLD_SLOTS")) slots = std::atoi(e);
     std::vector<char> late(ns_all, 0);
     {

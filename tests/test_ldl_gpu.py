@@ -188,7 +188,7 @@ def test_root_backward_in_forward_bitwise(case, monkeypatch):
     _check_case(K, Lw, well=case != "block_ipm")
 
 
-@pytest.mark.parametrize("pipe", ["0", "1"])
+@pytest.mark.parametrize("pipe", ["1", "2"])
 @pytest.mark.parametrize("kpan", ["1", "2", "4"])
 @pytest.mark.parametrize("n,m", [(320, 100), (130, 200)])
 def test_big_front_panel_groups(kpan, n, m, pipe, monkeypatch):
@@ -197,7 +197,7 @@ def test_big_front_panel_groups(kpan, n, m, pipe, monkeypatch):
     groups of MADIPM_BIG_KPAN panels (1 = right-looking per panel): pivots and solution of the oracle."""
     import scipy.sparse as sp
     monkeypatch.setenv("MADIPM_BIG_KPAN", kpan)
-    monkeypatch.setenv("MADIPM_FACT_PIPE", pipe)  # k_big_diag's 64 x 64 tile: pipelined or barrier schedule
+    monkeypatch.setenv("MADIPM_FACT_PIPE", pipe)  # k_big_diag's 64 x 64 tile: barrier (1) or pipelined (2) schedule
     rng = np.random.default_rng(11)
     B = rng.standard_normal((n, n))
     H = B @ B.T / n + np.eye(n)
