@@ -42,6 +42,10 @@ typedef struct madipm_ldl_opts {
   int32_t nshards;         /* > 1: subtree-sharded factorisation with nshards shards on THIS device
                               (single process, local all-reduce; SURVEY §8 e); default 1.  Across
                               GPUs use madipm_solver_create_dist / madipm_ldl_analyze_shard. */
+  int32_t cholesky;        /* 1: Cholesky semantics — the matrix must be SPD, any pivot that is not > 0
+                              fails the factorisation (is_factorized == false): the cuDSS CHOLESKY
+                              configuration the reference pairs with NormalKKTSystem
+                              (test/test_gpu.jl:11); default 0 (quasi-definite LDL^T)  [ABI 0.2] */
 } madipm_ldl_opts;
 
 typedef struct madipm_ldl_info {

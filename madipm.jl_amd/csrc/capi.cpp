@@ -52,7 +52,17 @@ struct madipm_ldl {
   LinSolver* lin = nullptr;        // factorize / solve entry
   hipStream_t last_stream = nullptr;
   bool pending = false;
+  // sharded solve protocol (ABI 0.2): the phase the next madipm_ldl_solve_phase call must be (1 when
+  // idle).  Phase 2 returns the all-gather buffer and phase 3 is required — a binding that follows the
+  // 0.1 protocol (phase 2, then an all-reduce of x) is refused at its next call instead of silently
+  // getting a wrong x
+  int solve_next = 1;
 };
+static void require_idle(const madipm_ldl* ls) {
+  MADIPM_REQUIRE(ls->solve_next == 1, "sharded solve protocol: phase " + std::to_string(ls->solve_next) +
+                                          " of madipm_ldl_solve_phase is pending (phase 2 returns the gather "
+                                          "buffer, phase 3 scatters it: ABI 0.2)");
+}
 
 struct madipm_comm {
   std::unique_ptr<Comm> c;
@@ -73,7 +83,7 @@ static SymbolicOptions to_sym_opts(const madipm_ldl_opts* o) {
 
 extern "C" {
 
-int madipm_version(void) { return 100; }
+int madipm_version(void) { return 200; }  // 0.2.0: three-phase sharded solve
 
 const char* madipm_last_error(void) { return last_error(); }
 
@@ -98,6 +108,7 @@ void madipm_ldl_default_opts(madipm_ldl_opts* o) {
   o->small_front_max = 128;
   o->pivot_tol = 0.0;
   o->nshards = 1;
+  o->cholesky = 0;
 }
 
 int madipm_symbolic_analyze(int32_t n, const int64_t* colptr, const int32_t* rowval,
@@ -210,6 +221,9 @@ int madipm_ldl_analyze(int32_t n, const int64_t* colptr, const int32_t* rowval, 
     ls->s = ls->own.get();
     ls->lin = ls->s;
   }
+  ls->lin->spd = o.cholesky != 0;
+  if (ls->g)
+    for (int q = 0; q < ls->g->nshards(); ++q) ls->g->shard(q).spd = ls->lin->spd;
   *out = ls.release();
   return 0;
   MADIPM_API_END
@@ -230,6 +244,7 @@ int madipm_ldl_analyze_shard(int32_t n, const int64_t* colptr, const int32_t* ro
   ls->own = std::make_unique<LDLSolver>(n, colptr, rowval, so, o.pivot_tol, user_perm);
   ls->s = ls->own.get();
   ls->lin = ls->s;
+  ls->lin->spd = o.cholesky != 0;
   *out = ls.release();
   return 0;
   MADIPM_API_END
@@ -239,6 +254,7 @@ int madipm_ldl_factorize_phase(madipm_ldl_t ls, int32_t phase, const double* d_n
                                double** xbuf, int64_t* xlen) {
   MADIPM_API_BEGIN
   MADIPM_REQUIRE(ls && ls->own && (phase == 1 || phase == 2), "bad argument");
+  require_idle(ls);
   hipStream_t st = (hipStream_t)stream;
   if (phase == 1) {
     ls->s->fact_phase1(d_nzval, st);
@@ -257,6 +273,9 @@ int madipm_ldl_solve_phase(madipm_ldl_t ls, int32_t phase, double* d_x, madipm_s
                            int64_t* xlen) {
   MADIPM_API_BEGIN
   MADIPM_REQUIRE(ls && ls->own && phase >= 1 && phase <= 3 && d_x, "bad argument");
+  MADIPM_REQUIRE(phase == ls->solve_next, "sharded solve protocol: phase " + std::to_string(phase) + " called, phase " +
+                                             std::to_string(ls->solve_next) + " expected (1 -> 2 -> 3; ABI 0.2)");
+  ls->solve_next = phase == 3 ? 1 : phase + 1;
   hipStream_t st = (hipStream_t)stream;
   if (phase == 1) {
     ls->s->solve_phase1(d_x, st);
@@ -364,6 +383,7 @@ int madipm_ldl_factorize_async(madipm_ldl_t ls, const double* d_nzval, madipm_st
 int madipm_ldl_factorize(madipm_ldl_t ls, const double* d_nzval, madipm_stream_t stream) {
   MADIPM_API_BEGIN
   MADIPM_REQUIRE(ls, "null handle");
+  require_idle(ls);
   ls->lin->factorize_async(d_nzval, (hipStream_t)stream);
   ls->pending = false;
   return ls->lin->status((hipStream_t)stream);
@@ -384,6 +404,7 @@ int madipm_ldl_is_factorized(madipm_ldl_t ls) {
 int madipm_ldl_solve(madipm_ldl_t ls, double* d_x, int32_t nrhs, madipm_stream_t stream) {
   MADIPM_API_BEGIN
   MADIPM_REQUIRE(ls && (d_x || ls->s->n() == 0), "null argument");
+  require_idle(ls);
   for (int k = 0; k < nrhs; ++k) ls->lin->solve_async(d_x + (int64_t)k * ls->s->n(), (hipStream_t)stream);
   return 0;
   MADIPM_API_END

@@ -638,83 +638,16 @@ __device__ __forceinline__ void task_of(const int32_t* __restrict__ list, int& s
 constexpr int LDA = 65;
 constexpr int LDM = 17;
 
-// Factor the 16x16 diagonal sub-block K of A64 with ONE wave (LDS column broadcast, no barriers):
-// writes the unit-lower L_KK (strictly lower part) into A64, d into Dl, and M_K = L_KK^{-T} D_K^{-1}
-// (16x16, ld 17) into MK.  The same row operations applied to an identity give X = L_KK^{-1}.
-__device__ __forceinline__ void factor16(double* A64, double* Dl, double* MK, double* cb, double* xb, int K, int lane) {
-  const int il = lane & 15, cg = lane >> 4;
-  const int i = 16 * K + il;
-  double a[4], x[4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    const int jl = cg + 4 * m;
-    a[m] = (jl <= il) ? A64[i + (16 * K + jl) * LDA] : 0.0;
-    x[m] = (jl == il) ? 1.0 : 0.0;
-  }
-#pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    if (cg == (t & 3)) cb[t * LDM + il] = a[t >> 2];
-    if (il == t) {
-#pragma unroll
-      for (int m = 0; m < 4; ++m) xb[t * LDM + cg + 4 * m] = x[m];
-    }
-    wave_sync();
-    const double dt = cb[t * LDM + t];
-    const double li = (il > t) ? cb[t * LDM + il] / dt : 0.0;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int jl = cg + 4 * m;
-      const double cj = cb[t * LDM + jl];
-      const double xt = xb[t * LDM + jl];
-      a[m] = fma(jl > t ? -li : 0.0, cj, a[m]);
-      x[m] = fma(jl > t ? 0.0 : -li, xt, x[m]);
-    }
-  }
-  wave_sync();
-  const double di = cb[il * LDM + il];
-#pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    const int jl = cg + 4 * m;
-    if (jl < il) A64[i + (16 * K + jl) * LDA] = a[m] / cb[jl * LDM + jl];
-    MK[jl * LDM + il] = (jl <= il) ? x[m] / di : 0.0;  // M[k=jl][n=il] = X(il, jl) / d_il
-  }
-  if (cg == 0) Dl[i] = di;
-  wave_sync();
-}
-
 // Blocked LDL^T of the LDS tile A64 (lower part valid) by 4 waves: after the call A64 holds the
 // strictly-lower L (diagonal untouched), Dl the pivots and Ms[K] the four M_K blocks.
 template <bool PK, bool RCP>
 __device__ __forceinline__ void factor16r(double* A, int r, int ld, int k0, int kw, double* Dl, double* MK, int lane);
-// f16r (MADIPM_F16R): 2 / 1 = the register-resident diagonal factor (reciprocal / IEEE quotient) on the
-// tile's 16-pivot blocks (identity-padded past kw: always 16 pivots), 0 = the LDS hand-off factor16
-template <bool PK, bool RCP>
-__device__ __forceinline__ void blocked_factor_pipe(double* A, int r, int w, int ld, double* Dl, double* MK0,
-                                                    double* MK1, int defer, int64_t* pt, double* MKall);
-__device__ __forceinline__ void diag64(double* A64, double* Dl, double* Ms, double* cbuf, int tid, int f16r,
-                                       int fpipe) {
-  // MADIPM_FACT_PIPE=2: the pipelined schedule (blocked_factor_pipe) on the identity-padded 64 x 64 tile
-  // too — measured slower there (supportcase10 k_big_diag 18.1 -> 19.8 us, profiles/r3_p8_*: four pivot
-  // blocks leave the other waves too little to overlap), so the barrier schedule stays the default
-  if (fpipe == 2 && f16r) {
-    if (f16r == 2)
-      blocked_factor_pipe<false, true>(A64, 64, 64, LDA, Dl, nullptr, nullptr, 0, nullptr, Ms);
-    else
-      blocked_factor_pipe<false, false>(A64, 64, 64, LDA, Dl, nullptr, nullptr, 0, nullptr, Ms);
-    return;
-  }
+// (the pipelined schedule of blocked_factor_pipe on this tile was measured slower — supportcase10
+// k_big_diag 18.1 -> 19.8 us, r3: four pivot blocks leave the other waves too little to overlap)
+__device__ __forceinline__ void diag64(double* A64, double* Dl, double* Ms, int tid) {
   const int lane = tid & 63, w = tid >> 6;
-  double* cb = cbuf + w * 2 * 16 * LDM;
-  double* xb = cb + 16 * LDM;
   for (int K = 0; K < 4; ++K) {
-    if (w == K) {
-      if (f16r == 2)
-        factor16r<false, true>(A64, 64, LDA, 16 * K, 16, Dl, Ms + K * 16 * LDM, lane);
-      else if (f16r == 1)
-        factor16r<false, false>(A64, 64, LDA, 16 * K, 16, Dl, Ms + K * 16 * LDM, lane);
-      else
-        factor16(A64, Dl, Ms + K * 16 * LDM, cb, xb, K, lane);
-    }
+    if (w == K) factor16r<false, true>(A64, 64, LDA, 16 * K, 16, Dl, Ms + K * 16 * LDM, lane);
     __syncthreads();
     dbl4 acc = {0.0, 0.0, 0.0, 0.0};
     if (w > K) {  // L_wK = A_wK M_K
@@ -772,80 +705,14 @@ __device__ __forceinline__ int fidx(int i, int j, int r, int ld) {
 
 // Factor the 16 x 16 diagonal block K at (k0, k0) of the front in LDS with ONE wave (identity-padded
 // past kw): writes the strictly-lower unit L_KK into A, d into Dl[k0 + i] and M_K = L_KK^{-T} D^{-1}
-// (ld LDM, zero above the diagonal) into MK.  The elements are spread over the whole wave: lane (i = lane & 15,
-// g = lane >> 4) holds A(i, 4g .. 4g+3) and X(i, 4g .. 4g+3).  Step t: the 16 lanes holding column t
-// write it to LDS (lane i == t: row t of X), then every lane reads back the pivot, its row's entry and
-// its four columns' entries (one wave: a wave-scope fence orders them, no barrier).  l = a / d is
-// the IEEE quotient (the level path's rounding); a lane does 4 + 4 FMAs per step and no SGPR
-// broadcasts (a lane-per-row version with v_readlane broadcasts needs ~34 of them per step and ran
-// 4.5 us per block against 3.7 us for this one).
-// cb: 512 doubles of LDS scratch.
-template <bool PK>
-__device__ __forceinline__ void factor16s(double* A, int r, int ld, int k0, int kw, double* Dl, double* MK, double* cb,
-                                          int lane) {
-  const int i = lane & 15, g = lane >> 4;
-  const int ic = min(i, kw - 1);
-  double a[4], x[4], v[4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    const int j = 4 * g + m, jc = min(j, kw - 1);
-    v[m] = A[fidx<PK>(k0 + max(ic, jc), k0 + min(ic, jc), r, ld)];  // upper part mirrored (never read)
-  }
-  LDL_PIN4(v);  // keep the loads unconditional (pinned after all four are issued)
-#pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    const int j = 4 * g + m;
-    a[m] = (i < kw && j < kw) ? v[m] : (i == j ? 1.0 : 0.0);
-    x[m] = (i == j) ? 1.0 : 0.0;
-  }
-  double* col = cb;        // col[16 t + i] = A(i, t) at step t
-  double* xrw = cb + 256;  // xrw[16 t + j] = X(t, j) at step t
-  double dmine = 1.0;
-#pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    const int gt = t >> 2, mt = t & 3;
-    if (g == gt) col[16 * t + i] = a[mt];
-    if (i == t) {
-      reinterpret_cast<double2*>(xrw + 16 * t + 4 * g)[0] = double2{x[0], x[1]};
-      reinterpret_cast<double2*>(xrw + 16 * t + 4 * g)[1] = double2{x[2], x[3]};
-    }
-    wave_sync();  // cross-lane hand-off through LDS: keep the reads after the writes
-    const double dt = col[16 * t + t];
-    const double ci = col[16 * t + i];
-    const double2 c01 = reinterpret_cast<const double2*>(col + 16 * t + 4 * g)[0];
-    const double2 c23 = reinterpret_cast<const double2*>(col + 16 * t + 4 * g)[1];
-    const double2 x01 = reinterpret_cast<const double2*>(xrw + 16 * t + 4 * g)[0];
-    const double2 x23 = reinterpret_cast<const double2*>(xrw + 16 * t + 4 * g)[1];
-    const double cj[4] = {c01.x, c01.y, c23.x, c23.y}, xr[4] = {x01.x, x01.y, x23.x, x23.y};
-    const double li = (i > t) ? ci / dt : 0.0;  // IEEE quotient
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int j = 4 * g + m;
-      a[m] = (j > t) ? fma(-li, cj[m], a[m]) : a[m];
-      x[m] = (j <= t) ? fma(-li, xr[m], x[m]) : x[m];
-    }
-    if (i == t) dmine = dt;
-    if (g == gt && i > t) a[mt] = li;
-  }
-#pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    const int j = 4 * g + m;
-    if (j < i && i < kw) A[fidx<PK>(k0 + i, k0 + j, r, ld)] = a[m];
-    MK[j * LDM + i] = (j <= i) ? x[m] / dmine : 0.0;
-  }
-  if (g == 0 && i < kw) Dl[k0 + i] = dmine;
-  wave_sync();
-}
-
-// Register-resident variant of factor16s (same interface and output): no LDS hand-off per step.
+// (ld LDM, zero above the diagonal) into MK — register-resident, no LDS hand-off per step (the LDS
+// hand-off variant took ~3.8 us per block against ~2.6 us for this one, r3).
 // Lane (i = lane & 15, g = lane >> 4) holds A(i, j) and X(i, j) for the four columns j = 4m + g in
 // a[m], x[m]: column t lives in register t >> 2 of row group t & 3.  Step t:
 //   d_t = A(t, t): v_readlane (wave-uniform);
 //   A(i, t) to every row group: v_permlane16_swap + v_permlane32_swap (gfx950) of row group t & 3;
 //   A(t, j), X(t, j) of the lane's columns: DPP row_newbcast:t inside the lane's 16-lane row.
-// Every row i > t is updated with the mirrored row t (A(t, j), j > t) where factor16s reads column t
-// (A(j, t)): both hold the same Schur complement entry, rounded along mirrored paths, so the two
-// variants agree to rounding (not bitwise).  l = A(i, t) / d_t is the same IEEE quotient.
+// Every row i > t is updated with the mirrored row t (A(t, j), j > t).
 template <int T>
 __device__ __forceinline__ double dpp_row_bcast(double v) {  // lane T of every 16-lane row, to the row
   int lo = __double2loint(v), hi = __double2hiint(v);
@@ -873,7 +740,7 @@ __device__ __forceinline__ void fmac_row_bcast(double& acc, double mul) {
                : "+v"(acc)
                : "v"(mul), "n"(T));
 }
-// RCP (MADIPM_F16R=2): l = A(i, t) * (1 / d_t) with the reciprocal from v_rcp_f64 + two Newton steps
+// RCP: l = A(i, t) * (1 / d_t) with the reciprocal from v_rcp_f64 + two Newton steps
 // (within an ulp of the IEEE quotient; ~6 dependent instructions on the pivot chain instead of the
 // ~10 of the IEEE division sequence)
 __device__ __forceinline__ double recip_nr(double d) {
@@ -1199,19 +1066,8 @@ __device__ __forceinline__ void schur_strips(double* A, int r, int ld, int w, co
 // pt (diagnostics, MADIPM_TREE_DEBUG): thread 0 accumulates the phase times (first pivot block,
 // panels, J = 0 strips, lookahead sections, Schur pass) into pt[0..4]
 template <bool PK>
-__device__ __forceinline__ void factor16x(double* A, int r, int ld, int k0, int kw, double* Dl, double* MK, double* cb,
-                                          int lane, int f16r) {
-  if (f16r == 2)
-    factor16r<PK, true>(A, r, ld, k0, kw, Dl, MK, lane);
-  else if (f16r)
-    factor16r<PK, false>(A, r, ld, k0, kw, Dl, MK, lane);
-  else
-    factor16s<PK>(A, r, ld, k0, kw, Dl, MK, cb, lane);
-}
-
-template <bool PK>
 __device__ __forceinline__ void blocked_factor_lds(double* A, int r, int w, int ld, double* Dl, double* MK, double* cbuf,
-                                                   int defer = 0, int64_t* pt = nullptr, int f16r = 0) {
+                                                   int defer = 0, int64_t* pt = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), nw = blockDim.x >> 6;
   const int nblk = (w + 15) >> 4;
@@ -1226,7 +1082,7 @@ __device__ __forceinline__ void blocked_factor_lds(double* A, int r, int w, int 
     }
   };
   const int64_t cyc0 = (pt && tid == 0) ? (int64_t)clock64() : 0;
-  if (wv == 0) factor16x<PK>(A, r, ld, 0, min(16, w), Dl, MK, cbuf, lane, f16r);
+  if (wv == 0) factor16r<PK, true>(A, r, ld, 0, min(16, w), Dl, MK, lane);
   __syncthreads();
   stamp(0);
   const int64_t cyc1 = (pt && tid == 0) ? (int64_t)clock64() : 0;
@@ -1252,7 +1108,7 @@ __device__ __forceinline__ void blocked_factor_lds(double* A, int r, int w, int 
       // ... then one wave factorises it while the others update the rest (J >= 1)
       const int fw = (kb + 1) % nw;
       if (wv == fw)
-        factor16x<PK>(A, r, ld, R0, min(16, w - R0), Dl, MK, cbuf, lane, f16r);
+        factor16r<PK, true>(A, r, ld, R0, min(16, w - R0), Dl, MK, lane);
       else
         trail_strips<PK>(A, r, ld, k0, kw, R0, nbr, 1, jhi, dk, (wv - fw + nw - 1) % nw, nw - 1, lane, jend);
     } else if (!defer) {
@@ -1316,11 +1172,11 @@ __device__ __forceinline__ void pipe_add(int* f) {
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(f, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <bool PK, bool RCP>
+template <bool PK>
 __device__ __forceinline__ void blocked_factor_pipe(double* A, int r, int w, int ld, double* Dl, double* MK0,
-                                                    double* MK1, int defer, int64_t* pt, double* MKall) {
-  // MKall != nullptr: block k's M_K is kept at MKall + 16 k LDM (k_big_diag hands all of them to
-  // k_big_trsm) instead of the two alternating buffers MK0 / MK1
+                                                    double* MK1, int defer, int64_t* pt, int32_t* err, int fault) {
+  constexpr bool RCP = true;
+  double* const MKall = nullptr;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), nw = blockDim.x >> 6;
   const int no = nw - 1;  // waves 1 .. nw - 1: panel rest + trailing update
@@ -1371,7 +1227,7 @@ __device__ __forceinline__ void blocked_factor_pipe(double* A, int r, int w, int
         lap(tx);
         factor16r<PK, RCP>(A, r, ld, R0, min(16, w - R0), Dl,
                            MKall ? MKall + (kb + 1) * 16 * LDM : ((kb & 1) ? MK0 : MK1), lane);
-        pipe_set(&pc.mk, kb + 2);
+        if (!(fault && kb == 0)) pipe_set(&pc.mk, kb + 2);  // fault: MADIPM_DEBUG_PIPE_FAULT (tests only)
         lap(tf);
       }
     } else {
@@ -1416,6 +1272,10 @@ __device__ __forceinline__ void blocked_factor_pipe(double* A, int r, int w, int
   }
   if (dbg && tid == 64) pc.ow = tw;
   __syncthreads();
+  // a lost hand-off (a wait that timed out) leaves a wrong factor: raise the sticky status error that
+  // status() turns into a failure (the flag polls between fronts do the same)
+  if (tid == 0 && __hip_atomic_load(&pc.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) && err)
+    __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int64_t t2 = (pt && tid == 0) ? wall_clock64() : 0;
   if (defer) {
     schur_strips<PK>(A, r, ld, w, Dl, wv, nw, lane);
@@ -1434,12 +1294,10 @@ __device__ __forceinline__ void blocked_factor_pipe(double* A, int r, int w, int
 template <bool PK>
 __device__ __forceinline__ void factor_lds(const FrontTab& T, double* A, int r, int w, int ld, double* Dl, double* MK,
                                            double* cbuf, int64_t* pt = nullptr) {
-  if (T.fpipe && T.f16r == 2 && (blockDim.x >> 6) >= 2)
-    blocked_factor_pipe<PK, true>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer, pt, nullptr);
-  else if (T.fpipe && T.f16r && (blockDim.x >> 6) >= 2)
-    blocked_factor_pipe<PK, false>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer, pt, nullptr);
+  if (T.fpipe && (blockDim.x >> 6) >= 2)
+    blocked_factor_pipe<PK>(A, r, w, ld, Dl, MK, cbuf, 1, pt, T.err, T.pipe_fault);
   else
-    blocked_factor_lds<PK>(A, r, w, ld, Dl, MK, cbuf, T.schur_defer, pt, T.f16r);
+    blocked_factor_lds<PK>(A, r, w, ld, Dl, MK, cbuf, 1, pt);
 }
 
 
@@ -2025,7 +1883,6 @@ __global__ __launch_bounds__(NT) void k_big_diag(FrontTab T, const int32_t* __re
   __shared__ double A64[64 * LDA];
   __shared__ double Ms[4 * 16 * LDM];
   __shared__ double Dl[64];
-  __shared__ double cbuf[4 * 2 * 16 * LDM];
   int s, item;
   task_of(list, s, item);
   (void)item;
@@ -2047,7 +1904,7 @@ __global__ __launch_bounds__(NT) void k_big_diag(FrontTab T, const int32_t* __re
     }
   }
   __syncthreads();
-  diag64(A64, Dl, Ms, cbuf, tid, T.f16r, T.fpipe);
+  diag64(A64, Dl, Ms, tid);
   for (int j = wv; j < kw; j += 4)
     if (lane >= j && lane < kw) F[lane + (int64_t)j * r] = (lane == j) ? Dl[j] : A64[lane + j * LDA];
   if (tid < kw) {
@@ -3689,14 +3546,14 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   perm_.upload(S.perm);
   T_.first = first_;
   {
-    const char* ev = std::getenv("MADIPM_SCHUR_DEFER");
-    T_.schur_defer = (ev && ev[0] == '0') ? 0 : 1;
     const char* ek = std::getenv("MADIPM_BIG_KPAN");  // panels per deferred big-front update group
     big_kpan_ = ek ? std::max(1, std::min(8, std::atoi(ek))) : 4;
-    const char* e16 = std::getenv("MADIPM_F16R");  // register-resident 16-pivot block factor (factor16r)
-    T_.f16r = e16 ? std::max(0, std::min(2, std::atoi(e16))) : 2;  // r3: reciprocal default (k_fact_tree -3 us)
-    const char* ep = std::getenv("MADIPM_FACT_PIPE");  // pipelined in-LDS factorisation schedule
-    T_.fpipe = ep ? std::max(0, std::min(2, std::atoi(ep))) : 1;  // 2: also k_big_diag's tile
+    // pipelined in-LDS factorisation schedule (1, default); 0 = the barrier schedule, bitwise the same
+    // factor (test_ldl_fact_pipe_bitwise)
+    const char* ep = std::getenv("MADIPM_FACT_PIPE");
+    T_.fpipe = (ep && ep[0] == '0') ? 0 : 1;
+    const char* ef = std::getenv("MADIPM_DEBUG_PIPE_FAULT");  // tests: drop one hand-off (sticky error)
+    T_.pipe_fault = (ef && ef[0] == '1') ? 1 : 0;
   }
   T_.nrows = nrows_;
   T_.row_ptr = row_ptr_;
@@ -4436,6 +4293,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   MADIPM_HIP(hipHostMalloc((void**)&h_status_, sizeof(LDLStatus), hipHostMallocDefault));
   st_ = status_.p;
   h_st_ = h_status_;
+  T_.err = &st_->err;
   status_.zero();
   h_st_->err = 0;
   static bool attr_done = false;
@@ -4704,6 +4562,7 @@ bool LDLSolver::external_status(LDLStatus* dev, LDLStatus* host) {
   if (sharded() || !dev || !host) return false;
   st_ = dev;
   h_st_ = host;
+  T_.err = &st_->err;
   ext_status_ = true;
   k_status_init<<<1, 1, 0, nullptr>>>(st_, 1);
   MADIPM_HIP(hipDeviceSynchronize());
@@ -4791,7 +4650,7 @@ void LDLSolver::tree_debug_dump(hipStream_t s, const char* what, const int64_t* 
         fprintf(stderr, "  store level %d: U issue %.2f  drain+flag %.2f  L/D %.2f us\n", lv, sq[lv * 3] / na[lv],
                 sq[lv * 3 + 1] / na[lv], sq[lv * 3 + 2] / na[lv]);
     for (int lv = 0; lv < S_.nlevels; ++lv)
-      if (na[lv] && T_.fpipe && T_.f16r)
+      if (na[lv] && T_.fpipe)
         fprintf(stderr,
                 "  factor level %d: %d fronts  first16 %.2f  block steps %.2f  (wave 0: waits %.2f  diag factors %.2f; "
                 "wave 1 waits %.2f)  schur %.2f us\n",

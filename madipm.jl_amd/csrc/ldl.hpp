@@ -67,9 +67,9 @@ struct FrontTab {
   const int32_t* fold_lmax;
   const uint2* fold_prod;
   const uint8_t* fs_img;  // 1: fscratch holds the front's LDS image (tree fronts), else ld r
-  int schur_defer;  // in-LDS factorisation: update block U in one pass after the pivots (MADIPM_SCHUR_DEFER)
-  int f16r;         // 16-pivot diagonal blocks factorised in registers (factor16r; MADIPM_F16R=2 reciprocal (default), 1 IEEE quotient, 0 factor16s)
+  int32_t* err;     // the status block's sticky error (LDLStatus::err): a timed-out hand-off inside a front
   int fpipe;        // pipelined in-LDS schedule (blocked_factor_pipe; MADIPM_FACT_PIPE=0: blocked_factor_lds)
+  int pipe_fault;   // tests (MADIPM_DEBUG_PIPE_FAULT=1): blocked_factor_pipe drops one hand-off
 };
 
 struct SolveTask {

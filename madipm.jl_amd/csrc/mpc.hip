@@ -482,7 +482,8 @@ __device__ void block_argmin4(const double (&v)[4], const int (&ix)[4], double* 
   }
 }
 
-__device__ void alpha_body(const DV& D, int mode, double tau_param, int base, int bid, int nblk, bool from_p);
+template <bool FROM_P>
+__device__ void alpha_body(const DV& D, int mode, double tau_param, int base, int bid, int nblk);
 
 // nres < gridDim.x: blocks [nres, gridDim.x) run the step test of mode amode (alpha_body, partials
 // from slot PART_ALPHA) beside the nres residual blocks — one launch for both
@@ -490,7 +491,7 @@ template <int G>
 __global__ __launch_bounds__(NT) void k_residual(DV D, double dw, double dc, int nres, int amode, double atau) {
   const int n = D.n, m = D.m, nlb = D.nlb;
   if ((int)blockIdx.x >= nres) {
-    alpha_body(D, amode, atau, PART_ALPHA, (int)blockIdx.x - nres, (int)gridDim.x - nres, true);
+    alpha_body<true>(D, amode, atau, PART_ALPHA, (int)blockIdx.x - nres, (int)gridDim.x - nres);
     return;
   }
   const bool lead = (threadIdx.x & (G - 1)) == 0;
@@ -543,8 +544,12 @@ __global__ __launch_bounds__(NT) void k_residual(DV D, double dw, double dc, int
 
 // get_alpha_max_primal / get_alpha_max_dual (kernels.jl:226-272): min-ratio with argmin
 // from_p: dz formed here from the reduced rhs p and dx, exactly as k_residual's finish_aug_solve
-// forms it (the step-test blocks of a k_residual launch run beside the residual blocks that store it)
-__device__ void alpha_body(const DV& D, int mode, double tau_param, int base, int bid, int nblk, bool from_p) {
+// forms it (the step-test blocks of a k_residual launch run beside the residual blocks that store it).
+// The reduced-rhs operands (p, l_lower, l_diag, u_lower, u_diag) exist only in the FROM_P instance:
+// madipm_update_step's standalone DV leaves them null.
+template <bool FROM_P>
+__device__ void alpha_body(const DV& D, int mode, double tau_param, int base, int bid, int nblk) {
+  constexpr bool from_p = FROM_P;
   const int n = D.n, m = D.m, nlb = D.nlb, nub = D.nub;
   const double tau = alpha_tau(D, mode, tau_param);
   double v[4] = {INF, INF, INF, INF};
@@ -555,11 +560,12 @@ __device__ void alpha_body(const DV& D, int mode, double tau_param, int base, in
     const int tl = t < nlb ? (int)t : 0, tu = t < nub ? (int)t : 0;
     const int il = nlb > 0 ? D.ind_lb[tl] : 0, iu = nub > 0 ? D.ind_ub[tu] : 0;
     const double dxl = D.d[il], xl_x = D.x[il], xl_l = D.xl[il], zl = D.zl[il];
-    const double pl = from_p ? D.p[nlb > 0 ? n + m + tl : 0] : D.d[nlb > 0 ? n + m + tl : 0], lo = D.l_lower[tl],
-                 ldg = D.l_diag[tl];
+    const double pl = from_p ? D.p[nlb > 0 ? n + m + tl : 0] : D.d[nlb > 0 ? n + m + tl : 0];
+    const double lo = from_p ? D.l_lower[tl] : 0.0, ldg = from_p ? D.l_diag[tl] : 1.0;
     const double dxu = D.d[iu], xu_x = D.x[iu], xu_u = D.xu[iu], zu = D.zu[iu];
     const int qu = nub > 0 ? n + m + nlb + tu : 0;  // in range
-    const double pu = from_p ? D.p[qu] : D.d[qu], uo = D.u_lower[tu], udg = D.u_diag[tu];
+    const double pu = from_p ? D.p[qu] : D.d[qu];
+    const double uo = from_p ? D.u_lower[tu] : 0.0, udg = from_p ? D.u_diag[tu] : 1.0;
     if (t < nlb) {
       const double dx = dxl;
       if (dx < 0) amin_upd(v[0], ix[0], (-xl_x + xl_l) * tau / dx, (int)t);
@@ -577,7 +583,7 @@ __device__ void alpha_body(const DV& D, int mode, double tau_param, int base, in
 }
 
 __global__ __launch_bounds__(NT) void k_alpha(DV D, int mode, double tau_param, int base) {
-  alpha_body(D, mode, tau_param, base, blockIdx.x, gridDim.x, false);
+  alpha_body<false>(D, mode, tau_param, base, blockIdx.x, gridDim.x);
 }
 
 enum { MU_PRED = 0, MU_FULL = 1, MU_GONDZIO = 2 };
@@ -1071,12 +1077,14 @@ __global__ __launch_bounds__(FT) void k_final(DV D, int kind, FinParams P) {
       st_sc1(L2 + 16 * FG + g, a);
     }
     if (P.dbg && g == 0) P.dbg[5] = (int64_t)wall_clock64();  // level 1 reduced
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    s_last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == FG - 1;
+    // release: this workgroup's level-2 partials are visible before its ticket; the last
+    // workgroup's acquire (below) pairs with every earlier release on the ticket's RMW chain
+    s_last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == FG - 1;
     if (P.dbg && s_last) P.dbg[6] = (int64_t)wall_clock64();  // last ticket taken
   }
   __syncthreads();
   if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every thread of the last workgroup: see the partials
   // level 2 (last workgroup): every level-2 partial loaded at once (one per thread, sc1), then thread k
   // combines value slot k over the workgroups in order
   const int t = threadIdx.x;

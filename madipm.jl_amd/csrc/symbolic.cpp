@@ -1034,56 +1034,30 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     };
     std::vector<Prod> pr;
     std::vector<int64_t> bnd;
-    // k_fact_tree runs one workgroup per CU, tickets in level order: the tree fronts past the first
-    // `slots` start only when an earlier front retires, so folding (staging the leaves inside the
-    // front's own critical path) is left to the micro launch for those late fronts
-    // (MADIPM_FOLD_SLOTS overrides the MI355X CU count; 0 = no limit).  r3: no limit by default — with
-    // the pipelined in-LDS factorisation the late fronts' folds cost k_fact_tree less (163 -> 189 us)
-    // than the micro launch + gather pre-assembly they replace (~40 us and three launches): ex10
-    // 1547 -> 1593 iters/s (profiles/r3_p8b_*)
-    int slots = 0;
-    if (const char* e = std::getenv("MADIPM_FOLD_SLOTS")) slots = std::atoi(e);
-    std::vector<char> late(ns_all, 0);
     {
       // k_fact_tree's ticket order: by level (children before parents, so a workgroup waiting on its
       // children never blocks the tickets they need), and within a level by descending tail — the
       // estimated work from the front up to the root — so the fronts of the longest chains take the
-      // first CUs (MADIPM_TREE_PRIO=0: plain level order)
+      // first CUs.  Every tree front folds its micro leaves (r3: leaving the leaves of the fronts past
+      // the first 256 tickets to a micro launch + gather pre-assembly measured 1547 vs 1593 iters/s)
       std::vector<double> tail(ns_all, 0.0);
       for (int s = ns_all - 1; s >= 0; --s) {  // parents have larger indices (postorder)
         const double r = S.nrows[s], w = S.first[s + 1] - S.first[s];
         tail[s] = r * r + r * w + (S.parent[s] >= 0 ? tail[S.parent[s]] : 0.0);
       }
-      const char* pe = std::getenv("MADIPM_TREE_PRIO");
-      const int prio = pe ? std::atoi(pe) : 1;
       std::vector<int> ord;
       for (int lev = 0; lev < S.nlevels; ++lev) {
         const size_t o0 = ord.size();
         for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q)
           if (S.ftree[S.level_list[q]]) ord.push_back(S.level_list[q]);
-        if (prio == 1)
-          std::stable_sort(ord.begin() + o0, ord.end(), [&](int a, int b) { return tail[a] > tail[b]; });
+        std::stable_sort(ord.begin() + o0, ord.end(), [&](int a, int b) { return tail[a] > tail[b]; });
       }
-      // MADIPM_TREE_PRIO=2: one global order by descending tail (a child's tail exceeds its parent's,
-      // so this is topological): the longest chains' upper fronts take CUs before other chains' leaves
-      if (prio == 2)
-        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return tail[a] > tail[b]; });
       S.ft_order.assign(ord.begin(), ord.end());
-      if (slots > 0 && (int)ord.size() > slots) {
-        // every front past the first `slots` tickets leaves its leaves to the micro launch + gather: a
-        // late front's fold lies on the critical path (it starts when an earlier front retires), while
-        // the micro launch and the gather run before the tree on the whole GPU (ex10: tree span 210 ->
-        // 178 us; MADIPM_FOLD_LATE=cut restores the r2 rule: only the level cut by the slot count)
-        const char* la = std::getenv("MADIPM_FOLD_LATE");
-        const bool all = !(la && std::strcmp(la, "cut") == 0);
-        const int lcut = S.level[ord[slots]];
-        for (size_t q = slots; q < ord.size() && (all || S.level[ord[q]] == lcut); ++q) late[ord[q]] = 1;
-      }
     }
     for (int s = 0; s < ns_all; ++s) {
       S.mc_ptr[s + 1] = S.mc_ptr[s];
       S.fold_bptr[s + 1] = S.fold_bptr[s];
-      if (!on || !S.ftree[s] || late[s]) continue;
+      if (!on || !S.ftree[s]) continue;
       const int64_t r = S.nrows[s];
       int64_t nmc = 0, nrow = 0;
       bool ok = true;

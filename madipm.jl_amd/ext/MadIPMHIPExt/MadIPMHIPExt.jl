@@ -124,6 +124,7 @@ struct LdlOpts
     small_front_max::Int32
     pivot_tol::Float64
     nshards::Int32
+    cholesky::Int32      # ABI 0.2: Cholesky semantics (CHOLESKY with NormalKKTSystem, test/test_gpu.jl:11)
 end
 
 Base.@kwdef mutable struct HIPLDLOptions <: MadNLP.AbstractOptions
@@ -131,6 +132,7 @@ Base.@kwdef mutable struct HIPLDLOptions <: MadNLP.AbstractOptions
     relax::Int32 = 1
     small_front_max::Int32 = 128
     pivot_tol::Float64 = 0.0
+    cholesky::Bool = false         # MadNLPGPU's cudss_algorithm = CHOLESKY counterpart
 end
 
 mutable struct HIPLDLSolver{T} <: MadNLP.AbstractLinearSolver{T}
@@ -145,7 +147,7 @@ function HIPLDLSolver(csc::ROCSparseMatrixCSC{T,Int32}; opt=HIPLDLOptions(),
                       logger=MadNLP.MadNLPLogger()) where T
     colptr = Int64.(Array(csc.colPtr)) .- 1
     rowval = Int32.(Array(csc.rowVal)) .- Int32(1)
-    o = Ref(LdlOpts(opt.ordering, 10.0, opt.relax, opt.small_front_max, opt.pivot_tol, Int32(1)))
+    o = Ref(LdlOpts(opt.ordering, 10.0, opt.relax, opt.small_front_max, opt.pivot_tol, Int32(1), Int32(opt.cholesky)))
     h = Ref{Ptr{Cvoid}}(C_NULL)
     check(ccall((:madipm_ldl_analyze, libmadipm), Cint,
                 (Int32, Ptr{Int64}, Ptr{Int32}, Ref{LdlOpts}, Ptr{Int32}, Ref{Ptr{Cvoid}}),

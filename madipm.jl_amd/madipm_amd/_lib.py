@@ -29,7 +29,8 @@ vp = C.c_void_p
 
 class LDLOpts(C.Structure):
     _fields_ = [("ordering", C.c_int32), ("dense_alpha", C.c_double), ("relax", C.c_int32),
-                ("small_front_max", C.c_int32), ("pivot_tol", C.c_double), ("nshards", C.c_int32)]
+                ("small_front_max", C.c_int32), ("pivot_tol", C.c_double), ("nshards", C.c_int32),
+                ("cholesky", C.c_int32)]
 
 
 class LDLInfo(C.Structure):

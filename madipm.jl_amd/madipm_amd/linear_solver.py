@@ -18,16 +18,18 @@ class HIPLDLSolver:
     """Multifrontal supernodal LDL^T on the GPU (libmadipm_hip)."""
 
     def __init__(self, n, colptr, rowval, *, ordering=4, relax=1, pivot_tol=0.0, perm=None,
-                 small_front_max=128, nshards=1, shard=None):
+                 small_front_max=128, nshards=1, shard=None, cholesky=False):
         """nshards > 1 and shard None: all shards of a subtree-sharded factorisation on this device
         (SURVEY §8 e, local all-reduce).  shard = r: only shard r (one process per GPU); drive it with
-        factorize_phase / solve_phase and your own collective (or use MPCSolver(comm=...))."""
+        factorize_phase / solve_phase and your own collective (or use MPCSolver(comm=...)).
+        cholesky=True: Cholesky semantics (SPD; a pivot that is not > 0 fails — cuDSS CHOLESKY, the
+        reference's NormalKKTSystem pairing, test/test_gpu.jl:11)."""
         self.n = int(n)
         self._colptr = np.ascontiguousarray(colptr, np.int64)
         self._rowval = np.ascontiguousarray(rowval, np.int32)
         opts = L.default_ldl_opts(ordering=2 if perm is not None else ordering, relax=relax,
                                   pivot_tol=pivot_tol, small_front_max=small_front_max,
-                                  nshards=nshards if shard is None else 1)
+                                  nshards=nshards if shard is None else 1, cholesky=int(bool(cholesky)))
         up = None if perm is None else np.ascontiguousarray(perm, np.int32)
         upp = L.ptr(up, C.c_int32) if up is not None else None
         h = L.vp()

@@ -357,7 +357,24 @@ class OracleMPC:
                 dg = dg + zl * dist_u + zu * dist_l
                 K.setdiag(np.concatenate([dg, self.du_diag]))
                 K = K.tocsc()
-        if getattr(self, "linear_solver", "superlu") == "pardiso":
+        ls = getattr(self, "linear_solver", "superlu")
+        if not isinstance(ls, str):
+            # a linear-solver PLUGIN (the reference's `linear_solver = LS` seam, src/structure.jl:79-123):
+            # LS(aug_com) once per pattern (normalkkt.jl:113-115; the lower triangle in CSC), then
+            # MadNLP.factorize!(ls) with the values (linear_solver.jl:10 via factorize_wrapper!),
+            # MadIPM.is_factorized(ls) (utils.jl:54-62, linear_solver.jl:11) and, in kkt_solve,
+            # MadNLP.solve!(ls, x) (linear_solver.jl:26).  Tests plug the HIP library in here to run the
+            # reference-shaped loop around it (test/test_gpu.jl:9-19).
+            Lw = sp.tril(K).tocsc()
+            Lw.sort_indices()
+            pat = getattr(self, "_plugin_pattern", None)
+            if pat is None or not (np.array_equal(pat[0], Lw.indptr) and np.array_equal(pat[1], Lw.indices)):
+                self._plugin = ls(Lw)
+                self._plugin_pattern = (Lw.indptr.copy(), Lw.indices.copy())
+            self._plugin.factorize(Lw.data)
+            self._factorized = bool(self._plugin.is_factorized())
+            self._lu = self._plugin
+        elif ls == "pardiso":
             # CPU baseline (oracle/pardiso.py): MKL PARDISO, pattern analysed once per solver
             from .pardiso import PardisoLDL
             F = getattr(self, "_pardiso", None)
@@ -365,7 +382,7 @@ class OracleMPC:
                 F = self._pardiso = PardisoLDL(K, getattr(self, "ldl_perm", None))
             self._factorized = F.factorize(K)
             self._lu = F
-        elif getattr(self, "linear_solver", "superlu") == "ldl":
+        elif ls == "ldl":
             # oracle/ldl_ref.c: LDLFactorizations' up-looking LDL^T (static pivots) in the order
             # `ldl_perm` (default: SuperLU's minimum degree on A+A^T)
             from .ldl import OracleLDL

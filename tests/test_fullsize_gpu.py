@@ -1,6 +1,7 @@
-"""Parity at the BENCHMARKED sizes (BASELINE.json configs[1], [2], [3]).
+"""Parity at the BENCHMARKED sizes (BASELINE.json configs[1] .. [4]).
 
-* ex10 and supportcase10 stand-ins at full size, exactly as bench.py builds and solves them
+* ex10, supportcase10 and neos-5052403 stand-ins at full size (neos: nnz(L) = 1.1e8, 2.7e11 flops per
+  factorisation — PARDISO-sized; ~90 s of CPU on 8 threads), exactly as bench.py builds and solves them
   (presolve_qp -> scale_qp -> standard_form_qp; FixedRegularization(1e-8, -1e-8), AdaptiveStep(0.99),
   tol 1e-8): the GPU solve vs the oracle (oracle/mpc.py) driven by MKL PARDISO in the GPU's pivot
   order.  Status equal, iterations within 1, objective within 1e-6 max(1, |obj|) (BASELINE.md rule).
@@ -25,7 +26,7 @@ def _gpu_solve(qp, **extra):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("config", ["ex10", "supportcase10"])
+@pytest.mark.parametrize("config", ["ex10", "supportcase10", "neos"])
 def test_fullsize_vs_oracle(config):
     import bench
     from oracle.mpc import OracleMPC, OracleOptions
@@ -47,6 +48,29 @@ def test_fullsize_vs_oracle(config):
     # the returned primal points agree to the IPM's tolerance (both are 1e-8-optimal vertices/faces)
     dx = np.max(np.abs(gpu.solution - ref.solution)) / max(1.0, np.max(np.abs(ref.solution)))
     assert dx <= 1e-4, dx
+    if config == "neos":  # the optimality conditions of the returned point as well
+        p = _kkt_properties(qp, gpu)
+        assert p["pr"] <= 1e-6 and p["du"] <= 1e-6 and p["bounds"] <= 1e-8, p
+        assert abs(p["pobj"] - p["dobj"]) <= 1e-6 * max(1.0, abs(p["pobj"])), p
+
+
+@pytest.mark.timeout(900)
+def test_neos_fullsize_subtree_sharded():
+    """configs[4] is the config BASELINE.json assigns to the 8-GPU subtree split: the full-size neos
+    stand-in solved with the LDL^T cut into 8 shards (ShardGroup on this one device: every shard's
+    subtrees, the packed top-front exchange, the redundant top factorisation and the solution
+    all-gather, with a local all-reduce standing in for RCCL) follows the unsharded trajectory — same
+    status and iteration count, objective and solution within 1e-8."""
+    import bench
+    qp, _ = bench.build_problem("neos")
+    s1, g1 = _gpu_solve(qp)
+    s8, g8 = _gpu_solve(qp, nshards=8)
+    assert s8.ldl_info()["xch_fact"] > 0
+    assert g1.status_name == g8.status_name == "SOLVE_SUCCEEDED"
+    assert g1.iter == g8.iter, (g1.iter, g8.iter)
+    assert abs(g8.objective - g1.objective) <= 1e-8 * max(1.0, abs(g1.objective)), (g8.objective, g1.objective)
+    dx = np.max(np.abs(g8.solution - g1.solution)) / max(1.0, np.max(np.abs(g1.solution)))
+    assert dx <= 1e-8, dx
 
 
 def _kkt_properties(qp, st):

@@ -95,30 +95,15 @@ def test_ldl_tree_and_level_paths(tree_fact, tree_solve, well, monkeypatch):
     assert ls.inertia() == (4000, 0, 3000)
 
 
-@pytest.mark.parametrize("defer", ["0", "1"])
-@pytest.mark.parametrize("sfm", [128, 192])
-def test_ldl_schur_update_variants(defer, sfm, monkeypatch):
-    """In-LDS factorisation with the update block's Schur complement formed once after all pivots
-    (MADIPM_SCHUR_DEFER=1, default) or at every 16-pivot step (0): the oracle's pivots to 1e-12
-    (well conditioned), square (<= 128 rows) and packed (<= 192 rows) LDS storage."""
-    monkeypatch.setenv("MADIPM_SCHUR_DEFER", defer)
-    K, Lw = block_angular_k2(3000, 4000, 20, 7, well=True)
-    ls = _check_case(K, Lw, small_front_max=sfm, well=True)
-    assert ls.inertia() == (4000, 0, 3000)
-
-
-@pytest.mark.parametrize("f16r", ["0", "1", "2"])
 @pytest.mark.parametrize("sfm", [128, 192])
 @pytest.mark.parametrize("well", [True, False])
-def test_ldl_diag_block_variants(f16r, sfm, well, monkeypatch):
-    """The 16-pivot diagonal blocks of the in-LDS factorisation factorised in registers (factor16r:
-    DPP row broadcasts + gfx950 permlane swaps; l = a * (1/d) with a Newton-refined v_rcp_f64,
-    MADIPM_F16R=2, default, or the IEEE quotient a / d, 1) or through an LDS hand-off per pivot
-    (factor16s, 0): the oracle's pivots to 1e-12 (well conditioned) and its solution; the variants
-    round differently (mirrored Schur paths, reciprocal vs quotient), so they agree to rounding.
-    The block-angular K2 has fronts of 16 .. 150 columns (several diagonal blocks each) and a
+def test_ldl_in_lds_fronts(sfm, well):
+    """The in-LDS factorisation (16-pivot diagonal blocks factorised in registers — DPP row broadcasts
+    + gfx950 permlane swaps, l = a * (1/d) with a Newton-refined v_rcp_f64 — panel and trailing update
+    on f64 MFMA, the update block's Schur complement formed once after all pivots): the oracle's pivots
+    to 1e-12 (well conditioned) and its solution, square (<= 128 rows) and packed (<= 192 rows)
+    storage.  The block-angular K2 has fronts of 16 .. 150 columns (several diagonal blocks each) and a
     120-column root (k_small_blocked); the QP case a dense front."""
-    monkeypatch.setenv("MADIPM_F16R", f16r)
     K, Lw = block_angular_k2(3000, 4000, 20, 7, well=well)
     ls = _check_case(K, Lw, small_front_max=sfm, well=well)
     assert ls.inertia() == (4000, 0, 3000)
@@ -139,19 +124,15 @@ def _factor_solve(K, Lw, sfm, seed=0):
     return ls.diag().copy(), x.cpu().numpy(), ls
 
 
-@pytest.mark.parametrize("f16r", ["1", "2"])
-@pytest.mark.parametrize("defer", ["0", "1"])
 @pytest.mark.parametrize("sfm", [128, 192])
 @pytest.mark.parametrize("case", ["block_well", "block_ipm", "dense_front", "random"])
-def test_ldl_fact_pipe_bitwise(case, sfm, defer, f16r, monkeypatch):
+def test_ldl_fact_pipe_bitwise(case, sfm, monkeypatch):
     """The pipelined in-LDS schedule (blocked_factor_pipe: wave 0 runs the pivot chain, the other
     waves the panel and trailing update, LDS-counter hand-offs; MADIPM_FACT_PIPE=1, default) forms
     every tile with the same MFMA sequence from the same operands as the barrier schedule
     (blocked_factor_lds, MADIPM_FACT_PIPE=0): pivots and solution agree BITWISE, on k_fact_tree
     (8 waves) and k_small_blocked (4 waves; the 120-column root, dense fronts of 1-12 pivot blocks,
-    square and packed storage, deferred and per-step Schur updates) — and the oracle's to 1e-12."""
-    monkeypatch.setenv("MADIPM_SCHUR_DEFER", defer)
-    monkeypatch.setenv("MADIPM_F16R", f16r)
+    square and packed storage) — and the oracle's to 1e-12."""
     if case.startswith("block"):
         K, Lw = block_angular_k2(3000, 4000, 20, 7, well=case == "block_well")
     elif case == "dense_front":
@@ -168,6 +149,20 @@ def test_ldl_fact_pipe_bitwise(case, sfm, defer, f16r, monkeypatch):
     assert np.array_equal(x0.view(np.uint64), x1.view(np.uint64))
     if case != "block_ipm":
         _check_case(K, Lw, small_front_max=sfm, well=True)
+
+
+def test_ldl_pipe_lost_handoff_is_an_error(monkeypatch):
+    """A hand-off of the pipelined in-LDS schedule that never arrives (MADIPM_DEBUG_PIPE_FAULT=1 drops
+    the first M_K publication of every front) must not yield a silently wrong factor: the waits time
+    out, the front raises the status block's sticky error and factorize() fails loudly."""
+    from madipm_amd.linear_solver import HIPLDLSolver
+    monkeypatch.setenv("MADIPM_DEBUG_PIPE_FAULT", "1")
+    K, Lw = _dense_k2(150, 1000, 5)
+    ls = HIPLDLSolver(K.shape[0], Lw.indptr, Lw.indices, small_front_max=192)
+    with pytest.raises(Exception, match="hand-off"):
+        ls.factorize(torch.from_numpy(Lw.data.copy()).cuda())
+    monkeypatch.setenv("MADIPM_DEBUG_PIPE_FAULT", "0")
+    _factor_solve(K, Lw, 192)  # a fresh solver factorises normally
 
 
 @pytest.mark.parametrize("case", ["block_well", "block_ipm", "random"])
@@ -188,16 +183,14 @@ def test_root_backward_in_forward_bitwise(case, monkeypatch):
     _check_case(K, Lw, well=case != "block_ipm")
 
 
-@pytest.mark.parametrize("pipe", ["1", "2"])
 @pytest.mark.parametrize("kpan", ["1", "2", "4"])
 @pytest.mark.parametrize("n,m", [(320, 100), (130, 200)])
-def test_big_front_panel_groups(kpan, n, m, pipe, monkeypatch):
+def test_big_front_panel_groups(kpan, n, m, monkeypatch):
     """A dense K2 (dense SPD H, dense A: one big front of n + m columns, several 64-column panels
     with a partial last one) on the big-front path with the deferred multi-panel trailing update in
     groups of MADIPM_BIG_KPAN panels (1 = right-looking per panel): pivots and solution of the oracle."""
     import scipy.sparse as sp
     monkeypatch.setenv("MADIPM_BIG_KPAN", kpan)
-    monkeypatch.setenv("MADIPM_FACT_PIPE", pipe)  # k_big_diag's 64 x 64 tile: barrier (1) or pipelined (2) schedule
     rng = np.random.default_rng(11)
     B = rng.standard_normal((n, n))
     H = B @ B.T / n + np.eye(n)

@@ -176,3 +176,28 @@ def test_maximize_sign_flip():
     gmin = MPCSolver(_qp(name="min", **kw), regularization=FixedRegularization(1e-8, -1e-8)).solve()
     assert abs(gmin.objective + gpu.objective) <= 1e-7
     assert np.allclose(gmin.solution, gpu.solution, atol=1e-6)
+
+
+def test_max_wall_time_stop():
+    """MAXIMUM_WALLTIME_EXCEEDED (src/solver.jl:216-217: `elapsed_time(solver) >= max_wall_time`, tested
+    after the optimality / infeasibility / divergence / max_iter rules): with max_wall_time = 0 the
+    first termination test stops at the starting point — the oracle's starting point, objective to
+    1e-9; with a budget below the full solve's loop time the solve stops early, after at least that
+    budget, with the status and an iterate that is not optimal yet."""
+    from madipm_amd import MPCSolver, FixedRegularization, MAXIMUM_WALLTIME_EXCEEDED, SOLVE_SUCCEEDED
+    from madipm_amd.instances import random_lp
+    qp = random_lp(300, 700, 0.02, 5)
+    reg = FixedRegularization(1e-8, -1e-8)
+    gpu = MPCSolver(qp, regularization=reg, max_iter=300, max_wall_time=0.0).solve()
+    ref = OracleMPC(qp, OracleOptions(regularization=("fixed", 1e-8, -1e-8), max_iter=300, max_wall_time=0.0)).solve()
+    assert gpu.status == MAXIMUM_WALLTIME_EXCEEDED == ref.status
+    assert gpu.iter == ref.iter == 0
+    assert abs(gpu.objective - ref.objective) <= 1e-9 * max(1.0, abs(ref.objective))
+    s = MPCSolver(qp, regularization=reg, max_iter=300)
+    full = s.solve()
+    assert full.status == SOLVE_SUCCEEDED and full.iter >= 6
+    budget = 0.4 * full.counters.total_time
+    part = MPCSolver(qp, regularization=reg, max_iter=300, max_wall_time=budget).solve()
+    assert part.status == MAXIMUM_WALLTIME_EXCEEDED
+    assert 0 < part.iter < full.iter
+    assert part.counters.total_time >= budget

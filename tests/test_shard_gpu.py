@@ -124,11 +124,18 @@ def test_phase_protocol_with_separate_shards():
     bufs = [s.solve_phase(2, x) for s, x in zip(sh, xs)]
     assert bufs[0][1] == sh[0].info()["xch_gather"]
     local_allreduce([p for p, _ in bufs], bufs[0][1])  # the all-gather (other slices are zero)
+    # ABI 0.2 protocol guard: a 0.1-style caller (phase 2, then no phase 3) is refused at its next call
+    with pytest.raises(Exception, match="phase 3"):
+        sh[0].solve_phase(1, xs[0])
+    with pytest.raises(Exception, match="pending"):
+        sh[0].solve(xs[0])
     for s, x in zip(sh, xs):
         assert s.solve_phase(3, x) == (None, 0)
     torch.cuda.synchronize()
     for x in xs:
         assert np.max(np.abs(x.cpu().numpy() - x0)) <= 1e-12 * np.max(np.abs(x0))
+    with pytest.raises(Exception, match="phase 1 expected"):
+        sh[0].solve_phase(2, xs[0])
 
 
 def test_sharded_pivot_failure_reaches_every_shard():

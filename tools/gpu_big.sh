@@ -10,7 +10,7 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 for C in $CFGS; do
   S=8; [ "$C" = dense_qp ] && S=2
-  timeout -k 10 500 python bench.py --config $C --steps $S --warmup 1 --no-cpu --no-opt > $OUT/${C}_bench.log 2>&1 && echo "$C bench ok" || { echo "$C bench FAILED"; tail -20 $OUT/${C}_bench.log; exit 1; }
+  timeout -k 10 500 python bench.py --config $C --steps $S --warmup 1 --no-cpu > $OUT/${C}_bench.log 2>&1 && echo "$C bench ok" || { echo "$C bench FAILED"; tail -20 $OUT/${C}_bench.log; exit 1; }
   tail -1 $OUT/${C}_bench.log | cut -c1-600
   timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$C -o run -- python3 bench.py --config $C --steps 2 --warmup 1 --no-cpu --no-opt > $OUT/prof_$C.log 2>&1 && echo "$C rocprof ok" || { echo "$C rocprof FAILED"; tail -20 $OUT/prof_$C.log; exit 1; }
   python tools/prof_summary.py $OUT/prof_$C > $OUT/${C}_prof_summary.txt 2>&1 || true
