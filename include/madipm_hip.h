@@ -69,6 +69,9 @@ typedef struct madipm_ldl_info {
                               sides); 0 unsharded */
   int64_t xch_gather;      /* sharded: doubles of the per-solve in-place all-gather of the shards'
                               subtree solution slices (nshards slices); 0 unsharded */
+  int32_t tree_fronts;     /* fronts factorised by the dependency-driven tree launch (k_fact_tree) [ABI 0.2] */
+  int32_t tree_medium;     /* of which medium fronts (192 < r <= 256: factorised in HBM, one 64-column
+                              panel in LDS at a time) [ABI 0.2] */
 } madipm_ldl_info;
 
 void madipm_ldl_default_opts(madipm_ldl_opts* opts);

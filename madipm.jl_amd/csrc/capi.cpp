@@ -172,6 +172,12 @@ static void fill_info(const SymbolicPlan& p, const LinSolver* ls, madipm_ldl_inf
   info->xch_fact = ls ? ls->xch_fact() : 0;
   info->xch_solve = ls ? ls->xch_solve() : 0;
   info->xch_gather = ls ? ls->xch_gather() : 0;
+  info->tree_fronts = info->tree_medium = 0;
+  for (int s = 0; s < (int)p.ftree.size(); ++s)
+    if (p.ftree[s]) {
+      ++info->tree_fronts;
+      info->tree_medium += p.nrows[s] > SymbolicPlan::kFactTreeMax;
+    }
 }
 
 int madipm_symbolic_info(madipm_symbolic_t sym, madipm_ldl_info* info) {

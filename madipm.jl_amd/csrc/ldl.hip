@@ -1181,6 +1181,9 @@ __device__ __forceinline__ void blocked_factor_pipe(double* A, int r, int w, int
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), nw = blockDim.x >> 6;
   const int no = nw - 1;  // waves 1 .. nw - 1: panel rest + trailing update
   const int nblk = (w + 15) >> 4;
+  // defer 2: the caller forms the update block's Schur complement itself (the medium fronts' panels,
+  // whose trailing matrix lives in HBM): rows below the pivots get their L only
+  const bool schur = defer == 1;
   defer = defer && w < r;
   const int jend = defer ? w : r;
   PipeCtr& pc = pipe_ctr();
@@ -1277,7 +1280,7 @@ __device__ __forceinline__ void blocked_factor_pipe(double* A, int r, int w, int
   if (tid == 0 && __hip_atomic_load(&pc.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) && err)
     __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int64_t t2 = (pt && tid == 0) ? wall_clock64() : 0;
-  if (defer) {
+  if (defer && schur) {
     schur_strips<PK>(A, r, ld, w, Dl, wv, nw, lane);
     __syncthreads();
   }
@@ -1844,6 +1847,151 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
   }
 }
 
+// ---- Medium tree fronts (kFactTreeMax < r <= kFactTreeMedMax): the front F (r x r, ld r, big-front
+// storage: L = F[:, :w], U = F[w:, w:] in place) stays in HBM — pre-assembled there by the gather pass
+// (original entries + pre-leaf children) — and ONE workgroup factorises it panel by panel, right-looking:
+//   children: the tree children's update blocks are added into F (read-modify-write, child order);
+//   panel k (columns c0 .. c0 + pw, pw <= 64): rows c0 .. r staged into LDS as an (r - c0) x pw front,
+//     factorised by the in-LDS schedule without its Schur pass (blocked_factor_pipe, defer 2), written
+//     back (L, d on the diagonal, D, pivot check);
+//   trailing update in HBM: F[i, j] -= sum_t L(i, t) d_t L(j, t) over the panel's columns, i >= j >= c0 + pw,
+//     16 x 16 tiles on f64 MFMA with both operands from the LDS panel (tile rows along the lanes:
+//     16 consecutive rows of one column per store, coalesced); the last panel's tiles are the update
+//     block U, stored write-through (sc1) for the parent, then the flag.
+// (The level path ran each 64-column panel of these fronts as three launches, k_big_diag -> k_big_trsm
+// -> k_big_update, per level: ~37 us per panel plus the launch gaps, supportcase10's fronts r ~ 230.)
+constexpr int MED_PW = 64;
+__device__ __forceinline__ void med_trailing(double* __restrict__ F, int r, int c0, int pw, const double* A, int ld,
+                                             const double* Dl, bool last) {
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
+  const int rp = r - c0;                // panel rows (LDS row i' = front row c0 + i')
+  const int nb = (rp - pw + 15) >> 4;   // 16-row blocks of the trailing matrix
+  const int ntile = nb * (nb + 1) / 2;
+  const int nks = (pw + 3) >> 2;
+  const int kl = lane >> 4, il = lane & 15;
+  for (int t = wv; t < ntile; t += nw) {
+    // tile t -> (I, J), J <= I, row-major over the lower triangle
+    int I = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
+    while ((I + 1) * (I + 2) / 2 <= t) ++I;
+    while (I * (I + 1) / 2 > t) --I;
+    const int J = t - I * (I + 1) / 2;
+    const int i0 = pw + 16 * I, j0 = pw + 16 * J;  // LDS rows of the tile's rows (i) and columns (j)
+    // C prefetch: lane (n = il -> row i0 + il, m = kl + 4 g -> column j0 + kl + 4 g), clamped in range
+    const int ic = min(i0 + il, rp - 1);
+    double c[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int jc = min(j0 + kl + 4 * g, rp - 1);
+      c[g] = F[(int64_t)(c0 + ic) + (int64_t)(c0 + jc) * r];
+    }
+    dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+    const int ja = min(j0 + il, rp - 1), ib = min(i0 + il, rp - 1);
+    for (int ks = 0; ks < nks; ++ks) {
+      const int k = 4 * ks + kl;
+      const int kc = min(k, pw - 1);
+      const double d = (k < pw) ? Dl[kc] : 0.0;
+      const double av = A[ja + kc * ld] * d;   // A operand: (m = il -> column j0 + il, k)
+      const double bv = A[ib + kc * ld];       // B operand: (k, n = il -> row i0 + il)
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+    }
+    // result lane l, element g: (m = kl + 4 g -> column j0 + m, n = il -> row i0 + il)
+    const int i = i0 + il;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int j = j0 + kl + 4 * g;
+      if (i < rp && j < rp && i >= j) {
+        double* q = F + (int64_t)(c0 + i) + (int64_t)(c0 + j) * r;
+        const double v = c[g] - acc[g];
+        if (last)
+          __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+          *q = v;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void fact_med_front(const FrontTab& T, int s, const int32_t* __restrict__ dep, int q0, int q1,
+                                               int32_t* flags, int epoch, double* arena, double* D, LDLStatus* st,
+                                               double tol, int32_t* err, double* A, double* Dl, double* MK, double* cbuf) {
+  const int tid = threadIdx.x;
+  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+  double* __restrict__ F = arena + T.l_off[s];
+  if (tid < 64) poll_deps(dep, q0, q1, flags, epoch, err);
+  __syncthreads();
+  // tree children's update blocks (agent-scope loads: written by other workgroups), child order
+  for (int q = q0; q < q1; ++q) {
+    const int c = dep[q];
+    const int uc = T.nrows[c] - (T.first[c + 1] - T.first[c]);
+    const int64_t uld = T.u_ld[c];
+    const double* U = arena + T.u_off[c];
+    const int32_t* __restrict__ rl = T.rel + T.rel_ptr[c];
+    const int ne = uc * uc;
+    for (int base = 0; base < ne; base += FTN * 8) {
+      double x[8];
+      int64_t dst[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int e = min(base + k * FTN + tid, ne - 1);
+        const int b = e / uc, a = e - b * uc;
+        const bool ok = base + k * FTN + tid < ne && a >= b;
+        x[k] = __hip_atomic_load(U + a + (int64_t)b * uld, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        dst[k] = ok ? (int64_t)rl[a] + (int64_t)rl[b] * r : -1;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (dst[k] >= 0) F[dst[k]] += x[k];
+    }
+    __syncthreads();
+  }
+  for (int c0 = 0; c0 < w; c0 += MED_PW) {
+    const int pw = min(MED_PW, w - c0), rp = r - c0, ld = rp | 1;
+    const bool last = c0 + pw >= w;
+    // stage rows c0 .. r of the panel's columns (lower part) into LDS, 16 loads in flight per thread
+    const int ne = rp * pw;
+    for (int base = 0; base < ne; base += FTN * 16) {
+      double v[16];
+      int dst[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int e = base + k * FTN + tid;
+        const int ec = min(e, ne - 1);
+        const int j = ec / rp, i = ec - j * rp;
+        v[k] = F[(int64_t)(c0 + i) + (int64_t)(c0 + j) * r];
+        dst[k] = (e < ne && i >= j) ? i + j * ld : -1;
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (dst[k] >= 0) A[dst[k]] = v[k];
+    }
+    __syncthreads();
+    blocked_factor_pipe<false>(A, rp, pw, ld, Dl, MK, cbuf, 2, nullptr, T.err, 0);
+    __syncthreads();
+    // write back: L (d on the diagonal), D + pivot check
+    for (int base = 0; base < ne; base += FTN * 8) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int e = base + k * FTN + tid;
+        if (e < ne) {
+          const int j = e / rp, i = e - j * rp;
+          if (i >= j) F[(int64_t)(c0 + i) + (int64_t)(c0 + j) * r] = (i == j) ? Dl[j] : A[i + j * ld];
+        }
+      }
+    }
+    if (tid < pw) {
+      const double d = Dl[tid];
+      D[f0 + c0 + tid] = d;
+      if (bad_pivot(d, tol)) atomicMin(&st->fail_pivot, f0 + c0 + tid + 1);
+    }
+    if (rp > pw) med_trailing(F, r, c0, pw, A, ld, Dl, last);
+    __syncthreads();  // the next panel's staging reads the updated trailing matrix; A is rewritten
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store(&flags[s], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ __launch_bounds__(FTN) void k_fact_tree(FrontTab T, const int32_t* __restrict__ order, int nt,
                                                   const int32_t* __restrict__ dep_ptr, const int32_t* __restrict__ dep,
                                                   int32_t* counter, int32_t* flags, int epoch,
@@ -1863,7 +2011,9 @@ __global__ __launch_bounds__(FTN) void k_fact_tree(FrontTab T, const int32_t* __
   const int s = order[t];
   int64_t* dg = dbg ? dbg + 24 * t : nullptr;
   if (dg && threadIdx.x == 0) dg[0] = wall_clock64();
-  if (T.nrows[s] <= 128 && !T.fold_pk[s])
+  if (T.nrows[s] > SymbolicPlan::kFactTreeMax)
+    fact_med_front(T, s, dep, dep_ptr[t], dep_ptr[t + 1], flags, epoch, arena, D, st, tol, err, A, Dl, MK, cbuf);
+  else if (T.nrows[s] <= 128 && !T.fold_pk[s])
     fact_tree_front<false>(T, s, dep, dep_ptr[t], dep_ptr[t + 1], flags, epoch, Kx, arena, fscratch, D, st, tol, err, A, Dl,
                            MK, cbuf, rels, dg);
   else
@@ -3037,81 +3187,191 @@ __device__ __forceinline__ void bwd_subst_t(double (&v)[3], const double* LT, in
   }
 }
 
-// Folded micro leaves of a chain task (w <= 2, r <= 32, no children; their parents are fronts of the
-// chain), one thread per leaf, every load of a leaf issued before its arithmetic.
-// Forward (k_fwd_micro's arithmetic): x0 = b0, x1 = b1 - l10 x0 to xi; the update entries
-// (0 - l_a0 x0) - l_a1 x1 to the parent's gather range (gbuf), read back by the chain's fronts.
-__device__ __forceinline__ void fwd_leaves(const SolveLeaf* __restrict__ lv, int n0, int n1, const int2* __restrict__ lrow,
-                                           const double* __restrict__ arena, const double* __restrict__ b,
-                                           double* __restrict__ xi, double* __restrict__ gbuf) {
-  for (int k = n0 + (int)threadIdx.x; k < n1; k += NT) {
-    const SolveLeaf L = lv[k];
-    const int r = L.rw & 255, w = L.rw >> 8, u = r - w;
-    const double* __restrict__ P = arena + L.loff;
-    const double b0 = b[L.p0];
-    const double b1 = (w == 2) ? b[L.p1] : 0.0, l10 = (w == 2) ? P[1] : 0.0;
-    const double x0 = b0, x1 = (w == 2) ? b1 - l10 * x0 : 0.0;
-    xi[L.f0] = x0;
-    if (w == 2) xi[L.f0 + 1] = x1;
-    for (int a0 = 0; a0 < u; a0 += 8) {
-      double p[8], q[8];
-      int d[8];
+// ---- Medium tree fronts in the tree solves (SMALL_SOLVE_MAX < r <= kFactTreeMedMax): the L panel
+// (r x w, up to 256 x 256) does not fit LDS, so it is streamed in column chunks, double-buffered: wave 0
+// substitutes chunk c while waves 1..3 stage chunk c +- 1.  v (forward) / x (backward) stay in wave 0's
+// registers, 4 rows per lane.
+constexpr int MED_SOLVE_MAX = SymbolicPlan::kFactTreeMedMax;
+constexpr int MCW = 32, MLDT = MCW + 2;           // forward chunk: pivot columns, row-major ld
+constexpr int MFBUF = MED_SOLVE_MAX * MLDT;       // doubles per forward chunk buffer
+constexpr int MLDC = MED_SOLVE_MAX + 2;           // backward chunk: col-major ld
+constexpr int MBBUF = MCW * MLDC;                 // doubles per backward chunk buffer
+constexpr int MED_FWD_LDS = 2 * MFBUF, MED_BWD_LDS = 2 * MBBUF + 2 * MED_SOLVE_MAX;  // doubles
+
+// rows [ra, r) x columns [c0, c0 + MCW) of L (ld r) -> LT[(i - ra) MLDT + (t - c0)] = L(i, t) for
+// t < w and i > t, else 0; threads lt = 0 .. nthr - 1 of the caller's group
+__device__ __forceinline__ void stage_fwd_chunk(const double* __restrict__ L, double* LT, int r, int w, int ra, int c0,
+                                                int lt, int nthr) {
+  const int nrow = r - ra, nel = nrow * MCW;
+  ColWalk wk(lt, nrow, nthr);
+  for (int base = 0; base < nel; base += nthr * 8) {
+    double v[8];
+    int dst[8];
+    bool ok[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int a = min(a0 + j, u - 1);
-        p[j] = P[w + a];
-        q[j] = (w == 2) ? P[w + a + r] : 0.0;
-        d[j] = lrow[L.roff + a].x;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (a0 + j < u) gbuf[d[j]] = (0.0 - p[j] * x0) - q[j] * x1;
+    for (int k = 0; k < 8; ++k) {
+      const int q = base + k * nthr + lt, i = ra + wk.i, t = c0 + wk.j;
+      ok[k] = t < w && i > t;
+      v[k] = L[min(i, r - 1) + (int64_t)min(t, w - 1) * r];  // clamped, in range: masked below
+      dst[k] = q < nel ? wk.i * MLDT + wk.j : -1;
+      wk.next();
     }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (dst[k] >= 0) LT[dst[k]] = ok[k] ? v[k] : 0.0;
   }
 }
 
-// Backward (k_bwd_micro's arithmetic, rows summed in order): the rows' final x (ancestors: the chain's
-// fronts, stored earlier by this workgroup -> sc1 loads) -> x of the two pivots, to xi and the caller's b.
-__device__ __forceinline__ void bwd_leaves(const SolveLeaf* __restrict__ lv, int n0, int n1, const int2* __restrict__ lrow,
-                                           const double* __restrict__ arena, const double* __restrict__ D,
-                                           double* __restrict__ xi, double* __restrict__ out) {
-  for (int k = n0 + (int)threadIdx.x; k < n1; k += NT) {
-    const SolveLeaf L = lv[k];
-    const int r = L.rw & 255, w = L.rw >> 8, u = r - w;
-    const double* __restrict__ P = arena + L.loff;
-    double a0 = 0.0, a1 = 0.0;
-    for (int c0 = 0; c0 < u; c0 += 8) {
-      int src[8];
+template <int HB>
+__device__ __forceinline__ void fwd_block_m(double (&v)[4], const double* LT, int r, int ra, int tc, int t0, int lane) {
+  double lb[4][16];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) src[j] = lrow[L.roff + min(c0 + j, u - 1)].y;
-      double p[8], q[8], x[8];
+  for (int h = HB; h < 4; ++h) {
+    const double2* rp = reinterpret_cast<const double2*>(LT + (min(lane + 64 * h, r - 1) - ra) * MLDT + tc);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int a = min(c0 + j, u - 1);
-        p[j] = P[w + a];
-        q[j] = (w == 2) ? P[w + a + r] : 0.0;
-        x[j] = ld_sc1(xi + src[j]);
-      }
+    for (int m = 0; m < 8; ++m) {
+      const double2 q = rp[m];
+      lb[h][2 * m] = q.x;
+      lb[h][2 * m + 1] = q.y;
+    }
+  }
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (c0 + j < u) {
-          a0 = fma(p[j], x[j], a0);
-          a1 = fma(q[j], x[j], a1);
+  for (int k = 0; k < 16; ++k) {
+    const double xt = readlane_f64(v[HB], (t0 & 63) + k);
+#pragma unroll
+    for (int h = HB; h < 4; ++h) v[h] = fma(-lb[h][k], xt, v[h]);
+  }
+}
+
+// column chunk [c0, c0 + MCW) of L (ld r), rows [c0, r) -> LC[(j - c0) MLDC + (t - c0)] = L(t, j) for
+// j < w and t > j, else 0
+__device__ __forceinline__ void stage_bwd_chunk(const double* __restrict__ L, double* LC, int r, int w, int c0, int lt,
+                                                int nthr) {
+  const int nrow = r - c0, nel = nrow * MCW;
+  ColWalk wk(lt, nrow, nthr);
+  for (int base = 0; base < nel; base += nthr * 8) {
+    double v[8];
+    int dst[8];
+    bool ok[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int q = base + k * nthr + lt, t = c0 + wk.i, j = c0 + wk.j;
+      ok[k] = j < w && t > j;
+      v[k] = L[min(t, r - 1) + (int64_t)min(j, w - 1) * r];
+      dst[k] = q < nel ? wk.j * MLDC + wk.i : -1;
+      wk.next();
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (dst[k] >= 0) LC[dst[k]] = ok[k] ? v[k] : 0.0;
+  }
+}
+
+// forward solve of a medium tree front (all NT threads; v0: the gathered initial values of its rows)
+__device__ __forceinline__ void fwd_med_front(const FrontTab& T, int s, const double* __restrict__ arena, double* Ls,
+                                              const double* v0, double* xi, double* uvec, int32_t* tflags, int epoch) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+  const double* __restrict__ L = arena + T.l_off[s];
+  const int nch = (((w + 15) & ~15) + MCW - 1) / MCW;
+  double* buf[2] = {Ls, Ls + MFBUF};
+  stage_fwd_chunk(L, buf[0], r, w, 0, 0, tid, NT);
+  double v[4];
+  double* dst[4];
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    const int i = lane + 64 * h;
+    v[h] = (i < r) ? v0[i] : 0.0;
+    dst[h] = (wv == 0 && i >= w && i < r) ? uvec_dst(T, s, i - w, uvec) : xi + f0 + min(i, w - 1);
+  }
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    const int c0 = c * MCW;
+    if (wv == 0) {
+      const int ra = (c0 >> 6) << 6;
+      const double* LT = buf[c & 1];
+      const int tend = min(c0 + MCW, (w + 15) & ~15);
+      for (int t0 = c0; t0 < tend; t0 += 16) {
+        const int tc = t0 - c0;
+        switch (t0 >> 6) {
+          case 0: fwd_block_m<0>(v, LT, r, ra, tc, t0, lane); break;
+          case 1: fwd_block_m<1>(v, LT, r, ra, tc, t0, lane); break;
+          case 2: fwd_block_m<2>(v, LT, r, ra, tc, t0, lane); break;
+          default: fwd_block_m<3>(v, LT, r, ra, tc, t0, lane); break;
         }
+      }
+    } else if (c + 1 < nch) {
+      const int c1 = c0 + MCW;
+      stage_fwd_chunk(L, buf[(c + 1) & 1], r, w, (c1 >> 6) << 6, c1, tid - 64, NT - 64);
     }
-    const double l10 = (w == 2) ? P[1] : 0.0;
-    const double v1 = (w == 2) ? xi[L.f0 + 1] / D[L.f0 + 1] - a1 : 0.0;
-    const double v0 = xi[L.f0] / D[L.f0] - a0 - l10 * v1;
-    xi[L.f0] = v0;
-    out[L.p0] = v0;
-    if (w == 2) {
-      xi[L.f0 + 1] = v1;
-      out[L.p1] = v1;
-    }
+    __syncthreads();
   }
+  if (wv == 0) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+      if (lane + 64 * h < r) st_sc1(dst[h], v[h]);
+    publish_sc1(&tflags[s], epoch);
+  }
+  __syncthreads();
 }
 
-// The same leaves as flat launches (MADIPM_SOLVE_FOLD=1, default): LPL lanes per leaf, each lane forms
+// backward solve of a medium tree front (all NT threads): chunks from the last to the first; xall holds
+// the final x of every row below the current chunk (the ancestors' rows, then this front's later pivots)
+__device__ __forceinline__ void bwd_med_front(const FrontTab& T, int s, const double* __restrict__ arena,
+                                              const double* __restrict__ D, double* Ls, double* xi, double* out,
+                                              const int32_t* __restrict__ pdep, int t, int32_t* tflags, int epoch,
+                                              int32_t* err) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s], nb = r - w;
+  const double* __restrict__ L = arena + T.l_off[s];
+  double* buf[2] = {Ls, Ls + MBBUF};
+  double* xall = Ls + 2 * MBBUF;            // r doubles
+  double* ownv = xall + MED_SOLVE_MAX;      // w doubles: the forward values / d
+  const int nch = (w + MCW - 1) / MCW;
+  // symbolic / previous-launch data before the wait: the rows below, the own values, the last chunk
+  const int rk = (tid < nb) ? T.rows[T.row_ptr[s] + w + tid] : 0;
+  if (tid < w) ownv[tid] = xi[f0 + tid] / D[f0 + tid];
+  stage_bwd_chunk(L, buf[(nch - 1) & 1], r, w, (nch - 1) * MCW, tid, NT);
+  if (tid < 64 && pdep[t] >= 0) poll_deps(pdep, t, t + 1, tflags, epoch, err);
+  __syncthreads();
+  if (tid < nb) xall[w + tid] = ld_sc1(xi + rk);
+  __syncthreads();
+  const bool wo = T.wout[s];
+  const int jl = lane & 31, half = lane >> 5;
+  for (int c = nch - 1; c >= 0; --c) {
+    const int c0 = c * MCW, c1 = min(c0 + MCW, w), j = c0 + jl;
+    if (wv == 0) {
+      const double* LC = buf[c & 1] + jl * MLDC;
+      // rows below the chunk (two half-waves: even / odd rows), then the chunk's own triangle
+      double a0 = 0.0, a1 = 0.0;
+      int q = c1 + half;
+      for (; q + 2 < r; q += 4) {
+        a0 = fma(LC[q - c0], xall[q], a0);
+        a1 = fma(LC[q + 2 - c0], xall[q + 2], a1);
+      }
+      for (; q < r; q += 2) a0 = fma(LC[q - c0], xall[q], a0);
+      double acc = a0 + a1;
+      acc = (half == 0) ? acc + __shfl_xor(acc, 32, 64) : __shfl_xor(acc, 32, 64) + acc;
+      double x = (j < w) ? ownv[min(j, w - 1)] - acc : 0.0;
+      for (int tt = c1 - 1; tt > c0; --tt) {  // x_j -= L(tt, j) x_tt, j < tt
+        const double xt = readlane_f64(x, tt - c0);
+        x = fma(-LC[tt - c0], xt, x);
+      }
+      if (half == 0 && j < w) {
+        xall[j] = x;
+        st_sc1(xi + f0 + j, x);
+        if (wo) out[T.perm[f0 + j]] = x;
+      }
+    } else if (c > 0) {
+      stage_bwd_chunk(L, buf[(c - 1) & 1], r, w, (c - 1) * MCW, tid - 64, NT - 64);
+    }
+    __syncthreads();
+  }
+  if (tid < 64) publish_sc1(&tflags[s], epoch);
+  __syncthreads();
+}
+
+// The micro leaves under tree fronts as flat launches: LPL lanes per leaf, each lane forms
 // x0, x1 itself (the same loads) and takes rows a = j, j + LPL, ...; the leaf record carries every
 // index, so a lane's loads are one dependent level deep (record -> b, L, row table).  Forward before
 // k_fwd_tree (it gathers the update entries from gbuf), backward after k_bwd_tree (final ancestors).
@@ -3212,11 +3472,9 @@ __global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __re
                                                  int32_t* counter, int32_t* tflags, int epoch, int lds_doubles,
                                                  const double* __restrict__ arena, const double* __restrict__ b,
                                                  double* xi, double* uvec, int32_t* err, int64_t* dbg,
-                                                 const int32_t* __restrict__ lptr, const SolveLeaf* __restrict__ leaves,
-                                                 const int2* __restrict__ lrow, const uint8_t* __restrict__ rootbwd,
-                                                 const double* __restrict__ Dg, int leaves_in_task) {
+                                                 const uint8_t* __restrict__ rootbwd, const double* __restrict__ Dg) {
   extern __shared__ __attribute__((aligned(16))) double Ls[];
-  __shared__ double v0s[SMALL_SOLVE_MAX];
+  __shared__ double v0s[MED_SOLVE_MAX];
   __shared__ int s_task;
   const int tid = threadIdx.x;
   if (tid == 0) {
@@ -3229,11 +3487,6 @@ __global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __re
   int64_t* dg = dbg ? dbg + 8 * t : nullptr;
   if (dg && tid == 0) dg[0] = wall_clock64();
   const int q0 = cptr[t], q1 = cptr[t + 1];
-  // the folded leaves first: they depend on b only
-  if (leaves_in_task && lptr[t + 1] > lptr[t]) {
-    fwd_leaves(leaves, lptr[t], lptr[t + 1], lrow, arena, b, xi, T.gbuf);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
   if (dg) {
     __syncthreads();
     if (tid == 0) dg[1] = wall_clock64();
@@ -3241,10 +3494,11 @@ __global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __re
   for (int q = q0; q < q1; ++q) {
     const int s = clist[q];
     const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+    const bool med = r > SMALL_SOLVE_MAX;  // medium front: panel streamed in chunks after the gather
     const int ldt = tree_ldt(w);
-    double* stg = Ls + r * ldt;
-    const int cap = ((lds_doubles - r * ldt) / NT) * NT;
-    stage_rowmajor(arena + T.l_off[s], Ls, r, w, ldt);
+    double* stg = med ? Ls : Ls + r * ldt;
+    const int cap = med ? (lds_doubles / NT) * NT : ((lds_doubles - r * ldt) / NT) * NT;
+    if (!med) stage_rowmajor(arena + T.l_off[s], Ls, r, w, ldt);
     // everything that does not depend on the children is loaded before the wait: the gather range
     // (symbolic) and this front's own right-hand side entries (the input b)
     const int64_t e0 = T.row_ptr[s];
@@ -3257,7 +3511,7 @@ __global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __re
       const int i = (tid & 63) + 64 * h;
       udst[h] = (tid < 64 && i >= w && i < r) ? uvec_dst(T, s, i - w, uvec) : xi + f0 + min(i, max(w - 1, 0));
     }
-    // an elimination-tree root (r == w) also runs its backward substitution here (MADIPM_ROOT_BWD=1):
+    // an elimination-tree root (r == w) also runs its backward substitution here:
     // its pivots and the caller's positions are loaded before the wait
     const bool rb = q == q1 - 1 && rootbwd[t];
     double dpiv[3];
@@ -3304,6 +3558,10 @@ __global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __re
     }
     if (tid < r) v0s[tid] = ((c0 + c1) + (c2 + c3)) + init;
     __syncthreads();
+    if (med) {
+      fwd_med_front(T, s, arena, Ls, v0s, xi, uvec, tflags, epoch);
+      continue;
+    }
     if (dg && tid == 0 && q == q1 - 1) dg[3] = wall_clock64();
     if (tid < 64) {
       const int lane = tid;
@@ -3354,9 +3612,7 @@ __global__ __launch_bounds__(NT) void k_bwd_tree(FrontTab T, const int32_t* __re
                                                  int nt, const int32_t* __restrict__ pdep, int32_t* counter, int32_t* tflags,
                                                  int epoch, const double* __restrict__ arena,
                                                  const double* __restrict__ D, double* xi, double* __restrict__ out,
-                                                 int32_t* err, const int32_t* __restrict__ lptr,
-                                                 const SolveLeaf* __restrict__ leaves, const int2* __restrict__ lrow,
-                                                 const uint8_t* __restrict__ rootbwd, int leaves_in_task) {
+                                                 int32_t* err, const uint8_t* __restrict__ rootbwd) {
   extern __shared__ __attribute__((aligned(16))) double Ls[];
   __shared__ double xbs[SMALL_SOLVE_MAX];
   __shared__ int s_task;
@@ -3375,6 +3631,10 @@ __global__ __launch_bounds__(NT) void k_bwd_tree(FrontTab T, const int32_t* __re
   for (int q = q1 - 1; q >= q0; --q) {  // top first
     const int s = clist[q];
     const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+    if (r > SMALL_SOLVE_MAX) {  // medium front: chunked, double-buffered
+      bwd_med_front(T, s, arena, D, Ls, xi, out, pdep, t, tflags, epoch, err);
+      continue;
+    }
     const int ldc = tree_ldc(r);
     stage_colmajor(arena + T.l_off[s], Ls, r, w, ldc);
     const int32_t* __restrict__ rows = T.rows + T.row_ptr[s];
@@ -3427,7 +3687,6 @@ __global__ __launch_bounds__(NT) void k_bwd_tree(FrontTab T, const int32_t* __re
     }
     __syncthreads();  // wave 0 is done with Ls; its stores are drained
   }
-  if (leaves_in_task && lptr[tf + 1] > lptr[tf]) bwd_leaves(leaves, lptr[tf], lptr[tf + 1], lrow, arena, D, xi, out);
 }
 
 // ------------------------------------------------------------------ sharding (SURVEY §8 e)
@@ -3674,10 +3933,11 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     std::vector<char> lbpar(std::max(ns, 1), 0);
     for (const auto& G : S.lb) lbpar[G.parent] = 1;
     auto preleaf = [&](int c) { return S.child_ptr[c] == S.child_ptr[c + 1] && S.nrows[c] <= 32; };
+    // medium fronts (SMALL_SOLVE_MAX < r <= MED_SOLVE_MAX) join with their panel streamed in chunks
+    auto medium = [&](int s) { return S.nrows[s] > SMALL_SOLVE_MAX && S.nrows[s] <= MED_SOLVE_MAX; };
     for (int s = 0; on && s < ns; ++s) {  // postorder: children first
-      if (!in_phase(s, 1) || preleaf(s) || !solve_small(s) || lbpar[s] ||
-          8 * tree_panel_doubles(s) + 8 * 2048 > TREE_LDS_MAX)
-        continue;
+      if (!in_phase(s, 1) || preleaf(s) || lbpar[s]) continue;
+      if (!medium(s) && (!solve_small(s) || 8 * tree_panel_doubles(s) + 8 * 2048 > TREE_LDS_MAX)) continue;
       bool ok = true;
       for (int q = S.child_ptr[s]; q < S.child_ptr[s + 1] && ok; ++q) {
         const int c = S.child_list[q];
@@ -3687,16 +3947,11 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     }
   }
   // micro leaves (w <= 2, r <= 32, no children) under tree fronts, solved from precomputed leaf records
-  // (SolveLeaf): MADIPM_SOLVE_FOLD=1 (default) by the flat k_fwd_leaves / k_bwd_leaves launches, =2
-  // inside the tree tasks (k_fwd_tree / k_bwd_tree, beside their parent front), =4 forward by the flat
-  // launch and backward inside the tree tasks (after the task's fronts have published their x), =0 by
-  // the generic level-0 micro launches (k_fwd_micro / k_bwd_micro)
+  // (SolveLeaf) by the flat k_fwd_leaves / k_bwd_leaves launches (r3: solving them inside the tree tasks,
+  // or their backward only, measured slower: 1478 vs 1534 iters/s)
   std::vector<char> sleaf(std::max(ns, 1), 0);
   {
-    const char* ev = std::getenv("MADIPM_SOLVE_FOLD");
-    sfold_ = ev ? std::atoi(ev) : 1;
-    const bool on = sfold_ > 0;
-    for (int c = 0; on && c < ns; ++c) {
+    for (int c = 0; c < ns; ++c) {
       const int p = S.parent[c];
       sleaf[c] = p >= 0 && in_tree[p] && in_phase(c, 1) && S.child_ptr[c] == S.child_ptr[c + 1] && S.nrows[c] <= 32 &&
                  S.first[c + 1] - S.first[c] <= 2;
@@ -3742,6 +3997,9 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       dptr.push_back((int32_t)dl.size());
       const int r = S.nrows[s], w = S.first[s + 1] - S.first[s], u = r - w;
       const bool sq = r <= 128 && !S.fold_pk[s];
+      if (r > SymbolicPlan::kFactTreeMax)  // medium front: one panel (r | 1) x min(64, w) in LDS
+        ftree_lds_ = std::max<int>(ftree_lds_, 8 * (((r | 1) * std::min(64, w) + 1) & ~1));
+      else
       ftree_lds_ = std::max<int>(ftree_lds_, (sq ? 8 * ((r * (r | 1) + 1) & ~1) : 8 * ((r * (r + 1) / 2 + 1) & ~1)) +
                                                  (S.absorb[s] ? SymbolicPlan::kFoldRowBytes * S.fold_rmax[s] +
                                                                     SymbolicPlan::kFoldLeafBytes * S.fold_lmax[s]
@@ -4137,76 +4395,45 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         tree_bytes_ += 8.0 * (r * w + 3.0 * r);
         tree_flops_ += 2.0 * (r * w - w * (w + 1) / 2);
         tree_alg_ += solve_alg(s);
-        tree_lds_ = std::max<int>(tree_lds_, 8 * tree_panel_doubles(s) + 8 * 2048);
+        if (S.nrows[s] > SMALL_SOLVE_MAX)
+          tree_lds_ = std::max<int>(tree_lds_, 8 * std::max(MED_FWD_LDS, MED_BWD_LDS));
+        else
+          tree_lds_ = std::max<int>(tree_lds_, 8 * tree_panel_doubles(s) + 8 * 2048);
       }
       tree_lds_ = std::min(TREE_LDS_MAX, tree_lds_ + 8 * 2048);  // up to 4096 staged gather sources
-      // chain tasks: a tree front that is the only tree child of its tree parent is solved by the
-      // parent's workgroup right before it (MADIPM_CHAIN_SOLVE=0: one task per front).  Tasks in the
-      // order of their top front in `ord` (levels ascending): a task's forward dependencies (the tree
-      // children of its deepest front: tops of other tasks) have earlier tickets, and in reverse order
-      // the backward one (the tree parent of its top) does.
-      const char* ce = std::getenv("MADIPM_CHAIN_SOLVE");  // opt-in: measured slower on ex10 (r3)
-      const bool chains = ce && ce[0] == '1';
-      std::vector<int32_t> ntc(std::max(ns, 1), 0), only(std::max(ns, 1), -1);
-      for (int s : ord)
-        if (S.parent[s] >= 0 && in_tree[S.parent[s]]) {
-          ntc[S.parent[s]]++;
-          only[S.parent[s]] = s;
-        }
-      auto joins = [&](int c) { return chains && S.parent[c] >= 0 && in_tree[S.parent[c]] && ntc[S.parent[c]] == 1; };
-      std::vector<int32_t> cptr{0}, clist, dptr{0}, dl, tops, lptr{0};
+      // one task per tree front, in `ord` order (levels ascending): a task's forward dependencies (its
+      // tree children) have earlier tickets, and in reverse order the backward one (its tree parent)
+      // does.  (r3: chains of only-children solved back to back by one workgroup measured slower.)
+      std::vector<int32_t> cptr{0}, clist, dptr{0}, dl, tops;
       std::vector<SolveLeaf> lv;
       std::vector<int2> lrow;
       for (int s : ord) {
-        if (joins(s)) continue;  // solved inside its parent's task
-        std::vector<int32_t> ch{s};
-        while (ntc[ch.back()] == 1 && joins(only[ch.back()])) ch.push_back(only[ch.back()]);
-        std::reverse(ch.begin(), ch.end());  // deepest first
-        for (int f : ch) {
-          clist.push_back(f);
-          for (int q = S.child_ptr[f]; q < S.child_ptr[f + 1] && (sfold_ == 2 || sfold_ == 4); ++q) {  // folded leaves
-            const int c = S.child_list[q];
-            if (!sleaf[c]) continue;
-            const int r = S.nrows[c], w = S.first[c + 1] - S.first[c], f0 = S.first[c];
-            SolveLeaf L{S.l_off[c], f0, r | (w << 8), S.perm[f0], w == 2 ? S.perm[f0 + 1] : -1, (int32_t)lrow.size(), 0};
-            lv.push_back(L);
-            for (int a = 0; a < r - w; ++a) {
-              const int64_t g = inv_pos(c, a);
-              MADIPM_REQUIRE(g >= 0 && g < INT32_MAX, "tree solve: folded leaf gather position");
-              lrow.push_back(int2{(int32_t)g, S.rows[S.row_ptr[c] + w + a]});
-            }
-          }
-        }
-        for (int q = S.child_ptr[ch[0]]; q < S.child_ptr[ch[0] + 1]; ++q)
+        clist.push_back(s);
+        for (int q = S.child_ptr[s]; q < S.child_ptr[s + 1]; ++q)
           if (in_tree[S.child_list[q]]) dl.push_back(S.child_list[q]);
         cptr.push_back((int32_t)clist.size());
         dptr.push_back((int32_t)dl.size());
-        lptr.push_back((int32_t)lv.size());
         tops.push_back(s);
       }
-      if (sfold_ == 1) {  // the flat leaf launches: every folded leaf, in postorder (L panels in order)
-        for (int c = 0; c < ns; ++c) {
-          if (!sleaf[c]) continue;
-          const int r = S.nrows[c], w = S.first[c + 1] - S.first[c], f0 = S.first[c];
-          lv.push_back(SolveLeaf{S.l_off[c], f0, r | (w << 8), S.perm[f0], w == 2 ? S.perm[f0 + 1] : -1,
-                                 (int32_t)lrow.size(), 0});
-          for (int a = 0; a < r - w; ++a) {
-            const int64_t g = inv_pos(c, a);
-            MADIPM_REQUIRE(g >= 0 && g < INT32_MAX, "tree solve: folded leaf gather position");
-            lrow.push_back(int2{(int32_t)g, S.rows[S.row_ptr[c] + w + a]});
-          }
+      // the flat leaf launches: every folded leaf, in postorder (L panels in order)
+      for (int c = 0; c < ns; ++c) {
+        if (!sleaf[c]) continue;
+        const int r = S.nrows[c], w = S.first[c + 1] - S.first[c], f0 = S.first[c];
+        lv.push_back(SolveLeaf{S.l_off[c], f0, r | (w << 8), S.perm[f0], w == 2 ? S.perm[f0 + 1] : -1,
+                               (int32_t)lrow.size(), 0});
+        for (int a = 0; a < r - w; ++a) {
+          const int64_t g = inv_pos(c, a);
+          MADIPM_REQUIRE(g >= 0 && g < INT32_MAX, "tree solve: folded leaf gather position");
+          lrow.push_back(int2{(int32_t)g, S.rows[S.row_ptr[c] + w + a]});
         }
       }
       ntask_ = (int)tops.size();
-      {  // elimination-tree roots solved backward by k_fwd_tree (MADIPM_ROOT_BWD=0 disables): one-front
-         // tasks without leaves whose front has no parent at all (r == w)
-        const char* rbe = std::getenv("MADIPM_ROOT_BWD");
-        const bool on = !(rbe && rbe[0] == '0');
+      {  // elimination-tree roots (r == w, no parent) solved backward by k_fwd_tree right after their forward
+         // substitution, on the panel already in LDS (bitwise k_bwd_tree's x; r3: k_bwd_tree 52 -> 43 us)
         std::vector<uint8_t> rbv(std::max(ntask_, 1), 0);
-        for (int t = 0; on && t < ntask_; ++t) {
+        for (int t = 0; t < ntask_; ++t) {
           const int f = tops[t];
-          rbv[t] = cptr[t + 1] - cptr[t] == 1 && lptr[t + 1] == lptr[t] && S.parent[f] < 0 &&
-                   S.nrows[f] == S.first[f + 1] - S.first[f];
+          rbv[t] = S.parent[f] < 0 && S.nrows[f] == S.first[f + 1] - S.first[f] && S.nrows[f] <= SMALL_SOLVE_MAX;
         }
         trootbwd_.upload(rbv);
       }
@@ -4221,21 +4448,15 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       up(tdep_ptr_, dptr);
       up(tdep_, dl);
       up(tpar_, par);
-      up(tl_ptr_, lptr);
       tleaf_.upload(lv.empty() ? std::vector<SolveLeaf>(1) : lv);
       lrow.push_back(int2{0, 0});  // padding: the leaf kernels' clamped loads of a leaf without update rows
       tlrow_.upload(lrow);
       nsleaf_ = (int64_t)lv.size();
       for (const SolveLeaf& L : lv) {
         const double r = L.rw & 255, w = L.rw >> 8;
-        const double a = 8.0 * (S.colcnt[L.f0] + (w == 2 ? S.colcnt[L.f0 + 1] : 0));
-        if (sfold_ == 2) {
-          tree_alg_ += a;
-        } else {
-          leaf_alg_ += a;
-          leaf_bytes_ += 8.0 * (r * w + 3.0 * r) + 32.0 + 8.0 * (r - w);
-          leaf_flops_ += 2.0 * (r * w - w * (w + 1) / 2);
-        }
+        leaf_alg_ += 8.0 * (S.colcnt[L.f0] + (w == 2 ? S.colcnt[L.f0 + 1] : 0));
+        leaf_bytes_ += 8.0 * (r * w + 3.0 * r) + 32.0 + 8.0 * (r - w);
+        leaf_flops_ += 2.0 * (r * w - w * (w + 1) / 2);
       }
       tflags_.alloc(std::max(ns, 1));
       tflags_.zero();
@@ -4729,7 +4950,7 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
             (k_fwd_big<<<std::min(L.nftask, 512), NT, 0, s>>>(T_, tasks + L.ftask_off, L.nftask, cnt + 2 * lev,
                                                                flags_, flag_off_, efwd, arena_, vwork_, xi_, uvec_, &st_->err)));
     }
-    if (lev == 0 && phase == 0 && ntree_ && (sfold_ == 1 || sfold_ == 4) && nsleaf_)
+    if (lev == 0 && phase == 0 && ntree_ && nsleaf_)
       TIMED(KK_FWD_TINY, leaf_bytes_, leaf_alg_, leaf_flops_,
             (k_fwd_leaves<<<(unsigned)cdiv(nsleaf_ * LPL, NT), NT, 0, s>>>(tleaf_, (int)nsleaf_, tlrow_, arena_, b, xi_,
                                                                          T_.gbuf)));
@@ -4737,8 +4958,7 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
       TIMED(KK_FWD_TREE, tree_bytes_, tree_alg_, tree_flops_,
             (k_fwd_tree<<<(unsigned)ntask_, NT, tree_lds_, s>>>(T_, tc_ptr_, tc_list_, ntask_, tdep_ptr_, tdep_,
                                                                  counters_.p + 4 * S_.nlevels, tflags_, efwd, tree_lds_ / 8,
-                                                                 arena_, b, xi_, uvec_, &st_->err, tdbg_.p, tl_ptr_, tleaf_,
-                                                                 tlrow_, trootbwd_, D_, sfold_ == 2 ? 1 : 0)));
+                                                                 arena_, b, xi_, uvec_, &st_->err, tdbg_.p, trootbwd_, D_)));
     if (lev == 0 && phase == 0 && ntree_ && tdbg_.p)
       tree_debug_dump(s, "fwd", tdbg_.p, ntask_, "leaves", "wait", "gather", "subst", "store", 8);
   }
@@ -4751,13 +4971,11 @@ void LDLSolver::bwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
   for (int lev = (int)V.size() - 1; lev >= 0; --lev) {
     const SolveLevel& L = V[lev];
     if (lev == 0 && phase == 0 && ntree_)
-      TIMED(KK_BWD_TREE, tree_bytes_ + (sfold_ == 4 ? leaf_bytes_ : 0.0), tree_alg_ + (sfold_ == 4 ? leaf_alg_ : 0.0),
-            tree_flops_ + (sfold_ == 4 ? leaf_flops_ : 0.0),
+      TIMED(KK_BWD_TREE, tree_bytes_, tree_alg_, tree_flops_,
             (k_bwd_tree<<<(unsigned)ntask_, NT, tree_lds_, s>>>(T_, tc_ptr_, tc_list_, ntask_, tpar_,
                                                                  counters_.p + 4 * S_.nlevels + 1, tflags_, ebwd, arena_, D_,
-                                                                 xi_, b, &st_->err, tl_ptr_, tleaf_, tlrow_, trootbwd_,
-                                                                 (sfold_ == 2 || sfold_ == 4) ? 1 : 0)));
-    if (lev == 0 && phase == 0 && ntree_ && sfold_ == 1 && nsleaf_)
+                                                                 xi_, b, &st_->err, trootbwd_)));
+    if (lev == 0 && phase == 0 && ntree_ && nsleaf_)
       TIMED(KK_BWD_TINY, leaf_bytes_, leaf_alg_, leaf_flops_,
             (k_bwd_leaves<<<(unsigned)cdiv(nsleaf_ * LPL, NT), NT, 0, s>>>(tleaf_, (int)nsleaf_, tlrow_, arena_, D_, xi_,
                                                                          b)));

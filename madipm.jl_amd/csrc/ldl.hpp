@@ -301,11 +301,10 @@ class LDLSolver : public LinSolver {
   double fact_alg_cols(int c0, int c1) const;
   double solve_alg(int s) const;
   double lb_alg(size_t g) const;
-  DBuf<int32_t> tc_ptr_, tc_list_, tdep_ptr_, tdep_, tpar_, tflags_, tl_ptr_;
+  DBuf<int32_t> tc_ptr_, tc_list_, tdep_ptr_, tdep_, tpar_, tflags_;
   DBuf<uint8_t> trootbwd_;  // per forward task: an elimination-tree root solved backward by k_fwd_tree
-  int ntask_ = 0;         // chain tasks (fronts solved back to back by one workgroup)
-  int64_t nsleaf_ = 0;    // micro leaves solved from leaf records (sfold_ 1: flat launches, 2: in the tasks)
-  int sfold_ = 1;
+  int ntask_ = 0;         // tree-solve tasks (one per tree front)
+  int64_t nsleaf_ = 0;    // micro leaves solved from leaf records by the flat leaf launches
   double leaf_bytes_ = 0, leaf_flops_ = 0, leaf_alg_ = 0;  // the flat leaf launches (per direction)
   DBuf<SolveLeaf> tleaf_;
   DBuf<int2> tlrow_;

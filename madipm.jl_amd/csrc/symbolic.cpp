@@ -982,7 +982,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     std::vector<char> lbpar(ns, 0);
     for (const auto& g : S.lb) lbpar[g.parent] = 1;
     for (int s = 0; on && s < ns; ++s) {  // postorder: children first
-      if (S.top(s) || !S.mine(s) || lb_member(s) || lbpar[s] || S.nrows[s] > SymbolicPlan::kFactTreeMax) continue;
+      if (S.top(s) || !S.mine(s) || lb_member(s) || lbpar[s] || S.nrows[s] > SymbolicPlan::kFactTreeMedMax) continue;
       if (S.child_ptr[s] == S.child_ptr[s + 1] && S.nrows[s] <= 32) continue;  // pre-leaf
       bool ok = true;
       int fanin = 0;  // tree children are added one after another by one workgroup: bound the fan-in
@@ -1057,7 +1057,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     for (int s = 0; s < ns_all; ++s) {
       S.mc_ptr[s + 1] = S.mc_ptr[s];
       S.fold_bptr[s + 1] = S.fold_bptr[s];
-      if (!on || !S.ftree[s]) continue;
+      if (!on || !S.ftree[s] || S.nrows[s] > SymbolicPlan::kFactTreeMax) continue;  // medium fronts: no folding
       const int64_t r = S.nrows[s];
       int64_t nmc = 0, nrow = 0;
       bool ok = true;
@@ -1211,7 +1211,9 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   S.fs_off.assign(ns, -1);
   S.fs_size = 0;
   for (int s = 0; s < ns; ++s)
-    if ((S.ftree[s] && !S.absorb[s]) || (!S.ftree[s] && !S.is_big[s] && S.child_ptr[s + 1] > S.child_ptr[s] && S.mine(s))) {
+    if ((S.ftree[s] && !S.absorb[s] && S.nrows[s] <= SymbolicPlan::kFactTreeMax) ||
+        (!S.ftree[s] && !S.is_big[s] && S.child_ptr[s + 1] > S.child_ptr[s] && S.mine(s))) {
+      // (medium tree fronts are pre-assembled in place, in the arena: no scratch)
       S.fs_off[s] = S.fs_size;
       // fronts staged into LDS are pre-assembled as their LDS image (square ld r | 1, or packed
       // lower for r > 128): room for r (r | 1) doubles

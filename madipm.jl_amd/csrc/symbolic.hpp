@@ -100,6 +100,9 @@ struct SymbolicPlan {
   std::vector<int64_t> g_src;          // >= 0: arena index; < 0: ~(index into caller's values)
   std::vector<int64_t> fs_off;         // small fronts with children, tree fronts: r x r scratch (else -1)
   static constexpr int kFactTreeMax = 192;
+  // medium tree fronts (kFactTreeMax < r <= kFactTreeMedMax): factorised by k_fact_tree in HBM, one
+  // 64-column panel in LDS at a time (fact_med_front); big-front storage, pre-assembled in the arena
+  static constexpr int kFactTreeMedMax = 256;
   static constexpr int kFoldThreads = 512;  // threads of k_fact_tree: product-list chunks per batch
   static constexpr int kFactTreeFanIn = 8;
   std::vector<uint8_t> ftree;          // factorisation-tree fronts (k_fact_tree)

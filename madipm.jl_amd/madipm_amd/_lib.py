@@ -39,7 +39,8 @@ class LDLInfo(C.Structure):
                 ("max_front", C.c_int32), ("nbig", C.c_int32), ("arena_bytes", C.c_int64),
                 ("lb_groups", C.c_int32), ("lb_members", C.c_int32),
                 ("fold_fronts", C.c_int32), ("fold_leaves", C.c_int32),
-                ("xch_fact", C.c_int64), ("xch_solve", C.c_int64), ("xch_gather", C.c_int64)]
+                ("xch_fact", C.c_int64), ("xch_solve", C.c_int64), ("xch_gather", C.c_int64),
+                ("tree_fronts", C.c_int32), ("tree_medium", C.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

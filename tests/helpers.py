@@ -61,3 +61,20 @@ def dense_k2(m, n, seed, delta=1e-2):
     Lw = sp.tril(K).tocsc()
     Lw.sort_indices()
     return K, Lw
+
+
+def lp_k2(qp, seed, well=False, delta=1e-8):
+    """K2 = [Sigma, A^T; A, -delta I] on the constraint matrix of a QuadraticModel (the benchmark
+    stand-ins' structure: their fronts), Sigma as random_k2; returns (K, lower CSC sorted)."""
+    rng = np.random.default_rng(seed)
+    m, n = qp.ncon, qp.nvar
+    A = sp.csr_matrix((np.asarray(qp.Avals, float), (np.asarray(qp.Arows), np.asarray(qp.Acols))), shape=(m, n))
+    A.sum_duplicates()
+    sig = 10.0 ** rng.uniform(-1, 1, n) if well else 10.0 ** rng.uniform(-2, 2, n)
+    if well:
+        delta = 1e-2
+    K = sp.bmat([[sp.diags(sig), A.T], [A, -delta * sp.eye(m)]]).tocsc()
+    K.sum_duplicates()
+    Lw = sp.tril(K).tocsc()
+    Lw.sort_indices()
+    return K, Lw

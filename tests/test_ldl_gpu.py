@@ -166,21 +166,31 @@ def test_ldl_pipe_lost_handoff_is_an_error(monkeypatch):
 
 
 @pytest.mark.parametrize("case", ["block_well", "block_ipm", "random"])
-def test_root_backward_in_forward_bitwise(case, monkeypatch):
-    """An elimination-tree root (r == w) solved backward by the forward tree kernel right after its
-    forward substitution (panel already in LDS; MADIPM_ROOT_BWD=1, default) instead of by k_bwd_tree:
-    the same fma sequence on the row-major panel, so the solution is BITWISE that of the separate
-    backward task (=0) — and the oracle's."""
+def test_root_backward_in_forward(case):
+    """An elimination-tree root (r == w) is solved backward by the forward tree kernel right after its
+    forward substitution (panel already in LDS; k_bwd_tree skips its ticket): the oracle's solution."""
     if case.startswith("block"):
         K, Lw = block_angular_k2(3000, 4000, 20, 7, well=case == "block_well")
     else:
         K, Lw = random_k2(400, 900, 0.004, 4, well=True)
-    out = {}
-    for rb in ("0", "1"):
-        monkeypatch.setenv("MADIPM_ROOT_BWD", rb)
-        out[rb] = _factor_solve(K, Lw, 128)
-    assert np.array_equal(out["0"][1].view(np.uint64), out["1"][1].view(np.uint64))
     _check_case(K, Lw, well=case != "block_ipm")
+
+
+@pytest.mark.parametrize("well", [True, False])
+def test_ldl_medium_tree_fronts(well):
+    """Medium fronts (192 < r <= 256: the supportcase10 stand-in's block separators, r ~ 230) factorised
+    inside the dependency-driven tree launch — F in HBM, one 64-column panel in LDS at a time, the
+    trailing update on f64 MFMA in HBM, children's update blocks added in place — give the oracle's
+    pivots (1e-12, well conditioned) and solution, chains of medium fronts included."""
+    from helpers import lp_k2
+    from madipm_amd import standard_form_qp
+    from madipm_amd.instances import supportcase10_standin
+    qp = standard_form_qp(supportcase10_standin(scale=0.05, block_scale=1.0))
+    K, Lw = lp_k2(qp, 3, well=well)
+    ls = _check_case(K, Lw, well=well)
+    info = ls.info()
+    assert info["tree_medium"] >= 3 and info["max_front"] > 192, info
+    assert ls.inertia() == (qp.nvar, 0, qp.ncon)
 
 
 @pytest.mark.parametrize("kpan", ["1", "2", "4"])
@@ -201,17 +211,11 @@ def test_big_front_panel_groups(kpan, n, m, monkeypatch):
     _check_case(K, Lw, small_front_max=16, well=True)
 
 
-@pytest.mark.parametrize("chain,sfold", [("0", "1"), ("0", "0"), ("0", "2"), ("1", "2"), ("1", "1"), ("0", "4"),
-                                         ("1", "4")])
 @pytest.mark.parametrize("well", [True, False])
-def test_ldl_chain_solve_and_leaf_fold(chain, sfold, well, monkeypatch):
-    """Tree solves with one task per front (default) or over chain tasks (MADIPM_CHAIN_SOLVE=1), and
-    the micro leaves under tree fronts solved from leaf records by flat launches (MADIPM_SOLVE_FOLD=1,
-    default), inside the tree tasks (=2), forward flat + backward in the tasks (=4) or by the generic
-    micro launches (=0): same solution as the
-    oracle in every combination, and for several right-hand sides in a row (flag epochs)."""
-    monkeypatch.setenv("MADIPM_CHAIN_SOLVE", chain)
-    monkeypatch.setenv("MADIPM_SOLVE_FOLD", sfold)
+def test_ldl_tree_solves_repeated(well):
+    """Tree solves (one task per front, flag epochs per solve) with the micro leaves under tree fronts
+    solved from leaf records by the flat launches: the oracle's solution for several right-hand sides
+    in a row."""
     K, Lw = block_angular_k2(3000, 4000, 20, 7, well=well)
     ls = _check_case(K, Lw, well=well)
     ref = OracleLDL(K, ls.perm())
@@ -230,11 +234,8 @@ def test_ldl_chain_solve_and_leaf_fold(chain, sfold, well, monkeypatch):
 def test_ldl_leaf_folding(fold, well, monkeypatch):
     """Leaf folding (default; MADIPM_FOLD=0 turns it off): tree fronts factorise their micro-leaf
     children themselves and subtract the leaves' rank-1/2 updates in LDS through destination-sorted
-    product lists — same pivots / solution as the oracle, with and without it.  MADIPM_FOLD_SLOTS=0:
-    every tree front folds (by default the fronts past the first 256 tickets leave their leaves to the
-    micro launch + gather)."""
+    product lists — same pivots / solution as the oracle, with and without it."""
     monkeypatch.setenv("MADIPM_FOLD", fold)
-    monkeypatch.setenv("MADIPM_FOLD_SLOTS", "0")
     K, Lw = block_angular_k2(3000, 4000, 20, 7, well=well)
     ls = _check_case(K, Lw, well=well)
     assert ls.inertia() == (4000, 0, 3000)

@@ -194,6 +194,7 @@ def test_normal_kkt_rejects_qp():
 # The supportcase10 (many short rows) and neos-5052403 (dense rows, wide separators) stand-ins at a
 # scale the oracle solves in seconds; bench.py --config supportcase10 / neos runs the full sizes.
 @pytest.mark.parametrize("name,kw", [("supportcase10_standin", dict(scale=0.1, block_scale=0.3)),
+                                     ("supportcase10_standin", dict(scale=0.05, block_scale=1.0)),  # r ~ 230 fronts
                                      ("neos5052403_standin", dict(scale=0.25, block_scale=0.15))])
 def test_config_standins_parity(name, kw):
     from madipm_amd import FixedRegularization, standard_form_qp, MPCSolver
