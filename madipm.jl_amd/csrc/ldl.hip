@@ -3044,7 +3044,8 @@ __global__ __launch_bounds__(NT) void k_bwd_big(FrontTab T, const SolveTask* __r
 // upper triangle + diagonal zeroed and the pivot columns zero-padded to a multiple of 16, so every
 // block loads its L entries unconditionally (16-byte LDS reads, immediate offsets) and the
 // dependency chain is one readlane + one fma per pivot.
-constexpr int TREE_LDS_MAX = 156 * 1024;  // dynamic LDS of the tree solves (+ ~2 KB static)
+// dynamic LDS of the tree solves (+ ~2 KB static): two 256-thread workgroups per CU
+constexpr int TREE_SOLVE_LDS = 76 * 1024;
 __device__ __forceinline__ int tree_ldt(int w) { return ((w + 15) & ~15) + 2; }  // forward: row-major ld
 __device__ __forceinline__ int tree_ldc(int r) { return ((r + 31) & ~31) + 2; }  // backward: col-major ld
 
@@ -3187,12 +3188,14 @@ __device__ __forceinline__ void bwd_subst_t(double (&v)[3], const double* LT, in
   }
 }
 
-// ---- Medium tree fronts in the tree solves (SMALL_SOLVE_MAX < r <= kFactTreeMedMax): the L panel
-// (r x w, up to 256 x 256) does not fit LDS, so it is streamed in column chunks, double-buffered: wave 0
+// ---- Chunked tree-solve fronts: medium fronts (SMALL_SOLVE_MAX < r <= kFactTreeMedMax) and every
+// front whose whole panel would not fit the tree solves' LDS budget (TREE_SOLVE_LDS: two workgroups per
+// CU, so the 272 level-1/2 fronts of ex10 all start at once — with one per CU, 16 of them waited for
+// a level-1 front to retire).  The L panel is streamed in 16-column chunks, double-buffered: wave 0
 // substitutes chunk c while waves 1..3 stage chunk c +- 1.  v (forward) / x (backward) stay in wave 0's
 // registers, 4 rows per lane.
 constexpr int MED_SOLVE_MAX = SymbolicPlan::kFactTreeMedMax;
-constexpr int MCW = 32, MLDT = MCW + 2;           // forward chunk: pivot columns, row-major ld
+constexpr int MCW = 16, MLDT = MCW + 2;           // forward chunk: pivot columns, row-major ld
 constexpr int MFBUF = MED_SOLVE_MAX * MLDT;       // doubles per forward chunk buffer
 constexpr int MLDC = MED_SOLVE_MAX + 2;           // backward chunk: col-major ld
 constexpr int MBBUF = MCW * MLDC;                 // doubles per backward chunk buffer
@@ -3337,27 +3340,32 @@ __device__ __forceinline__ void bwd_med_front(const FrontTab& T, int s, const do
   if (tid < nb) xall[w + tid] = ld_sc1(xi + rk);
   __syncthreads();
   const bool wo = T.wout[s];
-  const int jl = lane & 31, half = lane >> 5;
+  constexpr int NG = 64 / MCW;  // lane groups of the wave: group g sums the rows t = c1 + g (mod NG)
+  const int jl = lane % MCW, grp = lane / MCW;
   for (int c = nch - 1; c >= 0; --c) {
     const int c0 = c * MCW, c1 = min(c0 + MCW, w), j = c0 + jl;
     if (wv == 0) {
       const double* LC = buf[c & 1] + jl * MLDC;
-      // rows below the chunk (two half-waves: even / odd rows), then the chunk's own triangle
+      // rows below the chunk (NG lane groups, interleaved rows), then the chunk's own triangle
       double a0 = 0.0, a1 = 0.0;
-      int q = c1 + half;
-      for (; q + 2 < r; q += 4) {
+      int q = c1 + grp;
+      for (; q + NG < r; q += 2 * NG) {
         a0 = fma(LC[q - c0], xall[q], a0);
-        a1 = fma(LC[q + 2 - c0], xall[q + 2], a1);
+        a1 = fma(LC[q + NG - c0], xall[q + NG], a1);
       }
-      for (; q < r; q += 2) a0 = fma(LC[q - c0], xall[q], a0);
-      double acc = a0 + a1;
-      acc = (half == 0) ? acc + __shfl_xor(acc, 32, 64) : __shfl_xor(acc, 32, 64) + acc;
+      for (; q < r; q += NG) a0 = fma(LC[q - c0], xall[q], a0);
+      const double part = a0 + a1;
+      double p[NG];
+#pragma unroll
+      for (int g = 0; g < NG; ++g) p[g] = __shfl(part, jl + MCW * g, 64);
+      static_assert(NG == 4, "bwd_med_front: four lane groups");
+      const double acc = (p[0] + p[1]) + (p[2] + p[3]);  // the same fixed order in every lane group
       double x = (j < w) ? ownv[min(j, w - 1)] - acc : 0.0;
       for (int tt = c1 - 1; tt > c0; --tt) {  // x_j -= L(tt, j) x_tt, j < tt
         const double xt = readlane_f64(x, tt - c0);
         x = fma(-LC[tt - c0], xt, x);
       }
-      if (half == 0 && j < w) {
+      if (grp == 0 && j < w) {
         xall[j] = x;
         st_sc1(xi + f0 + j, x);
         if (wo) out[T.perm[f0 + j]] = x;
@@ -3472,7 +3480,8 @@ __global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __re
                                                  int32_t* counter, int32_t* tflags, int epoch, int lds_doubles,
                                                  const double* __restrict__ arena, const double* __restrict__ b,
                                                  double* xi, double* uvec, int32_t* err, int64_t* dbg,
-                                                 const uint8_t* __restrict__ rootbwd, const double* __restrict__ Dg) {
+                                                 const uint8_t* __restrict__ rootbwd, const double* __restrict__ Dg,
+                                                 const uint8_t* __restrict__ tchunk) {
   extern __shared__ __attribute__((aligned(16))) double Ls[];
   __shared__ double v0s[MED_SOLVE_MAX];
   __shared__ int s_task;
@@ -3494,7 +3503,7 @@ __global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __re
   for (int q = q0; q < q1; ++q) {
     const int s = clist[q];
     const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
-    const bool med = r > SMALL_SOLVE_MAX;  // medium front: panel streamed in chunks after the gather
+    const bool med = tchunk[s];  // chunked front: panel streamed after the gather
     const int ldt = tree_ldt(w);
     double* stg = med ? Ls : Ls + r * ldt;
     const int cap = med ? (lds_doubles / NT) * NT : ((lds_doubles - r * ldt) / NT) * NT;
@@ -3612,7 +3621,8 @@ __global__ __launch_bounds__(NT) void k_bwd_tree(FrontTab T, const int32_t* __re
                                                  int nt, const int32_t* __restrict__ pdep, int32_t* counter, int32_t* tflags,
                                                  int epoch, const double* __restrict__ arena,
                                                  const double* __restrict__ D, double* xi, double* __restrict__ out,
-                                                 int32_t* err, const uint8_t* __restrict__ rootbwd) {
+                                                 int32_t* err, const uint8_t* __restrict__ rootbwd,
+                                                 const uint8_t* __restrict__ tchunk) {
   extern __shared__ __attribute__((aligned(16))) double Ls[];
   __shared__ double xbs[SMALL_SOLVE_MAX];
   __shared__ int s_task;
@@ -3631,7 +3641,7 @@ __global__ __launch_bounds__(NT) void k_bwd_tree(FrontTab T, const int32_t* __re
   for (int q = q1 - 1; q >= q0; --q) {  // top first
     const int s = clist[q];
     const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
-    if (r > SMALL_SOLVE_MAX) {  // medium front: chunked, double-buffered
+    if (tchunk[s]) {  // chunked front: panel streamed, double-buffered
       bwd_med_front(T, s, arena, D, Ls, xi, out, pdep, t, tflags, epoch, err);
       continue;
     }
@@ -3933,11 +3943,10 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     std::vector<char> lbpar(std::max(ns, 1), 0);
     for (const auto& G : S.lb) lbpar[G.parent] = 1;
     auto preleaf = [&](int c) { return S.child_ptr[c] == S.child_ptr[c + 1] && S.nrows[c] <= 32; };
-    // medium fronts (SMALL_SOLVE_MAX < r <= MED_SOLVE_MAX) join with their panel streamed in chunks
-    auto medium = [&](int s) { return S.nrows[s] > SMALL_SOLVE_MAX && S.nrows[s] <= MED_SOLVE_MAX; };
+    // fronts whose whole panel (+ 8 KB of gather staging) does not fit TREE_SOLVE_LDS, medium fronts
+    // (SMALL_SOLVE_MAX < r <= MED_SOLVE_MAX) included, join with their panel streamed in chunks
     for (int s = 0; on && s < ns; ++s) {  // postorder: children first
-      if (!in_phase(s, 1) || preleaf(s) || lbpar[s]) continue;
-      if (!medium(s) && (!solve_small(s) || 8 * tree_panel_doubles(s) + 8 * 2048 > TREE_LDS_MAX)) continue;
+      if (!in_phase(s, 1) || preleaf(s) || lbpar[s] || S.nrows[s] > MED_SOLVE_MAX) continue;
       bool ok = true;
       for (int q = S.child_ptr[s]; q < S.child_ptr[s + 1] && ok; ++q) {
         const int c = S.child_list[q];
@@ -4389,18 +4398,19 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
             MADIPM_REQUIRE(upm[S.rel_ptr[c] + a] >= 0, "tree gather map");
           }
       auto inv_pos = [&](int c, int a) { return upm[S.rel_ptr[c] + a]; };
-      tree_lds_ = 0;
+      tree_lds_ = 8 * 1024;
+      std::vector<uint8_t> chunk(std::max(ns, 1), 0);
       for (int s : ord) {
         const double r = S.nrows[s], w = S.first[s + 1] - S.first[s];
         tree_bytes_ += 8.0 * (r * w + 3.0 * r);
         tree_flops_ += 2.0 * (r * w - w * (w + 1) / 2);
         tree_alg_ += solve_alg(s);
-        if (S.nrows[s] > SMALL_SOLVE_MAX)
-          tree_lds_ = std::max<int>(tree_lds_, 8 * std::max(MED_FWD_LDS, MED_BWD_LDS));
-        else
-          tree_lds_ = std::max<int>(tree_lds_, 8 * tree_panel_doubles(s) + 8 * 2048);
+        chunk[s] = S.nrows[s] > SMALL_SOLVE_MAX || 8 * tree_panel_doubles(s) + 8 * 1024 > TREE_SOLVE_LDS;
+        tree_lds_ = std::max<int>(tree_lds_, chunk[s] ? 8 * std::max(MED_FWD_LDS, MED_BWD_LDS)
+                                                      : 8 * tree_panel_doubles(s) + 8 * 1024);
       }
-      tree_lds_ = std::min(TREE_LDS_MAX, tree_lds_ + 8 * 2048);  // up to 4096 staged gather sources
+      tree_lds_ = TREE_SOLVE_LDS;  // the rest of the budget stages gather sources
+      tchunk_.upload(chunk);
       // one task per tree front, in `ord` order (levels ascending): a task's forward dependencies (its
       // tree children) have earlier tickets, and in reverse order the backward one (its tree parent)
       // does.  (r3: chains of only-children solved back to back by one workgroup measured slower.)
@@ -4433,7 +4443,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         std::vector<uint8_t> rbv(std::max(ntask_, 1), 0);
         for (int t = 0; t < ntask_; ++t) {
           const int f = tops[t];
-          rbv[t] = S.parent[f] < 0 && S.nrows[f] == S.first[f + 1] - S.first[f] && S.nrows[f] <= SMALL_SOLVE_MAX;
+          rbv[t] = S.parent[f] < 0 && S.nrows[f] == S.first[f + 1] - S.first[f] && !chunk[f];
         }
         trootbwd_.upload(rbv);
       }
@@ -4527,10 +4537,10 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_small_blocked<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    192 * 193 / 2 * 8));
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_bwd_small, hipFuncAttributeMaxDynamicSharedMemorySize, 129 * 128 * 8));
-    MADIPM_HIP(hipFuncSetAttribute((const void*)k_fwd_tree, hipFuncAttributeMaxDynamicSharedMemorySize, TREE_LDS_MAX));
+    MADIPM_HIP(hipFuncSetAttribute((const void*)k_fwd_tree, hipFuncAttributeMaxDynamicSharedMemorySize, TREE_SOLVE_LDS));
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_fact_tree, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)SymbolicPlan::kFactTreeLdsMax));
-    MADIPM_HIP(hipFuncSetAttribute((const void*)k_bwd_tree, hipFuncAttributeMaxDynamicSharedMemorySize, TREE_LDS_MAX));
+    MADIPM_HIP(hipFuncSetAttribute((const void*)k_bwd_tree, hipFuncAttributeMaxDynamicSharedMemorySize, TREE_SOLVE_LDS));
     attr_done = true;
   }
   MADIPM_HIP(hipDeviceSynchronize());
@@ -4958,7 +4968,8 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
       TIMED(KK_FWD_TREE, tree_bytes_, tree_alg_, tree_flops_,
             (k_fwd_tree<<<(unsigned)ntask_, NT, tree_lds_, s>>>(T_, tc_ptr_, tc_list_, ntask_, tdep_ptr_, tdep_,
                                                                  counters_.p + 4 * S_.nlevels, tflags_, efwd, tree_lds_ / 8,
-                                                                 arena_, b, xi_, uvec_, &st_->err, tdbg_.p, trootbwd_, D_)));
+                                                                 arena_, b, xi_, uvec_, &st_->err, tdbg_.p, trootbwd_, D_,
+                                                                 tchunk_)));
     if (lev == 0 && phase == 0 && ntree_ && tdbg_.p)
       tree_debug_dump(s, "fwd", tdbg_.p, ntask_, "leaves", "wait", "gather", "subst", "store", 8);
   }
@@ -4974,7 +4985,7 @@ void LDLSolver::bwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
       TIMED(KK_BWD_TREE, tree_bytes_, tree_alg_, tree_flops_,
             (k_bwd_tree<<<(unsigned)ntask_, NT, tree_lds_, s>>>(T_, tc_ptr_, tc_list_, ntask_, tpar_,
                                                                  counters_.p + 4 * S_.nlevels + 1, tflags_, ebwd, arena_, D_,
-                                                                 xi_, b, &st_->err, trootbwd_)));
+                                                                 xi_, b, &st_->err, trootbwd_, tchunk_)));
     if (lev == 0 && phase == 0 && ntree_ && nsleaf_)
       TIMED(KK_BWD_TINY, leaf_bytes_, leaf_alg_, leaf_flops_,
             (k_bwd_leaves<<<(unsigned)cdiv(nsleaf_ * LPL, NT), NT, 0, s>>>(tleaf_, (int)nsleaf_, tlrow_, arena_, D_, xi_,
