@@ -99,14 +99,49 @@ __device__ __forceinline__ double csr_dot(const DCsr& A, int row, const double* 
   return s;
 }
 
+// Wave reductions with the pairing of the `for (o = 32; o; o >>= 1) a = op(a, __shfl_down(a, o))` tree
+// (lane i combines lane i + o; lane 0 ends with the same value bit for bit), without the LDS crossbar:
+// o = 32 / 16 by the gfx950 half-row swaps (v_permlane32_swap / v_permlane16_swap: the swapped-in half
+// is lane i + o for the lanes the tree reads), o = 8, 4, 2, 1 by DPP row_shl:o inside each 16-lane row.
+// (ds_bpermute costs an LDS round trip per step: k_final's level-1 tree took ~2 us, MADIPM_FINAL_DEBUG.)
+template <int O>
+__device__ __forceinline__ int lane_down_i32(int v) {
+  if constexpr (O == 32) {
+    const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (int)p[1];
+  } else if constexpr (O == 16) {
+    const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (int)p[1];
+  } else {
+    return __builtin_amdgcn_update_dpp(v, v, 0x100 + O, 0xf, 0xf, false);  // row_shl:O
+  }
+}
+template <int O>
+__device__ __forceinline__ double lane_down(double v) {
+  return __hiloint2double(lane_down_i32<O>(__double2hiint(v)), lane_down_i32<O>(__double2loint(v)));
+}
+template <int OP>
+__device__ __forceinline__ double wave_reduce(double a) {
+  a = comb(a, lane_down<32>(a), OP);
+  a = comb(a, lane_down<16>(a), OP);
+  a = comb(a, lane_down<8>(a), OP);
+  a = comb(a, lane_down<4>(a), OP);
+  a = comb(a, lane_down<2>(a), OP);
+  return comb(a, lane_down<1>(a), OP);
+}
+template <int O>
+__device__ __forceinline__ void argmin_step(double& a, int& b);
+__device__ __forceinline__ double wave_reduce_op(double a, int op) {
+  return op == OP_SUM ? wave_reduce<OP_SUM>(a) : (op == OP_MAX ? wave_reduce<OP_MAX>(a) : wave_reduce<OP_MIN>(a));
+}
+
 template <int NV>
 __device__ void block_partials(double (&v)[NV], const int (&ops)[NV], double* part, int base = 0, int bid = -1) {
   __shared__ double sh[NV][NT / 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
-    double a = v[k];
-    for (int o = 32; o > 0; o >>= 1) a = comb(a, __shfl_down(a, o, 64), ops[k]);
+    const double a = wave_reduce_op(v[k], ops[k]);
     if (lane == 0) sh[k][wv] = a;
   }
   __syncthreads();
@@ -127,6 +162,21 @@ __device__ __forceinline__ void amin_upd(double& v, int& ix, double nv, int ni) 
   const bool take = (nv < v) | ((nv == v) & (ni > ix));  // no short circuit: selects, not branches
   v = take ? nv : v;
   ix = take ? ni : ix;
+}
+
+template <int O>
+__device__ __forceinline__ void argmin_step(double& a, int& b) {
+  const double a2 = lane_down<O>(a);
+  const int b2 = lane_down_i32<O>(b);
+  amin_upd(a, b, a2, b2);
+}
+__device__ __forceinline__ void wave_argmin(double& a, int& b) {
+  argmin_step<32>(a, b);
+  argmin_step<16>(a, b);
+  argmin_step<8>(a, b);
+  argmin_step<4>(a, b);
+  argmin_step<2>(a, b);
+  argmin_step<1>(a, b);
 }
 
 #define GRID_LOOP(i, N) for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < (N); i += (int64_t)gridDim.x * blockDim.x)
@@ -347,7 +397,7 @@ __global__ __launch_bounds__(NT) void k_rhs(DV D, int mode, double mu_g, int res
       for (int k = 0; k < 4; ++k) a[k] += D.part[pidx(b, k)];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      for (int o = 32; o > 0; o >>= 1) a[k] += __shfl_down(a[k], o, 64);
+      a[k] = wave_reduce<OP_SUM>(a[k]);
       if (lane == 0) shm[k][wv] = a[k];
     }
     __syncthreads();
@@ -461,11 +511,7 @@ __device__ void block_argmin4(const double (&v)[4], const int (&ix)[4], double* 
   for (int k = 0; k < 4; ++k) {
     double a = v[k];
     int b = ix[k];
-    for (int o = 32; o > 0; o >>= 1) {
-      const double a2 = __shfl_down(a, o, 64);
-      const int b2 = __shfl_down(b, o, 64);
-      amin_upd(a, b, a2, b2);
-    }
+    wave_argmin(a, b);
     if (lane == 0) {
       sv[k][wv] = a;
       si[k][wv] = b;
@@ -1026,18 +1072,22 @@ __global__ __launch_bounds__(FT) void k_final(DV D, int kind, FinParams P) {
     ai[k] = (AL && b < nba) ? (int)aq[AL ? 4 + k : 0] : -1;
   }
   double e1 = (EV && b < P.nb_eval) ? eq : 0.0;
-  for (int o = 32; o > 0; o >>= 1) {
+  // every value's tree in lockstep (one latency chain for all of them), the __shfl_down pairing
+  auto stage = [&](auto otag) {
+    constexpr int O = decltype(otag)::value;
 #pragma unroll
-    for (int k = 0; k < NV; ++k) w1[k] = comb(w1[k], __shfl_down(w1[k], o, 64), fin_op(KIND, k));
+    for (int k = 0; k < NV; ++k) w1[k] = comb(w1[k], lane_down<O>(w1[k]), fin_op(KIND, k));
     if (AL)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const double a2 = __shfl_down(av[k], o, 64);
-        const int b2 = __shfl_down(ai[k], o, 64);
-        amin_upd(av[k], ai[k], a2, b2);
-      }
-    if (EV) e1 += __shfl_down(e1, o, 64);
-  }
+      for (int k = 0; k < 4; ++k) argmin_step<O>(av[k], ai[k]);
+    if (EV) e1 += lane_down<O>(e1);
+  };
+  stage(std::integral_constant<int, 32>{});
+  stage(std::integral_constant<int, 16>{});
+  stage(std::integral_constant<int, 8>{});
+  stage(std::integral_constant<int, 4>{});
+  stage(std::integral_constant<int, 2>{});
+  stage(std::integral_constant<int, 1>{});
   __shared__ double shv[NL2][FT / 64];
   __shared__ int shx[4][FT / 64];
   if (lane == 0) {
