@@ -2419,6 +2419,101 @@ __global__ __launch_bounds__(NT, SYRK_WAVES) void k_lb_syrk(const double* __rest
   }
 }
 
+// Trailing update of a big front's panel group on 128 x 128 lower tiles (the group's K = 64 kpan columns,
+// tiles relative to the group's end c0): C -= (L_I D) L_J^T, four waves x 64 x 64 quadrants of f64 MFMA
+// 16x16x4, K-chunks of 16 double-buffered through LDS (k_lb_syrk's engine on the front's own columns).
+// A 128-tile reads 2 x 128 K doubles per 2 x 128^2 K flops — twice k_big_update's 64-tile arithmetic
+// intensity, on the update that carries ~90 % of neos' factorisation flops.
+__global__ __launch_bounds__(NT, 2) void k_big_upd128(FrontTab T, const int32_t* __restrict__ list, int step, int kpan,
+                                                     double* __restrict__ arena, const double* __restrict__ D) {
+  __shared__ __attribute__((aligned(16))) double As[2][SYK * SYLD];  // (L D)[I rows]
+  __shared__ __attribute__((aligned(16))) double Bs[2][SYK * SYLD];  // L[J rows]
+  int s, tij;
+  task_of(list, s, tij);
+  const int ti = tij & 0xffff, tj = (tij >> 16) & 0x7fff;
+  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+  const int g0 = (step / kpan) * kpan;
+  const int k0 = 64 * g0, k1 = min(64 * (g0 + kpan), w);  // K range = the group's columns
+  const int c0 = k1;
+  const int I0 = c0 + ti * SYT, J0 = c0 + tj * SYT;
+  double* __restrict__ F = arena + T.l_off[s];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wm = (wv >> 1) * 64, wn = (wv & 1) * 64;
+  const int lr = tid & (SYT - 1), lk = tid >> 7;
+  dbl4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+  double ra[8], rb[8], rd[8];
+  const int ri = min(I0 + lr, r - 1), rj = min(J0 + lr, r - 1);
+  auto gload = [&](int kb) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int kc = min(kb + lk + 2 * q, k1 - 1);
+      const int64_t col = (int64_t)kc * r;
+      ra[q] = F[ri + col];
+      rb[q] = F[rj + col];
+      rd[q] = D[f0 + kc];
+    }
+  };
+  auto sstore = [&](int kb, int buf) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const bool ok = kb + lk + 2 * q < k1;
+      As[buf][(lk + 2 * q) * SYLD + lr] = (ok && I0 + lr < r) ? ra[q] * rd[q] : 0.0;
+      Bs[buf][(lk + 2 * q) * SYLD + lr] = (ok && J0 + lr < r) ? rb[q] : 0.0;
+    }
+  };
+  gload(k0);
+  sstore(k0, 0);
+  __syncthreads();
+  int buf = 0;
+  for (int kb = k0; kb < k1; kb += SYK) {
+    const bool more = kb + SYK < k1;
+    if (more) gload(kb + SYK);
+#pragma unroll
+    for (int k4 = 0; k4 < SYK / 4; ++k4) {
+      const int kk = 4 * k4 + (lane >> 4);
+      double fa[4], fb[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        fa[t] = Bs[buf][kk * SYLD + wn + 16 * t + (lane & 15)];
+        fb[t] = As[buf][kk * SYLD + wm + 16 * t + (lane & 15)];
+      }
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[a], fb[b], acc[a][b], 0, 0, 0);
+    }
+    if (more) {
+      sstore(kb + SYK, buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+  // acc[a][b][g]: row i = I0 + wm + 16 b + (lane & 15), column j = J0 + wn + 16 a + (lane >> 4) + 4 g;
+  // the C reads of a column block from clamped addresses, all in flight, the writes masked
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    double fv[4][4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int i = min(I0 + wm + 16 * b + (lane & 15), r - 1), j = min(J0 + wn + 16 * a + (lane >> 4) + 4 * g, r - 1);
+        fv[b][g] = F[i + (int64_t)j * r];
+      }
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int i = I0 + wm + 16 * b + (lane & 15), j = J0 + wn + 16 * a + (lane >> 4) + 4 * g;
+        if (i < r && j <= i) F[i + (int64_t)j * r] = fv[b][g] - acc[a][b][g];
+      }
+  }
+}
+
 // forward: s_j = b(c_j) / d_j, t = W s (two passes: column chunks of LBF_COLS -> partials, then the
 // chunks summed in order), the group's update vector = -t; the members' forward values are b(c_j)
 constexpr int LBF_COLS = 256;
@@ -2814,6 +2909,43 @@ __device__ __forceinline__ void publish_flag(int32_t* f, int epoch) {
   }
 }
 
+// Triangular solves of a 64-pivot diagonal block by one wave, 16 pivots per batch: the batch's L
+// entries are loaded first, then each pivot's value is broadcast by v_readlane (an SGPR, a few cycles)
+// — a __shfl (ds_bpermute) per pivot put an LDS round trip on the chain: ~5 us per 64-pivot block.
+// forward: a[lane] -= L(lane, t) a[t] for t < lane, t < kw; L(i, t) at Ld[t * 65 + i]
+__device__ __forceinline__ double tri_fwd64(double a, const double* Ld, int kw, int lane) {
+  for (int t0 = 0; t0 < kw; t0 += 16) {
+    double lb[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) lb[k] = Ld[min(t0 + k, 63) * 65 + lane];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int tt = t0 + k;
+      const double xt = readlane_f64(a, min(tt, 63));
+      const double na = a - lb[k] * xt;
+      a = (lane > tt && tt < kw) ? na : a;
+    }
+  }
+  return a;
+}
+// backward (transposed): a[lane] -= L(t, lane) a[t] for t > lane, t < kw, from t = kw - 1 down;
+// L(t, j) at Ld[t * 65 + j]
+__device__ __forceinline__ double tri_bwd64(double a, const double* Ld, int kw, int lane) {
+  for (int t1 = kw - 1; t1 > 0; t1 -= 16) {
+    double lb[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) lb[k] = Ld[max(t1 - k, 0) * 65 + lane];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int tt = t1 - k;
+      const double xt = readlane_f64(a, max(tt, 0));
+      const double na = a - lb[k] * xt;
+      a = (lane < tt && tt > 0) ? na : a;
+    }
+  }
+  return a;
+}
+
 // Forward, big fronts: task = (front, 64-row block i).  acc(rows) = v(rows) - sum_{panels p < i} L(rows,p) x_p,
 // then (pivot block) x_i = L_ii^{-1} acc, published through flags[flag_off[front] + i].
 __global__ __launch_bounds__(NT) void k_fwd_big(FrontTab T, const SolveTask* __restrict__ tasks, int ntasks,
@@ -2878,10 +3010,7 @@ __global__ __launch_bounds__(NT) void k_fwd_big(FrontTab T, const SolveTask* __r
     if (g == 0) {
       double a = (lane < nrow) ? vwork[T.row_ptr[s] + row] - ((part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]))
                                : 0.0;
-      for (int tt = 0; tt < kw; ++tt) {
-        const double xt = __shfl(a, tt, 64);
-        if (lane > tt) a -= Ld[tt * 65 + lane] * xt;
-      }
+      a = tri_fwd64(a, Ld, kw, lane);
       if (lane < nrow) {
         if (row < w)
           xi[f0 + row] = a;
@@ -3013,10 +3142,7 @@ __global__ __launch_bounds__(NT) void k_bwd_big(FrontTab T, const SolveTask* __r
         const int c = f0 + c0 + lane;
         a = xi[c] / D[c] - ((part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]));
       }
-      for (int tt = kw - 1; tt > 0; --tt) {
-        const double xt = __shfl(a, tt, 64);
-        if (lane < tt) a -= Ld[tt * 65 + lane] * xt;
-      }
+      a = tri_bwd64(a, Ld, kw, lane);
       if (lane < kw) {
         const int c = f0 + c0 + lane;
         xi[c] = a;
@@ -4209,8 +4335,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       int maxsteps = 0;
       for (int s : big) maxsteps = std::max<int>(maxsteps, (int)cdiv(S.first[s + 1] - S.first[s], 64));
       for (int p = 0; p < maxsteps; ++p) {
-        std::vector<int32_t> td, tt, tu;  // (front, item) pairs
-        double kb[3] = {0, 0, 0}, kf[3] = {0, 0, 0}, ka = 0;
+        std::vector<int32_t> td, tt, tu, tu128;  // (front, item) pairs
+        double kb[4] = {0, 0, 0, 0}, kf[4] = {0, 0, 0, 0}, ka = 0;
         for (int s : big) {
           const int w = S.first[s + 1] - S.first[s], r = S.nrows[s];
           const int npan = (int)cdiv(w, 64);
@@ -4236,17 +4362,18 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
               for (int i = j; i < nt; ++i) tu.insert(tu.end(), {s, i | (j << 16)});
             kb[2] += 8.0 * (2.0 * nb * nc + nb * dk + nc * dk);  // C in/out + the panel rows once
             kf[2] += 2.0 * dk * nc * (nb - 0.5 * nc);
-          } else {
-            const int c0 = gend, ntt = (int)cdiv(r - c0, 64);
+          } else {  // 128 x 128 tiles (k_big_upd128)
+            const int c0 = gend, ntt = (int)cdiv(r - c0, 128);
             const double K = gend - 64 * g0, nbt = r - c0;
             for (int i = 0; i < ntt; ++i)
-              for (int j = 0; j <= i; ++j) tu.insert(tu.end(), {s, (int32_t)((uint32_t)(i | (j << 16)) | 0x80000000u)});
-            kb[2] += 8.0 * (nbt * (nbt + 1) + 2.0 * nbt * K);  // C in/out once per group + the group's panels
-            kf[2] += K * nbt * (nbt + 1);
+              for (int j = 0; j <= i; ++j) tu128.insert(tu128.end(), {s, i | (j << 16)});
+            kb[3] += 8.0 * (nbt * (nbt + 1) + 2.0 * nbt * K);  // C in/out once per group + the group's panels
+            kf[3] += K * nbt * (nbt + 1);
           }
         }
-        const std::pair<int, std::vector<int32_t>*> kinds[3] = {{BIG_DIAG, &td}, {BIG_TRSM, &tt}, {BIG_UPDATE, &tu}};
-        for (int q = 0; q < 3; ++q) {
+        const std::pair<int, std::vector<int32_t>*> kinds[4] = {
+            {BIG_DIAG, &td}, {BIG_TRSM, &tt}, {BIG_UPDATE, &tu}, {BIG_UPDATE128, &tu128}};
+        for (int q = 0; q < 4; ++q) {
           const auto& kv = kinds[q];
           if (kv.second->empty()) continue;
           align2();
@@ -4712,6 +4839,10 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
       case BIG_UPDATE:
         TIMED(KK_UPDATE, L.bytes, 0.0, L.flops,
               (k_big_update<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, big_kpan_, arena_, D_)));
+        break;
+      case BIG_UPDATE128:
+        TIMED(KK_UPDATE, L.bytes, 0.0, L.flops,
+              (k_big_upd128<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, big_kpan_, arena_, D_)));
         break;
       case LB_BUILD:
         TIMED(KK_LB_BUILD, L.bytes, L.alg, 0.0,

@@ -233,7 +233,7 @@ class LDLSolver : public LinSolver {
 
  private:
   enum Kind { ASSEMBLE = 0, SMALL32 = 1, SMALL64 = 2, SMALL128 = 3, BIG_DIAG = 4, BIG_TRSM = 5, BIG_UPDATE = 6,
-              LB_BUILD = 7, LB_SYRK = 8, MICRO = 9, SMALL192 = 10, FTREE = 11 };
+              LB_BUILD = 7, LB_SYRK = 8, MICRO = 9, SMALL192 = 10, FTREE = 11, BIG_UPDATE128 = 12 };
   struct Launch {
     int kind;
     int step;       // panel step for BIG_DIAG / BIG_TRSM / BIG_UPDATE
