@@ -495,32 +495,34 @@ __global__ __launch_bounds__(NT) void k_asm_chunks(const int64_t* __restrict__ g
   part[c] = v;
 }
 
-// Phase 2: one workgroup (1024 threads) per 64x64 lower tile of F (SymbolicPlan step 10): entry =
-// sum of its chunk sums in order, staged in LDS; then the big children's update blocks are added
-// child by child (coalesced along the child's rows); the tile is written to the front (big: arena,
-// ld r; small: scratch, ld r).  No atomics, deterministic.
-constexpr int ANT = 1024;
+// Phase 2: one workgroup (1024 threads) per 64x64 lower tile of F (SymbolicPlan step 10): thread t
+// owns the tile entries (row t & 63, columns t >> 6 + 16 k), k < 4.  Entry = sum of its chunk sums in
+// order; then the big children's update blocks are added child by child in child order, in the
+// owner's registers: per batch of ABN children the tile's row and column maps (tile row -> child row,
+// or -1) are built in LDS (one barrier), then every thread issues the batch's loads (ABN x 4 from
+// clamped addresses) and adds them, masked, in child order.  No atomics, deterministic, and no
+// barrier per child (r3 put one barrier and one round trip per child and tile: neos 8 ms per
+// factorisation).  The tile is written to the front (big: arena, ld r; small: scratch, ld r).
+constexpr int ANT = 1024, ABN = 8;
 __global__ __launch_bounds__(ANT) void k_assemble(FrontTab T, const SymbolicPlan::AsmTile* __restrict__ tiles,
                                                   const int32_t* __restrict__ gptr, const double* __restrict__ part,
                                                   const int32_t* __restrict__ bt, double* __restrict__ arena,
                                                   double* __restrict__ fscratch) {
-  __shared__ double Ft[64 * 64];
   const SymbolicPlan::AsmTile tl = tiles[blockIdx.x];
   const int s = tl.front, ti = tl.tij & 0xffff, tj = (tl.tij >> 16) & 0x7fff;
   const bool acc = tl.tij < 0;  // SymbolicPlan::kAccumulate: F += tile (sharded top fronts, phase 2)
   const int r = T.nrows[s];
   const int I0 = ti * 64, J0 = tj * 64;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  double v[4] = {0.0, 0.0, 0.0, 0.0};
   if (tl.gptr >= 0) {
     const int32_t* __restrict__ gp = gptr + tl.gptr;
     const double* __restrict__ pc = part + tl.gchk;
     int q0[4], q1[4];
-    double v[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       q0[k] = gp[tid + k * ANT];
       q1[k] = gp[tid + k * ANT + 1];
-      v[k] = 0.0;
     }
     int len = 0;
 #pragma unroll
@@ -536,88 +538,69 @@ __global__ __launch_bounds__(ANT) void k_assemble(FrontTab T, const SymbolicPlan
 #pragma unroll
         for (int u = 0; u < 4; ++u) v[k] += x[k][u];
     }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) Ft[tid + k * ANT] = v[k];
-  } else {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) Ft[tid + k * ANT] = 0.0;
   }
   if (tl.bt1 > tl.bt0) {
-    // Big children's update blocks, child by child (fixed order: a barrier between children, whose
-    // entries may land on the same tile entry).  The children's symbolic table (bt entry, U offset
-    // and ld, row-map offset) is staged in LDS per 64 children, so a child's operand loads (its row
-    // map and U entries, ~9 per lane) are ONE round trip, issued while the previous child's adds run
-    // (r2 read bt -> u_off -> rel / U per child: three dependent round trips each).  A wave takes 4
-    // columns (b0 + wv + 16 j) and a lane one row (a0 + lane) of the child's <= 64 x 64 block; masked
-    // lanes load from inside the same column (no extra lines), added nothing.
-    constexpr int CH = 64;
-    __shared__ int32_t sbt[CH * 5], sld[CH];
-    __shared__ int64_t suo[CH], srp[CH];
-    constexpr int NW = ANT / 64;
-    struct Ops {  // one child's operands for this lane (raw: the row map is applied at the add)
-      double u[4];
-      int ra, rb[4], ok;
-    };
-    auto load = [&](int k, Ops& o) {
-      const int b0 = sbt[5 * k + 1], b1 = sbt[5 * k + 2], a0 = sbt[5 * k + 3], a1 = sbt[5 * k + 4];
-      const double* __restrict__ U = arena + suo[k];
-      const int64_t ldc = sld[k];
-      const int32_t* __restrict__ rel = T.rel + srp[k];
-      const int a = a0 + lane, ac = min(a, a1 - 1);
-      o.ra = rel[ac];
-      o.ok = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int bk = b0 + wv + NW * j, bc = min(bk, b1 - 1);
-        o.rb[j] = rel[bc];
-        o.u[j] = U[max(ac, bc) + (int64_t)bc * ldc];
-        o.ok |= ((bk < b1) & (a < a1) & (a >= bk)) << j;
-      }
-    };
-    auto add = [&](const Ops& o) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if ((o.ok >> j) & 1) Ft[(o.ra - I0) + (o.rb[j] - J0) * 64] += o.u[j];
-    };
-    for (int kc = tl.bt0; kc < tl.bt1; kc += CH) {
-      const int nk = min(CH, tl.bt1 - kc);
-      __syncthreads();  // the chunk sums are in Ft; the previous table is no longer read
-      if (tid < nk * 5) sbt[tid] = bt[5 * kc + tid];
-      __syncthreads();
-      if (tid < nk) {
-        const int c = sbt[5 * tid];
-        suo[tid] = T.u_off[c];
-        sld[tid] = (int32_t)T.u_ld[c];
-        srp[tid] = T.rel_ptr[c];
+    __shared__ int32_t rmap[ABN][64], cmap[ABN][64];
+    __shared__ int64_t suo[ABN];
+    __shared__ int32_t sld[ABN];
+    for (int kc = tl.bt0; kc < tl.bt1; kc += ABN) {
+      const int nk = min(ABN, tl.bt1 - kc);
+      // maps of the batch: -1, then child rows a in [a0, a1) at their tile rows (rel ascending: each
+      // tile row receives at most one child row), the same for the columns
+      if (tid < ABN * 64) {
+        rmap[tid >> 6][lane] = -1;
+        cmap[tid >> 6][lane] = -1;
       }
       __syncthreads();
-      // two operand sets, alternately loaded and added (no register copies: a copy of a loaded value
-      // waits for it, which serialised the pipeline)
-      // the loads are issued unconditionally (clamped child: a conditional issue leaves the wait
-      // counter ambiguous and the compiler waits for everything)
-      Ops o0, o1;
-      load(0, o0);
-      for (int k = 0; k < nk; k += 2) {
-        load(min(k + 1, nk - 1), o1);
-        add(o0);
-        __syncthreads();
-        if (k + 1 >= nk) break;
-        load(min(k + 2, nk - 1), o0);
-        add(o1);
-        __syncthreads();
+      if (tid < nk * 64) {
+        const int k = tid >> 6;
+        const int32_t* e = bt + 5 * (kc + k);
+        const int c = e[0], b0 = e[1], b1 = e[2], a0 = e[3], a1 = e[4];
+        const int32_t* __restrict__ rel = T.rel + T.rel_ptr[c];
+        if (a0 + lane < a1) rmap[k][rel[a0 + lane] - I0] = a0 + lane;
+        if (b0 + lane < b1) cmap[k][rel[b0 + lane] - J0] = b0 + lane;
+        if (lane == 0) {
+          suo[k] = T.u_off[c];
+          sld[k] = (int32_t)T.u_ld[c];
+        }
       }
+      __syncthreads();
+      // every load of the batch first (clamped to entry (0, 0) of the child's block), then the adds
+      double x[ABN][4];
+      int ok[ABN];
+#pragma unroll
+      for (int k = 0; k < ABN; ++k) {
+        const int kk = min(k, nk - 1);
+        const int a = rmap[kk][lane];
+        const double* __restrict__ U = arena + suo[kk];
+        const int64_t ldc = sld[kk];
+        ok[k] = 0;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int bb = cmap[kk][wv + 16 * m];
+          const bool hit = k < nk && a >= 0 && bb >= 0 && a >= bb;
+          x[k][m] = U[(hit ? a : 0) + (int64_t)(hit ? bb : 0) * ldc];
+          ok[k] |= (int)hit << m;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < ABN; ++k)
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+          if ((ok[k] >> m) & 1) v[m] += x[k][m];
+      __syncthreads();  // the maps are rebuilt by the next batch
     }
   }
-  __syncthreads();
   const int64_t fso = T.fs_off[s];
   double* __restrict__ F = (fso >= 0 ? fscratch + fso : arena + T.l_off[s]);
   const int i = I0 + lane;
   const int img = (fso >= 0) ? T.fs_img[s] : 0;  // tree front: write its LDS image
-  for (int jj = wv; jj < 64; jj += ANT / 64) {
-    const int j = J0 + jj;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int j = J0 + wv + 16 * m;
     if (i < r && j < r && i >= j) {
       const int64_t q = !img ? i + (int64_t)j * r : (r > 128 ? (int64_t)((j * (2 * r - j - 1)) >> 1) + i : i + (int64_t)j * (r | 1));
-      F[q] = acc ? F[q] + Ft[lane + jj * 64] : Ft[lane + jj * 64];
+      F[q] = acc ? F[q] + v[m] : v[m];
     }
   }
 }
