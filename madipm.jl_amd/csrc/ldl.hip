@@ -1549,11 +1549,41 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
     }
   };
   load_group(e, T.fold_prod + tb_po[0] + tid, 0, tb_pl[0]);
+  // the leaf rows' K entries of batch b + 1 are loaded into registers during batch b (indices before
+  // its pivots, values before its products) and stored after its products: only batch 0's gather is
+  // exposed (r3: every batch's gather, two dependent round trips, lay on the front's critical path).
+  // A batch of more than RPT x FTN rows gathers its remaining passes in place.
+  int32_t sa[RPT], sb[RPT];
+  double va[RPT], vb[RPT];
+  auto gather_idx = [&](int64_t j0, int nrow, int q0) {
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+      const int q = q0 + u * FTN + tid;
+      sa[u] = (q < nrow) ? T.ab_src0[j0 + q] : -1;
+      sb[u] = (q < nrow) ? T.ab_src1[j0 + q] : -1;
+    }
+  };
+  auto gather_val = [&]() {
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+      va[u] = (sa[u] >= 0) ? Kx[sa[u]] : 0.0;
+      vb[u] = (sb[u] >= 0) ? Kx[sb[u]] : 0.0;
+    }
+  };
+  auto gather_store = [&](int nrow, int q0) {
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+      const int q = q0 + u * FTN + tid;
+      if (q < nrow) LQ[q] = double2{va[u], vb[u]};
+    }
+  };
+  gather_idx(tb_j[0], (int)(tb_j[1] - tb_j[0]), 0);
+  gather_val();
   for (int b = 0; b < nb; ++b) {
     const int k0 = tb_k[b], k1 = tb_k[b + 1];
     const int64_t j0 = tb_j[b];
     const int nrow = (int)(tb_j[b + 1] - j0), nleaf = k1 - k0;
-    // (1) the leaf rows' K entries (leaf tables loaded beside them)
+    // (1) the leaf rows' K entries (the first pass in registers already; leaf tables loaded beside them)
     int32_t lf[2], lw[2];
     int64_t lo[2];
 #pragma unroll
@@ -1563,25 +1593,11 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
       lw[h] = (k < nleaf) ? T.ab_wrc[k0 + k] : 0;
       lo[h] = (k < nleaf) ? T.ab_loff[k0 + k] : 0;
     }
-    for (int q0 = 0; q0 < nrow; q0 += RPT * FTN) {
-      int32_t sa[RPT], sb[RPT];
-#pragma unroll
-      for (int u = 0; u < RPT; ++u) {
-        const int q = q0 + u * FTN + tid;
-        sa[u] = (q < nrow) ? T.ab_src0[j0 + q] : -1;
-        sb[u] = (q < nrow) ? T.ab_src1[j0 + q] : -1;
-      }
-      double va[RPT], vb[RPT];
-#pragma unroll
-      for (int u = 0; u < RPT; ++u) {
-        va[u] = (sa[u] >= 0) ? Kx[sa[u]] : 0.0;
-        vb[u] = (sb[u] >= 0) ? Kx[sb[u]] : 0.0;
-      }
-#pragma unroll
-      for (int u = 0; u < RPT; ++u) {
-        const int q = q0 + u * FTN + tid;
-        if (q < nrow) LQ[q] = double2{va[u], vb[u]};
-      }
+    gather_store(nrow, 0);
+    for (int q0 = RPT * FTN; q0 < nrow; q0 += RPT * FTN) {
+      gather_idx(j0, nrow, q0);
+      gather_val();
+      gather_store(nrow, q0);
     }
     for (int k = tid, h = 0; k < nleaf; k += FTN, ++h) {
       const int q0 = (h == 0) ? lf[0] : (h == 1 ? lf[1] : (int)(T.ab_first[k0 + k] - j0));
@@ -1593,6 +1609,8 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
     }
     __syncthreads();
     lap(0);
+    const bool pre = b + 1 < nb;  // prefetch the next batch's first pass
+    if (pre) gather_idx(tb_j[b + 1], (int)(tb_j[b + 2] - tb_j[b + 1]), 0);
     // (2) per leaf: pivots (+ D and the pivot check)
     for (int k = tid; k < nleaf; k += FTN) {
       const int f0 = T.ab_f0[k0 + k], wrc = pwrc[k], w = wrc & 255, rc = wrc >> 8;
@@ -1638,6 +1656,7 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
     }
     __syncthreads();
     lap(2);
+    if (pre) gather_val();
     // (4) this thread's chunks of the destination-sorted products (entry k of chunk c at NCH k + c:
     // each load instruction is coalesced)
     const uint2* __restrict__ P = T.fold_prod + tb_po[b] + tid;
