@@ -18,6 +18,8 @@
 // spins on its counter, overlapped with the factorisation and the speculated directions).
 #include <algorithm>
 #include <array>
+#include <atomic>
+#include <thread>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -1307,43 +1309,123 @@ int MPCSolver::blocks(int64_t n) const {
 // of a dependent chain of rows (the row loads are latency-bound)
 int MPCSolver::spmv_blocks(int64_t rows) const { return blocks(rows * spmv_g_); }
 
+// ---- host construction helpers, threaded for the dense-QP config (5e8 entries in A): every O(nnz) pass
+// runs on analysis_threads() host threads over contiguous input chunks, with per-thread counts and
+// offsets in thread order, so the result is the one-thread result bit for bit (r3: 38 s of analysis_s
+// on the box, mostly single-threaded passes and growing vectors over the 5e8 entries).
+template <class F>
+static void par_range(int64_t n, F f, int64_t grain = (int64_t)1 << 20) {
+  const int T = (int)std::min<int64_t>(analysis_threads(), std::max<int64_t>(1, n / grain));
+  if (T <= 1) {
+    f(0, (int64_t)0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t) th.emplace_back(f, t, n * t / T, n * (t + 1) / T);
+  for (auto& x : th) x.join();
+}
+static int par_threads(int64_t n, int64_t grain = (int64_t)1 << 20) {
+  return (int)std::min<int64_t>(analysis_threads(), std::max<int64_t>(1, n / grain));
+}
+
+// CSR (sorted by (row, col), duplicates summed in input order) of the COO (r, c, v): a stable counting
+// sort by row — per-thread row counts over input chunks, offsets in thread order — then each row's
+// run sorted by column only when it is not already (O(nnz) for the usual column- or row-major input;
+// a comparison sort of 1e9 dense-QP entries took minutes) and duplicates merged
+static void csr_from_coo(int nrow, int64_t nnz, const int32_t* r, const int32_t* c, const double* v,
+                         std::vector<int64_t>& rp, std::vector<int32_t>& ci, std::vector<double>& cv) {
+  const int T = par_threads(nnz);
+  std::vector<std::vector<int64_t>> cnt(T, std::vector<int64_t>(nrow + 1, 0));
+  auto chunk = [&](int t) { return std::make_pair(nnz * t / T, nnz * (t + 1) / T); };
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        auto [k0, k1] = chunk(t);
+        int64_t* cn = cnt[t].data();
+        for (int64_t k = k0; k < k1; ++k) cn[r[k]]++;
+      });
+    for (auto& x : th) x.join();
+  }
+  std::vector<int64_t> start(nrow + 1, 0);
+  for (int i = 0; i < nrow; ++i) {
+    int64_t acc = start[i];
+    for (int t = 0; t < T; ++t) {
+      const int64_t c_ = cnt[t][i];
+      cnt[t][i] = acc;  // this thread's first slot in row i
+      acc += c_;
+    }
+    start[i + 1] = acc;
+  }
+  std::vector<int32_t> tc(nnz);
+  std::vector<double> tv(nnz);
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        auto [k0, k1] = chunk(t);
+        int64_t* off = cnt[t].data();
+        for (int64_t k = k0; k < k1; ++k) {
+          const int64_t q = off[r[k]]++;
+          tc[q] = c[k];
+          tv[q] = v[k];
+        }
+      });
+    for (auto& x : th) x.join();
+  }
+  // per row: sort if needed (stable: duplicates keep input order), count the distinct columns
+  std::vector<int64_t> uniq(nrow + 1, 0);
+  par_range(nrow, [&](int, int64_t i0, int64_t i1) {
+    std::vector<std::pair<int32_t, double>> buf;
+    for (int64_t i = i0; i < i1; ++i) {
+      const int64_t b = start[i], e = start[i + 1];
+      bool sorted = true;
+      for (int64_t q = b; q + 1 < e && sorted; ++q) sorted = tc[q] <= tc[q + 1];
+      if (!sorted) {
+        buf.clear();
+        for (int64_t q = b; q < e; ++q) buf.emplace_back(tc[q], tv[q]);
+        std::stable_sort(buf.begin(), buf.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+        for (int64_t q = b; q < e; ++q) tc[q] = buf[q - b].first, tv[q] = buf[q - b].second;
+      }
+      int64_t u = 0;
+      for (int64_t q = b; q < e; ++q) u += (q == b || tc[q] != tc[q - 1]);
+      uniq[i + 1] = u;
+    }
+  }, 4096);
+  for (int i = 0; i < nrow; ++i) uniq[i + 1] += uniq[i];
+  if (uniq[nrow] == nnz) {  // no duplicates: the sorted runs are the CSR
+    rp = std::move(start);
+    ci = std::move(tc);
+    cv = std::move(tv);
+    return;
+  }
+  rp = uniq;
+  ci.assign(uniq[nrow], 0);
+  cv.assign(uniq[nrow], 0.0);
+  par_range(nrow, [&](int, int64_t i0, int64_t i1) {
+    for (int64_t i = i0; i < i1; ++i) {
+      int64_t o = rp[i] - 1;
+      for (int64_t q = start[i]; q < start[i + 1]; ++q) {
+        if (q == start[i] || tc[q] != tc[q - 1]) {
+          ++o;
+          ci[o] = tc[q];
+          cv[o] = tv[q];
+        } else {
+          cv[o] += tv[q];
+        }
+      }
+    }
+  }, 4096);
+}
 static void csr_from_coo(int nrow, const std::vector<int32_t>& r, const std::vector<int32_t>& c,
                          const std::vector<double>& v, std::vector<int64_t>& rp, std::vector<int32_t>& ci,
                          std::vector<double>& cv) {
-  // sorted by (row, col), duplicates summed in input order.  Counting sort by row (stable), then each
-  // row's run sorted by column only when it is not already (O(nnz) for the usual column-major or
-  // row-major input; a comparison sort of 1e9 dense-QP entries took minutes)
-  const int64_t nnz = (int64_t)r.size();
-  std::vector<int64_t> start(nrow + 1, 0);
-  for (int64_t k = 0; k < nnz; ++k) start[r[k] + 1]++;
-  for (int i = 0; i < nrow; ++i) start[i + 1] += start[i];
-  std::vector<int64_t> idx(nnz);
-  {
-    std::vector<int64_t> fill(start.begin(), start.end() - 1);
-    for (int64_t k = 0; k < nnz; ++k) idx[fill[r[k]]++] = k;
-  }
-  rp.assign(nrow + 1, 0);
-  ci.clear();
-  cv.clear();
-  ci.reserve(nnz);
-  cv.reserve(nnz);
-  for (int i = 0; i < nrow; ++i) {
-    const auto b = idx.begin() + start[i], e = idx.begin() + start[i + 1];
-    bool sorted = true;
-    for (auto q = b; q + 1 < e && sorted; ++q) sorted = c[*q] <= c[*(q + 1)];
-    if (!sorted) std::stable_sort(b, e, [&](int64_t x, int64_t y) { return c[x] < c[y]; });
-    const size_t row0 = ci.size();
-    for (auto q = b; q < e; ++q) {
-      const int64_t k = *q;
-      if (ci.size() > row0 && ci.back() == c[k]) {
-        cv.back() += v[k];
-        continue;
-      }
-      ci.push_back(c[k]);
-      cv.push_back(v[k]);
-    }
-    rp[i + 1] = (int64_t)ci.size();
-  }
+  csr_from_coo(nrow, (int64_t)r.size(), r.data(), c.data(), v.data(), rp, ci, cv);
+}
+template <class T>
+static void par_copy(std::vector<T>& dst, const T* src, int64_t n) {
+  dst.resize(n);
+  par_range(n, [&](int, int64_t a, int64_t b) { std::copy(src + a, src + b, dst.data() + a); }, (int64_t)1 << 22);
 }
 
 MPCSolver::MPCSolver(const madipm_qp& qp, const madipm_options& opt, Comm* comm) : opt_(opt), comm_(comm) {
@@ -1400,13 +1482,20 @@ void MPCSolver::setup_host(const madipm_qp& q) {
   P.Hr.assign(q.Hrows, q.Hrows + q.nnzh);
   P.Hc.assign(q.Hcols, q.Hcols + q.nnzh);
   P.Hv.assign(q.Hvals, q.Hvals + q.nnzh);
-  P.Ar.assign(q.Arows, q.Arows + q.nnzj);
-  P.Ac.assign(q.Acols, q.Acols + q.nnzj);
-  P.Av.assign(q.Avals, q.Avals + q.nnzj);
+  par_copy(P.Ar, q.Arows, q.nnzj);
+  par_copy(P.Ac, q.Acols, q.nnzj);
+  par_copy(P.Av, q.Avals, q.nnzj);
   for (int64_t k = 0; k < q.nnzh; ++k)
     MADIPM_REQUIRE(P.Hr[k] >= P.Hc[k] && P.Hr[k] < nx && P.Hc[k] >= 0, "H must be lower-triangular COO in range");
-  for (int64_t k = 0; k < q.nnzj; ++k)
-    MADIPM_REQUIRE(P.Ar[k] >= 0 && P.Ar[k] < m && P.Ac[k] >= 0 && P.Ac[k] < nx, "A index out of range");
+  {
+    std::atomic<bool> bad{false};
+    par_range(q.nnzj, [&](int, int64_t a, int64_t b) {
+      bool ok = true;
+      for (int64_t k = a; k < b; ++k) ok &= P.Ar[k] >= 0 && P.Ar[k] < m && P.Ac[k] >= 0 && P.Ac[k] < nx;
+      if (!ok) bad = true;
+    });
+    MADIPM_REQUIRE(!bad, "A index out of range");
+  }
   // ---- index sets: MadNLP.get_index_constraints (EnforceEquality, MakeParameter) [EXT]
   for (int i = 0; i < m; ++i)
     if (P.lcon[i] != P.ucon[i]) P.ind_ineq.push_back(i);
@@ -1487,7 +1576,16 @@ void MPCSolver::setup_host(const madipm_qp& q) {
     for (double v : g) gmax = std::max(gmax, std::fabs(v));
     P.obj_scale = gmax > 0 ? std::min(1.0, 100.0 / gmax) : 1.0;
     std::vector<double> rowmax(m, 0.0);
-    for (size_t k = 0; k < P.Av.size(); ++k) rowmax[P.Ar[k]] = std::max(rowmax[P.Ar[k]], std::fabs(P.Av[k]));
+    {  // per-thread row maxima, then their maximum (order-free)
+      const int64_t nz = (int64_t)P.Av.size();
+      std::vector<std::vector<double>> rm(par_threads(nz), std::vector<double>(m, 0.0));
+      par_range(nz, [&](int t, int64_t a, int64_t b) {
+        double* x = rm[t].data();
+        for (int64_t k = a; k < b; ++k) x[P.Ar[k]] = std::max(x[P.Ar[k]], std::fabs(P.Av[k]));
+      });
+      for (const auto& x : rm)
+        for (int i = 0; i < m; ++i) rowmax[i] = std::max(rowmax[i], x[i]);
+    }
     for (int i = 0; i < m; ++i) P.con_scale[i] = std::min(1.0, 100.0 / rowmax[i]);
     for (int k = 0; k < P.ns; ++k) {
       const double cs = P.con_scale[P.ind_ineq[k]];
@@ -1546,16 +1644,35 @@ void MPCSolver::setup_host(const madipm_qp& q) {
   // scaled Jacobian with slack columns (m x n); fixed columns zeroed (their term -> cfix)
   std::vector<int32_t> jr, jc;
   std::vector<double> jv;
-  for (size_t k = 0; k < P.Av.size(); ++k) {
-    const int r = P.Ar[k], c = P.Ac[k];
-    const double v = P.con_scale[r] * P.Av[k];
-    if (P.fixed[c]) {
-      cfix[r] += v * P.x[c];
-      continue;
+  {
+    const int64_t nz = (int64_t)P.Av.size();
+    bool anyfix = false;
+    for (int i = 0; i < nx && !anyfix; ++i) anyfix = P.fixed[i];
+    if (anyfix) {  // cfix sums in input order: the sequential pass
+      for (int64_t k = 0; k < nz; ++k) {
+        const int r = P.Ar[k], c = P.Ac[k];
+        const double v = P.con_scale[r] * P.Av[k];
+        if (P.fixed[c]) {
+          cfix[r] += v * P.x[c];
+          continue;
+        }
+        jr.push_back(r);
+        jc.push_back(c);
+        jv.push_back(v);
+      }
+    } else {  // no fixed column: every entry kept, in input order
+      jr.resize(nz);
+      jc.resize(nz);
+      jv.resize(nz);
+      par_range(nz, [&](int, int64_t a, int64_t b) {
+        for (int64_t k = a; k < b; ++k) {
+          const int r = P.Ar[k];
+          jr[k] = r;
+          jc[k] = P.Ac[k];
+          jv[k] = P.con_scale[r] * P.Av[k];
+        }
+      });
     }
-    jr.push_back(r);
-    jc.push_back(c);
-    jv.push_back(v);
   }
   for (int k = 0; k < P.ns; ++k) {
     jr.push_back(P.ind_ineq[k]);
@@ -1567,35 +1684,43 @@ void MPCSolver::setup_host(const madipm_qp& q) {
   std::vector<double> Jcv, JTcv;
   csr_from_coo(m, jr, jc, jv, Jrp, Jci, Jcv);
   csr_from_coo(n, jc, jr, jv, JTrp, JTci, JTcv);
+  std::vector<int32_t>().swap(jr);
+  std::vector<int32_t>().swap(jc);
+  std::vector<double>().swap(jv);
   std::vector<double> cs(n, 0.0);
   for (int i = 0; i < nx; ++i) cs[i] = P.obj_scale * P.sgn * P.c[i];
   c0s_ = P.obj_scale * (P.sgn * P.c0) + const_fixed;
-  // K2 lower CSC: diag(n+m) + H strictly-lower + J at rows n+r  (SparseKKTSystem [EXT])
-  std::vector<int32_t> kr, kc;
-  std::vector<double> kv;
-  for (int i = 0; i < n + m; ++i) {
-    kr.push_back(i);
-    kc.push_back(i);
-    kv.push_back(0.0);
-  }
-  for (int i = 0; i < n; ++i)
-    for (int64_t q = Hrp[i]; q < Hrp[i + 1]; ++q)
-      if (Hci[q] < i) {
-        kr.push_back(i);
-        kc.push_back(Hci[q]);
-        kv.push_back(Hcv[q]);
-      }
-  for (int r = 0; r < m; ++r)
-    for (int64_t q = Jrp[r]; q < Jrp[r + 1]; ++q) {
-      kr.push_back(n + r);
-      kc.push_back(Jci[q]);
-      kv.push_back(Jcv[q]);
-    }
-  // CSC = CSR of the transpose pattern (col-major)
-  std::vector<int64_t> Kcp;
+  // K2 lower CSC: diag(n+m) + H strictly-lower + J at rows n+r  (SparseKKTSystem [EXT]), built by
+  // columns: column j < n = [j; H's rows i > j (row j of the symmetric CSR H, ascending); n + the rows r
+  // of column j of J (row j of J^T's CSR, ascending)], column j >= n = [j]
+  std::vector<int64_t> Kcp(n + m + 1, 0);
   std::vector<int32_t> Kri;
   std::vector<double> Kv;
-  csr_from_coo(n + m, kc, kr, kv, Kcp, Kri, Kv);
+  {
+    std::vector<int64_t> hup(n, 0);  // per column: H entries below the diagonal
+    for (int i = 0; i < n; ++i)
+      for (int64_t q = Hrp[i]; q < Hrp[i + 1]; ++q) hup[i] += Hci[q] > i;
+    for (int j = 0; j < n + m; ++j) Kcp[j + 1] = Kcp[j] + 1 + (j < n ? hup[j] + (JTrp[j + 1] - JTrp[j]) : 0);
+    Kri.resize(Kcp[n + m]);
+    Kv.resize(Kcp[n + m]);
+    par_range(n + m, [&](int, int64_t j0, int64_t j1) {
+      for (int64_t j = j0; j < j1; ++j) {
+        int64_t o = Kcp[j];
+        Kri[o] = (int32_t)j;
+        Kv[o++] = 0.0;
+        if (j >= n) continue;
+        for (int64_t q = Hrp[j]; q < Hrp[j + 1]; ++q)
+          if (Hci[q] > j) {
+            Kri[o] = Hci[q];
+            Kv[o++] = Hcv[q];
+          }
+        for (int64_t q = JTrp[j]; q < JTrp[j + 1]; ++q) {
+          Kri[o] = n + JTci[q];
+          Kv[o++] = JTcv[q];
+        }
+      }
+    }, 1024);
+  }
   nnzK_ = (int64_t)Kri.size();
   if (const char* e = std::getenv("MADIPM_PART_BLOCKS")) maxb_ = std::max(1, std::min(MAXB, std::atoi(e)));
   if (const char* e = std::getenv("MADIPM_SPEC_NEAR")) spec_near_ = std::max(0.0, std::atof(e));
@@ -1608,11 +1733,7 @@ void MPCSolver::setup_host(const madipm_qp& q) {
     spmv_g_ = 4;
     while (spmv_g_ < 64 && spmv_g_ * 2 < avg) spmv_g_ *= 2;
   }
-  std::vector<int64_t> diag_pos(n + m, -1);
-  for (int j = 0; j < n + m; ++j)
-    for (int64_t q = Kcp[j]; q < Kcp[j + 1]; ++q)
-      if (Kri[q] == j) diag_pos[j] = q;
-  for (int j = 0; j < n + m; ++j) MADIPM_REQUIRE(diag_pos[j] >= 0, "missing KKT diagonal");
+  std::vector<int64_t> diag_pos(Kcp.begin(), Kcp.end() - 1);  // the diagonal leads every column
 
   // ---- KKT formulation + LDL^T symbolic analysis + device plan (linear-solver constructor)
   kkt_ = opt_.kkt_system;

@@ -20,16 +20,6 @@
 
 namespace madipm {
 
-namespace {
-
-constexpr int NT_FOLD = SymbolicPlan::kFoldThreads;  // threads of k_fact_tree (product-list chunks)
-
-struct Pattern {
-  // strictly-lower pattern of P K P^T: column lists (rows > col) and row lists (cols < row)
-  std::vector<int64_t> cp, rp;
-  std::vector<int32_t> ci, ri;
-};
-
 // Host threads for the O(nnz) passes of the analysis (MADIPM_ANALYSIS_THREADS, default: the
 // hardware threads, at most 16).  Every parallel pass gives the sequential result bit for bit.
 int analysis_threads() {
@@ -40,6 +30,16 @@ int analysis_threads() {
   }();
   return nt;
 }
+
+namespace {
+
+constexpr int NT_FOLD = SymbolicPlan::kFoldThreads;  // threads of k_fact_tree (product-list chunks)
+
+struct Pattern {
+  // strictly-lower pattern of P K P^T: column lists (rows > col) and row lists (cols < row)
+  std::vector<int64_t> cp, rp;
+  std::vector<int32_t> ci, ri;
+};
 
 // f(t, j0, j1) on T contiguous column ranges balanced by entries (colptr), one thread each
 template <class F>

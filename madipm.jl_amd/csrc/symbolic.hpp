@@ -187,6 +187,10 @@ struct SymbolicPlan {
 
 // Analyse the symmetric matrix given by its lower-triangular CSC pattern (0-based, entries with
 // row >= col, unique).  Throws madipm::Error on invalid input.
+// Host threads of the O(nnz) analysis / construction passes (MADIPM_ANALYSIS_THREADS, default the
+// hardware threads, at most 16)
+int analysis_threads();
+
 void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const SymbolicOptions& opt,
                       const int32_t* user_perm, SymbolicPlan& plan);
 
