@@ -527,16 +527,19 @@ __global__ __launch_bounds__(ANT) void k_assemble(FrontTab T, const SymbolicPlan
     int len = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) len = max(len, q1[k] - q0[k]);
-    for (int it = 0; it < len; it += 4) {
-      double x[4][4];
+    // 8 chunk sums per entry and round, 32 loads in flight per thread (a high-fan-in root entry
+    // has ~20 chunks: 3 rounds, not 5)
+    for (int it = 0; it < len; it += 8) {
+      double x[4][8];
 #pragma unroll
       for (int k = 0; k < 4; ++k)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) x[k][u] = (q0[k] + it + u < q1[k]) ? pc[q0[k] + it + u] : 0.0;
+        for (int u = 0; u < 8; ++u) x[k][u] = pc[min(q0[k] + it + u, max(q1[k] - 1, q0[k]))];
 #pragma unroll
       for (int k = 0; k < 4; ++k)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[k] += x[k][u];
+        for (int u = 0; u < 8; ++u)
+          if (q0[k] + it + u < q1[k]) v[k] += x[k][u];
     }
   }
   if (tl.bt1 > tl.bt0) {

@@ -23,11 +23,44 @@ import os
 import sys
 
 
+def _topo(cpu: int) -> dict:
+    """(package, core, SMT siblings) of a CPU from sysfs (None where not readable)."""
+    base = f"/sys/devices/system/cpu/cpu{cpu}/topology/"
+    out = {"cpu": cpu}
+    for k, f in (("package", "physical_package_id"), ("core", "core_id"), ("siblings", "thread_siblings_list")):
+        try:
+            with open(base + f) as fh:
+                v = fh.read().strip()
+            out[k] = int(v) if k != "siblings" else v
+        except OSError:
+            out[k] = None
+    return out
+
+
 def _pin(threads: int) -> list:
+    """Pin to `threads` CPUs of the affinity set, one per physical core first (an SMT sibling shares
+    the core's FPUs and caches with the thread beside it: MKL's threads then compete for them)."""
     cpus = sorted(os.sched_getaffinity(0))
-    use = cpus[:threads]
+    topo = [_topo(c) for c in cpus]
+    seen, first, rest = set(), [], []
+    for t in topo:
+        key = (t["package"], t["core"])
+        if t["core"] is None or key not in seen:
+            seen.add(key)
+            first.append(t["cpu"])
+        else:
+            rest.append(t["cpu"])
+    use = (first + rest)[:threads]
     os.sched_setaffinity(0, use)
     return use
+
+
+def _loadavg():
+    try:
+        with open("/proc/loadavg") as f:
+            return f.read().split()[:3]
+    except OSError:
+        return None
 
 
 def _cgroup_quota():
@@ -56,6 +89,7 @@ def main():
     os.environ["OMP_WAIT_POLICY"] = "PASSIVE"
     os.environ["MKL_DYNAMIC"] = "FALSE"
     os.environ["OPENBLAS_NUM_THREADS"] = "1"     # numpy's own BLAS: the loop's vector work is serial
+    naff = len(os.sched_getaffinity(0))
     cpus = _pin(tmax)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "madipm.jl_amd"))
@@ -71,8 +105,11 @@ def main():
     perm = np.load(args.perm) if args.perm else None
     runs = []
     ref = None
+    import resource
+    load0 = _loadavg()
     for t in counts:
         got = pardiso.set_threads(t)
+        ru0 = resource.getrusage(resource.RUSAGE_SELF)
         o = OracleMPC(qp, OracleOptions(regularization=("fixed", 1e-8, -1e-8), step_rule=("adaptive", 0.99),
                                         max_iter=300, tol=1e-8), record_trace=False)
         o.linear_solver = "pardiso"
@@ -80,13 +117,19 @@ def main():
         t0 = time.perf_counter()
         st = o.solve()
         wall = time.perf_counter() - t0
+        ru1 = resource.getrusage(resource.RUSAGE_SELF)
+        cpu_s = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
         F = o._pardiso
         fs = F.t_factor + F.t_solve
         runs.append({"threads": got, "iters": st.iter, "iters_per_s": st.iter / fs if fs > 0 else None,
                      "loop_s": st.total_time, "wall_s": wall, "pardiso_factor_s": F.t_factor,
                      "pardiso_solve_s": F.t_solve, "factorizations": F.nfactor, "solves": F.nsolve,
                      "pardiso_analysis_s": F.t_analysis, "nnzL_pardiso": F.nnzL,
-                     "perturbed_pivots": F.nperturbed, "status": st.status, "objective": st.objective})
+                     "perturbed_pivots": F.nperturbed, "status": st.status, "objective": st.objective,
+                     # process CPU time / wall: how many of the t threads actually ran (a cgroup quota,
+                     # co-tenants or SMT siblings show up as a ratio well below t)
+                     "cpu_s": cpu_s, "cpu_per_wall": cpu_s / wall if wall > 0 else None,
+                     "involuntary_switches": ru1.ru_nivcsw - ru0.ru_nivcsw})
         if ref is None:
             ref = st
         F.free()
@@ -102,7 +145,9 @@ def main():
            "value_threads": top["iters_per_s"], "threads_max": top["threads"],
            "value_1thread": one["iters_per_s"] if one else None,
            "loop_iters_per_s": best["iters"] / best["loop_s"] if best["loop_s"] > 0 else None,
-           "sweep": runs, "cpus": cpus, "cgroup_cpu_quota": _cgroup_quota(),
+           "sweep": runs, "cpus": cpus, "cpu_topology": [_topo(c) for c in cpus],
+           "affinity_cpus_before_pin": naff,
+           "loadavg_before": load0, "loadavg_after": _loadavg(), "cgroup_cpu_quota": _cgroup_quota(),
            "env": {k: os.environ.get(k) for k in ("MKL_THREADING_LAYER", "KMP_BLOCKTIME", "OMP_WAIT_POLICY")},
            "ref_status": ref.status, "ref_objective": ref.objective, "ref_iter": ref.iter}
     print(json.dumps(out))
