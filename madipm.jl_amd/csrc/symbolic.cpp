@@ -131,13 +131,49 @@ void etree(int N, const Pattern& P, std::vector<int32_t>& parent) {
     }
 }
 
+// Postorder of the etree with every node's heaviest child subtree (most columns) visited LAST: the
+// parent's first column then follows that child's last one, so relaxed amalgamation (step 4, which
+// merges column-adjacent child -> parent pairs only) can merge a front with its main child — a chain
+// of tree fronts under a separator becomes fewer, larger fronts (fewer dependent levels on the GPU).
+// MADIPM_HEAVY_LAST=0: children in index order.
 void postorder(int N, const std::vector<int32_t>& parent, std::vector<int32_t>& post) {
   std::vector<int32_t> head(N, -1), next(N, -1), stack(N);
-  for (int j = N - 1; j >= 0; --j)
-    if (parent[j] != -1) {
-      next[j] = head[parent[j]];
-      head[parent[j]] = j;
+  const char* hl = std::getenv("MADIPM_HEAVY_LAST");
+  if (hl && hl[0] == '0') {
+    for (int j = N - 1; j >= 0; --j)
+      if (parent[j] != -1) {
+        next[j] = head[parent[j]];
+        head[parent[j]] = j;
+      }
+  } else {
+    std::vector<int64_t> sz(N, 1);
+    for (int j = 0; j < N; ++j)
+      if (parent[j] != -1) sz[parent[j]] += sz[j];  // parent[j] > j: children are complete
+    std::vector<int32_t> heavy(N, -1);
+    for (int j = 0; j < N; ++j) {
+      const int p = parent[j];
+      if (p != -1 && (heavy[p] == -1 || sz[j] >= sz[heavy[p]])) heavy[p] = j;
     }
+    // children in index order, the heavy one moved to the end of its parent's list
+    for (int j = N - 1; j >= 0; --j)
+      if (parent[j] != -1 && heavy[parent[j]] != j) {
+        next[j] = head[parent[j]];
+        head[parent[j]] = j;
+      }
+    std::vector<int32_t> tail(N, -1);
+    for (int p = 0; p < N; ++p) {
+      const int h = heavy[p];
+      if (h == -1) continue;
+      if (head[p] == -1) {
+        head[p] = h;
+      } else {
+        int t = head[p];
+        while (next[t] != -1) t = next[t];
+        next[t] = h;
+      }
+      next[h] = -1;
+    }
+  }
   post.assign(N, 0);
   int k = 0;
   for (int j = 0; j < N; ++j) {
