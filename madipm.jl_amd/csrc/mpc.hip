@@ -1722,7 +1722,6 @@ void MPCSolver::setup_host(const madipm_qp& q) {
     }, 1024);
   }
   nnzK_ = (int64_t)Kri.size();
-  if (const char* e = std::getenv("MADIPM_PART_BLOCKS")) maxb_ = std::max(1, std::min(MAXB, std::atoi(e)));
   if (const char* e = std::getenv("MADIPM_SPEC_NEAR")) spec_near_ = std::max(0.0, std::atof(e));
   if (const char* e = std::getenv("MADIPM_FINAL_DEBUG"); e && e[0] == '1') {
     fdbg_.alloc(8 * kFinDbg);

@@ -1004,9 +1004,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   // Sharded: a top front is assembled in two parts — "external" (original entries on shard 0 + this
   // shard's subtree-root children; written, zeros included, then all-reduced) and "internal" (its top
   // children, accumulated after the all-reduce at the front's level).
-  // tuning knob (experiments): MADIPM_GATHER_MAX overrides opt.gather_max
-  int gather_max = opt.gather_max;
-  if (const char* e = std::getenv("MADIPM_GATHER_MAX")) gather_max = std::atoi(e);
+  const int gather_max = opt.gather_max;
   // factorisation tree (k_fact_tree): phase-1 fronts of <= kFactTreeMax rows whose children are all
   // pre-leaves (leaves of <= 32 rows, factorised by the level-0 launches) or tree fronts.  Their
   // original entries and pre-leaf children are pre-assembled into scratch by ONE gather pass after
