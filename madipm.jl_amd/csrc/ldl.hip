@@ -1216,7 +1216,7 @@ __device__ __forceinline__ void blocked_factor_pipe(double* A, int r, int w, int
         lap(tx);
         factor16r<PK, RCP>(A, r, ld, R0, min(16, w - R0), Dl,
                            MKall ? MKall + (kb + 1) * 16 * LDM : ((kb & 1) ? MK0 : MK1), lane);
-        if (!(fault && kb == 0)) pipe_set(&pc.mk, kb + 2);  // fault: MADIPM_DEBUG_PIPE_FAULT (tests only)
+        if (!fault) pipe_set(&pc.mk, kb + 2);  // fault: MADIPM_DEBUG_PIPE_FAULT (tests only): never published
         lap(tf);
       }
     } else {

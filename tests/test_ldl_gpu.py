@@ -152,9 +152,9 @@ def test_ldl_fact_pipe_bitwise(case, sfm, monkeypatch):
 
 
 def test_ldl_pipe_lost_handoff_is_an_error(monkeypatch):
-    """A hand-off of the pipelined in-LDS schedule that never arrives (MADIPM_DEBUG_PIPE_FAULT=1 drops
-    the first M_K publication of every front) must not yield a silently wrong factor: the waits time
-    out, the front raises the status block's sticky error and factorize() fails loudly."""
+    """A hand-off of the pipelined in-LDS schedule that never arrives (MADIPM_DEBUG_PIPE_FAULT=1: the
+    pivot-chain wave never publishes M_K) must not yield a silently wrong factor: the waits time out,
+    the front raises the status block's sticky error and factorize() fails loudly."""
     from madipm_amd.linear_solver import HIPLDLSolver
     monkeypatch.setenv("MADIPM_DEBUG_PIPE_FAULT", "1")
     K, Lw = _dense_k2(150, 1000, 5)
