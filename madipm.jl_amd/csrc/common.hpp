@@ -3,7 +3,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 #include <stdexcept>
 #include <string>
@@ -67,6 +69,21 @@ struct DBuf {
     if (n) MADIPM_HIP(hipMemsetAsync(p, 0, n * sizeof(T), s));
   }
   operator T*() const { return p; }
+};
+
+// MADIPM_SYMBOLIC_TIMING=1: wall time of each construction phase on stderr (diagnostics: the dense
+// QP's analysis_s breakdown)
+struct PhaseClock {
+  const char* who;
+  bool on = std::getenv("MADIPM_SYMBOLIC_TIMING") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  explicit PhaseClock(const char* w) : who(w) {}
+  void operator()(const char* what) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "%s %-28s %9.3f s\n", who, what, std::chrono::duration<double>(n - t).count());
+    t = n;
+  }
 };
 
 }  // namespace madipm

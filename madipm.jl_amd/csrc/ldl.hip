@@ -3924,7 +3924,9 @@ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const SymbolicOptions& sopt,
                      double ptol, const int32_t* user_perm, Comm* comm)
     : pivot_tol(ptol), comm_(comm) {
+  PhaseClock clk("LDLSolver");
   symbolic_analyze(n, colptr, rowval, sopt, user_perm, S_);
+  clk("symbolic_analyze");
   const SymbolicPlan& S = S_;
   MADIPM_REQUIRE(S.nshards == 1 || comm == nullptr || (comm->size == S.nshards && comm->rank == S.shard),
                  "communicator does not match the shard layout");
@@ -4127,6 +4129,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     lbpart_.alloc(std::max<int64_t>(np, 1));
   }
 
+  clk("tables + uploads");
   // ---- factorisation tree tables (k_fact_tree)
   {
     std::vector<int32_t> ord(S.ft_order), dptr{0}, dl;  // ticket order (SymbolicPlan::ft_order)
@@ -4676,6 +4679,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     attr_done = true;
   }
   MADIPM_HIP(hipDeviceSynchronize());
+  clk("schedules + workspace");
 }
 
 LDLSolver::~LDLSolver() {

@@ -1458,6 +1458,7 @@ std::unique_ptr<LinSolver> MPCSolver::make_linsolver(int n, const int64_t* cp, c
 // Host-side construction: MPCSolver(...) (structure.jl:79-178), MadNLP.initialize!/set_scaling!
 // [EXT] and the K2 pattern of SparseKKTSystem [EXT].
 void MPCSolver::setup_host(const madipm_qp& q) {
+  PhaseClock clk("setup_host");
   H_ = std::make_unique<QPHost>();
   QPHost& P = *H_;
   MADIPM_REQUIRE(q.nvar >= 0 && q.ncon >= 0, "negative dimensions");
@@ -1496,6 +1497,7 @@ void MPCSolver::setup_host(const madipm_qp& q) {
     });
     MADIPM_REQUIRE(!bad, "A index out of range");
   }
+  clk("copy + validate");
   // ---- index sets: MadNLP.get_index_constraints (EnforceEquality, MakeParameter) [EXT]
   for (int i = 0; i < m; ++i)
     if (P.lcon[i] != P.ucon[i]) P.ind_ineq.push_back(i);
@@ -1596,6 +1598,7 @@ void MPCSolver::setup_host(const madipm_qp& q) {
     for (int i = 0; i < m; ++i) P.rhs[i] *= P.con_scale[i];
   }
   obj_scale_ = P.obj_scale;
+  clk("initialize + scaling");
 
   // ---- device problem data
   nx_ = nx;
@@ -1679,6 +1682,7 @@ void MPCSolver::setup_host(const madipm_qp& q) {
     jc.push_back(nx + k);
     jv.push_back(-1.0);
   }
+  clk("H CSR + J COO");
   std::vector<int64_t> Jrp, JTrp;
   std::vector<int32_t> Jci, JTci;
   std::vector<double> Jcv, JTcv;
@@ -1687,6 +1691,7 @@ void MPCSolver::setup_host(const madipm_qp& q) {
   std::vector<int32_t>().swap(jr);
   std::vector<int32_t>().swap(jc);
   std::vector<double>().swap(jv);
+  clk("J, J^T CSR");
   std::vector<double> cs(n, 0.0);
   for (int i = 0; i < nx; ++i) cs[i] = P.obj_scale * P.sgn * P.c[i];
   c0s_ = P.obj_scale * (P.sgn * P.c0) + const_fixed;
@@ -1722,6 +1727,7 @@ void MPCSolver::setup_host(const madipm_qp& q) {
     }, 1024);
   }
   nnzK_ = (int64_t)Kri.size();
+  clk("K2 CSC");
   if (const char* e = std::getenv("MADIPM_SPEC_NEAR")) spec_near_ = std::max(0.0, std::atof(e));
   if (const char* e = std::getenv("MADIPM_FINAL_DEBUG"); e && e[0] == '1') {
     fdbg_.alloc(8 * kFinDbg);
@@ -1801,6 +1807,7 @@ void MPCSolver::setup_host(const madipm_qp& q) {
     ldl_ = make_linsolver(n + m, Kcp.data(), Kri.data(), so);
   }
 
+  clk("linear solver (analysis + plan)");
   // ---- uploads
   std::vector<int32_t> lbpos(n, -1), ubpos(n, -1);
   for (int k = 0; k < nlb_; ++k) lbpos[P.ind_lb[k]] = k;
@@ -1881,6 +1888,7 @@ void MPCSolver::setup_host(const madipm_qp& q) {
   }
   st_.zero(s);
   MADIPM_HIP(hipStreamSynchronize(s));
+  clk("uploads");
   // norm_b (solver.jl:173) on host
   norm_b_ = 0;
   for (double v : P.rhs) norm_b_ = std::max(norm_b_, std::fabs(v));

@@ -35,10 +35,27 @@ namespace {
 
 constexpr int NT_FOLD = SymbolicPlan::kFoldThreads;  // threads of k_fact_tree (product-list chunks)
 
+// allocator whose resize() leaves new elements uninitialised: the index arrays below are written in
+// full by the threads that fill them (first touch in parallel instead of a serial zero fill)
+template <class T>
+struct NoInit : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = NoInit<U>;
+  };
+  NoInit() = default;
+  template <class U>
+  NoInit(const NoInit<U>&) {}
+  template <class U>
+  void construct(U* p) { ::new ((void*)p) U; }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
+};
+
 struct Pattern {
   // strictly-lower pattern of P K P^T: column lists (rows > col) and row lists (cols < row)
   std::vector<int64_t> cp, rp;
-  std::vector<int32_t> ci, ri;
+  std::vector<int32_t, NoInit<int32_t>> ci, ri;
 };
 
 // f(t, j0, j1) on T contiguous column ranges balanced by entries (colptr), one thread each
@@ -60,11 +77,94 @@ void par_columns(int N, const int64_t* colptr, int T, F f) {
   for (auto& x : th) x.join();
 }
 
+// Twin leaves: columns j with an empty row list (no neighbour to their left: etree leaves, L's
+// column j = the column list of P K P^T, no fill) whose column list is the same row set as an
+// earlier such column's (its representative; twin[j] = that column, else -1).  A twin adds to the
+// graph only the clique its representative already adds, so the etree and the other columns' counts
+// are those of the pattern without the twins' entries; a twin's parent is its representative's (the
+// least row of the shared set) and its count is the representative's.  A QP with a diagonal Hessian
+// and dense A in natural order: all x columns but one are twins (dense 50k x 10k: 5e8 of the
+// 5e8 entries skipped by the etree's path compression and the column counts).
+// Candidates by (length, two order-free hashes); the set equality is then checked exactly.
+void find_twins(int N, const Pattern& P, const std::vector<uint8_t>& leaf, std::vector<int32_t>& twin) {
+  twin.assign(N, -1);
+  auto mix = [](uint64_t x) {  // splitmix64 finaliser
+    x += 0x9e3779b97f4a7c15ull;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+  };
+  struct Key {
+    int64_t len;
+    uint64_t h1, h2;
+    int32_t j;
+  };
+  std::vector<Key> keys;
+  for (int j = 0; j < N; ++j)
+    if (leaf[j] && P.cp[j + 1] - P.cp[j] >= 2) keys.push_back({P.cp[j + 1] - P.cp[j], 0, 0, j});
+  if (keys.size() < 2) return;
+  {
+    const int T = std::max(1, std::min<int>(analysis_threads(), (int)(keys.size() / 256)));
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t]() {
+        for (size_t q = t; q < keys.size(); q += T) {
+          uint64_t a = 0, b = 0;
+          for (int64_t p = P.cp[keys[q].j]; p < P.cp[keys[q].j + 1]; ++p) {
+            const uint64_t h = mix((uint64_t)P.ci[p]);
+            a += h;
+            b ^= mix(h ^ 0x5bd1e9955bd1e995ull);
+          }
+          keys[q].h1 = a;
+          keys[q].h2 = b;
+        }
+      });
+    for (auto& x : th) x.join();
+  }
+  std::sort(keys.begin(), keys.end(), [](const Key& x, const Key& y) {
+    if (x.len != y.len) return x.len < y.len;
+    if (x.h1 != y.h1) return x.h1 < y.h1;
+    if (x.h2 != y.h2) return x.h2 < y.h2;
+    return x.j < y.j;
+  });
+  // exact check per candidate group: the representative's rows marked, each member's rows must hit
+  // distinct marks (a mark is cleared on its hit and restored after the member)
+  std::vector<uint8_t> mark(N, 0);
+  for (size_t g0 = 0, g1; g0 < keys.size(); g0 = g1) {
+    g1 = g0 + 1;
+    while (g1 < keys.size() && keys[g1].len == keys[g0].len && keys[g1].h1 == keys[g0].h1 &&
+           keys[g1].h2 == keys[g0].h2)
+      ++g1;
+    if (g1 - g0 < 2) continue;
+    const int rep = keys[g0].j;
+    for (int64_t p = P.cp[rep]; p < P.cp[rep + 1]; ++p) mark[P.ci[p]] = 1;
+    const int T = std::max(1, std::min<int>(analysis_threads(), (int)((g1 - g0) / 64)));
+    std::vector<std::thread> th;
+    std::vector<std::vector<uint8_t>> tm(T > 1 ? T : 0);
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t]() {
+        std::vector<uint8_t>& m = T > 1 ? tm[t] : mark;
+        if (T > 1) m = mark;
+        for (size_t q = g0 + 1 + t; q < g1; q += T) {
+          const int j = keys[q].j;
+          int64_t p = P.cp[j];
+          for (; p < P.cp[j + 1] && m[P.ci[p]]; ++p) m[P.ci[p]] = 0;
+          const bool same = p == P.cp[j + 1];
+          for (int64_t r = P.cp[j]; r < p; ++r) m[P.ci[r]] = 1;
+          if (same) twin[j] = rep;
+        }
+      });
+    for (auto& x : th) x.join();
+    for (int64_t p = P.cp[rep]; p < P.cp[rep + 1]; ++p) mark[P.ci[p]] = 0;
+  }
+}
+
 // Strictly-lower pattern of P K P^T by column and by row: a counting sort of the entries into
 // column / row buckets.  Threaded over column ranges when the matrix is dense enough to pay (private
-// bucket counts per thread, offsets in thread order: the same bucket order as one pass).
+// bucket counts per thread, offsets in thread order: the same bucket order as one pass).  The row
+// lists leave out the entries of twin leaves (find_twins, from the column lists): no pass reads them.
 void build_pattern(int N, const int64_t* colptr, const int32_t* rowval, const std::vector<int32_t>& pinv,
-                   Pattern& P) {
+                   Pattern& P, std::vector<int32_t>& twin) {
   const int64_t nnz = colptr[N];
   int T = analysis_threads();
   if (nnz < 16 * (int64_t)N || (int64_t)T * N > (int64_t)1 << 27 || nnz < ((int64_t)1 << 22)) T = 1;
@@ -83,40 +183,76 @@ void build_pattern(int N, const int64_t* colptr, const int32_t* rowval, const st
       }
     }
   });
-  P.cp.assign(N + 1, 0);
-  P.rp.assign(N + 1, 0);
-  for (int k = 0; k < N; ++k) {  // bucket starts, then each thread's offset inside each bucket
-    int64_t sc = 0, sr = 0;
-    for (int t = 0; t < T; ++t) {
-      const int64_t c = cc[t][k], r = rc[t][k];
-      cc[t][k] = sc;
-      rc[t][k] = sr;
-      sc += c;
-      sr += r;
+  // bucket starts, then each thread's offset inside each bucket
+  auto offsets = [&](std::vector<std::vector<int64_t>>& cnt, std::vector<int64_t>& ptr) {
+    ptr.assign(N + 1, 0);
+    for (int k = 0; k < N; ++k) {
+      int64_t sum = 0;
+      for (int t = 0; t < T; ++t) {
+        const int64_t c = cnt[t][k];
+        cnt[t][k] = sum;
+        sum += c;
+      }
+      ptr[k + 1] = ptr[k] + sum;
     }
-    P.cp[k + 1] = P.cp[k] + sc;
-    P.rp[k + 1] = P.rp[k] + sr;
-  }
+  };
+  std::vector<uint8_t> leaf(N, 1);
+  for (int t = 0; t < T; ++t)
+    for (int k = 0; k < N; ++k)
+      if (rc[t][k]) leaf[k] = 0;
+  offsets(cc, P.cp);
   P.ci.resize(P.cp[N]);
-  P.ri.resize(P.rp[N]);
   par_columns(N, colptr, T, [&](int t, int j0, int j1) {
     int64_t* c = cc[t].data();
-    int64_t* r = rc[t].data();
     for (int j = j0; j < j1; ++j) {
       const int b = pinv[j];
       for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p) {
         const int i = rowval[p];
         if (i == j) continue;
         const int a = pinv[i];
+        const int lo = std::min(a, b);
+        P.ci[P.cp[lo] + c[lo]++] = std::max(a, b);
+      }
+    }
+  });
+  find_twins(N, P, leaf, twin);
+  // row lists without the twins' entries (a twin has no left neighbour: its whole input column is
+  // its column list, skipped)
+  for (int t = 0; t < T; ++t) std::fill(rc[t].begin(), rc[t].end(), 0);
+  par_columns(N, colptr, T, [&](int t, int j0, int j1) {
+    int64_t* r = rc[t].data();
+    for (int j = j0; j < j1; ++j) {
+      const int b = pinv[j];
+      if (twin[b] >= 0) continue;
+      for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p) {
+        const int i = rowval[p];
+        if (i == j) continue;
+        const int a = pinv[i];
+        if (twin[std::min(a, b)] < 0) r[std::max(a, b)]++;
+      }
+    }
+  });
+  offsets(rc, P.rp);
+  P.ri.resize(P.rp[N]);
+  par_columns(N, colptr, T, [&](int t, int j0, int j1) {
+    int64_t* r = rc[t].data();
+    for (int j = j0; j < j1; ++j) {
+      const int b = pinv[j];
+      if (twin[b] >= 0) continue;
+      for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p) {
+        const int i = rowval[p];
+        if (i == j) continue;
+        const int a = pinv[i];
         const int hi = std::max(a, b), lo = std::min(a, b);
-        P.ci[P.cp[lo] + c[lo]++] = hi;
-        P.ri[P.rp[hi] + r[hi]++] = lo;
+        if (twin[lo] < 0) P.ri[P.rp[hi] + r[hi]++] = lo;
       }
     }
   });
 }
 
-void etree(int N, const Pattern& P, std::vector<int32_t>& parent) {
+// Liu's algorithm over the row lists (twins' entries left out by build_pattern), then the twins
+// given their representative's parent
+void etree(int N, const Pattern& P, const std::vector<int32_t>& twin, std::vector<int32_t>& parent) {
   parent.assign(N, -1);
   std::vector<int32_t> anc(N, -1);
   for (int k = 0; k < N; ++k)
@@ -129,6 +265,8 @@ void etree(int N, const Pattern& P, std::vector<int32_t>& parent) {
         i = inext;
       }
     }
+  for (int j = 0; j < N; ++j)
+    if (twin[j] >= 0) parent[j] = parent[twin[j]];
 }
 
 // Postorder of the etree with every node's heaviest child subtree (most columns) visited LAST: the
@@ -195,7 +333,10 @@ void postorder(int N, const std::vector<int32_t>& parent, std::vector<int32_t>& 
 }
 
 // Column counts of L (diagonal included) for a matrix whose labelling is a postorder of its etree.
-void column_counts(int N, const Pattern& P, const std::vector<int32_t>& parent, std::vector<int64_t>& cnt) {
+// Twins (find_twins): their entries skipped (the other columns' counts are those of the pattern
+// without them), their own count set to their representative's.
+void column_counts(int N, const Pattern& P, const std::vector<int32_t>& parent, const std::vector<int32_t>& twin,
+                   std::vector<int64_t>& cnt) {
   cnt.assign(N, 0);
   std::vector<int32_t> first(N, -1), maxfirst(N, -1), prevleaf(N, -1), anc(N);
   for (int k = 0; k < N; ++k) {
@@ -206,7 +347,7 @@ void column_counts(int N, const Pattern& P, const std::vector<int32_t>& parent, 
   std::iota(anc.begin(), anc.end(), 0);
   for (int j = 0; j < N; ++j) {
     if (parent[j] != -1) cnt[parent[j]]--;
-    for (int64_t p = P.cp[j]; p < P.cp[j + 1]; ++p) {
+    for (int64_t p = twin[j] >= 0 ? P.cp[j + 1] : P.cp[j]; p < P.cp[j + 1]; ++p) {
       int i = P.ci[p];  // i > j
       if (first[j] <= maxfirst[i]) continue;  // j is not a leaf of the i-th row subtree
       maxfirst[i] = first[j];
@@ -229,6 +370,8 @@ void column_counts(int N, const Pattern& P, const std::vector<int32_t>& parent, 
   }
   for (int j = 0; j < N; ++j)
     if (parent[j] != -1) cnt[parent[j]] += cnt[j];
+  for (int j = 0; j < N; ++j)
+    if (twin[j] >= 0) cnt[j] = cnt[twin[j]];
 }
 
 inline int64_t trap(int64_t w, int64_t r) { return w * r - w * (w - 1) / 2; }
@@ -238,7 +381,7 @@ inline int64_t trap(int64_t w, int64_t r) { return w * r - w * (w - 1) / 2; }
 // the factorisation flops sum_j (c_j - 1)(c_j + 2).  Candidate orders are compared by flops and the
 // winner's analysis is kept (no second pass over the matrix for it).
 struct OrderAnalysis {
-  std::vector<int32_t> perm, pinv, parent;
+  std::vector<int32_t> perm, pinv, parent, twin;
   std::vector<int64_t> cnt;
   Pattern P;
   double flops = 0.0;
@@ -259,10 +402,11 @@ void analyse_order(int N, const int64_t* colptr, const int32_t* rowval, std::vec
     MADIPM_REQUIRE(perm[k] >= 0 && perm[k] < N && A.pinv[perm[k]] == -1, "ordering is not a permutation");
     A.pinv[perm[k]] = k;
   }
-  build_pattern(N, colptr, rowval, A.pinv, A.P);
-  stamp("pattern");
   std::vector<int32_t> post;
-  etree(N, A.P, A.parent);
+  std::vector<int32_t>& twin = A.twin;
+  build_pattern(N, colptr, rowval, A.pinv, A.P, twin);
+  stamp("pattern + twin leaves");
+  etree(N, A.P, twin, A.parent);
   stamp("etree");
   postorder(N, A.parent, post);
   bool ident = true;  // the ordering is already a postorder (e.g. natural order of a QP's K2): no relabel
@@ -272,12 +416,12 @@ void analyse_order(int N, const int64_t* colptr, const int32_t* rowval, std::vec
     for (int k = 0; k < N; ++k) perm2[k] = perm[post[k]];
     perm.swap(perm2);
     for (int k = 0; k < N; ++k) A.pinv[perm[k]] = k;
-    build_pattern(N, colptr, rowval, A.pinv, A.P);
-    etree(N, A.P, A.parent);
+    build_pattern(N, colptr, rowval, A.pinv, A.P, twin);
+    etree(N, A.P, twin, A.parent);
   }
   A.perm.swap(perm);
   stamp("postorder/relabel");
-  column_counts(N, A.P, A.parent, A.cnt);
+  column_counts(N, A.P, A.parent, twin, A.cnt);
   stamp("column counts");
   A.flops = 0.0;
   for (int64_t c : A.cnt) A.flops += (double)(c - 1) * (double)(c + 2);
@@ -308,13 +452,28 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   // the factorisation maps each entry to its symmetric position, so a full symmetric matrix would
   // be counted twice and is rejected.
   bool has_upper = false;
-  for (int j = 0; j < N; ++j) {
-    MADIPM_REQUIRE(colptr[j + 1] >= colptr[j], "colptr not monotone");
-    for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p) {
-      int i = rowval[p];
-      MADIPM_REQUIRE(i >= 0 && i < N, "row index out of range");
-      if (i == j) diagcount[j]++;
-      if (i < j) has_upper = true;
+  for (int j = 0; j < N; ++j) MADIPM_REQUIRE(colptr[j + 1] >= colptr[j], "colptr not monotone");
+  {
+    const int T = nnz < ((int64_t)1 << 22) ? 1 : analysis_threads();
+    std::vector<uint8_t> up(T, 0), bad(T, 0);
+    par_columns(N, colptr, T, [&](int t, int j0, int j1) {
+      bool b = false, u = false;  // thread-local: no shared line written per entry
+      for (int j = j0; j < j1; ++j) {
+        int64_t d = 0;
+        for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p) {
+          const int i = rowval[p];
+          b |= i < 0 || i >= N;
+          d += i == j;
+          u |= i < j;
+        }
+        diagcount[j] = d;
+      }
+      bad[t] = b;
+      up[t] = u;
+    });
+    for (int t = 0; t < T; ++t) {
+      MADIPM_REQUIRE(!bad[t], "row index out of range");
+      has_upper = has_upper || up[t];
     }
   }
   if (has_upper) {
@@ -521,10 +680,20 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   std::vector<uint8_t> has_left;
   if (use_lb) {
     has_left.assign(N, 0);
-    for (int j = 0; j < N; ++j)
-      for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p)
-        if (rowval[p] != j) has_left[rowval[p]] = 1;
+    {  // per-thread flags, OR-ed (order-free)
+      const int T = nnz < ((int64_t)1 << 22) ? 1 : analysis_threads();
+      std::vector<std::vector<uint8_t>> hl(T, std::vector<uint8_t>(N, 0));
+      par_columns(N, colptr, T, [&](int t, int j0, int j1) {
+        uint8_t* h = hl[t].data();
+        for (int j = j0; j < j1; ++j)
+          for (int64_t p = colptr[j]; p < colptr[j + 1]; ++p)
+            if (rowval[p] != j) h[rowval[p]] = 1;
+      });
+      for (int t = 0; t < T; ++t)
+        for (int i = 0; i < N; ++i) has_left[i] |= hl[t][i];
+    }
     std::vector<int32_t> seen(N, -1);
+    std::vector<uint8_t> inmem(N, 0);
     for (int s = 0; s < ns; ++s) {
       std::vector<int32_t> mem;
       for (int64_t q = S.child_ptr[s]; q < S.child_ptr[s + 1]; ++q) {
@@ -537,15 +706,18 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       if ((int)mem.size() < opt.lb_min_count) continue;
       std::vector<int32_t> U;
       int64_t tot = 0;
+      for (int c : mem) inmem[S.first[c]] = 1;
       for (int c : mem) {
         const int j = S.first[c];
         tot += P.cp[j + 1] - P.cp[j];
+        if (OA.twin[j] >= 0 && inmem[OA.twin[j]]) continue;  // its rows are its representative's
         for (int64_t p = P.cp[j]; p < P.cp[j + 1]; ++p)
           if (seen[P.ci[p]] != s) {
             seen[P.ci[p]] = s;
             U.push_back(P.ci[p]);
           }
       }
+      for (int c : mem) inmem[S.first[c]] = 0;
       const double dens = (double)tot / ((double)U.size() * (double)mem.size());
       if (dens < opt.lb_min_density) continue;
       std::sort(U.begin(), U.end());
@@ -660,24 +832,50 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         pos_in_u[lr] = k;
       }
       const size_t m0 = S.lb_mem.size();
+      const int T = std::min<int>(analysis_threads(), std::max<int>(1, (int)(mem.size() / 64)));
+      // a member whose CSC column has the previous member's rows (its own diagonal at the same
+      // position) shares that member's W-row map (dense QP: one map of m + 1 entries, not 5e8)
+      std::vector<uint8_t> same(mem.size(), 0);
+      {
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t)
+          th.emplace_back([&, t]() {
+            for (size_t k = 1 + t; k < mem.size(); k += T) {
+              const int oa = perm[S.first[mem[k - 1]]], ob = perm[S.first[mem[k]]];
+              const int64_t len = colptr[oa + 1] - colptr[oa];
+              if (colptr[ob + 1] - colptr[ob] != len) continue;
+              const int32_t* a = rowval + colptr[oa];
+              const int32_t* b = rowval + colptr[ob];
+              int64_t p = 0;
+              for (; p < len && (a[p] == b[p] || (a[p] == oa && b[p] == ob)); ++p) {
+              }
+              same[k] = p == len;
+            }
+          });
+        for (auto& x : th) x.join();
+      }
       int64_t wtot = (int64_t)S.lb_wrow.size();
-      for (int c : mem) {
-        const int oc = perm[S.first[c]];
-        S.lb_mem.push_back(S.first[c]);
+      for (size_t k = 0; k < mem.size(); ++k) {
+        const int oc = perm[S.first[mem[k]]];
+        S.lb_mem.push_back(S.first[mem[k]]);
         S.lb_cs.push_back(colptr[oc]);
         S.lb_ce.push_back(colptr[oc + 1]);
-        S.lb_wbase.push_back(wtot);
-        wtot += colptr[oc + 1] - colptr[oc];
+        if (same[k]) {
+          S.lb_wbase.push_back(S.lb_wbase.back());
+        } else {
+          S.lb_wbase.push_back(wtot);
+          wtot += colptr[oc + 1] - colptr[oc];
+        }
       }
       S.lb_wrow.resize(wtot);  // once (the threads below fill it)
-      // every entry of the members' CSC columns -> its W row (threads over members)
-      const int T = std::min<int>(analysis_threads(), std::max<int>(1, (int)(mem.size() / 64)));
+      // every entry of the distinct members' CSC columns -> its W row (threads over members)
       std::vector<std::thread> th;
       bool bad = false;
       std::vector<uint8_t> badt(T, 0);
       for (int t = 0; t < T; ++t)
         th.emplace_back([&, t]() {
           for (size_t q = m0 + t; q < m0 + mem.size(); q += T) {
+            if (same[q - m0]) continue;
             const int oc = perm[S.lb_mem[q]];
             int32_t* wr = S.lb_wrow.data() + S.lb_wbase[q];
             for (int64_t e = colptr[oc]; e < colptr[oc + 1]; ++e) {
@@ -897,7 +1095,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     // external forward sums.  A group with no member here vanishes on this shard.
     if (!S.lb.empty()) {
       size_t ng = 0, nm = 0, nw = 0;
-      int64_t wsize = 0;
+      int64_t wsize = 0, moved_from = -1, moved_to = 0;
       for (size_t gi = 0; gi < S.lb.size(); ++gi) {
         SymbolicPlan::LBGroup g = S.lb[gi];
         const int64_t m0 = g.mem_off;
@@ -910,9 +1108,15 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
           S.lb_mem[nm] = S.lb_mem[q];
           S.lb_cs[nm] = S.lb_cs[q];
           S.lb_ce[nm] = S.lb_ce[q];
-          std::memmove(S.lb_wrow.data() + nw, S.lb_wrow.data() + wb, sizeof(int32_t) * (size_t)len);
-          S.lb_wbase[nm] = (int64_t)nw;
-          nw += (size_t)len;
+          // shared maps (6b) are consecutive: moved once, for their first kept member (a destination
+          // never passes a later map's source, so the maps not moved yet stay intact)
+          if (wb != moved_from) {
+            std::memmove(S.lb_wrow.data() + nw, S.lb_wrow.data() + wb, sizeof(int32_t) * (size_t)len);
+            moved_from = wb;
+            moved_to = (int64_t)nw;
+            nw += (size_t)len;
+          }
+          S.lb_wbase[nm] = moved_to;
           ++nm;
           ++n;
         }

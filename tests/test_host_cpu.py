@@ -348,3 +348,41 @@ def test_dense_block_orderings_defer_constraint_vertices(ordering):
     S = Symbolic(N, colptr, rows, default_ldl_opts(ordering=ordering))
     assert S.info()["nnzL"] == n * (m + 1) + m * (m + 1) // 2
     assert sorted(S.perm()[-m:].tolist()) == list(range(n, N))
+
+
+def _twin_k2(seed):
+    """K2 of an LP-like QP whose x columns come in groups with identical A columns (twin leaves of the
+    etree) next to unique ones, a few H couplings (non-leaves) and an empty column."""
+    rng = np.random.default_rng(seed)
+    n, m = 90, 25
+    A = np.zeros((m, n))
+    base = [rng.random(m) < 0.3 for _ in range(6)]
+    for j in range(n):
+        if j % 3 == 0:
+            A[:, j] = base[j % 6] * rng.standard_normal(m)         # twins: 6 shared row sets
+        elif j != 7:
+            A[:, j] = (rng.random(m) < 0.15) * rng.standard_normal(m)
+    H = np.diag(rng.random(n) + 0.1)
+    for _ in range(5):                                               # couplings: these are not leaves
+        a, b = rng.choice(n, 2, replace=False)
+        H[a, b] = H[b, a] = 0.01
+    K = sp.csc_matrix(np.block([[H, A.T], [A, -1e-8 * np.eye(m)]]))
+    Lw = sp.tril(K).tocsc()
+    Lw.sort_indices()
+    return K, Lw
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+@pytest.mark.parametrize("ordering", [0, 1, 4])
+def test_symbolic_twin_leaves(seed, ordering):
+    """Twin leaves (symbolic.cpp find_twins: leaves with identical column sets, skipped by the etree
+    and the column counts) give the same nnz(L) as brute-force elimination and the oracle LDL^T."""
+    from madipm_amd._lib import Symbolic, default_ldl_opts
+    from oracle.ldl import OracleLDL
+    K, Lw = _twin_k2(seed)
+    S = Symbolic(K.shape[0], Lw.indptr, Lw.indices, default_ldl_opts(ordering=ordering))
+    perm = S.perm()
+    assert S.info()["nnzL"] == _brute_nnzL(K, perm)
+    F = OracleLDL(K, perm)
+    assert F.factorize() == K.shape[0]
+    assert F.nnzL() == S.info()["nnzL"]
