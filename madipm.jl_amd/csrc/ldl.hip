@@ -1500,9 +1500,12 @@ __device__ __forceinline__ FoldBatchTab& fold_batch_tab() {
   return t;
 }
 
+// cval / cdst: per thread, the parked sum and destination of a chunk's first run when it continues
+// the left neighbour's run (k_fact_tree's MK / cbuf, idle during the fold)
 template <bool PK>
 __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A, const double* Kx, double* arena,
-                                            double* D, LDLStatus* st, double tol, double* ext, int64_t* fdg) {
+                                            double* D, LDLStatus* st, double tol, double* ext, double* cval,
+                                            int32_t* cdst, int64_t* fdg) {
   int64_t tph[4] = {0, 0, 0, 0}, tc = fdg ? wall_clock64() : 0;
   auto lap = [&](int k) {
     if (fdg) {
@@ -1539,16 +1542,14 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
     if (tid < nb) tb_po[tid] = po, tb_pl[tid] = pl;
   }
   __syncthreads();
-  // product entries: thread t walks chunks t, t + FTN, ... (kFoldChains independent accumulation
-  // chains); a group holds GH entries of each
-  constexpr int NC = SymbolicPlan::kFoldChains, NCH = NC * FTN, GH = GP / NC;
-  static_assert(GP % NC == 0, "fold: whole groups per chain");
-  uint2 e[GP];
-  auto load_group = [&](uint2 (&g)[GP], const uint2* P, int k, int len) {
+  // product entries (SymbolicPlan::fold_prod): thread t walks chunk t, GP entries per group
+  constexpr uint32_t PAD = SymbolicPlan::kFoldPad;
+  uint32_t e[GP];
+  auto load_group = [&](uint32_t (&g)[GP], const uint32_t* P, int k, int len) {
 #pragma unroll
     for (int u = 0; u < GP; ++u) {
-      const int kk = k + u / NC;  // uniform: a scalar branch, not a per-lane wait
-      g[u] = (kk < len) ? P[(int64_t)kk * NCH + (u % NC) * FTN] : uint2{0u, 0u};
+      const int kk = k + u;  // uniform: a scalar branch, not a per-lane wait
+      g[u] = (kk < len) ? P[(int64_t)kk * FTN] : PAD;
     }
   };
   load_group(e, T.fold_prod + tb_po[0] + tid, 0, tb_pl[0]);
@@ -1660,45 +1661,64 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
     __syncthreads();
     lap(2);
     if (pre) gather_val();
-    // (4) this thread's chunks of the destination-sorted products (entry k of chunk c at NCH k + c:
-    // each load instruction is coalesced)
-    const uint2* __restrict__ P = T.fold_prod + tb_po[b] + tid;
+    // (4) this thread's chunk of the destination-sorted products (entry k at FTN k + tid: each load
+    // instruction is coalesced)
+    const uint32_t* __restrict__ P = T.fold_prod + tb_po[b] + tid;
     const int len = tb_pl[b];
-    double acc[NC];  // per chain: the negated sum of its open run
-#pragma unroll
-    for (int c = 0; c < NC; ++c) acc[c] = 0.0;
-    for (int k = 0; k < len; k += GH) {
-      uint2 nx[GP];
-      if (k + GH < len) {
-        load_group(nx, P, k + GH, len);
+    const uint32_t head = T.fold_chead[(int64_t)(b0 + b) * FTN + tid];
+    int d = (int)(head & 0xffffu);              // the running destination
+    bool park = (head & SymbolicPlan::kFoldCont) != 0;  // the first run continues the left chunk's
+    cdst[tid] = -1;
+    double acc = 0.0;  // the negated sum of the open run
+    for (int k = 0; k < len; k += GP) {
+      uint32_t nx[GP];
+      if (k + GP < len) {
+        load_group(nx, P, k + GP, len);
       } else if (b + 1 < nb) {  // the next batch's first group
         load_group(nx, T.fold_prod + tb_po[b + 1] + tid, 0, tb_pl[b + 1]);
       }
-      // every LDS operand of the group is read before its first update of A
+      // every LDS operand of the group is read before its first update of A (a kFoldPad entry reads
+      // row 0 and adds nothing)
       double v[GP];
 #pragma unroll
       for (int u = 0; u < GP; ++u) {
-        const double2 la = LQ[e[u].x >> 16], pb = PQ[e[u].y & ~SymbolicPlan::kFoldRunEnd];
-        v[u] = fma(la.x, pb.x, la.y * pb.y);
+        const uint32_t q1 = e[u] & 0xfffu, q2 = (e[u] >> 12) & 0xfffu;
+        const bool pad = q1 == PAD;
+        const double2 la = LQ[pad ? 0u : q1], pb = PQ[q2];
+        v[u] = pad ? 0.0 : fma(la.x, pb.x, la.y * pb.y);
       }
-      // a destination is owned by one chain and gets one run per batch; the run's sum is subtracted
-      // at its last entry (marked by the analysis) with a non-returning LDS atomic — one writer per
-      // address, so the result is deterministic, and no wait for the old value (a plain
-      // read-modify-write would serialise every run on the LDS round trip).  Branch-free: selects and
-      // one predicated atomic per entry; padding never ends a run, and acc restarts every batch.
+      // a run's sum is subtracted at its last entry with a non-returning LDS atomic — one writer per
+      // address (a run split by a chunk cut parks its continuation parts instead), so the result is
+      // deterministic, and no wait for the old value.  Selects and one predicated atomic per entry;
+      // padding never ends a run, and acc restarts every batch.
 #pragma unroll
       for (int u = 0; u < GP; ++u) {
-        const bool end = (int32_t)e[u].y < 0;
-        const double sum = acc[u % NC] - v[u];
-        if (end) __hip_atomic_fetch_add(A + (e[u].x & 0xffffu), sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        acc[u % NC] = end ? 0.0 : sum;
+        d += (int)((e[u] >> 24) & 127u);
+        const bool end = (int32_t)e[u] < 0;
+        const double sum = acc - v[u];
+        if (end && park) {
+          cval[tid] = sum;
+          cdst[tid] = d;
+        } else if (end) {
+          __hip_atomic_fetch_add(A + d, sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        park = park && !end;
+        acc = end ? 0.0 : sum;
       }
-      if (k + GH < len || b + 1 < nb) {
+      if (k + GP < len || b + 1 < nb) {
 #pragma unroll
         for (int u = 0; u < GP; ++u) e[u] = nx[u];
       }
     }
     if (len == 0 && b + 1 < nb) load_group(e, T.fold_prod + tb_po[b + 1] + tid, 0, tb_pl[b + 1]);
+    __syncthreads();
+    // the parked parts, left to right: the first chunk of each continued run adds the run's parts
+    if (cdst[tid] >= 0 && (tid == 0 || cdst[tid - 1] != cdst[tid])) {
+      const int dd = cdst[tid];
+      double t = 0.0;
+      for (int u = tid; u < FTN && cdst[u] == dd; ++u) t += cval[u];
+      A[dd] += t;
+    }
     __syncthreads();
     lap(3);
   }
@@ -1783,7 +1803,8 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
       A[fidx<PK>(d - dj * r, dj, r, ld)] = Kx[T.asm_src[q]];
     }
     __syncthreads();
-    fold_leaves<PK>(T, s, A, Kx, arena, D, st, tol, A + ((ntot + 1) & ~1), dg ? dg + 16 : nullptr);  // 16-byte aligned
+    fold_leaves<PK>(T, s, A, Kx, arena, D, st, tol, A + ((ntot + 1) & ~1), cbuf, reinterpret_cast<int32_t*>(MK),
+                    dg ? dg + 16 : nullptr);  // 16-byte aligned
   } else {  // pre-assembled as the LDS image: a straight copy, 16 loads in flight per thread
     const double* __restrict__ src = fscratch + T.fs_off[s];
     const int n = PK ? r * (r + 1) / 2 : r * ld;
@@ -4209,7 +4230,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       up32(fold_plen_, S.fold_plen);
       up32(fold_rmax_, S.fold_rmax);
       up32(fold_lmax_, S.fold_lmax);
-      fold_prod_.upload(S.fold_prod.empty() ? std::vector<uint32_t>{0u, 0u} : S.fold_prod);
+      fold_prod_.upload(S.fold_prod.empty() ? std::vector<uint32_t>{SymbolicPlan::kFoldPad} : S.fold_prod);
+      fold_chead_.upload(S.fold_chead.empty() ? std::vector<uint32_t>{0u} : S.fold_chead);
       T_.absorb = absorb_;
       T_.fold_pk = fold_pk_;
       T_.mc_ptr = mc_ptr_;
@@ -4227,7 +4249,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       T_.fold_plen = fold_plen_;
       T_.fold_rmax = fold_rmax_;
       T_.fold_lmax = fold_lmax_;
-      T_.fold_prod = reinterpret_cast<const uint2*>(fold_prod_.p);
+      T_.fold_prod = fold_prod_.p;
+      T_.fold_chead = fold_chead_.p;
     }
     fcnt_.alloc(4);
     fcnt_.zero();

@@ -65,7 +65,8 @@ struct FrontTab {
   const int32_t* fold_plen;
   const int32_t* fold_rmax;
   const int32_t* fold_lmax;
-  const uint2* fold_prod;
+  const uint32_t* fold_prod;
+  const uint32_t* fold_chead;
   const uint8_t* fs_img;  // 1: fscratch holds the front's LDS image (tree fronts), else ld r
   int32_t* err;     // the status block's sticky error (LDLStatus::err): a timed-out hand-off inside a front
   int fpipe;        // pipelined in-LDS schedule (blocked_factor_pipe; MADIPM_FACT_PIPE=0: blocked_factor_lds)
@@ -324,7 +325,7 @@ class LDLSolver : public LinSolver {
   DBuf<int32_t> ab_src0_, ab_src1_, ab_k_, ab_f0_, ab_wrc_, fold_bptr_, fold_bat_, fold_plen_, fold_rmax_, fold_lmax_;
   DBuf<uint8_t> absorb_, fold_pk_, fs_img_;
   DBuf<int32_t> mc_ptr_;
-  DBuf<uint32_t> fold_prod_;
+  DBuf<uint32_t> fold_prod_, fold_chead_;
   DBuf<double> xch_;
   DBuf<double> xpack_;     // sharded: packed top-front lower triangles (+ status slots), all-reduced
   DBuf<int64_t> topcol_;   // per top-front column: arena offset, packed offset, length

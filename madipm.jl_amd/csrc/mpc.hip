@@ -33,8 +33,13 @@ namespace madipm {
 
 struct QPHost {
   int nx = 0, m = 0, n = 0, ns = 0;
-  std::vector<double> c, lvar, uvar, lcon, ucon, x0, y0, Hv, Av;
-  std::vector<int32_t> Hr, Hc, Ar, Ac;
+  std::vector<double> c, lvar, uvar, lcon, ucon, x0, y0, Hv;
+  std::vector<int32_t> Hr, Hc;
+  // A's COO: the caller's arrays, read during construction only (no host copy: 8 GB for the dense QP)
+  const int32_t* Ar = nullptr;
+  const int32_t* Ac = nullptr;
+  const double* Av = nullptr;
+  int64_t nnzA = 0;
   double c0 = 0, sgn = 1;
   bool minimize = true;
   std::vector<int32_t> ind_ineq, ind_fixed, ind_lb, ind_ub;
@@ -1234,6 +1239,21 @@ __global__ void k_publish(const DevState* __restrict__ st, DevState* host, uint3
 __global__ void k_copy(double* __restrict__ dst, const double* __restrict__ src, int64_t n) {
   GRID_LOOP(i, n) dst[i] = src[i];
 }
+// get_solution's constraint values: one wave per row of J (CSR), the columns < nx (A's; the slack
+// columns left out), a fixed-order wave sum, + cfix (the fixed columns' terms)
+__global__ __launch_bounds__(NT) void k_cons(const int64_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                                             const double* __restrict__ v, const double* __restrict__ x,
+                                             const double* __restrict__ cfix, int m, int nx, double* __restrict__ out) {
+  const int row = blockIdx.x * (NT / 64) + threadIdx.x / 64, l = threadIdx.x & 63;
+  if (row >= m) return;
+  double a = 0.0;
+  for (int64_t p = rp[row] + l; p < rp[row + 1]; p += 64) {
+    const int c = ci[p];
+    if (c < nx) a = fma(v[p], x[c], a);
+  }
+  a = wave_reduce<OP_SUM>(a);
+  if (l == 0) out[row] = a + cfix[row];
+}
 __global__ void k_axpy_x(DV D) {
   GRID_LOOP(i, D.n) D.x[i] += D.d[i];
 }
@@ -1422,11 +1442,6 @@ static void csr_from_coo(int nrow, const std::vector<int32_t>& r, const std::vec
                          std::vector<double>& cv) {
   csr_from_coo(nrow, (int64_t)r.size(), r.data(), c.data(), v.data(), rp, ci, cv);
 }
-template <class T>
-static void par_copy(std::vector<T>& dst, const T* src, int64_t n) {
-  dst.resize(n);
-  par_range(n, [&](int, int64_t a, int64_t b) { std::copy(src + a, src + b, dst.data() + a); }, (int64_t)1 << 22);
-}
 
 MPCSolver::MPCSolver(const madipm_qp& qp, const madipm_options& opt, Comm* comm) : opt_(opt), comm_(comm) {
   const double t0 = now();
@@ -1483,9 +1498,10 @@ void MPCSolver::setup_host(const madipm_qp& q) {
   P.Hr.assign(q.Hrows, q.Hrows + q.nnzh);
   P.Hc.assign(q.Hcols, q.Hcols + q.nnzh);
   P.Hv.assign(q.Hvals, q.Hvals + q.nnzh);
-  par_copy(P.Ar, q.Arows, q.nnzj);
-  par_copy(P.Ac, q.Acols, q.nnzj);
-  par_copy(P.Av, q.Avals, q.nnzj);
+  P.Ar = q.Arows;
+  P.Ac = q.Acols;
+  P.Av = q.Avals;
+  P.nnzA = q.nnzj;
   for (int64_t k = 0; k < q.nnzh; ++k)
     MADIPM_REQUIRE(P.Hr[k] >= P.Hc[k] && P.Hr[k] < nx && P.Hc[k] >= 0, "H must be lower-triangular COO in range");
   {
@@ -1541,7 +1557,7 @@ void MPCSolver::setup_host(const madipm_qp& q) {
   }
   if (P.ns) {
     std::vector<double> ax(m, 0.0);
-    for (size_t k = 0; k < P.Av.size(); ++k) ax[P.Ar[k]] += P.Av[k] * P.x[P.Ac[k]];
+    for (int64_t k = 0; k < P.nnzA; ++k) ax[P.Ar[k]] += P.Av[k] * P.x[P.Ac[k]];
     for (int k = 0; k < P.ns; ++k) P.x[nx + k] = ax[P.ind_ineq[k]];
   }
   // initialize_variables! (Ipopt bound push) [EXT]
@@ -1579,7 +1595,7 @@ void MPCSolver::setup_host(const madipm_qp& q) {
     P.obj_scale = gmax > 0 ? std::min(1.0, 100.0 / gmax) : 1.0;
     std::vector<double> rowmax(m, 0.0);
     {  // per-thread row maxima, then their maximum (order-free)
-      const int64_t nz = (int64_t)P.Av.size();
+      const int64_t nz = P.nnzA;
       std::vector<std::vector<double>> rm(par_threads(nz), std::vector<double>(m, 0.0));
       par_range(nz, [&](int t, int64_t a, int64_t b) {
         double* x = rm[t].data();
@@ -1648,7 +1664,7 @@ void MPCSolver::setup_host(const madipm_qp& q) {
   std::vector<int32_t> jr, jc;
   std::vector<double> jv;
   {
-    const int64_t nz = (int64_t)P.Av.size();
+    const int64_t nz = P.nnzA;
     bool anyfix = false;
     for (int i = 0; i < nx && !anyfix; ++i) anyfix = P.fixed[i];
     if (anyfix) {  // cfix sums in input order: the sequential pass
@@ -2473,9 +2489,15 @@ void MPCSolver::get_solution(double* x, double* y, double* zl, double* zu, doubl
     for (int i = 0; i < nx_; ++i) zu[i] = zuh[i] / obj_scale_;
   if (y)
     for (int j = 0; j < m_; ++j) y[j] = yh[j] * P.con_scale[j] / obj_scale_;
-  if (cons) {
-    std::fill(cons, cons + m_, 0.0);
-    for (size_t k = 0; k < P.Av.size(); ++k) cons[P.Ar[k]] += P.Av[k] * xh[P.Ac[k]];
+  if (cons && m_) {  // A x = (J's columns < nx) x / con_scale + the fixed columns' part (cfix / con_scale)
+    DBuf<double> ax;
+    ax.alloc(m_);
+    k_cons<<<(unsigned)((m_ + NT / 64 - 1) / (NT / 64)), NT, 0, stream_>>>(Jrp_, Jci_, Jv_, x_, cfix_, m_, nx_, ax);
+    MADIPM_HIP(hipGetLastError());
+    std::vector<double> h(m_);
+    MADIPM_HIP(hipMemcpyAsync(h.data(), ax.p, sizeof(double) * m_, hipMemcpyDeviceToHost, stream_));
+    MADIPM_HIP(hipStreamSynchronize(stream_));
+    for (int j = 0; j < m_; ++j) cons[j] = h[j] / P.con_scale[j];
   }
 }
 

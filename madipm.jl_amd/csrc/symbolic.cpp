@@ -1249,6 +1249,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   S.fold_poff.clear();
   S.fold_plen.clear();
   S.fold_prod.clear();
+  S.fold_chead.clear();
   S.ab_first.clear();
   S.ab_src0.clear();
   S.ab_src1.clear();
@@ -1271,7 +1272,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       uint32_t dst, q1, q2;
     };
     std::vector<Prod> pr;
-    std::vector<int64_t> bnd;
+    std::vector<std::vector<uint32_t>> enc;
     {
       // k_fact_tree's ticket order: by level (children before parents, so a workgroup waiting on its
       // children never blocks the tickets they need), and within a level by descending tail — the
@@ -1325,7 +1326,9 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         for (int64_t qc = S.child_ptr[s]; qc < S.child_ptr[s + 1]; ++qc) {
           const int c = S.child_list[qc];
           if (S.ftree[c]) continue;
-          if (nl == 0 || RB * (rows + S.nrows[c]) + LB * (nl + 1) > budget) ++nb, rows = 0, nl = 0;
+          if (nl == 0 || RB * (rows + S.nrows[c]) + LB * (nl + 1) > budget ||
+              rows + S.nrows[c] > SymbolicPlan::kFoldRowsMax)
+            ++nb, rows = 0, nl = 0;
           rows += S.nrows[c];
           ++nl;
         }
@@ -1368,7 +1371,9 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       while (kb < k1) {
         int ke = kb;
         int64_t rows = 0;
-        while (ke < k1 && RB * (rows + S.nrows[S.mc_list[ke]]) + LB * (ke - kb + 1) <= budget) rows += S.nrows[S.mc_list[ke++]];
+        while (ke < k1 && RB * (rows + S.nrows[S.mc_list[ke]]) + LB * (ke - kb + 1) <= budget &&
+               rows + S.nrows[S.mc_list[ke]] <= SymbolicPlan::kFoldRowsMax)
+          rows += S.nrows[S.mc_list[ke++]];
         MADIPM_REQUIRE(ke > kb, "fold: a leaf does not fit the batch budget");
         S.fold_bat.push_back(kb);
         S.fold_row0.push_back(S.ab_first[kb]);
@@ -1386,37 +1391,38 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
               pr.push_back({fidx(rl[a - wc], rl[b - wc]), qb0 + a, qb0 + b});
         }
         std::stable_sort(pr.begin(), pr.end(), [](const Prod& x, const Prod& y) { return x.dst < y.dst; });
-        // NCH chunks at destination boundaries, balanced by count
-        constexpr int NCH = SymbolicPlan::kFoldChains * NT_FOLD;
+        // NCH chunks of equal length (a run split where a cut falls), each encoded with its running
+        // destination (SymbolicPlan: one word per entry, kFoldPad steps for jumps beyond 127)
+        constexpr int NCH = NT_FOLD;
+        constexpr uint32_t PAD = SymbolicPlan::kFoldPad;
         const int64_t P = (int64_t)pr.size();
-        bnd.assign(NCH + 1, P);
-        bnd[0] = 0;
-        for (int t = 1; t < NCH; ++t) {
-          int64_t q = std::max(bnd[t - 1], (P * t) / NCH);
-          while (q > 0 && q < P && pr[q].dst == pr[q - 1].dst) ++q;
-          bnd[t] = q;
-        }
-        int64_t len = 0;
-        for (int t = 0; t < NCH; ++t) len = std::max(len, bnd[t + 1] - bnd[t]);
-        const int64_t off = (int64_t)S.fold_prod.size() / 2;
-        S.fold_poff.push_back(off);
-        S.fold_plen.push_back((int32_t)len);
-        S.fold_prod.resize(2 * (off + len * NCH));
-        for (int t = 0; t < NCH; ++t)
-          for (int64_t k = 0; k < len; ++k) {
-            uint32_t* e = &S.fold_prod[2 * (off + k * NCH + t)];
-            const int64_t q = bnd[t] + k;
-            if (q < bnd[t + 1]) {
-              MADIPM_REQUIRE(pr[q].dst < 65536 && pr[q].q1 < 65536 && pr[q].q2 < SymbolicPlan::kFoldRunEnd,
-                             "fold: index beyond 16 bits");
-              const bool end = q + 1 == bnd[t + 1] || pr[q + 1].dst != pr[q].dst;
-              e[0] = pr[q].dst | (pr[q].q1 << 16);
-              e[1] = pr[q].q2 | (end ? SymbolicPlan::kFoldRunEnd : 0u);
-            } else {  // padding: row 0 (always staged), never the end of a run
-              e[0] = 0;
-              e[1] = 0;
+        enc.assign(NCH, {});
+        for (int t = 0; t < NCH; ++t) {
+          const int64_t q0 = P * t / NCH, q1 = P * (t + 1) / NCH;
+          std::vector<uint32_t>& E = enc[t];
+          uint32_t head = 0;
+          if (q0 < q1) {
+            uint32_t d = pr[q0].dst;
+            head = d | ((q0 > 0 && pr[q0 - 1].dst == d) ? SymbolicPlan::kFoldCont : 0u);
+            for (int64_t q = q0; q < q1; ++q) {
+              MADIPM_REQUIRE(pr[q].dst < 65536 && pr[q].q1 < PAD && pr[q].q2 < PAD, "fold: index beyond its field");
+              uint32_t dd = pr[q].dst - d;
+              for (; dd > 127; dd -= 127) E.push_back(PAD | (127u << 24));
+              d = pr[q].dst;
+              const bool end = q + 1 == q1 || pr[q + 1].dst != d;
+              E.push_back(pr[q].q1 | (pr[q].q2 << 12) | (dd << 24) | (end ? SymbolicPlan::kFoldRunEnd : 0u));
             }
           }
+          S.fold_chead.push_back(head);
+        }
+        int64_t len = 0;
+        for (int t = 0; t < NCH; ++t) len = std::max<int64_t>(len, (int64_t)enc[t].size());
+        const int64_t off = (int64_t)S.fold_prod.size();
+        S.fold_poff.push_back(off);
+        S.fold_plen.push_back((int32_t)len);
+        S.fold_prod.resize(off + len * NCH, PAD);  // padding: no product, no step, no run end
+        for (int t = 0; t < NCH; ++t)
+          for (size_t k = 0; k < enc[t].size(); ++k) S.fold_prod[off + (int64_t)k * NCH + t] = enc[t][k];
         kb = ke;
       }
       S.fold_bptr[s + 1] = (int32_t)S.fold_bat.size();
@@ -1435,7 +1441,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         a[1] += S.mc_ptr[s + 1] - S.mc_ptr[s];
         a[2] += (double)(S.ab_first[S.mc_ptr[s + 1]] - S.ab_first[S.mc_ptr[s]]);
         for (int b = S.fold_bptr[s]; b < S.fold_bptr[s + 1]; ++b)
-          a[3] += (double)S.fold_plen[b] * SymbolicPlan::kFoldChains * NT_FOLD;
+          a[3] += (double)S.fold_plen[b] * NT_FOLD;
         a[4] += S.fold_bptr[s + 1] - S.fold_bptr[s];
         a[5] += S.nrows[s];
       }

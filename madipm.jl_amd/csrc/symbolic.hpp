@@ -113,21 +113,25 @@ struct SymbolicPlan {
   // the gather pre-assembly summing them.  Leaf rows are flattened per front in child order (ab_*);
   // the leaves are cut into batches whose rows fit LDS beside the front.  Per batch the products
   // (F(i, j) -= l(q1) . p(q2) over the two leaf columns, p = l d) are sorted by LDS destination
-  // (leaf order within one destination), cut into kFoldChains x kFoldThreads chunks at destination
-  // boundaries (thread t walks chunks t, t + kFoldThreads, ... as independent accumulation chains)
-  // and stored interleaved (entry k of chunk c at fold_poff + kFoldChains kFoldThreads k + c) so each
-  // load instruction is coalesced.  An entry's top bit marks the last product of its destination run
-  // (the run's sum is subtracted there); padding entries carry no mark and read row 0.
+  // (leaf order within one destination) and cut into kFoldThreads chunks of equal length, a
+  // destination run split where a cut falls (thread t walks chunk t; entry k of chunk t at
+  // fold_poff + kFoldThreads k + t, so each load instruction is coalesced).  One 32-bit word per
+  // entry: q1 | q2 << 12 | dd << 24 | run end << 31 — batch-local rows (12 bits; kFoldPad as q1: no
+  // product) and the step dd of the thread's running destination (from fold_chead's base; a step
+  // beyond 127 takes kFoldPad entries).  A run's sum is subtracted at its last entry in the chunk; the
+  // first run of a chunk that continues its left neighbour's run is parked in LDS instead and added
+  // after the products, left to right (every destination: one atomic writer + a fixed-order tail).
+  // r3: cutting only at destination boundaries padded the chunks to the longest run (2x the products
+  // at ex10's level-1/2 fronts) and 2 words per entry carried the destination of every product.
   static constexpr int64_t kFactTreeLdsMax = 150 * 1024;  // dynamic LDS of k_fact_tree
   static constexpr int64_t kFoldLdsMax = 148 * 1024;      // fold front + leaf rows (k_fact_tree's
                                                           // static LDS is ~10.4 KB of the CU's 160 KB)
   static constexpr int kFoldRowBytes = 36;                // LDS per leaf row: (l0, l1), (l0 d0, l1 d1), leaf
   static constexpr int kFoldLeafBytes = 48;               // LDS per leaf: d0, d1, f10, L offset, row0, w | rc
-  // product chunks per k_fact_tree thread.  2 (independent accumulation chains) measured slower on
-  // ex10: a chunk cannot split a destination run, so the longest runs set the padded length and the
-  // product slots grew 80k -> 135k per level-2 front (tree span 178 -> 190 us)
-  static constexpr int kFoldChains = 1;
-  static constexpr uint32_t kFoldRunEnd = 1u << 31;       // entry word 1: last product of its run
+  static constexpr uint32_t kFoldRunEnd = 1u << 31;       // entry: last product of its run (in the chunk)
+  static constexpr uint32_t kFoldPad = 0xfffu;            // q1 of an entry without a product
+  static constexpr int kFoldRowsMax = 4095;               // leaf rows per batch: 12-bit indices below kFoldPad
+  static constexpr uint32_t kFoldCont = 1u << 31;         // fold_chead: the chunk's first run continues
   static constexpr int kFoldMaxBatches = 32;              // leaf batches per folding front (LDS table)
   std::vector<uint8_t> absorb;        // front folds its micro leaves
   std::vector<uint8_t> fold_pk;       // fold front stored packed in LDS (to leave room for the leaf rows)
@@ -140,8 +144,9 @@ struct SymbolicPlan {
   std::vector<int64_t> fold_row0;     // per batch: its first flat leaf row (ab_first of fold_bat); + sentinel
   std::vector<int64_t> fold_poff;     // per batch: first product entry
   std::vector<int32_t> fold_plen;     // per batch: entries per chunk
+  std::vector<uint32_t> fold_chead;   // per batch x kFoldThreads: base destination | kFoldCont
   std::vector<int32_t> fold_rmax, fold_lmax;  // per front: largest batch (rows, leaves): its LDS carve
-  std::vector<uint32_t> fold_prod;    // 2 words per entry: dst | q1 << 16, q2 | run end (batch-local rows)
+  std::vector<uint32_t> fold_prod;    // one word per entry (above)
   int64_t fs_size = 0;
   // forward-solve gather: for every front row, the children's update-vector entries in child order
   std::vector<int64_t> sv_ptr, sv_src;  // sv_ptr indexed by row_ptr[s] + i
