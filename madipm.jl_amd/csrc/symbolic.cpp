@@ -1471,8 +1471,9 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   S.chunk_lev.assign(2 * S.nlevels + 3, 0);
   S.g_chunk.clear();
   {
-    std::vector<int32_t> key, cnt;
-    std::vector<int64_t> src, sorted;
+    std::vector<int32_t> key, tcnt, cnt(4097);
+    std::vector<int64_t> src, bysrc, sorted;
+    std::vector<int32_t> bykey;
     // children of s whose update blocks this assembly reads: 0 all, 1 top children only, 2 this
     // shard's subtree children only
     auto child_ok = [&](int c, int which) {
@@ -1514,35 +1515,49 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
             src.push_back(S.u_off[c] + aa + (int64_t)bb * S.u_ld[c]);
           }
       }
-      // stable counting sort by key (keeps originals-then-children order per entry)
-      const int64_t nkeys = (int64_t)ntile * 4096;
-      cnt.assign(nkeys + 1, 0);
-      for (int32_t k : key) cnt[k + 1]++;
-      for (int64_t k = 0; k < nkeys; ++k) cnt[k + 1] += cnt[k];
-      sorted.resize(src.size());
+      // stable counting sort by key (keeps originals-then-children order per entry), in two passes:
+      // by tile, then inside each tile with entries by its 4096 positions — O(entries + tiles), not
+      // O(r^2) per front (neos' 1257 big fronts: 13.7 -> 0.5 s)
+      tcnt.assign(ntile + 1, 0);
+      for (int32_t k : key) tcnt[(k >> 12) + 1]++;
+      for (int t = 0; t < ntile; ++t) tcnt[t + 1] += tcnt[t];
+      bykey.resize(key.size());
+      bysrc.resize(src.size());
       {
-        std::vector<int32_t> fill(cnt.begin(), cnt.end() - 1);
-        for (size_t e = 0; e < key.size(); ++e) sorted[fill[key[e]]++] = src[e];
+        std::vector<int32_t> fill(tcnt.begin(), tcnt.end() - 1);
+        for (size_t e = 0; e < key.size(); ++e) {
+          const int32_t q = fill[key[e] >> 12]++;
+          bykey[q] = key[e] & 4095;
+          bysrc[q] = src[e];
+        }
       }
+      sorted.resize(src.size());
       for (int ti = 0; ti < nt; ++ti)
         for (int tj = 0; tj <= ti; ++tj) {
           const int t = ti * (ti + 1) / 2 + tj;
           SymbolicPlan::AsmTile at{};
           at.front = s;
           at.tij = ti | (tj << 16) | (acc ? SymbolicPlan::kAccumulate : 0);
-          const int64_t k0 = (int64_t)t * 4096, k1 = k0 + 4096;
-          const bool has_g = cnt[k1] > cnt[k0];
+          const int64_t e0 = tcnt[t], e1 = tcnt[t + 1];
+          const bool has_g = e1 > e0;
           if (has_g) {
+            std::fill(cnt.begin(), cnt.end(), 0);
+            for (int64_t e = e0; e < e1; ++e) cnt[bykey[e] + 1]++;
+            for (int k = 0; k < 4096; ++k) cnt[k + 1] += cnt[k];
+            {
+              std::vector<int32_t> fill(cnt.begin(), cnt.end() - 1);
+              for (int64_t e = e0; e < e1; ++e) sorted[e0 + fill[bykey[e]]++] = bysrc[e];
+            }
             at.gptr = (int64_t)S.g_ptr.size();
             at.gchk = (int64_t)S.g_chunk.size();
             int32_t nchk = 0;
-            const int64_t sbase = (int64_t)S.g_src.size() - cnt[k0];
-            for (int64_t k = k0; k < k1; ++k) {
+            const int64_t sbase = (int64_t)S.g_src.size();
+            for (int k = 0; k < 4096; ++k) {
               S.g_ptr.push_back(nchk);
               for (int64_t c = cnt[k]; c < cnt[k + 1]; c += SymbolicPlan::kChunk, ++nchk) S.g_chunk.push_back(sbase + c);
             }
             S.g_ptr.push_back(nchk);
-            S.g_src.insert(S.g_src.end(), sorted.begin() + cnt[k0], sorted.begin() + cnt[k1]);
+            S.g_src.insert(S.g_src.end(), sorted.begin() + e0, sorted.begin() + e1);
           } else {
             at.gptr = -1;
             at.gchk = 0;
