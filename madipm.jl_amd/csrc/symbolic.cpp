@@ -1397,8 +1397,11 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         constexpr uint32_t PAD = SymbolicPlan::kFoldPad;
         const int64_t P = (int64_t)pr.size();
         enc.assign(NCH, {});
+        // (fewer products than chunks: one per chunk, the empty chunks last — the parts of a split
+        // run always lie in adjacent chunks, which the kernel's left-to-right tail sum relies on)
         for (int t = 0; t < NCH; ++t) {
-          const int64_t q0 = P * t / NCH, q1 = P * (t + 1) / NCH;
+          const int64_t q0 = P < NCH ? std::min<int64_t>(t, P) : P * t / NCH;
+          const int64_t q1 = P < NCH ? std::min<int64_t>(t + 1, P) : P * (t + 1) / NCH;
           std::vector<uint32_t>& E = enc[t];
           uint32_t head = 0;
           if (q0 < q1) {
