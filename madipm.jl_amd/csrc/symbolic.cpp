@@ -1320,19 +1320,29 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         budget = LMAX - pk_bytes(r);
       }
       if (budget < RB * 32 + LB) continue;  // not even one leaf fits beside the front
+      // a batch of `rows` leaf rows and `nl` leaves fits when the front's LDS carve — sized by the
+      // largest batch's rows and the largest batch's leaf count, possibly two different batches —
+      // stays within the budget
+      auto fits = [&](int64_t rows, int64_t nl, int64_t rmax, int64_t lmax) {
+        return RB * std::max(rows, rmax) + LB * std::max(nl, lmax) <= budget && rows <= SymbolicPlan::kFoldRowsMax;
+      };
       {  // the batch table lives in LDS: fronts needing more batches leave their leaves unfolded
         int nb = 0;
-        int64_t rows = 0, nl = 0;
-        for (int64_t qc = S.child_ptr[s]; qc < S.child_ptr[s + 1]; ++qc) {
+        int64_t rows = 0, nl = 0, rmax = 0, lmax = 0;
+        bool ok2 = true;
+        for (int64_t qc = S.child_ptr[s]; qc < S.child_ptr[s + 1] && ok2; ++qc) {
           const int c = S.child_list[qc];
           if (S.ftree[c]) continue;
-          if (nl == 0 || RB * (rows + S.nrows[c]) + LB * (nl + 1) > budget ||
-              rows + S.nrows[c] > SymbolicPlan::kFoldRowsMax)
+          if (nl == 0 || !fits(rows + S.nrows[c], nl + 1, rmax, lmax)) {
             ++nb, rows = 0, nl = 0;
+            ok2 = fits(S.nrows[c], 1, rmax, lmax);
+          }
           rows += S.nrows[c];
           ++nl;
+          rmax = std::max(rmax, rows);
+          lmax = std::max(lmax, nl);
         }
-        if (nb > SymbolicPlan::kFoldMaxBatches) continue;
+        if (!ok2 || nb > SymbolicPlan::kFoldMaxBatches) continue;
       }
       S.absorb[s] = 1;
       S.fold_pk[s] = (uint8_t)pk;
@@ -1371,8 +1381,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       while (kb < k1) {
         int ke = kb;
         int64_t rows = 0;
-        while (ke < k1 && RB * (rows + S.nrows[S.mc_list[ke]]) + LB * (ke - kb + 1) <= budget &&
-               rows + S.nrows[S.mc_list[ke]] <= SymbolicPlan::kFoldRowsMax)
+        while (ke < k1 && fits(rows + S.nrows[S.mc_list[ke]], ke - kb + 1, S.fold_rmax[s], S.fold_lmax[s]))
           rows += S.nrows[S.mc_list[ke++]];
         MADIPM_REQUIRE(ke > kb, "fold: a leaf does not fit the batch budget");
         S.fold_bat.push_back(kb);
@@ -1429,6 +1438,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         kb = ke;
       }
       S.fold_bptr[s + 1] = (int32_t)S.fold_bat.size();
+      MADIPM_REQUIRE(RB * S.fold_rmax[s] + LB * S.fold_lmax[s] <= budget, "fold: LDS carve beyond the budget");
     }
     S.ab_first.push_back((int64_t)S.ab_src0.size());
     // sentinels: the batch after a front's last one starts at that front's end (leaves and rows are
