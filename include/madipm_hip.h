@@ -172,7 +172,7 @@ void madipm_comm_destroy(madipm_comm_t comm);
  * 11 k_bwd_below, 12 k_bwd_big, 13 k_bwd_small, 14 k_fwd_tiny, 15 k_bwd_tiny, 16 k_lb_build,
  * 17 k_lb_syrk, 18 k_lb_gemv).  Setting a mask
  * clears the statistics. */
-#define MADIPM_NKERNELS 22
+#define MADIPM_NKERNELS 23
 typedef struct madipm_kstat {
   char name[32];
   int64_t launches;

@@ -83,7 +83,7 @@ static SymbolicOptions to_sym_opts(const madipm_ldl_opts* o) {
 
 extern "C" {
 
-int madipm_version(void) { return 200; }  // 0.2.0: three-phase sharded solve
+int madipm_version(void) { return 201; }  // 0.2.1: MADIPM_NKERNELS 23 (k_asm_update)
 
 const char* madipm_last_error(void) { return last_error(); }
 

@@ -504,17 +504,16 @@ __global__ __launch_bounds__(NT) void k_asm_chunks(const int64_t* __restrict__ g
 // barrier per child (r3 put one barrier and one round trip per child and tile: neos 8 ms per
 // factorisation).  The tile is written to the front (big: arena, ld r; small: scratch, ld r).
 constexpr int ANT = 1024, ABN = 8;
-__global__ __launch_bounds__(ANT) void k_assemble(FrontTab T, const SymbolicPlan::AsmTile* __restrict__ tiles,
-                                                  const int32_t* __restrict__ gptr, const double* __restrict__ part,
-                                                  const int32_t* __restrict__ bt, double* __restrict__ arena,
-                                                  double* __restrict__ fscratch) {
-  const SymbolicPlan::AsmTile tl = tiles[blockIdx.x];
-  const int s = tl.front, ti = tl.tij & 0xffff, tj = (tl.tij >> 16) & 0x7fff;
-  const bool acc = tl.tij < 0;  // SymbolicPlan::kAccumulate: F += tile (sharded top fronts, phase 2)
-  const int r = T.nrows[s];
+// the tile's entries (thread: row lane, columns wv + 16 m) = chunk sums + big children's blocks
+__device__ __forceinline__ void asm_tile_sum(const FrontTab& T, const SymbolicPlan::AsmTile& tl,
+                                             const int32_t* __restrict__ gptr, const double* __restrict__ part,
+                                             const int32_t* __restrict__ bt, const double* __restrict__ arena,
+                                             double (&v)[4]) {
+  const int ti = tl.tij & 0xffff, tj = (tl.tij >> 16) & 0x7fff;
   const int I0 = ti * 64, J0 = tj * 64;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  double v[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int m = 0; m < 4; ++m) v[m] = 0.0;
   if (tl.gptr >= 0) {
     const int32_t* __restrict__ gp = gptr + tl.gptr;
     const double* __restrict__ pc = part + tl.gchk;
@@ -594,6 +593,20 @@ __global__ __launch_bounds__(ANT) void k_assemble(FrontTab T, const SymbolicPlan
       __syncthreads();  // the maps are rebuilt by the next batch
     }
   }
+}
+
+__global__ __launch_bounds__(ANT) void k_assemble(FrontTab T, const SymbolicPlan::AsmTile* __restrict__ tiles,
+                                                  const int32_t* __restrict__ gptr, const double* __restrict__ part,
+                                                  const int32_t* __restrict__ bt, double* __restrict__ arena,
+                                                  double* __restrict__ fscratch) {
+  const SymbolicPlan::AsmTile tl = tiles[blockIdx.x];
+  const int s = tl.front, ti = tl.tij & 0xffff, tj = (tl.tij >> 16) & 0x7fff;
+  const bool acc = tl.tij < 0;  // SymbolicPlan::kAccumulate: F += tile (sharded top fronts, phase 2)
+  const int r = T.nrows[s];
+  const int I0 = ti * 64, J0 = tj * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  double v[4];
+  asm_tile_sum(T, tl, gptr, part, bt, arena, v);
   const int64_t fso = T.fs_off[s];
   double* __restrict__ F = (fso >= 0 ? fscratch + fso : arena + T.l_off[s]);
   const int i = I0 + lane;
@@ -605,6 +618,71 @@ __global__ __launch_bounds__(ANT) void k_assemble(FrontTab T, const SymbolicPlan
       const int64_t q = !img ? i + (int64_t)j * r : (r > 128 ? (int64_t)((j * (2 * r - j - 1)) >> 1) + i : i + (int64_t)j * (r | 1));
       F[q] = acc ? F[q] + v[m] : v[m];
     }
+  }
+}
+
+// Single-panel big fronts (SymbolicPlan::fused, w <= 64): once k_big_diag / k_big_trsm have written
+// the panel's L and D, ONE pass per 64x64 tile assembles the trailing entries (asm_tile_sum, as
+// k_assemble) and subtracts L_I D L_J^T (K = w, f64 MFMA 16x16x4, one 16x16 block per wave) before
+// the tile's only store.  The level path moved every trailing entry through HBM three times
+// (k_assemble's store, k_big_upd128's load and store); neos' 1220 skinny big fronts (w <= 39, r up to
+// 2.7k) are mostly trailing matrix.  Column block 0's tiles (assembled for the panel by k_assemble)
+// get their columns >= w here.  Operands and MFMA order are k_big_upd128's (A = L_J, B = (L D)_I,
+// K ascending, one accumulator): the same U bit for bit.
+__global__ __launch_bounds__(ANT) void k_asm_update(FrontTab T, const SymbolicPlan::AsmTile* __restrict__ tiles,
+                                                    const int32_t* __restrict__ gptr, const double* __restrict__ part,
+                                                    const int32_t* __restrict__ bt, double* __restrict__ arena,
+                                                    const double* __restrict__ D) {
+  constexpr int LDT = 80, LDR = 65;  // [k][row] operands (k_big_update's conflict-free stride); result tile
+  __shared__ __attribute__((aligned(16))) double Wt[64 * LDT];  // (L D)[I rows]
+  __shared__ __attribute__((aligned(16))) double Lt[64 * LDT];  // L[J rows]
+  __shared__ double R[64 * LDR];                                 // L_I D L_J^T, [i - I0 + (j - J0) LDR]
+  const SymbolicPlan::AsmTile tl = tiles[blockIdx.x];
+  const int s = tl.front, ti = tl.tij & 0xffff, tj = (tl.tij >> 16) & 0x7fff;
+  const int r = T.nrows[s], f0 = T.first[s], w = T.first[s + 1] - f0;
+  const int I0 = ti * 64, J0 = tj * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  double* __restrict__ F = arena + T.l_off[s];
+  {  // the panel rows of I and J (row lane, columns wv + 16 q): loads from clamped addresses, masked at the store
+    double a[4], b[4], d[4];
+    const int ri = min(I0 + lane, r - 1), rj = min(J0 + lane, r - 1);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int kc = min(wv + 16 * q, w - 1);
+      a[q] = F[ri + (int64_t)kc * r];
+      b[q] = F[rj + (int64_t)kc * r];
+      d[q] = D[f0 + kc];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = wv + 16 * q;
+      Wt[k * LDT + lane] = (k < w && I0 + lane < r) ? a[q] * d[q] : 0.0;
+      Lt[k * LDT + lane] = (k < w && J0 + lane < r) ? b[q] : 0.0;
+    }
+  }
+  double v[4];
+  asm_tile_sum(T, tl, gptr, part, bt, arena, v);
+  __syncthreads();  // the operands in LDS
+  {
+    const int bi = wv & 3, bj = wv >> 2;
+    dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+    const int nks = (w + 3) >> 2;
+    for (int ks = 0; ks < nks; ++ks) {  // wave-uniform
+      const int kk = 4 * ks + (lane >> 4);
+      const double a = Lt[kk * LDT + 16 * bj + (lane & 15)];
+      const double b = Wt[kk * LDT + 16 * bi + (lane & 15)];
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    }
+    // acc[g]: row i = I0 + 16 bi + (lane & 15), column j = J0 + 16 bj + (lane >> 4) + 4 g
+#pragma unroll
+    for (int g = 0; g < 4; ++g) R[(16 * bi + (lane & 15)) + (16 * bj + (lane >> 4) + 4 * g) * LDR] = acc[g];
+  }
+  __syncthreads();
+  const int i = I0 + lane;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int j = J0 + wv + 16 * m;
+    if (i < r && j < r && i >= j && j >= w) F[i + (int64_t)j * r] = v[m] - R[lane + (wv + 16 * m) * LDR];
   }
 }
 
@@ -4266,16 +4344,18 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   auto align2 = [&]() {
     if (sched.size() & 1) sched.push_back(0);
   };
+  // phase-1 level groups: the fused fronts' tiles past their column block 0 wait for k_asm_update
+  auto asm_end = [&](int g) { return g < NL ? S.atile_fz1[g] : S.atile_lev[g + 1]; };
   auto asm_launch = [&](int g, std::vector<Launch>& out) {
-    if (S.atile_lev[g + 1] <= S.atile_lev[g]) return;
-    Launch L{ASSEMBLE, 0, S.atile_lev[g], 0, S.atile_lev[g + 1] - S.atile_lev[g], S.chunk_lev[g],
+    if (asm_end(g) <= S.atile_lev[g]) return;
+    Launch L{ASSEMBLE, 0, S.atile_lev[g], 0, asm_end(g) - S.atile_lev[g], S.chunk_lev[g],
              S.chunk_lev[g + 1] - S.chunk_lev[g]};
     // algorithmic traffic: chunk pass reads (index, value) per source, writes one partial per chunk;
     // the tile pass reads the entry offsets + partials (+ big-children blocks), writes the lower tile
     const int64_t nsrc = S.g_chunk[S.chunk_lev[g + 1]] - S.g_chunk[S.chunk_lev[g]];
     L.bytes2 = 16.0 * nsrc + 16.0 * L.nchunk;
     L.flops2 = (double)nsrc;
-    for (int32_t t = S.atile_lev[g]; t < S.atile_lev[g + 1]; ++t) {
+    for (int32_t t = S.atile_lev[g]; t < asm_end(g); ++t) {
       const SymbolicPlan::AsmTile& at = S.atiles[t];
       const int r = S.nrows[at.front], ti = at.tij & 0xffff, tj = (at.tij >> 16) & 0x7fff;
       const double nr = std::min(64, r - 64 * ti), nc = std::min(64, r - 64 * tj);
@@ -4382,6 +4462,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
           kf[1] += nb * dk * dk;
           td.insert(td.end(), {s, 0});
           for (int i = 0; i < nt; ++i) tt.insert(tt.end(), {s, i});
+          if (S.fused[s]) continue;  // its trailing update: k_asm_update (below)
           // deferred multi-panel update (k_big_update): panel groups of big_kpan_ panels; inside a
           // group each panel updates the group's later panels only (local tiles), the group's last
           // panel updates the rest of the front with K = the whole group (trailing tiles)
@@ -4414,6 +4495,26 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
           L.flops = kf[q];
           out.push_back(L);
           sched.insert(sched.end(), kv.second->begin(), kv.second->end());
+        }
+        if (p == 0 && phase == 1 && S.atile_fz0[lev] < S.atile_lev[lev + 1]) {
+          // the fused fronts' trailing tiles: assembled + updated after their panel (one launch)
+          const int32_t t0 = S.atile_fz0[lev], t1 = S.atile_lev[lev + 1];
+          Launch L{ASM_UPDATE, 0, t0, 0, t1 - t0};
+          for (int32_t t = t0; t < t1; ++t) {
+            const SymbolicPlan::AsmTile& at = S.atiles[t];
+            const int f = at.front, r = S.nrows[f], w = S.first[f + 1] - S.first[f];
+            const int ti = at.tij & 0xffff, tj = (at.tij >> 16) & 0x7fff;
+            const double nr = std::min(64, r - 64 * ti), nc = std::min(64, r - 64 * tj);
+            // the written entries + the chunk sums' offsets + the panel rows of I and J (+ big children)
+            L.bytes += 8.0 * (ti == tj ? nr * (nr + 1) / 2 : nr * nc) + (at.gptr >= 0 ? 4.0 * 4097 : 0.0) +
+                       8.0 * (nr + nc) * w;
+            for (int k = at.bt0; k < at.bt1; ++k) {
+              const int32_t* e = &S.bt[5 * k];
+              for (int b = e[1]; b < e[2]; ++b) L.bytes += 8.0 * std::max(0, e[4] - std::max(b, e[3]));
+            }
+            L.flops += 2.0 * nr * nc * w;
+          }
+          out.push_back(L);
         }
       }
     }
@@ -4723,7 +4824,7 @@ const char* kernel_kind_name(int k) {
                                         "k_big_trsm",   "k_big_update", "k_inertia",    "k_fwd_small",    "k_fwd_gather",
                                         "k_fwd_big",    "k_bwd_below",  "k_bwd_big",    "k_bwd_small",
                                         "k_fwd_tiny",   "k_bwd_tiny",   "k_lb_build",   "k_lb_syrk",      "k_lb_gemv",
-                                        "k_fwd_tree",   "k_bwd_tree",   "k_fact_tree"};
+                                        "k_fwd_tree",   "k_bwd_tree",   "k_fact_tree",    "k_asm_update"};
   return (k >= 0 && k < KK_COUNT) ? names[k] : "?";
 }
 
@@ -4871,6 +4972,10 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
       case BIG_UPDATE:
         TIMED(KK_UPDATE, L.bytes, 0.0, L.flops,
               (k_big_update<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, big_kpan_, arena_, D_)));
+        break;
+      case ASM_UPDATE:
+        TIMED(KK_ASM_UPDATE, L.bytes, 0.0, L.flops,
+              (k_asm_update<<<(unsigned)L.items, ANT, 0, s>>>(T_, atiles_.p + L.off, g_ptr_, gpart_, bt_, arena_, D_)));
         break;
       case BIG_UPDATE128:
         TIMED(KK_UPDATE, L.bytes, 0.0, L.flops,

@@ -113,7 +113,7 @@ __device__ __forceinline__ void ldl_status_end(LDLStatus* st) { st->t1 = wall_cl
 enum KernelKind {
   KK_ASM_CHUNKS = 0, KK_ASSEMBLE, KK_TINY, KK_SMALL, KK_DIAG, KK_TRSM, KK_UPDATE, KK_INERTIA,
   KK_FWD_SMALL, KK_FWD_GATHER, KK_FWD_BIG, KK_BWD_BELOW, KK_BWD_BIG, KK_BWD_SMALL, KK_FWD_TINY, KK_BWD_TINY,
-  KK_LB_BUILD, KK_LB_SYRK, KK_LB_GEMV, KK_FWD_TREE, KK_BWD_TREE, KK_FACT_TREE,
+  KK_LB_BUILD, KK_LB_SYRK, KK_LB_GEMV, KK_FWD_TREE, KK_BWD_TREE, KK_FACT_TREE, KK_ASM_UPDATE,
   KK_COUNT
 };
 const char* kernel_kind_name(int k);
@@ -234,7 +234,8 @@ class LDLSolver : public LinSolver {
 
  private:
   enum Kind { ASSEMBLE = 0, SMALL32 = 1, SMALL64 = 2, SMALL128 = 3, BIG_DIAG = 4, BIG_TRSM = 5, BIG_UPDATE = 6,
-              LB_BUILD = 7, LB_SYRK = 8, MICRO = 9, SMALL192 = 10, FTREE = 11, BIG_UPDATE128 = 12 };
+              LB_BUILD = 7, LB_SYRK = 8, MICRO = 9, SMALL192 = 10, FTREE = 11, BIG_UPDATE128 = 12,
+              ASM_UPDATE = 13 };
   struct Launch {
     int kind;
     int step;       // panel step for BIG_DIAG / BIG_TRSM / BIG_UPDATE

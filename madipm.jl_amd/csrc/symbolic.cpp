@@ -1496,7 +1496,8 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       if (which == 3) return !S.ftree[c];  // tree front: pre-leaf children only
       return !S.top(c) && S.owner[c] == S.shard;
     };
-    auto emit = [&](int s, bool orig, int which, bool acc, bool emit_empty) {
+    // tsel: 0 every tile, 1 the tiles of column block 0 only, 2 the others only
+    auto emit = [&](int s, bool orig, int which, bool acc, bool emit_empty, int tsel = 0) {
       const int r = S.nrows[s];
       const int nt = (r + 63) / 64;
       const int ntile = nt * (nt + 1) / 2;
@@ -1547,6 +1548,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       sorted.resize(src.size());
       for (int ti = 0; ti < nt; ++ti)
         for (int tj = 0; tj <= ti; ++tj) {
+          if ((tsel == 1 && tj != 0) || (tsel == 2 && tj == 0)) continue;
           const int t = ti * (ti + 1) / 2 + tj;
           SymbolicPlan::AsmTile at{};
           at.front = s;
@@ -1598,14 +1600,38 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       S.atile_lev[g + 1] = (int32_t)S.atiles.size();
       S.chunk_lev[g + 1] = (int64_t)S.g_chunk.size();
     };
-    // phase 1: this shard's fronts (all fronts when unsharded), level by level
+    // phase 1: this shard's fronts (all fronts when unsharded), level by level.  Single-panel big
+    // fronts (w <= 64; SymbolicPlan::fused) last: their column block 0 (the panel, assembled before the
+    // panel factorisation), then their other tiles, which k_asm_update assembles after the panel's
+    // L is known and writes once, updated (C - L_I D L_J^T) — the tiles of column block 0 join that
+    // launch too for their columns >= w.  The group: [plain..., fused block 0..., fused rest...).
+    S.fused.assign(ns, 0);
+    {
+      const char* ev = std::getenv("MADIPM_FUSED_UPDATE");
+      const bool on = !(ev && ev[0] == '0');
+      std::vector<char> lbpar(ns, 0);
+      for (const auto& g : S.lb) lbpar[g.parent] = 1;
+      for (int s = 0; on && s < ns; ++s) {
+        const int w = S.first[s + 1] - S.first[s];
+        S.fused[s] = S.is_big[s] && !S.top(s) && S.mine(s) && !lb_member(s) && !S.ftree[s] && !lbpar[s] &&
+                     S.fs_off[s] < 0 && w <= 64 && S.nrows[s] > w;
+      }
+    }
+    S.atile_fz0.assign(NL, 0);
+    S.atile_fz1.assign(NL, 0);
     for (int lev = 0; lev < NL; ++lev) {
       for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
         const int s = S.level_list[q];
-        if (S.top(s) || !S.mine(s) || lb_member(s) || S.ftree[s]) continue;
+        if (S.top(s) || !S.mine(s) || lb_member(s) || S.ftree[s] || S.fused[s]) continue;
         if (!S.is_big[s] && S.fs_off[s] < 0) continue;
         emit(s, true, 0, false, true);
       }
+      S.atile_fz0[lev] = (int32_t)S.atiles.size();
+      for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q)
+        if (S.fused[S.level_list[q]]) emit(S.level_list[q], true, 0, false, true, 1);
+      S.atile_fz1[lev] = (int32_t)S.atiles.size();
+      for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q)
+        if (S.fused[S.level_list[q]]) emit(S.level_list[q], true, 0, false, true, 2);
       close_group(lev);
     }
     // top fronts, external part (before the all-reduce; zeros included)

@@ -95,6 +95,12 @@ struct SymbolicPlan {
   // contributions of their top children), g = 2 nlevels + 1 = the factorisation-tree pre-assembly
   std::vector<int32_t> atile_lev;      // size 2 nlevels + 3
   std::vector<int64_t> chunk_lev;
+  // single-panel big fronts (w <= 64) whose trailing tiles are assembled and updated by ONE launch
+  // after the panel factorisation (k_asm_update): per phase-1 level, the group's tiles are
+  // [atile_lev, atile_fz0) plain, [atile_fz0, atile_fz1) the fused fronts' column block 0,
+  // [atile_fz1, atile_lev + 1) their other tiles
+  std::vector<uint8_t> fused;
+  std::vector<int32_t> atile_fz0, atile_fz1;
   std::vector<int32_t> g_ptr, bt;
   std::vector<int64_t> g_chunk;        // chunk c = sources [g_chunk[c], g_chunk[c+1])
   std::vector<int64_t> g_src;          // >= 0: arena index; < 0: ~(index into caller's values)
