@@ -2131,6 +2131,42 @@ __global__ __launch_bounds__(FTN) void k_fact_tree(FrontTab T, const int32_t* __
 
 // Diagonal block of 64-column panel `step` (one workgroup per front): load, blocked factorisation,
 // write L11 (d on the diagonal), D and the M_K blocks for k_big_trsm.
+// The diagonal block of panel `step` of front s, staged in A64 (lower part, identity-padded past kw):
+// blocked factorisation, then L11 (d on the diagonal), D and the M_K blocks for k_big_trsm.
+__device__ __forceinline__ void big_diag_tail(const FrontTab& T, int s, int step, double* A64, double* Ms, double* Dl,
+                                              double* __restrict__ arena, double* __restrict__ D,
+                                              double* __restrict__ Mbuf, LDLStatus* st, double tol) {
+  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+  const int k0 = step * 64, kw = min(64, w - k0);
+  double* __restrict__ F = arena + T.l_off[s] + k0 + (int64_t)k0 * r;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  diag64(A64, Dl, Ms, tid);
+  for (int j = wv; j < kw; j += 4)
+    if (lane >= j && lane < kw) F[lane + (int64_t)j * r] = (lane == j) ? Dl[j] : A64[lane + j * LDA];
+  if (tid < kw) {
+    const double d = Dl[tid];
+    D[f0 + k0 + tid] = d;
+    if (bad_pivot(d, tol)) atomicMin(&st->fail_pivot, f0 + k0 + tid + 1);
+  }
+  double* __restrict__ M = Mbuf + (int64_t)T.bigslot[s] * 4096;
+  for (int e = tid; e < 4 * 16 * LDM; e += NT) M[e] = Ms[e];
+}
+
+// Lookahead: the update launch of panel `step` leaves panel step + 1's diagonal tile final in the
+// workgroup of its task (0, 0), which factorises it right away (big_diag_tail) while the launch's
+// other tiles are still updated — no k_big_diag launch, and its latency off the panel chain, for
+// every panel but the first.  Entry (i, j) of the tile (< 64 each) arrives through put(i, j, v).
+__device__ __forceinline__ bool big_next_diag(const FrontTab& T, int s, int step) {
+  return 64 * (step + 1) < T.first[s + 1] - T.first[s];
+}
+__device__ __forceinline__ void big_diag_prepare(double* A64, int kw) {
+  const int tid = threadIdx.x;
+  for (int e = tid; e < 64 * 64; e += NT) {
+    const int i = e & 63, j = e >> 6;
+    A64[i + j * LDA] = (i < kw && j < kw) ? 0.0 : (i == j ? 1.0 : 0.0);
+  }
+}
+
 __global__ __launch_bounds__(NT) void k_big_diag(FrontTab T, const int32_t* __restrict__ list, int step,
                                                  double* __restrict__ arena, double* __restrict__ D,
                                                  double* __restrict__ Mbuf, LDLStatus* st, double tol) {
@@ -2158,16 +2194,7 @@ __global__ __launch_bounds__(NT) void k_big_diag(FrontTab T, const int32_t* __re
     }
   }
   __syncthreads();
-  diag64(A64, Dl, Ms, tid);
-  for (int j = wv; j < kw; j += 4)
-    if (lane >= j && lane < kw) F[lane + (int64_t)j * r] = (lane == j) ? Dl[j] : A64[lane + j * LDA];
-  if (tid < kw) {
-    const double d = Dl[tid];
-    D[f0 + k0 + tid] = d;
-    if (bad_pivot(d, tol)) atomicMin(&st->fail_pivot, f0 + k0 + tid + 1);
-  }
-  double* __restrict__ M = Mbuf + (int64_t)T.bigslot[s] * 4096;
-  for (int e = tid; e < 4 * 16 * LDM; e += NT) M[e] = Ms[e];
+  big_diag_tail(T, s, step, A64, Ms, Dl, arena, D, Mbuf, st, tol);
 }
 
 // Rows below the diagonal block of panel `step` (64-row tiles; wave w owns 16 rows): blocked
@@ -2255,10 +2282,12 @@ __global__ __launch_bounds__(NT) void k_big_trsm(FrontTab T, const int32_t* __re
 // staged through LDS one after another; the next chunk's operands are loaded (from
 // clamped addresses) while the current chunk's MFMAs run.
 __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __restrict__ list, int step, int kpan,
-                                                   double* __restrict__ arena, const double* __restrict__ D) {
+                                                   double* __restrict__ arena, double* __restrict__ D,
+                                                   double* __restrict__ Mbuf, LDLStatus* st, double tol) {
   constexpr int LDT = 80;  // [k][row] layout: conflict-free ds_read_b64 for the 16x4 operand pattern
   __shared__ __attribute__((aligned(16))) double Wt[64 * LDT];
   __shared__ __attribute__((aligned(16))) double Lt[64 * LDT];
+  static_assert(64 * LDA <= 64 * LDT && 4 * 16 * LDM + 64 <= 64 * LDT, "lookahead diagonal block aliases Wt / Lt");
   int s, tij;
   task_of(list, s, tij);
   const int ti = tij & 0xffff, tj = (tij >> 16) & 0x7fff;
@@ -2346,6 +2375,28 @@ __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __
         const int j = J0 + qc + bj * 16 + (lane >> 4) + 4 * g;
         if (i < r && j < jlim && i >= j) F[i + (int64_t)j * r] = c[bj][bi][g] - acc[bj][bi][g];
       }
+  // lookahead: task (0, 0) of a local update holds the next panel's diagonal tile, final now (the
+  // panel's last local update; the next panel lies inside the group, below jlim)
+  if (!trailing && ti == 0 && tj == 0 && big_next_diag(T, s, step)) {
+    double* A64 = Wt;  // the operand tiles are free: aliased by the diagonal block, M_K and pivots
+    double* Ms = Lt;
+    double* Dl = Lt + 4 * 16 * LDM;
+    const int kw = min(64, w - c0);
+    __syncthreads();  // every wave's last MFMA operand read
+    big_diag_prepare(A64, kw);
+    __syncthreads();
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int i = qr + bi * 16 + (lane & 15), j = qc + bj * 16 + (lane >> 4) + 4 * g;
+          if (i < kw && j < kw && i >= j) A64[i + j * LDA] = c[bj][bi][g] - acc[bj][bi][g];
+        }
+    __syncthreads();
+    big_diag_tail(T, s, step + 1, A64, Ms, Dl, arena, D, Mbuf, st, tol);
+  }
 }
 
 // (pos, neg, zero) of D over the columns with colmask == want (colmask NULL: all)
@@ -2529,9 +2580,13 @@ __global__ __launch_bounds__(NT, SYRK_WAVES) void k_lb_syrk(const double* __rest
 // A 128-tile reads 2 x 128 K doubles per 2 x 128^2 K flops — twice k_big_update's 64-tile arithmetic
 // intensity, on the update that carries ~90 % of neos' factorisation flops.
 __global__ __launch_bounds__(NT, 2) void k_big_upd128(FrontTab T, const int32_t* __restrict__ list, int step, int kpan,
-                                                     double* __restrict__ arena, const double* __restrict__ D) {
-  __shared__ __attribute__((aligned(16))) double As[2][SYK * SYLD];  // (L D)[I rows]
-  __shared__ __attribute__((aligned(16))) double Bs[2][SYK * SYLD];  // L[J rows]
+                                                     double* __restrict__ arena, double* __restrict__ D,
+                                                     double* __restrict__ Mbuf, LDLStatus* st, double tol) {
+  // one buffer: As[2] then Bs[2]; after the MFMAs task (0, 0) reuses it for the lookahead diagonal block
+  __shared__ __attribute__((aligned(16))) double AB[4 * SYK * SYLD];
+  double (*As)[SYK * SYLD] = reinterpret_cast<double (*)[SYK * SYLD]>(AB);           // (L D)[I rows]
+  double (*Bs)[SYK * SYLD] = reinterpret_cast<double (*)[SYK * SYLD]>(AB + 2 * SYK * SYLD);  // L[J rows]
+  static_assert(64 * LDA + 4 * 16 * LDM + 64 <= 4 * SYK * SYLD, "lookahead diagonal block aliases As / Bs");
   int s, tij;
   task_of(list, s, tij);
   const int ti = tij & 0xffff, tj = (tij >> 16) & 0x7fff;
@@ -2614,7 +2669,32 @@ __global__ __launch_bounds__(NT, 2) void k_big_upd128(FrontTab T, const int32_t*
       for (int g = 0; g < 4; ++g) {
         const int i = I0 + wm + 16 * b + (lane & 15), j = J0 + wn + 16 * a + (lane >> 4) + 4 * g;
         if (i < r && j <= i) F[i + (int64_t)j * r] = fv[b][g] - acc[a][b][g];
+        acc[a][b][g] = fv[b][g] - acc[a][b][g];  // kept for the lookahead diagonal block below
       }
+  }
+  // lookahead: task (0, 0) holds the next panel's diagonal tile (rows / columns [c0, c0 + 64): wave 0's
+  // quadrant), final now — the group's trailing update is its last before that panel
+  if (ti == 0 && tj == 0 && 64 * (step + 1) == c0 && big_next_diag(T, s, step)) {
+    double* A64 = AB;
+    double* Ms = AB + 64 * LDA;
+    double* Dl = Ms + 4 * 16 * LDM;
+    const int kw = min(64, w - c0);
+    __syncthreads();  // every wave's last MFMA operand read
+    big_diag_prepare(A64, kw);
+    __syncthreads();
+    if (wv == 0) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int i = 16 * b + (lane & 15), j = 16 * a + (lane >> 4) + 4 * g;
+            if (i < kw && j < kw && i >= j) A64[i + j * LDA] = acc[a][b][g];
+          }
+    }
+    __syncthreads();
+    big_diag_tail(T, s, step + 1, A64, Ms, Dl, arena, D, Mbuf, st, tol);
   }
 }
 
@@ -4460,7 +4540,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
           kf[0] += dk * dk * dk / 3.0;
           kb[1] += 8.0 * (2.0 * nb * dk + nt * (dk * (dk + 1) / 2 + 4 * 16 * 17));  // trsm: rows in/out + L11, M per tile
           kf[1] += nb * dk * dk;
-          td.insert(td.end(), {s, 0});
+          if (p == 0) td.insert(td.end(), {s, 0});  // later panels: the previous update's task (0, 0)
           for (int i = 0; i < nt; ++i) tt.insert(tt.end(), {s, i});
           if (S.fused[s]) continue;  // its trailing update: k_asm_update (below)
           // deferred multi-panel update (k_big_update): panel groups of big_kpan_ panels; inside a
@@ -4485,13 +4565,17 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         }
         const std::pair<int, std::vector<int32_t>*> kinds[4] = {
             {BIG_DIAG, &td}, {BIG_TRSM, &tt}, {BIG_UPDATE, &tu}, {BIG_UPDATE128, &tu128}};
+        bool alg_done = false;  // the panels' 8(d) bytes ride on the step's first launch (k_big_diag at
+                                // step 0, k_big_trsm after: the diagonal blocks are factorised by the
+                                // previous step's update launch)
         for (int q = 0; q < 4; ++q) {
           const auto& kv = kinds[q];
           if (kv.second->empty()) continue;
           align2();
           Launch L{kv.first, p, (int64_t)sched.size(), 0, (int64_t)kv.second->size() / 2};
           L.bytes = kb[q];
-          L.alg = q == 0 ? ka : 0.0;
+          L.alg = alg_done ? 0.0 : ka;
+          alg_done = true;
           L.flops = kf[q];
           out.push_back(L);
           sched.insert(sched.end(), kv.second->begin(), kv.second->end());
@@ -4971,7 +5055,8 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
         break;
       case BIG_UPDATE:
         TIMED(KK_UPDATE, L.bytes, 0.0, L.flops,
-              (k_big_update<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, big_kpan_, arena_, D_)));
+              (k_big_update<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, big_kpan_, arena_, D_, minv_, st_,
+                                                              pivot_tol)));
         break;
       case ASM_UPDATE:
         TIMED(KK_ASM_UPDATE, L.bytes, 0.0, L.flops,
@@ -4979,7 +5064,8 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
         break;
       case BIG_UPDATE128:
         TIMED(KK_UPDATE, L.bytes, 0.0, L.flops,
-              (k_big_upd128<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, big_kpan_, arena_, D_)));
+              (k_big_upd128<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, big_kpan_, arena_, D_, minv_, st_,
+                                                              pivot_tol)));
         break;
       case LB_BUILD:
         TIMED(KK_LB_BUILD, L.bytes, L.alg, 0.0,
