@@ -5051,10 +5051,10 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
               (k_big_diag<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_, minv_, st_, pivot_tol)));
         break;
       case BIG_TRSM:
-        TIMED(KK_TRSM, L.bytes, 0.0, L.flops, (k_big_trsm<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_, minv_)));
+        TIMED(KK_TRSM, L.bytes, L.alg, L.flops, (k_big_trsm<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, arena_, D_, minv_)));
         break;
       case BIG_UPDATE:
-        TIMED(KK_UPDATE, L.bytes, 0.0, L.flops,
+        TIMED(KK_UPDATE, L.bytes, L.alg, L.flops,
               (k_big_update<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, big_kpan_, arena_, D_, minv_, st_,
                                                               pivot_tol)));
         break;
@@ -5063,7 +5063,7 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
               (k_asm_update<<<(unsigned)L.items, ANT, 0, s>>>(T_, atiles_.p + L.off, g_ptr_, gpart_, bt_, arena_, D_)));
         break;
       case BIG_UPDATE128:
-        TIMED(KK_UPDATE, L.bytes, 0.0, L.flops,
+        TIMED(KK_UPDATE, L.bytes, L.alg, L.flops,
               (k_big_upd128<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, big_kpan_, arena_, D_, minv_, st_,
                                                               pivot_tol)));
         break;
