@@ -12,6 +12,8 @@
 // Quasi-definite KKT matrices (FixedRegularization(1e-8,-1e-8)) admit static
 // pivoting in any symmetric order; zero / non-finite pivots are reported (is_factorized=false).
 #include <algorithm>
+#include <atomic>
+#include <thread>
 #include <array>
 #include <map>
 #include <climits>
@@ -503,12 +505,12 @@ __global__ __launch_bounds__(NT) void k_asm_chunks(const int64_t* __restrict__ g
 // clamped addresses) and adds them, masked, in child order.  No atomics, deterministic, and no
 // barrier per child (r3 put one barrier and one round trip per child and tile: neos 8 ms per
 // factorisation).  The tile is written to the front (big: arena, ld r; small: scratch, ld r).
-constexpr int ANT = 1024, ABN = 8;
+constexpr int ANT = 1024, ABN = 4;
 // the tile's entries (this thread's: tile-local rows ei[m], columns ej[m], m < 4; the 1024 threads
 // cover the 64 x 64 tile) = chunk sums + big children's blocks
 __device__ __forceinline__ void asm_tile_sum(const FrontTab& T, const SymbolicPlan::AsmTile& tl,
                                              const int32_t* __restrict__ gptr, const double* __restrict__ part,
-                                             const int32_t* __restrict__ bt, const double* __restrict__ arena,
+                                             const BigChildRec* __restrict__ brec, const double* __restrict__ arena,
                                              const int (&ei)[4], const int (&ej)[4], double (&v)[4]) {
   const int ti = tl.tij & 0xffff, tj = (tl.tij >> 16) & 0x7fff;
   const int I0 = ti * 64, J0 = tj * 64;
@@ -542,62 +544,51 @@ __device__ __forceinline__ void asm_tile_sum(const FrontTab& T, const SymbolicPl
           if (q0[k] + it + u < q1[k]) v[k] += x[k][u];
     }
   }
-  if (tl.bt1 > tl.bt0) {
-    __shared__ int32_t rmap[ABN][64], cmap[ABN][64];
-    __shared__ int64_t suo[ABN];
-    __shared__ int32_t sld[ABN];
-    for (int kc = tl.bt0; kc < tl.bt1; kc += ABN) {
-      const int nk = min(ABN, tl.bt1 - kc);
-      // maps of the batch: -1, then child rows a in [a0, a1) at their tile rows (rel ascending: each
-      // tile row receives at most one child row), the same for the columns
-      if (tid < ABN * 64) {
-        rmap[tid >> 6][lane] = -1;
-        cmap[tid >> 6][lane] = -1;
+  // big children: their (tile, child) records hold the tile's row / column maps (tile row -> child
+  // row, -1 outside the child; built once at plan time) and the child's U block: every thread reads
+  // its own entries' map slots and U entries — two dependent round trips per batch of ABN children,
+  // no LDS, no barrier (r3 staged the table in LDS and added children two by two between barriers;
+  // r4's first version built the maps in LDS from rel per batch: one round trip and two barriers more)
+  for (int kc = tl.bt0; kc < tl.bt1; kc += ABN) {  // uniform
+    const int nk = min(ABN, tl.bt1 - kc);
+    int64_t uo[ABN];
+    int ldc[ABN], a[ABN][4], bb[ABN][4];
+#pragma unroll
+    for (int k = 0; k < ABN; ++k) {
+      const BigChildRec& R = brec[kc + min(k, nk - 1)];
+      uo[k] = R.u_off;
+      ldc[k] = R.u_ld;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        a[k][m] = R.rmap[ei[m]];
+        bb[k][m] = R.cmap[ej[m]];
       }
-      __syncthreads();
-      if (tid < nk * 64) {
-        const int k = tid >> 6;
-        const int32_t* e = bt + 5 * (kc + k);
-        const int c = e[0], b0 = e[1], b1 = e[2], a0 = e[3], a1 = e[4];
-        const int32_t* __restrict__ rel = T.rel + T.rel_ptr[c];
-        if (a0 + lane < a1) rmap[k][rel[a0 + lane] - I0] = a0 + lane;
-        if (b0 + lane < b1) cmap[k][rel[b0 + lane] - J0] = b0 + lane;
-        if (lane == 0) {
-          suo[k] = T.u_off[c];
-          sld[k] = (int32_t)T.u_ld[c];
-        }
-      }
-      __syncthreads();
-      // every load of the batch first (clamped to entry (0, 0) of the child's block), then the adds
-      double x[ABN][4];
-      int ok[ABN];
-#pragma unroll
-      for (int k = 0; k < ABN; ++k) {
-        const int kk = min(k, nk - 1);
-        const double* __restrict__ U = arena + suo[kk];
-        const int64_t ldc = sld[kk];
-        ok[k] = 0;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const int a = rmap[kk][ei[m]], bb = cmap[kk][ej[m]];
-          const bool hit = k < nk && a >= 0 && bb >= 0 && a >= bb;
-          x[k][m] = U[(hit ? a : 0) + (int64_t)(hit ? bb : 0) * ldc];
-          ok[k] |= (int)hit << m;
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < ABN; ++k)
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-          if ((ok[k] >> m) & 1) v[m] += x[k][m];
-      __syncthreads();  // the maps are rebuilt by the next batch
     }
+    // every U load of the batch first (clamped to entry (0, 0) of the child's block), then the adds
+    double x[ABN][4];
+#pragma unroll
+    for (int k = 0; k < ABN; ++k)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const bool hit = k < nk && a[k][m] >= 0 && bb[k][m] >= 0 && a[k][m] >= bb[k][m];
+        x[k][m] = arena[uo[k] + (hit ? a[k][m] + (int64_t)bb[k][m] * ldc[k] : 0)];
+        a[k][m] = hit;
+      }
+#pragma unroll
+    for (int k = 0; k < ABN; ++k)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        if (a[k][m]) v[m] += x[k][m];
   }
+  (void)tid;
+  (void)lane;
+  (void)I0;
+  (void)J0;
 }
 
 __global__ __launch_bounds__(ANT) void k_assemble(FrontTab T, const SymbolicPlan::AsmTile* __restrict__ tiles,
                                                   const int32_t* __restrict__ gptr, const double* __restrict__ part,
-                                                  const int32_t* __restrict__ bt, double* __restrict__ arena,
+                                                  const BigChildRec* __restrict__ brec, double* __restrict__ arena,
                                                   double* __restrict__ fscratch) {
   const SymbolicPlan::AsmTile tl = tiles[blockIdx.x];
   const int s = tl.front, ti = tl.tij & 0xffff, tj = (tl.tij >> 16) & 0x7fff;
@@ -607,7 +598,7 @@ __global__ __launch_bounds__(ANT) void k_assemble(FrontTab T, const SymbolicPlan
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   double v[4];
   const int ei[4] = {lane, lane, lane, lane}, ej[4] = {wv, wv + 16, wv + 32, wv + 48};
-  asm_tile_sum(T, tl, gptr, part, bt, arena, ei, ej, v);
+  asm_tile_sum(T, tl, gptr, part, brec, arena, ei, ej, v);
   const int64_t fso = T.fs_off[s];
   double* __restrict__ F = (fso >= 0 ? fscratch + fso : arena + T.l_off[s]);
   const int i = I0 + lane;
@@ -636,7 +627,7 @@ __global__ __launch_bounds__(ANT) void k_assemble(FrontTab T, const SymbolicPlan
 constexpr int AU_LDT = 80;  // [k][row] operand stride (conflict-free ds_read_b64 for the 16x4 pattern)
 __global__ __launch_bounds__(ANT) void k_asm_update(FrontTab T, const SymbolicPlan::AsmTile* __restrict__ tiles,
                                                     const int32_t* __restrict__ gptr, const double* __restrict__ part,
-                                                    const int32_t* __restrict__ bt, double* __restrict__ arena,
+                                                    const BigChildRec* __restrict__ brec, double* __restrict__ arena,
                                                     const double* __restrict__ D, int kmax) {
   extern __shared__ __attribute__((aligned(16))) double AUs[];
   double* Wt = AUs;                  // (L D)[I rows], kmax x AU_LDT
@@ -676,7 +667,7 @@ __global__ __launch_bounds__(ANT) void k_asm_update(FrontTab T, const SymbolicPl
     ej[g] = 16 * bj + (lane >> 4) + 4 * g;
   }
   double v[4];
-  asm_tile_sum(T, tl, gptr, part, bt, arena, ei, ej, v);
+  asm_tile_sum(T, tl, gptr, part, brec, arena, ei, ej, v);
   __syncthreads();  // the operands in LDS
   dbl4 acc = {0.0, 0.0, 0.0, 0.0};
   const int nks = (w + 3) >> 2;
@@ -4178,7 +4169,34 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   }
   g_chunk_.upload(S.g_chunk);
   gpart_.alloc(std::max<size_t>(S.g_chunk.size(), 1));
-  bt_.upload(S.bt);
+  {  // big-child records of the assembly tiles (BigChildRec): the tile's row / column maps from rel
+    const int64_t nb = (int64_t)S.bt.size() / 5;
+    std::vector<BigChildRec> br(std::max<int64_t>(nb, 1));
+    const int T = (int)std::min<int64_t>(analysis_threads(), std::max<int64_t>(1, nb / 4096));
+    std::vector<std::thread> th;
+    std::atomic<bool> bad{false};
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t]() {
+        for (int64_t k = t; k < nb; k += T) {
+          const int32_t* e = &S.bt[5 * k];
+          const int c = e[0], b0 = e[1], b1 = e[2], a0 = e[3], a1 = e[4];
+          const int32_t* rel = S.rel.data() + S.rel_ptr[c];
+          BigChildRec& R = br[k];
+          R.u_off = S.u_off[c];
+          R.u_ld = S.u_ld[c];
+          R.pad = 0;
+          std::fill(R.rmap, R.rmap + 64, (int16_t)-1);
+          std::fill(R.cmap, R.cmap + 64, (int16_t)-1);
+          const int I0 = rel[a0] & ~63, J0 = rel[b0] & ~63;
+          if (a1 > 32767 || b1 > 32767) bad = true;  // int16 maps
+          for (int q = a0; q < a1; ++q) R.rmap[rel[q] - I0] = (int16_t)q;
+          for (int q = b0; q < b1; ++q) R.cmap[rel[q] - J0] = (int16_t)q;
+        }
+      });
+    for (auto& x : th) x.join();
+    MADIPM_REQUIRE(!bad, "assembly: a child update block of more than 32767 rows");
+    brec_.upload(br);
+  }
   fscratch_.alloc(std::max<int64_t>(S.fs_size, 1));
   T_.fs_off = fs_off_;
   {
@@ -5038,7 +5056,7 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
                             : k_asm_chunks<int64_t><<<(unsigned)cdiv(L.nchunk, NT), NT, 0, s>>>(
                                   g_chunk_, g_src_, L.chunk0, L.nchunk, Kx, arena_, gpart_)));
         TIMED(KK_ASSEMBLE, L.bytes, 0.0, L.flops,
-              (k_assemble<<<(unsigned)L.items, ANT, 0, s>>>(T_, atiles_.p + L.off, g_ptr_, gpart_, bt_, arena_, fscratch_)));
+              (k_assemble<<<(unsigned)L.items, ANT, 0, s>>>(T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_)));
         break;
       case MICRO:
         TIMED(KK_TINY, L.bytes, L.alg, L.flops,
@@ -5076,7 +5094,7 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
       case ASM_UPDATE:  // nf = the launch's K rows (the widest panel, rounded up to 4)
         TIMED(KK_ASM_UPDATE, L.bytes, 0.0, L.flops,
               (k_asm_update<<<(unsigned)L.items, ANT, 2 * L.nf * AU_LDT * 8, s>>>(T_, atiles_.p + L.off, g_ptr_, gpart_,
-                                                                                   bt_, arena_, D_, L.nf)));
+                                                                                   brec_, arena_, D_, L.nf)));
         break;
       case BIG_UPDATE128:
         TIMED(KK_UPDATE, L.bytes, L.alg, L.flops,

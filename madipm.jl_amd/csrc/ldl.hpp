@@ -73,6 +73,14 @@ struct FrontTab {
   int pipe_fault;   // tests (MADIPM_DEBUG_PIPE_FAULT=1): blocked_factor_pipe drops one hand-off
 };
 
+// assembly: a big child's block on one 64x64 tile of its parent (SymbolicPlan::bt entry): the tile's
+// row and column maps (tile row -> the child's update row, -1 outside the child) and the child's U
+struct BigChildRec {
+  int64_t u_off;
+  int32_t u_ld, pad;
+  int16_t rmap[64], cmap[64];
+};
+
 struct SolveTask {
   int32_t front, blk;
 };
@@ -343,7 +351,8 @@ class LDLSolver : public LinSolver {
   int epoch_ = 0;
   // device data
   DBuf<int32_t> first_, nrows_, rows_, u_ld_, child_ptr_, child_list_, rel_, perm_, sched_;
-  DBuf<int32_t> bigslot_, g_ptr_, bt_;
+  DBuf<int32_t> bigslot_, g_ptr_;
+  DBuf<BigChildRec> brec_;
   DBuf<int64_t> fs_off_, sv_ptr_, sv_src_, g_src_, g_chunk_;
   DBuf<int32_t> g_src32_;
   DBuf<SymbolicPlan::AsmTile> atiles_;
