@@ -3353,6 +3353,7 @@ __global__ __launch_bounds__(NT) void k_bwd_big(FrontTab T, const SolveTask* __r
 // block loads its L entries unconditionally (16-byte LDS reads, immediate offsets) and the
 // dependency chain is one readlane + one fma per pivot.
 // dynamic LDS of the tree solves (+ ~2 KB static): two 256-thread workgroups per CU
+constexpr int TREE_ROOT_LDS = 150 * 1024;  // the big etree roots' own forward launch (LDSolver: nroot_task_)
 constexpr int TREE_SOLVE_LDS = 76 * 1024;
 __device__ __forceinline__ int tree_ldt(int w) { return ((w + 15) & ~15) + 2; }  // forward: row-major ld
 __device__ __forceinline__ int tree_ldc(int r) { return ((r + 31) & ~31) + 2; }  // backward: col-major ld
@@ -4755,10 +4756,21 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     };
     build_solve(1, slev1_);
     {  // tree solve tables
-      std::vector<int32_t> ord;
+      // elimination-tree roots (r == w, no parent) whose panel needs more LDS than the tree launches'
+      // TREE_SOLVE_LDS (two workgroups per CU) go last, into their own forward launch with the LDS they
+      // need (ex10's 120-column coupling root: 125 KB), solved forward and backward there in one pass
+      // (r3: the root sized every tree task's LDS; r4's first cut streamed it in chunks: slower)
+      auto big_root = [&](int s) {
+        const int r = S.nrows[s], w = S.first[s + 1] - S.first[s];
+        const int64_t need = 8 * tree_panel_doubles(s) + 8 * 1024;
+        return S.parent[s] < 0 && r == w && r <= SMALL_SOLVE_MAX && need > TREE_SOLVE_LDS && need <= TREE_ROOT_LDS;
+      };
+      std::vector<int32_t> ord, roots;
       for (int lev = 0; lev < NL; ++lev)
         for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q)
-          if (in_tree[S.level_list[q]]) ord.push_back(S.level_list[q]);
+          if (in_tree[S.level_list[q]]) (big_root(S.level_list[q]) ? roots : ord).push_back(S.level_list[q]);
+      nroot_task_ = (int)roots.size();
+      ord.insert(ord.end(), roots.begin(), roots.end());
       ntree_ = (int)ord.size();
       // children of tree fronts scatter their forward update entries straight into the parent's
       // gather range (sv order, gbuf); everyone else keeps its own update vector (uvec)
@@ -4779,9 +4791,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         tree_bytes_ += 8.0 * (r * w + 3.0 * r);
         tree_flops_ += 2.0 * (r * w - w * (w + 1) / 2);
         tree_alg_ += solve_alg(s);
-        chunk[s] = S.nrows[s] > SMALL_SOLVE_MAX || 8 * tree_panel_doubles(s) + 8 * 1024 > TREE_SOLVE_LDS;
-        tree_lds_ = std::max<int>(tree_lds_, chunk[s] ? 8 * std::max(MED_FWD_LDS, MED_BWD_LDS)
-                                                      : 8 * tree_panel_doubles(s) + 8 * 1024);
+        chunk[s] = !big_root(s) && (S.nrows[s] > SMALL_SOLVE_MAX || 8 * tree_panel_doubles(s) + 8 * 1024 > TREE_SOLVE_LDS);
+        if (big_root(s)) root_lds_ = std::max<int>(root_lds_, 8 * tree_panel_doubles(s) + 8 * 1024);
       }
       tree_lds_ = TREE_SOLVE_LDS;  // the rest of the budget stages gather sources
       tchunk_.upload(chunk);
@@ -4911,7 +4922,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_small_blocked<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    192 * 193 / 2 * 8));
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_bwd_small, hipFuncAttributeMaxDynamicSharedMemorySize, 129 * 128 * 8));
-    MADIPM_HIP(hipFuncSetAttribute((const void*)k_fwd_tree, hipFuncAttributeMaxDynamicSharedMemorySize, TREE_SOLVE_LDS));
+    MADIPM_HIP(hipFuncSetAttribute((const void*)k_fwd_tree, hipFuncAttributeMaxDynamicSharedMemorySize, TREE_ROOT_LDS));
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_fact_tree, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)SymbolicPlan::kFactTreeLdsMax));
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_bwd_tree, hipFuncAttributeMaxDynamicSharedMemorySize, TREE_SOLVE_LDS));
@@ -5353,11 +5364,21 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
             (k_fwd_leaves<<<(unsigned)cdiv(nsleaf_ * LPL, NT), NT, 0, s>>>(tleaf_, (int)nsleaf_, tlrow_, arena_, b, xi_,
                                                                          T_.gbuf)));
     if (lev == 0 && phase == 0 && ntree_)
-      TIMED(KK_FWD_TREE, tree_bytes_, tree_alg_, tree_flops_,
-            (k_fwd_tree<<<(unsigned)ntask_, NT, tree_lds_, s>>>(T_, tc_ptr_, tc_list_, ntask_, tdep_ptr_, tdep_,
-                                                                 counters_.p + 4 * S_.nlevels, tflags_, efwd, tree_lds_ / 8,
-                                                                 arena_, b, xi_, uvec_, &st_->err, tdbg_.p, trootbwd_, D_,
-                                                                 tchunk_)));
+    {
+      const int nlo = ntask_ - nroot_task_;  // the big roots last, in their own launch (more LDS)
+      if (nlo > 0)
+        TIMED(KK_FWD_TREE, tree_bytes_, tree_alg_, tree_flops_,
+              (k_fwd_tree<<<(unsigned)nlo, NT, tree_lds_, s>>>(T_, tc_ptr_, tc_list_, nlo, tdep_ptr_, tdep_,
+                                                              counters_.p + 4 * S_.nlevels, tflags_, efwd, tree_lds_ / 8,
+                                                              arena_, b, xi_, uvec_, &st_->err, tdbg_.p, trootbwd_, D_,
+                                                              tchunk_)));
+      if (nroot_task_)
+        TIMED(KK_FWD_TREE, nlo > 0 ? 0.0 : tree_bytes_, nlo > 0 ? 0.0 : tree_alg_, nlo > 0 ? 0.0 : tree_flops_,
+              (k_fwd_tree<<<(unsigned)nroot_task_, NT, root_lds_, s>>>(
+                  T_, tc_ptr_.p + nlo, tc_list_, nroot_task_, tdep_ptr_.p + nlo, tdep_, counters_.p + 4 * S_.nlevels + 2,
+                  tflags_, efwd, root_lds_ / 8, arena_, b, xi_, uvec_, &st_->err, tdbg_.p ? tdbg_.p + 8 * nlo : nullptr,
+                  trootbwd_.p + nlo, D_, tchunk_)));
+    }
     if (lev == 0 && phase == 0 && ntree_ && tdbg_.p)
       tree_debug_dump(s, "fwd", tdbg_.p, ntask_, "leaves", "wait", "gather", "subst", "store", 8);
   }

@@ -1352,8 +1352,11 @@ static int par_threads(int64_t n, int64_t grain = (int64_t)1 << 20) {
 // sort by row — per-thread row counts over input chunks, offsets in thread order — then each row's
 // run sorted by column only when it is not already (O(nnz) for the usual column- or row-major input;
 // a comparison sort of 1e9 dense-QP entries took minutes) and duplicates merged
-static void csr_from_coo(int nrow, int64_t nnz, const int32_t* r, const int32_t* c, const double* v,
-                         std::vector<int64_t>& rp, std::vector<int32_t>& ci, std::vector<double>& cv) {
+// entry k of the COO: row R(k), column C(k), value V(k) (accessors: the scaled Jacobian is read
+// straight from the caller's A, no COO copy); the CSR arrays are filled in full by the threads
+template <class R, class C, class V>
+static void csr_from_coo(int nrow, int64_t nnz, R r, C c, V v, std::vector<int64_t>& rp, hvec<int32_t>& ci,
+                         hvec<double>& cv) {
   const int T = par_threads(nnz);
   std::vector<std::vector<int64_t>> cnt(T, std::vector<int64_t>(nrow + 1, 0));
   auto chunk = [&](int t) { return std::make_pair(nnz * t / T, nnz * (t + 1) / T); };
@@ -1363,7 +1366,7 @@ static void csr_from_coo(int nrow, int64_t nnz, const int32_t* r, const int32_t*
       th.emplace_back([&, t] {
         auto [k0, k1] = chunk(t);
         int64_t* cn = cnt[t].data();
-        for (int64_t k = k0; k < k1; ++k) cn[r[k]]++;
+        for (int64_t k = k0; k < k1; ++k) cn[r(k)]++;
       });
     for (auto& x : th) x.join();
   }
@@ -1377,8 +1380,8 @@ static void csr_from_coo(int nrow, int64_t nnz, const int32_t* r, const int32_t*
     }
     start[i + 1] = acc;
   }
-  std::vector<int32_t> tc(nnz);
-  std::vector<double> tv(nnz);
+  hvec<int32_t> tc(nnz);
+  hvec<double> tv(nnz);
   {
     std::vector<std::thread> th;
     for (int t = 0; t < T; ++t)
@@ -1386,9 +1389,9 @@ static void csr_from_coo(int nrow, int64_t nnz, const int32_t* r, const int32_t*
         auto [k0, k1] = chunk(t);
         int64_t* off = cnt[t].data();
         for (int64_t k = k0; k < k1; ++k) {
-          const int64_t q = off[r[k]]++;
-          tc[q] = c[k];
-          tv[q] = v[k];
+          const int64_t q = off[r(k)]++;
+          tc[q] = c(k);
+          tv[q] = v(k);
         }
       });
     for (auto& x : th) x.join();
@@ -1420,8 +1423,8 @@ static void csr_from_coo(int nrow, int64_t nnz, const int32_t* r, const int32_t*
     return;
   }
   rp = uniq;
-  ci.assign(uniq[nrow], 0);
-  cv.assign(uniq[nrow], 0.0);
+  ci.resize(uniq[nrow]);
+  cv.resize(uniq[nrow]);
   par_range(nrow, [&](int, int64_t i0, int64_t i1) {
     for (int64_t i = i0; i < i1; ++i) {
       int64_t o = rp[i] - 1;
@@ -1438,9 +1441,12 @@ static void csr_from_coo(int nrow, int64_t nnz, const int32_t* r, const int32_t*
   }, 4096);
 }
 static void csr_from_coo(int nrow, const std::vector<int32_t>& r, const std::vector<int32_t>& c,
-                         const std::vector<double>& v, std::vector<int64_t>& rp, std::vector<int32_t>& ci,
-                         std::vector<double>& cv) {
-  csr_from_coo(nrow, (int64_t)r.size(), r.data(), c.data(), v.data(), rp, ci, cv);
+                         const std::vector<double>& v, std::vector<int64_t>& rp, hvec<int32_t>& ci, hvec<double>& cv) {
+  const int32_t *rr = r.data(), *cc = c.data();
+  const double* vv = v.data();
+  csr_from_coo(
+      nrow, (int64_t)r.size(), [=](int64_t k) { return rr[k]; }, [=](int64_t k) { return cc[k]; },
+      [=](int64_t k) { return vv[k]; }, rp, ci, cv);
 }
 
 MPCSolver::MPCSolver(const madipm_qp& qp, const madipm_options& opt, Comm* comm) : opt_(opt), comm_(comm) {
@@ -1657,16 +1663,17 @@ void MPCSolver::setup_host(const madipm_qp& q) {
     }
   }
   std::vector<int64_t> Hrp;
-  std::vector<int32_t> Hci;
-  std::vector<double> Hcv;
+  hvec<int32_t> Hci;
+  hvec<double> Hcv;
   csr_from_coo(n, hr, hc, hv, Hrp, Hci, Hcv);
-  // scaled Jacobian with slack columns (m x n); fixed columns zeroed (their term -> cfix)
+  // scaled Jacobian with slack columns (m x n); fixed columns zeroed (their term -> cfix).  Without a
+  // fixed column every entry is kept in input order and read straight from the caller's A
   std::vector<int32_t> jr, jc;
   std::vector<double> jv;
+  bool anyfix = false;
+  for (int i = 0; i < nx && !anyfix; ++i) anyfix = P.fixed[i];
   {
     const int64_t nz = P.nnzA;
-    bool anyfix = false;
-    for (int i = 0; i < nx && !anyfix; ++i) anyfix = P.fixed[i];
     if (anyfix) {  // cfix sums in input order: the sequential pass
       for (int64_t k = 0; k < nz; ++k) {
         const int r = P.Ar[k], c = P.Ac[k];
@@ -1679,34 +1686,33 @@ void MPCSolver::setup_host(const madipm_qp& q) {
         jc.push_back(c);
         jv.push_back(v);
       }
-    } else {  // no fixed column: every entry kept, in input order
-      jr.resize(nz);
-      jc.resize(nz);
-      jv.resize(nz);
-      par_range(nz, [&](int, int64_t a, int64_t b) {
-        for (int64_t k = a; k < b; ++k) {
-          const int r = P.Ar[k];
-          jr[k] = r;
-          jc[k] = P.Ac[k];
-          jv[k] = P.con_scale[r] * P.Av[k];
-        }
-      });
+      for (int k = 0; k < P.ns; ++k) {
+        jr.push_back(P.ind_ineq[k]);
+        jc.push_back(nx + k);
+        jv.push_back(-1.0);
+      }
     }
-  }
-  for (int k = 0; k < P.ns; ++k) {
-    jr.push_back(P.ind_ineq[k]);
-    jc.push_back(nx + k);
-    jv.push_back(-1.0);
   }
   clk("H CSR + J COO");
   std::vector<int64_t> Jrp, JTrp;
-  std::vector<int32_t> Jci, JTci;
-  std::vector<double> Jcv, JTcv;
-  csr_from_coo(m, jr, jc, jv, Jrp, Jci, Jcv);
-  csr_from_coo(n, jc, jr, jv, JTrp, JTci, JTcv);
-  std::vector<int32_t>().swap(jr);
-  std::vector<int32_t>().swap(jc);
-  std::vector<double>().swap(jv);
+  hvec<int32_t> Jci, JTci;
+  hvec<double> Jcv, JTcv;
+  if (anyfix) {
+    csr_from_coo(m, jr, jc, jv, Jrp, Jci, Jcv);
+    csr_from_coo(n, jc, jr, jv, JTrp, JTci, JTcv);
+    std::vector<int32_t>().swap(jr);
+    std::vector<int32_t>().swap(jc);
+    std::vector<double>().swap(jv);
+  } else {  // entries k < nnzA: A's (scaled); then one -1 per slack column
+    const int64_t na = P.nnzA, nj = na + P.ns;
+    const int32_t *Ar = P.Ar, *Ac = P.Ac, *ineq = P.ind_ineq.data();
+    const double *Av = P.Av, *cs = P.con_scale.data();
+    auto row = [=](int64_t k) { return k < na ? Ar[k] : ineq[k - na]; };
+    auto col = [=](int64_t k) { return k < na ? Ac[k] : (int32_t)(nx + (k - na)); };
+    auto val = [=](int64_t k) { return k < na ? cs[Ar[k]] * Av[k] : -1.0; };
+    csr_from_coo(m, nj, row, col, val, Jrp, Jci, Jcv);
+    csr_from_coo(n, nj, col, row, val, JTrp, JTci, JTcv);
+  }
   clk("J, J^T CSR");
   std::vector<double> cs(n, 0.0);
   for (int i = 0; i < nx; ++i) cs[i] = P.obj_scale * P.sgn * P.c[i];
@@ -1715,8 +1721,8 @@ void MPCSolver::setup_host(const madipm_qp& q) {
   // columns: column j < n = [j; H's rows i > j (row j of the symmetric CSR H, ascending); n + the rows r
   // of column j of J (row j of J^T's CSR, ascending)], column j >= n = [j]
   std::vector<int64_t> Kcp(n + m + 1, 0);
-  std::vector<int32_t> Kri;
-  std::vector<double> Kv;
+  hvec<int32_t> Kri;
+  hvec<double> Kv;
   {
     std::vector<int64_t> hup(n, 0);  // per column: H entries below the diagonal
     for (int i = 0; i < n; ++i)
@@ -1885,10 +1891,12 @@ void MPCSolver::setup_host(const madipm_qp& q) {
     zeros(Dinv_, n);
     zeros(bufm_, m);
   } else if (kkt_ == KKT_K25) {
-    std::vector<int32_t> krow(Kri), kcol(Kri.size());
-    for (int j = 0; j < n + m; ++j)
-      for (int64_t q = Kcp[j]; q < Kcp[j + 1]; ++q) kcol[q] = j;
-    up(Krow_, krow);
+    hvec<int32_t> kcol(Kri.size());
+    par_range(n + m, [&](int, int64_t j0, int64_t j1) {
+      for (int64_t j = j0; j < j1; ++j)
+        for (int64_t q = Kcp[j]; q < Kcp[j + 1]; ++q) kcol[q] = (int32_t)j;
+    }, 1024);
+    up(Krow_, Kri);
     up(Kcol_, kcol);
     up(K0_, Kv);
     zeros(sk_, n);

@@ -35,27 +35,10 @@ namespace {
 
 constexpr int NT_FOLD = SymbolicPlan::kFoldThreads;  // threads of k_fact_tree (product-list chunks)
 
-// allocator whose resize() leaves new elements uninitialised: the index arrays below are written in
-// full by the threads that fill them (first touch in parallel instead of a serial zero fill)
-template <class T>
-struct NoInit : std::allocator<T> {
-  template <class U>
-  struct rebind {
-    using other = NoInit<U>;
-  };
-  NoInit() = default;
-  template <class U>
-  NoInit(const NoInit<U>&) {}
-  template <class U>
-  void construct(U* p) { ::new ((void*)p) U; }
-  template <class U, class... A>
-  void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
-};
-
 struct Pattern {
   // strictly-lower pattern of P K P^T: column lists (rows > col) and row lists (cols < row)
   std::vector<int64_t> cp, rp;
-  std::vector<int32_t, NoInit<int32_t>> ci, ri;
+  hvec<int32_t> ci, ri;
 };
 
 // f(t, j0, j1) on T contiguous column ranges balanced by entries (colptr), one thread each
