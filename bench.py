@@ -171,9 +171,11 @@ def roofline(stats: list, dominant: str):
     else:
         ach, peak, unit = nbytes / avg_s / 1e9, PEAK_HBM_GBS, "GB/s"
     traffic, src, traffic_lo = None, None, None
-    def _rv(path):  # r<round>_v<n>: numeric order (r2_v10 after r2_v3)
-        m = re.search(r"r(\d+)_v(\d+)", os.path.basename(path))
-        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
+    def _rv(path):  # r<round>_v<n> (numeric: r2_v10 after r2_v3) or r<round>_<letters> (r4_i after r4_h)
+        m = re.search(r"r(\d+)_(?:v(\d+)|([a-z]+))_", os.path.basename(path))
+        if not m:
+            return (-1, -1)
+        return (int(m.group(1)), int(m.group(2)) if m.group(2) else sum(ord(ch) * 128 ** -k for k, ch in enumerate(m.group(3))))
 
     pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), key=_rv)
     if pmc:  # PMC counters can not be read inside the timed run: the latest committed pass of this workload
