@@ -4802,7 +4802,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         tree_flops_ += 2.0 * (r * w - w * (w + 1) / 2);
         tree_alg_ += solve_alg(s);
         chunk[s] = !big_root(s) && (S.nrows[s] > SMALL_SOLVE_MAX || 8 * tree_panel_doubles(s) + 8 * 1024 > TREE_SOLVE_LDS);
-        if (big_root(s)) root_lds_ = std::max<int>(root_lds_, 8 * tree_panel_doubles(s) + 8 * 1024);
+        if (big_root(s)) root_lds_ = TREE_ROOT_LDS;  // the rest beyond the panel stages its gather (all children)
       }
       tree_lds_ = TREE_SOLVE_LDS;  // the rest of the budget stages gather sources
       tchunk_.upload(chunk);
