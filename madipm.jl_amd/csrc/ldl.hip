@@ -2280,7 +2280,7 @@ __global__ __launch_bounds__(NT) void k_big_trsm(FrontTab T, const int32_t* __re
 // staged through LDS one after another; the next chunk's operands are loaded (from
 // clamped addresses) while the current chunk's MFMAs run.
 __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __restrict__ list, int step, int kpan,
-                                                   int left, double* __restrict__ arena, double* __restrict__ D,
+                                                   double* __restrict__ arena, double* __restrict__ D,
                                                    double* __restrict__ Mbuf, LDLStatus* st, double tol) {
   constexpr int LDT = 80;  // [k][row] layout: conflict-free ds_read_b64 for the 16x4 operand pattern
   __shared__ __attribute__((aligned(16))) double Wt[64 * LDT];
@@ -2293,13 +2293,10 @@ __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
   const int g0 = (step / kpan) * kpan;                         // first panel of the group
   const int gend = min(64 * (g0 + kpan), w);                   // first column after the group
-  // left (local mode): left-looking inside the group — the next panel's column block alone, updated
-  // once by all the group's panels so far (K = [64 g0, end of panel step)), instead of every later
-  // panel of the group by panel `step` alone
-  const int kb = (trailing || left) ? 64 * g0 : 64 * step;     // K range [kb, ke)
+  const int kb = trailing ? 64 * g0 : 64 * step;               // K range [kb, ke)
   const int ke = trailing ? gend : min(64 * step + 64, w);
   const int c0 = ke;                                           // tiles relative to the K range's end
-  const int jlim = trailing ? r : (left ? min(ke + 64, gend) : gend);
+  const int jlim = trailing ? r : gend;
   const int I0 = c0 + ti * 64, J0 = c0 + tj * 64;
   const int nch = (ke - kb + 63) >> 6;                         // K chunks of 64 (<= kpan)
   double* __restrict__ F = arena + T.l_off[s];
@@ -4131,8 +4128,6 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   {
     const char* ek = std::getenv("MADIPM_BIG_KPAN");  // panels per deferred big-front update group
     big_kpan_ = ek ? std::max(1, std::min(8, std::atoi(ek))) : 4;
-    const char* el = std::getenv("MADIPM_BIG_LEFT");  // left-looking update inside a panel group (A/B)
-    big_left_ = (el && el[0] == '0') ? 0 : 1;
     // pipelined in-LDS factorisation schedule (1, default); 0 = the barrier schedule, bitwise the same
     // factor (test_ldl_fact_pipe_bitwise)
     const char* ep = std::getenv("MADIPM_FACT_PIPE");
@@ -4580,12 +4575,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
           // panel updates the rest of the front with K = the whole group (trailing tiles)
           const int g0 = (p / big_kpan_) * big_kpan_, gl = std::min(g0 + big_kpan_, npan) - 1;
           const int gend = std::min(64 * (gl + 1), w);
-          if (p < gl && big_left_) {  // left-looking: the next panel's column block, K = the group so far
-            const double K = k0 + kw - 64 * g0, nc = std::min(64, gend - (k0 + kw));
-            for (int i = 0; i < nt; ++i) tu.insert(tu.end(), {s, i});
-            kb[2] += 8.0 * (2.0 * nb * nc + nb * K + nc * K);  // C in/out + the group's rows once
-            kf[2] += 2.0 * K * nc * (nb - 0.5 * nc);
-          } else if (p < gl) {
+          if (p < gl) {
             const double nc = gend - (k0 + kw);  // the group's later columns
             for (int j = 0; j < (int)cdiv((int)nc, 64); ++j)
               for (int i = j; i < nt; ++i) tu.insert(tu.end(), {s, i | (j << 16)});
@@ -5109,8 +5099,8 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
         break;
       case BIG_UPDATE:
         TIMED(KK_UPDATE, L.bytes, L.alg, L.flops,
-              (k_big_update<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, big_kpan_, big_left_, arena_, D_, minv_,
-                                                              st_, pivot_tol)));
+              (k_big_update<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, big_kpan_, arena_, D_, minv_, st_,
+                                                              pivot_tol)));
         break;
       case ASM_UPDATE:  // nf = the launch's K rows (the widest panel, rounded up to 4)
         TIMED(KK_ASM_UPDATE, L.bytes, 0.0, L.flops,

@@ -313,7 +313,6 @@ class LDLSolver : public LinSolver {
   double lb_alg(size_t g) const;
   DBuf<int32_t> tc_ptr_, tc_list_, tdep_ptr_, tdep_, tpar_, tflags_;
   DBuf<uint8_t> trootbwd_;  // per forward task: an elimination-tree root solved backward by k_fwd_tree
-  int big_left_ = 1;  // left-looking big-front update inside a panel group (MADIPM_BIG_LEFT)
   int nroot_task_ = 0, root_lds_ = 0;  // tree-solve tasks of big etree roots (last, own forward launch)
   DBuf<uint8_t> tchunk_;    // per front: tree solves stream its panel in chunks (fwd_med_front / bwd_med_front)
   int ntask_ = 0;         // tree-solve tasks (one per tree front)
