@@ -3359,16 +3359,17 @@ __device__ __forceinline__ int tree_ldt(int w) { return ((w + 15) & ~15) + 2; } 
 __device__ __forceinline__ int tree_ldc(int r) { return ((r + 31) & ~31) + 2; }  // backward: col-major ld
 
 // forward staging: LT[i * ldt + t] = L(i, t) for t < min(i, w), else 0 (t < w16)
+template <int NTH = NT>
 __device__ __forceinline__ void stage_rowmajor(const double* __restrict__ L, double* LT, int r, int w, int ldt) {
   const int w16 = (w + 15) & ~15;
   const int nel = r * w16;
-  ColWalk wk(threadIdx.x, r);
-  for (int base = 0; base < nel; base += NT * 16) {
+  ColWalk wk(threadIdx.x, r, NTH);
+  for (int base = 0; base < nel; base += NTH * 16) {
     double v[16];
     int dst[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-      const int q = base + k * NT + threadIdx.x;
+      const int q = base + k * NTH + threadIdx.x;
       v[k] = (q < nel && wk.j < w && wk.i > wk.j) ? L[q] : 0.0;
       dst[k] = (q < nel) ? wk.i * ldt + wk.j : -1;
       wk.next();
@@ -3923,6 +3924,78 @@ __global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __re
     dg[5] = wall_clock64();
     dg[6] = clist[q1 - 1];
     dg[7] = T.nrows[clist[q1 - 1]];
+  }
+}
+
+// The big elimination-tree roots of the tree solves (LDLSolver::nroot_task_: r == w, panel beyond the
+// tree launches' 76 KB; ex10's 120-column coupling root), one 1024-thread workgroup each, after the
+// forward tree launch (every child has scattered its update entries): the panel staged row-major in
+// one round of loads, each row's gather segment summed by four threads (strided, all loads in
+// flight), then the forward and backward substitutions on the staged panel (k_fwd_tree's root-backward
+// path: the same fma sequences).  In k_fwd_tree the root's single 256-thread workgroup staged 125 KB
+// of panel and its ~20k gather entries through the LDS left beside the panel: 26-34 us per solve.
+constexpr int RSN = 1024;
+__global__ __launch_bounds__(RSN) void k_root_solve(FrontTab T, const int32_t* __restrict__ fronts,
+                                                    const double* __restrict__ arena, double* b, double* xi,
+                                                    const double* __restrict__ Dg, int32_t* tflags, int epoch) {
+  extern __shared__ __attribute__((aligned(16))) double Ls[];
+  __shared__ double part[4 * SMALL_SOLVE_MAX], inits[SMALL_SOLVE_MAX];
+  const int s = fronts[blockIdx.x];
+  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int ldt = tree_ldt(w);
+  // gather: row i = tid >> 2 summed by threads k = tid & 3 over the entries lo + 4 m + k of its segment
+  // (the tail past the last full group of 4 by k = 0, in order: k_fwd_tree's summation)
+  const int i = tid >> 2, k = tid & 3;
+  const int64_t e0 = T.row_ptr[s];
+  int64_t lo = 0, len = 0;
+  if (i < r) {
+    lo = T.sv_ptr[e0 + i];
+    len = T.sv_ptr[e0 + i + 1] - lo;
+  }
+  const double init = (i < r && k == 0) ? fwd_init(T, s, i, w, f0, b) : 0.0;
+  stage_rowmajor<RSN>(arena + T.l_off[s], Ls, r, w, ldt);
+  double c = 0.0;
+  const int64_t q4 = len >> 2;
+  for (int64_t m0 = 0; m0 < q4; m0 += 8) {
+    double x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = T.gbuf[lo + 4 * min(m0 + u, max(q4 - 1, (int64_t)0)) + k];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (m0 + u < q4) c += x[u];
+  }
+  if (k == 0)
+    for (int64_t p = 4 * q4; p < len; ++p) c += T.gbuf[lo + p];
+  if (i < r) {
+    part[4 * i + k] = c;
+    if (k == 0) inits[i] = init;
+  }
+  __syncthreads();  // the panel and the partial sums
+  if (tid < 64) {
+    double v[3], dpiv[3];
+    int pj[3];
+#pragma unroll
+    for (int h = 0; h < 3; ++h) {
+      const int ii = lane + 64 * h;
+      v[h] = (ii < r) ? ((part[4 * ii] + part[4 * ii + 1]) + (part[4 * ii + 2] + part[4 * ii + 3])) + inits[ii] : 0.0;
+      const int j = min(ii, max(w - 1, 0));
+      dpiv[h] = Dg[f0 + j];
+      pj[h] = T.perm[f0 + j];
+    }
+    fwd_subst_t(v, Ls, ldt, r, w, lane);
+#pragma unroll
+    for (int h = 0; h < 3; ++h) v[h] = (lane + 64 * h < w) ? v[h] / dpiv[h] : 0.0;
+    bwd_subst_t(v, Ls, ldt, w, lane);
+#pragma unroll
+    for (int h = 0; h < 3; ++h) {
+      const int j = lane + 64 * h;
+      if (j < w) {
+        st_sc1(xi + f0 + j, v[h]);
+        if (T.wout[s]) b[pj[h]] = v[h];
+      }
+    }
+    publish_sc1(&tflags[s], epoch + 1);  // the backward epoch: k_bwd_tree's children of the root wait on it
   }
 }
 
@@ -4792,7 +4865,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         tree_flops_ += 2.0 * (r * w - w * (w + 1) / 2);
         tree_alg_ += solve_alg(s);
         chunk[s] = !big_root(s) && (S.nrows[s] > SMALL_SOLVE_MAX || 8 * tree_panel_doubles(s) + 8 * 1024 > TREE_SOLVE_LDS);
-        if (big_root(s)) root_lds_ = TREE_ROOT_LDS;  // the rest beyond the panel stages its gather (all children)
+        if (big_root(s)) root_lds_ = std::max<int>(root_lds_, 8 * tree_panel_doubles(s));  // k_root_solve: the panel
       }
       tree_lds_ = TREE_SOLVE_LDS;  // the rest of the budget stages gather sources
       tchunk_.upload(chunk);
@@ -4922,7 +4995,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_small_blocked<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    192 * 193 / 2 * 8));
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_bwd_small, hipFuncAttributeMaxDynamicSharedMemorySize, 129 * 128 * 8));
-    MADIPM_HIP(hipFuncSetAttribute((const void*)k_fwd_tree, hipFuncAttributeMaxDynamicSharedMemorySize, TREE_ROOT_LDS));
+    MADIPM_HIP(hipFuncSetAttribute((const void*)k_fwd_tree, hipFuncAttributeMaxDynamicSharedMemorySize, TREE_SOLVE_LDS));
+    MADIPM_HIP(hipFuncSetAttribute((const void*)k_root_solve, hipFuncAttributeMaxDynamicSharedMemorySize, TREE_ROOT_LDS));
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_fact_tree, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)SymbolicPlan::kFactTreeLdsMax));
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_bwd_tree, hipFuncAttributeMaxDynamicSharedMemorySize, TREE_SOLVE_LDS));
@@ -5374,10 +5448,8 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
                                                               tchunk_)));
       if (nroot_task_)
         TIMED(KK_FWD_TREE, nlo > 0 ? 0.0 : tree_bytes_, nlo > 0 ? 0.0 : tree_alg_, nlo > 0 ? 0.0 : tree_flops_,
-              (k_fwd_tree<<<(unsigned)nroot_task_, NT, root_lds_, s>>>(
-                  T_, tc_ptr_.p + nlo, tc_list_, nroot_task_, tdep_ptr_.p + nlo, tdep_, counters_.p + 4 * S_.nlevels + 2,
-                  tflags_, efwd, root_lds_ / 8, arena_, b, xi_, uvec_, &st_->err, tdbg_.p ? tdbg_.p + 8 * nlo : nullptr,
-                  trootbwd_.p + nlo, D_, tchunk_)));
+              (k_root_solve<<<(unsigned)nroot_task_, RSN, root_lds_, s>>>(T_, tc_list_.p + nlo, arena_, b, xi_, D_, tflags_,
+                                                                         efwd)));
     }
     if (lev == 0 && phase == 0 && ntree_ && tdbg_.p)
       tree_debug_dump(s, "fwd", tdbg_.p, ntask_, "leaves", "wait", "gather", "subst", "store", 8);
