@@ -3510,6 +3510,8 @@ constexpr int MFBUF = MED_SOLVE_MAX * MLDT;       // doubles per forward chunk b
 constexpr int MLDC = MED_SOLVE_MAX + 2;           // backward chunk: col-major ld
 constexpr int MBBUF = MCW * MLDC;                 // doubles per backward chunk buffer
 constexpr int MED_FWD_LDS = 2 * MFBUF, MED_BWD_LDS = 2 * MBBUF + 2 * MED_SOLVE_MAX;  // doubles
+static_assert(8 * MED_FWD_LDS <= TREE_SOLVE_LDS && 8 * MED_BWD_LDS <= TREE_SOLVE_LDS,
+              "chunked tree-solve buffers fit the tree launches' LDS");
 
 // rows [ra, r) x columns [c0, c0 + MCW) of L (ld r) -> LT[(i - ra) MLDT + (t - c0)] = L(i, t) for
 // t < w and i > t, else 0; threads lt = 0 .. nthr - 1 of the caller's group
