@@ -1972,21 +1972,33 @@ __device__ __forceinline__ void med_trailing(double* __restrict__ F, int r, int 
   const int ntile = nb * (nb + 1) / 2;
   const int nks = (pw + 3) >> 2;
   const int kl = lane >> 4, il = lane & 15;
-  for (int t = wv; t < ntile; t += nw) {
-    // tile t -> (I, J), J <= I, row-major over the lower triangle
+  // tile t -> (I, J), J <= I, row-major over the lower triangle; its C entries (lane: row i0 + il,
+  // columns j0 + kl + 4 g), clamped in range — the next tile's C is loaded before this tile's MFMAs
+  auto coords = [&](int t, int& i0, int& j0) {
     int I = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
     while ((I + 1) * (I + 2) / 2 <= t) ++I;
     while (I * (I + 1) / 2 > t) --I;
     const int J = t - I * (I + 1) / 2;
-    const int i0 = pw + 16 * I, j0 = pw + 16 * J;  // LDS rows of the tile's rows (i) and columns (j)
-    // C prefetch: lane (n = il -> row i0 + il, m = kl + 4 g -> column j0 + kl + 4 g), clamped in range
+    i0 = pw + 16 * I;  // LDS rows of the tile's rows (i) and columns (j)
+    j0 = pw + 16 * J;
+  };
+  auto load_c = [&](int t, double (&c)[4]) {
+    int i0, j0;
+    coords(min(t, ntile - 1), i0, j0);
     const int ic = min(i0 + il, rp - 1);
-    double c[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int jc = min(j0 + kl + 4 * g, rp - 1);
       c[g] = F[(int64_t)(c0 + ic) + (int64_t)(c0 + jc) * r];
     }
+  };
+  double c[4];
+  if (wv < ntile) load_c(wv, c);
+  for (int t = wv; t < ntile; t += nw) {
+    int i0, j0;
+    coords(t, i0, j0);
+    double cn[4];
+    load_c(t + nw, cn);  // (clamped: the last tile's again when there is no next)
     dbl4 acc = {0.0, 0.0, 0.0, 0.0};
     const int ja = min(j0 + il, rp - 1), ib = min(i0 + il, rp - 1);
     for (int ks = 0; ks < nks; ++ks) {
@@ -2011,6 +2023,8 @@ __device__ __forceinline__ void med_trailing(double* __restrict__ F, int r, int 
           *q = v;
       }
     }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) c[g] = cn[g];
   }
 }
 
