@@ -126,6 +126,8 @@ __device__ __forceinline__ void stage_panel(const double* __restrict__ L, double
   }
 }
 
+__global__ void k_status_end(LDLStatus* st) { ldl_status_end(st); }
+
 __global__ void k_status_init(LDLStatus* st, int all = 0) {
   const uint64_t now = wall_clock64();
   if (all) {
@@ -4726,6 +4728,20 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     if (phase == 1 && NL == 1 && nftree_) ftree_launch();
   };
   build_fact(1, fact1_);
+  {  // tail overlap (MADIPM_TAIL_OVERLAP=0 disables): the launches after the tree kernel
+    const char* et = std::getenv("MADIPM_TAIL_OVERLAP");
+    size_t cut = fact1_.size();
+    for (size_t k = 0; k < fact1_.size(); ++k)
+      if (fact1_[k].kind == FTREE) cut = k + 1;
+    tail_ok_ = !(et && et[0] == '0') && S.nshards == 1 && nftree_ > 0 && cut < fact1_.size();
+    if (tail_ok_) {
+      fact1_head_.assign(fact1_.begin(), fact1_.begin() + cut);
+      fact1_tail_.assign(fact1_.begin() + cut, fact1_.end());
+      MADIPM_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+      MADIPM_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
+      MADIPM_HIP(hipEventCreateWithFlags(&ev_tail_, hipEventDisableTiming));
+    }
+  }
   if (S.nshards > 1) {
     asm_launch(NL, fact1_);  // top fronts, external part (all-reduced next)
     for (size_t g = 0; g < S.lb.size(); ++g)  // this shard's batched leaves under top fronts: into it
@@ -4859,6 +4875,19 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q)
           if (in_tree[S.level_list[q]]) (big_root(S.level_list[q]) ? roots : ord).push_back(S.level_list[q]);
       nroot_task_ = (int)roots.size();
+      if (tail_ok_) {  // tail overlap: fronts factorised after the tree kernel (above level 0, outside
+                       // k_fact_tree, or absorbed by such a front) must not be solved by k_fwd_tree before the join
+        std::vector<int> lvl(std::max(ns, 1), 0);
+        for (int lev = 0; lev < NL; ++lev)
+          for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) lvl[S.level_list[q]] = lev;
+        auto head = [&](int f) {
+          const int p = S.parent[f];
+          const bool absorbed = p >= 0 && S.absorb[p];
+          if (S.ftree[f]) return !(absorbed && !S.ftree[p]);
+          return lvl[f] == 0 && !absorbed;
+        };
+        for (int f : ord) tree_join_early_ = tree_join_early_ || !head(f);
+      }
       ord.insert(ord.end(), roots.begin(), roots.end());
       ntree_ = (int)ord.size();
       // children of tree fronts scatter their forward update entries straight into the parent's
@@ -5026,6 +5055,9 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
 
 LDLSolver::~LDLSolver() {
   if (h_status_) (void)hipHostFree(h_status_);
+  if (ev_fork_) (void)hipEventDestroy(ev_fork_);
+  if (ev_tail_) (void)hipEventDestroy(ev_tail_);
+  if (side_) (void)hipStreamDestroy(side_);
   for (hipEvent_t e : evs_) (void)hipEventDestroy(e);
 }
 
@@ -5234,7 +5266,24 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
 // assembly and the shard's status slot.
 void LDLSolver::fact_phase1(const double* Kx, hipStream_t s) {
   if (S_.N == 0) return;
+  join(s);  // the previous factorisation's tail (normally joined by its solve already)
   if (!(ext_reset && ext_status_ && !sharded())) k_status_init<<<1, 1, 0, s>>>(st_);
+  if (tail_active()) {
+    // the launches after the tree kernel (the fronts above the tree: ex10's root assembly and root
+    // factor) on the side stream, beside the driver's next kernels and the next solve's leaves and
+    // forward tree, which need only the tree's factor; the solve joins before k_root_solve / the
+    // level solves above the tree, status() and the next factorisation join too
+    run_fact(fact1_head_, Kx, s);
+    MADIPM_HIP(hipEventRecord(ev_fork_, s));
+    MADIPM_HIP(hipStreamWaitEvent(side_, ev_fork_, 0));
+    run_fact(fact1_tail_, Kx, side_);
+    k_status_end<<<1, 1, 0, side_>>>(st_);
+    MADIPM_HIP(hipEventRecord(ev_tail_, side_));
+    MADIPM_HIP(hipGetLastError());
+    tail_pending_ = true;
+    inertia_stale_ = true;
+    return;
+  }
   run_fact(fact1_, Kx, s);
   const int nb = (int)std::min<int64_t>(64, cdiv(S_.N, NT));
   const int spdf = spd ? 1 : 0;
@@ -5291,6 +5340,7 @@ bool LDLSolver::external_status(LDLStatus* dev, LDLStatus* host) {
 
 double LDLSolver::fact_seconds(hipStream_t s) {
   if (S_.N == 0) return 0.0;
+  join(s);
   LDLStatus h;
   MADIPM_HIP(hipMemcpyAsync(&h, st_, sizeof(LDLStatus), hipMemcpyDeviceToHost, s));
   MADIPM_HIP(hipStreamSynchronize(s));
@@ -5305,6 +5355,7 @@ double LDLSolver::fact_seconds(hipStream_t s) {
 void LDLSolver::count_inertia(hipStream_t s) {
   if (!inertia_stale_ || S_.N == 0) return;
   inertia_stale_ = false;
+  join(s);
   const int nb = (int)std::min<int64_t>(64, cdiv(S_.N, NT));
   k_zero_counts<<<1, 1, 0, s>>>(st_);
   k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, st_, 0, nullptr, 1);
@@ -5312,11 +5363,18 @@ void LDLSolver::count_inertia(hipStream_t s) {
   status(s, true);
 }
 
+void LDLSolver::join(hipStream_t s) {
+  if (!tail_pending_) return;
+  MADIPM_HIP(hipStreamWaitEvent(s, ev_tail_, 0));
+  tail_pending_ = false;
+}
+
 int LDLSolver::status(hipStream_t s, bool sync) {
   if (S_.N == 0) {
     factorized = true;
     return 0;
   }
+  if (sync) join(s);
   if (sync && ext_status_) MADIPM_HIP(hipMemcpyAsync(h_st_, st_, sizeof(LDLStatus), hipMemcpyDeviceToHost, s));
   if (sync) MADIPM_HIP(hipStreamSynchronize(s));
   if (h_st_->err) {  // a lost hand-off gives a wrong factor or solve: never report it as success
@@ -5430,6 +5488,7 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
   if (phase == 0 && !S_.lb.empty()) lb_fwd(b, s);
   for (int lev = 0; lev < (int)V.size(); ++lev) {
     const SolveLevel& L = V[lev];
+    if (lev > 0) join(s);  // no-op after the tree's join
     if (L.nmicro)
       TIMED(KK_FWD_TINY, L.micro_bytes, L.micro_alg, L.micro_flops,
             (k_fwd_micro<<<(unsigned)cdiv(L.nmicro, NT / MG), NT, 0, s>>>(T_, sched_.p + L.micro_off, L.nmicro, arena_, b,
@@ -5456,12 +5515,14 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
     if (lev == 0 && phase == 0 && ntree_)
     {
       const int nlo = ntask_ - nroot_task_;  // the big roots last, in their own launch (more LDS)
+      if (tree_join_early_) join(s);
       if (nlo > 0)
         TIMED(KK_FWD_TREE, tree_bytes_, tree_alg_, tree_flops_,
               (k_fwd_tree<<<(unsigned)nlo, NT, tree_lds_, s>>>(T_, tc_ptr_, tc_list_, nlo, tdep_ptr_, tdep_,
                                                               counters_.p + 4 * S_.nlevels, tflags_, efwd, tree_lds_ / 8,
                                                               arena_, b, xi_, uvec_, &st_->err, tdbg_.p, trootbwd_, D_,
                                                               tchunk_)));
+      join(s);  // the factorisation's tail (the fronts above the tree) ran beside the launches above
       if (nroot_task_)
         TIMED(KK_FWD_TREE, nlo > 0 ? 0.0 : tree_bytes_, nlo > 0 ? 0.0 : tree_alg_, nlo > 0 ? 0.0 : tree_flops_,
               (k_root_solve<<<(unsigned)nroot_task_, RSN, root_lds_, s>>>(T_, tc_list_.p + nlo, arena_, b, xi_, D_, tflags_,

@@ -541,6 +541,194 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     analyse_order(N, colptr, rowval, std::move(id), OA);
   }
   stamp("2: etree, counts");
+  const bool use_lb = opt.leaf_batch && !has_upper;
+  struct SN {
+    int first, w;
+    int64_t r, zeros;
+  };
+  double bigm = opt.big_merge;
+  if (const char* e = std::getenv("MADIPM_BIG_MERGE")) bigm = std::atof(e);
+  // the trailing update's flops (2 w per entry of the (r - w) x (r - w) lower triangle)
+  auto upd_flops = [](int64_t w, int64_t r) { return 2.0 * (double)w * (double)(r - w) * (double)(r - w + 1) / 2.0; };
+  std::vector<int32_t> nchild;
+  std::vector<uint8_t> lbcand;
+  std::vector<SN> sn;
+  // steps 3 - 4 (fundamental supernodes, batched-leaf candidates, relaxed amalgamation) of an order
+  auto amalgamate = [&](const OrderAnalysis& A) {
+    const std::vector<int32_t>& parent = A.parent;
+    const std::vector<int64_t>& cnt = A.cnt;
+    stamp("before 3");
+    // ---------------- 3. fundamental supernodes
+    nchild.assign(N, 0);
+    for (int j = 0; j < N; ++j)
+      if (parent[j] != -1) nchild[parent[j]]++;
+    std::vector<SN> fund;
+    fund.push_back({0, 1, cnt[0], 0});
+    for (int j = 1; j < N; ++j) {
+      if (parent[j - 1] == j && cnt[j - 1] == cnt[j] + 1 && nchild[j] == 1) {
+        fund.back().w++;
+      } else {
+        fund.push_back({j, 1, cnt[j], 0});
+      }
+    }
+
+    stamp("before 3b");
+    // ---------------- 3b. batched-leaf candidates: single-column etree leaves with a large update,
+    // many under the same parent column (a QP with a diagonal Hessian and dense A: every x_j).  They
+    // are kept out of relaxed amalgamation; step 6b decides the groups.
+    lbcand.assign(N, 0);
+    // batched leaves read their K column as one contiguous CSC run (diagonal + rows below): lower only
+    if (use_lb) {
+      std::vector<int32_t> npar(N, 0);
+      for (const SN& f : fund)
+        if (f.w == 1 && nchild[f.first] == 0 && f.r - 1 >= opt.lb_min_rows && parent[f.first] != -1)
+          npar[parent[f.first]]++;
+      for (const SN& f : fund)
+        if (f.w == 1 && nchild[f.first] == 0 && f.r - 1 >= opt.lb_min_rows && parent[f.first] != -1 &&
+            npar[parent[f.first]] >= opt.lb_min_count)
+          lbcand[f.first] = 1;
+    }
+
+    stamp("before 4");
+    // ---------------- 4. relaxed amalgamation (merge a front with its column-adjacent child)
+    sn.clear();
+    sn.reserve(fund.size());
+    for (const SN& f : fund) {
+      SN p = f;
+      while ((opt.relax || bigm > 0.0) && !sn.empty()) {
+        const SN& c = sn.back();
+        int clast = c.first + c.w - 1;
+        if (clast + 1 != p.first) break;
+        if (lbcand[c.first] || lbcand[p.first]) break;  // batched-leaf candidates stay single columns
+        int par = parent[clast];
+        if (par < p.first || par >= p.first + p.w) break;
+        int64_t ncols = c.w + p.w;
+        int64_t rnew = c.w + p.r;
+        int64_t Enew = trap(ncols, rnew);
+        int64_t zeros = Enew - (trap(c.w, c.r) - c.zeros) - (trap(p.w, p.r) - p.zeros);
+        double frac = (double)zeros / (double)Enew;
+        bool merge = opt.relax && (ncols <= opt.nrelax[0] || (ncols <= opt.nrelax[1] && frac < opt.zrelax[0]) ||
+                                   (ncols <= opt.nrelax[2] && frac < opt.zrelax[1]) || frac < opt.zrelax[2]);
+        if (!merge && bigm > 0.0 && c.r > opt.big_merge_rows) {
+          // the child's update block: written once, read once by the parent's assembly; the zeros: written
+          // by the factorisation, read by the two sweeps of each of ~2 solves
+          const double u = (double)(c.r - c.w), saved = 16.0 * u * (u + 1) / 2.0, zbytes = 5.0 * 8.0 * (double)zeros;
+          const double xfl = upd_flops(ncols, rnew) - upd_flops(c.w, c.r) - upd_flops(p.w, p.r);
+          merge = saved - zbytes > xfl / bigm;
+        }
+        if (!merge) break;
+        p.first = c.first;
+        p.w = (int)ncols;
+        p.r = rnew;
+        p.zeros = zeros;
+        sn.pop_back();
+      }
+      sn.push_back(p);
+    }
+  };
+  amalgamate(OA);
+  if (bigm > 0.0) {
+    // 2b. sibling merges: relaxed amalgamation merges a front with its column-ADJACENT child only (the
+    // last one in postorder), so of a parent's children with HBM-sized update blocks (more than
+    // big_merge_rows rows) all but one would write their block for the parent to read back.  Reorder:
+    // every such child's own columns (with those of its merged descendants) are moved to right before
+    // its parent's, the largest last; the rest of its subtree stays where it was.  The order stays an
+    // elimination order of the same etree (every column still follows its descendants: same fill,
+    // counts and tree), and step 4's cost rule then merges the moved children one after the other.
+    // A moved child that the rule does not merge would split its subtree's label range: those are
+    // kept in place and the order is rebuilt (a few rounds), else the reorder is dropped.
+    const std::vector<int32_t>& par0 = OA.parent;
+    const std::vector<int64_t>& cnt0 = OA.cnt;
+    std::vector<uint8_t> delay(N, 0);
+    bool any = false;
+    for (int j = 0; j < N; ++j)
+      if (par0[j] != -1 && cnt0[j] > opt.big_merge_rows && !lbcand[j]) any = delay[j] = 1;
+    std::vector<int32_t> chead(N, -1), cnext(N, -1), dhead(N, -1), dnext(N, -1), dl, order, newpos(N), stk;
+    for (int attempt = 0; any && attempt < 4; ++attempt) {
+      // children lists in label order; delayed children (also) in (count, label) order
+      std::fill(chead.begin(), chead.end(), -1);
+      std::fill(dhead.begin(), dhead.end(), -1);
+      for (int c = N - 1; c >= 0; --c)
+        if (par0[c] != -1) {
+          cnext[c] = chead[par0[c]];
+          chead[par0[c]] = c;
+        }
+      dl.clear();
+      for (int c = 0; c < N; ++c)
+        if (delay[c]) dl.push_back(c);
+      std::stable_sort(dl.begin(), dl.end(), [&](int a, int b) { return cnt0[a] < cnt0[b]; });
+      for (int q = (int)dl.size() - 1; q >= 0; --q) {
+        const int c = dl[q];
+        dnext[c] = dhead[par0[c]];
+        dhead[par0[c]] = c;
+      }
+      // emission: full(v) = early(v) + late(v); early(v) = per child c: c delayed ? early(c) : full(c);
+      // late(v) = late(d) per delayed child d (sorted), then v.  Explicit stack of (node, kind) tasks.
+      enum { FULL = 0, EARLY = 1, LATE = 2, OUT = 3 };
+      order.clear();
+      order.reserve(N);
+      for (int root = 0; root < N; ++root) {
+        if (par0[root] != -1) continue;
+        stk.push_back(root * 4 + FULL);
+        while (!stk.empty()) {
+          const int t = stk.back(), v = t >> 2, kind = t & 3;
+          stk.pop_back();
+          if (kind == OUT) {
+            order.push_back(v);
+          } else if (kind == FULL) {
+            stk.push_back(v * 4 + LATE);
+            stk.push_back(v * 4 + EARLY);
+          } else if (kind == EARLY) {  // children pushed last-first: popped in label order
+            size_t m = stk.size();
+            for (int c = chead[v]; c != -1; c = cnext[c]) stk.push_back(c * 4 + (delay[c] ? EARLY : FULL));
+            std::reverse(stk.begin() + m, stk.end());
+          } else {
+            stk.push_back(v * 4 + OUT);
+            size_t m = stk.size();
+            for (int d = dhead[v]; d != -1; d = dnext[d]) stk.push_back(d * 4 + LATE);
+            std::reverse(stk.begin() + m, stk.end());
+          }
+        }
+      }
+      MADIPM_REQUIRE((int)order.size() == N && N < (1 << 29), "merge reorder");
+      OrderAnalysis B;
+      B.perm.resize(N);
+      B.pinv.resize(N);
+      for (int k = 0; k < N; ++k) {
+        newpos[order[k]] = k;
+        B.perm[k] = OA.perm[order[k]];
+        B.pinv[B.perm[k]] = k;
+      }
+      B.parent.resize(N);
+      B.cnt.resize(N);
+      for (int k = 0; k < N; ++k) {
+        const int p = par0[order[k]];
+        B.parent[k] = p == -1 ? -1 : newpos[p];
+        B.cnt[k] = cnt0[order[k]];
+      }
+      B.flops = OA.flops;
+      build_pattern(N, colptr, rowval, B.pinv, B.P, B.twin);
+      amalgamate(B);
+      // every moved child merged into its parent's front?
+      std::vector<int32_t> sof(N);
+      for (int q = 0; q < (int)sn.size(); ++q)
+        for (int j = sn[q].first; j < sn[q].first + sn[q].w; ++j) sof[j] = q;
+      bool ok = true;
+      for (int c = 0; c < N; ++c)
+        if (delay[c] && sof[newpos[c]] != sof[newpos[par0[c]]]) {
+          delay[c] = 0;
+          ok = false;
+        }
+      if (ok) {
+        std::swap(OA, B);
+        break;
+      }
+      any = false;
+      for (int c = 0; c < N && !any; ++c) any = delay[c];
+      if (!any || attempt == 3) amalgamate(OA);  // back to the unmoved order
+    }
+    stamp("2b: sibling-merge order");
+  }
   std::vector<int32_t>& perm = OA.perm;
   std::vector<int32_t>& pinv = OA.pinv;
   std::vector<int32_t>& parent = OA.parent;
@@ -556,72 +744,6 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     S.kcol[j] = (int32_t)(P.cp[j + 1] - P.cp[j] + (diagcount[perm[j]] ? 1 : 0));
   }
 
-  stamp("before 3");
-  // ---------------- 3. fundamental supernodes
-  std::vector<int32_t> nchild(N, 0);
-  for (int j = 0; j < N; ++j)
-    if (parent[j] != -1) nchild[parent[j]]++;
-  struct SN {
-    int first, w;
-    int64_t r, zeros;
-  };
-  std::vector<SN> fund;
-  fund.push_back({0, 1, cnt[0], 0});
-  for (int j = 1; j < N; ++j) {
-    if (parent[j - 1] == j && cnt[j - 1] == cnt[j] + 1 && nchild[j] == 1) {
-      fund.back().w++;
-    } else {
-      fund.push_back({j, 1, cnt[j], 0});
-    }
-  }
-
-  stamp("before 3b");
-  // ---------------- 3b. batched-leaf candidates: single-column etree leaves with a large update,
-  // many under the same parent column (a QP with a diagonal Hessian and dense A: every x_j).  They
-  // are kept out of relaxed amalgamation; step 6b decides the groups.
-  std::vector<uint8_t> lbcand(N, 0);
-  // batched leaves read their K column as one contiguous CSC run (diagonal + rows below): lower only
-  const bool use_lb = opt.leaf_batch && !has_upper;
-  if (use_lb) {
-    std::vector<int32_t> npar(N, 0);
-    for (const SN& f : fund)
-      if (f.w == 1 && nchild[f.first] == 0 && f.r - 1 >= opt.lb_min_rows && parent[f.first] != -1)
-        npar[parent[f.first]]++;
-    for (const SN& f : fund)
-      if (f.w == 1 && nchild[f.first] == 0 && f.r - 1 >= opt.lb_min_rows && parent[f.first] != -1 &&
-          npar[parent[f.first]] >= opt.lb_min_count)
-        lbcand[f.first] = 1;
-  }
-
-  stamp("before 4");
-  // ---------------- 4. relaxed amalgamation (merge a front with its column-adjacent child)
-  std::vector<SN> sn;
-  sn.reserve(fund.size());
-  for (const SN& f : fund) {
-    SN p = f;
-    while (opt.relax && !sn.empty()) {
-      const SN& c = sn.back();
-      int clast = c.first + c.w - 1;
-      if (clast + 1 != p.first) break;
-      if (lbcand[c.first] || lbcand[p.first]) break;  // batched-leaf candidates stay single columns
-      int par = parent[clast];
-      if (par < p.first || par >= p.first + p.w) break;
-      int64_t ncols = c.w + p.w;
-      int64_t rnew = c.w + p.r;
-      int64_t Enew = trap(ncols, rnew);
-      int64_t zeros = Enew - (trap(c.w, c.r) - c.zeros) - (trap(p.w, p.r) - p.zeros);
-      double frac = (double)zeros / (double)Enew;
-      bool merge = ncols <= opt.nrelax[0] || (ncols <= opt.nrelax[1] && frac < opt.zrelax[0]) ||
-                   (ncols <= opt.nrelax[2] && frac < opt.zrelax[1]) || frac < opt.zrelax[2];
-      if (!merge) break;
-      p.first = c.first;
-      p.w = (int)ncols;
-      p.r = rnew;
-      p.zeros = zeros;
-      sn.pop_back();
-    }
-    sn.push_back(p);
-  }
   const int ns = (int)sn.size();
   S.nsuper = ns;
   S.first.resize(ns + 1);

@@ -30,9 +30,15 @@ struct SymbolicOptions {
   int ordering = 1;          // 0: natural, 1: AMD, 2: user permutation, 3: nested dissection,
                              // 4: auto (AMD and ND, the one with fewer factorisation flops)
   double dense_alpha = 10.0; // AMD dense threshold = max(16, alpha*sqrt(n))
-  int relax = 1;             // relaxed supernode amalgamation on/off
+  int relax = 1;             // relaxed supernode amalgamation (zero-fraction rule) on/off
   int nrelax[3] = {4, 16, 48};
   double zrelax[3] = {0.8, 0.1, 0.05};
+  // cost-based amalgamation of HBM-sized fronts (child rows > big_merge_rows): a child merges into
+  // its parent when the update block it would write and its parent read back (16 B per entry) costs
+  // more than the merge's extra trailing-update flops / big_merge (flops per byte, the f64 MFMA / HBM
+  // ratio) plus the explicit zeros' traffic.  0 disables (env MADIPM_BIG_MERGE overrides).
+  double big_merge = 6.0;
+  int big_merge_rows = 256;
   int small_front_max = 128; // fronts with r <= this are factorised in LDS by one workgroup (max 192)
   int gather_max = 128;      // children with update blocks of more rows are added block-wise (bt), not gathered
   int fact_tree = 1;         // dependency-driven factorisation of the LDS-sized subtrees (k_fact_tree)

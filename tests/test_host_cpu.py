@@ -386,3 +386,54 @@ def test_symbolic_twin_leaves(seed, ordering):
     F = OracleLDL(K, perm)
     assert F.factorize() == K.shape[0]
     assert F.nnzL() == S.info()["nnzL"]
+
+
+def _sibling_k2(seed, nblk=4, bw=20, border=300):
+    """K of `nblk` diagonal blocks (bw columns each, sparse inside) all coupled to a border of `border`
+    variables (dense clique): the blocks are etree siblings under the border, each with an update block
+    of ~border rows (HBM-sized: > big_merge_rows)."""
+    rng = np.random.default_rng(seed)
+    N = nblk * bw + border
+    K = np.zeros((N, N))
+    for b in range(nblk):
+        s = slice(b * bw, (b + 1) * bw)
+        K[s, s] = (rng.random((bw, bw)) < 0.3) * rng.standard_normal((bw, bw))
+        K[s, nblk * bw:] = (rng.random((bw, border)) < 0.9) * rng.standard_normal((bw, border))
+    K[nblk * bw:, nblk * bw:] = rng.standard_normal((border, border))
+    K = K + K.T + 4 * N * np.eye(N)
+    K = sp.csc_matrix(K)
+    Lw = sp.tril(K).tocsc()
+    Lw.sort_indices()
+    return K, Lw
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_symbolic_sibling_merge(seed, monkeypatch):
+    """Cost-based amalgamation of HBM-sized fronts (symbolic.cpp step 2b + step 4's big_merge rule):
+    sibling children with large update blocks are moved next to their parent and merged into it.  The
+    moved order is an elimination order of the same etree: the same nnz(L) (brute force and the oracle
+    LDL^T on it), a postordered front tree, and fewer fronts than without the rule.  relax=0: the
+    zero-fraction amalgamation off, the cost rule alone."""
+    from madipm_amd._lib import Symbolic, default_ldl_opts
+    from oracle.ldl import OracleLDL
+    K, Lw = _sibling_k2(seed)
+    monkeypatch.setenv("MADIPM_BIG_MERGE", "0")
+    S0 = Symbolic(K.shape[0], Lw.indptr, Lw.indices, default_ldl_opts(ordering=1, relax=0))
+    monkeypatch.setenv("MADIPM_BIG_MERGE", "6")
+    S1 = Symbolic(K.shape[0], Lw.indptr, Lw.indices, default_ldl_opts(ordering=1, relax=0))
+    i0, i1 = S0.info(), S1.info()
+    perm = S1.perm()
+    assert sorted(perm.tolist()) == list(range(K.shape[0]))
+    assert i1["nnzL"] == i0["nnzL"] == _brute_nnzL(K, perm)
+    F = OracleLDL(K, perm)
+    assert F.factorize() == K.shape[0]
+    assert F.nnzL() == i1["nnzL"]
+    first, parent, nrows = S1.supernodes()
+    ns = i1["nsuper"]
+    assert np.all((parent == -1) | (parent > np.arange(ns)))
+    assert np.all(nrows >= np.diff(first))
+    # the siblings merged: no front with more than 256 rows has a parent any more
+    p0 = S0.supernodes()[1]
+    assert np.sum((S0.supernodes()[2] > 256) & (p0 >= 0)) >= 2
+    assert np.sum((nrows > 256) & (parent >= 0)) == 0
+    assert ns < i0["nsuper"] and i1["nnzL_stored"] >= i0["nnzL_stored"]
