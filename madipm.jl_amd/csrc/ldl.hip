@@ -4728,12 +4728,12 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     if (phase == 1 && NL == 1 && nftree_) ftree_launch();
   };
   build_fact(1, fact1_);
-  {  // tail overlap (MADIPM_TAIL_OVERLAP=0 disables): the launches after the tree kernel
+  {  // tail overlap (opt-in, MADIPM_TAIL_OVERLAP=1, until measured on the GPU): the launches after the tree kernel
     const char* et = std::getenv("MADIPM_TAIL_OVERLAP");
     size_t cut = fact1_.size();
     for (size_t k = 0; k < fact1_.size(); ++k)
       if (fact1_[k].kind == FTREE) cut = k + 1;
-    tail_ok_ = !(et && et[0] == '0') && S.nshards == 1 && nftree_ > 0 && cut < fact1_.size();
+    tail_ok_ = et && et[0] == '1' && S.nshards == 1 && nftree_ > 0 && cut < fact1_.size();
     if (tail_ok_) {
       fact1_head_.assign(fact1_.begin(), fact1_.begin() + cut);
       fact1_tail_.assign(fact1_.begin() + cut, fact1_.end());
