@@ -12,10 +12,16 @@
 // bipartite matching on the cut edges, Hopcroft–Karp).  Order = [part A][part B][separator],
 // recursively; disconnected subgraphs are ordered component by component with no separator;
 // leaves, and subgraphs without a good separator (|S| > sep_ratio |V|), are ordered by AMD.
+// Host-parallel: the two sides of a separator, runs of components and the bisection tries of a
+// large subgraph are independent and run on threads of their own (NDOptions::threads); every
+// subproblem's random stream is seeded from its position in the recursion, so the order is the same
+// whatever the thread count.
 #include <algorithm>
 #include <cstdint>
 #include <numeric>
 #include <queue>
+#include <thread>
+#include <cstdlib>
 #include <vector>
 
 #include "common.hpp"
@@ -60,12 +66,14 @@ bool coarsen(const Graph& g, Graph& c, std::vector<int32_t>& cmap, Rng& rng) {
       }
     }
     if (best == -1) {
-      match[v] = v;
+      match[v] = -2;  // no unmatched neighbour left: alone
     } else {
       match[v] = best;
       match[best] = v;
     }
   }
+  for (int v = 0; v < n; ++v)
+    if (match[v] == -2) match[v] = v;
   cmap.assign(n, -1);
   int nc = 0;
   for (int v = 0; v < n; ++v)
@@ -367,18 +375,35 @@ void vertex_separator(const Graph& g, const std::vector<uint8_t>& part, std::vec
     if (zr[b]) sep[R[b]] = 1;
 }
 
+// Per-thread scratch: global -> local id of the subgraph being built (-1 outside).  Every task that
+// runs on a thread of its own gets its own map, so concurrent subgraphs never see each other's ids.
+struct Ctx {
+  std::vector<int32_t> loc;
+  explicit Ctx(int n) : loc(n, -1) {}
+};
+
+// seeds of the subproblems: a fixed function of the parent's seed and the child's index, so the
+// order does not depend on how the recursion is spread over threads
+inline uint64_t child_seed(uint64_t s, uint64_t k) {
+  uint64_t z = s + 0x9E3779B97F4A7C15ull * (k + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
 struct Dissector {
   const std::vector<int64_t>& Ap;
   const std::vector<int32_t>& Ai;
   const NDOptions& opt;
-  std::vector<int32_t> loc;  // global -> local id of the subgraph being built (-1 outside)
-  std::vector<int32_t> out;
-  Rng rng{12345};
+  const int n;
+  // subgraphs below this size never get a thread of their own (the spawn costs more than the work)
+  static constexpr int kParMin = 4096;
 
-  Dissector(const std::vector<int64_t>& p, const std::vector<int32_t>& i, const NDOptions& o, int n)
-      : Ap(p), Ai(i), opt(o), loc(n, -1) {}
+  Dissector(const std::vector<int64_t>& p, const std::vector<int32_t>& i, const NDOptions& o, int nn)
+      : Ap(p), Ai(i), opt(o), n(nn) {}
 
-  void induced(const std::vector<int32_t>& verts, Graph& g) {
+  void induced(Ctx& cx, const std::vector<int32_t>& verts, Graph& g) const {
+    std::vector<int32_t>& loc = cx.loc;
     for (size_t k = 0; k < verts.size(); ++k) loc[verts[k]] = (int32_t)k;
     g.n = (int)verts.size();
     g.p.assign(g.n + 1, 0);
@@ -393,12 +418,10 @@ struct Dissector {
     }
     g.ew.assign(g.adj.size(), 1);
     g.vw.assign(g.n, 1);
-  }
-  void clear_loc(const std::vector<int32_t>& verts) {
     for (int v : verts) loc[v] = -1;
   }
 
-  void leaf(const std::vector<int32_t>& verts, const Graph& g) {
+  void leaf(const std::vector<int32_t>& verts, const Graph& g, std::vector<int32_t>& out) const {
     std::vector<int32_t> lp;
     if (g.n > 2) {
       amd_order(g.n, g.p, g.adj, lp, opt.dense_alpha);
@@ -409,12 +432,37 @@ struct Dissector {
     for (int k : lp) out.push_back(verts[k]);
   }
 
-  void dissect(const std::vector<int32_t>& verts, int depth) {
+  // Orders `parts` (disjoint vertex sets) one after another into `out`: in this thread when `par`
+  // is 1, else split into two runs of about equal vertex count, the second on a thread of its own.
+  void dissect_list(Ctx& cx, std::vector<std::vector<int32_t>>& parts, size_t p0, size_t p1, int depth,
+                    uint64_t seed, int par, std::vector<int32_t>& out) const {
+    int64_t tot = 0;
+    for (size_t k = p0; k < p1; ++k) tot += (int64_t)parts[k].size();
+    if (par <= 1 || p1 - p0 < 2 || tot < 2 * kParMin) {
+      for (size_t k = p0; k < p1; ++k) dissect(cx, parts[k], depth, child_seed(seed, k), 1, out);
+      return;
+    }
+    size_t mid = p0 + 1;
+    int64_t acc = (int64_t)parts[p0].size();
+    while (mid + 1 < p1 && 2 * (acc + (int64_t)parts[mid].size()) <= tot) acc += (int64_t)parts[mid++].size();
+    std::vector<int32_t> out2;
+    std::thread th([&] {
+      Ctx c2(n);
+      dissect_list(c2, parts, mid, p1, depth, seed, par / 2, out2);
+    });
+    dissect_list(cx, parts, p0, mid, depth, seed, par - par / 2, out);
+    th.join();
+    out.insert(out.end(), out2.begin(), out2.end());
+  }
+
+  void dissect(Ctx& cx, const std::vector<int32_t>& verts, int depth, uint64_t seed, int par,
+               std::vector<int32_t>& out) const {
+    PhaseClock clk("  nd top");  // MADIPM_SYMBOLIC_TIMING: the top bisection and the rest
+    if (depth > 0) clk.on = false;
     Graph g;
-    induced(verts, g);
-    clear_loc(verts);
+    induced(cx, verts, g);
     if (g.n <= opt.leaf_size || depth > 60) {
-      leaf(verts, g);
+      leaf(verts, g, out);
       return;
     }
     // connected components
@@ -435,45 +483,85 @@ struct Dissector {
     if (nc > 1) {
       std::vector<std::vector<int32_t>> parts(nc);
       for (int k = 0; k < g.n; ++k) parts[comp[k]].push_back(verts[k]);
-      for (auto& pv : parts) dissect(pv, depth + 1);
+      g = Graph();
+      dissect_list(cx, parts, 0, parts.size(), depth + 1, seed, par, out);
       return;
     }
-    // best of a few multilevel bisections, scored by separator size and balance
-    std::vector<uint8_t> part, sep, bpart, bsep;
-    double bscore = 1e300;
+    // best of a few multilevel bisections, scored by separator size and balance; the tries are
+    // independent (a seed each) and run on threads of their own where the budget allows
     const int tries = g.n > 20000 ? opt.tries : 1;  // several tries only where separators matter most
-    for (int t = 0; t < tries; ++t) {
-      bisect(g, part, rng);
-      vertex_separator(g, part, sep);
-      int64_t ns = 0, na = 0, nb = 0;
+    std::vector<std::vector<uint8_t>> parts(tries), seps(tries);
+    auto one_try = [&](int t) {
+      Rng rng(child_seed(seed, 1000 + (uint64_t)t));
+      bisect(g, parts[t], rng);
+      vertex_separator(g, parts[t], seps[t]);
+    };
+    auto sizes = [&](int t, int64_t& ns, int64_t& na, int64_t& nb) {
+      ns = na = nb = 0;
       for (int k = 0; k < g.n; ++k) {
-        if (sep[k])
+        if (seps[t][k])
           ++ns;
-        else if (part[k] == 0)
+        else if (parts[t][k] == 0)
           ++na;
         else
           ++nb;
       }
+    };
+    if (tries > 1 && par > 1) {
+      std::vector<std::thread> th;
+      for (int t = 1; t < tries; ++t) th.emplace_back(one_try, t);
+      one_try(0);
+      for (auto& x : th) x.join();
+    } else {
+      one_try(0);
+      int64_t ns0, na0, nb0;
+      sizes(0, ns0, na0, nb0);
+      // (the scoring below stops at a first try without a small separator: the others are not needed)
+      const bool stop = na0 != 0 && nb0 != 0 && ns0 > 2.0 * opt.sep_ratio * g.n;
+      for (int t = 1; t < tries && !stop; ++t) one_try(t);
+    }
+    clk("bisection tries");
+    int best = -1;
+    double bscore = 1e300;
+    for (int t = 0; t < tries; ++t) {
+      int64_t ns, na, nb;
+      sizes(t, ns, na, nb);
       if (na == 0 || nb == 0) continue;
       if (t == 0 && ns > 2.0 * opt.sep_ratio * g.n) break;  // no small separator here: AMD
       const double score = (double)ns * (1.0 + 2.0 * std::abs((double)(na - nb)) / (double)g.n);
       if (score < bscore) {
         bscore = score;
-        bpart = part;
-        bsep = sep;
+        best = t;
       }
     }
     int64_t ns = 0;
-    for (uint8_t s : bsep) ns += s;
-    if (bpart.empty() || ns > opt.sep_ratio * g.n) {
-      leaf(verts, g);
+    if (best >= 0)
+      for (uint8_t s : seps[best]) ns += s;
+    if (best < 0 || ns > opt.sep_ratio * g.n) {
+      leaf(verts, g, out);
       return;
     }
-    std::vector<int32_t> A, B, S;
-    for (int k = 0; k < g.n; ++k) (bsep[k] ? S : (bpart[k] == 0 ? A : B)).push_back(verts[k]);
+    std::vector<std::vector<int32_t>> ab(2);
+    std::vector<int32_t> S;
+    for (int k = 0; k < g.n; ++k) (seps[best][k] ? S : ab[parts[best][k]]).push_back(verts[k]);
     g = Graph();
-    dissect(A, depth + 1);
-    dissect(B, depth + 1);
+    parts.clear();
+    seps.clear();
+    // [A][B][separator]: A and B in parallel when both are large enough
+    if (par > 1 && (int64_t)ab[0].size() >= kParMin && (int64_t)ab[1].size() >= kParMin) {
+      std::vector<int32_t> outB;
+      std::thread th([&] {
+        Ctx c2(n);
+        dissect(c2, ab[1], depth + 1, child_seed(seed, 2), par / 2, outB);
+      });
+      dissect(cx, ab[0], depth + 1, child_seed(seed, 1), par - par / 2, out);
+      th.join();
+      clk("both sides");
+      out.insert(out.end(), outB.begin(), outB.end());
+    } else {
+      dissect(cx, ab[0], depth + 1, child_seed(seed, 1), 1, out);
+      dissect(cx, ab[1], depth + 1, child_seed(seed, 2), 1, out);
+    }
     out.insert(out.end(), S.begin(), S.end());
   }
 };
@@ -483,6 +571,7 @@ struct Dissector {
 void nd_order(int n, const std::vector<int64_t>& Ap, const std::vector<int32_t>& Ai, std::vector<int32_t>& perm,
               const NDOptions& opt) {
   Dissector d(Ap, Ai, opt, n);
+  std::vector<int32_t> out;
   // Dense vertices (degree above AMD's threshold, max(16, alpha sqrt(n))) are deferred and ordered
   // last, as AMD does: they would sit in every separator anyway, and leaving them in the graph makes
   // each level's induced subgraph / bisection cost O(their degree) -- for a dense-column QP (A dense,
@@ -505,11 +594,12 @@ void nd_order(int n, const std::vector<int64_t>& Ap, const std::vector<int32_t>&
   std::vector<int32_t> all, deferred;
   all.reserve(n);
   for (int v = 0; v < n; ++v) (Ap[v + 1] - Ap[v] > dense ? deferred : all).push_back(v);
-  d.out.reserve(n);
-  d.dissect(all, 0);
-  d.out.insert(d.out.end(), deferred.begin(), deferred.end());
-  MADIPM_REQUIRE((int)d.out.size() == n, "nested dissection lost vertices");
-  perm.swap(d.out);
+  out.reserve(n);
+  Ctx cx(n);
+  d.dissect(cx, all, 0, opt.seed, std::max(1, opt.threads), out);
+  out.insert(out.end(), deferred.begin(), deferred.end());
+  MADIPM_REQUIRE((int)out.size() == n, "nested dissection lost vertices");
+  perm.swap(out);
 }
 
 }  // namespace madipm

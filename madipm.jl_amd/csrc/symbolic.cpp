@@ -14,6 +14,7 @@
 #include <chrono>
 #include <cstdio>
 #include <thread>
+#include <atomic>
 #include <memory>
 
 #include "common.hpp"
@@ -507,31 +508,55 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         Ai[fill[j]++] = i;
       }
     std::vector<int64_t>().swap(fill);
-    std::vector<int32_t> pa, pn;
-    if (opt.ordering != 3) amd_order(N, Ap, Ai, pa, opt.dense_alpha);
-    stamp("1: AMD");
-    if (opt.ordering != 1) {
+    // Nested dissection is randomised (matchings, initial partitions).  On graphs with more than
+    // kBigAdj adjacency entries its fill varies with the seed far more than with anything else (neos
+    // stand-in: 240-323 GFLOP over seeds; ex10 and supportcase10, below the bound: within 0.5 %), so
+    // there it runs with kNdSeeds fixed seeds at once — each with a share of the analysis threads —
+    // and the order with the fewest flops is kept (lowest seed on ties: the same choice whatever the
+    // thread count).  ordering = auto adds AMD (one thread) beside ND and keeps the overall best; AMD
+    // is skipped above kBigAdj, where it is the slowest step of the analysis and ND wins anyway on
+    // the benchmark LPs (AMD vs ND flops: ex10 4.5e10 vs 2.6e8, supportcase10 6.0e8 vs 3.4e8, neos
+    // 4.2e11 vs 2.5e11).  Every candidate is analysed in full (etree + column counts).
+    constexpr int kNdSeeds = 4;
+    constexpr int64_t kBigAdj = 4000000, kNdSeedsMaxAdj = 40000000;
+    std::vector<int32_t> pa;
+    const bool use_nd = opt.ordering != 1;
+    const bool use_amd = opt.ordering == 1 || (opt.ordering == 4 && Ap[N] <= kBigAdj);
+    const int nseeds = use_nd ? (Ap[N] > kBigAdj && Ap[N] <= kNdSeedsMaxAdj ? kNdSeeds : 1) : 0;
+    std::vector<OrderAnalysis> B(nseeds);
+    OrderAnalysis A;
+    const int T = analysis_threads();
+    const int per = std::max(1, (T - (use_amd ? 1 : 0)) / std::max(1, nseeds));
+    auto run_nd = [&](int k) {
       NDOptions nopt;
       nopt.dense_alpha = opt.dense_alpha;
+      nopt.threads = per;
+      nopt.seed = 12345 + (uint64_t)k;
+      std::vector<int32_t> pn;
       nd_order(N, Ap, Ai, pn, nopt);
-    }
-    stamp("1: ND");
+      analyse_order(N, colptr, rowval, std::move(pn), B[k]);
+    };
+    std::vector<std::thread> th;
+    if (use_amd)
+      th.emplace_back([&] {
+        amd_order(N, Ap, Ai, pa, opt.dense_alpha);
+        analyse_order(N, colptr, rowval, std::move(pa), A);
+      });
+    for (int k = 1; k < nseeds; ++k) th.emplace_back(run_nd, k);
+    if (nseeds) run_nd(0);
+    for (auto& x : th) x.join();
+    stamp("1: orderings (ND seeds, AMD) + analysis");
     std::vector<int64_t>().swap(Ap);
     std::vector<int32_t>().swap(Ai);
-    if (opt.ordering != 3) {
-      analyse_order(N, colptr, rowval, std::move(pa), OA);
-      S.order_flops_amd = OA.flops;
-    }
-    if (opt.ordering != 1) {
-      if (opt.ordering == 4 && pn == OA.perm) {  // ND found AMD's (postordered) order: nothing to compare
-        S.order_flops_nd = OA.flops;
-      } else {
-        OrderAnalysis B;
-        analyse_order(N, colptr, rowval, std::move(pn), B);
-        S.order_flops_nd = B.flops;
-        if (opt.ordering == 3 || B.flops < OA.flops) std::swap(OA, B);
-      }
-    }
+    int best = -1;
+    for (int k = 0; k < nseeds; ++k)
+      if (best < 0 || B[k].flops < B[best].flops) best = k;
+    if (use_amd) S.order_flops_amd = A.flops;
+    if (best >= 0) S.order_flops_nd = B[best].flops;
+    if (best >= 0 && (!use_amd || B[best].flops < A.flops))
+      std::swap(OA, B[best]);
+    else
+      std::swap(OA, A);
   } else if (opt.ordering == 2) {
     MADIPM_REQUIRE(user_perm != nullptr, "user permutation missing");
     analyse_order(N, colptr, rowval, std::vector<int32_t>(user_perm, user_perm + N), OA);
@@ -1372,12 +1397,9 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     };
     auto sq_bytes = [](int64_t r) { return 8 * ((r * (r | 1) + 1) & ~1LL); };
     auto pk_bytes = [](int64_t r) { return 8 * ((r * (r + 1) / 2 + 1) & ~1LL); };
-    std::vector<int64_t> col0(32), col1(32);
     struct Prod {
       uint32_t dst, q1, q2;
     };
-    std::vector<Prod> pr;
-    std::vector<std::vector<uint32_t>> enc;
     {
       // k_fact_tree's ticket order: by level (children before parents, so a workgroup waiting on its
       // children never blocks the tickets they need), and within a level by descending tail — the
@@ -1398,10 +1420,25 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       }
       S.ft_order.assign(ord.begin(), ord.end());
     }
-    for (int s = 0; s < ns_all; ++s) {
-      S.mc_ptr[s + 1] = S.mc_ptr[s];
-      S.fold_bptr[s + 1] = S.fold_bptr[s];
-      if (!on || !S.ftree[s] || S.nrows[s] > SymbolicPlan::kFactTreeMax) continue;  // medium fronts: no folding
+    // One front's fold tables, with part-local offsets: the fronts are independent, so they run on
+    // the analysis threads and the parts are appended in front order afterwards (offsets shifted —
+    // the tables are the sequential ones bit for bit).
+    struct FoldPart {
+      std::vector<int32_t> mc_list, ab_src0, ab_src1, ab_k, ab_wrc, fold_bat, fold_plen;
+      std::vector<int64_t> ab_first, ab_f0, fold_row0, fold_poff;
+      std::vector<uint32_t> fold_prod, fold_chead;
+    };
+    struct FoldScratch {
+      std::vector<int64_t> col0 = std::vector<int64_t>(32), col1 = std::vector<int64_t>(32);
+      std::vector<Prod> pr;
+      std::vector<std::vector<uint32_t>> enc;
+    };
+    auto fold_front = [&](int s, FoldPart& P, FoldScratch& X) {
+      auto& pr = X.pr;
+      auto& enc = X.enc;
+      auto& col0 = X.col0;
+      auto& col1 = X.col1;
+      if (!on || !S.ftree[s] || S.nrows[s] > SymbolicPlan::kFactTreeMax) return;  // medium fronts: no folding
       const int64_t r = S.nrows[s];
       int64_t nmc = 0, nrow = 0;
       bool ok = true;
@@ -1412,7 +1449,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         ++nmc;
         nrow += S.nrows[c];
       }
-      if (!ok || nmc == 0) continue;
+      if (!ok || nmc == 0) return;
       // storage: square (r <= 128) when the front and all its leaf rows fit, else packed lower;
       // leaves in batches when even that does not fit
       int pk;
@@ -1424,7 +1461,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         pk = 1;
         budget = LMAX - pk_bytes(r);
       }
-      if (budget < RB * 32 + LB) continue;  // not even one leaf fits beside the front
+      if (budget < RB * 32 + LB) return;  // not even one leaf fits beside the front
       // a batch of `rows` leaf rows and `nl` leaves fits when the front's LDS carve — sized by the
       // largest batch's rows and the largest batch's leaf count, possibly two different batches —
       // stays within the budget
@@ -1447,7 +1484,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
           rmax = std::max(rmax, rows);
           lmax = std::max(lmax, nl);
         }
-        if (!ok2 || nb > SymbolicPlan::kFoldMaxBatches) continue;
+        if (!ok2 || nb > SymbolicPlan::kFoldMaxBatches) return;
       }
       S.absorb[s] = 1;
       S.fold_pk[s] = (uint8_t)pk;
@@ -1455,18 +1492,17 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       auto fidx = [&](int64_t i, int64_t j) -> uint32_t {
         return (uint32_t)(pk ? (j * (2 * r - j - 1)) / 2 + i : i + j * ld);
       };
-      const int k0 = (int)S.mc_list.size();
+      const int k0 = 0;  // part-local leaf indices (shifted when the parts are appended)
       for (int64_t qc = S.child_ptr[s]; qc < S.child_ptr[s + 1]; ++qc)
-        if (!S.ftree[S.child_list[qc]]) S.mc_list.push_back(S.child_list[qc]);
-      const int k1 = (int)S.mc_list.size();
-      S.mc_ptr[s + 1] = k1;
+        if (!S.ftree[S.child_list[qc]]) P.mc_list.push_back(S.child_list[qc]);
+      const int k1 = (int)P.mc_list.size();
       // flat leaf rows (child order)
       for (int k = k0; k < k1; ++k) {
-        const int c = S.mc_list[k];
+        const int c = P.mc_list[k];
         const int rc = S.nrows[c], wc = S.first[c + 1] - S.first[c];
-        S.ab_first.push_back((int64_t)S.ab_src0.size());
-        S.ab_f0.push_back(S.first[c]);
-        S.ab_wrc.push_back(wc | (rc << 8));
+        P.ab_first.push_back((int64_t)P.ab_src0.size());
+        P.ab_f0.push_back(S.first[c]);
+        P.ab_wrc.push_back(wc | (rc << 8));
         std::fill(col0.begin(), col0.end(), -1);
         std::fill(col1.begin(), col1.end(), -1);
         for (int64_t q = S.asm_ptr[c]; q < S.asm_ptr[c + 1]; ++q) {
@@ -1476,9 +1512,9 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         }
         for (int i = 0; i < rc; ++i) {
           MADIPM_REQUIRE(col0[i] < INT32_MAX && col1[i] < INT32_MAX, "folded leaf: CSC index beyond int32");
-          S.ab_src0.push_back((int32_t)col0[i]);
-          S.ab_src1.push_back((int32_t)col1[i]);
-          S.ab_k.push_back(k);
+          P.ab_src0.push_back((int32_t)col0[i]);
+          P.ab_src1.push_back((int32_t)col1[i]);
+          P.ab_k.push_back(k);
         }
       }
       // batches and their product lists
@@ -1486,20 +1522,20 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       while (kb < k1) {
         int ke = kb;
         int64_t rows = 0;
-        while (ke < k1 && fits(rows + S.nrows[S.mc_list[ke]], ke - kb + 1, S.fold_rmax[s], S.fold_lmax[s]))
-          rows += S.nrows[S.mc_list[ke++]];
+        while (ke < k1 && fits(rows + S.nrows[P.mc_list[ke]], ke - kb + 1, S.fold_rmax[s], S.fold_lmax[s]))
+          rows += S.nrows[P.mc_list[ke++]];
         MADIPM_REQUIRE(ke > kb, "fold: a leaf does not fit the batch budget");
-        S.fold_bat.push_back(kb);
-        S.fold_row0.push_back(S.ab_first[kb]);
+        P.fold_bat.push_back(kb);
+        P.fold_row0.push_back(P.ab_first[kb]);
         S.fold_rmax[s] = std::max<int32_t>(S.fold_rmax[s], (int32_t)rows);
         S.fold_lmax[s] = std::max<int32_t>(S.fold_lmax[s], ke - kb);
-        const int64_t row0 = S.ab_first[kb];
+        const int64_t row0 = P.ab_first[kb];
         pr.clear();
         for (int k = kb; k < ke; ++k) {
-          const int c = S.mc_list[k];
+          const int c = P.mc_list[k];
           const int rc = S.nrows[c], wc = S.first[c + 1] - S.first[c];
           const int32_t* rl = S.rel.data() + S.rel_ptr[c];
-          const uint32_t qb0 = (uint32_t)(S.ab_first[k] - row0);
+          const uint32_t qb0 = (uint32_t)(P.ab_first[k] - row0);
           for (int a = wc; a < rc; ++a)
             for (int b = wc; b <= a; ++b)  // rel ascending: parent row of b <= that of a
               pr.push_back({fidx(rl[a - wc], rl[b - wc]), qb0 + a, qb0 + b});
@@ -1509,13 +1545,13 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         // destination (SymbolicPlan: one word per entry, kFoldPad steps for jumps beyond 127)
         constexpr int NCH = NT_FOLD;
         constexpr uint32_t PAD = SymbolicPlan::kFoldPad;
-        const int64_t P = (int64_t)pr.size();
+        const int64_t NP = (int64_t)pr.size();
         enc.assign(NCH, {});
         // (fewer products than chunks: one per chunk, the empty chunks last — the parts of a split
         // run always lie in adjacent chunks, which the kernel's left-to-right tail sum relies on)
         for (int t = 0; t < NCH; ++t) {
-          const int64_t q0 = P < NCH ? std::min<int64_t>(t, P) : P * t / NCH;
-          const int64_t q1 = P < NCH ? std::min<int64_t>(t + 1, P) : P * (t + 1) / NCH;
+          const int64_t q0 = NP < NCH ? std::min<int64_t>(t, NP) : NP * t / NCH;
+          const int64_t q1 = NP < NCH ? std::min<int64_t>(t + 1, NP) : NP * (t + 1) / NCH;
           std::vector<uint32_t>& E = enc[t];
           uint32_t head = 0;
           if (q0 < q1) {
@@ -1530,20 +1566,55 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
               E.push_back(pr[q].q1 | (pr[q].q2 << 12) | (dd << 24) | (end ? SymbolicPlan::kFoldRunEnd : 0u));
             }
           }
-          S.fold_chead.push_back(head);
+          P.fold_chead.push_back(head);
         }
         int64_t len = 0;
         for (int t = 0; t < NCH; ++t) len = std::max<int64_t>(len, (int64_t)enc[t].size());
-        const int64_t off = (int64_t)S.fold_prod.size();
-        S.fold_poff.push_back(off);
-        S.fold_plen.push_back((int32_t)len);
-        S.fold_prod.resize(off + len * NCH, PAD);  // padding: no product, no step, no run end
+        const int64_t off = (int64_t)P.fold_prod.size();
+        P.fold_poff.push_back(off);
+        P.fold_plen.push_back((int32_t)len);
+        P.fold_prod.resize(off + len * NCH, PAD);  // padding: no product, no step, no run end
         for (int t = 0; t < NCH; ++t)
-          for (size_t k = 0; k < enc[t].size(); ++k) S.fold_prod[off + (int64_t)k * NCH + t] = enc[t][k];
+          for (size_t k = 0; k < enc[t].size(); ++k) P.fold_prod[off + (int64_t)k * NCH + t] = enc[t][k];
         kb = ke;
       }
-      S.fold_bptr[s + 1] = (int32_t)S.fold_bat.size();
       MADIPM_REQUIRE(RB * S.fold_rmax[s] + LB * S.fold_lmax[s] <= budget, "fold: LDS carve beyond the budget");
+    };
+    {
+      std::vector<FoldPart> fparts(ns_all);
+      std::atomic<int> next{0};
+      const int T = std::max(1, std::min<int>(analysis_threads(), ns_all / 256));
+      auto worker = [&] {
+        FoldScratch X;
+        for (int s0; (s0 = next.fetch_add(64)) < ns_all;)
+          for (int s = s0; s < std::min(ns_all, s0 + 64); ++s) fold_front(s, fparts[s], X);
+      };
+      std::vector<std::thread> th;
+      for (int t = 1; t < T; ++t) th.emplace_back(worker);
+      worker();
+      for (auto& x : th) x.join();
+      for (int s = 0; s < ns_all; ++s) {
+        FoldPart& P = fparts[s];
+        const int32_t mbase = (int32_t)S.mc_list.size();
+        const int64_t abase = (int64_t)S.ab_src0.size(), pbase = (int64_t)S.fold_prod.size();
+        S.mc_list.insert(S.mc_list.end(), P.mc_list.begin(), P.mc_list.end());
+        for (int64_t v : P.ab_first) S.ab_first.push_back(v + abase);
+        S.ab_f0.insert(S.ab_f0.end(), P.ab_f0.begin(), P.ab_f0.end());
+        S.ab_wrc.insert(S.ab_wrc.end(), P.ab_wrc.begin(), P.ab_wrc.end());
+        S.ab_src0.insert(S.ab_src0.end(), P.ab_src0.begin(), P.ab_src0.end());
+        S.ab_src1.insert(S.ab_src1.end(), P.ab_src1.begin(), P.ab_src1.end());
+        for (int32_t v : P.ab_k) S.ab_k.push_back(v + mbase);
+        for (int32_t v : P.fold_bat) S.fold_bat.push_back(v + mbase);
+        for (int64_t v : P.fold_row0) S.fold_row0.push_back(v + abase);
+        for (int64_t v : P.fold_poff) S.fold_poff.push_back(v + pbase);
+        S.fold_plen.insert(S.fold_plen.end(), P.fold_plen.begin(), P.fold_plen.end());
+        S.fold_prod.insert(S.fold_prod.end(), P.fold_prod.begin(), P.fold_prod.end());
+        S.fold_chead.insert(S.fold_chead.end(), P.fold_chead.begin(), P.fold_chead.end());
+        S.mc_ptr[s + 1] = (int32_t)S.mc_list.size();
+        S.fold_bptr[s + 1] = (int32_t)S.fold_bat.size();
+        FoldPart().mc_list.swap(P.mc_list);
+        std::vector<uint32_t>().swap(P.fold_prod);
+      }
     }
     S.ab_first.push_back((int64_t)S.ab_src0.size());
     // sentinels: the batch after a front's last one starts at that front's end (leaves and rows are
@@ -1570,6 +1641,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
                   acc[lv * 6 + 3] / acc[lv * 6], acc[lv * 6 + 4] / acc[lv * 6]);
     }
   }
+  stamp("10a: fold product lists");
   S.fs_off.assign(ns, -1);
   S.fs_size = 0;
   for (int s = 0; s < ns; ++s)
@@ -1589,9 +1661,6 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   S.chunk_lev.assign(2 * S.nlevels + 3, 0);
   S.g_chunk.clear();
   {
-    std::vector<int32_t> key, tcnt, cnt(4097);
-    std::vector<int64_t> src, bysrc, sorted;
-    std::vector<int32_t> bykey;
     // children of s whose update blocks this assembly reads: 0 all, 1 top children only, 2 this
     // shard's subtree children only
     auto child_ok = [&](int c, int which) {
@@ -1601,8 +1670,27 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       if (which == 3) return !S.ftree[c];  // tree front: pre-leaf children only
       return !S.top(c) && S.owner[c] == S.shard;
     };
+    // One emit = the tiles of one front, written into a part of its own with part-local offsets (the
+    // fronts are independent, so the emits run on the analysis threads; the parts are appended in
+    // emit order afterwards, offsets shifted — the plan is the sequential one bit for bit).
+    struct Part {
+      std::vector<SymbolicPlan::AsmTile> atiles;
+      std::vector<int32_t> g_ptr, bt;
+      std::vector<int64_t> g_chunk, g_src;
+    };
+    struct Scratch {
+      std::vector<int32_t> key, tcnt, cnt = std::vector<int32_t>(4097), bykey;
+      std::vector<int64_t> src, bysrc, sorted;
+    };
     // tsel: 0 every tile, 1 the tiles of column block 0 only, 2 the others only
-    auto emit = [&](int s, bool orig, int which, bool acc, bool emit_empty, int tsel = 0) {
+    auto emit = [&](Part& P, Scratch& X, int s, bool orig, int which, bool acc, bool emit_empty, int tsel) {
+      auto& key = X.key;
+      auto& tcnt = X.tcnt;
+      auto& cnt = X.cnt;
+      auto& bykey = X.bykey;
+      auto& src = X.src;
+      auto& bysrc = X.bysrc;
+      auto& sorted = X.sorted;
       const int r = S.nrows[s];
       const int nt = (r + 63) / 64;
       const int ntile = nt * (nt + 1) / 2;
@@ -1668,21 +1756,21 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
               std::vector<int32_t> fill(cnt.begin(), cnt.end() - 1);
               for (int64_t e = e0; e < e1; ++e) sorted[e0 + fill[bykey[e]]++] = bysrc[e];
             }
-            at.gptr = (int64_t)S.g_ptr.size();
-            at.gchk = (int64_t)S.g_chunk.size();
+            at.gptr = (int64_t)P.g_ptr.size();
+            at.gchk = (int64_t)P.g_chunk.size();
             int32_t nchk = 0;
-            const int64_t sbase = (int64_t)S.g_src.size();
+            const int64_t sbase = (int64_t)P.g_src.size();
             for (int k = 0; k < 4096; ++k) {
-              S.g_ptr.push_back(nchk);
-              for (int64_t c = cnt[k]; c < cnt[k + 1]; c += SymbolicPlan::kChunk, ++nchk) S.g_chunk.push_back(sbase + c);
+              P.g_ptr.push_back(nchk);
+              for (int64_t c = cnt[k]; c < cnt[k + 1]; c += SymbolicPlan::kChunk, ++nchk) P.g_chunk.push_back(sbase + c);
             }
-            S.g_ptr.push_back(nchk);
-            S.g_src.insert(S.g_src.end(), sorted.begin() + e0, sorted.begin() + e1);
+            P.g_ptr.push_back(nchk);
+            P.g_src.insert(P.g_src.end(), sorted.begin() + e0, sorted.begin() + e1);
           } else {
             at.gptr = -1;
             at.gchk = 0;
           }
-          at.bt0 = (int32_t)(S.bt.size() / 5);
+          at.bt0 = (int32_t)(P.bt.size() / 5);
           const int I0 = ti * 64, I1 = std::min(r, I0 + 64), J0 = tj * 64, J1 = std::min(r, J0 + 64);
           for (int c : bigch) {
             const int uc = S.nrows[c] - (S.first[c + 1] - S.first[c]);
@@ -1693,18 +1781,26 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
             const int a1 = (int)(std::lower_bound(relc + a0, relc + uc, I1) - relc);
             if (b0 < b1 && a0 < a1 && a1 - 1 >= b0) {
               const int32_t e[5] = {c, b0, b1, a0, a1};
-              S.bt.insert(S.bt.end(), e, e + 5);
+              P.bt.insert(P.bt.end(), e, e + 5);
             }
           }
-          at.bt1 = (int32_t)(S.bt.size() / 5);
-          if (has_g || at.bt1 > at.bt0 || emit_empty) S.atiles.push_back(at);
+          at.bt1 = (int32_t)(P.bt.size() / 5);
+          if (has_g || at.bt1 > at.bt0 || emit_empty) P.atiles.push_back(at);
         }
     };
-    const int NL = S.nlevels;
-    auto close_group = [&](int g) {
-      S.atile_lev[g + 1] = (int32_t)S.atiles.size();
-      S.chunk_lev[g + 1] = (int64_t)S.g_chunk.size();
+    // the plan as a sequence of operations: emits, and marks recording where a group / the fused
+    // fronts' tiles begin (mark kinds: 0 close_group(g), 1 atile_fz0[g], 2 atile_fz1[g])
+    struct Op {
+      int s, which, tsel;
+      bool orig, acc, emit_empty;
+      int mark, g;
     };
+    std::vector<Op> ops;
+    auto op_emit = [&](int s, bool orig, int which, bool acc, bool emit_empty, int tsel = 0) {
+      ops.push_back(Op{s, which, tsel, orig, acc, emit_empty, -1, 0});
+    };
+    auto op_mark = [&](int kind, int g) { ops.push_back(Op{0, 0, 0, false, false, false, kind, g}); };
+    const int NL = S.nlevels;
     // phase 1: this shard's fronts (all fronts when unsharded), level by level.  Single-panel big
     // fronts (w <= 64; SymbolicPlan::fused) last: their column block 0 (the panel, assembled before the
     // panel factorisation), then their other tiles, which k_asm_update assembles after the panel's
@@ -1729,38 +1825,112 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         const int s = S.level_list[q];
         if (S.top(s) || !S.mine(s) || lb_member(s) || S.ftree[s] || S.fused[s]) continue;
         if (!S.is_big[s] && S.fs_off[s] < 0) continue;
-        emit(s, true, 0, false, true);
+        op_emit(s, true, 0, false, true);
       }
-      S.atile_fz0[lev] = (int32_t)S.atiles.size();
+      op_mark(1, lev);
       for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q)
-        if (S.fused[S.level_list[q]]) emit(S.level_list[q], true, 0, false, true, 1);
-      S.atile_fz1[lev] = (int32_t)S.atiles.size();
+        if (S.fused[S.level_list[q]]) op_emit(S.level_list[q], true, 0, false, true, 1);
+      op_mark(2, lev);
       for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q)
-        if (S.fused[S.level_list[q]]) emit(S.level_list[q], true, 0, false, true, 2);
-      close_group(lev);
+        if (S.fused[S.level_list[q]]) op_emit(S.level_list[q], true, 0, false, true, 2);
+      op_mark(0, lev);
     }
     // top fronts, external part (before the all-reduce; zeros included)
     for (int s = 0; s < ns; ++s)
-      if (S.top(s)) emit(s, S.shard == 0, 2, false, true);
-    close_group(NL);
+      if (S.top(s)) op_emit(s, S.shard == 0, 2, false, true);
+    op_mark(0, NL);
     // phase 2: top fronts, internal part (their top children), level by level
     for (int lev = 0; lev < NL; ++lev) {
       for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) {
         const int s = S.level_list[q];
-        if (S.top(s)) emit(s, false, 1, true, false);
+        if (S.top(s)) op_emit(s, false, 1, true, false);
       }
-      close_group(NL + 1 + lev);
+      op_mark(0, NL + 1 + lev);
     }
     // factorisation-tree pre-assembly (after the level-0 launches), tree fronts in level order
     for (int lev = 0; lev < NL; ++lev)
       for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q)
-        if (S.ftree[S.level_list[q]] && !S.absorb[S.level_list[q]]) emit(S.level_list[q], true, 3, false, true);
-    close_group(2 * NL + 1);
+        if (S.ftree[S.level_list[q]] && !S.absorb[S.level_list[q]]) op_emit(S.level_list[q], true, 3, false, true);
+    op_mark(0, 2 * NL + 1);
+    // the emits, dealt dynamically to the analysis threads (heaviest fronts vary a lot in cost)
+    std::vector<Part> parts(ops.size());
+    {
+      std::atomic<size_t> next{0};
+      int64_t work = 0;
+      for (const Op& o : ops)
+        if (o.mark < 0) work += (int64_t)S.nrows[o.s] * S.nrows[o.s];
+      const int T = std::max(1, std::min<int>(analysis_threads(), (int)(work / 200000)));
+      auto worker = [&] {
+        Scratch X;
+        for (size_t k; (k = next.fetch_add(1)) < ops.size();) {
+          const Op& o = ops[k];
+          if (o.mark < 0) emit(parts[k], X, o.s, o.orig, o.which, o.acc, o.emit_empty, o.tsel);
+        }
+      };
+      std::vector<std::thread> th;
+      for (int t = 1; t < T; ++t) th.emplace_back(worker);
+      worker();
+      for (auto& x : th) x.join();
+    }
+    // append the parts in emit order, offsets shifted
+    {
+      size_t na = 0, np = 0, nb = 0, nc = 0, nsrc = 0;
+      for (const Part& P : parts) {
+        na += P.atiles.size();
+        np += P.g_ptr.size();
+        nb += P.bt.size();
+        nc += P.g_chunk.size();
+        nsrc += P.g_src.size();
+      }
+      S.atiles.reserve(na);
+      S.g_ptr.reserve(np);
+      S.bt.reserve(nb);
+      S.g_chunk.reserve(nc + 1);
+      S.g_src.reserve(nsrc);
+    }
+    for (size_t k = 0; k < ops.size(); ++k) {
+      const Op& o = ops[k];
+      if (o.mark == 0) {
+        S.atile_lev[o.g + 1] = (int32_t)S.atiles.size();
+        S.chunk_lev[o.g + 1] = (int64_t)S.g_chunk.size();
+        continue;
+      }
+      if (o.mark == 1) {
+        S.atile_fz0[o.g] = (int32_t)S.atiles.size();
+        continue;
+      }
+      if (o.mark == 2) {
+        S.atile_fz1[o.g] = (int32_t)S.atiles.size();
+        continue;
+      }
+      Part& P = parts[k];
+      const int64_t pbase = (int64_t)S.g_ptr.size(), cbase = (int64_t)S.g_chunk.size();
+      const int64_t sbase = (int64_t)S.g_src.size();
+      const int32_t bbase = (int32_t)(S.bt.size() / 5);
+      for (SymbolicPlan::AsmTile at : P.atiles) {
+        if (at.gptr >= 0) {
+          at.gptr += pbase;
+          at.gchk += cbase;
+        }
+        at.bt0 += bbase;
+        at.bt1 += bbase;
+        S.atiles.push_back(at);
+      }
+      S.g_ptr.insert(S.g_ptr.end(), P.g_ptr.begin(), P.g_ptr.end());
+      for (int64_t c : P.g_chunk) S.g_chunk.push_back(c + sbase);
+      S.g_src.insert(S.g_src.end(), P.g_src.begin(), P.g_src.end());
+      S.bt.insert(S.bt.end(), P.bt.begin(), P.bt.end());
+      Part().atiles.swap(P.atiles);  // release as we go
+      std::vector<int32_t>().swap(P.g_ptr);
+      std::vector<int64_t>().swap(P.g_src);
+      std::vector<int64_t>().swap(P.g_chunk);
+    }
     S.g_chunk.push_back((int64_t)S.g_src.size());  // sentinel
     MADIPM_REQUIRE(S.g_src.size() < (size_t)INT32_MAX * 2 && S.atiles.size() < (size_t)INT32_MAX, "assembly plan too large");
   }
 
-  stamp("before 11");
+  stamp("10b: assembly plan");
+
   // ---------------- 11. forward-solve gather lists (child order).  Sharded: a top front's rows list
   // only its top children (sv); its subtree-root children of this shard are listed in sx (the
   // external forward contribution, exchanged before the top forward solve).

@@ -20,6 +20,8 @@ struct NDOptions {
   int tries = 3;             // multilevel bisections per subgraph (best separator kept)
   double sep_ratio = 0.1;    // a separator larger than this fraction => AMD for the subgraph
   double dense_alpha = 10.0; // for the AMD leaves
+  int threads = 1;           // host threads for independent subgraphs / tries (the order does not depend on it)
+  uint64_t seed = 12345;     // root of every subproblem's random stream
 };
 
 // Nested dissection (csrc/nd.cpp); same input convention as amd_order.

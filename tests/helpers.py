@@ -78,3 +78,34 @@ def lp_k2(qp, seed, well=False, delta=1e-8):
     Lw = sp.tril(K).tocsc()
     Lw.sort_indices()
     return K, Lw
+
+
+def kkt_properties(qp, st):
+    """Optimality measures of (x, y, zl, zu) for min/max c'x + x'Hx/2 + c0, Ax = b, l <= x <= u
+    (unscaled).  The multipliers are those of the problem the solver minimises, sigma f with
+    sigma = +1 (minimise) / -1 (maximise) (MadNLP's objective sign [EXT]; the reference flips only the
+    reported objective back, /root/reference/src/utils.jl:150-156): stationarity
+    sigma (c + Hx) + A'y - zl + zu = 0, and the dual bound of min sigma f,
+    sigma c0 - y'b + zl'l - zu'u - sigma x'Hx/2 (src/kernels.jl:408-430), is reported in the
+    problem's own sense (times sigma) so that it compares with the primal objective."""
+    import scipy.sparse as sp
+    n, m = qp.nvar, qp.ncon
+    sg = 1.0 if getattr(qp, "minimize", True) else -1.0
+    A = sp.csr_matrix((qp.Avals, (qp.Arows, qp.Acols)), shape=(m, n))
+    x, y, zl, zu = st.solution, st.multipliers, st.multipliers_L, st.multipliers_U
+    hx = np.zeros(n)
+    np.add.at(hx, qp.Hrows, qp.Hvals * x[qp.Hcols])
+    off = qp.Hrows != qp.Hcols
+    np.add.at(hx, qp.Hcols[off], qp.Hvals[off] * x[qp.Hrows[off]])
+    b = qp.lcon
+    pr = np.max(np.abs(A @ x - b)) / (1.0 + np.max(np.abs(b)))
+    g = sg * (qp.c + hx)
+    du = np.max(np.abs(g + A.T @ y - zl + zu)) / (1.0 + np.max(np.abs(qp.c)))
+    lo, hi = np.isfinite(qp.lvar), np.isfinite(qp.uvar)
+    compl = max(np.max(np.abs((x - qp.lvar)[lo] * zl[lo]), initial=0.0),
+                np.max(np.abs((qp.uvar - x)[hi] * zu[hi]), initial=0.0))
+    pobj = qp.c0 + qp.c @ x + 0.5 * x @ hx
+    dobj = sg * (sg * qp.c0 - y @ b + zl[lo] @ qp.lvar[lo] - zu[hi] @ qp.uvar[hi] - sg * 0.5 * x @ hx)
+    return dict(pr=pr, du=du, compl=compl, pobj=pobj, dobj=dobj,
+                bounds=max(np.max((qp.lvar - x)[lo], initial=-1.0), np.max((x - qp.uvar)[hi], initial=-1.0)),
+                zmin=min(np.min(zl[lo], initial=0.0), np.min(zu[hi], initial=0.0)))

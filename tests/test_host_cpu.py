@@ -437,3 +437,39 @@ def test_symbolic_sibling_merge(seed, monkeypatch):
     assert np.sum((S0.supernodes()[2] > 256) & (p0 >= 0)) >= 2
     assert np.sum((nrows > 256) & (parent >= 0)) == 0
     assert ns < i0["nsuper"] and i1["nnzL_stored"] >= i0["nnzL_stored"]
+
+
+_THREADS_PROBE = r"""
+import sys, hashlib
+sys.path[:0] = [sys.argv[1], sys.argv[1] + '/madipm.jl_amd', sys.argv[1] + '/tests']
+import numpy as np
+from helpers import lp_k2
+from madipm_amd import standard_form_qp
+from madipm_amd import instances as I
+from madipm_amd._lib import Symbolic, default_ldl_opts
+qp = standard_form_qp(I.ex10_standin(scale=0.1))
+K, Lw = lp_k2(qp, 0)
+for ordering in (3, 4):
+    S = Symbolic(K.shape[0], Lw.indptr, Lw.indices, default_ldl_opts(ordering=ordering))
+    first, parent, nrows = S.supernodes()
+    h = hashlib.sha256(S.perm().tobytes() + first.tobytes() + parent.tobytes() + nrows.tobytes()).hexdigest()
+    print(ordering, S.info()["nnzL"], h)
+"""
+
+
+def test_analysis_independent_of_thread_count():
+    """Nested dissection runs its independent subgraphs, bisection tries and seeds on host threads
+    (csrc/nd.cpp, symbolic.cpp step 1), the fold tables and the assembly plan per front on threads
+    (step 10): the order, the fronts and the plan must not depend on MADIPM_ANALYSIS_THREADS (read
+    once per process, hence the subprocesses)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = []
+    for t in ("1", "3", "8"):
+        env = dict(os.environ, MADIPM_ANALYSIS_THREADS=t)
+        r = subprocess.run([sys.executable, "-c", _THREADS_PROBE, root], env=env, capture_output=True,
+                           text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(r.stdout)
+    assert outs[0] == outs[1] == outs[2], outs

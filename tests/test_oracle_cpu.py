@@ -194,3 +194,41 @@ def test_oracle_failed_factorization_is_internal_error():
     st = o.solve()
     assert st.status == SOLVE_SUCCEEDED and abs(st.objective - 1.0) <= 1e-7
     assert all(abs(t["del_w"] - 1e-8) <= 1e-20 for t in st.trace[1:])
+
+
+@pytest.mark.skipif(not __import__("oracle.pardiso", fromlist=["available"]).available(), reason="MKL absent")
+def test_kkt_properties_maximisation_stand_in():
+    """The optimality measures the full-size GPU tests threshold (helpers.kkt_properties), pinned on a
+    maximisation stand-in (every MIPLIB stand-in is minimize=False) where the oracle runs: with the
+    solver's objective sign sigma = -1 the returned (x, y, zl, zu) satisfy the KKT conditions to the
+    IPM's tolerance and the dual bound equals the primal objective; HiGHS gives the same optimum."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    import bench
+    from helpers import kkt_properties
+    from oracle import pardiso
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)), "tools"))
+    from make_golden_fullsize import highs_standard_form
+    qp, _ = bench.build_problem("ex10@0.05")
+    assert not qp.minimize
+    pardiso.set_threads(1)
+    o = OracleMPC(qp, OracleOptions(regularization=("fixed", 1e-8, -1e-8), step_rule=("adaptive", 0.99),
+                                    max_iter=300, tol=1e-8), record_trace=False)
+    o.linear_solver = "pardiso"
+    st = o.solve()
+    assert st.status == SOLVE_SUCCEEDED
+    p = kkt_properties(qp, st)
+    assert p["pr"] <= 1e-6 and p["du"] <= 1e-6, p
+    assert abs(p["pobj"] - p["dobj"]) <= 1e-6 * max(1.0, abs(p["pobj"])), p
+    assert abs(p["pobj"] - st.objective) <= 1e-9 * max(1.0, abs(p["pobj"]))
+    h = highs_standard_form(qp)
+    assert abs(st.objective - h["objective"]) <= 1e-6 * max(1.0, abs(h["objective"])), (st.objective, h)
+
+
+def test_fullsize_highs_fixture_present():
+    """tests/golden/fullsize_highs.json (tools/make_golden_fullsize.py) pins the full-size stand-ins'
+    optima for the GPU tests (tests/test_fullsize_gpu.py)."""
+    with open(os.path.join(os.path.dirname(__file__), "golden", "fullsize_highs.json")) as f:
+        g = json.load(f)
+    for c in ("ex10", "supportcase10", "neos"):
+        assert g[c]["status"] == 0 and not g[c]["minimize"] and np.isfinite(g[c]["objective"]), g[c]
