@@ -253,6 +253,52 @@ def collective_volume(info, warm, world=None):
     return out
 
 
+def timed_leg(solver, steps, warmup, dist, sharded, barrier):
+    """One timed MPC run of a built solver: `warmup` untimed iterations, then EXACTLY `steps` iterations
+    after initialize!, bracketed by barriers (barrier() also synchronises the device); whole-job numbers
+    by `aggregate` (max time over ranks)."""
+    solver.set_kernel_timing()
+    solver.set_max_iter(max(warmup, 1))
+    solver.solve()
+    warm = solver.kernel_stats()
+    solver.set_kernel_timing(0)
+    solver.set_max_iter(steps)
+    solver.initialize()
+    barrier()
+    t0 = time.perf_counter()
+    st = solver.solve(fetch_solution=False)
+    barrier()
+    dt = time.perf_counter() - t0
+    dt, it, per_rank = aggregate(dt, st.iter, dist, sharded)
+    return {"iters_per_s": it / dt, "ms_per_iter": 1e3 * dt / max(st.iter, 1), "steps": steps, "warmup": warmup,
+            "per_rank_s": per_rank}, warm
+
+
+def neos_leg(args, comm, dist, sharded, barrier, world):
+    """BASELINE.json configs[4] — the config it assigns to the 8-GPU elimination-tree subtree split —
+    at every N: unsharded at N = 1, subtree-sharded over the N ranks (RCCL) at N > 1, so the driver's
+    SCALE run measures the sharded path where the tree actually shards (ex10's tree has one 120-row
+    top front).  Reported under the line's "neos" key; `value` stays on the ex10 workload."""
+    from madipm_amd import MPCSolver
+    qp, name = build_problem("neos")
+    t_an = time.perf_counter()
+    solver = MPCSolver(qp, comm=comm, **solver_opts())
+    t_analysis = time.perf_counter() - t_an
+    info = solver.ldl_info()
+    leg, warm = timed_leg(solver, args.neos_steps, 2, dist, sharded, barrier)
+    solver.set_max_iter(300)
+    t1 = time.perf_counter()
+    so = solver.solve()
+    e2e = time.perf_counter() - t1
+    leg.update({"workload": name, "parallelism": f"subtree-shard{world}" if sharded else f"replicas{world}",
+                "nnzL": info["nnzL"], "fact_flops": info["flops"], "analysis_s": t_analysis,
+                "status": so.status_name, "iters_to_opt": so.iter, "objective": so.objective,
+                "wall_clock_to_opt_s": so.counters.total_time, "end_to_end_s": t_analysis + e2e,
+                "collectives": collective_volume(info, warm, world)})
+    del solver
+    return leg
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -266,6 +312,9 @@ def main():
     ap.add_argument("--ordering", type=int, default=None, help="LDL ordering override (0 natural, 1 AMD, 3 ND, 4 auto)")
     ap.add_argument("--mode", choices=["shard", "replicas"], default="shard",
                     help="N > 1: one subtree-sharded solve (RCCL) or N independent replicas")
+    ap.add_argument("--neos", action=argparse.BooleanOptionalAction, default=True,
+                    help="also time configs[4] (neos stand-in; sharded over the ranks at N > 1) under the 'neos' key")
+    ap.add_argument("--neos-steps", type=int, default=8)
     args = ap.parse_args()
 
     import torch
@@ -336,7 +385,18 @@ def main():
         e2e = time.perf_counter() - t1
         opt = {"status": so.status_name, "iters_to_opt": so.iter, "wall_clock_to_opt_s": so.counters.total_time,
                "init_plus_loop_s": e2e, "analysis_s": t_analysis, "objective": so.objective,
-               "linear_solver_time_s": so.counters.linear_solver_time}
+               "linear_solver_time_s": so.counters.linear_solver_time,
+               # end-to-end = symbolic analysis + initialisation + loop to optimality
+               "end_to_end_s": t_analysis + e2e}
+
+    kperm = solver.kkt_perm() if rank == 0 else None
+    neos = None
+    if args.neos and not args.config.startswith("neos"):
+        del solver
+        try:
+            neos = neos_leg(args, comm, dist, sharded, barrier, world)
+        except Exception as e:  # pragma: no cover - reported, not hidden
+            neos = {"error": repr(e)}
 
     if rank == 0:
         out = {
@@ -364,12 +424,13 @@ def main():
             "per_rank_s": per_rank,
             "loop_total_time_s": st.counters.total_time,  # the library's own clock around the K iterations (rank 0)
             "collectives": collective_volume(info, warm, world),
+            "neos": neos,
             "cpu_baseline": None,
             "parity": None,
         }
         if not args.no_cpu and world == 1 and not args.config.startswith(("dense_qp", "neos")):
             try:
-                (r_status, r_obj, r_iter), out["cpu_baseline"] = cpu_baseline(args.config, solver.kkt_perm(),
+                (r_status, r_obj, r_iter), out["cpu_baseline"] = cpu_baseline(args.config, kperm,
                                                                                baseline_threads())
                 if opt:
                     # parity at the benchmarked size: the GPU solve to optimality vs the oracle's (same

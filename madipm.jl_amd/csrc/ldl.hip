@@ -126,8 +126,6 @@ __device__ __forceinline__ void stage_panel(const double* __restrict__ L, double
   }
 }
 
-__global__ void k_status_end(LDLStatus* st) { ldl_status_end(st); }
-
 __global__ void k_status_init(LDLStatus* st, int all = 0) {
   const uint64_t now = wall_clock64();
   if (all) {
@@ -878,7 +876,7 @@ __device__ __forceinline__ bool poll_flag(int32_t* f, int epoch, int32_t* err) {
   while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
     __builtin_amdgcn_s_sleep(1);
     if (++spins > (1 << 25)) {
-      atomicExch(err, 1);
+      atomicOr(err, kErrHandoff);
       return false;
     }
   }
@@ -897,7 +895,7 @@ __device__ __forceinline__ void poll_deps(const int32_t* __restrict__ dep, int q
       if (__all(ok)) break;
       __builtin_amdgcn_s_sleep(1);
       if (++spins > (1 << 25)) {
-        if (lane == 0) atomicExch(err, 1);
+        if (lane == 0) atomicOr(err, kErrHandoff);
         break;
       }
     }
@@ -1342,7 +1340,7 @@ __device__ __forceinline__ void blocked_factor_pipe(double* A, int r, int w, int
   // a lost hand-off (a wait that timed out) leaves a wrong factor: raise the sticky status error that
   // status() turns into a failure (the flag polls between fronts do the same)
   if (tid == 0 && __hip_atomic_load(&pc.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) && err)
-    __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_or(err, kErrHandoff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int64_t t2 = (pt && tid == 0) ? wall_clock64() : 0;
   if (defer && schur) {
     schur_strips<PK>(A, r, ld, w, Dl, wv, nw, lane);
@@ -1606,6 +1604,10 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
   int32_t* kk = pwrc + LM;                                   // per batch row: batch-local leaf
   const int tid = threadIdx.x;
   const int b0 = T.fold_bptr[s], nb = T.fold_bptr[s + 1] - b0;
+  if (nb > SymbolicPlan::kFoldMaxBatches) {  // the batch table below has room for kFoldMaxBatches
+    if (tid == 0) __hip_atomic_fetch_or(T.err, kErrLdsCarve, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
   // the batch table (first leaf, first row, product offset and length), loaded once into LDS: read
   // from global per batch it cost two dependent round trips at each batch's gather and products
   FoldBatchTab& ft = fold_batch_tab();
@@ -1665,6 +1667,10 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
     const int k0 = tb_k[b], k1 = tb_k[b + 1];
     const int64_t j0 = tb_j[b];
     const int nrow = (int)(tb_j[b + 1] - j0), nleaf = k1 - k0;
+    if (nrow > RM || nleaf > LM || nleaf > 2 * FTN) {  // a batch beyond the carve the front was sized by
+      if (tid == 0) __hip_atomic_fetch_or(T.err, kErrLdsCarve, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;  // (uniform: the batch table is in LDS)
+    }
     // (1) the leaf rows' K entries (the first pass in registers already; leaf tables loaded beside them)
     int32_t lf[2], lw[2];
     int64_t lo[2];
@@ -1872,6 +1878,21 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
   const int tid = threadIdx.x;
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
   const int ld = PK ? 0 : (r | 1);
+  {  // the front and its leaf batches must fit the launch's LDS: else a sticky error, never a write
+     // past the carve (the symbolic analysis sizes both; this catches a plan that breaks it)
+    const int ntot = PK ? r * (r + 1) / 2 : r * ld;
+    const int64_t need = 8 * (int64_t)((ntot + 1) & ~1) +
+                         (T.absorb[s] ? (int64_t)SymbolicPlan::kFoldRowBytes * T.fold_rmax[s] +
+                                            (int64_t)SymbolicPlan::kFoldLeafBytes * T.fold_lmax[s]
+                                      : 0);
+    if (need > T.lds_cap) {
+      if (tid == 0) {
+        __hip_atomic_fetch_or(T.err, kErrLdsCarve, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&flags[s], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);  // release the parent
+      }
+      return;
+    }
+  }
   if (T.absorb[s]) {  // original entries, then the micro-leaf children folded in LDS
     const int ntot = PK ? r * (r + 1) / 2 : r * ld;
     for (int q = tid; q < ntot; q += FTN) A[q] = 0.0;
@@ -3089,7 +3110,7 @@ __device__ __forceinline__ bool wait_flag(int32_t* f, int epoch, int32_t* err) {
   while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
     __builtin_amdgcn_s_sleep(1);
     if (++spins > (1 << 25)) {
-      atomicExch(err, 1);
+      atomicOr(err, kErrHandoff);
       return false;
     }
   }
@@ -4474,6 +4495,10 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         fprintf(stderr, "tree level %d: %4.0f fronts  r avg %.0f max %.0f  w avg %.1f  LDS avg %.0f max %.0f KB  leaves avg %.0f\n", l,
                 a[0], a[1] / a[0], a[2], a[3] / a[0], a[4] / a[0] / 1024, a[5] / 1024, a[6] / a[0]);
     }
+    // the device-side carve check compares against this (MADIPM_DEBUG_LDS_SHRINK=<bytes>, tests only:
+    // pretend the launch has that much less, so the check fires)
+    T_.lds_cap = ftree_lds_;
+    if (const char* e = std::getenv("MADIPM_DEBUG_LDS_SHRINK")) T_.lds_cap -= std::atoi(e);
     auto up = [](DBuf<int32_t>& d, const std::vector<int32_t>& v) { d.upload(v.empty() ? std::vector<int32_t>{0} : v); };
     up(ft_order_, ord);
     up(ft_dptr_, dptr);
@@ -4728,20 +4753,6 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     if (phase == 1 && NL == 1 && nftree_) ftree_launch();
   };
   build_fact(1, fact1_);
-  {  // tail overlap (opt-in, MADIPM_TAIL_OVERLAP=1, until measured on the GPU): the launches after the tree kernel
-    const char* et = std::getenv("MADIPM_TAIL_OVERLAP");
-    size_t cut = fact1_.size();
-    for (size_t k = 0; k < fact1_.size(); ++k)
-      if (fact1_[k].kind == FTREE) cut = k + 1;
-    tail_ok_ = et && et[0] == '1' && S.nshards == 1 && nftree_ > 0 && cut < fact1_.size();
-    if (tail_ok_) {
-      fact1_head_.assign(fact1_.begin(), fact1_.begin() + cut);
-      fact1_tail_.assign(fact1_.begin() + cut, fact1_.end());
-      MADIPM_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
-      MADIPM_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
-      MADIPM_HIP(hipEventCreateWithFlags(&ev_tail_, hipEventDisableTiming));
-    }
-  }
   if (S.nshards > 1) {
     asm_launch(NL, fact1_);  // top fronts, external part (all-reduced next)
     for (size_t g = 0; g < S.lb.size(); ++g)  // this shard's batched leaves under top fronts: into it
@@ -4875,19 +4886,6 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q)
           if (in_tree[S.level_list[q]]) (big_root(S.level_list[q]) ? roots : ord).push_back(S.level_list[q]);
       nroot_task_ = (int)roots.size();
-      if (tail_ok_) {  // tail overlap: fronts factorised after the tree kernel (above level 0, outside
-                       // k_fact_tree, or absorbed by such a front) must not be solved by k_fwd_tree before the join
-        std::vector<int> lvl(std::max(ns, 1), 0);
-        for (int lev = 0; lev < NL; ++lev)
-          for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q) lvl[S.level_list[q]] = lev;
-        auto head = [&](int f) {
-          const int p = S.parent[f];
-          const bool absorbed = p >= 0 && S.absorb[p];
-          if (S.ftree[f]) return !(absorbed && !S.ftree[p]);
-          return lvl[f] == 0 && !absorbed;
-        };
-        for (int f : ord) tree_join_early_ = tree_join_early_ || !head(f);
-      }
       ord.insert(ord.end(), roots.begin(), roots.end());
       ntree_ = (int)ord.size();
       // children of tree fronts scatter their forward update entries straight into the parent's
@@ -5055,9 +5053,6 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
 
 LDLSolver::~LDLSolver() {
   if (h_status_) (void)hipHostFree(h_status_);
-  if (ev_fork_) (void)hipEventDestroy(ev_fork_);
-  if (ev_tail_) (void)hipEventDestroy(ev_tail_);
-  if (side_) (void)hipStreamDestroy(side_);
   for (hipEvent_t e : evs_) (void)hipEventDestroy(e);
 }
 
@@ -5266,24 +5261,7 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
 // assembly and the shard's status slot.
 void LDLSolver::fact_phase1(const double* Kx, hipStream_t s) {
   if (S_.N == 0) return;
-  join(s);  // the previous factorisation's tail (normally joined by its solve already)
   if (!(ext_reset && ext_status_ && !sharded())) k_status_init<<<1, 1, 0, s>>>(st_);
-  if (tail_active()) {
-    // the launches after the tree kernel (the fronts above the tree: ex10's root assembly and root
-    // factor) on the side stream, beside the driver's next kernels and the next solve's leaves and
-    // forward tree, which need only the tree's factor; the solve joins before k_root_solve / the
-    // level solves above the tree, status() and the next factorisation join too
-    run_fact(fact1_head_, Kx, s);
-    MADIPM_HIP(hipEventRecord(ev_fork_, s));
-    MADIPM_HIP(hipStreamWaitEvent(side_, ev_fork_, 0));
-    run_fact(fact1_tail_, Kx, side_);
-    k_status_end<<<1, 1, 0, side_>>>(st_);
-    MADIPM_HIP(hipEventRecord(ev_tail_, side_));
-    MADIPM_HIP(hipGetLastError());
-    tail_pending_ = true;
-    inertia_stale_ = true;
-    return;
-  }
   run_fact(fact1_, Kx, s);
   const int nb = (int)std::min<int64_t>(64, cdiv(S_.N, NT));
   const int spdf = spd ? 1 : 0;
@@ -5340,7 +5318,6 @@ bool LDLSolver::external_status(LDLStatus* dev, LDLStatus* host) {
 
 double LDLSolver::fact_seconds(hipStream_t s) {
   if (S_.N == 0) return 0.0;
-  join(s);
   LDLStatus h;
   MADIPM_HIP(hipMemcpyAsync(&h, st_, sizeof(LDLStatus), hipMemcpyDeviceToHost, s));
   MADIPM_HIP(hipStreamSynchronize(s));
@@ -5355,7 +5332,6 @@ double LDLSolver::fact_seconds(hipStream_t s) {
 void LDLSolver::count_inertia(hipStream_t s) {
   if (!inertia_stale_ || S_.N == 0) return;
   inertia_stale_ = false;
-  join(s);
   const int nb = (int)std::min<int64_t>(64, cdiv(S_.N, NT));
   k_zero_counts<<<1, 1, 0, s>>>(st_);
   k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, st_, 0, nullptr, 1);
@@ -5363,24 +5339,20 @@ void LDLSolver::count_inertia(hipStream_t s) {
   status(s, true);
 }
 
-void LDLSolver::join(hipStream_t s) {
-  if (!tail_pending_) return;
-  MADIPM_HIP(hipStreamWaitEvent(s, ev_tail_, 0));
-  tail_pending_ = false;
-}
-
 int LDLSolver::status(hipStream_t s, bool sync) {
   if (S_.N == 0) {
     factorized = true;
     return 0;
   }
-  if (sync) join(s);
   if (sync && ext_status_) MADIPM_HIP(hipMemcpyAsync(h_st_, st_, sizeof(LDLStatus), hipMemcpyDeviceToHost, s));
   if (sync) MADIPM_HIP(hipStreamSynchronize(s));
-  if (h_st_->err) {  // a lost hand-off gives a wrong factor or solve: never report it as success
+  if (h_st_->err) {  // a lost hand-off or a carve overflow gives a wrong factor or solve: never success
+    const int e = h_st_->err;
     h_st_->err = 0;
     k_status_init<<<1, 1, 0, s>>>(st_, 1);
     MADIPM_HIP(hipStreamSynchronize(s));
+    if (e & kErrLdsCarve)
+      throw Error("LDL^T: a front or folded-leaf batch exceeded k_fact_tree's LDS carve (factor is invalid)", -5);
     throw Error("LDL^T: a dependency hand-off between fronts timed out (factor or solve is invalid)", -5);
   }
   npos = h_st_->npos;
@@ -5488,7 +5460,6 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
   if (phase == 0 && !S_.lb.empty()) lb_fwd(b, s);
   for (int lev = 0; lev < (int)V.size(); ++lev) {
     const SolveLevel& L = V[lev];
-    if (lev > 0) join(s);  // no-op after the tree's join
     if (L.nmicro)
       TIMED(KK_FWD_TINY, L.micro_bytes, L.micro_alg, L.micro_flops,
             (k_fwd_micro<<<(unsigned)cdiv(L.nmicro, NT / MG), NT, 0, s>>>(T_, sched_.p + L.micro_off, L.nmicro, arena_, b,
@@ -5515,14 +5486,12 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
     if (lev == 0 && phase == 0 && ntree_)
     {
       const int nlo = ntask_ - nroot_task_;  // the big roots last, in their own launch (more LDS)
-      if (tree_join_early_) join(s);
       if (nlo > 0)
         TIMED(KK_FWD_TREE, tree_bytes_, tree_alg_, tree_flops_,
               (k_fwd_tree<<<(unsigned)nlo, NT, tree_lds_, s>>>(T_, tc_ptr_, tc_list_, nlo, tdep_ptr_, tdep_,
                                                               counters_.p + 4 * S_.nlevels, tflags_, efwd, tree_lds_ / 8,
                                                               arena_, b, xi_, uvec_, &st_->err, tdbg_.p, trootbwd_, D_,
                                                               tchunk_)));
-      join(s);  // the factorisation's tail (the fronts above the tree) ran beside the launches above
       if (nroot_task_)
         TIMED(KK_FWD_TREE, nlo > 0 ? 0.0 : tree_bytes_, nlo > 0 ? 0.0 : tree_alg_, nlo > 0 ? 0.0 : tree_flops_,
               (k_root_solve<<<(unsigned)nroot_task_, RSN, root_lds_, s>>>(T_, tc_list_.p + nlo, arena_, b, xi_, D_, tflags_,

@@ -71,7 +71,12 @@ struct FrontTab {
   int32_t* err;     // the status block's sticky error (LDLStatus::err): a timed-out hand-off inside a front
   int fpipe;        // pipelined in-LDS schedule (blocked_factor_pipe; MADIPM_FACT_PIPE=0: blocked_factor_lds)
   int pipe_fault;   // tests (MADIPM_DEBUG_PIPE_FAULT=1): blocked_factor_pipe drops one hand-off
+  int lds_cap;      // k_fact_tree's dynamic LDS (bytes): a front (+ its leaf batches) beyond it is an error
 };
+
+// LDLStatus::err bits (sticky; status() raises on any)
+constexpr int32_t kErrHandoff = 1;   // a dependency hand-off (flag poll) timed out
+constexpr int32_t kErrLdsCarve = 2;  // a k_fact_tree front or leaf batch did not fit its LDS carve
 
 // assembly: a big child's block on one 64x64 tile of its parent (SymbolicPlan::bt entry): the tile's
 // row and column maps (tile row -> the child's update row, -1 outside the child) and the child's U
@@ -183,13 +188,6 @@ class LinSolver {
   //     ldl_status_end); the pivot check does not need it unless spd, and inertia() counts on demand
   bool ext_reset = false, lazy_inertia = false;
   virtual void count_inertia(hipStream_t s) { (void)s; }
-  // tail overlap (LDLSolver): the factorisation's launches after the tree kernel run on a side
-  // stream beside the next solve's forward tree; join(s) orders s after them (status, the next
-  // factorisation and the driver's status reset and state read-back do it; once per factorisation,
-  // the driver uses one stream), and the factorisation then stamps its own end (the driver's next
-  // kernel must not: stamps_end())
-  virtual void join(hipStream_t s) { (void)s; }
-  virtual bool stamps_end() const { return false; }
 };
 
 class LDLSolver : public LinSolver {
@@ -217,8 +215,6 @@ class LDLSolver : public LinSolver {
   //              solve_phase3
   void fact_phase1(const double* Kx, hipStream_t s);
   void count_inertia(hipStream_t s) override;  // lazy_inertia: the counts of the current factor
-  void join(hipStream_t s) override;
-  bool stamps_end() const override { return tail_active(); }
   void fact_phase2(hipStream_t s);
   void solve_phase1(double* b, hipStream_t s);
   void solve_phase2(double* b, hipStream_t s);
@@ -294,13 +290,6 @@ class LDLSolver : public LinSolver {
   FrontTab T_{};
   Comm* comm_ = nullptr;
   std::vector<Launch> fact1_, fact2_;      // phase 1 (this shard's subtrees; everything unsharded), phase 2 (top)
-  // tail overlap: fact1_ split after the tree kernel (head on the caller's stream, tail on side_)
-  std::vector<Launch> fact1_head_, fact1_tail_;
-  bool tail_ok_ = false, tail_pending_ = false;  // pending: not yet joined into the caller's stream
-  bool tree_join_early_ = false;  // a k_fwd_tree task's front is factorised by the tail: join before it
-  hipStream_t side_ = nullptr;
-  hipEvent_t ev_fork_ = nullptr, ev_tail_ = nullptr;
-  bool tail_active() const { return tail_ok_ && ext_status_ && lazy_inertia && !spd; }
   std::vector<SolveLevel> slev1_, slev2_;  // per level, leaves first
   int64_t xg_off_ = 0;                     // (top front, 256-row chunk) pairs of the external forward gather
   int nxg_ = 0;

@@ -2005,17 +2005,11 @@ const double* MPCSolver::kvals() const { return kkt_ == KKT_NORMAL ? Cx_.p : Kx_
 // the pool grows only when a solve needs more pairs than any earlier one did
 void MPCSolver::timed_factorize() {
   ldl_->factorize_async(kvals(), stream_);
-  // the next k_rhs stamps the factorisation's end (unless the factorisation's own tail does)
-  fact_end_pending_ = ldl_->lazy_inertia && !ldl_->stamps_end();
+  fact_end_pending_ = ldl_->lazy_inertia;  // the next k_rhs stamps the factorisation's end
 }
 
-// the status block the kernel right before a factorisation resets (LinSolver::ext_reset), or nullptr;
-// the previous factorisation's tail (LinSolver::join) is ordered before that kernel
-LDLStatus* MPCSolver::fact_reset() {
-  if (!ldl_->ext_reset) return nullptr;
-  ldl_->join(stream_);
-  return &st_.p->ldl_status;
-}
+// the status block the kernel right before a factorisation resets (LinSolver::ext_reset), or nullptr
+LDLStatus* MPCSolver::fact_reset() const { return ldl_->ext_reset ? &st_.p->ldl_status : nullptr; }
 // the status block the first kernel after a factorisation stamps (LinSolver::lazy_inertia), or nullptr
 LDLStatus* MPCSolver::take_fact_end() {
   LDLStatus* p = fact_end_pending_ ? &st_.p->ldl_status : nullptr;
@@ -2078,14 +2072,11 @@ void MPCSolver::solve_system(int mode, double mu, int reset, int amode, double a
   const int nb = blocks(n_ + m_), nbs = spmv_blocks(n_ + m_);
   DevState* host = nullptr;
   uint32_t seq = 0;
-  // read_state() folded into this launch, or, when the factorisation's tail runs beside the solve
-  // (LinSolver::stamps_end), into the residual's finaliser after it (the status is complete there)
-  const bool pub_late = publish_next_ && ldl_->stamps_end();
-  if (publish_next_ && !pub_late) {
+  if (publish_next_) {  // read_state() folded into this launch
     host = hst_;
     seq = ++pub_seq_;
+    publish_next_ = false;
   }
-  publish_next_ = false;
   MuFold mf{0, 0.0, 0.0, 0.0};
   if (mu_nb > 0) mf = MuFold{mu_nb, (double)(nlb_ + nub_), H_->has_ineq ? 1.0 : 0.0, opt_.mu_min};
   k_rhs<<<nb, NT, 0, stream_>>>(D, mode, mu, reset, host, hseq_, seq, mf, take_fact_end());
@@ -2094,7 +2085,7 @@ void MPCSolver::solve_system(int mode, double mu, int reset, int amode, double a
   // blocks) and is finalised with the residual
   const int nbz = amode >= 0 ? blocks(std::max(nlb_, nub_)) : 0;
   SPMV_LAUNCH(k_residual, nbs + nbz, stream_, D, del_w_, del_c_, nbs, amode, atau);
-  launch_reduce_final(FIN_RESID, nbs, amode, 0, nullptr, pub_late);
+  launch_reduce_final(FIN_RESID, nbs, amode);
 }
 
 // gondzio_correction_direction! (solver.jl:245-298): host-controlled loop, one read-back per solve
@@ -2137,7 +2128,6 @@ void MPCSolver::gondzio() {
 }
 
 void MPCSolver::read_state() {
-  ldl_->join(stream_);  // the published LDL status includes the factorisation's tail
   k_publish<<<1, 64, 0, stream_>>>(st_, hst_, hseq_, ++pub_seq_);
   MADIPM_HIP(hipGetLastError());
 }

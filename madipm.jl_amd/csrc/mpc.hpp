@@ -81,7 +81,7 @@ class MPCSolver {
   void kkt_solve();
   void factor_enqueue(double dw, double dc);
   void timed_factorize();
-  LDLStatus* fact_reset();
+  LDLStatus* fact_reset() const;
   LDLStatus* take_fact_end();
   int blocks(int64_t n) const;
   int spmv_blocks(int64_t rows) const;

@@ -50,7 +50,7 @@ struct Rng {
 };
 
 // Heavy-edge matching and contraction.  Returns false when the graph hardly shrinks.
-bool coarsen(const Graph& g, Graph& c, std::vector<int32_t>& cmap, Rng& rng) {
+bool coarsen(const Graph& g, Graph& c, std::vector<int32_t>& cmap, Rng& rng, int threads) {
   const int n = g.n;
   std::vector<int32_t> match(n, -1), order(n);
   std::iota(order.begin(), order.end(), 0);
@@ -82,36 +82,60 @@ bool coarsen(const Graph& g, Graph& c, std::vector<int32_t>& cmap, Rng& rng) {
   c.n = nc;
   c.vw.assign(nc, 0);
   c.p.assign(nc + 1, 0);
-  c.adj.clear();
-  c.ew.clear();
-  std::vector<int32_t> pos(nc, -1), members(2);
   std::vector<int32_t> rep(nc, -1);
   for (int v = 0; v < n; ++v)
     if (rep[cmap[v]] == -1) rep[cmap[v]] = v;
-  for (int cv = 0; cv < nc; ++cv) {
-    const int v = rep[cv];
-    const int u = match[v];
-    const int nm = (u == v) ? 1 : 2;
-    members[0] = v;
-    members[1] = u;
-    const int64_t start = (int64_t)c.adj.size();
-    for (int k = 0; k < nm; ++k) {
-      const int x = members[k];
-      c.vw[cv] += g.vw[x];
-      for (int64_t e = g.p[x]; e < g.p[x + 1]; ++e) {
-        const int cu = cmap[g.adj[e]];
-        if (cu == cv) continue;
-        if (pos[cu] >= start && pos[cu] < (int64_t)c.adj.size() && c.adj[pos[cu]] == cu) {
-          c.ew[pos[cu]] += g.ew[e];
-        } else {
-          pos[cu] = (int32_t)c.adj.size();
-          c.adj.push_back(cu);
-          c.ew.push_back(g.ew[e]);
+  // contraction of coarse vertices [cv0, cv1) into (adj, ew), c.p[cv + 1] = its degree; a coarse
+  // vertex's list is its members' neighbours in adjacency order, duplicates merged — the same lists
+  // whether one thread builds them all or each of `threads` builds a range (then concatenated)
+  auto contract = [&](int cv0, int cv1, std::vector<int32_t>& adj, std::vector<int32_t>& ew) {
+    std::vector<int32_t> pos(nc, -1);
+    for (int cv = cv0; cv < cv1; ++cv) {
+      const int v = rep[cv];
+      const int u = match[v];
+      const int members[2] = {v, u};
+      const int64_t start = (int64_t)adj.size();
+      for (int k = 0; k < (u == v ? 1 : 2); ++k) {
+        const int x = members[k];
+        c.vw[cv] += g.vw[x];
+        for (int64_t e = g.p[x]; e < g.p[x + 1]; ++e) {
+          const int cu = cmap[g.adj[e]];
+          if (cu == cv) continue;
+          if (pos[cu] >= start && pos[cu] < (int64_t)adj.size() && adj[pos[cu]] == cu) {
+            ew[pos[cu]] += g.ew[e];
+          } else {
+            pos[cu] = (int32_t)adj.size();
+            adj.push_back(cu);
+            ew.push_back(g.ew[e]);
+          }
         }
       }
+      c.p[cv + 1] = (int64_t)adj.size() - start;
     }
-    c.p[cv + 1] = (int64_t)c.adj.size();
+  };
+  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(threads, (int64_t)g.adj.size() / 500000));
+  c.adj.clear();
+  c.ew.clear();
+  if (T <= 1) {
+    c.adj.reserve(g.adj.size());
+    c.ew.reserve(g.adj.size());
+    contract(0, nc, c.adj, c.ew);
+  } else {
+    std::vector<std::vector<int32_t>> ta(T), te(T);
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t] { contract((int)((int64_t)nc * t / T), (int)((int64_t)nc * (t + 1) / T), ta[t], te[t]); });
+    for (auto& x : th) x.join();
+    size_t tot = 0;
+    for (int t = 0; t < T; ++t) tot += ta[t].size();
+    c.adj.reserve(tot);
+    c.ew.reserve(tot);
+    for (int t = 0; t < T; ++t) {
+      c.adj.insert(c.adj.end(), ta[t].begin(), ta[t].end());
+      c.ew.insert(c.ew.end(), te[t].begin(), te[t].end());
+    }
   }
+  for (int cv = 0; cv < nc; ++cv) c.p[cv + 1] += c.p[cv];
   return true;
 }
 
@@ -221,14 +245,14 @@ void refine(const Graph& g, std::vector<uint8_t>& part, double imbalance) {
 }
 
 // Multilevel bisection of a connected graph; returns the partition of the finest graph.
-void bisect(const Graph& g0, std::vector<uint8_t>& part, Rng& rng) {
+void bisect(const Graph& g0, std::vector<uint8_t>& part, Rng& rng, int threads) {
   std::vector<Graph> levels;
   std::vector<std::vector<int32_t>> maps;
   levels.push_back(g0);
   while (levels.back().n > 120) {
     Graph c;
     std::vector<int32_t> cmap;
-    if (!coarsen(levels.back(), c, cmap, rng)) break;
+    if (!coarsen(levels.back(), c, cmap, rng, threads)) break;
     levels.push_back(std::move(c));
     maps.push_back(std::move(cmap));
   }
@@ -493,7 +517,7 @@ struct Dissector {
     std::vector<std::vector<uint8_t>> parts(tries), seps(tries);
     auto one_try = [&](int t) {
       Rng rng(child_seed(seed, 1000 + (uint64_t)t));
-      bisect(g, parts[t], rng);
+      bisect(g, parts[t], rng, tries > 1 ? std::max(1, par / tries) : par);
       vertex_separator(g, parts[t], seps[t]);
     };
     auto sizes = [&](int t, int64_t& ns, int64_t& na, int64_t& nb) {

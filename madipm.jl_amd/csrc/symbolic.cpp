@@ -532,6 +532,9 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       nopt.dense_alpha = opt.dense_alpha;
       nopt.threads = per;
       nopt.seed = 12345 + (uint64_t)k;
+      // with several seeds, one bisection per subgraph: the seeds are the tries (neos: the same best
+      // order with 1, 2 or 3 tries per seed, a third of the top-level work)
+      if (nseeds > 1) nopt.tries = 1;
       std::vector<int32_t> pn;
       nd_order(N, Ap, Ai, pn, nopt);
       analyse_order(N, colptr, rowval, std::move(pn), B[k]);

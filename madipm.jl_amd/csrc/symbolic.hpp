@@ -38,9 +38,10 @@ struct SymbolicOptions {
   // cost-based amalgamation of HBM-sized fronts (child rows > big_merge_rows): a child merges into
   // its parent when the update block it would write and its parent read back (16 B per entry) costs
   // more than the merge's extra trailing-update flops / big_merge (flops per byte, the f64 MFMA / HBM
-  // ratio) plus the explicit zeros' traffic.  0 disables (env MADIPM_BIG_MERGE overrides; off by
-  // default until measured on the GPU, 6 is the modelled ratio).
-  double big_merge = 0.0;
+  // ratio) plus the explicit zeros' traffic.  0 disables (env MADIPM_BIG_MERGE overrides).  Measured
+  // (r5, profiles/r5_a_*): neos 31.5 -> 35.9 iters/s with 6; ex10 / supportcase10 have no front above
+  // big_merge_rows and are unchanged.
+  double big_merge = 6.0;
   int big_merge_rows = 256;
   int small_front_max = 128; // fronts with r <= this are factorised in LDS by one workgroup (max 192)
   int gather_max = 128;      // children with update blocks of more rows are added block-wise (bt), not gathered

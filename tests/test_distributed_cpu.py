@@ -60,3 +60,58 @@ def test_collective_volume():
     assert v["fact_bytes"] == 8000 and v["solve_bytes"] == 6400 and v["bytes_per_iter"] == 8 * (1000 + 3 * 800)
     # ring model, P = 2: all-reduce m -> m doubles sent per rank, all-gather G -> G / 2
     assert v["wire_bytes_per_rank_per_iter"] == pytest.approx(8 * (1000 + 3 * (300 + 250)))
+
+
+class _FakeSolver:
+    """Stands in for MPCSolver in bench.timed_leg (host logic only): rank r's loop takes 0.05 (r + 1) s."""
+
+    def __init__(self, rank):
+        self.rank, self.k = rank, 0
+
+    def set_kernel_timing(self, mask=1):
+        pass
+
+    def kernel_stats(self):
+        return [{"name": "k_fact_tree", "launches": 2}, {"name": "k_bwd_tree", "launches": 4}]
+
+    def set_max_iter(self, k):
+        self.k = k
+
+    def initialize(self):
+        pass
+
+    def solve(self, fetch_solution=True):
+        import time
+        import types
+        time.sleep(0.05 * (self.rank + 1) if not fetch_solution else 0.0)
+        return types.SimpleNamespace(iter=self.k)
+
+
+def _leg_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    leg, warm = bench.timed_leg(_FakeSolver(rank), 6, 2, dist, True, dist.barrier)
+    q.put((rank, leg, [k["name"] for k in warm]))
+    dist.destroy_process_group()
+
+
+def test_two_rank_timed_leg():
+    """bench.timed_leg (the 'neos' key's sharded leg at N > 1): the time is the max over ranks, the
+    iterations are the one sharded solve's, every rank's own time is reported."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_leg_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    for rank, leg, warm in res:
+        assert warm == ["k_fact_tree", "k_bwd_tree"]
+        # (the closing barrier holds rank 0 until rank 1's slower loop is done: both see >= 0.1 s)
+        assert len(leg["per_rank_s"]) == 2 and min(leg["per_rank_s"]) >= 0.1
+        assert leg["steps"] == 6 and leg["iters_per_s"] == pytest.approx(6 / max(leg["per_rank_s"]))
+        assert leg["ms_per_iter"] == pytest.approx(1e3 * max(leg["per_rank_s"]) / 6)

@@ -165,6 +165,26 @@ def test_ldl_pipe_lost_handoff_is_an_error(monkeypatch):
     _factor_solve(K, Lw, 192)  # a fresh solver factorises normally
 
 
+@pytest.mark.parametrize("shrink", ["8", "1048576"])
+def test_ldl_fold_carve_overflow_is_an_error(shrink, monkeypatch):
+    """k_fact_tree checks on the device that every front and each of its folded-leaf batches fit the
+    launch's LDS carve (r4: a fold batch larger than its front's carve factorised silently wrong).
+    MADIPM_DEBUG_LDS_SHRINK pretends the launch has fewer bytes — by 8 (the largest front alone
+    overflows) or by 1 MB (every front) — so the check must fire: factorize() raises, never a silent
+    wrong factor, and a fresh solver factorises normally."""
+    from helpers import lp_k2
+    from madipm_amd import standard_form_qp
+    from madipm_amd.instances import ex10_standin
+    from madipm_amd.linear_solver import HIPLDLSolver
+    K, Lw = lp_k2(standard_form_qp(ex10_standin(scale=0.05)), 0, well=True)
+    monkeypatch.setenv("MADIPM_DEBUG_LDS_SHRINK", shrink)
+    ls = HIPLDLSolver(K.shape[0], Lw.indptr, Lw.indices)
+    with pytest.raises(Exception, match="LDS carve"):
+        ls.factorize(torch.from_numpy(Lw.data.copy()).cuda())
+    monkeypatch.delenv("MADIPM_DEBUG_LDS_SHRINK")
+    _check_case(K, Lw, well=True)
+
+
 @pytest.mark.parametrize("case", ["block_well", "block_ipm", "random"])
 def test_root_backward_in_forward(case):
     """An elimination-tree root (r == w) is solved backward by the forward tree kernel right after its
