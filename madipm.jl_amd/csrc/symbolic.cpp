@@ -1645,6 +1645,37 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     }
   }
   stamp("10a: fold product lists");
+  // the folded micro leaves never write an update block (their products go straight into the parent's
+  // LDS front): lay the arena out again without their (r - w)^2 blocks, so the leaves' L panels are
+  // contiguous in postorder (ex10: 138 MB of the arena were unused leaf blocks between 272-byte L
+  // panels — the leaf solves and the fold's L stores touched a cache line per panel piece)
+  if (!S.mc_list.empty()) {
+    std::vector<uint8_t> folded(ns, 0);
+    for (int c : S.mc_list) folded[c] = 1;
+    int64_t cur2 = 0;
+    for (size_t so = 0; so < storage_order.size(); ++so) {
+      const int s = storage_order[so];
+      if (so == ntop_begin) S.top_lo = cur2;
+      if (lb_member(s)) {
+        S.l_off[s] = S.u_off[s] = cur2;
+        continue;
+      }
+      const int64_t r = S.nrows[s], w = S.first[s + 1] - S.first[s];
+      S.l_off[s] = cur2;
+      if (!S.is_big[s]) {
+        S.u_off[s] = cur2 + r * w;
+        cur2 += r * w + (folded[s] ? 0 : (r - w) * (r - w));
+      } else {
+        S.u_off[s] = cur2 + w * r + w;
+        cur2 += r * r;
+      }
+      cur2 = (cur2 + 1) & ~(int64_t)1;
+    }
+    if (ntop_begin == storage_order.size()) S.top_lo = cur2;
+    S.top_hi = cur2;
+    if (S.nshards > 1) cur2 += 4 * S.nshards;
+    S.arena_size = cur2;
+  }
   S.fs_off.assign(ns, -1);
   S.fs_size = 0;
   for (int s = 0; s < ns; ++s)
