@@ -1037,15 +1037,17 @@ __device__ void fin_tail(const DV& D, int kind, const FinParams& P, const double
 // picks the instance).  Level-2 partials and the
 // ticket live past the NPART x MAXB partials (part_): L2 = part + NPART MAXB, NL2 x FG doubles, then the
 // ticket counter (reset by the last workgroup).
-template <int KIND, bool AL, bool EV>
-__global__ __launch_bounds__(FT) void k_final(DV D, int kind, FinParams P) {
+// NG == 1 (producers of at most FT1 blocks, MPCSolver::maxb_): ONE workgroup of FT1 threads reduces
+// every partial in one round trip — no level-2 partials, no ticket.
+template <int KIND, bool AL, bool EV, int NG = FG, int NTH = FT>
+__global__ __launch_bounds__(NTH) void k_final(DV D, int kind, FinParams P) {
   constexpr int NV = fin_nv(KIND);
   __shared__ double res[NL2];
   __shared__ int s_last;
   DevState* st = D.st;
   double* L2 = D.part + NPART * MAXB;
   int32_t* ticket = reinterpret_cast<int32_t*>(L2 + NL2 * FG);
-  const int g = blockIdx.x, b = g * FT + threadIdx.x;
+  const int g = blockIdx.x, b = g * NTH + threadIdx.x;
   if (P.dbg && threadIdx.x == 0 && g == 0) {
     P.dbg[0] = (int64_t)wall_clock64();
     P.dbg[3] = kind | (AL && NV > 0 ? 16 : 0) | (EV ? 32 : 0);
@@ -1095,8 +1097,8 @@ __global__ __launch_bounds__(FT) void k_final(DV D, int kind, FinParams P) {
   stage(std::integral_constant<int, 4>{});
   stage(std::integral_constant<int, 2>{});
   stage(std::integral_constant<int, 1>{});
-  __shared__ double shv[NL2][FT / 64];
-  __shared__ int shx[4][FT / 64];
+  __shared__ double shv[NL2][NTH / 64];
+  __shared__ int shx[4][NTH / 64];
   if (lane == 0) {
 #pragma unroll
     for (int k = 0; k < NV; ++k) shv[k][wv] = w1[k];
@@ -1109,6 +1111,29 @@ __global__ __launch_bounds__(FT) void k_final(DV D, int kind, FinParams P) {
     if (EV) shv[16][wv] = e1;
   }
   __syncthreads();
+  if constexpr (NG == 1) {  // the waves in order, straight into res[]
+    const int t = threadIdx.x;
+    if (t < NV) {
+      double a = shv[t][0];
+#pragma unroll
+      for (int w = 1; w < NTH / 64; ++w) a = comb(a, shv[t][w], fin_op(KIND, t));
+      res[t] = a;
+    } else if (AL && t >= 8 && t < 12) {
+      double a = shv[t][0];
+      int ix = shx[t - 8][0];
+#pragma unroll
+      for (int w = 1; w < NTH / 64; ++w) amin_upd(a, ix, shv[t][w], shx[t - 8][w]);
+      res[t] = a;
+      res[t + 4] = (double)ix;
+    } else if (EV && t == 16) {
+      double a = shv[16][0];
+#pragma unroll
+      for (int w = 1; w < NTH / 64; ++w) a += shv[16][w];
+      res[16] = a;
+    }
+    if (P.dbg && t == 0) P.dbg[5] = P.dbg[6] = (int64_t)wall_clock64();
+    __syncthreads();
+  } else {
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
@@ -1173,9 +1198,11 @@ __global__ __launch_bounds__(FT) void k_final(DV D, int kind, FinParams P) {
     res[16] = a;
   }
   __syncthreads();
+  }  // NG > 1
+  const int t = threadIdx.x;
   if (t >= 64) return;
   if (t == 0) {
-    *ticket = 0;  // every workgroup has taken its ticket: reset for the next launch
+    if (NG > 1) *ticket = 0;  // every workgroup has taken its ticket: reset for the next launch
     if (P.dbg) P.dbg[1] = (int64_t)wall_clock64();
     if (AL) {
       double a[4];
@@ -1206,30 +1233,41 @@ __global__ __launch_bounds__(FT) void k_final(DV D, int kind, FinParams P) {
 }
 
 // the k_final instance of a finaliser launch (slots, fused step test, fused objective)
+constexpr int FT1 = 1024;  // the single-workgroup finaliser's threads (one partial block each)
 void launch_final(const DV& D, int kind, const FinParams& P, hipStream_t s) {
+  // one workgroup when every producer launch had at most FT1 blocks (maxb_ <= FT1), else FG of them
+  const bool one = std::max(P.nb, std::max(P.nb_alpha, P.nb_eval)) <= FT1;
+#define LF(K, AL, EV)                                                 \
+  do {                                                                \
+    if (one)                                                          \
+      k_final<K, AL, EV, 1, FT1><<<1, FT1, 0, s>>>(D, kind, P);       \
+    else                                                              \
+      k_final<K, AL, EV><<<FG, FT, 0, s>>>(D, kind, P);               \
+  } while (0)
   switch (kind) {
-    case FIN_ALPHA: k_final<FIN_ALPHA, true, false><<<FG, FT, 0, s>>>(D, kind, P); break;
+    case FIN_ALPHA: LF(FIN_ALPHA, true, false); break;
     case FIN_RESID:
       if (P.nb_alpha > 0)
-        k_final<FIN_RESID, true, false><<<FG, FT, 0, s>>>(D, kind, P);
+        LF(FIN_RESID, true, false);
       else
-        k_final<FIN_RESID, false, false><<<FG, FT, 0, s>>>(D, kind, P);
+        LF(FIN_RESID, false, false);
       break;
-    case FIN_MU_PRED: k_final<FIN_MU_PRED, false, false><<<FG, FT, 0, s>>>(D, kind, P); break;
-    case FIN_MU_FULL: k_final<FIN_MU_FULL, false, false><<<FG, FT, 0, s>>>(D, kind, P); break;
-    case FIN_MU_GONDZIO: k_final<FIN_MU_GONDZIO, false, false><<<FG, FT, 0, s>>>(D, kind, P); break;
-    case FIN_ZINIT: k_final<FIN_ZINIT, false, false><<<FG, FT, 0, s>>>(D, kind, P); break;
-    case FIN_EVAL: k_final<FIN_EVAL, false, false><<<FG, FT, 0, s>>>(D, kind, P); break;
-    case FIN_ZSHIFT2: k_final<FIN_ZSHIFT2, false, false><<<FG, FT, 0, s>>>(D, kind, P); break;
+    case FIN_MU_PRED: LF(FIN_MU_PRED, false, false); break;
+    case FIN_MU_FULL: LF(FIN_MU_FULL, false, false); break;
+    case FIN_MU_GONDZIO: LF(FIN_MU_GONDZIO, false, false); break;
+    case FIN_ZINIT: LF(FIN_ZINIT, false, false); break;
+    case FIN_EVAL: LF(FIN_EVAL, false, false); break;
+    case FIN_ZSHIFT2: LF(FIN_ZSHIFT2, false, false); break;
     case FIN_TERM:
       if (P.nb_eval > 0)
-        k_final<FIN_TERM, false, true><<<FG, FT, 0, s>>>(D, kind, P);
+        LF(FIN_TERM, false, true);
       else
-        k_final<FIN_TERM, false, false><<<FG, FT, 0, s>>>(D, kind, P);
+        LF(FIN_TERM, false, false);
       break;
-    case FIN_ZSHIFT1: k_final<FIN_ZSHIFT1, false, false><<<FG, FT, 0, s>>>(D, kind, P); break;
+    case FIN_ZSHIFT1: LF(FIN_ZSHIFT1, false, false); break;
     default: throw Error("k_final: unknown finaliser kind", -2);
   }
+#undef LF
 }
 
 __global__ void k_publish(const DevState* __restrict__ st, DevState* host, uint32_t* hseq, uint32_t seq) {
@@ -1751,6 +1789,7 @@ void MPCSolver::setup_host(const madipm_qp& q) {
   nnzK_ = (int64_t)Kri.size();
   clk("K2 CSC");
   if (const char* e = std::getenv("MADIPM_SPEC_NEAR")) spec_near_ = std::max(0.0, std::atof(e));
+  if (const char* e = std::getenv("MADIPM_PART_BLOCKS")) maxb_ = std::max(64, std::min(MAXB, std::atoi(e)));
   if (const char* e = std::getenv("MADIPM_FINAL_DEBUG"); e && e[0] == '1') {
     fdbg_.alloc(8 * kFinDbg);
     MADIPM_HIP(hipMemset(fdbg_.p, 0, 8 * kFinDbg * sizeof(int64_t)));
