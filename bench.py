@@ -153,7 +153,7 @@ STATUS = {1: "SOLVE_SUCCEEDED", 2: "INFEASIBLE_PROBLEM_DETECTED", -1: "MAXIMUM_I
 PEAK_F64_TFS = 78.6
 
 
-def roofline(stats: list, dominant: str):
+def roofline(stats: list, dominant: str, config: str = "ex10"):
     """Roofline object for the dominant kernel from the live HIP-event statistics of the timed region.
     achieved = SURVEY 8(d)'s algorithmic bytes per launch (8 nnzL + 12 nnzK of the columns the launch
     factorises, exact column counts of the symbolic analysis; 8 nnzL of the columns a solve launch
@@ -177,7 +177,14 @@ def roofline(stats: list, dominant: str):
             return (-1, -1)
         return (int(m.group(1)), int(m.group(2)) if m.group(2) else sum(ord(ch) * 128 ** -k for k, ch in enumerate(m.group(3))))
 
-    pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), key=_rv)
+    # the newest PMC pass of THIS workload: files tagged r<round>_<letter>_<config>_pmc_traffic.json, or
+    # untagged ones (r<round>_<v>_pmc_traffic.json: ex10, the bench workload)
+    cfgs = ("ex10", "supportcase10", "neos", "dense_qp")
+    def _mine(path):
+        b = os.path.basename(path)
+        tagged = [c for c in cfgs if f"_{c}_pmc_traffic" in b]
+        return (config in tagged) if tagged else config == "ex10"
+    pmc = sorted((f for f in glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")) if _mine(f)), key=_rv)
     if pmc:  # PMC counters can not be read inside the timed run: the latest committed pass of this workload
         ent = json.load(open(pmc[-1]))["kernels"].get(dominant)
         if ent:
@@ -372,7 +379,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     iters = st.iter
-    roof = roofline(solver.kernel_stats(), dominant)
+    roof = roofline(solver.kernel_stats(), dominant, args.config.partition("@")[0])
     solver.set_kernel_timing(0)
     dt, total_iters, per_rank = aggregate(dt, iters, dist, sharded)
 

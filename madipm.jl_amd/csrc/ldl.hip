@@ -3205,11 +3205,18 @@ __global__ __launch_bounds__(NT) void k_fwd_big(FrontTab T, const SolveTask* __r
         if (g + 4 * e < kw) Ld[(g + 4 * e) * 65 + lane] = (lane < nrow) ? v[e] : 0.0;
     }
     double acc = 0.0;
-    for (int p = 0; p < np; ++p) {
-      double lv[16];
+    // the panel pieces are final (factorisation): panel p + 1's loads are issued before panel p's flag
+    // wait and x loads, so one L round trip per task is exposed instead of one per panel
+    double lv[16], ln[16];
+    auto load_panel = [&](double (&dst)[16], int p) {
       const int cb = p * 64 + g * 16;
 #pragma unroll
-      for (int cc = 0; cc < 16; ++cc) lv[cc] = L[rowc + (int64_t)min(cb + cc, w - 1) * r];
+      for (int cc = 0; cc < 16; ++cc) dst[cc] = L[rowc + (int64_t)min(cb + cc, w - 1) * r];
+    };
+    if (np > 0) load_panel(lv, 0);
+    for (int p = 0; p < np; ++p) {
+      if (p + 1 < np) load_panel(ln, p + 1);  // wave-uniform
+      const int cb = p * 64 + g * 16;
 #pragma unroll
       for (int cc = 0; cc < 16; ++cc) lv[cc] = (lane < nrow && cb + cc < w) ? lv[cc] : 0.0;
       if (tid == 0) wait_flag(&flags[flag_off[s] + p], epoch, err);
@@ -3222,6 +3229,8 @@ __global__ __launch_bounds__(NT) void k_fwd_big(FrontTab T, const SolveTask* __r
       __syncthreads();
 #pragma unroll
       for (int cc = 0; cc < 16; ++cc) acc += lv[cc] * xs[g * 16 + cc];
+#pragma unroll
+      for (int cc = 0; cc < 16; ++cc) lv[cc] = ln[cc];
       __syncthreads();
     }
     part[g][lane] = acc;
@@ -3264,21 +3273,29 @@ __global__ __launch_bounds__(NT) void k_bwd_below(FrontTab T, const int32_t* __r
   const int R0 = w + chunk * BWD_CHUNK, R1 = min(r, R0 + BWD_CHUNK);
   const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
   double acc = 0.0;
+  // unconditional loads from clamped addresses, masked at the LDS stores; the next row block's loads
+  // are issued before this block's products (one round trip exposed per task, not per block)
+  double v[16], vn[16], xv = 0.0, xvn = 0.0;
+  auto load_blk = [&](double (&dst)[16], double& x, int rb) {
+    const int nr = min(64, R1 - rb);
+    const int rc = rb + min(lane, nr - 1);
+#pragma unroll
+    for (int e = 0; e < 16; ++e) dst[e] = L[rc + (int64_t)(c0 + min(g + 4 * e, kw - 1)) * r];
+    x = (tid < 64) ? xi[rows[rb + min(tid, nr - 1)]] : 0.0;
+  };
+  if (R0 < R1) load_blk(v, xv, R0);
   for (int rb = R0; rb < R1; rb += 64) {
     const int nr = min(64, R1 - rb);
-    {  // unconditional loads from clamped addresses, masked at the LDS stores
-      double v[16];
-      const int rc = rb + min(lane, nr - 1);
 #pragma unroll
-      for (int e = 0; e < 16; ++e) v[e] = L[rc + (int64_t)(c0 + min(g + 4 * e, kw - 1)) * r];
-      const double xv = (tid < 64) ? xi[rows[rb + min(tid, nr - 1)]] : 0.0;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) tile[lane * 65 + g + 4 * e] = (lane < nr && g + 4 * e < kw) ? v[e] : 0.0;
-      if (tid < 64) xr[tid] = (tid < nr) ? xv : 0.0;
-    }
+    for (int e = 0; e < 16; ++e) tile[lane * 65 + g + 4 * e] = (lane < nr && g + 4 * e < kw) ? v[e] : 0.0;
+    if (tid < 64) xr[tid] = (tid < nr) ? xv : 0.0;
     __syncthreads();
+    if (rb + 64 < R1) load_blk(vn, xvn, rb + 64);  // block-uniform
 #pragma unroll
     for (int rr = 0; rr < 16; ++rr) acc += tile[(g * 16 + rr) * 65 + lane] * xr[g * 16 + rr];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) v[e] = vn[e];
+    xv = xvn;
     __syncthreads();
   }
   part[g][lane] = acc;
@@ -3323,18 +3340,25 @@ __global__ __launch_bounds__(NT) void k_bwd_big(FrontTab T, const SolveTask* __r
         if (g + 4 * e < kw) Ld[lane * 65 + g + 4 * e] = (lane < kw) ? v[e] : 0.0;
     }
     double acc = 0.0;  // partial for column c0+lane over this wave's rows of each tile
-    // pivot panels q = npan-1 .. p+1 (wait for each); the rows below come from k_bwd_below
-    for (int k = 0; k < npan - 1 - p; ++k) {
+    // pivot panels q = npan-1 .. p+1 (wait for each); the rows below come from k_bwd_below.  A tile's
+    // L values are final: they are loaded before the wait for its x (the next tile's during this
+    // tile's products), only the x values wait for the flag
+    const int nq = npan - 1 - p;
+    double v[16], vn[16];
+    auto load_tile = [&](double (&dst)[16], int q) {
+      const int rb = q * 64, nr = min(64, w - rb);
+      const int rc = rb + min(lane, nr - 1);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) dst[e] = L[rc + (int64_t)(c0 + min(g + 4 * e, kw - 1)) * r];
+    };
+    if (nq > 0) load_tile(v, npan - 1);
+    for (int k = 0; k < nq; ++k) {
       const int q = npan - 1 - k;
       const int rb = q * 64, nr = min(64, w - rb);
       if (tid == 0) wait_flag(&flags[flag_off[s] + q], epoch, err);
       __syncthreads();
       // stage the 64 x 64 tile L(rb.., c0..) (coalesced over rows) and the x values of its rows
       {
-        double v[16];
-        const int rc = rb + min(lane, nr - 1);
-#pragma unroll
-        for (int e = 0; e < 16; ++e) v[e] = L[rc + (int64_t)(c0 + min(g + 4 * e, kw - 1)) * r];
         const double xv = (tid < 64) ? xi[f0 + rb + min(tid, nr - 1)] : 0.0;
 #pragma unroll
         for (int e = 0; e < 16; ++e)
@@ -3342,8 +3366,11 @@ __global__ __launch_bounds__(NT) void k_bwd_big(FrontTab T, const SolveTask* __r
         if (tid < 64) xr[tid] = (tid < nr) ? xv : 0.0;
       }
       __syncthreads();
+      if (k + 1 < nq) load_tile(vn, q - 1);  // block-uniform
 #pragma unroll
       for (int rr = 0; rr < 16; ++rr) acc += tile[(g * 16 + rr) * 65 + lane] * xr[g * 16 + rr];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) v[e] = vn[e];
       __syncthreads();
     }
     if (g == 0 && r > w) {
@@ -4240,6 +4267,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   {
     const char* ek = std::getenv("MADIPM_BIG_KPAN");  // panels per deferred big-front update group
     big_kpan_ = ek ? std::max(1, std::min(8, std::atoi(ek))) : 4;
+    // persistent workgroups of the big-front solve kernels (2 per CU; MADIPM_BIG_SOLVE_WG for A/B)
+    if (const char* eg = std::getenv("MADIPM_BIG_SOLVE_WG")) big_solve_wg_ = std::max(64, std::atoi(eg));
     // pipelined in-LDS factorisation schedule (1, default); 0 = the barrier schedule, bitwise the same
     // factor (test_ldl_fact_pipe_bitwise)
     const char* ep = std::getenv("MADIPM_FACT_PIPE");
@@ -5476,7 +5505,7 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
       TIMED(KK_FWD_GATHER, L.gat_bytes, 0.0, 0.0,
             (k_fwd_gather<<<L.ngat, NT, 0, s>>>(T_, sched_.p + L.gat_off, b, uvec_, vwork_)));
       TIMED(KK_FWD_BIG, L.big_bytes, L.big_alg + L.below_alg, L.big_flops,
-            (k_fwd_big<<<std::min(L.nftask, 512), NT, 0, s>>>(T_, tasks + L.ftask_off, L.nftask, cnt + 2 * lev,
+            (k_fwd_big<<<std::min(L.nftask, big_solve_wg_), NT, 0, s>>>(T_, tasks + L.ftask_off, L.nftask, cnt + 2 * lev,
                                                                flags_, flag_off_, efwd, arena_, vwork_, xi_, uvec_, &st_->err)));
     }
     if (lev == 0 && phase == 0 && ntree_ && nsleaf_)
@@ -5522,7 +5551,7 @@ void LDLSolver::bwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
             (k_bwd_below<<<L.nbelow, NT, 0, s>>>(T_, sched_.p + L.below_off, bp_off_, arena_, xi_, bpart_)));
     if (L.nbig)
       TIMED(KK_BWD_BIG, L.big_bytes - L.below_bytes, L.big_alg, L.big_flops - 0.25 * L.below_bytes,
-            (k_bwd_big<<<std::min(L.nbtask, 512), NT, 0, s>>>(T_, tasks + L.btask_off, L.nbtask, cnt + 2 * lev + 1,
+            (k_bwd_big<<<std::min(L.nbtask, big_solve_wg_), NT, 0, s>>>(T_, tasks + L.btask_off, L.nbtask, cnt + 2 * lev + 1,
                                                                flags_, flag_off_, ebwd, arena_, D_, xi_, b, bp_off_, bpart_,
                                                                &st_->err)));
     if (L.nsmall)

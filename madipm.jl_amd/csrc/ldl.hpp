@@ -337,6 +337,7 @@ class LDLSolver : public LinSolver {
   DBuf<int32_t> ft_order_, ft_dptr_, ft_dep_, fflags_, fcnt_;
   DBuf<int64_t> fdbg_, ab_first_, ab_loff_, fold_poff_, fold_row0_;
   int big_kpan_ = 4;  // big fronts: panels per deferred trailing-update group (MADIPM_BIG_KPAN)
+  int big_solve_wg_ = 512;
   DBuf<int32_t> ab_src0_, ab_src1_, ab_k_, ab_f0_, ab_wrc_, fold_bptr_, fold_bat_, fold_plen_, fold_rmax_, fold_lmax_;
   DBuf<uint8_t> absorb_, fold_pk_, fs_img_;
   DBuf<int32_t> mc_ptr_;

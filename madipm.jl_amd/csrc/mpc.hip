@@ -1789,7 +1789,6 @@ void MPCSolver::setup_host(const madipm_qp& q) {
   nnzK_ = (int64_t)Kri.size();
   clk("K2 CSC");
   if (const char* e = std::getenv("MADIPM_SPEC_NEAR")) spec_near_ = std::max(0.0, std::atof(e));
-  if (const char* e = std::getenv("MADIPM_PART_BLOCKS")) maxb_ = std::max(64, std::min(MAXB, std::atoi(e)));
   if (const char* e = std::getenv("MADIPM_FINAL_DEBUG"); e && e[0] == '1') {
     fdbg_.alloc(8 * kFinDbg);
     MADIPM_HIP(hipMemset(fdbg_.p, 0, 8 * kFinDbg * sizeof(int64_t)));

@@ -111,7 +111,7 @@ class MPCSolver {
   static constexpr int kFinDbg = 4096;
   DBuf<int64_t> fdbg_;  // MADIPM_FINAL_DEBUG: k_final stamps (ring of kFinDbg launches)
   int64_t fdbg_n_ = 0;
-  int maxb_ = 2048;  // partial-reduction blocks per producer launch (<= MAXB; MADIPM_PART_BLOCKS)
+  int maxb_ = 2048;  // partial-reduction blocks per producer launch (<= MAXB; r3 / r5: 1024 or 512 measured slower)
   DBuf<double> sk_, K0_, Dinv_, bufm_, Cx_;
   DBuf<int32_t> Krow_, Kcol_, cprod_;
   DBuf<int64_t> cpp_;
