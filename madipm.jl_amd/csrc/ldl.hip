@@ -1576,6 +1576,9 @@ __device__ __forceinline__ FoldBatchTab& fold_batch_tab() {
   return t;
 }
 
+#ifndef MADIPM_FOLD_GP
+#define MADIPM_FOLD_GP 16  // fold product entries per thread and group (32 spills; variants: tools/build_variant.sh)
+#endif
 // cval / cdst: per thread, the parked sum and destination of a chunk's first run when it continues
 // the left neighbour's run (k_fact_tree's MK / cbuf, idle during the fold)
 template <bool PK>
@@ -1591,7 +1594,7 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
     }
   };
   constexpr int RPT = 8;   // leaf rows per thread and pass
-  constexpr int GP = 16;   // product entries per thread and group
+  constexpr int GP = MADIPM_FOLD_GP;  // product entries per thread and group
   const int RM = T.fold_rmax[s], LM = T.fold_lmax[s];
   double2* LQ = reinterpret_cast<double2*>(ext);  // per batch row: K values of columns 0/1, then (l0, l1)
   double2* PQ = LQ + RM;                          // (l0 d0, l1 d1)
