@@ -2171,6 +2171,10 @@ __global__ __launch_bounds__(FTN) void k_fact_tree(FrontTab T, const int32_t* __
 // write L11 (d on the diagonal), D and the M_K blocks for k_big_trsm.
 // The diagonal block of panel `step` of front s, staged in A64 (lower part, identity-padded past kw):
 // blocked factorisation, then L11 (d on the diagonal), D and the M_K blocks for k_big_trsm.
+// the flag value of "panel `step`'s diagonal block is factorised" in the current factorisation
+__device__ __forceinline__ int32_t big_dflag_value(const FrontTab& T, int step) {
+  return (int32_t)(((uint32_t)T.bepoch << 10) | ((uint32_t)step & 1023u)) & 0x7fffffff;
+}
 __device__ __forceinline__ void big_diag_tail(const FrontTab& T, int s, int step, double* A64, double* Ms, double* Dl,
                                               double* __restrict__ arena, double* __restrict__ D,
                                               double* __restrict__ Mbuf, LDLStatus* st, double tol) {
@@ -2188,6 +2192,14 @@ __device__ __forceinline__ void big_diag_tail(const FrontTab& T, int s, int step
   }
   double* __restrict__ M = Mbuf + (int64_t)T.bigslot[s] * 4096;
   for (int e = tid; e < 4 * 16 * LDM; e += NT) M[e] = Ms[e];
+  // published for the trsm tiles fused into the same update launch (k_big_update): every wave's
+  // stores drained, then one release + flag store (value: factorisation epoch | panel)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_store(&T.dflag[s], big_dflag_value(T, step), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // Lookahead: the update launch of panel `step` leaves panel step + 1's diagonal tile final in the
@@ -2323,9 +2335,11 @@ __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __
                                                    double* __restrict__ arena, double* __restrict__ D,
                                                    double* __restrict__ Mbuf, LDLStatus* st, double tol) {
   constexpr int LDT = 80;  // [k][row] layout: conflict-free ds_read_b64 for the 16x4 operand pattern
-  __shared__ __attribute__((aligned(16))) double Wt[64 * LDT];
-  __shared__ __attribute__((aligned(16))) double Lt[64 * LDT];
+  __shared__ __attribute__((aligned(16))) double WLt[2 * 64 * LDT];
+  double* Wt = WLt;
+  double* Lt = WLt + 64 * LDT;
   static_assert(64 * LDA <= 64 * LDT && 4 * 16 * LDM + 64 <= 64 * LDT, "lookahead diagonal block aliases Wt / Lt");
+  static_assert(64 * LDA + 4 * 16 * LDM + 64 + 4 * 17 * 64 <= 2 * 64 * LDT, "fused trsm tiles alias Wt | Lt");
   int s, tij;
   task_of(list, s, tij);
   const int ti = tij & 0xffff, tj = (tij >> 16) & 0x7fff;
@@ -2402,17 +2416,105 @@ __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __
     }
     if (ch + 1 < nch) __syncthreads();  // the LDS tiles are rewritten by the next chunk
   }
+  // fused trsm: a local tile of the next panel's column block below its diagonal block (ti >= 1,
+  // tj = 0) is exactly a k_big_trsm tile of panel step + 1 (a full panel): instead of storing it for
+  // the next launch to reload, it waits for task (0, 0)'s diagonal factor of that panel (this launch,
+  // big_diag_tail's flag) and solves it here (k_big_trsm's arithmetic, bitwise the same L)
+  const bool fuse = T.fuse_trsm && !trailing && tj == 0 && ti >= 1 && 64 * (step + 2) <= w;
   // D layout: col n = lane&15 (-> row i of F), row m = (lane>>4) + 4g (-> column j of F)
+  if (!fuse)
 #pragma unroll
-  for (int bj = 0; bj < 2; ++bj)
+    for (int bj = 0; bj < 2; ++bj)
 #pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
+      for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int i = I0 + qr + bi * 16 + (lane & 15);
-        const int j = J0 + qc + bj * 16 + (lane >> 4) + 4 * g;
-        if (i < r && j < jlim && i >= j) F[i + (int64_t)j * r] = c[bj][bi][g] - acc[bj][bi][g];
+        for (int g = 0; g < 4; ++g) {
+          const int i = I0 + qr + bi * 16 + (lane & 15);
+          const int j = J0 + qc + bj * 16 + (lane >> 4) + 4 * g;
+          if (i < r && j < jlim && i >= j) F[i + (int64_t)j * r] = c[bj][bi][g] - acc[bj][bi][g];
+        }
+  if (fuse) {
+    double* L11 = WLt;
+    double* Ms = L11 + 64 * LDA;
+    double* Dl = Ms + 4 * 16 * LDM;
+    double* Sl = Dl + 64;  // 4 slabs of 16 rows x 64 columns, S[m + 17 j]
+    __syncthreads();       // every wave's last operand read of Wt / Lt
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int il = qr + bi * 16 + (lane & 15);  // tile row: slab il >> 4, row il & 15
+          const int jl = qc + bj * 16 + (lane >> 4) + 4 * g;
+          Sl[(il >> 4) * 17 * 64 + (il & 15) + 17 * jl] = (I0 + il < r) ? c[bj][bi][g] - acc[bj][bi][g] : 0.0;
+        }
+    const int k0 = 64 * (step + 1);
+    if (tid == 0) {
+      const int32_t want = big_dflag_value(T, step + 1);
+      int spins = 0;
+      while (__hip_atomic_load(&T.dflag[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1 << 25)) {
+          __hip_atomic_fetch_or(T.err, kErrHandoff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
       }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every thread: see the diagonal factor
+    {
+      const double* __restrict__ M = Mbuf + (int64_t)T.bigslot[s] * 4096;
+      double lv[16], mv[5], dv;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) lv[e] = F[(k0 + lane) + (int64_t)(k0 + wv + 4 * e) * r];
+#pragma unroll
+      for (int e = 0; e < 5; ++e) mv[e] = M[min(tid + e * NT, 4 * 16 * LDM - 1)];
+      dv = D[f0 + k0 + (tid & 63)];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int j = wv + 4 * e;
+        L11[lane + j * LDA] = (lane > j) ? lv[e] : 0.0;
+      }
+#pragma unroll
+      for (int e = 0; e < 5; ++e)
+        if (tid + e * NT < 4 * 16 * LDM) Ms[tid + e * NT] = mv[e];
+      if (tid < 64) Dl[tid] = dv;
+    }
+    __syncthreads();
+    double* S = Sl + wv * 17 * 64;
+    const int row = I0 + 16 * wv + (lane & 15);
+    for (int K = 0; K < 4; ++K) {
+      dbl4 a4 = {0.0, 0.0, 0.0, 0.0};
+      for (int J = 0; J < K; ++J) {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const int k = 16 * J + 4 * ks + (lane >> 4);
+          const double av = S[(lane & 15) + k * 17] * Dl[k];
+          const double bv = L11[(16 * K + (lane & 15)) + k * LDA];
+          a4 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, a4, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) S[((lane >> 4) + 4 * g) + (16 * K + (lane & 15)) * 17] -= a4[g];
+      wave_sync();
+      dbl4 l = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int k = 4 * ks + (lane >> 4);
+        const double av = S[(lane & 15) + (16 * K + k) * 17];
+        const double bv = Ms[K * 16 * LDM + k * LDM + (lane & 15)];
+        l = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, l, 0, 0, 0);
+      }
+      wave_sync();
+#pragma unroll
+      for (int g = 0; g < 4; ++g) S[((lane >> 4) + 4 * g) + (16 * K + (lane & 15)) * 17] = l[g];
+      wave_sync();
+    }
+    for (int j = lane >> 4; j < 64; j += 4)
+      if (row < r) F[row + (int64_t)(k0 + j) * r] = S[(lane & 15) + j * 17];
+    return;
+  }
   // lookahead: task (0, 0) of a local update holds the next panel's diagonal tile, final now (the
   // panel's last local update; the next panel lies inside the group, below jlim)
   if (!trailing && ti == 0 && tj == 0 && big_next_diag(T, s, step)) {
@@ -4270,6 +4372,9 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   {
     const char* ek = std::getenv("MADIPM_BIG_KPAN");  // panels per deferred big-front update group
     big_kpan_ = ek ? std::max(1, std::min(8, std::atoi(ek))) : 4;
+    // big fronts: the next panel's trsm tiles fused into the local update launch (1, default)
+    const char* ef2 = std::getenv("MADIPM_FUSE_TRSM");
+    T_.fuse_trsm = (ef2 && ef2[0] == '0') ? 0 : 1;
     // persistent workgroups of the big-front solve kernels (2 per CU; MADIPM_BIG_SOLVE_WG for A/B)
     if (const char* eg = std::getenv("MADIPM_BIG_SOLVE_WG")) big_solve_wg_ = std::max(64, std::atoi(eg));
     // pipelined in-LDS factorisation schedule (1, default); 0 = the barrier schedule, bitwise the same
@@ -4716,7 +4821,11 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
           kb[1] += 8.0 * (2.0 * nb * dk + nt * (dk * (dk + 1) / 2 + 4 * 16 * 17));  // trsm: rows in/out + L11, M per tile
           kf[1] += nb * dk * dk;
           if (p == 0) td.insert(td.end(), {s, 0});  // later panels: the previous update's task (0, 0)
-          for (int i = 0; i < nt; ++i) tt.insert(tt.end(), {s, i});
+          // a full panel inside its group (not the group's first): its trsm tiles were solved by the
+          // previous step's local update launch (k_big_update, fused trsm)
+          const bool fused_trsm = T_.fuse_trsm && p >= 1 && p % big_kpan_ != 0 && !S.fused[s] && 64 * (p + 1) <= w;
+          if (!fused_trsm)
+            for (int i = 0; i < nt; ++i) tt.insert(tt.end(), {s, i});
           if (S.fused[s]) continue;  // its trailing update: k_asm_update (below)
           // deferred multi-panel update (k_big_update): panel groups of big_kpan_ panels; inside a
           // group each panel updates the group's later panels only (local tiles), the group's last
@@ -5030,6 +5139,9 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   }
   sched_.upload(sched.empty() ? std::vector<int32_t>{0} : sched);
   arena_.alloc(std::max<int64_t>(S.arena_size, 2));
+  dflag_.alloc(std::max(S.nsuper, 1));  // big fronts' diagonal-block flags (fused trsm tiles)
+  dflag_.zero();
+  T_.dflag = dflag_;
   if (S.nshards > 1) {  // top fronts: the strict upper triangles are never written, keep them 0
     MADIPM_HIP(hipMemset(arena_.p + S.top_lo, 0, sizeof(double) * (S.arena_size - S.top_lo)));
     // exchange buffer: the top fronts' lower triangles (column by column) + 4 status slots per shard
@@ -5205,6 +5317,7 @@ double LDLSolver::solve_alg(int s) const {
 }
 
 void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStream_t s) {
+  T_.bepoch = (int)(++bepoch_ & 0x1fffff);  // tags this factorisation's diagonal-block flags
   for (const Launch& L : LL) {
     const int32_t* list = sched_.p + L.off;
     switch (L.kind) {
