@@ -2171,10 +2171,6 @@ __global__ __launch_bounds__(FTN) void k_fact_tree(FrontTab T, const int32_t* __
 // write L11 (d on the diagonal), D and the M_K blocks for k_big_trsm.
 // The diagonal block of panel `step` of front s, staged in A64 (lower part, identity-padded past kw):
 // blocked factorisation, then L11 (d on the diagonal), D and the M_K blocks for k_big_trsm.
-// the flag value of "panel `step`'s diagonal block is factorised" in the current factorisation
-__device__ __forceinline__ int32_t big_dflag_value(const FrontTab& T, int step) {
-  return (int32_t)(((uint32_t)T.bepoch << 10) | ((uint32_t)step & 1023u)) & 0x7fffffff;
-}
 __device__ __forceinline__ void big_diag_tail(const FrontTab& T, int s, int step, double* A64, double* Ms, double* Dl,
                                               double* __restrict__ arena, double* __restrict__ D,
                                               double* __restrict__ Mbuf, LDLStatus* st, double tol) {
@@ -2192,14 +2188,6 @@ __device__ __forceinline__ void big_diag_tail(const FrontTab& T, int s, int step
   }
   double* __restrict__ M = Mbuf + (int64_t)T.bigslot[s] * 4096;
   for (int e = tid; e < 4 * 16 * LDM; e += NT) M[e] = Ms[e];
-  // published for the trsm tiles fused into the same update launch (k_big_update): every wave's
-  // stores drained, then one release + flag store (value: factorisation epoch | panel)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __hip_atomic_store(&T.dflag[s], big_dflag_value(T, step), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
 }
 
 // Lookahead: the update launch of panel `step` leaves panel step + 1's diagonal tile final in the
@@ -2339,7 +2327,6 @@ __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __
   double* Wt = WLt;
   double* Lt = WLt + 64 * LDT;
   static_assert(64 * LDA <= 64 * LDT && 4 * 16 * LDM + 64 <= 64 * LDT, "lookahead diagonal block aliases Wt / Lt");
-  static_assert(64 * LDA + 4 * 16 * LDM + 64 + 4 * 17 * 64 <= 2 * 64 * LDT, "fused trsm tiles alias Wt | Lt");
   int s, tij;
   task_of(list, s, tij);
   const int ti = tij & 0xffff, tj = (tij >> 16) & 0x7fff;
@@ -2416,105 +2403,17 @@ __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __
     }
     if (ch + 1 < nch) __syncthreads();  // the LDS tiles are rewritten by the next chunk
   }
-  // fused trsm: a local tile of the next panel's column block below its diagonal block (ti >= 1,
-  // tj = 0) is exactly a k_big_trsm tile of panel step + 1 (a full panel): instead of storing it for
-  // the next launch to reload, it waits for task (0, 0)'s diagonal factor of that panel (this launch,
-  // big_diag_tail's flag) and solves it here (k_big_trsm's arithmetic, bitwise the same L)
-  const bool fuse = T.fuse_trsm && !trailing && tj == 0 && ti >= 1 && 64 * (step + 2) <= w;
   // D layout: col n = lane&15 (-> row i of F), row m = (lane>>4) + 4g (-> column j of F)
-  if (!fuse)
 #pragma unroll
-    for (int bj = 0; bj < 2; ++bj)
+  for (int bj = 0; bj < 2; ++bj)
 #pragma unroll
-      for (int bi = 0; bi < 2; ++bi)
+    for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int i = I0 + qr + bi * 16 + (lane & 15);
-          const int j = J0 + qc + bj * 16 + (lane >> 4) + 4 * g;
-          if (i < r && j < jlim && i >= j) F[i + (int64_t)j * r] = c[bj][bi][g] - acc[bj][bi][g];
-        }
-  if (fuse) {
-    double* L11 = WLt;
-    double* Ms = L11 + 64 * LDA;
-    double* Dl = Ms + 4 * 16 * LDM;
-    double* Sl = Dl + 64;  // 4 slabs of 16 rows x 64 columns, S[m + 17 j]
-    __syncthreads();       // every wave's last operand read of Wt / Lt
-#pragma unroll
-    for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-      for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int il = qr + bi * 16 + (lane & 15);  // tile row: slab il >> 4, row il & 15
-          const int jl = qc + bj * 16 + (lane >> 4) + 4 * g;
-          Sl[(il >> 4) * 17 * 64 + (il & 15) + 17 * jl] = (I0 + il < r) ? c[bj][bi][g] - acc[bj][bi][g] : 0.0;
-        }
-    const int k0 = 64 * (step + 1);
-    if (tid == 0) {
-      const int32_t want = big_dflag_value(T, step + 1);
-      int spins = 0;
-      while (__hip_atomic_load(&T.dflag[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1 << 25)) {
-          __hip_atomic_fetch_or(T.err, kErrHandoff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
+      for (int g = 0; g < 4; ++g) {
+        const int i = I0 + qr + bi * 16 + (lane & 15);
+        const int j = J0 + qc + bj * 16 + (lane >> 4) + 4 * g;
+        if (i < r && j < jlim && i >= j) F[i + (int64_t)j * r] = c[bj][bi][g] - acc[bj][bi][g];
       }
-    }
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every thread: see the diagonal factor
-    {
-      const double* __restrict__ M = Mbuf + (int64_t)T.bigslot[s] * 4096;
-      double lv[16], mv[5], dv;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) lv[e] = F[(k0 + lane) + (int64_t)(k0 + wv + 4 * e) * r];
-#pragma unroll
-      for (int e = 0; e < 5; ++e) mv[e] = M[min(tid + e * NT, 4 * 16 * LDM - 1)];
-      dv = D[f0 + k0 + (tid & 63)];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int j = wv + 4 * e;
-        L11[lane + j * LDA] = (lane > j) ? lv[e] : 0.0;
-      }
-#pragma unroll
-      for (int e = 0; e < 5; ++e)
-        if (tid + e * NT < 4 * 16 * LDM) Ms[tid + e * NT] = mv[e];
-      if (tid < 64) Dl[tid] = dv;
-    }
-    __syncthreads();
-    double* S = Sl + wv * 17 * 64;
-    const int row = I0 + 16 * wv + (lane & 15);
-    for (int K = 0; K < 4; ++K) {
-      dbl4 a4 = {0.0, 0.0, 0.0, 0.0};
-      for (int J = 0; J < K; ++J) {
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          const int k = 16 * J + 4 * ks + (lane >> 4);
-          const double av = S[(lane & 15) + k * 17] * Dl[k];
-          const double bv = L11[(16 * K + (lane & 15)) + k * LDA];
-          a4 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, a4, 0, 0, 0);
-        }
-      }
-#pragma unroll
-      for (int g = 0; g < 4; ++g) S[((lane >> 4) + 4 * g) + (16 * K + (lane & 15)) * 17] -= a4[g];
-      wave_sync();
-      dbl4 l = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int k = 4 * ks + (lane >> 4);
-        const double av = S[(lane & 15) + (16 * K + k) * 17];
-        const double bv = Ms[K * 16 * LDM + k * LDM + (lane & 15)];
-        l = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, l, 0, 0, 0);
-      }
-      wave_sync();
-#pragma unroll
-      for (int g = 0; g < 4; ++g) S[((lane >> 4) + 4 * g) + (16 * K + (lane & 15)) * 17] = l[g];
-      wave_sync();
-    }
-    for (int j = lane >> 4; j < 64; j += 4)
-      if (row < r) F[row + (int64_t)(k0 + j) * r] = S[(lane & 15) + j * 17];
-    return;
-  }
   // lookahead: task (0, 0) of a local update holds the next panel's diagonal tile, final now (the
   // panel's last local update; the next panel lies inside the group, below jlim)
   if (!trailing && ti == 0 && tj == 0 && big_next_diag(T, s, step)) {
@@ -3270,8 +3169,33 @@ __device__ __forceinline__ double tri_bwd64(double a, const double* Ld, int kw, 
   return a;
 }
 
+// Panel solutions handed between the big-front solve tasks as self-validating 8-byte words (the LL
+// idea): value halves each stored with the solve's epoch in the upper 32 bits by single-copy-atomic
+// 8-byte stores, so a consumer lane polls its two words until both carry the epoch — the data is the
+// flag: no release fence and drain before a flag store, no acquire and second round trip after it.
+__device__ __forceinline__ void ll_put(uint64_t* w, double v, int epoch) {
+  const uint64_t tag = (uint64_t)(uint32_t)epoch << 32;
+  __hip_atomic_store(w, tag | (uint32_t)__double2loint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(w + 1, tag | (uint32_t)__double2hiint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ll_get(const uint64_t* w, int epoch, int32_t* err) {
+  uint64_t a, b;
+  int spins = 0;
+  for (;;) {
+    a = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    b = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((uint32_t)(a >> 32) == (uint32_t)epoch && (uint32_t)(b >> 32) == (uint32_t)epoch) break;
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > (1 << 25)) {
+      atomicOr(err, kErrHandoff);
+      break;
+    }
+  }
+  return __hiloint2double((int)(uint32_t)b, (int)(uint32_t)a);
+}
+
 // Forward, big fronts: task = (front, 64-row block i).  acc(rows) = v(rows) - sum_{panels p < i} L(rows,p) x_p,
-// then (pivot block) x_i = L_ii^{-1} acc, published through flags[flag_off[front] + i].
+// then (pivot block) x_i = L_ii^{-1} acc, handed to the later row blocks through T.xll (ll_put / ll_get).
 __global__ __launch_bounds__(NT) void k_fwd_big(FrontTab T, const SolveTask* __restrict__ tasks, int ntasks,
                                                 int32_t* counter, int32_t* flags, const int32_t* __restrict__ flag_off,
                                                 int epoch, const double* __restrict__ arena,
@@ -3324,12 +3248,9 @@ __global__ __launch_bounds__(NT) void k_fwd_big(FrontTab T, const SolveTask* __r
       const int cb = p * 64 + g * 16;
 #pragma unroll
       for (int cc = 0; cc < 16; ++cc) lv[cc] = (lane < nrow && cb + cc < w) ? lv[cc] : 0.0;
-      if (tid == 0) wait_flag(&flags[flag_off[s] + p], epoch, err);
-      __syncthreads();
       if (tid < 64) {
-        const int c = p * 64 + tid;
-        const double xv = xi[f0 + min(c, w - 1)];
-        xs[tid] = (c < w) ? xv : 0.0;
+        const double xv = ll_get(T.xll + ((int64_t)flag_off[s] + p) * 128 + 2 * tid, epoch, err);
+        xs[tid] = (p * 64 + tid < w) ? xv : 0.0;
       }
       __syncthreads();
 #pragma unroll
@@ -3344,13 +3265,13 @@ __global__ __launch_bounds__(NT) void k_fwd_big(FrontTab T, const SolveTask* __r
       double a = (lane < nrow) ? vwork[T.row_ptr[s] + row] - ((part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]))
                                : 0.0;
       a = tri_fwd64(a, Ld, kw, lane);
+      if (pivot_blk) ll_put(T.xll + ((int64_t)flag_off[s] + i) * 128 + 2 * lane, a, epoch);  // every lane: 0 past nrow
       if (lane < nrow) {
         if (row < w)
           xi[f0 + row] = a;
         else
           uvec[T.uvec_off[s] + row - w] = a;
       }
-      if (pivot_blk) publish_flag(&flags[flag_off[s] + i], epoch);
     }
     __syncthreads();
   }
@@ -3460,11 +3381,10 @@ __global__ __launch_bounds__(NT) void k_bwd_big(FrontTab T, const SolveTask* __r
     for (int k = 0; k < nq; ++k) {
       const int q = npan - 1 - k;
       const int rb = q * 64, nr = min(64, w - rb);
-      if (tid == 0) wait_flag(&flags[flag_off[s] + q], epoch, err);
-      __syncthreads();
-      // stage the 64 x 64 tile L(rb.., c0..) (coalesced over rows) and the x values of its rows
+      // stage the 64 x 64 tile L(rb.., c0..) (coalesced over rows) and the x values of its rows (the
+      // panel's solution words, ll_get: they are the hand-off)
       {
-        const double xv = (tid < 64) ? xi[f0 + rb + min(tid, nr - 1)] : 0.0;
+        const double xv = (tid < 64) ? ll_get(T.xll + ((int64_t)flag_off[s] + q) * 128 + 2 * tid, epoch, err) : 0.0;
 #pragma unroll
         for (int e = 0; e < 16; ++e)
           if (g + 4 * e < kw) tile[lane * 65 + g + 4 * e] = (lane < nr) ? v[e] : 0.0;
@@ -3494,12 +3414,12 @@ __global__ __launch_bounds__(NT) void k_bwd_big(FrontTab T, const SolveTask* __r
         a = xi[c] / D[c] - ((part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]));
       }
       a = tri_bwd64(a, Ld, kw, lane);
+      ll_put(T.xll + ((int64_t)flag_off[s] + p) * 128 + 2 * lane, a, epoch);  // every lane (masked by the readers)
       if (lane < kw) {
         const int c = f0 + c0 + lane;
         xi[c] = a;
         if (T.wout[s]) out[T.perm[c]] = a;
       }
-      publish_flag(&flags[flag_off[s] + p], epoch);
     }
     __syncthreads();
   }
@@ -4372,9 +4292,6 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   {
     const char* ek = std::getenv("MADIPM_BIG_KPAN");  // panels per deferred big-front update group
     big_kpan_ = ek ? std::max(1, std::min(8, std::atoi(ek))) : 4;
-    // big fronts: the next panel's trsm tiles fused into the local update launch (1, default)
-    const char* ef2 = std::getenv("MADIPM_FUSE_TRSM");
-    T_.fuse_trsm = (ef2 && ef2[0] == '0') ? 0 : 1;
     // persistent workgroups of the big-front solve kernels (2 per CU; MADIPM_BIG_SOLVE_WG for A/B)
     if (const char* eg = std::getenv("MADIPM_BIG_SOLVE_WG")) big_solve_wg_ = std::max(64, std::atoi(eg));
     // pipelined in-LDS factorisation schedule (1, default); 0 = the barrier schedule, bitwise the same
@@ -4821,11 +4738,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
           kb[1] += 8.0 * (2.0 * nb * dk + nt * (dk * (dk + 1) / 2 + 4 * 16 * 17));  // trsm: rows in/out + L11, M per tile
           kf[1] += nb * dk * dk;
           if (p == 0) td.insert(td.end(), {s, 0});  // later panels: the previous update's task (0, 0)
-          // a full panel inside its group (not the group's first): its trsm tiles were solved by the
-          // previous step's local update launch (k_big_update, fused trsm)
-          const bool fused_trsm = T_.fuse_trsm && p >= 1 && p % big_kpan_ != 0 && !S.fused[s] && 64 * (p + 1) <= w;
-          if (!fused_trsm)
-            for (int i = 0; i < nt; ++i) tt.insert(tt.end(), {s, i});
+          for (int i = 0; i < nt; ++i) tt.insert(tt.end(), {s, i});
           if (S.fused[s]) continue;  // its trailing update: k_asm_update (below)
           // deferred multi-panel update (k_big_update): panel groups of big_kpan_ panels; inside a
           // group each panel updates the group's later panels only (local tiles), the group's last
@@ -5134,14 +5047,16 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     bpart_.alloc(std::max<int64_t>(nbpart, 1) * 64);
     flags_.alloc(std::max<int64_t>(nflags, 1));
     flags_.zero();
+    // the big fronts' panel solutions as self-validating words (ll_put / ll_get): 64 values x 2 halves
+    // per panel flag
+    xll_.alloc(std::max<int64_t>(nflags, 1) * 128);
+    xll_.zero();
+    T_.xll = xll_;
     counters_.alloc(4 * std::max(NL, 1) + 4);  // + the tree-solve tickets (4 NL, 4 NL + 1)
     counters_.zero();
   }
   sched_.upload(sched.empty() ? std::vector<int32_t>{0} : sched);
   arena_.alloc(std::max<int64_t>(S.arena_size, 2));
-  dflag_.alloc(std::max(S.nsuper, 1));  // big fronts' diagonal-block flags (fused trsm tiles)
-  dflag_.zero();
-  T_.dflag = dflag_;
   if (S.nshards > 1) {  // top fronts: the strict upper triangles are never written, keep them 0
     MADIPM_HIP(hipMemset(arena_.p + S.top_lo, 0, sizeof(double) * (S.arena_size - S.top_lo)));
     // exchange buffer: the top fronts' lower triangles (column by column) + 4 status slots per shard
@@ -5317,7 +5232,6 @@ double LDLSolver::solve_alg(int s) const {
 }
 
 void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStream_t s) {
-  T_.bepoch = (int)(++bepoch_ & 0x1fffff);  // tags this factorisation's diagonal-block flags
   for (const Launch& L : LL) {
     const int32_t* list = sched_.p + L.off;
     switch (L.kind) {

@@ -72,12 +72,7 @@ struct FrontTab {
   int fpipe;        // pipelined in-LDS schedule (blocked_factor_pipe; MADIPM_FACT_PIPE=0: blocked_factor_lds)
   int pipe_fault;   // tests (MADIPM_DEBUG_PIPE_FAULT=1): blocked_factor_pipe drops one hand-off
   int lds_cap;      // k_fact_tree's dynamic LDS (bytes): a front (+ its leaf batches) beyond it is an error
-  // big fronts: the next panel's trsm tiles fused into the local update launch (MADIPM_FUSE_TRSM=0:
-  // separate k_big_trsm launches); dflag[s] = the latest factorised diagonal block of front s, tagged
-  // with the factorisation epoch bepoch (big_dflag_value)
-  int fuse_trsm;
-  int bepoch;
-  int32_t* dflag;
+  uint64_t* xll;  // big-front solves: panel solutions as self-validating words (ll_put / ll_get)
 };
 
 // LDLStatus::err bits (sticky; status() raises on any)
@@ -340,8 +335,8 @@ class LDLSolver : public LinSolver {
   int nftree_ = 0, ftree_lds_ = 0, fepoch_ = 0;
   bool ftree_checked_ = false;
   double ftree_bytes_ = 0, ftree_flops_ = 0, ftree_alg_ = 0;
-  DBuf<int32_t> ft_order_, ft_dptr_, ft_dep_, fflags_, fcnt_, dflag_;
-  int64_t bepoch_ = 0;  // factorisations run (tags the big fronts' diagonal-block flags)
+  DBuf<int32_t> ft_order_, ft_dptr_, ft_dep_, fflags_, fcnt_;
+  DBuf<uint64_t> xll_;
   DBuf<int64_t> fdbg_, ab_first_, ab_loff_, fold_poff_, fold_row0_;
   int big_kpan_ = 4;  // big fronts: panels per deferred trailing-update group (MADIPM_BIG_KPAN)
   int big_solve_wg_ = 512;

@@ -165,24 +165,6 @@ def test_ldl_pipe_lost_handoff_is_an_error(monkeypatch):
     _factor_solve(K, Lw, 192)  # a fresh solver factorises normally
 
 
-@pytest.mark.parametrize("kpan", ["4", "3"])
-def test_big_trsm_fused_bitwise(kpan, monkeypatch):
-    """Big fronts: the next panel's trsm tiles solved inside the local update launch (k_big_update,
-    waiting on task (0, 0)'s diagonal factor of that panel; MADIPM_FUSE_TRSM=1, default) give BITWISE
-    the pivots and solution of separate k_big_trsm launches (=0) — the same arithmetic on the same
-    values — and the oracle's.  A 600-row dense root (10 panels) crosses panel groups of kpan."""
-    monkeypatch.setenv("MADIPM_BIG_KPAN", kpan)
-    K, Lw = _dense_k2(600, 1500, 11)
-    out = {}
-    for f in ("0", "1"):
-        monkeypatch.setenv("MADIPM_FUSE_TRSM", f)
-        out[f] = _factor_solve(K, Lw, 128)
-    (d0, x0, _), (d1, x1, _) = out["0"], out["1"]
-    assert np.array_equal(d0.view(np.uint64), d1.view(np.uint64)), f"pivots differ at {np.flatnonzero(d0 != d1)[:8]}"
-    assert np.array_equal(x0.view(np.uint64), x1.view(np.uint64))
-    _check_case(K, Lw, well=True)
-
-
 @pytest.mark.parametrize("shrink", ["8", "1048576"])
 def test_ldl_fold_carve_overflow_is_an_error(shrink, monkeypatch):
     """k_fact_tree checks on the device that every front and each of its folded-leaf batches fit the
