@@ -281,7 +281,9 @@ int madipm_ldl_solve_phase(madipm_ldl_t ls, int32_t phase, double* d_x, madipm_s
   MADIPM_REQUIRE(ls && ls->own && phase >= 1 && phase <= 3 && d_x, "bad argument");
   MADIPM_REQUIRE(phase == ls->solve_next, "sharded solve protocol: phase " + std::to_string(phase) + " called, phase " +
                                              std::to_string(ls->solve_next) + " expected (1 -> 2 -> 3; ABI 0.2)");
-  ls->solve_next = phase == 3 ? 1 : phase + 1;
+  // the protocol advances only once the phase is enqueued: a phase that throws (a HIP error) resets it
+  // to phase 1, so the handle is not left refusing every later call
+  ls->solve_next = 1;
   hipStream_t st = (hipStream_t)stream;
   if (phase == 1) {
     ls->s->solve_phase1(d_x, st);
@@ -296,6 +298,7 @@ int madipm_ldl_solve_phase(madipm_ldl_t ls, int32_t phase, double* d_x, madipm_s
     if (xbuf) *xbuf = nullptr;
     if (xlen) *xlen = 0;
   }
+  ls->solve_next = phase == 3 ? 1 : phase + 1;
   return 0;
   MADIPM_API_END
 }
@@ -379,6 +382,7 @@ int madipm_ldl_get_info(madipm_ldl_t ls, madipm_ldl_info* info) {
 int madipm_ldl_factorize_async(madipm_ldl_t ls, const double* d_nzval, madipm_stream_t stream) {
   MADIPM_API_BEGIN
   MADIPM_REQUIRE(ls, "null handle");
+  require_idle(ls);  // not between the phases of a sharded solve (as madipm_ldl_factorize)
   ls->lin->factorize_async(d_nzval, (hipStream_t)stream);
   ls->last_stream = (hipStream_t)stream;
   ls->pending = true;

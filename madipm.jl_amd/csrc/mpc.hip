@@ -1395,7 +1395,9 @@ static int par_threads(int64_t n, int64_t grain = (int64_t)1 << 20) {
 template <class R, class C, class V>
 static void csr_from_coo(int nrow, int64_t nnz, R r, C c, V v, std::vector<int64_t>& rp, hvec<int32_t>& ci,
                          hvec<double>& cv) {
-  const int T = par_threads(nnz);
+  // per-thread row counts cost T (nrow + 1) int64: bound T so that they stay within the entries' own
+  // size (a tall sparse matrix with millions of rows would otherwise take gigabytes of scratch)
+  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(par_threads(nnz), nnz / (4 * ((int64_t)nrow + 1))));
   std::vector<std::vector<int64_t>> cnt(T, std::vector<int64_t>(nrow + 1, 0));
   auto chunk = [&](int t) { return std::make_pair(nnz * t / T, nnz * (t + 1) / T); };
   {
@@ -1640,11 +1642,13 @@ void MPCSolver::setup_host(const madipm_qp& q) {
     std::vector<double> rowmax(m, 0.0);
     {  // per-thread row maxima, then their maximum (order-free)
       const int64_t nz = P.nnzA;
-      std::vector<std::vector<double>> rm(par_threads(nz), std::vector<double>(m, 0.0));
+      // at most nz / (4 m) threads: their m-long maxima stay within the entries' own size
+      const int64_t tc = std::max<int64_t>(1, std::min<int64_t>(par_threads(nz), nz / (4 * std::max(m, 1))));
+      std::vector<std::vector<double>> rm(tc, std::vector<double>(m, 0.0));
       par_range(nz, [&](int t, int64_t a, int64_t b) {
         double* x = rm[t].data();
         for (int64_t k = a; k < b; ++k) x[P.Ar[k]] = std::max(x[P.Ar[k]], std::fabs(P.Av[k]));
-      });
+      }, std::max<int64_t>((int64_t)1 << 20, (nz + tc - 1) / tc));
       for (const auto& x : rm)
         for (int i = 0; i < m; ++i) rowmax[i] = std::max(rowmax[i], x[i]);
     }
