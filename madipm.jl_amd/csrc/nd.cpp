@@ -86,8 +86,7 @@ bool coarsen(const Graph& g, Graph& c, std::vector<int32_t>& cmap, Rng& rng, int
   for (int v = 0; v < n; ++v)
     if (rep[cmap[v]] == -1) rep[cmap[v]] = v;
   // contraction of coarse vertices [cv0, cv1) into (adj, ew), c.p[cv + 1] = its degree; a coarse
-  // vertex's list is its members' neighbours in adjacency order, duplicates merged — the same lists
-  // whether one thread builds them all or each of `threads` builds a range (then concatenated)
+  // vertex's list is its members' neighbours in adjacency order, duplicates merged
   auto contract = [&](int cv0, int cv1, std::vector<int32_t>& adj, std::vector<int32_t>& ew) {
     std::vector<int32_t> pos(nc, -1);
     for (int cv = cv0; cv < cv1; ++cv) {
@@ -113,28 +112,14 @@ bool coarsen(const Graph& g, Graph& c, std::vector<int32_t>& cmap, Rng& rng, int
       c.p[cv + 1] = (int64_t)adj.size() - start;
     }
   };
-  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(threads, (int64_t)g.adj.size() / 500000));
+  // (one thread: contracting ranges on threads and concatenating measured 2-4x slower per level on
+  // ex10's top graph — fresh per-thread buffers faulting in concurrently — so `threads` is unused)
+  (void)threads;
   c.adj.clear();
   c.ew.clear();
-  if (T <= 1) {
-    c.adj.reserve(g.adj.size());
-    c.ew.reserve(g.adj.size());
-    contract(0, nc, c.adj, c.ew);
-  } else {
-    std::vector<std::vector<int32_t>> ta(T), te(T);
-    std::vector<std::thread> th;
-    for (int t = 0; t < T; ++t)
-      th.emplace_back([&, t] { contract((int)((int64_t)nc * t / T), (int)((int64_t)nc * (t + 1) / T), ta[t], te[t]); });
-    for (auto& x : th) x.join();
-    size_t tot = 0;
-    for (int t = 0; t < T; ++t) tot += ta[t].size();
-    c.adj.reserve(tot);
-    c.ew.reserve(tot);
-    for (int t = 0; t < T; ++t) {
-      c.adj.insert(c.adj.end(), ta[t].begin(), ta[t].end());
-      c.ew.insert(c.ew.end(), te[t].begin(), te[t].end());
-    }
-  }
+  c.adj.reserve(g.adj.size());
+  c.ew.reserve(g.adj.size());
+  contract(0, nc, c.adj, c.ew);
   for (int cv = 0; cv < nc; ++cv) c.p[cv + 1] += c.p[cv];
   return true;
 }
@@ -194,6 +179,7 @@ void grow(const Graph& g, int seed, std::vector<uint8_t>& part) {
 void refine(const Graph& g, std::vector<uint8_t>& part, double imbalance) {
   const int64_t W = g.total_vw();
   const int64_t maxw = (int64_t)((0.5 + imbalance) * W) + 1;
+  int64_t cut = -1;  // the cut weight after the pass (its change is tracked by the moves: cur)
   for (int pass = 0; pass < 4; ++pass) {
     int64_t wside[2] = {0, 0};
     for (int v = 0; v < g.n; ++v) wside[part[v]] += g.vw[v];
@@ -240,7 +226,10 @@ void refine(const Graph& g, std::vector<uint8_t>& part, double imbalance) {
       }
     }
     for (size_t k = moves.size(); k > best_len; --k) part[moves[k - 1]] ^= 1;  // roll back
-    if (best == 0 || -best * 200 < cut_weight(g, part)) break;  // converged (< 0.5 % gain)
+    if (best == 0) break;
+    if (cut < 0) cut = cut_weight(g, part);  // once; then updated by each pass's kept moves
+    else cut += best;
+    if (-best * 200 < cut) break;  // converged (< 0.5 % gain)
   }
 }
 
@@ -305,8 +294,11 @@ void vertex_separator(const Graph& g, const std::vector<uint8_t>& part, std::vec
   // Hopcroft–Karp
   std::vector<int32_t> ml(nl, -1), mr(nr, -1), dist(nl);
   const int INF = 1 << 30;
+  std::vector<int32_t> bq;
+  bq.reserve(nl);
   auto bfs = [&]() {
-    std::vector<int32_t> q;
+    std::vector<int32_t>& q = bq;
+    q.clear();
     bool found = false;
     for (int a = 0; a < nl; ++a) {
       if (ml[a] == -1) {
@@ -335,7 +327,6 @@ void vertex_separator(const Graph& g, const std::vector<uint8_t>& part, std::vec
   std::vector<int32_t> stk;
   auto dfs = [&](int root) {  // iterative augmenting-path search along the BFS layers
     stk.assign(1, root);
-    std::vector<int32_t> via;
     while (!stk.empty()) {
       const int a = stk.back();
       bool advanced = false;

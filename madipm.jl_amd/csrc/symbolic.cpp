@@ -514,14 +514,15 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     // there it runs with kNdSeeds fixed seeds at once — each with a share of the analysis threads —
     // and the order with the fewest flops is kept (lowest seed on ties: the same choice whatever the
     // thread count).  ordering = auto adds AMD (one thread) beside ND and keeps the overall best; AMD
-    // is skipped above kBigAdj, where it is the slowest step of the analysis and ND wins anyway on
-    // the benchmark LPs (AMD vs ND flops: ex10 4.5e10 vs 2.6e8, supportcase10 6.0e8 vs 3.4e8, neos
-    // 4.2e11 vs 2.5e11).  Every candidate is analysed in full (etree + column counts).
+    // is skipped above kAmdMaxAdj, where it is the slowest step of the analysis (ex10: 0.62 s of AMD
+    // beside 0.4 s of ND on the threads) and ND wins anyway on the benchmark LPs (AMD vs ND flops:
+    // ex10 4.5e10 vs 2.6e8, supportcase10 6.0e8 vs 3.4e8, neos 4.2e11 vs 2.5e11).  Every candidate is
+    // analysed in full (etree + column counts).
     constexpr int kNdSeeds = 4;
-    constexpr int64_t kBigAdj = 4000000, kNdSeedsMaxAdj = 40000000;
+    constexpr int64_t kBigAdj = 4000000, kNdSeedsMaxAdj = 40000000, kAmdMaxAdj = 1000000;
     std::vector<int32_t> pa;
     const bool use_nd = opt.ordering != 1;
-    const bool use_amd = opt.ordering == 1 || (opt.ordering == 4 && Ap[N] <= kBigAdj);
+    const bool use_amd = opt.ordering == 1 || (opt.ordering == 4 && Ap[N] <= kAmdMaxAdj);
     const int nseeds = use_nd ? (Ap[N] > kBigAdj && Ap[N] <= kNdSeedsMaxAdj ? kNdSeeds : 1) : 0;
     std::vector<OrderAnalysis> B(nseeds);
     OrderAnalysis A;
@@ -1433,7 +1434,8 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     };
     struct FoldScratch {
       std::vector<int64_t> col0 = std::vector<int64_t>(32), col1 = std::vector<int64_t>(32);
-      std::vector<Prod> pr;
+      std::vector<Prod> pr, pr2;
+      std::vector<int64_t> cnt;
       std::vector<std::vector<uint32_t>> enc;
     };
     auto fold_front = [&](int s, FoldPart& P, FoldScratch& X) {
@@ -1543,7 +1545,17 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
             for (int b = wc; b <= a; ++b)  // rel ascending: parent row of b <= that of a
               pr.push_back({fidx(rl[a - wc], rl[b - wc]), qb0 + a, qb0 + b});
         }
-        std::stable_sort(pr.begin(), pr.end(), [](const Prod& x, const Prod& y) { return x.dst < y.dst; });
+        {  // counting sort by destination: stable (leaf order within a destination), O(products)
+          uint32_t dmax = 0;
+          for (const Prod& x : pr) dmax = std::max(dmax, x.dst);
+          auto& cnt = X.cnt;
+          cnt.assign((size_t)dmax + 2, 0);
+          for (const Prod& x : pr) cnt[x.dst + 1]++;
+          for (size_t k = 1; k < cnt.size(); ++k) cnt[k] += cnt[k - 1];
+          X.pr2.resize(pr.size());
+          for (const Prod& x : pr) X.pr2[cnt[x.dst]++] = x;
+          pr.swap(X.pr2);
+        }
         // NCH chunks of equal length (a run split where a cut falls), each encoded with its running
         // destination (SymbolicPlan: one word per entry, kFoldPad steps for jumps beyond 127)
         constexpr int NCH = NT_FOLD;
@@ -1596,28 +1608,69 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       for (int t = 1; t < T; ++t) th.emplace_back(worker);
       worker();
       for (auto& x : th) x.join();
+      stamp("10a: fold tables per front (threads)");
+      // the parts appended in front order: offsets by prefix sums, copies (with the shifts) on threads
+      std::vector<int64_t> om(ns_all + 1), oa(ns_all + 1), op(ns_all + 1), ob(ns_all + 1);
+      om[0] = (int64_t)S.mc_list.size();
+      oa[0] = (int64_t)S.ab_src0.size();
+      op[0] = (int64_t)S.fold_prod.size();
+      ob[0] = (int64_t)S.fold_bat.size();
+      const int64_t f0 = (int64_t)S.ab_first.size() - om[0], h0 = (int64_t)S.fold_chead.size() - ob[0] * NT_FOLD;
       for (int s = 0; s < ns_all; ++s) {
-        FoldPart& P = fparts[s];
-        const int32_t mbase = (int32_t)S.mc_list.size();
-        const int64_t abase = (int64_t)S.ab_src0.size(), pbase = (int64_t)S.fold_prod.size();
-        S.mc_list.insert(S.mc_list.end(), P.mc_list.begin(), P.mc_list.end());
-        for (int64_t v : P.ab_first) S.ab_first.push_back(v + abase);
-        S.ab_f0.insert(S.ab_f0.end(), P.ab_f0.begin(), P.ab_f0.end());
-        S.ab_wrc.insert(S.ab_wrc.end(), P.ab_wrc.begin(), P.ab_wrc.end());
-        S.ab_src0.insert(S.ab_src0.end(), P.ab_src0.begin(), P.ab_src0.end());
-        S.ab_src1.insert(S.ab_src1.end(), P.ab_src1.begin(), P.ab_src1.end());
-        for (int32_t v : P.ab_k) S.ab_k.push_back(v + mbase);
-        for (int32_t v : P.fold_bat) S.fold_bat.push_back(v + mbase);
-        for (int64_t v : P.fold_row0) S.fold_row0.push_back(v + abase);
-        for (int64_t v : P.fold_poff) S.fold_poff.push_back(v + pbase);
-        S.fold_plen.insert(S.fold_plen.end(), P.fold_plen.begin(), P.fold_plen.end());
-        S.fold_prod.insert(S.fold_prod.end(), P.fold_prod.begin(), P.fold_prod.end());
-        S.fold_chead.insert(S.fold_chead.end(), P.fold_chead.begin(), P.fold_chead.end());
-        S.mc_ptr[s + 1] = (int32_t)S.mc_list.size();
-        S.fold_bptr[s + 1] = (int32_t)S.fold_bat.size();
-        FoldPart().mc_list.swap(P.mc_list);
-        std::vector<uint32_t>().swap(P.fold_prod);
+        const FoldPart& P = fparts[s];
+        om[s + 1] = om[s] + (int64_t)P.mc_list.size();
+        oa[s + 1] = oa[s] + (int64_t)P.ab_src0.size();
+        op[s + 1] = op[s] + (int64_t)P.fold_prod.size();
+        ob[s + 1] = ob[s] + (int64_t)P.fold_bat.size();
+        S.mc_ptr[s + 1] = (int32_t)om[s + 1];
+        S.fold_bptr[s + 1] = (int32_t)ob[s + 1];
       }
+      S.mc_list.resize(om[ns_all]);
+      S.ab_first.resize(f0 + om[ns_all]);
+      S.ab_f0.resize(om[ns_all]);
+      S.ab_wrc.resize(om[ns_all]);
+      S.ab_src0.resize(oa[ns_all]);
+      S.ab_src1.resize(oa[ns_all]);
+      S.ab_k.resize(oa[ns_all]);
+      S.fold_bat.resize(ob[ns_all]);
+      S.fold_row0.resize(ob[ns_all]);
+      S.fold_poff.resize(ob[ns_all]);
+      S.fold_plen.resize(ob[ns_all]);
+      S.fold_chead.resize(h0 + ob[ns_all] * NT_FOLD);
+      S.fold_prod.resize(op[ns_all]);
+      next = 0;
+      auto copier = [&] {
+        for (int s0; (s0 = next.fetch_add(64)) < ns_all;)
+          for (int s = s0; s < std::min(ns_all, s0 + 64); ++s) {
+            FoldPart& P = fparts[s];
+            const int32_t mbase = (int32_t)om[s];
+            const int64_t abase = oa[s], pbase = op[s], m = om[s], bb = ob[s];
+            for (size_t k = 0; k < P.mc_list.size(); ++k) {
+              S.mc_list[m + k] = P.mc_list[k];
+              S.ab_first[f0 + m + k] = P.ab_first[k] + abase;
+              S.ab_f0[m + k] = (int32_t)P.ab_f0[k];
+              S.ab_wrc[m + k] = P.ab_wrc[k];
+            }
+            for (size_t k = 0; k < P.ab_src0.size(); ++k) {
+              S.ab_src0[abase + k] = P.ab_src0[k];
+              S.ab_src1[abase + k] = P.ab_src1[k];
+              S.ab_k[abase + k] = P.ab_k[k] + mbase;
+            }
+            for (size_t k = 0; k < P.fold_bat.size(); ++k) {
+              S.fold_bat[bb + k] = P.fold_bat[k] + mbase;
+              S.fold_row0[bb + k] = P.fold_row0[k] + abase;
+              S.fold_poff[bb + k] = P.fold_poff[k] + pbase;
+              S.fold_plen[bb + k] = P.fold_plen[k];
+            }
+            std::copy(P.fold_chead.begin(), P.fold_chead.end(), S.fold_chead.begin() + h0 + bb * NT_FOLD);
+            std::copy(P.fold_prod.begin(), P.fold_prod.end(), S.fold_prod.begin() + pbase);
+            P = FoldPart();
+          }
+      };
+      th.clear();
+      for (int t = 1; t < T; ++t) th.emplace_back(copier);
+      copier();
+      for (auto& x : th) x.join();
     }
     S.ab_first.push_back((int64_t)S.ab_src0.size());
     // sentinels: the batch after a front's last one starts at that front's end (leaves and rows are
