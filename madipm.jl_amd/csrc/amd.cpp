@@ -50,10 +50,10 @@ int64_t tree_dfs(int j, int64_t k, std::vector<int32_t>& head, const std::vector
 
 }  // namespace
 
-void amd_order(int n, const std::vector<int64_t>& Ap, const std::vector<int32_t>& Ai,
-               std::vector<int32_t>& perm, double dense_alpha) {
+bool amd_order(int n, const std::vector<int64_t>& Ap, const std::vector<int32_t>& Ai,
+               std::vector<int32_t>& perm, double dense_alpha, const std::atomic<double>* cap) {
   perm.assign(n, 0);
-  if (n == 0) return;
+  if (n == 0) return true;
   const int64_t nz = Ap[n];
   int64_t dense = (int64_t)std::max(16.0, dense_alpha * std::sqrt((double)n));
   dense = std::min<int64_t>(n - 2, dense);
@@ -109,6 +109,10 @@ void amd_order(int n, const std::vector<int64_t>& Ap, const std::vector<int32_t>
   }
 
   int64_t mindeg = 0, lemax = 0;
+  // flops lower bound of the pivots eliminated so far: pivot k's element Lk is its exact pattern
+  // (dense nodes left out: they only add), so its nvk columns count dk + nvk, ..., dk + 1 entries
+  double lb = 0.0;
+  int64_t npiv = 0;
   while (nel < n) {
     // ---- select a node of minimum approximate degree
     int k = -1;
@@ -301,6 +305,15 @@ void amd_order(int n, const std::vector<int64_t>& Ap, const std::vector<int32_t>
       iw[q++] = i;
     }
     nv[k] = (int32_t)nvk;
+    if (cap) {
+      const double a = (double)dk + 1.0, b = (double)(dk + nvk);  // sum over c in [a, b] of c^2 + c - 2
+      auto s2 = [](double x) { return x * (x + 1.0) * (2.0 * x + 1.0) / 6.0; };
+      lb += (s2(b) - s2(a - 1.0)) + (b * (b + 1.0) - (a - 1.0) * a) / 2.0 - 2.0 * (b - a + 1.0);
+      if ((++npiv & 255) == 0 && lb > cap->load(std::memory_order_relaxed)) {
+        perm.clear();
+        return false;
+      }
+    }
     if ((len[k] = (int32_t)(q - pk1)) == 0) {
       pe[k] = -1;
       w[k] = 0;
@@ -333,6 +346,7 @@ void amd_order(int n, const std::vector<int64_t>& Ap, const std::vector<int32_t>
   int64_t o = 0;
   for (int64_t t = 0; t <= n && o < n; ++t)
     if (post[t] != n) perm[o++] = post[t];
+  return true;
 }
 
 }  // namespace madipm

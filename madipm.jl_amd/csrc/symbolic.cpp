@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <thread>
 #include <atomic>
+#include <limits>
 #include <memory>
 
 #include "common.hpp"
@@ -514,15 +515,17 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     // there it runs with kNdSeeds fixed seeds at once — each with a share of the analysis threads —
     // and the order with the fewest flops is kept (lowest seed on ties: the same choice whatever the
     // thread count).  ordering = auto adds AMD (one thread) beside ND and keeps the overall best; AMD
-    // is skipped above kAmdMaxAdj, where it is the slowest step of the analysis (ex10: 0.62 s of AMD
-    // beside 0.4 s of ND on the threads) and ND wins anyway on the benchmark LPs (AMD vs ND flops:
-    // ex10 4.5e10 vs 2.6e8, supportcase10 6.0e8 vs 3.4e8, neos 4.2e11 vs 2.5e11).  Every candidate is
-    // analysed in full (etree + column counts).
+    // is skipped above kBigAdj, where it is the slowest step of the analysis and ND wins anyway on
+    // the benchmark LPs (AMD vs ND flops: ex10 4.5e10 vs 2.6e8, supportcase10 6.0e8 vs 3.4e8, neos
+    // 4.2e11 vs 2.5e11; the neos stand-in at scale 0.1: AMD 1.9e10 vs ND 3.6e10).  Once ND's order is
+    // analysed, AMD stops as soon as a lower bound of its flops exceeds ND's (amd_order's cap: it
+    // could only lose — the choice is the one without the stop; ex10's AMD took 0.62 s beside ~0.4 s
+    // of ND).  Every candidate is analysed in full (etree + column counts).
     constexpr int kNdSeeds = 4;
-    constexpr int64_t kBigAdj = 4000000, kNdSeedsMaxAdj = 40000000, kAmdMaxAdj = 1000000;
+    constexpr int64_t kBigAdj = 4000000, kNdSeedsMaxAdj = 40000000;
     std::vector<int32_t> pa;
     const bool use_nd = opt.ordering != 1;
-    const bool use_amd = opt.ordering == 1 || (opt.ordering == 4 && Ap[N] <= kAmdMaxAdj);
+    const bool use_amd = opt.ordering == 1 || (opt.ordering == 4 && Ap[N] <= kBigAdj);
     const int nseeds = use_nd ? (Ap[N] > kBigAdj && Ap[N] <= kNdSeedsMaxAdj ? kNdSeeds : 1) : 0;
     std::vector<OrderAnalysis> B(nseeds);
     OrderAnalysis A;
@@ -541,13 +544,21 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       analyse_order(N, colptr, rowval, std::move(pn), B[k]);
     };
     std::vector<std::thread> th;
+    std::atomic<double> amd_cap{std::numeric_limits<double>::infinity()};
+    bool amd_done = true;
     if (use_amd)
       th.emplace_back([&] {
-        amd_order(N, Ap, Ai, pa, opt.dense_alpha);
-        analyse_order(N, colptr, rowval, std::move(pa), A);
+        amd_done = amd_order(N, Ap, Ai, pa, opt.dense_alpha, use_nd ? &amd_cap : nullptr);
+        if (amd_done)
+          analyse_order(N, colptr, rowval, std::move(pa), A);
+        else
+          A.flops = std::numeric_limits<double>::infinity();  // stopped: it could not beat ND
       });
     for (int k = 1; k < nseeds; ++k) th.emplace_back(run_nd, k);
-    if (nseeds) run_nd(0);
+    if (nseeds) {
+      run_nd(0);
+      if (nseeds == 1) amd_cap.store(B[0].flops);  // (seeds > 1: no AMD, kBigAdj)
+    }
     for (auto& x : th) x.join();
     stamp("1: orderings (ND seeds, AMD) + analysis");
     std::vector<int64_t>().swap(Ap);
@@ -1351,6 +1362,8 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   {
     const char* ev = std::getenv("MADIPM_TREE_FACT");
     const bool on = opt.fact_tree && !(ev && ev[0] == '0');
+    int fanin_max = SymbolicPlan::kFactTreeFanIn;
+    if (const char* e = std::getenv("MADIPM_TREE_FANIN")) fanin_max = std::atoi(e);  // A/B knob
     std::vector<char> lbpar(ns, 0);
     for (const auto& g : S.lb) lbpar[g.parent] = 1;
     for (int s = 0; on && s < ns; ++s) {  // postorder: children first
@@ -1363,7 +1376,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         fanin += S.ftree[c];
         ok = S.ftree[c] || (S.child_ptr[c] == S.child_ptr[c + 1] && S.nrows[c] <= 32 && !lb_member(c));
       }
-      S.ftree[s] = ok && fanin <= SymbolicPlan::kFactTreeFanIn;
+      S.ftree[s] = ok && fanin <= fanin_max;
     }
   }
   // leaf folding (SymbolicPlan::absorb): a tree front whose pre-leaf children are all micro leaves

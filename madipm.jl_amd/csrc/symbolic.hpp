@@ -8,12 +8,16 @@
 #pragma once
 
 #include <cstdint>
+#include <atomic>
 #include <vector>
 
 namespace madipm {
 
-void amd_order(int n, const std::vector<int64_t>& Ap, const std::vector<int32_t>& Ai,
-               std::vector<int32_t>& perm, double dense_alpha = 10.0);
+// cap (optional): AMD stops early — returns false, perm empty — once a lower bound of its order's
+// flops (sum (c - 1)(c + 2) over the column counts of the pivots eliminated so far) exceeds *cap, i.e.
+// once it can no longer beat an order of *cap flops
+bool amd_order(int n, const std::vector<int64_t>& Ap, const std::vector<int32_t>& Ai,
+               std::vector<int32_t>& perm, double dense_alpha = 10.0, const std::atomic<double>* cap = nullptr);
 
 struct NDOptions {
   int leaf_size = 256;       // subgraphs up to this size are ordered by AMD
