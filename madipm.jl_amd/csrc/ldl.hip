@@ -816,12 +816,21 @@ __device__ __forceinline__ void f16r_step(double (&a)[4], double (&x)[4], double
   const double dt = readlane_f64(a[mt], T + 16 * gt);
   const double ci = xrow_bcast<gt>(a[mt]);
   const double li = (i > T) ? (RCP ? ci * recip_nr(dt) : ci / dt) : 0.0;  // IEEE quotient unless RCP
+  // A(i, j) -= l_i A(t, j) for j > t; X(i, j) -= l_i X(t, j) for j <= t (a zero multiplier elsewhere:
+  // exact, the products are finite); the column ranges are static except for one register.  The
+  // register holding the next pivot column goes first and the X updates (off the pivot chain) last:
+  // the waves issue in order, so the next step's readlane then finds its operand ready (the same
+  // operations as before, in another order: bitwise the same factor)
+  constexpr int mn = (T + 1 < 16) ? ((T + 1) >> 2) : -1;
+  if constexpr (mn >= 0) fmac_row_bcast<T>(a[mn], (4 * mn + g > T) ? -li : 0.0);
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
     const int j = 4 * m + g;
-    // A(i, j) -= l_i A(t, j) for j > t; X(i, j) -= l_i X(t, j) for j <= t (a zero multiplier elsewhere:
-    // exact, the products are finite); the column ranges are static except for one register
-    if (4 * m + 3 > T) fmac_row_bcast<T>(a[m], (j > T) ? -li : 0.0);
+    if (m != mn && 4 * m + 3 > T) fmac_row_bcast<T>(a[m], (j > T) ? -li : 0.0);
+  }
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int j = 4 * m + g;
     if (4 * m <= T) fmac_row_bcast<T>(x[m], (j <= T) ? -li : 0.0);
   }
   if (i == T) dmine = dt;
@@ -1370,6 +1379,11 @@ __device__ __forceinline__ void factor_lds(const FrontTab& T, double* A, int r, 
 // pivot check.  SC1: U stored write-through (handed to a parent inside the same launch).
 template <bool PK, bool SC1>
 __device__ __forceinline__ void writeout_u(const double* A, int r, int w, int ld, double* Uo, int uld);
+// offset of column b of a u x u update block: square ld uld, or packed lower (uld == 0: column b
+// holds rows b .. u - 1, entry (a, b) at b (2u - b - 1) / 2 + a)
+__device__ __forceinline__ int64_t ucol_off(int b, int u, int64_t uld) {
+  return uld ? (int64_t)b * uld : ((int64_t)b * (2 * u - b - 1)) >> 1;
+}
 template <bool PK>
 __device__ __forceinline__ void writeout_ld(const double* A, int r, int w, int ld, const double* Dl, double* L, double* D,
                                            int f0, LDLStatus* st, double tol) {
@@ -1451,7 +1465,7 @@ __device__ __forceinline__ void writeout_u_cols(const double* A, int r, int w, i
 #pragma unroll
     for (int cb = 0; cb < NC; ++cb) {
       const int b = b0 + cb;
-      double* col = Uo + (int64_t)b * uld;
+      double* col = Uo + ucol_off(b, u, uld);
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
         const int a = b + lane + 64 * h;
@@ -1552,8 +1566,8 @@ __global__ __launch_bounds__(SBT) void k_small_blocked(FrontTab T, const int32_t
 // A tree front folds its micro-leaf children (w <= 2, r <= 32; SymbolicPlan::absorb) into its LDS
 // front instead of k_micro_factor writing their update blocks to HBM and the gather pre-assembly
 // summing them.  Per batch of leaves: (1) thread per leaf row gathers the row's entries of the leaf's
-// two columns from the caller's K values; (2) thread per leaf: pivots d0, l10, d1; (3) thread per
-// leaf row: its l (and l d) in LDS; (4) the product list: thread t walks its chunk of destination-sorted products
+// two columns from the caller's K values; (2) thread per leaf row: the leaf's pivots d0, l10, d1 (from
+// its first two rows) and the row's l (and l d) in LDS; (3) the product list: thread t walks its chunk of destination-sorted products
 // F(i, j) -= l0(q1) l0(q2) d0 + l1(q1) l1(q2) d1, one partial sum per destination run, so every
 // entry of F has one writer and a fixed order (leaf order) — no atomics, balanced by product count
 // whatever the row density.
@@ -1582,7 +1596,7 @@ __device__ __forceinline__ FoldBatchTab& fold_batch_tab() {
 // cval / cdst: per thread, the parked sum and destination of a chunk's first run when it continues
 // the left neighbour's run (k_fact_tree's MK / cbuf, idle during the fold)
 template <bool PK>
-__device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A, const double* Kx, double* arena,
+__device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, int r, int ld, double* A, const double* Kx, double* arena,
                                             double* D, LDLStatus* st, double tol, double* ext, double* cval,
                                             int32_t* cdst, int64_t* fdg) {
   int64_t tph[4] = {0, 0, 0, 0}, tc = fdg ? wall_clock64() : 0;
@@ -1598,10 +1612,8 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
   const int RM = T.fold_rmax[s], LM = T.fold_lmax[s];
   double2* LQ = reinterpret_cast<double2*>(ext);  // per batch row: K values of columns 0/1, then (l0, l1)
   double2* PQ = LQ + RM;                          // (l0 d0, l1 d1)
-  double* pd0 = reinterpret_cast<double*>(PQ + RM);
-  double* pd1 = pd0 + LM;
-  double* pf10 = pd1 + LM;
-  int64_t* ploff = reinterpret_cast<int64_t*>(pf10 + LM);
+  int32_t* pf0 = reinterpret_cast<int32_t*>(PQ + RM);     // per leaf: first pivot (in 3 LM doubles of carve)
+  int64_t* ploff = reinterpret_cast<int64_t*>(reinterpret_cast<double*>(pf0) + 3 * LM);
   int32_t* prow0 = reinterpret_cast<int32_t*>(ploff + LM);  // batch-local first row of the leaf
   int32_t* pwrc = prow0 + LM;
   int32_t* kk = pwrc + LM;                                   // per batch row: batch-local leaf
@@ -1616,15 +1628,15 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
   FoldBatchTab& ft = fold_batch_tab();
   int32_t *tb_k = ft.k, *tb_pl = ft.pl;
   int64_t *tb_j = ft.j, *tb_po = ft.po;
+  int32_t rk = 0, rpl = 0;
+  int64_t rj = 0, rpo = 0;
   if (tid <= nb) {
     const int bq = b0 + tid, bc = min(bq, b0 + nb - 1);  // the sentinel entry (tid == nb) is the next batch's start
-    const int32_t k = T.fold_bat[bq], pl = T.fold_plen[bc];
-    const int64_t j = T.fold_row0[bq], po = T.fold_poff[bc];
-    tb_k[tid] = k;
-    tb_j[tid] = j;
-    if (tid < nb) tb_po[tid] = po, tb_pl[tid] = pl;
+    rk = T.fold_bat[bq];
+    rpl = T.fold_plen[bc];
+    rj = T.fold_row0[bq];
+    rpo = T.fold_poff[bc];
   }
-  __syncthreads();
   // product entries (SymbolicPlan::fold_prod): thread t walks chunk t, GP entries per group
   constexpr uint32_t PAD = SymbolicPlan::kFoldPad;
   uint32_t e[GP];
@@ -1635,7 +1647,6 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
       g[u] = (kk < len) ? P[(int64_t)kk * FTN] : PAD;
     }
   };
-  load_group(e, T.fold_prod + tb_po[0] + tid, 0, tb_pl[0]);
   // the leaf rows' K entries of batch b + 1 are loaded into registers during batch b (indices before
   // its pivots, values before its products) and stored after its products: only batch 0's gather is
   // exposed (r3: every batch's gather, two dependent round trips, lay on the front's critical path).
@@ -1664,8 +1675,57 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
       if (q < nrow) LQ[q] = double2{va[u], vb[u]};
     }
   };
-  gather_idx(tb_j[0], (int)(tb_j[1] - tb_j[0]), 0);
+  // the leaf tables (first row, w | rc, L offset, first pivot) of batch b + 1 are loaded during batch
+  // b's L and product phases (after batch b's pivots consumed them): no exposed round trip in the
+  // gather and pivot phases (r5: two per batch, ~3 us of the level-2 fronts' ~13 us per batch)
+  int64_t laf[2], llo[2];
+  int32_t lwr[2], lf0[2];
+  auto leaf_tab = [&](int kb, int nl) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = tid + h * FTN;
+      const bool ok = k < nl;
+      laf[h] = ok ? T.ab_first[kb + k] : 0;
+      lwr[h] = ok ? T.ab_wrc[kb + k] : 0;
+      llo[h] = ok ? T.ab_loff[kb + k] : 0;
+      lf0[h] = ok ? T.ab_f0[kb + k] : 0;
+    }
+  };
+  // batch 0's leaf tables, first gather pass and first product group (its table entries as uniform
+  // loads) and this front's original K entries, all in one round trip; their K values (the leaf rows'
+  // and the front's own) in a second — the zero fill of the front beside them
+  if (nb > 0) {
+    const int kq0 = T.fold_bat[b0];
+    const int64_t r0 = T.fold_row0[b0], r1 = T.fold_row0[b0 + 1];
+    leaf_tab(kq0, T.fold_bat[b0 + 1] - kq0);
+    gather_idx(r0, (int)(r1 - r0), 0);
+    load_group(e, T.fold_prod + T.fold_poff[b0] + tid, 0, T.fold_plen[b0]);
+  } else {
+    gather_idx(0, 0, 0);  // no leaves: no loads
+  }
+  const int64_t qa = T.asm_ptr[s] + tid, qe = T.asm_ptr[s + 1];
+  const bool a0 = qa < qe;
+  const int ad = a0 ? (int)T.asm_dst[qa] : 0;
+  const int64_t as = a0 ? T.asm_src[qa] : 0;
+  const int ntot = PK ? r * (r + 1) / 2 : r * ld;
+  for (int q = tid; q < ntot; q += FTN) A[q] = 0.0;
+  const double av = a0 ? Kx[as] : 0.0;
   gather_val();
+  if (tid <= nb) {
+    tb_k[tid] = rk;
+    tb_j[tid] = rj;
+    if (tid < nb) tb_po[tid] = rpo, tb_pl[tid] = rpl;
+  }
+  __syncthreads();  // the zero fill
+  if (a0) {
+    const int dj = ad / r;  // d < r^2: 32-bit division
+    A[fidx<PK>(ad - dj * r, dj, r, ld)] = av;
+  }
+  for (int64_t q = qa + FTN; q < qe; q += FTN) {
+    const int d = (int)T.asm_dst[q], dj = d / r;
+    A[fidx<PK>(d - dj * r, dj, r, ld)] = Kx[T.asm_src[q]];
+  }
+  __syncthreads();  // the batch table and the original entries
   for (int b = 0; b < nb; ++b) {
     const int k0 = tb_k[b], k1 = tb_k[b + 1];
     const int64_t j0 = tb_j[b];
@@ -1674,60 +1734,44 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
       if (tid == 0) __hip_atomic_fetch_or(T.err, kErrLdsCarve, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;  // (uniform: the batch table is in LDS)
     }
-    // (1) the leaf rows' K entries (the first pass in registers already; leaf tables loaded beside them)
-    int32_t lf[2], lw[2];
-    int64_t lo[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int k = tid + h * FTN;
-      lf[h] = (k < nleaf) ? (int32_t)(T.ab_first[k0 + k] - j0) : 0;
-      lw[h] = (k < nleaf) ? T.ab_wrc[k0 + k] : 0;
-      lo[h] = (k < nleaf) ? T.ab_loff[k0 + k] : 0;
-    }
+    // (1) the leaf rows' K entries (the first pass and the leaf tables in registers already)
     gather_store(nrow, 0);
     for (int q0 = RPT * FTN; q0 < nrow; q0 += RPT * FTN) {
       gather_idx(j0, nrow, q0);
       gather_val();
       gather_store(nrow, q0);
     }
-    for (int k = tid, h = 0; k < nleaf; k += FTN, ++h) {
-      const int q0 = (h == 0) ? lf[0] : (h == 1 ? lf[1] : (int)(T.ab_first[k0 + k] - j0));
-      const int wrc = (h == 0) ? lw[0] : (h == 1 ? lw[1] : T.ab_wrc[k0 + k]);
-      prow0[k] = q0;
-      pwrc[k] = wrc;
-      ploff[k] = (h == 0) ? lo[0] : (h == 1 ? lo[1] : T.ab_loff[k0 + k]);
-      for (int i = 0; i < (wrc >> 8); ++i) kk[q0 + i] = k;
-    }
-    __syncthreads();
-    lap(0);
-    const bool pre = b + 1 < nb;  // prefetch the next batch's first pass
-    if (pre) gather_idx(tb_j[b + 1], (int)(tb_j[b + 2] - tb_j[b + 1]), 0);
-    // (2) per leaf: pivots (+ D and the pivot check)
-    for (int k = tid; k < nleaf; k += FTN) {
-      const int f0 = T.ab_f0[k0 + k], wrc = pwrc[k], w = wrc & 255, rc = wrc >> 8;
-      const int jf = prow0[k];
-      const double d0 = LQ[jf].x;
-      const double f10 = (rc > 1) ? LQ[jf + 1].x : 0.0;
-      const double l10 = (w == 2) ? f10 / d0 : 0.0;
-      const double d1 = (w == 2) ? LQ[jf + 1].y - l10 * f10 : 0.0;
-      pd0[k] = d0;
-      pd1[k] = d1;
-      pf10[k] = f10;
-      D[f0] = d0;
-      if (bad_pivot(d0, tol)) atomicMin(&st->fail_pivot, f0 + 1);
-      if (w == 2) {
-        D[f0 + 1] = d1;
-        if (bad_pivot(d1, tol)) atomicMin(&st->fail_pivot, f0 + 2);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = tid + h * FTN;
+      if (k < nleaf) {
+        const int q0 = (int)(laf[h] - j0), wrc = lwr[h];
+        prow0[k] = q0;
+        pwrc[k] = wrc;
+        ploff[k] = llo[h];
+        pf0[k] = lf0[h];
+        for (int i = 0; i < (wrc >> 8); ++i) kk[q0 + i] = k;
       }
     }
     __syncthreads();
+    lap(0);
+    const bool pre = b + 1 < nb;  // prefetch the next batch's first pass and leaf tables
+    if (pre) {
+      gather_idx(tb_j[b + 1], (int)(tb_j[b + 2] - tb_j[b + 1]), 0);
+      leaf_tab(tb_k[b + 1], tb_k[b + 2] - tb_k[b + 1]);
+    }
     lap(1);
-    // (3) per leaf row: L entries (HBM panel for the solves: d on the diagonal, zero above; LDS: l
-    // and l d of the update rows)
+    // (2) per leaf row: the leaf's pivots from its first two rows (rows i < w, never rewritten here;
+    // every row's thread forms them itself: no per-leaf phase and barrier), then its L entries (HBM
+    // panel for the solves: d on the diagonal, zero above; LDS: l and l d of the update rows); the
+    // first row's thread stores D and checks the pivots
     for (int q = tid; q < nrow; q += FTN) {
       const int k = kk[q];
-      const int wrc = pwrc[k], w = wrc & 255, rc = wrc >> 8, i = q - prow0[k];
-      const double d0 = pd0[k], d1 = pd1[k], f10 = pf10[k];
+      const int wrc = pwrc[k], w = wrc & 255, rc = wrc >> 8, jf = prow0[k], i = q - jf;
+      const double2 r0 = LQ[jf], r1 = (w == 2) ? LQ[jf + 1] : double2{0.0, 0.0};
+      const double d0 = r0.x, f10 = r1.x;
+      const double l10 = (w == 2) ? f10 / d0 : 0.0;
+      const double d1 = (w == 2) ? r1.y - l10 * f10 : 0.0;
       double* __restrict__ L = arena + ploff[k];
       if (i >= w) {
         const double2 a = LQ[q];
@@ -1740,15 +1784,22 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, double* A,
       } else if (i == 0) {
         L[0] = d0;
         if (w == 2) L[rc] = 0.0;
+        const int f0 = pf0[k];
+        D[f0] = d0;
+        if (bad_pivot(d0, tol)) atomicMin(&st->fail_pivot, f0 + 1);
+        if (w == 2) {
+          D[f0 + 1] = d1;
+          if (bad_pivot(d1, tol)) atomicMin(&st->fail_pivot, f0 + 2);
+        }
       } else {  // i == 1, w == 2
-        L[1] = f10 / d0;
+        L[1] = l10;
         L[1 + rc] = d1;
       }
     }
     __syncthreads();
     lap(2);
     if (pre) gather_val();
-    // (4) this thread's chunk of the destination-sorted products (entry k at FTN k + tid: each load
+    // (3) this thread's chunk of the destination-sorted products (entry k at FTN k + tid: each load
     // instruction is coalesced)
     const uint32_t* __restrict__ P = T.fold_prod + tb_po[b] + tid;
     const int len = tb_pl[b];
@@ -1845,7 +1896,7 @@ __device__ __forceinline__ void push_cols(double* A, int r, int ld, const double
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
         const int ac = min(b0 + cb + lane + 64 * h, uc - 1);
-        x[cb][h] = __hip_atomic_load(U + ac + (int64_t)bc * uld, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        x[cb][h] = __hip_atomic_load(U + ac + ucol_off(bc, uc, uld), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     // then the destinations (relative indices in LDS) and the read-modify-writes
@@ -1898,14 +1949,7 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
   }
   if (T.absorb[s]) {  // original entries, then the micro-leaf children folded in LDS
     const int ntot = PK ? r * (r + 1) / 2 : r * ld;
-    for (int q = tid; q < ntot; q += FTN) A[q] = 0.0;
-    __syncthreads();
-    for (int64_t q = T.asm_ptr[s] + tid; q < T.asm_ptr[s + 1]; q += FTN) {
-      const int d = (int)T.asm_dst[q], dj = d / r;  // d < r^2: 32-bit division
-      A[fidx<PK>(d - dj * r, dj, r, ld)] = Kx[T.asm_src[q]];
-    }
-    __syncthreads();
-    fold_leaves<PK>(T, s, A, Kx, arena, D, st, tol, A + ((ntot + 1) & ~1), cbuf, reinterpret_cast<int32_t*>(MK),
+    fold_leaves<PK>(T, s, r, ld, A, Kx, arena, D, st, tol, A + ((ntot + 1) & ~1), cbuf, reinterpret_cast<int32_t*>(MK),
                     dg ? dg + 16 : nullptr);  // 16-byte aligned
   } else {  // pre-assembled as the LDS image: a straight copy, 16 loads in flight per thread
     const double* __restrict__ src = fscratch + T.fs_off[s];
@@ -2078,7 +2122,7 @@ __device__ __forceinline__ void fact_med_front(const FrontTab& T, int s, const i
         const int e = min(base + k * FTN + tid, ne - 1);
         const int b = e / uc, a = e - b * uc;
         const bool ok = base + k * FTN + tid < ne && a >= b;
-        x[k] = __hip_atomic_load(U + a + (int64_t)b * uld, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        x[k] = __hip_atomic_load(U + max(a, b) + ucol_off(b, uc, uld), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         dst[k] = ok ? (int64_t)rl[a] + (int64_t)rl[b] * r : -1;
       }
 #pragma unroll
@@ -2618,21 +2662,32 @@ __global__ __launch_bounds__(NT, SYRK_WAVES) void k_lb_syrk(const double* __rest
 // 16x16x4, K-chunks of 16 double-buffered through LDS (k_lb_syrk's engine on the front's own columns).
 // A 128-tile reads 2 x 128 K doubles per 2 x 128^2 K flops — twice k_big_update's 64-tile arithmetic
 // intensity, on the update that carries ~90 % of neos' factorisation flops.
+// Split K (nsplit > 1, launches of few tiles: one workgroup per CU ran each tile's K chain with its
+// loads exposed, ~67 us per tile whatever the launch size on neos): workgroup blockIdx.x takes part
+// blockIdx.x % nsplit of tile blockIdx.x / nsplit's K range (16-column chunks), stores its partial
+// product write-through (psum), and the last part to take the tile's ticket sums the partials in part
+// order (fixed: bitwise reproducible), then runs the epilogue (and the lookahead of tile (0, 0)).
+constexpr int UPD_PART = 4 * 4 * 4 * NT;  // partial product doubles of one part (acc of every thread)
 __global__ __launch_bounds__(NT, 2) void k_big_upd128(FrontTab T, const int32_t* __restrict__ list, int step, int kpan,
                                                      double* __restrict__ arena, double* __restrict__ D,
-                                                     double* __restrict__ Mbuf, LDLStatus* st, double tol) {
+                                                     double* __restrict__ Mbuf, LDLStatus* st, double tol,
+                                                     int nsplit, double* __restrict__ psum, int32_t* ptick) {
   // one buffer: As[2] then Bs[2]; after the MFMAs task (0, 0) reuses it for the lookahead diagonal block
   __shared__ __attribute__((aligned(16))) double AB[4 * SYK * SYLD];
+  __shared__ int s_last;
   double (*As)[SYK * SYLD] = reinterpret_cast<double (*)[SYK * SYLD]>(AB);           // (L D)[I rows]
   double (*Bs)[SYK * SYLD] = reinterpret_cast<double (*)[SYK * SYLD]>(AB + 2 * SYK * SYLD);  // L[J rows]
   static_assert(64 * LDA + 4 * 16 * LDM + 64 <= 4 * SYK * SYLD, "lookahead diagonal block aliases As / Bs");
-  int s, tij;
-  task_of(list, s, tij);
+  const int tile = blockIdx.x / nsplit, part = blockIdx.x - tile * nsplit;
+  const int2 task = reinterpret_cast<const int2*>(list)[tile];
+  const int s = task.x, tij = task.y;
   const int ti = tij & 0xffff, tj = (tij >> 16) & 0x7fff;
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
   const int g0 = (step / kpan) * kpan;
-  const int k0 = 64 * g0, k1 = min(64 * (g0 + kpan), w);  // K range = the group's columns
-  const int c0 = k1;
+  const int kg0 = 64 * g0, k1g = min(64 * (g0 + kpan), w);  // K range = the group's columns
+  const int c0 = k1g;
+  const int kps = ((k1g - kg0 + nsplit - 1) / nsplit + SYK - 1) / SYK * SYK;  // this part's K columns
+  const int k0 = min(kg0 + part * kps, k1g), k1 = min(k0 + kps, k1g);
   const int I0 = c0 + ti * SYT, J0 = c0 + tj * SYT;
   double* __restrict__ F = arena + T.l_off[s];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -2663,31 +2718,71 @@ __global__ __launch_bounds__(NT, 2) void k_big_upd128(FrontTab T, const int32_t*
       Bs[buf][(lk + 2 * q) * SYLD + lr] = (ok && J0 + lr < r) ? rb[q] : 0.0;
     }
   };
-  gload(k0);
-  sstore(k0, 0);
-  __syncthreads();
-  int buf = 0;
-  for (int kb = k0; kb < k1; kb += SYK) {
-    const bool more = kb + SYK < k1;
-    if (more) gload(kb + SYK);
+  if (k0 < k1) {  // (a split part past the group's K has nothing to multiply)
+    gload(k0);
+    sstore(k0, 0);
+    __syncthreads();
+    int buf = 0;
+    for (int kb = k0; kb < k1; kb += SYK) {
+      const bool more = kb + SYK < k1;
+      if (more) gload(kb + SYK);
 #pragma unroll
-    for (int k4 = 0; k4 < SYK / 4; ++k4) {
-      const int kk = 4 * k4 + (lane >> 4);
-      double fa[4], fb[4];
+      for (int k4 = 0; k4 < SYK / 4; ++k4) {
+        const int kk = 4 * k4 + (lane >> 4);
+        double fa[4], fb[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        fa[t] = Bs[buf][kk * SYLD + wn + 16 * t + (lane & 15)];
-        fb[t] = As[buf][kk * SYLD + wm + 16 * t + (lane & 15)];
+        for (int t = 0; t < 4; ++t) {
+          fa[t] = Bs[buf][kk * SYLD + wn + 16 * t + (lane & 15)];
+          fb[t] = As[buf][kk * SYLD + wm + 16 * t + (lane & 15)];
+        }
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[a], fb[b], acc[a][b], 0, 0, 0);
+      }
+      if (more) {
+        sstore(kb + SYK, buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+      }
+    }
+  }
+  if (nsplit > 1) {  // the tile's parts: partials write-through, the last part sums them in part order
+    double* __restrict__ mine = psum + ((int64_t)tile * nsplit + part) * UPD_PART;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) st_sc1(mine + ((a * 4 + b) * 4 + g) * NT + tid, acc[a][b][g]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+      s_last = __hip_atomic_fetch_add(ptick + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsplit - 1;
+    __syncthreads();
+    if (!s_last) return;
+    if (tid == 0) ptick[tile] = 0;  // every part has taken its ticket: ready for the next launch
+    // the sum in part order, every part (this one's too) read back: 8 values of every part per round,
+    // all 32 loads in flight (unconditional, the part index clamped; a load per value in a runtime
+    // loop compiled to one memory round trip per load)
+    const double* __restrict__ all = psum + (int64_t)tile * nsplit * UPD_PART;
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+      double pv[4][8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double* pq = all + (int64_t)min(q, nsplit - 1) * UPD_PART + tid;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) pv[q][u] = ld_sc1(pq + (h * 8 + u) * NT);
       }
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
+      for (int u = 0; u < 8; ++u) {
+        const int e = h * 8 + u, a = e >> 4, b = (e >> 2) & 3, g = e & 3;
+        double v = pv[0][u];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[a], fb[b], acc[a][b], 0, 0, 0);
-    }
-    if (more) {
-      sstore(kb + SYK, buf ^ 1);
-      __syncthreads();
-      buf ^= 1;
+        for (int q = 1; q < 4; ++q) v = (q < nsplit) ? v + pv[q][u] : v;
+        acc[a][b][g] = v;
+      }
     }
   }
   // acc[a][b][g]: row i = I0 + wm + 16 b + (lane & 15), column j = J0 + wn + 16 a + (lane >> 4) + 4 g;
@@ -3932,12 +4027,14 @@ __global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __re
       dpiv[h] = (rb && tid < 64) ? Dg[f0 + j] : 1.0;
       pj[h] = (rb && tid < 64) ? T.perm[f0 + j] : 0;
     }
-    if (q == q0 && tid < 64) poll_deps(dep, dep_ptr[t], dep_ptr[t + 1], tflags, epoch, err);
-    __syncthreads();  // + the previous front's / the leaves' drained stores (vmcnt 0 before it)
-    if (dg && tid == 0 && q == q0) dg[2] = wall_clock64();
     // initial vector: the children scattered their update entries into this front's contiguous range
-    // gbuf[P0, P1) in row order; staged through LDS (16 coalesced loads in flight per thread), then
-    // thread i sums row i's segment in order (4 partial sums)
+    // gbuf[P0, P1) in row order, each row's entries from childless children (the leaves, solved by an
+    // earlier launch) first and from its tree children (this launch) last (sv_nt, LDLSolver ctor).  The
+    // leaf part is summed BEFORE the wait: staged through LDS (16 coalesced loads in flight per
+    // thread), thread i sums row i's leaf entries in order (4 partial sums); after the wait only the
+    // tree children's few entries per row are loaded (one round trip)
+    const int ntr = (tid < r) ? (int)T.sv_nt[e0 + tid] : 0;
+    const int64_t pl1 = pr1 - ntr;  // the row's leaf part: [pr0, pl1)
     double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0;
     for (int64_t base = P0; base < P1; base += cap) {
       const int n = (int)min((int64_t)cap, P1 - base);
@@ -3955,7 +4052,7 @@ __global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __re
         }
       }
       __syncthreads();
-      const int lo = (int)(max(pr0, base) - base), hi = (int)(min(pr1, base + n) - base);
+      const int lo = (int)(max(pr0, base) - base), hi = (int)(min(pl1, base + n) - base);
       int p = lo;
       for (; p + 3 < hi; p += 4) {
         c0 += stg[p];
@@ -3966,7 +4063,12 @@ __global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __re
       for (; p < hi; ++p) c0 += stg[p];
       __syncthreads();
     }
-    if (tid < r) v0s[tid] = ((c0 + c1) + (c2 + c3)) + init;
+    if (q == q0 && tid < 64) poll_deps(dep, dep_ptr[t], dep_ptr[t + 1], tflags, epoch, err);
+    __syncthreads();  // + the previous front's / the leaves' drained stores (vmcnt 0 before it)
+    if (dg && tid == 0 && q == q0) dg[2] = wall_clock64();
+    double ct = 0.0;  // the tree children's entries of this row, in order
+    for (int k = 0; k < ntr; ++k) ct += ld_sc1(T.gbuf + pl1 + k);
+    if (tid < r) v0s[tid] = (((c0 + c1) + (c2 + c3)) + ct) + init;
     __syncthreads();
     if (med) {
       fwd_med_front(T, s, arena, Ls, v0s, xi, uvec, tflags, epoch);
@@ -4278,7 +4380,18 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   rows_.upload(S.rows);
   l_off_.upload(S.l_off);
   u_off_.upload(S.u_off);
-  u_ld_.upload(S.u_ld);
+  {  // a small tree front whose parent is a tree front stores its update block packed lower
+     // (u (u + 1) / 2, column-major; u_ld 0 on the device): written by k_fact_tree's write-out and read
+     // only by its tree parent's push (or a medium parent's add) — about half the square block's lines
+    std::vector<int32_t> uld(S.u_ld);
+    for (int f = 0; f < S.nsuper; ++f) {
+      const int p = S.parent[f];
+      if (!S.ftree.empty() && S.ftree[f] && S.nrows[f] <= SymbolicPlan::kFactTreeMax && p >= 0 && S.ftree[p] &&
+          S.nrows[f] > S.first[f + 1] - S.first[f])
+        uld[f] = 0;
+    }
+    u_ld_.upload(uld);
+  }
   uvec_off_.upload(S.uvec_off);
   asm_ptr_.upload(S.asm_ptr);
   asm_src_.upload(S.asm_src);
@@ -4292,6 +4405,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   {
     const char* ek = std::getenv("MADIPM_BIG_KPAN");  // panels per deferred big-front update group
     big_kpan_ = ek ? std::max(1, std::min(8, std::atoi(ek))) : 4;
+    const char* es = std::getenv("MADIPM_UPD_SPLIT");  // A/B: 0 = one workgroup per k_big_upd128 tile
+    upd_split_ = !(es && es[0] == '0');
     // persistent workgroups of the big-front solve kernels (2 per CU; MADIPM_BIG_SOLVE_WG for A/B)
     if (const char* eg = std::getenv("MADIPM_BIG_SOLVE_WG")) big_solve_wg_ = std::max(64, std::atoi(eg));
     // pipelined in-LDS factorisation schedule (1, default); 0 = the barrier schedule, bitwise the same
@@ -4319,6 +4434,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   fs_off_.upload(S.fs_off);
   sv_ptr_.upload(S.sv_ptr);
   sv_src_.upload(S.sv_src);
+  sv_nt_.alloc(std::max<int64_t>(S.row_ptr[S.nsuper], 1));  // the tree solve's split (set with its tables)
+  sv_nt_.zero();
   atiles_.upload(S.atiles);
   g_ptr_.upload(S.g_ptr);
   {
@@ -4380,6 +4497,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   }
   T_.sv_ptr = sv_ptr_;
   T_.sv_src = sv_src_;
+  T_.sv_nt = sv_nt_;
   const int ns = S.nsuper, NL = S.nlevels;
   {
     std::vector<int32_t> slot(std::max(ns, 1), -1);
@@ -4774,6 +4892,9 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
           L.alg = alg_done ? 0.0 : ka;
           alg_done = true;
           if (kv.first == BIG_UPDATE || kv.first == BIG_UPDATE128) last_upd = (int64_t)out.size();
+          if (kv.first == BIG_UPDATE128)  // K split over 2-4 workgroups per tile when the tiles alone
+                                          // would leave most CUs idle (k_big_upd128; nf = the split)
+            L.nf = !upd_split_ ? 1 : L.items <= 128 ? 4 : L.items <= 170 ? 3 : L.items <= 256 ? 2 : 1;
           L.flops = kf[q];
           out.push_back(L);
           sched.insert(sched.end(), kv.second->begin(), kv.second->end());
@@ -4812,6 +4933,20 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     for (size_t g = 0; g < S.lb.size(); ++g)  // this shard's batched leaves under top fronts: into it
       if (S.top(S.lb[g].parent)) lb_syrk_launch((int)g, fact1_);
     build_fact(2, fact2_);
+  }
+  {  // k_big_upd128's split-K scratch: partial products and per-tile tickets of the largest split launch
+    int64_t np = 0, nt = 0;
+    for (const auto* V : {&fact1_, &fact2_})
+      for (const Launch& L : *V)
+        if (L.kind == BIG_UPDATE128 && L.nf > 1) {
+          np = std::max<int64_t>(np, L.items * L.nf);
+          nt = std::max<int64_t>(nt, L.items);
+        }
+    if (np) {
+      upsum_.alloc((size_t)np * UPD_PART);
+      uptick_.alloc((size_t)nt);
+      uptick_.zero();
+    }
   }
 
   // ---- solve schedules: per level, small fronts (wave per front) and big fronts (task queues)
@@ -4944,9 +5079,38 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       ntree_ = (int)ord.size();
       // children of tree fronts scatter their forward update entries straight into the parent's
       // gather range (sv order, gbuf); everyone else keeps its own update vector (uvec)
+      // each tree-front row's gather entries: those of fronts solved by earlier launches (the flat
+      // leaves, batched-leaf groups, level-path children) first, those of tree tasks (this launch)
+      // last, sv_nt[row] of them — k_fwd_tree sums the first part before it waits for its children
+      std::vector<int64_t> svs(S.sv_src);
+      {
+        std::vector<uint8_t> from_task((size_t)std::max<int64_t>(S.uvec_size, 1), 0);
+        for (int s : ord)
+          if (S.uvec_off[s] >= 0)
+            for (int a = 0; a < S.nrows[s] - (S.first[s + 1] - S.first[s]); ++a) from_task[S.uvec_off[s] + a] = 1;
+        std::vector<uint16_t> nt((size_t)std::max<int64_t>(S.row_ptr[ns], 1), 0);
+        std::vector<int64_t> tail;
+        for (int s : ord)
+          for (int i = 0; i < S.nrows[s]; ++i) {
+            const int64_t t = S.row_ptr[s] + i, p0 = S.sv_ptr[t], p1 = S.sv_ptr[t + 1];
+            tail.clear();
+            int64_t o = p0;
+            for (int64_t p = p0; p < p1; ++p)
+              if (from_task[S.sv_src[p]])
+                tail.push_back(S.sv_src[p]);
+              else
+                svs[o++] = S.sv_src[p];
+            for (int64_t v : tail) svs[o++] = v;
+            MADIPM_REQUIRE(tail.size() <= 65535, "tree solve: tree-task entries of one row beyond 16 bits");
+            nt[t] = (uint16_t)tail.size();
+          }
+        sv_src_.upload(svs);
+        sv_nt_.upload(nt);
+        MADIPM_HIP(hipStreamSynchronize(nullptr));  // the host vectors end with this block
+      }
       std::vector<int64_t> inv((size_t)std::max<int64_t>(S.uvec_size, 1), -1), upm((size_t)std::max<int64_t>(S.rel_ptr[ns], 1), -1);
       for (int s : ord)
-        for (int64_t p = S.sv_ptr[S.row_ptr[s]]; p < S.sv_ptr[S.row_ptr[s] + S.nrows[s]]; ++p) inv[S.sv_src[p]] = p;
+        for (int64_t p = S.sv_ptr[S.row_ptr[s]]; p < S.sv_ptr[S.row_ptr[s] + S.nrows[s]]; ++p) inv[svs[p]] = p;
       for (int c = 0; c < ns; ++c)
         if (S.parent[c] >= 0 && in_tree[S.parent[c]])
           for (int64_t a = 0; a < S.rel_ptr[c + 1] - S.rel_ptr[c]; ++a) {
@@ -5285,8 +5449,8 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
         break;
       case BIG_UPDATE128:
         TIMED(KK_UPDATE, L.bytes, L.alg, L.flops,
-              (k_big_upd128<<<(unsigned)L.items, NT, 0, s>>>(T_, list, L.step, big_kpan_, arena_, D_, minv_, st_,
-                                                              pivot_tol)));
+              (k_big_upd128<<<(unsigned)(L.items * std::max(1, L.nf)), NT, 0, s>>>(
+                  T_, list, L.step, big_kpan_, arena_, D_, minv_, st_, pivot_tol, std::max(1, L.nf), upsum_, uptick_)));
         break;
       case LB_BUILD:
         TIMED(KK_LB_BUILD, L.bytes, L.alg, 0.0,
@@ -5471,12 +5635,22 @@ void LDLSolver::tree_debug_dump(hipStream_t s, const char* what, const int64_t* 
                 lv, na[lv], ab[lv * 6 + 5] / na[lv], ab[lv * 6] / na[lv], ab[lv * 6 + 1] / na[lv], ab[lv * 6 + 2] / na[lv],
                 ab[lv * 6 + 3] / na[lv], ab[lv * 6 + 4] / na[lv]);
   }
+  // tasks that stamped nothing (the big roots: k_root_solve) are skipped; a stamp a path did not
+  // take (a chunked front's) repeats the previous one
+  for (int t = 0; t < nt; ++t) {
+    int64_t* d = &h[8 * t];
+    if (d[0] == 0) continue;
+    for (int k = 1; k <= 5; ++k)
+      if (d[k] == 0) d[k] = d[k - 1];
+  }
   int64_t t0 = INT64_MAX, t1 = 0;
-  for (int t = 0; t < nt; ++t) t0 = std::min(t0, h[8 * t]), t1 = std::max(t1, h[8 * t + 5]);
+  for (int t = 0; t < nt; ++t)
+    if (h[8 * t]) t0 = std::min(t0, h[8 * t]), t1 = std::max(t1, h[8 * t + 5]);
   std::vector<double> acc((size_t)S_.nlevels * 8, 0.0);
   std::vector<int> cnt(S_.nlevels, 0);
   for (int t = 0; t < nt; ++t) {
     const int64_t* d = &h[8 * t];
+    if (d[0] == 0) continue;
     const int lv = S_.level[(int)d[6]];
     cnt[lv]++;
     acc[lv * 8 + 0] += (d[0] - t0) * 0.01;

@@ -36,6 +36,7 @@ struct FrontTab {
   const int64_t* fs_off;   // small fronts assembled by k_assemble: r x r scratch offset (else -1)
   const int64_t* sv_ptr;   // forward-solve gather lists (indexed by row_ptr[s] + i)
   const int64_t* sv_src;
+  const uint16_t* sv_nt;   // per row: its trailing gather entries from tree tasks (tree solve tables)
   const int32_t* bigslot;  // big front -> slot in the panel-inverse scratch (64x64 per slot)
   // sharding: top fronts start their forward solve from the exchanged vector xch[xoff[s] + i]
   // (xoff = -1 elsewhere); wout[s] = 0 would suppress the write of x to the caller's vector (every
@@ -337,8 +338,12 @@ class LDLSolver : public LinSolver {
   double ftree_bytes_ = 0, ftree_flops_ = 0, ftree_alg_ = 0;
   DBuf<int32_t> ft_order_, ft_dptr_, ft_dep_, fflags_, fcnt_;
   DBuf<uint64_t> xll_;
+  DBuf<uint16_t> sv_nt_;
   DBuf<int64_t> fdbg_, ab_first_, ab_loff_, fold_poff_, fold_row0_;
   int big_kpan_ = 4;  // big fronts: panels per deferred trailing-update group (MADIPM_BIG_KPAN)
+  bool upd_split_ = true;  // k_big_upd128 split K on launches of few tiles (MADIPM_UPD_SPLIT=0: off)
+  DBuf<double> upsum_;    // its partial products
+  DBuf<int32_t> uptick_;  // its per-tile tickets (reset by each tile's last part)
   int big_solve_wg_ = 512;
   DBuf<int32_t> ab_src0_, ab_src1_, ab_k_, ab_f0_, ab_wrc_, fold_bptr_, fold_bat_, fold_plen_, fold_rmax_, fold_lmax_;
   DBuf<uint8_t> absorb_, fold_pk_, fs_img_;

@@ -213,14 +213,18 @@ def test_ldl_medium_tree_fronts(well):
     assert ls.inertia() == (qp.nvar, 0, qp.ncon)
 
 
+@pytest.mark.parametrize("split", ["1", "0"])
 @pytest.mark.parametrize("kpan", ["1", "2", "4"])
 @pytest.mark.parametrize("n,m", [(320, 100), (130, 200)])
-def test_big_front_panel_groups(kpan, n, m, monkeypatch):
+def test_big_front_panel_groups(kpan, n, m, split, monkeypatch):
     """A dense K2 (dense SPD H, dense A: one big front of n + m columns, several 64-column panels
     with a partial last one) on the big-front path with the deferred multi-panel trailing update in
-    groups of MADIPM_BIG_KPAN panels (1 = right-looking per panel): pivots and solution of the oracle."""
+    groups of MADIPM_BIG_KPAN panels (1 = right-looking per panel): pivots and solution of the oracle.
+    Its 128-tile trailing launches have few tiles, so k_big_upd128 splits their K over 2-4 workgroups
+    per tile (partials summed in part order by the tile's last part); MADIPM_UPD_SPLIT=0: unsplit."""
     import scipy.sparse as sp
     monkeypatch.setenv("MADIPM_BIG_KPAN", kpan)
+    monkeypatch.setenv("MADIPM_UPD_SPLIT", split)
     rng = np.random.default_rng(11)
     B = rng.standard_normal((n, n))
     H = B @ B.T / n + np.eye(n)
