@@ -1598,7 +1598,7 @@ __device__ __forceinline__ FoldBatchTab& fold_batch_tab() {
 template <bool PK>
 __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, int r, int ld, double* A, const double* Kx, double* arena,
                                             double* D, LDLStatus* st, double tol, double* ext, double* cval,
-                                            int32_t* cdst, int64_t* fdg) {
+                                            int32_t* cdst, int64_t* fdg, int bbeg, int bend, bool with_asm) {
   int64_t tph[4] = {0, 0, 0, 0}, tc = fdg ? wall_clock64() : 0;
   auto lap = [&](int k) {
     if (fdg) {
@@ -1618,7 +1618,7 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, int r, int
   int32_t* pwrc = prow0 + LM;
   int32_t* kk = pwrc + LM;                                   // per batch row: batch-local leaf
   const int tid = threadIdx.x;
-  const int b0 = T.fold_bptr[s], nb = T.fold_bptr[s + 1] - b0;
+  const int b0 = bbeg, nb = bend - bbeg;  // the batches [bbeg, bend) of the front's (a helper: its share)
   if (nb > SymbolicPlan::kFoldMaxBatches) {  // the batch table below has room for kFoldMaxBatches
     if (tid == 0) __hip_atomic_fetch_or(T.err, kErrLdsCarve, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
@@ -1703,7 +1703,7 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, int r, int
   } else {
     gather_idx(0, 0, 0);  // no leaves: no loads
   }
-  const int64_t qa = T.asm_ptr[s] + tid, qe = T.asm_ptr[s + 1];
+  const int64_t qa = with_asm ? T.asm_ptr[s] + tid : 0, qe = with_asm ? T.asm_ptr[s + 1] : 0;
   const bool a0 = qa < qe;
   const int ad = a0 ? (int)T.asm_dst[qa] : 0;
   const int64_t as = a0 ? T.asm_src[qa] : 0;
@@ -1950,7 +1950,7 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
   if (T.absorb[s]) {  // original entries, then the micro-leaf children folded in LDS
     const int ntot = PK ? r * (r + 1) / 2 : r * ld;
     fold_leaves<PK>(T, s, r, ld, A, Kx, arena, D, st, tol, A + ((ntot + 1) & ~1), cbuf, reinterpret_cast<int32_t*>(MK),
-                    dg ? dg + 16 : nullptr);  // 16-byte aligned
+                    dg ? dg + 16 : nullptr, T.fold_own0[s], T.fold_bptr[s + 1], true);  // 16-byte aligned
   } else {  // pre-assembled as the LDS image: a straight copy, 16 loads in flight per thread
     const double* __restrict__ src = fscratch + T.fs_off[s];
     const int n = PK ? r * (r + 1) / 2 : r * ld;
@@ -1977,9 +1977,26 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
     const int uc = T.nrows[c] - (T.first[c + 1] - T.first[c]);
     for (int a = tid; a < uc; a += FTN) rels[a] = T.rel[T.rel_ptr[c] + a];
   }
+  const int hh = T.absorb[s] ? T.fold_help[s] : -1;  // the fold helper that folded the first batches
   if (tid < 64) poll_deps(dep, q0, q1, flags, epoch, err);
+  if (hh >= 0 && tid == 0) poll_flag(flags + T.fhelp[hh].flag, epoch, err);
   __syncthreads();
   if (dg && tid == 0) dg[2] = wall_clock64();
+  if (hh >= 0) {  // its image (this front's LDS layout) added entry by entry, 16 loads in flight per thread
+    const double* __restrict__ img = T.fimg + T.fhelp[hh].img;
+    const int ntot = PK ? r * (r + 1) / 2 : r * ld;
+    for (int base = 0; base < ntot; base += FTN * 16) {
+      double v[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v[k] = ld_sc1(img + min(base + k * FTN + tid, ntot - 1));
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int q = base + k * FTN + tid;
+        if (q < ntot) A[q] += v[k];
+      }
+    }
+    __syncthreads();
+  }
   for (int q = q0; q < q1; ++q) {  // tree children, child order
     const int c = dep[q];
     const int uc = T.nrows[c] - (T.first[c + 1] - T.first[c]);
@@ -2178,7 +2195,39 @@ __device__ __forceinline__ void fact_med_front(const FrontTab& T, int s, const i
   if (tid == 0) __hip_atomic_store(&flags[s], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(FTN) void k_fact_tree(FrontTab T, const int32_t* __restrict__ order, int nt,
+// A fold helper: the first batches of a front's micro leaves (FoldHelp [b0, b1)) folded into a zeroed
+// LDS image of the front — their L and D written as the front's own — and the image stored
+// write-through for the front, which adds it after its own batches and waits (fixed order: bitwise
+// reproducible).  The helpers take the first tickets, so the heaviest fronts' folds are split over two
+// CUs (ex10: 272 fronts of 35-50 us of folding on 256 CUs made the 16 late level-2 fronts the chain).
+template <bool PK>
+__device__ __forceinline__ void fold_help_task(const FrontTab& T, int h, int32_t* flags, int epoch, const double* Kx,
+                                               double* arena, double* D, LDLStatus* st, double tol, double* A,
+                                               double* MK, double* cbuf) {
+  const int tid = threadIdx.x;
+  const FoldHelp H = T.fhelp[h];
+  const int s = H.front, r = T.nrows[s], ld = PK ? 0 : (r | 1);
+  const int ntot = PK ? r * (r + 1) / 2 : r * ld;
+  const int64_t need = 8 * (int64_t)((ntot + 1) & ~1) + (int64_t)SymbolicPlan::kFoldRowBytes * T.fold_rmax[s] +
+                       (int64_t)SymbolicPlan::kFoldLeafBytes * T.fold_lmax[s];
+  if (need > T.lds_cap) {  // as the front's own check: a sticky error, never a write past the carve
+    if (tid == 0) {
+      __hip_atomic_fetch_or(T.err, kErrLdsCarve, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&flags[H.flag], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  fold_leaves<PK>(T, s, r, ld, A, Kx, arena, D, st, tol, A + ((ntot + 1) & ~1), cbuf, reinterpret_cast<int32_t*>(MK),
+                  nullptr, H.b0, H.b1, false);
+  __syncthreads();
+  double* __restrict__ img = T.fimg + H.img;
+  for (int q = tid; q < ntot; q += FTN) st_sc1(img + q, A[q]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store(&flags[H.flag], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(FTN) void k_fact_tree(FrontTab T, const int32_t* __restrict__ order, int nt, int nhelp,
                                                   const int32_t* __restrict__ dep_ptr, const int32_t* __restrict__ dep,
                                                   int32_t* counter, int32_t* flags, int epoch,
                                                   const double* __restrict__ Kx, double* arena,
@@ -2194,7 +2243,14 @@ __global__ __launch_bounds__(FTN) void k_fact_tree(FrontTab T, const int32_t* __
   __syncthreads();
   const int t = s_task;
   if (t >= nt) return;
-  const int s = order[t];
+  if (t < nhelp) {  // fold helper tickets first (no dependencies)
+    const int sh = T.fhelp[t].front;
+    if (T.nrows[sh] <= 128 && !T.fold_pk[sh])
+      fold_help_task<false>(T, t, flags, epoch, Kx, arena, D, st, tol, A, MK, cbuf);
+    else
+      fold_help_task<true>(T, t, flags, epoch, Kx, arena, D, st, tol, A, MK, cbuf);
+  } else {
+  const int s = order[t - nhelp];
   int64_t* dg = dbg ? dbg + 24 * t : nullptr;
   if (dg && threadIdx.x == 0) dg[0] = wall_clock64();
   if (T.nrows[s] > SymbolicPlan::kFactTreeMax)
@@ -2205,6 +2261,7 @@ __global__ __launch_bounds__(FTN) void k_fact_tree(FrontTab T, const int32_t* __
   else
     fact_tree_front<true>(T, s, dep, dep_ptr[t], dep_ptr[t + 1], flags, epoch, Kx, arena, fscratch, D, st, tol, err, A, Dl,
                           MK, cbuf, rels, dg);
+  }
   if (threadIdx.x == 0 && atomicAdd(counter + 1, 1) == nt - 1) {  // last one out: reset the tickets
     counter[0] = 0;
     counter[1] = 0;
@@ -4672,10 +4729,51 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     T_.lds_cap = ftree_lds_;
     if (const char* e = std::getenv("MADIPM_DEBUG_LDS_SHRINK")) T_.lds_cap -= std::atoi(e);
     auto up = [](DBuf<int32_t>& d, const std::vector<int32_t>& v) { d.upload(v.empty() ? std::vector<int32_t>{0} : v); };
+    // fold helpers: a front with two or more leaf batches hands the first half of them to a helper
+    // ticket (before every front's; the helpers with the most batches first), folds the rest itself
+    // and adds the helper's image after its waits (MADIPM_FOLD_HELP=0: no helpers)
+    {
+      const char* eh = std::getenv("MADIPM_FOLD_HELP");
+      const bool on = !(eh && eh[0] == '0');
+      int min_nb = 3;  // fronts of at least this many batches get a helper (MADIPM_FOLD_HELP_MIN: A/B)
+      if (const char* em = std::getenv("MADIPM_FOLD_HELP_MIN")) min_nb = std::max(2, std::atoi(em));
+      int share4 = 2;  // the helper's share of the batches, in quarters (MADIPM_FOLD_HELP_SHARE: A/B)
+      if (const char* es = std::getenv("MADIPM_FOLD_HELP_SHARE")) share4 = std::max(1, std::min(3, std::atoi(es)));
+      std::vector<int32_t> own0(std::max(ns, 1), 0), help(std::max(ns, 1), -1);
+      std::vector<FoldHelp> hv;
+      int64_t img = 0;
+      for (int f = 0; f < ns; ++f) own0[f] = S.fold_bptr.empty() ? 0 : S.fold_bptr[f];
+      for (int f : ord) {
+        if (!on || !S.absorb[f]) continue;
+        const int b0 = S.fold_bptr[f], nb = S.fold_bptr[f + 1] - b0;
+        if (nb < min_nb) continue;
+        const int r = S.nrows[f];
+        const bool sq = r <= 128 && !S.fold_pk[f];
+        const int64_t ntot = sq ? (int64_t)r * (r | 1) : (int64_t)r * (r + 1) / 2;
+        hv.push_back(FoldHelp{f, b0, b0 + std::max(1, std::min(nb - 1, nb * share4 / 4)), 0, img});
+        img += (ntot + 1) & ~1LL;
+      }
+      std::stable_sort(hv.begin(), hv.end(), [](const FoldHelp& a, const FoldHelp& b) { return a.b1 - a.b0 > b.b1 - b.b0; });
+      nfhelp_ = (int)hv.size();
+      for (int h = 0; h < nfhelp_; ++h) {
+        hv[h].flag = ns + h;
+        help[hv[h].front] = h;
+        own0[hv[h].front] = hv[h].b1;
+      }
+      fold_own0_.upload(own0);
+      fold_help_.upload(help);
+      fhelp_.upload(hv.empty() ? std::vector<FoldHelp>{FoldHelp{0, 0, 0, 0, 0}} : hv);
+      fimg_.alloc((size_t)std::max<int64_t>(img, 2));
+      T_.fold_own0 = fold_own0_;
+      T_.fold_help = fold_help_;
+      T_.fhelp = fhelp_;
+      T_.fimg = fimg_;
+      dptr.insert(dptr.begin(), (size_t)nfhelp_, 0);  // dep_ptr by ticket: the helpers' ranges are empty
+    }
     up(ft_order_, ord);
     up(ft_dptr_, dptr);
     up(ft_dep_, dl);
-    fflags_.alloc(std::max(ns, 1));
+    fflags_.alloc(std::max(ns + nfhelp_, 1));
     fflags_.zero();
     {
       auto up8 = [](DBuf<uint8_t>& d, const std::vector<uint8_t>& v) { d.upload(v.empty() ? std::vector<uint8_t>{0} : v); };
@@ -4728,7 +4826,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     fcnt_.zero();
     const char* dv = std::getenv("MADIPM_TREE_DEBUG");
     if (dv && dv[0] == '1' && nftree_) {
-      fdbg_.alloc((int64_t)24 * nftree_);
+      fdbg_.alloc((int64_t)24 * (nftree_ + nfhelp_));
       fdbg_.zero();
     }
   }
@@ -5471,10 +5569,11 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
         }
         ++fepoch_;
         TIMED(KK_FACT_TREE, L.bytes, L.alg, L.flops,
-              (k_fact_tree<<<(unsigned)nftree_, FTN, L.lds_bytes, s>>>(T_, ft_order_, nftree_, ft_dptr_, ft_dep_, fcnt_,
-                                                                      fflags_, fepoch_, Kx, arena_, fscratch_, D_, st_,
-                                                                      pivot_tol, &st_->err, fdbg_.p)));
-        if (fdbg_.p) tree_debug_dump(s, "fact", fdbg_.p, nftree_, "stage", "wait", "push", "factor", "store", 24);
+              (k_fact_tree<<<(unsigned)(nftree_ + nfhelp_), FTN, L.lds_bytes, s>>>(
+                  T_, ft_order_, nftree_ + nfhelp_, nfhelp_, ft_dptr_, ft_dep_, fcnt_, fflags_, fepoch_, Kx, arena_,
+                  fscratch_, D_, st_, pivot_tol, &st_->err, fdbg_.p)));
+        if (fdbg_.p)  // (the helper tickets stamp nothing: the fronts' records follow them)
+          tree_debug_dump(s, "fact", fdbg_.p + 24 * nfhelp_, nftree_, "stage", "wait", "push", "factor", "store", 24);
         break;
     }
   }

@@ -15,6 +15,11 @@
 
 namespace madipm {
 
+struct FoldHelp {
+  int32_t front, b0, b1, flag;  // the front, its batches [b0, b1), the flag the helper publishes
+  int64_t img;                  // its image in FrontTab::fimg (the front's LDS layout, ntot doubles)
+};
+
 // Device view of the front table (SoA, all device pointers).
 struct FrontTab {
   const int32_t* first;
@@ -73,6 +78,13 @@ struct FrontTab {
   int fpipe;        // pipelined in-LDS schedule (blocked_factor_pipe; MADIPM_FACT_PIPE=0: blocked_factor_lds)
   int pipe_fault;   // tests (MADIPM_DEBUG_PIPE_FAULT=1): blocked_factor_pipe drops one hand-off
   int lds_cap;      // k_fact_tree's dynamic LDS (bytes): a front (+ its leaf batches) beyond it is an error
+  // fold helpers (k_fact_tree tickets before the fronts): a helper folds the first batches of a front's
+  // micro leaves into a zeroed LDS image and hands it over in HBM (fimg); the front folds the rest
+  // from fold_own0[s] and adds the image after its waits (fold_help[s] = the helper, -1: none)
+  const int32_t* fold_own0;
+  const int32_t* fold_help;
+  const FoldHelp* fhelp;
+  double* fimg;
   uint64_t* xll;  // big-front solves: panel solutions as self-validating words (ll_put / ll_get)
 };
 
@@ -346,6 +358,10 @@ class LDLSolver : public LinSolver {
   DBuf<int32_t> uptick_;  // its per-tile tickets (reset by each tile's last part)
   int big_solve_wg_ = 512;
   DBuf<int32_t> ab_src0_, ab_src1_, ab_k_, ab_f0_, ab_wrc_, fold_bptr_, fold_bat_, fold_plen_, fold_rmax_, fold_lmax_;
+  DBuf<int32_t> fold_own0_, fold_help_;
+  DBuf<FoldHelp> fhelp_;
+  DBuf<double> fimg_;
+  int nfhelp_ = 0;  // fold helper tickets (k_fact_tree: before the fronts')
   DBuf<uint8_t> absorb_, fold_pk_, fs_img_;
   DBuf<int32_t> mc_ptr_;
   DBuf<uint32_t> fold_prod_, fold_chead_;

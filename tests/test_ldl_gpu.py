@@ -185,6 +185,24 @@ def test_ldl_fold_carve_overflow_is_an_error(shrink, monkeypatch):
     _check_case(K, Lw, well=True)
 
 
+@pytest.mark.parametrize("help_", ["1", "0"])
+@pytest.mark.parametrize("well", [True, False])
+def test_fold_helpers(help_, well, monkeypatch):
+    """Fold helpers: a tree front with two or more leaf batches hands the first half to a helper
+    ticket, which folds them into a zeroed LDS image of the front (their L and D written as the
+    front's), stores it write-through and publishes a flag; the front folds the rest and adds the image
+    after its waits.  The ex10 stand-in at 0.1 (level-1/2 fronts of 3-4 batches): the oracle's pivots
+    (1e-12, well conditioned) and solution with helpers on and off (MADIPM_FOLD_HELP=0)."""
+    from helpers import lp_k2
+    from madipm_amd import standard_form_qp
+    from madipm_amd.instances import ex10_standin
+    monkeypatch.setenv("MADIPM_FOLD_HELP", help_)
+    qp = standard_form_qp(ex10_standin(scale=0.1))
+    K, Lw = lp_k2(qp, 1, well=well)
+    ls = _check_case(K, Lw, well=well)
+    assert ls.inertia() == (qp.nvar, 0, qp.ncon)
+
+
 @pytest.mark.parametrize("case", ["block_well", "block_ipm", "random"])
 def test_root_backward_in_forward(case):
     """An elimination-tree root (r == w) is solved backward by the forward tree kernel right after its
