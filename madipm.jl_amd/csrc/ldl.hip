@@ -1598,7 +1598,7 @@ __device__ __forceinline__ FoldBatchTab& fold_batch_tab() {
 template <bool PK>
 __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, int r, int ld, double* A, const double* Kx, double* arena,
                                             double* D, LDLStatus* st, double tol, double* ext, double* cval,
-                                            int32_t* cdst, int64_t* fdg, int bbeg, int bend, bool with_asm) {
+                                            int32_t* cdst, int64_t* fdg, const FoldStart& F0, bool with_asm) {
   int64_t tph[4] = {0, 0, 0, 0}, tc = fdg ? wall_clock64() : 0;
   auto lap = [&](int k) {
     if (fdg) {
@@ -1618,7 +1618,7 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, int r, int
   int32_t* pwrc = prow0 + LM;
   int32_t* kk = pwrc + LM;                                   // per batch row: batch-local leaf
   const int tid = threadIdx.x;
-  const int b0 = bbeg, nb = bend - bbeg;  // the batches [bbeg, bend) of the front's (a helper: its share)
+  const int b0 = F0.b0, nb = F0.b1 - F0.b0;  // the front's batches (a helper: its share)
   if (nb > SymbolicPlan::kFoldMaxBatches) {  // the batch table below has room for kFoldMaxBatches
     if (tid == 0) __hip_atomic_fetch_or(T.err, kErrLdsCarve, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
@@ -1695,11 +1695,9 @@ __device__ __forceinline__ void fold_leaves(const FrontTab& T, int s, int r, int
   // loads) and this front's original K entries, all in one round trip; their K values (the leaf rows'
   // and the front's own) in a second — the zero fill of the front beside them
   if (nb > 0) {
-    const int kq0 = T.fold_bat[b0];
-    const int64_t r0 = T.fold_row0[b0], r1 = T.fold_row0[b0 + 1];
-    leaf_tab(kq0, T.fold_bat[b0 + 1] - kq0);
-    gather_idx(r0, (int)(r1 - r0), 0);
-    load_group(e, T.fold_prod + T.fold_poff[b0] + tid, 0, T.fold_plen[b0]);
+    leaf_tab(F0.kq0, F0.kq1 - F0.kq0);
+    gather_idx(F0.row0, (int)(F0.row1 - F0.row0), 0);
+    load_group(e, T.fold_prod + F0.poff + tid, 0, F0.plen);
   } else {
     gather_idx(0, 0, 0);  // no leaves: no loads
   }
@@ -1932,6 +1930,7 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
   const int tid = threadIdx.x;
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
   const int ld = PK ? 0 : (r | 1);
+  const FoldStart F0 = T.fstart[s];  // (with the front's other words: no dependent round trip later)
   {  // the front and its leaf batches must fit the launch's LDS: else a sticky error, never a write
      // past the carve (the symbolic analysis sizes both; this catches a plan that breaks it)
     const int ntot = PK ? r * (r + 1) / 2 : r * ld;
@@ -1950,7 +1949,7 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
   if (T.absorb[s]) {  // original entries, then the micro-leaf children folded in LDS
     const int ntot = PK ? r * (r + 1) / 2 : r * ld;
     fold_leaves<PK>(T, s, r, ld, A, Kx, arena, D, st, tol, A + ((ntot + 1) & ~1), cbuf, reinterpret_cast<int32_t*>(MK),
-                    dg ? dg + 16 : nullptr, T.fold_own0[s], T.fold_bptr[s + 1], true);  // 16-byte aligned
+                    dg ? dg + 16 : nullptr, F0, true);  // 16-byte aligned
   } else {  // pre-assembled as the LDS image: a straight copy, 16 loads in flight per thread
     const double* __restrict__ src = fscratch + T.fs_off[s];
     const int n = PK ? r * (r + 1) / 2 : r * ld;
@@ -2218,7 +2217,7 @@ __device__ __forceinline__ void fold_help_task(const FrontTab& T, int h, int32_t
     return;
   }
   fold_leaves<PK>(T, s, r, ld, A, Kx, arena, D, st, tol, A + ((ntot + 1) & ~1), cbuf, reinterpret_cast<int32_t*>(MK),
-                  nullptr, H.b0, H.b1, false);
+                  nullptr, H.fs, false);
   __syncthreads();
   double* __restrict__ img = T.fimg + H.img;
   for (int q = tid; q < ntot; q += FTN) st_sc1(img + q, A[q]);
@@ -4257,6 +4256,7 @@ __global__ __launch_bounds__(NT) void k_bwd_tree(FrontTab T, const int32_t* __re
                                                  const uint8_t* __restrict__ tchunk) {
   extern __shared__ __attribute__((aligned(16))) double Ls[];
   __shared__ double xbs[SMALL_SOLVE_MAX];
+  __shared__ double bpart[3][64];  // waves 1..3: their share of the update rows' products (w <= 64)
   __shared__ int s_task;
   const int tid = threadIdx.x;
   if (tid == 0) {
@@ -4297,19 +4297,42 @@ __global__ __launch_bounds__(NT) void k_bwd_tree(FrontTab T, const int32_t* __re
     __syncthreads();  // + the previous (parent) front's drained x stores
     if (tid < nb) xbs[tid] = ld_sc1(xi + rk);
     __syncthreads();
+    // the update rows' products L(w + k, j) x_k: for a front of <= 64 pivots and >= 64 update rows the
+    // four waves each take a quarter of the rows (ex10's level 1-3 fronts: 70-128 rows, one column per
+    // lane) and wave 0 adds the parts in wave order; else wave 0 alone, three columns per lane
+    const bool split = w <= 64 && nb >= 64;  // uniform
+    double part = 0.0;
+    if (split) {
+      const int wv = tid >> 6, kb0 = (nb * wv) >> 2, kb1 = (nb * (wv + 1)) >> 2;
+      const int cj = min(lane, w - 1);
+      double a0 = 0.0, a1 = 0.0;
+      int k = kb0;
+      for (; k + 1 < kb1; k += 2) {
+        a0 = fma(Ls[(w + k) + cj * ldc], xbs[k], a0);
+        a1 = fma(Ls[(w + k + 1) + cj * ldc], xbs[k + 1], a1);
+      }
+      if (k < kb1) a0 = fma(Ls[(w + k) + cj * ldc], xbs[k], a0);
+      part = a0 + a1;
+      if (wv > 0) bpart[wv - 1][lane] = part;
+      __syncthreads();
+    }
     if (tid < 64) {
       int cj[3];
 #pragma unroll
       for (int h = 0; h < 3; ++h) cj[h] = min(lane + 64 * h, w - 1);
       double acc[3][2] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
-      for (int k8 = 0; k8 < nb; k8 += 8) {
+      if (split) {
+        acc[0][0] = ((part + bpart[0][lane]) + bpart[1][lane]) + bpart[2][lane];
+      } else {
+        for (int k8 = 0; k8 < nb; k8 += 8) {
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) {
-          const int k = k8 + kk;
-          if (k < nb) {
-            const double x = xbs[k];
+          for (int kk = 0; kk < 8; ++kk) {
+            const int k = k8 + kk;
+            if (k < nb) {
+              const double x = xbs[k];
 #pragma unroll
-            for (int h = 0; h < 3; ++h) acc[h][kk & 1] = fma(Ls[(w + k) + cj[h] * ldc], x, acc[h][kk & 1]);
+              for (int h = 0; h < 3; ++h) acc[h][kk & 1] = fma(Ls[(w + k) + cj[h] * ldc], x, acc[h][kk & 1]);
+            }
           }
         }
       }
@@ -4739,10 +4762,24 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       if (const char* em = std::getenv("MADIPM_FOLD_HELP_MIN")) min_nb = std::max(2, std::atoi(em));
       int share4 = 2;  // the helper's share of the batches, in quarters (MADIPM_FOLD_HELP_SHARE: A/B)
       if (const char* es = std::getenv("MADIPM_FOLD_HELP_SHARE")) share4 = std::max(1, std::min(3, std::atoi(es)));
-      std::vector<int32_t> own0(std::max(ns, 1), 0), help(std::max(ns, 1), -1);
+      std::vector<int32_t> help(std::max(ns, 1), -1);
+      std::vector<FoldStart> fst(std::max(ns, 1), FoldStart{0, 0, 0, 0, 0, 0, 0, 0, 0});
+      auto start = [&](int b0, int b1) {  // batches [b0, b1) and the first one's table entries
+        FoldStart F{b0, b1, 0, 0, 0, 0, 0, 0, 0};
+        if (b1 > b0) {
+          F.kq0 = S.fold_bat[b0];
+          F.kq1 = S.fold_bat[b0 + 1];
+          F.row0 = S.fold_row0[b0];
+          F.row1 = S.fold_row0[b0 + 1];
+          F.poff = S.fold_poff[b0];
+          F.plen = S.fold_plen[b0];
+        }
+        return F;
+      };
       std::vector<FoldHelp> hv;
       int64_t img = 0;
-      for (int f = 0; f < ns; ++f) own0[f] = S.fold_bptr.empty() ? 0 : S.fold_bptr[f];
+      if (!S.fold_bptr.empty())
+        for (int f = 0; f < ns; ++f) fst[f] = start(S.fold_bptr[f], S.fold_bptr[f + 1]);
       for (int f : ord) {
         if (!on || !S.absorb[f]) continue;
         const int b0 = S.fold_bptr[f], nb = S.fold_bptr[f + 1] - b0;
@@ -4750,21 +4787,22 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         const int r = S.nrows[f];
         const bool sq = r <= 128 && !S.fold_pk[f];
         const int64_t ntot = sq ? (int64_t)r * (r | 1) : (int64_t)r * (r + 1) / 2;
-        hv.push_back(FoldHelp{f, b0, b0 + std::max(1, std::min(nb - 1, nb * share4 / 4)), 0, img});
+        hv.push_back(FoldHelp{f, 0, img, start(b0, b0 + std::max(1, std::min(nb - 1, nb * share4 / 4)))});
         img += (ntot + 1) & ~1LL;
       }
-      std::stable_sort(hv.begin(), hv.end(), [](const FoldHelp& a, const FoldHelp& b) { return a.b1 - a.b0 > b.b1 - b.b0; });
+      std::stable_sort(hv.begin(), hv.end(),
+                       [](const FoldHelp& a, const FoldHelp& b) { return a.fs.b1 - a.fs.b0 > b.fs.b1 - b.fs.b0; });
       nfhelp_ = (int)hv.size();
       for (int h = 0; h < nfhelp_; ++h) {
         hv[h].flag = ns + h;
         help[hv[h].front] = h;
-        own0[hv[h].front] = hv[h].b1;
+        fst[hv[h].front] = start(hv[h].fs.b1, S.fold_bptr[hv[h].front + 1]);  // the front keeps the rest
       }
-      fold_own0_.upload(own0);
+      fstart_.upload(fst);
       fold_help_.upload(help);
-      fhelp_.upload(hv.empty() ? std::vector<FoldHelp>{FoldHelp{0, 0, 0, 0, 0}} : hv);
+      fhelp_.upload(hv.empty() ? std::vector<FoldHelp>{FoldHelp{0, 0, 0, FoldStart{0, 0, 0, 0, 0, 0, 0, 0, 0}}} : hv);
       fimg_.alloc((size_t)std::max<int64_t>(img, 2));
-      T_.fold_own0 = fold_own0_;
+      T_.fstart = fstart_;
       T_.fold_help = fold_help_;
       T_.fhelp = fhelp_;
       T_.fimg = fimg_;

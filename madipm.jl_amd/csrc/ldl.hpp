@@ -15,9 +15,19 @@
 
 namespace madipm {
 
+// the batch range a k_fact_tree task folds and its first batch's table entries, in one record loaded
+// with the task's other per-front words (r5: the first batch's entries were a dependent round trip)
+struct FoldStart {
+  int32_t b0, b1;      // batches [b0, b1)
+  int32_t kq0, kq1;    // the first batch's leaves [kq0, kq1) (fold_bat)
+  int64_t row0, row1;  // its flat leaf rows (fold_row0)
+  int64_t poff;        // its product entries (fold_poff, fold_plen)
+  int32_t plen, pad;
+};
 struct FoldHelp {
-  int32_t front, b0, b1, flag;  // the front, its batches [b0, b1), the flag the helper publishes
-  int64_t img;                  // its image in FrontTab::fimg (the front's LDS layout, ntot doubles)
+  int32_t front, flag;  // the front, the flag the helper publishes
+  int64_t img;          // its image in FrontTab::fimg (the front's LDS layout, ntot doubles)
+  FoldStart fs;         // its batches
 };
 
 // Device view of the front table (SoA, all device pointers).
@@ -80,8 +90,8 @@ struct FrontTab {
   int lds_cap;      // k_fact_tree's dynamic LDS (bytes): a front (+ its leaf batches) beyond it is an error
   // fold helpers (k_fact_tree tickets before the fronts): a helper folds the first batches of a front's
   // micro leaves into a zeroed LDS image and hands it over in HBM (fimg); the front folds the rest
-  // from fold_own0[s] and adds the image after its waits (fold_help[s] = the helper, -1: none)
-  const int32_t* fold_own0;
+  // from fstart[s] and adds the image after its waits (fold_help[s] = the helper, -1: none)
+  const FoldStart* fstart;  // per front: the batches it folds itself
   const int32_t* fold_help;
   const FoldHelp* fhelp;
   double* fimg;
@@ -358,7 +368,8 @@ class LDLSolver : public LinSolver {
   DBuf<int32_t> uptick_;  // its per-tile tickets (reset by each tile's last part)
   int big_solve_wg_ = 512;
   DBuf<int32_t> ab_src0_, ab_src1_, ab_k_, ab_f0_, ab_wrc_, fold_bptr_, fold_bat_, fold_plen_, fold_rmax_, fold_lmax_;
-  DBuf<int32_t> fold_own0_, fold_help_;
+  DBuf<FoldStart> fstart_;
+  DBuf<int32_t> fold_help_;
   DBuf<FoldHelp> fhelp_;
   DBuf<double> fimg_;
   int nfhelp_ = 0;  // fold helper tickets (k_fact_tree: before the fronts')
