@@ -2030,6 +2030,27 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   }
 
   stamp("10b: assembly plan");
+  if (std::getenv("MADIPM_ASM_STATS")) {  // diagnostics: per assembly group, tiles, big-child blocks, chunks
+    for (size_t g = 0; g + 1 < S.atile_lev.size(); ++g) {
+      const int32_t t0 = S.atile_lev[g], t1 = S.atile_lev[g + 1];
+      if (t1 <= t0) continue;
+      double bc = 0, bmax = 0, ch = 0, chmax = 0, nent = 0;
+      for (int32_t t = t0; t < t1; ++t) {
+        const auto& A = S.atiles[t];
+        const double nb = (A.bt1 - A.bt0);
+        bc += nb;
+        bmax = std::max(bmax, nb);
+        if (A.gptr >= 0) {
+          const double c = S.g_ptr[A.gptr + 4096] - S.g_ptr[A.gptr];
+          ch += c;
+          chmax = std::max(chmax, c);
+          nent += 4096;
+        }
+      }
+      fprintf(stderr, "asm group %zu: %d tiles  big-child blocks %.1f/tile (max %.0f)  chunks %.2f/entry (tile max %.0f)\n", g,
+              t1 - t0, bc / (t1 - t0), bmax, nent > 0 ? ch / nent : 0.0, chmax);
+    }
+  }
 
   // ---------------- 11. forward-solve gather lists (child order).  Sharded: a top front's rows list
   // only its top children (sv); its subtree-root children of this shard are listed in sx (the
