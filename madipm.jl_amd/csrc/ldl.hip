@@ -4203,15 +4203,24 @@ __global__ __launch_bounds__(RSN) void k_root_solve(FrontTab T, const int32_t* _
     len = T.sv_ptr[e0 + i + 1] - lo;
   }
   const double init = (i < r && k == 0) ? fwd_init(T, s, i, w, f0, b) : 0.0;
+  // wave 0's pivots and the caller's positions, loaded with everything else (not after the barrier)
+  double dpiv[3];
+  int pj[3];
+#pragma unroll
+  for (int h = 0; h < 3; ++h) {
+    const int j = min(lane + 64 * h, max(w - 1, 0));
+    dpiv[h] = (tid < 64) ? Dg[f0 + j] : 1.0;
+    pj[h] = (tid < 64) ? T.perm[f0 + j] : 0;
+  }
   stage_rowmajor<RSN>(arena + T.l_off[s], Ls, r, w, ldt);
   double c = 0.0;
   const int64_t q4 = len >> 2;
-  for (int64_t m0 = 0; m0 < q4; m0 += 8) {
-    double x[8];
+  for (int64_t m0 = 0; m0 < q4; m0 += 16) {  // 16 loads in flight (ex10's root rows: ~14 per thread)
+    double x[16];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) x[u] = T.gbuf[lo + 4 * min(m0 + u, max(q4 - 1, (int64_t)0)) + k];
+    for (int u = 0; u < 16; ++u) x[u] = T.gbuf[lo + 4 * min(m0 + u, max(q4 - 1, (int64_t)0)) + k];
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
+    for (int u = 0; u < 16; ++u)
       if (m0 + u < q4) c += x[u];
   }
   if (k == 0)
@@ -4222,15 +4231,11 @@ __global__ __launch_bounds__(RSN) void k_root_solve(FrontTab T, const int32_t* _
   }
   __syncthreads();  // the panel and the partial sums
   if (tid < 64) {
-    double v[3], dpiv[3];
-    int pj[3];
+    double v[3];
 #pragma unroll
     for (int h = 0; h < 3; ++h) {
       const int ii = lane + 64 * h;
       v[h] = (ii < r) ? ((part[4 * ii] + part[4 * ii + 1]) + (part[4 * ii + 2] + part[4 * ii + 3])) + inits[ii] : 0.0;
-      const int j = min(ii, max(w - 1, 0));
-      dpiv[h] = Dg[f0 + j];
-      pj[h] = T.perm[f0 + j];
     }
     fwd_subst_t(v, Ls, ldt, r, w, lane);
 #pragma unroll
