@@ -2078,13 +2078,18 @@ __device__ __forceinline__ void med_trailing(double* __restrict__ F, int r, int 
       c[g] = F[(int64_t)(c0 + ic) + (int64_t)(c0 + jc) * r];
     }
   };
-  double c[4];
-  if (wv < ntile) load_c(wv, c);
+  // C of the next TWO tiles in flight while a tile's MFMAs run (one ahead left each wave's C loads
+  // exposed: a tile's 16 k-steps take ~0.4 us against a ~1-2 us HBM round trip)
+  double c[4], cn[4];
+  if (wv < ntile) {
+    load_c(wv, c);
+    load_c(wv + nw, cn);
+  }
   for (int t = wv; t < ntile; t += nw) {
     int i0, j0;
     coords(t, i0, j0);
-    double cn[4];
-    load_c(t + nw, cn);  // (clamped: the last tile's again when there is no next)
+    double cnn[4];
+    load_c(t + 2 * nw, cnn);  // (clamped: the last tile's again when there is no such tile)
     dbl4 acc = {0.0, 0.0, 0.0, 0.0};
     const int ja = min(j0 + il, rp - 1), ib = min(i0 + il, rp - 1);
     for (int ks = 0; ks < nks; ++ks) {
@@ -2110,7 +2115,10 @@ __device__ __forceinline__ void med_trailing(double* __restrict__ F, int r, int 
       }
     }
 #pragma unroll
-    for (int g = 0; g < 4; ++g) c[g] = cn[g];
+    for (int g = 0; g < 4; ++g) {
+      c[g] = cn[g];
+      cn[g] = cnn[g];
+    }
   }
 }
 
@@ -2141,9 +2149,14 @@ __device__ __forceinline__ void fact_med_front(const FrontTab& T, int s, const i
         x[k] = __hip_atomic_load(U + max(a, b) + ucol_off(b, uc, uld), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         dst[k] = ok ? (int64_t)rl[a] + (int64_t)rl[b] * r : -1;
       }
+      // the read-modify-writes: every F load of the round first, unconditional from clamped addresses
+      // (a masked += compiled into a branch with a wait inside: 8 serial round trips per round)
+      double f[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] = F[max(dst[k], (int64_t)0)];
 #pragma unroll
       for (int k = 0; k < 8; ++k)
-        if (dst[k] >= 0) F[dst[k]] += x[k];
+        if (dst[k] >= 0) F[dst[k]] = f[k] + x[k];
     }
     __syncthreads();
   }
