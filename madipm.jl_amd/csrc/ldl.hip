@@ -2124,12 +2124,15 @@ __device__ __forceinline__ void med_trailing(double* __restrict__ F, int r, int 
 
 __device__ __forceinline__ void fact_med_front(const FrontTab& T, int s, const int32_t* __restrict__ dep, int q0, int q1,
                                                int32_t* flags, int epoch, double* arena, double* D, LDLStatus* st,
-                                               double tol, int32_t* err, double* A, double* Dl, double* MK, double* cbuf) {
+                                               double tol, int32_t* err, double* A, double* Dl, double* MK, double* cbuf,
+                                               int64_t* dg) {
   const int tid = threadIdx.x;
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
   double* __restrict__ F = arena + T.l_off[s];
+  if (dg && tid == 0) dg[1] = wall_clock64();  // (no staging: the front lives in HBM)
   if (tid < 64) poll_deps(dep, q0, q1, flags, epoch, err);
   __syncthreads();
+  if (dg && tid == 0) dg[2] = wall_clock64();
   // tree children's update blocks (agent-scope loads: written by other workgroups), child order
   for (int q = q0; q < q1; ++q) {
     const int c = dep[q];
@@ -2160,6 +2163,7 @@ __device__ __forceinline__ void fact_med_front(const FrontTab& T, int s, const i
     }
     __syncthreads();
   }
+  if (dg && tid == 0) dg[3] = wall_clock64();
   for (int c0 = 0; c0 < w; c0 += MED_PW) {
     const int pw = min(MED_PW, w - c0), rp = r - c0, ld = rp | 1;
     const bool last = c0 + pw >= w;
@@ -2202,9 +2206,15 @@ __device__ __forceinline__ void fact_med_front(const FrontTab& T, int s, const i
     if (rp > pw) med_trailing(F, r, c0, pw, A, ld, Dl, last);
     __syncthreads();  // the next panel's staging reads the updated trailing matrix; A is rewritten
   }
+  if (dg && tid == 0) dg[4] = wall_clock64();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) __hip_atomic_store(&flags[s], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (dg && tid == 0) {
+    dg[5] = wall_clock64();
+    dg[6] = s;
+    dg[7] = r;
+  }
 }
 
 // A fold helper: the first batches of a front's micro leaves (FoldHelp [b0, b1)) folded into a zeroed
@@ -2266,7 +2276,7 @@ __global__ __launch_bounds__(FTN) void k_fact_tree(FrontTab T, const int32_t* __
   int64_t* dg = dbg ? dbg + 24 * t : nullptr;
   if (dg && threadIdx.x == 0) dg[0] = wall_clock64();
   if (T.nrows[s] > SymbolicPlan::kFactTreeMax)
-    fact_med_front(T, s, dep, dep_ptr[t], dep_ptr[t + 1], flags, epoch, arena, D, st, tol, err, A, Dl, MK, cbuf);
+    fact_med_front(T, s, dep, dep_ptr[t], dep_ptr[t + 1], flags, epoch, arena, D, st, tol, err, A, Dl, MK, cbuf, dg);
   else if (T.nrows[s] <= 128 && !T.fold_pk[s])
     fact_tree_front<false>(T, s, dep, dep_ptr[t], dep_ptr[t + 1], flags, epoch, Kx, arena, fscratch, D, st, tol, err, A, Dl,
                            MK, cbuf, rels, dg);
