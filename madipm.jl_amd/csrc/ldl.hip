@@ -72,9 +72,12 @@ __device__ __forceinline__ int64_t lower_bound_dev(const T* a, int64_t lo, int64
 // initial forward value of row i of front s: own right-hand side entry, or (sharded top fronts) the
 // exchanged sum of b and the other shards' subtree updates
 __device__ __forceinline__ double fwd_init(const FrontTab& T, int s, int i, int w, int f0, const double* __restrict__ b) {
+  // the caller's entry loaded unconditionally (clamped row): its two dependent loads issue beside the
+  // xoff load instead of after it (a load under a branch waits for everything before it)
+  const double bv = b[T.perm[f0 + min(i, max(w - 1, 0))]];
   const int64_t xo = T.xoff[s];
   if (xo >= 0) return T.xch[xo + i];
-  return (i < w) ? b[T.perm[f0 + i]] : 0.0;
+  return (i < w) ? bv : 0.0;
 }
 
 // Destination of update entry a of front s: its slot in the tree parent's contiguous gather range
@@ -82,6 +85,25 @@ __device__ __forceinline__ double fwd_init(const FrontTab& T, int s, int i, int 
 __device__ __forceinline__ double* uvec_dst(const FrontTab& T, int s, int a, double* uvec) {
   const int64_t p = T.upos[T.rel_ptr[s] + a];
   return p >= 0 ? T.gbuf + p : uvec + T.uvec_off[s] + a;
+}
+
+// uvec_dst of the rows lane + 64 h (h < NH) of front s for a whole wave at once: the front's words
+// once (uniform), every row's slot loaded unconditionally from a clamped row, then selected — uvec_dst
+// per row under its row mask was three dependent round trips per row (k_fwd_tree: nine before the
+// wait of every front, ~10 us of the level-1 fronts' start)
+template <int NH>
+__device__ __forceinline__ void uvec_dsts(const FrontTab& T, int s, int w, int r, int f0, bool act, int lane,
+                                          double* uvec, double* xi, double* (&dst)[NH]) {
+  const int64_t rp = T.rel_ptr[s], uo = T.uvec_off[s];
+  const int amax = r - w - 1;  // (uniform) the front's last update row
+  int64_t p[NH];
+#pragma unroll
+  for (int h = 0; h < NH; ++h) p[h] = amax >= 0 ? T.upos[rp + min(max(lane + 64 * h - w, 0), amax)] : -1;
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    const int i = lane + 64 * h;
+    dst[h] = (act && i >= w && i < r) ? (p[h] >= 0 ? T.gbuf + p[h] : uvec + uo + (i - w)) : xi + f0 + min(i, max(w - 1, 0));
+  }
 }
 
 // HBM panel (r x w, ld r) -> LDS (ld rl), all threads, 16 independent loads per thread per batch
@@ -2144,14 +2166,25 @@ __device__ __forceinline__ void fact_med_front(const FrontTab& T, int s, const i
     for (int base = 0; base < ne; base += FTN * 8) {
       double x[8];
       int64_t dst[8];
+      int32_t ra[8], rb[8];
+      bool ok[8];
+      // every load of the round first and unconditional (a, b are in range: e is clamped) — the
+      // relative indices loaded under `ok` compiled into a branch with a wait per entry, 8 serial
+      // round trips per round (r5: the critical level-3/4 medium fronts of supportcase10 spent 40-60
+      // us here)
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int e = min(base + k * FTN + tid, ne - 1);
         const int b = e / uc, a = e - b * uc;
-        const bool ok = base + k * FTN + tid < ne && a >= b;
+        ok[k] = base + k * FTN + tid < ne && a >= b;
         x[k] = __hip_atomic_load(U + max(a, b) + ucol_off(b, uc, uld), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        dst[k] = ok ? (int64_t)rl[a] + (int64_t)rl[b] * r : -1;
+        ra[k] = rl[a];
+        rb[k] = rl[b];
       }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(ra[k]), "+v"(rb[k]));
+#pragma unroll
+      for (int k = 0; k < 8; ++k) dst[k] = ok[k] ? (int64_t)ra[k] + (int64_t)rb[k] * r : -1;
       // the read-modify-writes: every F load of the round first, unconditional from clamped addresses
       // (a masked += compiled into a branch with a wait inside: 8 serial round trips per round)
       double f[8];
@@ -3856,11 +3889,11 @@ __device__ __forceinline__ void fwd_med_front(const FrontTab& T, int s, const do
   stage_fwd_chunk(L, buf[0], r, w, 0, 0, tid, NT);
   double v[4];
   double* dst[4];
+  uvec_dsts<4>(T, s, w, r, f0, wv == 0, lane, uvec, xi, dst);
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
     const int i = lane + 64 * h;
     v[h] = (i < r) ? v0[i] : 0.0;
-    dst[h] = (wv == 0 && i >= w && i < r) ? uvec_dst(T, s, i - w, uvec) : xi + f0 + min(i, w - 1);
   }
   __syncthreads();
   for (int c = 0; c < nch; ++c) {
@@ -4090,11 +4123,7 @@ __global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __re
     const int64_t pr0 = (tid < r) ? T.sv_ptr[e0 + tid] : 0, pr1 = (tid < r) ? T.sv_ptr[e0 + tid + 1] : 0;
     const double init = (tid < r) ? fwd_init(T, s, tid, w, f0, b) : 0.0;
     double* udst[3];  // wave 0: where its rows' results go (x for pivots, the parent's gather slot below)
-#pragma unroll
-    for (int h = 0; h < 3; ++h) {
-      const int i = (tid & 63) + 64 * h;
-      udst[h] = (tid < 64 && i >= w && i < r) ? uvec_dst(T, s, i - w, uvec) : xi + f0 + min(i, max(w - 1, 0));
-    }
+    uvec_dsts<3>(T, s, w, r, f0, tid < 64, tid & 63, uvec, xi, udst);
     // an elimination-tree root (r == w) also runs its backward substitution here:
     // its pivots and the caller's positions are loaded before the wait
     const bool rb = q == q1 - 1 && rootbwd[t];
@@ -4309,12 +4338,15 @@ __global__ __launch_bounds__(NT) void k_bwd_tree(FrontTab T, const int32_t* __re
     stage_colmajor(arena + T.l_off[s], Ls, r, w, ldc);
     const int32_t* __restrict__ rows = T.rows + T.row_ptr[s];
     const int nb = r - w;
-    double own[3];  // this front's forward values (previous launch): plain loads
+    double own[3];  // this front's forward values (previous launch): plain loads, unconditional from
+                    // clamped rows (loads under the mask compiled into a wait each), masked after
 #pragma unroll
     for (int h = 0; h < 3; ++h) {
-      const int j = lane + 64 * h;
-      own[h] = (tid < 64 && j < w) ? xi[f0 + j] / D[f0 + j] : 0.0;
+      const int jc = min(lane + 64 * h, max(w - 1, 0));
+      own[h] = xi[f0 + jc] / D[f0 + jc];
     }
+#pragma unroll
+    for (int h = 0; h < 3; ++h) own[h] = (tid < 64 && lane + 64 * h < w) ? own[h] : 0.0;
     static_assert(SMALL_SOLVE_MAX < NT, "k_bwd_tree: one update row per thread");
     const int rk = (tid < nb) ? rows[w + tid] : 0;  // symbolic: loaded before the wait
     int pj[3];  // wave 0: the caller's positions of its pivots
