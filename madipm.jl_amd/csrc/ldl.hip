@@ -1953,6 +1953,11 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
   const int ld = PK ? 0 : (r | 1);
   const FoldStart F0 = T.fstart[s];  // (with the front's other words: no dependent round trip later)
+  // the fold helper (if any) and its flag / image, loaded now — after the fold they were two dependent
+  // round trips in front of the children's wait
+  const int hh = T.absorb[s] ? T.fold_help[s] : -1;
+  const int hflag = hh >= 0 ? T.fhelp[hh].flag : 0;
+  const int64_t himg = hh >= 0 ? T.fhelp[hh].img : 0;
   {  // the front and its leaf batches must fit the launch's LDS: else a sticky error, never a write
      // past the carve (the symbolic analysis sizes both; this catches a plan that breaks it)
     const int ntot = PK ? r * (r + 1) / 2 : r * ld;
@@ -1998,13 +2003,12 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
     const int uc = T.nrows[c] - (T.first[c + 1] - T.first[c]);
     for (int a = tid; a < uc; a += FTN) rels[a] = T.rel[T.rel_ptr[c] + a];
   }
-  const int hh = T.absorb[s] ? T.fold_help[s] : -1;  // the fold helper that folded the first batches
   if (tid < 64) poll_deps(dep, q0, q1, flags, epoch, err);
-  if (hh >= 0 && tid == 0) poll_flag(flags + T.fhelp[hh].flag, epoch, err);
+  if (hh >= 0 && tid == 0) poll_flag(flags + hflag, epoch, err);  // the helper that folded the first batches
   __syncthreads();
   if (dg && tid == 0) dg[2] = wall_clock64();
   if (hh >= 0) {  // its image (this front's LDS layout) added entry by entry, 16 loads in flight per thread
-    const double* __restrict__ img = T.fimg + T.fhelp[hh].img;
+    const double* __restrict__ img = T.fimg + himg;
     const int ntot = PK ? r * (r + 1) / 2 : r * ld;
     for (int base = 0; base < ntot; base += FTN * 16) {
       double v[16];
