@@ -521,106 +521,121 @@ __global__ __launch_bounds__(NT) void k_asm_chunks(const int64_t* __restrict__ g
 
 // Phase 2: one workgroup (1024 threads) per 64x64 lower tile of F (SymbolicPlan step 10): thread t
 // owns the tile entries (row t & 63, columns t >> 6 + 16 k), k < 4.  Entry = sum of its chunk sums in
-// order; then the big children's update blocks are added child by child in child order, in the
-// owner's registers: per batch of ABN children the tile's row and column maps (tile row -> child row,
-// or -1) are built in LDS (one barrier), then every thread issues the batch's loads (ABN x 4 from
-// clamped addresses) and adds them, masked, in child order.  No atomics, deterministic, and no
-// barrier per child (r3 put one barrier and one round trip per child and tile: neos 8 ms per
-// factorisation).  The tile is written to the front (big: arena, ld r; small: scratch, ld r).
-constexpr int ANT = 1024, ABN = 4;
-// the tile's entries (this thread's: tile-local rows ei[m], columns ej[m], m < 4; the 1024 threads
-// cover the 64 x 64 tile) = chunk sums + big children's blocks
-__device__ __forceinline__ void asm_tile_sum(const FrontTab& T, const SymbolicPlan::AsmTile& tl,
-                                             const int32_t* __restrict__ gptr, const double* __restrict__ part,
-                                             const BigChildRec* __restrict__ brec, const double* __restrict__ arena,
-                                             const int (&ei)[4], const int (&ej)[4], double (&v)[4]) {
-  const int ti = tl.tij & 0xffff, tj = (tl.tij >> 16) & 0x7fff;
-  const int I0 = ti * 64, J0 = tj * 64;
-  const int tid = threadIdx.x, lane = tid & 63;
+// order; then, when the tile has big children, the entries go to an LDS tile and the children's
+// update blocks are added record by record in child order (asm_children_lds).  No atomics,
+// deterministic.  The tile is written to the front (big: arena, ld r; small: scratch, ld r).
+constexpr int ANT = 1024;
+// this thread's entries (tile-local rows ei[m], columns ej[m], m < 4; the 1024 threads cover the
+// 64 x 64 tile) = their chunk sums, each in chunk order: CU chunk sums per entry and round, 4 CU loads
+// in flight per thread
+template <int CU>
+__device__ __forceinline__ void asm_chunk_sum(const SymbolicPlan::AsmTile& tl, const int32_t* __restrict__ gptr,
+                                              const double* __restrict__ part, const int (&ei)[4], const int (&ej)[4],
+                                              double (&v)[4]) {
 #pragma unroll
   for (int m = 0; m < 4; ++m) v[m] = 0.0;
-  if (tl.gptr >= 0) {
-    const int32_t* __restrict__ gp = gptr + tl.gptr;
-    const double* __restrict__ pc = part + tl.gchk;
-    int q0[4], q1[4];
+  if (tl.gptr < 0) return;
+  const int32_t* __restrict__ gp = gptr + tl.gptr;
+  const double* __restrict__ pc = part + tl.gchk;
+  int q0[4], q1[4], len = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      q0[k] = gp[ei[k] + 64 * ej[k]];
-      q1[k] = gp[ei[k] + 64 * ej[k] + 1];
-    }
-    int len = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) len = max(len, q1[k] - q0[k]);
-    // 8 chunk sums per entry and round, 32 loads in flight per thread (a high-fan-in root entry
-    // has ~20 chunks: 3 rounds, not 5)
-    for (int it = 0; it < len; it += 8) {
-      double x[4][8];
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-#pragma unroll
-        for (int u = 0; u < 8; ++u) x[k][u] = pc[min(q0[k] + it + u, max(q1[k] - 1, q0[k]))];
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (q0[k] + it + u < q1[k]) v[k] += x[k][u];
-    }
+  for (int m = 0; m < 4; ++m) {
+    q0[m] = gp[ei[m] + 64 * ej[m]];
+    q1[m] = gp[ei[m] + 64 * ej[m] + 1];
   }
-  // big children: their (tile, child) records hold the tile's row / column maps (tile row -> child
-  // row, -1 outside the child; built once at plan time) and the child's U block: every thread reads
-  // its own entries' map slots and U entries — two dependent round trips per batch of ABN children,
-  // no LDS, no barrier (r3 staged the table in LDS and added children two by two between barriers;
-  // r4's first version built the maps in LDS from rel per batch: one round trip and two barriers more)
-  for (int kc = tl.bt0; kc < tl.bt1; kc += ABN) {  // uniform
-    const int nk = min(ABN, tl.bt1 - kc);
-    int64_t uo[ABN];
-    int ldc[ABN], a[ABN][4], bb[ABN][4];
 #pragma unroll
-    for (int k = 0; k < ABN; ++k) {
-      const BigChildRec& R = brec[kc + min(k, nk - 1)];
-      uo[k] = R.u_off;
-      ldc[k] = R.u_ld;
+  for (int m = 0; m < 4; ++m) len = max(len, q1[m] - q0[m]);
+  for (int it = 0; it < len; it += CU) {
+    double x[4][CU];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        a[k][m] = R.rmap[ei[m]];
-        bb[k][m] = R.cmap[ej[m]];
-      }
-    }
-    // every U load of the batch first (clamped to entry (0, 0) of the child's block), then the adds
-    double x[ABN][4];
+    for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int k = 0; k < ABN; ++k)
+      for (int u = 0; u < CU; ++u) x[m][u] = pc[min(q0[m] + it + u, max(q1[m] - 1, q0[m]))];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const bool hit = k < nk && a[k][m] >= 0 && bb[k][m] >= 0 && a[k][m] >= bb[k][m];
-        x[k][m] = arena[uo[k] + (hit ? a[k][m] + (int64_t)bb[k][m] * ldc[k] : 0)];
-        a[k][m] = hit;
-      }
+    for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int k = 0; k < ABN; ++k)
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-        if (a[k][m]) v[m] += x[k][m];
+      for (int u = 0; u < CU; ++u)
+        if (q0[m] + it + u < q1[m]) v[m] += x[m][u];
   }
-  (void)tid;
-  (void)lane;
-  (void)I0;
-  (void)J0;
 }
 
-__global__ __launch_bounds__(ANT) void k_assemble(FrontTab T, const SymbolicPlan::AsmTile* __restrict__ tiles,
-                                                  const int32_t* __restrict__ gptr, const double* __restrict__ part,
-                                                  const BigChildRec* __restrict__ brec, double* __restrict__ arena,
-                                                  double* __restrict__ fscratch) {
+// The big children's blocks added into the LDS tile Ts (64 x 64, column-major, ld 64), record by
+// record in child order (BigChildRec: a child's hits on the tile are the na x nb block of its U at
+// (a0, b0), <= 1024 entries per record): thread e takes the record's entry e — consecutive threads
+// read consecutive rows of the child's column, and a wave past the record's entries issues nothing —
+// and a barrier separates the records.  The loads of ABR records are in flight before the first
+// add.  r3-r5 had every thread pull its own four entries from every child through row / column maps:
+// ~5% of those loads hit (neos), and the address unit was the bound (TA busy 83%, r6_b).
+template <int ABR>
+__device__ __forceinline__ void asm_children_lds(int bt0, int bt1, const BigChildRec* __restrict__ brec,
+                                                 const double* __restrict__ arena, double* Ts) {
+  const int tid = threadIdx.x;
+  const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
+  for (int kc = bt0; kc < bt1; kc += ABR) {  // uniform
+    const int nk = min(ABR, bt1 - kc);
+    // the batch's record headers first (scalar loads, none waited for alone), then its entry loads
+    int4 h0[ABR], h1[ABR];
+#pragma unroll
+    for (int k = 0; k < ABR; ++k) {
+      const int4* __restrict__ hp = reinterpret_cast<const int4*>(brec + kc + min(k, nk - 1));
+      h0[k] = hp[0];
+      h1[k] = hp[1];
+    }
+    // the loaded values are only combined at the adds: nothing inside the uniform branch waits
+    double x[ABR];
+    int rb[ABR], cbt[ABR];
+    uint32_t ok = 0;
+#pragma unroll
+    for (int k = 0; k < ABR; ++k) {
+      x[k] = 0.0;
+      rb[k] = cbt[k] = 0;
+      const int64_t uo = (int64_t)(((uint64_t)(uint32_t)h0[k].y << 32) | (uint32_t)h0[k].x);
+      const int ldc = h0[k].z, a0 = h0[k].w, b0 = h1[k].x;
+      const int na = h1[k].y & 0xffff, nab = na * ((uint32_t)h1[k].y >> 16);
+      if (k < nk && wbase < nab) {  // uniform
+        const int e = min(tid, nab - 1);
+        const int j = (int)(((uint32_t)e * (uint32_t)h1[k].z) >> 16), i = e - j * na;
+        const int ra = a0 + i, cb = b0 + j;
+        x[k] = arena[uo + ra + (int64_t)cb * ldc];
+        const BigChildRec* __restrict__ R = brec + kc + k;
+        rb[k] = R->rows[i];
+        cbt[k] = R->cols[j];
+        ok |= (uint32_t)(tid < nab && ra >= cb) << k;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < ABR; ++k)
+      if (k < nk) {  // uniform
+        if ((ok >> k) & 1u) Ts[cbt[k] * 64 + rb[k]] += x[k];
+        __syncthreads();
+      }
+  }
+}
+
+// k_assemble runs two tiles per CU (8 waves per SIMD, <= 64 VGPRs: 2 chunk sums per entry and
+// round, 8 big-child records per batch)
+__global__ __launch_bounds__(ANT, 8) void k_assemble(FrontTab T, const SymbolicPlan::AsmTile* __restrict__ tiles,
+                                                     const int32_t* __restrict__ gptr, const double* __restrict__ part,
+                                                     const BigChildRec* __restrict__ brec, double* __restrict__ arena,
+                                                     double* __restrict__ fscratch) {
+  __shared__ double Ts[64 * 64];
   const SymbolicPlan::AsmTile tl = tiles[blockIdx.x];
   const int s = tl.front, ti = tl.tij & 0xffff, tj = (tl.tij >> 16) & 0x7fff;
   const bool acc = tl.tij < 0;  // SymbolicPlan::kAccumulate: F += tile (sharded top fronts, phase 2)
   const int r = T.nrows[s];
   const int I0 = ti * 64, J0 = tj * 64;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  double v[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int ei[4] = {lane, lane, lane, lane}, ej[4] = {wv, wv + 16, wv + 32, wv + 48};
-  asm_tile_sum(T, tl, gptr, part, brec, arena, ei, ej, v);
+  double v[4];
+  asm_chunk_sum<2>(tl, gptr, part, ei, ej, v);
+  if (tl.bt1 > tl.bt0) {  // uniform
+#pragma unroll
+    for (int m = 0; m < 4; ++m) Ts[ej[m] * 64 + lane] = v[m];
+    __syncthreads();
+    asm_children_lds<8>(tl.bt0, tl.bt1, brec, arena, Ts);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) v[m] = Ts[ej[m] * 64 + lane];
+  }
   const int64_t fso = T.fs_off[s];
   double* __restrict__ F = (fso >= 0 ? fscratch + fso : arena + T.l_off[s]);
   const int i = I0 + lane;
@@ -636,8 +651,8 @@ __global__ __launch_bounds__(ANT) void k_assemble(FrontTab T, const SymbolicPlan
 }
 
 // Single-panel big fronts (SymbolicPlan::fused, w <= 64): once k_big_diag / k_big_trsm have written
-// the panel's L and D, ONE pass per 64x64 tile assembles the trailing entries (asm_tile_sum, as
-// k_assemble) and subtracts L_I D L_J^T (K = w, f64 MFMA 16x16x4) before the tile's only store.  The
+// the panel's L and D, ONE pass per 64x64 tile assembles the trailing entries (asm_chunk_sum and
+// asm_children_lds, as k_assemble) and subtracts L_I D L_J^T (K = w, f64 MFMA 16x16x4) before the tile's only store.  The
 // level path moved every trailing entry through HBM three times (k_assemble's store, k_big_upd128's
 // load and store); neos' 1220 skinny big fronts (w <= 39, r up to 2.7k) are mostly trailing matrix.
 // Each of the 16 waves owns one 16x16 block, and each thread assembles exactly the four entries its
@@ -652,6 +667,7 @@ __global__ __launch_bounds__(ANT) void k_asm_update(FrontTab T, const SymbolicPl
                                                     const BigChildRec* __restrict__ brec, double* __restrict__ arena,
                                                     const double* __restrict__ D, int kmax) {
   extern __shared__ __attribute__((aligned(16))) double AUs[];
+  __shared__ double Ts[64 * 64];     // the assembled tile (tiles with big children)
   double* Wt = AUs;                  // (L D)[I rows], kmax x AU_LDT
   double* Lt = AUs + kmax * AU_LDT;  // L[J rows]
   const SymbolicPlan::AsmTile tl = tiles[blockIdx.x];
@@ -689,7 +705,15 @@ __global__ __launch_bounds__(ANT) void k_asm_update(FrontTab T, const SymbolicPl
     ej[g] = 16 * bj + (lane >> 4) + 4 * g;
   }
   double v[4];
-  asm_tile_sum(T, tl, gptr, part, brec, arena, ei, ej, v);
+  asm_chunk_sum<4>(tl, gptr, part, ei, ej, v);
+  if (tl.bt1 > tl.bt0) {  // uniform: big children through the LDS tile (as k_assemble)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) Ts[ej[g] * 64 + ei[g]] = v[g];
+    __syncthreads();
+    asm_children_lds<8>(tl.bt0, tl.bt1, brec, arena, Ts);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) v[g] = Ts[ej[g] * 64 + ei[g]];
+  }
   __syncthreads();  // the operands in LDS
   dbl4 acc = {0.0, 0.0, 0.0, 0.0};
   const int nks = (w + 3) >> 2;
@@ -4580,8 +4604,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   sv_src_.upload(S.sv_src);
   sv_nt_.alloc(std::max<int64_t>(S.row_ptr[S.nsuper], 1));  // the tree solve's split (set with its tables)
   sv_nt_.zero();
-  atiles_.upload(S.atiles);
-  g_ptr_.upload(S.g_ptr);
+  g_ptr_.upload(S.g_ptr);  // atiles_: with the big-child records below (bt renumbered)
   {
     // int32 sources when every arena / K index fits (leaf update blocks stay materialised: forming
     // them from the leaves' L panels in the gather was measured slower, r1 — 6 scattered loads per
@@ -4597,33 +4620,51 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   }
   g_chunk_.upload(S.g_chunk);
   gpart_.alloc(std::max<size_t>(S.g_chunk.size(), 1));
-  {  // big-child records of the assembly tiles (BigChildRec): the tile's row / column maps from rel
+  {  // big-child records of the assembly tiles (BigChildRec): a bt entry's block, split into column
+     // ranges of <= kBigRecEntries entries; the tiles' bt0 / bt1 renumbered to the records
     const int64_t nb = (int64_t)S.bt.size() / 5;
-    std::vector<BigChildRec> br(std::max<int64_t>(nb, 1));
+    std::vector<int64_t> rptr(nb + 1, 0);
+    for (int64_t k = 0; k < nb; ++k) {
+      const int32_t* e = &S.bt[5 * k];
+      const int na = e[4] - e[3], nbt = e[2] - e[1], cpr = kBigRecEntries / na;
+      MADIPM_REQUIRE(na >= 1 && na <= 64 && nbt >= 1 && nbt <= 64, "assembly: big-child block outside its tile");
+      rptr[k + 1] = rptr[k] + (nbt + cpr - 1) / cpr;
+    }
+    MADIPM_REQUIRE(rptr[nb] < INT32_MAX, "assembly: too many big-child records");
+    std::vector<BigChildRec> br(std::max<int64_t>(rptr[nb], 1));
     const int T = (int)std::min<int64_t>(analysis_threads(), std::max<int64_t>(1, nb / 4096));
     std::vector<std::thread> th;
-    std::atomic<bool> bad{false};
     for (int t = 0; t < T; ++t)
       th.emplace_back([&, t]() {
         for (int64_t k = t; k < nb; k += T) {
           const int32_t* e = &S.bt[5 * k];
           const int c = e[0], b0 = e[1], b1 = e[2], a0 = e[3], a1 = e[4];
           const int32_t* rel = S.rel.data() + S.rel_ptr[c];
-          BigChildRec& R = br[k];
-          R.u_off = S.u_off[c];
-          R.u_ld = S.u_ld[c];
-          R.pad = 0;
-          std::fill(R.rmap, R.rmap + 64, (int16_t)-1);
-          std::fill(R.cmap, R.cmap + 64, (int16_t)-1);
           const int I0 = rel[a0] & ~63, J0 = rel[b0] & ~63;
-          if (a1 > 32767 || b1 > 32767) bad = true;  // int16 maps
-          for (int q = a0; q < a1; ++q) R.rmap[rel[q] - I0] = (int16_t)q;
-          for (int q = b0; q < b1; ++q) R.cmap[rel[q] - J0] = (int16_t)q;
+          const int na = a1 - a0, cpr = kBigRecEntries / na;
+          for (int64_t q = rptr[k]; q < rptr[k + 1]; ++q) {
+            BigChildRec& R = br[q];
+            R = BigChildRec{};
+            R.u_off = S.u_off[c];
+            R.u_ld = S.u_ld[c];
+            R.a0 = a0;
+            R.b0 = b0 + (int)(q - rptr[k]) * cpr;
+            R.na = (uint16_t)na;
+            R.nb = (uint16_t)std::min(cpr, b1 - R.b0);
+            R.na_inv = (65536u + na - 1) / na;
+            for (int i = 0; i < na; ++i) R.rows[i] = (uint8_t)(rel[a0 + i] - I0);
+            for (int j = 0; j < R.nb; ++j) R.cols[j] = (uint8_t)(rel[R.b0 + j] - J0);
+          }
         }
       });
     for (auto& x : th) x.join();
-    MADIPM_REQUIRE(!bad, "assembly: a child update block of more than 32767 rows");
     brec_.upload(br);
+    std::vector<SymbolicPlan::AsmTile> at(S.atiles);
+    for (auto& a : at) {
+      a.bt0 = (int32_t)rptr[a.bt0];
+      a.bt1 = (int32_t)rptr[a.bt1];
+    }
+    atiles_.upload(at);
   }
   fscratch_.alloc(std::max<int64_t>(S.fs_size, 1));
   T_.fs_off = fs_off_;

@@ -102,12 +102,18 @@ struct FrontTab {
 constexpr int32_t kErrHandoff = 1;   // a dependency hand-off (flag poll) timed out
 constexpr int32_t kErrLdsCarve = 2;  // a k_fact_tree front or leaf batch did not fit its LDS carve
 
-// assembly: a big child's block on one 64x64 tile of its parent (SymbolicPlan::bt entry): the tile's
-// row and column maps (tile row -> the child's update row, -1 outside the child) and the child's U
+// assembly: a big child's block on one 64x64 tile of its parent (SymbolicPlan::bt entry, split by
+// column ranges so that na * nb <= kBigRecEntries).  The child's update rows on the tile are the
+// consecutive rows a0 .. a0 + na - 1 (its rows are a sorted subset of the parent's), its columns
+// b0 .. b0 + nb - 1; rows[i] / cols[j] = their tile row / column.  Entry e < na nb of the record is
+// (i, j) = (e mod na, e div na), e div na = (e * na_inv) >> 16 (exact for e < 1024, na <= 64).
+constexpr int kBigRecEntries = 1024;
 struct BigChildRec {
   int64_t u_off;
-  int32_t u_ld, pad;
-  int16_t rmap[64], cmap[64];
+  int32_t u_ld, a0, b0;
+  uint16_t na, nb;
+  uint32_t na_inv, pad;
+  uint8_t rows[64], cols[64];
 };
 
 struct SolveTask {

@@ -1,0 +1,11 @@
+#!/bin/bash
+# k_assemble at two tiles per CU: ldl GPU tests, neos bench, neos rocprof timeline
+set -o pipefail
+TAG=${1:?tag}
+OUT=gpurun_out/$TAG; mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_ldl_gpu.py -m gpu > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
+tail -2 $OUT/pytest.log
+timeout -k 10 300 python bench.py --config neos --steps 8 --warmup 2 --no-cpu --no-neos --no-opt --no-highs > $OUT/bench_neos.log 2>&1 || { tail -20 $OUT/bench_neos.log; exit 1; }
+tail -1 $OUT/bench_neos.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('neos', round(d['value'],2))"
+bash tools/gpu_prof.sh $TAG "neos" 4 || exit 1
+grep -E "k_assemble|k_asm" $OUT/neos_iter_timeline.txt
