@@ -519,44 +519,61 @@ __global__ __launch_bounds__(NT) void k_asm_chunks(const int64_t* __restrict__ g
   part[c] = v;
 }
 
-// Phase 2: one workgroup (1024 threads) per 64x64 lower tile of F (SymbolicPlan step 10): thread t
-// owns the tile entries (row t & 63, columns t >> 6 + 16 k), k < 4.  Entry = sum of its chunk sums in
-// order; then, when the tile has big children, the entries go to an LDS tile and the children's
-// update blocks are added record by record in child order (asm_children_lds).  No atomics,
-// deterministic.  The tile is written to the front (big: arena, ld r; small: scratch, ld r).
+// Phase 2: one workgroup (1024 threads) per 64x64 lower tile of F (SymbolicPlan step 10), assembled
+// in an LDS tile: entry = sum of its chunk sums in chunk order (asm_chunks_lds), then the big
+// children's update blocks record by record in child order (asm_children_lds); thread t writes out
+// the entries (row t & 63, columns t >> 6 + 16 k), k < 4.  No atomics, deterministic.  The tile is written to the front (big: arena, ld r; small: scratch, ld r).
 constexpr int ANT = 1024;
-// this thread's entries (tile-local rows ei[m], columns ej[m], m < 4; the 1024 threads cover the
-// 64 x 64 tile) = their chunk sums, each in chunk order: CU chunk sums per entry and round, 4 CU loads
-// in flight per thread
+// The tile's chunk sums into the LDS tile Ts (64 x 64, column-major, ld 64; zeroed first): the
+// tile's nonempty entries (its g_ptr list: ne, then position | first chunk << 12 per entry, then the
+// chunk count << 12) spread over the threads, up to 4 per thread, each entry's chunk sums added in
+// chunk order, CU per entry and round in flight.  A wave past the list issues no load.  Ends with a
+// barrier.  (r3-r5 read a dense 4097-offset table per tile: 32 KB of offset loads for a tree front's
+// tile of ~40 nonempty entries, neos.)
 template <int CU>
-__device__ __forceinline__ void asm_chunk_sum(const SymbolicPlan::AsmTile& tl, const int32_t* __restrict__ gptr,
-                                              const double* __restrict__ part, const int (&ei)[4], const int (&ej)[4],
-                                              double (&v)[4]) {
+__device__ __forceinline__ void asm_chunks_lds(const SymbolicPlan::AsmTile& tl, const int32_t* __restrict__ gent,
+                                               const double* __restrict__ part, double* Ts) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
 #pragma unroll
-  for (int m = 0; m < 4; ++m) v[m] = 0.0;
-  if (tl.gptr < 0) return;
-  const int32_t* __restrict__ gp = gptr + tl.gptr;
-  const double* __restrict__ pc = part + tl.gchk;
-  int q0[4], q1[4], len = 0;
+  for (int m = 0; m < 4; ++m) Ts[(wv + 16 * m) * 64 + lane] = 0.0;
+  __syncthreads();
+  if (tl.gptr >= 0) {  // uniform
+    const int32_t* __restrict__ ge = gent + tl.gptr;
+    const double* __restrict__ pc = part + tl.gchk;
+    const int ne = ge[0];
+    int pos[4], c0[4], c1[4], len = 0;
 #pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    q0[m] = gp[ei[m] + 64 * ej[m]];
-    q1[m] = gp[ei[m] + 64 * ej[m] + 1];
-  }
+    for (int m = 0; m < 4; ++m) {
+      pos[m] = -1;
+      c0[m] = c1[m] = 0;
+      if (wbase + ANT * m < ne) {  // uniform
+        const int k = tid + ANT * m, kk = min(k, ne - 1);
+        const int e0 = ge[1 + kk], e1 = ge[2 + kk];
+        c0[m] = e0 >> 12;
+        c1[m] = k < ne ? e1 >> 12 : c0[m];
+        pos[m] = k < ne ? (e0 & 4095) : -1;
+        len = max(len, c1[m] - c0[m]);
+      }
+    }
+    double v[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int it = 0; it < len; it += CU) {
+      double x[4][CU];
 #pragma unroll
-  for (int m = 0; m < 4; ++m) len = max(len, q1[m] - q0[m]);
-  for (int it = 0; it < len; it += CU) {
-    double x[4][CU];
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int u = 0; u < CU; ++u) x[m][u] = pc[min(c0[m] + it + u, max(c1[m] - 1, c0[m]))];
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int u = 0; u < CU; ++u)
+          if (c0[m] + it + u < c1[m]) v[m] += x[m][u];
+    }
 #pragma unroll
     for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int u = 0; u < CU; ++u) x[m][u] = pc[min(q0[m] + it + u, max(q1[m] - 1, q0[m]))];
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int u = 0; u < CU; ++u)
-        if (q0[m] + it + u < q1[m]) v[m] += x[m][u];
+      if (pos[m] >= 0) Ts[pos[m]] = v[m];
   }
+  __syncthreads();
 }
 
 // The big children's blocks added into the LDS tile Ts (64 x 64, column-major, ld 64), record by
@@ -613,7 +630,7 @@ __device__ __forceinline__ void asm_children_lds(int bt0, int bt1, const BigChil
 }
 
 // k_assemble runs two tiles per CU (8 waves per SIMD, <= 64 VGPRs: 2 chunk sums per entry and
-// round, 8 big-child records per batch)
+// round, 8 big-child records per batch; 32 KB of LDS each)
 __global__ __launch_bounds__(ANT, 8) void k_assemble(FrontTab T, const SymbolicPlan::AsmTile* __restrict__ tiles,
                                                      const int32_t* __restrict__ gptr, const double* __restrict__ part,
                                                      const BigChildRec* __restrict__ brec, double* __restrict__ arena,
@@ -625,17 +642,11 @@ __global__ __launch_bounds__(ANT, 8) void k_assemble(FrontTab T, const SymbolicP
   const int r = T.nrows[s];
   const int I0 = ti * 64, J0 = tj * 64;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int ei[4] = {lane, lane, lane, lane}, ej[4] = {wv, wv + 16, wv + 32, wv + 48};
+  asm_chunks_lds<2>(tl, gptr, part, Ts);
+  asm_children_lds<8>(tl.bt0, tl.bt1, brec, arena, Ts);
   double v[4];
-  asm_chunk_sum<2>(tl, gptr, part, ei, ej, v);
-  if (tl.bt1 > tl.bt0) {  // uniform
 #pragma unroll
-    for (int m = 0; m < 4; ++m) Ts[ej[m] * 64 + lane] = v[m];
-    __syncthreads();
-    asm_children_lds<8>(tl.bt0, tl.bt1, brec, arena, Ts);
-#pragma unroll
-    for (int m = 0; m < 4; ++m) v[m] = Ts[ej[m] * 64 + lane];
-  }
+  for (int m = 0; m < 4; ++m) v[m] = Ts[(wv + 16 * m) * 64 + lane];
   const int64_t fso = T.fs_off[s];
   double* __restrict__ F = (fso >= 0 ? fscratch + fso : arena + T.l_off[s]);
   const int i = I0 + lane;
@@ -651,14 +662,14 @@ __global__ __launch_bounds__(ANT, 8) void k_assemble(FrontTab T, const SymbolicP
 }
 
 // Single-panel big fronts (SymbolicPlan::fused, w <= 64): once k_big_diag / k_big_trsm have written
-// the panel's L and D, ONE pass per 64x64 tile assembles the trailing entries (asm_chunk_sum and
+// the panel's L and D, ONE pass per 64x64 tile assembles the trailing entries (asm_chunks_lds and
 // asm_children_lds, as k_assemble) and subtracts L_I D L_J^T (K = w, f64 MFMA 16x16x4) before the tile's only store.  The
 // level path moved every trailing entry through HBM three times (k_assemble's store, k_big_upd128's
 // load and store); neos' 1220 skinny big fronts (w <= 39, r up to 2.7k) are mostly trailing matrix.
 // Each of the 16 waves owns one 16x16 block, and each thread assembles exactly the four entries its
 // MFMA result holds (no result tile in LDS); the operands are staged [k][row] for the K = kmax rows
-// the launch needs (dynamic LDS: 2 x kmax x 80 doubles, 51 KB at neos' w <= 39 — two workgroups per
-// CU).  Column block 0's tiles (assembled for the panel by k_assemble) get their columns >= w here.
+// the launch needs (dynamic LDS: 2 x kmax x 80 doubles, 51 KB at neos' w <= 39, beside the 32 KB
+// assembled tile).  Column block 0's tiles (assembled for the panel by k_assemble) get their columns >= w here.
 // Operands and MFMA order are k_big_upd128's (A = L_J, B = (L D)_I, K ascending, one accumulator):
 // the same U bit for bit.
 constexpr int AU_LDT = 80;  // [k][row] operand stride (conflict-free ds_read_b64 for the 16x4 pattern)
@@ -667,7 +678,7 @@ __global__ __launch_bounds__(ANT) void k_asm_update(FrontTab T, const SymbolicPl
                                                     const BigChildRec* __restrict__ brec, double* __restrict__ arena,
                                                     const double* __restrict__ D, int kmax) {
   extern __shared__ __attribute__((aligned(16))) double AUs[];
-  __shared__ double Ts[64 * 64];     // the assembled tile (tiles with big children)
+  __shared__ double Ts[64 * 64];     // the assembled tile
   double* Wt = AUs;                  // (L D)[I rows], kmax x AU_LDT
   double* Lt = AUs + kmax * AU_LDT;  // L[J rows]
   const SymbolicPlan::AsmTile tl = tiles[blockIdx.x];
@@ -704,16 +715,11 @@ __global__ __launch_bounds__(ANT) void k_asm_update(FrontTab T, const SymbolicPl
     ei[g] = 16 * bi + (lane & 15);
     ej[g] = 16 * bj + (lane >> 4) + 4 * g;
   }
+  asm_chunks_lds<4>(tl, gptr, part, Ts);
+  asm_children_lds<8>(tl.bt0, tl.bt1, brec, arena, Ts);
   double v[4];
-  asm_chunk_sum<4>(tl, gptr, part, ei, ej, v);
-  if (tl.bt1 > tl.bt0) {  // uniform: big children through the LDS tile (as k_assemble)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) Ts[ej[g] * 64 + ei[g]] = v[g];
-    __syncthreads();
-    asm_children_lds<8>(tl.bt0, tl.bt1, brec, arena, Ts);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) v[g] = Ts[ej[g] * 64 + ei[g]];
-  }
+  for (int g = 0; g < 4; ++g) v[g] = Ts[ej[g] * 64 + ei[g]];
   __syncthreads();  // the operands in LDS
   dbl4 acc = {0.0, 0.0, 0.0, 0.0};
   const int nks = (w + 3) >> 2;
@@ -4995,7 +5001,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       const int r = S.nrows[at.front], ti = at.tij & 0xffff, tj = (at.tij >> 16) & 0x7fff;
       const double nr = std::min(64, r - 64 * ti), nc = std::min(64, r - 64 * tj);
       L.bytes += 8.0 * (ti == tj ? nr * (nr + 1) / 2 : nr * nc) * (at.tij < 0 ? 2.0 : 1.0) +
-                 (at.gptr >= 0 ? 4.0 * 4097 : 0.0);
+                 (at.gptr >= 0 ? 4.0 * (S.g_ptr[at.gptr] + 2) : 0.0);
       for (int k = at.bt0; k < at.bt1; ++k) {
         const int32_t* e = &S.bt[5 * k];
         for (int b = e[1]; b < e[2]; ++b) L.bytes += 8.0 * std::max(0, e[4] - std::max(b, e[3]));
@@ -5154,7 +5160,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
             const int ti = at.tij & 0xffff, tj = (at.tij >> 16) & 0x7fff;
             const double nr = std::min(64, r - 64 * ti), nc = std::min(64, r - 64 * tj);
             // the written entries + the chunk sums' offsets + the panel rows of I and J (+ big children)
-            L.bytes += 8.0 * (ti == tj ? nr * (nr + 1) / 2 : nr * nc) + (at.gptr >= 0 ? 4.0 * 4097 : 0.0) +
+            L.bytes += 8.0 * (ti == tj ? nr * (nr + 1) / 2 : nr * nc) + (at.gptr >= 0 ? 4.0 * (S.g_ptr[at.gptr] + 2) : 0.0) +
                        8.0 * (nr + nc) * w;
             for (int k = at.bt0; k < at.bt1; ++k) {
               const int32_t* e = &S.bt[5 * k];

@@ -1856,15 +1856,23 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
               std::vector<int32_t> fill(cnt.begin(), cnt.end() - 1);
               for (int64_t e = e0; e < e1; ++e) sorted[e0 + fill[bykey[e]]++] = bysrc[e];
             }
+            // the tile's entry list: ne, then per nonempty entry its position | first chunk << 12,
+            // then the chunk count << 12 (a dense 4097-offset table per tile was 1.5 GB on neos,
+            // mostly for tree-front tiles of ~40 nonempty entries)
             at.gptr = (int64_t)P.g_ptr.size();
             at.gchk = (int64_t)P.g_chunk.size();
-            int32_t nchk = 0;
+            int32_t nchk = 0, ne = 0;
             const int64_t sbase = (int64_t)P.g_src.size();
+            P.g_ptr.push_back(0);
             for (int k = 0; k < 4096; ++k) {
-              P.g_ptr.push_back(nchk);
+              if (cnt[k + 1] == cnt[k]) continue;
+              P.g_ptr.push_back(k | nchk << 12);
+              ++ne;
               for (int64_t c = cnt[k]; c < cnt[k + 1]; c += SymbolicPlan::kChunk, ++nchk) P.g_chunk.push_back(sbase + c);
             }
-            P.g_ptr.push_back(nchk);
+            MADIPM_REQUIRE(nchk < (1 << 19), "assembly: more than 2^19 chunks on one tile");
+            P.g_ptr.push_back(nchk << 12);
+            P.g_ptr[at.gptr] = ne;
             P.g_src.insert(P.g_src.end(), sorted.begin() + e0, sorted.begin() + e1);
           } else {
             at.gptr = -1;
@@ -2041,7 +2049,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
         bc += nb;
         bmax = std::max(bmax, nb);
         if (A.gptr >= 0) {
-          const double c = S.g_ptr[A.gptr + 4096] - S.g_ptr[A.gptr];
+          const double c = S.g_ptr[A.gptr + S.g_ptr[A.gptr] + 1] >> 12;
           ch += c;
           chmax = std::max(chmax, c);
           nent += 4096;

@@ -100,7 +100,7 @@ struct SymbolicPlan {
   struct AsmTile {
     int32_t front, tij;    // tij = ti | tj << 16 (| kAccumulate)
     int32_t bt0, bt1;      // range in bt (5 ints per big-child block: child, b0, b1, a0, a1)
-    int64_t gptr, gchk;    // base of the 4097 per-entry chunk offsets in g_ptr (-1: none), first chunk
+    int64_t gptr, gchk;    // the tile's entry list in g_ptr (-1: none; ne, ne x (pos | chunk << 12), nchk << 12), first chunk
   };
   std::vector<AsmTile> atiles;
   // assembly groups (ranges of atiles / chunks): g in [0, nlevels) = phase-1 levels (this shard's
