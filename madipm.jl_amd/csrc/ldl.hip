@@ -526,7 +526,7 @@ __global__ __launch_bounds__(NT) void k_asm_chunks(const int64_t* __restrict__ g
 constexpr int ANT = 1024;
 // The tile's chunk sums into the LDS tile Ts (64 x 64, column-major, ld 64; zeroed first): the
 // tile's nonempty entries (its g_ptr list: ne, then position | first chunk << 12 per entry, then the
-// chunk count << 12) spread over the threads, up to 4 per thread, each entry's chunk sums added in
+// chunk count << 12; ne also in the device tile's gptr >> 48) spread over the threads, up to 4 per thread, each entry's chunk sums added in
 // chunk order, CU per entry and round in flight.  A wave past the list issues no load.  Ends with a
 // barrier.  (r3-r5 read a dense 4097-offset table per tile: 32 KB of offset loads for a tree front's
 // tile of ~40 nonempty entries, neos.)
@@ -539,9 +539,9 @@ __device__ __forceinline__ void asm_chunks_lds(const SymbolicPlan::AsmTile& tl, 
   for (int m = 0; m < 4; ++m) Ts[(wv + 16 * m) * 64 + lane] = 0.0;
   __syncthreads();
   if (tl.gptr >= 0) {  // uniform
-    const int32_t* __restrict__ ge = gent + tl.gptr;
+    const int32_t* __restrict__ ge = gent + (tl.gptr & (((int64_t)1 << 48) - 1));
     const double* __restrict__ pc = part + tl.gchk;
-    const int ne = ge[0];
+    const int ne = (int)(tl.gptr >> 48);
     int pos[4], c0[4], c1[4], len = 0;
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
@@ -630,8 +630,11 @@ __device__ __forceinline__ void asm_children_lds(int bt0, int bt1, const BigChil
 }
 
 // k_assemble runs two tiles per CU (8 waves per SIMD, <= 64 VGPRs: 2 chunk sums per entry and
-// round, 8 big-child records per batch; 32 KB of LDS each)
-__global__ __launch_bounds__(ANT, 8) void k_assemble(FrontTab T, const SymbolicPlan::AsmTile* __restrict__ tiles,
+// round, 8 big-child records per batch; 32 KB of LDS each).  Launches of few tiles (a root's
+// high-fan-in assembly: ex10's 3 root tiles, up to 8 chunks per entry) take the CU = 8 instance,
+// one round of chunk loads per entry, one tile per CU.
+template <int CU>
+__global__ __launch_bounds__(ANT, CU == 2 ? 8 : 4) void k_assemble(FrontTab T, const SymbolicPlan::AsmTile* __restrict__ tiles,
                                                      const int32_t* __restrict__ gptr, const double* __restrict__ part,
                                                      const BigChildRec* __restrict__ brec, double* __restrict__ arena,
                                                      double* __restrict__ fscratch) {
@@ -642,7 +645,7 @@ __global__ __launch_bounds__(ANT, 8) void k_assemble(FrontTab T, const SymbolicP
   const int r = T.nrows[s];
   const int I0 = ti * 64, J0 = tj * 64;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  asm_chunks_lds<2>(tl, gptr, part, Ts);
+  asm_chunks_lds<CU>(tl, gptr, part, Ts);
   asm_children_lds<8>(tl.bt0, tl.bt1, brec, arena, Ts);
   double v[4];
 #pragma unroll
@@ -4669,6 +4672,9 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     for (auto& a : at) {
       a.bt0 = (int32_t)rptr[a.bt0];
       a.bt1 = (int32_t)rptr[a.bt1];
+      // the tile's nonempty-entry count rides in gptr's top 16 bits (asm_chunks_lds: no load of it)
+      MADIPM_REQUIRE(a.gptr < ((int64_t)1 << 48), "assembly: entry list offset past 2^48");
+      if (a.gptr >= 0) a.gptr |= (int64_t)S.g_ptr[a.gptr] << 48;
     }
     atiles_.upload(at);
   }
@@ -5654,7 +5660,8 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
                             : k_asm_chunks<int64_t><<<(unsigned)cdiv(L.nchunk, NT), NT, 0, s>>>(
                                   g_chunk_, g_src_, L.chunk0, L.nchunk, Kx, arena_, gpart_)));
         TIMED(KK_ASSEMBLE, L.bytes, 0.0, L.flops,
-              (k_assemble<<<(unsigned)L.items, ANT, 0, s>>>(T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_)));
+              (L.items < 256 ? k_assemble<8><<<(unsigned)L.items, ANT, 0, s>>>(T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_)
+                             : k_assemble<2><<<(unsigned)L.items, ANT, 0, s>>>(T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_)));
         break;
       case MICRO:
         TIMED(KK_TINY, L.bytes, L.alg, L.flops,

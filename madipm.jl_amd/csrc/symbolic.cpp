@@ -2042,21 +2042,37 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     for (size_t g = 0; g + 1 < S.atile_lev.size(); ++g) {
       const int32_t t0 = S.atile_lev[g], t1 = S.atile_lev[g + 1];
       if (t1 <= t0) continue;
-      double bc = 0, bmax = 0, ch = 0, chmax = 0, nent = 0;
+      double bc = 0, bmax = 0, ch = 0, chmax = 0, nent = 0, nne = 0, nsrc = 0, c1 = 0, smax = 0, s16 = 0, s64 = 0;
       for (int32_t t = t0; t < t1; ++t) {
         const auto& A = S.atiles[t];
         const double nb = (A.bt1 - A.bt0);
         bc += nb;
         bmax = std::max(bmax, nb);
         if (A.gptr >= 0) {
-          const double c = S.g_ptr[A.gptr + S.g_ptr[A.gptr] + 1] >> 12;
+          const int32_t ne = S.g_ptr[A.gptr];
+          const double c = S.g_ptr[A.gptr + ne + 1] >> 12;
           ch += c;
           chmax = std::max(chmax, c);
           nent += 4096;
+          nne += ne;
+          for (int64_t k = 0; k < (int64_t)c; ++k) {
+            const int64_t q = A.gchk + k, ns = S.g_chunk[q + 1] - S.g_chunk[q];
+            nsrc += (double)ns;
+            c1 += ns == 1;
+          }
+          for (int32_t e = 0; e < ne; ++e) {
+            const int32_t ce = (S.g_ptr[A.gptr + 2 + e] >> 12) - (S.g_ptr[A.gptr + 1 + e] >> 12);
+            const int64_t se = S.g_chunk[A.gchk + (S.g_ptr[A.gptr + 1 + e] >> 12) + ce] - S.g_chunk[A.gchk + (S.g_ptr[A.gptr + 1 + e] >> 12)];
+            smax = std::max(smax, (double)se);
+            s16 += se > 16;
+            s64 += se > 64;
+          }
         }
       }
-      fprintf(stderr, "asm group %zu: %d tiles  big-child blocks %.1f/tile (max %.0f)  chunks %.2f/entry (tile max %.0f)\n", g,
-              t1 - t0, bc / (t1 - t0), bmax, nent > 0 ? ch / nent : 0.0, chmax);
+      fprintf(stderr, "asm group %zu: %d tiles  big-child blocks %.1f/tile (max %.0f)  chunks %.2f/entry (tile max %.0f)"
+              "  nonempty entries %.0f/tile  sources %.2f/chunk  single-source chunks %.0f%%  entry sources max %.0f, >16 %.0f, >64 %.0f\n", g,
+              t1 - t0, bc / (t1 - t0), bmax, nent > 0 ? ch / nent : 0.0, chmax, nne / (t1 - t0), ch > 0 ? nsrc / ch : 0.0,
+              ch > 0 ? 100.0 * c1 / ch : 0.0, smax, s16, s64);
     }
   }
 
