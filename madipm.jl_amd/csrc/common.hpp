@@ -13,26 +13,9 @@
 #include <utility>
 #include <vector>
 
-namespace madipm {
+#include "hvec.hpp"
 
-// allocator whose resize() leaves new elements uninitialised: big host index / value arrays that the
-// threads filling them write in full (first touch in parallel instead of a serial zero fill)
-template <class T>
-struct NoInit : std::allocator<T> {
-  template <class U>
-  struct rebind {
-    using other = NoInit<U>;
-  };
-  NoInit() = default;
-  template <class U>
-  NoInit(const NoInit<U>&) {}
-  template <class U>
-  void construct(U* p) { ::new ((void*)p) U; }
-  template <class U, class... A>
-  void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
-};
-template <class T>
-using hvec = std::vector<T, NoInit<T>>;
+namespace madipm {
 
 // Thread-local last error text, returned by madipm_last_error().
 void set_last_error(const std::string& msg);
@@ -85,7 +68,8 @@ struct DBuf {
     if (count > n) alloc(count);
     if (count) MADIPM_HIP(hipMemcpyAsync(p, h, count * sizeof(T), hipMemcpyHostToDevice, s));
   }
-  void upload(const std::vector<T>& v, hipStream_t s = nullptr) { upload(v.data(), v.size(), s); }
+  template <class A>
+  void upload(const std::vector<T, A>& v, hipStream_t s = nullptr) { upload(v.data(), v.size(), s); }
   void zero(hipStream_t s = nullptr) {
     if (n) MADIPM_HIP(hipMemsetAsync(p, 0, n * sizeof(T), s));
   }

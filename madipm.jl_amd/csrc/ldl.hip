@@ -4618,10 +4618,27 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     // int32 sources when every arena / K index fits (leaf update blocks stay materialised: forming
     // them from the leaves' L panels in the gather was measured slower, r1 — 6 scattered loads per
     // source instead of 1)
-    bool fits = !S.g_src.empty();
-    for (int64_t q : S.g_src) fits = fits && q >= INT32_MIN && q < (1LL << 30);
+    // (the check and the narrowing on the analysis threads: ~170 M sources on neos)
+    const int64_t ns = (int64_t)S.g_src.size();
+    const int T = (int)std::max<int64_t>(1, std::min<int64_t>(analysis_threads(), ns / 4000000));
+    hvec<int32_t> g32(ns);
+    std::atomic<bool> fits{ns > 0};
+    {
+      std::vector<std::thread> th;
+      for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t]() {
+          const int64_t q0 = ns * t / T, q1 = ns * (t + 1) / T;
+          bool ok = true;
+          for (int64_t q = q0; q < q1; ++q) {
+            const int64_t v = S.g_src[q];
+            ok = ok && v >= INT32_MIN && v < (1LL << 30);
+            g32[q] = (int32_t)v;
+          }
+          if (!ok) fits = false;
+        });
+      for (auto& x : th) x.join();
+    }
     if (fits) {
-      std::vector<int32_t> g32(S.g_src.begin(), S.g_src.end());
       g_src32_.upload(g32);
     } else {
       g_src_.upload(S.g_src);

@@ -11,6 +11,8 @@
 #include <atomic>
 #include <vector>
 
+#include "hvec.hpp"
+
 namespace madipm {
 
 // cap (optional): AMD stops early — returns false, perm empty — once a lower bound of its order's
@@ -116,8 +118,8 @@ struct SymbolicPlan {
   std::vector<uint8_t> fused;
   std::vector<int32_t> atile_fz0, atile_fz1;
   std::vector<int32_t> g_ptr, bt;
-  std::vector<int64_t> g_chunk;        // chunk c = sources [g_chunk[c], g_chunk[c+1])
-  std::vector<int64_t> g_src;          // >= 0: arena index; < 0: ~(index into caller's values)
+  hvec<int64_t> g_chunk;               // chunk c = sources [g_chunk[c], g_chunk[c+1])
+  hvec<int64_t> g_src;                 // >= 0: arena index; < 0: ~(index into caller's values)
   std::vector<int64_t> fs_off;         // small fronts with children, tree fronts: r x r scratch (else -1)
   static constexpr int kFactTreeMax = 192;
   // medium tree fronts (kFactTreeMax < r <= kFactTreeMedMax): factorised by k_fact_tree in HBM, one
