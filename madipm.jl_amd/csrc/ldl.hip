@@ -496,11 +496,13 @@ __global__ __launch_bounds__(NT) void k_tiny_factor(FrontTab T, const int32_t* _
 // Chunk sums: thread per chunk of <= kChunk sources, summed in source order.  Sources are int32
 // when the arena and K fit (IDX = int32_t), else int64.
 template <typename IDX>
-__global__ __launch_bounds__(NT) void k_asm_chunks(const int64_t* __restrict__ gchunk, const IDX* __restrict__ gsrc,
-                                                   int64_t c0, int64_t n, const double* __restrict__ Kx,
-                                                   const double* __restrict__ arena, double* __restrict__ part) {
-  const int64_t c = c0 + (int64_t)blockIdx.x * NT + threadIdx.x;
-  if (c >= c0 + n) return;
+__global__ __launch_bounds__(NT) void k_asm_chunks(const int64_t* __restrict__ ids, const int64_t* __restrict__ gchunk,
+                                                   const IDX* __restrict__ gsrc, int64_t c0, int64_t n,
+                                                   const double* __restrict__ Kx, const double* __restrict__ arena,
+                                                   double* __restrict__ part) {
+  const int64_t ci = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (ci >= n) return;
+  const int64_t c = ids[c0 + ci];  // the chunks of the launch's chunk-path tiles (asm_chunks_lds)
   const int64_t p0 = gchunk[c], p1 = gchunk[c + 1];
   constexpr int KC = SymbolicPlan::kChunk;
   // every index, then every value operand in flight before the sum: unconditional loads (clamped
@@ -524,22 +526,102 @@ __global__ __launch_bounds__(NT) void k_asm_chunks(const int64_t* __restrict__ g
 // children's update blocks record by record in child order (asm_children_lds); thread t writes out
 // the entries (row t & 63, columns t >> 6 + 16 k), k < 4.  No atomics, deterministic.  The tile is written to the front (big: arena, ld r; small: scratch, ld r).
 constexpr int ANT = 1024;
+// tiles of at most kAsmLdsWin windows of kAsmLdsSrc sources sum them from LDS (asm_chunks_lds),
+// without k_asm_chunks
+constexpr int kAsmLdsSrc = 5 * ANT, kAsmLdsWin = 4;
 // The tile's chunk sums into the LDS tile Ts (64 x 64, column-major, ld 64; zeroed first): the
 // tile's nonempty entries (its g_ptr list: ne, then position | first chunk << 12 per entry, then the
-// chunk count << 12; ne also in the device tile's gptr >> 48) spread over the threads, up to 4 per thread, each entry's chunk sums added in
+// chunk count << 12; ne also in the device tile's gptr >> 48, bit 47: the source path below) spread
+// over the threads, up to 4 per thread, each entry's chunk sums added in
 // chunk order, CU per entry and round in flight.  A wave past the list issues no load.  Ends with a
 // barrier.  (r3-r5 read a dense 4097-offset table per tile: 32 KB of offset loads for a tree front's
 // tile of ~40 nonempty entries, neos.)
-template <int CU>
+template <int CU, typename IDX>
 __device__ __forceinline__ void asm_chunks_lds(const SymbolicPlan::AsmTile& tl, const int32_t* __restrict__ gent,
-                                               const double* __restrict__ part, double* Ts) {
+                                               const double* __restrict__ part, const IDX* __restrict__ gsrc,
+                                               const double* __restrict__ Kx, const double* __restrict__ arena,
+                                               double* Ts, double* vals) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
 #pragma unroll
   for (int m = 0; m < 4; ++m) Ts[(wv + 16 * m) * 64 + lane] = 0.0;
+  if (tl.gptr >= 0 && ((tl.gptr >> 47) & 1)) {  // uniform: a tile of <= kAsmLdsWin windows of sources
+    // Its entry list holds source offsets (pos | first source << 12): the tile's sources are gathered
+    // straight into LDS (thread per source, consecutive indices: coalesced), then each entry sums its
+    // sources from LDS in 8-source chunks, in order — k_asm_chunks' partial sums, then their sum, as
+    // the chunk path: the same bits, without the chunk launch and its partials in HBM.
+    const int32_t* __restrict__ ge = gent + (tl.gptr & (((int64_t)1 << 47) - 1));
+    const int ne = (int)(tl.gptr >> 48);
+    const int64_t sb = tl.gchk & (((int64_t)1 << 48) - 1);
+    const int ns = (int)(tl.gchk >> 48);
+    int pos[4], s0[4], s1[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      pos[m] = -1;
+      s0[m] = s1[m] = 0;
+      if (wbase + ANT * m < ne) {  // uniform
+        const int k = tid + ANT * m, kk = min(k, ne - 1);
+        const int e0 = ge[1 + kk], e1 = ge[2 + kk];
+        s0[m] = e0 >> 12;
+        s1[m] = k < ne ? e1 >> 12 : s0[m];
+        pos[m] = k < ne ? (e0 & 4095) : -1;
+      }
+    }
+    // windows of kAsmLdsSrc sources; an entry whose sources straddle a window carries its running
+    // chunk sum to the next (the chunk boundaries stay every kChunk sources from the entry's first)
+    double v[4] = {0.0, 0.0, 0.0, 0.0}, cs[4] = {0.0, 0.0, 0.0, 0.0};
+    int nx[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) nx[m] = s0[m];
+    for (int w0 = 0; w0 < ns; w0 += kAsmLdsSrc) {  // uniform
+      const int wn = min(kAsmLdsSrc, ns - w0);
+      int64_t q[kAsmLdsSrc / ANT];
+#pragma unroll
+      for (int u = 0; u < kAsmLdsSrc / ANT; ++u)
+        q[u] = (wbase + ANT * u < wn) ? (int64_t)gsrc[sb + w0 + min(tid + ANT * u, wn - 1)] : 0;
+      double x[kAsmLdsSrc / ANT];
+#pragma unroll
+      for (int u = 0; u < kAsmLdsSrc / ANT; ++u)
+        x[u] = (wbase + ANT * u < wn) ? *((q[u] < 0) ? Kx + ~q[u] : arena + q[u]) : 0.0;
+#pragma unroll
+      for (int u = 0; u < kAsmLdsSrc / ANT; ++u)
+        if (tid + ANT * u < wn) vals[tid + ANT * u] = x[u];
+      __syncthreads();  // the window's sources (and the zeroed tile)
+      const int we = w0 + wn;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        if (pos[m] < 0 || nx[m] >= s1[m] || nx[m] >= we) continue;
+        if (nx[m] == s0[m] && s1[m] <= we) {  // the whole entry in this window (the common case)
+          for (int c = s0[m]; c < s1[m]; c += SymbolicPlan::kChunk) {
+            double ck = 0.0;
+#pragma unroll
+            for (int u = 0; u < SymbolicPlan::kChunk; ++u)
+              if (c + u < s1[m]) ck += vals[c + u - w0];
+            v[m] += ck;
+          }
+          nx[m] = s1[m];
+        } else {
+          const int e = min(s1[m], we);
+          for (; nx[m] < e; ++nx[m]) {
+            cs[m] += vals[nx[m] - w0];
+            if (((nx[m] + 1 - s0[m]) % SymbolicPlan::kChunk) == 0 || nx[m] + 1 == s1[m]) {
+              v[m] += cs[m];
+              cs[m] = 0.0;
+            }
+          }
+        }
+      }
+      __syncthreads();  // every entry done with the window before the next overwrites it
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      if (pos[m] >= 0) Ts[pos[m]] = v[m];
+    __syncthreads();
+    return;
+  }
   __syncthreads();
   if (tl.gptr >= 0) {  // uniform
-    const int32_t* __restrict__ ge = gent + (tl.gptr & (((int64_t)1 << 48) - 1));
+    const int32_t* __restrict__ ge = gent + (tl.gptr & (((int64_t)1 << 47) - 1));
     const double* __restrict__ pc = part + tl.gchk;
     const int ne = (int)(tl.gptr >> 48);
     int pos[4], c0[4], c1[4], len = 0;
@@ -633,19 +715,21 @@ __device__ __forceinline__ void asm_children_lds(int bt0, int bt1, const BigChil
 // round, 8 big-child records per batch; 32 KB of LDS each).  Launches of few tiles (a root's
 // high-fan-in assembly: ex10's 3 root tiles, up to 8 chunks per entry) take the CU = 8 instance,
 // one round of chunk loads per entry, one tile per CU.
-template <int CU>
+template <int CU, typename IDX>
 __global__ __launch_bounds__(ANT, CU == 2 ? 8 : 4) void k_assemble(FrontTab T, const SymbolicPlan::AsmTile* __restrict__ tiles,
                                                      const int32_t* __restrict__ gptr, const double* __restrict__ part,
                                                      const BigChildRec* __restrict__ brec, double* __restrict__ arena,
-                                                     double* __restrict__ fscratch) {
+                                                     double* __restrict__ fscratch, const IDX* __restrict__ gsrc,
+                                                     const double* __restrict__ Kx) {
   __shared__ double Ts[64 * 64];
+  __shared__ double vals[kAsmLdsSrc];
   const SymbolicPlan::AsmTile tl = tiles[blockIdx.x];
   const int s = tl.front, ti = tl.tij & 0xffff, tj = (tl.tij >> 16) & 0x7fff;
   const bool acc = tl.tij < 0;  // SymbolicPlan::kAccumulate: F += tile (sharded top fronts, phase 2)
   const int r = T.nrows[s];
   const int I0 = ti * 64, J0 = tj * 64;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  asm_chunks_lds<CU>(tl, gptr, part, Ts);
+  asm_chunks_lds<CU>(tl, gptr, part, gsrc, Kx, arena, Ts, vals);
   asm_children_lds<8>(tl.bt0, tl.bt1, brec, arena, Ts);
   double v[4];
 #pragma unroll
@@ -676,12 +760,15 @@ __global__ __launch_bounds__(ANT, CU == 2 ? 8 : 4) void k_assemble(FrontTab T, c
 // Operands and MFMA order are k_big_upd128's (A = L_J, B = (L D)_I, K ascending, one accumulator):
 // the same U bit for bit.
 constexpr int AU_LDT = 80;  // [k][row] operand stride (conflict-free ds_read_b64 for the 16x4 pattern)
+template <typename IDX>
 __global__ __launch_bounds__(ANT) void k_asm_update(FrontTab T, const SymbolicPlan::AsmTile* __restrict__ tiles,
                                                     const int32_t* __restrict__ gptr, const double* __restrict__ part,
                                                     const BigChildRec* __restrict__ brec, double* __restrict__ arena,
-                                                    const double* __restrict__ D, int kmax) {
+                                                    const double* __restrict__ D, int kmax, const IDX* __restrict__ gsrc,
+                                                    const double* __restrict__ Kx) {
   extern __shared__ __attribute__((aligned(16))) double AUs[];
   __shared__ double Ts[64 * 64];     // the assembled tile
+  __shared__ double vals[kAsmLdsSrc];  // its sources (asm_chunks_lds)
   double* Wt = AUs;                  // (L D)[I rows], kmax x AU_LDT
   double* Lt = AUs + kmax * AU_LDT;  // L[J rows]
   const SymbolicPlan::AsmTile tl = tiles[blockIdx.x];
@@ -718,7 +805,7 @@ __global__ __launch_bounds__(ANT) void k_asm_update(FrontTab T, const SymbolicPl
     ei[g] = 16 * bi + (lane & 15);
     ej[g] = 16 * bj + (lane >> 4) + 4 * g;
   }
-  asm_chunks_lds<4>(tl, gptr, part, Ts);
+  asm_chunks_lds<4>(tl, gptr, part, gsrc, Kx, arena, Ts, vals);
   asm_children_lds<8>(tl.bt0, tl.bt1, brec, arena, Ts);
   double v[4];
 #pragma unroll
@@ -4613,7 +4700,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   sv_src_.upload(S.sv_src);
   sv_nt_.alloc(std::max<int64_t>(S.row_ptr[S.nsuper], 1));  // the tree solve's split (set with its tables)
   sv_nt_.zero();
-  g_ptr_.upload(S.g_ptr);  // atiles_: with the big-child records below (bt renumbered)
+  // g_ptr_, atiles_: with the big-child records below (bt renumbered, source-path tiles)
   {
     // int32 sources when every arena / K index fits (leaf update blocks stay materialised: forming
     // them from the leaves' L panels in the gather was measured slower, r1 — 6 scattered loads per
@@ -4646,6 +4733,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   }
   g_chunk_.upload(S.g_chunk);
   gpart_.alloc(std::max<size_t>(S.g_chunk.size(), 1));
+  std::vector<int64_t> asm_cid_off;  // per assembly group: its chunk-path chunks' range in chunk_ids_
   {  // big-child records of the assembly tiles (BigChildRec): a bt entry's block, split into column
      // ranges of <= kBigRecEntries entries; the tiles' bt0 / bt1 renumbered to the records
     const int64_t nb = (int64_t)S.bt.size() / 5;
@@ -4690,9 +4778,42 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       a.bt0 = (int32_t)rptr[a.bt0];
       a.bt1 = (int32_t)rptr[a.bt1];
       // the tile's nonempty-entry count rides in gptr's top 16 bits (asm_chunks_lds: no load of it)
-      MADIPM_REQUIRE(a.gptr < ((int64_t)1 << 48), "assembly: entry list offset past 2^48");
+      MADIPM_REQUIRE(a.gptr < ((int64_t)1 << 47), "assembly: entry list offset past 2^47");
       if (a.gptr >= 0) a.gptr |= (int64_t)S.g_ptr[a.gptr] << 48;
     }
+    // Tiles of <= kAsmLdsWin x kAsmLdsSrc sources sum them from LDS (asm_chunks_lds): their entry lists point at
+    // sources (pos | first source << 12, then the count << 12), gptr bit 47 set, gchk = the first
+    // source | the count << 48; the chunk pass keeps only the other tiles' chunks (chunk_ids_, per
+    // assembly group).  MADIPM_ASM_LDS_SRC=0: every tile through the chunk pass (A/B).
+    const char* el = std::getenv("MADIPM_ASM_LDS_SRC");
+    const bool lds_src = !(el && el[0] == '0');
+    std::vector<int32_t> gp2(S.g_ptr);
+    std::vector<int64_t> cids;
+    asm_cid_off.assign(S.atile_lev.size(), 0);
+    for (size_t g = 0; g + 1 < S.atile_lev.size(); ++g) {
+      asm_cid_off[g] = (int64_t)cids.size();
+      for (int32_t t = S.atile_lev[g]; t < S.atile_lev[g + 1]; ++t) {
+        const SymbolicPlan::AsmTile& a0 = S.atiles[t];
+        if (a0.gptr < 0) continue;
+        const int32_t ne = S.g_ptr[a0.gptr];
+        const int64_t nchk = S.g_ptr[a0.gptr + ne + 1] >> 12, cb = a0.gchk;
+        const int64_t sb = S.g_chunk[cb], ns = S.g_chunk[cb + nchk] - sb;
+        if (lds_src && ns <= (int64_t)kAsmLdsSrc * kAsmLdsWin && sb < ((int64_t)1 << 48)) {
+          for (int32_t k = 0; k < ne; ++k) {
+            const int32_t e = S.g_ptr[a0.gptr + 1 + k];
+            gp2[a0.gptr + 1 + k] = (e & 4095) | (int32_t)((S.g_chunk[cb + (e >> 12)] - sb) << 12);
+          }
+          gp2[a0.gptr + ne + 1] = (int32_t)(ns << 12);
+          at[t].gptr |= (int64_t)1 << 47;
+          at[t].gchk = sb | (ns << 48);
+        } else {
+          for (int64_t c = cb; c < cb + nchk; ++c) cids.push_back(c);
+        }
+      }
+    }
+    asm_cid_off.back() = (int64_t)cids.size();
+    g_ptr_.upload(gp2);
+    chunk_ids_.upload(cids);
     atiles_.upload(at);
   }
   fscratch_.alloc(std::max<int64_t>(S.fs_size, 1));
@@ -5012,8 +5133,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   auto asm_end = [&](int g) { return g < NL ? S.atile_fz1[g] : S.atile_lev[g + 1]; };
   auto asm_launch = [&](int g, std::vector<Launch>& out) {
     if (asm_end(g) <= S.atile_lev[g]) return;
-    Launch L{ASSEMBLE, 0, S.atile_lev[g], 0, asm_end(g) - S.atile_lev[g], S.chunk_lev[g],
-             S.chunk_lev[g + 1] - S.chunk_lev[g]};
+    Launch L{ASSEMBLE, 0, S.atile_lev[g], 0, asm_end(g) - S.atile_lev[g], asm_cid_off[g],
+             asm_cid_off[g + 1] - asm_cid_off[g]};  // the chunks of the group's chunk-path tiles
     // algorithmic traffic: chunk pass reads (index, value) per source, writes one partial per chunk;
     // the tile pass reads the entry offsets + partials (+ big-children blocks), writes the lower tile
     const int64_t nsrc = S.g_chunk[S.chunk_lev[g + 1]] - S.g_chunk[S.chunk_lev[g]];
@@ -5536,7 +5657,9 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_fact_tree, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)SymbolicPlan::kFactTreeLdsMax));
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_bwd_tree, hipFuncAttributeMaxDynamicSharedMemorySize, TREE_SOLVE_LDS));
-    MADIPM_HIP(hipFuncSetAttribute((const void*)k_asm_update, hipFuncAttributeMaxDynamicSharedMemorySize,
+    MADIPM_HIP(hipFuncSetAttribute((const void*)k_asm_update<int32_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   2 * 64 * AU_LDT * 8));
+    MADIPM_HIP(hipFuncSetAttribute((const void*)k_asm_update<int64_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    2 * 64 * AU_LDT * 8));
     attr_done = true;
   }
@@ -5673,12 +5796,21 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
         if (L.nchunk)
           TIMED(KK_ASM_CHUNKS, L.bytes2, 0.0, L.flops2,
                 (g_src32_.p ? k_asm_chunks<int32_t><<<(unsigned)cdiv(L.nchunk, NT), NT, 0, s>>>(
-                                  g_chunk_, g_src32_, L.chunk0, L.nchunk, Kx, arena_, gpart_)
+                                  chunk_ids_, g_chunk_, g_src32_, L.chunk0, L.nchunk, Kx, arena_, gpart_)
                             : k_asm_chunks<int64_t><<<(unsigned)cdiv(L.nchunk, NT), NT, 0, s>>>(
-                                  g_chunk_, g_src_, L.chunk0, L.nchunk, Kx, arena_, gpart_)));
-        TIMED(KK_ASSEMBLE, L.bytes, 0.0, L.flops,
-              (L.items < 256 ? k_assemble<8><<<(unsigned)L.items, ANT, 0, s>>>(T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_)
-                             : k_assemble<2><<<(unsigned)L.items, ANT, 0, s>>>(T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_)));
+                                  chunk_ids_, g_chunk_, g_src_, L.chunk0, L.nchunk, Kx, arena_, gpart_)));
+        if (g_src32_.p)
+          TIMED(KK_ASSEMBLE, L.bytes, 0.0, L.flops,
+                (L.items < 256 ? k_assemble<8, int32_t><<<(unsigned)L.items, ANT, 0, s>>>(
+                                     T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_, g_src32_.p, Kx)
+                               : k_assemble<2, int32_t><<<(unsigned)L.items, ANT, 0, s>>>(
+                                     T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_, g_src32_.p, Kx)));
+        else
+          TIMED(KK_ASSEMBLE, L.bytes, 0.0, L.flops,
+                (L.items < 256 ? k_assemble<8, int64_t><<<(unsigned)L.items, ANT, 0, s>>>(
+                                     T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_, g_src_.p, Kx)
+                               : k_assemble<2, int64_t><<<(unsigned)L.items, ANT, 0, s>>>(
+                                     T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_, g_src_.p, Kx)));
         break;
       case MICRO:
         TIMED(KK_TINY, L.bytes, L.alg, L.flops,
@@ -5715,8 +5847,10 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
         break;
       case ASM_UPDATE:  // nf = the launch's K rows (the widest panel, rounded up to 4)
         TIMED(KK_ASM_UPDATE, L.bytes, 0.0, L.flops,
-              (k_asm_update<<<(unsigned)L.items, ANT, 2 * L.nf * AU_LDT * 8, s>>>(T_, atiles_.p + L.off, g_ptr_, gpart_,
-                                                                                   brec_, arena_, D_, L.nf)));
+              (g_src32_.p ? k_asm_update<int32_t><<<(unsigned)L.items, ANT, 2 * L.nf * AU_LDT * 8, s>>>(
+                                T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, D_, L.nf, g_src32_.p, Kx)
+                          : k_asm_update<int64_t><<<(unsigned)L.items, ANT, 2 * L.nf * AU_LDT * 8, s>>>(
+                                T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, D_, L.nf, g_src_.p, Kx)));
         break;
       case BIG_UPDATE128:
         TIMED(KK_UPDATE, L.bytes, L.alg, L.flops,

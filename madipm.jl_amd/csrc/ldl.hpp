@@ -400,7 +400,7 @@ class LDLSolver : public LinSolver {
   DBuf<int32_t> first_, nrows_, rows_, u_ld_, child_ptr_, child_list_, rel_, perm_, sched_;
   DBuf<int32_t> bigslot_, g_ptr_;
   DBuf<BigChildRec> brec_;
-  DBuf<int64_t> fs_off_, sv_ptr_, sv_src_, g_src_, g_chunk_;
+  DBuf<int64_t> fs_off_, sv_ptr_, sv_src_, g_src_, g_chunk_, chunk_ids_;
   DBuf<int32_t> g_src32_;
   DBuf<SymbolicPlan::AsmTile> atiles_;
   DBuf<double> minv_, fscratch_, gpart_;
