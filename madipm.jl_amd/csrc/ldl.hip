@@ -526,9 +526,12 @@ __global__ __launch_bounds__(NT) void k_asm_chunks(const int64_t* __restrict__ i
 // children's update blocks record by record in child order (asm_children_lds); thread t writes out
 // the entries (row t & 63, columns t >> 6 + 16 k), k < 4.  No atomics, deterministic.  The tile is written to the front (big: arena, ld r; small: scratch, ld r).
 constexpr int ANT = 1024;
-// tiles of at most kAsmLdsWin windows of kAsmLdsSrc sources sum them from LDS (asm_chunks_lds),
-// without k_asm_chunks
-constexpr int kAsmLdsSrc = 5 * ANT, kAsmLdsWin = 4;
+// tiles of at most kAsmLdsSrc sources gather them into LDS and sum them there (asm_chunks_lds),
+// without k_asm_chunks.  (A windowed variant for bigger tiles — entries carrying their chunk sums
+// across windows — gave a wrong pivot on device whenever a tile took more than one window
+// (test_batched_leaf_columns_parity[100-800-0-128], r5_zi) although the same logic checks out on the
+// host: removed, not shipped.)
+constexpr int kAsmLdsSrc = 5 * ANT;
 // The tile's chunk sums into the LDS tile Ts (64 x 64, column-major, ld 64; zeroed first): the
 // tile's nonempty entries (its g_ptr list: ne, then position | first chunk << 12 per entry, then the
 // chunk count << 12; ne also in the device tile's gptr >> 48, bit 47: the source path below) spread
@@ -536,7 +539,7 @@ constexpr int kAsmLdsSrc = 5 * ANT, kAsmLdsWin = 4;
 // chunk order, CU per entry and round in flight.  A wave past the list issues no load.  Ends with a
 // barrier.  (r3-r5 read a dense 4097-offset table per tile: 32 KB of offset loads for a tree front's
 // tile of ~40 nonempty entries, neos.)
-template <int CU, typename IDX>
+template <int CU, typename IDX, int WS = 5 * 1024>
 __device__ __forceinline__ void asm_chunks_lds(const SymbolicPlan::AsmTile& tl, const int32_t* __restrict__ gent,
                                                const double* __restrict__ part, const IDX* __restrict__ gsrc,
                                                const double* __restrict__ Kx, const double* __restrict__ arena,
@@ -545,7 +548,7 @@ __device__ __forceinline__ void asm_chunks_lds(const SymbolicPlan::AsmTile& tl, 
   const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
 #pragma unroll
   for (int m = 0; m < 4; ++m) Ts[(wv + 16 * m) * 64 + lane] = 0.0;
-  if (tl.gptr >= 0 && ((tl.gptr >> 47) & 1)) {  // uniform: a tile of <= kAsmLdsWin windows of sources
+  if (tl.gptr >= 0 && ((tl.gptr >> 47) & 1)) {  // uniform: a tile of <= WS sources
     // Its entry list holds source offsets (pos | first source << 12): the tile's sources are gathered
     // straight into LDS (thread per source, consecutive indices: coalesced), then each entry sums its
     // sources from LDS in 8-source chunks, in order — k_asm_chunks' partial sums, then their sum, as
@@ -567,55 +570,29 @@ __device__ __forceinline__ void asm_chunks_lds(const SymbolicPlan::AsmTile& tl, 
         pos[m] = k < ne ? (e0 & 4095) : -1;
       }
     }
-    // windows of kAsmLdsSrc sources; an entry whose sources straddle a window carries its running
-    // chunk sum to the next (the chunk boundaries stay every kChunk sources from the entry's first)
-    double v[4] = {0.0, 0.0, 0.0, 0.0}, cs[4] = {0.0, 0.0, 0.0, 0.0};
-    int nx[4];
+    int64_t q[WS / ANT];
 #pragma unroll
-    for (int m = 0; m < 4; ++m) nx[m] = s0[m];
-    for (int w0 = 0; w0 < ns; w0 += kAsmLdsSrc) {  // uniform
-      const int wn = min(kAsmLdsSrc, ns - w0);
-      int64_t q[kAsmLdsSrc / ANT];
+    for (int u = 0; u < WS / ANT; ++u) q[u] = (wbase + ANT * u < ns) ? (int64_t)gsrc[sb + min(tid + ANT * u, ns - 1)] : 0;
+    double x[WS / ANT];
 #pragma unroll
-      for (int u = 0; u < kAsmLdsSrc / ANT; ++u)
-        q[u] = (wbase + ANT * u < wn) ? (int64_t)gsrc[sb + w0 + min(tid + ANT * u, wn - 1)] : 0;
-      double x[kAsmLdsSrc / ANT];
+    for (int u = 0; u < WS / ANT; ++u) x[u] = (wbase + ANT * u < ns) ? *((q[u] < 0) ? Kx + ~q[u] : arena + q[u]) : 0.0;
 #pragma unroll
-      for (int u = 0; u < kAsmLdsSrc / ANT; ++u)
-        x[u] = (wbase + ANT * u < wn) ? *((q[u] < 0) ? Kx + ~q[u] : arena + q[u]) : 0.0;
+    for (int u = 0; u < WS / ANT; ++u)
+      if (tid + ANT * u < ns) vals[tid + ANT * u] = x[u];
+    __syncthreads();  // the tile's sources (and the zeroed tile)
 #pragma unroll
-      for (int u = 0; u < kAsmLdsSrc / ANT; ++u)
-        if (tid + ANT * u < wn) vals[tid + ANT * u] = x[u];
-      __syncthreads();  // the window's sources (and the zeroed tile)
-      const int we = w0 + wn;
+    for (int m = 0; m < 4; ++m) {
+      if (pos[m] < 0) continue;
+      double v = 0.0;
+      for (int c = s0[m]; c < s1[m]; c += SymbolicPlan::kChunk) {
+        double ck = 0.0;
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        if (pos[m] < 0 || nx[m] >= s1[m] || nx[m] >= we) continue;
-        if (nx[m] == s0[m] && s1[m] <= we) {  // the whole entry in this window (the common case)
-          for (int c = s0[m]; c < s1[m]; c += SymbolicPlan::kChunk) {
-            double ck = 0.0;
-#pragma unroll
-            for (int u = 0; u < SymbolicPlan::kChunk; ++u)
-              if (c + u < s1[m]) ck += vals[c + u - w0];
-            v[m] += ck;
-          }
-          nx[m] = s1[m];
-        } else {
-          const int e = min(s1[m], we);
-          for (; nx[m] < e; ++nx[m]) {
-            cs[m] += vals[nx[m] - w0];
-            if (((nx[m] + 1 - s0[m]) % SymbolicPlan::kChunk) == 0 || nx[m] + 1 == s1[m]) {
-              v[m] += cs[m];
-              cs[m] = 0.0;
-            }
-          }
-        }
+        for (int u = 0; u < SymbolicPlan::kChunk; ++u)
+          if (c + u < s1[m]) ck += vals[c + u];
+        v += ck;
       }
-      __syncthreads();  // every entry done with the window before the next overwrites it
+      Ts[pos[m]] = v;
     }
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-      if (pos[m] >= 0) Ts[pos[m]] = v[m];
     __syncthreads();
     return;
   }
@@ -721,15 +698,16 @@ __global__ __launch_bounds__(ANT, CU == 2 ? 8 : 4) void k_assemble(FrontTab T, c
                                                      const BigChildRec* __restrict__ brec, double* __restrict__ arena,
                                                      double* __restrict__ fscratch, const IDX* __restrict__ gsrc,
                                                      const double* __restrict__ Kx) {
+  constexpr int WS = kAsmLdsSrc;
   __shared__ double Ts[64 * 64];
-  __shared__ double vals[kAsmLdsSrc];
+  extern __shared__ __attribute__((aligned(16))) double vals[];  // WS doubles (dynamic: past 64 KB of static LDS)
   const SymbolicPlan::AsmTile tl = tiles[blockIdx.x];
   const int s = tl.front, ti = tl.tij & 0xffff, tj = (tl.tij >> 16) & 0x7fff;
   const bool acc = tl.tij < 0;  // SymbolicPlan::kAccumulate: F += tile (sharded top fronts, phase 2)
   const int r = T.nrows[s];
   const int I0 = ti * 64, J0 = tj * 64;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  asm_chunks_lds<CU>(tl, gptr, part, gsrc, Kx, arena, Ts, vals);
+  asm_chunks_lds<CU, IDX, WS>(tl, gptr, part, gsrc, Kx, arena, Ts, vals);
   asm_children_lds<8>(tl.bt0, tl.bt1, brec, arena, Ts);
   double v[4];
 #pragma unroll
@@ -768,9 +746,9 @@ __global__ __launch_bounds__(ANT) void k_asm_update(FrontTab T, const SymbolicPl
                                                     const double* __restrict__ Kx) {
   extern __shared__ __attribute__((aligned(16))) double AUs[];
   __shared__ double Ts[64 * 64];     // the assembled tile
-  __shared__ double vals[kAsmLdsSrc];  // its sources (asm_chunks_lds)
   double* Wt = AUs;                  // (L D)[I rows], kmax x AU_LDT
   double* Lt = AUs + kmax * AU_LDT;  // L[J rows]
+  double* vals = AUs + 2 * kmax * AU_LDT;  // the tile's sources (asm_chunks_lds), kAsmLdsSrc doubles
   const SymbolicPlan::AsmTile tl = tiles[blockIdx.x];
   const int s = tl.front, ti = tl.tij & 0xffff, tj = (tl.tij >> 16) & 0x7fff;
   const int r = T.nrows[s], f0 = T.first[s], w = T.first[s + 1] - f0;
@@ -805,7 +783,7 @@ __global__ __launch_bounds__(ANT) void k_asm_update(FrontTab T, const SymbolicPl
     ei[g] = 16 * bi + (lane & 15);
     ej[g] = 16 * bj + (lane >> 4) + 4 * g;
   }
-  asm_chunks_lds<4>(tl, gptr, part, gsrc, Kx, arena, Ts, vals);
+  asm_chunks_lds<4, IDX, kAsmLdsSrc>(tl, gptr, part, gsrc, Kx, arena, Ts, vals);
   asm_children_lds<8>(tl.bt0, tl.bt1, brec, arena, Ts);
   double v[4];
 #pragma unroll
@@ -4781,7 +4759,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       MADIPM_REQUIRE(a.gptr < ((int64_t)1 << 47), "assembly: entry list offset past 2^47");
       if (a.gptr >= 0) a.gptr |= (int64_t)S.g_ptr[a.gptr] << 48;
     }
-    // Tiles of <= kAsmLdsWin x kAsmLdsSrc sources sum them from LDS (asm_chunks_lds): their entry lists point at
+    // Tiles of <= kAsmLdsSrc sources sum them from LDS (asm_chunks_lds): their entry lists point at
     // sources (pos | first source << 12, then the count << 12), gptr bit 47 set, gchk = the first
     // source | the count << 48; the chunk pass keeps only the other tiles' chunks (chunk_ids_, per
     // assembly group).  MADIPM_ASM_LDS_SRC=0: every tile through the chunk pass (A/B).
@@ -4798,7 +4776,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         const int32_t ne = S.g_ptr[a0.gptr];
         const int64_t nchk = S.g_ptr[a0.gptr + ne + 1] >> 12, cb = a0.gchk;
         const int64_t sb = S.g_chunk[cb], ns = S.g_chunk[cb + nchk] - sb;
-        if (lds_src && ns <= (int64_t)kAsmLdsSrc * kAsmLdsWin && sb < ((int64_t)1 << 48)) {
+        if (lds_src && ns <= kAsmLdsSrc && sb < ((int64_t)1 << 48)) {
           for (int32_t k = 0; k < ne; ++k) {
             const int32_t e = S.g_ptr[a0.gptr + 1 + k];
             gp2[a0.gptr + 1 + k] = (e & 4095) | (int32_t)((S.g_chunk[cb + (e >> 12)] - sb) << 12);
@@ -5658,9 +5636,13 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
                                    (int)SymbolicPlan::kFactTreeLdsMax));
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_bwd_tree, hipFuncAttributeMaxDynamicSharedMemorySize, TREE_SOLVE_LDS));
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_asm_update<int32_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   2 * 64 * AU_LDT * 8));
+                                   2 * 64 * AU_LDT * 8 + 8 * kAsmLdsSrc));
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_asm_update<int64_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   2 * 64 * AU_LDT * 8));
+                                   2 * 64 * AU_LDT * 8 + 8 * kAsmLdsSrc));
+    MADIPM_HIP(hipFuncSetAttribute((const void*)k_assemble<8, int32_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   8 * kAsmLdsSrc));
+    MADIPM_HIP(hipFuncSetAttribute((const void*)k_assemble<8, int64_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   8 * kAsmLdsSrc));
     attr_done = true;
   }
   MADIPM_HIP(hipDeviceSynchronize());
@@ -5801,15 +5783,15 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
                                   chunk_ids_, g_chunk_, g_src_, L.chunk0, L.nchunk, Kx, arena_, gpart_)));
         if (g_src32_.p)
           TIMED(KK_ASSEMBLE, L.bytes, 0.0, L.flops,
-                (L.items < 256 ? k_assemble<8, int32_t><<<(unsigned)L.items, ANT, 0, s>>>(
+                (L.items < 256 ? k_assemble<8, int32_t><<<(unsigned)L.items, ANT, 8 * kAsmLdsSrc, s>>>(
                                      T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_, g_src32_.p, Kx)
-                               : k_assemble<2, int32_t><<<(unsigned)L.items, ANT, 0, s>>>(
+                               : k_assemble<2, int32_t><<<(unsigned)L.items, ANT, 8 * kAsmLdsSrc, s>>>(
                                      T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_, g_src32_.p, Kx)));
         else
           TIMED(KK_ASSEMBLE, L.bytes, 0.0, L.flops,
-                (L.items < 256 ? k_assemble<8, int64_t><<<(unsigned)L.items, ANT, 0, s>>>(
+                (L.items < 256 ? k_assemble<8, int64_t><<<(unsigned)L.items, ANT, 8 * kAsmLdsSrc, s>>>(
                                      T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_, g_src_.p, Kx)
-                               : k_assemble<2, int64_t><<<(unsigned)L.items, ANT, 0, s>>>(
+                               : k_assemble<2, int64_t><<<(unsigned)L.items, ANT, 8 * kAsmLdsSrc, s>>>(
                                      T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_, g_src_.p, Kx)));
         break;
       case MICRO:
@@ -5847,9 +5829,9 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
         break;
       case ASM_UPDATE:  // nf = the launch's K rows (the widest panel, rounded up to 4)
         TIMED(KK_ASM_UPDATE, L.bytes, 0.0, L.flops,
-              (g_src32_.p ? k_asm_update<int32_t><<<(unsigned)L.items, ANT, 2 * L.nf * AU_LDT * 8, s>>>(
+              (g_src32_.p ? k_asm_update<int32_t><<<(unsigned)L.items, ANT, 2 * L.nf * AU_LDT * 8 + 8 * kAsmLdsSrc, s>>>(
                                 T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, D_, L.nf, g_src32_.p, Kx)
-                          : k_asm_update<int64_t><<<(unsigned)L.items, ANT, 2 * L.nf * AU_LDT * 8, s>>>(
+                          : k_asm_update<int64_t><<<(unsigned)L.items, ANT, 2 * L.nf * AU_LDT * 8 + 8 * kAsmLdsSrc, s>>>(
                                 T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, D_, L.nf, g_src_.p, Kx)));
         break;
       case BIG_UPDATE128:
