@@ -526,12 +526,12 @@ __global__ __launch_bounds__(NT) void k_asm_chunks(const int64_t* __restrict__ i
 // children's update blocks record by record in child order (asm_children_lds); thread t writes out
 // the entries (row t & 63, columns t >> 6 + 16 k), k < 4.  No atomics, deterministic.  The tile is written to the front (big: arena, ld r; small: scratch, ld r).
 constexpr int ANT = 1024;
-// tiles of at most kAsmLdsSrc sources gather them into LDS and sum them there (asm_chunks_lds),
-// without k_asm_chunks.  (A windowed variant for bigger tiles — entries carrying their chunk sums
-// across windows — gave a wrong pivot on device whenever a tile took more than one window
-// (test_batched_leaf_columns_parity[100-800-0-128], r5_zi) although the same logic checks out on the
-// host: removed, not shipped.)
-constexpr int kAsmLdsSrc = 5 * ANT;
+// tiles of at most kAsmLdsWin windows of kAsmLdsSrc sources (one window in launches of < 256 tiles:
+// their few workgroups would carry a root's whole gather — ex10's 3 root tiles of 32k sources took
+// 1816 -> 1645 iters/s through the LDS path; the chunk pass spreads it over the chip) gather them into
+// LDS and sum them there (asm_chunks_lds), without k_asm_chunks.  (r5_zi: the source count rode in gchk's top 16 bits and was read back with a signed
+// shift — a tile of >= 2^15 sources read a negative count and summed nothing; unsigned now)
+constexpr int kAsmLdsSrc = 5 * ANT, kAsmLdsWin = 4;
 // The tile's chunk sums into the LDS tile Ts (64 x 64, column-major, ld 64; zeroed first): the
 // tile's nonempty entries (its g_ptr list: ne, then position | first chunk << 12 per entry, then the
 // chunk count << 12; ne also in the device tile's gptr >> 48, bit 47: the source path below) spread
@@ -548,7 +548,7 @@ __device__ __forceinline__ void asm_chunks_lds(const SymbolicPlan::AsmTile& tl, 
   const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
 #pragma unroll
   for (int m = 0; m < 4; ++m) Ts[(wv + 16 * m) * 64 + lane] = 0.0;
-  if (tl.gptr >= 0 && ((tl.gptr >> 47) & 1)) {  // uniform: a tile of <= WS sources
+  if (tl.gptr >= 0 && ((tl.gptr >> 47) & 1)) {  // uniform: a tile of <= kAsmLdsWin windows of sources
     // Its entry list holds source offsets (pos | first source << 12): the tile's sources are gathered
     // straight into LDS (thread per source, consecutive indices: coalesced), then each entry sums its
     // sources from LDS in 8-source chunks, in order — k_asm_chunks' partial sums, then their sum, as
@@ -556,7 +556,7 @@ __device__ __forceinline__ void asm_chunks_lds(const SymbolicPlan::AsmTile& tl, 
     const int32_t* __restrict__ ge = gent + (tl.gptr & (((int64_t)1 << 47) - 1));
     const int ne = (int)(tl.gptr >> 48);
     const int64_t sb = tl.gchk & (((int64_t)1 << 48) - 1);
-    const int ns = (int)(tl.gchk >> 48);
+    const int ns = (int)((uint64_t)tl.gchk >> 48);  // unsigned: a count >= 2^15 sets the sign bit
     int pos[4], s0[4], s1[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
@@ -570,29 +570,55 @@ __device__ __forceinline__ void asm_chunks_lds(const SymbolicPlan::AsmTile& tl, 
         pos[m] = k < ne ? (e0 & 4095) : -1;
       }
     }
-    int64_t q[WS / ANT];
+    // windows of WS sources; an entry whose sources straddle a window carries its running
+    // chunk sum to the next (the chunk boundaries stay every kChunk sources from the entry's first)
+    double v[4] = {0.0, 0.0, 0.0, 0.0}, cs[4] = {0.0, 0.0, 0.0, 0.0};
+    int nx[4];
 #pragma unroll
-    for (int u = 0; u < WS / ANT; ++u) q[u] = (wbase + ANT * u < ns) ? (int64_t)gsrc[sb + min(tid + ANT * u, ns - 1)] : 0;
-    double x[WS / ANT];
+    for (int m = 0; m < 4; ++m) nx[m] = s0[m];
+    for (int w0 = 0; w0 < ns; w0 += WS) {  // uniform
+      const int wn = min(WS, ns - w0);
+      int64_t q[WS / ANT];
 #pragma unroll
-    for (int u = 0; u < WS / ANT; ++u) x[u] = (wbase + ANT * u < ns) ? *((q[u] < 0) ? Kx + ~q[u] : arena + q[u]) : 0.0;
+      for (int u = 0; u < WS / ANT; ++u)
+        q[u] = (wbase + ANT * u < wn) ? (int64_t)gsrc[sb + w0 + min(tid + ANT * u, wn - 1)] : 0;
+      double x[WS / ANT];
 #pragma unroll
-    for (int u = 0; u < WS / ANT; ++u)
-      if (tid + ANT * u < ns) vals[tid + ANT * u] = x[u];
-    __syncthreads();  // the tile's sources (and the zeroed tile)
+      for (int u = 0; u < WS / ANT; ++u)
+        x[u] = (wbase + ANT * u < wn) ? *((q[u] < 0) ? Kx + ~q[u] : arena + q[u]) : 0.0;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      if (pos[m] < 0) continue;
-      double v = 0.0;
-      for (int c = s0[m]; c < s1[m]; c += SymbolicPlan::kChunk) {
-        double ck = 0.0;
+      for (int u = 0; u < WS / ANT; ++u)
+        if (tid + ANT * u < wn) vals[tid + ANT * u] = x[u];
+      __syncthreads();  // the window's sources (and the zeroed tile)
+      const int we = w0 + wn;
 #pragma unroll
-        for (int u = 0; u < SymbolicPlan::kChunk; ++u)
-          if (c + u < s1[m]) ck += vals[c + u];
-        v += ck;
+      for (int m = 0; m < 4; ++m) {
+        if (pos[m] < 0 || nx[m] >= s1[m] || nx[m] >= we) continue;
+        if (nx[m] == s0[m] && s1[m] <= we) {  // the whole entry in this window (the common case)
+          for (int c = s0[m]; c < s1[m]; c += SymbolicPlan::kChunk) {
+            double ck = 0.0;
+#pragma unroll
+            for (int u = 0; u < SymbolicPlan::kChunk; ++u)
+              if (c + u < s1[m]) ck += vals[c + u - w0];
+            v[m] += ck;
+          }
+          nx[m] = s1[m];
+        } else {
+          const int e = min(s1[m], we);
+          for (; nx[m] < e; ++nx[m]) {
+            cs[m] += vals[nx[m] - w0];
+            if (((nx[m] + 1 - s0[m]) % SymbolicPlan::kChunk) == 0 || nx[m] + 1 == s1[m]) {
+              v[m] += cs[m];
+              cs[m] = 0.0;
+            }
+          }
+        }
       }
-      Ts[pos[m]] = v;
+      __syncthreads();  // every entry done with the window before the next overwrites it
     }
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      if (pos[m] >= 0) Ts[pos[m]] = v[m];
     __syncthreads();
     return;
   }
@@ -4759,7 +4785,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       MADIPM_REQUIRE(a.gptr < ((int64_t)1 << 47), "assembly: entry list offset past 2^47");
       if (a.gptr >= 0) a.gptr |= (int64_t)S.g_ptr[a.gptr] << 48;
     }
-    // Tiles of <= kAsmLdsSrc sources sum them from LDS (asm_chunks_lds): their entry lists point at
+    // Tiles of <= kAsmLdsWin windows of sources sum them from LDS (asm_chunks_lds): their entry lists point at
     // sources (pos | first source << 12, then the count << 12), gptr bit 47 set, gchk = the first
     // source | the count << 48; the chunk pass keeps only the other tiles' chunks (chunk_ids_, per
     // assembly group).  MADIPM_ASM_LDS_SRC=0: every tile through the chunk pass (A/B).
@@ -4776,7 +4802,11 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         const int32_t ne = S.g_ptr[a0.gptr];
         const int64_t nchk = S.g_ptr[a0.gptr + ne + 1] >> 12, cb = a0.gchk;
         const int64_t sb = S.g_chunk[cb], ns = S.g_chunk[cb + nchk] - sb;
-        if (lds_src && ns <= kAsmLdsSrc && sb < ((int64_t)1 << 48)) {
+        // one window in k_assemble's launches of < 256 tiles (LDLSolver::run_fact's one-tile-per-CU
+        // instance), kAsmLdsWin elsewhere (k_asm_update: the tiles past the group's fused-front mark)
+        const int32_t aend = (int)g < S.nlevels ? S.atile_fz1[g] : S.atile_lev[g + 1];
+        const int64_t nwin = (t < aend && aend - S.atile_lev[g] < 256) ? 1 : kAsmLdsWin;
+        if (lds_src && ns <= kAsmLdsSrc * nwin && sb < ((int64_t)1 << 48)) {
           for (int32_t k = 0; k < ne; ++k) {
             const int32_t e = S.g_ptr[a0.gptr + 1 + k];
             gp2[a0.gptr + 1 + k] = (e & 4095) | (int32_t)((S.g_chunk[cb + (e >> 12)] - sb) << 12);
