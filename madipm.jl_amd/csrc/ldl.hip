@@ -531,7 +531,12 @@ constexpr int ANT = 1024;
 // 1816 -> 1645 iters/s through the LDS path; the chunk pass spreads it over the chip) gather them into
 // LDS and sum them there (asm_chunks_lds), without k_asm_chunks.  (r5_zi: the source count rode in gchk's top 16 bits and was read back with a signed
 // shift — a tile of >= 2^15 sources read a negative count and summed nothing; unsigned now)
-constexpr int kAsmLdsSrc = 5 * ANT, kAsmLdsWin = 4;
+// The windows straddle: an entry whose sources cross a window boundary carries its running chunk
+// sum to the next (the straddle branch below); MADIPM_ASM_LDS_WIN=n (tests) puts every tile of up to
+// n windows on this path, whatever its launch size.  kAsmLdsWinMax bounds n: the count rides in 16
+// bits of gchk, and the kernel checks it against FrontTab::asm_src_cap (kErrAsmSrc).
+constexpr int kAsmLdsSrc = 5 * ANT, kAsmLdsWin = 4, kAsmLdsWinMax = 12;
+static_assert(kAsmLdsSrc * kAsmLdsWinMax < 65536, "the tile's source count rides in 16 bits");
 // The tile's chunk sums into the LDS tile Ts (64 x 64, column-major, ld 64; zeroed first): the
 // tile's nonempty entries (its g_ptr list: ne, then position | first chunk << 12 per entry, then the
 // chunk count << 12; ne also in the device tile's gptr >> 48, bit 47: the source path below) spread
@@ -543,7 +548,7 @@ template <int CU, typename IDX, int WS = 5 * 1024>
 __device__ __forceinline__ void asm_chunks_lds(const SymbolicPlan::AsmTile& tl, const int32_t* __restrict__ gent,
                                                const double* __restrict__ part, const IDX* __restrict__ gsrc,
                                                const double* __restrict__ Kx, const double* __restrict__ arena,
-                                               double* Ts, double* vals) {
+                                               double* Ts, double* vals, int32_t* err, int src_cap) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
 #pragma unroll
@@ -556,7 +561,11 @@ __device__ __forceinline__ void asm_chunks_lds(const SymbolicPlan::AsmTile& tl, 
     const int32_t* __restrict__ ge = gent + (tl.gptr & (((int64_t)1 << 47) - 1));
     const int ne = (int)(tl.gptr >> 48);
     const int64_t sb = tl.gchk & (((int64_t)1 << 48) - 1);
-    const int ns = (int)((uint64_t)tl.gchk >> 48);  // unsigned: a count >= 2^15 sets the sign bit
+    int ns = (int)((uint64_t)tl.gchk >> 48);  // unsigned: a count >= 2^15 sets the sign bit
+    if (ns > src_cap) {  // uniform: the plan promised at most kAsmLdsWinMax windows — never a silent sum
+      if (tid == 0) __hip_atomic_fetch_or(err, kErrAsmSrc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ns = 0;
+    }
     int pos[4], s0[4], s1[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
@@ -733,7 +742,7 @@ __global__ __launch_bounds__(ANT, CU == 2 ? 8 : 4) void k_assemble(FrontTab T, c
   const int r = T.nrows[s];
   const int I0 = ti * 64, J0 = tj * 64;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  asm_chunks_lds<CU, IDX, WS>(tl, gptr, part, gsrc, Kx, arena, Ts, vals);
+  asm_chunks_lds<CU, IDX, WS>(tl, gptr, part, gsrc, Kx, arena, Ts, vals, T.err, T.asm_src_cap);
   asm_children_lds<8>(tl.bt0, tl.bt1, brec, arena, Ts);
   double v[4];
 #pragma unroll
@@ -809,7 +818,7 @@ __global__ __launch_bounds__(ANT) void k_asm_update(FrontTab T, const SymbolicPl
     ei[g] = 16 * bi + (lane & 15);
     ej[g] = 16 * bj + (lane >> 4) + 4 * g;
   }
-  asm_chunks_lds<4, IDX, kAsmLdsSrc>(tl, gptr, part, gsrc, Kx, arena, Ts, vals);
+  asm_chunks_lds<4, IDX, kAsmLdsSrc>(tl, gptr, part, gsrc, Kx, arena, Ts, vals, T.err, T.asm_src_cap);
   asm_children_lds<8>(tl.bt0, tl.bt1, brec, arena, Ts);
   double v[4];
 #pragma unroll
@@ -4683,6 +4692,10 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     T_.fpipe = (ep && ep[0] == '0') ? 0 : 1;
     const char* ef = std::getenv("MADIPM_DEBUG_PIPE_FAULT");  // tests: drop one hand-off (sticky error)
     T_.pipe_fault = (ef && ef[0] == '1') ? 1 : 0;
+    // the assembly's device-side source-count check (MADIPM_DEBUG_ASM_SRC_CAP=<n>, tests only: a
+    // smaller bound, so the check fires)
+    T_.asm_src_cap = kAsmLdsSrc * kAsmLdsWinMax;
+    if (const char* e = std::getenv("MADIPM_DEBUG_ASM_SRC_CAP")) T_.asm_src_cap = std::atoi(e);
   }
   T_.nrows = nrows_;
   T_.row_ptr = row_ptr_;
@@ -4791,8 +4804,11 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     // assembly group).  MADIPM_ASM_LDS_SRC=0: every tile through the chunk pass (A/B).
     const char* el = std::getenv("MADIPM_ASM_LDS_SRC");
     const bool lds_src = !(el && el[0] == '0');
+    int force_win = 0;  // tests: every tile of <= n windows on the LDS source path (no launch-size rule)
+    if (const char* ew = std::getenv("MADIPM_ASM_LDS_WIN")) force_win = std::max(0, std::min(kAsmLdsWinMax, std::atoi(ew)));
     std::vector<int32_t> gp2(S.g_ptr);
     std::vector<int64_t> cids;
+    int64_t st_lds = 0, st_multi = 0, st_straddle = 0, st_chunk = 0, st_nsmax = 0;  // MADIPM_ASM_STATS
     asm_cid_off.assign(S.atile_lev.size(), 0);
     for (size_t g = 0; g + 1 < S.atile_lev.size(); ++g) {
       asm_cid_off[g] = (int64_t)cids.size();
@@ -4805,7 +4821,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         // one window in k_assemble's launches of < 256 tiles (LDLSolver::run_fact's one-tile-per-CU
         // instance), kAsmLdsWin elsewhere (k_asm_update: the tiles past the group's fused-front mark)
         const int32_t aend = (int)g < S.nlevels ? S.atile_fz1[g] : S.atile_lev[g + 1];
-        const int64_t nwin = (t < aend && aend - S.atile_lev[g] < 256) ? 1 : kAsmLdsWin;
+        const int64_t nwin = force_win ? force_win : (t < aend && aend - S.atile_lev[g] < 256) ? 1 : kAsmLdsWin;
         if (lds_src && ns <= kAsmLdsSrc * nwin && sb < ((int64_t)1 << 48)) {
           for (int32_t k = 0; k < ne; ++k) {
             const int32_t e = S.g_ptr[a0.gptr + 1 + k];
@@ -4814,12 +4830,23 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
           gp2[a0.gptr + ne + 1] = (int32_t)(ns << 12);
           at[t].gptr |= (int64_t)1 << 47;
           at[t].gchk = sb | (ns << 48);
+          ++st_lds;
+          st_multi += ns > kAsmLdsSrc;
+          st_nsmax = std::max(st_nsmax, ns);
+          for (int32_t k = 0; k < ne; ++k) {  // entries whose sources cross a window boundary
+            const int64_t a = gp2[a0.gptr + 1 + k] >> 12, b = gp2[a0.gptr + 2 + k] >> 12;
+            st_straddle += b > a && a / kAsmLdsSrc != (b - 1) / kAsmLdsSrc;
+          }
         } else {
           for (int64_t c = cb; c < cb + nchk; ++c) cids.push_back(c);
+          ++st_chunk;
         }
       }
     }
     asm_cid_off.back() = (int64_t)cids.size();
+    if (std::getenv("MADIPM_ASM_STATS"))
+      fprintf(stderr, "asm lds-src: tiles %lld (multi-window %lld, straddling entries %lld, max sources %lld)  chunk-path tiles %lld\n",
+              (long long)st_lds, (long long)st_multi, (long long)st_straddle, (long long)st_nsmax, (long long)st_chunk);
     g_ptr_.upload(gp2);
     chunk_ids_.upload(cids);
     atiles_.upload(at);
@@ -5673,6 +5700,26 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
                                    8 * kAsmLdsSrc));
     MADIPM_HIP(hipFuncSetAttribute((const void*)k_assemble<8, int64_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    8 * kAsmLdsSrc));
+    MADIPM_HIP(hipFuncSetAttribute((const void*)k_assemble<2, int32_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   8 * kAsmLdsSrc));
+    MADIPM_HIP(hipFuncSetAttribute((const void*)k_assemble<2, int64_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   8 * kAsmLdsSrc));
+    {  // static + dynamic LDS of the assembly kernels must fit one CU (160 KB on gfx950), as k_fact_tree's
+      int dev = 0, cu_lds = 0;
+      MADIPM_HIP(hipGetDevice(&dev));
+      MADIPM_HIP(hipDeviceGetAttribute(&cu_lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev));
+      auto chk = [&](const void* f, size_t dyn, const char* nm) {
+        hipFuncAttributes fa{};
+        MADIPM_HIP(hipFuncGetAttributes(&fa, f));
+        MADIPM_REQUIRE(fa.sharedSizeBytes + dyn <= (size_t)cu_lds,
+                       std::string(nm) + ": LDS " + std::to_string(fa.sharedSizeBytes) + " + " + std::to_string(dyn) +
+                           " bytes exceeds the CU's " + std::to_string(cu_lds));
+      };
+      chk((const void*)k_assemble<2, int32_t>, 8 * kAsmLdsSrc, "k_assemble");
+      chk((const void*)k_assemble<8, int64_t>, 8 * kAsmLdsSrc, "k_assemble");
+      chk((const void*)k_asm_update<int32_t>, 2 * 64 * AU_LDT * 8 + 8 * kAsmLdsSrc, "k_asm_update");
+      chk((const void*)k_asm_update<int64_t>, 2 * 64 * AU_LDT * 8 + 8 * kAsmLdsSrc, "k_asm_update");
+    }
     attr_done = true;
   }
   MADIPM_HIP(hipDeviceSynchronize());
@@ -5992,6 +6039,8 @@ int LDLSolver::status(hipStream_t s, bool sync) {
     h_st_->err = 0;
     k_status_init<<<1, 1, 0, s>>>(st_, 1);
     MADIPM_HIP(hipStreamSynchronize(s));
+    if (e & kErrAsmSrc)
+      throw Error("LDL^T: an assembly tile's source count exceeded the LDS source path's windows (factor is invalid)", -5);
     if (e & kErrLdsCarve)
       throw Error("LDL^T: a front or folded-leaf batch exceeded k_fact_tree's LDS carve (factor is invalid)", -5);
     throw Error("LDL^T: a dependency hand-off between fronts timed out (factor or solve is invalid)", -5);

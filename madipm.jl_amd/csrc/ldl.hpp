@@ -88,6 +88,7 @@ struct FrontTab {
   int fpipe;        // pipelined in-LDS schedule (blocked_factor_pipe; MADIPM_FACT_PIPE=0: blocked_factor_lds)
   int pipe_fault;   // tests (MADIPM_DEBUG_PIPE_FAULT=1): blocked_factor_pipe drops one hand-off
   int lds_cap;      // k_fact_tree's dynamic LDS (bytes): a front (+ its leaf batches) beyond it is an error
+  int asm_src_cap;  // assembly LDS source path: a tile of more sources is an error (kErrAsmSrc); tests shrink it
   // fold helpers (k_fact_tree tickets before the fronts): a helper folds the first batches of a front's
   // micro leaves into a zeroed LDS image and hands it over in HBM (fimg); the front folds the rest
   // from fstart[s] and adds the image after its waits (fold_help[s] = the helper, -1: none)
@@ -101,6 +102,7 @@ struct FrontTab {
 // LDLStatus::err bits (sticky; status() raises on any)
 constexpr int32_t kErrHandoff = 1;   // a dependency hand-off (flag poll) timed out
 constexpr int32_t kErrLdsCarve = 2;  // a k_fact_tree front or leaf batch did not fit its LDS carve
+constexpr int32_t kErrAsmSrc = 4;    // an assembly tile on the LDS source path has more sources than its windows
 
 // assembly: a big child's block on one 64x64 tile of its parent (SymbolicPlan::bt entry, split by
 // column ranges so that na * nb <= kBigRecEntries).  The child's update rows on the tile are the

@@ -1483,8 +1483,11 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       // a batch of `rows` leaf rows and `nl` leaves fits when the front's LDS carve — sized by the
       // largest batch's rows and the largest batch's leaf count, possibly two different batches —
       // stays within the budget
+      // stays within the budget; and at most 2 kFoldThreads leaves per batch (k_fact_tree's fold_leaves
+      // holds a batch's leaf table in two registers per thread: a bigger batch is a carve error there)
       auto fits = [&](int64_t rows, int64_t nl, int64_t rmax, int64_t lmax) {
-        return RB * std::max(rows, rmax) + LB * std::max(nl, lmax) <= budget && rows <= SymbolicPlan::kFoldRowsMax;
+        return RB * std::max(rows, rmax) + LB * std::max(nl, lmax) <= budget && rows <= SymbolicPlan::kFoldRowsMax &&
+               nl <= SymbolicPlan::kFoldLeavesMax;
       };
       {  // the batch table lives in LDS: fronts needing more batches leave their leaves unfolded
         int nb = 0;

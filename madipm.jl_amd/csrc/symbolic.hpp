@@ -152,6 +152,7 @@ struct SymbolicPlan {
   static constexpr int kFoldLeafBytes = 48;               // LDS per leaf: d0, d1, f10, L offset, row0, w | rc
   static constexpr uint32_t kFoldRunEnd = 1u << 31;       // entry: last product of its run (in the chunk)
   static constexpr uint32_t kFoldPad = 0xfffu;            // q1 of an entry without a product
+  static constexpr int kFoldLeavesMax = 2 * kFoldThreads;  // leaves per batch: fold_leaves' two table registers per thread
   static constexpr int kFoldRowsMax = 4095;               // leaf rows per batch: 12-bit indices below kFoldPad
   static constexpr uint32_t kFoldCont = 1u << 31;         // fold_chead: the chunk's first run continues
   static constexpr int kFoldMaxBatches = 32;              // leaf batches per folding front (LDS table)

@@ -109,3 +109,17 @@ def kkt_properties(qp, st):
     return dict(pr=pr, du=du, compl=compl, pobj=pobj, dobj=dobj,
                 bounds=max(np.max((qp.lvar - x)[lo], initial=-1.0), np.max((x - qp.uvar)[hi], initial=-1.0)),
                 zmin=min(np.min(zl[lo], initial=0.0), np.min(zu[hi], initial=0.0)))
+
+
+def many_leaf_k2(n, seed=0):
+    """K2 of an LP with one constraint row over n columns (delta = 1e-2, well conditioned): every x_j is
+    a two-row micro leaf (x_j, y) under the one tree front y, which folds all n of them — more than
+    k_fact_tree's fold_leaves holds per batch (2 x 512 leaf-table registers) once n > 1024."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(seed)
+    A = sp.csr_matrix(rng.uniform(0.5, 1.5, (1, n)))
+    K = sp.bmat([[sp.diags(10.0 ** rng.uniform(-1, 1, n)), A.T], [A, -1e-2 * sp.eye(1)]]).tocsc()
+    K.sum_duplicates()
+    Lw = sp.tril(K).tocsc()
+    Lw.sort_indices()
+    return K, Lw

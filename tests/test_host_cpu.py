@@ -473,3 +473,15 @@ def test_analysis_independent_of_thread_count():
         assert r.returncode == 0, r.stderr[-2000:]
         outs.append(r.stdout)
     assert outs[0] == outs[1] == outs[2], outs
+
+
+@pytest.mark.parametrize("n", [1300, 2500])
+def test_fold_batches_hold_at_most_1024_leaves(n):
+    """A tree front with more than 2 x 512 micro leaves still folds them (fold_leaves keeps a
+    batch's leaf table in two registers per thread, so the planner caps a batch at kFoldLeavesMax
+    leaves and cuts more batches; the GPU side is test_ldl_gpu.py::test_fold_many_leaves)."""
+    from helpers import many_leaf_k2
+    from madipm_amd._lib import Symbolic, default_ldl_opts
+    K, Lw = many_leaf_k2(n)
+    info = Symbolic(K.shape[0], Lw.indptr, Lw.indices, default_ldl_opts(ordering=4)).info()
+    assert info["fold_fronts"] == 1 and info["fold_leaves"] > 1024, info

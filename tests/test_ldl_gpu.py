@@ -414,3 +414,16 @@ def test_alg_bytes_sum_to_survey_counts(case):
     st = ls.kernel_stats()
     sol = sum(k["alg_bytes"] for k in st if k["name"] in solve_kinds)
     assert sol == pytest.approx(16.0 * info["nnzL"], rel=1e-12), (case, sol)
+
+
+@pytest.mark.parametrize("n", [1300, 2500])
+def test_fold_many_leaves(n):
+    """One tree front folding > 1024 two-row micro leaves: the planner cuts batches of at
+    most kFoldLeavesMax leaves, so k_fact_tree folds them without a carve error — the oracle's pivots
+    (1e-12) and solution."""
+    from helpers import many_leaf_k2
+    K, Lw = many_leaf_k2(n)
+    ls = _check_case(K, Lw, well=True)
+    info = ls.info()
+    assert info["fold_fronts"] == 1 and info["fold_leaves"] > 1024, info
+    assert ls.inertia() == (n, 0, 1)
