@@ -11,6 +11,13 @@ workload: BASELINE.json configs[1] — MIPLIB ex10 LP relaxation, fp64, 1 GPU.  
 step    : one MPC iteration (factorize + predictor/corrector solves + step), inputs resident in HBM.
           W warmup iterations (untimed solve), then EXACTLY K iterations of a fresh solve after
           initialize! (the MPC loop only, as cnt.total_time in src/solver.jl:181,407).
+legs    : every other BASELINE config gets a leg of the same schema under its own key of the line
+          ("supportcase10" configs[3], "dense_qp" configs[2], "neos" configs[4]): iters/s over a timed
+          run, the dominant kernel's roofline (HIP events on the launch stream; PMC traffic from the
+          newest committed profiles/*_<config>_pmc_traffic.json), the iteration roofline, analysis /
+          end-to-end time to optimality and a parity object (the HiGHS optimum of the same stand-in,
+          tests/golden/fullsize_highs.json, plus the returned point's KKT measures).  N > 1: the neos
+          leg only (subtree-sharded; the dense QP's 12 GB host instance per rank is not replicated).
 multi-GPU: (N > 1, launched by torch.distributed.run) ONE solve of the workload with the LDL^T
           subtree-sharded across the N GPUs (SURVEY §8 e): one process per GPU, each owns
           a set of elimination-tree subtrees, the common ancestors ("top" fronts) are factorised
@@ -260,50 +267,154 @@ def collective_volume(info, warm, world=None):
     return out
 
 
-def timed_leg(solver, steps, warmup, dist, sharded, barrier):
-    """One timed MPC run of a built solver: `warmup` untimed iterations, then EXACTLY `steps` iterations
-    after initialize!, bracketed by barriers (barrier() also synchronises the device); whole-job numbers
-    by `aggregate` (max time over ranks)."""
+def kkt_measures(qp, st) -> dict:
+    """Optimality measures of the returned unscaled point (x, y, zl, zu) of min/max c'x + x'Hx/2 + c0,
+    Ax = b, l <= x <= u, in the solver's sign convention (sigma = -1 for a maximisation: the reference
+    flips only the reported objective, src/utils.jl:150-156): relative primal residual, relative
+    stationarity sigma (c + Hx) + A'y - zl + zu, the bound violation, and the duality gap between the
+    primal objective and the Lagrangian dual bound (src/kernels.jl:408-430).  The dense QP instance
+    (column-major A, madipm_amd.instances.dense_qp) is applied as a dense (n x m) view: no 5e8-entry
+    sparse matrix on the host."""
+    import numpy as np
+    n, m = qp.nvar, qp.ncon
+    sg = 1.0 if getattr(qp, "minimize", True) else -1.0
+    x, y, zl, zu = st.solution, st.multipliers, st.multipliers_L, st.multipliers_U
+    if qp.nnzj == n * m and qp.name.startswith("dense_qp"):
+        V = np.asarray(qp.Avals).reshape(n, m)  # row j = column j of A
+        Ax, Aty = V.T @ x, V @ y
+    else:
+        import scipy.sparse as sp
+        A = sp.csr_matrix((qp.Avals, (qp.Arows, qp.Acols)), shape=(m, n))
+        Ax, Aty = A @ x, A.T @ y
+    hx = np.zeros(n)
+    np.add.at(hx, qp.Hrows, qp.Hvals * x[qp.Hcols])
+    off = qp.Hrows != qp.Hcols
+    np.add.at(hx, qp.Hcols[off], qp.Hvals[off] * x[qp.Hrows[off]])
+    b = qp.lcon
+    lo, hi = np.isfinite(qp.lvar), np.isfinite(qp.uvar)
+    pobj = qp.c0 + qp.c @ x + 0.5 * x @ hx
+    dobj = sg * (sg * qp.c0 - y @ b + zl[lo] @ qp.lvar[lo] - zu[hi] @ qp.uvar[hi] - sg * 0.5 * x @ hx)
+    return {"pr": float(np.max(np.abs(Ax - b)) / (1.0 + np.max(np.abs(b)))),
+            "du": float(np.max(np.abs(sg * (qp.c + hx) + Aty - zl + zu)) / (1.0 + np.max(np.abs(qp.c)))),
+            "bounds": float(max(np.max((qp.lvar - x)[lo], initial=-1.0), np.max((x - qp.uvar)[hi], initial=-1.0))),
+            "pobj": float(pobj), "dobj": float(dobj), "gap_rel": float(abs(pobj - dobj) / max(1.0, abs(pobj)))}
+
+
+def golden_parity(config: str, qp, so) -> dict:
+    """Parity of a solve to optimality: the HiGHS 1.x IPM + crossover optimum of the same seeded
+    stand-in (tests/golden/fullsize_highs.json, tools/make_golden_fullsize.py; full-size configs only)
+    at BASELINE.md's |dobj| <= 1e-6 max(1, |obj|), and the point's own KKT measures (absolute
+    thresholds pr, du <= 1e-6, gap <= 1e-6 relative).  A config with no HiGHS optimum (the dense QP:
+    scipy's HiGHS has no QP) rests on the KKT certificate alone (convex: feasible + zero gap =
+    optimal) — parity unpinned against any reference fixture."""
+    out = {"status": so.status_name, "iters": so.iter, "objective": so.objective}
+    try:
+        k = kkt_measures(qp, so)
+    except Exception as e:  # pragma: no cover - reported, not hidden
+        k = {"error": repr(e)}
+    out["kkt"] = k
+    ok = so.status_name == "SOLVE_SUCCEEDED" and "error" not in k and k["pr"] <= 1e-6 and k["du"] <= 1e-6 \
+        and k["gap_rel"] <= 1e-6 and k["bounds"] <= 1e-8
+    name, _, sc = config.partition("@")
+    try:
+        g = json.load(open(os.path.join(ROOT, "tests", "golden", "fullsize_highs.json"))).get(name) if not sc else None
+    except OSError:
+        g = None
+    if g and g.get("nvar") == qp.nvar and g.get("ncon") == qp.ncon:
+        rel = abs(so.objective - g["objective"]) / max(1.0, abs(g["objective"]))
+        out.update({"reference": "HiGHS IPM + crossover optimum of the same stand-in (tests/golden/fullsize_highs.json)",
+                    "objective_ref": g["objective"], "rel_obj_diff": rel})
+        ok = ok and rel <= 1e-6
+    else:
+        out["reference"] = "KKT certificate of the returned point only (no reference fixture: parity unpinned)"
+    out["ok"] = bool(ok)
+    return out
+
+
+def timed_leg(solver, steps, warmup, dist, sharded, barrier, config="ex10"):
+    """The timed part of a leg: `warmup` untimed iterations with every LDL^T kernel kind event-timed
+    (the dominant kind), then EXACTLY `steps` iterations after initialize!, bracketed by barriers
+    (barrier() also synchronises the device), HIP events around the dominant kind only (its roofline);
+    whole-job numbers by `aggregate` (max time over ranks).  Returns (leg, warm stats, stats)."""
+    import torch
     solver.set_kernel_timing()
     solver.set_max_iter(max(warmup, 1))
     solver.solve()
     warm = solver.kernel_stats()
-    solver.set_kernel_timing(0)
+    dominant = max(warm, key=lambda k: k["time_ms"])["name"]
+    breakdown = {k["name"]: round(k["time_ms"], 3) for k in sorted(warm, key=lambda k: -k["time_ms"]) if k["launches"]}
+    solver.set_kernel_timing(1 << [k["name"] for k in warm].index(dominant))
     solver.set_max_iter(steps)
     solver.initialize()
     barrier()
     t0 = time.perf_counter()
+    # the MPC loop only: update_solution!'s host copies of the solution vectors come after the
+    # reference's cnt.total_time (src/solver.jl:406-413) and are not part of an iteration
     st = solver.solve(fetch_solution=False)
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
-    dt, it, per_rank = aggregate(dt, st.iter, dist, sharded)
-    return {"iters_per_s": it / dt, "ms_per_iter": 1e3 * dt / max(st.iter, 1), "steps": steps, "warmup": warmup,
-            "per_rank_s": per_rank}, warm
+    iters = st.iter
+    roof = roofline(solver.kernel_stats(), dominant, config)
+    solver.set_kernel_timing(0)
+    dt, total_iters, per_rank = aggregate(dt, iters, dist, sharded)
+    return ({"iters_per_s": total_iters / dt, "ms_per_iter": 1e3 * dt / max(iters, 1), "steps": steps,
+             "warmup": warmup, "iters_timed": iters, "roofline": roof, "kernel_ms_warmup": breakdown,
+             "per_rank_s": per_rank}, warm, st)
 
 
-def neos_leg(args, comm, dist, sharded, barrier, world):
-    """BASELINE.json configs[4] — the config it assigns to the 8-GPU elimination-tree subtree split —
-    at every N: unsharded at N = 1, subtree-sharded over the N ranks (RCCL) at N > 1, so the driver's
-    SCALE run measures the sharded path where the tree actually shards (ex10's tree has one 120-row
-    top front).  Reported under the line's "neos" key; `value` stays on the ex10 workload."""
+def run_leg(config, steps, warmup, comm=None, dist=None, sharded=False, barrier=None, world=1, opt=True,
+            ordering=None):
+    """One BASELINE config end to end: build (the reference pipeline), analysis + upload (timed), W
+    warmup iterations with every LDL^T kernel kind event-timed (the dominant kind), EXACTLY `steps`
+    iterations after initialize! with HIP events around the dominant kind only, whole-job numbers
+    (max time over ranks), then (opt) a solve to optimality: status, iterations, loop time, end to end
+    = analysis + initialisation + loop, and golden_parity.  Returns (leg dict, solver, qp)."""
+    import torch
     from madipm_amd import MPCSolver
-    qp, name = build_problem("neos")
+    if barrier is None:
+        def barrier():
+            if dist is not None:
+                dist.barrier()
+            torch.cuda.synchronize()
+    qp, name = build_problem(config)
+    extra = {}
+    if config.startswith("dense_qp"):
+        # x first (natural order): the x columns are batched leaves eliminated by one MFMA SYRK; AMD/ND
+        # on the complete bipartite graph of a dense A would only rediscover this order, slowly
+        extra["ordering"] = 0
+    if ordering is not None:
+        extra["ordering"] = ordering
     t_an = time.perf_counter()
-    solver = MPCSolver(qp, comm=comm, **solver_opts())
+    solver = MPCSolver(qp, comm=comm, **solver_opts(), **extra)
     t_analysis = time.perf_counter() - t_an
     info = solver.ldl_info()
-    leg, warm = timed_leg(solver, args.neos_steps, 2, dist, sharded, barrier)
-    solver.set_max_iter(300)
-    t1 = time.perf_counter()
-    so = solver.solve()
-    e2e = time.perf_counter() - t1
-    leg.update({"workload": name, "parallelism": f"subtree-shard{world}" if sharded else f"replicas{world}",
-                "nnzL": info["nnzL"], "fact_flops": info["flops"], "analysis_s": t_analysis,
-                "status": so.status_name, "iters_to_opt": so.iter, "objective": so.objective,
-                "wall_clock_to_opt_s": so.counters.total_time, "end_to_end_s": t_analysis + e2e,
+    leg, warm, st = timed_leg(solver, steps, warmup, dist, sharded, barrier, config.partition("@")[0])
+    ms = leg["ms_per_iter"]
+    leg.update({"workload": name, "nvar": qp.nvar, "ncon": qp.ncon, "nnzj": qp.nnzj, "kkt_n": info["n"],
+                "nnzL": info["nnzL"], "nnzL_stored": info["nnzL_stored"], "fact_flops": info["flops"],
+                "fronts": info["nsuper"], "levels": info["nlevels"], "leaf_batch_members": info["lb_members"],
+                "parallelism": f"subtree-shard{world}" if sharded else f"replicas{world}",
+                "analysis_s": t_analysis, "iteration_roofline": iteration_roofline(info, ms),
+                "loop_total_time_s": st.counters.total_time,  # the library's own clock around the K iterations
                 "collectives": collective_volume(info, warm, world)})
-    del solver
-    return leg
+    if opt:
+        solver.set_max_iter(300)
+        t1 = time.perf_counter()
+        so = solver.solve()
+        e2e = time.perf_counter() - t1
+        leg.update({"status": so.status_name, "iters_to_opt": so.iter, "wall_clock_to_opt_s": so.counters.total_time,
+                    "init_plus_loop_s": e2e, "objective": so.objective,
+                    "linear_solver_time_s": so.counters.linear_solver_time,
+                    # SURVEY 8(d): end-to-end = symbolic analysis + initialisation + loop to optimality
+                    "end_to_end_s": t_analysis + e2e})
+        if dist is None or dist.get_rank() == 0:
+            leg["parity"] = golden_parity(config, qp, so)
+    return leg, solver, qp
+
+
+LEG_STEPS = {"supportcase10": (20, 2), "dense_qp": (3, 1), "neos": (8, 2)}  # (timed steps, warmup) per leg
 
 
 def main():
@@ -319,9 +430,12 @@ def main():
     ap.add_argument("--ordering", type=int, default=None, help="LDL ordering override (0 natural, 1 AMD, 3 ND, 4 auto)")
     ap.add_argument("--mode", choices=["shard", "replicas"], default="shard",
                     help="N > 1: one subtree-sharded solve (RCCL) or N independent replicas")
+    ap.add_argument("--legs", default=None,
+                    help="comma list of extra BASELINE configs timed under their own keys (default: "
+                         "supportcase10,dense_qp,neos at N = 1, neos at N > 1; 'none' for none)")
     ap.add_argument("--neos", action=argparse.BooleanOptionalAction, default=True,
-                    help="also time configs[4] (neos stand-in; sharded over the ranks at N > 1) under the 'neos' key")
-    ap.add_argument("--neos-steps", type=int, default=8)
+                    help="--no-neos drops the neos leg")
+    ap.add_argument("--neos-steps", type=int, default=LEG_STEPS["neos"][0])
     args = ap.parse_args()
 
     import torch
@@ -339,117 +453,93 @@ def main():
         dist.init_process_group("gloo")
     sharded = world > 1 and args.mode == "shard"
 
-    from madipm_amd import MPCSolver, RCCLComm
-    qp, cfgname = build_problem(args.config)
+    from madipm_amd import RCCLComm
     comm = RCCLComm.from_torch(dist) if sharded else None
-    t_an = time.perf_counter()
-    extra = {}
-    if args.config.startswith("dense_qp"):
-        # x first (natural order): the x columns are batched leaves eliminated by one MFMA SYRK; AMD/ND
-        # on the complete bipartite graph of a dense A would only rediscover this order, slowly
-        extra["ordering"] = 0
-    if args.ordering is not None:
-        extra["ordering"] = args.ordering
-    solver = MPCSolver(qp, comm=comm, **solver_opts(), **extra)
-    t_analysis = time.perf_counter() - t_an
-    info = solver.ldl_info()
 
     def barrier():
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
 
-    # warmup: W iterations (untimed); every LDL^T kernel kind timed to find the dominant one
-    solver.set_kernel_timing()
-    solver.set_max_iter(max(args.warmup, 1))
-    solver.solve()
-    warm = solver.kernel_stats()
-    dominant = max(warm, key=lambda k: k["time_ms"])["name"]
-    breakdown = {k["name"]: round(k["time_ms"], 3) for k in sorted(warm, key=lambda k: -k["time_ms"]) if k["launches"]}
-    # timed: EXACTLY K MPC iterations after initialize!; HIP events around the dominant kernel only
-    solver.set_kernel_timing(1 << [k["name"] for k in warm].index(dominant))
-    solver.set_max_iter(args.steps)
-    solver.initialize()
-    barrier()
-    t0 = time.perf_counter()
-    # the MPC loop only: update_solution!'s host copies of the solution vectors come after the
-    # reference's cnt.total_time (src/solver.jl:406-413) and are not part of an iteration
-    st = solver.solve(fetch_solution=False)
-    torch.cuda.synchronize()
-    barrier()
-    dt = time.perf_counter() - t0
-    iters = st.iter
-    roof = roofline(solver.kernel_stats(), dominant, args.config.partition("@")[0])
-    solver.set_kernel_timing(0)
-    dt, total_iters, per_rank = aggregate(dt, iters, dist, sharded)
-
-    # wall-clock to optimality (the reference's total_time; max_iter 300)
-    opt = {}
-    if not args.no_opt:
-        solver.set_max_iter(300)
-        t1 = time.perf_counter()
-        so = solver.solve()
-        e2e = time.perf_counter() - t1
-        opt = {"status": so.status_name, "iters_to_opt": so.iter, "wall_clock_to_opt_s": so.counters.total_time,
-               "init_plus_loop_s": e2e, "analysis_s": t_analysis, "objective": so.objective,
-               "linear_solver_time_s": so.counters.linear_solver_time,
-               # end-to-end = symbolic analysis + initialisation + loop to optimality
-               "end_to_end_s": t_analysis + e2e}
-
+    main_leg, solver, qp = run_leg(args.config, args.steps, args.warmup, comm, dist, sharded, barrier, world,
+                                   opt=not args.no_opt, ordering=args.ordering)
     kperm = solver.kkt_perm() if rank == 0 else None
-    neos = None
-    if args.neos and not args.config.startswith("neos"):
-        del solver
+    del solver
+
+    base = args.config.partition("@")[0]
+    if args.legs is None:
+        legs = ["supportcase10", "dense_qp", "neos"] if world == 1 else ["neos"]
+    else:
+        legs = [] if args.legs == "none" else [c for c in args.legs.split(",") if c]
+    if not args.neos:
+        legs = [c for c in legs if c != "neos"]
+    legs = [c for c in legs if c.partition("@")[0] != base]
+    extra = {}
+    for c in legs:
+        steps, warm = LEG_STEPS.get(c.partition("@")[0], (8, 2))
+        if c.startswith("neos"):
+            steps = args.neos_steps
         try:
-            neos = neos_leg(args, comm, dist, sharded, barrier, world)
+            leg, s2, q2 = run_leg(c, steps, warm, comm, dist, sharded, barrier, world, opt=True)
+            del s2, q2
         except Exception as e:  # pragma: no cover - reported, not hidden
-            neos = {"error": repr(e)}
+            leg = {"error": repr(e)}
+        extra[c] = leg
+        import gc
+        gc.collect()
 
     if rank == 0:
+        it = main_leg
+        opt_keys = ("status", "iters_to_opt", "wall_clock_to_opt_s", "init_plus_loop_s", "analysis_s", "objective",
+                    "linear_solver_time_s", "end_to_end_s")
+        cfg = {k: it[k] for k in ("workload", "nvar", "ncon", "nnzj", "kkt_n", "nnzL", "nnzL_stored", "fact_flops",
+                                  "fronts", "levels", "leaf_batch_members", "parallelism")}
+        cfg.update({k: it[k] for k in opt_keys if k in it})
+        cfg["analysis_s"] = it["analysis_s"]
         out = {
             "metric": "IPM iters/sec + wall-clock-to-opt, MIPLIB LP, 1/2/4/8 MI355X vs host CPU",
-            "value": total_iters / dt,
+            "value": it["iters_per_s"],
             "unit": "iters/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": 1e3 * dt / max(iters, 1),
+            "ms_per_step": it["ms_per_iter"],
             "higher_is_better": True,
             "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "rocm": rocm_version(),
-            "data": "synthetic (seeded structured stand-in; no MIPLIB MPS offline)",
-            "config": {"workload": cfgname, "nvar": qp.nvar, "ncon": qp.ncon, "nnzj": qp.nnzj,
-                       "kkt_n": info["n"], "nnzL": info["nnzL"], "nnzL_stored": info["nnzL_stored"],
-                       "fact_flops": info["flops"], "fronts": info["nsuper"], "levels": info["nlevels"],
-                       "leaf_batch_members": info["lb_members"],
-                       "parallelism": (f"subtree-shard{world}" if sharded else f"replicas{world}"), **opt},
-            "roofline": roof,
-            "iteration_roofline": iteration_roofline(info, 1e3 * dt / max(iters, 1)),
-            "kernel_ms_warmup": breakdown,
-            "per_rank_s": per_rank,
-            "loop_total_time_s": st.counters.total_time,  # the library's own clock around the K iterations (rank 0)
-            "collectives": collective_volume(info, warm, world),
-            "neos": neos,
+            "data": "synthetic (seeded structured stand-ins; no MIPLIB MPS offline)",
+            "config": cfg,
+            "roofline": it["roofline"],
+            "iteration_roofline": it["iteration_roofline"],
+            "kernel_ms_warmup": it["kernel_ms_warmup"],
+            "per_rank_s": it["per_rank_s"],
+            "loop_total_time_s": it["loop_total_time_s"],
+            "collectives": it["collectives"],
+            **extra,
             "cpu_baseline": None,
-            "parity": None,
+            "parity": it.get("parity"),
         }
-        if not args.no_cpu and world == 1 and not args.config.startswith(("dense_qp", "neos")):
+        if not args.no_cpu and world == 1 and not base.startswith(("dense_qp", "neos")):
             try:
                 (r_status, r_obj, r_iter), out["cpu_baseline"] = cpu_baseline(args.config, kperm,
                                                                                baseline_threads())
-                if opt:
+                if "objective" in it:
                     # parity at the benchmarked size: the GPU solve to optimality vs the oracle's (same
-                    # problem, same settings; BASELINE.md parity rule |dobj| <= 1e-6 max(1, |obj|))
-                    rel = abs(opt["objective"] - r_obj) / max(1.0, abs(r_obj))
-                    out["parity"] = {"reference": "oracle/mpc.py + MKL PARDISO (CPU)",
-                                     "status_gpu": opt["status"], "status_ref": STATUS.get(r_status, r_status),
-                                     "status_equal": STATUS.get(r_status) == opt["status"],
-                                     "objective_gpu": opt["objective"], "objective_ref": r_obj,
-                                     "rel_obj_diff": rel, "iters_gpu": opt["iters_to_opt"], "iters_ref": r_iter,
-                                     "ok": bool(STATUS.get(r_status) == opt["status"] and rel <= 1e-6
-                                                and abs(opt["iters_to_opt"] - r_iter) <= 1)}
+                    # problem, same settings; BASELINE.md parity rule |dobj| <= 1e-6 max(1, |obj|)),
+                    # beside the HiGHS optimum and the KKT measures of golden_parity
+                    rel = abs(it["objective"] - r_obj) / max(1.0, abs(r_obj))
+                    p = out["parity"] or {}
+                    p["oracle"] = {"reference": "oracle/mpc.py + MKL PARDISO (CPU)",
+                                   "status_gpu": it["status"], "status_ref": STATUS.get(r_status, r_status),
+                                   "status_equal": STATUS.get(r_status) == it["status"],
+                                   "objective_gpu": it["objective"], "objective_ref": r_obj,
+                                   "rel_obj_diff": rel, "iters_gpu": it["iters_to_opt"], "iters_ref": r_iter,
+                                   "ok": bool(STATUS.get(r_status) == it["status"] and rel <= 1e-6
+                                              and abs(it["iters_to_opt"] - r_iter) <= 1)}
+                    p["ok"] = bool(p.get("ok", True) and p["oracle"]["ok"])
+                    out["parity"] = p
             except Exception as e:  # pragma: no cover - reported, not hidden
                 out["cpu_baseline"] = {"error": repr(e)}
             if args.highs:

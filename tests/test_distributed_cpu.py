@@ -72,7 +72,8 @@ class _FakeSolver:
         pass
 
     def kernel_stats(self):
-        return [{"name": "k_fact_tree", "launches": 2}, {"name": "k_bwd_tree", "launches": 4}]
+        return [{"name": "k_fact_tree", "launches": 2, "time_ms": 0.4, "flops": 2e6, "alg_bytes": 8e6, "bytes": 1e7},
+                {"name": "k_bwd_tree", "launches": 4, "time_ms": 0.2, "flops": 1e5, "alg_bytes": 4e6, "bytes": 5e6}]
 
     def set_max_iter(self, k):
         self.k = k
@@ -91,13 +92,13 @@ def _leg_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import bench
-    leg, warm = bench.timed_leg(_FakeSolver(rank), 6, 2, dist, True, dist.barrier)
+    leg, warm, _ = bench.timed_leg(_FakeSolver(rank), 6, 2, dist, True, dist.barrier)
     q.put((rank, leg, [k["name"] for k in warm]))
     dist.destroy_process_group()
 
 
 def test_two_rank_timed_leg():
-    """bench.timed_leg (the 'neos' key's sharded leg at N > 1): the time is the max over ranks, the
+    """bench.timed_leg (every leg's timed part; the 'neos' leg is sharded at N > 1): the time is the max over ranks, the
     iterations are the one sharded solve's, every rank's own time is reported."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -115,3 +116,6 @@ def test_two_rank_timed_leg():
         assert len(leg["per_rank_s"]) == 2 and min(leg["per_rank_s"]) >= 0.1
         assert leg["steps"] == 6 and leg["iters_per_s"] == pytest.approx(6 / max(leg["per_rank_s"]))
         assert leg["ms_per_iter"] == pytest.approx(1e3 * max(leg["per_rank_s"]) / 6)
+        # the dominant kind's roofline from the event statistics: (8 MB / 2) / (0.4 ms / 2) = 20 GB/s
+        assert leg["roofline"]["kernel"] == "k_fact_tree" and leg["roofline"]["bound"] == "hbm"
+        assert leg["roofline"]["achieved"] == pytest.approx(20.0)
