@@ -2090,7 +2090,8 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
   // round trips in front of the children's wait
   const int hh = T.absorb[s] ? T.fold_help[s] : -1;
   const int hflag = hh >= 0 ? T.fhelp[hh].flag : 0;
-  const int64_t himg = hh >= 0 ? T.fhelp[hh].img : 0;
+  const int64_t himg = hh >= 0 ? T.fhelp[hh].img : 0, hdofs = hh >= 0 ? T.fhelp[hh].dofs : 0;
+  const int hnimg = hh >= 0 ? T.fhelp[hh].nimg : 0;
   {  // the front and its leaf batches must fit the launch's LDS: else a sticky error, never a write
      // past the carve (the symbolic analysis sizes both; this catches a plan that breaks it)
     const int ntot = PK ? r * (r + 1) / 2 : r * ld;
@@ -2140,18 +2141,22 @@ __device__ __forceinline__ void fact_tree_front(const FrontTab& T, int s, const 
   if (hh >= 0 && tid == 0) poll_flag(flags + hflag, epoch, err);  // the helper that folded the first batches
   __syncthreads();
   if (dg && tid == 0) dg[2] = wall_clock64();
-  if (hh >= 0) {  // its image (this front's LDS layout) added entry by entry, 16 loads in flight per thread
+  if (hh >= 0) {  // its image — the entries its products reached, in LDS order — added entry by entry,
+                  // 16 loads in flight per thread (the untouched entries, zero in the image, are skipped)
     const double* __restrict__ img = T.fimg + himg;
-    const int ntot = PK ? r * (r + 1) / 2 : r * ld;
-    for (int base = 0; base < ntot; base += FTN * 16) {
+    const uint16_t* __restrict__ hd = T.fimg_dst + hdofs;
+    for (int base = 0; base < hnimg; base += FTN * 16) {
       double v[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) v[k] = ld_sc1(img + min(base + k * FTN + tid, ntot - 1));
+      int q[16];
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
-        const int q = base + k * FTN + tid;
-        if (q < ntot) A[q] += v[k];
+        const int e = min(base + k * FTN + tid, hnimg - 1);
+        v[k] = ld_sc1(img + e);
+        q[k] = hd[e];
       }
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (base + k * FTN + tid < hnimg) A[q[k]] += v[k];
     }
     __syncthreads();
   }
@@ -2412,8 +2417,9 @@ __device__ __forceinline__ void fold_help_task(const FrontTab& T, int h, int32_t
   fold_leaves<PK>(T, s, r, ld, A, Kx, arena, D, st, tol, A + ((ntot + 1) & ~1), cbuf, reinterpret_cast<int32_t*>(MK),
                   nullptr, H.fs, false);
   __syncthreads();
-  double* __restrict__ img = T.fimg + H.img;
-  for (int q = tid; q < ntot; q += FTN) st_sc1(img + q, A[q]);
+  double* __restrict__ img = T.fimg + H.img;  // only the entries its products reached (fimg_dst)
+  const uint16_t* __restrict__ hd = T.fimg_dst + H.dofs;
+  for (int k = tid; k < H.nimg; k += FTN) st_sc1(img + k, A[hd[k]]);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) __hip_atomic_store(&flags[H.flag], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -5067,18 +5073,43 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         return F;
       };
       std::vector<FoldHelp> hv;
+      std::vector<uint16_t> hdst;  // per helper: the sorted LDS destinations its batches' products reach
       int64_t img = 0;
+      // the run-end entries of a batch's product chunks name every destination it writes (a parked
+      // continuation ends at its run's destination too): the image holds exactly those
+      auto dests = [&](int b0, int b1, std::vector<uint16_t>& out) {
+        std::vector<int32_t> v;
+        for (int b = b0; b < b1; ++b) {
+          const int64_t po = S.fold_poff[b];
+          const int len = S.fold_plen[b];
+          for (int t = 0; t < SymbolicPlan::kFoldThreads; ++t) {
+            int d = (int)(S.fold_chead[(int64_t)b * SymbolicPlan::kFoldThreads + t] & 0xffffu);
+            for (int k = 0; k < len; ++k) {
+              const uint32_t e = S.fold_prod[po + (int64_t)SymbolicPlan::kFoldThreads * k + t];
+              d += (int)((e >> 24) & 127u);
+              if ((int32_t)e < 0) v.push_back(d);
+            }
+          }
+        }
+        std::sort(v.begin(), v.end());
+        v.erase(std::unique(v.begin(), v.end()), v.end());
+        for (int x : v) {
+          MADIPM_REQUIRE(x >= 0 && x < 65536, "fold helper: LDS destination beyond 16 bits");
+          out.push_back((uint16_t)x);
+        }
+        return (int32_t)v.size();
+      };
       if (!S.fold_bptr.empty())
         for (int f = 0; f < ns; ++f) fst[f] = start(S.fold_bptr[f], S.fold_bptr[f + 1]);
       for (int f : ord) {
         if (!on || !S.absorb[f]) continue;
         const int b0 = S.fold_bptr[f], nb = S.fold_bptr[f + 1] - b0;
         if (nb < min_nb) continue;
-        const int r = S.nrows[f];
-        const bool sq = r <= 128 && !S.fold_pk[f];
-        const int64_t ntot = sq ? (int64_t)r * (r | 1) : (int64_t)r * (r + 1) / 2;
-        hv.push_back(FoldHelp{f, 0, img, start(b0, b0 + std::max(1, std::min(nb - 1, nb * share4 / 4)))});
-        img += (ntot + 1) & ~1LL;
+        const int hb1 = b0 + std::max(1, std::min(nb - 1, nb * share4 / 4));
+        const int64_t dofs = (int64_t)hdst.size();
+        const int32_t nimg = dests(b0, hb1, hdst);
+        hv.push_back(FoldHelp{f, 0, img, dofs, nimg, 0, start(b0, hb1)});
+        img += (nimg + 1) & ~1LL;
       }
       std::stable_sort(hv.begin(), hv.end(),
                        [](const FoldHelp& a, const FoldHelp& b) { return a.fs.b1 - a.fs.b0 > b.fs.b1 - b.fs.b0; });
@@ -5090,8 +5121,13 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       }
       fstart_.upload(fst);
       fold_help_.upload(help);
-      fhelp_.upload(hv.empty() ? std::vector<FoldHelp>{FoldHelp{0, 0, 0, FoldStart{0, 0, 0, 0, 0, 0, 0, 0, 0}}} : hv);
+      fhelp_.upload(hv.empty() ? std::vector<FoldHelp>{FoldHelp{0, 0, 0, 0, 0, 0, FoldStart{0, 0, 0, 0, 0, 0, 0, 0, 0}}} : hv);
       fimg_.alloc((size_t)std::max<int64_t>(img, 2));
+      fimg_dst_.upload(hdst.empty() ? std::vector<uint16_t>{0} : hdst);
+      T_.fimg_dst = fimg_dst_;
+      if (std::getenv("MADIPM_TREE_DEBUG"))
+        fprintf(stderr, "fold helpers: %d, image entries %lld (%.1f MB per factorisation, stored + read)\n", nfhelp_,
+                (long long)hdst.size(), 16e-6 * (double)hdst.size());
       T_.fstart = fstart_;
       T_.fold_help = fold_help_;
       T_.fhelp = fhelp_;

@@ -26,7 +26,9 @@ struct FoldStart {
 };
 struct FoldHelp {
   int32_t front, flag;  // the front, the flag the helper publishes
-  int64_t img;          // its image in FrontTab::fimg (the front's LDS layout, ntot doubles)
+  int64_t img;          // its image in FrontTab::fimg: nimg doubles, entry k = LDS entry fimg_dst[dofs + k]
+  int64_t dofs;         // its destinations in FrontTab::fimg_dst (the LDS entries its batches' products reach)
+  int32_t nimg, pad;
   FoldStart fs;         // its batches
 };
 
@@ -96,6 +98,7 @@ struct FrontTab {
   const int32_t* fold_help;
   const FoldHelp* fhelp;
   double* fimg;
+  const uint16_t* fimg_dst;  // per helper: the sorted LDS destinations of its products (FoldHelp::dofs)
   uint64_t* xll;  // big-front solves: panel solutions as self-validating words (ll_put / ll_get)
 };
 
@@ -380,6 +383,7 @@ class LDLSolver : public LinSolver {
   DBuf<int32_t> fold_help_;
   DBuf<FoldHelp> fhelp_;
   DBuf<double> fimg_;
+  DBuf<uint16_t> fimg_dst_;
   int nfhelp_ = 0;  // fold helper tickets (k_fact_tree: before the fronts')
   DBuf<uint8_t> absorb_, fold_pk_, fs_img_;
   DBuf<int32_t> mc_ptr_;

@@ -6,7 +6,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 for spec in "$@"; do
   label=${spec%%|*}; envs=${spec#*|}
-  env $envs timeout -k 10 200 python bench.py --no-cpu --no-opt --no-neos --steps 20 > $OUT/b_$label.log 2>&1 || { echo "$label FAILED"; tail -5 $OUT/b_$label.log; exit 1; }
+  env $envs timeout -k 10 200 python bench.py --no-cpu --no-opt --legs none --steps 20 > $OUT/b_$label.log 2>&1 || { echo "$label FAILED"; tail -5 $OUT/b_$label.log; exit 1; }
   python - $OUT/b_$label.log $label <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])

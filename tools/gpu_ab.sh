@@ -15,7 +15,7 @@ fi
 for c in $CFGS; do
   for E in - $KNOBS; do
     [ "$E" = "-" ] && E=""
-    env $E timeout -k 10 300 python bench.py --config $c --steps $STEPS --warmup 3 --no-cpu --no-neos > $OUT/bench_${c}_${E:-default}.log 2>&1 \
+    env $E timeout -k 10 300 python bench.py --config $c --steps $STEPS --warmup 3 --no-cpu --legs none > $OUT/bench_${c}_${E:-default}.log 2>&1 \
       || { echo "bench $c ${E:-default} FAILED"; tail -20 $OUT/bench_${c}_${E:-default}.log; exit 1; }
     echo "$c ${E:-default}: $(tail -1 $OUT/bench_${c}_${E:-default}.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); c=d["config"]; print(round(d["value"],1), round(d["ms_per_step"],4), c.get("status"), c.get("iters_to_opt"), c.get("wall_clock_to_opt_s"), c.get("objective"), c.get("analysis_s"))' 2>&1 | cut -c1-300)"
   done
