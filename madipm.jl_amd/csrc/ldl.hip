@@ -2470,23 +2470,41 @@ __global__ __launch_bounds__(FTN) void k_fact_tree(FrontTab T, const int32_t* __
 // write L11 (d on the diagonal), D and the M_K blocks for k_big_trsm.
 // The diagonal block of panel `step` of front s, staged in A64 (lower part, identity-padded past kw):
 // blocked factorisation, then L11 (d on the diagonal), D and the M_K blocks for k_big_trsm.
+// Loads / stores of the big-front panel kernels: plain in their own launches (kernel boundaries order
+// them), write-through (sc1) stores and sc1 loads inside k_big_chain, whose tasks hand tiles to each
+// other within one launch (every handed-off byte stored sc1 and drained before the flag, every load
+// of it sc1: the guide's Guideline 16, R1 without an acquire).
+template <bool SC>
+__device__ __forceinline__ double ldF(const double* p) {
+  if constexpr (SC) return ld_sc1(p);
+  else return *p;
+}
+template <bool SC>
+__device__ __forceinline__ void stF(double* p, double v) {
+  if constexpr (SC) st_sc1(p, v);
+  else *p = v;
+}
+constexpr int BIG_MSZ = 4 * 16 * LDM;  // doubles of one panel's M_K blocks
+
+// the diagonal block of panel `step`, staged in A64: factorised; L11 (d on the diagonal), D and the
+// M_K blocks (to M: the front's slot in Mbuf, or the panel's slot in k_big_chain's Mch) written
+template <bool SC = false>
 __device__ __forceinline__ void big_diag_tail(const FrontTab& T, int s, int step, double* A64, double* Ms, double* Dl,
                                               double* __restrict__ arena, double* __restrict__ D,
-                                              double* __restrict__ Mbuf, LDLStatus* st, double tol) {
+                                              double* __restrict__ M, LDLStatus* st, double tol) {
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
   const int k0 = step * 64, kw = min(64, w - k0);
   double* __restrict__ F = arena + T.l_off[s] + k0 + (int64_t)k0 * r;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   diag64(A64, Dl, Ms, tid);
   for (int j = wv; j < kw; j += 4)
-    if (lane >= j && lane < kw) F[lane + (int64_t)j * r] = (lane == j) ? Dl[j] : A64[lane + j * LDA];
+    if (lane >= j && lane < kw) stF<SC>(F + lane + (int64_t)j * r, (lane == j) ? Dl[j] : A64[lane + j * LDA]);
   if (tid < kw) {
     const double d = Dl[tid];
-    D[f0 + k0 + tid] = d;
+    stF<SC>(D + f0 + k0 + tid, d);
     if (bad_pivot(d, tol)) atomicMin(&st->fail_pivot, f0 + k0 + tid + 1);
   }
-  double* __restrict__ M = Mbuf + (int64_t)T.bigslot[s] * 4096;
-  for (int e = tid; e < 4 * 16 * LDM; e += NT) M[e] = Ms[e];
+  for (int e = tid; e < BIG_MSZ; e += NT) stF<SC>(M + e, Ms[e]);
 }
 
 // Lookahead: the update launch of panel `step` leaves panel step + 1's diagonal tile final in the
@@ -2531,27 +2549,25 @@ __global__ __launch_bounds__(NT) void k_big_diag(FrontTab T, const int32_t* __re
     }
   }
   __syncthreads();
-  big_diag_tail(T, s, step, A64, Ms, Dl, arena, D, Mbuf, st, tol);
+  big_diag_tail(T, s, step, A64, Ms, Dl, arena, D, Mbuf + (int64_t)T.bigslot[s] * 4096, st, tol);
 }
 
 // Rows below the diagonal block of panel `step` (64-row tiles; wave w owns 16 rows): blocked
 // forward substitution X_K = A_K - sum_{J<K} (L_J D_J) L_KJ^T, L_K = X_K M_K, all on f64 MFMA.
-__global__ __launch_bounds__(NT) void k_big_trsm(FrontTab T, const int32_t* __restrict__ list, int step,
-                                                 double* __restrict__ arena, const double* __restrict__ D,
-                                                 const double* __restrict__ Mbuf) {
-  __shared__ double L11[64 * LDA];
-  __shared__ double Ms[4 * 16 * LDM];
-  __shared__ double Dl[64];
-  __shared__ double Sl[4][17 * 64];  // per-wave slab: 16 rows x 64 cols, S[m + 17 * j]
-  int s, rt;
-  task_of(list, s, rt);
+// LDS of one k_big_trsm task: L11 (64 x LDA), the M_K blocks, the pivots, four 16 x 64 slabs
+constexpr int TRSM_LDS = 64 * LDA + BIG_MSZ + 64 + 4 * 17 * 64;
+template <bool SC>
+__device__ __forceinline__ void trsm_body(const FrontTab& T, int s, int step, int rt, double* __restrict__ arena,
+                                          const double* __restrict__ D, const double* __restrict__ M, double* sm) {
+  double* L11 = sm;
+  double* Ms = sm + 64 * LDA;
+  double* Dl = Ms + BIG_MSZ;
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
   const int k0 = step * 64, kw = min(64, w - k0);
   const int I0 = k0 + kw + rt * 64;
   double* __restrict__ F = arena + T.l_off[s];
-  const double* __restrict__ M = Mbuf + (int64_t)T.bigslot[s] * 4096;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  double* S = Sl[wv];
+  double* S = Dl + 64 + wv * (17 * 64);  // this wave's slab: 16 rows x 64 cols, S[m + 17 * j]
   const int row = I0 + 16 * wv + (lane & 15);  // slab row of this lane; 4 columns per pass
   {
     // every operand load in flight at once from clamped addresses, masked at the LDS stores (a
@@ -2560,12 +2576,12 @@ __global__ __launch_bounds__(NT) void k_big_trsm(FrontTab T, const int32_t* __re
     const int lc = min(lane, kw - 1), rc = min(row, r - 1);
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      lv[e] = F[(k0 + lc) + (int64_t)(k0 + min(wv + 4 * e, kw - 1)) * r];
-      sv[e] = F[rc + (int64_t)(k0 + min((lane >> 4) + 4 * e, kw - 1)) * r];
+      lv[e] = ldF<SC>(F + (k0 + lc) + (int64_t)(k0 + min(wv + 4 * e, kw - 1)) * r);
+      sv[e] = ldF<SC>(F + rc + (int64_t)(k0 + min((lane >> 4) + 4 * e, kw - 1)) * r);
     }
 #pragma unroll
-    for (int e = 0; e < 5; ++e) mv[e] = M[min(tid + e * NT, 4 * 16 * LDM - 1)];
-    dv = D[f0 + k0 + min(tid, kw - 1)];
+    for (int e = 0; e < 5; ++e) mv[e] = ldF<SC>(M + min(tid + e * NT, BIG_MSZ - 1));
+    dv = ldF<SC>(D + f0 + k0 + min(tid, kw - 1));
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int j = wv + 4 * e, jj = (lane >> 4) + 4 * e;
@@ -2574,7 +2590,7 @@ __global__ __launch_bounds__(NT) void k_big_trsm(FrontTab T, const int32_t* __re
     }
 #pragma unroll
     for (int e = 0; e < 5; ++e)
-      if (tid + e * NT < 4 * 16 * LDM) Ms[tid + e * NT] = mv[e];
+      if (tid + e * NT < BIG_MSZ) Ms[tid + e * NT] = mv[e];
     if (tid < 64) Dl[tid] = (tid < kw) ? dv : 1.0;
   }
   __syncthreads();
@@ -2606,7 +2622,18 @@ __global__ __launch_bounds__(NT) void k_big_trsm(FrontTab T, const int32_t* __re
     wave_sync();
   }
   for (int j = lane >> 4; j < kw; j += 4)
-    if (row < r) F[row + (int64_t)(k0 + j) * r] = S[(lane & 15) + j * 17];
+    if (row < r) stF<SC>(F + row + (int64_t)(k0 + j) * r, S[(lane & 15) + j * 17]);
+}
+
+// Rows below the diagonal block of panel `step` (64-row tiles; wave w owns 16 rows): blocked
+// forward substitution X_K = A_K - sum_{J<K} (L_J D_J) L_KJ^T, L_K = X_K M_K, all on f64 MFMA.
+__global__ __launch_bounds__(NT) void k_big_trsm(FrontTab T, const int32_t* __restrict__ list, int step,
+                                                 double* __restrict__ arena, const double* __restrict__ D,
+                                                 const double* __restrict__ Mbuf) {
+  __shared__ __attribute__((aligned(16))) double sm[TRSM_LDS];
+  int s, rt;
+  task_of(list, s, rt);
+  trsm_body<false>(T, s, step, rt, arena, D, Mbuf + (int64_t)T.bigslot[s] * 4096, sm);
 }
 
 // Trailing update of one 64x64 lower tile: C -= (L_I D) L_J^T, f64 MFMA 16x16x4, over K = the
@@ -2618,16 +2645,18 @@ __global__ __launch_bounds__(NT) void k_big_trsm(FrontTab T, const int32_t* __re
 // kpan = 1: every step is a group of one (the r2 right-looking update).  The K chunks of 64 are
 // staged through LDS one after another; the next chunk's operands are loaded (from
 // clamped addresses) while the current chunk's MFMAs run.
-__global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __restrict__ list, int step, int kpan,
-                                                   double* __restrict__ arena, double* __restrict__ D,
-                                                   double* __restrict__ Mbuf, LDLStatus* st, double tol) {
-  constexpr int LDT = 80;  // [k][row] layout: conflict-free ds_read_b64 for the 16x4 operand pattern
-  __shared__ __attribute__((aligned(16))) double WLt[2 * 64 * LDT];
+constexpr int UPD_LDT = 80;  // [k][row] layout: conflict-free ds_read_b64 for the 16x4 operand pattern
+constexpr int UPD_LDS = 2 * 64 * UPD_LDT;
+// Mnext: where the lookahead diagonal block's M_K blocks go (the front's Mbuf slot; k_big_chain: the
+// next panel's slot)
+template <bool SC>
+__device__ __forceinline__ void update_body(const FrontTab& T, int s, int step, int kpan, int tij,
+                                            double* __restrict__ arena, double* __restrict__ D,
+                                            double* __restrict__ Mnext, LDLStatus* st, double tol, double* WLt) {
+  constexpr int LDT = UPD_LDT;
   double* Wt = WLt;
   double* Lt = WLt + 64 * LDT;
   static_assert(64 * LDA <= 64 * LDT && 4 * 16 * LDM + 64 <= 64 * LDT, "lookahead diagonal block aliases Wt / Lt");
-  int s, tij;
-  task_of(list, s, tij);
   const int ti = tij & 0xffff, tj = (tij >> 16) & 0x7fff;
   const bool trailing = tij < 0;
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
@@ -2652,9 +2681,9 @@ __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __
     for (int e = 0; e < 16; ++e) {
       const int kk = min(kb + 64 * ch + wv + 4 * e, ke - 1);
       const int64_t col = (int64_t)kk * r;
-      wl[e] = F[ri + col];
-      ll[e] = F[rj + col];
-      dk[e] = D[f0 + kk];
+      wl[e] = ldF<SC>(F + ri + col);
+      ll[e] = ldF<SC>(F + rj + col);
+      dk[e] = ldF<SC>(D + f0 + kk);
     }
   };
   load(0);
@@ -2668,7 +2697,7 @@ __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __
       for (int g = 0; g < 4; ++g) {
         const int i = min(I0 + qr + bi * 16 + (lane & 15), r - 1);
         const int j = min(J0 + qc + bj * 16 + (lane >> 4) + 4 * g, r - 1);
-        c[bj][bi][g] = F[i + (int64_t)j * r];  // masked at the store
+        c[bj][bi][g] = ldF<SC>(F + i + (int64_t)j * r);  // masked at the store
       }
   dbl4 acc[2][2];
 #pragma unroll
@@ -2711,7 +2740,7 @@ __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __
       for (int g = 0; g < 4; ++g) {
         const int i = I0 + qr + bi * 16 + (lane & 15);
         const int j = J0 + qc + bj * 16 + (lane >> 4) + 4 * g;
-        if (i < r && j < jlim && i >= j) F[i + (int64_t)j * r] = c[bj][bi][g] - acc[bj][bi][g];
+        if (i < r && j < jlim && i >= j) stF<SC>(F + i + (int64_t)j * r, c[bj][bi][g] - acc[bj][bi][g]);
       }
   // lookahead: task (0, 0) of a local update holds the next panel's diagonal tile, final now (the
   // panel's last local update; the next panel lies inside the group, below jlim)
@@ -2720,6 +2749,7 @@ __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __
     double* Ms = Lt;
     double* Dl = Lt + 4 * 16 * LDM;
     const int kw = min(64, w - c0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tile's C stores land before L11's (same addresses)
     __syncthreads();  // every wave's last MFMA operand read
     big_diag_prepare(A64, kw);
     __syncthreads();
@@ -2733,7 +2763,90 @@ __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __
           if (i < kw && j < kw && i >= j) A64[i + j * LDA] = c[bj][bi][g] - acc[bj][bi][g];
         }
     __syncthreads();
-    big_diag_tail(T, s, step + 1, A64, Ms, Dl, arena, D, Mbuf, st, tol);
+    big_diag_tail<SC>(T, s, step + 1, A64, Ms, Dl, arena, D, Mnext, st, tol);
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __restrict__ list, int step, int kpan,
+                                                   double* __restrict__ arena, double* __restrict__ D,
+                                                   double* __restrict__ Mbuf, LDLStatus* st, double tol) {
+  __shared__ __attribute__((aligned(16))) double WLt[UPD_LDS];
+  int s, tij;
+  task_of(list, s, tij);
+  update_body<false>(T, s, step, kpan, tij, arena, D, Mbuf + (int64_t)T.bigslot[s] * 4096, st, tol, WLt);
+}
+
+// One panel group of the level's big fronts in ONE launch (r6): the group's k_big_trsm tiles and
+// local k_big_update tiles (steps g0 .. g0 + kpan - 1 of every front) as tasks of a dependency-driven
+// persistent kernel instead of one launch per step and kind (neos: 337 launches per factorisation, each
+// boundary a ~4.6 us gap, and the panel chain diag -> trsm -> update serialised by them).  Tasks are in
+// topological order (a step's trsm tiles, then its updates, then the next step); a workgroup takes the
+// next ticket, polls the flags of its <= 3 dependencies, runs the task and publishes its flag:
+//   trsm (s, p, rt):     the diagonal block of panel p (the update task (s, p - 1, 0, 0) factorised it)
+//                        and the row tile's panel-p block after its last local update (s, p - 1, rt + 1, 0);
+//   update (s, p, i, j): the trsm tiles (s, p, i) and (s, p, j) (its L_I and L_J rows) and the tile's
+//                        previous update (s, p - 1, i + 1, j + 1);
+// (for p = g0 every input was written by earlier launches).  A workgroup only waits for lower tickets,
+// taken by running workgroups: no deadlock whatever the residency.  Every handed-off value is stored
+// write-through (sc1) and drained before the flag; every load of one is sc1.  Each panel's M_K blocks go
+// to a slot of their own (Mch, per front and panel): a later diagonal block never overwrites the one a
+// slow trsm task of the previous panel still reads.  Same operands and MFMA order as the per-step
+// kernels: the same factor bit for bit.
+struct ChainTask {
+  int32_t s, step, item, kind;  // kind 0: trsm (item = row tile), 1: local update (item = ti | tj << 16)
+};
+__global__ __launch_bounds__(NT, 2) void k_big_chain(FrontTab T, const ChainTask* __restrict__ tasks, const int4* __restrict__ deps,
+                                                  int ntask, int32_t* flags, int epoch, int32_t* counter, int kpan,
+                                                  double* __restrict__ arena, double* __restrict__ D,
+                                                  const double* __restrict__ Mbuf, double* __restrict__ Mch,
+                                                  const int64_t* __restrict__ mslot, LDLStatus* st, double tol,
+                                                  int32_t* err) {
+  // 80 KB: two workgroups per CU (the ticket word borrows the first double: read before any task uses it)
+  __shared__ __attribute__((aligned(16))) double sm[UPD_LDS > TRSM_LDS ? UPD_LDS : TRSM_LDS];
+  int* s_t = reinterpret_cast<int*>(sm);
+  const int tid = threadIdx.x, lane = tid & 63;
+  for (;;) {
+    __syncthreads();  // the previous task's LDS reads
+    if (tid == 0) *s_t = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int t = *s_t;
+    __syncthreads();  // every wave has the ticket before a task overwrites the word
+    if (t >= ntask) break;
+    const ChainTask tk = tasks[t];
+    if (tid < 64) {
+      const int4 dp = deps[t];
+      const int d = lane == 0 ? dp.x : lane == 1 ? dp.y : lane == 2 ? dp.z : -1;
+      int spins = 0;
+      for (;;) {
+        const bool ok = d < 0 || __hip_atomic_load(flags + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+        if (__all(ok)) break;
+        __builtin_amdgcn_s_sleep(1);
+        ++spins;
+        // bounded: a lost hand-off raises the sticky error, and once raised no later wait spins
+        // (the launch drains in milliseconds, the factor is reported invalid)
+        if (spins > (1 << 25) ||
+            ((spins & 1023) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+          if (lane == 0) atomicOr(err, kErrHandoff);
+          break;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only (sc1 loads follow)
+    }
+    __syncthreads();
+    const int g0 = (tk.step / kpan) * kpan;
+    if (tk.kind == 0) {
+      const double* M = tk.step == g0 ? Mbuf + (int64_t)T.bigslot[tk.s] * 4096 : Mch + (mslot[tk.s] + tk.step) * BIG_MSZ;
+      trsm_body<true>(T, tk.s, tk.step, tk.item, arena, D, M, sm);
+    } else {
+      update_body<true>(T, tk.s, tk.step, kpan, tk.item, arena, D, Mch + (mslot[tk.s] + tk.step + 1) * BIG_MSZ, st, tol, sm);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's sc1 stores drained
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(flags + t, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (tid == 0 && atomicAdd(counter + 1, 1) == (int)gridDim.x - 1) {  // last one out: reset the tickets
+    counter[0] = 0;
+    counter[1] = 0;
   }
 }
 
@@ -3083,7 +3196,7 @@ __global__ __launch_bounds__(NT, 2) void k_big_upd128(FrontTab T, const int32_t*
           }
     }
     __syncthreads();
-    big_diag_tail(T, s, step + 1, A64, Ms, Dl, arena, D, Mbuf, st, tol);
+    big_diag_tail(T, s, step + 1, A64, Ms, Dl, arena, D, Mbuf + (int64_t)T.bigslot[s] * 4096, st, tol);
   }
 }
 
@@ -4690,6 +4803,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     big_kpan_ = ek ? std::max(1, std::min(8, std::atoi(ek))) : 4;
     const char* es = std::getenv("MADIPM_UPD_SPLIT");  // A/B: 0 = one workgroup per k_big_upd128 tile
     upd_split_ = !(es && es[0] == '0');
+    const char* ec = std::getenv("MADIPM_BIG_CHAIN");  // A/B: 0 = one launch per panel step and kind
+    big_chain_ = !(ec && ec[0] == '0');
     // persistent workgroups of the big-front solve kernels (2 per CU; MADIPM_BIG_SOLVE_WG for A/B)
     if (const char* eg = std::getenv("MADIPM_BIG_SOLVE_WG")) big_solve_wg_ = std::max(64, std::atoi(eg));
     // pipelined in-LDS factorisation schedule (1, default); 0 = the barrier schedule, bitwise the same
@@ -5233,6 +5348,153 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     L.bytes = 8.0 * (double)G.m * G.n + 16.0 * (double)G.m * (G.m + 1) / 2.0 * cdiv(G.n, LB_KCHUNK);
     out.push_back(L);
   };
+  // The big fronts of a level, panel group by panel group (k_big_chain): step 0's diagonal blocks
+  // (k_big_diag), then per group ONE chain launch (the group's trsm tiles and local updates, every
+  // front) and ONE k_big_upd128 launch (the trailing update of every front whose group ends there: its
+  // task (0, 0) factorises the next group's first diagonal block), and after group 0 the fused fronts'
+  // k_asm_update.  The same tiles, operands and order of sums as the per-step launches below.
+  std::vector<int32_t> ctask, cdep;  // chain tasks (s, step, item, kind) and their deps (4 per task)
+  std::vector<int64_t> mslot(std::max(S.nsuper, 1), 0);
+  int64_t nmslot = 0;
+  for (int f = 0; f < S.nsuper; ++f)
+    if (S.is_big[f]) {
+      mslot[f] = nmslot;
+      nmslot += cdiv(S.first[f + 1] - S.first[f], 64) + 1;
+    }
+  auto chain_level = [&](const std::vector<int32_t>& big, int lev, int phase, std::vector<Launch>& out) {
+    int maxsteps = 0;
+    for (int s : big) maxsteps = std::max<int>(maxsteps, (int)cdiv(S.first[s + 1] - S.first[s], 64));
+    const int kp = big_kpan_;
+    double pend_alg = 0.0;  // 8(d) bytes of panels whose launch carried nothing (added to the next launch)
+    for (int g0 = 0; g0 < maxsteps; g0 += kp) {
+      if (g0 == 0) {  // the first diagonal blocks
+        align2();
+        Launch L{BIG_DIAG, 0, (int64_t)sched.size(), 0, 0};
+        for (int s : big) {
+          const int w = S.first[s + 1] - S.first[s];
+          const double dk = std::min(64, w);
+          sched.insert(sched.end(), {s, 0});
+          L.items++;
+          L.bytes += 8.0 * (dk * (dk + 1) + 4 * 16 * 17);
+          L.flops += dk * dk * dk / 3.0;
+          L.alg += fact_alg_cols(S.first[s], S.first[s] + (int)dk);
+        }
+        out.push_back(L);
+      }
+      // the chain: per step, every front's trsm tiles, then its local updates
+      Launch C{BIG_CHAIN, g0, (int64_t)(ctask.size() / 4), 0, 0};
+      C.alg = pend_alg;
+      pend_alg = 0.0;
+      std::map<std::tuple<int, int, int, int, int>, int> tix;  // (kind, s, p, i, j) -> launch-local ticket
+      for (int p = g0; p < std::min(g0 + kp, maxsteps); ++p) {
+        for (int kind = 0; kind < 2; ++kind)
+          for (int s : big) {
+            const int w = S.first[s + 1] - S.first[s], r = S.nrows[s];
+            const int npan = (int)cdiv(w, 64);
+            if (npan <= p) continue;
+            const int k0 = p * 64, kw = std::min(64, w - k0);
+            const int nt = (int)cdiv(r - k0 - kw, 64);
+            const double dk = kw, nb = r - k0 - kw;
+            const int gl = std::min(g0 + kp, npan) - 1;
+            const int gend = std::min(64 * (gl + 1), w);
+            if (kind == 0) {
+              if (p > 0) C.alg += fact_alg_cols(S.first[s] + k0, S.first[s] + k0 + kw);
+              C.bytes += 8.0 * (2.0 * nb * dk + nt * (dk * (dk + 1) / 2 + 4 * 16 * 17));
+              C.flops += nb * dk * dk;
+              for (int rt = 0; rt < nt; ++rt) {
+                const int t = (int)C.items++;
+                tix[{0, s, p, rt, 0}] = t;
+                ctask.insert(ctask.end(), {s, p, rt, 0});
+                // the diagonal block (factorised by the previous step's update task (0, 0)) and the
+                // update tiles of the previous step that hold this tile's rows of panel p: tile rt + 1
+                // (full panel), tiles rt and rt + 1 (a partial last panel: rows from 64 p + kw)
+                int d0 = -1, d1 = -1, d2 = -1;
+                if (p > g0) {
+                  const int ntp = (int)cdiv(r - 64 * p, 64);  // the previous step's row tiles
+                  const int ia = (kw + 64 * rt) / 64, ib = std::min((kw + 64 * rt + 63) / 64, ntp - 1);
+                  d0 = tix.at({1, s, p - 1, 0, 0});
+                  d1 = tix.at({1, s, p - 1, ia, 0});
+                  d2 = ib != ia ? tix.at({1, s, p - 1, ib, 0}) : -1;
+                }
+                cdep.insert(cdep.end(), {d0, d1, d2, 0});
+              }
+            } else {
+              if (S.fused[s] || p >= gl) continue;
+              const double nc = gend - (k0 + kw);
+              C.bytes += 8.0 * (2.0 * nb * nc + nb * dk + nc * dk);
+              C.flops += 2.0 * dk * nc * (nb - 0.5 * nc);
+              for (int j = 0; j < (int)cdiv((int)nc, 64); ++j)
+                for (int i = j; i < nt; ++i) {
+                  const int t = (int)C.items++;
+                  tix[{1, s, p, i, j}] = t;
+                  ctask.insert(ctask.end(), {s, p, i | (j << 16), 1});
+                  const int di = tix.at({0, s, p, i, 0}), dj = i != j ? tix.at({0, s, p, j, 0}) : -1;
+                  const int dp = p > g0 ? tix.at({1, s, p - 1, i + 1, j + 1}) : -1;
+                  cdep.insert(cdep.end(), {di, dj, dp, 0});
+                }
+            }
+          }
+      }
+      if (C.items) {
+        out.push_back(C);
+      } else {
+        pend_alg += C.alg;
+      }
+      // the trailing updates of every front whose group ends here
+      align2();
+      Launch U{BIG_UPDATE128, g0 + kp - 1, (int64_t)sched.size(), 0, 0};
+      for (int s : big) {
+        const int w = S.first[s + 1] - S.first[s], r = S.nrows[s];
+        const int npan = (int)cdiv(w, 64);
+        if (npan <= g0 || S.fused[s]) continue;
+        const int gend = std::min(64 * (g0 + kp), w);
+        const int c0 = gend, ntt = (int)cdiv(r - c0, 128);
+        const double K = gend - 64 * g0, nbt = r - c0;
+        for (int i = 0; i < ntt; ++i)
+          for (int j = 0; j <= i; ++j) {
+            sched.insert(sched.end(), {s, i | (j << 16)});
+            U.items++;
+          }
+        U.bytes += 8.0 * (nbt * (nbt + 1) + 2.0 * nbt * K);
+        U.flops += K * nbt * (nbt + 1);
+      }
+      if (U.items) {
+        U.nf = !upd_split_ ? 1 : U.items <= 128 ? 4 : U.items <= 170 ? 3 : U.items <= 256 ? 2 : 1;
+        U.alg = pend_alg;
+        pend_alg = 0.0;
+        out.push_back(U);
+      }
+      if (g0 == 0 && phase == 1 && S.atile_fz0[lev] < S.atile_lev[lev + 1]) {
+        // the fused fronts' trailing tiles: assembled + updated after their panel (one launch)
+        const int32_t t0 = S.atile_fz0[lev], t1 = S.atile_lev[lev + 1];
+        Launch L{ASM_UPDATE, 0, t0, 4, t1 - t0};
+        for (int32_t t = t0; t < t1; ++t) {
+          const SymbolicPlan::AsmTile& at = S.atiles[t];
+          const int f = at.front, r = S.nrows[f], w = S.first[f + 1] - S.first[f];
+          L.nf = std::max(L.nf, (w + 3) & ~3);
+          const int ti = at.tij & 0xffff, tj = (at.tij >> 16) & 0x7fff;
+          const double nr = std::min(64, r - 64 * ti), nc = std::min(64, r - 64 * tj);
+          L.bytes += 8.0 * (ti == tj ? nr * (nr + 1) / 2 : nr * nc) + (at.gptr >= 0 ? 4.0 * (S.g_ptr[at.gptr] + 2) : 0.0) +
+                     8.0 * (nr + nc) * w;
+          for (int k = at.bt0; k < at.bt1; ++k) {
+            const int32_t* e = &S.bt[5 * k];
+            for (int b = e[1]; b < e[2]; ++b) L.bytes += 8.0 * std::max(0, e[4] - std::max(b, e[3]));
+          }
+          L.flops += 2.0 * nr * nc * w;
+        }
+        L.alg = pend_alg;
+        pend_alg = 0.0;
+        out.push_back(L);
+      }
+    }
+    if (pend_alg > 0.0) {  // (a level whose last panels launched nothing: onto its last launch)
+      for (auto it = out.rbegin(); it != out.rend(); ++it)
+        if (it->kind == BIG_CHAIN || it->kind == BIG_UPDATE128 || it->kind == BIG_DIAG || it->kind == ASM_UPDATE) {
+          it->alg += pend_alg;
+          break;
+        }
+    }
+  };
   auto build_fact = [&](int phase, std::vector<Launch>& out) {
     if (phase == 1 && !S.lb.empty()) {
       Launch L{LB_BUILD, 0, 0, 0, (int64_t)S.lb_mem.size()};
@@ -5299,6 +5561,10 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
           sched.insert(sched.end(), cls[c].begin(), cls[c].end());
         }
       if (big.empty()) continue;
+      if (big_chain_) {
+        chain_level(big, lev, phase, out);
+        continue;
+      }
       int maxsteps = 0;
       for (int s : big) maxsteps = std::max<int>(maxsteps, (int)cdiv(S.first[s + 1] - S.first[s], 64));
       int64_t last_upd = -1;  // the latest update launch (it factorised the next step's diagonal blocks)
@@ -5395,6 +5661,20 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     for (size_t g = 0; g < S.lb.size(); ++g)  // this shard's batched leaves under top fronts: into it
       if (S.top(S.lb[g].parent)) lb_syrk_launch((int)g, fact1_);
     build_fact(2, fact2_);
+  }
+  if (!ctask.empty()) {  // chain tasks, dependencies, flags, counters, per-panel M_K slots
+    chain_tasks_.upload(ctask);
+    chain_deps_.upload(cdep);
+    chain_flags_.alloc((int64_t)ctask.size() / 4);
+    chain_flags_.zero();
+    chain_cnt_.alloc(2);
+    chain_cnt_.zero();
+    chain_m_.alloc(std::max<int64_t>(nmslot, 1) * BIG_MSZ);
+    chain_mslot_.upload(mslot);
+    int dev = 0, ncu = 0;
+    MADIPM_HIP(hipGetDevice(&dev));
+    MADIPM_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    chain_grid_ = std::max(1, 2 * ncu);  // two workgroups per CU (80 KB of LDS, <= 256 registers)
   }
   {  // k_big_upd128's split-K scratch: partial products and per-tile tickets of the largest split launch
     int64_t np = 0, nt = 0;
@@ -5884,6 +6164,7 @@ double LDLSolver::solve_alg(int s) const {
 }
 
 void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStream_t s) {
+  ++cepoch_;  // k_big_chain's flags: this factorisation's epoch (never 0)
   for (const Launch& L : LL) {
     const int32_t* list = sched_.p + L.off;
     switch (L.kind) {
@@ -5946,6 +6227,13 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
                                 T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, D_, L.nf, g_src32_.p, Kx)
                           : k_asm_update<int64_t><<<(unsigned)L.items, ANT, 2 * L.nf * AU_LDT * 8 + 8 * kAsmLdsSrc, s>>>(
                                 T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, D_, L.nf, g_src_.p, Kx)));
+        break;
+      case BIG_CHAIN:  // off = the launch's first task, items = its tasks
+        TIMED(KK_TRSM, L.bytes, L.alg, L.flops,
+              (k_big_chain<<<(unsigned)std::min<int64_t>(L.items, chain_grid_), NT, 0, s>>>(
+                  T_, reinterpret_cast<const ChainTask*>(chain_tasks_.p) + L.off,
+                  reinterpret_cast<const int4*>(chain_deps_.p) + L.off, (int)L.items, chain_flags_.p + L.off, cepoch_,
+                  chain_cnt_.p, big_kpan_, arena_, D_, minv_, chain_m_, chain_mslot_, st_, pivot_tol, &st_->err)));
         break;
       case BIG_UPDATE128:
         TIMED(KK_UPDATE, L.bytes, L.alg, L.flops,

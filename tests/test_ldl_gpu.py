@@ -427,3 +427,52 @@ def test_fold_many_leaves(n):
     info = ls.info()
     assert info["fold_fronts"] == 1 and info["fold_leaves"] > 1024, info
     assert ls.inertia() == (n, 0, 1)
+
+
+def _dense_kkt(n, m, seed=11):
+    import scipy.sparse as sp
+    rng = np.random.default_rng(seed)
+    B = rng.standard_normal((n, n))
+    H = B @ B.T / n + np.eye(n)
+    A = rng.standard_normal((m, n))
+    K = sp.csc_matrix(np.block([[H, A.T], [A, -1e-2 * np.eye(m)]]))
+    Lw = sp.tril(K).tocsc()
+    Lw.sort_indices()
+    return K, Lw
+
+
+@pytest.mark.parametrize("kpan", ["1", "2", "4"])
+@pytest.mark.parametrize("case", ["dense_320_100", "dense_130_200", "qp_dense_front", "neos_0.1"])
+def test_big_chain_bitwise(case, kpan, monkeypatch):
+    """k_big_chain (default, r6): a panel group's trsm and local-update tiles of every big front of a
+    level as dependency-ordered tasks of ONE persistent launch (sc1 hand-offs, per-panel M_K slots)
+    instead of one launch per step and kind (MADIPM_BIG_CHAIN=0).  Same operands and MFMA order: the
+    pivots and the solution agree BITWISE, and with the oracle (1e-12, well conditioned).  Dense K2s
+    with partial last panels (420 and 330 columns: rows of the last trsm straddle two update tiles),
+    a QP with a dense front, and the neos stand-in at 0.1 (many big fronts per level, fused fronts)."""
+    from helpers import lp_k2
+    monkeypatch.setenv("MADIPM_BIG_KPAN", kpan)
+    if case.startswith("dense"):
+        n, m = map(int, case.split("_")[1:])
+        K, Lw = _dense_kkt(n, m)
+        sfm = 16
+    elif case == "qp_dense_front":
+        K, Lw = random_k2(150, 400, 0.05, 11, qp=True, well=True)
+        sfm = 128
+    else:
+        from madipm_amd import standard_form_qp
+        from madipm_amd import instances as I
+        K, Lw = lp_k2(standard_form_qp(I.neos5052403_standin(scale=0.1)), 2, well=True)
+        sfm = 128
+    out = {}
+    for chain in ("0", "1"):
+        monkeypatch.setenv("MADIPM_BIG_CHAIN", chain)
+        out[chain] = _factor_solve(K, Lw, sfm)
+    (d0, x0, ls0), (d1, x1, _) = out["0"], out["1"]
+    assert ls0.info()["nbig"] >= 1
+    bad = np.flatnonzero(d0.view(np.uint64) != d1.view(np.uint64))
+    assert bad.size == 0, f"{bad.size} pivots differ, first {bad[:8]}"
+    assert np.array_equal(x0.view(np.uint64), x1.view(np.uint64))
+    ref = OracleLDL(K, ls0.perm())
+    assert ref.factorize() == K.shape[0]
+    _check_pivots(d1, ref.diag(), K)
