@@ -2471,23 +2471,27 @@ __global__ __launch_bounds__(FTN) void k_fact_tree(FrontTab T, const int32_t* __
 // The diagonal block of panel `step` of front s, staged in A64 (lower part, identity-padded past kw):
 // blocked factorisation, then L11 (d on the diagonal), D and the M_K blocks for k_big_trsm.
 // Loads / stores of the big-front panel kernels: plain in their own launches (kernel boundaries order
-// them), write-through (sc1) stores and sc1 loads inside k_big_chain, whose tasks hand tiles to each
+// them), write-through (sc1) stores and sc1 loads inside k_big_dag, whose tasks hand tiles to each
 // other within one launch (every handed-off byte stored sc1 and drained before the flag, every load
 // of it sc1: the guide's Guideline 16, R1 without an acquire).
+// (global address space explicitly: inside a non-inlined task body a generic pointer compiles to flat_
+// loads / stores, which also count on lgkmcnt — every LDS wait then waits for them — and are not the
+// global_ sc1 accesses the hand-off protocol requires)
+typedef __attribute__((address_space(1))) double gdouble;
 template <bool SC>
 __device__ __forceinline__ double ldF(const double* p) {
-  if constexpr (SC) return ld_sc1(p);
-  else return *p;
+  if constexpr (SC) return __hip_atomic_load((const gdouble*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *(const gdouble*)p;
 }
 template <bool SC>
 __device__ __forceinline__ void stF(double* p, double v) {
-  if constexpr (SC) st_sc1(p, v);
-  else *p = v;
+  if constexpr (SC) __hip_atomic_store((gdouble*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *(gdouble*)p = v;
 }
 constexpr int BIG_MSZ = 4 * 16 * LDM;  // doubles of one panel's M_K blocks
 
 // the diagonal block of panel `step`, staged in A64: factorised; L11 (d on the diagonal), D and the
-// M_K blocks (to M: the front's slot in Mbuf, or the panel's slot in k_big_chain's Mch) written
+// M_K blocks (to M: the front's slot in Mbuf, or the panel's slot in k_big_dag's Mch) written
 template <bool SC = false>
 __device__ __forceinline__ void big_diag_tail(const FrontTab& T, int s, int step, double* A64, double* Ms, double* Dl,
                                               double* __restrict__ arena, double* __restrict__ D,
@@ -2522,26 +2526,26 @@ __device__ __forceinline__ void big_diag_prepare(double* A64, int kw) {
   }
 }
 
-__global__ __launch_bounds__(NT) void k_big_diag(FrontTab T, const int32_t* __restrict__ list, int step,
-                                                 double* __restrict__ arena, double* __restrict__ D,
-                                                 double* __restrict__ Mbuf, LDLStatus* st, double tol) {
-  __shared__ double A64[64 * LDA];
-  __shared__ double Ms[4 * 16 * LDM];
-  __shared__ double Dl[64];
-  int s, item;
-  task_of(list, s, item);
-  (void)item;
+// the diagonal block of panel `step`: staged (identity-padded past kw), factorised, written (big_diag_tail)
+template <bool SC>
+__device__ __forceinline__ void diag_body(const FrontTab& T, int s, int step, double* __restrict__ arena,
+                                          double* __restrict__ D, double* __restrict__ M, LDLStatus* st, double tol,
+                                          double* sm) {
+  double* A64 = sm;
+  double* Ms = sm + 64 * LDA;
+  double* Dl = Ms + 4 * 16 * LDM;
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
   const int k0 = step * 64, kw = min(64, w - k0);
-  double* __restrict__ F = arena + T.l_off[s] + k0 + (int64_t)k0 * r;
+  const double* __restrict__ F = arena + T.l_off[s] + k0 + (int64_t)k0 * r;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  (void)f0;
   {
     // all 16 loads in flight from clamped addresses, masked after (a predicated load compiles into a
     // branch with a wait of its own)
     double v[16];
     const int lc = min(lane, kw - 1);
 #pragma unroll
-    for (int e = 0; e < 16; ++e) v[e] = F[lc + (int64_t)min(wv + 4 * e, kw - 1) * r];
+    for (int e = 0; e < 16; ++e) v[e] = ldF<SC>(F + lc + (int64_t)min(wv + 4 * e, kw - 1) * r);
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int j = wv + 4 * e;
@@ -2549,7 +2553,17 @@ __global__ __launch_bounds__(NT) void k_big_diag(FrontTab T, const int32_t* __re
     }
   }
   __syncthreads();
-  big_diag_tail(T, s, step, A64, Ms, Dl, arena, D, Mbuf + (int64_t)T.bigslot[s] * 4096, st, tol);
+  big_diag_tail<SC>(T, s, step, A64, Ms, Dl, arena, D, M, st, tol);
+}
+constexpr int DIAG_LDS = 64 * LDA + 4 * 16 * LDM + 64;
+__global__ __launch_bounds__(NT) void k_big_diag(FrontTab T, const int32_t* __restrict__ list, int step,
+                                                 double* __restrict__ arena, double* __restrict__ D,
+                                                 double* __restrict__ Mbuf, LDLStatus* st, double tol) {
+  __shared__ __attribute__((aligned(16))) double sm[DIAG_LDS];
+  int s, item;
+  task_of(list, s, item);
+  (void)item;
+  diag_body<false>(T, s, step, arena, D, Mbuf + (int64_t)T.bigslot[s] * 4096, st, tol, sm);
 }
 
 // Rows below the diagonal block of panel `step` (64-row tiles; wave w owns 16 rows): blocked
@@ -2647,7 +2661,7 @@ __global__ __launch_bounds__(NT) void k_big_trsm(FrontTab T, const int32_t* __re
 // clamped addresses) while the current chunk's MFMAs run.
 constexpr int UPD_LDT = 80;  // [k][row] layout: conflict-free ds_read_b64 for the 16x4 operand pattern
 constexpr int UPD_LDS = 2 * 64 * UPD_LDT;
-// Mnext: where the lookahead diagonal block's M_K blocks go (the front's Mbuf slot; k_big_chain: the
+// Mnext: where the lookahead diagonal block's M_K blocks go (the front's Mbuf slot; k_big_dag: the
 // next panel's slot)
 template <bool SC>
 __device__ __forceinline__ void update_body(const FrontTab& T, int s, int step, int kpan, int tij,
@@ -2744,7 +2758,8 @@ __device__ __forceinline__ void update_body(const FrontTab& T, int s, int step, 
       }
   // lookahead: task (0, 0) of a local update holds the next panel's diagonal tile, final now (the
   // panel's last local update; the next panel lies inside the group, below jlim)
-  if (!trailing && ti == 0 && tj == 0 && big_next_diag(T, s, step)) {
+  // (trailing mode, k_big_dag's tiles next to the group: only when the group is full, c0 = its end)
+  if (ti == 0 && tj == 0 && (!trailing || 64 * (step + 1) == c0) && big_next_diag(T, s, step)) {
     double* A64 = Wt;  // the operand tiles are free: aliased by the diagonal block, M_K and pivots
     double* Ms = Lt;
     double* Dl = Lt + 4 * 16 * LDM;
@@ -2774,80 +2789,6 @@ __global__ __launch_bounds__(NT) void k_big_update(FrontTab T, const int32_t* __
   int s, tij;
   task_of(list, s, tij);
   update_body<false>(T, s, step, kpan, tij, arena, D, Mbuf + (int64_t)T.bigslot[s] * 4096, st, tol, WLt);
-}
-
-// One panel group of the level's big fronts in ONE launch (r6): the group's k_big_trsm tiles and
-// local k_big_update tiles (steps g0 .. g0 + kpan - 1 of every front) as tasks of a dependency-driven
-// persistent kernel instead of one launch per step and kind (neos: 337 launches per factorisation, each
-// boundary a ~4.6 us gap, and the panel chain diag -> trsm -> update serialised by them).  Tasks are in
-// topological order (a step's trsm tiles, then its updates, then the next step); a workgroup takes the
-// next ticket, polls the flags of its <= 3 dependencies, runs the task and publishes its flag:
-//   trsm (s, p, rt):     the diagonal block of panel p (the update task (s, p - 1, 0, 0) factorised it)
-//                        and the row tile's panel-p block after its last local update (s, p - 1, rt + 1, 0);
-//   update (s, p, i, j): the trsm tiles (s, p, i) and (s, p, j) (its L_I and L_J rows) and the tile's
-//                        previous update (s, p - 1, i + 1, j + 1);
-// (for p = g0 every input was written by earlier launches).  A workgroup only waits for lower tickets,
-// taken by running workgroups: no deadlock whatever the residency.  Every handed-off value is stored
-// write-through (sc1) and drained before the flag; every load of one is sc1.  Each panel's M_K blocks go
-// to a slot of their own (Mch, per front and panel): a later diagonal block never overwrites the one a
-// slow trsm task of the previous panel still reads.  Same operands and MFMA order as the per-step
-// kernels: the same factor bit for bit.
-struct ChainTask {
-  int32_t s, step, item, kind;  // kind 0: trsm (item = row tile), 1: local update (item = ti | tj << 16)
-};
-__global__ __launch_bounds__(NT, 2) void k_big_chain(FrontTab T, const ChainTask* __restrict__ tasks, const int4* __restrict__ deps,
-                                                  int ntask, int32_t* flags, int epoch, int32_t* counter, int kpan,
-                                                  double* __restrict__ arena, double* __restrict__ D,
-                                                  const double* __restrict__ Mbuf, double* __restrict__ Mch,
-                                                  const int64_t* __restrict__ mslot, LDLStatus* st, double tol,
-                                                  int32_t* err) {
-  // 80 KB: two workgroups per CU (the ticket word borrows the first double: read before any task uses it)
-  __shared__ __attribute__((aligned(16))) double sm[UPD_LDS > TRSM_LDS ? UPD_LDS : TRSM_LDS];
-  int* s_t = reinterpret_cast<int*>(sm);
-  const int tid = threadIdx.x, lane = tid & 63;
-  for (;;) {
-    __syncthreads();  // the previous task's LDS reads
-    if (tid == 0) *s_t = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const int t = *s_t;
-    __syncthreads();  // every wave has the ticket before a task overwrites the word
-    if (t >= ntask) break;
-    const ChainTask tk = tasks[t];
-    if (tid < 64) {
-      const int4 dp = deps[t];
-      const int d = lane == 0 ? dp.x : lane == 1 ? dp.y : lane == 2 ? dp.z : -1;
-      int spins = 0;
-      for (;;) {
-        const bool ok = d < 0 || __hip_atomic_load(flags + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
-        if (__all(ok)) break;
-        __builtin_amdgcn_s_sleep(1);
-        ++spins;
-        // bounded: a lost hand-off raises the sticky error, and once raised no later wait spins
-        // (the launch drains in milliseconds, the factor is reported invalid)
-        if (spins > (1 << 25) ||
-            ((spins & 1023) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-          if (lane == 0) atomicOr(err, kErrHandoff);
-          break;
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only (sc1 loads follow)
-    }
-    __syncthreads();
-    const int g0 = (tk.step / kpan) * kpan;
-    if (tk.kind == 0) {
-      const double* M = tk.step == g0 ? Mbuf + (int64_t)T.bigslot[tk.s] * 4096 : Mch + (mslot[tk.s] + tk.step) * BIG_MSZ;
-      trsm_body<true>(T, tk.s, tk.step, tk.item, arena, D, M, sm);
-    } else {
-      update_body<true>(T, tk.s, tk.step, kpan, tk.item, arena, D, Mch + (mslot[tk.s] + tk.step + 1) * BIG_MSZ, st, tol, sm);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's sc1 stores drained
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store(flags + t, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (tid == 0 && atomicAdd(counter + 1, 1) == (int)gridDim.x - 1) {  // last one out: reset the tickets
-    counter[0] = 0;
-    counter[1] = 0;
-  }
 }
 
 // (pos, neg, zero) of D over the columns with colmask == want (colmask NULL: all)
@@ -3036,16 +2977,75 @@ __global__ __launch_bounds__(NT, SYRK_WAVES) void k_lb_syrk(const double* __rest
 // product write-through (psum), and the last part to take the tile's ticket sums the partials in part
 // order (fixed: bitwise reproducible), then runs the epilogue (and the lookahead of tile (0, 0)).
 constexpr int UPD_PART = 4 * 4 * 4 * NT;  // partial product doubles of one part (acc of every thread)
+constexpr int U128_LDS = 4 * SYK * SYLD;   // As[2] then Bs[2]
+// acc[a][b] += sum_{k in [k0, k1)} (L D)[I0 + rows, k] L[J0 + cols, k] on a 128 x 128 tile of front F (ld r):
+// four waves x 64 x 64 quadrants of f64 MFMA 16x16x4, K-chunks of 16 double-buffered through LDS (AB)
+template <bool SC>
+__device__ __forceinline__ void upd128_gemm(const double* __restrict__ F, const double* __restrict__ D, int f0, int r,
+                                            int I0, int J0, int k0, int k1, double* AB, dbl4 (&acc)[4][4]) {
+  double (*As)[SYK * SYLD] = reinterpret_cast<double (*)[SYK * SYLD]>(AB);           // (L D)[I rows]
+  double (*Bs)[SYK * SYLD] = reinterpret_cast<double (*)[SYK * SYLD]>(AB + 2 * SYK * SYLD);  // L[J rows]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wm = (wv >> 1) * 64, wn = (wv & 1) * 64;
+  const int lr = tid & (SYT - 1), lk = tid >> 7;
+  double ra[8], rb[8], rd[8];
+  const int ri = min(I0 + lr, r - 1), rj = min(J0 + lr, r - 1);
+  auto gload = [&](int kb) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int kc = min(kb + lk + 2 * q, k1 - 1);
+      const int64_t col = (int64_t)kc * r;
+      ra[q] = ldF<SC>(F + ri + col);
+      rb[q] = ldF<SC>(F + rj + col);
+      rd[q] = ldF<SC>(D + f0 + kc);
+    }
+  };
+  auto sstore = [&](int kb, int buf) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const bool ok = kb + lk + 2 * q < k1;
+      As[buf][(lk + 2 * q) * SYLD + lr] = (ok && I0 + lr < r) ? ra[q] * rd[q] : 0.0;
+      Bs[buf][(lk + 2 * q) * SYLD + lr] = (ok && J0 + lr < r) ? rb[q] : 0.0;
+    }
+  };
+  if (k0 >= k1) return;  // (a split part past the group's K has nothing to multiply)
+  gload(k0);
+  sstore(k0, 0);
+  __syncthreads();
+  int buf = 0;
+  for (int kb = k0; kb < k1; kb += SYK) {
+    const bool more = kb + SYK < k1;
+    if (more) gload(kb + SYK);
+#pragma unroll
+    for (int k4 = 0; k4 < SYK / 4; ++k4) {
+      const int kk = 4 * k4 + (lane >> 4);
+      double fa[4], fb[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        fa[t] = Bs[buf][kk * SYLD + wn + 16 * t + (lane & 15)];
+        fb[t] = As[buf][kk * SYLD + wm + 16 * t + (lane & 15)];
+      }
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[a], fb[b], acc[a][b], 0, 0, 0);
+    }
+    if (more) {
+      sstore(kb + SYK, buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+}
+
 __global__ __launch_bounds__(NT, 2) void k_big_upd128(FrontTab T, const int32_t* __restrict__ list, int step, int kpan,
                                                      double* __restrict__ arena, double* __restrict__ D,
                                                      double* __restrict__ Mbuf, LDLStatus* st, double tol,
                                                      int nsplit, double* __restrict__ psum, int32_t* ptick) {
   // one buffer: As[2] then Bs[2]; after the MFMAs task (0, 0) reuses it for the lookahead diagonal block
-  __shared__ __attribute__((aligned(16))) double AB[4 * SYK * SYLD];
+  __shared__ __attribute__((aligned(16))) double AB[U128_LDS];
   __shared__ int s_last;
-  double (*As)[SYK * SYLD] = reinterpret_cast<double (*)[SYK * SYLD]>(AB);           // (L D)[I rows]
-  double (*Bs)[SYK * SYLD] = reinterpret_cast<double (*)[SYK * SYLD]>(AB + 2 * SYK * SYLD);  // L[J rows]
-  static_assert(64 * LDA + 4 * 16 * LDM + 64 <= 4 * SYK * SYLD, "lookahead diagonal block aliases As / Bs");
+  static_assert(64 * LDA + 4 * 16 * LDM + 64 <= U128_LDS, "lookahead diagonal block aliases As / Bs");
   const int tile = blockIdx.x / nsplit, part = blockIdx.x - tile * nsplit;
   const int2 task = reinterpret_cast<const int2*>(list)[tile];
   const int s = task.x, tij = task.y;
@@ -3060,61 +3060,12 @@ __global__ __launch_bounds__(NT, 2) void k_big_upd128(FrontTab T, const int32_t*
   double* __restrict__ F = arena + T.l_off[s];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wm = (wv >> 1) * 64, wn = (wv & 1) * 64;
-  const int lr = tid & (SYT - 1), lk = tid >> 7;
   dbl4 acc[4][4];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
-  double ra[8], rb[8], rd[8];
-  const int ri = min(I0 + lr, r - 1), rj = min(J0 + lr, r - 1);
-  auto gload = [&](int kb) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int kc = min(kb + lk + 2 * q, k1 - 1);
-      const int64_t col = (int64_t)kc * r;
-      ra[q] = F[ri + col];
-      rb[q] = F[rj + col];
-      rd[q] = D[f0 + kc];
-    }
-  };
-  auto sstore = [&](int kb, int buf) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const bool ok = kb + lk + 2 * q < k1;
-      As[buf][(lk + 2 * q) * SYLD + lr] = (ok && I0 + lr < r) ? ra[q] * rd[q] : 0.0;
-      Bs[buf][(lk + 2 * q) * SYLD + lr] = (ok && J0 + lr < r) ? rb[q] : 0.0;
-    }
-  };
-  if (k0 < k1) {  // (a split part past the group's K has nothing to multiply)
-    gload(k0);
-    sstore(k0, 0);
-    __syncthreads();
-    int buf = 0;
-    for (int kb = k0; kb < k1; kb += SYK) {
-      const bool more = kb + SYK < k1;
-      if (more) gload(kb + SYK);
-#pragma unroll
-      for (int k4 = 0; k4 < SYK / 4; ++k4) {
-        const int kk = 4 * k4 + (lane >> 4);
-        double fa[4], fb[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          fa[t] = Bs[buf][kk * SYLD + wn + 16 * t + (lane & 15)];
-          fb[t] = As[buf][kk * SYLD + wm + 16 * t + (lane & 15)];
-        }
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-          for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[a], fb[b], acc[a][b], 0, 0, 0);
-      }
-      if (more) {
-        sstore(kb + SYK, buf ^ 1);
-        __syncthreads();
-        buf ^= 1;
-      }
-    }
-  }
+  upd128_gemm<false>(F, D, f0, r, I0, J0, k0, k1, AB, acc);
   if (nsplit > 1) {  // the tile's parts: partials write-through, the last part sums them in part order
     double* __restrict__ mine = psum + ((int64_t)tile * nsplit + part) * UPD_PART;
 #pragma unroll
@@ -3197,6 +3148,143 @@ __global__ __launch_bounds__(NT, 2) void k_big_upd128(FrontTab T, const int32_t*
     }
     __syncthreads();
     big_diag_tail(T, s, step + 1, A64, Ms, Dl, arena, D, Mbuf + (int64_t)T.bigslot[s] * 4096, st, tol);
+  }
+}
+
+// All big fronts of a level in ONE launch (r6): their 64-column panels' diagonal blocks, trsm tiles,
+// local updates and trailing updates as tasks of a dependency-driven persistent kernel, instead of a
+// k_big_diag / k_big_trsm / k_big_update / k_big_upd128 launch per panel step and kind (neos: ~400
+// launches per factorisation, each boundary a ~4.6 us gap, and the panel chain diag -> trsm -> update
+// serialised by them).  Per panel group G (kpan panels, columns [64 g0, gend)):
+//   chain(G):  trsm tiles (kind 0) and local updates inside the group (kind 1, as k_big_update mode 0;
+//              task (0, 0) factorises the next panel's diagonal block);
+//   feed(G):   the trailing update of the next group's columns [gend, gend + 64 kpan), 64 x 64 tiles with
+//              K = the group (kind 1, k_big_update's trailing mode; tile (0, 0) factorises the next
+//              group's first diagonal block);
+//   bulk(G):   the rest of the trailing matrix, 128 x 128 tiles (kind 2, k_big_upd128's engine, K unsplit).
+// Tickets run chain(0) feed(0) chain(1) bulk(0) feed(1) chain(2) bulk(1) ... : the next group's panel
+// chain only needs the feed tiles, so it runs while the previous group's bulk update occupies the chip.
+// A task's dependencies (host-built, LDLSolver::build_schedules) are the last earlier writers of every
+// 64 x 64 block of the front it reads or read-modify-writes: all earlier tickets (a workgroup waits only
+// for tickets taken by running workgroups: no deadlock whatever the residency).  Every handed-off value
+// is stored write-through (sc1) and drained before the task's flag, every load of one is sc1; each
+// panel's M_K blocks go to a slot of their own (Mch, per front and panel).  Same operands and MFMA order
+// as the per-step kernels with K unsplit (MADIPM_UPD_SPLIT=0): the same factor bit for bit.
+// the task bodies as calls (one register allocation per body, not the union of four inlined ones)
+__device__ __attribute__((noinline)) void dag_trsm(const FrontTab& T, int s, int step, int rt, double* arena,
+                                                   const double* D, const double* M, double* sm) {
+  trsm_body<true>(T, s, step, rt, arena, D, M, sm);
+}
+__device__ __attribute__((noinline)) void dag_update(const FrontTab& T, int s, int step, int kpan, int tij, double* arena,
+                                                     double* D, double* Mnext, LDLStatus* st, double tol, double* sm) {
+  update_body<true>(T, s, step, kpan, tij, arena, D, Mnext, st, tol, sm);
+}
+__device__ __attribute__((noinline)) void dag_diag(const FrontTab& T, int s, double* arena, double* D, double* M,
+                                                   LDLStatus* st, double tol, double* sm) {
+  diag_body<true>(T, s, 0, arena, D, M, st, tol, sm);
+}
+__device__ __attribute__((noinline)) void dag_bulk(const FrontTab& T, int s, int step, int kpan, int item, double* arena,
+                                                   const double* D, double* sm) {
+  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+  const int g0 = (step / kpan) * kpan, gend = min(64 * (g0 + kpan), w), cb = gend + 64 * kpan;
+  const int I0 = cb + 128 * (item & 0xffff), J0 = cb + 128 * ((item >> 16) & 0x7fff);
+  double* __restrict__ F = arena + T.l_off[s];
+  const int tid = threadIdx.x, lane = tid & 63;
+  dbl4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+  upd128_gemm<true>(F, D, f0, r, I0, J0, 64 * g0, gend, sm, acc);
+  const int wv = tid >> 6, wm = (wv >> 1) * 64, wn = (wv & 1) * 64;
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    double fv[4][4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int i = min(I0 + wm + 16 * b + (lane & 15), r - 1), j = min(J0 + wn + 16 * a + (lane >> 4) + 4 * g, r - 1);
+        fv[b][g] = ldF<true>(F + i + (int64_t)j * r);
+      }
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int i = I0 + wm + 16 * b + (lane & 15), j = J0 + wn + 16 * a + (lane >> 4) + 4 * g;
+        if (i < r && j <= i) stF<true>(F + i + (int64_t)j * r, fv[b][g] - acc[a][b][g]);
+      }
+  }
+}
+
+struct DagTask {
+  int32_t s, step, item, kind;  // 0 trsm (item: row tile), 1 64-tile update (ti | tj << 16, bit 31: trailing),
+                                // 2 128-tile trailing update (I | J << 16), 3 first diagonal block
+};
+constexpr int DAG_LDS = UPD_LDS > TRSM_LDS ? (UPD_LDS > U128_LDS ? UPD_LDS : U128_LDS) : (TRSM_LDS > U128_LDS ? TRSM_LDS : U128_LDS);
+static_assert(DAG_LDS * 8 <= 80 * 1024 && DIAG_LDS <= DAG_LDS, "two k_big_dag workgroups per CU");
+__global__ __launch_bounds__(NT, 2) void k_big_dag(FrontTab T, const DagTask* __restrict__ tasks, const int32_t* __restrict__ dptr,
+                                                   const int32_t* __restrict__ dlist, int ntask, int32_t* flags, int epoch,
+                                                   int32_t* counter, int kpan, double* __restrict__ arena,
+                                                   double* __restrict__ D, double* __restrict__ Mch,
+                                                   const int64_t* __restrict__ mslot, LDLStatus* st, double tol,
+                                                   int32_t* err, int64_t* dbg) {
+  // 80 KB: two workgroups per CU (the ticket word borrows the first double: read before any task uses it)
+  __shared__ __attribute__((aligned(16))) double sm[DAG_LDS];
+  int* s_t = reinterpret_cast<int*>(sm);
+  const int tid = threadIdx.x, lane = tid & 63;
+  for (;;) {
+    __syncthreads();  // the previous task's LDS reads
+    if (tid == 0) *s_t = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int t = *s_t;
+    __syncthreads();  // every wave has the ticket before a task overwrites the word
+    if (t >= ntask) break;
+    const DagTask tk = tasks[t];
+    if (dbg && tid == 0) dbg[4 * t] = wall_clock64();
+    if (tid < 64) {  // wave 0 polls the dependencies' flags, 64 at a time
+      const int q0 = dptr[t], q1 = dptr[t + 1];
+      for (int q = q0; q < q1; q += 64) {
+        const int d = q + lane < q1 ? dlist[q + lane] : -1;
+        int spins = 0;
+        for (;;) {
+          const bool ok = d < 0 || __hip_atomic_load(flags + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+          if (__all(ok)) break;
+          __builtin_amdgcn_s_sleep(1);
+          ++spins;
+          // bounded: a lost hand-off raises the sticky error, and once raised no later wait spins
+          // (the launch drains in milliseconds, the factor is reported invalid)
+          if (spins > (1 << 25) ||
+              ((spins & 1023) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+            if (lane == 0) atomicOr(err, kErrHandoff);
+            break;
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only (sc1 loads follow)
+    }
+    __syncthreads();
+    if (dbg && tid == 0) dbg[4 * t + 1] = wall_clock64();
+    double* Mp = Mch + mslot[tk.s] * BIG_MSZ;  // the front's per-panel M_K slots
+    if (tk.kind == 0)
+      dag_trsm(T, tk.s, tk.step, tk.item, arena, D, Mp + (int64_t)tk.step * BIG_MSZ, sm);
+    else if (tk.kind == 1)
+      dag_update(T, tk.s, tk.step, kpan, tk.item, arena, D, Mp + (int64_t)(tk.step + 1) * BIG_MSZ, st, tol, sm);
+    else if (tk.kind == 3)
+      dag_diag(T, tk.s, arena, D, Mp, st, tol, sm);
+    else  // 128 x 128 trailing tile, columns past the feed tiles: rows / columns cb + 128 (I, J)
+      dag_bulk(T, tk.s, tk.step, kpan, tk.item, arena, D, sm);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's sc1 stores drained
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(flags + t, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (dbg && tid == 0) {
+      dbg[4 * t + 2] = wall_clock64();
+      dbg[4 * t + 3] = blockIdx.x;
+    }
+  }
+  if (tid == 0 && atomicAdd(counter + 1, 1) == (int)gridDim.x - 1) {  // last one out: reset the tickets
+    counter[0] = 0;
+    counter[1] = 0;
   }
 }
 
@@ -4803,8 +4891,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     big_kpan_ = ek ? std::max(1, std::min(8, std::atoi(ek))) : 4;
     const char* es = std::getenv("MADIPM_UPD_SPLIT");  // A/B: 0 = one workgroup per k_big_upd128 tile
     upd_split_ = !(es && es[0] == '0');
-    const char* ec = std::getenv("MADIPM_BIG_CHAIN");  // A/B: 0 = one launch per panel step and kind
-    big_chain_ = !(ec && ec[0] == '0');
+    const char* ec = std::getenv("MADIPM_BIG_DAG");  // A/B: 0 = one launch per panel step and kind
+    big_dag_ = !(ec && ec[0] == '0');
     // persistent workgroups of the big-front solve kernels (2 per CU; MADIPM_BIG_SOLVE_WG for A/B)
     if (const char* eg = std::getenv("MADIPM_BIG_SOLVE_WG")) big_solve_wg_ = std::max(64, std::atoi(eg));
     // pipelined in-LDS factorisation schedule (1, default); 0 = the barrier schedule, bitwise the same
@@ -5348,12 +5436,13 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     L.bytes = 8.0 * (double)G.m * G.n + 16.0 * (double)G.m * (G.m + 1) / 2.0 * cdiv(G.n, LB_KCHUNK);
     out.push_back(L);
   };
-  // The big fronts of a level, panel group by panel group (k_big_chain): step 0's diagonal blocks
-  // (k_big_diag), then per group ONE chain launch (the group's trsm tiles and local updates, every
-  // front) and ONE k_big_upd128 launch (the trailing update of every front whose group ends there: its
-  // task (0, 0) factorises the next group's first diagonal block), and after group 0 the fused fronts'
-  // k_asm_update.  The same tiles, operands and order of sums as the per-step launches below.
-  std::vector<int32_t> ctask, cdep;  // chain tasks (s, step, item, kind) and their deps (4 per task)
+  // The big fronts of a level in one k_big_dag launch: tasks in ticket order DIAG(0) | chain(0) feed(0) |
+  // chain(1) bulk(0) feed(1) | chain(2) bulk(1) feed(2) | ... | bulk(last) (k_big_dag's comment), every
+  // front of the level interleaved; each task's dependencies are the last earlier writers of the 64 x 64
+  // blocks of its front that it reads or read-modify-writes (every writer also reads what it writes, so
+  // the last writer stands for all earlier ones).  Then the fused fronts' k_asm_update.  The same tiles,
+  // operands and order of sums as the per-step launches with K unsplit.
+  std::vector<int32_t> dtask, ddptr{0}, ddlist;  // DagTask words, CSR of dependencies (launch-local tickets)
   std::vector<int64_t> mslot(std::max(S.nsuper, 1), 0);
   int64_t nmslot = 0;
   for (int f = 0; f < S.nsuper; ++f)
@@ -5361,32 +5450,99 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       mslot[f] = nmslot;
       nmslot += cdiv(S.first[f + 1] - S.first[f], 64) + 1;
     }
-  auto chain_level = [&](const std::vector<int32_t>& big, int lev, int phase, std::vector<Launch>& out) {
+  auto dag_level = [&](const std::vector<int32_t>& big, int lev, int phase, std::vector<Launch>& out) {
+    const int kp = big_kpan_;
+    Launch L{BIG_DAG, 0, (int64_t)(dtask.size() / 4), 0, 0};
+    // per front, the live written rectangles bucketed by the 64 x 64 blocks they touch: a task depends on
+    // every live rectangle its reads or read-modify-writes intersect; a write drops the rectangles (per
+    // block) it covers — it depends on them, so it stands for them — and adds its own
+    struct Ent {
+      int r0, r1, c0, c1, w;
+    };
+    std::map<int, std::vector<std::vector<Ent>>> live;
+    std::vector<int32_t> deps;
+    std::vector<Ent> wr;
+    std::vector<int> wrs;
+    auto region = [&](int s, int r0, int r1, int c0, int c1, bool write) {
+      const int nb = (int)cdiv(S.nrows[s], 64);
+      auto& g = live[s];
+      if (g.empty()) g.resize((size_t)nb * nb);
+      r1 = std::min(r1, S.nrows[s]);
+      c1 = std::min(c1, S.nrows[s]);
+      if (r0 >= r1 || c0 >= c1) return;
+      for (int R = r0 >> 6; R <= (r1 - 1) >> 6; ++R)
+        for (int C = c0 >> 6; C <= std::min((c1 - 1) >> 6, R); ++C)
+          for (const Ent& e : g[(size_t)R * nb + C])
+            if (e.r0 < r1 && r0 < e.r1 && e.c0 < c1 && c0 < e.c1) deps.push_back(e.w);
+      if (write) {
+        wr.push_back(Ent{r0, r1, c0, c1, -1});
+        wrs.push_back(s);
+      }
+    };
+    auto emit = [&](int s, int step, int item, int kind) {
+      const int t = (int)L.items++;
+      std::sort(deps.begin(), deps.end());
+      deps.erase(std::unique(deps.begin(), deps.end()), deps.end());
+      for (int d : deps) ddlist.push_back(d);
+      ddptr.push_back((int32_t)ddlist.size());
+      for (size_t k = 0; k < wr.size(); ++k) {
+        const Ent q{wr[k].r0, wr[k].r1, wr[k].c0, wr[k].c1, t};
+        const int f = wrs[k], nb = (int)cdiv(S.nrows[f], 64);
+        auto& g = live[f];
+        for (int R = q.r0 >> 6; R <= (q.r1 - 1) >> 6; ++R)
+          for (int C = q.c0 >> 6; C <= std::min((q.c1 - 1) >> 6, R); ++C) {
+            auto& cell = g[(size_t)R * nb + C];
+            const int br0 = R * 64, br1 = br0 + 64, bc0 = C * 64, bc1 = bc0 + 64;
+            cell.erase(std::remove_if(cell.begin(), cell.end(), [&](const Ent& e) {
+                         const int a0 = std::max(e.r0, br0), a1 = std::min(e.r1, br1);
+                         const int b0 = std::max(e.c0, bc0), b1 = std::min(e.c1, bc1);
+                         return a0 >= q.r0 && a1 <= q.r1 && b0 >= q.c0 && b1 <= q.c1;  // covered here
+                       }),
+                       cell.end());
+            cell.push_back(q);
+          }
+      }
+      deps.clear();
+      wr.clear();
+      wrs.clear();
+      dtask.insert(dtask.end(), {s, step, item, kind});
+    };
     int maxsteps = 0;
     for (int s : big) maxsteps = std::max<int>(maxsteps, (int)cdiv(S.first[s + 1] - S.first[s], 64));
-    const int kp = big_kpan_;
-    double pend_alg = 0.0;  // 8(d) bytes of panels whose launch carried nothing (added to the next launch)
-    for (int g0 = 0; g0 < maxsteps; g0 += kp) {
-      if (g0 == 0) {  // the first diagonal blocks
-        align2();
-        Launch L{BIG_DIAG, 0, (int64_t)sched.size(), 0, 0};
-        for (int s : big) {
-          const int w = S.first[s + 1] - S.first[s];
-          const double dk = std::min(64, w);
-          sched.insert(sched.end(), {s, 0});
-          L.items++;
-          L.bytes += 8.0 * (dk * (dk + 1) + 4 * 16 * 17);
-          L.flops += dk * dk * dk / 3.0;
-          L.alg += fact_alg_cols(S.first[s], S.first[s] + (int)dk);
-        }
-        out.push_back(L);
+    // first diagonal blocks
+    for (int s : big) {
+      const int w = S.first[s + 1] - S.first[s], kw = std::min(64, w);
+      region(s, 0, kw, 0, kw, true);
+      emit(s, 0, 0, 3);
+      L.bytes += 8.0 * (kw * (kw + 1.0) + 4 * 16 * 17);
+      L.flops += (double)kw * kw * kw / 3.0;
+    }
+    for (int s : big) L.alg += fact_alg(s);  // every column of the level's big fronts
+    auto bulk = [&](int g0) {  // 128 x 128 trailing tiles of group [g0, g0 + kp), columns past the feed tiles
+      for (int s : big) {
+        const int w = S.first[s + 1] - S.first[s], r = S.nrows[s];
+        if ((int)cdiv(w, 64) <= g0 || S.fused[s]) continue;
+        const int gend = std::min(64 * (g0 + kp), w), cb = gend + 64 * kp;
+        if (cb >= r) continue;
+        const int nt = (int)cdiv(r - cb, 128);
+        const double K = gend - 64 * g0, nbt = r - cb;
+        L.bytes += 8.0 * (nbt * (nbt + 1) + 2.0 * nbt * K);
+        L.flops += K * nbt * (nbt + 1);
+        // column by column: the first columns feed the next group's feed tiles (and its bulk's first
+        // columns), so their tickets come first and are done by the time those wait for them
+        for (int J = 0; J < nt; ++J)
+          for (int I = J; I < nt; ++I) {
+            const int i0 = cb + 128 * I, j0 = cb + 128 * J;
+            region(s, i0, i0 + 128, 64 * g0, gend, false);  // (L D)_I and L_J: the group's panels
+            region(s, j0, j0 + 128, 64 * g0, gend, false);
+            region(s, i0, i0 + 128, j0, j0 + 128, true);
+            emit(s, g0 + kp - 1, I | (J << 16), 2);
+          }
       }
-      // the chain: per step, every front's trsm tiles, then its local updates
-      Launch C{BIG_CHAIN, g0, (int64_t)(ctask.size() / 4), 0, 0};
-      C.alg = pend_alg;
-      pend_alg = 0.0;
-      std::map<std::tuple<int, int, int, int, int>, int> tix;  // (kind, s, p, i, j) -> launch-local ticket
-      for (int p = g0; p < std::min(g0 + kp, maxsteps); ++p) {
+    };
+    for (int g0 = 0; g0 < maxsteps; g0 += kp) {
+      // chain: per step, every front's trsm tiles, then its local updates
+      for (int p = g0; p < std::min(g0 + kp, maxsteps); ++p)
         for (int kind = 0; kind < 2; ++kind)
           for (int s : big) {
             const int w = S.first[s + 1] - S.first[s], r = S.nrows[s];
@@ -5395,104 +5551,73 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
             const int k0 = p * 64, kw = std::min(64, w - k0);
             const int nt = (int)cdiv(r - k0 - kw, 64);
             const double dk = kw, nb = r - k0 - kw;
-            const int gl = std::min(g0 + kp, npan) - 1;
-            const int gend = std::min(64 * (gl + 1), w);
+            const int gl = std::min(g0 + kp, npan) - 1, gend = std::min(64 * (gl + 1), w);
             if (kind == 0) {
-              if (p > 0) C.alg += fact_alg_cols(S.first[s] + k0, S.first[s] + k0 + kw);
-              C.bytes += 8.0 * (2.0 * nb * dk + nt * (dk * (dk + 1) / 2 + 4 * 16 * 17));
-              C.flops += nb * dk * dk;
+              L.bytes += 8.0 * (2.0 * nb * dk + nt * (dk * (dk + 1) / 2 + 4 * 16 * 17));
+              L.flops += nb * dk * dk;
               for (int rt = 0; rt < nt; ++rt) {
-                const int t = (int)C.items++;
-                tix[{0, s, p, rt, 0}] = t;
-                ctask.insert(ctask.end(), {s, p, rt, 0});
-                // the diagonal block (factorised by the previous step's update task (0, 0)) and the
-                // update tiles of the previous step that hold this tile's rows of panel p: tile rt + 1
-                // (full panel), tiles rt and rt + 1 (a partial last panel: rows from 64 p + kw)
-                int d0 = -1, d1 = -1, d2 = -1;
-                if (p > g0) {
-                  const int ntp = (int)cdiv(r - 64 * p, 64);  // the previous step's row tiles
-                  const int ia = (kw + 64 * rt) / 64, ib = std::min((kw + 64 * rt + 63) / 64, ntp - 1);
-                  d0 = tix.at({1, s, p - 1, 0, 0});
-                  d1 = tix.at({1, s, p - 1, ia, 0});
-                  d2 = ib != ia ? tix.at({1, s, p - 1, ib, 0}) : -1;
-                }
-                cdep.insert(cdep.end(), {d0, d1, d2, 0});
+                const int R0 = k0 + kw + 64 * rt;
+                region(s, k0, k0 + kw, k0, k0 + kw, false);  // L11, D, M_K
+                region(s, R0, R0 + 64, k0, k0 + kw, true);
+                emit(s, p, rt, 0);
               }
             } else {
               if (S.fused[s] || p >= gl) continue;
-              const double nc = gend - (k0 + kw);
-              C.bytes += 8.0 * (2.0 * nb * nc + nb * dk + nc * dk);
-              C.flops += 2.0 * dk * nc * (nb - 0.5 * nc);
+              const int c0 = k0 + 64;
+              const double nc = gend - c0;
+              L.bytes += 8.0 * (2.0 * nb * nc + nb * dk + nc * dk);
+              L.flops += 2.0 * dk * nc * (nb - 0.5 * nc);
               for (int j = 0; j < (int)cdiv((int)nc, 64); ++j)
                 for (int i = j; i < nt; ++i) {
-                  const int t = (int)C.items++;
-                  tix[{1, s, p, i, j}] = t;
-                  ctask.insert(ctask.end(), {s, p, i | (j << 16), 1});
-                  const int di = tix.at({0, s, p, i, 0}), dj = i != j ? tix.at({0, s, p, j, 0}) : -1;
-                  const int dp = p > g0 ? tix.at({1, s, p - 1, i + 1, j + 1}) : -1;
-                  cdep.insert(cdep.end(), {di, dj, dp, 0});
+                  region(s, c0 + 64 * i, c0 + 64 * i + 64, k0, k0 + 64, false);
+                  region(s, c0 + 64 * j, c0 + 64 * j + 64, k0, k0 + 64, false);
+                  region(s, c0 + 64 * i, c0 + 64 * i + 64, c0 + 64 * j, std::min(c0 + 64 * j + 64, gend), true);
+                  emit(s, p, i | (j << 16), 1);
                 }
             }
           }
-      }
-      if (C.items) {
-        out.push_back(C);
-      } else {
-        pend_alg += C.alg;
-      }
-      // the trailing updates of every front whose group ends here
-      align2();
-      Launch U{BIG_UPDATE128, g0 + kp - 1, (int64_t)sched.size(), 0, 0};
+      if (g0 > 0) bulk(g0 - kp);
+      // feed: the trailing update of the next group's columns, 64 x 64 tiles (k_big_update trailing mode)
       for (int s : big) {
         const int w = S.first[s + 1] - S.first[s], r = S.nrows[s];
-        const int npan = (int)cdiv(w, 64);
-        if (npan <= g0 || S.fused[s]) continue;
+        if ((int)cdiv(w, 64) <= g0 || S.fused[s]) continue;
         const int gend = std::min(64 * (g0 + kp), w);
-        const int c0 = gend, ntt = (int)cdiv(r - c0, 128);
-        const double K = gend - 64 * g0, nbt = r - c0;
-        for (int i = 0; i < ntt; ++i)
-          for (int j = 0; j <= i; ++j) {
-            sched.insert(sched.end(), {s, i | (j << 16)});
-            U.items++;
+        if (gend >= r) continue;
+        const int nt = (int)cdiv(r - gend, 64), ncb = std::min(kp, nt);
+        const double K = gend - 64 * g0, nbt = r - gend, nc = std::min(64.0 * kp, nbt);
+        L.bytes += 8.0 * (2.0 * nbt * nc + (nbt + nc) * K);
+        L.flops += 2.0 * K * nc * (nbt - 0.5 * nc);
+        for (int j = 0; j < ncb; ++j)
+          for (int i = j; i < nt; ++i) {
+            const int i0 = gend + 64 * i, j0 = gend + 64 * j;
+            region(s, i0, i0 + 64, 64 * g0, gend, false);
+            region(s, j0, j0 + 64, 64 * g0, gend, false);
+            region(s, i0, i0 + 64, j0, j0 + 64, true);
+            emit(s, g0 + kp - 1, (int)((uint32_t)i | ((uint32_t)j << 16) | 0x80000000u), 1);
           }
-        U.bytes += 8.0 * (nbt * (nbt + 1) + 2.0 * nbt * K);
-        U.flops += K * nbt * (nbt + 1);
-      }
-      if (U.items) {
-        U.nf = !upd_split_ ? 1 : U.items <= 128 ? 4 : U.items <= 170 ? 3 : U.items <= 256 ? 2 : 1;
-        U.alg = pend_alg;
-        pend_alg = 0.0;
-        out.push_back(U);
-      }
-      if (g0 == 0 && phase == 1 && S.atile_fz0[lev] < S.atile_lev[lev + 1]) {
-        // the fused fronts' trailing tiles: assembled + updated after their panel (one launch)
-        const int32_t t0 = S.atile_fz0[lev], t1 = S.atile_lev[lev + 1];
-        Launch L{ASM_UPDATE, 0, t0, 4, t1 - t0};
-        for (int32_t t = t0; t < t1; ++t) {
-          const SymbolicPlan::AsmTile& at = S.atiles[t];
-          const int f = at.front, r = S.nrows[f], w = S.first[f + 1] - S.first[f];
-          L.nf = std::max(L.nf, (w + 3) & ~3);
-          const int ti = at.tij & 0xffff, tj = (at.tij >> 16) & 0x7fff;
-          const double nr = std::min(64, r - 64 * ti), nc = std::min(64, r - 64 * tj);
-          L.bytes += 8.0 * (ti == tj ? nr * (nr + 1) / 2 : nr * nc) + (at.gptr >= 0 ? 4.0 * (S.g_ptr[at.gptr] + 2) : 0.0) +
-                     8.0 * (nr + nc) * w;
-          for (int k = at.bt0; k < at.bt1; ++k) {
-            const int32_t* e = &S.bt[5 * k];
-            for (int b = e[1]; b < e[2]; ++b) L.bytes += 8.0 * std::max(0, e[4] - std::max(b, e[3]));
-          }
-          L.flops += 2.0 * nr * nc * w;
-        }
-        L.alg = pend_alg;
-        pend_alg = 0.0;
-        out.push_back(L);
       }
     }
-    if (pend_alg > 0.0) {  // (a level whose last panels launched nothing: onto its last launch)
-      for (auto it = out.rbegin(); it != out.rend(); ++it)
-        if (it->kind == BIG_CHAIN || it->kind == BIG_UPDATE128 || it->kind == BIG_DIAG || it->kind == ASM_UPDATE) {
-          it->alg += pend_alg;
-          break;
+    bulk(((maxsteps - 1) / kp) * kp);
+    out.push_back(L);
+    if (phase == 1 && S.atile_fz0[lev] < S.atile_lev[lev + 1]) {
+      // the fused fronts' trailing tiles: assembled + updated after their panel (one launch)
+      const int32_t t0 = S.atile_fz0[lev], t1 = S.atile_lev[lev + 1];
+      Launch A{ASM_UPDATE, 0, t0, 4, t1 - t0};
+      for (int32_t t = t0; t < t1; ++t) {
+        const SymbolicPlan::AsmTile& at = S.atiles[t];
+        const int f = at.front, r = S.nrows[f], w = S.first[f + 1] - S.first[f];
+        A.nf = std::max(A.nf, (w + 3) & ~3);
+        const int ti = at.tij & 0xffff, tj = (at.tij >> 16) & 0x7fff;
+        const double nr = std::min(64, r - 64 * ti), nc = std::min(64, r - 64 * tj);
+        A.bytes += 8.0 * (ti == tj ? nr * (nr + 1) / 2 : nr * nc) + (at.gptr >= 0 ? 4.0 * (S.g_ptr[at.gptr] + 2) : 0.0) +
+                   8.0 * (nr + nc) * w;
+        for (int k = at.bt0; k < at.bt1; ++k) {
+          const int32_t* e = &S.bt[5 * k];
+          for (int b = e[1]; b < e[2]; ++b) A.bytes += 8.0 * std::max(0, e[4] - std::max(b, e[3]));
         }
+        A.flops += 2.0 * nr * nc * w;
+      }
+      out.push_back(A);
     }
   };
   auto build_fact = [&](int phase, std::vector<Launch>& out) {
@@ -5561,8 +5686,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
           sched.insert(sched.end(), cls[c].begin(), cls[c].end());
         }
       if (big.empty()) continue;
-      if (big_chain_) {
-        chain_level(big, lev, phase, out);
+      if (big_dag_) {
+        dag_level(big, lev, phase, out);
         continue;
       }
       int maxsteps = 0;
@@ -5662,19 +5787,25 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       if (S.top(S.lb[g].parent)) lb_syrk_launch((int)g, fact1_);
     build_fact(2, fact2_);
   }
-  if (!ctask.empty()) {  // chain tasks, dependencies, flags, counters, per-panel M_K slots
-    chain_tasks_.upload(ctask);
-    chain_deps_.upload(cdep);
-    chain_flags_.alloc((int64_t)ctask.size() / 4);
-    chain_flags_.zero();
-    chain_cnt_.alloc(2);
-    chain_cnt_.zero();
-    chain_m_.alloc(std::max<int64_t>(nmslot, 1) * BIG_MSZ);
-    chain_mslot_.upload(mslot);
+  if (!dtask.empty()) {  // DAG tasks, dependencies, flags, counters, per-panel M_K slots
+    dag_tasks_.upload(dtask);
+    dag_dptr_.upload(ddptr);
+    dag_dlist_.upload(ddlist.empty() ? std::vector<int32_t>{0} : ddlist);
+    dag_flags_.alloc((int64_t)dtask.size() / 4);
+    dag_flags_.zero();
+    dag_cnt_.alloc(2);
+    dag_cnt_.zero();
+    dag_m_.alloc(std::max<int64_t>(nmslot, 1) * BIG_MSZ);
+    dag_mslot_.upload(mslot);
     int dev = 0, ncu = 0;
     MADIPM_HIP(hipGetDevice(&dev));
     MADIPM_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    chain_grid_ = std::max(1, 2 * ncu);  // two workgroups per CU (80 KB of LDS, <= 256 registers)
+    dag_grid_ = std::max(1, 2 * ncu);  // two workgroups per CU (80 KB of LDS, <= 256 registers)
+    if (const char* ed = std::getenv("MADIPM_DAG_DEBUG"); ed && ed[0] == '1') {  // per-task stamps (diagnostics)
+      dag_dbg_.alloc((int64_t)dtask.size());
+      dag_dbg_.zero();
+      dag_kind_ = dtask;
+    }
   }
   {  // k_big_upd128's split-K scratch: partial products and per-tile tickets of the largest split launch
     int64_t np = 0, nt = 0;
@@ -6164,7 +6295,7 @@ double LDLSolver::solve_alg(int s) const {
 }
 
 void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStream_t s) {
-  ++cepoch_;  // k_big_chain's flags: this factorisation's epoch (never 0)
+  ++cepoch_;  // k_big_dag's flags: this factorisation's epoch (never 0)
   for (const Launch& L : LL) {
     const int32_t* list = sched_.p + L.off;
     switch (L.kind) {
@@ -6228,12 +6359,13 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
                           : k_asm_update<int64_t><<<(unsigned)L.items, ANT, 2 * L.nf * AU_LDT * 8 + 8 * kAsmLdsSrc, s>>>(
                                 T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, D_, L.nf, g_src_.p, Kx)));
         break;
-      case BIG_CHAIN:  // off = the launch's first task, items = its tasks
+      case BIG_DAG:  // off = the launch's first task (global index), items = its tasks
         TIMED(KK_TRSM, L.bytes, L.alg, L.flops,
-              (k_big_chain<<<(unsigned)std::min<int64_t>(L.items, chain_grid_), NT, 0, s>>>(
-                  T_, reinterpret_cast<const ChainTask*>(chain_tasks_.p) + L.off,
-                  reinterpret_cast<const int4*>(chain_deps_.p) + L.off, (int)L.items, chain_flags_.p + L.off, cepoch_,
-                  chain_cnt_.p, big_kpan_, arena_, D_, minv_, chain_m_, chain_mslot_, st_, pivot_tol, &st_->err)));
+              (k_big_dag<<<(unsigned)std::min<int64_t>(L.items, dag_grid_), NT, 0, s>>>(
+                  T_, reinterpret_cast<const DagTask*>(dag_tasks_.p) + L.off, dag_dptr_.p + L.off, dag_dlist_.p,
+                  (int)L.items, dag_flags_.p + L.off, cepoch_, dag_cnt_.p, big_kpan_, arena_, D_, dag_m_, dag_mslot_,
+                  st_, pivot_tol, &st_->err, dag_dbg_.p ? dag_dbg_.p + 4 * L.off : nullptr)));
+        if (dag_dbg_.p) dag_debug_dump(s, L);
         break;
       case BIG_UPDATE128:
         TIMED(KK_UPDATE, L.bytes, L.alg, L.flops,
@@ -6379,6 +6511,33 @@ int LDLSolver::status(hipStream_t s, bool sync) {
 
 // MADIPM_TREE_DEBUG=1: per-task wall-clock phases of the tree kernels (100 MHz counter), summarised
 // per level on stderr for the first few launches (diagnostics only)
+// MADIPM_DAG_DEBUG=1: per kind of k_big_dag task (trsm, 64-tile update, 128-tile update, diagonal
+// block) the tasks, their mean wait for dependencies and mean run time, and the launch's span and the
+// workgroup-time it kept busy / waiting (first few launches; 100 MHz clock)
+void LDLSolver::dag_debug_dump(hipStream_t s, const Launch& L) {
+  static int calls = 0;
+  if (++calls > 12) return;
+  MADIPM_HIP(hipStreamSynchronize(s));
+  std::vector<int64_t> h((size_t)4 * L.items);
+  MADIPM_HIP(hipMemcpy(h.data(), dag_dbg_.p + 4 * L.off, h.size() * 8, hipMemcpyDeviceToHost));
+  double n[4] = {0, 0, 0, 0}, wt[4] = {0, 0, 0, 0}, rt[4] = {0, 0, 0, 0};
+  int64_t t0 = INT64_MAX, t1 = 0;
+  for (int64_t t = 0; t < L.items; ++t) {
+    const int k = dag_kind_[4 * (L.off + t) + 3];
+    n[k] += 1;
+    wt[k] += (double)(h[4 * t + 1] - h[4 * t]);
+    rt[k] += (double)(h[4 * t + 2] - h[4 * t + 1]);
+    t0 = std::min(t0, h[4 * t]);
+    t1 = std::max(t1, h[4 * t + 2]);
+  }
+  const char* nm[4] = {"trsm", "upd64", "upd128", "diag"};
+  fprintf(stderr, "dag launch: %lld tasks, span %.1f us, wait %.1f / run %.1f WG-ms\n", (long long)L.items, (t1 - t0) / 100.0,
+          (wt[0] + wt[1] + wt[2] + wt[3]) / 1e5, (rt[0] + rt[1] + rt[2] + rt[3]) / 1e5);
+  for (int k = 0; k < 4; ++k)
+    if (n[k] > 0)
+      fprintf(stderr, "  %-7s %6.0f tasks  wait %7.2f us  run %7.2f us (mean)\n", nm[k], n[k], wt[k] / n[k] / 100.0, rt[k] / n[k] / 100.0);
+}
+
 void LDLSolver::tree_debug_dump(hipStream_t s, const char* what, const int64_t* dbuf, int nt, const char* p1,
                                 const char* p2, const char* p3, const char* p4, const char* p5, int stride) {
   static int ndump = 0;

@@ -283,7 +283,7 @@ class LDLSolver : public LinSolver {
  private:
   enum Kind { ASSEMBLE = 0, SMALL32 = 1, SMALL64 = 2, SMALL128 = 3, BIG_DIAG = 4, BIG_TRSM = 5, BIG_UPDATE = 6,
               LB_BUILD = 7, LB_SYRK = 8, MICRO = 9, SMALL192 = 10, FTREE = 11, BIG_UPDATE128 = 12,
-              ASM_UPDATE = 13, BIG_CHAIN = 14 };
+              ASM_UPDATE = 13, BIG_DAG = 14 };
   struct Launch {
     int kind;
     int step;       // panel step for BIG_DIAG / BIG_TRSM / BIG_UPDATE
@@ -374,15 +374,19 @@ class LDLSolver : public LinSolver {
   DBuf<uint16_t> sv_nt_;
   DBuf<int64_t> fdbg_, ab_first_, ab_loff_, fold_poff_, fold_row0_;
   int big_kpan_ = 4;  // big fronts: panels per deferred trailing-update group (MADIPM_BIG_KPAN)
-  bool big_chain_ = true;  // a panel group's trsm + local update tiles in one k_big_chain launch (MADIPM_BIG_CHAIN=0: per step)
-  DBuf<int32_t> chain_tasks_;  // ChainTask (4 int32) per task of every chain launch, in launch order
-  DBuf<int32_t> chain_deps_;   // int4 per task: the launch-local tickets it waits for (-1: none)
-  DBuf<int32_t> chain_flags_;  // per task: the epoch of the factorisation that completed it
-  DBuf<int32_t> chain_cnt_;    // ticket + done counters (reset by the last workgroup out)
-  DBuf<double> chain_m_;       // M_K blocks per (big front, panel)
-  DBuf<int64_t> chain_mslot_;  // per front: its first panel's slot in chain_m_
+  bool big_dag_ = true;  // a level's big fronts in one k_big_dag launch (MADIPM_BIG_DAG=0: per panel step and kind)
+  DBuf<int32_t> dag_tasks_;  // DagTask (4 int32) per task of every DAG launch, in launch order
+  DBuf<int32_t> dag_dptr_;   // per task: its first dependency in dag_dlist_ (launch-local tickets), + end
+  DBuf<int32_t> dag_dlist_;
+  DBuf<int32_t> dag_flags_;  // per task: the epoch of the factorisation that completed it
+  DBuf<int32_t> dag_cnt_;    // ticket + done counters (reset by the last workgroup out)
+  DBuf<double> dag_m_;       // M_K blocks per (big front, panel)
+  DBuf<int64_t> dag_mslot_;  // per front: its first panel's slot in dag_m_
   int cepoch_ = 0;
-  int chain_grid_ = 256;
+  int dag_grid_ = 256;
+  DBuf<int64_t> dag_dbg_;          // MADIPM_DAG_DEBUG: 4 stamps per task
+  std::vector<int32_t> dag_kind_;  // (its host copy of the task words)
+  void dag_debug_dump(hipStream_t s, const Launch& L);
   bool upd_split_ = true;  // k_big_upd128 split K on launches of few tiles (MADIPM_UPD_SPLIT=0: off)
   DBuf<double> upsum_;    // its partial products
   DBuf<int32_t> uptick_;  // its per-tile tickets (reset by each tile's last part)

@@ -442,14 +442,17 @@ def _dense_kkt(n, m, seed=11):
 
 
 @pytest.mark.parametrize("kpan", ["1", "2", "4"])
-@pytest.mark.parametrize("case", ["dense_320_100", "dense_130_200", "qp_dense_front", "neos_0.1"])
-def test_big_chain_bitwise(case, kpan, monkeypatch):
-    """k_big_chain (default, r6): a panel group's trsm and local-update tiles of every big front of a
-    level as dependency-ordered tasks of ONE persistent launch (sc1 hand-offs, per-panel M_K slots)
-    instead of one launch per step and kind (MADIPM_BIG_CHAIN=0).  Same operands and MFMA order: the
-    pivots and the solution agree BITWISE, and with the oracle (1e-12, well conditioned).  Dense K2s
-    with partial last panels (420 and 330 columns: rows of the last trsm straddle two update tiles),
-    a QP with a dense front, and the neos stand-in at 0.1 (many big fronts per level, fused fronts)."""
+@pytest.mark.parametrize("case", ["dense_320_100", "dense_130_200", "dense_700_60", "qp_dense_front", "neos_0.1"])
+def test_big_dag_bitwise(case, kpan, monkeypatch):
+    """k_big_dag (default, r6): every big front of a level in ONE persistent launch — first diagonal
+    blocks, trsm tiles, local updates, the next group's columns as 64 x 64 trailing tiles and the rest as
+    128 x 128 tiles — as dependency-ordered tasks (sc1 hand-offs, per-panel M_K slots, dependencies = the
+    earlier writers of every rectangle a task reads or rewrites) instead of one launch per panel step and
+    kind (MADIPM_BIG_DAG=0).  Same operands and MFMA order as the per-step launches with K unsplit
+    (MADIPM_UPD_SPLIT=0): the pivots and the solution agree BITWISE, and with the oracle (1e-12, well
+    conditioned).  Dense K2s with partial last panels and groups (420, 330 and 760 columns: misaligned
+    trsm rows, trailing tiles straddling the previous group's tiles), a QP with a dense front, and the
+    neos stand-in at 0.1 (many big fronts per level, fused fronts)."""
     from helpers import lp_k2
     monkeypatch.setenv("MADIPM_BIG_KPAN", kpan)
     if case.startswith("dense"):
@@ -465,9 +468,10 @@ def test_big_chain_bitwise(case, kpan, monkeypatch):
         K, Lw = lp_k2(standard_form_qp(I.neos5052403_standin(scale=0.1)), 2, well=True)
         sfm = 128
     out = {}
-    for chain in ("0", "1"):
-        monkeypatch.setenv("MADIPM_BIG_CHAIN", chain)
-        out[chain] = _factor_solve(K, Lw, sfm)
+    for dag in ("0", "1"):
+        monkeypatch.setenv("MADIPM_BIG_DAG", dag)
+        monkeypatch.setenv("MADIPM_UPD_SPLIT", "0")
+        out[dag] = _factor_solve(K, Lw, sfm)
     (d0, x0, ls0), (d1, x1, _) = out["0"], out["1"]
     assert ls0.info()["nbig"] >= 1
     bad = np.flatnonzero(d0.view(np.uint64) != d1.view(np.uint64))
