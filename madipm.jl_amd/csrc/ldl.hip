@@ -3266,6 +3266,12 @@ __global__ __launch_bounds__(NT, 2) void k_big_dag(FrontTab T, const DagTask* __
     __syncthreads();
     if (dbg && tid == 0) dbg[4 * t + 1] = wall_clock64();
     double* Mp = Mch + mslot[tk.s] * BIG_MSZ;  // the front's per-panel M_K slots
+    // the panel chain's tasks (latency-bound, on the critical path) issue ahead of a co-resident 128-tile
+    // update's waves (MFMA-bound, off it)
+    if (tk.kind == 2)
+      __builtin_amdgcn_s_setprio(0);
+    else
+      __builtin_amdgcn_s_setprio(2);
     if (tk.kind == 0)
       dag_trsm(T, tk.s, tk.step, tk.item, arena, D, Mp + (int64_t)tk.step * BIG_MSZ, sm);
     else if (tk.kind == 1)
@@ -5541,41 +5547,58 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       }
     };
     for (int g0 = 0; g0 < maxsteps; g0 += kp) {
-      // chain: per step, every front's trsm tiles, then its local updates
+      // chain, per step: the critical tasks of every front first — trsm tiles 0 and 1 and the updates of
+      // tiles (0, 0) (with the next diagonal block), (1, 0) and (1, 1), which the next step's first
+      // tasks wait for — then the other trsm tiles and local updates
       for (int p = g0; p < std::min(g0 + kp, maxsteps); ++p)
-        for (int kind = 0; kind < 2; ++kind)
-          for (int s : big) {
-            const int w = S.first[s + 1] - S.first[s], r = S.nrows[s];
-            const int npan = (int)cdiv(w, 64);
-            if (npan <= p) continue;
-            const int k0 = p * 64, kw = std::min(64, w - k0);
-            const int nt = (int)cdiv(r - k0 - kw, 64);
-            const double dk = kw, nb = r - k0 - kw;
-            const int gl = std::min(g0 + kp, npan) - 1, gend = std::min(64 * (gl + 1), w);
-            if (kind == 0) {
-              L.bytes += 8.0 * (2.0 * nb * dk + nt * (dk * (dk + 1) / 2 + 4 * 16 * 17));
-              L.flops += nb * dk * dk;
-              for (int rt = 0; rt < nt; ++rt) {
+        for (int phase2 = 0; phase2 < 2; ++phase2)
+          for (int kind = 0; kind < 2; ++kind)
+            for (int s : big) {
+              const int w = S.first[s + 1] - S.first[s], r = S.nrows[s];
+              const int npan = (int)cdiv(w, 64);
+              if (npan <= p) continue;
+              const int k0 = p * 64, kw = std::min(64, w - k0);
+              const int nt = (int)cdiv(r - k0 - kw, 64);
+              const double dk = kw, nb = r - k0 - kw;
+              const int gl = std::min(g0 + kp, npan) - 1, gend = std::min(64 * (gl + 1), w);
+              const bool local = !S.fused[s] && p < gl;  // local updates (then kw = 64, c0 = k0 + 64)
+              const int c0 = k0 + 64;
+              const int ncol = local ? (int)cdiv(gend - c0, 64) : 0;
+              auto trsm = [&](int rt) {
                 const int R0 = k0 + kw + 64 * rt;
                 region(s, k0, k0 + kw, k0, k0 + kw, false);  // L11, D, M_K
                 region(s, R0, R0 + 64, k0, k0 + kw, true);
-                emit(s, p, rt, 0);
-              }
-            } else {
-              if (S.fused[s] || p >= gl) continue;
-              const int c0 = k0 + 64;
-              const double nc = gend - c0;
-              L.bytes += 8.0 * (2.0 * nb * nc + nb * dk + nc * dk);
-              L.flops += 2.0 * dk * nc * (nb - 0.5 * nc);
-              for (int j = 0; j < (int)cdiv((int)nc, 64); ++j)
-                for (int i = j; i < nt; ++i) {
-                  region(s, c0 + 64 * i, c0 + 64 * i + 64, k0, k0 + 64, false);
-                  region(s, c0 + 64 * j, c0 + 64 * j + 64, k0, k0 + 64, false);
-                  region(s, c0 + 64 * i, c0 + 64 * i + 64, c0 + 64 * j, std::min(c0 + 64 * j + 64, gend), true);
-                  emit(s, p, i | (j << 16), 1);
+              };
+              auto upd = [&](int i, int j) {
+                region(s, c0 + 64 * i, c0 + 64 * i + 64, k0, k0 + 64, false);
+                region(s, c0 + 64 * j, c0 + 64 * j + 64, k0, k0 + 64, false);
+                region(s, c0 + 64 * i, c0 + 64 * i + 64, c0 + 64 * j, std::min(c0 + 64 * j + 64, gend), true);
+              };
+              const bool crit = phase2 == 0;
+              if (kind == 0) {
+                if (crit) {
+                  L.bytes += 8.0 * (2.0 * nb * dk + nt * (dk * (dk + 1) / 2 + 4 * 16 * 17));
+                  L.flops += nb * dk * dk;
+                  if (local) {
+                    const double nc = gend - c0;
+                    L.bytes += 8.0 * (2.0 * nb * nc + nb * dk + nc * dk);
+                    L.flops += 2.0 * dk * nc * (nb - 0.5 * nc);
+                  }
                 }
+                for (int rt = crit ? 0 : 2; rt < (crit ? std::min(nt, 2) : nt); ++rt) {
+                  trsm(rt);
+                  emit(s, p, rt, 0);
+                }
+              } else if (local) {
+                for (int j = 0; j < ncol; ++j)
+                  for (int i = j; i < nt; ++i) {
+                    const bool c = (i == 1 && j <= 1) || (i == 0 && j == 0);
+                    if (c != crit) continue;
+                    upd(i, j);
+                    emit(s, p, i | (j << 16), 1);
+                  }
+              }
             }
-          }
       if (g0 > 0) bulk(g0 - kp);
       // feed: the trailing update of the next group's columns, 64 x 64 tiles (k_big_update trailing mode)
       for (int s : big) {
@@ -6520,7 +6543,7 @@ void LDLSolver::dag_debug_dump(hipStream_t s, const Launch& L) {
   MADIPM_HIP(hipStreamSynchronize(s));
   std::vector<int64_t> h((size_t)4 * L.items);
   MADIPM_HIP(hipMemcpy(h.data(), dag_dbg_.p + 4 * L.off, h.size() * 8, hipMemcpyDeviceToHost));
-  double n[4] = {0, 0, 0, 0}, wt[4] = {0, 0, 0, 0}, rt[4] = {0, 0, 0, 0};
+  double n[5] = {0, 0, 0, 0, 0}, wt[5] = {0, 0, 0, 0, 0}, rt[5] = {0, 0, 0, 0, 0};
   int64_t t0 = INT64_MAX, t1 = 0;
   for (int64_t t = 0; t < L.items; ++t) {
     const int k = dag_kind_[4 * (L.off + t) + 3];
@@ -6530,10 +6553,10 @@ void LDLSolver::dag_debug_dump(hipStream_t s, const Launch& L) {
     t0 = std::min(t0, h[4 * t]);
     t1 = std::max(t1, h[4 * t + 2]);
   }
-  const char* nm[4] = {"trsm", "upd64", "upd128", "diag"};
+  const char* nm[5] = {"trsm", "upd64", "upd128", "diag", "step"};
   fprintf(stderr, "dag launch: %lld tasks, span %.1f us, wait %.1f / run %.1f WG-ms\n", (long long)L.items, (t1 - t0) / 100.0,
-          (wt[0] + wt[1] + wt[2] + wt[3]) / 1e5, (rt[0] + rt[1] + rt[2] + rt[3]) / 1e5);
-  for (int k = 0; k < 4; ++k)
+          (wt[0] + wt[1] + wt[2] + wt[3] + wt[4]) / 1e5, (rt[0] + rt[1] + rt[2] + rt[3] + rt[4]) / 1e5);
+  for (int k = 0; k < 5; ++k)
     if (n[k] > 0)
       fprintf(stderr, "  %-7s %6.0f tasks  wait %7.2f us  run %7.2f us (mean)\n", nm[k], n[k], wt[k] / n[k] / 100.0, rt[k] / n[k] / 100.0);
 }
