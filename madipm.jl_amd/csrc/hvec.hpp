@@ -3,6 +3,8 @@
 #pragma once
 
 #include <memory>
+#include <thread>
+#include <tuple>
 #include <utility>
 #include <vector>
 
@@ -26,5 +28,12 @@ struct NoInit : std::allocator<T> {
 };
 template <class T>
 using hvec = std::vector<T, NoInit<T>>;
+
+// Frees the given containers on a detached thread (big host arrays whose release only costs time).
+template <class... V>
+void free_async(V&&... v) {
+  auto* box = new std::tuple<std::decay_t<V>...>(std::move(v)...);
+  std::thread([box] { delete box; }).detach();
+}
 
 }  // namespace madipm

@@ -1497,7 +1497,10 @@ MPCSolver::MPCSolver(const madipm_qp& qp, const madipm_options& opt, Comm* comm)
   MADIPM_HIP(hipHostMalloc((void**)&hst_, seq_off + 64, hipHostMallocCoherent));
   std::memset((void*)hst_, 0, seq_off + 64);
   hseq_ = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(hst_) + seq_off);
+  PhaseClock clk("MPCSolver");
+  clk("stream + host state");
   setup_host(qp);
+  clk("setup_host (its locals freed)");
   t_init_ = now() - t0;
 }
 
@@ -1958,6 +1961,10 @@ void MPCSolver::setup_host(const madipm_qp& q) {
   // norm_b (solver.jl:173) on host
   norm_b_ = 0;
   for (double v : P.rhs) norm_b_ = std::max(norm_b_, std::fabs(v));
+  // the host copies of J, J^T and K2 (dense QP: ~18 GB) are released on a thread of their own: their
+  // page-table teardown took 2.1 s of the construction on the box (r6) with nothing waiting for it
+  free_async(std::move(Jci), std::move(JTci), std::move(Jcv), std::move(JTcv), std::move(Kri), std::move(Kv),
+             std::move(Hci), std::move(Hcv));
 }
 
 // Launch helpers (the DV view is rebuilt from member buffers; cheap, host-only)
