@@ -170,9 +170,9 @@ void madipm_comm_destroy(madipm_comm_t comm);
  * (kinds: 0 k_asm_chunks, 1 k_assemble, 2 k_tiny_factor, 3 k_small_factor, 4 k_big_diag,
  * 5 k_big_trsm, 6 k_big_update, 7 k_inertia, 8 k_fwd_small, 9 k_fwd_gather, 10 k_fwd_big,
  * 11 k_bwd_below, 12 k_bwd_big, 13 k_bwd_small, 14 k_fwd_tiny, 15 k_bwd_tiny, 16 k_lb_build,
- * 17 k_lb_syrk, 18 k_lb_gemv).  Setting a mask
- * clears the statistics. */
-#define MADIPM_NKERNELS 23
+ * 17 k_lb_syrk, 18 k_lb_gemv, 19 k_fwd_tree, 20 k_bwd_tree, 21 k_fact_tree, 22 k_asm_update,
+ * 23 k_big_dag [ABI 0.2.2]).  Setting a mask clears the statistics. */
+#define MADIPM_NKERNELS 24
 typedef struct madipm_kstat {
   char name[32];
   int64_t launches;

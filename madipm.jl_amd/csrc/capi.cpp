@@ -83,7 +83,7 @@ static SymbolicOptions to_sym_opts(const madipm_ldl_opts* o) {
 
 extern "C" {
 
-int madipm_version(void) { return 201; }  // 0.2.1: MADIPM_NKERNELS 23 (k_asm_update)
+int madipm_version(void) { return 202; }  // 0.2.2: MADIPM_NKERNELS 24 (k_big_dag)
 
 const char* madipm_last_error(void) { return last_error(); }
 

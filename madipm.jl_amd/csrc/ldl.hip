@@ -6214,7 +6214,7 @@ const char* kernel_kind_name(int k) {
                                         "k_big_trsm",   "k_big_update", "k_inertia",    "k_fwd_small",    "k_fwd_gather",
                                         "k_fwd_big",    "k_bwd_below",  "k_bwd_big",    "k_bwd_small",
                                         "k_fwd_tiny",   "k_bwd_tiny",   "k_lb_build",   "k_lb_syrk",      "k_lb_gemv",
-                                        "k_fwd_tree",   "k_bwd_tree",   "k_fact_tree",    "k_asm_update"};
+                                        "k_fwd_tree",   "k_bwd_tree",   "k_fact_tree",    "k_asm_update", "k_big_dag"};
   return (k >= 0 && k < KK_COUNT) ? names[k] : "?";
 }
 
@@ -6383,7 +6383,7 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
                                 T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, D_, L.nf, g_src_.p, Kx)));
         break;
       case BIG_DAG:  // off = the launch's first task (global index), items = its tasks
-        TIMED(KK_TRSM, L.bytes, L.alg, L.flops,
+        TIMED(KK_BIG_DAG, L.bytes, L.alg, L.flops,
               (k_big_dag<<<(unsigned)std::min<int64_t>(L.items, dag_grid_), NT, 0, s>>>(
                   T_, reinterpret_cast<const DagTask*>(dag_tasks_.p) + L.off, dag_dptr_.p + L.off, dag_dlist_.p,
                   (int)L.items, dag_flags_.p + L.off, cepoch_, dag_cnt_.p, big_kpan_, arena_, D_, dag_m_, dag_mslot_,

@@ -161,7 +161,7 @@ __device__ __forceinline__ void ldl_status_end(LDLStatus* st) { st->t1 = wall_cl
 enum KernelKind {
   KK_ASM_CHUNKS = 0, KK_ASSEMBLE, KK_TINY, KK_SMALL, KK_DIAG, KK_TRSM, KK_UPDATE, KK_INERTIA,
   KK_FWD_SMALL, KK_FWD_GATHER, KK_FWD_BIG, KK_BWD_BELOW, KK_BWD_BIG, KK_BWD_SMALL, KK_FWD_TINY, KK_BWD_TINY,
-  KK_LB_BUILD, KK_LB_SYRK, KK_LB_GEMV, KK_FWD_TREE, KK_BWD_TREE, KK_FACT_TREE, KK_ASM_UPDATE,
+  KK_LB_BUILD, KK_LB_SYRK, KK_LB_GEMV, KK_FWD_TREE, KK_BWD_TREE, KK_FACT_TREE, KK_ASM_UPDATE, KK_BIG_DAG,
   KK_COUNT
 };
 const char* kernel_kind_name(int k);

@@ -46,7 +46,7 @@ class LDLInfo(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
-NKERNELS = 23  # MADIPM_NKERNELS
+NKERNELS = 24  # MADIPM_NKERNELS
 
 
 class KStat(C.Structure):
