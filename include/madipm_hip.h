@@ -72,6 +72,10 @@ typedef struct madipm_ldl_info {
   int32_t tree_fronts;     /* fronts factorised by the dependency-driven tree launch (k_fact_tree) [ABI 0.2] */
   int32_t tree_medium;     /* of which medium fronts (192 < r <= 256: factorised in HBM, one 64-column
                               panel in LDS at a time) [ABI 0.2] */
+  int32_t root_tail_async; /* 1: the elimination-tree roots after the tree launch are assembled and
+                              factorised on a side stream, beside the next solve's forward leaves and
+                              tree fronts (MADIPM_ROOT_ASYNC, default on) [ABI 0.2.3] */
+  int32_t pad_;
 } madipm_ldl_info;
 
 void madipm_ldl_default_opts(madipm_ldl_opts* opts);

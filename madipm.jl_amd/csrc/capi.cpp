@@ -83,7 +83,7 @@ static SymbolicOptions to_sym_opts(const madipm_ldl_opts* o) {
 
 extern "C" {
 
-int madipm_version(void) { return 202; }  // 0.2.2: MADIPM_NKERNELS 24 (k_big_dag)
+int madipm_version(void) { return 203; }  // 0.2.3: madipm_ldl_info.root_tail_async (0.2.2: MADIPM_NKERNELS 24)
 
 const char* madipm_last_error(void) { return last_error(); }
 
@@ -178,6 +178,8 @@ static void fill_info(const SymbolicPlan& p, const LinSolver* ls, madipm_ldl_inf
       ++info->tree_fronts;
       info->tree_medium += p.nrows[s] > SymbolicPlan::kFactTreeMax;
     }
+  info->root_tail_async = ls && ls->tail_async() ? 1 : 0;
+  info->pad_ = 0;
 }
 
 int madipm_symbolic_info(madipm_symbolic_t sym, madipm_ldl_info* info) {

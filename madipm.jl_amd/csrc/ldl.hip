@@ -732,7 +732,7 @@ __global__ __launch_bounds__(ANT, CU == 2 ? 8 : 4) void k_assemble(FrontTab T, c
                                                      const int32_t* __restrict__ gptr, const double* __restrict__ part,
                                                      const BigChildRec* __restrict__ brec, double* __restrict__ arena,
                                                      double* __restrict__ fscratch, const IDX* __restrict__ gsrc,
-                                                     const double* __restrict__ Kx) {
+                                                     const double* __restrict__ Kx, int32_t* go, int go_epoch) {
   constexpr int WS = kAsmLdsSrc;
   __shared__ double Ts[64 * 64];
   extern __shared__ __attribute__((aligned(16))) double vals[];  // WS doubles (dynamic: past 64 KB of static LDS)
@@ -756,7 +756,23 @@ __global__ __launch_bounds__(ANT, CU == 2 ? 8 : 4) void k_assemble(FrontTab T, c
     const int j = J0 + wv + 16 * m;
     if (i < r && j < r && i >= j) {
       const int64_t q = !img ? i + (int64_t)j * r : (r > 128 ? (int64_t)((j * (2 * r - j - 1)) >> 1) + i : i + (int64_t)j * (r | 1));
-      F[q] = acc ? F[q] + v[m] : v[m];
+      const double x = acc ? F[q] + v[m] : v[m];
+      if (go)
+        __hip_atomic_store(F + q, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (st_sc1): to the root tail
+      else
+        F[q] = x;
+    }
+  }
+  if (go) {  // the root tail's release (LDLSolver::root_async_): the last tile out raises go[0]
+    // (form R1: write-through stores drained, one relaxed counter / flag per workgroup)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int old = __hip_atomic_fetch_add(go + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == (int)gridDim.x - 1) {
+        __hip_atomic_store(go + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(go, go_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
 }
@@ -1675,7 +1691,8 @@ template <bool PK>
 __global__ __launch_bounds__(SBT) void k_small_blocked(FrontTab T, const int32_t* __restrict__ fronts,
                                                       const double* __restrict__ Kx, double* __restrict__ arena,
                                                       const double* __restrict__ fscratch, double* __restrict__ D,
-                                                      LDLStatus* st, double tol) {
+                                                      LDLStatus* st, double tol, LDLStatus* stamp, int32_t* go,
+                                                      int go_epoch) {
   extern __shared__ __attribute__((aligned(16))) double A[];  // lower part of F (square ld r|1, or packed)
   __shared__ double Dl[192];
   __shared__ double MK[16 * LDM];
@@ -1684,6 +1701,15 @@ __global__ __launch_bounds__(SBT) void k_small_blocked(FrontTab T, const int32_t
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
   const int ld = r | 1;
   const int tid = threadIdx.x;
+  // the root tail (LDLSolver::root_async_): launched on the side stream ahead of time, it waits for
+  // the root assembly's go[0] (k_assemble's last tile, main stream), then acquires its stores.  The
+  // pivot chain runs beside the solve's kernels on this CU: its waves issue first
+  if (go) {
+    __builtin_amdgcn_s_setprio(3);
+    if (tid < 64) poll_flag(go, go_epoch, T.err);
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
   const int64_t fso = T.fs_off[s];
   if (fso >= 0 && !T.fs_img[s]) {  // batched-leaf parent: the SYRK and k_assemble wrote ld r
     stage_front<PK, SBT>(fscratch + fso, A, r, ld);
@@ -1715,6 +1741,15 @@ __global__ __launch_bounds__(SBT) void k_small_blocked(FrontTab T, const int32_t
   __syncthreads();
   factor_lds<PK>(T, A, r, w, ld, Dl, MK, cbuf);
   blocked_writeout<PK, false>(A, r, w, ld, Dl, arena + T.l_off[s], arena + T.u_off[s], T.u_ld[s], D, f0, st, tol);
+  if (go) {  // released to k_root_solve (go[2 + front]: the epoch); nothing of this kernel follows
+    __threadfence();
+    __syncthreads();
+  }
+  if (tid == 0) {
+    // lazy inertia: the factorisation's end
+    if (stamp) atomicMax(reinterpret_cast<unsigned long long*>(&stamp->t1), (unsigned long long)wall_clock64());
+    if (go) __hip_atomic_store(go + 2 + blockIdx.x, go_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // ------------------------------------------------------------------ leaf folding
@@ -4588,7 +4623,8 @@ __global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __re
 constexpr int RSN = 1024;
 __global__ __launch_bounds__(RSN) void k_root_solve(FrontTab T, const int32_t* __restrict__ fronts,
                                                     const double* __restrict__ arena, double* b, double* xi,
-                                                    const double* __restrict__ Dg, int32_t* tflags, int epoch) {
+                                                    const double* __restrict__ Dg, int32_t* tflags, int epoch,
+                                                    const int32_t* rdone, int nrd, int repoch) {
   extern __shared__ __attribute__((aligned(16))) double Ls[];
   __shared__ double part[4 * SMALL_SOLVE_MAX], inits[SMALL_SOLVE_MAX];
   const int s = fronts[blockIdx.x];
@@ -4605,16 +4641,21 @@ __global__ __launch_bounds__(RSN) void k_root_solve(FrontTab T, const int32_t* _
     len = T.sv_ptr[e0 + i + 1] - lo;
   }
   const double init = (i < r && k == 0) ? fwd_init(T, s, i, w, f0, b) : 0.0;
-  // wave 0's pivots and the caller's positions, loaded with everything else (not after the barrier)
+  // wave 0's pivots and the caller's positions, and the panel: loaded with everything else, except
+  // right after a factorisation whose root tail ran on the side stream (nrd > 0: after the gather,
+  // the tail's done flags and the acquire)
   double dpiv[3];
   int pj[3];
+  auto factor_loads = [&]() {
 #pragma unroll
-  for (int h = 0; h < 3; ++h) {
-    const int j = min(lane + 64 * h, max(w - 1, 0));
-    dpiv[h] = (tid < 64) ? Dg[f0 + j] : 1.0;
-    pj[h] = (tid < 64) ? T.perm[f0 + j] : 0;
-  }
-  stage_rowmajor<RSN>(arena + T.l_off[s], Ls, r, w, ldt);
+    for (int h = 0; h < 3; ++h) {
+      const int j = min(lane + 64 * h, max(w - 1, 0));
+      dpiv[h] = (tid < 64) ? Dg[f0 + j] : 1.0;
+      pj[h] = (tid < 64) ? T.perm[f0 + j] : 0;
+    }
+    stage_rowmajor<RSN>(arena + T.l_off[s], Ls, r, w, ldt);
+  };
+  if (nrd == 0) factor_loads();
   double c = 0.0;
   const int64_t q4 = len >> 2;
   for (int64_t m0 = 0; m0 < q4; m0 += 16) {  // 16 loads in flight (ex10's root rows: ~14 per thread)
@@ -4630,6 +4671,24 @@ __global__ __launch_bounds__(RSN) void k_root_solve(FrontTab T, const int32_t* _
   if (i < r) {
     part[4 * i + k] = c;
     if (k == 0) inits[i] = init;
+  }
+  if (nrd > 0) {  // the root tail on the side stream (LDLSolver::root_async_): every root factorised
+    if (tid < 64) {
+      int spins = 0;
+      for (;;) {
+        const bool ok = lane >= nrd ||
+                        __hip_atomic_load(rdone + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == repoch;
+        if (__all(ok)) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1 << 25)) {
+          if (lane == 0) atomicOr(T.err, kErrHandoff);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    factor_loads();
   }
   __syncthreads();  // the panel and the partial sums
   if (tid < 64) {
@@ -5846,6 +5905,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   }
 
   // ---- solve schedules: per level, small fronts (wave per front) and big fronts (task queues)
+  std::vector<uint8_t> rootf(std::max(ns, 1), 0);  // fronts solved by k_root_solve
   {
     std::vector<int32_t> flag_off(ns, 0);
     int64_t nflags = 0;
@@ -5971,6 +6031,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         for (int q = S.level_ptr[lev]; q < S.level_ptr[lev + 1]; ++q)
           if (in_tree[S.level_list[q]]) (big_root(S.level_list[q]) ? roots : ord).push_back(S.level_list[q]);
       nroot_task_ = (int)roots.size();
+      for (int s : roots) rootf[s] = 1;
       ord.insert(ord.end(), roots.begin(), roots.end());
       ntree_ = (int)ord.size();
       // children of tree fronts scatter their forward update entries straight into the parent's
@@ -6115,6 +6176,39 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     counters_.alloc(4 * std::max(NL, 1) + 4);  // + the tree-solve tickets (4 NL, 4 NL + 1)
     counters_.zero();
   }
+  {  // the root tail: the launches after the last tree launch factorise only k_root_solve's fronts
+    size_t ft = SIZE_MAX;
+    for (size_t i = 0; i < fact1_.size(); ++i)
+      if (fact1_[i].kind == FTREE) ft = i;
+    // after it: assembly launches, the last of which assembles the roots, then ONE factorisation
+    // launch (SMALL*) of <= 64 roots, all of them solved by k_root_solve
+    const size_t nl = fact1_.size();
+    bool ok = S.nshards == 1 && nroot_task_ > 0 && ft != SIZE_MAX && ft + 2 < nl && fact1_[nl - 2].kind == ASSEMBLE;
+    for (size_t i = ft + 1; ok && i + 1 < nl; ++i) ok = fact1_[i].kind == ASSEMBLE;
+    if (ok) {
+      const Launch& L = fact1_[nl - 1];
+      ok = (L.kind == SMALL64 || L.kind == SMALL128 || L.kind == SMALL192) && L.items <= 64 && L.items <= nroot_task_;
+      for (int64_t k = 0; ok && k < L.items; ++k) ok = rootf[sched[L.off + k]] != 0;
+    }
+    const char* ra = std::getenv("MADIPM_ROOT_ASYNC");
+    root_async_ = ok && !(ra && ra[0] == '0');
+    if (ra && ra[0] == '2') {  // diagnostics: why (not)
+      std::string k;
+      for (const Launch& L : fact1_) k += std::to_string(L.kind) + "/" + std::to_string(L.items) + " ";
+      fprintf(stderr, "root tail: async %d (roots %d, tree launch %lld, launches kind/items: %s)\n", (int)root_async_,
+              nroot_task_, ft == SIZE_MAX ? -1LL : (long long)ft, k.c_str());
+    }
+    if (root_async_) {
+      side0_ = nl - 1;
+      nroot_side_ = (int)fact1_[nl - 1].items;
+      int lo = 0, hi = 0;  // the tail is the critical path beside the forward solve: the higher priority
+      MADIPM_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      MADIPM_HIP(hipStreamCreateWithPriority(&side_, hipStreamNonBlocking, hi));
+      MADIPM_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+      rflag_.alloc(2 + 64);  // go, the assembly's tile counter, one done flag per root
+      rflag_.zero();
+    }
+  }
   sched_.upload(sched.empty() ? std::vector<int32_t>{0} : sched);
   arena_.alloc(std::max<int64_t>(S.arena_size, 2));
   if (S.nshards > 1) {  // top fronts: the strict upper triangles are never written, keep them 0
@@ -6197,6 +6291,11 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
 }
 
 LDLSolver::~LDLSolver() {
+  if (side_) {  // a root tail never joined (a factorisation nothing solved with) ends before its buffers
+    (void)hipStreamSynchronize(side_);
+    (void)hipStreamDestroy(side_);
+  }
+  if (ev_join_) (void)hipEventDestroy(ev_join_);
   if (h_status_) (void)hipHostFree(h_status_);
   for (hipEvent_t e : evs_) (void)hipEventDestroy(e);
 }
@@ -6317,9 +6416,13 @@ double LDLSolver::solve_alg(int s) const {
   return b;
 }
 
-void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStream_t s) {
-  ++cepoch_;  // k_big_dag's flags: this factorisation's epoch (never 0)
-  for (const Launch& L : LL) {
+void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStream_t s, size_t b, size_t e,
+                         LDLStatus* stamp) {
+  if (b == 0) ++cepoch_;  // k_big_dag's flags: this factorisation's epoch (never 0)
+  for (size_t li = b; li < std::min(e, LL.size()); ++li) {
+    const Launch& L = LL[li];
+    // the root tail (root_async_): the roots' assembly raises go, their factorisation waits for it
+    int32_t* go = (root_async_ && &LL == &fact1_ && (li + 1 == side0_ || li == side0_)) ? rflag_.p : nullptr;
     const int32_t* list = sched_.p + L.off;
     switch (L.kind) {
       case ASSEMBLE:
@@ -6332,15 +6435,19 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
         if (g_src32_.p)
           TIMED(KK_ASSEMBLE, L.bytes, 0.0, L.flops,
                 (L.items < 256 ? k_assemble<8, int32_t><<<(unsigned)L.items, ANT, 8 * kAsmLdsSrc, s>>>(
-                                     T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_, g_src32_.p, Kx)
+                                     T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_, g_src32_.p, Kx, go,
+                                     repoch_)
                                : k_assemble<2, int32_t><<<(unsigned)L.items, ANT, 8 * kAsmLdsSrc, s>>>(
-                                     T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_, g_src32_.p, Kx)));
+                                     T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_, g_src32_.p, Kx, go,
+                                     repoch_)));
         else
           TIMED(KK_ASSEMBLE, L.bytes, 0.0, L.flops,
                 (L.items < 256 ? k_assemble<8, int64_t><<<(unsigned)L.items, ANT, 8 * kAsmLdsSrc, s>>>(
-                                     T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_, g_src_.p, Kx)
+                                     T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_, g_src_.p, Kx, go,
+                                     repoch_)
                                : k_assemble<2, int64_t><<<(unsigned)L.items, ANT, 8 * kAsmLdsSrc, s>>>(
-                                     T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_, g_src_.p, Kx)));
+                                     T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_, g_src_.p, Kx, go,
+                                     repoch_)));
         break;
       case MICRO:
         TIMED(KK_TINY, L.bytes, L.alg, L.flops,
@@ -6356,12 +6463,12 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
       case SMALL128:
         TIMED(KK_SMALL, L.bytes, L.alg, L.flops,
               (k_small_blocked<false><<<(unsigned)L.items, SBT, L.lds_bytes, s>>>(T_, list, Kx, arena_, fscratch_, D_,
-                                                                                st_, pivot_tol)));
+                                                                                st_, pivot_tol, stamp, go, repoch_)));
         break;
       case SMALL192:
         TIMED(KK_SMALL, L.bytes, L.alg, L.flops,
               (k_small_blocked<true><<<(unsigned)L.items, SBT, L.lds_bytes, s>>>(T_, list, Kx, arena_, fscratch_, D_,
-                                                                               st_, pivot_tol)));
+                                                                               st_, pivot_tol, stamp, go, repoch_)));
         break;
       case BIG_DIAG:
         TIMED(KK_DIAG, L.bytes, L.alg, L.flops,
@@ -6428,12 +6535,28 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
 // assembly and the shard's status slot.
 void LDLSolver::fact_phase1(const double* Kx, hipStream_t s) {
   if (S_.N == 0) return;
+  join(s);  // the previous factorisation's root tail writes the same arena
   if (!(ext_reset && ext_status_ && !sharded())) k_status_init<<<1, 1, 0, s>>>(st_);
-  run_fact(fact1_, Kx, s);
+  const bool lazy = !sharded() && lazy_inertia && !spd && ext_status_;
+  if (root_async_) {
+    // the tree launch and the roots' assembly on s, the roots' factorisation on side_, where it waits
+    // on the device for the assembly's go flag (no cross-stream event: its ~17 us of latency, r6_w).
+    // s goes on to the caller's next kernels (the solve's right-hand side, forward leaves and tree
+    // fronts), which read nothing the tail writes; k_root_solve waits for the tail's done flags.
+    // Lazy inertia: the root kernel stamps t1.
+    ++repoch_;
+    run_fact(fact1_, Kx, s, 0, side0_);
+    run_fact(fact1_, Kx, side_, side0_, fact1_.size(), lazy ? st_ : nullptr);
+    MADIPM_HIP(hipEventRecord(ev_join_, side_));
+    root_pending_ = true;
+    if (!lazy) join(s);  // k_inertia and the status copy below need the whole factor
+  } else {
+    run_fact(fact1_, Kx, s);
+  }
   const int nb = (int)std::min<int64_t>(64, cdiv(S_.N, NT));
   const int spdf = spd ? 1 : 0;
   if (!sharded()) {
-    if (lazy_inertia && !spd && ext_status_) {  // the driver's next kernel stamps t1
+    if (lazy) {  // the driver's next kernel (root_async_: the root kernel) stamps t1
       inertia_stale_ = true;
       return;
     }
@@ -6483,8 +6606,15 @@ bool LDLSolver::external_status(LDLStatus* dev, LDLStatus* host) {
   return true;
 }
 
+void LDLSolver::join(hipStream_t s) {
+  if (!root_pending_) return;
+  MADIPM_HIP(hipStreamWaitEvent(s, ev_join_, 0));
+  root_pending_ = false;
+}
+
 double LDLSolver::fact_seconds(hipStream_t s) {
   if (S_.N == 0) return 0.0;
+  join(s);
   LDLStatus h;
   MADIPM_HIP(hipMemcpyAsync(&h, st_, sizeof(LDLStatus), hipMemcpyDeviceToHost, s));
   MADIPM_HIP(hipStreamSynchronize(s));
@@ -6499,6 +6629,7 @@ double LDLSolver::fact_seconds(hipStream_t s) {
 void LDLSolver::count_inertia(hipStream_t s) {
   if (!inertia_stale_ || S_.N == 0) return;
   inertia_stale_ = false;
+  join(s);
   const int nb = (int)std::min<int64_t>(64, cdiv(S_.N, NT));
   k_zero_counts<<<1, 1, 0, s>>>(st_);
   k_inertia<<<nb, NT, 0, s>>>(D_, S_.N, st_, 0, nullptr, 1);
@@ -6511,6 +6642,7 @@ int LDLSolver::status(hipStream_t s, bool sync) {
     factorized = true;
     return 0;
   }
+  if (sync) join(s);
   if (sync && ext_status_) MADIPM_HIP(hipMemcpyAsync(h_st_, st_, sizeof(LDLStatus), hipMemcpyDeviceToHost, s));
   if (sync) MADIPM_HIP(hipStreamSynchronize(s));
   if (h_st_->err) {  // a lost hand-off or a carve overflow gives a wrong factor or solve: never success
@@ -6700,11 +6832,14 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
                                                               tchunk_)));
       if (nroot_task_)
         TIMED(KK_FWD_TREE, nlo > 0 ? 0.0 : tree_bytes_, nlo > 0 ? 0.0 : tree_alg_, nlo > 0 ? 0.0 : tree_flops_,
-              (k_root_solve<<<(unsigned)nroot_task_, RSN, root_lds_, s>>>(T_, tc_list_.p + nlo, arena_, b, xi_, D_, tflags_,
-                                                                         efwd)));
+              (k_root_solve<<<(unsigned)nroot_task_, RSN, root_lds_, s>>>(
+                  T_, tc_list_.p + nlo, arena_, b, xi_, D_, tflags_, efwd, rflag_.p ? rflag_.p + 2 : nullptr,
+                  root_pending_ ? nroot_side_ : 0, repoch_)));
+      root_pending_ = false;  // (root_async_) the first k_root_solve after a factorisation waited for its tail
     }
     if (lev == 0 && phase == 0 && ntree_ && tdbg_.p)
       tree_debug_dump(s, "fwd", tdbg_.p, ntask_, "leaves", "wait", "gather", "subst", "store", 8);
+    if (lev == 0) join(s);  // (no-op: root_async_ has no fronts above the tree)
   }
 }
 
@@ -6759,6 +6894,7 @@ void LDLSolver::solve_phase1(double* b, hipStream_t s) {
   for (const SolveLevel& L : slev2_) queues |= L.nbig > 0;
   if (queues) MADIPM_HIP(hipMemsetAsync(counters_.p, 0, counters_.n * sizeof(int32_t), s));
   fwd_levels(slev1_, 0, b, s);
+  join(s);
   if (!sharded()) {
     bwd_levels(slev1_, 0, b, s);
   } else if (nxg_) {

@@ -223,6 +223,13 @@ class LinSolver {
   //     ldl_status_end); the pivot check does not need it unless spd, and inertia() counts on demand
   bool ext_reset = false, lazy_inertia = false;
   virtual void count_inertia(hipStream_t s) { (void)s; }
+  // The factorisation's tail (an elimination-tree root factorised after the tree launch, LDLSolver::
+  // root_async_) may run on a side stream after factorize_async returns, beside the next solve's
+  // forward leaves and tree fronts.  join(s) orders s after it; solve_async, status(s, true),
+  // count_inertia and fact_seconds join by themselves.  With tail_async() the status carried by a
+  // kernel enqueued right after factorize_async is not final: read it after the next solve.
+  virtual bool tail_async() const { return false; }
+  virtual void join(hipStream_t s) { (void)s; }
 };
 
 class LDLSolver : public LinSolver {
@@ -265,6 +272,8 @@ class LDLSolver : public LinSolver {
   int64_t xch_solve() const override { return sharded() ? solve_xlen() : 0; }
   int64_t xch_gather() const override { return sharded() ? S_.nshards * gper_ : 0; }
   double fact_seconds(hipStream_t s) override;
+  bool tail_async() const override { return root_async_; }
+  void join(hipStream_t s) override;
 
   const SymbolicPlan& plan() const override { return S_; }
   int n() const override { return S_.N; }
@@ -328,7 +337,20 @@ class LDLSolver : public LinSolver {
   std::vector<SolveLevel> slev1_, slev2_;  // per level, leaves first
   int64_t xg_off_ = 0;                     // (top front, 256-row chunk) pairs of the external forward gather
   int nxg_ = 0;
-  void run_fact(const std::vector<Launch>& L, const double* Kx, hipStream_t s);
+  // launches [b, e) of L on s; stamp: SMALL* launches stamp the factorisation's end into it
+  void run_fact(const std::vector<Launch>& L, const double* Kx, hipStream_t s, size_t b = 0, size_t e = SIZE_MAX,
+                LDLStatus* stamp = nullptr);
+  // the root tail on a side stream (MADIPM_ROOT_ASYNC, default on): fact1_[side0_] (the last launch)
+  // factorises elimination-tree roots that only k_root_solve reads.  It is enqueued on side_ and waits
+  // on the device for rflag_[0] == repoch_ (raised by the roots' assembly, fact1_[side0_ - 1], on the
+  // caller's stream), then raises rflag_[2 + k] for k_root_solve; ev_join_ (recorded after it) joins
+  // the host-side users (status, fact_seconds, a factorisation no solve followed)
+  bool root_async_ = false, root_pending_ = false;
+  size_t side0_ = 0;
+  int nroot_side_ = 0, repoch_ = 0;
+  DBuf<int32_t> rflag_;
+  hipStream_t side_ = nullptr;
+  hipEvent_t ev_join_ = nullptr;
   void fwd_levels(const std::vector<SolveLevel>& V, int phase, double* b, hipStream_t s);
   void bwd_levels(const std::vector<SolveLevel>& V, int phase, double* b, hipStream_t s);
   DBuf<int64_t> xoff_, sx_ptr_, sx_src_;

@@ -2054,7 +2054,8 @@ const double* MPCSolver::kvals() const { return kkt_ == KKT_NORMAL ? Cx_.p : Kx_
 // the pool grows only when a solve needs more pairs than any earlier one did
 void MPCSolver::timed_factorize() {
   ldl_->factorize_async(kvals(), stream_);
-  fact_end_pending_ = ldl_->lazy_inertia;  // the next k_rhs stamps the factorisation's end
+  // the next k_rhs stamps the factorisation's end (an asynchronous tail stamps its own)
+  fact_end_pending_ = ldl_->lazy_inertia && !ldl_->tail_async();
 }
 
 // the status block the kernel right before a factorisation resets (LinSolver::ext_reset), or nullptr
@@ -2121,7 +2122,12 @@ void MPCSolver::solve_system(int mode, double mu, int reset, int amode, double a
   const int nb = blocks(n_ + m_), nbs = spmv_blocks(n_ + m_);
   DevState* host = nullptr;
   uint32_t seq = 0;
-  if (publish_next_) {  // read_state() folded into this launch
+  bool late = false;  // published by the residual's finaliser instead: after the solve joined the
+                      // factorisation's asynchronous tail, whose pivot check the state carries
+  if (publish_next_ && ldl_->tail_async()) {
+    late = true;
+    publish_next_ = false;
+  } else if (publish_next_) {  // read_state() folded into this launch
     host = hst_;
     seq = ++pub_seq_;
     publish_next_ = false;
@@ -2134,7 +2140,7 @@ void MPCSolver::solve_system(int mode, double mu, int reset, int amode, double a
   // blocks) and is finalised with the residual
   const int nbz = amode >= 0 ? blocks(std::max(nlb_, nub_)) : 0;
   SPMV_LAUNCH(k_residual, nbs + nbz, stream_, D, del_w_, del_c_, nbs, amode, atau);
-  launch_reduce_final(FIN_RESID, nbs, amode);
+  launch_reduce_final(FIN_RESID, nbs, amode, 0, nullptr, late);
 }
 
 // gondzio_correction_direction! (solver.jl:245-298): host-controlled loop, one read-back per solve
@@ -2182,12 +2188,14 @@ void MPCSolver::read_state() {
 }
 
 // Host spin on the publication counter (no event record in the stream: each one costs a ~5 us
-// bubble between kernels); bounded, and a failed stream surfaces as its HIP error.
+// bubble between kernels); bounded, and a failed stream surfaces as its HIP error.  The stream is
+// queried only once a wait has lasted 2 ms: a query puts a marker into the stream, another ~6 us
+// bubble at the point the host had enqueued to (r6_x: before the predictor's k_rhs and k_apply)
 void MPCSolver::wait_state() {
   const double t0 = now();
   for (uint64_t spin = 0;; ++spin) {
     if (__atomic_load_n(hseq_, __ATOMIC_ACQUIRE) == pub_seq_) return;
-    if ((spin & 1023) == 1023) {
+    if ((spin & 1023) == 1023 && now() - t0 > 2e-3) {
       const hipError_t e = hipStreamQuery(stream_);
       if (e != hipSuccess && e != hipErrorNotReady) MADIPM_HIP(e);
       if (e == hipSuccess && __atomic_load_n(hseq_, __ATOMIC_ACQUIRE) != pub_seq_)
@@ -2446,6 +2454,7 @@ int MPCSolver::solve(madipm_stats* stats) {
         directions(false, true);
         step_size(true);
       } else {
+        ldl_->join(s);  // the factorisation's asynchronous tail (its pivot check) before the read-back
         read_state();
       }
       wait_state();

@@ -40,7 +40,8 @@ class LDLInfo(C.Structure):
                 ("lb_groups", C.c_int32), ("lb_members", C.c_int32),
                 ("fold_fronts", C.c_int32), ("fold_leaves", C.c_int32),
                 ("xch_fact", C.c_int64), ("xch_solve", C.c_int64), ("xch_gather", C.c_int64),
-                ("tree_fronts", C.c_int32), ("tree_medium", C.c_int32)]
+                ("tree_fronts", C.c_int32), ("tree_medium", C.c_int32),
+                ("root_tail_async", C.c_int32), ("pad_", C.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     lib = ctypes.CDLL(str(_lib.LIB_PATH))
     missing = [n for n in sorted(names) if not hasattr(lib, n)]
     assert not missing, missing
-    assert _lib.madipm_version() == 202
+    assert _lib.madipm_version() == 203
 
 
 def test_library_reports_errors_without_gpu():

@@ -1,5 +1,6 @@
 """Per-launch timeline of one MPC iteration from a rocprofv3 kernel-trace csv (third-to-last k_term
-to second-to-last): kernel, template, workgroups, duration, gap to the previous launch."""
+to second-to-last): kernel, template, workgroups, duration, gap to the previous launch's end (negative:
+concurrent launches on two streams), start relative to the iteration's first launch."""
 import csv, glob, os, re, sys
 d = sys.argv[1]
 f = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
@@ -18,5 +19,7 @@ for i in range(a, b):
         continue
     gap = (int(r['Start_Timestamp']) - int(tr[i - 1]['End_Timestamp'])) / 1e3
     tm = re.search(r'<(\d+)>', r['Kernel_Name'])
-    print(f"{names[i]:18s}{'<' + tm.group(1) + '>' if tm else '   ':5s} wg={int(r['Grid_Size_X']) // int(r['Workgroup_Size_X']):6d} {dur:7.1f}us gap {gap:5.1f}")
+    t = (int(r['Start_Timestamp']) - int(tr[a]['Start_Timestamp'])) / 1e3
+    print(f"{names[i]:18s}{'<' + tm.group(1) + '>' if tm else '   ':5s} wg={int(r['Grid_Size_X']) // int(r['Workgroup_Size_X']):6d} "
+          f"{dur:7.1f}us gap {gap:5.1f}  at {t:6.1f}")
 print(f"iteration: busy {tot:.1f} us, span {(int(tr[b]['Start_Timestamp']) - int(tr[a]['Start_Timestamp'])) / 1e3:.1f} us")
