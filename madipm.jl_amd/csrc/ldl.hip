@@ -4474,7 +4474,8 @@ __global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __re
                                                  const double* __restrict__ arena, const double* __restrict__ b,
                                                  double* xi, double* uvec, int32_t* err, int64_t* dbg,
                                                  const uint8_t* __restrict__ rootbwd, const double* __restrict__ Dg,
-                                                 const uint8_t* __restrict__ tchunk) {
+                                                 const uint8_t* __restrict__ tchunk, const uint8_t* __restrict__ tside,
+                                                 const int32_t* rdone, int nrd, int repoch) {
   extern __shared__ __attribute__((aligned(16))) double Ls[];
   __shared__ double v0s[MED_SOLVE_MAX];
   __shared__ int s_task;
@@ -4500,7 +4501,10 @@ __global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __re
     const int ldt = tree_ldt(w);
     double* stg = med ? Ls : Ls + r * ldt;
     const int cap = med ? (lds_doubles / NT) * NT : ((lds_doubles - r * ldt) / NT) * NT;
-    if (!med) stage_rowmajor(arena + T.l_off[s], Ls, r, w, ldt);
+    // a root factorised on the side stream (LDLSolver::root_async_, first solve after the
+    // factorisation): its panel and pivots only after the tail's done flags
+    const bool sw = nrd > 0 && tside[t] && q == q1 - 1;
+    if (!med && !sw) stage_rowmajor(arena + T.l_off[s], Ls, r, w, ldt);
     // everything that does not depend on the children is loaded before the wait: the gather range
     // (symbolic) and this front's own right-hand side entries (the input b)
     const int64_t e0 = T.row_ptr[s];
@@ -4558,6 +4562,31 @@ __global__ __launch_bounds__(NT) void k_fwd_tree(FrontTab T, const int32_t* __re
     }
     if (q == q0 && tid < 64) poll_deps(dep, dep_ptr[t], dep_ptr[t + 1], tflags, epoch, err);
     __syncthreads();  // + the previous front's / the leaves' drained stores (vmcnt 0 before it)
+    if (sw) {
+      if (tid < 64) {
+        const int lane = tid;
+        int spins = 0;
+        for (;;) {
+          const bool ok = lane >= nrd ||
+                          __hip_atomic_load(rdone + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == repoch;
+          if (__all(ok)) break;
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > (1 << 25)) {
+            if (lane == 0) atomicOr(err, kErrHandoff);
+            break;
+          }
+        }
+      }
+      __syncthreads();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (!med) stage_rowmajor(arena + T.l_off[s], Ls, r, w, ldt);
+#pragma unroll
+      for (int h = 0; h < 3; ++h) {
+        const int j = min((tid & 63) + 64 * h, max(w - 1, 0));
+        dpiv[h] = (rb && tid < 64) ? Dg[f0 + j] : 1.0;
+      }
+      __syncthreads();
+    }
     if (dg && tid == 0 && q == q0) dg[2] = wall_clock64();
     double ct = 0.0;  // the tree children's entries of this row, in order
     for (int k = 0; k < ntr; ++k) ct += ld_sc1(T.gbuf + pl1 + k);
@@ -5905,7 +5934,8 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   }
 
   // ---- solve schedules: per level, small fronts (wave per front) and big fronts (task queues)
-  std::vector<uint8_t> rootf(std::max(ns, 1), 0);  // fronts solved by k_root_solve
+  std::vector<uint8_t> rootf(std::max(ns, 1), 0);  // roots solved by k_root_solve (1) / a k_fwd_tree task (2)
+  std::vector<int32_t> tfront;                      // tree-solve task -> its (top) front
   {
     std::vector<int32_t> flag_off(ns, 0);
     int64_t nflags = 0;
@@ -6114,12 +6144,14 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
         }
       }
       ntask_ = (int)tops.size();
+      tfront = tops;
       {  // elimination-tree roots (r == w, no parent) solved backward by k_fwd_tree right after their forward
          // substitution, on the panel already in LDS (bitwise k_bwd_tree's x; r3: k_bwd_tree 52 -> 43 us)
         std::vector<uint8_t> rbv(std::max(ntask_, 1), 0);
         for (int t = 0; t < ntask_; ++t) {
           const int f = tops[t];
           rbv[t] = S.parent[f] < 0 && S.nrows[f] == S.first[f + 1] - S.first[f] && !chunk[f];
+          if (rbv[t] && !rootf[f]) rootf[f] = 2;  // solved forward and backward by its k_fwd_tree task
         }
         trootbwd_.upload(rbv);
       }
@@ -6183,11 +6215,11 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     // after it: assembly launches, the last of which assembles the roots, then ONE factorisation
     // launch (SMALL*) of <= 64 roots, all of them solved by k_root_solve
     const size_t nl = fact1_.size();
-    bool ok = S.nshards == 1 && nroot_task_ > 0 && ft != SIZE_MAX && ft + 2 < nl && fact1_[nl - 2].kind == ASSEMBLE;
+    bool ok = S.nshards == 1 && ntree_ > 0 && ft != SIZE_MAX && ft + 2 < nl && fact1_[nl - 2].kind == ASSEMBLE;
     for (size_t i = ft + 1; ok && i + 1 < nl; ++i) ok = fact1_[i].kind == ASSEMBLE;
     if (ok) {
       const Launch& L = fact1_[nl - 1];
-      ok = (L.kind == SMALL64 || L.kind == SMALL128 || L.kind == SMALL192) && L.items <= 64 && L.items <= nroot_task_;
+      ok = (L.kind == SMALL64 || L.kind == SMALL128 || L.kind == SMALL192) && L.items <= 64;
       for (int64_t k = 0; ok && k < L.items; ++k) ok = rootf[sched[L.off + k]] != 0;
     }
     const char* ra = std::getenv("MADIPM_ROOT_ASYNC");
@@ -6195,8 +6227,14 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     if (ra && ra[0] == '2') {  // diagnostics: why (not)
       std::string k;
       for (const Launch& L : fact1_) k += std::to_string(L.kind) + "/" + std::to_string(L.items) + " ";
-      fprintf(stderr, "root tail: async %d (roots %d, tree launch %lld, launches kind/items: %s)\n", (int)root_async_,
-              nroot_task_, ft == SIZE_MAX ? -1LL : (long long)ft, k.c_str());
+      std::string rk;
+      if (nl > 0)
+        for (int64_t q = 0; q < std::min<int64_t>(fact1_[nl - 1].items, 8); ++q) {
+          const int f = sched[fact1_[nl - 1].off + q];
+          rk += std::to_string(f) + ":" + std::to_string(rootf[f]) + ":r" + std::to_string(S.nrows[f]) + " ";
+        }
+      fprintf(stderr, "root tail: async %d (roots %d, tree launch %lld, launches kind/items: %s; last launch fronts %s)\n",
+              (int)root_async_, nroot_task_, ft == SIZE_MAX ? -1LL : (long long)ft, k.c_str(), rk.c_str());
     }
     if (root_async_) {
       side0_ = nl - 1;
@@ -6207,6 +6245,16 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       MADIPM_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
       rflag_.alloc(2 + 64);  // go, the assembly's tile counter, one done flag per root
       rflag_.zero();
+      // the k_fwd_tree tasks of the side roots wait for the tail themselves (supportcase10's root)
+      std::vector<uint8_t> ts(std::max(ntask_, 1), 0);
+      const Launch& L = fact1_[nl - 1];
+      for (int64_t k = 0; k < L.items; ++k) {
+        const int f = sched[L.off + k];
+        if (rootf[f] == 2)
+          for (int t = 0; t < ntask_; ++t)
+            if (tfront[t] == f) ts[t] = 1, side_tree_ = true;
+      }
+      tside_.upload(ts);
     }
   }
   sched_.upload(sched.empty() ? std::vector<int32_t>{0} : sched);
@@ -6826,10 +6874,11 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
       const int nlo = ntask_ - nroot_task_;  // the big roots last, in their own launch (more LDS)
       if (nlo > 0)
         TIMED(KK_FWD_TREE, tree_bytes_, tree_alg_, tree_flops_,
-              (k_fwd_tree<<<(unsigned)nlo, NT, tree_lds_, s>>>(T_, tc_ptr_, tc_list_, nlo, tdep_ptr_, tdep_,
-                                                              counters_.p + 4 * S_.nlevels, tflags_, efwd, tree_lds_ / 8,
-                                                              arena_, b, xi_, uvec_, &st_->err, tdbg_.p, trootbwd_, D_,
-                                                              tchunk_)));
+              (k_fwd_tree<<<(unsigned)nlo, NT, tree_lds_, s>>>(
+                  T_, tc_ptr_, tc_list_, nlo, tdep_ptr_, tdep_, counters_.p + 4 * S_.nlevels, tflags_, efwd, tree_lds_ / 8,
+                  arena_, b, xi_, uvec_, &st_->err, tdbg_.p, trootbwd_, D_, tchunk_, tside_.p,
+                  rflag_.p ? rflag_.p + 2 : nullptr, root_pending_ && side_tree_ ? nroot_side_ : 0, repoch_)));
+      if (side_tree_) root_pending_ = false;  // (root_async_) its side roots waited for the tail
       if (nroot_task_)
         TIMED(KK_FWD_TREE, nlo > 0 ? 0.0 : tree_bytes_, nlo > 0 ? 0.0 : tree_alg_, nlo > 0 ? 0.0 : tree_flops_,
               (k_root_solve<<<(unsigned)nroot_task_, RSN, root_lds_, s>>>(

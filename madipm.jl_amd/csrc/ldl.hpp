@@ -348,7 +348,9 @@ class LDLSolver : public LinSolver {
   bool root_async_ = false, root_pending_ = false;
   size_t side0_ = 0;
   int nroot_side_ = 0, repoch_ = 0;
+  bool side_tree_ = false;  // some side root is solved by its k_fwd_tree task (tside_), not k_root_solve
   DBuf<int32_t> rflag_;
+  DBuf<uint8_t> tside_;
   hipStream_t side_ = nullptr;
   hipEvent_t ev_join_ = nullptr;
   void fwd_levels(const std::vector<SolveLevel>& V, int phase, double* b, hipStream_t s);

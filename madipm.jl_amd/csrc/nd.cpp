@@ -235,6 +235,8 @@ void refine(const Graph& g, std::vector<uint8_t>& part, double imbalance) {
 
 // Multilevel bisection of a connected graph; returns the partition of the finest graph.
 void bisect(const Graph& g0, std::vector<uint8_t>& part, Rng& rng, int threads) {
+  PhaseClock clk("  nd bisect");  // MADIPM_SYMBOLIC_TIMING: the phases of a bisection of > 1e5 vertices
+  if (g0.n < 100000) clk.on = false;
   std::vector<Graph> levels;
   std::vector<std::vector<int32_t>> maps;
   levels.push_back(g0);
@@ -245,6 +247,7 @@ void bisect(const Graph& g0, std::vector<uint8_t>& part, Rng& rng, int threads) 
     levels.push_back(std::move(c));
     maps.push_back(std::move(cmap));
   }
+  clk("coarsen");
   const Graph& gc = levels.back();
   int64_t best = -1;
   std::vector<uint8_t> trial;
@@ -257,12 +260,14 @@ void bisect(const Graph& g0, std::vector<uint8_t>& part, Rng& rng, int threads) 
       part = trial;
     }
   }
+  clk("initial partitions");
   for (int l = (int)levels.size() - 2; l >= 0; --l) {
     std::vector<uint8_t> fine(levels[l].n);
     for (int v = 0; v < levels[l].n; ++v) fine[v] = part[maps[l][v]];
     part.swap(fine);
     refine(levels[l], part, 0.05);
   }
+  clk("uncoarsen + refine");
 }
 
 // Minimum vertex cover of the cut edges (König), returned as sep[v] = 1.
@@ -473,7 +478,7 @@ struct Dissector {
   void dissect(Ctx& cx, const std::vector<int32_t>& verts, int depth, uint64_t seed, int par,
                std::vector<int32_t>& out) const {
     PhaseClock clk("  nd top");  // MADIPM_SYMBOLIC_TIMING: the top bisection and the rest
-    if (depth > 0) clk.on = false;
+    if (2 * verts.size() < (size_t)n) clk.on = false;  // the top bisection (below any component split)
     Graph g;
     induced(cx, verts, g);
     if (g.n <= opt.leaf_size || depth > 60) {
@@ -611,7 +616,9 @@ void nd_order(int n, const std::vector<int64_t>& Ap, const std::vector<int32_t>&
   for (int v = 0; v < n; ++v) (Ap[v + 1] - Ap[v] > dense ? deferred : all).push_back(v);
   out.reserve(n);
   Ctx cx(n);
+  PhaseClock clk("  nd order");
   d.dissect(cx, all, 0, opt.seed, std::max(1, opt.threads), out);
+  clk("dissection");
   out.insert(out.end(), deferred.begin(), deferred.end());
   MADIPM_REQUIRE((int)out.size() == n, "nested dissection lost vertices");
   perm.swap(out);
