@@ -6223,7 +6223,17 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       for (int64_t k = 0; ok && k < L.items; ++k) ok = rootf[sched[L.off + k]] != 0;
     }
     const char* ra = std::getenv("MADIPM_ROOT_ASYNC");
-    root_async_ = ok && !(ra && ra[0] == '0');
+    // the tail's kernel waits on the device for a kernel of the caller's stream: never where kernels
+    // are serialised (counter collection — rocprofv3 --pmc dispatches one kernel at a time, and the
+    // waiting kernel would hold the GPU until its wait times out — AMD_SERIALIZE_KERNEL,
+    // HIP_LAUNCH_BLOCKING)
+    auto set = [](const char* k) {
+      const char* v = std::getenv(k);
+      return v && v[0] && v[0] != '0';
+    };
+    const bool serial = set("ROCPROF_COUNTER_COLLECTION") || set("ROCPROF_COUNTERS") || set("AMD_SERIALIZE_KERNEL") ||
+                        set("HIP_LAUNCH_BLOCKING");
+    root_async_ = ok && !serial && !(ra && ra[0] == '0');
     if (ra && ra[0] == '2') {  // diagnostics: why (not)
       std::string k;
       for (const Launch& L : fact1_) k += std::to_string(L.kind) + "/" + std::to_string(L.items) + " ";
@@ -6373,7 +6383,7 @@ void LDLSolver::set_timing(unsigned mask) {
 }
 
 bool LDLSolver::t_begin(int kind, hipStream_t s) {
-  if (!(tmask_ >> kind & 1u)) return false;
+  if (!(tmask_ >> kind & 1u) || untimed_) return false;
   while (evs_.size() < ev_used_ + 2) {
     hipEvent_t e;  // no system-scope fence: the timestamps bracket the kernel, not a cache flush
     MADIPM_HIP(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
@@ -6594,7 +6604,11 @@ void LDLSolver::fact_phase1(const double* Kx, hipStream_t s) {
     // Lazy inertia: the root kernel stamps t1.
     ++repoch_;
     run_fact(fact1_, Kx, s, 0, side0_);
+    // not event-timed: the launch waits on the device from its enqueue (during the previous solve)
+    // until the go flag, and events would count that wait as the kernel's time
+    untimed_ = true;
     run_fact(fact1_, Kx, side_, side0_, fact1_.size(), lazy ? st_ : nullptr);
+    untimed_ = false;
     MADIPM_HIP(hipEventRecord(ev_join_, side_));
     root_pending_ = true;
     if (!lazy) join(s);  // k_inertia and the status copy below need the whole factor

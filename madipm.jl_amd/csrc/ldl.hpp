@@ -345,7 +345,7 @@ class LDLSolver : public LinSolver {
   // on the device for rflag_[0] == repoch_ (raised by the roots' assembly, fact1_[side0_ - 1], on the
   // caller's stream), then raises rflag_[2 + k] for k_root_solve; ev_join_ (recorded after it) joins
   // the host-side users (status, fact_seconds, a factorisation no solve followed)
-  bool root_async_ = false, root_pending_ = false;
+  bool root_async_ = false, root_pending_ = false, untimed_ = false;
   size_t side0_ = 0;
   int nroot_side_ = 0, repoch_ = 0;
   bool side_tree_ = false;  // some side root is solved by its k_fwd_tree task (tside_), not k_root_solve

@@ -112,3 +112,17 @@ def test_root_async_pivot_failure_reaches_the_host(name, monkeypatch):
     vals[Lw.indptr[j]] = np.nan  # its diagonal entry: a non-finite pivot
     assert ls.factorize(torch.from_numpy(vals).cuda()) != 0
     assert ls.factorize(torch.from_numpy(Lw.data.copy()).cuda()) == 0
+
+
+@pytest.mark.parametrize("var", ["ROCPROF_COUNTER_COLLECTION", "AMD_SERIALIZE_KERNEL", "HIP_LAUNCH_BLOCKING"])
+def test_root_async_off_when_kernels_serialise(var, monkeypatch):
+    """Counter collection (rocprofv3 --pmc) and the HIP serialisation knobs run one kernel at a time:
+    the tail's kernel would wait on the device for a kernel that cannot start.  The solver then keeps
+    the tail on the caller's stream (r6_ze: a --pmc pass ended in the hand-off timeout)."""
+    from madipm_amd.linear_solver import HIPLDLSolver
+    K, Lw = _k2("ex10")
+    monkeypatch.setenv("MADIPM_ROOT_ASYNC", "1")
+    monkeypatch.setenv(var, "1")
+    ls = HIPLDLSolver(K.shape[0], Lw.indptr, Lw.indices)
+    assert ls.info()["root_tail_async"] == 0
+    assert ls.factorize(torch.from_numpy(Lw.data.copy()).cuda()) == 0
