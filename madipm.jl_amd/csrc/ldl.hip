@@ -496,12 +496,10 @@ __global__ __launch_bounds__(NT) void k_tiny_factor(FrontTab T, const int32_t* _
 // Chunk sums: thread per chunk of <= kChunk sources, summed in source order.  Sources are int32
 // when the arena and K fit (IDX = int32_t), else int64.
 template <typename IDX>
-__global__ __launch_bounds__(NT) void k_asm_chunks(const int64_t* __restrict__ ids, const int64_t* __restrict__ gchunk,
-                                                   const IDX* __restrict__ gsrc, int64_t c0, int64_t n,
-                                                   const double* __restrict__ Kx, const double* __restrict__ arena,
-                                                   double* __restrict__ part) {
-  const int64_t ci = (int64_t)blockIdx.x * NT + threadIdx.x;
-  if (ci >= n) return;
+__device__ __forceinline__ void asm_chunk_sum(const int64_t* __restrict__ ids, const int64_t* __restrict__ gchunk,
+                                              const IDX* __restrict__ gsrc, int64_t c0, int64_t ci,
+                                              const double* __restrict__ Kx, const double* __restrict__ arena,
+                                              double* __restrict__ part, bool sc1) {
   const int64_t c = ids[c0 + ci];  // the chunks of the launch's chunk-path tiles (asm_chunks_lds)
   const int64_t p0 = gchunk[c], p1 = gchunk[c + 1];
   constexpr int KC = SymbolicPlan::kChunk;
@@ -518,7 +516,23 @@ __global__ __launch_bounds__(NT) void k_asm_chunks(const int64_t* __restrict__ i
 #pragma unroll
   for (int u = 0; u < KC; ++u)
     if (p0 + u < p1) v += x[u];
-  part[c] = v;
+  if (sc1)
+    __hip_atomic_store(part + c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    part[c] = v;
+}
+template <typename IDX>
+__global__ __launch_bounds__(NT) void k_asm_chunks(const int64_t* __restrict__ ids, const int64_t* __restrict__ gchunk,
+                                                   const IDX* __restrict__ gsrc, int64_t c0, int64_t n,
+                                                   const double* __restrict__ Kx, const double* __restrict__ arena,
+                                                   double* __restrict__ part, int32_t* cflag, int epoch) {
+  const int64_t ci = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (ci < n) asm_chunk_sum(ids, gchunk, gsrc, c0, ci, Kx, arena, part, cflag != nullptr);
+  if (cflag) {  // the root tail (LDLSolver::root_async_): handed to its k_assemble on the side stream
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // form R1: write-through sums drained, one flag
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(cflag + blockIdx.x, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // Phase 2: one workgroup (1024 threads) per 64x64 lower tile of F (SymbolicPlan step 10), assembled
@@ -732,10 +746,31 @@ __global__ __launch_bounds__(ANT, CU == 2 ? 8 : 4) void k_assemble(FrontTab T, c
                                                      const int32_t* __restrict__ gptr, const double* __restrict__ part,
                                                      const BigChildRec* __restrict__ brec, double* __restrict__ arena,
                                                      double* __restrict__ fscratch, const IDX* __restrict__ gsrc,
-                                                     const double* __restrict__ Kx, int32_t* go, int go_epoch) {
+                                                     const double* __restrict__ Kx, int32_t* go, int go_epoch,
+                                                     const int32_t* cwait, int ncw) {
   constexpr int WS = kAsmLdsSrc;
   __shared__ double Ts[64 * 64];
   extern __shared__ __attribute__((aligned(16))) double vals[];  // WS doubles (dynamic: past 64 KB of static LDS)
+  if (ncw > 0) {  // the root tail's assembly on the side stream: the chunk pass's blocks (main stream) first
+    if (threadIdx.x < 64) {
+      const int lane = threadIdx.x;
+      for (int q0 = 0; q0 < ncw; q0 += 64) {
+        int spins = 0;
+        for (;;) {
+          const bool ok = q0 + lane >= ncw ||
+                          __hip_atomic_load(cwait + q0 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == go_epoch;
+          if (__all(ok)) break;
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > (1 << 25)) {
+            if (lane == 0) atomicOr(T.err, kErrHandoff);
+            break;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the chunk sums, the children's blocks, K
+  }
   const SymbolicPlan::AsmTile tl = tiles[blockIdx.x];
   const int s = tl.front, ti = tl.tij & 0xffff, tj = (tl.tij >> 16) & 0x7fff;
   const bool acc = tl.tij < 0;  // SymbolicPlan::kAccumulate: F += tile (sharded top fronts, phase 2)
@@ -6253,7 +6288,12 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       MADIPM_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
       MADIPM_HIP(hipStreamCreateWithPriority(&side_, hipStreamNonBlocking, hi));
       MADIPM_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
-      rflag_.alloc(2 + 64);  // go, the assembly's tile counter, one done flag per root
+      // the roots' assembly tiles on the side stream too, behind the chunk pass's block flags
+      // (MADIPM_ROOT_ASM_SIDE=0: on the caller's stream)
+      const char* ea = std::getenv("MADIPM_ROOT_ASM_SIDE");
+      asm_side_ = fact1_[nl - 2].nchunk > 0 && !(ea && ea[0] == '0');
+      const int64_t ncb = asm_side_ ? cdiv(fact1_[nl - 2].nchunk, NT) : 0;
+      rflag_.alloc(2 + 64 + ncb);  // go, the assembly's tile counter, one done flag per root, chunk blocks
       rflag_.zero();
       // the k_fwd_tree tasks of the side roots wait for the tail themselves (supportcase10's root)
       std::vector<uint8_t> ts(std::max(ntask_, 1), 0);
@@ -6483,30 +6523,38 @@ void LDLSolver::run_fact(const std::vector<Launch>& LL, const double* Kx, hipStr
     int32_t* go = (root_async_ && &LL == &fact1_ && (li + 1 == side0_ || li == side0_)) ? rflag_.p : nullptr;
     const int32_t* list = sched_.p + L.off;
     switch (L.kind) {
-      case ASSEMBLE:
-        if (L.nchunk)
+      case ASSEMBLE: {
+        // root_async_ with asm_side_: the roots' assembly (the launch before side0_) runs its chunk pass on
+        // the caller's stream, each block raising a flag, and its tiles on side_, waiting for those flags
+        const bool split = go && asm_side_ && li + 1 == side0_;
+        const bool chunks = L.nchunk && !(split && side_phase_);
+        const bool tiles = !(split && !side_phase_);
+        int32_t* cfl = split ? rflag_.p + 2 + 64 : nullptr;
+        const int ncw = split ? (int)cdiv(L.nchunk, NT) : 0;
+        if (chunks)
           TIMED(KK_ASM_CHUNKS, L.bytes2, 0.0, L.flops2,
                 (g_src32_.p ? k_asm_chunks<int32_t><<<(unsigned)cdiv(L.nchunk, NT), NT, 0, s>>>(
-                                  chunk_ids_, g_chunk_, g_src32_, L.chunk0, L.nchunk, Kx, arena_, gpart_)
+                                  chunk_ids_, g_chunk_, g_src32_, L.chunk0, L.nchunk, Kx, arena_, gpart_, cfl, repoch_)
                             : k_asm_chunks<int64_t><<<(unsigned)cdiv(L.nchunk, NT), NT, 0, s>>>(
-                                  chunk_ids_, g_chunk_, g_src_, L.chunk0, L.nchunk, Kx, arena_, gpart_)));
-        if (g_src32_.p)
+                                  chunk_ids_, g_chunk_, g_src_, L.chunk0, L.nchunk, Kx, arena_, gpart_, cfl, repoch_)));
+        if (tiles && g_src32_.p)
           TIMED(KK_ASSEMBLE, L.bytes, 0.0, L.flops,
                 (L.items < 256 ? k_assemble<8, int32_t><<<(unsigned)L.items, ANT, 8 * kAsmLdsSrc, s>>>(
                                      T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_, g_src32_.p, Kx, go,
-                                     repoch_)
+                                     repoch_, cfl, ncw)
                                : k_assemble<2, int32_t><<<(unsigned)L.items, ANT, 8 * kAsmLdsSrc, s>>>(
                                      T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_, g_src32_.p, Kx, go,
-                                     repoch_)));
-        else
+                                     repoch_, cfl, ncw)));
+        else if (tiles)
           TIMED(KK_ASSEMBLE, L.bytes, 0.0, L.flops,
                 (L.items < 256 ? k_assemble<8, int64_t><<<(unsigned)L.items, ANT, 8 * kAsmLdsSrc, s>>>(
                                      T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_, g_src_.p, Kx, go,
-                                     repoch_)
+                                     repoch_, cfl, ncw)
                                : k_assemble<2, int64_t><<<(unsigned)L.items, ANT, 8 * kAsmLdsSrc, s>>>(
                                      T_, atiles_.p + L.off, g_ptr_, gpart_, brec_, arena_, fscratch_, g_src_.p, Kx, go,
-                                     repoch_)));
+                                     repoch_, cfl, ncw)));
         break;
+      }
       case MICRO:
         TIMED(KK_TINY, L.bytes, L.alg, L.flops,
               (k_micro_factor<<<(unsigned)cdiv(L.items, NT / MG), NT, 0, s>>>(T_, list, (int)L.items, Kx, arena_, D_,
@@ -6606,9 +6654,9 @@ void LDLSolver::fact_phase1(const double* Kx, hipStream_t s) {
     run_fact(fact1_, Kx, s, 0, side0_);
     // not event-timed: the launch waits on the device from its enqueue (during the previous solve)
     // until the go flag, and events would count that wait as the kernel's time
-    untimed_ = true;
-    run_fact(fact1_, Kx, side_, side0_, fact1_.size(), lazy ? st_ : nullptr);
-    untimed_ = false;
+    untimed_ = side_phase_ = true;
+    run_fact(fact1_, Kx, side_, asm_side_ ? side0_ - 1 : side0_, fact1_.size(), lazy ? st_ : nullptr);
+    untimed_ = side_phase_ = false;
     MADIPM_HIP(hipEventRecord(ev_join_, side_));
     root_pending_ = true;
     if (!lazy) join(s);  // k_inertia and the status copy below need the whole factor

@@ -346,6 +346,7 @@ class LDLSolver : public LinSolver {
   // caller's stream), then raises rflag_[2 + k] for k_root_solve; ev_join_ (recorded after it) joins
   // the host-side users (status, fact_seconds, a factorisation no solve followed)
   bool root_async_ = false, root_pending_ = false, untimed_ = false;
+  bool asm_side_ = false, side_phase_ = false;  // the roots' assembly tiles on side_ too; run_fact is enqueuing side_'s part
   size_t side0_ = 0;
   int nroot_side_ = 0, repoch_ = 0;
   bool side_tree_ = false;  // some side root is solved by its k_fwd_tree task (tside_), not k_root_solve
