@@ -1972,9 +1972,29 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
       for (const Op& o : ops)
         if (o.mark < 0) work += (int64_t)S.nrows[o.s] * S.nrows[o.s];
       const int T = std::max(1, std::min<int>(analysis_threads(), (int)(work / 200000)));
+      // heaviest emits first (longest-processing-time order: neos' 16 block separators take 0.15-0.6 s
+      // each and, dealt in level order, finished last on a few threads).  Each emit fills its own part:
+      // the order they run in changes nothing in the plan.
+      std::vector<int64_t> cost(ops.size(), -1);
+      for (size_t k = 0; k < ops.size(); ++k) {
+        const Op& o = ops[k];
+        if (o.mark >= 0) continue;
+        int64_t e = o.orig ? S.asm_ptr[o.s + 1] - S.asm_ptr[o.s] : 0;  // its sources (entries) estimate
+        for (int64_t qc = S.child_ptr[o.s]; qc < S.child_ptr[o.s + 1]; ++qc) {
+          const int c = S.child_list[qc];
+          if (!child_ok(c, o.which)) continue;
+          const int64_t uc = S.nrows[c] - (S.first[c + 1] - S.first[c]);
+          if (uc <= gather_max || o.which == 3) e += uc * (uc + 1) / 2;
+        }
+        cost[k] = e + (int64_t)S.nrows[o.s] * S.nrows[o.s] / 64;  // + its tiles
+      }
+      std::vector<size_t> order(ops.size());
+      std::iota(order.begin(), order.end(), (size_t)0);
+      std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return cost[a] > cost[b]; });
       auto worker = [&] {
         Scratch X;
-        for (size_t k; (k = next.fetch_add(1)) < ops.size();) {
+        for (size_t q; (q = next.fetch_add(1)) < ops.size();) {
+          const size_t k = order[q];
           const Op& o = ops[k];
           if (o.mark < 0) emit(parts[k], X, o.s, o.orig, o.which, o.acc, o.emit_empty, o.tsel);
         }
