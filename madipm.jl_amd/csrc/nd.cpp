@@ -50,7 +50,8 @@ struct Rng {
 };
 
 // Heavy-edge matching and contraction.  Returns false when the graph hardly shrinks.
-bool coarsen(const Graph& g, Graph& c, std::vector<int32_t>& cmap, Rng& rng, int threads) {
+bool coarsen(const Graph& g, Graph& c, std::vector<int32_t>& cmap, std::vector<uint64_t>& scratch, Rng& rng,
+             int threads) {
   const int n = g.n;
   std::vector<int32_t> match(n, -1), order(n);
   std::iota(order.begin(), order.end(), 0);
@@ -85,42 +86,74 @@ bool coarsen(const Graph& g, Graph& c, std::vector<int32_t>& cmap, Rng& rng, int
   std::vector<int32_t> rep(nc, -1);
   for (int v = 0; v < n; ++v)
     if (rep[cmap[v]] == -1) rep[cmap[v]] = v;
-  // contraction of coarse vertices [cv0, cv1) into (adj, ew), c.p[cv + 1] = its degree; a coarse
-  // vertex's list is its members' neighbours in adjacency order, duplicates merged
-  auto contract = [&](int cv0, int cv1, std::vector<int32_t>& adj, std::vector<int32_t>& ew) {
-    std::vector<int32_t> pos(nc, -1);
+  // Contraction: a coarse vertex's list is its members' neighbours in adjacency order, duplicates
+  // merged.  Each coarse vertex is written at its upper-bound offset (its members' degrees: the
+  // offsets sum to g's adjacency) into the scratch, ranges of coarse vertices on threads of their
+  // own, then packed.  The scratch lives for the whole bisection (sized by its finest level), so its
+  // pages fault in once: fresh per-thread buffers per level faulting in concurrently measured 2-4x
+  // slower than one thread.  The result does not depend on the thread count.
+  std::vector<int64_t> off(nc + 1, 0);
+  for (int cv = 0; cv < nc; ++cv) {
+    const int v = rep[cv], u = match[v];
+    off[cv + 1] = off[cv] + (g.p[v + 1] - g.p[v]) + (u == v ? 0 : g.p[u + 1] - g.p[u]);
+  }
+  if (scratch.size() < (size_t)off[nc]) scratch.resize(off[nc]);  // (first level: the largest)
+  uint64_t* tmp = scratch.data();  // (neighbour, weight) pairs
+  auto contract = [&](int cv0, int cv1) {
+    std::vector<int64_t> pos(nc, -1);
     for (int cv = cv0; cv < cv1; ++cv) {
       const int v = rep[cv];
       const int u = match[v];
       const int members[2] = {v, u};
-      const int64_t start = (int64_t)adj.size();
+      const int64_t start = off[cv];
+      int64_t cur = start;
+      int32_t w = 0;
       for (int k = 0; k < (u == v ? 1 : 2); ++k) {
         const int x = members[k];
-        c.vw[cv] += g.vw[x];
+        w += g.vw[x];
         for (int64_t e = g.p[x]; e < g.p[x + 1]; ++e) {
           const int cu = cmap[g.adj[e]];
           if (cu == cv) continue;
-          if (pos[cu] >= start && pos[cu] < (int64_t)adj.size() && adj[pos[cu]] == cu) {
-            ew[pos[cu]] += g.ew[e];
+          const int64_t q = pos[cu];
+          if (q >= start) {
+            tmp[q] += (uint64_t)(uint32_t)g.ew[e] << 32;
           } else {
-            pos[cu] = (int32_t)adj.size();
-            adj.push_back(cu);
-            ew.push_back(g.ew[e]);
+            pos[cu] = cur;
+            tmp[cur++] = (uint32_t)cu | ((uint64_t)(uint32_t)g.ew[e] << 32);
           }
         }
       }
-      c.p[cv + 1] = (int64_t)adj.size() - start;
+      c.vw[cv] = w;
+      c.p[cv + 1] = cur - start;
     }
   };
-  // (one thread: contracting ranges on threads and concatenating measured 2-4x slower per level on
-  // ex10's top graph — fresh per-thread buffers faulting in concurrently — so `threads` is unused)
-  (void)threads;
-  c.adj.clear();
-  c.ew.clear();
-  c.adj.reserve(g.adj.size());
-  c.ew.reserve(g.adj.size());
-  contract(0, nc, c.adj, c.ew);
+  const int T = std::max(1, std::min(threads, (int)(off[nc] / 200000)));
+  std::vector<int> cut(T + 1, nc);
+  cut[0] = 0;
+  for (int t = 1; t < T; ++t)
+    cut[t] = (int)(std::lower_bound(off.begin(), off.end(), off[nc] * t / T) - off.begin());
+  auto on_threads = [&](auto&& f) {
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back(f, cut[t], cut[t + 1]);
+    f(cut[0], cut[1]);
+    for (auto& x : th) x.join();
+  };
+  on_threads(contract);
   for (int cv = 0; cv < nc; ++cv) c.p[cv + 1] += c.p[cv];
+  c.adj.resize(c.p[nc]);
+  c.ew.resize(c.p[nc]);
+  on_threads([&](int cv0, int cv1) {
+    for (int cv = cv0; cv < cv1; ++cv) {
+      const uint64_t* src = tmp + off[cv];
+      int32_t* a = c.adj.data() + c.p[cv];
+      int32_t* ew = c.ew.data() + c.p[cv];
+      const int64_t d = c.p[cv + 1] - c.p[cv];
+      for (int64_t k = 0; k < d; ++k) {
+        a[k] = (int32_t)(uint32_t)src[k];
+        ew[k] = (int32_t)(src[k] >> 32);
+      }
+    }
+  });
   return true;
 }
 
@@ -175,24 +208,57 @@ void grow(const Graph& g, int seed, std::vector<uint8_t>& part) {
   }
 }
 
-// Boundary FM refinement with a balance bound; a few passes, best prefix kept.
-void refine(const Graph& g, std::vector<uint8_t>& part, double imbalance) {
+// Boundary FM refinement with a balance bound; a few passes, best prefix kept.  Each pass starts
+// from every vertex's gain (external - internal edge weight) and the boundary vertices, one scan of
+// the edges split over `threads` (the moves themselves are few: ~64-80 per pass, 2-3 % of a pass's
+// time on ex10's levels, the scan the rest).  The heap is built from the boundary in one go: pops
+// follow the (gain, vertex) order alone, whatever the push order.
+void refine(const Graph& g, std::vector<uint8_t>& part, double imbalance, int threads) {
   const int64_t W = g.total_vw();
   const int64_t maxw = (int64_t)((0.5 + imbalance) * W) + 1;
+  const int T = std::max(1, std::min(threads, (int)(g.adj.size() / 250000)));
+  std::vector<int> cut_v(T + 1, g.n);
+  cut_v[0] = 0;
+  for (int t = 1; t < T; ++t)
+    cut_v[t] = (int)(std::lower_bound(g.p.begin(), g.p.end(), (int64_t)g.adj.size() * t / T) - g.p.begin());
+  std::vector<int64_t> gain(g.n), ext(T);
+  std::vector<uint8_t> bnd(g.n);
+  auto scan = [&](int t) {
+    int64_t x = 0;
+    for (int v = cut_v[t]; v < cut_v[t + 1]; ++v) {
+      int64_t gv = 0, xv = 0;
+      bool b = false;
+      for (int64_t e = g.p[v]; e < g.p[v + 1]; ++e) {
+        const bool c = part[g.adj[e]] != part[v];
+        gv += c ? g.ew[e] : -g.ew[e];
+        xv += c ? g.ew[e] : 0;
+        b |= c;
+      }
+      gain[v] = gv;
+      bnd[v] = b;
+      x += xv;
+    }
+    ext[t] = x;
+  };
   int64_t cut = -1;  // the cut weight after the pass (its change is tracked by the moves: cur)
   for (int pass = 0; pass < 4; ++pass) {
     int64_t wside[2] = {0, 0};
     for (int v = 0; v < g.n; ++v) wside[part[v]] += g.vw[v];
-    std::vector<int64_t> gain(g.n, 0);
+    {
+      std::vector<std::thread> th;
+      for (int t = 1; t < T; ++t) th.emplace_back(scan, t);
+      scan(0);
+      for (auto& x : th) x.join();
+    }
+    if (cut < 0) {  // the cut before the first pass: half the external weight
+      cut = 0;
+      for (int64_t x : ext) cut += x;
+      cut /= 2;
+    }
+    std::vector<std::pair<int64_t, int>> init;
     for (int v = 0; v < g.n; ++v)
-      for (int64_t e = g.p[v]; e < g.p[v + 1]; ++e) gain[v] += (part[g.adj[e]] != part[v]) ? g.ew[e] : -g.ew[e];
-    std::priority_queue<std::pair<int64_t, int>> pq;
-    for (int v = 0; v < g.n; ++v)
-      for (int64_t e = g.p[v]; e < g.p[v + 1]; ++e)
-        if (part[g.adj[e]] != part[v]) {
-          pq.push({gain[v], v});
-          break;
-        }
+      if (bnd[v]) init.emplace_back(gain[v], v);
+    std::priority_queue<std::pair<int64_t, int>> pq(std::less<std::pair<int64_t, int>>(), std::move(init));
     std::vector<uint8_t> locked(g.n, 0);
     std::vector<int> moves;
     int64_t cur = 0, best = 0;
@@ -227,8 +293,7 @@ void refine(const Graph& g, std::vector<uint8_t>& part, double imbalance) {
     }
     for (size_t k = moves.size(); k > best_len; --k) part[moves[k - 1]] ^= 1;  // roll back
     if (best == 0) break;
-    if (cut < 0) cut = cut_weight(g, part);  // once; then updated by each pass's kept moves
-    else cut += best;
+    cut += best;  // (each move changes the cut by exactly -gain: cur tracks it)
     if (-best * 200 < cut) break;  // converged (< 0.5 % gain)
   }
 }
@@ -237,23 +302,25 @@ void refine(const Graph& g, std::vector<uint8_t>& part, double imbalance) {
 void bisect(const Graph& g0, std::vector<uint8_t>& part, Rng& rng, int threads) {
   PhaseClock clk("  nd bisect");  // MADIPM_SYMBOLIC_TIMING: the phases of a bisection of > 1e5 vertices
   if (g0.n < 100000) clk.on = false;
-  std::vector<Graph> levels;
+  std::vector<Graph> coarse;  // levels 1, 2, ... (level 0: g0 itself)
   std::vector<std::vector<int32_t>> maps;
-  levels.push_back(g0);
-  while (levels.back().n > 120) {
+  std::vector<uint64_t> scratch;
+  auto level = [&](int l) -> const Graph& { return l == 0 ? g0 : coarse[l - 1]; };
+  while (level((int)coarse.size()).n > 120) {
     Graph c;
     std::vector<int32_t> cmap;
-    if (!coarsen(levels.back(), c, cmap, rng, threads)) break;
-    levels.push_back(std::move(c));
+    if (!coarsen(level((int)coarse.size()), c, cmap, scratch, rng, threads)) break;
+    coarse.push_back(std::move(c));
     maps.push_back(std::move(cmap));
   }
+  std::vector<uint64_t>().swap(scratch);
   clk("coarsen");
-  const Graph& gc = levels.back();
+  const Graph& gc = level((int)coarse.size());
   int64_t best = -1;
   std::vector<uint8_t> trial;
   for (int t = 0; t < 8; ++t) {
     grow(gc, (int)(rng.next() % gc.n), trial);
-    refine(gc, trial, 0.05);
+    refine(gc, trial, 0.05, 1);
     const int64_t cw = cut_weight(gc, trial);
     if (best < 0 || cw < best) {
       best = cw;
@@ -261,11 +328,11 @@ void bisect(const Graph& g0, std::vector<uint8_t>& part, Rng& rng, int threads) 
     }
   }
   clk("initial partitions");
-  for (int l = (int)levels.size() - 2; l >= 0; --l) {
-    std::vector<uint8_t> fine(levels[l].n);
-    for (int v = 0; v < levels[l].n; ++v) fine[v] = part[maps[l][v]];
+  for (int l = (int)coarse.size() - 1; l >= 0; --l) {
+    std::vector<uint8_t> fine(level(l).n);
+    for (int v = 0; v < level(l).n; ++v) fine[v] = part[maps[l][v]];
     part.swap(fine);
-    refine(levels[l], part, 0.05);
+    refine(level(l), part, 0.05, threads);
   }
   clk("uncoarsen + refine");
 }

@@ -1055,7 +1055,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
   int32_t* eb = eb_buf.get();
   auto member_col = [&](int j) { return lb_member(col2sn[pinv[j]]); };
   int TA = analysis_threads();
-  if (nnz < ((int64_t)1 << 22) || (int64_t)TA * (ns + N) > (int64_t)1 << 27) TA = 1;
+  if (nnz < ((int64_t)1 << 19) || (int64_t)TA * (ns + N) > (int64_t)1 << 27) TA = 1;
   std::vector<std::vector<int64_t>> acnt(TA, std::vector<int64_t>(ns + 1, 0));
   par_columns(N, colptr, TA, [&](int t, int j0, int j1) {
     int64_t* cnt_t = acnt[t].data();

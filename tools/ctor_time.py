@@ -1,26 +1,28 @@
-"""Construction time of MPCSolver on one config (run on the GPU box, MADIPM_SYMBOLIC_TIMING=1 for the
-phases): python tools/ctor_time.py [config]"""
+"""Wall time of MPCSolver construction (bench.py's `analysis_s`) per bench config on the GPU box, with
+each construction phase on stderr (MADIPM_SYMBOLIC_TIMING=1 python tools/ctor_time.py ex10 neos).
+As in bench.py, torch's CUDA context exists before the first construction; every config is
+constructed twice (the first construction of the process pays one-off runtime set-up)."""
+import os
 import sys
 import time
 
-sys.path[:0] = [".", "madipm.jl_amd"]
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "madipm.jl_amd"))
 import torch  # noqa: E402
 
-torch.cuda.set_device(0)
+import bench  # noqa: E402
+from madipm_amd import MPCSolver  # noqa: E402
 from madipm_amd import _lib  # noqa: E402
 
-_lib.madipm_set_device(0)
-import bench  # noqa: E402
-
-cfg = sys.argv[1] if len(sys.argv) > 1 else "dense_qp"
-t = time.perf_counter()
-qp, _ = bench.build_problem(cfg)
-print("build", round(time.perf_counter() - t, 2), flush=True)
-from madipm_amd import MPCSolver  # noqa: E402
-
-t = time.perf_counter()
-s = MPCSolver(qp, **bench.solver_opts(), **({"ordering": 0} if cfg.startswith("dense_qp") else {}))
-print("ctor", round(time.perf_counter() - t, 2), flush=True)
-t = time.perf_counter()
-del s
-print("del", round(time.perf_counter() - t, 2), flush=True)
+torch.cuda.set_device(0)
+_lib.check(_lib.madipm_set_device(0), "madipm_set_device")
+torch.zeros(1, device="cuda")
+for name in sys.argv[1:]:
+    qp, _ = bench.build_problem(name)
+    for rep in range(2):
+        t = time.perf_counter()
+        s = MPCSolver(qp, **bench.solver_opts())
+        dt = time.perf_counter() - t
+        print(f"{name} ctor {dt:.3f} s", flush=True)
+        print(f"{name} ctor {dt:.3f} s", file=sys.stderr, flush=True)
+        del s
