@@ -4688,9 +4688,11 @@ constexpr int RSN = 1024;
 __global__ __launch_bounds__(RSN) void k_root_solve(FrontTab T, const int32_t* __restrict__ fronts,
                                                     const double* __restrict__ arena, double* b, double* xi,
                                                     const double* __restrict__ Dg, int32_t* tflags, int epoch,
-                                                    const int32_t* rdone, int nrd, int repoch) {
+                                                    const int32_t* rdone, int nrd, int repoch, int64_t* dbg) {
   extern __shared__ __attribute__((aligned(16))) double Ls[];
   __shared__ double part[4 * SMALL_SOLVE_MAX], inits[SMALL_SOLVE_MAX];
+  int64_t* dg = dbg ? dbg + 8 * blockIdx.x : nullptr;  // MADIPM_TREE_DEBUG: phase stamps
+  if (dg && threadIdx.x == 0) dg[0] = wall_clock64();
   const int s = fronts[blockIdx.x];
   const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -4736,6 +4738,7 @@ __global__ __launch_bounds__(RSN) void k_root_solve(FrontTab T, const int32_t* _
     part[4 * i + k] = c;
     if (k == 0) inits[i] = init;
   }
+  if (dg && tid == 0) dg[1] = wall_clock64();
   if (nrd > 0) {  // the root tail on the side stream (LDLSolver::root_async_): every root factorised
     if (tid < 64) {
       int spins = 0;
@@ -4752,9 +4755,14 @@ __global__ __launch_bounds__(RSN) void k_root_solve(FrontTab T, const int32_t* _
     }
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (dg && tid == 0) dg[2] = wall_clock64();
     factor_loads();
   }
   __syncthreads();  // the panel and the partial sums
+  if (dg && tid == 0) {
+    if (nrd == 0) dg[2] = dg[1];
+    dg[3] = wall_clock64();
+  }
   if (tid < 64) {
     double v[3];
 #pragma unroll
@@ -4763,9 +4771,11 @@ __global__ __launch_bounds__(RSN) void k_root_solve(FrontTab T, const int32_t* _
       v[h] = (ii < r) ? ((part[4 * ii] + part[4 * ii + 1]) + (part[4 * ii + 2] + part[4 * ii + 3])) + inits[ii] : 0.0;
     }
     fwd_subst_t(v, Ls, ldt, r, w, lane);
+    if (dg && tid == 0) dg[4] = wall_clock64();
 #pragma unroll
     for (int h = 0; h < 3; ++h) v[h] = (lane + 64 * h < w) ? v[h] / dpiv[h] : 0.0;
     bwd_subst_t(v, Ls, ldt, w, lane);
+    if (dg && tid == 0) dg[5] = wall_clock64();
 #pragma unroll
     for (int h = 0; h < 3; ++h) {
       const int j = lane + 64 * h;
@@ -4775,6 +4785,7 @@ __global__ __launch_bounds__(RSN) void k_root_solve(FrontTab T, const int32_t* _
       }
     }
     publish_sc1(&tflags[s], epoch + 1);  // the backward epoch: k_bwd_tree's children of the root wait on it
+    if (dg && tid == 0) dg[6] = wall_clock64();
   }
 }
 
@@ -5380,6 +5391,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     T_.lds_cap = ftree_lds_;
     if (const char* e = std::getenv("MADIPM_DEBUG_LDS_SHRINK")) T_.lds_cap -= std::atoi(e);
     auto up = [](DBuf<int32_t>& d, const std::vector<int32_t>& v) { d.upload(v.empty() ? std::vector<int32_t>{0} : v); };
+    clk("  tree tables");
     // fold helpers: a front with two or more leaf batches hands the first half of them to a helper
     // ticket (before every front's; the helpers with the most batches first), folds the rest itself
     // and adds the helper's image after its waits (MADIPM_FOLD_HELP=0: no helpers)
@@ -5408,9 +5420,10 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       std::vector<uint16_t> hdst;  // per helper: the sorted LDS destinations its batches' products reach
       int64_t img = 0;
       // the run-end entries of a batch's product chunks name every destination it writes (a parked
-      // continuation ends at its run's destination too): the image holds exactly those
-      auto dests = [&](int b0, int b1, std::vector<uint16_t>& out) {
-        std::vector<int32_t> v;
+      // continuation ends at its run's destination too): the image holds exactly those, ascending.
+      // Helpers are independent: their lists are built on threads (marks over the 16-bit LDS space,
+      // then the distinct ones sorted), then appended in ticket order.
+      auto dests = [&](int b0, int b1, std::vector<uint8_t>& mark, std::vector<uint16_t>& out) {
         for (int b = b0; b < b1; ++b) {
           const int64_t po = S.fold_poff[b];
           const int len = S.fold_plen[b];
@@ -5419,28 +5432,46 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
             for (int k = 0; k < len; ++k) {
               const uint32_t e = S.fold_prod[po + (int64_t)SymbolicPlan::kFoldThreads * k + t];
               d += (int)((e >> 24) & 127u);
-              if ((int32_t)e < 0) v.push_back(d);
+              if ((int32_t)e < 0) {
+                MADIPM_REQUIRE(d >= 0 && d < 65536, "fold helper: LDS destination beyond 16 bits");
+                if (!mark[d]) {
+                  mark[d] = 1;
+                  out.push_back((uint16_t)d);
+                }
+              }
             }
           }
         }
-        std::sort(v.begin(), v.end());
-        v.erase(std::unique(v.begin(), v.end()), v.end());
-        for (int x : v) {
-          MADIPM_REQUIRE(x >= 0 && x < 65536, "fold helper: LDS destination beyond 16 bits");
-          out.push_back((uint16_t)x);
-        }
-        return (int32_t)v.size();
+        std::sort(out.begin(), out.end());
+        for (uint16_t x : out) mark[x] = 0;
       };
       if (!S.fold_bptr.empty())
         for (int f = 0; f < ns; ++f) fst[f] = start(S.fold_bptr[f], S.fold_bptr[f + 1]);
+      std::vector<std::array<int, 3>> cand;  // (front, first batch, end of the helper's batches), ticket order
       for (int f : ord) {
         if (!on || !S.absorb[f]) continue;
         const int b0 = S.fold_bptr[f], nb = S.fold_bptr[f + 1] - b0;
         if (nb < min_nb) continue;
-        const int hb1 = b0 + std::max(1, std::min(nb - 1, nb * share4 / 4));
+        cand.push_back({f, b0, b0 + std::max(1, std::min(nb - 1, nb * share4 / 4))});
+      }
+      std::vector<std::vector<uint16_t>> cd(cand.size());
+      {
+        std::atomic<size_t> next{0};
+        auto work = [&] {
+          std::vector<uint8_t> mark(65536, 0);
+          for (size_t k; (k = next.fetch_add(1)) < cand.size();) dests(cand[k][1], cand[k][2], mark, cd[k]);
+        };
+        const int nt = std::max(1, std::min<int>(analysis_threads(), (int)(cand.size() / 8)));
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; ++t) th.emplace_back(work);
+        work();
+        for (auto& x : th) x.join();
+      }
+      for (size_t k = 0; k < cand.size(); ++k) {
         const int64_t dofs = (int64_t)hdst.size();
-        const int32_t nimg = dests(b0, hb1, hdst);
-        hv.push_back(FoldHelp{f, 0, img, dofs, nimg, 0, start(b0, hb1)});
+        const int32_t nimg = (int32_t)cd[k].size();
+        hdst.insert(hdst.end(), cd[k].begin(), cd[k].end());
+        hv.push_back(FoldHelp{cand[k][0], 0, img, dofs, nimg, 0, start(cand[k][1], cand[k][2])});
         img += (nimg + 1) & ~1LL;
       }
       std::stable_sort(hv.begin(), hv.end(),
@@ -5466,6 +5497,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       T_.fimg = fimg_;
       dptr.insert(dptr.begin(), (size_t)nfhelp_, 0);  // dep_ptr by ticket: the helpers' ranges are empty
     }
+    clk("  fold helpers");
     up(ft_order_, ord);
     up(ft_dptr_, dptr);
     up(ft_dep_, dl);
@@ -5528,6 +5560,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   }
 
   // ---- factorisation launch schedules (phase 1: this shard's subtrees; phase 2: the top fronts)
+  clk("  fold table uploads");
   std::vector<int32_t> sched;
   auto align2 = [&]() {
     if (sched.size() & 1) sched.push_back(0);
@@ -5926,6 +5959,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     }
     if (phase == 1 && NL == 1 && nftree_) ftree_launch();
   };
+  clk("  launch plans (before build_fact)");
   build_fact(1, fact1_);
   if (S.nshards > 1) {
     asm_launch(NL, fact1_);  // top fronts, external part (all-reduced next)
@@ -5969,6 +6003,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
   }
 
   // ---- solve schedules: per level, small fronts (wave per front) and big fronts (task queues)
+  clk("  build_fact + dag tables");
   std::vector<uint8_t> rootf(std::max(ns, 1), 0);  // roots solved by k_root_solve (1) / a k_fwd_tree task (2)
   std::vector<int32_t> tfront;                      // tree-solve task -> its (top) front
   {
@@ -6307,6 +6342,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
       tside_.upload(ts);
     }
   }
+  clk("  tree solve tables + root tail");
   sched_.upload(sched.empty() ? std::vector<int32_t>{0} : sched);
   arena_.alloc(std::max<int64_t>(S.arena_size, 2));
   if (S.nshards > 1) {  // top fronts: the strict upper triangles are never written, keep them 0
@@ -6328,6 +6364,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     xpack_.alloc(po + 4 * S.nshards);
     xpack_.zero();
   }
+  clk("  sched upload + arena");
   D_.alloc(std::max(S.N, 1));
   xi_.alloc(std::max(S.N, 1));
   uvec_.alloc(std::max<int64_t>(S.uvec_size, 1));
@@ -6384,6 +6421,7 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
     }
     attr_done = true;
   }
+  clk("  buffers + attributes");
   MADIPM_HIP(hipDeviceSynchronize());
   clk("schedules + workspace");
 }
@@ -6945,7 +6983,19 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
         TIMED(KK_FWD_TREE, nlo > 0 ? 0.0 : tree_bytes_, nlo > 0 ? 0.0 : tree_alg_, nlo > 0 ? 0.0 : tree_flops_,
               (k_root_solve<<<(unsigned)nroot_task_, RSN, root_lds_, s>>>(
                   T_, tc_list_.p + nlo, arena_, b, xi_, D_, tflags_, efwd, rflag_.p ? rflag_.p + 2 : nullptr,
-                  root_pending_ ? nroot_side_ : 0, repoch_)));
+                  root_pending_ ? nroot_side_ : 0, repoch_, tdbg_.p ? tdbg_.p + 8 * nlo : nullptr)));
+      if (nroot_task_ && tdbg_.p) {  // MADIPM_TREE_DEBUG: the root solve's phases
+        std::vector<int64_t> h(8 * nroot_task_);
+        MADIPM_HIP(hipMemcpyAsync(h.data(), tdbg_.p + 8 * nlo, h.size() * 8, hipMemcpyDeviceToHost, s));
+        MADIPM_HIP(hipMemsetAsync(tdbg_.p + 8 * nlo, 0, h.size() * 8, s));  // not tree tasks' stamps
+        MADIPM_HIP(hipStreamSynchronize(s));
+        for (int q = 0; q < nroot_task_; ++q) {
+          const int64_t* d = &h[8 * q];
+          fprintf(stderr, "root solve %d: gather %.2f  wait %.2f  panel %.2f  fwd %.2f  bwd %.2f  store %.2f us\n", q,
+                  (d[1] - d[0]) * 0.01, (d[2] - d[1]) * 0.01, (d[3] - d[2]) * 0.01, (d[4] - d[3]) * 0.01,
+                  (d[5] - d[4]) * 0.01, (d[6] - d[5]) * 0.01);
+        }
+      }
       root_pending_ = false;  // (root_async_) the first k_root_solve after a factorisation waited for its tail
     }
     if (lev == 0 && phase == 0 && ntree_ && tdbg_.p)

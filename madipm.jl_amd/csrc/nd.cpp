@@ -22,6 +22,8 @@
 #include <queue>
 #include <thread>
 #include <cstdlib>
+#include <utility>
+#include <memory>
 #include <vector>
 
 #include "common.hpp"
@@ -31,10 +33,35 @@ namespace madipm {
 
 namespace {
 
+// std::allocator whose value-less construct leaves the element uninitialised: resize() of the big
+// per-level arrays then costs no zero pass, and their pages first fault in on the threads that fill them
+template <class T>
+struct UninitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = UninitAlloc<U>;
+  };
+  UninitAlloc() = default;
+  template <class U>
+  UninitAlloc(const UninitAlloc<U>&) noexcept {}
+  template <class U, class... A>
+  void construct(U* q, A&&... a) {
+    ::new ((void*)q) U(std::forward<A>(a)...);
+  }
+  template <class U>
+  void construct(U* q) noexcept {
+    ::new ((void*)q) U;
+  }
+};
+template <class T>
+using RawVec = std::vector<T, UninitAlloc<T>>;
+
 struct Graph {
   int n = 0;
   std::vector<int64_t> p;
-  std::vector<int32_t> adj, ew, vw;
+  RawVec<int32_t> adj, ew;
+  std::vector<int32_t> vw;
+  bool unit_ew = false;  // every edge weight 1 (an induced subgraph; coarse graphs: false)
   int64_t total_vw() const { return std::accumulate(vw.begin(), vw.end(), (int64_t)0); }
 };
 
@@ -50,7 +77,7 @@ struct Rng {
 };
 
 // Heavy-edge matching and contraction.  Returns false when the graph hardly shrinks.
-bool coarsen(const Graph& g, Graph& c, std::vector<int32_t>& cmap, std::vector<uint64_t>& scratch, Rng& rng,
+bool coarsen(const Graph& g, Graph& c, std::vector<int32_t>& cmap, RawVec<uint64_t>& scratch, Rng& rng,
              int threads) {
   const int n = g.n;
   std::vector<int32_t> match(n, -1), order(n);
@@ -59,11 +86,19 @@ bool coarsen(const Graph& g, Graph& c, std::vector<int32_t>& cmap, std::vector<u
   for (int v : order) {
     if (match[v] != -1) continue;
     int best = -1, bw = -1;
-    for (int64_t e = g.p[v]; e < g.p[v + 1]; ++e) {
-      const int u = g.adj[e];
-      if (match[u] == -1 && g.ew[e] > bw) {
-        bw = g.ew[e];
-        best = u;
+    if (g.unit_ew) {  // the heaviest edge is the first one to an unmatched neighbour (ties: the first)
+      for (int64_t e = g.p[v]; e < g.p[v + 1]; ++e)
+        if (match[g.adj[e]] == -1) {
+          best = g.adj[e];
+          break;
+        }
+    } else {
+      for (int64_t e = g.p[v]; e < g.p[v + 1]; ++e) {
+        const int u = g.adj[e];
+        if (match[u] == -1 && g.ew[e] > bw) {
+          bw = g.ew[e];
+          best = u;
+        }
       }
     }
     if (best == -1) {
@@ -304,7 +339,7 @@ void bisect(const Graph& g0, std::vector<uint8_t>& part, Rng& rng, int threads) 
   if (g0.n < 100000) clk.on = false;
   std::vector<Graph> coarse;  // levels 1, 2, ... (level 0: g0 itself)
   std::vector<std::vector<int32_t>> maps;
-  std::vector<uint64_t> scratch;
+  RawVec<uint64_t> scratch;
   auto level = [&](int l) -> const Graph& { return l == 0 ? g0 : coarse[l - 1]; };
   while (level((int)coarse.size()).n > 120) {
     Graph c;
@@ -313,7 +348,7 @@ void bisect(const Graph& g0, std::vector<uint8_t>& part, Rng& rng, int threads) 
     coarse.push_back(std::move(c));
     maps.push_back(std::move(cmap));
   }
-  std::vector<uint64_t>().swap(scratch);
+  RawVec<uint64_t>().swap(scratch);
   clk("coarsen");
   const Graph& gc = level((int)coarse.size());
   int64_t best = -1;
@@ -489,21 +524,56 @@ struct Dissector {
   Dissector(const std::vector<int64_t>& p, const std::vector<int32_t>& i, const NDOptions& o, int nn)
       : Ap(p), Ai(i), opt(o), n(nn) {}
 
-  void induced(Ctx& cx, const std::vector<int32_t>& verts, Graph& g) const {
+  // (large subgraphs: degrees counted, then the lists filled, by vertex ranges on `par` threads)
+  void induced(Ctx& cx, const std::vector<int32_t>& verts, Graph& g, int par = 1) const {
     std::vector<int32_t>& loc = cx.loc;
     for (size_t k = 0; k < verts.size(); ++k) loc[verts[k]] = (int32_t)k;
     g.n = (int)verts.size();
     g.p.assign(g.n + 1, 0);
     g.adj.clear();
-    for (int k = 0; k < g.n; ++k) {
-      const int v = verts[k];
-      for (int64_t e = Ap[v]; e < Ap[v + 1]; ++e) {
-        const int u = loc[Ai[e]];
-        if (u >= 0 && u != k) g.adj.push_back(u);
+    const int T = g.n >= 50000 ? std::max(1, std::min(par, g.n / 25000)) : 1;
+    if (T == 1) {
+      for (int k = 0; k < g.n; ++k) {
+        const int v = verts[k];
+        for (int64_t e = Ap[v]; e < Ap[v + 1]; ++e) {
+          const int u = loc[Ai[e]];
+          if (u >= 0 && u != k) g.adj.push_back(u);
+        }
+        g.p[k + 1] = (int64_t)g.adj.size();
       }
-      g.p[k + 1] = (int64_t)g.adj.size();
+    } else {
+      auto on_threads = [&](auto&& f) {
+        std::vector<std::thread> th;
+        for (int t = 1; t < T; ++t) th.emplace_back(f, (int)((int64_t)g.n * t / T), (int)((int64_t)g.n * (t + 1) / T));
+        f(0, g.n / T);
+        for (auto& x : th) x.join();
+      };
+      on_threads([&](int k0, int k1) {
+        for (int k = k0; k < k1; ++k) {
+          const int v = verts[k];
+          int64_t d = 0;
+          for (int64_t e = Ap[v]; e < Ap[v + 1]; ++e) {
+            const int u = loc[Ai[e]];
+            d += u >= 0 && u != k;
+          }
+          g.p[k + 1] = d;
+        }
+      });
+      for (int k = 0; k < g.n; ++k) g.p[k + 1] += g.p[k];
+      g.adj.resize(g.p[g.n]);
+      on_threads([&](int k0, int k1) {
+        for (int k = k0; k < k1; ++k) {
+          const int v = verts[k];
+          int64_t q = g.p[k];
+          for (int64_t e = Ap[v]; e < Ap[v + 1]; ++e) {
+            const int u = loc[Ai[e]];
+            if (u >= 0 && u != k) g.adj[q++] = u;
+          }
+        }
+      });
     }
     g.ew.assign(g.adj.size(), 1);
+    g.unit_ew = true;
     g.vw.assign(g.n, 1);
     for (int v : verts) loc[v] = -1;
   }
@@ -511,7 +581,7 @@ struct Dissector {
   void leaf(const std::vector<int32_t>& verts, const Graph& g, std::vector<int32_t>& out) const {
     std::vector<int32_t> lp;
     if (g.n > 2) {
-      amd_order(g.n, g.p, g.adj, lp, opt.dense_alpha);
+      amd_order(g.n, g.p, std::vector<int32_t>(g.adj.begin(), g.adj.end()), lp, opt.dense_alpha);
     } else {
       lp.resize(g.n);
       std::iota(lp.begin(), lp.end(), 0);
@@ -547,7 +617,7 @@ struct Dissector {
     PhaseClock clk("  nd top");  // MADIPM_SYMBOLIC_TIMING: the top bisection and the rest
     if (2 * verts.size() < (size_t)n) clk.on = false;  // the top bisection (below any component split)
     Graph g;
-    induced(cx, verts, g);
+    induced(cx, verts, g, par);
     if (g.n <= opt.leaf_size || depth > 60) {
       leaf(verts, g, out);
       return;
