@@ -27,7 +27,8 @@ typedef void* madipm_stream_t; /* hipStream_t */
 int madipm_version(void);                 /* MAJOR*10000 + MINOR*100 + PATCH */
 const char* madipm_last_error(void);
 int madipm_device_count(void);            /* hipGetDeviceCount; 0 when no GPU is present */
-int madipm_set_device(int32_t dev);       /* hipSetDevice for the calling thread (one process per GPU) */
+int madipm_set_device(int32_t dev);       /* hipSetDevice for the calling thread (one process per GPU),
+                                            and the device's context created */
 
 /* ------------------------------------------------------------------ symbolic analysis (host)
  * Replaces the symbolic phase run by the linear-solver constructor `linear_solver(aug_com; opt)`

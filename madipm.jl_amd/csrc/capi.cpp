@@ -90,6 +90,7 @@ const char* madipm_last_error(void) { return last_error(); }
 int madipm_set_device(int32_t dev) {
   MADIPM_API_BEGIN
   MADIPM_HIP(hipSetDevice(dev));
+  MADIPM_HIP(hipFree(nullptr));  // the device's context now, not inside the first solver construction
   return 0;
   MADIPM_API_END
 }

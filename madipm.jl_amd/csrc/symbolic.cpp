@@ -512,7 +512,7 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     // Nested dissection is randomised (matchings, initial partitions).  On graphs with more than
     // kBigAdj adjacency entries its fill varies with the seed far more than with anything else (neos
     // stand-in: 240-323 GFLOP over seeds; ex10 and supportcase10, below the bound: within 0.5 %), so
-    // there it runs with kNdSeeds fixed seeds at once — each with a share of the analysis threads —
+    // there it runs with kNdSeeds fixed seeds at once — each free to use all the analysis threads —
     // and the order with the fewest flops is kept (lowest seed on ties: the same choice whatever the
     // thread count).  ordering = auto adds AMD (one thread) beside ND and keeps the overall best; AMD
     // is skipped above kBigAdj, where it is the slowest step of the analysis and ND wins anyway on
@@ -530,7 +530,10 @@ void symbolic_analyze(int N, const int64_t* colptr, const int32_t* rowval, const
     std::vector<OrderAnalysis> B(nseeds);
     OrderAnalysis A;
     const int T = analysis_threads();
-    const int per = std::max(1, (T - (use_amd ? 1 : 0)) / std::max(1, nseeds));
+    // every seed may use all the threads: the seeds finish ~0.5 s apart on neos, and a fixed share
+    // each left the early finishers' cores idle (box, neos symbolic: 2.27-2.44 s with T / 4 threads
+    // per seed, 2.03-2.13 s with T; the order does not depend on the thread count)
+    const int per = std::max(1, T - (use_amd ? 1 : 0));
     auto run_nd = [&](int k) {
       NDOptions nopt;
       nopt.dense_alpha = opt.dense_alpha;
