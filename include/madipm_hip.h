@@ -28,7 +28,8 @@ int madipm_version(void);                 /* MAJOR*10000 + MINOR*100 + PATCH */
 const char* madipm_last_error(void);
 int madipm_device_count(void);            /* hipGetDeviceCount; 0 when no GPU is present */
 int madipm_set_device(int32_t dev);       /* hipSetDevice for the calling thread (one process per GPU),
-                                            and the device's context created */
+                                            and the runtime's one-off device set-up done
+                                            (context, first stream) */
 
 /* ------------------------------------------------------------------ symbolic analysis (host)
  * Replaces the symbolic phase run by the linear-solver constructor `linear_solver(aug_com; opt)`

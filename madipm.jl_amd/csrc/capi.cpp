@@ -90,7 +90,13 @@ const char* madipm_last_error(void) { return last_error(); }
 int madipm_set_device(int32_t dev) {
   MADIPM_API_BEGIN
   MADIPM_HIP(hipSetDevice(dev));
-  MADIPM_HIP(hipFree(nullptr));  // the device's context now, not inside the first solver construction
+  // the runtime's one-off device set-up now (context, and the first stream of the process: 0.14 s on
+  // the box), not inside the first solver construction — as the reference's CUDA initialisation
+  // happens in its host-to-device conversion of the QP, before MPCSolver (benchmarks_gpu.jl:33-37)
+  MADIPM_HIP(hipFree(nullptr));
+  hipStream_t s = nullptr;
+  MADIPM_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  MADIPM_HIP(hipStreamDestroy(s));
   return 0;
   MADIPM_API_END
 }

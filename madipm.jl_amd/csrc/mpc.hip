@@ -1491,14 +1491,15 @@ static void csr_from_coo(int nrow, const std::vector<int32_t>& r, const std::vec
 
 MPCSolver::MPCSolver(const madipm_qp& qp, const madipm_options& opt, Comm* comm) : opt_(opt), comm_(comm) {
   const double t0 = now();
+  PhaseClock clk("MPCSolver");
   MADIPM_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  clk("stream");
   // state mirror + publication counter on their own line: coherent host memory, written by k_publish
   constexpr size_t seq_off = (sizeof(DevState) + 63) / 64 * 64;
   MADIPM_HIP(hipHostMalloc((void**)&hst_, seq_off + 64, hipHostMallocCoherent));
   std::memset((void*)hst_, 0, seq_off + 64);
   hseq_ = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(hst_) + seq_off);
-  PhaseClock clk("MPCSolver");
-  clk("stream + host state");
+  clk("host state");
   setup_host(qp);
   clk("setup_host (its locals freed)");
   t_init_ = now() - t0;
