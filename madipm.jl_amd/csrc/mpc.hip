@@ -218,6 +218,52 @@ __device__ __forceinline__ double gdot(const DCsr& A, int64_t row, const double*
   return s;
 }
 
+// gdot<G>(A, ra, xa) and gdot<G>(B, rb, xb) at once (a primal row's H and J^T parts): both rows'
+// extents, then each trip's entries and gathers of both, issued before either is summed — one chain
+// of dependent loads instead of two back to back.  Each sum in gdot's own order (same bits).
+template <int G>
+__device__ __forceinline__ void gdot2(const DCsr& A, int64_t ra, const double* __restrict__ xa, const DCsr& B,
+                                      int64_t rb, const double* __restrict__ xb, double& sa, double& sb) {
+  const int gl = threadIdx.x & (G - 1);
+  const int64_t a1 = A.rp[ra + 1], b1 = B.rp[rb + 1];
+  int64_t qa = A.rp[ra] + gl, qb = B.rp[rb] + gl;
+  sa = 0.0;
+  sb = 0.0;
+  while (qa < a1 || qb < b1) {
+    const bool ta = qa < a1, tb = qb < b1;
+    double va = 0.0, va2 = 0.0, ya = 0.0, ya2 = 0.0, vb = 0.0, vb2 = 0.0, yb = 0.0, yb2 = 0.0;
+    if (ta) {
+      const int64_t q2 = min(qa + G, a1 - 1);
+      va = A.v[qa];
+      va2 = A.v[q2];
+      ya = xa[A.ci[qa]];
+      ya2 = xa[A.ci[q2]];
+    }
+    if (tb) {
+      const int64_t q2 = min(qb + G, b1 - 1);
+      vb = B.v[qb];
+      vb2 = B.v[q2];
+      yb = xb[B.ci[qb]];
+      yb2 = xb[B.ci[q2]];
+    }
+    if (ta) {
+      sa = fma(va, ya, sa);
+      sa = fma((qa + G < a1) ? va2 : 0.0, ya2, sa);
+      qa += 2 * G;
+    }
+    if (tb) {
+      sb = fma(vb, yb, sb);
+      sb = fma((qb + G < b1) ? vb2 : 0.0, yb2, sb);
+      qb += 2 * G;
+    }
+  }
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) {
+    sa += __shfl_xor(sa, o, G);
+    sb += __shfl_xor(sb, o, G);
+  }
+}
+
 // ------------------------------------------------------------------ KKT diagonal (kernels.jl:124-149)
 // K2 (set_aug_diagonal! for SparseKKTSystem, kernels.jl:124-136): pr_diag into the K2 diagonal.
 // K2.5 (kernels.jl:139-149 + MadNLP._set_aug_diagonal! [EXT]): the primal block is scaled
@@ -559,7 +605,9 @@ __global__ __launch_bounds__(NT) void k_residual(DV D, double dw, double dc, int
     const double pl = D.p[kl >= 0 ? n + m + kl : i], llo = D.l_lower[kl0], ldi = D.l_diag[kl0];
     const double pu = D.p[ku >= 0 ? n + m + nlb + ku : i], ulo = D.u_lower[ku0], udi = D.u_diag[ku0];
     if (i < n) {
-      const double hj = gdot<G>(D.H, i, D.d) + gdot<G>(D.JT, i, D.d + n);
+      double hd, jd;
+      gdot2<G>(D.H, i, D.d, D.JT, i, D.d + n, hd, jd);
+      const double hj = hd + jd;
       if (!lead) continue;
       const double dx = dxi;
       double kv = hj + dw * dx;
@@ -702,8 +750,8 @@ __global__ __launch_bounds__(NT) void k_eval(DV D, int slot) {
   double op = 0.0;
   GROUP_LOOP(i, n + D.m, G) {
     if (i < n) {
-      const double hx = gdot<G>(D.H, i, D.x);
-      const double jy = gdot<G>(D.JT, i, D.y);
+      double hx, jy;
+      gdot2<G>(D.H, i, D.x, D.JT, i, D.y, hx, jy);
       if (!lead) continue;
       const double x = D.x[i];
       const double g = D.cs[i] + D.gfix[i];
