@@ -4688,19 +4688,23 @@ constexpr int RSN = 1024;
 __global__ __launch_bounds__(RSN) void k_root_solve(FrontTab T, const int32_t* __restrict__ fronts,
                                                     const double* __restrict__ arena, double* b, double* xi,
                                                     const double* __restrict__ Dg, int32_t* tflags, int epoch,
-                                                    const int32_t* rdone, int nrd, int repoch, int64_t* dbg) {
+                                                    const int32_t* rdone, int nrd, int repoch, int64_t* dbg,
+                                                    RootArgs RA) {
   extern __shared__ __attribute__((aligned(16))) double Ls[];
   __shared__ double part[4 * SMALL_SOLVE_MAX], inits[SMALL_SOLVE_MAX];
   int64_t* dg = dbg ? dbg + 8 * blockIdx.x : nullptr;  // MADIPM_TREE_DEBUG: phase stamps
   if (dg && threadIdx.x == 0) dg[0] = wall_clock64();
-  const int s = fronts[blockIdx.x];
-  const int f0 = T.first[s], w = T.first[s + 1] - f0, r = T.nrows[s];
+  const int q = blockIdx.x;
+  const bool ra = q < RA.n;  // (the shapes in the launch arguments; beyond kRootArgs, from the tables)
+  const int s = ra ? RA.s[q] : fronts[q];
+  const int f0 = ra ? RA.f0[q] : T.first[s], w = ra ? RA.w[q] : T.first[s + 1] - f0, r = ra ? RA.r[q] : T.nrows[s];
+  const int64_t loff = ra ? RA.loff[q] : T.l_off[s];
   const int tid = threadIdx.x, lane = tid & 63;
   const int ldt = tree_ldt(w);
   // gather: row i = tid >> 2 summed by threads k = tid & 3 over the entries lo + 4 m + k of its segment
   // (the tail past the last full group of 4 by k = 0, in order: k_fwd_tree's summation)
   const int i = tid >> 2, k = tid & 3;
-  const int64_t e0 = T.row_ptr[s];
+  const int64_t e0 = ra ? RA.e0[q] : T.row_ptr[s];
   int64_t lo = 0, len = 0;
   if (i < r) {
     lo = T.sv_ptr[e0 + i];
@@ -4719,7 +4723,7 @@ __global__ __launch_bounds__(RSN) void k_root_solve(FrontTab T, const int32_t* _
       dpiv[h] = (tid < 64) ? Dg[f0 + j] : 1.0;
       pj[h] = (tid < 64) ? T.perm[f0 + j] : 0;
     }
-    stage_rowmajor<RSN>(arena + T.l_off[s], Ls, r, w, ldt);
+    stage_rowmajor<RSN>(arena + loff, Ls, r, w, ldt);
   };
   if (nrd == 0) factor_loads();
   double c = 0.0;
@@ -6132,6 +6136,16 @@ LDLSolver::LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const 
           if (in_tree[S.level_list[q]]) (big_root(S.level_list[q]) ? roots : ord).push_back(S.level_list[q]);
       nroot_task_ = (int)roots.size();
       for (int s : roots) rootf[s] = 1;
+      rargs_.n = std::min(nroot_task_, kRootArgs);
+      for (int q = 0; q < rargs_.n; ++q) {
+        const int s = roots[q];
+        rargs_.s[q] = s;
+        rargs_.f0[q] = S.first[s];
+        rargs_.w[q] = S.first[s + 1] - S.first[s];
+        rargs_.r[q] = S.nrows[s];
+        rargs_.e0[q] = S.row_ptr[s];
+        rargs_.loff[q] = S.l_off[s];
+      }
       ord.insert(ord.end(), roots.begin(), roots.end());
       ntree_ = (int)ord.size();
       // children of tree fronts scatter their forward update entries straight into the parent's
@@ -6983,7 +6997,7 @@ void LDLSolver::fwd_levels(const std::vector<SolveLevel>& V, int phase, double* 
         TIMED(KK_FWD_TREE, nlo > 0 ? 0.0 : tree_bytes_, nlo > 0 ? 0.0 : tree_alg_, nlo > 0 ? 0.0 : tree_flops_,
               (k_root_solve<<<(unsigned)nroot_task_, RSN, root_lds_, s>>>(
                   T_, tc_list_.p + nlo, arena_, b, xi_, D_, tflags_, efwd, rflag_.p ? rflag_.p + 2 : nullptr,
-                  root_pending_ ? nroot_side_ : 0, repoch_, tdbg_.p ? tdbg_.p + 8 * nlo : nullptr)));
+                  root_pending_ ? nroot_side_ : 0, repoch_, tdbg_.p ? tdbg_.p + 8 * nlo : nullptr, rargs_)));
       if (nroot_task_ && tdbg_.p) {  // MADIPM_TREE_DEBUG: the root solve's phases
         std::vector<int64_t> h(8 * nroot_task_);
         MADIPM_HIP(hipMemcpyAsync(h.data(), tdbg_.p + 8 * nlo, h.size() * 8, hipMemcpyDeviceToHost, s));

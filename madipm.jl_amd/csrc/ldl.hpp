@@ -232,6 +232,15 @@ class LinSolver {
   virtual void join(hipStream_t s) { (void)s; }
 };
 
+// k_root_solve's fronts (up to kRootArgs) by value: their shapes come with the launch instead of two
+// dependent table loads (front id, then first / nrows / row_ptr / l_off) before the gather
+constexpr int kRootArgs = 4;
+struct RootArgs {
+  int32_t n;
+  int32_t s[kRootArgs], f0[kRootArgs], w[kRootArgs], r[kRootArgs];
+  int64_t e0[kRootArgs], loff[kRootArgs];
+};
+
 class LDLSolver : public LinSolver {
  public:
   LDLSolver(int n, const int64_t* colptr, const int32_t* rowval, const SymbolicOptions& sopt,
@@ -379,6 +388,7 @@ class LDLSolver : public LinSolver {
   DBuf<int32_t> tc_ptr_, tc_list_, tdep_ptr_, tdep_, tpar_, tflags_;
   DBuf<uint8_t> trootbwd_;  // per forward task: an elimination-tree root solved backward by k_fwd_tree
   int nroot_task_ = 0, root_lds_ = 0;  // tree-solve tasks of big etree roots (last, own forward launch)
+  RootArgs rargs_{};                   // their fronts' shapes, passed by value to k_root_solve
   DBuf<uint8_t> tchunk_;    // per front: tree solves stream its panel in chunks (fwd_med_front / bwd_med_front)
   int ntask_ = 0;         // tree-solve tasks (one per tree front)
   int64_t nsleaf_ = 0;    // micro leaves solved from leaf records by the flat leaf launches
