@@ -485,3 +485,25 @@ def test_fold_batches_hold_at_most_1024_leaves(n):
     K, Lw = many_leaf_k2(n)
     info = Symbolic(K.shape[0], Lw.indptr, Lw.indices, default_ldl_opts(ordering=4)).info()
     assert info["fold_fronts"] == 1 and info["fold_leaves"] > 1024, info
+
+
+# SHA-1 (16 hex digits) of the nested-dissection order (ordering 3) of seeded stand-ins, as produced by
+# the round-5 ND code and unchanged by r6's speed-ups (threaded contraction, refinement scans and
+# induced subgraphs, uninitialised level arrays, the unit-weight matching shortcut): checked against a
+# build of the r5 sources (tools/perm_hash.py for the full-size configs).  A deliberate change of the
+# ordering updates these values.
+_ND_PINNED = {("ex10", 0.2): "d5c08eaa5e16e99c", ("neos", 0.1): "609901f70409cd1a",
+              ("supportcase10", 0.1): "328a57c1bc0e6381"}
+
+
+@pytest.mark.parametrize("name,scale", sorted(_ND_PINNED))
+def test_nd_order_pinned(name, scale):
+    import hashlib
+    from helpers import lp_k2
+    from madipm_amd import standard_form_qp
+    from madipm_amd import instances as I
+    from madipm_amd._lib import Symbolic, default_ldl_opts
+    make = {"ex10": I.ex10_standin, "neos": I.neos5052403_standin, "supportcase10": I.supportcase10_standin}[name]
+    K, Lw = lp_k2(standard_form_qp(make(scale=scale)), 0, well=True)
+    S = Symbolic(K.shape[0], Lw.indptr, Lw.indices, default_ldl_opts(ordering=3))
+    assert hashlib.sha1(S.perm().tobytes()).hexdigest()[:16] == _ND_PINNED[(name, scale)]
